@@ -1,0 +1,239 @@
+#!/usr/bin/env python3
+"""Benchmark: batched eval_loss throughput (BASELINE.json metric, config C2 / C4-style sharding).
+
+One step = score the whole population once: compile the 10k trees into device programs, upload,
+run the interpreter over all rows, reduce, copy losses back, finalize (the full cost of one
+`eval_cost_batch` call of a search iteration).  Trees and data are synthetic (seeded), generated
+before timing; the dataset is resident in HBM when the timed region starts.
+
+  python bench.py [--gpus N] [--steps K] [--warmup W]
+N > 1 (launched by torch.distributed.run): weak scaling — every rank holds its own 1M-row shard of
+one N*1M-row dataset, computes per-tree partial Σloss + flags, and the ranks all-reduce them over
+RCCL (the path's real exchange step) before finalizing.
+"""
+import argparse
+import ctypes
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "symbolicregression.jl_amd"))
+sys.path.insert(0, os.path.join(ROOT, "oracle"))
+
+import sr_amd  # noqa: E402
+from sr_amd import Dataset, Options, _lib, flatten_trees, gen_random_population  # noqa: E402
+
+PEAK_FP32_TFLOPS = 157.3  # MI355X FP32 vector (= FP32 MFMA) dense peak, MI355X_MICROARCH.md
+
+
+def c2_workload(n_rows, n_trees, rank, nf=5):
+    opts = Options(binary_operators=["+", "-", "*", "/"], unary_operators=["cos", "exp", "log"])
+    trees = gen_random_population(n_trees, opts, nf, max_size=30, seed=1)
+    tb = flatten_trees(trees, np.float32)
+    rng = np.random.default_rng(2 + 1000 * rank)
+    X = rng.standard_normal((nf, n_rows)).astype(np.float32)
+    y = (2 * np.cos(X[3]) + X[0] ** 2 - 2 + 0.1 * np.random.default_rng(3 + 1000 * rank).standard_normal(n_rows)
+         ).astype(np.float32)
+    return opts, tb, X, y
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--rows", type=int, default=1 << 20, help="rows per GPU")
+    ap.add_argument("--trees", type=int, default=10000)
+    ap.add_argument("--cpu-trees", type=int, default=0, help="CPU-baseline tree sample (0 = auto)")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = None
+    if world > 1:
+        import torch
+        import torch.distributed as tdist
+
+        torch.cuda.set_device(local_rank)
+        tdist.init_process_group(backend="nccl")
+        dist = tdist
+
+    opts, tb, X, y = c2_workload(args.rows, args.trees, rank)
+    n_total = args.rows * world
+    ctx = sr_amd.get_context(local_rank)
+    ds = Dataset(X, y)
+    dsh = ds.device_handle(ctx)
+    oid = ctx.opset_id(opts.operators)
+    s = tb.to_struct()
+    nt = tb.n_trees
+
+    if world == 1:
+        losses = np.empty(nt, dtype=np.float32)
+        comp = np.empty(nt, dtype=np.uint8)
+
+        def step():
+            _lib.check(_lib.lib.sr_eval_loss_batch(ctx.handle, dsh, oid, ctypes.byref(s), None, 0, 0,
+                                                   losses.ctypes.data_as(ctypes.c_void_p),
+                                                   comp.ctypes.data_as(ctypes.c_void_p)))
+            return ctx.last_kernel_ms()[0]
+
+        def barrier():
+            pass
+    else:
+        import torch
+
+        dev = torch.device("cuda", local_rank)
+        sums = torch.zeros(nt, dtype=torch.float64, device=dev)
+        flags = torch.zeros(nt, dtype=torch.int32, device=dev)
+        losses = np.empty(nt, dtype=np.float32)
+        comp = np.empty(nt, dtype=np.uint8)
+
+        def step():
+            _lib.check(_lib.lib.sr_eval_loss_partials(ctx.handle, dsh, oid, ctypes.byref(s), n_total, 0,
+                                                      ctypes.c_void_p(sums.data_ptr()),
+                                                      ctypes.c_void_p(flags.data_ptr()), 1))
+            kms = ctx.last_kernel_ms()[0]
+            dist.all_reduce(sums, op=dist.ReduceOp.SUM)
+            dist.all_reduce(flags, op=dist.ReduceOp.BOR)
+            hs = sums.cpu().numpy()
+            hf = flags.cpu().numpy().astype(np.uint32)
+            # rare exact-sum path: trees only "close to overflow" (no non-finite anywhere)
+            big = np.nonzero(((hf & (_lib.SR_FLAG_NONFINITE | _lib.SR_FLAG_STATIC)) == 0) & ((hf & _lib.SR_FLAG_BIG) != 0))[0]
+            cs = None
+            mc = 0
+            if big.size:
+                m = ctypes.c_int()
+                _lib.check(_lib.lib.sr_max_checks(ctx.handle, oid, ctypes.byref(s), ctypes.byref(m)))
+                mc = int(m.value)
+                lst = np.ascontiguousarray(big, dtype=np.int64)
+                part = np.zeros((big.size, mc))
+                _lib.check(_lib.lib.sr_exact_check_partials(ctx.handle, dsh, oid, ctypes.byref(s),
+                                                            lst.ctypes.data_as(ctypes.c_void_p), big.size, mc,
+                                                            part.ctypes.data_as(ctypes.c_void_p)))
+                t = torch.from_numpy(part).to(dev)
+                dist.all_reduce(t, op=dist.ReduceOp.SUM)
+                cs = np.ascontiguousarray(t.cpu().numpy())
+            lst_p = None if not big.size else np.ascontiguousarray(big, dtype=np.int64)
+            p = lambda a: None if a is None else a.ctypes.data_as(ctypes.c_void_p)
+            _lib.check(_lib.lib.sr_finalize_losses(_lib.SR_DTYPE_F32, nt, p(np.ascontiguousarray(hs)),
+                                                   p(np.ascontiguousarray(hf)), float(n_total), p(lst_p),
+                                                   0 if lst_p is None else lst_p.size, mc, p(cs),
+                                                   p(losses), p(comp)))
+            return kms
+
+        def barrier():
+            dist.barrier()
+            torch.cuda.synchronize()
+
+    for _ in range(args.warmup):
+        step()
+    barrier()
+    kernel_ms = []
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        kernel_ms.append(step())
+    barrier()
+    dt = time.perf_counter() - t0
+    if dist is not None:
+        import torch
+
+        tt = torch.tensor([dt], dtype=torch.float64, device=torch.device("cuda", local_rank))
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        dt = float(tt.item())
+
+    nodes = int(tb.n_nodes)
+    ops = int(tb.n_operator_nodes)
+    node_evals = float(nodes) * float(n_total)            # all ranks
+    value = node_evals * args.steps / dt
+    # roofline of the interpreter kernel on this GPU: algorithmic flops per launch / kernel time
+    flops_per_launch = float(args.rows) * (ops + 3 * nt)
+    kmean = float(np.mean(kernel_ms))
+    achieved = flops_per_launch / (kmean * 1e-3) / 1e12
+    frac_complete = float(np.mean(comp.astype(bool)))
+
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        cpu = cpu_baseline(opts, tb, X, y, args.cpu_trees)
+
+    if rank == 0:
+        line = {
+            "metric": "tree-node x row evals/sec (batched eval_loss, fp32)",
+            "value": value,
+            "unit": "node-evals/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": dt / args.steps * 1e3,
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "f32",
+            "data": "synthetic (seeded): gen_random_tree_fixed_size population, X~N(0,1), y=2cos(x4)+x1^2-2+0.1N",
+            "config": {
+                "workload": "C2 batched eval_loss: 10k random trees (size U{1..30}; +,-,*,/,cos,exp,safe_log) x 1M rows x 5 features per GPU",
+                "n_trees": nt,
+                "tree_nodes": nodes,
+                "operator_nodes": ops,
+                "rows_per_gpu": args.rows,
+                "rows_total": n_total,
+                "nfeatures": 5,
+                "parallelism": f"rows sharded x{world}, RCCL all-reduce of per-tree partial sums" if world > 1 else "single GPU",
+                "fraction_complete": frac_complete,
+            },
+            "roofline": {
+                "bound": "valu",
+                "achieved": achieved,
+                "peak": PEAK_FP32_TFLOPS,
+                "unit": "TFLOP/s",
+                "frac": achieved / PEAK_FP32_TFLOPS,
+                "traffic": None,
+                "kernel": "sr_interp_kernel<float,4,8,LOSS,gather=false,BASIC>",
+                "kernel_ms_mean": kmean,
+                "flops_per_launch": flops_per_launch,
+                "flop_convention": "n_rows * sum_t(n_op(t) + 3), 1 flop per operator incl. transcendentals (SURVEY 8d)",
+            },
+            "cpu_baseline": cpu,
+        }
+        print(json.dumps(line), flush=True)
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+def cpu_baseline(opts, tb, X, y, n_sample):
+    """Oracle (C port of DE's array-at-a-time evaluator, OpenMP over trees) on a bounded sample:
+    a strided subset of the same trees over all rows (~10-30 s on 16 host cores)."""
+    from oracle import Oracle
+
+    threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or min(os.cpu_count() or 1, 16)
+    threads = min(threads, 16)
+    orc = Oracle.from_options(opts)
+
+    def run(n):
+        step = max(1, tb.n_trees // n)
+        sub = tb.subset(np.arange(0, tb.n_trees, step)[:n])
+        t0 = time.perf_counter()
+        orc.eval_loss_batch(sub, X, y, accum="ref", n_threads=threads)
+        return sub, step, time.perf_counter() - t0
+
+    if n_sample <= 0:  # pilot, then size the sample for ~15 s of CPU work
+        sub, step, dt = run(2 * threads)
+        n_sample = int(min(tb.n_trees, max(2 * threads, 2 * threads * 15.0 / max(dt, 1e-3))))
+    sub, step, dt = run(n_sample)
+    rate = float(sub.n_nodes) * X.shape[1] / dt
+    return {
+        "value": rate,
+        "unit": "node-evals/s",
+        "cores": threads,
+        "kind": "port",
+        "sample": f"{sub.n_trees} of {tb.n_trees} trees (every {step}th), all {X.shape[1]} rows, {dt:.1f} s",
+    }
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,171 @@
+/*
+ * sr_amd.h — C ABI of the MI355X fitness-evaluation library (libsr_amd.so).
+ *
+ * Drop-in boundary for SymbolicRegression.jl's scoring hot path:
+ *   eval_cost -> eval_loss -> _eval_loss -> eval_tree_dispatch -> DE.eval_tree_array
+ *   (reference src/LossFunctions.jl:64-117,139-159,193-209; src/InterfaceDynamicExpressions.jl:58-88).
+ * A Julia `ccall` binding flattens DynamicExpressions `Node{T,2}` trees into the
+ * pre-order struct-of-arrays `sr_tree_batch` below and calls these entry points.  Every function
+ * returns an `int` status (SR_OK = 0, negative = error); `sr_last_error()` gives a thread-local
+ * message.  Non-finite evaluations are NOT errors: they come back as complete = 0, loss = +Inf,
+ * exactly like `_eval_loss` returning `L(Inf)` (src/LossFunctions.jl:97-99).
+ *
+ * Ownership: the caller owns every host buffer (borrowed for the duration of the call); the
+ * library owns device memory behind the opaque handles.  All calls are synchronous.
+ */
+#ifndef SR_AMD_H
+#define SR_AMD_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define SR_AMD_VERSION 1
+
+/* status codes */
+#define SR_OK 0
+#define SR_ERR_INVALID_ARG (-1)
+#define SR_ERR_HIP (-2)
+#define SR_ERR_UNSUPPORTED_OP (-3)   /* operator outside the device catalog: caller keeps its CPU path */
+#define SR_ERR_BAD_TREE (-4)         /* malformed pre-order arrays, feature out of range */
+#define SR_ERR_TOO_DEEP (-5)         /* tree needs more stack slots than the kernel holds */
+#define SR_ERR_NO_DEVICE (-6)
+
+/* element types (Dataset{T}): Float32 / Float64 */
+#define SR_DTYPE_F32 0
+#define SR_DTYPE_F64 1
+
+/* elementwise losses (Options.elementwise_loss) */
+#define SR_LOSS_L2DIST 0 /* L2DistLoss() — the default (src/Options.jl:772) */
+#define SR_LOSS_L1DIST 1 /* L1DistLoss() */
+
+/* per-tree partial flag bits (sr_eval_loss_partials) */
+#define SR_FLAG_NONFINITE 1u /* some checked intermediate array holds NaN/Inf: complete = false */
+#define SR_FLAG_BIG 2u       /* some checked value is so large its array sum may overflow: exact check needed */
+#define SR_FLAG_STATIC 4u    /* tree is incomplete independent of X (constant checks, constant folding) */
+
+typedef struct sr_ctx sr_ctx;
+typedef struct sr_dataset sr_dataset;
+
+/*
+ * A batch of expression trees in DynamicExpressions' own node fields, pre-order (depth-first,
+ * parent before children, left before right — the order of `get_scalar_constants`,
+ * test/integration/ad/zygote/test_derivatives.jl:127-155).  Tree t occupies node positions
+ * [offsets[t], offsets[t+1]).
+ */
+typedef struct sr_tree_batch {
+  int64_t n_trees;
+  const int64_t* offsets;   /* [n_trees + 1] */
+  const uint8_t* degree;    /* Node.degree: 0 leaf, 1 unary, 2 binary */
+  const uint8_t* op;        /* Node.op: 1-based index into options.operators.ops[degree] */
+  const uint16_t* feature;  /* Node.feature: 1-based column of X (leaf, !constant) */
+  const uint8_t* constant;  /* Node.constant (leaf) */
+  const void* val;          /* Node.val (leaf, constant): Float32 or Float64 = dataset dtype */
+} sr_tree_batch;
+
+/* ------------------------------------------------------------------ library / device */
+const char* sr_last_error(void);
+int sr_version(void);
+int sr_device_count(int* count);
+/* Open a context on HIP device `device` (one process per GPU: pass LOCAL_RANK). */
+int sr_init(int device, sr_ctx** out);
+int sr_shutdown(sr_ctx* ctx);
+
+/*
+ * Register an operator set: the printed names of options.operators.ops[1] (unary) and
+ * ops[2] (binary), in order, e.g. {"cos","exp","log"} and {"+","-","*","/"}.  Names follow
+ * DynamicExpressions' printing ("log" = safe_log, "^" = safe_pow, ...; src/Operators.jl:126-185)
+ * and the function names themselves ("safe_log", "plus", ...) are accepted too.
+ * Returns SR_ERR_UNSUPPORTED_OP if any operator is outside the device catalog.
+ */
+int sr_register_opset(sr_ctx* ctx, int n_unary, const char* const* unary_names, int n_binary,
+                      const char* const* binary_names, int* opset_id);
+
+/*
+ * Upload a dataset (src/Dataset.jl:131-246).  X is Julia's column-major [nfeatures, n] matrix
+ * (address f + nfeatures*i); the device copy is transposed to per-feature contiguous rows.
+ * y has n entries; weights may be NULL (unweighted).  dtype is SR_DTYPE_F32 / SR_DTYPE_F64.
+ */
+int sr_dataset_upload(sr_ctx* ctx, int dtype, const void* X, int64_t nfeatures, int64_t n,
+                      const void* y, const void* weights, sr_dataset** out);
+int sr_dataset_free(sr_dataset* ds);
+int sr_dataset_info(const sr_dataset* ds, int* dtype, int64_t* nfeatures, int64_t* n);
+
+/*
+ * Batched eval_loss (src/LossFunctions.jl:90-117 applied to every tree).
+ * row_idx (0-based, may repeat) selects a SubDataset view (src/Dataset.jl:90-112,300-308);
+ * pass NULL / 0 for the full dataset.  out_loss[n_trees] has the dataset dtype (L == T);
+ * out_complete[n_trees] is the `complete` flag of eval_tree_array.
+ */
+int sr_eval_loss_batch(sr_ctx* ctx, const sr_dataset* ds, int opset_id, const sr_tree_batch* trees,
+                       const int64_t* row_idx, int64_t n_idx, int loss_kind, void* out_loss,
+                       uint8_t* out_complete);
+
+/*
+ * Batched eval_tree_array (src/InterfaceDynamicExpressions.jl:58-88): predictions
+ * out_pred[n_trees][n_rows] (dataset dtype, row-major per tree) and complete flags.
+ */
+int sr_eval_tree_array(sr_ctx* ctx, const sr_dataset* ds, int opset_id, const sr_tree_batch* trees,
+                       const int64_t* row_idx, int64_t n_idx, void* out_pred, uint8_t* out_complete);
+
+/*
+ * Row-sharded form for multi-GPU scoring.  The dataset on this rank holds one shard of the
+ * rows; n_total is the number of rows over ALL shards (it sets the overflow-check threshold).
+ * Writes per-tree partial Σ w·loss (f64) and flag bits (SR_FLAG_*).  With out_on_device = 1 the
+ * two output pointers are device pointers (e.g. a torch tensor to all-reduce with RCCL).
+ * Combine across ranks: sums add, flags OR; then call sr_exact_check_partials for trees whose
+ * combined flags == SR_FLAG_BIG and sr_finalize_losses.
+ */
+int sr_eval_loss_partials(sr_ctx* ctx, const sr_dataset* ds, int opset_id, const sr_tree_batch* trees,
+                          int64_t n_total, int loss_kind, double* out_sum, uint32_t* out_flags,
+                          int out_on_device);
+/* Maximum number of checked nodes per tree for `trees` (sizes sr_exact_check_partials output). */
+int sr_max_checks(sr_ctx* ctx, int opset_id, const sr_tree_batch* trees, int* max_checks);
+/*
+ * Exact array-sum validity check (DynamicExpressions' isfinite(sum(x)) on every checked node)
+ * for the trees listed in tree_list[n_list]; out_sums[n_list][max_checks] receive this shard's
+ * f64 sums (scaled by 2^-64 for f64 data).  Sum across ranks, then pass to sr_finalize_losses.
+ */
+int sr_exact_check_partials(sr_ctx* ctx, const sr_dataset* ds, int opset_id, const sr_tree_batch* trees,
+                            const int64_t* tree_list, int64_t n_list, int max_checks, double* out_sums);
+/*
+ * Host-side combine: loss = sum / denom (denom = n_total, or Σweights), +Inf when incomplete.
+ * check_sums may be NULL when no tree carries SR_FLAG_BIG alone.
+ */
+int sr_finalize_losses(int dtype, int64_t n_trees, const double* sums, const uint32_t* flags, double denom,
+                       const int64_t* tree_list, int64_t n_list, int max_checks, const double* check_sums,
+                       void* out_loss, uint8_t* out_complete);
+/* Σ weights of this shard (f64), or the row count when unweighted. */
+int sr_dataset_denominator(const sr_dataset* ds, double* denom);
+
+/*
+ * Forward-mode gradient of the loss with respect to every constant of every tree (the batched
+ * BFGS objective+gradient of src/ConstantOptimization.jl:77-167).  Constants are ordered
+ * pre-order per tree (get_scalar_constants); out_grad is laid out per tree at the running sum of
+ * constant counts.  out_loss / out_complete as in sr_eval_loss_batch.
+ */
+int sr_eval_grad_batch(sr_ctx* ctx, const sr_dataset* ds, int opset_id, const sr_tree_batch* trees,
+                       const int64_t* row_idx, int64_t n_idx, int loss_kind, void* out_loss,
+                       void* out_grad, uint8_t* out_complete);
+
+/*
+ * Host-only dry run of the tree compiler (no device needed): compile `trees` for an operator set
+ * and report, per tree, the program length in instructions (out_len), whether the tree is
+ * incomplete independent of X (out_static_bad), and the operand-stack depth it needs
+ * (*out_max_depth).  With out_code != NULL the raw 16-byte instructions (Σ out_len of them, the
+ * layout of SrIns in csrc/sr_ops.h) are copied there, up to code_capacity instructions.
+ */
+int sr_compile_info(int dtype, int n_unary, const char* const* unary_names, int n_binary,
+                    const char* const* binary_names, const sr_tree_batch* trees, int64_t n_rows,
+                    int64_t nfeatures, int32_t* out_len, uint8_t* out_static_bad, int32_t* out_max_depth,
+                    void* out_code, int64_t code_capacity);
+
+/* Timing of the last device call on this context (ms): kernel-only, via HIP events. */
+int sr_last_kernel_ms(sr_ctx* ctx, double* eval_ms, double* total_ms);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* SR_AMD_H */

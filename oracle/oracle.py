@@ -1,0 +1,119 @@
+"""TEST INFRASTRUCTURE ONLY — ctypes wrapper of the CPU oracle (``oracle/build/liboracle.so``).
+
+Used by ``tests/``, ``__graft_entry__.smoke()`` and ``bench.py``'s ``cpu_baseline`` leg as the
+parity checker / CPU baseline.  The product path (``symbolicregression.jl_amd``) never imports it.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import subprocess
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB = os.path.join(_HERE, "build", "liboracle.so")
+
+
+def build() -> None:
+    subprocess.run(["make", "-s", "-C", _HERE], check=True)
+
+
+def _load():
+    if not os.path.exists(LIB):
+        build()
+    lib = ctypes.CDLL(LIB)
+    P = ctypes.c_void_p
+    I64 = ctypes.c_int64
+    I = ctypes.c_int
+    lib.oracle_op_id.restype = I
+    lib.oracle_op_id.argtypes = [ctypes.c_char_p, I]
+    for sfx in ("f32", "f64"):
+        f = getattr(lib, f"oracle_eval_tree_{sfx}")
+        f.restype = I
+        f.argtypes = [I64, P, P, P, P, P, P, I, P, I, P, I64, I64, P, P]
+        f = getattr(lib, f"oracle_eval_loss_{sfx}")
+        f.restype = I
+        f.argtypes = [I64, P, P, P, P, P, P, I, P, I, P, I64, I64, P, P, I, I, P, P]
+        f = getattr(lib, f"oracle_eval_loss_batch_{sfx}")
+        f.restype = I
+        f.argtypes = [I64, P, P, P, P, P, P, P, I, P, I, P, I64, I64, P, P, I, I, I, P, P]
+    return lib
+
+
+_lib = None
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        _lib = _load()
+    return _lib
+
+
+def _p(a):
+    return None if a is None else a.ctypes.data_as(ctypes.c_void_p)
+
+
+def _ids(names, degree):
+    out = []
+    for n in names:
+        i = lib().oracle_op_id(n.encode(), degree)
+        if i == 0:
+            raise ValueError(f"oracle has no operator {n!r}")
+        out.append(i)
+    return np.array(out if out else [0], dtype=np.int32)
+
+
+class Oracle:
+    """CPU restatement of eval_tree_array / _eval_loss for one operator set."""
+
+    def __init__(self, unaops, binops):
+        self.unaops = tuple(unaops)
+        self.binops = tuple(binops)
+        self.un = _ids(self.unaops, 1)
+        self.bi = _ids(self.binops, 2)
+
+    @classmethod
+    def from_options(cls, options):
+        return cls(options.operators.unaops, options.operators.binops)
+
+    @staticmethod
+    def _sfx(dtype):
+        return "f32" if np.dtype(dtype) == np.float32 else "f64"
+
+    def eval_tree_array(self, tb, k, X):
+        """tb: TreeBatch-like (offsets/degree/op/feature/constant/val); X: [nf, n]."""
+        X = np.asarray(X)
+        dtype = X.dtype
+        Xj = np.ascontiguousarray(X.T)
+        b, e = int(tb.offsets[k]), int(tb.offsets[k + 1])
+        val = np.ascontiguousarray(tb.val[b:e].astype(dtype))
+        out = np.empty(X.shape[1], dtype=dtype)
+        comp = ctypes.c_int(0)
+        f = getattr(lib(), f"oracle_eval_tree_{self._sfx(dtype)}")
+        ok = f(e - b, _p(tb.degree[b:e]), _p(tb.op[b:e]), _p(tb.feature[b:e]), _p(tb.constant[b:e]), _p(val),
+               _p(self.un), len(self.unaops), _p(self.bi), len(self.binops), _p(Xj), X.shape[0], X.shape[1],
+               _p(out), ctypes.byref(comp))
+        if not ok:
+            raise ValueError("oracle: malformed tree")
+        return out, bool(comp.value)
+
+    def eval_loss_batch(self, tb, X, y, w=None, loss_kind=0, accum="f64", n_threads=1):
+        X = np.asarray(X)
+        dtype = X.dtype
+        Xj = np.ascontiguousarray(X.T)
+        y = np.ascontiguousarray(y, dtype=dtype)
+        w = None if w is None else np.ascontiguousarray(w, dtype=dtype)
+        val = np.ascontiguousarray(tb.val.astype(dtype))
+        n_trees = len(tb.offsets) - 1
+        loss = np.empty(n_trees, dtype=dtype)
+        comp = np.empty(n_trees, dtype=np.int32)
+        f = getattr(lib(), f"oracle_eval_loss_batch_{self._sfx(dtype)}")
+        ok = f(n_trees, _p(np.ascontiguousarray(tb.offsets, dtype=np.int64)), _p(tb.degree), _p(tb.op),
+               _p(tb.feature), _p(tb.constant), _p(val), _p(self.un), len(self.unaops), _p(self.bi),
+               len(self.binops), _p(Xj), X.shape[0], X.shape[1], _p(y), _p(w), int(loss_kind),
+               0 if accum == "ref" else 1, int(n_threads), _p(loss), _p(comp))
+        if not ok:
+            raise ValueError("oracle: malformed tree")
+        return loss, comp.astype(bool)

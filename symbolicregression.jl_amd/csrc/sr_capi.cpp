@@ -1,0 +1,767 @@
+// sr_capi.cpp — the C ABI (include/sr_amd.h) over the HIP interpreter.
+//
+// Call path of one batched scoring call (sr_eval_loss_batch):
+//   host: compile the trees (sr_compile.cpp) -> upload programs -> interpreter kernel (partials per
+//   row block) -> fixed-order reduce kernel -> copy per-tree {Σloss, flags} back -> rare exact-sum
+//   check for trees whose checked values came close to overflowing -> loss = Σ / denominator.
+// Mirrors reference src/LossFunctions.jl:90-117 (`_eval_loss`) for each tree of the batch.
+#include <hip/hip_runtime.h>
+
+#include <chrono>
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "../../include/sr_amd.h"
+#include "sr_compile.h"
+#include "sr_eval.h"
+
+namespace {
+
+thread_local std::string g_last_error;
+
+int set_error(int code, const std::string& msg) {
+  g_last_error = msg;
+  return code;
+}
+
+#define SR_HIP_CHECK(expr)                                                                          \
+  do {                                                                                              \
+    hipError_t _e = (expr);                                                                         \
+    if (_e != hipSuccess)                                                                           \
+      return set_error(SR_ERR_HIP, std::string(#expr) + ": " + hipGetErrorString(_e));              \
+  } while (0)
+
+struct DevBuf {
+  void* p = nullptr;
+  size_t cap = 0;
+  hipError_t ensure(size_t bytes) {
+    if (bytes <= cap) return hipSuccess;
+    if (p) {
+      hipError_t e = hipFree(p);
+      if (e != hipSuccess) return e;
+      p = nullptr;
+      cap = 0;
+    }
+    size_t want = bytes < 4096 ? 4096 : bytes + bytes / 4;
+    hipError_t e = hipMalloc(&p, want);
+    if (e == hipSuccess) cap = want;
+    return e;
+  }
+  void release() {
+    if (p) (void)hipFree(p);
+    p = nullptr;
+    cap = 0;
+  }
+  template <typename U>
+  U* as() const {
+    return static_cast<U*>(p);
+  }
+};
+
+}  // namespace
+
+struct sr_ctx {
+  int device = 0;
+  hipStream_t stream = nullptr;
+  hipEvent_t ev_start = nullptr, ev_k0 = nullptr, ev_k1 = nullptr, ev_end = nullptr;
+  std::mutex mu;
+  std::vector<SrOpset> opsets;
+  std::vector<int> tiers;
+  DevBuf code, offsets, static_bad, part_sum, part_flag, out_sum, out_flag, pred, row_idx, tree_list,
+      check_sums;
+  double last_eval_ms = 0.0, last_total_ms = 0.0;
+  int cu_count = 256;
+};
+
+struct sr_dataset {
+  sr_ctx* ctx = nullptr;
+  int dtype = SR_DTYPE_F32;
+  int64_t nf = 0, n = 0, ld = 0;
+  void* X = nullptr;  // [nf][ld]
+  void* y = nullptr;  // [ld] or NULL
+  void* w = nullptr;  // [ld] or NULL
+  std::vector<double> w_host;  // weights (for Σw of SubDataset views)
+  double wsum = 0.0;
+};
+
+namespace {
+
+constexpr int64_t kRowAlign = 1024;  // 256 lanes x 16 B
+
+// Work decomposition: row tiles of 256*R rows, grouped `tiles` per block; trees grouped G per block.
+struct Grid {
+  int G = 32, tiles = 1, n_row_blocks = 1, n_groups = 1;
+  int64_t n_blocks = 1;
+};
+template <typename T>
+Grid make_grid(int64_t n_rows, int64_t n_trees) {
+  constexpr int64_t rows_per_tile = 256 * (16 / sizeof(T));
+  Grid g;
+  const int64_t n_tiles = (n_rows + rows_per_tile - 1) / rows_per_tile;
+  int64_t tiles = (n_tiles + 255) / 256;  // keep <= 256 row blocks per tree
+  if (tiles < 1) tiles = 1;
+  g.tiles = int(tiles);
+  g.n_row_blocks = int((n_tiles + tiles - 1) / tiles);
+  if (g.n_row_blocks < 1) g.n_row_blocks = 1;
+  int G = 32;
+  while (G > 1 && int64_t(g.n_row_blocks) * ((n_trees + G - 1) / G) < 2048) G /= 2;
+  g.G = G;
+  g.n_groups = int((n_trees + G - 1) / G);
+  g.n_blocks = int64_t(g.n_row_blocks) * g.n_groups;
+  return g;
+}
+
+template <typename T>
+double t_max() {
+  return double(SrM<T>::big);
+}
+
+struct Lock {
+  std::lock_guard<std::mutex> g;
+  explicit Lock(sr_ctx* c) : g(c->mu) {}
+};
+
+int check_ctx(sr_ctx* ctx) {
+  if (!ctx) return set_error(SR_ERR_INVALID_ARG, "NULL context");
+  return SR_OK;
+}
+
+int validate_common(sr_ctx* ctx, const sr_dataset* ds, int opset_id, const sr_tree_batch* trees) {
+  if (check_ctx(ctx) != SR_OK) return SR_ERR_INVALID_ARG;
+  if (!ds || ds->ctx != ctx) return set_error(SR_ERR_INVALID_ARG, "dataset is NULL or belongs to another context");
+  if (opset_id < 0 || opset_id >= int(ctx->opsets.size()))
+    return set_error(SR_ERR_INVALID_ARG, "unknown opset id " + std::to_string(opset_id));
+  if (!trees) return set_error(SR_ERR_INVALID_ARG, "NULL tree batch");
+  if (trees->n_trees < 0) return set_error(SR_ERR_INVALID_ARG, "negative tree count");
+  if (trees->n_trees > (int64_t(1) << 30)) return set_error(SR_ERR_INVALID_ARG, "too many trees in one batch");
+  return SR_OK;
+}
+
+// Shared engine: compile + upload + interpreter(+reduce).  Leaves per-tree {sum, flag} in
+// ctx->out_sum / ctx->out_flag (device).  n_eval rows (full dataset or row_idx view).
+template <typename T>
+int run_batch(sr_ctx* ctx, const sr_dataset* ds, int opset_id, const sr_tree_batch* trees, const int64_t* row_idx,
+              int64_t n_idx, int64_t n_total, int loss_kind, int mode, SrProgramBatch<T>* prog, Grid* grid_out) {
+  const bool gather = row_idx != nullptr && n_idx > 0;
+  const int64_t n_eval = gather ? n_idx : ds->n;
+  if (n_eval <= 0) return set_error(SR_ERR_INVALID_ARG, "no rows to evaluate");
+  if (ds->nf > SR_MAX_FEATURES)
+    return set_error(SR_ERR_INVALID_ARG, "nfeatures > " + std::to_string(SR_MAX_FEATURES) +
+                                             " is not supported by the register-resident X tile");
+  if (loss_kind != SR_LOSS_L2DIST && loss_kind != SR_LOSS_L1DIST)
+    return set_error(SR_ERR_INVALID_ARG, "unsupported loss kind");
+  std::string err;
+  int rc = sr_compile_batch<T>(*trees, ctx->opsets[opset_id], n_total, ds->nf, false, prog, &err);
+  if (rc != SR_OK) return set_error(rc, err);
+  if (prog->max_depth > 4)
+    return set_error(SR_ERR_TOO_DEEP, "a tree needs " + std::to_string(prog->max_depth) +
+                                          " operand-stack slots; the kernel holds 4 (maxsize <= 94)");
+  const int64_t nt = trees->n_trees;
+  Grid g = make_grid<T>(n_eval, nt);
+  *grid_out = g;
+  if (nt == 0) return SR_OK;
+
+  hipStream_t s = ctx->stream;
+  SR_HIP_CHECK(hipEventRecord(ctx->ev_start, s));
+  SR_HIP_CHECK(ctx->code.ensure(prog->code.size() * sizeof(SrIns<T>) + 16));
+  SR_HIP_CHECK(ctx->offsets.ensure(prog->offsets.size() * sizeof(uint32_t)));
+  SR_HIP_CHECK(ctx->static_bad.ensure(prog->static_bad.size() + 16));
+  if (!prog->code.empty())
+    SR_HIP_CHECK(hipMemcpyAsync(ctx->code.p, prog->code.data(), prog->code.size() * sizeof(SrIns<T>),
+                                hipMemcpyHostToDevice, s));
+  SR_HIP_CHECK(hipMemcpyAsync(ctx->offsets.p, prog->offsets.data(), prog->offsets.size() * sizeof(uint32_t),
+                              hipMemcpyHostToDevice, s));
+  SR_HIP_CHECK(hipMemcpyAsync(ctx->static_bad.p, prog->static_bad.data(), prog->static_bad.size(),
+                              hipMemcpyHostToDevice, s));
+  if (gather) {
+    for (int64_t i = 0; i < n_idx; ++i)
+      if (row_idx[i] < 0 || row_idx[i] >= ds->n)
+        return set_error(SR_ERR_INVALID_ARG, "row index " + std::to_string(row_idx[i]) + " out of range");
+    SR_HIP_CHECK(ctx->row_idx.ensure(size_t(n_idx) * sizeof(int64_t)));
+    SR_HIP_CHECK(hipMemcpyAsync(ctx->row_idx.p, row_idx, size_t(n_idx) * sizeof(int64_t), hipMemcpyHostToDevice, s));
+  }
+  const size_t n_part = size_t(nt) * size_t(g.n_row_blocks);
+  SR_HIP_CHECK(ctx->part_sum.ensure(n_part * sizeof(double)));
+  SR_HIP_CHECK(ctx->part_flag.ensure(n_part * sizeof(uint32_t)));
+  SR_HIP_CHECK(ctx->out_sum.ensure(size_t(nt) * sizeof(double)));
+  SR_HIP_CHECK(ctx->out_flag.ensure(size_t(nt) * sizeof(uint32_t)));
+  if (mode == SR_MODE_PRED) SR_HIP_CHECK(ctx->pred.ensure(size_t(nt) * size_t(n_eval) * sizeof(T)));
+
+  SrEvalArgs<T> a{};
+  a.code = ctx->code.as<SrIns<T>>();
+  a.offsets = ctx->offsets.as<uint32_t>();
+  a.n_trees = int(nt);
+  a.trees_per_block = g.G;
+  a.X = static_cast<const T*>(ds->X);
+  a.y = static_cast<const T*>(ds->y);
+  a.w = static_cast<const T*>(ds->w);
+  a.row_idx = gather ? ctx->row_idx.as<int64_t>() : nullptr;
+  a.ld = ds->ld;
+  a.n_rows = n_eval;
+  a.nf = int(ds->nf);
+  a.tiles_per_block = g.tiles;
+  a.n_row_blocks = g.n_row_blocks;
+  // Σ over n_total rows of values below tbig cannot overflow T, even with rounding slack.
+  a.tbig = T(t_max<T>() / (2.0 * double(n_total > 0 ? n_total : 1)));
+  a.loss_kind = loss_kind;
+  a.part_sum = ctx->part_sum.as<double>();
+  a.part_flag = ctx->part_flag.as<uint32_t>();
+  a.pred = ctx->pred.as<T>();
+  a.pred_ld = n_eval;
+  a.scale = 1.0;
+  if (g.n_blocks > 0x7fffffff) return set_error(SR_ERR_INVALID_ARG, "grid too large");
+  const int tier = ctx->tiers[opset_id];
+  SR_HIP_CHECK(hipEventRecord(ctx->ev_k0, s));
+  SR_HIP_CHECK(sr_launch_interp<T>(a, mode, gather, tier, int(g.n_blocks), s));
+  SR_HIP_CHECK(hipEventRecord(ctx->ev_k1, s));
+  SR_HIP_CHECK(sr_launch_reduce(a.part_sum, a.part_flag, int(nt), g.n_row_blocks, ctx->static_bad.as<uint8_t>(),
+                                ctx->out_sum.as<double>(), ctx->out_flag.as<uint32_t>(), s));
+  return SR_OK;
+}
+
+// Exact isfinite(sum(array)) check of every CHECK node of the listed trees.  Writes this dataset
+// view's sums to host_sums[n_list][max_checks].
+template <typename T>
+int run_exact(sr_ctx* ctx, const sr_dataset* ds, const SrProgramBatch<T>& prog, const int64_t* row_idx,
+              int64_t n_idx, const int64_t* list, int64_t n_list, int max_checks, double* host_sums) {
+  if (n_list == 0 || max_checks == 0) return SR_OK;
+  const bool gather = row_idx != nullptr && n_idx > 0;
+  const int64_t n_eval = gather ? n_idx : ds->n;
+  hipStream_t s = ctx->stream;
+  Grid g = make_grid<T>(n_eval, 1);
+  SR_HIP_CHECK(ctx->tree_list.ensure(size_t(n_list) * sizeof(int64_t)));
+  SR_HIP_CHECK(ctx->check_sums.ensure(size_t(n_list) * max_checks * sizeof(double)));
+  SR_HIP_CHECK(hipMemcpyAsync(ctx->tree_list.p, list, size_t(n_list) * sizeof(int64_t), hipMemcpyHostToDevice, s));
+  SR_HIP_CHECK(hipMemsetAsync(ctx->check_sums.p, 0, size_t(n_list) * max_checks * sizeof(double), s));
+  SR_HIP_CHECK(ctx->part_sum.ensure(size_t(g.n_row_blocks) * sizeof(double) * size_t(n_list)));
+  SR_HIP_CHECK(ctx->part_flag.ensure(size_t(g.n_row_blocks) * sizeof(uint32_t) * size_t(n_list)));
+  SrEvalArgs<T> a{};
+  a.code = ctx->code.as<SrIns<T>>();
+  a.offsets = ctx->offsets.as<uint32_t>();
+  a.n_trees = int(n_list);
+  a.trees_per_block = 1;
+  a.X = static_cast<const T*>(ds->X);
+  a.y = static_cast<const T*>(ds->y);
+  a.w = static_cast<const T*>(ds->w);
+  a.row_idx = gather ? ctx->row_idx.as<int64_t>() : nullptr;
+  a.ld = ds->ld;
+  a.n_rows = n_eval;
+  a.nf = int(ds->nf);
+  a.tiles_per_block = g.tiles;
+  a.n_row_blocks = g.n_row_blocks;
+  a.tbig = T(0);
+  a.part_sum = ctx->part_sum.as<double>();
+  a.part_flag = ctx->part_flag.as<uint32_t>();
+  a.tree_list = ctx->tree_list.as<int64_t>();
+  a.max_checks = max_checks;
+  a.check_sums = ctx->check_sums.as<double>();
+  // f64 sums can overflow f64 itself: scale by 2^-64 (the threshold is scaled identically)
+  a.scale = sizeof(T) == 8 ? std::ldexp(1.0, -64) : 1.0;
+  const int64_t blocks = int64_t(g.n_row_blocks) * n_list;
+  if (blocks > 0x7fffffff) return set_error(SR_ERR_INVALID_ARG, "grid too large");
+  SR_HIP_CHECK(sr_launch_interp<T>(a, SR_MODE_EXACT, gather, SR_TIER_FULL, int(blocks), s));
+  SR_HIP_CHECK(hipMemcpyAsync(host_sums, ctx->check_sums.p, size_t(n_list) * max_checks * sizeof(double),
+                              hipMemcpyDeviceToHost, s));
+  SR_HIP_CHECK(hipStreamSynchronize(s));
+  (void)prog;
+  return SR_OK;
+}
+
+template <typename T>
+double exact_threshold() {
+  return sizeof(T) == 8 ? std::ldexp(t_max<T>(), -64) : t_max<T>();
+}
+
+// Finalize one tree: complete unless flagged; BIG-only trees look up their exact check sums.
+template <typename T>
+void finalize(int64_t nt, const double* sums, const uint32_t* flags, double denom, const int64_t* list,
+              int64_t n_list, int max_checks, const double* check_sums, T* out_loss, uint8_t* out_complete) {
+  std::vector<int64_t> pos;
+  if (n_list > 0) {
+    pos.assign(size_t(nt), -1);
+    for (int64_t i = 0; i < n_list; ++i) pos[size_t(list[i])] = i;
+  }
+  const double thr = exact_threshold<T>();
+  for (int64_t t = 0; t < nt; ++t) {
+    bool ok = (flags[t] & (SR_FLAG_NONFINITE | SR_FLAG_STATIC)) == 0;
+    if (ok && (flags[t] & SR_FLAG_BIG)) {
+      const int64_t p = pos.empty() ? -1 : pos[size_t(t)];
+      if (p >= 0 && check_sums) {
+        for (int k = 0; k < max_checks; ++k) {
+          const double v = check_sums[size_t(p) * max_checks + k];
+          if (!(std::fabs(v) <= thr)) ok = false;
+        }
+      }
+    }
+    out_complete[t] = ok ? 1 : 0;
+    out_loss[t] = ok ? T(sums[t] / denom) : T(INFINITY);
+  }
+}
+
+template <typename T>
+double view_denominator(const sr_dataset* ds, const int64_t* row_idx, int64_t n_idx) {
+  const bool gather = row_idx != nullptr && n_idx > 0;
+  if (!ds->w) return double(gather ? n_idx : ds->n);
+  if (!gather) return ds->wsum;
+  double s = 0.0;
+  for (int64_t i = 0; i < n_idx; ++i) s += ds->w_host[size_t(row_idx[i])];
+  return s;
+}
+
+template <typename T>
+int eval_loss_impl(sr_ctx* ctx, const sr_dataset* ds, int opset_id, const sr_tree_batch* trees,
+                   const int64_t* row_idx, int64_t n_idx, int loss_kind, void* out_loss, uint8_t* out_complete) {
+  const int64_t nt = trees->n_trees;
+  if (nt > 0 && (!out_loss || !out_complete)) return set_error(SR_ERR_INVALID_ARG, "NULL output buffers");
+  const bool gather = row_idx != nullptr && n_idx > 0;
+  const int64_t n_eval = gather ? n_idx : ds->n;
+  auto t0 = std::chrono::steady_clock::now();
+  SrProgramBatch<T> prog;
+  Grid g;
+  int rc = run_batch<T>(ctx, ds, opset_id, trees, row_idx, n_idx, n_eval, loss_kind, SR_MODE_LOSS, &prog, &g);
+  if (rc != SR_OK) return rc;
+  if (nt == 0) return SR_OK;
+  std::vector<double> sums(static_cast<size_t>(nt));
+  std::vector<uint32_t> flags(static_cast<size_t>(nt));
+  hipStream_t s = ctx->stream;
+  SR_HIP_CHECK(hipMemcpyAsync(sums.data(), ctx->out_sum.p, size_t(nt) * sizeof(double), hipMemcpyDeviceToHost, s));
+  SR_HIP_CHECK(hipMemcpyAsync(flags.data(), ctx->out_flag.p, size_t(nt) * sizeof(uint32_t), hipMemcpyDeviceToHost, s));
+  SR_HIP_CHECK(hipEventRecord(ctx->ev_end, s));
+  SR_HIP_CHECK(hipStreamSynchronize(s));
+  float ms = 0.f;
+  SR_HIP_CHECK(hipEventElapsedTime(&ms, ctx->ev_k0, ctx->ev_k1));
+  ctx->last_eval_ms = ms;
+  std::vector<int64_t> list;
+  for (int64_t t = 0; t < nt; ++t)
+    if ((flags[t] & (SR_FLAG_NONFINITE | SR_FLAG_STATIC)) == 0 && (flags[t] & SR_FLAG_BIG)) list.push_back(t);
+  std::vector<double> check_sums;
+  if (!list.empty()) {
+    check_sums.assign(list.size() * size_t(prog.max_checks), 0.0);
+    rc = run_exact<T>(ctx, ds, prog, row_idx, n_idx, list.data(), int64_t(list.size()), prog.max_checks,
+                      check_sums.data());
+    if (rc != SR_OK) return rc;
+  }
+  const double denom = view_denominator<T>(ds, row_idx, n_idx);
+  finalize<T>(nt, sums.data(), flags.data(), denom, list.data(), int64_t(list.size()), prog.max_checks,
+              check_sums.empty() ? nullptr : check_sums.data(), static_cast<T*>(out_loss), out_complete);
+  auto t1 = std::chrono::steady_clock::now();
+  ctx->last_total_ms = std::chrono::duration<double, std::milli>(t1 - t0).count();
+  (void)n_eval;
+  return SR_OK;
+}
+
+template <typename T>
+int eval_pred_impl(sr_ctx* ctx, const sr_dataset* ds, int opset_id, const sr_tree_batch* trees,
+                   const int64_t* row_idx, int64_t n_idx, void* out_pred, uint8_t* out_complete) {
+  const int64_t nt = trees->n_trees;
+  if (nt > 0 && (!out_pred || !out_complete)) return set_error(SR_ERR_INVALID_ARG, "NULL output buffers");
+  const bool gather = row_idx != nullptr && n_idx > 0;
+  const int64_t n_eval = gather ? n_idx : ds->n;
+  SrProgramBatch<T> prog;
+  Grid g;
+  int rc = run_batch<T>(ctx, ds, opset_id, trees, row_idx, n_idx, n_eval, SR_LOSS_L2DIST, SR_MODE_PRED, &prog, &g);
+  if (rc != SR_OK) return rc;
+  if (nt == 0) return SR_OK;
+  hipStream_t s = ctx->stream;
+  std::vector<double> sums(static_cast<size_t>(nt));
+  std::vector<uint32_t> flags(static_cast<size_t>(nt));
+  SR_HIP_CHECK(hipMemcpyAsync(out_pred, ctx->pred.p, size_t(nt) * size_t(n_eval) * sizeof(T), hipMemcpyDeviceToHost, s));
+  SR_HIP_CHECK(hipMemcpyAsync(flags.data(), ctx->out_flag.p, size_t(nt) * sizeof(uint32_t), hipMemcpyDeviceToHost, s));
+  SR_HIP_CHECK(hipStreamSynchronize(s));
+  std::vector<int64_t> list;
+  for (int64_t t = 0; t < nt; ++t)
+    if ((flags[t] & (SR_FLAG_NONFINITE | SR_FLAG_STATIC)) == 0 && (flags[t] & SR_FLAG_BIG)) list.push_back(t);
+  std::vector<double> check_sums;
+  if (!list.empty()) {
+    check_sums.assign(list.size() * size_t(prog.max_checks), 0.0);
+    rc = run_exact<T>(ctx, ds, prog, row_idx, n_idx, list.data(), int64_t(list.size()), prog.max_checks,
+                      check_sums.data());
+    if (rc != SR_OK) return rc;
+  }
+  std::vector<T> dummy(static_cast<size_t>(nt));
+  finalize<T>(nt, sums.data(), flags.data(), 1.0, list.data(), int64_t(list.size()), prog.max_checks,
+              check_sums.empty() ? nullptr : check_sums.data(), dummy.data(), out_complete);
+  // statically incomplete trees have no program: fill their rows with NaN
+  T* p = static_cast<T*>(out_pred);
+  for (int64_t t = 0; t < nt; ++t)
+    if (prog.static_bad[size_t(t)])
+      for (int64_t i = 0; i < n_eval; ++i) p[size_t(t) * size_t(n_eval) + size_t(i)] = T(NAN);
+  return SR_OK;
+}
+
+template <typename T>
+int upload_impl(sr_ctx* ctx, const void* X, int64_t nf, int64_t n, const void* y, const void* w, sr_dataset** out) {
+  auto* ds = new sr_dataset();
+  ds->ctx = ctx;
+  ds->dtype = sizeof(T) == 4 ? SR_DTYPE_F32 : SR_DTYPE_F64;
+  ds->nf = nf;
+  ds->n = n;
+  ds->ld = ((n + kRowAlign - 1) / kRowAlign) * kRowAlign;
+  hipStream_t s = ctx->stream;
+  auto fail = [&](hipError_t e, const char* what) {
+    if (ds->X) (void)hipFree(ds->X);
+    if (ds->y) (void)hipFree(ds->y);
+    if (ds->w) (void)hipFree(ds->w);
+    delete ds;
+    return set_error(SR_ERR_HIP, std::string(what) + ": " + hipGetErrorString(e));
+  };
+  hipError_t e;
+  if ((e = hipMalloc(&ds->X, size_t(nf) * size_t(ds->ld) * sizeof(T))) != hipSuccess) return fail(e, "hipMalloc X");
+  void* tmp = nullptr;
+  if ((e = hipMalloc(&tmp, size_t(nf) * size_t(n) * sizeof(T))) != hipSuccess) return fail(e, "hipMalloc staging");
+  if ((e = hipMemcpyAsync(tmp, X, size_t(nf) * size_t(n) * sizeof(T), hipMemcpyHostToDevice, s)) != hipSuccess) {
+    (void)hipFree(tmp);
+    return fail(e, "copy X");
+  }
+  if ((e = sr_launch_transpose<T>(static_cast<const T*>(tmp), nf, n, ds->ld, static_cast<T*>(ds->X), s)) != hipSuccess) {
+    (void)hipFree(tmp);
+    return fail(e, "transpose X");
+  }
+  if ((e = hipStreamSynchronize(s)) != hipSuccess) {
+    (void)hipFree(tmp);
+    return fail(e, "sync");
+  }
+  (void)hipFree(tmp);
+  if (y) {
+    if ((e = hipMalloc(&ds->y, size_t(ds->ld) * sizeof(T))) != hipSuccess) return fail(e, "hipMalloc y");
+    if ((e = hipMemcpyAsync(ds->y, y, size_t(n) * sizeof(T), hipMemcpyHostToDevice, s)) != hipSuccess) return fail(e, "copy y");
+    if ((e = sr_launch_pad<T>(static_cast<T*>(ds->y), n, ds->ld, T(0), 1, s)) != hipSuccess) return fail(e, "pad y");
+  }
+  if (w) {
+    const T* wh = static_cast<const T*>(w);
+    ds->w_host.resize(size_t(n));
+    double sum = 0.0;
+    for (int64_t i = 0; i < n; ++i) {
+      ds->w_host[size_t(i)] = double(wh[i]);
+      sum += double(wh[i]);
+    }
+    ds->wsum = sum;
+    if ((e = hipMalloc(&ds->w, size_t(ds->ld) * sizeof(T))) != hipSuccess) return fail(e, "hipMalloc w");
+    if ((e = hipMemcpyAsync(ds->w, w, size_t(n) * sizeof(T), hipMemcpyHostToDevice, s)) != hipSuccess) return fail(e, "copy w");
+    if ((e = sr_launch_pad<T>(static_cast<T*>(ds->w), n, ds->ld, T(0), 0, s)) != hipSuccess) return fail(e, "pad w");
+  }
+  if ((e = hipStreamSynchronize(s)) != hipSuccess) return fail(e, "sync");
+  *out = ds;
+  return SR_OK;
+}
+
+int tier_of(const SrOpset& o) {
+  auto basic_u = [](uint32_t u) {
+    return u == SR_U_NEG || u == SR_U_SQUARE || u == SR_U_CUBE || u == SR_U_EXP || u == SR_U_COS ||
+           u == SR_U_SIN || u == SR_U_LOG || u == SR_U_SQRT || u == SR_U_ABS;
+  };
+  auto basic_b = [](uint32_t b) { return b == SR_B_ADD || b == SR_B_SUB || b == SR_B_MUL || b == SR_B_DIV; };
+  for (uint32_t u : o.unary)
+    if (!basic_u(u)) return SR_TIER_FULL;
+  for (uint32_t b : o.binary)
+    if (!basic_b(b)) return SR_TIER_FULL;
+  return SR_TIER_BASIC;
+}
+
+}  // namespace
+
+// ====================================================================== C ABI
+extern "C" {
+
+const char* sr_last_error(void) { return g_last_error.c_str(); }
+int sr_version(void) { return SR_AMD_VERSION; }
+
+int sr_device_count(int* count) {
+  if (!count) return set_error(SR_ERR_INVALID_ARG, "NULL count");
+  int c = 0;
+  hipError_t e = hipGetDeviceCount(&c);
+  if (e != hipSuccess) {
+    *count = 0;
+    return set_error(SR_ERR_NO_DEVICE, std::string("hipGetDeviceCount: ") + hipGetErrorString(e));
+  }
+  *count = c;
+  return SR_OK;
+}
+
+int sr_init(int device, sr_ctx** out) {
+  if (!out) return set_error(SR_ERR_INVALID_ARG, "NULL output");
+  *out = nullptr;
+  int c = 0;
+  if (hipGetDeviceCount(&c) != hipSuccess || c <= 0) return set_error(SR_ERR_NO_DEVICE, "no HIP device visible");
+  if (device < 0 || device >= c) return set_error(SR_ERR_INVALID_ARG, "device index out of range");
+  SR_HIP_CHECK(hipSetDevice(device));
+  auto* ctx = new sr_ctx();
+  ctx->device = device;
+  hipDeviceProp_t prop;
+  if (hipGetDeviceProperties(&prop, device) == hipSuccess) ctx->cu_count = prop.multiProcessorCount;
+  hipError_t e = hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking);
+  if (e == hipSuccess) e = hipEventCreate(&ctx->ev_start);
+  if (e == hipSuccess) e = hipEventCreate(&ctx->ev_k0);
+  if (e == hipSuccess) e = hipEventCreate(&ctx->ev_k1);
+  if (e == hipSuccess) e = hipEventCreate(&ctx->ev_end);
+  if (e != hipSuccess) {
+    delete ctx;
+    return set_error(SR_ERR_HIP, std::string("stream/event creation: ") + hipGetErrorString(e));
+  }
+  *out = ctx;
+  return SR_OK;
+}
+
+int sr_shutdown(sr_ctx* ctx) {
+  if (!ctx) return SR_OK;
+  {
+    Lock l(ctx);
+    (void)hipSetDevice(ctx->device);
+    (void)hipStreamSynchronize(ctx->stream);
+    for (DevBuf* b : {&ctx->code, &ctx->offsets, &ctx->static_bad, &ctx->part_sum, &ctx->part_flag, &ctx->out_sum,
+                      &ctx->out_flag, &ctx->pred, &ctx->row_idx, &ctx->tree_list, &ctx->check_sums})
+      b->release();
+    (void)hipEventDestroy(ctx->ev_start);
+    (void)hipEventDestroy(ctx->ev_k0);
+    (void)hipEventDestroy(ctx->ev_k1);
+    (void)hipEventDestroy(ctx->ev_end);
+    (void)hipStreamDestroy(ctx->stream);
+  }
+  delete ctx;
+  return SR_OK;
+}
+
+int sr_register_opset(sr_ctx* ctx, int n_unary, const char* const* unary_names, int n_binary,
+                      const char* const* binary_names, int* opset_id) {
+  if (check_ctx(ctx) != SR_OK) return SR_ERR_INVALID_ARG;
+  if (!opset_id || n_unary < 0 || n_binary < 0 || (n_unary > 0 && !unary_names) || (n_binary > 0 && !binary_names))
+    return set_error(SR_ERR_INVALID_ARG, "bad operator name arrays");
+  if (n_unary > 255 || n_binary > 255) return set_error(SR_ERR_INVALID_ARG, "more than 255 operators of one degree");
+  SrOpset o;
+  for (int i = 0; i < n_unary; ++i) {
+    const uint32_t id = unary_names[i] ? sr_unary_id(unary_names[i]) : 0;
+    if (!id) return set_error(SR_ERR_UNSUPPORTED_OP, std::string("unsupported unary operator: ") +
+                                                         (unary_names[i] ? unary_names[i] : "(null)"));
+    o.unary.push_back(id);
+  }
+  for (int i = 0; i < n_binary; ++i) {
+    const uint32_t id = binary_names[i] ? sr_binary_id(binary_names[i]) : 0;
+    if (!id) return set_error(SR_ERR_UNSUPPORTED_OP, std::string("unsupported binary operator: ") +
+                                                         (binary_names[i] ? binary_names[i] : "(null)"));
+    o.binary.push_back(id);
+  }
+  Lock l(ctx);
+  ctx->opsets.push_back(o);
+  ctx->tiers.push_back(tier_of(o));
+  *opset_id = int(ctx->opsets.size()) - 1;
+  return SR_OK;
+}
+
+int sr_dataset_upload(sr_ctx* ctx, int dtype, const void* X, int64_t nfeatures, int64_t n, const void* y,
+                      const void* weights, sr_dataset** out) {
+  if (check_ctx(ctx) != SR_OK) return SR_ERR_INVALID_ARG;
+  if (!out || !X || nfeatures <= 0 || n <= 0) return set_error(SR_ERR_INVALID_ARG, "bad dataset arguments");
+  if (nfeatures > 65535) return set_error(SR_ERR_INVALID_ARG, "nfeatures exceeds Node.feature (UInt16)");
+  Lock l(ctx);
+  SR_HIP_CHECK(hipSetDevice(ctx->device));
+  if (dtype == SR_DTYPE_F32) return upload_impl<float>(ctx, X, nfeatures, n, y, weights, out);
+  if (dtype == SR_DTYPE_F64) return upload_impl<double>(ctx, X, nfeatures, n, y, weights, out);
+  return set_error(SR_ERR_INVALID_ARG, "unknown dtype");
+}
+
+int sr_dataset_free(sr_dataset* ds) {
+  if (!ds) return SR_OK;
+  if (ds->ctx) {
+    Lock l(ds->ctx);
+    (void)hipSetDevice(ds->ctx->device);
+    (void)hipStreamSynchronize(ds->ctx->stream);
+    if (ds->X) (void)hipFree(ds->X);
+    if (ds->y) (void)hipFree(ds->y);
+    if (ds->w) (void)hipFree(ds->w);
+  }
+  delete ds;
+  return SR_OK;
+}
+
+int sr_dataset_info(const sr_dataset* ds, int* dtype, int64_t* nfeatures, int64_t* n) {
+  if (!ds) return set_error(SR_ERR_INVALID_ARG, "NULL dataset");
+  if (dtype) *dtype = ds->dtype;
+  if (nfeatures) *nfeatures = ds->nf;
+  if (n) *n = ds->n;
+  return SR_OK;
+}
+
+int sr_dataset_denominator(const sr_dataset* ds, double* denom) {
+  if (!ds || !denom) return set_error(SR_ERR_INVALID_ARG, "NULL argument");
+  *denom = ds->w ? ds->wsum : double(ds->n);
+  return SR_OK;
+}
+
+int sr_eval_loss_batch(sr_ctx* ctx, const sr_dataset* ds, int opset_id, const sr_tree_batch* trees,
+                       const int64_t* row_idx, int64_t n_idx, int loss_kind, void* out_loss, uint8_t* out_complete) {
+  int rc = validate_common(ctx, ds, opset_id, trees);
+  if (rc != SR_OK) return rc;
+  Lock l(ctx);
+  SR_HIP_CHECK(hipSetDevice(ctx->device));
+  if (ds->dtype == SR_DTYPE_F32)
+    return eval_loss_impl<float>(ctx, ds, opset_id, trees, row_idx, n_idx, loss_kind, out_loss, out_complete);
+  return eval_loss_impl<double>(ctx, ds, opset_id, trees, row_idx, n_idx, loss_kind, out_loss, out_complete);
+}
+
+int sr_eval_tree_array(sr_ctx* ctx, const sr_dataset* ds, int opset_id, const sr_tree_batch* trees,
+                       const int64_t* row_idx, int64_t n_idx, void* out_pred, uint8_t* out_complete) {
+  int rc = validate_common(ctx, ds, opset_id, trees);
+  if (rc != SR_OK) return rc;
+  Lock l(ctx);
+  SR_HIP_CHECK(hipSetDevice(ctx->device));
+  if (ds->dtype == SR_DTYPE_F32)
+    return eval_pred_impl<float>(ctx, ds, opset_id, trees, row_idx, n_idx, out_pred, out_complete);
+  return eval_pred_impl<double>(ctx, ds, opset_id, trees, row_idx, n_idx, out_pred, out_complete);
+}
+
+int sr_eval_loss_partials(sr_ctx* ctx, const sr_dataset* ds, int opset_id, const sr_tree_batch* trees,
+                          int64_t n_total, int loss_kind, double* out_sum, uint32_t* out_flags, int out_on_device) {
+  int rc = validate_common(ctx, ds, opset_id, trees);
+  if (rc != SR_OK) return rc;
+  const int64_t nt = trees->n_trees;
+  if (nt > 0 && (!out_sum || !out_flags)) return set_error(SR_ERR_INVALID_ARG, "NULL output buffers");
+  if (n_total < ds->n) return set_error(SR_ERR_INVALID_ARG, "n_total smaller than this shard");
+  Lock l(ctx);
+  SR_HIP_CHECK(hipSetDevice(ctx->device));
+  Grid g;
+  auto t0 = std::chrono::steady_clock::now();
+  if (ds->dtype == SR_DTYPE_F32) {
+    SrProgramBatch<float> prog;
+    rc = run_batch<float>(ctx, ds, opset_id, trees, nullptr, 0, n_total, loss_kind, SR_MODE_LOSS, &prog, &g);
+  } else {
+    SrProgramBatch<double> prog;
+    rc = run_batch<double>(ctx, ds, opset_id, trees, nullptr, 0, n_total, loss_kind, SR_MODE_LOSS, &prog, &g);
+  }
+  if (rc != SR_OK || nt == 0) return rc;
+  hipStream_t s = ctx->stream;
+  const hipMemcpyKind kind = out_on_device ? hipMemcpyDeviceToDevice : hipMemcpyDeviceToHost;
+  SR_HIP_CHECK(hipMemcpyAsync(out_sum, ctx->out_sum.p, size_t(nt) * sizeof(double), kind, s));
+  SR_HIP_CHECK(hipMemcpyAsync(out_flags, ctx->out_flag.p, size_t(nt) * sizeof(uint32_t), kind, s));
+  SR_HIP_CHECK(hipStreamSynchronize(s));
+  float ms = 0.f;
+  SR_HIP_CHECK(hipEventElapsedTime(&ms, ctx->ev_k0, ctx->ev_k1));
+  ctx->last_eval_ms = ms;
+  ctx->last_total_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+  return SR_OK;
+}
+
+int sr_max_checks(sr_ctx* ctx, int opset_id, const sr_tree_batch* trees, int* max_checks) {
+  if (check_ctx(ctx) != SR_OK) return SR_ERR_INVALID_ARG;
+  if (!trees || !max_checks || opset_id < 0 || opset_id >= int(ctx->opsets.size()))
+    return set_error(SR_ERR_INVALID_ARG, "bad arguments");
+  SrProgramBatch<double> prog;
+  std::string err;
+  int rc = sr_compile_batch<double>(*trees, ctx->opsets[opset_id], 1, 65535, false, &prog, &err);
+  if (rc != SR_OK) return set_error(rc, err);
+  *max_checks = prog.max_checks;
+  return SR_OK;
+}
+
+int sr_exact_check_partials(sr_ctx* ctx, const sr_dataset* ds, int opset_id, const sr_tree_batch* trees,
+                            const int64_t* tree_list, int64_t n_list, int max_checks, double* out_sums) {
+  int rc = validate_common(ctx, ds, opset_id, trees);
+  if (rc != SR_OK) return rc;
+  if (n_list < 0 || (n_list > 0 && (!tree_list || !out_sums)) || max_checks < 0)
+    return set_error(SR_ERR_INVALID_ARG, "bad tree list");
+  for (int64_t i = 0; i < n_list; ++i)
+    if (tree_list[i] < 0 || tree_list[i] >= trees->n_trees) return set_error(SR_ERR_INVALID_ARG, "tree index out of range");
+  if (n_list == 0) return SR_OK;
+  Lock l(ctx);
+  SR_HIP_CHECK(hipSetDevice(ctx->device));
+  Grid g;
+  if (ds->dtype == SR_DTYPE_F32) {
+    SrProgramBatch<float> prog;
+    rc = run_batch<float>(ctx, ds, opset_id, trees, nullptr, 0, ds->n, SR_LOSS_L2DIST, SR_MODE_LOSS, &prog, &g);
+    if (rc != SR_OK) return rc;
+    if (prog.max_checks > max_checks) return set_error(SR_ERR_INVALID_ARG, "max_checks too small");
+    return run_exact<float>(ctx, ds, prog, nullptr, 0, tree_list, n_list, max_checks, out_sums);
+  }
+  SrProgramBatch<double> prog;
+  rc = run_batch<double>(ctx, ds, opset_id, trees, nullptr, 0, ds->n, SR_LOSS_L2DIST, SR_MODE_LOSS, &prog, &g);
+  if (rc != SR_OK) return rc;
+  if (prog.max_checks > max_checks) return set_error(SR_ERR_INVALID_ARG, "max_checks too small");
+  return run_exact<double>(ctx, ds, prog, nullptr, 0, tree_list, n_list, max_checks, out_sums);
+}
+
+int sr_finalize_losses(int dtype, int64_t n_trees, const double* sums, const uint32_t* flags, double denom,
+                       const int64_t* tree_list, int64_t n_list, int max_checks, const double* check_sums,
+                       void* out_loss, uint8_t* out_complete) {
+  if (n_trees < 0 || (n_trees > 0 && (!sums || !flags || !out_loss || !out_complete)))
+    return set_error(SR_ERR_INVALID_ARG, "bad arguments");
+  if (n_list > 0 && !tree_list) return set_error(SR_ERR_INVALID_ARG, "NULL tree list");
+  for (int64_t i = 0; i < n_list; ++i)
+    if (tree_list[i] < 0 || tree_list[i] >= n_trees) return set_error(SR_ERR_INVALID_ARG, "tree index out of range");
+  if (dtype == SR_DTYPE_F32)
+    finalize<float>(n_trees, sums, flags, denom, tree_list, n_list, max_checks, check_sums,
+                    static_cast<float*>(out_loss), out_complete);
+  else if (dtype == SR_DTYPE_F64)
+    finalize<double>(n_trees, sums, flags, denom, tree_list, n_list, max_checks, check_sums,
+                     static_cast<double*>(out_loss), out_complete);
+  else
+    return set_error(SR_ERR_INVALID_ARG, "unknown dtype");
+  return SR_OK;
+}
+
+int sr_eval_grad_batch(sr_ctx* ctx, const sr_dataset* ds, int opset_id, const sr_tree_batch* trees,
+                       const int64_t* row_idx, int64_t n_idx, int loss_kind, void* out_loss, void* out_grad,
+                       uint8_t* out_complete) {
+  (void)ctx; (void)ds; (void)opset_id; (void)trees; (void)row_idx; (void)n_idx; (void)loss_kind;
+  (void)out_loss; (void)out_grad; (void)out_complete;
+  return set_error(SR_ERR_INVALID_ARG, "sr_eval_grad_batch: forward-mode gradient kernel not built yet");
+}
+
+int sr_compile_info(int dtype, int n_unary, const char* const* unary_names, int n_binary,
+                    const char* const* binary_names, const sr_tree_batch* trees, int64_t n_rows,
+                    int64_t nfeatures, int32_t* out_len, uint8_t* out_static_bad, int32_t* out_max_depth,
+                    void* out_code, int64_t code_capacity) {
+  if (!trees || n_unary < 0 || n_binary < 0 || (n_unary > 0 && !unary_names) || (n_binary > 0 && !binary_names))
+    return set_error(SR_ERR_INVALID_ARG, "bad arguments");
+  SrOpset o;
+  for (int i = 0; i < n_unary; ++i) {
+    const uint32_t id = unary_names[i] ? sr_unary_id(unary_names[i]) : 0;
+    if (!id) return set_error(SR_ERR_UNSUPPORTED_OP, std::string("unsupported unary operator: ") +
+                                                         (unary_names[i] ? unary_names[i] : "(null)"));
+    o.unary.push_back(id);
+  }
+  for (int i = 0; i < n_binary; ++i) {
+    const uint32_t id = binary_names[i] ? sr_binary_id(binary_names[i]) : 0;
+    if (!id) return set_error(SR_ERR_UNSUPPORTED_OP, std::string("unsupported binary operator: ") +
+                                                         (binary_names[i] ? binary_names[i] : "(null)"));
+    o.binary.push_back(id);
+  }
+  std::string err;
+  auto report = [&](auto& prog) -> int {
+    const int64_t nt = trees->n_trees;
+    for (int64_t t = 0; t < nt; ++t) {
+      if (out_len) out_len[t] = int32_t(prog.offsets[size_t(t) + 1] - prog.offsets[size_t(t)]);
+      if (out_static_bad) out_static_bad[t] = prog.static_bad[size_t(t)];
+    }
+    if (out_max_depth) *out_max_depth = prog.max_depth;
+    if (out_code) {
+      const int64_t n = int64_t(prog.code.size()) < code_capacity ? int64_t(prog.code.size()) : code_capacity;
+      std::memcpy(out_code, prog.code.data(), size_t(n) * 16);
+    }
+    return SR_OK;
+  };
+  if (dtype == SR_DTYPE_F32) {
+    SrProgramBatch<float> prog;
+    int rc = sr_compile_batch<float>(*trees, o, n_rows, nfeatures, false, &prog, &err);
+    if (rc != SR_OK) return set_error(rc, err);
+    return report(prog);
+  }
+  if (dtype == SR_DTYPE_F64) {
+    SrProgramBatch<double> prog;
+    int rc = sr_compile_batch<double>(*trees, o, n_rows, nfeatures, false, &prog, &err);
+    if (rc != SR_OK) return set_error(rc, err);
+    return report(prog);
+  }
+  return set_error(SR_ERR_INVALID_ARG, "unknown dtype");
+}
+
+int sr_last_kernel_ms(sr_ctx* ctx, double* eval_ms, double* total_ms) {
+  if (check_ctx(ctx) != SR_OK) return SR_ERR_INVALID_ARG;
+  if (eval_ms) *eval_ms = ctx->last_eval_ms;
+  if (total_ms) *total_ms = ctx->last_total_ms;
+  return SR_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,518 @@
+// sr_compile.cpp — see sr_compile.h.  Reference semantics restated here:
+//   DynamicExpressions 2.4 `_eval_tree_array` / `dispatch_deg1_eval` / `dispatch_deg2_eval` /
+//   `dispatch_constant_tree` (not vendored; SymbolicRegression calls it from
+//   src/InterfaceDynamicExpressions.jl:81 and src/LossFunctions.jl:68,79), the fused-kernel list
+//   pinned by test/unit/evaluation/test_evaluation.jl:15-51 and the flag known answers of
+//   test/integration/ext/loopvectorization/test_nan_detection.jl:17-51.
+#include "sr_compile.h"
+
+#include <cmath>
+#include <cstring>
+#include <thread>
+
+namespace {
+
+struct NameId {
+  const char* name;
+  uint32_t id;
+};
+
+// Names as DynamicExpressions prints them (get_op_name, src/Operators.jl:126-160) plus the
+// Julia function names SymbolicRegression maps them to (OP_MAP, src/Options.jl:182-202).
+const NameId kUnary[] = {
+    {"neg", SR_U_NEG},       {"-", SR_U_NEG},          {"square", SR_U_SQUARE},  {"cube", SR_U_CUBE},
+    {"exp", SR_U_EXP},       {"cos", SR_U_COS},        {"sin", SR_U_SIN},        {"tan", SR_U_TAN},
+    {"log", SR_U_LOG},       {"safe_log", SR_U_LOG},   {"log2", SR_U_LOG2},      {"safe_log2", SR_U_LOG2},
+    {"log10", SR_U_LOG10},   {"safe_log10", SR_U_LOG10}, {"log1p", SR_U_LOG1P}, {"safe_log1p", SR_U_LOG1P},
+    {"sqrt", SR_U_SQRT},     {"safe_sqrt", SR_U_SQRT}, {"abs", SR_U_ABS},        {"sign", SR_U_SIGN},
+    {"tanh", SR_U_TANH},     {"sinh", SR_U_SINH},      {"cosh", SR_U_COSH},      {"atan", SR_U_ATAN},
+    {"asin", SR_U_ASIN},     {"safe_asin", SR_U_ASIN}, {"acos", SR_U_ACOS},      {"safe_acos", SR_U_ACOS},
+    {"acosh", SR_U_ACOSH},   {"safe_acosh", SR_U_ACOSH}, {"atanh", SR_U_ATANH}, {"safe_atanh", SR_U_ATANH},
+    {"asinh", SR_U_ASINH},   {"relu", SR_U_RELU},      {"inv", SR_U_INV},        {"erf", SR_U_ERF},
+    {"erfc", SR_U_ERFC},     {"gamma", SR_U_GAMMA},    {"round", SR_U_ROUND},    {"floor", SR_U_FLOOR},
+    {"ceil", SR_U_CEIL},     {"exp2", SR_U_EXP2},      {"expm1", SR_U_EXPM1},
+};
+const NameId kBinary[] = {
+    {"+", SR_B_ADD},          {"plus", SR_B_ADD},           {"-", SR_B_SUB},       {"sub", SR_B_SUB},
+    {"*", SR_B_MUL},          {"mult", SR_B_MUL},           {"/", SR_B_DIV},       {"div", SR_B_DIV},
+    {"^", SR_B_POW},          {"safe_pow", SR_B_POW},       {"pow", SR_B_POW},     {"max", SR_B_MAX},
+    {"min", SR_B_MIN},        {"mod", SR_B_MOD},            {">", SR_B_GREATER},   {"greater", SR_B_GREATER},
+    {"<", SR_B_LESS},         {"less", SR_B_LESS},          {">=", SR_B_GREATER_EQUAL},
+    {"greater_equal", SR_B_GREATER_EQUAL},                  {"<=", SR_B_LESS_EQUAL},
+    {"less_equal", SR_B_LESS_EQUAL},                        {"cond", SR_B_COND},
+    {"logical_or", SR_B_LOGICAL_OR},                        {"logical_and", SR_B_LOGICAL_AND},
+    {"atan2", SR_B_ATAN2},    {"atan", SR_B_ATAN2},
+};
+
+template <typename T>
+struct Tree {
+  // per node (pre-order position within the tree)
+  std::vector<int32_t> l, r;
+  const uint8_t* degree;
+  const uint8_t* op;
+  const uint16_t* feature;
+  const uint8_t* constant;
+  const T* val;
+  int64_t n;
+};
+
+template <typename T>
+struct TreeCompiler {
+  const SrOpset& ops;
+  int64_t n_rows;
+  int64_t nfeatures;
+  bool with_const_index;
+  Tree<T> t;
+  std::vector<uint8_t> is_const, folded, arr_check, infsub;
+  std::vector<T> fold_val;
+  std::vector<int32_t> const_slot;  // pre-order constant index of constant leaves
+  std::vector<int32_t> need;
+  std::vector<SrIns<T>> code;
+  bool bad = false;
+  int err = SR_OK;
+  std::string msg;
+  int depth = 0, max_depth = 0;
+  uint32_t n_checks = 0;
+  uint32_t n_consts = 0;
+  int64_t n_ops = 0;
+
+  TreeCompiler(const SrOpset& o, int64_t nr, int64_t nf, bool wci)
+      : ops(o), n_rows(nr), nfeatures(nf), with_const_index(wci) {}
+
+  bool leaf(int i) const { return t.degree[i] == 0; }
+  bool effleaf(int i) const { return t.degree[i] == 0 || folded[i]; }
+
+  uint32_t unary_id(int i) {
+    const int k = int(t.op[i]) - 1;
+    if (k < 0 || k >= int(ops.unary.size())) {
+      fail(SR_ERR_BAD_TREE, "unary op index out of range");
+      return SR_U_NONE;
+    }
+    return ops.unary[k];
+  }
+  uint32_t binary_id(int i) {
+    const int k = int(t.op[i]) - 1;
+    if (k < 0 || k >= int(ops.binary.size())) {
+      fail(SR_ERR_BAD_TREE, "binary op index out of range");
+      return SR_B_NONE;
+    }
+    return ops.binary[k];
+  }
+  void fail(int code, const char* m) {
+    if (err == SR_OK) {
+      err = code;
+      msg = m;
+    }
+  }
+
+  // Parse pre-order arrays into child links.
+  bool parse() {
+    const int64_t n = t.n;
+    if (n <= 0) {
+      fail(SR_ERR_BAD_TREE, "empty tree");
+      return false;
+    }
+    t.l.assign(n, -1);
+    t.r.assign(n, -1);
+    // iterative: stack of (node, children filled)
+    std::vector<int32_t> stk;
+    stk.reserve(64);
+    int64_t pos = 0;
+    // recursive descent with explicit stack of pending child slots
+    struct Slot { int32_t parent; int which; };
+    std::vector<Slot> pending;
+    pending.push_back({-1, 0});
+    while (!pending.empty()) {
+      Slot s = pending.back();
+      pending.pop_back();
+      if (pos >= n) {
+        fail(SR_ERR_BAD_TREE, "pre-order arrays end inside a subtree");
+        return false;
+      }
+      const int32_t i = int32_t(pos++);
+      if (s.parent >= 0) (s.which == 0 ? t.l : t.r)[s.parent] = i;
+      const int d = t.degree[i];
+      if (d > 2) {
+        fail(SR_ERR_BAD_TREE, "degree > 2");
+        return false;
+      }
+      if (d == 2) {
+        pending.push_back({i, 1});  // right after left
+        pending.push_back({i, 0});
+      } else if (d == 1) {
+        pending.push_back({i, 0});
+      } else if (!t.constant[i]) {
+        const int f = int(t.feature[i]);
+        if (f < 1 || f > nfeatures) {
+          fail(SR_ERR_BAD_TREE, "feature index out of range");
+          return false;
+        }
+      }
+    }
+    if (pos != n) {
+      fail(SR_ERR_BAD_TREE, "extra nodes after the root subtree");
+      return false;
+    }
+    return true;
+  }
+
+  // is_constant(tree) == all leaves constant (post-order over pre-order positions, reversed).
+  void mark_const() {
+    const int64_t n = t.n;
+    is_const.assign(n, 0);
+    for (int64_t i = n - 1; i >= 0; --i) {
+      const int d = t.degree[i];
+      if (d == 0) is_const[i] = t.constant[i] ? 1 : 0;
+      else if (d == 1) is_const[i] = is_const[t.l[i]];
+      else is_const[i] = is_const[t.l[i]] && is_const[t.r[i]];
+    }
+  }
+
+  // dispatch_constant_tree: scalar fold with is_valid after every op.  Leaf constants are
+  // validated too (unpinned choice — a non-finite leaf constant makes the subtree
+  // invalid, which also keeps Julia's cos(Inf) DomainError unreachable).
+  bool fold(int i, T* out) {
+    const int d = t.degree[i];
+    if (d == 0) {
+      *out = t.val[i];
+      return sr_isfinite(*out);
+    }
+    if (d == 1) {
+      T x;
+      if (!fold(t.l[i], &x)) return false;
+      const uint32_t id = unary_id(i);
+      *out = sr_unary<T>(id, x);
+      return sr_isfinite(*out);
+    }
+    T a, b;
+    if (!fold(t.l[i], &a)) return false;
+    if (!fold(t.r[i], &b)) return false;
+    const uint32_t id = binary_id(i);
+    *out = sr_binary<T>(id, a, b);
+    return sr_isfinite(*out);
+  }
+
+  // Scalar check of a constant leaf (DE @return_on_nonfinite_val in fused deg2 kernels).
+  void scalar_check(int i) {
+    if (leaf(i) && t.constant[i] && !sr_isfinite(t.val[i])) bad = true;
+  }
+
+  // Mirror of _eval_tree_array's control flow: decides fold / checks / fused kernels.
+  void evalmark(int i) {
+    const int d = t.degree[i];
+    if (d == 0) return;  // deg0_eval: copy / fill, no check here
+    if (is_const[i]) {   // constant-tree fast path
+      T v;
+      if (!fold(i, &v)) bad = true;
+      folded[i] = 1;
+      fold_val[i] = v;
+      return;
+    }
+    if (d == 1) {
+      const int c = t.l[i];
+      const int cd = t.degree[c];
+      if (cd == 2 && leaf(t.l[c]) && leaf(t.r[c])) {  // deg1_l2_ll0_lr0
+        infsub[i] = 1;
+        scalar_check(t.l[c]);
+        scalar_check(t.r[c]);
+      } else if (cd == 1 && leaf(t.l[c])) {            // deg1_l1_ll0
+        infsub[i] = 1;
+        scalar_check(t.l[c]);
+      } else {                                         // general deg1: child array checked
+        evalmark(c);
+        arr_check[c] = 1;
+      }
+      return;
+    }
+    const int a = t.l[i], b = t.r[i];
+    if (leaf(a) && leaf(b)) {          // deg2_l0_r0
+      scalar_check(a);
+      scalar_check(b);
+    } else if (leaf(b)) {              // deg2_r0: left evaluated + checked
+      evalmark(a);
+      arr_check[a] = 1;
+      scalar_check(b);
+    } else if (leaf(a)) {              // deg2_l0: right evaluated + checked
+      evalmark(b);
+      arr_check[b] = 1;
+      scalar_check(a);
+    } else {                           // general deg2: both checked
+      evalmark(a);
+      arr_check[a] = 1;
+      evalmark(b);
+      arr_check[b] = 1;
+    }
+  }
+
+  // Static form of isfinite(sum(fill(c, n))) for constant arrays that are checked.
+  void static_array_check(T c) {
+    if (!sr_isfinite(c)) {
+      bad = true;
+      return;
+    }
+    const double s = std::fabs(double(c)) * double(n_rows);
+    if (!(s <= double(SrM<T>::big))) bad = true;
+  }
+
+  int compute_need(int i) {
+    if (effleaf(i)) return need[i] = 0;
+    if (t.degree[i] == 1) return need[i] = compute_need(t.l[i]);
+    const int a = t.l[i], b = t.r[i];
+    const int na = compute_need(a), nb = compute_need(b);
+    if (effleaf(a)) return need[i] = nb;
+    if (effleaf(b)) return need[i] = na;
+    return need[i] = (na == nb) ? na + 1 : (na > nb ? na : nb);
+  }
+
+  // Leaf as a LOAD (push = false; PUSH is patched in later) or as a binary operand.
+  // is_operand: binary opcode base (variant FL/FR/CL/CR chosen from the leaf kind + side).
+  SrIns<T> leaf_ins(int i) {
+    SrIns<T> in{};
+    if (folded[i]) {
+      in.code = SR_OP_LOAD_CONST;
+      in.val = fold_val[i];
+      in.arg = 0xffffffffu;
+    } else if (t.constant[i]) {
+      in.code = SR_OP_LOAD_CONST;
+      in.val = t.val[i];
+      in.arg = with_const_index ? uint32_t(const_slot[i]) : 0xffffffffu;
+    } else {
+      in.code = SR_OP_LOAD_FEAT;
+      in.arg = uint32_t(t.feature[i]) - 1u;
+      in.val = T(0);
+    }
+    return in;
+  }
+  SrIns<T> operand_ins(int i, uint32_t bop, bool left) {
+    SrIns<T> in = leaf_ins(i);
+    const bool is_const = in.code == SR_OP_LOAD_CONST;
+    const uint32_t v = is_const ? (left ? SR_V_CL : SR_V_CR) : (left ? SR_V_FL : SR_V_FR);
+    in.code = SR_BIN_OPC(bop, v);
+    return in;
+  }
+
+  void emit_check(int i) {
+    if (!arr_check[i]) return;
+    if (effleaf(i) && (folded[i] || t.constant[i])) {
+      static_array_check(folded[i] ? fold_val[i] : t.val[i]);
+      return;
+    }
+    code.back().code |= SR_F_CHECK;
+    ++n_checks;
+  }
+
+  static void mark_push(SrIns<T>& in) {
+    // the first instruction of every subtree's code is a leaf LOAD
+    in.code = (in.code & ~0xffu) | ((in.code & 0xffu) + 2u);
+  }
+
+  void emit(int i) {
+    if (effleaf(i)) {
+      code.push_back(leaf_ins(i));
+      emit_check(i);
+      return;
+    }
+    const int d = t.degree[i];
+    ++n_ops;
+    if (d == 1) {
+      emit(t.l[i]);
+      SrIns<T> in{};
+      in.code = (SR_OP_UNARY0 + unary_id(i)) | (infsub[i] ? SR_F_INFSUB : 0u);
+      code.push_back(in);
+      emit_check(i);
+      return;
+    }
+    const int a = t.l[i], b = t.r[i];
+    const uint32_t bop = binary_id(i);
+    if (err != SR_OK) return;
+    if (effleaf(b)) {  // op(tos = left, operand = right leaf)
+      emit(a);
+      code.push_back(operand_ins(b, bop, false));
+    } else if (effleaf(a)) {  // op(operand = left leaf, tos = right)
+      emit(b);
+      code.push_back(operand_ins(a, bop, true));
+    } else if (need[a] >= need[b]) {  // left first, pushed; right in tos
+      emit(a);
+      const size_t start = code.size();
+      ++depth;
+      if (depth > max_depth) max_depth = depth;
+      emit(b);
+      mark_push(code[start]);
+      --depth;
+      SrIns<T> in{};
+      in.code = SR_BIN_OPC(bop, SR_V_SL);
+      code.push_back(in);
+    } else {  // right first, pushed; left in tos
+      emit(b);
+      const size_t start = code.size();
+      ++depth;
+      if (depth > max_depth) max_depth = depth;
+      emit(a);
+      mark_push(code[start]);
+      --depth;
+      SrIns<T> in{};
+      in.code = SR_BIN_OPC(bop, SR_V_SR);
+      code.push_back(in);
+    }
+    emit_check(i);
+  }
+
+  // Pre-order constant numbering (get_scalar_constants order).
+  void number_constants() {
+    const_slot.assign(t.n, -1);
+    uint32_t k = 0;
+    for (int64_t i = 0; i < t.n; ++i)
+      if (t.degree[i] == 0 && t.constant[i]) const_slot[i] = int32_t(k++);
+    n_consts = k;
+  }
+
+  bool run() {
+    if (!parse()) return false;
+    const int64_t n = t.n;
+    folded.assign(n, 0);
+    arr_check.assign(n, 0);
+    infsub.assign(n, 0);
+    fold_val.assign(n, T(0));
+    need.assign(n, 0);
+    number_constants();
+    if (with_const_index) {
+      // gradient programs keep every constant leaf live: no folding (is_const stays 0)
+      is_const.assign(n, 0);
+    } else {
+      mark_const();
+    }
+    evalmark(0);
+    arr_check[0] = 1;  // final is_bad_array check on the output
+    if (err != SR_OK) return false;
+    if (bad) {
+      code.clear();
+      return true;
+    }
+    compute_need(0);
+    emit(0);
+    if (err != SR_OK) return false;
+    if (bad) code.clear();
+    return true;
+  }
+};
+
+}  // namespace
+
+uint32_t sr_unary_id(const char* name) {
+  for (const auto& e : kUnary)
+    if (std::strcmp(e.name, name) == 0) return e.id;
+  return 0;
+}
+uint32_t sr_binary_id(const char* name) {
+  for (const auto& e : kBinary)
+    if (std::strcmp(e.name, name) == 0) return e.id;
+  return 0;
+}
+
+template <typename T>
+int sr_compile_batch(const sr_tree_batch& trees, const SrOpset& ops, int64_t n_rows, int64_t nfeatures,
+                     bool with_const_index, SrProgramBatch<T>* out, std::string* err) {
+  const int64_t nt = trees.n_trees;
+  if (nt < 0 || (nt > 0 && (!trees.offsets || !trees.degree || !trees.op || !trees.feature ||
+                            !trees.constant || !trees.val))) {
+    *err = "sr_tree_batch has NULL arrays";
+    return SR_ERR_INVALID_ARG;
+  }
+  struct PerTree {
+    std::vector<SrIns<T>> code;
+    uint8_t bad;
+    uint32_t checks, consts;
+    int depth;
+    int64_t nodes, ops;
+  };
+  std::vector<PerTree> per(size_t(nt > 0 ? nt : 0));
+  std::vector<int> errs(size_t(nt > 0 ? nt : 0), SR_OK);
+  std::vector<std::string> msgs;
+  const T* vals = static_cast<const T*>(trees.val);
+
+  auto work = [&](int64_t lo, int64_t hi) {
+    for (int64_t k = lo; k < hi; ++k) {
+      const int64_t b = trees.offsets[k], e = trees.offsets[k + 1];
+      TreeCompiler<T> tc(ops, n_rows, nfeatures, with_const_index);
+      tc.t.degree = trees.degree + b;
+      tc.t.op = trees.op + b;
+      tc.t.feature = trees.feature + b;
+      tc.t.constant = trees.constant + b;
+      tc.t.val = vals + b;
+      tc.t.n = e - b;
+      if (e < b) {
+        errs[k] = SR_ERR_BAD_TREE;
+        continue;
+      }
+      tc.run();
+      if (tc.err != SR_OK) {
+        errs[k] = tc.err;
+        continue;
+      }
+      PerTree& p = per[k];
+      p.code.swap(tc.code);
+      p.bad = (tc.bad || p.code.empty()) ? 1 : 0;
+      p.checks = tc.n_checks;
+      p.consts = tc.n_consts;
+      p.depth = tc.max_depth;
+      p.nodes = e - b;
+      p.ops = 0;
+      for (int64_t i = b; i < e; ++i) p.ops += trees.degree[i] > 0 ? 1 : 0;
+    }
+  };
+  int nthreads = 1;
+  if (nt >= 4096) {
+    unsigned hc = std::thread::hardware_concurrency();
+    nthreads = int(hc == 0 ? 4 : (hc > 16 ? 16 : hc));
+  }
+  if (nthreads <= 1) {
+    work(0, nt);
+  } else {
+    std::vector<std::thread> th;
+    const int64_t chunk = (nt + nthreads - 1) / nthreads;
+    for (int w = 0; w < nthreads; ++w) {
+      const int64_t lo = w * chunk, hi = (lo + chunk < nt) ? lo + chunk : nt;
+      if (lo >= hi) break;
+      th.emplace_back(work, lo, hi);
+    }
+    for (auto& x : th) x.join();
+  }
+  for (int64_t k = 0; k < nt; ++k)
+    if (errs[k] != SR_OK) {
+      *err = "tree " + std::to_string(k) + ": malformed tree or operator index";
+      return errs[k];
+    }
+  out->code.clear();
+  out->offsets.assign(size_t(nt + 1), 0);
+  out->static_bad.assign(size_t(nt), 0);
+  out->n_checks.assign(size_t(nt), 0);
+  out->n_consts.assign(size_t(nt), 0);
+  out->const_off.assign(size_t(nt + 1), 0);
+  out->max_depth = 0;
+  out->max_checks = 0;
+  out->total_nodes = 0;
+  out->total_ops = 0;
+  size_t total = 0;
+  for (int64_t k = 0; k < nt; ++k) total += per[k].code.size();
+  out->code.reserve(total);
+  for (int64_t k = 0; k < nt; ++k) {
+    const PerTree& p = per[k];
+    out->offsets[k] = uint32_t(out->code.size());
+    out->code.insert(out->code.end(), p.code.begin(), p.code.end());
+    out->static_bad[k] = p.bad;
+    out->n_checks[k] = p.checks;
+    out->n_consts[k] = p.consts;
+    out->const_off[k + 1] = out->const_off[k] + p.consts;
+    if (p.depth > out->max_depth) out->max_depth = p.depth;
+    if (int(p.checks) > out->max_checks) out->max_checks = int(p.checks);
+    out->total_nodes += p.nodes;
+    out->total_ops += p.ops;
+  }
+  out->offsets[nt] = uint32_t(out->code.size());
+  return SR_OK;
+}
+
+template int sr_compile_batch<float>(const sr_tree_batch&, const SrOpset&, int64_t, int64_t, bool,
+                                     SrProgramBatch<float>*, std::string*);
+template int sr_compile_batch<double>(const sr_tree_batch&, const SrOpset&, int64_t, int64_t, bool,
+                                      SrProgramBatch<double>*, std::string*);

@@ -1,0 +1,55 @@
+// sr_eval.h — kernel argument block and launchers shared by the kernels and the C ABI.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include "sr_ops.h"
+#include "../../include/sr_amd.h"
+
+enum { SR_MODE_LOSS = 0, SR_MODE_PRED = 1, SR_MODE_EXACT = 2 };
+enum { SR_TIER_BASIC = 0, SR_TIER_FULL = 1 };
+#define SR_MAX_FEATURES 16  // register-resident X tile: nfeatures <= 16
+
+template <typename T>
+struct SrEvalArgs {
+  // programs
+  const SrIns<T>* code;
+  const uint32_t* offsets;     // [n_trees + 1]
+  int n_trees;                 // trees (or listed trees in EXACT mode)
+  int trees_per_block;         // G
+  // data (per-feature rows, leading dimension ld; padded rows replicate row 0)
+  const T* X;
+  const T* y;                  // may be NULL (prediction only)
+  const T* w;                  // NULL -> unweighted
+  const int64_t* row_idx;      // GATHER mode: rows of the SubDataset
+  int64_t ld;
+  int64_t n_rows;              // rows evaluated
+  int nf;
+  int tiles_per_block;
+  int n_row_blocks;
+  T tbig;                      // |v| >= tbig may overflow the array-sum check
+  int loss_kind;
+  // outputs
+  double* part_sum;            // [n_trees][n_row_blocks]
+  uint32_t* part_flag;         // [n_trees][n_row_blocks]
+  T* pred;                     // PRED: [n_trees][pred_ld]
+  int64_t pred_ld;
+  // EXACT mode
+  const int64_t* tree_list;    // listed trees; check_sums row = position in the list
+  int max_checks;
+  double* check_sums;          // [n_list][max_checks]
+  double scale;
+};
+
+template <typename T, int MODE, bool GATHER, int TIER>
+hipError_t sr_dispatch_interp(const SrEvalArgs<T>& a, int n_blocks, hipStream_t s);
+template <typename T>
+size_t sr_interp_lds_bytes(int trees_per_block);
+
+template <typename T>
+hipError_t sr_launch_interp(const SrEvalArgs<T>& a, int mode, bool gather, int tier, int n_blocks, hipStream_t s);
+hipError_t sr_launch_reduce(const double* part_sum, const uint32_t* part_flag, int n_trees, int n_row_blocks,
+                            const uint8_t* static_bad, double* out_sum, uint32_t* out_flag, hipStream_t s);
+template <typename T>
+hipError_t sr_launch_transpose(const T* Xh_dev, int64_t nf, int64_t n, int64_t ld, T* Xd, hipStream_t s);
+template <typename T>
+hipError_t sr_launch_pad(T* v, int64_t n, int64_t ld, T pad_value, int replicate_first, hipStream_t s);

@@ -1,0 +1,281 @@
+// sr_ops.h — operator catalog for the MI355X evaluator (host + device).
+//
+// Every operator the device interpreter understands, with the exact semantics the
+// reference attaches to it:
+//   * arithmetic `+ - * /` are plain IEEE ops (Options.jl OP_MAP keeps `/` as IEEE `/`,
+//     src/Options.jl:182-202);
+//   * the "safe" operators return NaN outside their domain (src/Operators.jl:35-76);
+//   * `square/cube/neg/relu/greater/less/cond/logical_*` follow src/Operators.jl:81-124,
+//     including Julia's Bool*Float "strong zero" (`false * x == copysign(0, x)`);
+//   * `max/min/mod/sign/round` follow Julia Base float semantics.
+// The same functions are used by the host-side program compiler for constant folding
+// (DynamicExpressions' constant-subtree fast path) and by the HIP kernel.
+#pragma once
+#include <stdint.h>
+#include <math.h>
+
+#if defined(__HIPCC__)
+#include <hip/hip_runtime.h>
+#define SR_HD __host__ __device__
+#else
+#define SR_HD
+#endif
+
+// ---------------------------------------------------------------------------------------
+// Operator ids (semantic; independent of the position inside options.operators).
+// ---------------------------------------------------------------------------------------
+enum SrUnaryOp : uint32_t {
+  SR_U_NONE = 0,
+  SR_U_NEG, SR_U_SQUARE, SR_U_CUBE, SR_U_EXP, SR_U_COS, SR_U_SIN, SR_U_TAN,
+  SR_U_LOG, SR_U_LOG2, SR_U_LOG10, SR_U_LOG1P, SR_U_SQRT, SR_U_ABS, SR_U_SIGN,
+  SR_U_TANH, SR_U_SINH, SR_U_COSH, SR_U_ATAN, SR_U_ASIN, SR_U_ACOS, SR_U_ACOSH,
+  SR_U_ATANH, SR_U_ASINH, SR_U_RELU, SR_U_INV, SR_U_ERF, SR_U_ERFC, SR_U_GAMMA,
+  SR_U_ROUND, SR_U_FLOOR, SR_U_CEIL, SR_U_EXP2, SR_U_EXPM1,
+  SR_U_COUNT
+};
+
+enum SrBinaryOp : uint32_t {
+  SR_B_NONE = 0,
+  SR_B_ADD, SR_B_SUB, SR_B_MUL, SR_B_DIV, SR_B_POW, SR_B_MAX, SR_B_MIN, SR_B_MOD,
+  SR_B_GREATER, SR_B_LESS, SR_B_GREATER_EQUAL, SR_B_LESS_EQUAL, SR_B_COND,
+  SR_B_LOGICAL_OR, SR_B_LOGICAL_AND, SR_B_ATAN2,
+  SR_B_COUNT
+};
+
+// Elementwise losses (LossFunctions.jl SupervisedLoss value at (output, target)).
+enum SrLossKind : int32_t {
+  SR_LOSS_L2 = 0,   // L2DistLoss: abs2(output - target)   (default, src/Options.jl:772)
+  SR_LOSS_L1 = 1,   // L1DistLoss: abs(output - target)
+};
+
+// ---------------------------------------------------------------------------------------
+// Program instruction (one per evaluated node; 16 bytes for f32 and f64).
+//   code bits 0-7 : combined opcode (what to do + where the operand comes from):
+//       SR_OP_LOAD_FEAT / _CONST [/ _PUSH]           top-of-stack <- leaf (push old tos first)
+//       SR_OP_UNARY0 + u                               tos <- op_u(tos)
+//       SR_OP_BINARY0 + 6*(b-1) + variant              tos <- op_b(.,.) with operand variant:
+//           SR_V_SL: op(pop, tos)   SR_V_SR: op(tos, pop)
+//           SR_V_FL: op(X[f], tos)  SR_V_FR: op(tos, X[f])
+//           SR_V_CL: op(c, tos)     SR_V_CR: op(tos, c)
+//   code bit  8   : CHECK   this node's output array is validity-checked (DE early exit)
+//   code bit  9   : INFSUB  fused unary: non-finite input -> +Inf output (DE fused kernels)
+//   arg           : 0-based feature index (FEAT operands) / constant slot (gradient programs)
+//   val           : constant (CONST operands)
+// ---------------------------------------------------------------------------------------
+enum : uint32_t {
+  SR_OP_LOAD_FEAT = 0u, SR_OP_LOAD_CONST = 1u, SR_OP_LOAD_FEAT_PUSH = 2u, SR_OP_LOAD_CONST_PUSH = 3u,
+  SR_OP_UNARY0 = 3u,    // opcode = SR_OP_UNARY0 + SrUnaryOp (1..)
+  SR_OP_BINARY0 = 64u,  // opcode = SR_OP_BINARY0 + 6*(SrBinaryOp-1) + variant
+  SR_V_SL = 0u, SR_V_SR = 1u, SR_V_FL = 2u, SR_V_FR = 3u, SR_V_CL = 4u, SR_V_CR = 5u,
+  SR_F_CHECK = 1u << 8, SR_F_INFSUB = 1u << 9,
+};
+static_assert(SR_OP_UNARY0 + SR_U_COUNT <= SR_OP_BINARY0, "unary opcode range overlaps binary range");
+static_assert(SR_OP_BINARY0 + 6 * SR_B_COUNT <= 256, "binary opcode range exceeds 8 bits");
+#define SR_OPC(c) ((c) & 0xffu)
+#define SR_BIN_OPC(b, v) (SR_OP_BINARY0 + 6u * ((b) - 1u) + (v))
+
+template <typename T>
+struct alignas(16) SrIns {
+  uint32_t code;
+  uint32_t arg;
+  T val;
+};
+static_assert(sizeof(SrIns<float>) == 16, "f32 instruction must be 16 bytes");
+static_assert(sizeof(SrIns<double>) == 16, "f64 instruction must be 16 bytes");
+
+// ---------------------------------------------------------------------------------------
+// Type-dispatched libm (host: libm; device: ROCm OCML through the HIP math headers).
+// ---------------------------------------------------------------------------------------
+template <typename T> struct SrM;
+template <> struct SrM<float> {
+  static SR_HD inline float exp(float x) { return ::expf(x); }
+  static SR_HD inline float cos(float x) { return ::cosf(x); }
+  static SR_HD inline float sin(float x) { return ::sinf(x); }
+  static SR_HD inline float tan(float x) { return ::tanf(x); }
+  static SR_HD inline float log(float x) { return ::logf(x); }
+  static SR_HD inline float log2(float x) { return ::log2f(x); }
+  static SR_HD inline float log10(float x) { return ::log10f(x); }
+  static SR_HD inline float log1p(float x) { return ::log1pf(x); }
+  static SR_HD inline float sqrt(float x) { return ::sqrtf(x); }
+  static SR_HD inline float tanh(float x) { return ::tanhf(x); }
+  static SR_HD inline float sinh(float x) { return ::sinhf(x); }
+  static SR_HD inline float cosh(float x) { return ::coshf(x); }
+  static SR_HD inline float atan(float x) { return ::atanf(x); }
+  static SR_HD inline float asin(float x) { return ::asinf(x); }
+  static SR_HD inline float acos(float x) { return ::acosf(x); }
+  static SR_HD inline float acosh(float x) { return ::acoshf(x); }
+  static SR_HD inline float atanh(float x) { return ::atanhf(x); }
+  static SR_HD inline float asinh(float x) { return ::asinhf(x); }
+  static SR_HD inline float erf(float x) { return ::erff(x); }
+  static SR_HD inline float erfc(float x) { return ::erfcf(x); }
+  static SR_HD inline float tgamma(float x) { return ::tgammaf(x); }
+  static SR_HD inline float rint(float x) { return ::rintf(x); }
+  static SR_HD inline float floor(float x) { return ::floorf(x); }
+  static SR_HD inline float ceil(float x) { return ::ceilf(x); }
+  static SR_HD inline float exp2(float x) { return ::exp2f(x); }
+  static SR_HD inline float expm1(float x) { return ::expm1f(x); }
+  static SR_HD inline float pow(float x, float y) { return ::powf(x, y); }
+  static SR_HD inline float fmod(float x, float y) { return ::fmodf(x, y); }
+  static SR_HD inline float atan2(float y, float x) { return ::atan2f(y, x); }
+  static SR_HD inline float trunc(float x) { return ::truncf(x); }
+  static SR_HD inline float copysign(float x, float y) { return ::copysignf(x, y); }
+  static SR_HD inline float fabs(float x) { return ::fabsf(x); }
+  // Julia exp(::Float32) returns Inf above MAX_EXP = 88.72284f0 (base/special/exp.jl).
+  static constexpr float max_exp = 88.72284f;
+  static constexpr float big = 3.40282347e38f;
+};
+template <> struct SrM<double> {
+  static SR_HD inline double exp(double x) { return ::exp(x); }
+  static SR_HD inline double cos(double x) { return ::cos(x); }
+  static SR_HD inline double sin(double x) { return ::sin(x); }
+  static SR_HD inline double tan(double x) { return ::tan(x); }
+  static SR_HD inline double log(double x) { return ::log(x); }
+  static SR_HD inline double log2(double x) { return ::log2(x); }
+  static SR_HD inline double log10(double x) { return ::log10(x); }
+  static SR_HD inline double log1p(double x) { return ::log1p(x); }
+  static SR_HD inline double sqrt(double x) { return ::sqrt(x); }
+  static SR_HD inline double tanh(double x) { return ::tanh(x); }
+  static SR_HD inline double sinh(double x) { return ::sinh(x); }
+  static SR_HD inline double cosh(double x) { return ::cosh(x); }
+  static SR_HD inline double atan(double x) { return ::atan(x); }
+  static SR_HD inline double asin(double x) { return ::asin(x); }
+  static SR_HD inline double acos(double x) { return ::acos(x); }
+  static SR_HD inline double acosh(double x) { return ::acosh(x); }
+  static SR_HD inline double atanh(double x) { return ::atanh(x); }
+  static SR_HD inline double asinh(double x) { return ::asinh(x); }
+  static SR_HD inline double erf(double x) { return ::erf(x); }
+  static SR_HD inline double erfc(double x) { return ::erfc(x); }
+  static SR_HD inline double tgamma(double x) { return ::tgamma(x); }
+  static SR_HD inline double rint(double x) { return ::rint(x); }
+  static SR_HD inline double floor(double x) { return ::floor(x); }
+  static SR_HD inline double ceil(double x) { return ::ceil(x); }
+  static SR_HD inline double exp2(double x) { return ::exp2(x); }
+  static SR_HD inline double expm1(double x) { return ::expm1(x); }
+  static SR_HD inline double pow(double x, double y) { return ::pow(x, y); }
+  static SR_HD inline double fmod(double x, double y) { return ::fmod(x, y); }
+  static SR_HD inline double atan2(double y, double x) { return ::atan2(y, x); }
+  static SR_HD inline double trunc(double x) { return ::trunc(x); }
+  static SR_HD inline double copysign(double x, double y) { return ::copysign(x, y); }
+  static SR_HD inline double fabs(double x) { return ::fabs(x); }
+  static constexpr double max_exp = 709.7827128933841;
+  static constexpr double big = 1.7976931348623157e308;
+};
+
+template <typename T> SR_HD inline T sr_qnan() { return T(__builtin_nan("")); }
+template <typename T> SR_HD inline T sr_inf() { return T(__builtin_inf()); }
+template <typename T> SR_HD inline bool sr_isfinite(T x) { return __builtin_isfinite(x); }
+template <typename T> SR_HD inline bool sr_isnan(T x) { return __builtin_isnan(x); }
+// Julia Bool*Float: true*x == x, false*x == copysign(0, x)   (Base: bool.jl)
+template <typename T> SR_HD inline T sr_bool_mul(bool b, T x) { return b ? x : SrM<T>::copysign(T(0), x); }
+
+// ---------------------------------------------------------------------------------------
+// Unary operators.
+// ---------------------------------------------------------------------------------------
+template <typename T>
+SR_HD inline T sr_unary(uint32_t op, T x) {
+  using M = SrM<T>;
+  switch (op) {
+    case SR_U_NEG: return -x;
+    case SR_U_SQUARE: return x * x;                       // Operators.jl:81
+    case SR_U_CUBE: return x * x * x;                     // Operators.jl:82
+    case SR_U_EXP: return x > M::max_exp ? sr_inf<T>() : M::exp(x);
+    case SR_U_COS: return M::cos(x);
+    case SR_U_SIN: return M::sin(x);
+    case SR_U_TAN: return M::tan(x);
+    case SR_U_LOG: return x > T(0) ? M::log(x) : sr_qnan<T>();        // safe_log  :50-52
+    case SR_U_LOG2: return x > T(0) ? M::log2(x) : sr_qnan<T>();      // safe_log2 :53-55
+    case SR_U_LOG10: return x > T(0) ? M::log10(x) : sr_qnan<T>();    // safe_log10 :56-58
+    case SR_U_LOG1P: return x > T(-1) ? M::log1p(x) : sr_qnan<T>();   // safe_log1p :59-61
+    case SR_U_SQRT: return x >= T(0) ? M::sqrt(x) : sr_qnan<T>();     // safe_sqrt :74-76
+    case SR_U_ABS: return x < T(0) ? -x : (x == T(0) ? T(0) : x);
+    case SR_U_SIGN: return x < T(0) ? T(-1) : (x > T(0) ? T(1) : x);  // Julia sign (NaN -> NaN)
+    case SR_U_TANH: return M::tanh(x);
+    case SR_U_SINH: return M::sinh(x);
+    case SR_U_COSH: return M::cosh(x);
+    case SR_U_ATAN: return M::atan(x);
+    case SR_U_ASIN: return (T(-1) <= x && x <= T(1)) ? M::asin(x) : sr_qnan<T>();   // :62-64
+    case SR_U_ACOS: return (T(-1) <= x && x <= T(1)) ? M::acos(x) : sr_qnan<T>();   // :65-67
+    case SR_U_ACOSH: return x >= T(1) ? M::acosh(x) : sr_qnan<T>();                 // :68-70
+    case SR_U_ATANH: return (T(-1) <= x && x <= T(1)) ? M::atanh(x) : sr_qnan<T>(); // :71-73
+    case SR_U_ASINH: return M::asinh(x);
+    case SR_U_RELU: return sr_bool_mul<T>(x > T(0), x);                              // :115
+    case SR_U_INV: return T(1) / x;
+    case SR_U_ERF: return M::erf(x);
+    case SR_U_ERFC: return M::erfc(x);
+    case SR_U_GAMMA: { T g = M::tgamma(x); return __builtin_isinf(g) ? sr_qnan<T>() : g; } // :14-17
+    case SR_U_ROUND: return M::rint(x);   // Julia round: RoundNearest (ties to even)
+    case SR_U_FLOOR: return M::floor(x);
+    case SR_U_CEIL: return M::ceil(x);
+    case SR_U_EXP2: return M::exp2(x);
+    case SR_U_EXPM1: return M::expm1(x);
+    default: return sr_qnan<T>();
+  }
+}
+
+// safe_pow (src/Operators.jl:35-49): NaN on the invalid branches, else x^y.
+template <typename T>
+SR_HD inline T sr_safe_pow(T x, T y) {
+  const bool isint = (y - SrM<T>::trunc(y)) == T(0);   // Julia isinteger (false for Inf/NaN)
+  if (isint) {
+    if (y < T(0) && x == T(0)) return sr_qnan<T>();
+  } else {
+    if (y > T(0) && x < T(0)) return sr_qnan<T>();
+    if (y < T(0) && x <= T(0)) return sr_qnan<T>();
+  }
+  return SrM<T>::pow(x, y);
+}
+
+// Julia Base.max / Base.min on floats: NaN-propagating, -0.0 < 0.0.
+template <typename T>
+SR_HD inline T sr_jl_max(T x, T y) {
+  if (sr_isnan(x)) return x;
+  if (sr_isnan(y)) return y;
+  const bool sx = __builtin_signbit(x) != 0, sy = __builtin_signbit(y) != 0;
+  return (y > x || (sx && !sy && x == y)) ? y : x;
+}
+template <typename T>
+SR_HD inline T sr_jl_min(T x, T y) {
+  if (sr_isnan(x)) return x;
+  if (sr_isnan(y)) return y;
+  const bool sx = __builtin_signbit(x) != 0, sy = __builtin_signbit(y) != 0;
+  return (y < x || (sy && !sx && x == y)) ? y : x;
+}
+// Julia Base.mod on floats: r = rem(x, y); r == 0 -> copysign(r, y); sign mismatch -> r + y.
+template <typename T>
+SR_HD inline T sr_jl_mod(T x, T y) {
+  const T r = SrM<T>::fmod(x, y);
+  if (r == T(0)) return SrM<T>::copysign(r, y);
+  if ((r > T(0)) != (y > T(0))) return r + y;
+  return r;
+}
+
+template <typename T>
+SR_HD inline T sr_binary(uint32_t op, T x, T y) {
+  switch (op) {
+    case SR_B_ADD: return x + y;
+    case SR_B_SUB: return x - y;
+    case SR_B_MUL: return x * y;
+    case SR_B_DIV: return x / y;
+    case SR_B_POW: return sr_safe_pow<T>(x, y);
+    case SR_B_MAX: return sr_jl_max<T>(x, y);
+    case SR_B_MIN: return sr_jl_min<T>(x, y);
+    case SR_B_MOD: return sr_jl_mod<T>(x, y);
+    case SR_B_GREATER: return (x > y) ? T(1) : T(0);          // Operators.jl:98-100
+    case SR_B_LESS: return (x < y) ? T(1) : T(0);             // :101-103
+    case SR_B_GREATER_EQUAL: return (x >= y) ? T(1) : T(0);   // :104-106
+    case SR_B_LESS_EQUAL: return (x <= y) ? T(1) : T(0);      // :107-109
+    case SR_B_COND: return sr_bool_mul<T>(x > T(0), y);       // :110-112
+    case SR_B_LOGICAL_OR: return ((x > T(0)) || (y > T(0))) ? T(1) : T(0);   // :118-120
+    case SR_B_LOGICAL_AND: return ((x > T(0)) && (y > T(0))) ? T(1) : T(0);  // :121-123
+    case SR_B_ATAN2: return SrM<T>::atan2(x, y);              // Julia atan(y, x) with (x=y_arg)
+    default: return sr_qnan<T>();
+  }
+}
+
+// Elementwise loss value.
+template <typename T>
+SR_HD inline T sr_elem_loss(int32_t kind, T pred, T target) {
+  const T d = pred - target;
+  if (kind == SR_LOSS_L1) return d < T(0) ? -d : d;
+  return d * d;
+}

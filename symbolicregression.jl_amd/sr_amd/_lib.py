@@ -1,0 +1,163 @@
+"""ctypes binding of the C ABI in ``include/sr_amd.h`` (``lib/libsr_amd.so``).
+
+This is the same binding a Julia ``ccall`` wrapper makes; Python uses it for the
+host-side mirror of SymbolicRegression's scoring API and for the tests / benchmark.  There is no
+fallback: if the shared library is missing the import fails loudly.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+from ctypes import POINTER, c_char_p, c_double, c_int, c_int64, c_uint8, c_uint16, c_uint32, c_void_p
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.environ.get(
+    "SR_AMD_LIB", os.path.join(os.path.dirname(_HERE), "lib", "libsr_amd.so")
+)
+
+SR_OK = 0
+SR_ERR_INVALID_ARG = -1
+SR_ERR_HIP = -2
+SR_ERR_UNSUPPORTED_OP = -3
+SR_ERR_BAD_TREE = -4
+SR_ERR_TOO_DEEP = -5
+SR_ERR_NO_DEVICE = -6
+
+SR_DTYPE_F32 = 0
+SR_DTYPE_F64 = 1
+SR_LOSS_L2DIST = 0
+SR_LOSS_L1DIST = 1
+
+SR_FLAG_NONFINITE = 1
+SR_FLAG_BIG = 2
+SR_FLAG_STATIC = 4
+
+# Every symbol include/sr_amd.h declares (checked by tests/test_abi.py).
+EXPORTED_SYMBOLS = (
+    "sr_last_error",
+    "sr_version",
+    "sr_device_count",
+    "sr_init",
+    "sr_shutdown",
+    "sr_register_opset",
+    "sr_dataset_upload",
+    "sr_dataset_free",
+    "sr_dataset_info",
+    "sr_eval_loss_batch",
+    "sr_eval_tree_array",
+    "sr_eval_loss_partials",
+    "sr_max_checks",
+    "sr_exact_check_partials",
+    "sr_finalize_losses",
+    "sr_dataset_denominator",
+    "sr_eval_grad_batch",
+    "sr_compile_info",
+    "sr_last_kernel_ms",
+)
+
+
+class SRError(RuntimeError):
+    """Error returned by libsr_amd (status code + sr_last_error message)."""
+
+    def __init__(self, code: int, msg: str):
+        super().__init__(f"libsr_amd error {code}: {msg}")
+        self.code = code
+
+
+class UnsupportedOperatorError(SRError):
+    pass
+
+
+class SrTreeBatch(ctypes.Structure):
+    _fields_ = [
+        ("n_trees", c_int64),
+        ("offsets", POINTER(c_int64)),
+        ("degree", POINTER(c_uint8)),
+        ("op", POINTER(c_uint8)),
+        ("feature", POINTER(c_uint16)),
+        ("constant", POINTER(c_uint8)),
+        ("val", c_void_p),
+    ]
+
+
+def _load():
+    if not os.path.exists(LIB_PATH):
+        raise ImportError(
+            f"libsr_amd.so not found at {LIB_PATH}: build it with `make -C symbolicregression.jl_amd` "
+            "(or __graft_entry__.build()); there is no CPU fallback for the device path"
+        )
+    lib = ctypes.CDLL(LIB_PATH)
+    P = c_void_p
+    proto = {
+        "sr_last_error": (c_char_p, []),
+        "sr_version": (c_int, []),
+        "sr_device_count": (c_int, [POINTER(c_int)]),
+        "sr_init": (c_int, [c_int, POINTER(P)]),
+        "sr_shutdown": (c_int, [P]),
+        "sr_register_opset": (
+            c_int,
+            [P, c_int, POINTER(c_char_p), c_int, POINTER(c_char_p), POINTER(c_int)],
+        ),
+        "sr_dataset_upload": (c_int, [P, c_int, P, c_int64, c_int64, P, P, POINTER(P)]),
+        "sr_dataset_free": (c_int, [P]),
+        "sr_dataset_info": (c_int, [P, POINTER(c_int), POINTER(c_int64), POINTER(c_int64)]),
+        "sr_eval_loss_batch": (
+            c_int,
+            [P, P, c_int, POINTER(SrTreeBatch), P, c_int64, c_int, P, P],
+        ),
+        "sr_eval_tree_array": (c_int, [P, P, c_int, POINTER(SrTreeBatch), P, c_int64, P, P]),
+        "sr_eval_loss_partials": (
+            c_int,
+            [P, P, c_int, POINTER(SrTreeBatch), c_int64, c_int, P, P, c_int],
+        ),
+        "sr_max_checks": (c_int, [P, c_int, POINTER(SrTreeBatch), POINTER(c_int)]),
+        "sr_exact_check_partials": (
+            c_int,
+            [P, P, c_int, POINTER(SrTreeBatch), P, c_int64, c_int, P],
+        ),
+        "sr_finalize_losses": (
+            c_int,
+            [c_int, c_int64, P, P, c_double, P, c_int64, c_int, P, P, P],
+        ),
+        "sr_dataset_denominator": (c_int, [P, POINTER(c_double)]),
+        "sr_eval_grad_batch": (
+            c_int,
+            [P, P, c_int, POINTER(SrTreeBatch), P, c_int64, c_int, P, P, P],
+        ),
+        "sr_compile_info": (
+            c_int,
+            [c_int, c_int, POINTER(c_char_p), c_int, POINTER(c_char_p), POINTER(SrTreeBatch), c_int64,
+             c_int64, P, P, POINTER(c_int), P, c_int64],
+        ),
+        "sr_last_kernel_ms": (c_int, [P, POINTER(c_double), POINTER(c_double)]),
+    }
+    for name, (res, args) in proto.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    return lib
+
+
+lib = _load()
+
+
+def last_error() -> str:
+    msg = lib.sr_last_error()
+    return msg.decode() if msg else ""
+
+
+def check(rc: int) -> None:
+    if rc == SR_OK:
+        return
+    msg = last_error()
+    if rc == SR_ERR_UNSUPPORTED_OP:
+        raise UnsupportedOperatorError(rc, msg)
+    raise SRError(rc, msg)
+
+
+def device_count() -> int:
+    c = c_int(0)
+    rc = lib.sr_device_count(ctypes.byref(c))
+    if rc != SR_OK:
+        return 0
+    return int(c.value)

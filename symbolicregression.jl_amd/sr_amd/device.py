@@ -1,0 +1,64 @@
+"""Per-process device context: one ``sr_ctx`` per GPU (one process per GPU; LOCAL_RANK picks it)."""
+from __future__ import annotations
+
+import ctypes
+import os
+import threading
+
+from . import _lib
+
+_lock = threading.Lock()
+_contexts: dict = {}
+
+
+class DeviceContext:
+    def __init__(self, device: int):
+        self.device = device
+        h = ctypes.c_void_p()
+        _lib.check(_lib.lib.sr_init(device, ctypes.byref(h)))
+        self.handle = h
+        self._opsets: dict = {}
+
+    def opset_id(self, operators) -> int:
+        key = operators.key()
+        oid = self._opsets.get(key)
+        if oid is None:
+            un = (ctypes.c_char_p * max(1, len(operators.unaops)))(*[s.encode() for s in operators.unaops])
+            bi = (ctypes.c_char_p * max(1, len(operators.binops)))(*[s.encode() for s in operators.binops])
+            out = ctypes.c_int()
+            _lib.check(
+                _lib.lib.sr_register_opset(
+                    self.handle, len(operators.unaops), un, len(operators.binops), bi, ctypes.byref(out)
+                )
+            )
+            oid = int(out.value)
+            self._opsets[key] = oid
+        return oid
+
+    def last_kernel_ms(self):
+        a, b = ctypes.c_double(), ctypes.c_double()
+        _lib.check(_lib.lib.sr_last_kernel_ms(self.handle, ctypes.byref(a), ctypes.byref(b)))
+        return float(a.value), float(b.value)
+
+    def close(self):
+        if self.handle:
+            _lib.lib.sr_shutdown(self.handle)
+            self.handle = None
+
+
+def default_device() -> int:
+    return int(os.environ.get("SR_AMD_DEVICE", os.environ.get("LOCAL_RANK", "0")))
+
+
+def get_context(device: int | None = None) -> DeviceContext:
+    dev = default_device() if device is None else int(device)
+    with _lock:
+        ctx = _contexts.get(dev)
+        if ctx is None:
+            ctx = DeviceContext(dev)
+            _contexts[dev] = ctx
+        return ctx
+
+
+def device_available() -> bool:
+    return _lib.device_count() > 0

@@ -1,0 +1,77 @@
+"""``Options`` — the subset of SymbolicRegression's options that the scoring path reads.
+
+Reference: src/Options.jl:502-1214 (constructor + defaults), src/OptionsStruct.jl:177-259 (struct).
+The scoring path uses: the operator enum (after OP_MAP), ``elementwise_loss`` (default
+``L2DistLoss()``, src/Options.jl:772), ``parsimony`` (stored as Float32, src/OptionsStruct.jl:198),
+``loss_function``/``loss_function_expression`` (custom objectives stay on the caller's CPU path) and
+the new ``device`` switch that selects this evaluator (it rides next to ``turbo``/``bumper``,
+src/OptionsStruct.jl:186-187).
+"""
+from __future__ import annotations
+
+import numpy as np
+
+from .operators import OperatorEnum
+
+LOSSES = {"L2DistLoss": 0, "L2DistLoss()": 0, "l2": 0, "L1DistLoss": 1, "L1DistLoss()": 1, "l1": 1}
+
+
+class Options:
+    def __init__(
+        self,
+        binary_operators=("+", "-", "/", "*"),
+        unary_operators=(),
+        *,
+        operators: OperatorEnum | None = None,
+        elementwise_loss="L2DistLoss",
+        loss_function=None,
+        loss_function_expression=None,
+        parsimony: float = 0.0,
+        maxsize: int = 30,
+        maxdepth: int | None = None,
+        populations: int = 31,
+        population_size: int = 27,
+        ncycles_per_iteration: int = 380,
+        tournament_selection_n: int = 15,
+        tournament_selection_p: float = 0.982,
+        batching: bool = False,
+        batch_size: int = 50,
+        turbo: bool = False,
+        bumper: bool = False,
+        device: str = "mi355x",
+        deterministic: bool = False,
+        seed=None,
+    ):
+        self.operators = operators if operators is not None else OperatorEnum(unary_operators, binary_operators)
+        if callable(elementwise_loss) and not isinstance(elementwise_loss, str):
+            raise ValueError("custom elementwise loss functions stay on the reference CPU path")
+        if elementwise_loss not in LOSSES:
+            raise ValueError(f"elementwise_loss {elementwise_loss!r} is not supported by the device path")
+        self.elementwise_loss = elementwise_loss
+        self.loss_kind = LOSSES[elementwise_loss]
+        self.loss_function = loss_function
+        self.loss_function_expression = loss_function_expression
+        self.parsimony = np.float32(parsimony)
+        self.maxsize = int(maxsize)
+        self.maxdepth = int(maxdepth) if maxdepth is not None else int(maxsize)
+        self.populations = populations
+        self.population_size = population_size
+        self.ncycles_per_iteration = ncycles_per_iteration
+        self.tournament_selection_n = tournament_selection_n
+        self.tournament_selection_p = tournament_selection_p
+        self.batching = batching
+        self.batch_size = batch_size
+        self.turbo = turbo
+        self.bumper = bumper
+        if device not in ("mi355x", "gpu", "hip"):
+            raise ValueError("this package implements only the MI355X device path (device='mi355x')")
+        self.device = "mi355x"
+        self.deterministic = deterministic
+        self.seed = seed
+
+    @property
+    def nops(self):
+        return self.operators.nops
+
+    def __repr__(self):
+        return f"Options(operators={self.operators!r}, elementwise_loss={self.elementwise_loss}, parsimony={self.parsimony})"

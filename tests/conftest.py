@@ -1,0 +1,40 @@
+"""Test configuration: GPU marker, import paths, and on-demand build of the two native libraries.
+
+`-m gpu` tests need an MI355X (they call libsr_amd.so); everything else runs on CPU.
+"""
+import os
+import subprocess
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+PKG = os.path.join(ROOT, "symbolicregression.jl_amd")
+for p in (ROOT, PKG, os.path.join(ROOT, "oracle")):
+    if p not in sys.path:
+        sys.path.insert(0, p)
+
+
+def _ensure_built():
+    lib = os.path.join(PKG, "lib", "libsr_amd.so")
+    if not os.path.exists(lib):
+        subprocess.run(["make", "-s", "-j8", "-C", PKG], check=True)
+    orc = os.path.join(ROOT, "oracle", "build", "liboracle.so")
+    if not os.path.exists(orc):
+        subprocess.run(["make", "-s", "-C", os.path.join(ROOT, "oracle")], check=True)
+
+
+_ensure_built()
+
+
+def pytest_configure(config):
+    config.addinivalue_line("markers", "gpu: needs an MI355X GPU (runs libsr_amd kernels)")
+    config.addinivalue_line("markers", "slow: long-running")
+
+
+@pytest.fixture(scope="session")
+def golden():
+    import json
+
+    with open(os.path.join(ROOT, "tests", "golden", "reference_known_answers.json")) as f:
+        return json.load(f)

@@ -1,0 +1,91 @@
+"""CPU: the tree compiler (csrc/sr_compile.cpp, via the host-only sr_compile_info entry point).
+
+The compiled programs are executed by tests/bytecode_vm.py (numpy restatement of the kernel's
+instruction semantics) and compared with the oracle: this pins constant folding, DE check placement,
+fused-unary detection and Sethi–Ullman ordering without a GPU.
+"""
+import numpy as np
+import pytest
+
+import bytecode_vm as vm
+from parity_util import rel, well_conditioned
+from oracle import Oracle
+from sr_amd import Options, flatten_trees, gen_random_population, parse_expression
+
+OPTS = dict(binary_operators=["+", "-", "*", "/"], unary_operators=["cos", "exp", "log"])
+
+
+def _data(n, seed):
+    rng = np.random.default_rng(seed)
+    X = rng.standard_normal((5, n)).astype(np.float32)
+    y = (2 * np.cos(X[3]) + X[0] ** 2 - 2).astype(np.float32)
+    return X, y
+
+
+@pytest.mark.parametrize("seed", [1, 2, 3])
+def test_compiled_programs_match_oracle(seed):
+    opts = Options(**OPTS)
+    X, y = _data(257, seed)
+    tb = flatten_trees(gen_random_population(1500, opts, 5, seed=seed), np.float32)
+    loss, comp = vm.eval_loss_batch(opts, tb, X, y)
+    good, ol, oc = well_conditioned(Oracle.from_options(opts), tb, X, y)
+    mism = np.nonzero(comp != oc)[0]
+    assert len(mism) == 0, mism[:10]
+    assert good.sum() > 0.85 * oc.sum()  # most complete trees are well-conditioned
+    assert rel(loss[good], ol[good]).max() < 1e-4
+
+
+def test_stack_depth_bound_for_maxsize_30():
+    # Sethi-Ullman: a tree needing d stack slots has >= 1 + 2*m(d-1) nodes, m(0)=2 -> d <= 3 at 30 nodes
+    opts = Options(**OPTS)
+    tb = flatten_trees(gen_random_population(3000, opts, 5, seed=9), np.float32)
+    _, _, _, depth = vm.compile_info(opts, tb, 100, 5, np.float32)
+    assert depth <= 3
+
+
+def test_program_shapes():
+    opts = Options(**OPTS)
+    cases = {
+        "x1": 1,                          # LOAD
+        "x1 * 3.0": 2,                    # LOAD, MUL c
+        "cos(3.0 * 2.0)": 1,              # folded constant tree
+        "cos(x1) + cos(x2)": 5,           # LOAD,COS, LOAD+PUSH,COS, ADD stack
+        "(x1 * 2.0) * (3.0 * 4.0)": 3,    # folded right child -> constant operand
+    }
+    trees = [parse_expression(e, opts) for e in cases]
+    tb = flatten_trees(trees, np.float32)
+    code, offs, bad, depth = vm.compile_info(opts, tb, 100, 5, np.float32)
+    assert list(np.diff(offs)) == list(cases.values())
+    assert not bad.any()
+    # CHECK bit placement: cos(x1) is a general unary -> x1's array is checked; root always checked
+    k = list(cases).index("cos(x1) + cos(x2)")
+    c = code["code"][offs[k]:offs[k + 1]]
+    checks = [(int(v) >> 8) & 1 for v in c]
+    assert checks == [1, 1, 1, 1, 1]
+    # fused unary: cos(x1 * 2.0) carries INFSUB and no CHECK on the inner product
+    tb2 = flatten_trees([parse_expression("cos(x1 * 2.0)", opts)], np.float32)
+    code2, offs2, _, _ = vm.compile_info(opts, tb2, 100, 5, np.float32)
+    c2 = [int(v) for v in code2["code"][:offs2[1]]]
+    assert [(v >> 8) & 1 for v in c2] == [0, 0, 1]
+    assert [(v >> 9) & 1 for v in c2] == [0, 0, 1]
+
+
+def test_static_incomplete():
+    opts = Options(**OPTS)
+    exprs = ["x1 + inf", "cos(inf)", "exp(1000.0)", "x1 * nan", "1e36 * 1.0", "x1 + 1.0"]
+    tb = flatten_trees([parse_expression(e, opts) for e in exprs], np.float32)
+    _, _, bad, _ = vm.compile_info(opts, tb, 1000, 5, np.float32)
+    # constant 1e36 filled over 1000 rows: its array sum overflows Float32 -> statically incomplete
+    assert list(bad) == [True, True, True, True, True, False]
+    _, _, bad1, _ = vm.compile_info(opts, tb, 1, 5, np.float32)
+    assert list(bad1) == [True, True, True, True, False, False]
+
+
+def test_bad_trees_rejected():
+    from sr_amd import Node, SRError
+
+    opts = Options(**OPTS)
+    with pytest.raises(SRError):
+        vm.compile_info(opts, flatten_trees([Node(feature=6)]), 10, 5, np.float32)
+    with pytest.raises(SRError):
+        vm.compile_info(opts, flatten_trees([Node(op=9, l=Node(feature=1))]), 10, 5, np.float32)

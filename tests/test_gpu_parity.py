@@ -1,0 +1,344 @@
+"""GPU parity: libsr_amd (HIP, through the C ABI) vs the CPU oracle and the reference's known answers.
+
+Bars (BASELINE.json north_star): per-tree `complete` flags bit-exact; losses within 1e-4 relative
+(f32) / 1e-10 relative (f64) of the oracle; predictions within the reference tests' tolerances.
+"""
+import ctypes
+
+import numpy as np
+import pytest
+
+import sr_amd
+from oracle import Oracle
+from sr_amd import (Dataset, Node, Options, batch, eval_loss, eval_loss_batch, eval_tree_array, eval_tree_array_batch,
+                    flatten_trees, gen_random_population, parse_expression)
+from sr_amd import _lib
+from parity_util import well_conditioned
+
+pytestmark = pytest.mark.gpu
+
+C2_OPTS = dict(binary_operators=["+", "-", "*", "/"], unary_operators=["cos", "exp", "log"])
+FULL_OPTS = dict(
+    binary_operators=["+", "-", "*", "/", "^", "max", "min", "mod", ">", "<", "cond", "logical_or"],
+    unary_operators=["cos", "exp", "log", "sin", "tan", "sqrt", "abs", "tanh", "neg", "square", "cube",
+                     "log1p", "atan", "asinh", "relu", "inv", "erf", "sign", "floor"],
+)
+
+
+def _dt(name):
+    return np.float32 if name == "float32" else np.float64
+
+
+def _c2_data(n, nf=5, dtype=np.float32, seed=2):
+    rng = np.random.default_rng(seed)
+    X = rng.standard_normal((nf, n)).astype(dtype)
+    y = (2 * np.cos(X[3].astype(np.float64)) + X[0].astype(np.float64) ** 2 - 2
+         + 0.1 * np.random.default_rng(seed + 1).standard_normal(n)).astype(dtype)
+    return X, y
+
+
+def _rel(a, b):
+    a = np.asarray(a, dtype=np.float64)
+    b = np.asarray(b, dtype=np.float64)
+    both_inf = np.isinf(a) & np.isinf(b) & (np.sign(a) == np.sign(b))
+    with np.errstate(invalid="ignore"):
+        return np.where(both_inf, 0.0, np.abs(a - b) / np.maximum(np.abs(b), 1e-30))
+
+
+# ------------------------------------------------------------------ reference known answers
+def test_golden_fused_shapes(golden):
+    g = golden["fused_shapes"]
+    opts = Options(binary_operators=g["binary_operators"], unary_operators=g["unary_operators"])
+    X = np.array(g["X"], dtype=np.float32)
+    trees = [parse_expression(c["expr"], opts) for c in g["cases"]]
+    out, comp = eval_tree_array_batch(trees, Dataset(X), opts)
+    for k, case in enumerate(g["cases"]):
+        assert comp[k], case["expr"]
+        err = np.abs(out[k].astype(np.float64) - np.array(case["expected"])) / X.shape[1]
+        assert np.all(err < g["tolerance_abs_over_N"]), (case["expr"], err.max())
+
+
+def test_golden_nan_detection(golden):
+    g = golden["nan_detection"]
+    opts = Options(binary_operators=g["binary_operators"], unary_operators=g["unary_operators"])
+    for case in g["cases"]:
+        dt = _dt(case["dtype"])
+        t = parse_expression(case["expr"], opts)
+        X = np.array(case["X"], dtype=dt)
+        _, complete = eval_tree_array(t, X, opts)
+        assert complete is g["expected_complete"], case
+        d = Dataset(X, np.zeros(X.shape[1], dtype=dt))
+        loss, comp = eval_loss_batch([t], d, opts)
+        assert not comp[0] and np.isinf(loss[0]), case
+
+
+def test_golden_batched_dataset_mse(golden):
+    g = golden["batched_mse"]
+    opts = Options(binary_operators=g["binary_operators"], unary_operators=g["unary_operators"])
+    d = Dataset(np.array(g["X"]), np.array(g["y"]))
+    t = parse_expression(g["expr"], opts)
+    for case in g["cases"]:
+        view = d if case["indices"] is None else batch(d, case["indices"])
+        assert eval_loss(t, view, opts) == pytest.approx(case["loss"], rel=1e-12)
+
+
+@pytest.mark.parametrize("loss_name", ["L1DistLoss", "L2DistLoss"])
+def test_golden_losses(golden, loss_name):
+    g = golden["losses"]
+    x = np.array(g["x"], dtype=np.float32)
+    y = np.array(g["y"], dtype=np.float32)
+    w = np.array(g["w"], dtype=np.float32)
+    opts = Options(binary_operators=["+"], unary_operators=[], elementwise_loss=loss_name)
+    t = parse_expression("x1", opts)
+    assert abs(float(eval_loss(t, Dataset(x[None, :], y), opts)) - g[loss_name]["mean"]) < g["tolerance"]
+    assert abs(float(eval_loss(t, Dataset(x[None, :], y, weights=w), opts)) - g[loss_name]["weighted"]) < g["tolerance"]
+
+
+@pytest.mark.parametrize("dtype", [np.float32, np.float64])
+def test_golden_safe_operators(golden, dtype):
+    g = golden["safe_operators"]
+    for case in g["unary"]:
+        opts = Options(binary_operators=["+"], unary_operators=[case["op"]])
+        out, _ = eval_tree_array(parse_expression(f"{case['op']}(x1)", opts), np.array([[case["x"]]], dtype=dtype), opts)
+        if case["expected"] == "nan":
+            assert np.isnan(out[0]), case
+        else:
+            assert abs(float(out[0]) - case["expected"]) < g["tolerance"], case
+    for case in g["binary"]:
+        opts = Options(binary_operators=[case["op"]], unary_operators=[])
+        t = Node(op=1, l=Node(feature=1), r=Node(feature=2))
+        out, _ = eval_tree_array(t, np.array([[case["x"]], [case["y"]]], dtype=dtype), opts)
+        if case["expected"] == "nan":
+            assert np.isnan(out[0]), case
+        else:
+            assert abs(float(out[0]) - case["expected"]) < g["tolerance"], case
+
+
+def test_golden_tree_construction(golden):
+    g = golden["tree_construction"]
+    for case in g["cases"]:
+        dt = _dt(case["dtype"])
+        una = case["unaop"]
+        opts = Options(binary_operators=g["binary_operators"], unary_operators=[una, "abs"],
+                       parsimony=g["parsimony_default"])
+        good = parse_expression(g["good_expr"].replace("UNAOP", una), opts)
+        bad = parse_expression(g["bad_expr"].replace("UNAOP", una), opts)
+        d = Dataset(np.array(case["X"], dtype=dt), np.array(case["y"], dtype=dt))
+        l = eval_loss(good, d, opts)
+        assert abs(float(l)) < case["tolerance"], (una, case["dtype"], float(l))
+        assert l == sr_amd.eval_cost(d, good, opts)[1]
+        assert sr_amd.eval_cost(d, good, opts)[0] < sr_amd.eval_cost(d, bad, opts)[0]
+
+
+# ------------------------------------------------------------------ random populations vs oracle
+@pytest.mark.parametrize("opts_kw,n,n_trees,seed", [
+    (C2_OPTS, 4096, 3000, 1),
+    (C2_OPTS, 5000, 1500, 7),      # ragged rows (not a multiple of the 1024-row tile)
+    (FULL_OPTS, 3000, 2000, 3),
+    (C2_OPTS, 97, 500, 11),        # fewer rows than one wave
+])
+def test_population_f32_vs_oracle(opts_kw, n, n_trees, seed):
+    opts = Options(**opts_kw)
+    X, y = _c2_data(n, seed=seed)
+    trees = gen_random_population(n_trees, opts, 5, max_size=30, seed=seed)
+    tb = flatten_trees(trees, np.float32)
+    loss, comp = eval_loss_batch(tb, Dataset(X, y), opts)
+    orc = Oracle.from_options(opts)
+    good, o_loss, o_comp = well_conditioned(orc, tb, X, y)
+    mism = np.nonzero(comp != o_comp)[0]
+    assert len(mism) == 0, [(int(k), sr_amd.string_tree(tb.tree(int(k)), opts.operators)) for k in mism[:5]]
+    assert np.all(np.isinf(loss[~comp]))
+    assert good.sum() > 0.8 * comp.sum()
+    r = _rel(loss[good], o_loss[good])
+    assert np.max(r) < 1e-4, (np.argmax(r), np.max(r))
+    assert np.median(r) < 1e-6
+    # against the reference-order accumulation (sequential f32 fold) too
+    ref_loss, _ = orc.eval_loss_batch(tb, X, y, accum="ref", n_threads=8)
+    assert np.max(_rel(loss[good], ref_loss[good])) < 1e-4
+
+
+def test_population_f64_vs_oracle():
+    opts = Options(**C2_OPTS)
+    X, y = _c2_data(3000, dtype=np.float64, seed=5)
+    trees = gen_random_population(1500, opts, 5, max_size=30, dtype=np.float64, seed=5)
+    tb = flatten_trees(trees, np.float64)
+    loss, comp = eval_loss_batch(tb, Dataset(X, y), opts)
+    o_loss, o_comp = Oracle.from_options(opts).eval_loss_batch(tb, X, y, accum="f64", n_threads=8)
+    assert np.array_equal(comp, o_comp)
+    r = _rel(loss[comp], o_loss[comp])
+    assert np.median(r) < 1e-13
+    assert np.quantile(r, 0.95) < 1e-10, np.quantile(r, 0.95)
+
+
+def test_predictions_vs_oracle():
+    opts = Options(**FULL_OPTS)
+    X, _ = _c2_data(777, seed=9)
+    trees = gen_random_population(300, opts, 5, seed=9)
+    tb = flatten_trees(trees, np.float32)
+    out, comp = eval_tree_array_batch(tb, Dataset(X), opts)
+    orc = Oracle.from_options(opts)
+    for k in range(tb.n_trees):
+        o, c = orc.eval_tree_array(tb, k, X)
+        assert comp[k] == c, (k, sr_amd.string_tree(tb.tree(k), opts.operators))
+        if c:
+            o64, c64 = orc.eval_tree_array(tb.astype(np.float64), k, X.astype(np.float64))
+            # rows whose f32 value is rounding-dominated (|f32 - f64| > 1e-5 rel) are excluded
+            okrow = np.abs(o.astype(np.float64) - o64) <= 1e-5 * np.maximum(np.abs(o64), 1e-3)
+            np.testing.assert_allclose(out[k][okrow], o[okrow], rtol=1e-4, atol=1e-6)
+
+
+def test_weighted_and_gather_vs_oracle():
+    opts = Options(**C2_OPTS)
+    X, y = _c2_data(6000, seed=13)
+    w = np.abs(np.random.default_rng(14).standard_normal(6000)).astype(np.float32) + 0.1
+    d = Dataset(X, y, weights=w)
+    trees = gen_random_population(800, opts, 5, seed=13)
+    tb = flatten_trees(trees, np.float32)
+    orc = Oracle.from_options(opts)
+    loss, comp = eval_loss_batch(tb, d, opts)
+    good, ol, oc = well_conditioned(orc, tb, X, y, w=w)
+    assert np.array_equal(comp, oc)
+    assert np.max(_rel(loss[good], ol[good])) < 1e-4
+    # SubDataset (minibatch with replacement): gather path
+    idx = np.random.default_rng(15).integers(0, 6000, size=1500)
+    sub = batch(d, idx)
+    loss, comp = eval_loss_batch(tb, sub, opts)
+    good, ol, oc = well_conditioned(orc, tb, X[:, idx], y[idx], w=w[idx])
+    assert np.array_equal(comp, oc)
+    assert np.max(_rel(loss[good], ol[good])) < 1e-4
+
+
+def test_l1_loss_vs_oracle():
+    opts = Options(**C2_OPTS, elementwise_loss="L1DistLoss")
+    X, y = _c2_data(2048, seed=21)
+    tb = flatten_trees(gen_random_population(600, opts, 5, seed=21), np.float32)
+    loss, comp = eval_loss_batch(tb, Dataset(X, y), opts)
+    good, ol, oc = well_conditioned(Oracle.from_options(opts), tb, X, y, loss_kind=1)
+    assert np.array_equal(comp, oc)
+    assert np.max(_rel(loss[good], ol[good])) < 1e-4
+
+
+# ------------------------------------------------------------------ edge cases
+def test_edge_trees():
+    opts = Options(binary_operators=["+", "-", "*", "/"], unary_operators=["cos", "exp", "log"])
+    X, y = _c2_data(3000, seed=31)
+    X[2, 17] = 1e30  # one huge value in feature 3
+    exprs = [
+        "x1", "2.5", "inf", "nan", "cos(3.0)", "cos(inf)", "exp(1000.0)", "x1 + inf", "x1 * nan",
+        "exp(x1 * 100.0)", "log(x2)", "log(0.0 * x1)", "x3 * 1e10", "x3 * x3",
+        "cos(x1 / 0.0)", "exp(cos(x1 * x2))", "(x1 + x2) * (x3 - x4)", "((x1 * x2) + (x3 * x4)) * ((x5 + x1) - (x2 * x3))",
+        "1e36 * 1.0", "x1 * 0.0 + 1e34", "exp(88.0 + x1 * 0.0)", "exp(89.0 + x1 * 0.0)",
+        "exp(-200.0 * x1)", "1.0 / (x1 - x1)", "(x1 - x1) / (x2 - x2)",
+    ]
+    trees = [parse_expression(e, opts) for e in exprs]
+    tb = flatten_trees(trees, np.float32)
+    loss, comp = eval_loss_batch(tb, Dataset(X, y), opts)
+    ol, oc = Oracle.from_options(opts).eval_loss_batch(tb, X, y, accum="f64")
+    for k, e in enumerate(exprs):
+        assert comp[k] == oc[k], (e, comp[k], oc[k])
+        if oc[k]:
+            assert _rel(loss[k], ol[k]) < 1e-4 or (np.isinf(loss[k]) and np.isinf(ol[k])), (e, loss[k], ol[k])
+
+
+def test_sum_overflow_exact_path():
+    """Values finite row by row but whose array sum overflows Float32: DE's isfinite(sum(x)) check
+    flags them; values just below the limit must stay complete (exact-sum path)."""
+    opts = Options(binary_operators=["+", "-", "*", "/"], unary_operators=["cos"])
+    n = 4000
+    X = np.ones((1, n), dtype=np.float32)
+    y = np.zeros(n, dtype=np.float32)
+    exprs = [
+        "x1 * 1e35",          # 4000 * 1e35 = 4e38 > FLT_MAX -> incomplete
+        "x1 * 5e34",          # 2e38 -> complete (the root check passes; loss itself overflows to Inf)
+        "cos(x1 * 1e35)",     # fused: child of cos is not array-checked; cos bounded -> complete
+        "cos(x1) * 1e35",     # 4000 * 0.54e35 = 2.16e38 -> complete
+        "cos(x1 * 0.0) * 1e35 + x1 * 0.0",  # 4e38 at a checked node -> incomplete
+    ]
+    trees = [parse_expression(e, opts) for e in exprs]
+    tb = flatten_trees(trees, np.float32)
+    _, comp = eval_loss_batch(tb, Dataset(X, y), opts)
+    _, oc = Oracle.from_options(opts).eval_loss_batch(tb, X, y)
+    assert list(comp) == list(oc), list(zip(exprs, comp, oc))
+    assert list(oc) == [False, True, True, True, False]
+
+
+def test_ragged_sizes_and_determinism():
+    opts = Options(**C2_OPTS)
+    trees = gen_random_population(400, opts, 5, seed=41)
+    tb = flatten_trees(trees, np.float32)
+    orc = Oracle.from_options(opts)
+    for n in (1, 2, 63, 64, 255, 1023, 1024, 1025, 4097):
+        X, y = _c2_data(n, seed=n)
+        d = Dataset(X, y)
+        l1, c1 = eval_loss_batch(tb, d, opts)
+        l2, c2 = eval_loss_batch(tb, d, opts)
+        assert np.array_equal(l1, l2) and np.array_equal(c1, c2)  # bit-reproducible
+        good, ol, oc = well_conditioned(orc, tb, X, y)
+        assert np.array_equal(c1, oc), n
+        assert np.max(_rel(l1[good], ol[good]), initial=0.0) < 1e-4, n
+
+
+def test_empty_batch_and_errors():
+    opts = Options(**C2_OPTS)
+    X, y = _c2_data(100)
+    d = Dataset(X, y)
+    loss, comp = eval_loss_batch([], d, opts)
+    assert loss.shape == (0,)
+    bad = Node(feature=9)  # feature out of range
+    with pytest.raises(sr_amd.SRError):
+        eval_loss_batch([bad], d, opts)
+    with pytest.raises(IndexError):
+        batch(d, [0, 100])
+
+
+# ------------------------------------------------------------------ large sizes: size-independent properties
+def test_large_rows_properties():
+    """1M rows (BASELINE C2 size): linear trees against closed forms computed in f64 by numpy."""
+    opts = Options(**C2_OPTS)
+    n = 1 << 20
+    X, y = _c2_data(n, seed=51)
+    d = Dataset(X, y)
+    exprs = ["x1", "x1 * 2.0", "x1 + x2", "cos(x4) * 2.0 + x1 * x1 - 2.0"]
+    trees = [parse_expression(e, opts) for e in exprs]
+    loss, comp = eval_loss_batch(trees, d, opts)
+    assert comp.all()
+    x = X.astype(np.float64)
+    yy = y.astype(np.float64)
+    pred = [x[0], x[0] * 2.0, x[0] + x[1]]
+    for k in range(3):
+        exact = np.mean((pred[k] - yy) ** 2)
+        assert _rel(loss[k], exact) < 1e-5, (exprs[k], loss[k], exact)
+    # the generating formula: loss ~ noise variance 0.01
+    assert abs(float(loss[3]) - 0.01) < 1e-3
+    # same answer through a SubDataset covering all rows in order (gather path)
+    l2, c2 = eval_loss_batch(trees, batch(d, np.arange(n)), opts)
+    assert np.max(_rel(l2, loss)) < 1e-6
+
+
+def test_row_sharded_partials_match_single():
+    """The multi-GPU building block: Σ over row shards of sr_eval_loss_partials == one full eval."""
+    opts = Options(**C2_OPTS)
+    n = 20000
+    X, y = _c2_data(n, seed=61)
+    tb = flatten_trees(gen_random_population(700, opts, 5, seed=61), np.float32)
+    full_loss, full_comp = eval_loss_batch(tb, Dataset(X, y), opts)
+    ctx = sr_amd.get_context()
+    oid = ctx.opset_id(opts.operators)
+    sums = np.zeros(tb.n_trees)
+    flags = np.zeros(tb.n_trees, dtype=np.uint32)
+    shards = [Dataset(np.ascontiguousarray(X[:, a:b]), np.ascontiguousarray(y[a:b])) for a, b in ((0, 7000), (7000, n))]
+    s = tb.to_struct()
+    for sh in shards:
+        ps = np.zeros(tb.n_trees)
+        pf = np.zeros(tb.n_trees, dtype=np.uint32)
+        _lib.check(_lib.lib.sr_eval_loss_partials(ctx.handle, sh.device_handle(ctx), oid, ctypes.byref(s), n, 0,
+                                                  ps.ctypes.data_as(ctypes.c_void_p), pf.ctypes.data_as(ctypes.c_void_p), 0))
+        sums += ps
+        flags |= pf
+    out = np.empty(tb.n_trees, dtype=np.float32)
+    comp = np.empty(tb.n_trees, dtype=np.uint8)
+    _lib.check(_lib.lib.sr_finalize_losses(_lib.SR_DTYPE_F32, tb.n_trees, sums.ctypes.data_as(ctypes.c_void_p),
+                                           flags.ctypes.data_as(ctypes.c_void_p), float(n), None, 0, 0, None,
+                                           out.ctypes.data_as(ctypes.c_void_p), comp.ctypes.data_as(ctypes.c_void_p)))
+    assert np.array_equal(comp.astype(bool), full_comp)
+    assert np.max(_rel(out[full_comp], full_loss[full_comp])) < 1e-6
