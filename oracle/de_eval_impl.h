@@ -38,6 +38,7 @@ typedef struct {
   const int32_t* un_ids;
   const int32_t* bin_ids;
   int n_un, n_bin;
+  int perturb; /* 0, or +-1: scale every libm result by (1 + perturb * eps) (conditioning probe) */
 } FN(otree);
 
 /* ---------------------------------------------------------------- operators (src/Operators.jl) */
@@ -124,6 +125,28 @@ static T FN(o_binary)(int id, T x, T y) {
   return FN(o_nan)();
 }
 
+/* Conditioning probe: a libm whose results differ by +-1 ulp with a pseudo-random sign per
+ * (node, row) — independent last-bit differences, as between two correctly rounded libms.
+ * Seed p != 0 selects the sign pattern; exact IEEE ops (and sqrt) are left alone. */
+static int FN(psign)(int node, int64_t row, int p) {
+  uint32_t h = (uint32_t)node * 0x9E3779B1u ^ (uint32_t)row * 0x85EBCA77u ^ (uint32_t)p * 0xC2B2AE3Du;
+  h ^= h >> 16; h *= 0x7FEB352Du; h ^= h >> 15; h *= 0x846CA68Bu; h ^= h >> 16;
+  return (h & 1u) ? 1 : -1;
+}
+static T FN(perturb_unary)(int id, T v, int p, int node, int64_t row) {
+  if (!p) return v;
+  switch (id) {
+    case O_NEG: case O_SQUARE: case O_CUBE: case O_ABS: case O_SIGN: case O_RELU: case O_INV:
+    case O_ROUND: case O_FLOOR: case O_CEIL: case O_SQRT:
+      return v;
+  }
+  return v * ((T)1 + (T)FN(psign)(node, row, p) * PERTURB_EPS);
+}
+static T FN(perturb_binary)(int id, T v, int p, int node, int64_t row) {
+  if (!p || id != O_POW) return v;
+  return v * ((T)1 + (T)FN(psign)(node, row, p) * PERTURB_EPS);
+}
+
 /* ---------------------------------------------------------------- Julia sum (pairwise) */
 static T FN(jl_sum_range)(const T* a, int64_t lo, int64_t hi) { /* inclusive [lo, hi] */
   if (lo == hi) return a[lo];
@@ -197,13 +220,13 @@ static int FN(const_tree)(const FN(otree) * t, int i, T* out) {
   if (d == 1) {
     T x;
     if (!FN(const_tree)(t, t->left[i], &x)) return 0;
-    *out = FN(o_unary)(FN(uid)(t, i), x);
+    *out = FN(perturb_unary)(FN(uid)(t, i), FN(o_unary)(FN(uid)(t, i), x), t->perturb, i, 0);
     return isfinite(*out) ? 1 : 0;
   }
   T a, b;
   if (!FN(const_tree)(t, t->left[i], &a)) return 0;
   if (!FN(const_tree)(t, t->right[i], &b)) return 0;
-  *out = FN(o_binary)(FN(bid)(t, i), a, b);
+  *out = FN(perturb_binary)(FN(bid)(t, i), FN(o_binary)(FN(bid)(t, i), a, b), t->perturb, i, 0);
   return isfinite(*out) ? 1 : 0;
 }
 
@@ -252,8 +275,8 @@ static int FN(eval_rec)(const FN(otree) * t, int i, const FN(oview) * v, T** out
       for (int64_t j = 0; j < n; ++j) {
         const T a = t->constant[ll] ? t->val[ll] : FN(xat)(v, t->feature[ll] - 1, j);
         const T b = t->constant[lr] ? t->val[lr] : FN(xat)(v, t->feature[lr] - 1, j);
-        const T x_l = FN(o_binary)(op_l, a, b);
-        r[j] = isfinite(x_l) ? FN(o_unary)(op, x_l) : (T)INFINITY;
+        const T x_l = FN(perturb_binary)(op_l, FN(o_binary)(op_l, a, b), t->perturb, l, j);
+        r[j] = isfinite(x_l) ? FN(perturb_unary)(op, FN(o_unary)(op, x_l), t->perturb, i, j) : (T)INFINITY;
       }
       return 1;
     }
@@ -264,8 +287,8 @@ static int FN(eval_rec)(const FN(otree) * t, int i, const FN(oview) * v, T** out
       if (t->constant[ll] && !isfinite(t->val[ll])) return 0;
       for (int64_t j = 0; j < n; ++j) {
         const T a = t->constant[ll] ? t->val[ll] : FN(xat)(v, t->feature[ll] - 1, j);
-        const T x_l = FN(o_unary)(op_l, a);
-        r[j] = isfinite(x_l) ? FN(o_unary)(op, x_l) : (T)INFINITY;
+        const T x_l = FN(perturb_unary)(op_l, FN(o_unary)(op_l, a), t->perturb, l, j);
+        r[j] = isfinite(x_l) ? FN(perturb_unary)(op, FN(o_unary)(op, x_l), t->perturb, i, j) : (T)INFINITY;
       }
       return 1;
     }
@@ -276,7 +299,7 @@ static int FN(eval_rec)(const FN(otree) * t, int i, const FN(oview) * v, T** out
       free(c);
       return 0;
     }
-    for (int64_t j = 0; j < n; ++j) r[j] = FN(o_unary)(op, c[j]);
+    for (int64_t j = 0; j < n; ++j) r[j] = FN(perturb_unary)(op, FN(o_unary)(op, c[j]), t->perturb, i, j);
     free(c);
     return 1;
   }
@@ -290,7 +313,7 @@ static int FN(eval_rec)(const FN(otree) * t, int i, const FN(oview) * v, T** out
     for (int64_t j = 0; j < n; ++j) {
       const T a = t->constant[l] ? t->val[l] : FN(xat)(v, t->feature[l] - 1, j);
       const T b = t->constant[rr] ? t->val[rr] : FN(xat)(v, t->feature[rr] - 1, j);
-      r[j] = FN(o_binary)(op, a, b);
+      r[j] = FN(perturb_binary)(op, FN(o_binary)(op, a, b), t->perturb, i, j);
     }
     return 1;
   }
@@ -301,7 +324,7 @@ static int FN(eval_rec)(const FN(otree) * t, int i, const FN(oview) * v, T** out
     if (t->constant[rr] && !isfinite(t->val[rr])) { free(c); return 0; }
     for (int64_t j = 0; j < n; ++j) {
       const T b = t->constant[rr] ? t->val[rr] : FN(xat)(v, t->feature[rr] - 1, j);
-      r[j] = FN(o_binary)(op, c[j], b);
+      r[j] = FN(perturb_binary)(op, FN(o_binary)(op, c[j], b), t->perturb, i, j);
     }
     free(c);
     return 1;
@@ -313,7 +336,7 @@ static int FN(eval_rec)(const FN(otree) * t, int i, const FN(oview) * v, T** out
     if (t->constant[l] && !isfinite(t->val[l])) { free(c); return 0; }
     for (int64_t j = 0; j < n; ++j) {
       const T a = t->constant[l] ? t->val[l] : FN(xat)(v, t->feature[l] - 1, j);
-      r[j] = FN(o_binary)(op, a, c[j]);
+      r[j] = FN(perturb_binary)(op, FN(o_binary)(op, a, c[j]), t->perturb, i, j);
     }
     free(c);
     return 1;
@@ -325,7 +348,7 @@ static int FN(eval_rec)(const FN(otree) * t, int i, const FN(oview) * v, T** out
   T* b = NULL;
   ok = FN(eval_rec)(t, rr, v, &b);
   if (!ok || !FN(is_valid_array)(b, n)) { free(a); free(b); return 0; }
-  for (int64_t j = 0; j < n; ++j) r[j] = FN(o_binary)(op, a[j], b[j]);
+  for (int64_t j = 0; j < n; ++j) r[j] = FN(perturb_binary)(op, FN(o_binary)(op, a[j], b[j]), t->perturb, i, j);
   free(a);
   free(b);
   return 1;
@@ -335,8 +358,9 @@ static int FN(eval_rec)(const FN(otree) * t, int i, const FN(oview) * v, T** out
 int FN(oracle_eval_tree)(int64_t n_nodes, const uint8_t* degree, const uint8_t* op, const uint16_t* feature,
                          const uint8_t* constant, const T* val, const int32_t* un_ids, int n_un,
                          const int32_t* bin_ids, int n_bin, const T* X, int64_t nf, int64_t n, T* out,
-                         int* complete) {
+                         int* complete, int perturb) {
   FN(otree) t;
+  t.perturb = perturb;
   t.n = n_nodes; t.degree = degree; t.op = op; t.feature = feature; t.constant = constant; t.val = val;
   t.un_ids = un_ids; t.bin_ids = bin_ids; t.n_un = n_un; t.n_bin = n_bin;
   t.left = (int32_t*)malloc(sizeof(int32_t) * (size_t)n_nodes);
@@ -370,10 +394,10 @@ int FN(oracle_eval_tree)(int64_t n_nodes, const uint8_t* degree, const uint8_t* 
 int FN(oracle_eval_loss)(int64_t n_nodes, const uint8_t* degree, const uint8_t* op, const uint16_t* feature,
                          const uint8_t* constant, const T* val, const int32_t* un_ids, int n_un,
                          const int32_t* bin_ids, int n_bin, const T* X, int64_t nf, int64_t n, const T* y,
-                         const T* w, int loss_kind, int accum, T* loss, int* complete) {
+                         const T* w, int loss_kind, int accum, T* loss, int* complete, int perturb) {
   T* pred = FN(alloc)(n);
   if (!FN(oracle_eval_tree)(n_nodes, degree, op, feature, constant, val, un_ids, n_un, bin_ids, n_bin, X, nf, n,
-                            pred, complete)) {
+                            pred, complete, perturb)) {
     free(pred);
     return 0;
   }
@@ -411,14 +435,14 @@ int FN(oracle_eval_loss_batch)(int64_t n_trees, const int64_t* offsets, const ui
                                const uint16_t* feature, const uint8_t* constant, const T* val,
                                const int32_t* un_ids, int n_un, const int32_t* bin_ids, int n_bin, const T* X,
                                int64_t nf, int64_t n, const T* y, const T* w, int loss_kind, int accum,
-                               int n_threads, T* loss, int* complete) {
+                               int n_threads, T* loss, int* complete, int perturb) {
   int bad = 0;
 #pragma omp parallel for schedule(dynamic, 1) num_threads(n_threads) reduction(| : bad)
   for (int64_t k = 0; k < n_trees; ++k) {
     const int64_t b = offsets[k], e = offsets[k + 1];
     int c = 0;
     if (!FN(oracle_eval_loss)(e - b, degree + b, op + b, feature + b, constant + b, val + b, un_ids, n_un, bin_ids,
-                              n_bin, X, nf, n, y, w, loss_kind, accum, loss + k, &c))
+                              n_bin, X, nf, n, y, w, loss_kind, accum, loss + k, &c, perturb))
       bad |= 1;
     complete[k] = c;
   }

@@ -31,13 +31,13 @@ def _load():
     for sfx in ("f32", "f64"):
         f = getattr(lib, f"oracle_eval_tree_{sfx}")
         f.restype = I
-        f.argtypes = [I64, P, P, P, P, P, P, I, P, I, P, I64, I64, P, P]
+        f.argtypes = [I64, P, P, P, P, P, P, I, P, I, P, I64, I64, P, P, I]
         f = getattr(lib, f"oracle_eval_loss_{sfx}")
         f.restype = I
-        f.argtypes = [I64, P, P, P, P, P, P, I, P, I, P, I64, I64, P, P, I, I, P, P]
+        f.argtypes = [I64, P, P, P, P, P, P, I, P, I, P, I64, I64, P, P, I, I, P, P, I]
         f = getattr(lib, f"oracle_eval_loss_batch_{sfx}")
         f.restype = I
-        f.argtypes = [I64, P, P, P, P, P, P, P, I, P, I, P, I64, I64, P, P, I, I, I, P, P]
+        f.argtypes = [I64, P, P, P, P, P, P, P, I, P, I, P, I64, I64, P, P, I, I, I, P, P, I]
     return lib
 
 
@@ -82,7 +82,7 @@ class Oracle:
     def _sfx(dtype):
         return "f32" if np.dtype(dtype) == np.float32 else "f64"
 
-    def eval_tree_array(self, tb, k, X):
+    def eval_tree_array(self, tb, k, X, perturb=0):
         """tb: TreeBatch-like (offsets/degree/op/feature/constant/val); X: [nf, n]."""
         X = np.asarray(X)
         dtype = X.dtype
@@ -94,12 +94,12 @@ class Oracle:
         f = getattr(lib(), f"oracle_eval_tree_{self._sfx(dtype)}")
         ok = f(e - b, _p(tb.degree[b:e]), _p(tb.op[b:e]), _p(tb.feature[b:e]), _p(tb.constant[b:e]), _p(val),
                _p(self.un), len(self.unaops), _p(self.bi), len(self.binops), _p(Xj), X.shape[0], X.shape[1],
-               _p(out), ctypes.byref(comp))
+               _p(out), ctypes.byref(comp), int(perturb))
         if not ok:
             raise ValueError("oracle: malformed tree")
         return out, bool(comp.value)
 
-    def eval_loss_batch(self, tb, X, y, w=None, loss_kind=0, accum="f64", n_threads=1):
+    def eval_loss_batch(self, tb, X, y, w=None, loss_kind=0, accum="f64", n_threads=1, perturb=0):
         X = np.asarray(X)
         dtype = X.dtype
         Xj = np.ascontiguousarray(X.T)
@@ -113,7 +113,7 @@ class Oracle:
         ok = f(n_trees, _p(np.ascontiguousarray(tb.offsets, dtype=np.int64)), _p(tb.degree), _p(tb.op),
                _p(tb.feature), _p(tb.constant), _p(val), _p(self.un), len(self.unaops), _p(self.bi),
                len(self.binops), _p(Xj), X.shape[0], X.shape[1], _p(y), _p(w), int(loss_kind),
-               0 if accum == "ref" else 1, int(n_threads), _p(loss), _p(comp))
+               0 if accum == "ref" else 1, int(n_threads), _p(loss), _p(comp), int(perturb))
         if not ok:
             raise ValueError("oracle: malformed tree")
         return loss, comp.astype(bool)

@@ -83,23 +83,32 @@ hipError_t sr_launch_pad(T* v, int64_t n, int64_t ld, T pad_value, int replicate
 }
 
 template <typename T>
-hipError_t sr_launch_interp(const SrEvalArgs<T>& a, int mode, bool gather, int tier, int n_blocks, hipStream_t s) {
+hipError_t sr_launch_interp(const SrEvalArgs<T>& a, int mode, bool gather, int tier, SrVariant v, int n_blocks,
+                            hipStream_t s) {
+  constexpr int R = 16 / sizeof(T);
   if (mode == SR_MODE_LOSS) {
-    if (tier == SR_TIER_BASIC)
-      return gather ? sr_dispatch_interp<T, SR_MODE_LOSS, true, SR_TIER_BASIC>(a, n_blocks, s)
-                    : sr_dispatch_interp<T, SR_MODE_LOSS, false, SR_TIER_BASIC>(a, n_blocks, s);
-    return gather ? sr_dispatch_interp<T, SR_MODE_LOSS, true, SR_TIER_FULL>(a, n_blocks, s)
-                  : sr_dispatch_interp<T, SR_MODE_LOSS, false, SR_TIER_FULL>(a, n_blocks, s);
+    if (tier == SR_TIER_BASIC) {
+      if (!gather) {
+        if constexpr (sizeof(T) == 4) {
+          if (v.rows_per_lane == 8) return sr_dispatch_interp<T, 8, SR_MODE_LOSS, false, SR_TIER_BASIC, 1>(a, n_blocks, s);
+          if (v.var == 0) return sr_dispatch_interp<T, 4, SR_MODE_LOSS, false, SR_TIER_BASIC, 0>(a, n_blocks, s);
+        }
+        return sr_dispatch_interp<T, R, SR_MODE_LOSS, false, SR_TIER_BASIC, 1>(a, n_blocks, s);
+      }
+      return sr_dispatch_interp<T, R, SR_MODE_LOSS, true, SR_TIER_BASIC, 1>(a, n_blocks, s);
+    }
+    return gather ? sr_dispatch_interp<T, R, SR_MODE_LOSS, true, SR_TIER_FULL, 1>(a, n_blocks, s)
+                  : sr_dispatch_interp<T, R, SR_MODE_LOSS, false, SR_TIER_FULL, 1>(a, n_blocks, s);
   }
   if (mode == SR_MODE_PRED)
-    return gather ? sr_dispatch_interp<T, SR_MODE_PRED, true, SR_TIER_FULL>(a, n_blocks, s)
-                  : sr_dispatch_interp<T, SR_MODE_PRED, false, SR_TIER_FULL>(a, n_blocks, s);
-  return gather ? sr_dispatch_interp<T, SR_MODE_EXACT, true, SR_TIER_FULL>(a, n_blocks, s)
-                : sr_dispatch_interp<T, SR_MODE_EXACT, false, SR_TIER_FULL>(a, n_blocks, s);
+    return gather ? sr_dispatch_interp<T, R, SR_MODE_PRED, true, SR_TIER_FULL, 1>(a, n_blocks, s)
+                  : sr_dispatch_interp<T, R, SR_MODE_PRED, false, SR_TIER_FULL, 1>(a, n_blocks, s);
+  return gather ? sr_dispatch_interp<T, R, SR_MODE_EXACT, true, SR_TIER_FULL, 1>(a, n_blocks, s)
+                : sr_dispatch_interp<T, R, SR_MODE_EXACT, false, SR_TIER_FULL, 1>(a, n_blocks, s);
 }
 
-template hipError_t sr_launch_interp<float>(const SrEvalArgs<float>&, int, bool, int, int, hipStream_t);
-template hipError_t sr_launch_interp<double>(const SrEvalArgs<double>&, int, bool, int, int, hipStream_t);
+template hipError_t sr_launch_interp<float>(const SrEvalArgs<float>&, int, bool, int, SrVariant, int, hipStream_t);
+template hipError_t sr_launch_interp<double>(const SrEvalArgs<double>&, int, bool, int, SrVariant, int, hipStream_t);
 template hipError_t sr_launch_transpose<float>(const float*, int64_t, int64_t, int64_t, float*, hipStream_t);
 template hipError_t sr_launch_transpose<double>(const double*, int64_t, int64_t, int64_t, double*, hipStream_t);
 template hipError_t sr_launch_pad<float>(float*, int64_t, int64_t, float, int, hipStream_t);

@@ -10,6 +10,7 @@
 #include <chrono>
 #include <cmath>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <mutex>
 #include <string>
@@ -75,6 +76,8 @@ struct sr_ctx {
       check_sums;
   double last_eval_ms = 0.0, last_total_ms = 0.0;
   int cu_count = 256;
+  SrVariant variant{4, 1};  // SR_AMD_VARIANT (tuning): 0 default, 1 = R4 no prefetch, 2 = R8 prefetch
+  int tree_group = 0;       // SR_AMD_TREES_PER_BLOCK override (0 = heuristic)
 };
 
 struct sr_dataset {
@@ -90,7 +93,7 @@ struct sr_dataset {
 
 namespace {
 
-constexpr int64_t kRowAlign = 1024;  // 256 lanes x 16 B
+constexpr int64_t kRowAlign = 2048;  // one row tile at the widest variant (256 lanes x 8 rows)
 
 // Work decomposition: row tiles of 256*R rows, grouped `tiles` per block; trees grouped G per block.
 struct Grid {
@@ -98,8 +101,8 @@ struct Grid {
   int64_t n_blocks = 1;
 };
 template <typename T>
-Grid make_grid(int64_t n_rows, int64_t n_trees) {
-  constexpr int64_t rows_per_tile = 256 * (16 / sizeof(T));
+Grid make_grid(int64_t n_rows, int64_t n_trees, int rows_per_lane = 16 / sizeof(T), int g_override = 0) {
+  const int64_t rows_per_tile = 256 * int64_t(rows_per_lane);
   Grid g;
   const int64_t n_tiles = (n_rows + rows_per_tile - 1) / rows_per_tile;
   int64_t tiles = (n_tiles + 255) / 256;  // keep <= 256 row blocks per tree
@@ -109,6 +112,7 @@ Grid make_grid(int64_t n_rows, int64_t n_trees) {
   if (g.n_row_blocks < 1) g.n_row_blocks = 1;
   int G = 32;
   while (G > 1 && int64_t(g.n_row_blocks) * ((n_trees + G - 1) / G) < 2048) G /= 2;
+  if (g_override > 0) G = g_override;
   g.G = G;
   g.n_groups = int((n_trees + G - 1) / G);
   g.n_blocks = int64_t(g.n_row_blocks) * g.n_groups;
@@ -161,7 +165,9 @@ int run_batch(sr_ctx* ctx, const sr_dataset* ds, int opset_id, const sr_tree_bat
     return set_error(SR_ERR_TOO_DEEP, "a tree needs " + std::to_string(prog->max_depth) +
                                           " operand-stack slots; the kernel holds 4 (maxsize <= 94)");
   const int64_t nt = trees->n_trees;
-  Grid g = make_grid<T>(n_eval, nt);
+  const bool tuned = sizeof(T) == 4 && mode == SR_MODE_LOSS && !gather && ctx->tiers[opset_id] == SR_TIER_BASIC;
+  const SrVariant var = tuned ? ctx->variant : SrVariant{int(16 / sizeof(T)), 1};
+  Grid g = make_grid<T>(n_eval, nt, var.rows_per_lane, ctx->tree_group);
   *grid_out = g;
   if (nt == 0) return SR_OK;
 
@@ -216,7 +222,7 @@ int run_batch(sr_ctx* ctx, const sr_dataset* ds, int opset_id, const sr_tree_bat
   if (g.n_blocks > 0x7fffffff) return set_error(SR_ERR_INVALID_ARG, "grid too large");
   const int tier = ctx->tiers[opset_id];
   SR_HIP_CHECK(hipEventRecord(ctx->ev_k0, s));
-  SR_HIP_CHECK(sr_launch_interp<T>(a, mode, gather, tier, int(g.n_blocks), s));
+  SR_HIP_CHECK(sr_launch_interp<T>(a, mode, gather, tier, var, int(g.n_blocks), s));
   SR_HIP_CHECK(hipEventRecord(ctx->ev_k1, s));
   SR_HIP_CHECK(sr_launch_reduce(a.part_sum, a.part_flag, int(nt), g.n_row_blocks, ctx->static_bad.as<uint8_t>(),
                                 ctx->out_sum.as<double>(), ctx->out_flag.as<uint32_t>(), s));
@@ -263,7 +269,8 @@ int run_exact(sr_ctx* ctx, const sr_dataset* ds, const SrProgramBatch<T>& prog, 
   a.scale = sizeof(T) == 8 ? std::ldexp(1.0, -64) : 1.0;
   const int64_t blocks = int64_t(g.n_row_blocks) * n_list;
   if (blocks > 0x7fffffff) return set_error(SR_ERR_INVALID_ARG, "grid too large");
-  SR_HIP_CHECK(sr_launch_interp<T>(a, SR_MODE_EXACT, gather, SR_TIER_FULL, int(blocks), s));
+  SR_HIP_CHECK(sr_launch_interp<T>(a, SR_MODE_EXACT, gather, SR_TIER_FULL, SrVariant{int(16 / sizeof(T)), 1},
+                                   int(blocks), s));
   SR_HIP_CHECK(hipMemcpyAsync(host_sums, ctx->check_sums.p, size_t(n_list) * max_checks * sizeof(double),
                               hipMemcpyDeviceToHost, s));
   SR_HIP_CHECK(hipStreamSynchronize(s));
@@ -493,6 +500,12 @@ int sr_init(int device, sr_ctx** out) {
   ctx->device = device;
   hipDeviceProp_t prop;
   if (hipGetDeviceProperties(&prop, device) == hipSuccess) ctx->cu_count = prop.multiProcessorCount;
+  if (const char* v = std::getenv("SR_AMD_VARIANT")) {
+    const int k = std::atoi(v);
+    if (k == 1) ctx->variant = SrVariant{4, 0};
+    if (k == 2) ctx->variant = SrVariant{8, 1};
+  }
+  if (const char* v = std::getenv("SR_AMD_TREES_PER_BLOCK")) ctx->tree_group = std::atoi(v);
   hipError_t e = hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking);
   if (e == hipSuccess) e = hipEventCreate(&ctx->ev_start);
   if (e == hipSuccess) e = hipEventCreate(&ctx->ev_k0);

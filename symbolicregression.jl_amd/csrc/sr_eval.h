@@ -40,13 +40,19 @@ struct SrEvalArgs {
   double scale;
 };
 
-template <typename T, int MODE, bool GATHER, int TIER>
+template <typename T, int R, int MODE, bool GATHER, int TIER, int VAR>
 hipError_t sr_dispatch_interp(const SrEvalArgs<T>& a, int n_blocks, hipStream_t s);
 template <typename T>
-size_t sr_interp_lds_bytes(int trees_per_block);
+size_t sr_interp_lds_bytes(int trees_per_block, int rows_per_lane, int max_checks);
 
+// Kernel variant (tuning): rows per lane and instruction prefetch.  variant 0 = default.
+struct SrVariant {
+  int rows_per_lane;  // 4 or 8 (f32); 2 (f64)
+  int var;            // bit 0: prefetch next program word
+};
 template <typename T>
-hipError_t sr_launch_interp(const SrEvalArgs<T>& a, int mode, bool gather, int tier, int n_blocks, hipStream_t s);
+hipError_t sr_launch_interp(const SrEvalArgs<T>& a, int mode, bool gather, int tier, SrVariant v, int n_blocks,
+                            hipStream_t s);
 hipError_t sr_launch_reduce(const double* part_sum, const uint32_t* part_flag, int n_trees, int n_row_blocks,
                             const uint8_t* static_bad, double* out_sum, uint32_t* out_flag, hipStream_t s);
 template <typename T>

@@ -30,26 +30,34 @@
 #define SR_BLOCK (SR_WAVES * 64)
 #define SR_STACK_DEPTH 4
 
-template <typename T, int R>
-struct SrVec;
+// R values per lane moved as 16-byte vectors (dwordx4 / ds_*_b128).
+template <typename T>
+struct SrChunk;
 template <>
-struct SrVec<float, 4> {
-  static __device__ inline void load(const float* p, float (&o)[4]) {
-    const float4 v = *reinterpret_cast<const float4*>(p);
-    o[0] = v.x; o[1] = v.y; o[2] = v.z; o[3] = v.w;
-  }
-  static __device__ inline void store(float* p, const float (&o)[4]) {
-    *reinterpret_cast<float4*>(p) = make_float4(o[0], o[1], o[2], o[3]);
-  }
+struct SrChunk<float> {
+  using V = float4;
+  static constexpr int N = 4;
+  static __device__ inline void get(const V& v, float* o) { o[0] = v.x; o[1] = v.y; o[2] = v.z; o[3] = v.w; }
+  static __device__ inline V make(const float* o) { return make_float4(o[0], o[1], o[2], o[3]); }
 };
 template <>
-struct SrVec<double, 2> {
-  static __device__ inline void load(const double* p, double (&o)[2]) {
-    const double2 v = *reinterpret_cast<const double2*>(p);
-    o[0] = v.x; o[1] = v.y;
+struct SrChunk<double> {
+  using V = double2;
+  static constexpr int N = 2;
+  static __device__ inline void get(const V& v, double* o) { o[0] = v.x; o[1] = v.y; }
+  static __device__ inline V make(const double* o) { return make_double2(o[0], o[1]); }
+};
+template <typename T, int R>
+struct SrVec {
+  using C = SrChunk<T>;
+  static_assert(R % C::N == 0, "rows per lane must fill whole 16-byte vectors");
+  static __device__ inline void load(const T* p, T (&o)[R]) {
+#pragma unroll
+    for (int c = 0; c < R / C::N; ++c) C::get(reinterpret_cast<const typename C::V*>(p)[c], o + c * C::N);
   }
-  static __device__ inline void store(double* p, const double (&o)[2]) {
-    *reinterpret_cast<double2*>(p) = make_double2(o[0], o[1]);
+  static __device__ inline void store(T* p, const T (&o)[R]) {
+#pragma unroll
+    for (int c = 0; c < R / C::N; ++c) reinterpret_cast<typename C::V*>(p)[c] = C::make(o + c * C::N);
   }
 };
 
@@ -60,6 +68,31 @@ __device__ __forceinline__ T sr_wave_sum(T v) {
   return v;
 }
 __device__ __forceinline__ uint64_t sr_ballot(bool p) { return __builtin_amdgcn_ballot_w64(p); }
+
+// Feature operand X[f] for this lane's R rows.  Small tiles use one indexed register read
+// (s_set_gpr_idx_on + R moves); tiles above 32 registers would be demoted to scratch by LLVM when
+// indexed dynamically, so they branch on the (wave-uniform) feature index instead.
+template <typename T, int R, int FCAP>
+__device__ __forceinline__ void sr_fetch_feature(const T (&xr)[FCAP][R], uint32_t f, T (&o)[R]) {
+  if constexpr (FCAP * R <= 32) {
+#pragma unroll
+    for (int r = 0; r < R; ++r) o[r] = xr[f][r];
+  } else {
+#define SR_FCASE(K)                                        \
+  case K:                                                  \
+    if constexpr (K < FCAP) {                              \
+      _Pragma("unroll") for (int r = 0; r < R; ++r) o[r] = xr[K][r]; \
+    }                                                      \
+    break;
+    switch (f) {
+      SR_FCASE(0) SR_FCASE(1) SR_FCASE(2) SR_FCASE(3) SR_FCASE(4) SR_FCASE(5) SR_FCASE(6) SR_FCASE(7)
+      SR_FCASE(8) SR_FCASE(9) SR_FCASE(10) SR_FCASE(11) SR_FCASE(12) SR_FCASE(13) SR_FCASE(14) SR_FCASE(15)
+      default:
+        break;
+    }
+#undef SR_FCASE
+  }
+}
 
 // ------------------------------------------------------------------ dispatch cases
 // Operators of the BASIC tier are compiled into every kernel; the FULL tier adds the rest of the
@@ -108,15 +141,17 @@ __device__ __forceinline__ uint64_t sr_ballot(bool p) { return __builtin_amdgcn_
   }                                                                                            \
   case SR_BIN_OPC(ID, SR_V_FL): {                                                              \
     if (ENABLED) {                                                                             \
-      const uint32_t f = in.arg;                                                               \
-      SR_BIN_EACH(xr[f][r], tos[r], ID);                                                       \
+      T o[R];                                                                                  \
+      sr_fetch_feature<T, R, FCAP>(xr, in.arg, o);                                             \
+      SR_BIN_EACH(o[r], tos[r], ID);                                                           \
     }                                                                                          \
     break;                                                                                     \
   }                                                                                            \
   case SR_BIN_OPC(ID, SR_V_FR): {                                                              \
     if (ENABLED) {                                                                             \
-      const uint32_t f = in.arg;                                                               \
-      SR_BIN_EACH(tos[r], xr[f][r], ID);                                                       \
+      T o[R];                                                                                  \
+      sr_fetch_feature<T, R, FCAP>(xr, in.arg, o);                                             \
+      SR_BIN_EACH(tos[r], o[r], ID);                                                           \
     }                                                                                          \
     break;                                                                                     \
   }                                                                                            \
@@ -139,7 +174,8 @@ __device__ __forceinline__ uint64_t sr_ballot(bool p) { return __builtin_amdgcn_
 
 // ------------------------------------------------------------------ the interpreter kernel
 // MODE: SR_MODE_LOSS (partials), SR_MODE_PRED (write predictions), SR_MODE_EXACT (check sums).
-template <typename T, int R, int FCAP, int MODE, bool GATHER, int TIER>
+// VAR bit 0: prefetch the next program word while the current one executes.
+template <typename T, int R, int FCAP, int MODE, bool GATHER, int TIER, int VAR>
 __global__ void __launch_bounds__(SR_BLOCK) sr_interp_kernel(const SrEvalArgs<T> a) {
   constexpr int D = SR_STACK_DEPTH;
   extern __shared__ __attribute__((aligned(16))) unsigned char sr_smem[];
@@ -149,15 +185,14 @@ __global__ void __launch_bounds__(SR_BLOCK) sr_interp_kernel(const SrEvalArgs<T>
   const int G = a.trees_per_block;
 
   // LDS carve (all 16-byte aligned):
-  //   stack [SR_WAVES][D][64][R] T | y tile [256][R] T | w tile [256][R] T |
-  //   acc [SR_WAVES][G] f64 | flg [SR_WAVES][G] u32 | abort [G] u32
+  //   stack [SR_WAVES][D][64][R] T | acc [SR_WAVES][G] f64 | flg [SR_WAVES][G] u32 | abort [G] u32
   T* stk = reinterpret_cast<T*>(sr_smem) + (size_t(wave) * D * 64 + lane) * R;
-  T* ylds = reinterpret_cast<T*>(sr_smem) + size_t(SR_WAVES) * D * 64 * R + size_t(tid) * R;
-  T* wlds = ylds + size_t(SR_BLOCK) * R;
-  double* acc = reinterpret_cast<double*>(reinterpret_cast<T*>(sr_smem) + size_t(SR_WAVES) * D * 64 * R +
-                                          2 * size_t(SR_BLOCK) * R);
+  double* acc = reinterpret_cast<double*>(reinterpret_cast<T*>(sr_smem) + size_t(SR_WAVES) * D * 64 * R);
   uint32_t* flg = reinterpret_cast<uint32_t*>(acc + SR_WAVES * G);
   uint32_t* abort_flag = flg + SR_WAVES * G;
+  // EXACT mode: per-wave check-sum accumulators [SR_WAVES][max_checks] after the abort words
+  double* xacc = reinterpret_cast<double*>(abort_flag + ((G + 3) & ~3));
+  const int MC = (MODE == SR_MODE_EXACT) ? a.max_checks : 0;
 
   const int rb = blockIdx.x % a.n_row_blocks;
   const int tg = blockIdx.x / a.n_row_blocks;
@@ -167,6 +202,7 @@ __global__ void __launch_bounds__(SR_BLOCK) sr_interp_kernel(const SrEvalArgs<T>
     flg[i] = 0u;
   }
   for (int i = tid; i < G; i += SR_BLOCK) abort_flag[i] = 0u;
+  for (int i = tid; i < SR_WAVES * MC; i += SR_BLOCK) xacc[i] = 0.0;
   __syncthreads();
 
   const int tree0 = tg * G;
@@ -178,30 +214,19 @@ __global__ void __launch_bounds__(SR_BLOCK) sr_interp_kernel(const SrEvalArgs<T>
     const int64_t row0 = ((int64_t(rb) * a.tiles_per_block + tile) * SR_BLOCK + tid) * R;
     if (!sr_ballot(row0 < a.n_rows)) continue;  // whole wave past the end (uniform)
 
-    // ---- stage this lane's R rows: X in VGPRs, y / w in this lane's LDS slot
+    // ---- stage this lane's R rows of X in VGPRs (y / w are re-read at each tree's loss: L1/L2 hits)
     T xr[FCAP][R];
     bool valid[R];
 #pragma unroll
     for (int r = 0; r < R; ++r) valid[r] = (row0 + r) < a.n_rows;
+    int64_t idx[R];
     if (GATHER) {
-      int64_t idx[R];
 #pragma unroll
       for (int r = 0; r < R; ++r) idx[r] = a.row_idx[valid[r] ? row0 + r : 0];  // pad with row 0 of the view
 #pragma unroll
       for (int f = 0; f < FCAP; ++f) {
 #pragma unroll
         for (int r = 0; r < R; ++r) xr[f][r] = (f < a.nf) ? a.X[int64_t(f) * a.ld + idx[r]] : T(0);
-      }
-      T tmp[R];
-      if (a.y) {
-#pragma unroll
-        for (int r = 0; r < R; ++r) tmp[r] = a.y[idx[r]];
-        SrVec<T, R>::store(ylds, tmp);
-      }
-      if (weighted) {
-#pragma unroll
-        for (int r = 0; r < R; ++r) tmp[r] = a.w[idx[r]];
-        SrVec<T, R>::store(wlds, tmp);
       }
     } else {
 #pragma unroll
@@ -212,15 +237,6 @@ __global__ void __launch_bounds__(SR_BLOCK) sr_interp_kernel(const SrEvalArgs<T>
 #pragma unroll
           for (int r = 0; r < R; ++r) xr[f][r] = T(0);
         }
-      }
-      T tmp[R];
-      if (a.y) {
-        SrVec<T, R>::load(a.y + row0, tmp);
-        SrVec<T, R>::store(ylds, tmp);
-      }
-      if (weighted) {
-        SrVec<T, R>::load(a.w + row0, tmp);
-        SrVec<T, R>::store(wlds, tmp);
       }
     }
 
@@ -239,8 +255,15 @@ __global__ void __launch_bounds__(SR_BLOCK) sr_interp_kernel(const SrEvalArgs<T>
       int check_k = 0;
       uint64_t susp_any = 0;
 
+      SrIns<T> nxt = a.code[pb];
       for (uint32_t pc = pb; pc < pe; ++pc) {
-        const SrIns<T> in = a.code[pc];
+        SrIns<T> in;
+        if (VAR & 1) {
+          in = nxt;
+          nxt = a.code[pc + 1];  // the program buffer is padded by one instruction
+        } else {
+          in = a.code[pc];
+        }
         const uint32_t c = in.code;
         T save[R];
         if (c & SR_F_INFSUB) {
@@ -249,9 +272,7 @@ __global__ void __launch_bounds__(SR_BLOCK) sr_interp_kernel(const SrEvalArgs<T>
         }
         switch (SR_OPC(c)) {
           case SR_OP_LOAD_FEAT: {
-            const uint32_t f = in.arg;
-#pragma unroll
-            for (int r = 0; r < R; ++r) tos[r] = xr[f][r];
+            sr_fetch_feature<T, R, FCAP>(xr, in.arg, tos);
             break;
           }
           case SR_OP_LOAD_CONST: {
@@ -262,9 +283,7 @@ __global__ void __launch_bounds__(SR_BLOCK) sr_interp_kernel(const SrEvalArgs<T>
           case SR_OP_LOAD_FEAT_PUSH: {
             SrVec<T, R>::store(stk + size_t(sp) * 64 * R, tos);
             ++sp;
-            const uint32_t f = in.arg;
-#pragma unroll
-            for (int r = 0; r < R; ++r) tos[r] = xr[f][r];
+            sr_fetch_feature<T, R, FCAP>(xr, in.arg, tos);
             break;
           }
           case SR_OP_LOAD_CONST_PUSH: {
@@ -306,7 +325,7 @@ __global__ void __launch_bounds__(SR_BLOCK) sr_interp_kernel(const SrEvalArgs<T>
 #pragma unroll
               for (int r = 0; r < R; ++r) s += valid[r] ? double(tos[r]) * a.scale : 0.0;
               s = sr_wave_sum<double>(s);
-              if (lane == 0) atomicAdd(a.check_sums + size_t(tree0 + g) * a.max_checks + check_k, s);
+              if (lane == 0) xacc[wave * MC + check_k] += s;
               ++check_k;
             } else {
               // padded rows replicate row 0 of the view, so no row mask is needed here
@@ -338,11 +357,21 @@ __global__ void __launch_bounds__(SR_BLOCK) sr_interp_kernel(const SrEvalArgs<T>
           continue;
         }
         T yv[R];
-        SrVec<T, R>::load(ylds, yv);
+        if (GATHER) {
+#pragma unroll
+          for (int r = 0; r < R; ++r) yv[r] = a.y[idx[r]];
+        } else {
+          SrVec<T, R>::load(a.y + row0, yv);
+        }
         T s = T(0);
         if (weighted) {
           T wv[R];
-          SrVec<T, R>::load(wlds, wv);
+          if (GATHER) {
+#pragma unroll
+            for (int r = 0; r < R; ++r) wv[r] = a.w[idx[r]];
+          } else {
+            SrVec<T, R>::load(a.w + row0, wv);
+          }
 #pragma unroll
           for (int r = 0; r < R; ++r) {
             const T l = sr_elem_loss<T>(a.loss_kind, tos[r], yv[r]) * wv[r];
@@ -373,8 +402,17 @@ __global__ void __launch_bounds__(SR_BLOCK) sr_interp_kernel(const SrEvalArgs<T>
     }
   }
 
-  if (MODE == SR_MODE_EXACT) return;
   __syncthreads();
+  if (MODE == SR_MODE_EXACT) {
+    // one device-scope add per (block, check): 256-way instead of 4096-way contention per word
+    for (int k = tid; k < MC; k += SR_BLOCK) {
+      double v = 0.0;
+#pragma unroll
+      for (int w = 0; w < SR_WAVES; ++w) v += xacc[w * MC + k];
+      if (v != 0.0) atomicAdd(a.check_sums + size_t(tree0) * MC + k, v);
+    }
+    return;
+  }
   for (int g = tid; g < gcount; g += SR_BLOCK) {
     double s = 0.0;
     uint32_t f = 0u;
@@ -391,29 +429,28 @@ __global__ void __launch_bounds__(SR_BLOCK) sr_interp_kernel(const SrEvalArgs<T>
 
 // ------------------------------------------------------------------ launch helpers
 template <typename T>
-size_t sr_interp_lds_bytes(int trees_per_block) {
-  constexpr int R = 16 / sizeof(T);
-  return size_t(SR_WAVES) * SR_STACK_DEPTH * 64 * R * sizeof(T) + 2 * size_t(SR_BLOCK) * R * sizeof(T) +
+size_t sr_interp_lds_bytes(int trees_per_block, int rows_per_lane, int max_checks) {
+  return size_t(SR_WAVES) * SR_STACK_DEPTH * 64 * rows_per_lane * sizeof(T) +
          size_t(SR_WAVES) * trees_per_block * 8 + size_t(SR_WAVES) * trees_per_block * 4 +
-         size_t(trees_per_block) * 4;
+         size_t((trees_per_block + 3) & ~3) * 4 + size_t(SR_WAVES) * max_checks * 8;
 }
 
-template <typename T, int FCAP, int MODE, bool GATHER, int TIER>
+template <typename T, int R, int FCAP, int MODE, bool GATHER, int TIER, int VAR>
 static hipError_t launch_interp(const SrEvalArgs<T>& a, int n_blocks, hipStream_t s) {
-  constexpr int R = 16 / sizeof(T);
-  const size_t lds = sr_interp_lds_bytes<T>(a.trees_per_block);
-  hipLaunchKernelGGL((sr_interp_kernel<T, R, FCAP, MODE, GATHER, TIER>), dim3(n_blocks), dim3(SR_BLOCK), lds, s, a);
+  const size_t lds = sr_interp_lds_bytes<T>(a.trees_per_block, R, MODE == SR_MODE_EXACT ? a.max_checks : 0);
+  hipLaunchKernelGGL((sr_interp_kernel<T, R, FCAP, MODE, GATHER, TIER, VAR>), dim3(n_blocks), dim3(SR_BLOCK), lds, s,
+                     a);
   return hipGetLastError();
 }
 
-template <typename T, int MODE, bool GATHER, int TIER>
+template <typename T, int R, int MODE, bool GATHER, int TIER, int VAR>
 hipError_t sr_dispatch_interp(const SrEvalArgs<T>& a, int n_blocks, hipStream_t s) {
-  if (a.nf <= 4) return launch_interp<T, 4, MODE, GATHER, TIER>(a, n_blocks, s);
-  if (a.nf <= 8) return launch_interp<T, 8, MODE, GATHER, TIER>(a, n_blocks, s);
-  return launch_interp<T, SR_MAX_FEATURES, MODE, GATHER, TIER>(a, n_blocks, s);
+  if (a.nf <= 4) return launch_interp<T, R, 4, MODE, GATHER, TIER, VAR>(a, n_blocks, s);
+  if (a.nf <= 8) return launch_interp<T, R, 8, MODE, GATHER, TIER, VAR>(a, n_blocks, s);
+  return launch_interp<T, R, SR_MAX_FEATURES, MODE, GATHER, TIER, VAR>(a, n_blocks, s);
 }
 
 // Explicit instantiations are spread over several translation units (sr_inst_*.hip, one per
 // element type / mode) so the build compiles them in parallel; see the Makefile.
-#define SR_INSTANTIATE(T, MODE, GATHER, TIER) \
-  template hipError_t sr_dispatch_interp<T, MODE, GATHER, TIER>(const SrEvalArgs<T>&, int, hipStream_t);
+#define SR_INSTANTIATE(T, R, MODE, GATHER, TIER, VAR) \
+  template hipError_t sr_dispatch_interp<T, R, MODE, GATHER, TIER, VAR>(const SrEvalArgs<T>&, int, hipStream_t);

@@ -10,21 +10,21 @@ def rel(a, b):
         return np.where(both_inf, 0.0, np.abs(a - b) / np.maximum(np.abs(b), 1e-30))
 
 
-def well_conditioned(orc, tb, X, y, w=None, loss_kind=0, tol=1e-5):
-    """Trees whose Float32 loss is determined by the data, not by rounding.
+def well_conditioned(orc, tb, X, y, w=None, loss_kind=0, tol=2e-5):
+    """Trees whose loss is determined by the data, not by how the libm rounds.
 
-    The f32 loss of the oracle is compared with the same tree evaluated in f64 (constants and data
-    widened exactly).  Where they differ by more than `tol`, the f32 result is dominated by
-    rounding amplified through the tree (e.g. cos of exp(exp(x))): two correctly-rounded libms
-    (glibc, ROCm OCML, Julia's own) legitimately disagree there, so the 1e-4 loss bar of the
-    north star applies to the well-conditioned trees only; flags are compared on every tree.
-    Returns (mask, o32_loss, o32_complete).
+    The oracle evaluates every tree three times: as is, and twice with every libm result (exp,
+    cos, log, ...; not the IEEE-exact + - * / sqrt) nudged by one ulp with a pseudo-random sign
+    per (node, row) — the independent last-bit differences two libms make.  Where the loss moves
+    by more than `tol`, the tree amplifies last-bit differences (cancellation such as
+    c - log(exp(x)), cos of exp(exp(x)), ...): two correctly rounded libms (glibc, ROCm OCML,
+    Julia's own) legitimately disagree there, and so would the reference itself.  The north-star
+    loss bar (1e-4 relative) is applied to the well-conditioned trees; `complete` flags are
+    compared on every tree.  Returns (mask, loss, complete) of the unperturbed oracle.
     """
-    l32, c32 = orc.eval_loss_batch(tb, X, y, w=w, loss_kind=loss_kind, accum="f64", n_threads=8)
-    X64 = np.asarray(X, dtype=np.float64)
-    y64 = np.asarray(y, dtype=np.float64)
-    w64 = None if w is None else np.asarray(w, dtype=np.float64)
-    l64, c64 = orc.eval_loss_batch(tb.astype(np.float64), X64, y64, w=w64, loss_kind=loss_kind, accum="f64",
-                                   n_threads=8)
-    mask = c32 & c64 & (rel(l32, l64) < tol)
-    return mask, l32, c32
+    kw = dict(w=w, loss_kind=loss_kind, accum="f64", n_threads=8)
+    l0, c0 = orc.eval_loss_batch(tb, X, y, **kw)
+    lp, cp = orc.eval_loss_batch(tb, X, y, perturb=1, **kw)
+    lm, cm = orc.eval_loss_batch(tb, X, y, perturb=2, **kw)
+    mask = c0 & cp & cm & (rel(lp, l0) < tol) & (rel(lm, l0) < tol)
+    return mask, l0, c0
