@@ -181,9 +181,13 @@ def test_predictions_vs_oracle():
         o, c = orc.eval_tree_array(tb, k, X)
         assert comp[k] == c, (k, sr_amd.string_tree(tb.tree(k), opts.operators))
         if c:
-            o64, c64 = orc.eval_tree_array(tb.astype(np.float64), k, X.astype(np.float64))
-            # rows whose f32 value is rounding-dominated (|f32 - f64| > 1e-5 rel) are excluded
-            okrow = np.abs(o.astype(np.float64) - o64) <= 1e-5 * np.maximum(np.abs(o64), 1e-3)
+            # rows whose value moves under +-1-ulp libm perturbations are rounding-dominated
+            # (cancellation, or a floor/sign/comparison sitting on its threshold): excluded
+            p1, _ = orc.eval_tree_array(tb, k, X, perturb=1)
+            p2, _ = orc.eval_tree_array(tb, k, X, perturb=2)
+            scale = np.maximum(np.abs(o.astype(np.float64)), 1e-3)
+            okrow = (np.abs(p1 - o) <= 2e-5 * scale) & (np.abs(p2 - o) <= 2e-5 * scale)
+            assert okrow.mean() > 0.9
             np.testing.assert_allclose(out[k][okrow], o[okrow], rtol=1e-4, atol=1e-6)
 
 
