@@ -88,44 +88,13 @@ def main():
     else:
         import torch
 
-        dev = torch.device("cuda", local_rank)
-        sums = torch.zeros(nt, dtype=torch.float64, device=dev)
-        flags = torch.zeros(nt, dtype=torch.int32, device=dev)
-        losses = np.empty(nt, dtype=np.float32)
-        comp = np.empty(nt, dtype=np.uint8)
+        from sr_amd.distributed import eval_loss_sharded
+
+        result = {}
 
         def step():
-            _lib.check(_lib.lib.sr_eval_loss_partials(ctx.handle, dsh, oid, ctypes.byref(s), n_total, 0,
-                                                      ctypes.c_void_p(sums.data_ptr()),
-                                                      ctypes.c_void_p(flags.data_ptr()), 1))
-            kms = ctx.last_kernel_ms()[0]
-            dist.all_reduce(sums, op=dist.ReduceOp.SUM)
-            dist.all_reduce(flags, op=dist.ReduceOp.BOR)
-            hs = sums.cpu().numpy()
-            hf = flags.cpu().numpy().astype(np.uint32)
-            # rare exact-sum path: trees only "close to overflow" (no non-finite anywhere)
-            big = np.nonzero(((hf & (_lib.SR_FLAG_NONFINITE | _lib.SR_FLAG_STATIC)) == 0) & ((hf & _lib.SR_FLAG_BIG) != 0))[0]
-            cs = None
-            mc = 0
-            if big.size:
-                m = ctypes.c_int()
-                _lib.check(_lib.lib.sr_max_checks(ctx.handle, oid, ctypes.byref(s), ctypes.byref(m)))
-                mc = int(m.value)
-                lst = np.ascontiguousarray(big, dtype=np.int64)
-                part = np.zeros((big.size, mc))
-                _lib.check(_lib.lib.sr_exact_check_partials(ctx.handle, dsh, oid, ctypes.byref(s),
-                                                            lst.ctypes.data_as(ctypes.c_void_p), big.size, mc,
-                                                            part.ctypes.data_as(ctypes.c_void_p)))
-                t = torch.from_numpy(part).to(dev)
-                dist.all_reduce(t, op=dist.ReduceOp.SUM)
-                cs = np.ascontiguousarray(t.cpu().numpy())
-            lst_p = None if not big.size else np.ascontiguousarray(big, dtype=np.int64)
-            p = lambda a: None if a is None else a.ctypes.data_as(ctypes.c_void_p)
-            _lib.check(_lib.lib.sr_finalize_losses(_lib.SR_DTYPE_F32, nt, p(np.ascontiguousarray(hs)),
-                                                   p(np.ascontiguousarray(hf)), float(n_total), p(lst_p),
-                                                   0 if lst_p is None else lst_p.size, mc, p(cs),
-                                                   p(losses), p(comp)))
-            return kms
+            result["loss"], result["comp"] = eval_loss_sharded(tb, ds, opts, n_total)
+            return ctx.last_kernel_ms()[0]
 
         def barrier():
             dist.barrier()
@@ -155,6 +124,8 @@ def main():
     flops_per_launch = float(args.rows) * (ops + 3 * nt)
     kmean = float(np.mean(kernel_ms))
     achieved = flops_per_launch / (kmean * 1e-3) / 1e12
+    if world > 1:
+        comp = result["comp"]
     frac_complete = float(np.mean(comp.astype(bool)))
 
     cpu = None

@@ -1,0 +1,36 @@
+"""Kernel-time breakdown by operator mix (GPU box).  Prints one line per population."""
+import os, sys, time
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [os.path.join(ROOT, "symbolicregression.jl_amd")]
+import numpy as np
+import sr_amd
+from sr_amd import Options, Dataset, flatten_trees, gen_random_population, eval_loss_batch
+
+n = 1 << 20
+rng = np.random.default_rng(2)
+X = rng.standard_normal((5, n)).astype(np.float32)
+y = (2 * np.cos(X[3]) + X[0] ** 2 - 2).astype(np.float32)
+ds = Dataset(X, y)
+ctx = sr_amd.get_context()
+mixes = {
+    "arith(+-*/)": dict(binary_operators=["+", "-", "*"], unary_operators=["neg"]),
+    "arith+div": dict(binary_operators=["+", "-", "*", "/"], unary_operators=["neg"]),
+    "C2(+-*/ cos exp log)": dict(binary_operators=["+", "-", "*", "/"], unary_operators=["cos", "exp", "log"]),
+    "cos-only": dict(binary_operators=["+", "*"], unary_operators=["cos"]),
+    "exp-only": dict(binary_operators=["+", "*"], unary_operators=["exp"]),
+    "sin-only": dict(binary_operators=["+", "*"], unary_operators=["sin"]),
+}
+for name, kw in mixes.items():
+    opts = Options(**kw)
+    tb = flatten_trees(gen_random_population(10000, opts, 5, seed=1), np.float32)
+    eval_loss_batch(tb, ds, opts)
+    ks, ts = [], []
+    for _ in range(5):
+        t0 = time.perf_counter()
+        l, c = eval_loss_batch(tb, ds, opts)
+        ts.append(time.perf_counter() - t0)
+        ks.append(ctx.last_kernel_ms()[0])
+    k = float(np.median(ks)); t = float(np.median(ts)) * 1e3
+    ne = tb.n_nodes * n
+    print(f"{name:24s} nodes={tb.n_nodes:7d} ops={tb.n_operator_nodes:6d} complete={c.mean():.3f} "
+          f"kernel={k:7.3f}ms step={t:7.3f}ms  {ne / k / 1e9:8.1f} Gnode/s(kernel)  {ne / t / 1e9:8.1f} Gnode/s(step)", flush=True)
