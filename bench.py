@@ -164,7 +164,7 @@ def main():
                 "unit": "TFLOP/s",
                 "frac": achieved / PEAK_FP32_TFLOPS,
                 "traffic": None,
-                "kernel": "sr_interp_kernel<float,4,8,LOSS,gather=false,BASIC>",
+                "kernel": "sr_tile_kernel<float,8,LOSS,gather=false,BASIC>",
                 "kernel_ms_mean": kmean,
                 "flops_per_launch": flops_per_launch,
                 "flop_convention": "n_rows * sum_t(n_op(t) + 3), 1 flop per operator incl. transcendentals (SURVEY 8d)",

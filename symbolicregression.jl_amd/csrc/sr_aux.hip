@@ -1,5 +1,5 @@
 // sr_aux.hip — small kernels around the interpreter: fixed-order partial reduction, dataset
-// transpose/padding, and the runtime dispatcher over the explicitly instantiated interpreters.
+// transpose/padding, and the runtime dispatcher over the explicitly instantiated tile kernels.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -82,33 +82,66 @@ hipError_t sr_launch_pad(T* v, int64_t n, int64_t ld, T pad_value, int replicate
   return hipGetLastError();
 }
 
+// Rows per lane of each instantiated kernel (sr_inst_*.hip): f32 BASIC 8 (4 for tuning), f32 FULL 4,
+// f64 BASIC 4, f64 FULL 2.  `rows_per_lane` <= 0 picks the default.
 template <typename T>
-hipError_t sr_launch_interp(const SrEvalArgs<T>& a, int mode, bool gather, int tier, SrVariant v, int n_blocks,
-                            hipStream_t s) {
-  constexpr int R = 16 / sizeof(T);
-  if (mode == SR_MODE_LOSS) {
-    if (tier == SR_TIER_BASIC) {
-      if (!gather) {
-        if constexpr (sizeof(T) == 4) {
-          if (v.rows_per_lane == 8) return sr_dispatch_interp<T, 8, SR_MODE_LOSS, false, SR_TIER_BASIC, 1>(a, n_blocks, s);
-          if (v.var == 0) return sr_dispatch_interp<T, 4, SR_MODE_LOSS, false, SR_TIER_BASIC, 0>(a, n_blocks, s);
-        }
-        return sr_dispatch_interp<T, R, SR_MODE_LOSS, false, SR_TIER_BASIC, 1>(a, n_blocks, s);
-      }
-      return sr_dispatch_interp<T, R, SR_MODE_LOSS, true, SR_TIER_BASIC, 1>(a, n_blocks, s);
-    }
-    return gather ? sr_dispatch_interp<T, R, SR_MODE_LOSS, true, SR_TIER_FULL, 1>(a, n_blocks, s)
-                  : sr_dispatch_interp<T, R, SR_MODE_LOSS, false, SR_TIER_FULL, 1>(a, n_blocks, s);
+int sr_rows_per_lane(int mode, int tier, int requested) {
+  const bool basic = mode == SR_MODE_LOSS && tier == SR_TIER_BASIC;
+  if (sizeof(T) == 4) {
+    if (basic) return requested == 4 ? 4 : 8;
+    return 4;
   }
-  if (mode == SR_MODE_PRED)
-    return gather ? sr_dispatch_interp<T, R, SR_MODE_PRED, true, SR_TIER_FULL, 1>(a, n_blocks, s)
-                  : sr_dispatch_interp<T, R, SR_MODE_PRED, false, SR_TIER_FULL, 1>(a, n_blocks, s);
-  return gather ? sr_dispatch_interp<T, R, SR_MODE_EXACT, true, SR_TIER_FULL, 1>(a, n_blocks, s)
-                : sr_dispatch_interp<T, R, SR_MODE_EXACT, false, SR_TIER_FULL, 1>(a, n_blocks, s);
+  return basic ? 4 : 2;
+}
+template int sr_rows_per_lane<float>(int, int, int);
+template int sr_rows_per_lane<double>(int, int, int);
+
+size_t sr_tile_lds_bytes(int elem_size, int nf, int rows_per_lane, int stack_depth, int trees_per_block,
+                         int max_checks) {
+  const size_t rows = size_t(64) * rows_per_lane;
+  return size_t(nf) * rows * elem_size + 2 * rows * elem_size + size_t(4) * stack_depth * rows * elem_size +
+         size_t(trees_per_block) * 8 + size_t((trees_per_block + 3) & ~3) * 4 +
+         size_t(trees_per_block) * size_t(max_checks) * 8;
 }
 
-template hipError_t sr_launch_interp<float>(const SrEvalArgs<float>&, int, bool, int, SrVariant, int, hipStream_t);
-template hipError_t sr_launch_interp<double>(const SrEvalArgs<double>&, int, bool, int, SrVariant, int, hipStream_t);
+template <typename T>
+hipError_t sr_launch_eval(const SrEvalArgs<T>& a, int mode, bool gather, int tier, int rows_per_lane, int n_blocks,
+                          hipStream_t s) {
+  const int R = sr_rows_per_lane<T>(mode, tier, rows_per_lane);
+  if constexpr (sizeof(T) == 4) {
+    if (mode == SR_MODE_LOSS) {
+      if (tier == SR_TIER_BASIC) {
+        if (gather) return sr_launch_tile<T, 8, SR_MODE_LOSS, true, SR_TIER_BASIC>(a, n_blocks, s);
+        return R == 4 ? sr_launch_tile<T, 4, SR_MODE_LOSS, false, SR_TIER_BASIC>(a, n_blocks, s)
+                      : sr_launch_tile<T, 8, SR_MODE_LOSS, false, SR_TIER_BASIC>(a, n_blocks, s);
+      }
+      return gather ? sr_launch_tile<T, 4, SR_MODE_LOSS, true, SR_TIER_FULL>(a, n_blocks, s)
+                    : sr_launch_tile<T, 4, SR_MODE_LOSS, false, SR_TIER_FULL>(a, n_blocks, s);
+    }
+    if (mode == SR_MODE_PRED)
+      return gather ? sr_launch_tile<T, 4, SR_MODE_PRED, true, SR_TIER_FULL>(a, n_blocks, s)
+                    : sr_launch_tile<T, 4, SR_MODE_PRED, false, SR_TIER_FULL>(a, n_blocks, s);
+    return gather ? sr_launch_tile<T, 4, SR_MODE_EXACT, true, SR_TIER_FULL>(a, n_blocks, s)
+                  : sr_launch_tile<T, 4, SR_MODE_EXACT, false, SR_TIER_FULL>(a, n_blocks, s);
+  } else {
+    (void)R;
+    if (mode == SR_MODE_LOSS) {
+      if (tier == SR_TIER_BASIC)
+        return gather ? sr_launch_tile<T, 4, SR_MODE_LOSS, true, SR_TIER_BASIC>(a, n_blocks, s)
+                      : sr_launch_tile<T, 4, SR_MODE_LOSS, false, SR_TIER_BASIC>(a, n_blocks, s);
+      return gather ? sr_launch_tile<T, 2, SR_MODE_LOSS, true, SR_TIER_FULL>(a, n_blocks, s)
+                    : sr_launch_tile<T, 2, SR_MODE_LOSS, false, SR_TIER_FULL>(a, n_blocks, s);
+    }
+    if (mode == SR_MODE_PRED)
+      return gather ? sr_launch_tile<T, 2, SR_MODE_PRED, true, SR_TIER_FULL>(a, n_blocks, s)
+                    : sr_launch_tile<T, 2, SR_MODE_PRED, false, SR_TIER_FULL>(a, n_blocks, s);
+    return gather ? sr_launch_tile<T, 2, SR_MODE_EXACT, true, SR_TIER_FULL>(a, n_blocks, s)
+                  : sr_launch_tile<T, 2, SR_MODE_EXACT, false, SR_TIER_FULL>(a, n_blocks, s);
+  }
+}
+
+template hipError_t sr_launch_eval<float>(const SrEvalArgs<float>&, int, bool, int, int, int, hipStream_t);
+template hipError_t sr_launch_eval<double>(const SrEvalArgs<double>&, int, bool, int, int, int, hipStream_t);
 template hipError_t sr_launch_transpose<float>(const float*, int64_t, int64_t, int64_t, float*, hipStream_t);
 template hipError_t sr_launch_transpose<double>(const double*, int64_t, int64_t, int64_t, double*, hipStream_t);
 template hipError_t sr_launch_pad<float>(float*, int64_t, int64_t, float, int, hipStream_t);

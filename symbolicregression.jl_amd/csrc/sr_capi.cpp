@@ -76,7 +76,7 @@ struct sr_ctx {
       check_sums;
   double last_eval_ms = 0.0, last_total_ms = 0.0;
   int cu_count = 256;
-  SrVariant variant{4, 1};  // SR_AMD_VARIANT (tuning): 0 default, 1 = R4 no prefetch, 2 = R8 prefetch
+  int rows_override = 0;    // SR_AMD_ROWS_PER_LANE (tuning): 4 selects the f32 BASIC 4-rows/lane kernel
   int tree_group = 0;       // SR_AMD_TREES_PER_BLOCK override (0 = heuristic)
 };
 
@@ -93,29 +93,38 @@ struct sr_dataset {
 
 namespace {
 
-constexpr int64_t kRowAlign = 2048;  // one row tile at the widest variant (256 lanes x 8 rows)
+constexpr int64_t kRowAlign = 2048;  // a multiple of every kernel's row tile (64 lanes x R rows)
 
-// Work decomposition: row tiles of 256*R rows, grouped `tiles` per block; trees grouped G per block.
+// Work decomposition: row tiles of 64*R rows (one LDS image each), `tiles` per block; trees grouped G
+// per block (the block's 4 waves share the G trees of a tile).
 struct Grid {
-  int G = 32, tiles = 1, n_row_blocks = 1, n_groups = 1;
+  int G = 32, tiles = 1, n_row_blocks = 1, n_groups = 1, R = 8;
   int64_t n_blocks = 1;
+  size_t lds = 0;
 };
+constexpr size_t kLdsMax = 160 * 1024;
 template <typename T>
-Grid make_grid(int64_t n_rows, int64_t n_trees, int rows_per_lane = 16 / sizeof(T), int g_override = 0) {
-  const int64_t rows_per_tile = 256 * int64_t(rows_per_lane);
+Grid make_grid(int64_t n_rows, int64_t n_trees, int R, int nf, int depth, int max_checks, int g_override = 0) {
+  const int64_t rows_per_tile = 64 * int64_t(R);
   Grid g;
+  g.R = R;
   const int64_t n_tiles = (n_rows + rows_per_tile - 1) / rows_per_tile;
   int64_t tiles = (n_tiles + 255) / 256;  // keep <= 256 row blocks per tree
   if (tiles < 1) tiles = 1;
   g.tiles = int(tiles);
   g.n_row_blocks = int((n_tiles + tiles - 1) / tiles);
   if (g.n_row_blocks < 1) g.n_row_blocks = 1;
-  int G = 32;
-  while (G > 1 && int64_t(g.n_row_blocks) * ((n_trees + G - 1) / G) < 2048) G /= 2;
+  // more trees per tile amortise the tile's LDS staging and barriers (G 16 -> 128: -29% kernel time
+  // on the C2 population); shrink only to keep >= 4096 workgroups for small populations
+  int G = 128;
+  while (G > 4 && int64_t(g.n_row_blocks) * ((n_trees + G - 1) / G) < 4096) G /= 2;
   if (g_override > 0) G = g_override;
+  if (n_trees > 0 && G > n_trees) G = int(n_trees);
+  if (G < 1) G = 1;
   g.G = G;
   g.n_groups = int((n_trees + G - 1) / G);
   g.n_blocks = int64_t(g.n_row_blocks) * g.n_groups;
+  g.lds = sr_tile_lds_bytes(int(sizeof(T)), nf, R, depth, G, max_checks);
   return g;
 }
 
@@ -153,21 +162,20 @@ int run_batch(sr_ctx* ctx, const sr_dataset* ds, int opset_id, const sr_tree_bat
   const bool gather = row_idx != nullptr && n_idx > 0;
   const int64_t n_eval = gather ? n_idx : ds->n;
   if (n_eval <= 0) return set_error(SR_ERR_INVALID_ARG, "no rows to evaluate");
-  if (ds->nf > SR_MAX_FEATURES)
-    return set_error(SR_ERR_INVALID_ARG, "nfeatures > " + std::to_string(SR_MAX_FEATURES) +
-                                             " is not supported by the register-resident X tile");
   if (loss_kind != SR_LOSS_L2DIST && loss_kind != SR_LOSS_L1DIST)
     return set_error(SR_ERR_INVALID_ARG, "unsupported loss kind");
   std::string err;
   int rc = sr_compile_batch<T>(*trees, ctx->opsets[opset_id], n_total, ds->nf, false, prog, &err);
   if (rc != SR_OK) return set_error(rc, err);
-  if (prog->max_depth > 4)
-    return set_error(SR_ERR_TOO_DEEP, "a tree needs " + std::to_string(prog->max_depth) +
-                                          " operand-stack slots; the kernel holds 4 (maxsize <= 94)");
   const int64_t nt = trees->n_trees;
-  const bool tuned = sizeof(T) == 4 && mode == SR_MODE_LOSS && !gather && ctx->tiers[opset_id] == SR_TIER_BASIC;
-  const SrVariant var = tuned ? ctx->variant : SrVariant{int(16 / sizeof(T)), 1};
-  Grid g = make_grid<T>(n_eval, nt, var.rows_per_lane, ctx->tree_group);
+  const int tier = ctx->tiers[opset_id];
+  const int depth = prog->max_depth > 0 ? prog->max_depth : 1;
+  const int R = sr_rows_per_lane<T>(mode, tier, ctx->rows_override);
+  Grid g = make_grid<T>(n_eval, nt, R, int(ds->nf), depth, 0, ctx->tree_group);
+  if (g.lds > kLdsMax)
+    return set_error(SR_ERR_TOO_DEEP, "the row tile (" + std::to_string(ds->nf) + " features, " +
+                                          std::to_string(depth) + " stack slots) needs " + std::to_string(g.lds) +
+                                          " bytes of LDS; the limit is 160 KiB");
   *grid_out = g;
   if (nt == 0) return SR_OK;
 
@@ -211,6 +219,8 @@ int run_batch(sr_ctx* ctx, const sr_dataset* ds, int opset_id, const sr_tree_bat
   a.nf = int(ds->nf);
   a.tiles_per_block = g.tiles;
   a.n_row_blocks = g.n_row_blocks;
+  a.n_groups = g.n_groups;
+  a.stack_depth = depth;
   // Σ over n_total rows of values below tbig cannot overflow T, even with rounding slack.
   a.tbig = T(t_max<T>() / (2.0 * double(n_total > 0 ? n_total : 1)));
   a.loss_kind = loss_kind;
@@ -220,9 +230,8 @@ int run_batch(sr_ctx* ctx, const sr_dataset* ds, int opset_id, const sr_tree_bat
   a.pred_ld = n_eval;
   a.scale = 1.0;
   if (g.n_blocks > 0x7fffffff) return set_error(SR_ERR_INVALID_ARG, "grid too large");
-  const int tier = ctx->tiers[opset_id];
   SR_HIP_CHECK(hipEventRecord(ctx->ev_k0, s));
-  SR_HIP_CHECK(sr_launch_interp<T>(a, mode, gather, tier, var, int(g.n_blocks), s));
+  SR_HIP_CHECK(sr_launch_eval<T>(a, mode, gather, tier, ctx->rows_override, int(g.n_blocks), s));
   SR_HIP_CHECK(hipEventRecord(ctx->ev_k1, s));
   SR_HIP_CHECK(sr_launch_reduce(a.part_sum, a.part_flag, int(nt), g.n_row_blocks, ctx->static_bad.as<uint8_t>(),
                                 ctx->out_sum.as<double>(), ctx->out_flag.as<uint32_t>(), s));
@@ -238,7 +247,10 @@ int run_exact(sr_ctx* ctx, const sr_dataset* ds, const SrProgramBatch<T>& prog, 
   const bool gather = row_idx != nullptr && n_idx > 0;
   const int64_t n_eval = gather ? n_idx : ds->n;
   hipStream_t s = ctx->stream;
-  Grid g = make_grid<T>(n_eval, 1);
+  const int depth = prog.max_depth > 0 ? prog.max_depth : 1;
+  Grid g = make_grid<T>(n_eval, 1, sr_rows_per_lane<T>(SR_MODE_EXACT, SR_TIER_FULL, 0), int(ds->nf), depth,
+                        max_checks, 1);
+  if (g.lds > kLdsMax) return set_error(SR_ERR_TOO_DEEP, "exact-sum pass needs more LDS than 160 KiB");
   SR_HIP_CHECK(ctx->tree_list.ensure(size_t(n_list) * sizeof(int64_t)));
   SR_HIP_CHECK(ctx->check_sums.ensure(size_t(n_list) * max_checks * sizeof(double)));
   SR_HIP_CHECK(hipMemcpyAsync(ctx->tree_list.p, list, size_t(n_list) * sizeof(int64_t), hipMemcpyHostToDevice, s));
@@ -259,6 +271,8 @@ int run_exact(sr_ctx* ctx, const sr_dataset* ds, const SrProgramBatch<T>& prog, 
   a.nf = int(ds->nf);
   a.tiles_per_block = g.tiles;
   a.n_row_blocks = g.n_row_blocks;
+  a.n_groups = int(n_list);
+  a.stack_depth = depth;
   a.tbig = T(0);
   a.part_sum = ctx->part_sum.as<double>();
   a.part_flag = ctx->part_flag.as<uint32_t>();
@@ -269,12 +283,10 @@ int run_exact(sr_ctx* ctx, const sr_dataset* ds, const SrProgramBatch<T>& prog, 
   a.scale = sizeof(T) == 8 ? std::ldexp(1.0, -64) : 1.0;
   const int64_t blocks = int64_t(g.n_row_blocks) * n_list;
   if (blocks > 0x7fffffff) return set_error(SR_ERR_INVALID_ARG, "grid too large");
-  SR_HIP_CHECK(sr_launch_interp<T>(a, SR_MODE_EXACT, gather, SR_TIER_FULL, SrVariant{int(16 / sizeof(T)), 1},
-                                   int(blocks), s));
+  SR_HIP_CHECK(sr_launch_eval<T>(a, SR_MODE_EXACT, gather, SR_TIER_FULL, 0, int(blocks), s));
   SR_HIP_CHECK(hipMemcpyAsync(host_sums, ctx->check_sums.p, size_t(n_list) * max_checks * sizeof(double),
                               hipMemcpyDeviceToHost, s));
   SR_HIP_CHECK(hipStreamSynchronize(s));
-  (void)prog;
   return SR_OK;
 }
 
@@ -500,11 +512,7 @@ int sr_init(int device, sr_ctx** out) {
   ctx->device = device;
   hipDeviceProp_t prop;
   if (hipGetDeviceProperties(&prop, device) == hipSuccess) ctx->cu_count = prop.multiProcessorCount;
-  if (const char* v = std::getenv("SR_AMD_VARIANT")) {
-    const int k = std::atoi(v);
-    if (k == 1) ctx->variant = SrVariant{4, 0};
-    if (k == 2) ctx->variant = SrVariant{8, 1};
-  }
+  if (const char* v = std::getenv("SR_AMD_ROWS_PER_LANE")) ctx->rows_override = std::atoi(v);
   if (const char* v = std::getenv("SR_AMD_TREES_PER_BLOCK")) ctx->tree_group = std::atoi(v);
   hipError_t e = hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking);
   if (e == hipSuccess) e = hipEventCreate(&ctx->ev_start);

@@ -271,11 +271,11 @@ struct TreeCompiler {
     if (folded[i]) {
       in.code = SR_OP_LOAD_CONST;
       in.val = fold_val[i];
-      in.arg = 0xffffffffu;
+      in.arg = SR_A_INDEX;
     } else if (t.constant[i]) {
       in.code = SR_OP_LOAD_CONST;
       in.val = t.val[i];
-      in.arg = with_const_index ? uint32_t(const_slot[i]) : 0xffffffffu;
+      in.arg = with_const_index ? uint32_t(const_slot[i]) : SR_A_INDEX;
     } else {
       in.code = SR_OP_LOAD_FEAT;
       in.arg = uint32_t(t.feature[i]) - 1u;
@@ -297,7 +297,7 @@ struct TreeCompiler {
       static_array_check(folded[i] ? fold_val[i] : t.val[i]);
       return;
     }
-    code.back().code |= SR_F_CHECK;
+    code.back().arg |= SR_A_CHECK;
     ++n_checks;
   }
 
@@ -317,8 +317,19 @@ struct TreeCompiler {
     if (d == 1) {
       emit(t.l[i]);
       SrIns<T> in{};
-      in.code = (SR_OP_UNARY0 + unary_id(i)) | (infsub[i] ? SR_F_INFSUB : 0u);
+      if (infsub[i]) {  // fused unary: remember the operand on the stack, fix the output up after
+        SrIns<T> sv{};
+        sv.code = SR_OP_SAVE;
+        code.push_back(sv);
+        if (depth + 1 > max_depth) max_depth = depth + 1;
+      }
+      in.code = SR_OP_UNARY0 + unary_id(i);
       code.push_back(in);
+      if (infsub[i]) {
+        SrIns<T> fx{};
+        fx.code = SR_OP_FIXUP;
+        code.push_back(fx);
+      }
       emit_check(i);
       return;
     }
@@ -449,6 +460,7 @@ int sr_compile_batch(const sr_tree_batch& trees, const SrOpset& ops, int64_t n_r
         errs[k] = tc.err;
         continue;
       }
+      for (auto& in : tc.code) in.arg |= sr_operand_tag(in.code);
       PerTree& p = per[k];
       p.code.swap(tc.code);
       p.bad = (tc.bad || p.code.empty()) ? 1 : 0;

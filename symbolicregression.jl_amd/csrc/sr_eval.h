@@ -7,7 +7,6 @@
 
 enum { SR_MODE_LOSS = 0, SR_MODE_PRED = 1, SR_MODE_EXACT = 2 };
 enum { SR_TIER_BASIC = 0, SR_TIER_FULL = 1 };
-#define SR_MAX_FEATURES 16  // register-resident X tile: nfeatures <= 16
 
 template <typename T>
 struct SrEvalArgs {
@@ -26,6 +25,8 @@ struct SrEvalArgs {
   int nf;
   int tiles_per_block;
   int n_row_blocks;
+  int n_groups;                // tree groups (blockIdx = row_block * n_groups + group)
+  int stack_depth;             // LDS operand-stack slots per wave (>= 1)
   T tbig;                      // |v| >= tbig may overflow the array-sum check
   int loss_kind;
   // outputs
@@ -40,19 +41,18 @@ struct SrEvalArgs {
   double scale;
 };
 
-template <typename T, int R, int MODE, bool GATHER, int TIER, int VAR>
-hipError_t sr_dispatch_interp(const SrEvalArgs<T>& a, int n_blocks, hipStream_t s);
+template <typename T, int R, int MODE, bool GATHER, int TIER>
+hipError_t sr_launch_tile(const SrEvalArgs<T>& a, int n_blocks, hipStream_t s);
+// LDS bytes one workgroup of the tile kernel needs.
+size_t sr_tile_lds_bytes(int elem_size, int nf, int rows_per_lane, int stack_depth, int trees_per_block,
+                         int max_checks);
+// Rows per lane the dispatcher uses for (mode, tier); `requested` 4 selects the f32 BASIC tuning kernel.
 template <typename T>
-size_t sr_interp_lds_bytes(int trees_per_block, int rows_per_lane, int max_checks);
-
-// Kernel variant (tuning): rows per lane and instruction prefetch.  variant 0 = default.
-struct SrVariant {
-  int rows_per_lane;  // 4 or 8 (f32); 2 (f64)
-  int var;            // bit 0: prefetch next program word
-};
+int sr_rows_per_lane(int mode, int tier, int requested);
+// Runtime dispatch over the instantiated kernels.
 template <typename T>
-hipError_t sr_launch_interp(const SrEvalArgs<T>& a, int mode, bool gather, int tier, SrVariant v, int n_blocks,
-                            hipStream_t s);
+hipError_t sr_launch_eval(const SrEvalArgs<T>& a, int mode, bool gather, int tier, int rows_per_lane, int n_blocks,
+                          hipStream_t s);
 hipError_t sr_launch_reduce(const double* part_sum, const uint32_t* part_flag, int n_trees, int n_row_blocks,
                             const uint8_t* static_bad, double* out_sum, uint32_t* out_flag, hipStream_t s);
 template <typename T>

@@ -1,7 +1,6 @@
-// Explicit kernel instantiations: float, prediction and exact-check modes (full operator tier).
-#include "sr_interp_impl.h"
-SR_INSTANTIATE(float, 4, SR_MODE_PRED, false, SR_TIER_FULL, 1)
-SR_INSTANTIATE(float, 4, SR_MODE_PRED, true, SR_TIER_FULL, 1)
-SR_INSTANTIATE(float, 4, SR_MODE_EXACT, false, SR_TIER_FULL, 1)
-SR_INSTANTIATE(float, 4, SR_MODE_EXACT, true, SR_TIER_FULL, 1)
-template size_t sr_interp_lds_bytes<float>(int, int, int);
+// f32 prediction and exact-check-sum kernels (FULL tier, 4 rows/lane).
+#include "sr_tile_impl.h"
+SR_INSTANTIATE(float, 4, SR_MODE_PRED, false, SR_TIER_FULL)
+SR_INSTANTIATE(float, 4, SR_MODE_PRED, true, SR_TIER_FULL)
+SR_INSTANTIATE(float, 4, SR_MODE_EXACT, false, SR_TIER_FULL)
+SR_INSTANTIATE(float, 4, SR_MODE_EXACT, true, SR_TIER_FULL)

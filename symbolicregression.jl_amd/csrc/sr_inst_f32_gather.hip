@@ -1,4 +1,4 @@
-// Explicit kernel instantiations: float, loss mode over a SubDataset row view (minibatching).
-#include "sr_interp_impl.h"
-SR_INSTANTIATE(float, 4, SR_MODE_LOSS, true, SR_TIER_BASIC, 1)
-SR_INSTANTIATE(float, 4, SR_MODE_LOSS, true, SR_TIER_FULL, 1)
+// f32 loss kernels over a row view (SubDataset / minibatch).
+#include "sr_tile_impl.h"
+SR_INSTANTIATE(float, 8, SR_MODE_LOSS, true, SR_TIER_BASIC)
+SR_INSTANTIATE(float, 4, SR_MODE_LOSS, true, SR_TIER_FULL)

@@ -1,4 +1,4 @@
-// Explicit kernel instantiations: double, loss mode over a SubDataset row view (minibatching).
-#include "sr_interp_impl.h"
-SR_INSTANTIATE(double, 2, SR_MODE_LOSS, true, SR_TIER_BASIC, 1)
-SR_INSTANTIATE(double, 2, SR_MODE_LOSS, true, SR_TIER_FULL, 1)
+// f64 loss kernels over a row view (SubDataset / minibatch).
+#include "sr_tile_impl.h"
+SR_INSTANTIATE(double, 4, SR_MODE_LOSS, true, SR_TIER_BASIC)
+SR_INSTANTIATE(double, 2, SR_MODE_LOSS, true, SR_TIER_FULL)

@@ -1,4 +1,4 @@
-// Explicit kernel instantiations: double, loss mode (hot path), both operator tiers.
-#include "sr_interp_impl.h"
-SR_INSTANTIATE(double, 2, SR_MODE_LOSS, false, SR_TIER_BASIC, 1)
-SR_INSTANTIATE(double, 2, SR_MODE_LOSS, false, SR_TIER_FULL, 1)
+// f64 loss kernels over the full dataset: BASIC tier at 4 rows/lane, FULL tier at 2.
+#include "sr_tile_impl.h"
+SR_INSTANTIATE(double, 4, SR_MODE_LOSS, false, SR_TIER_BASIC)
+SR_INSTANTIATE(double, 2, SR_MODE_LOSS, false, SR_TIER_FULL)

@@ -50,28 +50,47 @@ enum SrLossKind : int32_t {
 
 // ---------------------------------------------------------------------------------------
 // Program instruction (one per evaluated node; 16 bytes for f32 and f64).
-//   code bits 0-7 : combined opcode (what to do + where the operand comes from):
+//   code          : combined opcode (what to do + where the operand comes from), < 256:
 //       SR_OP_LOAD_FEAT / _CONST [/ _PUSH]           top-of-stack <- leaf (push old tos first)
 //       SR_OP_UNARY0 + u                               tos <- op_u(tos)
 //       SR_OP_BINARY0 + 6*(b-1) + variant              tos <- op_b(.,.) with operand variant:
 //           SR_V_SL: op(pop, tos)   SR_V_SR: op(tos, pop)
 //           SR_V_FL: op(X[f], tos)  SR_V_FR: op(tos, X[f])
 //           SR_V_CL: op(c, tos)     SR_V_CR: op(tos, c)
-//   code bit  8   : CHECK   this node's output array is validity-checked (DE early exit)
-//   code bit  9   : INFSUB  fused unary: non-finite input -> +Inf output (DE fused kernels)
-//   arg           : 0-based feature index (FEAT operands) / constant slot (gradient programs)
+//       SR_OP_SAVE                                     push a copy of tos (tos unchanged)
+//       SR_OP_FIXUP                                    o <- pop; tos <- isfinite(o) ? tos : +Inf
+//         (SAVE / unary / FIXUP = DynamicExpressions' fused unary kernels: a non-finite input of
+//          the fused inner operation gives +Inf)
+//   arg bits 0-28 : 0-based feature index (FEAT operands) / constant slot (gradient programs)
+//   arg bit  29   : OPSTK   the operand is popped from the stack (SL, SR, FIXUP)
+//   arg bit  30   : OPFEAT  the operand is a feature row (LOAD_FEAT[_PUSH], FL, FR)
+//   arg bit  31   : CHECK   this node's output array is validity-checked (DE early exit)
+//   (OPSTK / OPFEAT let the interpreter fetch an instruction's operand one step ahead)
 //   val           : constant (CONST operands)
+// The opcode has a word of its own so the interpreter's dispatch reads it without masking.
 // ---------------------------------------------------------------------------------------
 enum : uint32_t {
   SR_OP_LOAD_FEAT = 0u, SR_OP_LOAD_CONST = 1u, SR_OP_LOAD_FEAT_PUSH = 2u, SR_OP_LOAD_CONST_PUSH = 3u,
   SR_OP_UNARY0 = 3u,    // opcode = SR_OP_UNARY0 + SrUnaryOp (1..)
+  SR_OP_SAVE = 62u, SR_OP_FIXUP = 63u,
   SR_OP_BINARY0 = 64u,  // opcode = SR_OP_BINARY0 + 6*(SrBinaryOp-1) + variant
   SR_V_SL = 0u, SR_V_SR = 1u, SR_V_FL = 2u, SR_V_FR = 3u, SR_V_CL = 4u, SR_V_CR = 5u,
-  SR_F_CHECK = 1u << 8, SR_F_INFSUB = 1u << 9,
+  SR_A_CHECK = 1u << 31, SR_A_OPFEAT = 1u << 30, SR_A_OPSTK = 1u << 29, SR_A_INDEX = (1u << 29) - 1u,
 };
-static_assert(SR_OP_UNARY0 + SR_U_COUNT <= SR_OP_BINARY0, "unary opcode range overlaps binary range");
+static_assert(SR_OP_UNARY0 + SR_U_COUNT <= SR_OP_SAVE, "unary opcode range overlaps SAVE/FIXUP");
 static_assert(SR_OP_BINARY0 + 6 * SR_B_COUNT <= 256, "binary opcode range exceeds 8 bits");
-#define SR_OPC(c) ((c) & 0xffu)
+
+// Operand-source tag of an opcode (SR_A_OPFEAT / SR_A_OPSTK / 0).
+inline uint32_t sr_operand_tag(uint32_t op) {
+  if (op == SR_OP_LOAD_FEAT || op == SR_OP_LOAD_FEAT_PUSH) return SR_A_OPFEAT;
+  if (op == SR_OP_FIXUP) return SR_A_OPSTK;
+  if (op >= SR_OP_BINARY0) {
+    const uint32_t v = (op - SR_OP_BINARY0) % 6u;
+    if (v == SR_V_FL || v == SR_V_FR) return SR_A_OPFEAT;
+    if (v == SR_V_SL || v == SR_V_SR) return SR_A_OPSTK;
+  }
+  return 0u;
+}
 #define SR_BIN_OPC(b, v) (SR_OP_BINARY0 + 6u * ((b) - 1u) + (v))
 
 template <typename T>

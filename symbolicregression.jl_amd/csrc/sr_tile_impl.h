@@ -1,0 +1,482 @@
+// sr_tile_impl.h — CDNA4 (gfx950) batched expression-tree interpreter (kernel template).
+//
+// What it replaces: DynamicExpressions' array-at-a-time `eval_tree_array` + SymbolicRegression's
+// `_eval_loss` (reference src/LossFunctions.jl:90-117), for a whole population at once.
+//
+// Execution model:
+//   * a workgroup = 4 wave64s owns one row block (`tiles` row tiles of 64*R rows each) and a group
+//     of G trees; per tile, the X rows (all features), y and weights are staged ONCE in LDS and
+//     shared by the 4 waves, which take different trees of the group (tree g -> wave g % 4);
+//   * lane `l` owns R rows of the tile: chunk c (16 bytes = C values) of lane l is tile row
+//     c*64*C + l*C + j, so every LDS read of a feature / stack slot is a conflict-free ds_read_b128
+//     and the LDS image of a tile is a plain copy of the global rows;
+//   * each wave interprets its tree's program: the program sits in VGPRs (one 16-byte instruction
+//     per lane, 64-instruction windows) and each step reads its words with v_readlane; one flat
+//     `switch` over the opcode dispatches to straight-line VALU bodies on the R-row top of stack
+//     (VGPRs); deeper stack slots live in a per-wave LDS stack sized to the batch's depth;
+//   * DynamicExpressions' early-exit checks: a CHECK instruction tests max|v| >= tbig with one
+//     integer max per lane and one ballot; only then is non-finiteness tested (dead tree: the wave
+//     stops and the whole workgroup skips the tree in later tiles);
+//   * per-tree loss: T per lane -> cross-lane wave sum -> f64 accumulator in LDS (one wave per
+//     (tree, tile), tiles in order: deterministic) -> one partial per (tree, row block) -> fixed-
+//     order reduce kernel (bit-reproducible).
+// Compile with -mllvm -structurizecfg-skip-uniform-regions=true: all branches here are
+// wave-uniform, and without the flag LLVM's structurizer turns the opcode switch into a chain of
+// exec-mask "flow" blocks with copies of the stack registers at every join.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "sr_eval.h"
+#include "sr_ops.h"
+
+#define SR_WAVES 4
+#define SR_BLOCK (SR_WAVES * 64)
+#ifndef SR_MIN_WAVES
+#define SR_MIN_WAVES
+#endif
+
+// 16-byte chunks of C values.
+template <typename T>
+struct SrChunk;
+template <>
+struct SrChunk<float> {
+  using V = float4;
+  static constexpr int N = 4;
+  static __device__ inline void get(const V& v, float* o) { o[0] = v.x; o[1] = v.y; o[2] = v.z; o[3] = v.w; }
+  static __device__ inline V make(const float* o) { return make_float4(o[0], o[1], o[2], o[3]); }
+};
+template <>
+struct SrChunk<double> {
+  using V = double2;
+  static constexpr int N = 2;
+  static __device__ inline void get(const V& v, double* o) { o[0] = v.x; o[1] = v.y; }
+  static __device__ inline V make(const double* o) { return make_double2(o[0], o[1]); }
+};
+
+// A lane's R values of one tile-shaped array (X feature row, stack slot, y, w): chunk c of lane l at
+// element (c*64 + l)*C.  `p` points at element l*C of chunk 0.
+template <typename T, int R>
+struct SrLane {
+  using Ch = SrChunk<T>;
+  static constexpr int C = Ch::N;
+  static constexpr int NC = R / C;
+  static_assert(R % C == 0, "rows per lane must fill whole 16-byte chunks");
+  static __device__ inline void load(const T* p, T (&o)[R]) {
+#pragma unroll
+    for (int c = 0; c < NC; ++c) Ch::get(*reinterpret_cast<const typename Ch::V*>(p + c * 64 * C), o + c * C);
+  }
+  static __device__ inline void store(T* p, const T (&o)[R]) {
+#pragma unroll
+    for (int c = 0; c < NC; ++c) *reinterpret_cast<typename Ch::V*>(p + c * 64 * C) = Ch::make(o + c * C);
+  }
+  // tile row (0-based within the tile) of value r of lane l
+  static __device__ inline int row(int l, int r) { return (r / C) * 64 * C + l * C + (r % C); }
+};
+
+template <typename T>
+__device__ __forceinline__ T sr_wave_sum(T v) {
+#pragma unroll
+  for (int off = 32; off >= 1; off >>= 1) v += __shfl_xor(v, off, 64);
+  return v;
+}
+__device__ __forceinline__ uint64_t sr_ballot(bool p) { return __builtin_amdgcn_ballot_w64(p); }
+
+// Magnitude key for the validity checks: ordered like |v| for finite values, and above every finite
+// value for Inf / NaN.  f64 uses the high word only (conservative: a few values just below tbig
+// also count as suspicious, which only sends the tree through the exact-sum path).
+template <typename T>
+struct SrBits;
+template <>
+struct SrBits<float> {
+  static __device__ inline uint32_t mag(float x) { return __float_as_uint(x) & 0x7fffffffu; }
+};
+template <>
+struct SrBits<double> {
+  static __device__ inline uint32_t mag(double x) {
+    return uint32_t(uint64_t(__double_as_longlong(x)) >> 32) & 0x7fffffffu;
+  }
+};
+
+// ------------------------------------------------------------------ dispatch cases
+// Operators of the BASIC tier are compiled into every kernel; the FULL tier adds the rest of the
+// catalog (more registers: transcendental constants are hoisted out of the loop by LLVM).
+#define SR_EACH(EXPR)                             \
+  _Pragma("unroll") for (int r = 0; r < R; ++r) { \
+    const T x = tos[r];                           \
+    tos[r] = (EXPR);                              \
+  }
+#define SR_UCASE(ID)             \
+  case SR_OP_UNARY0 + ID: {      \
+    SR_EACH(sr_unary<T>(ID, x)); \
+    break;                       \
+  }
+#define SR_UCASE_FULL(ID)          \
+  case SR_OP_UNARY0 + ID: {        \
+    if (TIER == SR_TIER_FULL) {    \
+      SR_EACH(sr_unary<T>(ID, x)); \
+    }                              \
+    break;                         \
+  }
+#define SR_BIN_EACH(AEXPR, BEXPR, ID)             \
+  _Pragma("unroll") for (int r = 0; r < R; ++r) { \
+    const T aa = (AEXPR);                         \
+    const T bb = (BEXPR);                         \
+    tos[r] = sr_binary<T>(ID, aa, bb);            \
+  }
+#define SR_BCASE_GEN(ID, ENABLED)                 \
+  case SR_BIN_OPC(ID, SR_V_SL): {                 \
+    if (ENABLED) {                                \
+      --sp;                                       \
+      T o[R];                                     \
+      L::load(stk_lane + sp * ROWS, o);           \
+      SR_BIN_EACH(o[r], tos[r], ID);              \
+    }                                             \
+    break;                                        \
+  }                                               \
+  case SR_BIN_OPC(ID, SR_V_SR): {                 \
+    if (ENABLED) {                                \
+      --sp;                                       \
+      T o[R];                                     \
+      L::load(stk_lane + sp * ROWS, o);           \
+      SR_BIN_EACH(tos[r], o[r], ID);              \
+    }                                             \
+    break;                                        \
+  }                                               \
+  case SR_BIN_OPC(ID, SR_V_FL): {                 \
+    if (ENABLED) {                                \
+      T o[R];                                     \
+      L::load(x_lane + fidx * ROWS, o);           \
+      SR_BIN_EACH(o[r], tos[r], ID);              \
+    }                                             \
+    break;                                        \
+  }                                               \
+  case SR_BIN_OPC(ID, SR_V_FR): {                 \
+    if (ENABLED) {                                \
+      T o[R];                                     \
+      L::load(x_lane + fidx * ROWS, o);           \
+      SR_BIN_EACH(tos[r], o[r], ID);              \
+    }                                             \
+    break;                                        \
+  }                                               \
+  case SR_BIN_OPC(ID, SR_V_CL): {                 \
+    if (ENABLED) {                                \
+      const T cv = cval;                          \
+      SR_BIN_EACH(cv, tos[r], ID);                \
+    }                                             \
+    break;                                        \
+  }                                               \
+  case SR_BIN_OPC(ID, SR_V_CR): {                 \
+    if (ENABLED) {                                \
+      const T cv = cval;                          \
+      SR_BIN_EACH(tos[r], cv, ID);                \
+    }                                             \
+    break;                                        \
+  }
+#define SR_BCASE(ID) SR_BCASE_GEN(ID, true)
+#define SR_BCASE_FULL(ID) SR_BCASE_GEN(ID, TIER == SR_TIER_FULL)
+
+// LDS carve, in bytes, 16-aligned: X tile [nf][ROWS] T | y [ROWS] | w [ROWS] | stack
+// [SR_WAVES][depth][ROWS] T | acc [G] f64 | flg [G] u32 (padded to 4) | xacc [G][max_checks] f64
+template <typename T>
+struct SrLdsPlan {
+  size_t x, y, w, stk, acc, flg, xacc, total;
+  __host__ __device__ SrLdsPlan(int nf, int rows, int depth, int G, int max_checks) {
+    size_t o = 0;
+    x = o;
+    o += size_t(nf) * rows * sizeof(T);
+    y = o;
+    o += size_t(rows) * sizeof(T);
+    w = o;
+    o += size_t(rows) * sizeof(T);
+    stk = o;
+    o += size_t(SR_WAVES) * size_t(depth) * rows * sizeof(T);
+    acc = o;
+    o += size_t(G) * 8;
+    flg = o;
+    o += size_t((G + 3) & ~3) * 4;
+    xacc = o;
+    o += size_t(G) * size_t(max_checks) * 8;
+    total = o;
+  }
+};
+
+// ------------------------------------------------------------------ the interpreter kernel
+// MODE: SR_MODE_LOSS (partials), SR_MODE_PRED (write predictions), SR_MODE_EXACT (check sums).
+template <typename T, int R, int MODE, bool GATHER, int TIER>
+__global__ void __launch_bounds__(SR_BLOCK SR_MIN_WAVES) sr_tile_kernel(const SrEvalArgs<T> a) {
+  using L = SrLane<T, R>;
+  constexpr int C = L::C;
+  constexpr int ROWS = 64 * R;
+  extern __shared__ __attribute__((aligned(16))) unsigned char sr_smem[];
+  const int tid = threadIdx.x;
+  const int wave = tid >> 6;
+  const int lane = tid & 63;
+  const int G = a.trees_per_block;
+  const int MC = (MODE == SR_MODE_EXACT) ? a.max_checks : 0;
+  const SrLdsPlan<T> plan(a.nf, ROWS, a.stack_depth, G, MC);
+  T* xs = reinterpret_cast<T*>(sr_smem + plan.x);
+  T* ys = reinterpret_cast<T*>(sr_smem + plan.y);
+  T* wsv = reinterpret_cast<T*>(sr_smem + plan.w);
+  double* acc = reinterpret_cast<double*>(sr_smem + plan.acc);
+  uint32_t* flg = reinterpret_cast<uint32_t*>(sr_smem + plan.flg);
+  double* xacc = reinterpret_cast<double*>(sr_smem + plan.xacc);
+  const T* x_lane = xs + lane * C;
+  const T* y_lane = ys + lane * C;
+  const T* w_lane = wsv + lane * C;
+  T* stk_lane = reinterpret_cast<T*>(sr_smem + plan.stk) + size_t(wave) * a.stack_depth * ROWS + lane * C;
+
+  // tree group fastest: the blocks resident at one time share few row blocks (X stays in L2)
+  const int tg = blockIdx.x % a.n_groups;
+  const int rb = blockIdx.x / a.n_groups;
+  const int tree0 = tg * G;
+  int gcount = a.n_trees - tree0;
+  if (gcount > G) gcount = G;
+  const bool weighted = a.w != nullptr;
+  const uint32_t thr = SrBits<T>::mag(a.tbig);
+
+  for (int i = tid; i < G; i += SR_BLOCK) {
+    acc[i] = 0.0;
+    flg[i] = 0u;
+  }
+  for (int i = tid; i < G * MC; i += SR_BLOCK) xacc[i] = 0.0;
+
+  for (int tile = 0; tile < a.tiles_per_block; ++tile) {
+    const int64_t row0 = (int64_t(rb) * a.tiles_per_block + tile) * ROWS;
+    if (row0 >= a.n_rows) break;  // uniform over the block
+    __syncthreads();              // previous tile's readers are done with the LDS image
+    // ---- stage the tile: X rows of every feature, y, w (a plain copy; padded rows replicate
+    // row 0 of the view, so every program sees finite, in-range data there)
+    if (!GATHER) {
+      constexpr int CPR = ROWS / C;  // 16-byte chunks per feature row
+      using V = typename SrChunk<T>::V;
+      const int n_chunks = a.nf * CPR;
+      for (int i = tid; i < n_chunks; i += SR_BLOCK) {
+        const int f = i / CPR, q = i - f * CPR;
+        reinterpret_cast<V*>(xs)[i] = *reinterpret_cast<const V*>(a.X + int64_t(f) * a.ld + row0 + q * C);
+      }
+      if (MODE != SR_MODE_EXACT && a.y) {
+        for (int i = tid; i < CPR; i += SR_BLOCK) {
+          reinterpret_cast<V*>(ys)[i] = *reinterpret_cast<const V*>(a.y + row0 + i * C);
+          if (weighted) reinterpret_cast<V*>(wsv)[i] = *reinterpret_cast<const V*>(a.w + row0 + i * C);
+        }
+      }
+    } else {
+      for (int i = tid; i < ROWS; i += SR_BLOCK) {
+        const int64_t v = row0 + i;
+        const int64_t src = a.row_idx[v < a.n_rows ? v : 0];
+        for (int f = 0; f < a.nf; ++f) xs[f * ROWS + i] = a.X[int64_t(f) * a.ld + src];
+        if (MODE != SR_MODE_EXACT && a.y) {
+          ys[i] = a.y[src];
+          if (weighted) wsv[i] = a.w[src];
+        }
+      }
+    }
+    __syncthreads();
+
+    for (int g = wave; g < gcount; g += SR_WAVES) {
+      const int tree = (MODE == SR_MODE_EXACT) ? int(a.tree_list[tree0 + g]) : tree0 + g;
+      if (MODE == SR_MODE_LOSS && (__builtin_amdgcn_readfirstlane(flg[g]) & SR_FLAG_NONFINITE)) continue;
+      const uint32_t pb = a.offsets[tree];
+      const uint32_t pe = a.offsets[tree + 1];
+      if (pb == pe) continue;  // statically incomplete (constant checks)
+
+      T tos[R];
+#pragma unroll
+      for (int r = 0; r < R; ++r) tos[r] = T(0);
+      int sp = 0;
+      bool dead = false;
+      bool susp_any = false;
+      int check_k = 0;
+
+      // The program is staged in VGPRs, one 16-byte instruction per lane (64-instruction windows);
+      // each step reads its words with v_readlane: no scalar-memory round trip per step, and the
+      // LDS waits (lgkmcnt) never wait on an instruction fetch.
+      uint32_t wc = 0, wa = 0, wl = 0, wh = 0;
+      for (uint32_t base = pb; base < pe; base += 64u) {
+        if (base + lane < pe) {
+          const uint4 v = *reinterpret_cast<const uint4*>(a.code + base + lane);
+          wc = v.x;
+          wa = v.y;
+          wl = v.z;
+          wh = v.w;
+        }
+        const uint32_t n_here = __builtin_amdgcn_readfirstlane((pe - base < 64u) ? pe - base : 64u);
+        // single-exit inner loop (a dead tree sets k past the window): a second loop exit would make
+        // LLVM add an exit-selector block to every iteration
+        for (uint32_t k = 0; k < n_here; ++k) {
+          const uint32_t c = uint32_t(__builtin_amdgcn_readlane(wc, k));
+          const uint32_t arg = uint32_t(__builtin_amdgcn_readlane(wa, k));
+          const uint32_t fidx = arg & SR_A_INDEX;
+          T cval;
+          if constexpr (sizeof(T) == 4) {
+            cval = __builtin_bit_cast(T, __builtin_amdgcn_readlane(wl, k));
+          } else {
+            // readlane returns int: widen through uint32_t (no sign extension into the high word)
+            cval = __builtin_bit_cast(T, uint64_t(uint32_t(__builtin_amdgcn_readlane(wl, k))) |
+                                             (uint64_t(uint32_t(__builtin_amdgcn_readlane(wh, k))) << 32));
+          }
+          switch (c) {
+            case SR_OP_LOAD_FEAT: {
+              L::load(x_lane + fidx * ROWS, tos);
+              break;
+            }
+            case SR_OP_LOAD_CONST: {
+#pragma unroll
+              for (int r = 0; r < R; ++r) tos[r] = cval;
+              break;
+            }
+            case SR_OP_LOAD_FEAT_PUSH: {
+              L::store(stk_lane + sp * ROWS, tos);
+              ++sp;
+              L::load(x_lane + fidx * ROWS, tos);
+              break;
+            }
+            case SR_OP_LOAD_CONST_PUSH: {
+              L::store(stk_lane + sp * ROWS, tos);
+              ++sp;
+#pragma unroll
+              for (int r = 0; r < R; ++r) tos[r] = cval;
+              break;
+            }
+            case SR_OP_SAVE: {
+              L::store(stk_lane + sp * ROWS, tos);
+              ++sp;
+              break;
+            }
+            case SR_OP_FIXUP: {
+              --sp;
+              T o[R];
+              L::load(stk_lane + sp * ROWS, o);
+#pragma unroll
+              for (int r = 0; r < R; ++r) tos[r] = sr_isfinite(o[r]) ? tos[r] : sr_inf<T>();
+              break;
+            }
+            // BASIC tier
+            SR_UCASE(SR_U_NEG) SR_UCASE(SR_U_SQUARE) SR_UCASE(SR_U_CUBE) SR_UCASE(SR_U_EXP)
+            SR_UCASE(SR_U_COS) SR_UCASE(SR_U_SIN) SR_UCASE(SR_U_LOG) SR_UCASE(SR_U_SQRT)
+            SR_UCASE(SR_U_ABS)
+            SR_BCASE(SR_B_ADD) SR_BCASE(SR_B_SUB) SR_BCASE(SR_B_MUL) SR_BCASE(SR_B_DIV)
+            // FULL tier
+            SR_UCASE_FULL(SR_U_TAN) SR_UCASE_FULL(SR_U_LOG2) SR_UCASE_FULL(SR_U_LOG10)
+            SR_UCASE_FULL(SR_U_LOG1P) SR_UCASE_FULL(SR_U_SIGN) SR_UCASE_FULL(SR_U_TANH)
+            SR_UCASE_FULL(SR_U_SINH) SR_UCASE_FULL(SR_U_COSH) SR_UCASE_FULL(SR_U_ATAN)
+            SR_UCASE_FULL(SR_U_ASIN) SR_UCASE_FULL(SR_U_ACOS) SR_UCASE_FULL(SR_U_ACOSH)
+            SR_UCASE_FULL(SR_U_ATANH) SR_UCASE_FULL(SR_U_ASINH) SR_UCASE_FULL(SR_U_RELU)
+            SR_UCASE_FULL(SR_U_INV) SR_UCASE_FULL(SR_U_ERF) SR_UCASE_FULL(SR_U_ERFC)
+            SR_UCASE_FULL(SR_U_GAMMA) SR_UCASE_FULL(SR_U_ROUND) SR_UCASE_FULL(SR_U_FLOOR)
+            SR_UCASE_FULL(SR_U_CEIL) SR_UCASE_FULL(SR_U_EXP2) SR_UCASE_FULL(SR_U_EXPM1)
+            SR_BCASE_FULL(SR_B_POW) SR_BCASE_FULL(SR_B_MAX) SR_BCASE_FULL(SR_B_MIN)
+            SR_BCASE_FULL(SR_B_MOD) SR_BCASE_FULL(SR_B_GREATER) SR_BCASE_FULL(SR_B_LESS)
+            SR_BCASE_FULL(SR_B_GREATER_EQUAL) SR_BCASE_FULL(SR_B_LESS_EQUAL) SR_BCASE_FULL(SR_B_COND)
+            SR_BCASE_FULL(SR_B_LOGICAL_OR) SR_BCASE_FULL(SR_B_LOGICAL_AND) SR_BCASE_FULL(SR_B_ATAN2)
+            default:
+              break;
+          }
+          if (arg & SR_A_CHECK) {
+            if (MODE == SR_MODE_EXACT) {
+              double s = 0.0;
+#pragma unroll
+              for (int r = 0; r < R; ++r)
+                s += (row0 + L::row(lane, r) < a.n_rows) ? double(tos[r]) * a.scale : 0.0;
+              s = sr_wave_sum<double>(s);
+              if (lane == 0) xacc[g * MC + check_k] += s;
+              ++check_k;
+            } else {
+              // |v| >= tbig (or NaN / Inf) in any row: one integer max per lane + one ballot;
+              // padded rows replicate row 0 of the view, so no row mask is needed here
+              uint32_t m = SrBits<T>::mag(tos[0]);
+#pragma unroll
+              for (int r = 1; r < R; ++r) m = max(m, SrBits<T>::mag(tos[r]));
+              if (sr_ballot(m >= thr)) {
+                susp_any = true;
+                bool nonfin = false;
+#pragma unroll
+                for (int r = 0; r < R; ++r) nonfin |= !sr_isfinite(tos[r]);
+                if (sr_ballot(nonfin)) {
+                  dead = true;
+                  k = 64u;
+                }
+              }
+            }
+          }
+        }
+        if (dead) break;
+      }
+
+      if (MODE == SR_MODE_LOSS) {
+        if (dead) {
+          if (lane == 0) flg[g] |= SR_FLAG_NONFINITE;
+          continue;
+        }
+        T yv[R];
+        L::load(y_lane, yv);
+        T s = T(0);
+        if (weighted) {
+          T wv[R];
+          L::load(w_lane, wv);
+#pragma unroll
+          for (int r = 0; r < R; ++r) {
+            const T l = sr_elem_loss<T>(a.loss_kind, tos[r], yv[r]) * wv[r];
+            s += (row0 + L::row(lane, r) < a.n_rows) ? l : T(0);
+          }
+        } else {
+#pragma unroll
+          for (int r = 0; r < R; ++r) {
+            const T l = sr_elem_loss<T>(a.loss_kind, tos[r], yv[r]);
+            s += (row0 + L::row(lane, r) < a.n_rows) ? l : T(0);
+          }
+        }
+        s = sr_wave_sum<T>(s);
+        if (lane == 0) {
+          acc[g] += double(s);
+          if (susp_any) flg[g] |= SR_FLAG_BIG;
+        }
+      } else if (MODE == SR_MODE_PRED) {
+        T* out = a.pred + int64_t(tree) * a.pred_ld + row0;
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+          const int i = L::row(lane, r);
+          if (row0 + i < a.n_rows) out[i] = dead ? sr_qnan<T>() : tos[r];
+        }
+        if (lane == 0) {
+          if (dead) flg[g] |= SR_FLAG_NONFINITE;
+          else if (susp_any) flg[g] |= SR_FLAG_BIG;
+        }
+      }
+    }
+  }
+
+  __syncthreads();
+  if (MODE == SR_MODE_EXACT) {
+    // one device-scope add per (block, tree, check)
+    for (int i = tid; i < gcount * MC; i += SR_BLOCK) {
+      const double v = xacc[i];
+      if (v != 0.0) atomicAdd(a.check_sums + size_t(tree0) * MC + i, v);
+    }
+    return;
+  }
+  for (int g = tid; g < gcount; g += SR_BLOCK) {
+    const size_t o = size_t(tree0 + g) * a.n_row_blocks + rb;
+    a.part_sum[o] = acc[g];
+    a.part_flag[o] = flg[g];
+  }
+}
+
+// ------------------------------------------------------------------ launch helpers
+template <typename T, int R, int MODE, bool GATHER, int TIER>
+hipError_t sr_launch_tile(const SrEvalArgs<T>& a, int n_blocks, hipStream_t s) {
+  const SrLdsPlan<T> plan(a.nf, 64 * R, a.stack_depth, a.trees_per_block,
+                          MODE == SR_MODE_EXACT ? a.max_checks : 0);
+  if (plan.total > 65536) {  // many features / a deep stack: opt in to the full 160 KiB of LDS
+    const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&sr_tile_kernel<T, R, MODE, GATHER, TIER>),
+                                             hipFuncAttributeMaxDynamicSharedMemorySize, int(plan.total));
+    if (e != hipSuccess) return e;
+  }
+  hipLaunchKernelGGL((sr_tile_kernel<T, R, MODE, GATHER, TIER>), dim3(n_blocks), dim3(SR_BLOCK), plan.total, s, a);
+  return hipGetLastError();
+}
+
+// Explicit instantiations are spread over several translation units (sr_inst_*.hip, one per
+// element type / mode) so the build compiles them in parallel; see the Makefile.
+#define SR_INSTANTIATE(T, R, MODE, GATHER, TIER) \
+  template hipError_t sr_launch_tile<T, R, MODE, GATHER, TIER>(const SrEvalArgs<T>&, int, hipStream_t);

@@ -1,7 +1,7 @@
 """TEST HELPER: a numpy interpreter of libsr_amd's compiled programs (csrc/sr_ops.h encoding).
 
 It executes exactly the instruction semantics of the HIP kernel (top-of-stack + operand stack,
-combined opcodes, CHECK / INFSUB bits) on the CPU, so CPU tests can validate the tree COMPILER
+combined opcodes, SAVE / FIXUP, the CHECK bit of arg) on the CPU, so CPU tests can validate the tree COMPILER
 (constant folding, check placement, fused-unary detection, Sethi–Ullman ordering) against the
 oracle without a GPU.  It is not part of the product and is never used as a fallback.
 """
@@ -82,16 +82,20 @@ def run_program(code, lo, hi, X, T):
     complete = True
     big = T(np.finfo(T).max)
     for pc in range(lo, hi):
-        c = int(code["code"][pc])
+        opc = int(code["code"][pc])
         arg = int(code["arg"][pc])
+        fidx = arg & ((1 << 29) - 1)  # bits 29/30: operand-source tags
         val = T(code["val"][pc])
-        opc = c & 0xFF
-        save = tos
         if opc <= 3:
             if opc >= 2:
                 stack.append(tos)
-            tos = X[arg].astype(T) if opc in (0, 2) else np.full(n, val, dtype=T)
-        elif opc < 64:
+            tos = X[fidx].astype(T) if opc in (0, 2) else np.full(n, val, dtype=T)
+        elif opc == 62:  # SAVE: push a copy of tos
+            stack.append(tos.copy())
+        elif opc == 63:  # FIXUP: non-finite saved operand -> +Inf
+            o = stack.pop()
+            tos = np.where(np.isfinite(o), tos, T(np.inf)).astype(T)
+        elif opc < 62:
             tos = _unary(opc - 3, tos, T).astype(T)
         else:
             bid, v = divmod(opc - 64, 6)
@@ -99,14 +103,12 @@ def run_program(code, lo, hi, X, T):
             if v in (0, 1):
                 o = stack.pop()
             elif v in (2, 3):
-                o = X[arg].astype(T)
+                o = X[fidx].astype(T)
             else:
                 o = np.full(n, val, dtype=T)
             a, b = (o, tos) if v in (0, 2, 4) else (tos, o)
             tos = _binary(bid, a, b).astype(T)
-        if c & (1 << 9):  # INFSUB
-            tos = np.where(np.isfinite(save), tos, T(np.inf)).astype(T)
-        if c & (1 << 8):  # CHECK: isfinite(sum(array)) (f64 sum)
+        if arg & (1 << 31):  # CHECK: isfinite(sum(array)) (f64 sum)
             s = np.sum(tos.astype(np.float64))
             if not np.isfinite(tos).all() or not abs(s) <= float(big):
                 complete = False

@@ -13,7 +13,7 @@ from oracle import Oracle
 from sr_amd import (Dataset, Node, Options, batch, eval_loss, eval_loss_batch, eval_tree_array, eval_tree_array_batch,
                     flatten_trees, gen_random_population, parse_expression)
 from sr_amd import _lib
-from parity_util import well_conditioned
+from parity_util import PERTURB_SEEDS, well_conditioned
 
 pytestmark = pytest.mark.gpu
 
@@ -184,10 +184,11 @@ def test_predictions_vs_oracle():
         if c:
             # rows whose value moves under +-1-ulp libm perturbations are rounding-dominated
             # (cancellation, or a floor/sign/comparison sitting on its threshold): excluded
-            p1, _ = orc.eval_tree_array(tb, k, X, perturb=1)
-            p2, _ = orc.eval_tree_array(tb, k, X, perturb=2)
             scale = np.maximum(np.abs(o.astype(np.float64)), 1e-3)
-            okrow = (np.abs(p1 - o) <= 2e-5 * scale) & (np.abs(p2 - o) <= 2e-5 * scale)
+            okrow = np.ones(o.shape, dtype=bool)
+            for seed in PERTURB_SEEDS:
+                p, _ = orc.eval_tree_array(tb, k, X, perturb=seed)
+                okrow &= np.abs(p - o) <= 2e-5 * scale
             compared += int(okrow.sum())
             total += okrow.size
             np.testing.assert_allclose(out[k][okrow], o[okrow], rtol=1e-4, atol=1e-6)

@@ -20,7 +20,10 @@ mixes = {
     "exp-only": dict(binary_operators=["+", "*"], unary_operators=["exp"]),
     "sin-only": dict(binary_operators=["+", "*"], unary_operators=["sin"]),
 }
+only = sys.argv[1:]  # optional: mix names to run (profiling one population at a time)
 for name, kw in mixes.items():
+    if only and not any(name.startswith(o) for o in only):
+        continue
     opts = Options(**kw)
     tb = flatten_trees(gen_random_population(10000, opts, 5, seed=1), np.float32)
     eval_loss_batch(tb, ds, opts)
