@@ -12,18 +12,21 @@ __device__ __forceinline__ T sr_wave_sum_aux(T v) {
   return v;
 }
 
-// One wave per tree: Σ over row blocks in a fixed lane/stride order (bit-reproducible), OR of flags.
+// One wave per launch position: Σ over row blocks in a fixed lane/stride order (bit-reproducible),
+// OR of flags; the result goes to the caller's tree index perm[position].
 __global__ void __launch_bounds__(256) sr_reduce_partials_kernel(const double* __restrict__ part_sum,
                                                                   const uint32_t* __restrict__ part_flag,
                                                                   int n_trees, int n_row_blocks,
+                                                                  const uint32_t* __restrict__ perm,
                                                                   const uint8_t* __restrict__ static_bad,
                                                                   double* __restrict__ out_sum,
                                                                   uint32_t* __restrict__ out_flag) {
-  const int tree = int((int64_t(blockIdx.x) * blockDim.x + threadIdx.x) >> 6);
+  const int pos = int((int64_t(blockIdx.x) * blockDim.x + threadIdx.x) >> 6);
   const int lane = threadIdx.x & 63;
-  if (tree >= n_trees) return;
-  const double* ps = part_sum + size_t(tree) * n_row_blocks;
-  const uint32_t* pf = part_flag + size_t(tree) * n_row_blocks;
+  if (pos >= n_trees) return;
+  const int tree = perm ? int(perm[pos]) : pos;
+  const double* ps = part_sum + size_t(pos) * n_row_blocks;
+  const uint32_t* pf = part_flag + size_t(pos) * n_row_blocks;
   double s = 0.0;
   uint32_t f = 0u;
   for (int i = lane; i < n_row_blocks; i += 64) {
@@ -59,11 +62,12 @@ __global__ void sr_pad_kernel(T* __restrict__ v, int64_t n, int64_t ld, T pad_va
 }
 
 hipError_t sr_launch_reduce(const double* part_sum, const uint32_t* part_flag, int n_trees, int n_row_blocks,
-                            const uint8_t* static_bad, double* out_sum, uint32_t* out_flag, hipStream_t s) {
+                            const uint32_t* perm, const uint8_t* static_bad, double* out_sum, uint32_t* out_flag,
+                            hipStream_t s) {
   if (n_trees <= 0) return hipSuccess;
   const int64_t blocks = (int64_t(n_trees) * 64 + 255) / 256;
   hipLaunchKernelGGL(sr_reduce_partials_kernel, dim3(unsigned(blocks)), dim3(256), 0, s, part_sum, part_flag,
-                     n_trees, n_row_blocks, static_bad, out_sum, out_flag);
+                     n_trees, n_row_blocks, perm, static_bad, out_sum, out_flag);
   return hipGetLastError();
 }
 
@@ -100,7 +104,6 @@ size_t sr_tile_lds_bytes(int elem_size, int nf, int rows_per_lane, int stack_dep
                          int max_checks) {
   const size_t rows = size_t(64) * rows_per_lane;
   return size_t(nf) * rows * elem_size + 2 * rows * elem_size + size_t(4) * stack_depth * rows * elem_size +
-         size_t(trees_per_block) * 8 + size_t((trees_per_block + 3) & ~3) * 4 +
          size_t(trees_per_block) * size_t(max_checks) * 8;
 }
 

@@ -7,6 +7,7 @@
 // Mirrors reference src/LossFunctions.jl:90-117 (`_eval_loss`) for each tree of the batch.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <chrono>
 #include <cmath>
 #include <cstdio>
@@ -73,11 +74,14 @@ struct sr_ctx {
   std::vector<SrOpset> opsets;
   std::vector<int> tiers;
   DevBuf code, offsets, static_bad, part_sum, part_flag, out_sum, out_flag, pred, row_idx, tree_list,
-      check_sums;
+      check_sums, perm, hint;
   double last_eval_ms = 0.0, last_total_ms = 0.0;
   int cu_count = 256;
   int rows_override = 0;    // SR_AMD_ROWS_PER_LANE (tuning): 4 selects the f32 BASIC 4-rows/lane kernel
   int tree_group = 0;       // SR_AMD_TREES_PER_BLOCK override (0 = heuristic)
+  bool cost_order = true;   // launch trees in decreasing estimated cost (SR_AMD_NO_SORT=1 disables)
+  bool dead_hints = true;   // share dead-tree hints across row blocks (SR_AMD_NO_HINT=1 disables)
+  std::vector<uint32_t> perm_host;
 };
 
 struct sr_dataset {
@@ -191,6 +195,25 @@ int run_batch(sr_ctx* ctx, const sr_dataset* ds, int opset_id, const sr_tree_bat
                               hipMemcpyHostToDevice, s));
   SR_HIP_CHECK(hipMemcpyAsync(ctx->static_bad.p, prog->static_bad.data(), prog->static_bad.size(),
                               hipMemcpyHostToDevice, s));
+  // launch order: decreasing estimated cost, so every block's waves get similar work
+  const uint32_t* perm_dev = nullptr;
+  if (ctx->cost_order && nt > 1) {
+    ctx->perm_host.resize(size_t(nt));
+    for (int64_t t = 0; t < nt; ++t) ctx->perm_host[size_t(t)] = uint32_t(t);
+    const std::vector<uint32_t>& cost = prog->cost;
+    std::stable_sort(ctx->perm_host.begin(), ctx->perm_host.end(),
+                     [&](uint32_t x, uint32_t y) { return cost[x] > cost[y]; });
+    SR_HIP_CHECK(ctx->perm.ensure(size_t(nt) * sizeof(uint32_t)));
+    SR_HIP_CHECK(hipMemcpyAsync(ctx->perm.p, ctx->perm_host.data(), size_t(nt) * sizeof(uint32_t),
+                                hipMemcpyHostToDevice, s));
+    perm_dev = ctx->perm.as<uint32_t>();
+  }
+  uint32_t* hint_dev = nullptr;
+  if (ctx->dead_hints && mode == SR_MODE_LOSS && g.n_row_blocks > 1) {
+    SR_HIP_CHECK(ctx->hint.ensure(size_t(nt) * sizeof(uint32_t)));
+    SR_HIP_CHECK(hipMemsetAsync(ctx->hint.p, 0, size_t(nt) * sizeof(uint32_t), s));
+    hint_dev = ctx->hint.as<uint32_t>();
+  }
   if (gather) {
     for (int64_t i = 0; i < n_idx; ++i)
       if (row_idx[i] < 0 || row_idx[i] >= ds->n)
@@ -208,6 +231,8 @@ int run_batch(sr_ctx* ctx, const sr_dataset* ds, int opset_id, const sr_tree_bat
   SrEvalArgs<T> a{};
   a.code = ctx->code.as<SrIns<T>>();
   a.offsets = ctx->offsets.as<uint32_t>();
+  a.perm = perm_dev;
+  a.hint = hint_dev;
   a.n_trees = int(nt);
   a.trees_per_block = g.G;
   a.X = static_cast<const T*>(ds->X);
@@ -233,8 +258,9 @@ int run_batch(sr_ctx* ctx, const sr_dataset* ds, int opset_id, const sr_tree_bat
   SR_HIP_CHECK(hipEventRecord(ctx->ev_k0, s));
   SR_HIP_CHECK(sr_launch_eval<T>(a, mode, gather, tier, ctx->rows_override, int(g.n_blocks), s));
   SR_HIP_CHECK(hipEventRecord(ctx->ev_k1, s));
-  SR_HIP_CHECK(sr_launch_reduce(a.part_sum, a.part_flag, int(nt), g.n_row_blocks, ctx->static_bad.as<uint8_t>(),
-                                ctx->out_sum.as<double>(), ctx->out_flag.as<uint32_t>(), s));
+  SR_HIP_CHECK(sr_launch_reduce(a.part_sum, a.part_flag, int(nt), g.n_row_blocks, perm_dev,
+                                ctx->static_bad.as<uint8_t>(), ctx->out_sum.as<double>(),
+                                ctx->out_flag.as<uint32_t>(), s));
   return SR_OK;
 }
 
@@ -251,9 +277,12 @@ int run_exact(sr_ctx* ctx, const sr_dataset* ds, const SrProgramBatch<T>& prog, 
   Grid g = make_grid<T>(n_eval, 1, sr_rows_per_lane<T>(SR_MODE_EXACT, SR_TIER_FULL, 0), int(ds->nf), depth,
                         max_checks, 1);
   if (g.lds > kLdsMax) return set_error(SR_ERR_TOO_DEEP, "exact-sum pass needs more LDS than 160 KiB");
-  SR_HIP_CHECK(ctx->tree_list.ensure(size_t(n_list) * sizeof(int64_t)));
+  std::vector<uint32_t> list32(static_cast<size_t>(n_list));
+  for (int64_t i = 0; i < n_list; ++i) list32[size_t(i)] = uint32_t(list[i]);
+  SR_HIP_CHECK(ctx->tree_list.ensure(size_t(n_list) * sizeof(uint32_t)));
   SR_HIP_CHECK(ctx->check_sums.ensure(size_t(n_list) * max_checks * sizeof(double)));
-  SR_HIP_CHECK(hipMemcpyAsync(ctx->tree_list.p, list, size_t(n_list) * sizeof(int64_t), hipMemcpyHostToDevice, s));
+  SR_HIP_CHECK(hipMemcpyAsync(ctx->tree_list.p, list32.data(), size_t(n_list) * sizeof(uint32_t),
+                              hipMemcpyHostToDevice, s));
   SR_HIP_CHECK(hipMemsetAsync(ctx->check_sums.p, 0, size_t(n_list) * max_checks * sizeof(double), s));
   SR_HIP_CHECK(ctx->part_sum.ensure(size_t(g.n_row_blocks) * sizeof(double) * size_t(n_list)));
   SR_HIP_CHECK(ctx->part_flag.ensure(size_t(g.n_row_blocks) * sizeof(uint32_t) * size_t(n_list)));
@@ -276,7 +305,7 @@ int run_exact(sr_ctx* ctx, const sr_dataset* ds, const SrProgramBatch<T>& prog, 
   a.tbig = T(0);
   a.part_sum = ctx->part_sum.as<double>();
   a.part_flag = ctx->part_flag.as<uint32_t>();
-  a.tree_list = ctx->tree_list.as<int64_t>();
+  a.perm = ctx->tree_list.as<uint32_t>();
   a.max_checks = max_checks;
   a.check_sums = ctx->check_sums.as<double>();
   // f64 sums can overflow f64 itself: scale by 2^-64 (the threshold is scaled identically)
@@ -514,6 +543,8 @@ int sr_init(int device, sr_ctx** out) {
   if (hipGetDeviceProperties(&prop, device) == hipSuccess) ctx->cu_count = prop.multiProcessorCount;
   if (const char* v = std::getenv("SR_AMD_ROWS_PER_LANE")) ctx->rows_override = std::atoi(v);
   if (const char* v = std::getenv("SR_AMD_TREES_PER_BLOCK")) ctx->tree_group = std::atoi(v);
+  if (const char* v = std::getenv("SR_AMD_NO_SORT")) ctx->cost_order = std::atoi(v) == 0;
+  if (const char* v = std::getenv("SR_AMD_NO_HINT")) ctx->dead_hints = std::atoi(v) == 0;
   hipError_t e = hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking);
   if (e == hipSuccess) e = hipEventCreate(&ctx->ev_start);
   if (e == hipSuccess) e = hipEventCreate(&ctx->ev_k0);
@@ -534,7 +565,8 @@ int sr_shutdown(sr_ctx* ctx) {
     (void)hipSetDevice(ctx->device);
     (void)hipStreamSynchronize(ctx->stream);
     for (DevBuf* b : {&ctx->code, &ctx->offsets, &ctx->static_bad, &ctx->part_sum, &ctx->part_flag, &ctx->out_sum,
-                      &ctx->out_flag, &ctx->pred, &ctx->row_idx, &ctx->tree_list, &ctx->check_sums})
+                      &ctx->out_flag, &ctx->pred, &ctx->row_idx, &ctx->tree_list, &ctx->check_sums,
+                      &ctx->perm, &ctx->hint})
       b->release();
     (void)hipEventDestroy(ctx->ev_start);
     (void)hipEventDestroy(ctx->ev_k0);

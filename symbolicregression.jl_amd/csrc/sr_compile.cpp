@@ -317,19 +317,9 @@ struct TreeCompiler {
     if (d == 1) {
       emit(t.l[i]);
       SrIns<T> in{};
-      if (infsub[i]) {  // fused unary: remember the operand on the stack, fix the output up after
-        SrIns<T> sv{};
-        sv.code = SR_OP_SAVE;
-        code.push_back(sv);
-        if (depth + 1 > max_depth) max_depth = depth + 1;
-      }
       in.code = SR_OP_UNARY0 + unary_id(i);
+      if (infsub[i]) in.arg = SR_A_INFSUB;  // fused unary: non-finite input -> +Inf
       code.push_back(in);
-      if (infsub[i]) {
-        SrIns<T> fx{};
-        fx.code = SR_OP_FIXUP;
-        code.push_back(fx);
-      }
       emit_check(i);
       return;
     }
@@ -409,6 +399,31 @@ struct TreeCompiler {
 
 }  // namespace
 
+uint32_t sr_instruction_cost(uint32_t code, uint32_t arg) {
+  uint32_t c = 6;  // dispatch + operand fetch
+  if (arg & SR_A_CHECK) c += 3;
+  if (arg & SR_A_INFSUB) c += 2;
+  if (code >= SR_OP_BINARY0) {
+    const uint32_t b = (code - SR_OP_BINARY0) / 6u + 1u;
+    if (b == SR_B_DIV) c += 10;
+    else if (b == SR_B_ADD || b == SR_B_SUB || b == SR_B_MUL) c += 1;
+    else c += 20;
+  } else if (code > SR_OP_UNARY0) {
+    const uint32_t u = code - SR_OP_UNARY0;
+    switch (u) {
+      case SR_U_NEG: case SR_U_SQUARE: case SR_U_CUBE: case SR_U_ABS: c += 2; break;
+      case SR_U_EXP: c += 14; break;
+      case SR_U_LOG: c += 16; break;
+      case SR_U_SQRT: c += 8; break;
+      case SR_U_COS: case SR_U_SIN: c += 32; break;
+      default: c += 30; break;
+    }
+  } else {
+    c += 1;
+  }
+  return c;
+}
+
 uint32_t sr_unary_id(const char* name) {
   for (const auto& e : kUnary)
     if (std::strcmp(e.name, name) == 0) return e.id;
@@ -432,7 +447,7 @@ int sr_compile_batch(const sr_tree_batch& trees, const SrOpset& ops, int64_t n_r
   struct PerTree {
     std::vector<SrIns<T>> code;
     uint8_t bad;
-    uint32_t checks, consts;
+    uint32_t checks, consts, cost;
     int depth;
     int64_t nodes, ops;
   };
@@ -460,8 +475,13 @@ int sr_compile_batch(const sr_tree_batch& trees, const SrOpset& ops, int64_t n_r
         errs[k] = tc.err;
         continue;
       }
-      for (auto& in : tc.code) in.arg |= sr_operand_tag(in.code);
+      uint32_t cost = 0;
+      for (auto& in : tc.code) {
+        in.arg |= sr_operand_tag(in.code);
+        cost += sr_instruction_cost(in.code, in.arg);
+      }
       PerTree& p = per[k];
+      p.cost = cost;
       p.code.swap(tc.code);
       p.bad = (tc.bad || p.code.empty()) ? 1 : 0;
       p.checks = tc.n_checks;
@@ -500,6 +520,7 @@ int sr_compile_batch(const sr_tree_batch& trees, const SrOpset& ops, int64_t n_r
   out->n_checks.assign(size_t(nt), 0);
   out->n_consts.assign(size_t(nt), 0);
   out->const_off.assign(size_t(nt + 1), 0);
+  out->cost.assign(size_t(nt), 0);
   out->max_depth = 0;
   out->max_checks = 0;
   out->total_nodes = 0;
@@ -512,6 +533,7 @@ int sr_compile_batch(const sr_tree_batch& trees, const SrOpset& ops, int64_t n_r
     out->offsets[k] = uint32_t(out->code.size());
     out->code.insert(out->code.end(), p.code.begin(), p.code.end());
     out->static_bad[k] = p.bad;
+    out->cost[k] = p.bad ? 0u : p.cost;
     out->n_checks[k] = p.checks;
     out->n_consts[k] = p.consts;
     out->const_off[k + 1] = out->const_off[k] + p.consts;

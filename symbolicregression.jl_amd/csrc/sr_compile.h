@@ -36,6 +36,7 @@ struct SrProgramBatch {
   std::vector<uint32_t> n_checks;   // CHECK instructions per tree
   std::vector<uint32_t> n_consts;   // constants per tree (pre-order, for gradients)
   std::vector<uint32_t> const_off;  // [n_trees + 1] prefix sum of n_consts
+  std::vector<uint32_t> cost;       // estimated device cost per tree (launch ordering / balancing)
   int max_depth = 0;                // operand-stack slots needed (below top-of-stack)
   int max_checks = 0;
   int64_t total_nodes = 0;          // Σ count_nodes (metric unit)
@@ -45,6 +46,10 @@ struct SrProgramBatch {
 // Compile a batch.  n_rows: rows the programs will be evaluated on (static overflow checks of
 // constant arrays).  nfeatures: columns of X.  with_const_index: emit constant-slot indices in
 // `arg` of CONST loads (gradient kernels).  Returns SR_OK or an error code with *err set.
+// Estimated cost of one program instruction on the device, in VALU-instruction-like units per row
+// step (dispatch overhead included): used only to order trees for load balance.
+uint32_t sr_instruction_cost(uint32_t code, uint32_t arg);
+
 template <typename T>
 int sr_compile_batch(const sr_tree_batch& trees, const SrOpset& ops, int64_t n_rows, int64_t nfeatures,
                      bool with_const_index, SrProgramBatch<T>* out, std::string* err);

@@ -12,7 +12,9 @@ template <typename T>
 struct SrEvalArgs {
   // programs
   const SrIns<T>* code;
-  const uint32_t* offsets;     // [n_trees + 1]
+  const uint32_t* offsets;     // [n_trees + 1], indexed by the caller's tree index
+  const uint32_t* perm;        // launch position -> caller's tree index (NULL: identity); EXACT: tree list
+  uint32_t* hint;              // [n_trees] per position: dead-tree hints across row blocks (LOSS; may be NULL)
   int n_trees;                 // trees (or listed trees in EXACT mode)
   int trees_per_block;         // G
   // data (per-feature rows, leading dimension ld; padded rows replicate row 0)
@@ -30,12 +32,11 @@ struct SrEvalArgs {
   T tbig;                      // |v| >= tbig may overflow the array-sum check
   int loss_kind;
   // outputs
-  double* part_sum;            // [n_trees][n_row_blocks]
-  uint32_t* part_flag;         // [n_trees][n_row_blocks]
+  double* part_sum;            // [n_trees][n_row_blocks], per launch position
+  uint32_t* part_flag;         // [n_trees][n_row_blocks], per launch position
   T* pred;                     // PRED: [n_trees][pred_ld]
   int64_t pred_ld;
-  // EXACT mode
-  const int64_t* tree_list;    // listed trees; check_sums row = position in the list
+  // EXACT mode (perm = listed trees; check_sums row = position in the list)
   int max_checks;
   double* check_sums;          // [n_list][max_checks]
   double scale;
@@ -54,7 +55,8 @@ template <typename T>
 hipError_t sr_launch_eval(const SrEvalArgs<T>& a, int mode, bool gather, int tier, int rows_per_lane, int n_blocks,
                           hipStream_t s);
 hipError_t sr_launch_reduce(const double* part_sum, const uint32_t* part_flag, int n_trees, int n_row_blocks,
-                            const uint8_t* static_bad, double* out_sum, uint32_t* out_flag, hipStream_t s);
+                            const uint32_t* perm, const uint8_t* static_bad, double* out_sum, uint32_t* out_flag,
+                            hipStream_t s);
 template <typename T>
 hipError_t sr_launch_transpose(const T* Xh_dev, int64_t nf, int64_t n, int64_t ld, T* Xd, hipStream_t s);
 template <typename T>

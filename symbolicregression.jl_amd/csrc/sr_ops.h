@@ -57,33 +57,30 @@ enum SrLossKind : int32_t {
 //           SR_V_SL: op(pop, tos)   SR_V_SR: op(tos, pop)
 //           SR_V_FL: op(X[f], tos)  SR_V_FR: op(tos, X[f])
 //           SR_V_CL: op(c, tos)     SR_V_CR: op(tos, c)
-//       SR_OP_SAVE                                     push a copy of tos (tos unchanged)
-//       SR_OP_FIXUP                                    o <- pop; tos <- isfinite(o) ? tos : +Inf
-//         (SAVE / unary / FIXUP = DynamicExpressions' fused unary kernels: a non-finite input of
-//          the fused inner operation gives +Inf)
-//   arg bits 0-28 : 0-based feature index (FEAT operands) / constant slot (gradient programs)
-//   arg bit  29   : OPSTK   the operand is popped from the stack (SL, SR, FIXUP)
+//   arg bits 0-27 : 0-based feature index (FEAT operands) / constant slot (gradient programs)
+//   arg bit  28   : INFSUB  (unary) tos <- isfinite(tos) ? op_u(tos) : +Inf — DynamicExpressions'
+//                   fused unary kernels (deg1_l2_ll0_lr0 / deg1_l1_ll0): a non-finite input of the
+//                   fused inner operation gives +Inf
+//   arg bit  29   : OPSTK   the operand is popped from the stack (SL, SR)
 //   arg bit  30   : OPFEAT  the operand is a feature row (LOAD_FEAT[_PUSH], FL, FR)
 //   arg bit  31   : CHECK   this node's output array is validity-checked (DE early exit)
-//   (OPSTK / OPFEAT let the interpreter fetch an instruction's operand one step ahead)
 //   val           : constant (CONST operands)
 // The opcode has a word of its own so the interpreter's dispatch reads it without masking.
 // ---------------------------------------------------------------------------------------
 enum : uint32_t {
   SR_OP_LOAD_FEAT = 0u, SR_OP_LOAD_CONST = 1u, SR_OP_LOAD_FEAT_PUSH = 2u, SR_OP_LOAD_CONST_PUSH = 3u,
   SR_OP_UNARY0 = 3u,    // opcode = SR_OP_UNARY0 + SrUnaryOp (1..)
-  SR_OP_SAVE = 62u, SR_OP_FIXUP = 63u,
   SR_OP_BINARY0 = 64u,  // opcode = SR_OP_BINARY0 + 6*(SrBinaryOp-1) + variant
   SR_V_SL = 0u, SR_V_SR = 1u, SR_V_FL = 2u, SR_V_FR = 3u, SR_V_CL = 4u, SR_V_CR = 5u,
-  SR_A_CHECK = 1u << 31, SR_A_OPFEAT = 1u << 30, SR_A_OPSTK = 1u << 29, SR_A_INDEX = (1u << 29) - 1u,
+  SR_A_CHECK = 1u << 31, SR_A_OPFEAT = 1u << 30, SR_A_OPSTK = 1u << 29, SR_A_INFSUB = 1u << 28,
+  SR_A_INDEX = (1u << 28) - 1u,
 };
-static_assert(SR_OP_UNARY0 + SR_U_COUNT <= SR_OP_SAVE, "unary opcode range overlaps SAVE/FIXUP");
+static_assert(SR_OP_UNARY0 + SR_U_COUNT <= SR_OP_BINARY0, "unary opcode range overlaps the binary range");
 static_assert(SR_OP_BINARY0 + 6 * SR_B_COUNT <= 256, "binary opcode range exceeds 8 bits");
 
 // Operand-source tag of an opcode (SR_A_OPFEAT / SR_A_OPSTK / 0).
 inline uint32_t sr_operand_tag(uint32_t op) {
   if (op == SR_OP_LOAD_FEAT || op == SR_OP_LOAD_FEAT_PUSH) return SR_A_OPFEAT;
-  if (op == SR_OP_FIXUP) return SR_A_OPSTK;
   if (op >= SR_OP_BINARY0) {
     const uint32_t v = (op - SR_OP_BINARY0) % 6u;
     if (v == SR_V_FL || v == SR_V_FR) return SR_A_OPFEAT;

@@ -73,11 +73,40 @@ struct SrLane {
   static __device__ inline int row(int l, int r) { return (r / C) * 64 * C + l * C + (r % C); }
 };
 
+// Whole-wave sum with DPP lane moves (pure VALU: no LDS round trips), in a fixed order:
+// pairs, quads (quad_perm), 8 (row_half_mirror), 16 (row_mirror), then rows 0+1 / 2+3
+// (row_bcast:15) and the two halves (row_bcast:31).  The total is read from lane 63 (uniform).
+template <int CTRL, int ROW_MASK = 0xf>
+__device__ __forceinline__ int sr_dpp(int v) {
+  return __builtin_amdgcn_update_dpp(0, v, CTRL, ROW_MASK, 0xf, false);
+}
+template <int CTRL, int ROW_MASK = 0xf>
+__device__ __forceinline__ float sr_dpp_add(float v) {
+  return v + __int_as_float(sr_dpp<CTRL, ROW_MASK>(__float_as_int(v)));
+}
+template <int CTRL, int ROW_MASK = 0xf>
+__device__ __forceinline__ double sr_dpp_add(double v) {
+  const uint64_t b = uint64_t(__double_as_longlong(v));
+  const uint32_t lo = uint32_t(sr_dpp<CTRL, ROW_MASK>(int(uint32_t(b))));
+  const uint32_t hi = uint32_t(sr_dpp<CTRL, ROW_MASK>(int(uint32_t(b >> 32))));
+  return v + __longlong_as_double(int64_t((uint64_t(hi) << 32) | lo));
+}
 template <typename T>
 __device__ __forceinline__ T sr_wave_sum(T v) {
-#pragma unroll
-  for (int off = 32; off >= 1; off >>= 1) v += __shfl_xor(v, off, 64);
-  return v;
+  v = sr_dpp_add<0xb1>(v);        // quad_perm [1,0,3,2]
+  v = sr_dpp_add<0x4e>(v);        // quad_perm [2,3,0,1]
+  v = sr_dpp_add<0x141>(v);       // row_half_mirror
+  v = sr_dpp_add<0x140>(v);       // row_mirror
+  v = sr_dpp_add<0x142, 0xa>(v);  // row_bcast:15 into rows 1, 3
+  v = sr_dpp_add<0x143, 0xc>(v);  // row_bcast:31 into rows 2, 3
+  if constexpr (sizeof(T) == 4) {
+    return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 63));
+  } else {
+    const uint64_t b = uint64_t(__double_as_longlong(v));
+    const uint32_t lo = uint32_t(__builtin_amdgcn_readlane(int(uint32_t(b)), 63));
+    const uint32_t hi = uint32_t(__builtin_amdgcn_readlane(int(uint32_t(b >> 32)), 63));
+    return __longlong_as_double(int64_t((uint64_t(hi) << 32) | lo));
+  }
 }
 __device__ __forceinline__ uint64_t sr_ballot(bool p) { return __builtin_amdgcn_ballot_w64(p); }
 
@@ -97,6 +126,29 @@ struct SrBits<double> {
   }
 };
 
+// Running max of |checked values| (deferred validity checks, BASIC tier): m <- max(m, |a|, |b|).
+// NaN operands are ignored by the IEEE max; the BASIC operators all map NaN to NaN, so a NaN at any
+// checked node reaches the root, whose values are tested for NaN explicitly.
+template <typename T>
+struct SrMaxAbs;
+template <>
+struct SrMaxAbs<float> {
+  static __device__ __forceinline__ float step(float m, float a, float b) {
+    float r;
+    asm("v_max3_f32 %0, %1, |%2|, |%3|" : "=v"(r) : "v"(m), "v"(a), "v"(b));
+    return r;
+  }
+};
+template <>
+struct SrMaxAbs<double> {
+  static __device__ __forceinline__ double step(double m, double a, double b) {
+    double r, q;
+    asm("v_max_f64 %0, %1, |%2|" : "=v"(q) : "v"(m), "v"(a));
+    asm("v_max_f64 %0, %1, |%2|" : "=v"(r) : "v"(q), "v"(b));
+    return r;
+  }
+};
+
 // ------------------------------------------------------------------ dispatch cases
 // Operators of the BASIC tier are compiled into every kernel; the FULL tier adds the rest of the
 // catalog (more registers: transcendental constants are hoisted out of the loop by LLVM).
@@ -105,18 +157,19 @@ struct SrBits<double> {
     const T x = tos[r];                           \
     tos[r] = (EXPR);                              \
   }
-#define SR_UCASE(ID)             \
-  case SR_OP_UNARY0 + ID: {      \
-    SR_EACH(sr_unary<T>(ID, x)); \
-    break;                       \
+#define SR_UCASE_GEN(ID, ENABLED)                                              \
+  case SR_OP_UNARY0 + ID: {                                                    \
+    if (ENABLED) {                                                             \
+      if (arg & SR_A_INFSUB) {                                                 \
+        SR_EACH(sr_isfinite(x) ? sr_unary<T>(ID, x) : sr_inf<T>());            \
+      } else {                                                                 \
+        SR_EACH(sr_unary<T>(ID, x));                                           \
+      }                                                                        \
+    }                                                                          \
+    break;                                                                     \
   }
-#define SR_UCASE_FULL(ID)          \
-  case SR_OP_UNARY0 + ID: {        \
-    if (TIER == SR_TIER_FULL) {    \
-      SR_EACH(sr_unary<T>(ID, x)); \
-    }                              \
-    break;                         \
-  }
+#define SR_UCASE(ID) SR_UCASE_GEN(ID, true)
+#define SR_UCASE_FULL(ID) SR_UCASE_GEN(ID, TIER == SR_TIER_FULL)
 #define SR_BIN_EACH(AEXPR, BEXPR, ID)             \
   _Pragma("unroll") for (int r = 0; r < R; ++r) { \
     const T aa = (AEXPR);                         \
@@ -176,10 +229,10 @@ struct SrBits<double> {
 #define SR_BCASE_FULL(ID) SR_BCASE_GEN(ID, TIER == SR_TIER_FULL)
 
 // LDS carve, in bytes, 16-aligned: X tile [nf][ROWS] T | y [ROWS] | w [ROWS] | stack
-// [SR_WAVES][depth][ROWS] T | acc [G] f64 | flg [G] u32 (padded to 4) | xacc [G][max_checks] f64
+// [SR_WAVES][depth][ROWS] T | xacc [G][max_checks] f64 (EXACT mode)
 template <typename T>
 struct SrLdsPlan {
-  size_t x, y, w, stk, acc, flg, xacc, total;
+  size_t x, y, w, stk, xacc, total;
   __host__ __device__ SrLdsPlan(int nf, int rows, int depth, int G, int max_checks) {
     size_t o = 0;
     x = o;
@@ -190,23 +243,34 @@ struct SrLdsPlan {
     o += size_t(rows) * sizeof(T);
     stk = o;
     o += size_t(SR_WAVES) * size_t(depth) * rows * sizeof(T);
-    acc = o;
-    o += size_t(G) * 8;
-    flg = o;
-    o += size_t((G + 3) & ~3) * 4;
     xacc = o;
     o += size_t(G) * size_t(max_checks) * 8;
     total = o;
   }
 };
 
+__device__ __forceinline__ uint4 sr_load_window(const void* code, uint32_t at) {
+  return *reinterpret_cast<const uint4*>(static_cast<const unsigned char*>(code) + size_t(at) * 16u);
+}
+
 // ------------------------------------------------------------------ the interpreter kernel
 // MODE: SR_MODE_LOSS (partials), SR_MODE_PRED (write predictions), SR_MODE_EXACT (check sums).
+//
+// Tree ownership: the block's G trees are positions tree0 .. tree0+G-1 of the launch order
+// (a.perm maps a position to the caller's tree index: the host orders trees by estimated cost so
+// the 4 waves of a block get equal work).  Wave w owns positions tree0 + w + 4j ("slot" j, j < 64);
+// everything per tree lives in that wave: program bounds in lane j's VGPRs, the loss accumulator in
+// lane j, the non-finite / suspicious bits in scalar masks.  While one tree runs, the first program
+// window of the wave's next tree is already in flight.
 template <typename T, int R, int MODE, bool GATHER, int TIER>
 __global__ void __launch_bounds__(SR_BLOCK SR_MIN_WAVES) sr_tile_kernel(const SrEvalArgs<T> a) {
   using L = SrLane<T, R>;
   constexpr int C = L::C;
   constexpr int ROWS = 64 * R;
+  // Deferred validity checks (BASIC tier): no per-check ballot or early exit; the
+  // tree's running max |checked value| and the root's NaN test decide at the end of the program.
+  constexpr bool FAST_CHECK = (TIER == SR_TIER_BASIC) && (MODE != SR_MODE_EXACT);
+  static_assert(R % 2 == 0, "rows per lane must be even");
   extern __shared__ __attribute__((aligned(16))) unsigned char sr_smem[];
   const int tid = threadIdx.x;
   const int wave = tid >> 6;
@@ -217,8 +281,6 @@ __global__ void __launch_bounds__(SR_BLOCK SR_MIN_WAVES) sr_tile_kernel(const Sr
   T* xs = reinterpret_cast<T*>(sr_smem + plan.x);
   T* ys = reinterpret_cast<T*>(sr_smem + plan.y);
   T* wsv = reinterpret_cast<T*>(sr_smem + plan.w);
-  double* acc = reinterpret_cast<double*>(sr_smem + plan.acc);
-  uint32_t* flg = reinterpret_cast<uint32_t*>(sr_smem + plan.flg);
   double* xacc = reinterpret_cast<double*>(sr_smem + plan.xacc);
   const T* x_lane = xs + lane * C;
   const T* y_lane = ys + lane * C;
@@ -234,15 +296,31 @@ __global__ void __launch_bounds__(SR_BLOCK SR_MIN_WAVES) sr_tile_kernel(const Sr
   const bool weighted = a.w != nullptr;
   const uint32_t thr = SrBits<T>::mag(a.tbig);
 
-  for (int i = tid; i < G; i += SR_BLOCK) {
-    acc[i] = 0.0;
-    flg[i] = 0u;
+  // this wave's slots
+  const int S = gcount > wave ? (gcount - wave + SR_WAVES - 1) / SR_WAVES : 0;
+  const int my_pos = tree0 + wave + SR_WAVES * lane;
+  uint32_t my_pb = 0u, my_pe = 0u;
+  if (lane < S) {
+    const uint32_t t = a.perm ? a.perm[my_pos] : uint32_t(my_pos);
+    my_pb = a.offsets[t];
+    my_pe = a.offsets[t + 1];
   }
+  const uint64_t live = sr_ballot(lane < S && my_pe > my_pb);  // empty program: statically incomplete
+  uint64_t dmask = 0u, bmask = 0u;
+  double accv = 0.0;
+  // dead-tree hints shared across row blocks (LOSS mode): a tree found non-finite by any block is
+  // skipped by blocks that start it later.  Loaded one tile ahead; only ever a hint (a skipped
+  // tree is reported non-finite, which the discovering block reports anyway).
+  const bool use_hint = (MODE == SR_MODE_LOSS) && a.hint != nullptr;
+  uint32_t hintv = 0u;
+  if (use_hint && lane < S) hintv = __hip_atomic_load(a.hint + my_pos, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+
   for (int i = tid; i < G * MC; i += SR_BLOCK) xacc[i] = 0.0;
 
   for (int tile = 0; tile < a.tiles_per_block; ++tile) {
     const int64_t row0 = (int64_t(rb) * a.tiles_per_block + tile) * ROWS;
     if (row0 >= a.n_rows) break;  // uniform over the block
+    const bool full_tile = row0 + ROWS <= a.n_rows;
     __syncthreads();              // previous tile's readers are done with the LDS image
     // ---- stage the tile: X rows of every feature, y, w (a plain copy; padded rows replicate
     // row 0 of the view, so every program sees finite, in-range data there)
@@ -273,13 +351,23 @@ __global__ void __launch_bounds__(SR_BLOCK SR_MIN_WAVES) sr_tile_kernel(const Sr
     }
     __syncthreads();
 
-    for (int g = wave; g < gcount; g += SR_WAVES) {
-      const int tree = (MODE == SR_MODE_EXACT) ? int(a.tree_list[tree0 + g]) : tree0 + g;
-      if (MODE == SR_MODE_LOSS && (__builtin_amdgcn_readfirstlane(flg[g]) & SR_FLAG_NONFINITE)) continue;
-      const uint32_t pb = a.offsets[tree];
-      const uint32_t pe = a.offsets[tree + 1];
-      if (pb == pe) continue;  // statically incomplete (constant checks)
-
+    if (use_hint) {
+      dmask |= sr_ballot(hintv != 0u) & live;
+      if (lane < S) hintv = __hip_atomic_load(a.hint + my_pos, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    uint64_t todo = (MODE == SR_MODE_LOSS) ? (live & ~dmask) : live;
+    if (todo) {
+      // Window stream: the 64-instruction program windows of this tile's trees, in order.  The
+      // next window (of this tree, or the first one of the next tree) is in flight while the current
+      // one runs; the running window is a register copy, so the interpreter loop never waits on it.
+      int nj = __builtin_ctzll(todo);
+      todo &= todo - 1u;
+      uint32_t nb = uint32_t(__builtin_amdgcn_readlane(int(my_pb), nj));
+      uint32_t ne = uint32_t(__builtin_amdgcn_readlane(int(my_pe), nj));
+      uint4 nx = make_uint4(0u, 0u, 0u, 0u);
+      if (nb + lane < ne) nx = sr_load_window(a.code, nb + lane);
+      int j = -1;
+      uint32_t tpe = 0u;
       T tos[R];
 #pragma unroll
       for (int r = 0; r < R; ++r) tos[r] = T(0);
@@ -287,20 +375,41 @@ __global__ void __launch_bounds__(SR_BLOCK SR_MIN_WAVES) sr_tile_kernel(const Sr
       bool dead = false;
       bool susp_any = false;
       int check_k = 0;
-
-      // The program is staged in VGPRs, one 16-byte instruction per lane (64-instruction windows);
-      // each step reads its words with v_readlane: no scalar-memory round trip per step, and the
-      // LDS waits (lgkmcnt) never wait on an instruction fetch.
-      uint32_t wc = 0, wa = 0, wl = 0, wh = 0;
-      for (uint32_t base = pb; base < pe; base += 64u) {
-        if (base + lane < pe) {
-          const uint4 v = *reinterpret_cast<const uint4*>(a.code + base + lane);
-          wc = v.x;
-          wa = v.y;
-          wl = v.z;
-          wh = v.w;
+      T mrun = T(0), mrun1 = T(0);  // FAST_CHECK: max |checked value| over this lane's rows (2 chains)
+      bool more = true;
+      while (more) {
+        const uint4 cw = nx;
+        const uint32_t base = nb;
+        if (nj != j) {  // a new tree starts
+          j = nj;
+          tpe = ne;
+#pragma unroll
+          for (int r = 0; r < R; ++r) tos[r] = T(0);
+          sp = 0;
+          dead = false;
+          susp_any = false;
+          check_k = 0;
+          mrun = T(0);
+          mrun1 = T(0);
         }
-        const uint32_t n_here = __builtin_amdgcn_readfirstlane((pe - base < 64u) ? pe - base : 64u);
+        if (base + 64u < tpe) {
+          nb = base + 64u;
+        } else if (todo) {
+          nj = __builtin_ctzll(todo);
+          todo &= todo - 1u;
+          nb = uint32_t(__builtin_amdgcn_readlane(int(my_pb), nj));
+          ne = uint32_t(__builtin_amdgcn_readlane(int(my_pe), nj));
+        } else {
+          more = false;
+        }
+        if (more && nb + lane < ne) nx = sr_load_window(a.code, nb + lane);
+        const int g = wave + SR_WAVES * j;
+
+      // The program sits in VGPRs, one 16-byte instruction per lane; each step reads its words with
+      // v_readlane.
+      if (!dead) {
+        const uint32_t wc = cw.x, wa = cw.y, wl = cw.z, wh = cw.w;
+        const uint32_t n_here = __builtin_amdgcn_readfirstlane((tpe - base < 64u) ? tpe - base : 64u);
         // single-exit inner loop (a dead tree sets k past the window): a second loop exit would make
         // LLVM add an exit-selector block to every iteration
         for (uint32_t k = 0; k < n_here; ++k) {
@@ -338,19 +447,6 @@ __global__ void __launch_bounds__(SR_BLOCK SR_MIN_WAVES) sr_tile_kernel(const Sr
               for (int r = 0; r < R; ++r) tos[r] = cval;
               break;
             }
-            case SR_OP_SAVE: {
-              L::store(stk_lane + sp * ROWS, tos);
-              ++sp;
-              break;
-            }
-            case SR_OP_FIXUP: {
-              --sp;
-              T o[R];
-              L::load(stk_lane + sp * ROWS, o);
-#pragma unroll
-              for (int r = 0; r < R; ++r) tos[r] = sr_isfinite(o[r]) ? tos[r] : sr_inf<T>();
-              break;
-            }
             // BASIC tier
             SR_UCASE(SR_U_NEG) SR_UCASE(SR_U_SQUARE) SR_UCASE(SR_U_CUBE) SR_UCASE(SR_U_EXP)
             SR_UCASE(SR_U_COS) SR_UCASE(SR_U_SIN) SR_UCASE(SR_U_LOG) SR_UCASE(SR_U_SQRT)
@@ -381,6 +477,12 @@ __global__ void __launch_bounds__(SR_BLOCK SR_MIN_WAVES) sr_tile_kernel(const Sr
               s = sr_wave_sum<double>(s);
               if (lane == 0) xacc[g * MC + check_k] += s;
               ++check_k;
+            } else if (FAST_CHECK) {
+#pragma unroll
+              for (int r = 0; r < R; r += 4) {
+                mrun = SrMaxAbs<T>::step(mrun, tos[r], tos[r + 1]);
+                if (r + 3 < R) mrun1 = SrMaxAbs<T>::step(mrun1, tos[r + 2], tos[r + 3]);
+              }
             } else {
               // |v| >= tbig (or NaN / Inf) in any row: one integer max per lane + one ballot;
               // padded rows replicate row 0 of the view, so no row mask is needed here
@@ -400,54 +502,68 @@ __global__ void __launch_bounds__(SR_BLOCK SR_MIN_WAVES) sr_tile_kernel(const Sr
             }
           }
         }
-        if (dead) break;
+      }
+      if (base + 64u >= tpe) {  // tree j is done on this tile
+      if (FAST_CHECK) {
+        // a checked value was +-Inf (or NaN reached the root): incomplete; a large finite one:
+        // the array-sum check may overflow -> exact path
+        bool nan_root = false;
+#pragma unroll
+        for (int r = 0; r < R; ++r) nan_root |= sr_isnan(tos[r]);
+        mrun = SrMaxAbs<T>::step(mrun, mrun1, T(0));
+        if (sr_ballot(nan_root || !(mrun <= SrM<T>::big))) {
+          dead = true;
+        } else if (sr_ballot(!(mrun < a.tbig))) {
+          susp_any = true;
+        }
       }
 
-      if (MODE == SR_MODE_LOSS) {
-        if (dead) {
-          if (lane == 0) flg[g] |= SR_FLAG_NONFINITE;
-          continue;
-        }
+      const uint64_t bit = uint64_t(1) << j;
+      if (MODE == SR_MODE_LOSS && dead) {
+        dmask |= bit;
+        if (use_hint && lane == 0)
+          __hip_atomic_fetch_or(a.hint + tree0 + g, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      } else if (MODE == SR_MODE_LOSS) {
         T yv[R];
         L::load(y_lane, yv);
-        T s = T(0);
+        T l[R];
         if (weighted) {
           T wv[R];
           L::load(w_lane, wv);
 #pragma unroll
-          for (int r = 0; r < R; ++r) {
-            const T l = sr_elem_loss<T>(a.loss_kind, tos[r], yv[r]) * wv[r];
-            s += (row0 + L::row(lane, r) < a.n_rows) ? l : T(0);
-          }
+          for (int r = 0; r < R; ++r) l[r] = sr_elem_loss<T>(a.loss_kind, tos[r], yv[r]) * wv[r];
         } else {
 #pragma unroll
-          for (int r = 0; r < R; ++r) {
-            const T l = sr_elem_loss<T>(a.loss_kind, tos[r], yv[r]);
-            s += (row0 + L::row(lane, r) < a.n_rows) ? l : T(0);
-          }
+          for (int r = 0; r < R; ++r) l[r] = sr_elem_loss<T>(a.loss_kind, tos[r], yv[r]);
         }
+        if (!full_tile) {  // rows past the end of the view (padding) do not count
+#pragma unroll
+          for (int r = 0; r < R; ++r) l[r] = (row0 + L::row(lane, r) < a.n_rows) ? l[r] : T(0);
+        }
+        T s = l[0];
+#pragma unroll
+        for (int r = 1; r < R; ++r) s += l[r];
         s = sr_wave_sum<T>(s);
-        if (lane == 0) {
-          acc[g] += double(s);
-          if (susp_any) flg[g] |= SR_FLAG_BIG;
-        }
+        accv += (lane == j) ? double(s) : 0.0;
+        if (susp_any) bmask |= bit;
       } else if (MODE == SR_MODE_PRED) {
+        const uint32_t tree = a.perm ? a.perm[tree0 + g] : uint32_t(tree0 + g);
         T* out = a.pred + int64_t(tree) * a.pred_ld + row0;
 #pragma unroll
         for (int r = 0; r < R; ++r) {
           const int i = L::row(lane, r);
           if (row0 + i < a.n_rows) out[i] = dead ? sr_qnan<T>() : tos[r];
         }
-        if (lane == 0) {
-          if (dead) flg[g] |= SR_FLAG_NONFINITE;
-          else if (susp_any) flg[g] |= SR_FLAG_BIG;
-        }
+        if (dead) dmask |= bit;
+        else if (susp_any) bmask |= bit;
       }
+      }  // tree done
+      }  // window stream
     }
   }
 
-  __syncthreads();
   if (MODE == SR_MODE_EXACT) {
+    __syncthreads();
     // one device-scope add per (block, tree, check)
     for (int i = tid; i < gcount * MC; i += SR_BLOCK) {
       const double v = xacc[i];
@@ -455,10 +571,10 @@ __global__ void __launch_bounds__(SR_BLOCK SR_MIN_WAVES) sr_tile_kernel(const Sr
     }
     return;
   }
-  for (int g = tid; g < gcount; g += SR_BLOCK) {
-    const size_t o = size_t(tree0 + g) * a.n_row_blocks + rb;
-    a.part_sum[o] = acc[g];
-    a.part_flag[o] = flg[g];
+  if (lane < S) {
+    const size_t o = size_t(my_pos) * a.n_row_blocks + rb;
+    a.part_sum[o] = accv;
+    a.part_flag[o] = (((dmask >> lane) & 1u) ? SR_FLAG_NONFINITE : 0u) | (((bmask >> lane) & 1u) ? SR_FLAG_BIG : 0u);
   }
 }
 

@@ -1,7 +1,7 @@
 """TEST HELPER: a numpy interpreter of libsr_amd's compiled programs (csrc/sr_ops.h encoding).
 
 It executes exactly the instruction semantics of the HIP kernel (top-of-stack + operand stack,
-combined opcodes, SAVE / FIXUP, the CHECK bit of arg) on the CPU, so CPU tests can validate the tree COMPILER
+combined opcodes, the INFSUB and CHECK bits of arg) on the CPU, so CPU tests can validate the tree COMPILER
 (constant folding, check placement, fused-unary detection, Sethi–Ullman ordering) against the
 oracle without a GPU.  It is not part of the product and is never used as a fallback.
 """
@@ -84,19 +84,17 @@ def run_program(code, lo, hi, X, T):
     for pc in range(lo, hi):
         opc = int(code["code"][pc])
         arg = int(code["arg"][pc])
-        fidx = arg & ((1 << 29) - 1)  # bits 29/30: operand-source tags
+        fidx = arg & ((1 << 28) - 1)  # bit 28: INFSUB, bits 29/30: operand-source tags
         val = T(code["val"][pc])
         if opc <= 3:
             if opc >= 2:
                 stack.append(tos)
             tos = X[fidx].astype(T) if opc in (0, 2) else np.full(n, val, dtype=T)
-        elif opc == 62:  # SAVE: push a copy of tos
-            stack.append(tos.copy())
-        elif opc == 63:  # FIXUP: non-finite saved operand -> +Inf
-            o = stack.pop()
-            tos = np.where(np.isfinite(o), tos, T(np.inf)).astype(T)
-        elif opc < 62:
-            tos = _unary(opc - 3, tos, T).astype(T)
+        elif opc < 64:
+            v = _unary(opc - 3, tos, T).astype(T)
+            if arg & (1 << 28):  # INFSUB: fused unary, non-finite input -> +Inf
+                v = np.where(np.isfinite(tos), v, T(np.inf)).astype(T)
+            tos = v
         else:
             bid, v = divmod(opc - 64, 6)
             bid += 1

@@ -62,12 +62,13 @@ def test_program_shapes():
     a = code["arg"][offs[k]:offs[k + 1]]
     checks = [(int(v) >> 31) & 1 for v in a]
     assert checks == [1, 1, 1, 1, 1]
-    # fused unary: cos(x1 * 2.0) -> LOAD x1, MUL c, SAVE, COS, FIXUP; no CHECK on the inner product
+    # fused unary: cos(x1 * 2.0) -> LOAD x1, MUL c, COS with INFSUB; no CHECK on the inner product
     tb2 = flatten_trees([parse_expression("cos(x1 * 2.0)", opts)], np.float32)
     code2, offs2, _, depth2 = vm.compile_info(opts, tb2, 100, 5, np.float32)
-    assert [int(v) for v in code2["code"][:offs2[1]]] == [0, 64 + 6 * 2 + 5, 62, 3 + 5, 63]
-    assert [(int(v) >> 31) & 1 for v in code2["arg"][:offs2[1]]] == [0, 0, 0, 0, 1]
-    assert depth2 == 1  # SAVE takes one stack slot
+    assert [int(v) for v in code2["code"][:offs2[1]]] == [0, 64 + 6 * 2 + 5, 3 + 5]
+    assert [(int(v) >> 31) & 1 for v in code2["arg"][:offs2[1]]] == [0, 0, 1]
+    assert [(int(v) >> 28) & 1 for v in code2["arg"][:offs2[1]]] == [0, 0, 1]
+    assert depth2 == 0  # the fused unary needs no stack slot
 
 
 def test_static_incomplete():

@@ -13,4 +13,5 @@ for pmc in "SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_SMEM" "SQ_WAVE_CYCLES 
   i=$((i+1))
   timeout -k 10 300 rocprofv3 --pmc $pmc --output-format csv -d $OUT/pmc$i -o pmc$i -- $B > $OUT/pmc$i.log 2>&1 || echo "pmc pass $i failed: $?" >> $OUT/errors.txt
 done
+python3 tools/pmc_summary.py $OUT > $OUT/summary.txt
 exit 0
