@@ -116,6 +116,7 @@ def main():
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         dt = float(tt.item())
 
+    grid_g = int(os.environ.get("SR_AMD_TREES_PER_BLOCK", "0")) or 128  # trees sharing one staged row tile
     nodes = int(tb.n_nodes)
     ops = int(tb.n_operator_nodes)
     node_evals = float(nodes) * float(n_total)            # all ranks
@@ -124,6 +125,10 @@ def main():
     flops_per_launch = float(args.rows) * (ops + 3 * nt)
     kmean = float(np.mean(kernel_ms))
     achieved = flops_per_launch / (kmean * 1e-3) / 1e12
+    # algorithmic bytes of the interpreter launch: one pass of X + y per tree group
+    n_passes = -(-nt // min(grid_g, nt))
+    bytes_per_launch = float(n_passes) * (5 + 1) * float(args.rows) * 4.0
+    traffic = measured_traffic()
     if world > 1:
         comp = result["comp"]
     frac_complete = float(np.mean(comp.astype(bool)))
@@ -163,17 +168,34 @@ def main():
                 "peak": PEAK_FP32_TFLOPS,
                 "unit": "TFLOP/s",
                 "frac": achieved / PEAK_FP32_TFLOPS,
-                "traffic": None,
+                "traffic": traffic.get("hbm_read_bytes_per_launch") if traffic else None,
+                "traffic_source": traffic.get("source") if traffic else None,
                 "kernel": "sr_tile_kernel<float,8,LOSS,gather=false,BASIC>",
                 "kernel_ms_mean": kmean,
                 "flops_per_launch": flops_per_launch,
                 "flop_convention": "n_rows * sum_t(n_op(t) + 3), 1 flop per operator incl. transcendentals (SURVEY 8d)",
+                "algorithmic_bytes_per_launch": bytes_per_launch,
+                "algorithmic_GBps": bytes_per_launch / (kmean * 1e-3) / 1e9,
+                "bytes_convention": "ceil(n_trees/G) passes x (nf+1) x n_rows x 4 B; X/y re-reads are served from L2/MALL",
             },
             "cpu_baseline": cpu,
         }
         print(json.dumps(line), flush=True)
     if dist is not None:
         dist.destroy_process_group()
+
+
+def measured_traffic():
+    """Per-launch HBM bytes of the interpreter kernel from the committed rocprofv3 PMC pass of this
+    same command (profiles/traffic.json, written by tools/profile.sh: FETCH_SIZE x2, gfx950)."""
+    p = os.path.join(ROOT, "profiles", "traffic.json")
+    try:
+        with open(p) as f:
+            t = json.load(f)
+    except (OSError, ValueError):
+        return None
+    t["source"] = "profiles/traffic.json (rocprofv3 --pmc FETCH_SIZE of bench.py)"
+    return t
 
 
 def cpu_baseline(opts, tb, X, y, n_sample):

@@ -1,17 +1,22 @@
 #!/bin/bash
-# Kernel trace + PMC counter passes of the benchmark (each pass its own rocprofv3 run).
+# rocprofv3 evidence for bench.py (each pass its own run): kernel trace + stats, then PMC passes.
+# Writes gpurun_out/prof/summary.txt and gpurun_out/prof/traffic.json (per-launch HBM read bytes of
+# the interpreter kernel, FETCH_SIZE x2 gfx950 correction, MI355X_MICROARCH.md HBM section).
 set -o pipefail
 cd $GRAFT_REPO_ROOT
 export TMPDIR=/tmp
 OUT=gpurun_out/prof
-mkdir -p $OUT
+rm -rf $OUT; mkdir -p $OUT
 B="python3 bench.py --steps 5 --warmup 1 --no-cpu-baseline"
-timeout -k 10 120 rocprofv3 -L > $OUT/counters_list.txt 2>&1 || true
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/kt -o kt -- $B > $OUT/kt.log 2>&1 || exit $?
 i=0
-for pmc in "SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_SMEM" "SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_SCA" "SQ_INSTS_LDS SQ_INSTS_VMEM SQ_WAIT_INST_ANY SQ_WAIT_ANY" "FETCH_SIZE" "GRBM_GUI_ACTIVE SQ_INSTS_BRANCH"; do
+for pmc in "SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_SMEM SQ_INSTS_BRANCH SQ_INSTS_LDS SQ_INSTS_VMEM SQ_WAVE_CYCLES" \
+           "SQ_BUSY_CYCLES SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_SCA SQ_ACTIVE_INST_LDS SQ_ACTIVE_INST_ANY SQ_WAIT_INST_ANY SQ_WAIT_ANY GRBM_GUI_ACTIVE" \
+           "SQ_INSTS_VALU_FLOPS_FP32 SQ_INSTS_VALU_FLOPS_FP32_TRANS SQ_INSTS_VALU_TRANS_F32 SQ_INSTS_VALU_ADD_F32 SQ_INSTS_VALU_MUL_F32 SQ_INSTS_VALU_FMA_F32 SQ_THREAD_CYCLES_VALU" \
+           "FETCH_SIZE" "WRITE_SIZE"; do
   i=$((i+1))
-  timeout -k 10 300 rocprofv3 --pmc $pmc --output-format csv -d $OUT/pmc$i -o pmc$i -- $B > $OUT/pmc$i.log 2>&1 || echo "pmc pass $i failed: $?" >> $OUT/errors.txt
+  timeout -s KILL 180 rocprofv3 --pmc $pmc --output-format csv -d $OUT/pmc$i -o pmc$i -- $B > $OUT/pmc$i.log 2>&1 || echo "pmc pass $i failed: $?" >> $OUT/errors.txt
 done
 python3 tools/pmc_summary.py $OUT > $OUT/summary.txt
+python3 tools/pmc_summary.py $OUT --traffic-json sr_tile_kernel > $OUT/traffic.json
 exit 0
