@@ -5,15 +5,10 @@
 
 #include "sr_eval.h"
 
-template <typename T>
-__device__ __forceinline__ T sr_wave_sum_aux(T v) {
-#pragma unroll
-  for (int off = 32; off >= 1; off >>= 1) v += __shfl_xor(v, off, 64);
-  return v;
-}
 
-// One wave per launch position: Σ over row blocks in a fixed lane/stride order (bit-reproducible),
-// OR of flags; the result goes to the caller's tree index perm[position].
+// One thread per launch position: Σ over row blocks in row-block order (bit-reproducible), OR of
+// flags (partials are laid out [row block][position], so neighbouring threads read neighbouring
+// words); the result goes to the caller's tree index perm[position].
 __global__ void __launch_bounds__(256) sr_reduce_partials_kernel(const double* __restrict__ part_sum,
                                                                   const uint32_t* __restrict__ part_flag,
                                                                   int n_trees, int n_row_blocks,
@@ -21,26 +16,18 @@ __global__ void __launch_bounds__(256) sr_reduce_partials_kernel(const double* _
                                                                   const uint8_t* __restrict__ static_bad,
                                                                   double* __restrict__ out_sum,
                                                                   uint32_t* __restrict__ out_flag) {
-  const int pos = int((int64_t(blockIdx.x) * blockDim.x + threadIdx.x) >> 6);
-  const int lane = threadIdx.x & 63;
+  const int pos = int(int64_t(blockIdx.x) * blockDim.x + threadIdx.x);
   if (pos >= n_trees) return;
   const int tree = perm ? int(perm[pos]) : pos;
-  const double* ps = part_sum + size_t(pos) * n_row_blocks;
-  const uint32_t* pf = part_flag + size_t(pos) * n_row_blocks;
   double s = 0.0;
   uint32_t f = 0u;
-  for (int i = lane; i < n_row_blocks; i += 64) {
-    s += ps[i];
-    f |= pf[i];
+  for (int i = 0; i < n_row_blocks; ++i) {
+    s += part_sum[size_t(i) * n_trees + pos];
+    f |= part_flag[size_t(i) * n_trees + pos];
   }
-  s = sr_wave_sum_aux<double>(s);
-#pragma unroll
-  for (int off = 32; off >= 1; off >>= 1) f |= __shfl_xor(f, off, 64);
-  if (lane == 0) {
-    if (static_bad && static_bad[tree]) f |= SR_FLAG_STATIC | SR_FLAG_NONFINITE;
-    out_sum[tree] = s;
-    out_flag[tree] = f;
-  }
+  if (static_bad && static_bad[tree]) f |= SR_FLAG_STATIC | SR_FLAG_NONFINITE;
+  out_sum[tree] = s;
+  out_flag[tree] = f;
 }
 
 // Julia [nf, n] column-major -> per-feature rows [nf][ld]; padded rows replicate row 0 so that the
@@ -65,7 +52,7 @@ hipError_t sr_launch_reduce(const double* part_sum, const uint32_t* part_flag, i
                             const uint32_t* perm, const uint8_t* static_bad, double* out_sum, uint32_t* out_flag,
                             hipStream_t s) {
   if (n_trees <= 0) return hipSuccess;
-  const int64_t blocks = (int64_t(n_trees) * 64 + 255) / 256;
+  const int64_t blocks = (int64_t(n_trees) + 255) / 256;
   hipLaunchKernelGGL(sr_reduce_partials_kernel, dim3(unsigned(blocks)), dim3(256), 0, s, part_sum, part_flag,
                      n_trees, n_row_blocks, perm, static_bad, out_sum, out_flag);
   return hipGetLastError();
@@ -92,7 +79,7 @@ template <typename T>
 int sr_rows_per_lane(int mode, int tier, int requested) {
   const bool basic = mode == SR_MODE_LOSS && tier == SR_TIER_BASIC;
   if (sizeof(T) == 4) {
-    if (basic) return requested == 4 ? 4 : 8;
+    if (basic) return (requested == 4 || requested == 16) ? requested : 8;
     return 4;
   }
   return basic ? 4 : 2;
@@ -101,22 +88,39 @@ template int sr_rows_per_lane<float>(int, int, int);
 template int sr_rows_per_lane<double>(int, int, int);
 
 size_t sr_tile_lds_bytes(int elem_size, int nf, int rows_per_lane, int stack_depth, int trees_per_block,
-                         int max_checks) {
+                         int max_checks, int waves, bool weighted) {
   const size_t rows = size_t(64) * rows_per_lane;
-  return size_t(nf) * rows * elem_size + 2 * rows * elem_size + size_t(4) * stack_depth * rows * elem_size +
-         size_t(trees_per_block) * size_t(max_checks) * 8;
+  return size_t(nf) * rows * elem_size + (weighted ? 2 : 1) * rows * elem_size +
+         size_t(waves) * stack_depth * rows * elem_size + size_t(trees_per_block) * size_t(max_checks) * 8;
+}
+
+// Waves per workgroup: the f32 BASIC loss kernel has 4- and 16-wave builds (SR_AMD_WAVES selects);
+// every other kernel runs 4 waves.
+int sr_waves_per_block(int elem_size, int mode, int tier, int rows_per_lane, int requested) {
+  if (elem_size == 4 && mode == SR_MODE_LOSS && tier == SR_TIER_BASIC && rows_per_lane == 8 && requested == 16)
+    return 16;
+  return 4;
+}
+
+// BASIC-tier loss kernels are built per elementwise loss (the loss code folds away).
+template <typename T, int R, bool GATHER>
+hipError_t sr_launch_basic_loss(const SrEvalArgs<T>& a, int n_blocks, hipStream_t s) {
+  if (a.loss_kind == SR_LOSS_L1) return sr_launch_tile<T, R, SR_MODE_LOSS, GATHER, SR_TIER_BASIC, 4, SR_LOSS_L1>(a, n_blocks, s);
+  return sr_launch_tile<T, R, SR_MODE_LOSS, GATHER, SR_TIER_BASIC, 4, SR_LOSS_L2>(a, n_blocks, s);
 }
 
 template <typename T>
-hipError_t sr_launch_eval(const SrEvalArgs<T>& a, int mode, bool gather, int tier, int rows_per_lane, int n_blocks,
-                          hipStream_t s) {
+hipError_t sr_launch_eval(const SrEvalArgs<T>& a, int mode, bool gather, int tier, int rows_per_lane, int waves,
+                          int n_blocks, hipStream_t s) {
   const int R = sr_rows_per_lane<T>(mode, tier, rows_per_lane);
   if constexpr (sizeof(T) == 4) {
     if (mode == SR_MODE_LOSS) {
       if (tier == SR_TIER_BASIC) {
-        if (gather) return sr_launch_tile<T, 8, SR_MODE_LOSS, true, SR_TIER_BASIC>(a, n_blocks, s);
-        return R == 4 ? sr_launch_tile<T, 4, SR_MODE_LOSS, false, SR_TIER_BASIC>(a, n_blocks, s)
-                      : sr_launch_tile<T, 8, SR_MODE_LOSS, false, SR_TIER_BASIC>(a, n_blocks, s);
+        if (gather) return sr_launch_basic_loss<T, 8, true>(a, n_blocks, s);
+        if (R == 16) return sr_launch_tile<T, 16, SR_MODE_LOSS, false, SR_TIER_BASIC>(a, n_blocks, s);
+        if (R == 4) return sr_launch_tile<T, 4, SR_MODE_LOSS, false, SR_TIER_BASIC>(a, n_blocks, s);
+        if (waves == 16) return sr_launch_tile<T, 8, SR_MODE_LOSS, false, SR_TIER_BASIC, 16>(a, n_blocks, s);
+        return sr_launch_basic_loss<T, 8, false>(a, n_blocks, s);
       }
       return gather ? sr_launch_tile<T, 4, SR_MODE_LOSS, true, SR_TIER_FULL>(a, n_blocks, s)
                     : sr_launch_tile<T, 4, SR_MODE_LOSS, false, SR_TIER_FULL>(a, n_blocks, s);
@@ -128,10 +132,10 @@ hipError_t sr_launch_eval(const SrEvalArgs<T>& a, int mode, bool gather, int tie
                   : sr_launch_tile<T, 4, SR_MODE_EXACT, false, SR_TIER_FULL>(a, n_blocks, s);
   } else {
     (void)R;
+    (void)waves;
     if (mode == SR_MODE_LOSS) {
       if (tier == SR_TIER_BASIC)
-        return gather ? sr_launch_tile<T, 4, SR_MODE_LOSS, true, SR_TIER_BASIC>(a, n_blocks, s)
-                      : sr_launch_tile<T, 4, SR_MODE_LOSS, false, SR_TIER_BASIC>(a, n_blocks, s);
+        return gather ? sr_launch_basic_loss<T, 4, true>(a, n_blocks, s) : sr_launch_basic_loss<T, 4, false>(a, n_blocks, s);
       return gather ? sr_launch_tile<T, 2, SR_MODE_LOSS, true, SR_TIER_FULL>(a, n_blocks, s)
                     : sr_launch_tile<T, 2, SR_MODE_LOSS, false, SR_TIER_FULL>(a, n_blocks, s);
     }
@@ -143,8 +147,8 @@ hipError_t sr_launch_eval(const SrEvalArgs<T>& a, int mode, bool gather, int tie
   }
 }
 
-template hipError_t sr_launch_eval<float>(const SrEvalArgs<float>&, int, bool, int, int, int, hipStream_t);
-template hipError_t sr_launch_eval<double>(const SrEvalArgs<double>&, int, bool, int, int, int, hipStream_t);
+template hipError_t sr_launch_eval<float>(const SrEvalArgs<float>&, int, bool, int, int, int, int, hipStream_t);
+template hipError_t sr_launch_eval<double>(const SrEvalArgs<double>&, int, bool, int, int, int, int, hipStream_t);
 template hipError_t sr_launch_transpose<float>(const float*, int64_t, int64_t, int64_t, float*, hipStream_t);
 template hipError_t sr_launch_transpose<double>(const double*, int64_t, int64_t, int64_t, double*, hipStream_t);
 template hipError_t sr_launch_pad<float>(float*, int64_t, int64_t, float, int, hipStream_t);

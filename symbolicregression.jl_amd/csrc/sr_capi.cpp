@@ -79,6 +79,7 @@ struct sr_ctx {
   int cu_count = 256;
   int rows_override = 0;    // SR_AMD_ROWS_PER_LANE (tuning): 4 selects the f32 BASIC 4-rows/lane kernel
   int tree_group = 0;       // SR_AMD_TREES_PER_BLOCK override (0 = heuristic)
+  int waves_override = 0;   // SR_AMD_WAVES (tuning): 16 selects the 16-wave f32 BASIC loss kernel
   bool cost_order = true;   // launch trees in decreasing estimated cost (SR_AMD_NO_SORT=1 disables)
   bool dead_hints = true;   // share dead-tree hints across row blocks (SR_AMD_NO_HINT=1 disables)
   std::vector<uint32_t> perm_host;
@@ -102,16 +103,18 @@ constexpr int64_t kRowAlign = 2048;  // a multiple of every kernel's row tile (6
 // Work decomposition: row tiles of 64*R rows (one LDS image each), `tiles` per block; trees grouped G
 // per block (the block's 4 waves share the G trees of a tile).
 struct Grid {
-  int G = 32, tiles = 1, n_row_blocks = 1, n_groups = 1, R = 8;
+  int G = 32, tiles = 1, n_row_blocks = 1, n_groups = 1, R = 8, W = 4;
   int64_t n_blocks = 1;
   size_t lds = 0;
 };
 constexpr size_t kLdsMax = 160 * 1024;
 template <typename T>
-Grid make_grid(int64_t n_rows, int64_t n_trees, int R, int nf, int depth, int max_checks, int g_override = 0) {
+Grid make_grid(int64_t n_rows, int64_t n_trees, int R, int W, int nf, int depth, int max_checks, bool weighted,
+               int g_override = 0) {
   const int64_t rows_per_tile = 64 * int64_t(R);
   Grid g;
   g.R = R;
+  g.W = W;
   const int64_t n_tiles = (n_rows + rows_per_tile - 1) / rows_per_tile;
   int64_t tiles = (n_tiles + 255) / 256;  // keep <= 256 row blocks per tree
   if (tiles < 1) tiles = 1;
@@ -123,12 +126,13 @@ Grid make_grid(int64_t n_rows, int64_t n_trees, int R, int nf, int depth, int ma
   int G = 128;
   while (G > 4 && int64_t(g.n_row_blocks) * ((n_trees + G - 1) / G) < 4096) G /= 2;
   if (g_override > 0) G = g_override;
+  if (G < W) G = W;  // at least one tree per wave
   if (n_trees > 0 && G > n_trees) G = int(n_trees);
   if (G < 1) G = 1;
   g.G = G;
   g.n_groups = int((n_trees + G - 1) / G);
   g.n_blocks = int64_t(g.n_row_blocks) * g.n_groups;
-  g.lds = sr_tile_lds_bytes(int(sizeof(T)), nf, R, depth, G, max_checks);
+  g.lds = sr_tile_lds_bytes(int(sizeof(T)), nf, R, depth, G, max_checks, W, weighted);
   return g;
 }
 
@@ -175,7 +179,8 @@ int run_batch(sr_ctx* ctx, const sr_dataset* ds, int opset_id, const sr_tree_bat
   const int tier = ctx->tiers[opset_id];
   const int depth = prog->max_depth > 0 ? prog->max_depth : 1;
   const int R = sr_rows_per_lane<T>(mode, tier, ctx->rows_override);
-  Grid g = make_grid<T>(n_eval, nt, R, int(ds->nf), depth, 0, ctx->tree_group);
+  const int W = sr_waves_per_block(int(sizeof(T)), mode, tier, R, ctx->waves_override);
+  Grid g = make_grid<T>(n_eval, nt, R, W, int(ds->nf), depth, 0, ds->w != nullptr, ctx->tree_group);
   if (g.lds > kLdsMax)
     return set_error(SR_ERR_TOO_DEEP, "the row tile (" + std::to_string(ds->nf) + " features, " +
                                           std::to_string(depth) + " stack slots) needs " + std::to_string(g.lds) +
@@ -256,7 +261,7 @@ int run_batch(sr_ctx* ctx, const sr_dataset* ds, int opset_id, const sr_tree_bat
   a.scale = 1.0;
   if (g.n_blocks > 0x7fffffff) return set_error(SR_ERR_INVALID_ARG, "grid too large");
   SR_HIP_CHECK(hipEventRecord(ctx->ev_k0, s));
-  SR_HIP_CHECK(sr_launch_eval<T>(a, mode, gather, tier, ctx->rows_override, int(g.n_blocks), s));
+  SR_HIP_CHECK(sr_launch_eval<T>(a, mode, gather, tier, ctx->rows_override, g.W, int(g.n_blocks), s));
   SR_HIP_CHECK(hipEventRecord(ctx->ev_k1, s));
   SR_HIP_CHECK(sr_launch_reduce(a.part_sum, a.part_flag, int(nt), g.n_row_blocks, perm_dev,
                                 ctx->static_bad.as<uint8_t>(), ctx->out_sum.as<double>(),
@@ -274,8 +279,8 @@ int run_exact(sr_ctx* ctx, const sr_dataset* ds, const SrProgramBatch<T>& prog, 
   const int64_t n_eval = gather ? n_idx : ds->n;
   hipStream_t s = ctx->stream;
   const int depth = prog.max_depth > 0 ? prog.max_depth : 1;
-  Grid g = make_grid<T>(n_eval, 1, sr_rows_per_lane<T>(SR_MODE_EXACT, SR_TIER_FULL, 0), int(ds->nf), depth,
-                        max_checks, 1);
+  Grid g = make_grid<T>(n_eval, 1, sr_rows_per_lane<T>(SR_MODE_EXACT, SR_TIER_FULL, 0), 4, int(ds->nf), depth,
+                        max_checks, ds->w != nullptr, 1);
   if (g.lds > kLdsMax) return set_error(SR_ERR_TOO_DEEP, "exact-sum pass needs more LDS than 160 KiB");
   std::vector<uint32_t> list32(static_cast<size_t>(n_list));
   for (int64_t i = 0; i < n_list; ++i) list32[size_t(i)] = uint32_t(list[i]);
@@ -312,7 +317,7 @@ int run_exact(sr_ctx* ctx, const sr_dataset* ds, const SrProgramBatch<T>& prog, 
   a.scale = sizeof(T) == 8 ? std::ldexp(1.0, -64) : 1.0;
   const int64_t blocks = int64_t(g.n_row_blocks) * n_list;
   if (blocks > 0x7fffffff) return set_error(SR_ERR_INVALID_ARG, "grid too large");
-  SR_HIP_CHECK(sr_launch_eval<T>(a, SR_MODE_EXACT, gather, SR_TIER_FULL, 0, int(blocks), s));
+  SR_HIP_CHECK(sr_launch_eval<T>(a, SR_MODE_EXACT, gather, SR_TIER_FULL, 0, 4, int(blocks), s));
   SR_HIP_CHECK(hipMemcpyAsync(host_sums, ctx->check_sums.p, size_t(n_list) * max_checks * sizeof(double),
                               hipMemcpyDeviceToHost, s));
   SR_HIP_CHECK(hipStreamSynchronize(s));
@@ -543,6 +548,7 @@ int sr_init(int device, sr_ctx** out) {
   if (hipGetDeviceProperties(&prop, device) == hipSuccess) ctx->cu_count = prop.multiProcessorCount;
   if (const char* v = std::getenv("SR_AMD_ROWS_PER_LANE")) ctx->rows_override = std::atoi(v);
   if (const char* v = std::getenv("SR_AMD_TREES_PER_BLOCK")) ctx->tree_group = std::atoi(v);
+  if (const char* v = std::getenv("SR_AMD_WAVES")) ctx->waves_override = std::atoi(v);
   if (const char* v = std::getenv("SR_AMD_NO_SORT")) ctx->cost_order = std::atoi(v) == 0;
   if (const char* v = std::getenv("SR_AMD_NO_HINT")) ctx->dead_hints = std::atoi(v) == 0;
   hipError_t e = hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking);

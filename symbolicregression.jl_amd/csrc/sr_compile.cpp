@@ -266,28 +266,37 @@ struct TreeCompiler {
 
   // Leaf as a LOAD (push = false; PUSH is patched in later) or as a binary operand.
   // is_operand: binary opcode base (variant FL/FR/CL/CR chosen from the leaf kind + side).
+  static constexpr uint32_t kNoSlot = 0xffffffffu;
+
   SrIns<T> leaf_ins(int i) {
     SrIns<T> in{};
+    in.cslot = kNoSlot;
     if (folded[i]) {
-      in.code = SR_OP_LOAD_CONST;
-      in.val = fold_val[i];
-      in.arg = SR_A_INDEX;
+      in.w0 = SR_OP_LOAD_CONST;
+      in.set_value(fold_val[i]);
     } else if (t.constant[i]) {
-      in.code = SR_OP_LOAD_CONST;
-      in.val = t.val[i];
-      in.arg = with_const_index ? uint32_t(const_slot[i]) : SR_A_INDEX;
+      in.w0 = SR_OP_LOAD_CONST;
+      in.set_value(t.val[i]);
+      if (with_const_index) in.cslot = uint32_t(const_slot[i]);
     } else {
-      in.code = SR_OP_LOAD_FEAT;
-      in.arg = uint32_t(t.feature[i]) - 1u;
-      in.val = T(0);
+      in.w0 = SR_OP_LOAD_FEAT | ((uint32_t(t.feature[i]) - 1u) << SR_W_OPND_SHIFT);
     }
     return in;
   }
+  static bool commutes(uint32_t bop) { return bop == SR_B_ADD || bop == SR_B_MUL; }
   SrIns<T> operand_ins(int i, uint32_t bop, bool left) {
     SrIns<T> in = leaf_ins(i);
-    const bool is_const = in.code == SR_OP_LOAD_CONST;
+    const bool is_const = in.opcode() == SR_OP_LOAD_CONST;
+    if (commutes(bop)) left = false;  // IEEE + and * commute: one variant per operand kind
     const uint32_t v = is_const ? (left ? SR_V_CL : SR_V_CR) : (left ? SR_V_FL : SR_V_FR);
-    in.code = SR_BIN_OPC(bop, v);
+    in.w0 = (in.w0 & ~SR_W_OPC) | SR_BIN_OPC(bop, v);
+    return in;
+  }
+  SrIns<T> stack_ins(uint32_t bop, bool left, int slot) {
+    SrIns<T> in{};
+    in.cslot = kNoSlot;
+    if (commutes(bop)) left = false;
+    in.w0 = SR_BIN_OPC(bop, left ? SR_V_SL : SR_V_SR) | (uint32_t(slot) << SR_W_OPND_SHIFT);
     return in;
   }
 
@@ -297,13 +306,18 @@ struct TreeCompiler {
       static_array_check(folded[i] ? fold_val[i] : t.val[i]);
       return;
     }
-    code.back().arg |= SR_A_CHECK;
+    code.back().w0 |= SR_W_CHECK;
     ++n_checks;
   }
 
-  static void mark_push(SrIns<T>& in) {
-    // the first instruction of every subtree's code is a leaf LOAD
-    in.code = (in.code & ~0xffu) | ((in.code & 0xffu) + 2u);
+  // The first instruction of every subtree's code is a leaf LOAD: it first stores the old top of
+  // stack to `slot`.
+  void mark_push(SrIns<T>& in, int slot) {
+    if (slot >= int(SR_MAX_STACK_SLOTS)) {
+      fail(SR_ERR_TOO_DEEP, "tree needs more operand-stack slots than the encoding holds");
+      return;
+    }
+    in.w0 |= uint32_t(slot + 1) << SR_W_PUSH_SHIFT;
   }
 
   void emit(int i) {
@@ -317,8 +331,9 @@ struct TreeCompiler {
     if (d == 1) {
       emit(t.l[i]);
       SrIns<T> in{};
-      in.code = SR_OP_UNARY0 + unary_id(i);
-      if (infsub[i]) in.arg = SR_A_INFSUB;  // fused unary: non-finite input -> +Inf
+      in.cslot = kNoSlot;
+      in.w0 = SR_OP_UNARY0 + unary_id(i);
+      if (infsub[i]) in.w0 |= SR_W_INFSUB;  // fused unary: non-finite input -> +Inf
       code.push_back(in);
       emit_check(i);
       return;
@@ -332,28 +347,17 @@ struct TreeCompiler {
     } else if (effleaf(a)) {  // op(operand = left leaf, tos = right)
       emit(b);
       code.push_back(operand_ins(a, bop, true));
-    } else if (need[a] >= need[b]) {  // left first, pushed; right in tos
-      emit(a);
+    } else {  // the operand needing more slots first, pushed to slot `depth`; the other in tos
+      const bool left_first = need[a] >= need[b];
+      emit(left_first ? a : b);
       const size_t start = code.size();
+      const int slot = depth;
       ++depth;
       if (depth > max_depth) max_depth = depth;
-      emit(b);
-      mark_push(code[start]);
+      emit(left_first ? b : a);
+      mark_push(code[start], slot);
       --depth;
-      SrIns<T> in{};
-      in.code = SR_BIN_OPC(bop, SR_V_SL);
-      code.push_back(in);
-    } else {  // right first, pushed; left in tos
-      emit(b);
-      const size_t start = code.size();
-      ++depth;
-      if (depth > max_depth) max_depth = depth;
-      emit(a);
-      mark_push(code[start]);
-      --depth;
-      SrIns<T> in{};
-      in.code = SR_BIN_OPC(bop, SR_V_SR);
-      code.push_back(in);
+      code.push_back(stack_ins(bop, left_first, slot));
     }
     emit_check(i);
   }
@@ -399,16 +403,17 @@ struct TreeCompiler {
 
 }  // namespace
 
-uint32_t sr_instruction_cost(uint32_t code, uint32_t arg) {
-  uint32_t c = 6;  // dispatch + operand fetch
-  if (arg & SR_A_CHECK) c += 3;
-  if (arg & SR_A_INFSUB) c += 2;
+uint32_t sr_instruction_cost(uint32_t w0) {
+  const uint32_t code = w0 & SR_W_OPC;
+  uint32_t c = 6;  // dispatch + operand fetch + validity tracking
+  if (w0 & SR_W_INFSUB) c += 2;
+  if (w0 & SR_W_PUSH_MASK) c += 2;
   if (code >= SR_OP_BINARY0) {
     const uint32_t b = (code - SR_OP_BINARY0) / 6u + 1u;
     if (b == SR_B_DIV) c += 10;
     else if (b == SR_B_ADD || b == SR_B_SUB || b == SR_B_MUL) c += 1;
     else c += 20;
-  } else if (code > SR_OP_UNARY0) {
+  } else if (code >= SR_OP_UNARY0 + 1u) {
     const uint32_t u = code - SR_OP_UNARY0;
     switch (u) {
       case SR_U_NEG: case SR_U_SQUARE: case SR_U_CUBE: case SR_U_ABS: c += 2; break;
@@ -476,10 +481,7 @@ int sr_compile_batch(const sr_tree_batch& trees, const SrOpset& ops, int64_t n_r
         continue;
       }
       uint32_t cost = 0;
-      for (auto& in : tc.code) {
-        in.arg |= sr_operand_tag(in.code);
-        cost += sr_instruction_cost(in.code, in.arg);
-      }
+      for (const auto& in : tc.code) cost += sr_instruction_cost(in.w0);
       PerTree& p = per[k];
       p.cost = cost;
       p.code.swap(tc.code);

@@ -32,8 +32,8 @@ struct SrEvalArgs {
   T tbig;                      // |v| >= tbig may overflow the array-sum check
   int loss_kind;
   // outputs
-  double* part_sum;            // [n_trees][n_row_blocks], per launch position
-  uint32_t* part_flag;         // [n_trees][n_row_blocks], per launch position
+  double* part_sum;            // [n_row_blocks][n_trees], per launch position
+  uint32_t* part_flag;         // [n_row_blocks][n_trees], per launch position
   T* pred;                     // PRED: [n_trees][pred_ld]
   int64_t pred_ld;
   // EXACT mode (perm = listed trees; check_sums row = position in the list)
@@ -42,18 +42,20 @@ struct SrEvalArgs {
   double scale;
 };
 
-template <typename T, int R, int MODE, bool GATHER, int TIER>
+template <typename T, int R, int MODE, bool GATHER, int TIER, int W = 4, int LK = -1>
 hipError_t sr_launch_tile(const SrEvalArgs<T>& a, int n_blocks, hipStream_t s);
-// LDS bytes one workgroup of the tile kernel needs.
+// LDS bytes one workgroup (W waves) of the tile kernel needs.
 size_t sr_tile_lds_bytes(int elem_size, int nf, int rows_per_lane, int stack_depth, int trees_per_block,
-                         int max_checks);
+                         int max_checks, int waves, bool weighted);
+// Waves per workgroup the dispatcher uses for (mode, tier, rows per lane); `requested` overrides.
+int sr_waves_per_block(int elem_size, int mode, int tier, int rows_per_lane, int requested);
 // Rows per lane the dispatcher uses for (mode, tier); `requested` 4 selects the f32 BASIC tuning kernel.
 template <typename T>
 int sr_rows_per_lane(int mode, int tier, int requested);
 // Runtime dispatch over the instantiated kernels.
 template <typename T>
-hipError_t sr_launch_eval(const SrEvalArgs<T>& a, int mode, bool gather, int tier, int rows_per_lane, int n_blocks,
-                          hipStream_t s);
+hipError_t sr_launch_eval(const SrEvalArgs<T>& a, int mode, bool gather, int tier, int rows_per_lane, int waves,
+                          int n_blocks, hipStream_t s);
 hipError_t sr_launch_reduce(const double* part_sum, const uint32_t* part_flag, int n_trees, int n_row_blocks,
                             const uint32_t* perm, const uint8_t* static_bad, double* out_sum, uint32_t* out_flag,
                             hipStream_t s);

@@ -49,52 +49,63 @@ enum SrLossKind : int32_t {
 };
 
 // ---------------------------------------------------------------------------------------
-// Program instruction (one per evaluated node; 16 bytes for f32 and f64).
-//   code          : combined opcode (what to do + where the operand comes from), < 256:
-//       SR_OP_LOAD_FEAT / _CONST [/ _PUSH]           top-of-stack <- leaf (push old tos first)
+// Program instruction: one per evaluated node (a leaf that is a binary node's operand is folded into
+// that node's instruction), 16 bytes for f32 and f64 alike.
+//   w0 bits  0-7  : opcode
+//       SR_OP_LOAD_FEAT  tos <- X[f]          SR_OP_LOAD_CONST  tos <- c
+//         (push field != 0: the old tos is first stored to stack slot push-1)
 //       SR_OP_UNARY0 + u                               tos <- op_u(tos)
 //       SR_OP_BINARY0 + 6*(b-1) + variant              tos <- op_b(.,.) with operand variant:
-//           SR_V_SL: op(pop, tos)   SR_V_SR: op(tos, pop)
+//           SR_V_SL: op(S[k], tos)  SR_V_SR: op(tos, S[k])   (S[k] = stack slot k, popped)
 //           SR_V_FL: op(X[f], tos)  SR_V_FR: op(tos, X[f])
 //           SR_V_CL: op(c, tos)     SR_V_CR: op(tos, c)
-//   arg bits 0-27 : 0-based feature index (FEAT operands) / constant slot (gradient programs)
-//   arg bit  28   : INFSUB  (unary) tos <- isfinite(tos) ? op_u(tos) : +Inf — DynamicExpressions'
-//                   fused unary kernels (deg1_l2_ll0_lr0 / deg1_l1_ll0): a non-finite input of the
-//                   fused inner operation gives +Inf
-//   arg bit  29   : OPSTK   the operand is popped from the stack (SL, SR)
-//   arg bit  30   : OPFEAT  the operand is a feature row (LOAD_FEAT[_PUSH], FL, FR)
-//   arg bit  31   : CHECK   this node's output array is validity-checked (DE early exit)
-//   val           : constant (CONST operands)
-// The opcode has a word of its own so the interpreter's dispatch reads it without masking.
+//         + and * only ever use the R variants (the compiler canonicalises: IEEE + and * commute)
+//   w0 bit   8    : CHECK   this node's output array is validity-checked (DE early exit)
+//   w0 bit   9    : INFSUB  (unary) tos <- isfinite(tos) ? op_u(tos) : +Inf — DynamicExpressions'
+//                   fused unary kernels (deg1_l2_ll0_lr0 / deg1_l1_ll0)
+//   w0 bits 10-15 : push slot + 1 (LOAD only; 0 = no push)
+//   w0 bits 16-31 : operand index: 0-based feature f (F variants, LOAD_FEAT) or stack slot k
+//                   (S variants); stack depths are static, so the compiler assigns the slots
+//   c0 (, c1)     : constant bits (C variants, LOAD_CONST): f32 in c0, f64 in c0 | c1 << 32
+//   cslot         : pre-order constant index of a constant leaf (gradient programs), else ~0
 // ---------------------------------------------------------------------------------------
 enum : uint32_t {
-  SR_OP_LOAD_FEAT = 0u, SR_OP_LOAD_CONST = 1u, SR_OP_LOAD_FEAT_PUSH = 2u, SR_OP_LOAD_CONST_PUSH = 3u,
-  SR_OP_UNARY0 = 3u,    // opcode = SR_OP_UNARY0 + SrUnaryOp (1..)
+  SR_OP_LOAD_FEAT = 0u, SR_OP_LOAD_CONST = 1u,
+  SR_OP_UNARY0 = 2u,    // opcode = SR_OP_UNARY0 + SrUnaryOp (1..)
   SR_OP_BINARY0 = 64u,  // opcode = SR_OP_BINARY0 + 6*(SrBinaryOp-1) + variant
   SR_V_SL = 0u, SR_V_SR = 1u, SR_V_FL = 2u, SR_V_FR = 3u, SR_V_CL = 4u, SR_V_CR = 5u,
-  SR_A_CHECK = 1u << 31, SR_A_OPFEAT = 1u << 30, SR_A_OPSTK = 1u << 29, SR_A_INFSUB = 1u << 28,
-  SR_A_INDEX = (1u << 28) - 1u,
+  SR_W_OPC = 0xffu, SR_W_CHECK = 1u << 8, SR_W_INFSUB = 1u << 9,
+  SR_W_PUSH_SHIFT = 10u, SR_W_PUSH_MASK = 0x3fu << 10, SR_W_OPND_SHIFT = 16u,
+  SR_MAX_STACK_SLOTS = 62u,
 };
 static_assert(SR_OP_UNARY0 + SR_U_COUNT <= SR_OP_BINARY0, "unary opcode range overlaps the binary range");
 static_assert(SR_OP_BINARY0 + 6 * SR_B_COUNT <= 256, "binary opcode range exceeds 8 bits");
-
-// Operand-source tag of an opcode (SR_A_OPFEAT / SR_A_OPSTK / 0).
-inline uint32_t sr_operand_tag(uint32_t op) {
-  if (op == SR_OP_LOAD_FEAT || op == SR_OP_LOAD_FEAT_PUSH) return SR_A_OPFEAT;
-  if (op >= SR_OP_BINARY0) {
-    const uint32_t v = (op - SR_OP_BINARY0) % 6u;
-    if (v == SR_V_FL || v == SR_V_FR) return SR_A_OPFEAT;
-    if (v == SR_V_SL || v == SR_V_SR) return SR_A_OPSTK;
-  }
-  return 0u;
-}
 #define SR_BIN_OPC(b, v) (SR_OP_BINARY0 + 6u * ((b) - 1u) + (v))
 
 template <typename T>
 struct alignas(16) SrIns {
-  uint32_t code;
-  uint32_t arg;
-  T val;
+  uint32_t w0;
+  uint32_t c0, c1;
+  uint32_t cslot;
+  SR_HD inline uint32_t opcode() const { return w0 & SR_W_OPC; }
+  SR_HD inline uint32_t operand() const { return w0 >> SR_W_OPND_SHIFT; }
+  SR_HD inline T value() const {
+    if constexpr (sizeof(T) == 4) {
+      return __builtin_bit_cast(T, c0);
+    } else {
+      return __builtin_bit_cast(T, uint64_t(c0) | (uint64_t(c1) << 32));
+    }
+  }
+  SR_HD inline void set_value(T v) {
+    if constexpr (sizeof(T) == 4) {
+      c0 = __builtin_bit_cast(uint32_t, v);
+      c1 = 0u;
+    } else {
+      const uint64_t b = __builtin_bit_cast(uint64_t, v);
+      c0 = uint32_t(b);
+      c1 = uint32_t(b >> 32);
+    }
+  }
 };
 static_assert(sizeof(SrIns<float>) == 16, "f32 instruction must be 16 bytes");
 static_assert(sizeof(SrIns<double>) == 16, "f64 instruction must be 16 bytes");

@@ -10,16 +10,17 @@
 //   * lane `l` owns R rows of the tile: chunk c (16 bytes = C values) of lane l is tile row
 //     c*64*C + l*C + j, so every LDS read of a feature / stack slot is a conflict-free ds_read_b128
 //     and the LDS image of a tile is a plain copy of the global rows;
-//   * each wave interprets its tree's program: the program sits in VGPRs (one 16-byte instruction
-//     per lane, 64-instruction windows) and each step reads its words with v_readlane; one flat
-//     `switch` over the opcode dispatches to straight-line VALU bodies on the R-row top of stack
-//     (VGPRs); deeper stack slots live in a per-wave LDS stack sized to the batch's depth;
-//   * DynamicExpressions' early-exit checks: a CHECK instruction tests max|v| >= tbig with one
-//     integer max per lane and one ballot; only then is non-finiteness tested (dead tree: the wave
-//     stops and the whole workgroup skips the tree in later tiles);
-//   * per-tree loss: T per lane -> cross-lane wave sum -> f64 accumulator in LDS (one wave per
-//     (tree, tile), tiles in order: deterministic) -> one partial per (tree, row block) -> fixed-
-//     order reduce kernel (bit-reproducible).
+//   * each wave interprets its trees' programs: the program sits in VGPRs (one 16-byte instruction
+//     per lane, 64-instruction windows, the next window in flight while one runs) and each step
+//     reads its opcode word with v_readlane; one flat `switch` over the opcode dispatches to
+//     straight-line VALU bodies on the R-row top of stack (VGPRs); operand stack slots (assigned
+//     statically by the compiler) live in a per-wave LDS area;
+//   * DynamicExpressions' validity checks: BASIC tier — every operator output updates a running
+//     max |v| (v_max3 with abs modifiers), decided once per tree and tile (Inf -> incomplete,
+//     >= tbig -> exact-sum path, NaN reaches the root); FULL tier — per CHECK node, integer-max
+//     test + ballot, early exit on a non-finite value;
+//   * per-tree loss: T per lane -> DPP wave sum -> f64 accumulator in the owning lane (tiles in
+//     order: deterministic) -> one partial per (row block, tree) -> fixed-order reduce kernel.
 // Compile with -mllvm -structurizecfg-skip-uniform-regions=true: all branches here are
 // wave-uniform, and without the flag LLVM's structurizer turns the opcode switch into a chain of
 // exec-mask "flow" blocks with copies of the stack registers at every join.
@@ -29,11 +30,12 @@
 #include "sr_eval.h"
 #include "sr_ops.h"
 
-#define SR_WAVES 4
-#define SR_BLOCK (SR_WAVES * 64)
-#ifndef SR_MIN_WAVES
-#define SR_MIN_WAVES
-#endif
+// Waves per workgroup W is a template parameter (4 by default); the minimum resident waves per
+// SIMD the register allocator must allow is derived from it (SrMinWaves).
+template <int W>
+struct SrMinWaves {
+  static constexpr int value = W >= 16 ? 8 : (W >= 8 ? 6 : 1);
+};
 
 // 16-byte chunks of C values.
 template <typename T>
@@ -149,100 +151,130 @@ struct SrMaxAbs<double> {
   }
 };
 
+
+// The constant of instruction k of a window (uniform): c0 (f32) or c0 | c1 << 32 (f64).
+template <typename T>
+__device__ __forceinline__ T sr_lane_value(uint32_t wc0, uint32_t wc1, uint32_t k) {
+  if constexpr (sizeof(T) == 4) {
+    return __builtin_bit_cast(T, __builtin_amdgcn_readlane(int(wc0), int(k)));
+  } else {
+    // readlane returns int: widen through uint32_t (no sign extension into the high word)
+    return __builtin_bit_cast(T, uint64_t(uint32_t(__builtin_amdgcn_readlane(int(wc0), int(k)))) |
+                                     (uint64_t(uint32_t(__builtin_amdgcn_readlane(int(wc1), int(k)))) << 32));
+  }
+}
+
 // ------------------------------------------------------------------ dispatch cases
-// Operators of the BASIC tier are compiled into every kernel; the FULL tier adds the rest of the
-// catalog (more registers: transcendental constants are hoisted out of the loop by LLVM).
 #define SR_EACH(EXPR)                             \
   _Pragma("unroll") for (int r = 0; r < R; ++r) { \
     const T x = tos[r];                           \
     tos[r] = (EXPR);                              \
   }
-#define SR_UCASE_GEN(ID, ENABLED)                                              \
-  case SR_OP_UNARY0 + ID: {                                                    \
-    if (ENABLED) {                                                             \
-      if (arg & SR_A_INFSUB) {                                                 \
-        SR_EACH(sr_isfinite(x) ? sr_unary<T>(ID, x) : sr_inf<T>());            \
-      } else {                                                                 \
-        SR_EACH(sr_unary<T>(ID, x));                                           \
-      }                                                                        \
-    }                                                                          \
-    break;                                                                     \
-  }
-#define SR_UCASE(ID) SR_UCASE_GEN(ID, true)
-#define SR_UCASE_FULL(ID) SR_UCASE_GEN(ID, TIER == SR_TIER_FULL)
 #define SR_BIN_EACH(AEXPR, BEXPR, ID)             \
   _Pragma("unroll") for (int r = 0; r < R; ++r) { \
     const T aa = (AEXPR);                         \
     const T bb = (BEXPR);                         \
     tos[r] = sr_binary<T>(ID, aa, bb);            \
   }
-#define SR_BCASE_GEN(ID, ENABLED)                 \
-  case SR_BIN_OPC(ID, SR_V_SL): {                 \
-    if (ENABLED) {                                \
-      --sp;                                       \
-      T o[R];                                     \
-      L::load(stk_lane + sp * ROWS, o);           \
-      SR_BIN_EACH(o[r], tos[r], ID);              \
-    }                                             \
-    break;                                        \
-  }                                               \
-  case SR_BIN_OPC(ID, SR_V_SR): {                 \
-    if (ENABLED) {                                \
-      --sp;                                       \
-      T o[R];                                     \
-      L::load(stk_lane + sp * ROWS, o);           \
-      SR_BIN_EACH(tos[r], o[r], ID);              \
-    }                                             \
-    break;                                        \
-  }                                               \
-  case SR_BIN_OPC(ID, SR_V_FL): {                 \
-    if (ENABLED) {                                \
-      T o[R];                                     \
-      L::load(x_lane + fidx * ROWS, o);           \
-      SR_BIN_EACH(o[r], tos[r], ID);              \
-    }                                             \
-    break;                                        \
-  }                                               \
-  case SR_BIN_OPC(ID, SR_V_FR): {                 \
-    if (ENABLED) {                                \
-      T o[R];                                     \
-      L::load(x_lane + fidx * ROWS, o);           \
-      SR_BIN_EACH(tos[r], o[r], ID);              \
-    }                                             \
-    break;                                        \
-  }                                               \
-  case SR_BIN_OPC(ID, SR_V_CL): {                 \
-    if (ENABLED) {                                \
-      const T cv = cval;                          \
-      SR_BIN_EACH(cv, tos[r], ID);                \
-    }                                             \
-    break;                                        \
-  }                                               \
-  case SR_BIN_OPC(ID, SR_V_CR): {                 \
-    if (ENABLED) {                                \
-      const T cv = cval;                          \
-      SR_BIN_EACH(tos[r], cv, ID);                \
-    }                                             \
-    break;                                        \
+// FAST_CHECK: every operator output joins the running max |v| of the tree
+#define SR_TRACK()                                                        \
+  if constexpr (FAST_CHECK) {                                             \
+    _Pragma("unroll") for (int r = 0; r < R; r += 4) {                    \
+      mrun = SrMaxAbs<T>::step(mrun, tos[r], tos[r + 1]);                 \
+      if (r + 3 < R) mrun1 = SrMaxAbs<T>::step(mrun1, tos[r + 2], tos[r + 3]); \
+    }                                                                     \
   }
-#define SR_BCASE(ID) SR_BCASE_GEN(ID, true)
-#define SR_BCASE_FULL(ID) SR_BCASE_GEN(ID, TIER == SR_TIER_FULL)
+#define SR_UCASE_GEN(ID, ENABLED)                                   \
+  case SR_OP_UNARY0 + ID: {                                         \
+    if (ENABLED) {                                                  \
+      if (w0 & SR_W_INFSUB) {                                       \
+        SR_EACH(sr_isfinite(x) ? sr_unary<T>(ID, x) : sr_inf<T>()); \
+      } else {                                                      \
+        SR_EACH(sr_unary<T>(ID, x));                                \
+      }                                                             \
+      SR_TRACK();                                                   \
+    }                                                               \
+    break;                                                          \
+  }
+#define SR_UCASE(ID) SR_UCASE_GEN(ID, true)
+#define SR_UCASE_FULL(ID) SR_UCASE_GEN(ID, TIER == SR_TIER_FULL)
+// operand addresses: stack slot / feature row in w0's operand field; constants from the c words
+#define SR_OPND_STK() (stk_lane + (w0 >> SR_W_OPND_SHIFT) * ROWS)
+#define SR_OPND_X() (x_lane + (w0 >> SR_W_OPND_SHIFT) * ROWS)
+#define SR_BCASE_R(ID, ENABLED)        \
+  case SR_BIN_OPC(ID, SR_V_SR): {      \
+    if (ENABLED) {                     \
+      T o[R];                          \
+      L::load(SR_OPND_STK(), o);       \
+      SR_BIN_EACH(tos[r], o[r], ID);   \
+      SR_TRACK();                      \
+    }                                  \
+    break;                             \
+  }                                    \
+  case SR_BIN_OPC(ID, SR_V_FR): {      \
+    if (ENABLED) {                     \
+      T o[R];                          \
+      L::load(SR_OPND_X(), o);         \
+      SR_BIN_EACH(tos[r], o[r], ID);   \
+      SR_TRACK();                      \
+    }                                  \
+    break;                             \
+  }                                    \
+  case SR_BIN_OPC(ID, SR_V_CR): {      \
+    if (ENABLED) {                     \
+      const T cv = SR_CVAL();          \
+      SR_BIN_EACH(tos[r], cv, ID);     \
+      SR_TRACK();                      \
+    }                                  \
+    break;                             \
+  }
+#define SR_BCASE_L(ID, ENABLED)        \
+  case SR_BIN_OPC(ID, SR_V_SL): {      \
+    if (ENABLED) {                     \
+      T o[R];                          \
+      L::load(SR_OPND_STK(), o);       \
+      SR_BIN_EACH(o[r], tos[r], ID);   \
+      SR_TRACK();                      \
+    }                                  \
+    break;                             \
+  }                                    \
+  case SR_BIN_OPC(ID, SR_V_FL): {      \
+    if (ENABLED) {                     \
+      T o[R];                          \
+      L::load(SR_OPND_X(), o);         \
+      SR_BIN_EACH(o[r], tos[r], ID);   \
+      SR_TRACK();                      \
+    }                                  \
+    break;                             \
+  }                                    \
+  case SR_BIN_OPC(ID, SR_V_CL): {      \
+    if (ENABLED) {                     \
+      const T cv = SR_CVAL();          \
+      SR_BIN_EACH(cv, tos[r], ID);     \
+      SR_TRACK();                      \
+    }                                  \
+    break;                             \
+  }
+// + and * commute: the compiler emits only their R variants
+#define SR_BCASE_COMM(ID) SR_BCASE_R(ID, true)
+#define SR_BCASE(ID) SR_BCASE_R(ID, true) SR_BCASE_L(ID, true)
+#define SR_BCASE_FULL(ID) SR_BCASE_R(ID, TIER == SR_TIER_FULL) SR_BCASE_L(ID, TIER == SR_TIER_FULL)
 
-// LDS carve, in bytes, 16-aligned: X tile [nf][ROWS] T | y [ROWS] | w [ROWS] | stack
-// [SR_WAVES][depth][ROWS] T | xacc [G][max_checks] f64 (EXACT mode)
+// LDS carve, in bytes, 16-aligned: X tile [nf][ROWS] T | y [ROWS] | w [ROWS] (weighted) | stack
+// [W][depth][ROWS] T | xacc [G][max_checks] f64 (EXACT mode)
 template <typename T>
 struct SrLdsPlan {
   size_t x, y, w, stk, xacc, total;
-  __host__ __device__ SrLdsPlan(int nf, int rows, int depth, int G, int max_checks) {
+  __host__ __device__ SrLdsPlan(int nf, int rows, int depth, int G, int max_checks, int waves, bool weighted) {
     size_t o = 0;
     x = o;
     o += size_t(nf) * rows * sizeof(T);
     y = o;
     o += size_t(rows) * sizeof(T);
     w = o;
-    o += size_t(rows) * sizeof(T);
+    if (weighted) o += size_t(rows) * sizeof(T);
     stk = o;
-    o += size_t(SR_WAVES) * size_t(depth) * rows * sizeof(T);
+    o += size_t(waves) * size_t(depth) * rows * sizeof(T);
     xacc = o;
     o += size_t(G) * size_t(max_checks) * 8;
     total = o;
@@ -258,26 +290,28 @@ __device__ __forceinline__ uint4 sr_load_window(const void* code, uint32_t at) {
 //
 // Tree ownership: the block's G trees are positions tree0 .. tree0+G-1 of the launch order
 // (a.perm maps a position to the caller's tree index: the host orders trees by estimated cost so
-// the 4 waves of a block get equal work).  Wave w owns positions tree0 + w + 4j ("slot" j, j < 64);
+// the waves of a block get equal work).  Wave w owns positions tree0 + w + W*j ("slot" j, j < 64);
 // everything per tree lives in that wave: program bounds in lane j's VGPRs, the loss accumulator in
-// lane j, the non-finite / suspicious bits in scalar masks.  While one tree runs, the first program
-// window of the wave's next tree is already in flight.
-template <typename T, int R, int MODE, bool GATHER, int TIER>
-__global__ void __launch_bounds__(SR_BLOCK SR_MIN_WAVES) sr_tile_kernel(const SrEvalArgs<T> a) {
+// lane j, the non-finite / suspicious bits in scalar masks.
+// LK: elementwise loss fixed at compile time (SR_LOSS_L2 / SR_LOSS_L1), or -1 = a.loss_kind.
+template <typename T, int R, int MODE, bool GATHER, int TIER, int W, int LK>
+__global__ void __launch_bounds__(W * 64, SrMinWaves<W>::value) sr_tile_kernel(const SrEvalArgs<T> a) {
+  constexpr int SR_WAVES = W;
+  constexpr int SR_BLOCK = W * 64;
   using L = SrLane<T, R>;
   constexpr int C = L::C;
   constexpr int ROWS = 64 * R;
-  // Deferred validity checks (BASIC tier): no per-check ballot or early exit; the
-  // tree's running max |checked value| and the root's NaN test decide at the end of the program.
-  constexpr bool FAST_CHECK = (TIER == SR_TIER_BASIC) && (MODE != SR_MODE_EXACT);
-  static_assert(R % 2 == 0, "rows per lane must be even");
+  // Deferred validity checks (BASIC tier loss kernels): no per-node branch, ballot or
+  // early exit; the tree's running max |v| and the root's NaN test decide at the end of the program.
+  constexpr bool FAST_CHECK = (TIER == SR_TIER_BASIC) && (MODE == SR_MODE_LOSS);
+  static_assert(R % 4 == 0 || R == 2, "rows per lane: 2 or a multiple of 4");
   extern __shared__ __attribute__((aligned(16))) unsigned char sr_smem[];
   const int tid = threadIdx.x;
   const int wave = tid >> 6;
   const int lane = tid & 63;
   const int G = a.trees_per_block;
   const int MC = (MODE == SR_MODE_EXACT) ? a.max_checks : 0;
-  const SrLdsPlan<T> plan(a.nf, ROWS, a.stack_depth, G, MC);
+  const SrLdsPlan<T> plan(a.nf, ROWS, a.stack_depth, G, MC, W, a.w != nullptr);
   T* xs = reinterpret_cast<T*>(sr_smem + plan.x);
   T* ys = reinterpret_cast<T*>(sr_smem + plan.y);
   T* wsv = reinterpret_cast<T*>(sr_smem + plan.w);
@@ -295,6 +329,7 @@ __global__ void __launch_bounds__(SR_BLOCK SR_MIN_WAVES) sr_tile_kernel(const Sr
   if (gcount > G) gcount = G;
   const bool weighted = a.w != nullptr;
   const uint32_t thr = SrBits<T>::mag(a.tbig);
+  const int lk = LK >= 0 ? LK : a.loss_kind;
 
   // this wave's slots
   const int S = gcount > wave ? (gcount - wave + SR_WAVES - 1) / SR_WAVES : 0;
@@ -356,102 +391,77 @@ __global__ void __launch_bounds__(SR_BLOCK SR_MIN_WAVES) sr_tile_kernel(const Sr
       if (lane < S) hintv = __hip_atomic_load(a.hint + my_pos, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
     uint64_t todo = (MODE == SR_MODE_LOSS) ? (live & ~dmask) : live;
-    if (todo) {
-      // Window stream: the 64-instruction program windows of this tile's trees, in order.  The
-      // next window (of this tree, or the first one of the next tree) is in flight while the current
-      // one runs; the running window is a register copy, so the interpreter loop never waits on it.
-      int nj = __builtin_ctzll(todo);
-      todo &= todo - 1u;
-      uint32_t nb = uint32_t(__builtin_amdgcn_readlane(int(my_pb), nj));
-      uint32_t ne = uint32_t(__builtin_amdgcn_readlane(int(my_pe), nj));
-      uint4 nx = make_uint4(0u, 0u, 0u, 0u);
-      if (nb + lane < ne) nx = sr_load_window(a.code, nb + lane);
-      int j = -1;
-      uint32_t tpe = 0u;
-      T tos[R];
+    if (!todo) continue;
+    // Window stream: the 64-instruction program windows of this tile's trees, in order.  The next
+    // window (of this tree, or the first one of the next tree) is in flight while the current one
+    // runs; the running window is a register copy, so the interpreter loop never waits on it.
+    int nj = __builtin_ctzll(todo);
+    todo &= todo - 1u;
+    uint32_t nb = uint32_t(__builtin_amdgcn_readlane(int(my_pb), nj));
+    uint32_t ne = uint32_t(__builtin_amdgcn_readlane(int(my_pe), nj));
+    uint4 nx = make_uint4(0u, 0u, 0u, 0u);
+    if (nb + lane < ne) nx = sr_load_window(a.code, nb + lane);
+    int j = -1;
+    uint32_t tpe = 0u;
+    T tos[R];
 #pragma unroll
-      for (int r = 0; r < R; ++r) tos[r] = T(0);
-      int sp = 0;
-      bool dead = false;
-      bool susp_any = false;
-      int check_k = 0;
-      T mrun = T(0), mrun1 = T(0);  // FAST_CHECK: max |checked value| over this lane's rows (2 chains)
-      bool more = true;
-      while (more) {
-        const uint4 cw = nx;
-        const uint32_t base = nb;
-        if (nj != j) {  // a new tree starts
-          j = nj;
-          tpe = ne;
-#pragma unroll
-          for (int r = 0; r < R; ++r) tos[r] = T(0);
-          sp = 0;
-          dead = false;
-          susp_any = false;
-          check_k = 0;
-          mrun = T(0);
-          mrun1 = T(0);
-        }
-        if (base + 64u < tpe) {
-          nb = base + 64u;
-        } else if (todo) {
-          nj = __builtin_ctzll(todo);
-          todo &= todo - 1u;
-          nb = uint32_t(__builtin_amdgcn_readlane(int(my_pb), nj));
-          ne = uint32_t(__builtin_amdgcn_readlane(int(my_pe), nj));
-        } else {
-          more = false;
-        }
-        if (more && nb + lane < ne) nx = sr_load_window(a.code, nb + lane);
-        const int g = wave + SR_WAVES * j;
+    for (int r = 0; r < R; ++r) tos[r] = T(0);
+    bool dead = false;
+    bool susp_any = false;
+    int check_k = 0;
+    T mrun = T(0), mrun1 = T(0);  // FAST_CHECK: running max |v| over this lane's rows (2 chains)
+    bool more = true;
+    while (more) {
+      const uint4 cw = nx;
+      const uint32_t base = nb;
+      if (nj != j) {  // a new tree starts (its first instruction is a LOAD: tos needs no reset)
+        j = nj;
+        tpe = ne;
+        dead = false;
+        susp_any = false;
+        check_k = 0;
+        mrun = T(0);
+        mrun1 = T(0);
+      }
+      if (base + 64u < tpe) {
+        nb = base + 64u;
+      } else if (todo) {
+        nj = __builtin_ctzll(todo);
+        todo &= todo - 1u;
+        nb = uint32_t(__builtin_amdgcn_readlane(int(my_pb), nj));
+        ne = uint32_t(__builtin_amdgcn_readlane(int(my_pe), nj));
+      } else {
+        more = false;
+      }
+      if (more && nb + lane < ne) nx = sr_load_window(a.code, nb + lane);
+      const int g = wave + SR_WAVES * j;
 
-      // The program sits in VGPRs, one 16-byte instruction per lane; each step reads its words with
-      // v_readlane.
       if (!dead) {
-        const uint32_t wc = cw.x, wa = cw.y, wl = cw.z, wh = cw.w;
+        const uint32_t wop = cw.x, wc0 = cw.y, wc1 = cw.z;
         const uint32_t n_here = __builtin_amdgcn_readfirstlane((tpe - base < 64u) ? tpe - base : 64u);
-        // single-exit inner loop (a dead tree sets k past the window): a second loop exit would make
+        // single-exit loop (a dead tree sets k past the window): a second loop exit would make
         // LLVM add an exit-selector block to every iteration
         for (uint32_t k = 0; k < n_here; ++k) {
-          const uint32_t c = uint32_t(__builtin_amdgcn_readlane(wc, k));
-          const uint32_t arg = uint32_t(__builtin_amdgcn_readlane(wa, k));
-          const uint32_t fidx = arg & SR_A_INDEX;
-          T cval;
-          if constexpr (sizeof(T) == 4) {
-            cval = __builtin_bit_cast(T, __builtin_amdgcn_readlane(wl, k));
-          } else {
-            // readlane returns int: widen through uint32_t (no sign extension into the high word)
-            cval = __builtin_bit_cast(T, uint64_t(uint32_t(__builtin_amdgcn_readlane(wl, k))) |
-                                             (uint64_t(uint32_t(__builtin_amdgcn_readlane(wh, k))) << 32));
-          }
-          switch (c) {
+          const uint32_t w0 = uint32_t(__builtin_amdgcn_readlane(int(wop), int(k)));
+#define SR_CVAL() sr_lane_value<T>(wc0, wc1, k)
+          switch (w0 & SR_W_OPC) {
             case SR_OP_LOAD_FEAT: {
-              L::load(x_lane + fidx * ROWS, tos);
+              if (w0 & SR_W_PUSH_MASK) L::store(stk_lane + (((w0 >> SR_W_PUSH_SHIFT) & 0x3fu) - 1u) * ROWS, tos);
+              L::load(SR_OPND_X(), tos);
               break;
             }
             case SR_OP_LOAD_CONST: {
+              if (w0 & SR_W_PUSH_MASK) L::store(stk_lane + (((w0 >> SR_W_PUSH_SHIFT) & 0x3fu) - 1u) * ROWS, tos);
+              const T cv = SR_CVAL();
 #pragma unroll
-              for (int r = 0; r < R; ++r) tos[r] = cval;
-              break;
-            }
-            case SR_OP_LOAD_FEAT_PUSH: {
-              L::store(stk_lane + sp * ROWS, tos);
-              ++sp;
-              L::load(x_lane + fidx * ROWS, tos);
-              break;
-            }
-            case SR_OP_LOAD_CONST_PUSH: {
-              L::store(stk_lane + sp * ROWS, tos);
-              ++sp;
-#pragma unroll
-              for (int r = 0; r < R; ++r) tos[r] = cval;
+              for (int r = 0; r < R; ++r) tos[r] = cv;
               break;
             }
             // BASIC tier
             SR_UCASE(SR_U_NEG) SR_UCASE(SR_U_SQUARE) SR_UCASE(SR_U_CUBE) SR_UCASE(SR_U_EXP)
             SR_UCASE(SR_U_COS) SR_UCASE(SR_U_SIN) SR_UCASE(SR_U_LOG) SR_UCASE(SR_U_SQRT)
             SR_UCASE(SR_U_ABS)
-            SR_BCASE(SR_B_ADD) SR_BCASE(SR_B_SUB) SR_BCASE(SR_B_MUL) SR_BCASE(SR_B_DIV)
+            SR_BCASE_COMM(SR_B_ADD) SR_BCASE_COMM(SR_B_MUL) SR_BCASE(SR_B_SUB) SR_BCASE(SR_B_DIV)
             // FULL tier
             SR_UCASE_FULL(SR_U_TAN) SR_UCASE_FULL(SR_U_LOG2) SR_UCASE_FULL(SR_U_LOG10)
             SR_UCASE_FULL(SR_U_LOG1P) SR_UCASE_FULL(SR_U_SIGN) SR_UCASE_FULL(SR_U_TANH)
@@ -468,7 +478,8 @@ __global__ void __launch_bounds__(SR_BLOCK SR_MIN_WAVES) sr_tile_kernel(const Sr
             default:
               break;
           }
-          if (arg & SR_A_CHECK) {
+#undef SR_CVAL
+          if (!FAST_CHECK && (w0 & SR_W_CHECK)) {
             if (MODE == SR_MODE_EXACT) {
               double s = 0.0;
 #pragma unroll
@@ -477,12 +488,6 @@ __global__ void __launch_bounds__(SR_BLOCK SR_MIN_WAVES) sr_tile_kernel(const Sr
               s = sr_wave_sum<double>(s);
               if (lane == 0) xacc[g * MC + check_k] += s;
               ++check_k;
-            } else if (FAST_CHECK) {
-#pragma unroll
-              for (int r = 0; r < R; r += 4) {
-                mrun = SrMaxAbs<T>::step(mrun, tos[r], tos[r + 1]);
-                if (r + 3 < R) mrun1 = SrMaxAbs<T>::step(mrun1, tos[r + 2], tos[r + 3]);
-              }
             } else {
               // |v| >= tbig (or NaN / Inf) in any row: one integer max per lane + one ballot;
               // padded rows replicate row 0 of the view, so no row mask is needed here
@@ -503,62 +508,84 @@ __global__ void __launch_bounds__(SR_BLOCK SR_MIN_WAVES) sr_tile_kernel(const Sr
           }
         }
       }
-      if (base + 64u >= tpe) {  // tree j is done on this tile
-      if (FAST_CHECK) {
-        // a checked value was +-Inf (or NaN reached the root): incomplete; a large finite one:
-        // the array-sum check may overflow -> exact path
-        bool nan_root = false;
-#pragma unroll
-        for (int r = 0; r < R; ++r) nan_root |= sr_isnan(tos[r]);
-        mrun = SrMaxAbs<T>::step(mrun, mrun1, T(0));
-        if (sr_ballot(nan_root || !(mrun <= SrM<T>::big))) {
-          dead = true;
-        } else if (sr_ballot(!(mrun < a.tbig))) {
-          susp_any = true;
-        }
-      }
 
-      const uint64_t bit = uint64_t(1) << j;
-      if (MODE == SR_MODE_LOSS && dead) {
-        dmask |= bit;
-        if (use_hint && lane == 0)
-          __hip_atomic_fetch_or(a.hint + tree0 + g, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      } else if (MODE == SR_MODE_LOSS) {
-        T yv[R];
-        L::load(y_lane, yv);
-        T l[R];
-        if (weighted) {
-          T wv[R];
-          L::load(w_lane, wv);
+      if (base + 64u >= tpe) {  // tree j is done on this tile
+        const uint64_t bit = uint64_t(1) << j;
+        if (MODE == SR_MODE_LOSS) {
+          T l[R];
+          if (!dead) {
+            T yv[R];
+            L::load(y_lane, yv);
+            if (weighted) {
+              T wv[R];
+              L::load(w_lane, wv);
 #pragma unroll
-          for (int r = 0; r < R; ++r) l[r] = sr_elem_loss<T>(a.loss_kind, tos[r], yv[r]) * wv[r];
-        } else {
+              for (int r = 0; r < R; ++r) l[r] = sr_elem_loss<T>(lk, tos[r], yv[r]) * wv[r];
+            } else {
 #pragma unroll
-          for (int r = 0; r < R; ++r) l[r] = sr_elem_loss<T>(a.loss_kind, tos[r], yv[r]);
+              for (int r = 0; r < R; ++r) l[r] = sr_elem_loss<T>(lk, tos[r], yv[r]);
+            }
+          }
+          if (FAST_CHECK) {
+            // the root is always checked; a checked value was +-Inf -> incomplete; NaN anywhere
+            // reaches the root (BASIC operators propagate NaN) and shows in its loss terms (or, with
+            // weights, in the root values); a large finite one: the array-sum check may overflow
+#pragma unroll
+            for (int r = 0; r < R; r += 4) {
+              mrun = SrMaxAbs<T>::step(mrun, tos[r], tos[r + 1]);
+              if (r + 3 < R) mrun1 = SrMaxAbs<T>::step(mrun1, tos[r + 2], tos[r + 3]);
+            }
+            mrun = SrMaxAbs<T>::step(mrun, mrun1, T(0));
+            bool nan_root = false;
+            if (weighted) {
+#pragma unroll
+              for (int r = 0; r < R; ++r) nan_root |= sr_isnan(tos[r]);
+            } else {
+              T q0 = l[0], q1 = l[1];
+#pragma unroll
+              for (int r = 2; r < R; r += 2) {
+                q0 += l[r];
+                q1 += l[r + 1];
+              }
+              nan_root = sr_isnan(q0 + q1);
+            }
+            if (sr_ballot(nan_root || !(mrun <= SrM<T>::big))) {
+              dead = true;
+            } else if (sr_ballot(!(mrun < a.tbig))) {
+              susp_any = true;
+            }
+          }
+          if (dead) {
+            dmask |= bit;
+            if (use_hint && lane == 0)
+              __hip_atomic_fetch_or(a.hint + tree0 + g, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          } else {
+            if (!full_tile) {  // rows past the end of the view (padding) do not count
+#pragma unroll
+              for (int r = 0; r < R; ++r) l[r] = (row0 + L::row(lane, r) < a.n_rows) ? l[r] : T(0);
+            }
+            // pairwise over the lane's rows (packed adds), then the wave
+#pragma unroll
+            for (int h = 1; h < R; h *= 2) {
+#pragma unroll
+              for (int r = 0; r + h < R; r += 2 * h) l[r] += l[r + h];
+            }
+            const T s = sr_wave_sum<T>(l[0]);
+            accv += (lane == j) ? double(s) : 0.0;
+            if (susp_any) bmask |= bit;
+          }
+        } else if (MODE == SR_MODE_PRED) {
+          const uint32_t tree = a.perm ? a.perm[tree0 + g] : uint32_t(tree0 + g);
+          T* out = a.pred + int64_t(tree) * a.pred_ld + row0;
+#pragma unroll
+          for (int r = 0; r < R; ++r) {
+            const int i = L::row(lane, r);
+            if (row0 + i < a.n_rows) out[i] = dead ? sr_qnan<T>() : tos[r];
+          }
+          if (dead) dmask |= bit;
+          else if (susp_any) bmask |= bit;
         }
-        if (!full_tile) {  // rows past the end of the view (padding) do not count
-#pragma unroll
-          for (int r = 0; r < R; ++r) l[r] = (row0 + L::row(lane, r) < a.n_rows) ? l[r] : T(0);
-        }
-        T s = l[0];
-#pragma unroll
-        for (int r = 1; r < R; ++r) s += l[r];
-        s = sr_wave_sum<T>(s);
-        accv += (lane == j) ? double(s) : 0.0;
-        if (susp_any) bmask |= bit;
-      } else if (MODE == SR_MODE_PRED) {
-        const uint32_t tree = a.perm ? a.perm[tree0 + g] : uint32_t(tree0 + g);
-        T* out = a.pred + int64_t(tree) * a.pred_ld + row0;
-#pragma unroll
-        for (int r = 0; r < R; ++r) {
-          const int i = L::row(lane, r);
-          if (row0 + i < a.n_rows) out[i] = dead ? sr_qnan<T>() : tos[r];
-        }
-        if (dead) dmask |= bit;
-        else if (susp_any) bmask |= bit;
       }
-      }  // tree done
-      }  // window stream
     }
   }
 
@@ -572,27 +599,33 @@ __global__ void __launch_bounds__(SR_BLOCK SR_MIN_WAVES) sr_tile_kernel(const Sr
     return;
   }
   if (lane < S) {
-    const size_t o = size_t(my_pos) * a.n_row_blocks + rb;
+    const size_t o = size_t(rb) * a.n_trees + my_pos;  // [row block][position]: a block writes one run
     a.part_sum[o] = accv;
     a.part_flag[o] = (((dmask >> lane) & 1u) ? SR_FLAG_NONFINITE : 0u) | (((bmask >> lane) & 1u) ? SR_FLAG_BIG : 0u);
   }
 }
 
 // ------------------------------------------------------------------ launch helpers
-template <typename T, int R, int MODE, bool GATHER, int TIER>
+template <typename T, int R, int MODE, bool GATHER, int TIER, int W, int LK>
 hipError_t sr_launch_tile(const SrEvalArgs<T>& a, int n_blocks, hipStream_t s) {
-  const SrLdsPlan<T> plan(a.nf, 64 * R, a.stack_depth, a.trees_per_block,
-                          MODE == SR_MODE_EXACT ? a.max_checks : 0);
+  const SrLdsPlan<T> plan(a.nf, 64 * R, a.stack_depth, a.trees_per_block, MODE == SR_MODE_EXACT ? a.max_checks : 0, W,
+                          a.w != nullptr);
+  const void* fn = reinterpret_cast<const void*>(&sr_tile_kernel<T, R, MODE, GATHER, TIER, W, LK>);
   if (plan.total > 65536) {  // many features / a deep stack: opt in to the full 160 KiB of LDS
-    const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&sr_tile_kernel<T, R, MODE, GATHER, TIER>),
-                                             hipFuncAttributeMaxDynamicSharedMemorySize, int(plan.total));
+    const hipError_t e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, int(plan.total));
     if (e != hipSuccess) return e;
   }
-  hipLaunchKernelGGL((sr_tile_kernel<T, R, MODE, GATHER, TIER>), dim3(n_blocks), dim3(SR_BLOCK), plan.total, s, a);
+  hipLaunchKernelGGL((sr_tile_kernel<T, R, MODE, GATHER, TIER, W, LK>), dim3(n_blocks), dim3(W * 64), plan.total, s, a);
   return hipGetLastError();
 }
 
 // Explicit instantiations are spread over several translation units (sr_inst_*.hip, one per
 // element type / mode) so the build compiles them in parallel; see the Makefile.
-#define SR_INSTANTIATE(T, R, MODE, GATHER, TIER) \
-  template hipError_t sr_launch_tile<T, R, MODE, GATHER, TIER>(const SrEvalArgs<T>&, int, hipStream_t);
+#define SR_INSTANTIATE_WL(T, R, MODE, GATHER, TIER, W, LK) \
+  template hipError_t sr_launch_tile<T, R, MODE, GATHER, TIER, W, LK>(const SrEvalArgs<T>&, int, hipStream_t);
+#define SR_INSTANTIATE_W(T, R, MODE, GATHER, TIER, W) SR_INSTANTIATE_WL(T, R, MODE, GATHER, TIER, W, -1)
+#define SR_INSTANTIATE(T, R, MODE, GATHER, TIER) SR_INSTANTIATE_WL(T, R, MODE, GATHER, TIER, 4, -1)
+// BASIC-tier loss kernels: one instantiation per elementwise loss
+#define SR_INSTANTIATE_LOSS(T, R, GATHER)                                   \
+  SR_INSTANTIATE_WL(T, R, SR_MODE_LOSS, GATHER, SR_TIER_BASIC, 4, SR_LOSS_L2) \
+  SR_INSTANTIATE_WL(T, R, SR_MODE_LOSS, GATHER, SR_TIER_BASIC, 4, SR_LOSS_L1)

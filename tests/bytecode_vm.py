@@ -1,7 +1,8 @@
 """TEST HELPER: a numpy interpreter of libsr_amd's compiled programs (csrc/sr_ops.h encoding).
 
-It executes exactly the instruction semantics of the HIP kernel (top-of-stack + operand stack,
-combined opcodes, the INFSUB and CHECK bits of arg) on the CPU, so CPU tests can validate the tree COMPILER
+It executes exactly the instruction semantics of the HIP kernel (top-of-stack + statically
+assigned operand-stack slots, combined opcodes, the push field and the INFSUB / CHECK bits of w0) on
+the CPU, so CPU tests can validate the tree COMPILER
 (constant folding, check placement, fused-unary detection, Sethi–Ullman ordering) against the
 oracle without a GPU.  It is not part of the product and is never used as a fallback.
 """
@@ -27,8 +28,8 @@ def compile_info(options, tb, n_rows, nfeatures, dtype):
     s = tb.to_struct()
     dt = _lib.SR_DTYPE_F32 if dtype == np.float32 else _lib.SR_DTYPE_F64
     cap = int(tb.n_nodes) + 16
-    rec = np.dtype([("code", "<u4"), ("arg", "<u4"), ("val", "<f4"), ("pad", "<u4")]) if dtype == np.float32 else \
-        np.dtype([("code", "<u4"), ("arg", "<u4"), ("val", "<f8")])
+    rec = np.dtype([("w0", "<u4"), ("val", "<f4"), ("c1", "<u4"), ("cslot", "<u4")]) if dtype == np.float32 else \
+        np.dtype([("w0", "<u4"), ("val", "<f8"), ("cslot", "<u4")], align=False)
     code = np.zeros(cap, dtype=rec)
     _lib.check(_lib.lib.sr_compile_info(dt, len(options.operators.unaops), un, len(options.operators.binops), bi,
                                         ctypes.byref(s), n_rows, nfeatures, lens.ctypes.data_as(ctypes.c_void_p),
@@ -74,39 +75,56 @@ def _binary(bid, a, b):
     raise NotImplementedError(bid)
 
 
+# w0 fields (csrc/sr_ops.h)
+OPC = 0xFF
+CHECK = 1 << 8
+INFSUB = 1 << 9
+
+
+def opcode(w0):
+    return int(w0) & OPC
+
+
+def operand(w0):
+    return int(w0) >> 16
+
+
+def push_slot(w0):
+    return ((int(w0) >> 10) & 0x3F) - 1
+
+
 def run_program(code, lo, hi, X, T):
-    """Execute one tree's program over all rows; returns (values, complete, check_arrays)."""
+    """Execute one tree's program over all rows; returns (values, complete)."""
     n = X.shape[1]
     tos = np.zeros(n, dtype=T)
-    stack = []
+    slots = {}
     complete = True
     big = T(np.finfo(T).max)
     for pc in range(lo, hi):
-        opc = int(code["code"][pc])
-        arg = int(code["arg"][pc])
-        fidx = arg & ((1 << 28) - 1)  # bit 28: INFSUB, bits 29/30: operand-source tags
+        w0 = int(code["w0"][pc])
+        opc = opcode(w0)
         val = T(code["val"][pc])
-        if opc <= 3:
-            if opc >= 2:
-                stack.append(tos)
-            tos = X[fidx].astype(T) if opc in (0, 2) else np.full(n, val, dtype=T)
+        if opc <= 1:  # LOAD_FEAT / LOAD_CONST, optionally pushing the old tos first
+            if push_slot(w0) >= 0:
+                slots[push_slot(w0)] = tos
+            tos = X[operand(w0)].astype(T) if opc == 0 else np.full(n, val, dtype=T)
         elif opc < 64:
-            v = _unary(opc - 3, tos, T).astype(T)
-            if arg & (1 << 28):  # INFSUB: fused unary, non-finite input -> +Inf
+            v = _unary(opc - 2, tos, T).astype(T)
+            if w0 & INFSUB:  # fused unary: non-finite input -> +Inf
                 v = np.where(np.isfinite(tos), v, T(np.inf)).astype(T)
             tos = v
         else:
             bid, v = divmod(opc - 64, 6)
             bid += 1
             if v in (0, 1):
-                o = stack.pop()
+                o = slots.pop(operand(w0))
             elif v in (2, 3):
-                o = X[fidx].astype(T)
+                o = X[operand(w0)].astype(T)
             else:
                 o = np.full(n, val, dtype=T)
             a, b = (o, tos) if v in (0, 2, 4) else (tos, o)
             tos = _binary(bid, a, b).astype(T)
-        if arg & (1 << 31):  # CHECK: isfinite(sum(array)) (f64 sum, DESIGN.md §3)
+        if w0 & CHECK:  # isfinite(sum(array)) (f64 sum, DESIGN.md §3)
             s = np.sum(tos.astype(np.float64))
             if not np.isfinite(tos).all() or not abs(s) <= float(big):
                 complete = False
