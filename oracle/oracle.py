@@ -117,3 +117,46 @@ class Oracle:
         if not ok:
             raise ValueError("oracle: malformed tree")
         return loss, comp.astype(bool)
+
+    def loss_grad_fd(self, tb, X, y, w=None, loss_kind=0, rel_step=1e-5, n_threads=8, with_error=False):
+        """Central finite differences of the f64 loss with respect to every tree's constants
+        (pre-order, get_scalar_constants), the gradient-free objective the reference's Optim BFGS
+        differentiates (src/ConstantOptimization.jl:77-116), Richardson-extrapolated over steps h
+        and h/2.  Returns (grads, loss, complete) in the layout of ``sr_amd.eval_grad_batch``
+        (plus |D(h) - D(h/2)|, a truncation-error estimate, with ``with_error``)."""
+        g1, loss0, comp0 = self._fd(tb, X, y, w, loss_kind, rel_step, n_threads)
+        g2, _, _ = self._fd(tb, X, y, w, loss_kind, rel_step / 2, n_threads)
+        g = (4 * g2 - g1) / 3
+        if with_error:
+            return g, loss0, comp0, np.abs(g2 - g1)
+        return g, loss0, comp0
+
+    def _fd(self, tb, X, y, w, loss_kind, rel_step, n_threads):
+        X = np.asarray(X, dtype=np.float64)
+        mask = (tb.degree == 0) & (tb.constant != 0)
+        cpos = np.nonzero(mask)[0]
+        base_val = tb.val.astype(np.float64)
+        loss0, comp0 = self.eval_loss_batch(tb, X, y, w, loss_kind, accum="f64", n_threads=n_threads)
+        if len(cpos) == 0:
+            return np.zeros(0), loss0, comp0
+        tree_of = np.searchsorted(tb.offsets, cpos, side="right") - 1
+        # one perturbed copy of the owning tree per (constant, sign)
+        reps = np.repeat(tree_of, 2)
+        starts, ends = tb.offsets[reps], tb.offsets[reps + 1]
+        sel = np.concatenate([np.arange(s, e) for s, e in zip(starts, ends)])
+        offs = np.concatenate([[0], np.cumsum(ends - starts)])
+        val = base_val[sel].copy()
+        h = rel_step * np.maximum(1.0, np.abs(base_val[cpos]))
+        for i, (p, t) in enumerate(zip(cpos, tree_of)):
+            for sgn, k in ((1.0, 2 * i), (-1.0, 2 * i + 1)):
+                val[offs[k] + (p - tb.offsets[t])] += sgn * h[i]
+
+        class _B:
+            pass
+
+        b = _B()
+        b.offsets, b.degree, b.op = offs, tb.degree[sel], tb.op[sel]
+        b.feature, b.constant, b.val = tb.feature[sel], tb.constant[sel], val
+        lp, _ = self.eval_loss_batch(b, X, y, w, loss_kind, accum="f64", n_threads=n_threads)
+        g = (lp[0::2] - lp[1::2]) / (2 * h)
+        return g, loss0, comp0

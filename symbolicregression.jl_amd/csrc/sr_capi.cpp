@@ -74,7 +74,7 @@ struct sr_ctx {
   std::vector<SrOpset> opsets;
   std::vector<int> tiers;
   DevBuf code, offsets, static_bad, part_sum, part_flag, out_sum, out_flag, pred, row_idx, tree_list,
-      check_sums, perm, hint;
+      check_sums, perm, hint, g_code, g_offsets, g_consts, g_const_off, g_items, g_part, g_out;
   double last_eval_ms = 0.0, last_total_ms = 0.0;
   int cu_count = 256;
   int rows_override = 0;    // SR_AMD_ROWS_PER_LANE (tuning): 4 selects the f32 BASIC 4-rows/lane kernel
@@ -502,6 +502,125 @@ int upload_impl(sr_ctx* ctx, const void* X, int64_t nf, int64_t n, const void* y
   return SR_OK;
 }
 
+// Batched forward-mode gradient (sr_eval_grad_batch): exact loss + complete flags from the loss
+// kernel, then d loss / d constants of every complete tree from the tangent kernel.
+template <typename T>
+int eval_grad_impl(sr_ctx* ctx, const sr_dataset* ds, int opset_id, const sr_tree_batch* trees,
+                   const int64_t* row_idx, int64_t n_idx, int loss_kind, void* out_loss, void* out_grad,
+                   uint8_t* out_complete) {
+  const SrOpset& ops = ctx->opsets[opset_id];
+  for (uint32_t u : ops.unary)
+    if (!sr_unary_grad_supported(u)) return set_error(SR_ERR_UNSUPPORTED_OP, "operator without a gradient rule");
+  for (uint32_t b : ops.binary)
+    if (!sr_binary_grad_supported(b)) return set_error(SR_ERR_UNSUPPORTED_OP, "operator without a gradient rule");
+  int rc = eval_loss_impl<T>(ctx, ds, opset_id, trees, row_idx, n_idx, loss_kind, out_loss, out_complete);
+  if (rc != SR_OK) return rc;
+  const int64_t nt = trees->n_trees;
+  if (nt == 0) return SR_OK;
+  const bool gather = row_idx != nullptr && n_idx > 0;
+  const int64_t n_eval = gather ? n_idx : ds->n;
+  SrProgramBatch<T> prog;
+  std::string err;
+  rc = sr_compile_batch<T>(*trees, ops, n_eval, ds->nf, true, &prog, &err);
+  if (rc != SR_OK) return set_error(rc, err);
+  // pre-order constants of every tree (get_scalar_constants order)
+  const T* vals = static_cast<const T*>(trees->val);
+  std::vector<T> consts;
+  consts.reserve(size_t(prog.const_off[size_t(nt)]));
+  for (int64_t t = 0; t < nt; ++t)
+    for (int64_t i = trees->offsets[t]; i < trees->offsets[t + 1]; ++i)
+      if (trees->degree[i] == 0 && trees->constant[i]) consts.push_back(vals[i]);
+  T* g = static_cast<T*>(out_grad);
+  std::fill(g, g + consts.size(), T(0));
+  // work items per tangent width: (tree, first constant)
+  std::vector<uint32_t> items[3], k0s[3];
+  const int kts[3] = {4, 8, 16};
+  for (int64_t t = 0; t < nt; ++t) {
+    const uint32_t nc = prog.n_consts[size_t(t)];
+    if (nc == 0 || !out_complete[t]) continue;
+    if (nc > 128) return set_error(SR_ERR_TOO_DEEP, "more than 128 constants in one tree");
+    const int b = nc <= 4 ? 0 : (nc <= 8 ? 1 : 2);
+    for (uint32_t k0 = 0; k0 < nc; k0 += uint32_t(kts[b])) {
+      items[b].push_back(uint32_t(t));
+      k0s[b].push_back(k0);
+    }
+  }
+  hipStream_t s = ctx->stream;
+  const int depth = prog.max_depth > 0 ? prog.max_depth : 1;
+  SR_HIP_CHECK(ctx->g_code.ensure(prog.code.size() * sizeof(SrIns<T>) + 16));
+  SR_HIP_CHECK(ctx->g_offsets.ensure(prog.offsets.size() * sizeof(uint32_t)));
+  SR_HIP_CHECK(ctx->g_consts.ensure(consts.size() * sizeof(T) + 16));
+  SR_HIP_CHECK(ctx->g_const_off.ensure(prog.const_off.size() * sizeof(uint32_t)));
+  if (!prog.code.empty())
+    SR_HIP_CHECK(hipMemcpyAsync(ctx->g_code.p, prog.code.data(), prog.code.size() * sizeof(SrIns<T>),
+                                hipMemcpyHostToDevice, s));
+  SR_HIP_CHECK(hipMemcpyAsync(ctx->g_offsets.p, prog.offsets.data(), prog.offsets.size() * sizeof(uint32_t),
+                              hipMemcpyHostToDevice, s));
+  if (!consts.empty())
+    SR_HIP_CHECK(hipMemcpyAsync(ctx->g_consts.p, consts.data(), consts.size() * sizeof(T), hipMemcpyHostToDevice, s));
+  SR_HIP_CHECK(hipMemcpyAsync(ctx->g_const_off.p, prog.const_off.data(), prog.const_off.size() * sizeof(uint32_t),
+                              hipMemcpyHostToDevice, s));
+  const double denom = view_denominator<T>(ds, row_idx, n_idx);
+  constexpr int kWaves = 4, kRowsPerTile = 256;
+  const int64_t n_tiles = (n_eval + kRowsPerTile - 1) / kRowsPerTile;
+  for (int b = 0; b < 3; ++b) {
+    const int64_t ni = int64_t(items[b].size());
+    if (ni == 0) continue;
+    const int kt = kts[b];
+    std::vector<uint32_t> packed(items[b]);
+    packed.insert(packed.end(), k0s[b].begin(), k0s[b].end());
+    SR_HIP_CHECK(ctx->g_items.ensure(packed.size() * sizeof(uint32_t)));
+    SR_HIP_CHECK(hipMemcpyAsync(ctx->g_items.p, packed.data(), packed.size() * sizeof(uint32_t),
+                                hipMemcpyHostToDevice, s));
+    const int64_t n_groups = (ni + kWaves - 1) / kWaves;
+    int64_t n_rb = (4096 + n_groups - 1) / n_groups;
+    if (n_rb > n_tiles) n_rb = n_tiles;
+    if (n_rb < 1) n_rb = 1;
+    const int64_t tiles_per_block = (n_tiles + n_rb - 1) / n_rb;
+    n_rb = (n_tiles + tiles_per_block - 1) / tiles_per_block;
+    if (n_rb * n_groups > 0x7fffffff) return set_error(SR_ERR_INVALID_ARG, "grid too large");
+    const size_t n_vals = size_t(ni) * size_t(kt);
+    SR_HIP_CHECK(ctx->g_part.ensure(size_t(n_rb) * n_vals * sizeof(double)));
+    SR_HIP_CHECK(ctx->g_out.ensure(n_vals * sizeof(double)));
+    SrGradArgs<T> a{};
+    a.code = ctx->g_code.as<SrIns<T>>();
+    a.offsets = ctx->g_offsets.as<uint32_t>();
+    a.consts = ctx->g_consts.as<T>();
+    a.const_off = ctx->g_const_off.as<uint32_t>();
+    a.item_tree = ctx->g_items.as<uint32_t>();
+    a.item_k0 = ctx->g_items.as<uint32_t>() + ni;
+    a.n_items = int(ni);
+    a.X = static_cast<const T*>(ds->X);
+    a.y = static_cast<const T*>(ds->y);
+    a.w = static_cast<const T*>(ds->w);
+    a.row_idx = gather ? ctx->row_idx.as<int64_t>() : nullptr;
+    a.ld = ds->ld;
+    a.n_rows = n_eval;
+    a.nf = int(ds->nf);
+    a.tiles_per_block = int(tiles_per_block);
+    a.n_row_blocks = int(n_rb);
+    a.n_groups = int(n_groups);
+    a.stack_depth = depth;
+    a.loss_kind = loss_kind;
+    a.part = ctx->g_part.as<double>();
+    const size_t lds = (size_t(a.nf) + 1 + (a.w ? 1 : 0)) * kRowsPerTile * sizeof(T) +
+                       size_t(kWaves) * depth * (1 + kt) * 64 * sizeof(T);
+    if (lds > kLdsMax) return set_error(SR_ERR_TOO_DEEP, "gradient tile needs more than 160 KiB of LDS");
+    SR_HIP_CHECK(sr_launch_grad_any<T>(a, kt, gather, int(n_rb * n_groups), s));
+    SR_HIP_CHECK(sr_launch_grad_reduce(a.part, int(n_rb), int(n_vals), ctx->g_out.as<double>(), s));
+    std::vector<double> out(n_vals);
+    SR_HIP_CHECK(hipMemcpyAsync(out.data(), ctx->g_out.p, n_vals * sizeof(double), hipMemcpyDeviceToHost, s));
+    SR_HIP_CHECK(hipStreamSynchronize(s));
+    for (int64_t i = 0; i < ni; ++i) {
+      const uint32_t t = items[b][size_t(i)], k0 = k0s[b][size_t(i)];
+      const uint32_t nc = prog.n_consts[t];
+      for (int q = 0; q < kt && k0 + uint32_t(q) < nc; ++q)
+        g[prog.const_off[t] + k0 + uint32_t(q)] = T(out[size_t(i) * kt + size_t(q)] / denom);
+    }
+  }
+  return SR_OK;
+}
+
 int tier_of(const SrOpset& o) {
   auto basic_u = [](uint32_t u) {
     return u == SR_U_NEG || u == SR_U_SQUARE || u == SR_U_CUBE || u == SR_U_EXP || u == SR_U_COS ||
@@ -572,7 +691,8 @@ int sr_shutdown(sr_ctx* ctx) {
     (void)hipStreamSynchronize(ctx->stream);
     for (DevBuf* b : {&ctx->code, &ctx->offsets, &ctx->static_bad, &ctx->part_sum, &ctx->part_flag, &ctx->out_sum,
                       &ctx->out_flag, &ctx->pred, &ctx->row_idx, &ctx->tree_list, &ctx->check_sums,
-                      &ctx->perm, &ctx->hint})
+                      &ctx->perm, &ctx->hint, &ctx->g_code, &ctx->g_offsets, &ctx->g_consts, &ctx->g_const_off,
+                      &ctx->g_items, &ctx->g_part, &ctx->g_out})
       b->release();
     (void)hipEventDestroy(ctx->ev_start);
     (void)hipEventDestroy(ctx->ev_k0);
@@ -763,9 +883,16 @@ int sr_finalize_losses(int dtype, int64_t n_trees, const double* sums, const uin
 int sr_eval_grad_batch(sr_ctx* ctx, const sr_dataset* ds, int opset_id, const sr_tree_batch* trees,
                        const int64_t* row_idx, int64_t n_idx, int loss_kind, void* out_loss, void* out_grad,
                        uint8_t* out_complete) {
-  (void)ctx; (void)ds; (void)opset_id; (void)trees; (void)row_idx; (void)n_idx; (void)loss_kind;
-  (void)out_loss; (void)out_grad; (void)out_complete;
-  return set_error(SR_ERR_INVALID_ARG, "sr_eval_grad_batch: forward-mode gradient kernel not built yet");
+  int rc = validate_common(ctx, ds, opset_id, trees);
+  if (rc != SR_OK) return rc;
+  if (trees->n_trees > 0 && (!out_loss || !out_grad || !out_complete))
+    return set_error(SR_ERR_INVALID_ARG, "NULL output buffers");
+  if (!ds->y) return set_error(SR_ERR_INVALID_ARG, "dataset has no y");
+  Lock l(ctx);
+  SR_HIP_CHECK(hipSetDevice(ctx->device));
+  if (ds->dtype == SR_DTYPE_F32)
+    return eval_grad_impl<float>(ctx, ds, opset_id, trees, row_idx, n_idx, loss_kind, out_loss, out_grad, out_complete);
+  return eval_grad_impl<double>(ctx, ds, opset_id, trees, row_idx, n_idx, loss_kind, out_loss, out_grad, out_complete);
 }
 
 int sr_compile_info(int dtype, int n_unary, const char* const* unary_names, int n_binary,

@@ -63,3 +63,32 @@ template <typename T>
 hipError_t sr_launch_transpose(const T* Xh_dev, int64_t nf, int64_t n, int64_t ld, T* Xd, hipStream_t s);
 template <typename T>
 hipError_t sr_launch_pad(T* v, int64_t n, int64_t ld, T pad_value, int replicate_first, hipStream_t s);
+
+// Arguments of the forward-mode constant-gradient kernel (csrc/sr_grad_impl.h).
+template <typename T>
+struct SrGradArgs {
+  const SrIns<T>* code;
+  const uint32_t* offsets;   // [n_trees + 1]
+  const T* consts;           // pre-order constants of every tree
+  const uint32_t* const_off; // [n_trees + 1]
+  const uint32_t* item_tree; // work item -> tree
+  const uint32_t* item_k0;   // work item -> first tangent (constant index)
+  int n_items;
+  const T* X;
+  const T* y;
+  const T* w;
+  const int64_t* row_idx;    // GATHER: rows of the SubDataset
+  int64_t ld;
+  int64_t n_rows;
+  int nf;
+  int tiles_per_block;
+  int n_row_blocks;
+  int n_groups;
+  int stack_depth;
+  int loss_kind;
+  double* part;              // [n_row_blocks][n_items][KT]
+};
+
+template <typename T>
+hipError_t sr_launch_grad_any(const SrGradArgs<T>& a, int kt, bool gather, int n_blocks, hipStream_t s);
+hipError_t sr_launch_grad_reduce(const double* part, int n_row_blocks, int n_vals, double* out, hipStream_t s);

@@ -1,0 +1,207 @@
+// sr_grad_impl.h — batched forward-mode gradient of the loss with respect to tree constants.
+//
+// What it replaces: the objective/gradient pair BFGS calls in SymbolicRegression's constant
+// optimisation (reference src/ConstantOptimization.jl:77-167: Evaluator / GradEvaluator with a
+// forward-mode autodiff backend, i.e. value_and_gradient of eval_loss with respect to
+// get_scalar_constants(tree)), for many (tree, constant vector) pairs in one launch.
+//
+// Execution model:
+//   * a workgroup = W wave64s = W work items (tree, first tangent k0) x one row block; per tile the
+//     X rows (all features), y and w are staged once in LDS and shared by the W waves;
+//   * one row per lane; every value carries KT tangents (dual numbers with KT partials, the
+//     constants k0 .. k0+KT-1 of the tree in pre-order), all in VGPRs; operand-stack slots
+//     (value + tangents) live in a per-wave LDS area;
+//   * constants come from a per-tree array (lane k holds constant k), so BFGS updates them without
+//     recompiling; a constant leaf with slot c seeds the one-hot tangent e_{c-k0};
+//   * per row, d loss / d pred (2(ŷ - y) for L2, sign for L1, times the weight) scales the tangents
+//     into per-lane accumulators that live across the row block; one DPP wave reduction per
+//     (item, tangent) at the end of the block -> [row block][item][KT] f64 partials.
+// Only complete trees are differentiated (the caller evaluates the loss and `complete` with the
+// exact loss kernel first: for an incomplete tree eval_loss is the constant L(Inf) and its
+// gradient is zero), so this kernel needs no validity checks.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "sr_eval.h"
+#include "sr_ops.h"
+#include "sr_tile_impl.h"
+
+// Value of lane l of v (l uniform).
+template <typename T>
+__device__ __forceinline__ T sr_readlane_val(T v, uint32_t l) {
+  if constexpr (sizeof(T) == 4) {
+    return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), int(l)));
+  } else {
+    const uint64_t b = uint64_t(__double_as_longlong(v));
+    const uint32_t lo = uint32_t(__builtin_amdgcn_readlane(int(uint32_t(b)), int(l)));
+    const uint32_t hi = uint32_t(__builtin_amdgcn_readlane(int(uint32_t(b >> 32)), int(l)));
+    return __longlong_as_double(int64_t((uint64_t(hi) << 32) | lo));
+  }
+}
+
+template <typename T, int KT, int W, bool GATHER>
+__global__ void __launch_bounds__(W * 64) sr_grad_kernel(const SrGradArgs<T> a) {
+  constexpr int SUB = 4;             // 64-row sub-tiles per staged tile
+  constexpr int ROWS = 64 * SUB;
+  constexpr int NV = 1 + KT;         // value + tangents
+  extern __shared__ __attribute__((aligned(16))) unsigned char sr_smem[];
+  const int tid = threadIdx.x;
+  const int wave = tid >> 6;
+  const int lane = tid & 63;
+  T* xs = reinterpret_cast<T*>(sr_smem);                       // [nf][ROWS]
+  T* ys = xs + size_t(a.nf) * ROWS;                            // [ROWS]
+  T* wsv = ys + ROWS;                                          // [ROWS] (weighted)
+  T* stk = wsv + (a.w ? ROWS : 0);                             // [W][depth][NV][64]
+  T* my_stk = stk + size_t(wave) * a.stack_depth * NV * 64 + lane;
+
+  const int tg = blockIdx.x % a.n_groups;
+  const int rb = blockIdx.x / a.n_groups;
+  const int item = tg * W + wave;
+  const bool active = item < a.n_items;
+  uint32_t pb = 0u, pe = 0u, k0 = 0u, cb = 0u, nconst = 0u;
+  if (active) {
+    const uint32_t t = a.item_tree[item];
+    pb = a.offsets[t];
+    pe = a.offsets[t + 1];
+    k0 = a.item_k0[item];
+    cb = a.const_off[t];
+    nconst = a.const_off[t + 1] - cb;
+  }
+  // this tree's constants: lane c holds constant c (programs are short: <= 64 constants per window
+  // of lanes, more live in further registers of the same lane set)
+  T cval0 = T(0), cval1 = T(0);
+  if (active && uint32_t(lane) < nconst) cval0 = a.consts[cb + lane];
+  if (active && uint32_t(lane) + 64u < nconst) cval1 = a.consts[cb + 64 + lane];
+
+  double acc[KT];  // per-lane f64 accumulators across the row block
+#pragma unroll
+  for (int k = 0; k < KT; ++k) acc[k] = 0.0;
+  const bool weighted = a.w != nullptr;
+
+  for (int tile = 0; tile < a.tiles_per_block; ++tile) {
+    const int64_t row0 = (int64_t(rb) * a.tiles_per_block + tile) * ROWS;
+    if (row0 >= a.n_rows) break;
+    __syncthreads();
+    for (int i = tid; i < ROWS; i += W * 64) {
+      const int64_t v = row0 + i;
+      const int64_t src = GATHER ? a.row_idx[v < a.n_rows ? v : 0] : (v < a.n_rows ? v : 0);
+      for (int f = 0; f < a.nf; ++f) xs[f * ROWS + i] = a.X[int64_t(f) * a.ld + src];
+      ys[i] = a.y[src];
+      if (weighted) wsv[i] = a.w[src];
+    }
+    __syncthreads();
+    if (!active || pe == pb) continue;
+
+    for (int sub = 0; sub < SUB; ++sub) {
+      const int r = sub * 64 + lane;
+      if (row0 + sub * 64 >= a.n_rows) break;  // uniform
+      T v = T(0);
+      T dv[KT];
+#pragma unroll
+      for (int k = 0; k < KT; ++k) dv[k] = T(0);
+      for (uint32_t base = pb; base < pe; base += 64u) {
+        uint4 cw = make_uint4(0u, 0u, 0u, 0u);
+        if (base + lane < pe) cw = sr_load_window(a.code, base + lane);
+        const uint32_t n_here = __builtin_amdgcn_readfirstlane((pe - base < 64u) ? pe - base : 64u);
+        for (uint32_t k = 0; k < n_here; ++k) {
+          const uint32_t w0 = uint32_t(__builtin_amdgcn_readlane(int(cw.x), int(k)));
+          const uint32_t opc = w0 & SR_W_OPC;
+          const uint32_t cs = uint32_t(__builtin_amdgcn_readlane(int(cw.w), int(k)));
+          // operand (value + tangents): feature / stack slot / constant
+          T ov = T(0);
+          T od[KT];
+#pragma unroll
+          for (int q = 0; q < KT; ++q) od[q] = T(0);
+          uint32_t variant = 6u;
+          if (opc >= SR_OP_BINARY0) variant = (opc - SR_OP_BINARY0) % 6u;
+          const bool load = opc <= SR_OP_LOAD_CONST;
+          if ((load && opc == SR_OP_LOAD_FEAT) || variant == SR_V_FL || variant == SR_V_FR) {
+            ov = xs[(w0 >> SR_W_OPND_SHIFT) * ROWS + r];
+          } else if ((load && opc == SR_OP_LOAD_CONST) || variant == SR_V_CL || variant == SR_V_CR) {
+            // constant slot cs: value from the tree's constant array, tangent e_{cs-k0}
+            ov = cs < 64u ? sr_readlane_val<T>(cval0, cs) : sr_readlane_val<T>(cval1, cs - 64u);
+            const int jj = int(cs) - int(k0);
+#pragma unroll
+            for (int q = 0; q < KT; ++q) od[q] = (q == jj) ? T(1) : T(0);
+          } else if (variant == SR_V_SL || variant == SR_V_SR) {
+            const T* sp = my_stk + size_t(w0 >> SR_W_OPND_SHIFT) * NV * 64;
+            ov = sp[0];
+#pragma unroll
+            for (int q = 0; q < KT; ++q) od[q] = sp[(q + 1) * 64];
+          }
+          if (load) {
+            if (w0 & SR_W_PUSH_MASK) {
+              T* sp = my_stk + size_t(((w0 >> SR_W_PUSH_SHIFT) & 0x3fu) - 1u) * NV * 64;
+              sp[0] = v;
+#pragma unroll
+              for (int q = 0; q < KT; ++q) sp[(q + 1) * 64] = dv[q];
+            }
+            v = ov;
+#pragma unroll
+            for (int q = 0; q < KT; ++q) dv[q] = od[q];
+          } else if (opc < SR_OP_BINARY0) {
+            const uint32_t u = opc - SR_OP_UNARY0;
+            const T x = v;
+            const T yv = sr_unary<T>(u, x);
+            // (fused unaries: complete trees have finite inner values, so INFSUB never fires)
+            const T dfx = sr_unary_deriv<T>(u, x, yv);
+            v = yv;
+#pragma unroll
+            for (int q = 0; q < KT; ++q) dv[q] = dfx * dv[q];
+          } else {
+            const uint32_t b = (opc - SR_OP_BINARY0) / 6u + 1u;
+            const bool left = variant == SR_V_SL || variant == SR_V_FL || variant == SR_V_CL;
+            const T av = left ? ov : v, bv = left ? v : ov;
+            const T rv = sr_binary<T>(b, av, bv);
+            T pa, pbv;
+            sr_binary_partials<T>(b, av, bv, rv, &pa, &pbv);
+            v = rv;
+            if (left) {
+#pragma unroll
+              for (int q = 0; q < KT; ++q) dv[q] = __builtin_fma(pa, od[q], pbv * dv[q]);
+            } else {
+#pragma unroll
+              for (int q = 0; q < KT; ++q) dv[q] = __builtin_fma(pa, dv[q], pbv * od[q]);
+            }
+          }
+        }
+      }
+      // d loss / d constant: (d loss / d pred) * d pred / d constant, padded rows excluded
+      T coef = sr_elem_loss_deriv<T>(a.loss_kind, v, ys[r]);
+      if (weighted) coef *= wsv[r];
+      if (row0 + r >= a.n_rows) coef = T(0);
+#pragma unroll
+      for (int q = 0; q < KT; ++q) acc[q] = __builtin_fma(double(coef), double(dv[q]), acc[q]);
+    }
+  }
+  if (!active) return;
+#pragma unroll
+  for (int q = 0; q < KT; ++q) {
+    const double s = sr_wave_sum<double>(acc[q]);
+    if (lane == 0) a.part[(size_t(rb) * a.n_items + item) * KT + q] = s;
+  }
+}
+
+template <typename T, int KT, int W, bool GATHER>
+hipError_t sr_launch_grad(const SrGradArgs<T>& a, int n_blocks, hipStream_t s) {
+  const size_t lds = (size_t(a.nf) + 1 + (a.w ? 1 : 0)) * 256 * sizeof(T) +
+                     size_t(W) * a.stack_depth * (1 + KT) * 64 * sizeof(T);
+  const void* fn = reinterpret_cast<const void*>(&sr_grad_kernel<T, KT, W, GATHER>);
+  if (lds > 65536) {
+    const hipError_t e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, int(lds));
+    if (e != hipSuccess) return e;
+  }
+  hipLaunchKernelGGL((sr_grad_kernel<T, KT, W, GATHER>), dim3(n_blocks), dim3(W * 64), lds, s, a);
+  return hipGetLastError();
+}
+
+// Σ over row blocks (fixed order) of the [row block][item][KT] partials -> out[item][KT].
+__global__ void __launch_bounds__(256) sr_grad_reduce_kernel(const double* __restrict__ part, int n_row_blocks,
+                                                              int n_vals, double* __restrict__ out) {
+  const int i = int(int64_t(blockIdx.x) * blockDim.x + threadIdx.x);
+  if (i >= n_vals) return;
+  double s = 0.0;
+  for (int b = 0; b < n_row_blocks; ++b) s += part[size_t(b) * n_vals + i];
+  out[i] = s;
+}

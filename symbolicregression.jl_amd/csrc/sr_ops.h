@@ -299,10 +299,86 @@ SR_HD inline T sr_binary(uint32_t op, T x, T y) {
   }
 }
 
+// ---------------------------------------------------------------------------------------
+// Derivatives for the forward-mode constant gradient (ConstantOptimization.jl with a forward-mode
+// autodiff backend).  Only evaluated on complete trees, i.e. on the valid branch of every safe
+// operator.  sr_grad_supported() says whether an operator has a rule here.
+// ---------------------------------------------------------------------------------------
+inline bool sr_unary_grad_supported(uint32_t op) { return op != SR_U_GAMMA && op != SR_U_NONE && op < SR_U_COUNT; }
+inline bool sr_binary_grad_supported(uint32_t op) { return op != SR_B_NONE && op < SR_B_COUNT; }
+
+// d op(x) / dx, given y = op(x)
+template <typename T>
+SR_HD inline T sr_unary_deriv(uint32_t op, T x, T y) {
+  using M = SrM<T>;
+  switch (op) {
+    case SR_U_NEG: return T(-1);
+    case SR_U_SQUARE: return T(2) * x;
+    case SR_U_CUBE: return T(3) * x * x;
+    case SR_U_EXP: return y;
+    case SR_U_COS: return -M::sin(x);
+    case SR_U_SIN: return M::cos(x);
+    case SR_U_TAN: return T(1) + y * y;
+    case SR_U_LOG: return T(1) / x;
+    case SR_U_LOG2: return T(1) / (x * T(0.6931471805599453));
+    case SR_U_LOG10: return T(1) / (x * T(2.302585092994046));
+    case SR_U_LOG1P: return T(1) / (T(1) + x);
+    case SR_U_SQRT: return T(0.5) / y;
+    case SR_U_ABS: return __builtin_signbit(x) ? T(-1) : T(1);  // Julia abs(::Dual)
+    case SR_U_SIGN: return T(0);
+    case SR_U_TANH: return T(1) - y * y;
+    case SR_U_SINH: return M::cosh(x);
+    case SR_U_COSH: return M::sinh(x);
+    case SR_U_ATAN: return T(1) / (T(1) + x * x);
+    case SR_U_ASIN: return T(1) / M::sqrt(T(1) - x * x);
+    case SR_U_ACOS: return T(-1) / M::sqrt(T(1) - x * x);
+    case SR_U_ACOSH: return T(1) / M::sqrt(x * x - T(1));
+    case SR_U_ATANH: return T(1) / (T(1) - x * x);
+    case SR_U_ASINH: return T(1) / M::sqrt(T(1) + x * x);
+    case SR_U_RELU: return x > T(0) ? T(1) : T(0);
+    case SR_U_INV: return -(y * y);
+    case SR_U_ERF: return T(1.1283791670955126) * M::exp(-(x * x));
+    case SR_U_ERFC: return T(-1.1283791670955126) * M::exp(-(x * x));
+    case SR_U_ROUND: case SR_U_FLOOR: case SR_U_CEIL: return T(0);
+    case SR_U_EXP2: return T(0.6931471805599453) * y;
+    case SR_U_EXPM1: return y + T(1);
+    default: return sr_qnan<T>();
+  }
+}
+
+// partial derivatives (d/da, d/db) of r = op(a, b)
+template <typename T>
+SR_HD inline void sr_binary_partials(uint32_t op, T a, T b, T r, T* pa, T* pb) {
+  using M = SrM<T>;
+  switch (op) {
+    case SR_B_ADD: *pa = T(1); *pb = T(1); return;
+    case SR_B_SUB: *pa = T(1); *pb = T(-1); return;
+    case SR_B_MUL: *pa = b; *pb = a; return;
+    case SR_B_DIV: *pa = T(1) / b; *pb = -r / b; return;
+    case SR_B_POW:
+      *pa = (a == T(0)) ? b * M::pow(a, b - T(1)) : b * r / a;
+      *pb = a > T(0) ? r * M::log(a) : T(0);
+      return;
+    case SR_B_MAX: { const bool ta = !(b > a); *pa = ta ? T(1) : T(0); *pb = ta ? T(0) : T(1); return; }  // ties: first
+    case SR_B_MIN: { const bool ta = !(b < a); *pa = ta ? T(1) : T(0); *pb = ta ? T(0) : T(1); return; }
+    case SR_B_MOD: *pa = T(1); *pb = -M::floor(a / b); return;
+    case SR_B_COND: *pa = T(0); *pb = a > T(0) ? T(1) : T(0); return;
+    case SR_B_ATAN2: { const T d = a * a + b * b; *pa = b / d; *pb = -a / d; return; }
+    default: *pa = T(0); *pb = T(0); return;  // comparisons / logical: piecewise constant
+  }
+}
+
 // Elementwise loss value.
 template <typename T>
 SR_HD inline T sr_elem_loss(int32_t kind, T pred, T target) {
   const T d = pred - target;
   if (kind == SR_LOSS_L1) return d < T(0) ? -d : d;
   return d * d;
+}
+// d loss / d pred
+template <typename T>
+SR_HD inline T sr_elem_loss_deriv(int32_t kind, T pred, T target) {
+  const T d = pred - target;
+  if (kind == SR_LOSS_L1) return d > T(0) ? T(1) : (d < T(0) ? T(-1) : T(0));
+  return T(2) * d;
 }

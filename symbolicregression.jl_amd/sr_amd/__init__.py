@@ -13,6 +13,7 @@ from .loss import (
     compute_complexity,
     eval_cost,
     eval_cost_batch,
+    eval_grad_batch,
     eval_loss,
     eval_loss_batch,
     eval_tree_array,
@@ -41,7 +42,7 @@ __all__ = [
     "Options", "OperatorEnum", "Dataset", "SubDataset", "batch", "Node", "TreeBatch", "flatten_trees",
     "extend_operators", "apply_unary", "apply_binary", "parse_expression", "string_tree",
     "get_scalar_constants", "set_scalar_constants", "eval_tree_array", "eval_tree_array_batch",
-    "eval_loss", "eval_loss_batch", "eval_cost", "eval_cost_batch", "loss_to_cost",
+    "eval_loss", "eval_loss_batch", "eval_grad_batch", "eval_cost", "eval_cost_batch", "loss_to_cost",
     "update_baseline_loss_", "score_func", "compute_complexity", "gen_random_tree_fixed_size",
     "gen_random_population", "make_random_leaf", "get_context", "device_available", "DeviceContext",
     "SRError", "UnsupportedOperatorError",

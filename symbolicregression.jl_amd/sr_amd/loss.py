@@ -63,6 +63,44 @@ def eval_loss_batch(trees, dataset, options, *, ctx=None):
     return losses, complete.astype(bool)
 
 
+def eval_grad_batch(trees, dataset, options, *, ctx=None):
+    """Loss and its gradient with respect to every tree's constants, for a whole batch.
+
+    Returns ``(losses[T], grads[T], complete[bool])``; ``grads`` holds each tree's constants in
+    pre-order (``get_scalar_constants``) at ``TreeBatch.constant_offsets()``.  This is the
+    objective/gradient pair of reference src/ConstantOptimization.jl:126-167 (``Evaluator`` /
+    ``GradEvaluator`` with a forward-mode backend) computed on the device by forward-mode dual
+    numbers; an incomplete tree has loss ``Inf`` and a zero gradient (``eval_loss`` is the
+    constant ``L(Inf)`` there).
+    """
+    if options.loss_function is not None or options.loss_function_expression is not None:
+        raise NotImplementedError("custom objectives are evaluated by the reference CPU path")
+    ctx = ctx or get_context()
+    full = dataset.full
+    tb = _as_batch(trees, full.dtype)
+    nt = tb.n_trees
+    losses = np.empty(nt, dtype=full.dtype)
+    complete = np.empty(nt, dtype=np.uint8)
+    grads = np.zeros(int(tb.constant_mask().sum()) + 1, dtype=full.dtype)
+    idx = dataset.indices
+    s = tb.to_struct()
+    _lib.check(
+        _lib.lib.sr_eval_grad_batch(
+            ctx.handle,
+            full.device_handle(ctx),
+            ctx.opset_id(options.operators),
+            ctypes.byref(s),
+            None if idx is None else idx.ctypes.data_as(ctypes.c_void_p),
+            0 if idx is None else int(idx.size),
+            options.loss_kind,
+            losses.ctypes.data_as(ctypes.c_void_p),
+            grads.ctypes.data_as(ctypes.c_void_p),
+            complete.ctypes.data_as(ctypes.c_void_p),
+        )
+    )
+    return losses, grads[:-1], complete.astype(bool)
+
+
 def eval_tree_array_batch(trees, dataset, options, *, ctx=None):
     """Predictions of every tree: (out[n_trees, n_rows], complete[n_trees])."""
     ctx = ctx or get_context()

@@ -272,6 +272,25 @@ class TreeBatch:
         s.val = self.val.ctypes.data_as(ctypes.c_void_p)
         return s
 
+    def constant_mask(self) -> np.ndarray:
+        return (self.degree == 0) & (self.constant != 0)
+
+    def constant_offsets(self) -> np.ndarray:
+        """[n_trees + 1] prefix sum of per-tree constant counts (pre-order, get_scalar_constants)."""
+        m = self.constant_mask().astype(np.int64)
+        c = np.concatenate([[0], np.cumsum(m)])
+        return c[self.offsets]
+
+    def get_constants(self) -> np.ndarray:
+        """All trees' constants, pre-order per tree, concatenated (see constant_offsets)."""
+        return self.val[self.constant_mask()].copy()
+
+    def with_constants(self, consts) -> "TreeBatch":
+        """Same trees with their constants replaced (set_scalar_constants! for the whole batch)."""
+        val = self.val.copy()
+        val[self.constant_mask()] = np.asarray(consts, dtype=val.dtype)
+        return TreeBatch(self.offsets, self.degree, self.op, self.feature, self.constant, val)
+
     def subset(self, idx) -> "TreeBatch":
         idx = np.asarray(idx, dtype=np.int64)
         starts, ends = self.offsets[idx], self.offsets[idx + 1]

@@ -1,0 +1,116 @@
+"""GPU: batched forward-mode loss gradient with respect to tree constants (sr_eval_grad_batch).
+
+Mirrors the reference's constant-derivative tests (test/integration/ad/zygote/test_derivatives.jl:
+91-123: d(3.2*x1)/dc = x1 and the two-constant "equation5" expression, constant order :127-155)
+re-expressed as gradients of the L2 loss with closed forms, plus random populations against
+central finite differences of the f64 CPU oracle (the gradient-free objective Optim's BFGS
+differentiates by default, src/ConstantOptimization.jl:77-116).
+"""
+import numpy as np
+import pytest
+
+from oracle import Oracle
+from sr_amd import Dataset, Options, eval_grad_batch, flatten_trees, gen_random_population, parse_expression
+
+pytestmark = pytest.mark.gpu
+
+
+def _data(n, seed, dtype):
+    rng = np.random.default_rng(seed)
+    X = rng.standard_normal((3, n)).astype(dtype)
+    y = (2 * np.cos(X[2]) + X[0] ** 2 - 2 + 0.1 * rng.standard_normal(n)).astype(dtype)
+    return X, y
+
+
+@pytest.mark.parametrize("dtype,tol", [(np.float64, 1e-12), (np.float32, 2e-5)])
+def test_known_answer_linear(dtype, tol):
+    opts = Options(binary_operators=["+", "*", "-", "/"], unary_operators=["cos", "exp", "sin"])
+    X, y = _data(3001, 0, dtype)
+    tb = flatten_trees([parse_expression("3.2 * x1", opts)], dtype)
+    loss, g, comp = eval_grad_batch(tb, Dataset(X, y), opts)
+    x1, yy = X[0].astype(np.float64), y.astype(np.float64)
+    ref = np.mean(2 * (3.2 * x1 - yy) * x1)  # d/dc mean((c*x1 - y)^2) at c = 3.2
+    assert comp[0] and g.shape == (1,)
+    assert abs(g[0] - ref) <= tol * max(1.0, abs(ref))
+    assert abs(loss[0] - np.mean((np.float64(dtype(3.2)) * x1 - yy) ** 2)) <= 1e-5 * loss[0]
+
+
+@pytest.mark.parametrize("dtype,tol", [(np.float64, 1e-10), (np.float32, 1e-4)])
+def test_known_answer_equation5(dtype, tol):
+    # equation5 (test_derivatives.jl:101-123) with the catalog's ops: pow_abs2(x1,x2) = abs(x1)^x2,
+    # custom_cos(x) = cos(x)^2 -> square(cos(x))
+    opts = Options(binary_operators=["+", "*", "-", "/", "^"], unary_operators=["cos", "abs", "square"])
+    X, y = _data(2000, 1, dtype)
+    X[0] = np.where(np.abs(X[0]) < 0.1, 0.5, X[0])  # keep c2 / x1 tame
+    c1, c2 = 2.1, -3.2
+    tree = parse_expression("((abs(x1) ^ x2) + x3) + (square(cos(2.1 + x3)) + (-3.2 / x1))", opts)
+    tb = flatten_trees([tree], dtype)
+    loss, g, comp = eval_grad_batch(tb, Dataset(X, y), opts)
+    x1, x2, x3, yy = (v.astype(np.float64) for v in (X[0], X[1], X[2], y))
+    pred = np.abs(x1) ** x2 + x3 + np.cos(c1 + x3) ** 2 + c2 / x1
+    d = 2 * (pred - yy)
+    ref = np.array([np.mean(d * (-2 * np.cos(c1 + x3) * np.sin(c1 + x3))), np.mean(d / x1)])
+    assert comp[0]
+    np.testing.assert_allclose(g, ref, rtol=tol, atol=tol * np.abs(ref).max())
+
+
+def test_population_f64_vs_finite_differences():
+    opts = Options(binary_operators=["+", "-", "*", "/"], unary_operators=["cos", "exp", "log", "sin"])
+    X, y = _data(1500, 2, np.float64)
+    trees = gen_random_population(400, opts, 3, seed=5)
+    tb = flatten_trees(trees, np.float64)
+    loss, g, comp = eval_grad_batch(tb, Dataset(X, y), opts)
+    g_fd, loss_o, comp_o, fd_err = Oracle.from_options(opts).loss_grad_fd(tb, X, y, with_error=True)
+    assert np.array_equal(comp, comp_o)
+    co = tb.constant_offsets()
+    n_checked = 0
+    for t in np.nonzero(comp)[0]:
+        a, b, e = g[co[t]:co[t + 1]], g_fd[co[t]:co[t + 1]], fd_err[co[t]:co[t + 1]]
+        if len(a) == 0:
+            continue
+        scale = max(1.0, float(np.abs(b).max()))
+        if e.max() > 1e-6 * scale:  # finite differences themselves unreliable (strong curvature)
+            continue
+        assert np.all(np.abs(a - b) <= 1e-6 * scale), (t, a, b)
+        n_checked += 1
+    assert n_checked > 50
+    # incomplete trees: L(Inf) and a zero gradient
+    for t in np.nonzero(~comp)[0]:
+        assert np.isinf(loss[t]) and np.all(g[co[t]:co[t + 1]] == 0)
+
+
+def test_population_f32_close_to_f64():
+    # same f32-representable data and constants in both precisions; trees whose f32 loss already
+    # differs from the f64 one (ill-conditioned evaluation) are not a gradient question
+    opts = Options(binary_operators=["+", "-", "*", "/"], unary_operators=["cos", "exp"])
+    X32, y32 = _data(4096, 3, np.float32)
+    tb32 = flatten_trees(gen_random_population(300, opts, 3, seed=6), np.float32)
+    l32, g32, c32 = eval_grad_batch(tb32, Dataset(X32, y32), opts)
+    l64, g64, c64 = eval_grad_batch(tb32.astype(np.float64), Dataset(X32.astype(np.float64), y32.astype(np.float64)), opts)
+    co = tb32.constant_offsets()
+    checked = bad = 0
+    for t in np.nonzero(c32 & c64)[0]:  # (f32 / f64 overflow thresholds differ)
+        a, b = g32[co[t]:co[t + 1]].astype(np.float64), g64[co[t]:co[t + 1]]
+        if len(b) == 0 or not abs(float(l32[t]) - l64[t]) <= 1e-5 * abs(l64[t]):
+            continue
+        checked += 1
+        scale = max(1.0, float(np.abs(b).max()))
+        bad += int(not np.all(np.abs(a - b) <= 1e-2 * scale))
+    assert checked > 100 and bad <= 0.04 * checked, (checked, bad)
+
+
+def test_many_constants_weighted_gather_l1():
+    # more constants than one tangent pass holds (16), weights, a SubDataset view and L1DistLoss
+    opts = Options(binary_operators=["+", "*"], unary_operators=["cos"], elementwise_loss="L1DistLoss")
+    X, y = _data(1000, 4, np.float64)
+    w = np.random.default_rng(9).uniform(0.5, 2.0, 1000)
+    expr = " + ".join(f"{0.1 * (k + 1)} * cos(x{1 + k % 3} + {0.05 * k})" for k in range(10))  # 20 constants
+    tb = flatten_trees([parse_expression(expr, opts)], np.float64)
+    idx = np.random.default_rng(10).integers(0, 1000, 300)
+    ds = Dataset(X, y, weights=w)
+    from sr_amd import SubDataset
+
+    loss, g, comp = eval_grad_batch(tb, SubDataset(ds, idx), opts)
+    g_fd, _, _ = Oracle.from_options(opts).loss_grad_fd(tb, X[:, idx], y[idx], w[idx], loss_kind=1)
+    assert comp[0] and len(g) == 20
+    np.testing.assert_allclose(g, g_fd, rtol=1e-5, atol=1e-6)
