@@ -7,6 +7,7 @@ score a whole population in one device launch.  All evaluation runs in ``libsr_a
 """
 from . import _lib
 from ._lib import SRError, UnsupportedOperatorError
+from .constant_optimization import optimize_constants_batch
 from .dataset import Dataset, SubDataset, batch
 from .device import DeviceContext, device_available, get_context
 from .loss import (
@@ -45,5 +46,5 @@ __all__ = [
     "eval_loss", "eval_loss_batch", "eval_grad_batch", "eval_cost", "eval_cost_batch", "loss_to_cost",
     "update_baseline_loss_", "score_func", "compute_complexity", "gen_random_tree_fixed_size",
     "gen_random_population", "make_random_leaf", "get_context", "device_available", "DeviceContext",
-    "SRError", "UnsupportedOperatorError",
+    "SRError", "UnsupportedOperatorError", "optimize_constants_batch",
 ]

@@ -36,6 +36,10 @@ class Options:
         tournament_selection_p: float = 0.982,
         batching: bool = False,
         batch_size: int = 50,
+        should_optimize_constants: bool = True,
+        optimizer_probability: float = 0.14,
+        optimizer_nrestarts: int = 2,
+        optimizer_iterations: int | None = None,
         turbo: bool = False,
         bumper: bool = False,
         device: str = "mi355x",
@@ -61,6 +65,11 @@ class Options:
         self.tournament_selection_p = tournament_selection_p
         self.batching = batching
         self.batch_size = batch_size
+        # constant optimisation (src/Options.jl:613-619, 988-997)
+        self.should_optimize_constants = should_optimize_constants
+        self.optimizer_probability = optimizer_probability
+        self.optimizer_nrestarts = optimizer_nrestarts
+        self.optimizer_iterations = 8 if optimizer_iterations is None else int(optimizer_iterations)
         self.turbo = turbo
         self.bumper = bumper
         if device not in ("mi355x", "gpu", "hip"):

@@ -114,3 +114,33 @@ def test_many_constants_weighted_gather_l1():
     g_fd, _, _ = Oracle.from_options(opts).loss_grad_fd(tb, X[:, idx], y[idx], w[idx], loss_kind=1)
     assert comp[0] and len(g) == 20
     np.testing.assert_allclose(g, g_fd, rtol=1e-5, atol=1e-6)
+
+
+def test_bfgs_batch_recovers_constants():
+    # batched BFGS / Newton (src/ConstantOptimization.jl:29-116) on trees whose optimum is known
+    from sr_amd import optimize_constants_batch
+
+    opts = Options(binary_operators=["+", "-", "*", "/"], unary_operators=["cos", "exp"])
+    rng = np.random.default_rng(11)
+    X = rng.standard_normal((3, 2000)).astype(np.float64)
+    y = 3.0 * X[0] + 1.5
+    trees = [parse_expression("1.0 * x1 + 1.0", opts),      # BFGS, 2 constants -> (3, 1.5)
+             parse_expression("x1 * 1.0", opts),             # Newton, 1 constant -> 3 (+ residual)
+             parse_expression("cos(x2) * 0.5", opts),        # nothing to gain much
+             parse_expression("x1 * x2", opts)]              # no constants
+    tb = flatten_trees(trees, np.float64)
+    ds = Dataset(X, y)
+    from sr_amd import eval_loss_batch
+
+    l0, _ = eval_loss_batch(tb, ds, opts)
+    new_tb, losses, improved, n_evals = optimize_constants_batch(tb, ds, opts, np.random.default_rng(0))
+    c = new_tb.get_constants()
+    assert improved[0] and improved[1] and not improved[3]
+    np.testing.assert_allclose(c[0:2], [3.0, 1.5], rtol=1e-6)
+    assert abs(c[2] - 3.0) < 0.1
+    assert losses[0] < 1e-10 and np.all(losses <= l0 + 1e-12)
+    assert np.all(n_evals[:2] > 1)
+    # a not-improved tree keeps its constants exactly
+    for k in np.nonzero(~improved)[0]:
+        co = tb.constant_offsets()
+        np.testing.assert_array_equal(new_tb.get_constants()[co[k]:co[k + 1]], tb.get_constants()[co[k]:co[k + 1]])
