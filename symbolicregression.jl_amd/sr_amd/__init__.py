@@ -38,6 +38,7 @@ from .node import (
 )
 from .operators import OperatorEnum
 from .options import Options
+from .search import HallOfFame, PopMember, RunningSearchStatistics, SearchOptions, equation_search
 
 __all__ = [
     "Options", "OperatorEnum", "Dataset", "SubDataset", "batch", "Node", "TreeBatch", "flatten_trees",
@@ -46,5 +47,6 @@ __all__ = [
     "eval_loss", "eval_loss_batch", "eval_grad_batch", "eval_cost", "eval_cost_batch", "loss_to_cost",
     "update_baseline_loss_", "score_func", "compute_complexity", "gen_random_tree_fixed_size",
     "gen_random_population", "make_random_leaf", "get_context", "device_available", "DeviceContext",
-    "SRError", "UnsupportedOperatorError", "optimize_constants_batch",
+    "SRError", "UnsupportedOperatorError", "optimize_constants_batch", "equation_search", "SearchOptions",
+    "PopMember", "HallOfFame", "RunningSearchStatistics",
 ]

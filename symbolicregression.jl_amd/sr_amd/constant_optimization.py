@@ -63,6 +63,11 @@ class _Objective:
 
 def _backtracking_step(phi0, dphi0, a1, a2, phix0, phix1, iteration):
     """One LineSearches.BackTracking (order 3) interpolation: the next trial step."""
+    with np.errstate(all="ignore"):
+        return _backtracking_step_impl(phi0, dphi0, a1, a2, phix0, phix1, iteration)
+
+
+def _backtracking_step_impl(phi0, dphi0, a1, a2, phix0, phix1, iteration):
     if iteration == 1:  # quadratic interpolation
         den = 2.0 * (phix1 - phi0 - dphi0 * a2)
         a_tmp = -(dphi0 * a2 * a2) / den if den != 0 else a2 * 0.5
