@@ -266,37 +266,38 @@ struct TreeCompiler {
 
   // Leaf as a LOAD (push = false; PUSH is patched in later) or as a binary operand.
   // is_operand: binary opcode base (variant FL/FR/CL/CR chosen from the leaf kind + side).
-  static constexpr uint32_t kNoSlot = 0xffffffffu;
+  static constexpr uint32_t kNoSlot = SR_M_INDEX;
 
   SrIns<T> leaf_ins(int i) {
     SrIns<T> in{};
-    in.cslot = kNoSlot;
+    in.meta = kNoSlot;
     if (folded[i]) {
-      in.w0 = SR_OP_LOAD_CONST;
+      in.op = SR_OP_LOAD_CONST;
       in.set_value(fold_val[i]);
     } else if (t.constant[i]) {
-      in.w0 = SR_OP_LOAD_CONST;
+      in.op = SR_OP_LOAD_CONST;
       in.set_value(t.val[i]);
-      if (with_const_index) in.cslot = uint32_t(const_slot[i]);
+      if (with_const_index) in.meta = uint32_t(const_slot[i]);
     } else {
-      in.w0 = SR_OP_LOAD_FEAT | ((uint32_t(t.feature[i]) - 1u) << SR_W_OPND_SHIFT);
+      in.op = SR_OP_LOAD_FEAT;
+      in.meta = uint32_t(t.feature[i]) - 1u;
     }
     return in;
   }
   static bool commutes(uint32_t bop) { return bop == SR_B_ADD || bop == SR_B_MUL; }
   SrIns<T> operand_ins(int i, uint32_t bop, bool left) {
     SrIns<T> in = leaf_ins(i);
-    const bool is_const = in.opcode() == SR_OP_LOAD_CONST;
+    const bool is_const = in.op == SR_OP_LOAD_CONST;
     if (commutes(bop)) left = false;  // IEEE + and * commute: one variant per operand kind
     const uint32_t v = is_const ? (left ? SR_V_CL : SR_V_CR) : (left ? SR_V_FL : SR_V_FR);
-    in.w0 = (in.w0 & ~SR_W_OPC) | SR_BIN_OPC(bop, v);
+    in.op = SR_BIN_OPC(bop, v);
     return in;
   }
   SrIns<T> stack_ins(uint32_t bop, bool left, int slot) {
     SrIns<T> in{};
-    in.cslot = kNoSlot;
     if (commutes(bop)) left = false;
-    in.w0 = SR_BIN_OPC(bop, left ? SR_V_SL : SR_V_SR) | (uint32_t(slot) << SR_W_OPND_SHIFT);
+    in.op = SR_BIN_OPC(bop, left ? SR_V_SL : SR_V_SR);
+    in.meta = uint32_t(slot);
     return in;
   }
 
@@ -306,7 +307,7 @@ struct TreeCompiler {
       static_array_check(folded[i] ? fold_val[i] : t.val[i]);
       return;
     }
-    code.back().w0 |= SR_W_CHECK;
+    code.back().meta |= SR_M_CHECK;
     ++n_checks;
   }
 
@@ -317,7 +318,8 @@ struct TreeCompiler {
       fail(SR_ERR_TOO_DEEP, "tree needs more operand-stack slots than the encoding holds");
       return;
     }
-    in.w0 |= uint32_t(slot + 1) << SR_W_PUSH_SHIFT;
+    in.op += SR_OP_LOAD_FEAT_PUSH - SR_OP_LOAD_FEAT;  // LOAD_x -> LOAD_x_PUSH
+    in.meta |= uint32_t(slot + 1) << SR_M_PUSH_SHIFT;
   }
 
   void emit(int i) {
@@ -331,9 +333,8 @@ struct TreeCompiler {
     if (d == 1) {
       emit(t.l[i]);
       SrIns<T> in{};
-      in.cslot = kNoSlot;
-      in.w0 = SR_OP_UNARY0 + unary_id(i);
-      if (infsub[i]) in.w0 |= SR_W_INFSUB;  // fused unary: non-finite input -> +Inf
+      // fused unary: non-finite input -> +Inf
+      in.op = (infsub[i] ? SR_OP_UNARY_INF0 : SR_OP_UNARY0) + unary_id(i);
       code.push_back(in);
       emit_check(i);
       return;
@@ -403,18 +404,17 @@ struct TreeCompiler {
 
 }  // namespace
 
-uint32_t sr_instruction_cost(uint32_t w0) {
-  const uint32_t code = w0 & SR_W_OPC;
+uint32_t sr_instruction_cost(uint32_t code) {
   uint32_t c = 6;  // dispatch + operand fetch + validity tracking
-  if (w0 & SR_W_INFSUB) c += 2;
-  if (w0 & SR_W_PUSH_MASK) c += 2;
+  if (code == SR_OP_LOAD_FEAT_PUSH || code == SR_OP_LOAD_CONST_PUSH) c += 2;
   if (code >= SR_OP_BINARY0) {
     const uint32_t b = (code - SR_OP_BINARY0) / 6u + 1u;
     if (b == SR_B_DIV) c += 10;
     else if (b == SR_B_ADD || b == SR_B_SUB || b == SR_B_MUL) c += 1;
     else c += 20;
-  } else if (code >= SR_OP_UNARY0 + 1u) {
-    const uint32_t u = code - SR_OP_UNARY0;
+  } else if (code > SR_OP_UNARY0) {
+    const uint32_t u = code >= SR_OP_UNARY_INF0 ? code - SR_OP_UNARY_INF0 : code - SR_OP_UNARY0;
+    if (code >= SR_OP_UNARY_INF0) c += 2;
     switch (u) {
       case SR_U_NEG: case SR_U_SQUARE: case SR_U_CUBE: case SR_U_ABS: c += 2; break;
       case SR_U_EXP: c += 14; break;
@@ -481,7 +481,7 @@ int sr_compile_batch(const sr_tree_batch& trees, const SrOpset& ops, int64_t n_r
         continue;
       }
       uint32_t cost = 0;
-      for (const auto& in : tc.code) cost += sr_instruction_cost(in.w0);
+      for (const auto& in : tc.code) cost += sr_instruction_cost(in.op);
       PerTree& p = per[k];
       p.cost = cost;
       p.code.swap(tc.code);

@@ -48,7 +48,7 @@ struct SrProgramBatch {
 // `arg` of CONST loads (gradient kernels).  Returns SR_OK or an error code with *err set.
 // Estimated cost of one program instruction on the device, in VALU-instruction-like units per row
 // step (dispatch overhead included): used only to order trees for load balance.
-uint32_t sr_instruction_cost(uint32_t w0);
+uint32_t sr_instruction_cost(uint32_t opcode);
 
 template <typename T>
 int sr_compile_batch(const sr_tree_batch& trees, const SrOpset& ops, int64_t n_rows, int64_t nfeatures,

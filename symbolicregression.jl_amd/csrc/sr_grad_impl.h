@@ -105,9 +105,9 @@ __global__ void __launch_bounds__(W * 64) sr_grad_kernel(const SrGradArgs<T> a) 
         if (base + lane < pe) cw = sr_load_window(a.code, base + lane);
         const uint32_t n_here = __builtin_amdgcn_readfirstlane((pe - base < 64u) ? pe - base : 64u);
         for (uint32_t k = 0; k < n_here; ++k) {
-          const uint32_t w0 = uint32_t(__builtin_amdgcn_readlane(int(cw.x), int(k)));
-          const uint32_t opc = w0 & SR_W_OPC;
-          const uint32_t cs = uint32_t(__builtin_amdgcn_readlane(int(cw.w), int(k)));
+          const uint32_t opc = uint32_t(__builtin_amdgcn_readlane(int(cw.x), int(k)));
+          const uint32_t meta = uint32_t(__builtin_amdgcn_readlane(int(cw.w), int(k)));
+          const uint32_t idx = meta & SR_M_INDEX;  // feature / stack slot / constant slot
           // operand (value + tangents): feature / stack slot / constant
           T ov = T(0);
           T od[KT];
@@ -115,24 +115,25 @@ __global__ void __launch_bounds__(W * 64) sr_grad_kernel(const SrGradArgs<T> a) 
           for (int q = 0; q < KT; ++q) od[q] = T(0);
           uint32_t variant = 6u;
           if (opc >= SR_OP_BINARY0) variant = (opc - SR_OP_BINARY0) % 6u;
-          const bool load = opc <= SR_OP_LOAD_CONST;
-          if ((load && opc == SR_OP_LOAD_FEAT) || variant == SR_V_FL || variant == SR_V_FR) {
-            ov = xs[(w0 >> SR_W_OPND_SHIFT) * ROWS + r];
-          } else if ((load && opc == SR_OP_LOAD_CONST) || variant == SR_V_CL || variant == SR_V_CR) {
-            // constant slot cs: value from the tree's constant array, tangent e_{cs-k0}
-            ov = cs < 64u ? sr_readlane_val<T>(cval0, cs) : sr_readlane_val<T>(cval1, cs - 64u);
-            const int jj = int(cs) - int(k0);
+          const bool load = opc <= SR_OP_LOAD_CONST_PUSH;
+          const bool load_feat = opc == SR_OP_LOAD_FEAT || opc == SR_OP_LOAD_FEAT_PUSH;
+          if ((load && load_feat) || variant == SR_V_FL || variant == SR_V_FR) {
+            ov = xs[idx * ROWS + r];
+          } else if (load || variant == SR_V_CL || variant == SR_V_CR) {
+            // constant slot idx: value from the tree's constant array, tangent e_{idx-k0}
+            ov = idx < 64u ? sr_readlane_val<T>(cval0, idx) : sr_readlane_val<T>(cval1, idx - 64u);
+            const int jj = int(idx) - int(k0);
 #pragma unroll
             for (int q = 0; q < KT; ++q) od[q] = (q == jj) ? T(1) : T(0);
           } else if (variant == SR_V_SL || variant == SR_V_SR) {
-            const T* sp = my_stk + size_t(w0 >> SR_W_OPND_SHIFT) * NV * 64;
+            const T* sp = my_stk + size_t(idx) * NV * 64;
             ov = sp[0];
 #pragma unroll
             for (int q = 0; q < KT; ++q) od[q] = sp[(q + 1) * 64];
           }
           if (load) {
-            if (w0 & SR_W_PUSH_MASK) {
-              T* sp = my_stk + size_t(((w0 >> SR_W_PUSH_SHIFT) & 0x3fu) - 1u) * NV * 64;
+            if (opc >= SR_OP_LOAD_FEAT_PUSH) {
+              T* sp = my_stk + size_t(((meta >> SR_M_PUSH_SHIFT) & 0x3fu) - 1u) * NV * 64;
               sp[0] = v;
 #pragma unroll
               for (int q = 0; q < KT; ++q) sp[(q + 1) * 64] = dv[q];
@@ -141,7 +142,7 @@ __global__ void __launch_bounds__(W * 64) sr_grad_kernel(const SrGradArgs<T> a) 
 #pragma unroll
             for (int q = 0; q < KT; ++q) dv[q] = od[q];
           } else if (opc < SR_OP_BINARY0) {
-            const uint32_t u = opc - SR_OP_UNARY0;
+            const uint32_t u = opc >= SR_OP_UNARY_INF0 ? opc - SR_OP_UNARY_INF0 : opc - SR_OP_UNARY0;
             const T x = v;
             const T yv = sr_unary<T>(u, x);
             // (fused unaries: complete trees have finite inner values, so INFSUB never fires)

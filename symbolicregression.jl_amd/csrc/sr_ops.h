@@ -50,45 +50,48 @@ enum SrLossKind : int32_t {
 
 // ---------------------------------------------------------------------------------------
 // Program instruction: one per evaluated node (a leaf that is a binary node's operand is folded into
-// that node's instruction), 16 bytes for f32 and f64 alike.
-//   w0 bits  0-7  : opcode
+// that node's instruction), 16 bytes for f32 and f64 alike.  The interpreter dispatches on `op`
+// as read (no decoding): every variant is its own opcode.
+//   op   : opcode
 //       SR_OP_LOAD_FEAT  tos <- X[f]          SR_OP_LOAD_CONST  tos <- c
-//         (push field != 0: the old tos is first stored to stack slot push-1)
-//       SR_OP_UNARY0 + u                               tos <- op_u(tos)
+//       SR_OP_LOAD_FEAT_PUSH / _CONST_PUSH: the old tos is first stored to stack slot `push`
+//       SR_OP_UNARY0 + u      tos <- op_u(tos)
+//       SR_OP_UNARY_INF0 + u  tos <- isfinite(tos) ? op_u(tos) : +Inf — DynamicExpressions' fused
+//                             unary kernels (deg1_l2_ll0_lr0 / deg1_l1_ll0)
 //       SR_OP_BINARY0 + 6*(b-1) + variant              tos <- op_b(.,.) with operand variant:
 //           SR_V_SL: op(S[k], tos)  SR_V_SR: op(tos, S[k])   (S[k] = stack slot k, popped)
 //           SR_V_FL: op(X[f], tos)  SR_V_FR: op(tos, X[f])
 //           SR_V_CL: op(c, tos)     SR_V_CR: op(tos, c)
 //         + and * only ever use the R variants (the compiler canonicalises: IEEE + and * commute)
-//   w0 bit   8    : CHECK   this node's output array is validity-checked (DE early exit)
-//   w0 bit   9    : INFSUB  (unary) tos <- isfinite(tos) ? op_u(tos) : +Inf — DynamicExpressions'
-//                   fused unary kernels (deg1_l2_ll0_lr0 / deg1_l1_ll0)
-//   w0 bits 10-15 : push slot + 1 (LOAD only; 0 = no push)
-//   w0 bits 16-31 : operand index: 0-based feature f (F variants, LOAD_FEAT) or stack slot k
-//                   (S variants); stack depths are static, so the compiler assigns the slots
-//   c0 (, c1)     : constant bits (C variants, LOAD_CONST): f32 in c0, f64 in c0 | c1 << 32
-//   cslot         : pre-order constant index of a constant leaf (gradient programs), else ~0
+//   c0 (, c1) : constant bits (C variants, LOAD_CONST*): f32 in c0, f64 in c0 | c1 << 32
+//   meta bits  0-15 : operand index: feature f (F variants, LOAD_FEAT*), stack slot k (S variants),
+//                     pre-order constant slot of a constant leaf (gradient programs; else 0xffff)
+//   meta bits 24-29 : push slot + 1 (LOAD_*_PUSH)
+//   meta bit  31    : CHECK   this node's output array is validity-checked (DE early exit)
+//   (bits 16-23 stay 0, so `meta << s` with s >= 8 is the operand's byte offset for a row stride
+//    of 2^s bytes: the flag bits shift out)
 // ---------------------------------------------------------------------------------------
 enum : uint32_t {
-  SR_OP_LOAD_FEAT = 0u, SR_OP_LOAD_CONST = 1u,
-  SR_OP_UNARY0 = 2u,    // opcode = SR_OP_UNARY0 + SrUnaryOp (1..)
-  SR_OP_BINARY0 = 64u,  // opcode = SR_OP_BINARY0 + 6*(SrBinaryOp-1) + variant
+  SR_OP_LOAD_FEAT = 0u, SR_OP_LOAD_CONST = 1u, SR_OP_LOAD_FEAT_PUSH = 2u, SR_OP_LOAD_CONST_PUSH = 3u,
+  SR_OP_UNARY0 = 4u,       // opcode = SR_OP_UNARY0 + SrUnaryOp (1..)
+  SR_OP_UNARY_INF0 = 40u,  // opcode = SR_OP_UNARY_INF0 + SrUnaryOp (fused: non-finite input -> +Inf)
+  SR_OP_BINARY0 = 80u,     // opcode = SR_OP_BINARY0 + 6*(SrBinaryOp-1) + variant
   SR_V_SL = 0u, SR_V_SR = 1u, SR_V_FL = 2u, SR_V_FR = 3u, SR_V_CL = 4u, SR_V_CR = 5u,
-  SR_W_OPC = 0xffu, SR_W_CHECK = 1u << 8, SR_W_INFSUB = 1u << 9,
-  SR_W_PUSH_SHIFT = 10u, SR_W_PUSH_MASK = 0x3fu << 10, SR_W_OPND_SHIFT = 16u,
+  SR_M_INDEX = 0xffffu, SR_M_PUSH_SHIFT = 24u, SR_M_PUSH_MASK = 0x3fu << 24, SR_M_CHECK = 1u << 31,
   SR_MAX_STACK_SLOTS = 62u,
 };
-static_assert(SR_OP_UNARY0 + SR_U_COUNT <= SR_OP_BINARY0, "unary opcode range overlaps the binary range");
+static_assert(SR_OP_UNARY0 + SR_U_COUNT <= SR_OP_UNARY_INF0, "unary opcode ranges overlap");
+static_assert(SR_OP_UNARY_INF0 + SR_U_COUNT <= SR_OP_BINARY0, "unary opcode range overlaps the binary range");
 static_assert(SR_OP_BINARY0 + 6 * SR_B_COUNT <= 256, "binary opcode range exceeds 8 bits");
 #define SR_BIN_OPC(b, v) (SR_OP_BINARY0 + 6u * ((b) - 1u) + (v))
 
 template <typename T>
 struct alignas(16) SrIns {
-  uint32_t w0;
+  uint32_t op;
   uint32_t c0, c1;
-  uint32_t cslot;
-  SR_HD inline uint32_t opcode() const { return w0 & SR_W_OPC; }
-  SR_HD inline uint32_t operand() const { return w0 >> SR_W_OPND_SHIFT; }
+  uint32_t meta;
+  SR_HD inline uint32_t operand() const { return meta & SR_M_INDEX; }
+  SR_HD inline int push_slot() const { return int((meta >> SR_M_PUSH_SHIFT) & 0x3fu) - 1; }
   SR_HD inline T value() const {
     if constexpr (sizeof(T) == 4) {
       return __builtin_bit_cast(T, c0);

@@ -27,6 +27,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <type_traits>
+
 #include "sr_eval.h"
 #include "sr_ops.h"
 
@@ -164,6 +166,18 @@ __device__ __forceinline__ T sr_lane_value(uint32_t wc0, uint32_t wc1, uint32_t 
   }
 }
 
+// Row `meta & SR_M_INDEX` of a [.][ROWS] LDS array: the byte offset is meta << log2(ROWS*sizeof(T))
+// in 32 bits, which drops meta's flag bits (24..31) since the shift is >= 8.
+template <int ROWS, typename P>
+__device__ __forceinline__ P* sr_row_at(P* base, uint32_t meta) {
+  constexpr uint32_t bytes = uint32_t(ROWS * sizeof(P));
+  constexpr uint32_t sh = bytes >= 8192u ? 13u : bytes >= 4096u ? 12u : bytes >= 2048u ? 11u
+                        : bytes >= 1024u ? 10u : bytes >= 512u ? 9u : 8u;
+  static_assert((1u << sh) == bytes, "row stride must be a power of two >= 256 bytes");
+  using B = typename std::conditional<std::is_const<P>::value, const char, char>::type;
+  return reinterpret_cast<P*>(reinterpret_cast<B*>(base) + (meta << sh));
+}
+
 // ------------------------------------------------------------------ dispatch cases
 #define SR_EACH(EXPR)                             \
   _Pragma("unroll") for (int r = 0; r < R; ++r) { \
@@ -184,23 +198,27 @@ __device__ __forceinline__ T sr_lane_value(uint32_t wc0, uint32_t wc1, uint32_t 
       if (r + 3 < R) mrun1 = SrMaxAbs<T>::step(mrun1, tos[r + 2], tos[r + 3]); \
     }                                                                     \
   }
-#define SR_UCASE_GEN(ID, ENABLED)                                   \
-  case SR_OP_UNARY0 + ID: {                                         \
-    if (ENABLED) {                                                  \
-      if (w0 & SR_W_INFSUB) {                                       \
-        SR_EACH(sr_isfinite(x) ? sr_unary<T>(ID, x) : sr_inf<T>()); \
-      } else {                                                      \
-        SR_EACH(sr_unary<T>(ID, x));                                \
-      }                                                             \
-      SR_TRACK();                                                   \
-    }                                                               \
-    break;                                                          \
+#define SR_UCASE_GEN(ID, ENABLED)                                 \
+  case SR_OP_UNARY0 + ID: {                                       \
+    if (ENABLED) {                                                \
+      SR_EACH(sr_unary<T>(ID, x));                                \
+      SR_TRACK();                                                 \
+    }                                                             \
+    break;                                                        \
+  }                                                               \
+  case SR_OP_UNARY_INF0 + ID: {                                   \
+    if (ENABLED) {                                                \
+      SR_EACH(sr_isfinite(x) ? sr_unary<T>(ID, x) : sr_inf<T>()); \
+      SR_TRACK();                                                 \
+    }                                                             \
+    break;                                                        \
   }
 #define SR_UCASE(ID) SR_UCASE_GEN(ID, true)
 #define SR_UCASE_FULL(ID) SR_UCASE_GEN(ID, TIER == SR_TIER_FULL)
-// operand addresses: stack slot / feature row in w0's operand field; constants from the c words
-#define SR_OPND_STK() (stk_lane + (w0 >> SR_W_OPND_SHIFT) * ROWS)
-#define SR_OPND_X() (x_lane + (w0 >> SR_W_OPND_SHIFT) * ROWS)
+// operand addresses: stack slot / feature row from the instruction's meta word (one shift: the
+// flag bits above the index shift out of the 32-bit byte offset); constants from the c words
+#define SR_OPND_STK() sr_row_at<ROWS>(stk_lane, SR_META())
+#define SR_OPND_X() sr_row_at<ROWS>(x_lane, SR_META())
 #define SR_BCASE_R(ID, ENABLED)        \
   case SR_BIN_OPC(ID, SR_V_SR): {      \
     if (ENABLED) {                     \
@@ -437,21 +455,28 @@ __global__ void __launch_bounds__(W * 64, SrMinWaves<W>::value) sr_tile_kernel(c
       const int g = wave + SR_WAVES * j;
 
       if (!dead) {
-        const uint32_t wop = cw.x, wc0 = cw.y, wc1 = cw.z;
+        const uint32_t wop = cw.x, wc0 = cw.y, wc1 = cw.z, wmeta = cw.w;
         const uint32_t n_here = __builtin_amdgcn_readfirstlane((tpe - base < 64u) ? tpe - base : 64u);
         // single-exit loop (a dead tree sets k past the window): a second loop exit would make
         // LLVM add an exit-selector block to every iteration
         for (uint32_t k = 0; k < n_here; ++k) {
-          const uint32_t w0 = uint32_t(__builtin_amdgcn_readlane(int(wop), int(k)));
+          const uint32_t op = uint32_t(__builtin_amdgcn_readlane(int(wop), int(k)));
 #define SR_CVAL() sr_lane_value<T>(wc0, wc1, k)
-          switch (w0 & SR_W_OPC) {
+#define SR_META() uint32_t(__builtin_amdgcn_readlane(int(wmeta), int(k)))
+#define SR_PUSH_TOS()                                                                      \
+  L::store(sr_row_at<ROWS>(stk_lane, ((SR_META() >> SR_M_PUSH_SHIFT) & 0x3fu) - 1u), tos)
+          switch (op) {
+            case SR_OP_LOAD_FEAT_PUSH:
+              SR_PUSH_TOS();
+              [[fallthrough]];
             case SR_OP_LOAD_FEAT: {
-              if (w0 & SR_W_PUSH_MASK) L::store(stk_lane + (((w0 >> SR_W_PUSH_SHIFT) & 0x3fu) - 1u) * ROWS, tos);
               L::load(SR_OPND_X(), tos);
               break;
             }
+            case SR_OP_LOAD_CONST_PUSH:
+              SR_PUSH_TOS();
+              [[fallthrough]];
             case SR_OP_LOAD_CONST: {
-              if (w0 & SR_W_PUSH_MASK) L::store(stk_lane + (((w0 >> SR_W_PUSH_SHIFT) & 0x3fu) - 1u) * ROWS, tos);
               const T cv = SR_CVAL();
 #pragma unroll
               for (int r = 0; r < R; ++r) tos[r] = cv;
@@ -479,7 +504,8 @@ __global__ void __launch_bounds__(W * 64, SrMinWaves<W>::value) sr_tile_kernel(c
               break;
           }
 #undef SR_CVAL
-          if (!FAST_CHECK && (w0 & SR_W_CHECK)) {
+#undef SR_PUSH_TOS
+          if (!FAST_CHECK && (SR_META() & SR_M_CHECK)) {
             if (MODE == SR_MODE_EXACT) {
               double s = 0.0;
 #pragma unroll

@@ -1,7 +1,7 @@
 """TEST HELPER: a numpy interpreter of libsr_amd's compiled programs (csrc/sr_ops.h encoding).
 
 It executes exactly the instruction semantics of the HIP kernel (top-of-stack + statically
-assigned operand-stack slots, combined opcodes, the push field and the INFSUB / CHECK bits of w0) on
+assigned operand-stack slots, combined opcodes, the push field and CHECK bit of the meta word) on
 the CPU, so CPU tests can validate the tree COMPILER
 (constant folding, check placement, fused-unary detection, Sethi–Ullman ordering) against the
 oracle without a GPU.  It is not part of the product and is never used as a fallback.
@@ -28,8 +28,8 @@ def compile_info(options, tb, n_rows, nfeatures, dtype):
     s = tb.to_struct()
     dt = _lib.SR_DTYPE_F32 if dtype == np.float32 else _lib.SR_DTYPE_F64
     cap = int(tb.n_nodes) + 16
-    rec = np.dtype([("w0", "<u4"), ("val", "<f4"), ("c1", "<u4"), ("cslot", "<u4")]) if dtype == np.float32 else \
-        np.dtype([("w0", "<u4"), ("val", "<f8"), ("cslot", "<u4")], align=False)
+    rec = np.dtype([("op", "<u4"), ("val", "<f4"), ("c1", "<u4"), ("meta", "<u4")]) if dtype == np.float32 else \
+        np.dtype([("op", "<u4"), ("val", "<f8"), ("meta", "<u4")], align=False)
     code = np.zeros(cap, dtype=rec)
     _lib.check(_lib.lib.sr_compile_info(dt, len(options.operators.unaops), un, len(options.operators.binops), bi,
                                         ctypes.byref(s), n_rows, nfeatures, lens.ctypes.data_as(ctypes.c_void_p),
@@ -75,22 +75,26 @@ def _binary(bid, a, b):
     raise NotImplementedError(bid)
 
 
-# w0 fields (csrc/sr_ops.h)
-OPC = 0xFF
-CHECK = 1 << 8
-INFSUB = 1 << 9
+# opcode ranges and meta fields (csrc/sr_ops.h)
+LOAD_FEAT, LOAD_CONST, LOAD_FEAT_PUSH, LOAD_CONST_PUSH = 0, 1, 2, 3
+UNARY0, UNARY_INF0, BINARY0 = 4, 40, 80
+CHECK = 1 << 31
 
 
-def opcode(w0):
-    return int(w0) & OPC
+def operand(meta):
+    return int(meta) & 0xFFFF
 
 
-def operand(w0):
-    return int(w0) >> 16
+def push_slot(meta):
+    return ((int(meta) >> 24) & 0x3F) - 1
 
 
-def push_slot(w0):
-    return ((int(w0) >> 10) & 0x3F) - 1
+def is_check(meta):
+    return (int(meta) >> 31) & 1
+
+
+def is_infsub(op):
+    return UNARY_INF0 <= int(op) < BINARY0
 
 
 def run_program(code, lo, hi, X, T):
@@ -101,30 +105,34 @@ def run_program(code, lo, hi, X, T):
     complete = True
     big = T(np.finfo(T).max)
     for pc in range(lo, hi):
-        w0 = int(code["w0"][pc])
-        opc = opcode(w0)
+        opc = int(code["op"][pc])
+        meta = int(code["meta"][pc])
         val = T(code["val"][pc])
-        if opc <= 1:  # LOAD_FEAT / LOAD_CONST, optionally pushing the old tos first
-            if push_slot(w0) >= 0:
-                slots[push_slot(w0)] = tos
-            tos = X[operand(w0)].astype(T) if opc == 0 else np.full(n, val, dtype=T)
-        elif opc < 64:
-            v = _unary(opc - 2, tos, T).astype(T)
-            if w0 & INFSUB:  # fused unary: non-finite input -> +Inf
+        if opc < UNARY0:  # LOAD_FEAT / LOAD_CONST, the _PUSH forms storing the old tos first
+            if opc >= LOAD_FEAT_PUSH:
+                assert push_slot(meta) >= 0
+                slots[push_slot(meta)] = tos
+            else:
+                assert push_slot(meta) < 0
+            tos = X[operand(meta)].astype(T) if opc in (LOAD_FEAT, LOAD_FEAT_PUSH) else np.full(n, val, dtype=T)
+        elif opc < BINARY0:
+            inf = is_infsub(opc)
+            v = _unary(opc - (UNARY_INF0 if inf else UNARY0), tos, T).astype(T)
+            if inf:  # fused unary: non-finite input -> +Inf
                 v = np.where(np.isfinite(tos), v, T(np.inf)).astype(T)
             tos = v
         else:
-            bid, v = divmod(opc - 64, 6)
+            bid, v = divmod(opc - BINARY0, 6)
             bid += 1
             if v in (0, 1):
-                o = slots.pop(operand(w0))
+                o = slots.pop(operand(meta))
             elif v in (2, 3):
-                o = X[operand(w0)].astype(T)
+                o = X[operand(meta)].astype(T)
             else:
                 o = np.full(n, val, dtype=T)
             a, b = (o, tos) if v in (0, 2, 4) else (tos, o)
             tos = _binary(bid, a, b).astype(T)
-        if w0 & CHECK:  # isfinite(sum(array)) (f64 sum)
+        if is_check(meta):  # isfinite(sum(array)) (f64 sum)
             s = np.sum(tos.astype(np.float64))
             if not np.isfinite(tos).all() or not abs(s) <= float(big):
                 complete = False

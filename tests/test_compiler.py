@@ -59,25 +59,25 @@ def test_program_shapes():
     assert not bad.any()
     # CHECK bit placement: cos(x1) is a general unary -> x1's array is checked; root always checked
     k = list(cases).index("cos(x1) + cos(x2)")
-    w = [int(v) for v in code["w0"][offs[k]:offs[k + 1]]]
-    assert [(v >> 8) & 1 for v in w] == [1, 1, 1, 1, 1]
-    # LOAD x1, COS, LOAD x2 pushing cos(x1) to slot 0, COS, ADD with slot 0 (commuted: R variant)
-    assert [vm.opcode(v) for v in w] == [0, 2 + 5, 0, 2 + 5, 64 + 1]
-    assert [vm.push_slot(v) for v in w] == [-1, -1, 0, -1, -1]
-    assert vm.operand(w[4]) == 0 and vm.operand(w[2]) == 1
-    # fused unary: cos(x1 * 2.0) -> LOAD x1, MUL c, COS with INFSUB; no CHECK on the inner product
+    ops = [int(v) for v in code["op"][offs[k]:offs[k + 1]]]
+    meta = [int(v) for v in code["meta"][offs[k]:offs[k + 1]]]
+    assert [vm.is_check(m) for m in meta] == [1, 1, 1, 1, 1]
+    # LOAD x1, COS, LOAD_PUSH x2 (cos(x1) to slot 0), COS, ADD with slot 0 (commuted: R variant)
+    assert ops == [0, 4 + 5, 2, 4 + 5, 80 + 1]
+    assert [vm.push_slot(m) for m in meta] == [-1, -1, 0, -1, -1]
+    assert vm.operand(meta[4]) == 0 and vm.operand(meta[2]) == 1
+    # fused unary: cos(x1 * 2.0) -> LOAD x1, MUL c, INF-COS; no CHECK on the inner product
     tb2 = flatten_trees([parse_expression("cos(x1 * 2.0)", opts)], np.float32)
     code2, offs2, _, depth2 = vm.compile_info(opts, tb2, 100, 5, np.float32)
-    w2 = [int(v) for v in code2["w0"][:offs2[1]]]
-    assert [vm.opcode(v) for v in w2] == [0, 64 + 6 * 2 + 5, 2 + 5]
-    assert [(v >> 8) & 1 for v in w2] == [0, 0, 1]
-    assert [(v >> 9) & 1 for v in w2] == [0, 0, 1]
+    ops2 = [int(v) for v in code2["op"][:offs2[1]]]
+    meta2 = [int(v) for v in code2["meta"][:offs2[1]]]
+    assert ops2 == [0, 80 + 6 * 2 + 5, 40 + 5]
+    assert [vm.is_check(m) for m in meta2] == [0, 0, 1]
     assert depth2 == 0  # the fused unary needs no stack slot
     # non-commutative stack operand keeps its side: (x1 - cos(x2)) - exp(x3) style trees
     tb3 = flatten_trees([parse_expression("cos(x1) - exp(x2)", opts)], np.float32)
     code3, offs3, _, _ = vm.compile_info(opts, tb3, 100, 5, np.float32)
-    w3 = [int(v) for v in code3["w0"][:offs3[1]]]
-    assert vm.opcode(w3[-1]) == 64 + 6 * 1 + 0  # SUB, SL: op(slot, tos)
+    assert int(code3["op"][offs3[1] - 1]) == 80 + 6 * 1 + 0  # SUB, SL: op(slot, tos)
 
 
 def test_static_incomplete():
