@@ -311,15 +311,54 @@ struct TreeCompiler {
     ++n_checks;
   }
 
-  // The first instruction of every subtree's code is a leaf LOAD: it first stores the old top of
-  // stack to `slot`.
+  // The first instruction of every subtree's code is a leaf LOAD or a PAIR: it first stores the
+  // old top of stack to `slot`.
   void mark_push(SrIns<T>& in, int slot) {
     if (slot >= int(SR_MAX_STACK_SLOTS)) {
       fail(SR_ERR_TOO_DEEP, "tree needs more operand-stack slots than the encoding holds");
       return;
     }
-    in.op += SR_OP_LOAD_FEAT_PUSH - SR_OP_LOAD_FEAT;  // LOAD_x -> LOAD_x_PUSH
+    if (in.op >= SR_OP_PAIR0) in.op += SR_P_PUSH;                    // PAIR v -> PAIR v + PUSH
+    else in.op += SR_OP_LOAD_FEAT_PUSH - SR_OP_LOAD_FEAT;            // LOAD_x -> LOAD_x_PUSH
     in.meta |= uint32_t(slot + 1) << SR_M_PUSH_SHIFT;
+  }
+
+  // A binary node whose children are both leaves (DE deg2_l0_r0: no array check on either leaf)
+  // as one PAIR instruction.  Gradient programs keep the plain form (the gradient kernel reads
+  // constants by slot).  Returns false when the pair form does not apply.
+  bool emit_pair(int i, uint32_t bop) {
+    const int a = t.l[i], b = t.r[i];
+    if (with_const_index || !effleaf(a) || !effleaf(b)) return false;
+    SrIns<T> la = leaf_ins(a), lb = leaf_ins(b);
+    const bool ca = la.op == SR_OP_LOAD_CONST, cb = lb.op == SR_OP_LOAD_CONST;
+    if (ca && cb) return false;  // (only when folding is off)
+    for (const int c : {a, b})   // a checked feature array needs its own LOAD (its CHECK bit)
+      if (arr_check[c] && !(folded[c] || t.constant[c])) return false;
+    for (const int c : {a, b})   // a checked constant array: the static check emit_check makes
+      if (arr_check[c]) static_array_check(folded[c] ? fold_val[c] : t.val[c]);
+    SrIns<T> in{};
+    if (!ca && !cb) {
+      in.op = SR_PAIR_OPC(bop, SR_P_FF);
+      in.meta = la.meta;
+      in.c0 = lb.meta;  // second feature
+    } else if (!ca) {
+      in.op = SR_PAIR_OPC(bop, SR_P_FC);
+      in.meta = la.meta;
+      in.c0 = lb.c0;
+      in.c1 = lb.c1;
+    } else if (commutes(bop)) {  // c op x == x op c (IEEE + and *)
+      in.op = SR_PAIR_OPC(bop, SR_P_FC);
+      in.meta = lb.meta;
+      in.c0 = la.c0;
+      in.c1 = la.c1;
+    } else {
+      in.op = SR_PAIR_OPC(bop, SR_P_CF);
+      in.meta = lb.meta;
+      in.c0 = la.c0;
+      in.c1 = la.c1;
+    }
+    code.push_back(in);
+    return true;
   }
 
   void emit(int i) {
@@ -342,7 +381,9 @@ struct TreeCompiler {
     const int a = t.l[i], b = t.r[i];
     const uint32_t bop = binary_id(i);
     if (err != SR_OK) return;
-    if (effleaf(b)) {  // op(tos = left, operand = right leaf)
+    if (emit_pair(i, bop)) {
+      // both operands in one instruction
+    } else if (effleaf(b)) {  // op(tos = left, operand = right leaf)
       emit(a);
       code.push_back(operand_ins(b, bop, false));
     } else if (effleaf(a)) {  // op(operand = left leaf, tos = right)
@@ -407,6 +448,10 @@ struct TreeCompiler {
 uint32_t sr_instruction_cost(uint32_t code) {
   uint32_t c = 6;  // dispatch + operand fetch + validity tracking
   if (code == SR_OP_LOAD_FEAT_PUSH || code == SR_OP_LOAD_CONST_PUSH) c += 2;
+  if (code >= SR_OP_PAIR0) {
+    c += ((code - SR_OP_PAIR0) % 6u >= SR_P_PUSH) ? 3 : 1;  // second operand (+ push)
+    code = SR_OP_BINARY0 + (code - SR_OP_PAIR0) / 6u * 6u;  // priced as its binary operator
+  }
   if (code >= SR_OP_BINARY0) {
     const uint32_t b = (code - SR_OP_BINARY0) / 6u + 1u;
     if (b == SR_B_DIV) c += 10;

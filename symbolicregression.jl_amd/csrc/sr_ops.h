@@ -63,6 +63,11 @@ enum SrLossKind : int32_t {
 //           SR_V_FL: op(X[f], tos)  SR_V_FR: op(tos, X[f])
 //           SR_V_CL: op(c, tos)     SR_V_CR: op(tos, c)
 //         + and * only ever use the R variants (the compiler canonicalises: IEEE + and * commute)
+//       SR_OP_PAIR0 + 6*(b-1) + pair variant   tos <- op_b(leaf, leaf) (a binary node whose children
+//           are both leaves — DE's deg2_l0_r0 — in one instruction):
+//           SR_P_FF: op(X[f], X[g])  SR_P_FC: op(X[f], c)  SR_P_CF: op(c, X[f])   (f in meta, g in c0)
+//           + SR_P_PUSH: the old tos is first stored to stack slot `push` (a subtree's first instruction)
+//         + and * never use CF (commuted to FC)
 //   c0 (, c1) : constant bits (C variants, LOAD_CONST*): f32 in c0, f64 in c0 | c1 << 32
 //   meta bits  0-15 : operand index: feature f (F variants, LOAD_FEAT*), stack slot k (S variants),
 //                     pre-order constant slot of a constant leaf (gradient programs; else 0xffff)
@@ -76,14 +81,17 @@ enum : uint32_t {
   SR_OP_UNARY0 = 4u,       // opcode = SR_OP_UNARY0 + SrUnaryOp (1..)
   SR_OP_UNARY_INF0 = 40u,  // opcode = SR_OP_UNARY_INF0 + SrUnaryOp (fused: non-finite input -> +Inf)
   SR_OP_BINARY0 = 80u,     // opcode = SR_OP_BINARY0 + 6*(SrBinaryOp-1) + variant
+  SR_OP_PAIR0 = 256u,      // opcode = SR_OP_PAIR0 + 6*(SrBinaryOp-1) + pair variant
   SR_V_SL = 0u, SR_V_SR = 1u, SR_V_FL = 2u, SR_V_FR = 3u, SR_V_CL = 4u, SR_V_CR = 5u,
+  SR_P_FF = 0u, SR_P_FC = 1u, SR_P_CF = 2u, SR_P_PUSH = 3u,
   SR_M_INDEX = 0xffffu, SR_M_PUSH_SHIFT = 24u, SR_M_PUSH_MASK = 0x3fu << 24, SR_M_CHECK = 1u << 31,
   SR_MAX_STACK_SLOTS = 62u,
 };
 static_assert(SR_OP_UNARY0 + SR_U_COUNT <= SR_OP_UNARY_INF0, "unary opcode ranges overlap");
 static_assert(SR_OP_UNARY_INF0 + SR_U_COUNT <= SR_OP_BINARY0, "unary opcode range overlaps the binary range");
-static_assert(SR_OP_BINARY0 + 6 * SR_B_COUNT <= 256, "binary opcode range exceeds 8 bits");
+static_assert(SR_OP_BINARY0 + 6 * SR_B_COUNT <= SR_OP_PAIR0, "binary opcode range overlaps the pair range");
 #define SR_BIN_OPC(b, v) (SR_OP_BINARY0 + 6u * ((b) - 1u) + (v))
+#define SR_PAIR_OPC(b, v) (SR_OP_PAIR0 + 6u * ((b) - 1u) + (v))
 
 template <typename T>
 struct alignas(16) SrIns {

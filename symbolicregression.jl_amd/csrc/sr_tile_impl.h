@@ -273,10 +273,46 @@ __device__ __forceinline__ P* sr_row_at(P* base, uint32_t meta) {
     }                                  \
     break;                             \
   }
-// + and * commute: the compiler emits only their R variants
-#define SR_BCASE_COMM(ID) SR_BCASE_R(ID, true)
-#define SR_BCASE(ID) SR_BCASE_R(ID, true) SR_BCASE_L(ID, true)
-#define SR_BCASE_FULL(ID) SR_BCASE_R(ID, TIER == SR_TIER_FULL) SR_BCASE_L(ID, TIER == SR_TIER_FULL)
+// PAIR instructions: op(leaf, leaf) with the first feature in meta, the second feature in c0 (FF)
+// or the constant in the c words (FC / CF); the PUSH forms first store the old tos
+#define SR_PCASE(ID, ENABLED, PV, BODY)                          \
+  case SR_PAIR_OPC(ID, PV): {                                    \
+    if (ENABLED) {                                               \
+      BODY;                                                      \
+      SR_TRACK();                                                \
+    }                                                            \
+    break;                                                       \
+  }                                                              \
+  case SR_PAIR_OPC(ID, PV + SR_P_PUSH): {                        \
+    if (ENABLED) {                                               \
+      SR_PUSH_TOS();                                             \
+      BODY;                                                      \
+      SR_TRACK();                                                \
+    }                                                            \
+    break;                                                       \
+  }
+#define SR_PAIR_FF(ID)                                                                   \
+  T o[R];                                                                                \
+  L::load(SR_OPND_X(), tos);                                                             \
+  L::load(sr_row_at<ROWS>(x_lane, uint32_t(__builtin_amdgcn_readlane(int(wc0), int(k)))), o); \
+  SR_BIN_EACH(tos[r], o[r], ID)
+#define SR_PAIR_FC(ID)       \
+  L::load(SR_OPND_X(), tos); \
+  const T cv = SR_CVAL();    \
+  SR_BIN_EACH(tos[r], cv, ID)
+#define SR_PAIR_CF(ID)       \
+  L::load(SR_OPND_X(), tos); \
+  const T cv = SR_CVAL();    \
+  SR_BIN_EACH(cv, tos[r], ID)
+#define SR_PCASES_R(ID, ENABLED) \
+  SR_PCASE(ID, ENABLED, SR_P_FF, SR_PAIR_FF(ID)) SR_PCASE(ID, ENABLED, SR_P_FC, SR_PAIR_FC(ID))
+#define SR_PCASES(ID, ENABLED) SR_PCASES_R(ID, ENABLED) SR_PCASE(ID, ENABLED, SR_P_CF, SR_PAIR_CF(ID))
+
+// + and * commute: the compiler emits only their R variants (and no CF pairs)
+#define SR_BCASE_COMM(ID) SR_BCASE_R(ID, true) SR_PCASES_R(ID, true)
+#define SR_BCASE(ID) SR_BCASE_R(ID, true) SR_BCASE_L(ID, true) SR_PCASES(ID, true)
+#define SR_BCASE_FULL(ID) \
+  SR_BCASE_R(ID, TIER == SR_TIER_FULL) SR_BCASE_L(ID, TIER == SR_TIER_FULL) SR_PCASES(ID, TIER == SR_TIER_FULL)
 
 // LDS carve, in bytes, 16-aligned: X tile [nf][ROWS] T | y [ROWS] | w [ROWS] (weighted) | stack
 // [W][depth][ROWS] T | xacc [G][max_checks] f64 (EXACT mode)
@@ -301,6 +337,16 @@ struct SrLdsPlan {
 
 __device__ __forceinline__ uint4 sr_load_window(const void* code, uint32_t at) {
   return *reinterpret_cast<const uint4*>(static_cast<const unsigned char*>(code) + size_t(at) * 16u);
+}
+
+// The tile interpreter's program window: instructions base .. base+SR_WIN-1 (those before `end`).
+// (An end-of-window opcode handled inside the switch would give the interpreter loop a second exit,
+// which the AMDGPU structurizer turns into per-iteration register copies: the trip count stays.)
+constexpr uint32_t SR_WIN = 64u;
+__device__ __forceinline__ uint4 sr_window(const void* code, uint32_t base, uint32_t end, int lane) {
+  uint4 w = make_uint4(0u, 0u, 0u, 0u);
+  if (base + uint32_t(lane) < end) w = sr_load_window(code, base + uint32_t(lane));
+  return w;
 }
 
 // ------------------------------------------------------------------ the interpreter kernel
@@ -417,8 +463,7 @@ __global__ void __launch_bounds__(W * 64, SrMinWaves<W>::value) sr_tile_kernel(c
     todo &= todo - 1u;
     uint32_t nb = uint32_t(__builtin_amdgcn_readlane(int(my_pb), nj));
     uint32_t ne = uint32_t(__builtin_amdgcn_readlane(int(my_pe), nj));
-    uint4 nx = make_uint4(0u, 0u, 0u, 0u);
-    if (nb + lane < ne) nx = sr_load_window(a.code, nb + lane);
+    uint4 nx = sr_window(a.code, nb, ne, lane);
     int j = -1;
     uint32_t tpe = 0u;
     T tos[R];
@@ -441,8 +486,8 @@ __global__ void __launch_bounds__(W * 64, SrMinWaves<W>::value) sr_tile_kernel(c
         mrun = T(0);
         mrun1 = T(0);
       }
-      if (base + 64u < tpe) {
-        nb = base + 64u;
+      if (base + SR_WIN < tpe) {
+        nb = base + SR_WIN;
       } else if (todo) {
         nj = __builtin_ctzll(todo);
         todo &= todo - 1u;
@@ -451,12 +496,12 @@ __global__ void __launch_bounds__(W * 64, SrMinWaves<W>::value) sr_tile_kernel(c
       } else {
         more = false;
       }
-      if (more && nb + lane < ne) nx = sr_load_window(a.code, nb + lane);
+      if (more) nx = sr_window(a.code, nb, ne, lane);
       const int g = wave + SR_WAVES * j;
 
       if (!dead) {
         const uint32_t wop = cw.x, wc0 = cw.y, wc1 = cw.z, wmeta = cw.w;
-        const uint32_t n_here = __builtin_amdgcn_readfirstlane((tpe - base < 64u) ? tpe - base : 64u);
+        const uint32_t n_here = __builtin_amdgcn_readfirstlane((tpe - base < SR_WIN) ? tpe - base : SR_WIN);
         // single-exit loop (a dead tree sets k past the window): a second loop exit would make
         // LLVM add an exit-selector block to every iteration
         for (uint32_t k = 0; k < n_here; ++k) {
@@ -527,7 +572,7 @@ __global__ void __launch_bounds__(W * 64, SrMinWaves<W>::value) sr_tile_kernel(c
                 for (int r = 0; r < R; ++r) nonfin |= !sr_isfinite(tos[r]);
                 if (sr_ballot(nonfin)) {
                   dead = true;
-                  k = 64u;
+                  k = SR_WIN;
                 }
               }
             }
@@ -535,7 +580,7 @@ __global__ void __launch_bounds__(W * 64, SrMinWaves<W>::value) sr_tile_kernel(c
         }
       }
 
-      if (base + 64u >= tpe) {  // tree j is done on this tile
+      if (base + SR_WIN >= tpe) {  // tree j is done on this tile
         const uint64_t bit = uint64_t(1) << j;
         if (MODE == SR_MODE_LOSS) {
           T l[R];

@@ -77,7 +77,7 @@ def _binary(bid, a, b):
 
 # opcode ranges and meta fields (csrc/sr_ops.h)
 LOAD_FEAT, LOAD_CONST, LOAD_FEAT_PUSH, LOAD_CONST_PUSH = 0, 1, 2, 3
-UNARY0, UNARY_INF0, BINARY0 = 4, 40, 80
+UNARY0, UNARY_INF0, BINARY0, PAIR0 = 4, 40, 80, 256
 CHECK = 1 << 31
 
 
@@ -121,6 +121,22 @@ def run_program(code, lo, hi, X, T):
             if inf:  # fused unary: non-finite input -> +Inf
                 v = np.where(np.isfinite(tos), v, T(np.inf)).astype(T)
             tos = v
+        elif opc >= PAIR0:  # op(leaf, leaf): FF / FC / CF (+3: push the old tos first)
+            bid, v = divmod(opc - PAIR0, 6)
+            bid += 1
+            if v >= 3:
+                slots[push_slot(meta)] = tos
+                v -= 3
+            xf = X[operand(meta)].astype(T)
+            if v == 0:
+                o = X[int(code["val"][pc].view(np.uint32) if T == np.float32 else
+                          np.array([code["val"][pc]]).view(np.uint64)[0] & 0xFFFFFFFF)].astype(T)
+                a, b = xf, o
+            elif v == 1:
+                a, b = xf, np.full(n, val, dtype=T)
+            else:
+                a, b = np.full(n, val, dtype=T), xf
+            tos = _binary(bid, a, b).astype(T)
         else:
             bid, v = divmod(opc - BINARY0, 6)
             bid += 1

@@ -47,10 +47,10 @@ def test_program_shapes():
     opts = Options(**OPTS)
     cases = {
         "x1": 1,                          # LOAD
-        "x1 * 3.0": 2,                    # LOAD, MUL c
+        "x1 * 3.0": 1,                    # PAIR MUL FC
         "cos(3.0 * 2.0)": 1,              # folded constant tree
         "cos(x1) + cos(x2)": 5,           # LOAD,COS, LOAD+PUSH,COS, ADD stack
-        "(x1 * 2.0) * (3.0 * 4.0)": 3,    # folded right child -> constant operand
+        "(x1 * 2.0) * (3.0 * 4.0)": 2,    # PAIR, then the folded right child as constant operand
     }
     trees = [parse_expression(e, opts) for e in cases]
     tb = flatten_trees(trees, np.float32)
@@ -66,18 +66,30 @@ def test_program_shapes():
     assert ops == [0, 4 + 5, 2, 4 + 5, 80 + 1]
     assert [vm.push_slot(m) for m in meta] == [-1, -1, 0, -1, -1]
     assert vm.operand(meta[4]) == 0 and vm.operand(meta[2]) == 1
-    # fused unary: cos(x1 * 2.0) -> LOAD x1, MUL c, INF-COS; no CHECK on the inner product
+    # fused unary: cos(x1 * 2.0) -> PAIR MUL FC, INF-COS; no CHECK on the inner product
     tb2 = flatten_trees([parse_expression("cos(x1 * 2.0)", opts)], np.float32)
     code2, offs2, _, depth2 = vm.compile_info(opts, tb2, 100, 5, np.float32)
     ops2 = [int(v) for v in code2["op"][:offs2[1]]]
     meta2 = [int(v) for v in code2["meta"][:offs2[1]]]
-    assert ops2 == [0, 80 + 6 * 2 + 5, 40 + 5]
-    assert [vm.is_check(m) for m in meta2] == [0, 0, 1]
+    assert ops2 == [256 + 6 * 2 + 1, 40 + 5]
+    assert [vm.is_check(m) for m in meta2] == [0, 1]
     assert depth2 == 0  # the fused unary needs no stack slot
     # non-commutative stack operand keeps its side: (x1 - cos(x2)) - exp(x3) style trees
     tb3 = flatten_trees([parse_expression("cos(x1) - exp(x2)", opts)], np.float32)
     code3, offs3, _, _ = vm.compile_info(opts, tb3, 100, 5, np.float32)
     assert int(code3["op"][offs3[1] - 1]) == 80 + 6 * 1 + 0  # SUB, SL: op(slot, tos)
+    # PAIR instructions: leaf-leaf binaries in one instruction (FF / FC / CF, + 3 with a push)
+    exprs = ["x1 * 3.0", "3.0 - x2", "x1 / x3", "3.0 * x2", "(x1 - x2) * (x3 + 2.0)"]
+    tb4 = flatten_trees([parse_expression(e, opts) for e in exprs], np.float32)
+    code4, offs4, _, _ = vm.compile_info(opts, tb4, 100, 5, np.float32)
+    prog = [[int(v) for v in code4["op"][offs4[k]:offs4[k + 1]]] for k in range(len(exprs))]
+    assert prog[0] == [256 + 6 * 2 + 1]
+    assert prog[1] == [256 + 6 * 1 + 2]
+    assert prog[2] == [256 + 6 * 3 + 0] and int(code4["c1"][offs4[2]]) == 0
+    assert int(code4["val"][offs4[2]].view(np.uint32)) == 2  # second feature (x3)
+    assert prog[3] == [256 + 6 * 2 + 1]  # commuted to FC
+    assert prog[4] == [256 + 6 * 1 + 0, 256 + 0 + 1 + 3, 80 + 6 * 2 + 1]
+    assert vm.push_slot(int(code4["meta"][offs4[4] + 1])) == 0
 
 
 def test_static_incomplete():
