@@ -165,6 +165,10 @@ int sr_compile_info(int dtype, int n_unary, const char* const* unary_names, int 
 /* Timing of the last device call on this context (ms): kernel-only, via HIP events. */
 int sr_last_kernel_ms(sr_ctx* ctx, double* eval_ms, double* total_ms);
 
+/* Host-side phases of the last sr_eval_loss_batch call (ms, wall clock), up to n of: compile,
+ * upload + launch, wait for the interpreter + reduction, exact-sum pass, finalize. */
+int sr_last_phase_ms(sr_ctx* ctx, double* out, int n);
+
 #ifdef __cplusplus
 }
 #endif

@@ -64,24 +64,73 @@ struct DevBuf {
   }
 };
 
+// Pinned host staging (programs, offsets, launch order): hipMemcpyAsync from it is a true async DMA,
+// so the host compiles the next chunk while the device runs the previous one.
+struct HostBuf {
+  void* p = nullptr;
+  size_t cap = 0;
+  hipError_t ensure(size_t bytes, hipStream_t s) {
+    if (bytes <= cap) return hipSuccess;
+    if (p) {
+      hipError_t e = hipStreamSynchronize(s);  // no DMA may still read the old buffer
+      if (e == hipSuccess) e = hipHostFree(p);
+      if (e != hipSuccess) return e;
+      p = nullptr;
+      cap = 0;
+    }
+    size_t want = bytes < 65536 ? 65536 : bytes + bytes / 4;
+    hipError_t e = hipHostMalloc(&p, want, hipHostMallocDefault);
+    if (e == hipSuccess) cap = want;
+    return e;
+  }
+  void release() {
+    if (p) (void)hipHostFree(p);
+    p = nullptr;
+    cap = 0;
+  }
+  template <typename U>
+  U* as() const {
+    return static_cast<U*>(p);
+  }
+};
+
+constexpr int kMaxChunks = 4;
+
 }  // namespace
 
 struct sr_ctx {
   int device = 0;
   hipStream_t stream = nullptr;
   hipEvent_t ev_start = nullptr, ev_k0 = nullptr, ev_k1 = nullptr, ev_end = nullptr;
+  hipEvent_t ev_c0[kMaxChunks] = {}, ev_c1[kMaxChunks] = {};  // per-chunk interpreter launches
+  int n_chunks_last = 0;
+  HostBuf h_code, h_offsets, h_static_bad, h_perm;
   std::mutex mu;
   std::vector<SrOpset> opsets;
   std::vector<int> tiers;
   DevBuf code, offsets, static_bad, part_sum, part_flag, out_sum, out_flag, pred, row_idx, tree_list,
       check_sums, perm, hint, g_code, g_offsets, g_consts, g_const_off, g_items, g_part, g_out;
   double last_eval_ms = 0.0, last_total_ms = 0.0;
+  // host-side phases of the last eval_loss call (ms): compile, upload+launch, wait, exact pass,
+  // finalize (sr_last_phase_ms)
+  double phase_ms[5] = {0, 0, 0, 0, 0};
+  std::chrono::steady_clock::time_point phase_t;
+  void start_phases(std::chrono::steady_clock::time_point t) {
+    phase_t = t;
+    for (double& v : phase_ms) v = 0.0;
+  }
+  void mark_phase(int i) {
+    const auto now = std::chrono::steady_clock::now();
+    phase_ms[i] = std::chrono::duration<double, std::milli>(now - phase_t).count();
+    phase_t = now;
+  }
   int cu_count = 256;
   int rows_override = 0;    // SR_AMD_ROWS_PER_LANE (tuning): 4 selects the f32 BASIC 4-rows/lane kernel
   int tree_group = 0;       // SR_AMD_TREES_PER_BLOCK override (0 = heuristic)
   int waves_override = 0;   // SR_AMD_WAVES (tuning): 16 selects the 16-wave f32 BASIC loss kernel
   bool cost_order = true;   // launch trees in decreasing estimated cost (SR_AMD_NO_SORT=1 disables)
   bool dead_hints = true;   // share dead-tree hints across row blocks (SR_AMD_NO_HINT=1 disables)
+  int chunks = 1;           // SR_AMD_CHUNKS: pipeline compile/launch over up to this many tree chunks
   std::vector<uint32_t> perm_host;
 };
 
@@ -164,6 +213,12 @@ int validate_common(sr_ctx* ctx, const sr_dataset* ds, int opset_id, const sr_tr
 
 // Shared engine: compile + upload + interpreter(+reduce).  Leaves per-tree {sum, flag} in
 // ctx->out_sum / ctx->out_flag (device).  n_eval rows (full dataset or row_idx view).
+//
+// Large LOSS batches are pipelined in up to kMaxChunks tree chunks: the host compiles chunk c+1
+// while the device runs chunk c (programs staged through pinned memory, async DMA).  Every chunk is
+// an independent launch over its own slice of the per-tree device arrays; `prog` receives the merged
+// per-tree summary (offsets into the device code buffer, static_bad, max_depth, max_checks) that
+// the exact-sum pass and the callers use — its `code` stays empty.
 template <typename T>
 int run_batch(sr_ctx* ctx, const sr_dataset* ds, int opset_id, const sr_tree_batch* trees, const int64_t* row_idx,
               int64_t n_idx, int64_t n_total, int loss_kind, int mode, SrProgramBatch<T>* prog, Grid* grid_out) {
@@ -172,101 +227,194 @@ int run_batch(sr_ctx* ctx, const sr_dataset* ds, int opset_id, const sr_tree_bat
   if (n_eval <= 0) return set_error(SR_ERR_INVALID_ARG, "no rows to evaluate");
   if (loss_kind != SR_LOSS_L2DIST && loss_kind != SR_LOSS_L1DIST)
     return set_error(SR_ERR_INVALID_ARG, "unsupported loss kind");
-  std::string err;
-  int rc = sr_compile_batch<T>(*trees, ctx->opsets[opset_id], n_total, ds->nf, false, prog, &err);
-  if (rc != SR_OK) return set_error(rc, err);
   const int64_t nt = trees->n_trees;
+  if (nt < 0) return set_error(SR_ERR_INVALID_ARG, "negative tree count");
+  if (nt > 0 && !trees->offsets) return set_error(SR_ERR_INVALID_ARG, "sr_tree_batch has NULL arrays");
+  const int64_t total_nodes = nt > 0 ? trees->offsets[nt] - trees->offsets[0] : 0;
+  if (total_nodes < 0 || total_nodes > int64_t(0xffffffffu) / 2)
+    return set_error(SR_ERR_INVALID_ARG, "tree batch node count out of range");
   const int tier = ctx->tiers[opset_id];
-  const int depth = prog->max_depth > 0 ? prog->max_depth : 1;
   const int R = sr_rows_per_lane<T>(mode, tier, ctx->rows_override);
   const int W = sr_waves_per_block(int(sizeof(T)), mode, tier, R, ctx->waves_override);
-  Grid g = make_grid<T>(n_eval, nt, R, W, int(ds->nf), depth, 0, ds->w != nullptr, ctx->tree_group);
-  if (g.lds > kLdsMax)
-    return set_error(SR_ERR_TOO_DEEP, "the row tile (" + std::to_string(ds->nf) + " features, " +
-                                          std::to_string(depth) + " stack slots) needs " + std::to_string(g.lds) +
-                                          " bytes of LDS; the limit is 160 KiB");
-  *grid_out = g;
-  if (nt == 0) return SR_OK;
-
   hipStream_t s = ctx->stream;
-  SR_HIP_CHECK(hipEventRecord(ctx->ev_start, s));
-  SR_HIP_CHECK(ctx->code.ensure(prog->code.size() * sizeof(SrIns<T>) + 16));
-  SR_HIP_CHECK(ctx->offsets.ensure(prog->offsets.size() * sizeof(uint32_t)));
-  SR_HIP_CHECK(ctx->static_bad.ensure(prog->static_bad.size() + 16));
-  if (!prog->code.empty())
-    SR_HIP_CHECK(hipMemcpyAsync(ctx->code.p, prog->code.data(), prog->code.size() * sizeof(SrIns<T>),
-                                hipMemcpyHostToDevice, s));
-  SR_HIP_CHECK(hipMemcpyAsync(ctx->offsets.p, prog->offsets.data(), prog->offsets.size() * sizeof(uint32_t),
-                              hipMemcpyHostToDevice, s));
-  SR_HIP_CHECK(hipMemcpyAsync(ctx->static_bad.p, prog->static_bad.data(), prog->static_bad.size(),
-                              hipMemcpyHostToDevice, s));
-  // launch order: decreasing estimated cost, so every block's waves get similar work
-  const uint32_t* perm_dev = nullptr;
-  if (ctx->cost_order && nt > 1) {
-    ctx->perm_host.resize(size_t(nt));
-    for (int64_t t = 0; t < nt; ++t) ctx->perm_host[size_t(t)] = uint32_t(t);
-    const std::vector<uint32_t>& cost = prog->cost;
-    std::stable_sort(ctx->perm_host.begin(), ctx->perm_host.end(),
-                     [&](uint32_t x, uint32_t y) { return cost[x] > cost[y]; });
-    SR_HIP_CHECK(ctx->perm.ensure(size_t(nt) * sizeof(uint32_t)));
-    SR_HIP_CHECK(hipMemcpyAsync(ctx->perm.p, ctx->perm_host.data(), size_t(nt) * sizeof(uint32_t),
-                                hipMemcpyHostToDevice, s));
-    perm_dev = ctx->perm.as<uint32_t>();
+
+  // chunking (SR_AMD_CHUNKS, default 1): LOSS mode only (PRED writes rows by caller tree index),
+  // >= kChunkTrees trees each.  Measured on the C2 population: 4 chunks cost more kernel time (each
+  // launch drains its own tail) than they hide once compiling is ~0.5 ms.
+  constexpr int64_t kChunkTrees = 2048;
+  int n_chunks = 1;
+  if (mode == SR_MODE_LOSS && ctx->chunks > 1) {
+    const int64_t k = nt / kChunkTrees;
+    const int64_t cap = ctx->chunks < kMaxChunks ? ctx->chunks : kMaxChunks;
+    n_chunks = int(k < 1 ? 1 : (k > cap ? cap : k));
   }
-  uint32_t* hint_dev = nullptr;
-  if (ctx->dead_hints && mode == SR_MODE_LOSS && g.n_row_blocks > 1) {
-    SR_HIP_CHECK(ctx->hint.ensure(size_t(nt) * sizeof(uint32_t)));
-    SR_HIP_CHECK(hipMemsetAsync(ctx->hint.p, 0, size_t(nt) * sizeof(uint32_t), s));
-    hint_dev = ctx->hint.as<uint32_t>();
-  }
+
+  // device + pinned buffers sized for the whole batch up front (a chunk's kernel may still run while
+  // the next one is staged): a program has at most one instruction per node
+  Grid g0 = make_grid<T>(n_eval, nt > 0 ? nt : 1, R, W, int(ds->nf), 1, 0, ds->w != nullptr, ctx->tree_group);
+  const int n_rb = g0.n_row_blocks;
+  const size_t code_cap = size_t(total_nodes) + 16;
+  SR_HIP_CHECK(ctx->code.ensure(code_cap * sizeof(SrIns<T>)));
+  SR_HIP_CHECK(ctx->offsets.ensure((size_t(nt) + 1) * sizeof(uint32_t)));
+  SR_HIP_CHECK(ctx->static_bad.ensure(size_t(nt) + 16));
+  SR_HIP_CHECK(ctx->perm.ensure((size_t(nt) + 1) * sizeof(uint32_t)));
+  SR_HIP_CHECK(ctx->h_code.ensure(code_cap * sizeof(SrIns<T>), s));
+  SR_HIP_CHECK(ctx->h_offsets.ensure((size_t(nt) + 1) * sizeof(uint32_t), s));
+  SR_HIP_CHECK(ctx->h_static_bad.ensure(size_t(nt) + 16, s));
+  SR_HIP_CHECK(ctx->h_perm.ensure((size_t(nt) + 1) * sizeof(uint32_t), s));
+  const size_t n_part = size_t(nt) * size_t(n_rb);
+  SR_HIP_CHECK(ctx->part_sum.ensure(n_part * sizeof(double) + 8));
+  SR_HIP_CHECK(ctx->part_flag.ensure(n_part * sizeof(uint32_t) + 4));
+  SR_HIP_CHECK(ctx->out_sum.ensure(size_t(nt) * sizeof(double) + 8));
+  SR_HIP_CHECK(ctx->out_flag.ensure(size_t(nt) * sizeof(uint32_t) + 4));
+  if (mode == SR_MODE_PRED) SR_HIP_CHECK(ctx->pred.ensure(size_t(nt) * size_t(n_eval) * sizeof(T) + 16));
+  const bool use_hint = ctx->dead_hints && mode == SR_MODE_LOSS && n_rb > 1;
+  if (use_hint) SR_HIP_CHECK(ctx->hint.ensure(size_t(nt) * sizeof(uint32_t) + 4));
   if (gather) {
     for (int64_t i = 0; i < n_idx; ++i)
       if (row_idx[i] < 0 || row_idx[i] >= ds->n)
         return set_error(SR_ERR_INVALID_ARG, "row index " + std::to_string(row_idx[i]) + " out of range");
     SR_HIP_CHECK(ctx->row_idx.ensure(size_t(n_idx) * sizeof(int64_t)));
-    SR_HIP_CHECK(hipMemcpyAsync(ctx->row_idx.p, row_idx, size_t(n_idx) * sizeof(int64_t), hipMemcpyHostToDevice, s));
   }
-  const size_t n_part = size_t(nt) * size_t(g.n_row_blocks);
-  SR_HIP_CHECK(ctx->part_sum.ensure(n_part * sizeof(double)));
-  SR_HIP_CHECK(ctx->part_flag.ensure(n_part * sizeof(uint32_t)));
-  SR_HIP_CHECK(ctx->out_sum.ensure(size_t(nt) * sizeof(double)));
-  SR_HIP_CHECK(ctx->out_flag.ensure(size_t(nt) * sizeof(uint32_t)));
-  if (mode == SR_MODE_PRED) SR_HIP_CHECK(ctx->pred.ensure(size_t(nt) * size_t(n_eval) * sizeof(T)));
 
-  SrEvalArgs<T> a{};
-  a.code = ctx->code.as<SrIns<T>>();
-  a.offsets = ctx->offsets.as<uint32_t>();
-  a.perm = perm_dev;
-  a.hint = hint_dev;
-  a.n_trees = int(nt);
-  a.trees_per_block = g.G;
-  a.X = static_cast<const T*>(ds->X);
-  a.y = static_cast<const T*>(ds->y);
-  a.w = static_cast<const T*>(ds->w);
-  a.row_idx = gather ? ctx->row_idx.as<int64_t>() : nullptr;
-  a.ld = ds->ld;
-  a.n_rows = n_eval;
-  a.nf = int(ds->nf);
-  a.tiles_per_block = g.tiles;
-  a.n_row_blocks = g.n_row_blocks;
-  a.n_groups = g.n_groups;
-  a.stack_depth = depth;
-  // Σ over n_total rows of values below tbig cannot overflow T, even with rounding slack.
-  a.tbig = T(t_max<T>() / (2.0 * double(n_total > 0 ? n_total : 1)));
-  a.loss_kind = loss_kind;
-  a.part_sum = ctx->part_sum.as<double>();
-  a.part_flag = ctx->part_flag.as<uint32_t>();
-  a.pred = ctx->pred.as<T>();
-  a.pred_ld = n_eval;
-  a.scale = 1.0;
-  if (g.n_blocks > 0x7fffffff) return set_error(SR_ERR_INVALID_ARG, "grid too large");
-  SR_HIP_CHECK(hipEventRecord(ctx->ev_k0, s));
-  SR_HIP_CHECK(sr_launch_eval<T>(a, mode, gather, tier, ctx->rows_override, g.W, int(g.n_blocks), s));
-  SR_HIP_CHECK(hipEventRecord(ctx->ev_k1, s));
-  SR_HIP_CHECK(sr_launch_reduce(a.part_sum, a.part_flag, int(nt), g.n_row_blocks, perm_dev,
-                                ctx->static_bad.as<uint8_t>(), ctx->out_sum.as<double>(),
-                                ctx->out_flag.as<uint32_t>(), s));
+  prog->code.clear();
+  prog->offsets.assign(size_t(nt) + 1, 0);
+  prog->static_bad.assign(size_t(nt), 0);
+  prog->max_depth = 0;
+  prog->max_checks = 0;
+  prog->total_nodes = 0;
+  prog->total_ops = 0;
+  SrIns<T>* h_code = ctx->h_code.as<SrIns<T>>();
+  uint32_t* h_off = ctx->h_offsets.as<uint32_t>();
+  uint8_t* h_bad = ctx->h_static_bad.as<uint8_t>();
+  uint32_t* h_perm = ctx->h_perm.as<uint32_t>();
+  ctx->n_chunks_last = 0;
+  SR_HIP_CHECK(hipEventRecord(ctx->ev_start, s));
+  if (gather)
+    SR_HIP_CHECK(hipMemcpyAsync(ctx->row_idx.p, row_idx, size_t(n_idx) * sizeof(int64_t), hipMemcpyHostToDevice, s));
+  if (use_hint) SR_HIP_CHECK(hipMemsetAsync(ctx->hint.p, 0, size_t(nt) * sizeof(uint32_t), s));
+
+  uint32_t code_base = 0;
+  Grid glast = g0;
+  std::string err;
+  for (int c = 0; c < n_chunks && nt > 0; ++c) {
+    const int64_t t0 = nt * c / n_chunks, t1 = nt * (c + 1) / n_chunks, nc = t1 - t0;
+    sr_tree_batch sub = *trees;
+    sub.n_trees = nc;
+    sub.offsets = trees->offsets + t0;  // node arrays stay indexed by absolute offsets
+    SrProgramBatch<T> pc;
+    int rc = sr_compile_batch<T>(sub, ctx->opsets[opset_id], n_total, ds->nf, false, &pc, &err);
+    if (rc != SR_OK) {
+      (void)hipStreamSynchronize(s);  // earlier chunks may still read the staging buffers
+      if (rc == SR_ERR_BAD_TREE || rc == SR_ERR_INVALID_ARG) {
+        // report the tree index of the whole batch
+        const size_t at = err.find("tree ");
+        if (at == 0) {
+          const int64_t k = std::atoll(err.c_str() + 5);
+          err = "tree " + std::to_string(k + t0) + err.substr(err.find(':'));
+        }
+      }
+      return set_error(rc, err);
+    }
+    if (c == 0) ctx->mark_phase(0);
+    const int depth = pc.max_depth > 0 ? pc.max_depth : 1;
+    Grid g = make_grid<T>(n_eval, nc, R, W, int(ds->nf), depth, 0, ds->w != nullptr, ctx->tree_group);
+    if (g.lds > kLdsMax) {
+      (void)hipStreamSynchronize(s);
+      return set_error(SR_ERR_TOO_DEEP, "the row tile (" + std::to_string(ds->nf) + " features, " +
+                                            std::to_string(depth) + " stack slots) needs " + std::to_string(g.lds) +
+                                            " bytes of LDS; the limit is 160 KiB");
+    }
+    glast = g;
+    // stage: code at code_base, offsets made absolute, static_bad, launch order (chunk-local)
+    const size_t ncode = pc.code.size();
+    if (code_base + ncode > code_cap) {
+      (void)hipStreamSynchronize(s);
+      return set_error(SR_ERR_INVALID_ARG, "program longer than its node count");
+    }
+    if (ncode) std::memcpy(h_code + code_base, pc.code.data(), ncode * sizeof(SrIns<T>));
+    for (int64_t i = 0; i <= nc; ++i) h_off[t0 + i] = code_base + pc.offsets[size_t(i)];
+    std::memcpy(h_bad + t0, pc.static_bad.data(), size_t(nc));
+    for (int64_t i = 0; i < nc; ++i) h_perm[t0 + i] = uint32_t(i);
+    if (ctx->cost_order && nc > 1) {
+      // decreasing estimated cost, so every block's waves get similar work (counting sort: costs
+      // are small integers; ties keep tree order)
+      const std::vector<uint32_t>& cost = pc.cost;
+      uint32_t cmax = 0;
+      for (uint32_t v : cost) cmax = v > cmax ? v : cmax;
+      std::vector<uint32_t> start(size_t(cmax) + 2, 0);
+      for (uint32_t v : cost) ++start[size_t(cmax - v) + 1];
+      for (size_t k = 1; k < start.size(); ++k) start[k] += start[k - 1];
+      for (int64_t i = 0; i < nc; ++i) h_perm[t0 + start[size_t(cmax - cost[size_t(i)])]++] = uint32_t(i);
+    }
+    if (ncode)
+      SR_HIP_CHECK(hipMemcpyAsync(ctx->code.as<SrIns<T>>() + code_base, h_code + code_base, ncode * sizeof(SrIns<T>),
+                                  hipMemcpyHostToDevice, s));
+    SR_HIP_CHECK(hipMemcpyAsync(ctx->offsets.as<uint32_t>() + t0, h_off + t0, size_t(nc + 1) * sizeof(uint32_t),
+                                hipMemcpyHostToDevice, s));
+    SR_HIP_CHECK(hipMemcpyAsync(ctx->static_bad.as<uint8_t>() + t0, h_bad + t0, size_t(nc), hipMemcpyHostToDevice, s));
+    SR_HIP_CHECK(hipMemcpyAsync(ctx->perm.as<uint32_t>() + t0, h_perm + t0, size_t(nc) * sizeof(uint32_t),
+                                hipMemcpyHostToDevice, s));
+    // merged summary
+    for (int64_t i = 0; i <= nc; ++i) prog->offsets[size_t(t0 + i)] = h_off[t0 + i];
+    std::memcpy(prog->static_bad.data() + t0, pc.static_bad.data(), size_t(nc));
+    if (pc.max_depth > prog->max_depth) prog->max_depth = pc.max_depth;
+    if (pc.max_checks > prog->max_checks) prog->max_checks = pc.max_checks;
+    prog->total_nodes += pc.total_nodes;
+    prog->total_ops += pc.total_ops;
+
+    SrEvalArgs<T> a{};
+    a.code = ctx->code.as<SrIns<T>>();
+    a.offsets = ctx->offsets.as<uint32_t>() + t0;
+    a.perm = ctx->perm.as<uint32_t>() + t0;
+    a.hint = use_hint ? ctx->hint.as<uint32_t>() + t0 : nullptr;
+    a.n_trees = int(nc);
+    a.trees_per_block = g.G;
+    a.X = static_cast<const T*>(ds->X);
+    a.y = static_cast<const T*>(ds->y);
+    a.w = static_cast<const T*>(ds->w);
+    a.row_idx = gather ? ctx->row_idx.as<int64_t>() : nullptr;
+    a.ld = ds->ld;
+    a.n_rows = n_eval;
+    a.nf = int(ds->nf);
+    a.tiles_per_block = g.tiles;
+    a.n_row_blocks = g.n_row_blocks;
+    a.n_groups = g.n_groups;
+    a.stack_depth = depth;
+    // Σ over n_total rows of values below tbig cannot overflow T, even with rounding slack.
+    a.tbig = T(t_max<T>() / (2.0 * double(n_total > 0 ? n_total : 1)));
+    a.loss_kind = loss_kind;
+    a.part_sum = ctx->part_sum.as<double>() + size_t(n_rb) * size_t(t0);
+    a.part_flag = ctx->part_flag.as<uint32_t>() + size_t(n_rb) * size_t(t0);
+    a.pred = ctx->pred.as<T>();
+    a.pred_ld = n_eval;
+    a.scale = 1.0;
+    if (g.n_blocks > 0x7fffffff || g.n_row_blocks != n_rb) {
+      (void)hipStreamSynchronize(s);
+      return set_error(SR_ERR_INVALID_ARG, "grid too large");
+    }
+    SR_HIP_CHECK(hipEventRecord(ctx->ev_c0[c], s));
+    SR_HIP_CHECK(sr_launch_eval<T>(a, mode, gather, tier, ctx->rows_override, g.W, int(g.n_blocks), s));
+    SR_HIP_CHECK(hipEventRecord(ctx->ev_c1[c], s));
+    SR_HIP_CHECK(sr_launch_reduce(a.part_sum, a.part_flag, int(nc), n_rb, a.perm, ctx->static_bad.as<uint8_t>() + t0,
+                                  ctx->out_sum.as<double>() + t0, ctx->out_flag.as<uint32_t>() + t0, s));
+    ctx->n_chunks_last = c + 1;
+    code_base += uint32_t(ncode);
+  }
+  if (nt == 0) ctx->mark_phase(0);
+  *grid_out = glast;
+  ctx->mark_phase(1);
   return SR_OK;
+}
+
+// Σ of the interpreter launch times of the last run_batch (ms).
+inline double chunk_kernel_ms(sr_ctx* ctx) {
+  double ms = 0.0;
+  for (int c = 0; c < ctx->n_chunks_last; ++c) {
+    float m = 0.f;
+    if (hipEventElapsedTime(&m, ctx->ev_c0[c], ctx->ev_c1[c]) == hipSuccess) ms += double(m);
+  }
+  return ms;
 }
 
 // Exact isfinite(sum(array)) check of every CHECK node of the listed trees.  Writes this dataset
@@ -373,6 +521,7 @@ int eval_loss_impl(sr_ctx* ctx, const sr_dataset* ds, int opset_id, const sr_tre
   const bool gather = row_idx != nullptr && n_idx > 0;
   const int64_t n_eval = gather ? n_idx : ds->n;
   auto t0 = std::chrono::steady_clock::now();
+  ctx->start_phases(t0);
   SrProgramBatch<T> prog;
   Grid g;
   int rc = run_batch<T>(ctx, ds, opset_id, trees, row_idx, n_idx, n_eval, loss_kind, SR_MODE_LOSS, &prog, &g);
@@ -385,9 +534,8 @@ int eval_loss_impl(sr_ctx* ctx, const sr_dataset* ds, int opset_id, const sr_tre
   SR_HIP_CHECK(hipMemcpyAsync(flags.data(), ctx->out_flag.p, size_t(nt) * sizeof(uint32_t), hipMemcpyDeviceToHost, s));
   SR_HIP_CHECK(hipEventRecord(ctx->ev_end, s));
   SR_HIP_CHECK(hipStreamSynchronize(s));
-  float ms = 0.f;
-  SR_HIP_CHECK(hipEventElapsedTime(&ms, ctx->ev_k0, ctx->ev_k1));
-  ctx->last_eval_ms = ms;
+  ctx->last_eval_ms = chunk_kernel_ms(ctx);
+  ctx->mark_phase(2);
   std::vector<int64_t> list;
   for (int64_t t = 0; t < nt; ++t)
     if ((flags[t] & (SR_FLAG_NONFINITE | SR_FLAG_STATIC)) == 0 && (flags[t] & SR_FLAG_BIG)) list.push_back(t);
@@ -398,9 +546,11 @@ int eval_loss_impl(sr_ctx* ctx, const sr_dataset* ds, int opset_id, const sr_tre
                       check_sums.data());
     if (rc != SR_OK) return rc;
   }
+  ctx->mark_phase(3);
   const double denom = view_denominator<T>(ds, row_idx, n_idx);
   finalize<T>(nt, sums.data(), flags.data(), denom, list.data(), int64_t(list.size()), prog.max_checks,
               check_sums.empty() ? nullptr : check_sums.data(), static_cast<T*>(out_loss), out_complete);
+  ctx->mark_phase(4);
   auto t1 = std::chrono::steady_clock::now();
   ctx->last_total_ms = std::chrono::duration<double, std::milli>(t1 - t0).count();
   (void)n_eval;
@@ -670,11 +820,16 @@ int sr_init(int device, sr_ctx** out) {
   if (const char* v = std::getenv("SR_AMD_WAVES")) ctx->waves_override = std::atoi(v);
   if (const char* v = std::getenv("SR_AMD_NO_SORT")) ctx->cost_order = std::atoi(v) == 0;
   if (const char* v = std::getenv("SR_AMD_NO_HINT")) ctx->dead_hints = std::atoi(v) == 0;
+  if (const char* v = std::getenv("SR_AMD_CHUNKS")) ctx->chunks = std::atoi(v);
   hipError_t e = hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking);
   if (e == hipSuccess) e = hipEventCreate(&ctx->ev_start);
   if (e == hipSuccess) e = hipEventCreate(&ctx->ev_k0);
   if (e == hipSuccess) e = hipEventCreate(&ctx->ev_k1);
   if (e == hipSuccess) e = hipEventCreate(&ctx->ev_end);
+  for (int c = 0; c < kMaxChunks; ++c) {
+    if (e == hipSuccess) e = hipEventCreate(&ctx->ev_c0[c]);
+    if (e == hipSuccess) e = hipEventCreate(&ctx->ev_c1[c]);
+  }
   if (e != hipSuccess) {
     delete ctx;
     return set_error(SR_ERR_HIP, std::string("stream/event creation: ") + hipGetErrorString(e));
@@ -694,6 +849,11 @@ int sr_shutdown(sr_ctx* ctx) {
                       &ctx->perm, &ctx->hint, &ctx->g_code, &ctx->g_offsets, &ctx->g_consts, &ctx->g_const_off,
                       &ctx->g_items, &ctx->g_part, &ctx->g_out})
       b->release();
+    for (HostBuf* b : {&ctx->h_code, &ctx->h_offsets, &ctx->h_static_bad, &ctx->h_perm}) b->release();
+    for (int c = 0; c < kMaxChunks; ++c) {
+      (void)hipEventDestroy(ctx->ev_c0[c]);
+      (void)hipEventDestroy(ctx->ev_c1[c]);
+    }
     (void)hipEventDestroy(ctx->ev_start);
     (void)hipEventDestroy(ctx->ev_k0);
     (void)hipEventDestroy(ctx->ev_k1);
@@ -816,9 +976,7 @@ int sr_eval_loss_partials(sr_ctx* ctx, const sr_dataset* ds, int opset_id, const
   SR_HIP_CHECK(hipMemcpyAsync(out_sum, ctx->out_sum.p, size_t(nt) * sizeof(double), kind, s));
   SR_HIP_CHECK(hipMemcpyAsync(out_flags, ctx->out_flag.p, size_t(nt) * sizeof(uint32_t), kind, s));
   SR_HIP_CHECK(hipStreamSynchronize(s));
-  float ms = 0.f;
-  SR_HIP_CHECK(hipEventElapsedTime(&ms, ctx->ev_k0, ctx->ev_k1));
-  ctx->last_eval_ms = ms;
+  ctx->last_eval_ms = chunk_kernel_ms(ctx);
   ctx->last_total_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
   return SR_OK;
 }
@@ -941,6 +1099,12 @@ int sr_compile_info(int dtype, int n_unary, const char* const* unary_names, int 
     return report(prog);
   }
   return set_error(SR_ERR_INVALID_ARG, "unknown dtype");
+}
+
+int sr_last_phase_ms(sr_ctx* ctx, double* out, int n) {
+  if (check_ctx(ctx) != SR_OK) return SR_ERR_INVALID_ARG;
+  for (int i = 0; i < n && i < 5; ++i) out[i] = ctx->phase_ms[i];
+  return SR_OK;
 }
 
 int sr_last_kernel_ms(sr_ctx* ctx, double* eval_ms, double* total_ms) {

@@ -6,11 +6,83 @@
 //   test/integration/ext/loopvectorization/test_nan_detection.jl:17-51.
 #include "sr_compile.h"
 
+#include <unistd.h>
+
+#include <atomic>
+#include <cstdlib>
 #include <cmath>
+#include <condition_variable>
 #include <cstring>
+#include <functional>
+#include <mutex>
 #include <thread>
 
 namespace {
+
+// Persistent compile workers: spawning threads per batch cost more than compiling 10k trees.
+// run(n, fn) calls fn(0..n-1) on the workers and the caller; one batch at a time.  A forked child
+// (no threads of its own) gets a fresh pool.
+class WorkerPool {
+ public:
+  static WorkerPool& get() {
+    static std::mutex m;
+    static WorkerPool* pool = nullptr;
+    std::lock_guard<std::mutex> g(m);
+    if (!pool || pool->pid_ != getpid()) pool = new WorkerPool();  // (a pre-fork pool is leaked)
+    return *pool;
+  }
+  int size() const { return int(threads_.size()) + 1; }
+  void run(int n, const std::function<void(int)>& fn) {
+    std::lock_guard<std::mutex> batch(batch_mu_);
+    {
+      std::lock_guard<std::mutex> g(mu_);
+      job_ = &fn;
+      n_jobs_ = n;
+      next_.store(0);
+      active_ = int(threads_.size());
+      ++gen_;
+    }
+    cv_.notify_all();
+    drain();
+    std::unique_lock<std::mutex> g(mu_);
+    done_.wait(g, [&] { return active_ == 0; });
+    job_ = nullptr;
+  }
+
+ private:
+  WorkerPool() : pid_(getpid()) {
+    unsigned hc = std::thread::hardware_concurrency();
+    int n = int(hc == 0 ? 4 : (hc > 16 ? 16 : hc));
+    if (const char* v = std::getenv("SR_AMD_COMPILE_THREADS")) n = std::atoi(v) > 0 ? std::atoi(v) : 1;
+    --n;  // the caller is a worker too
+    for (int i = 0; i < n; ++i) threads_.emplace_back([this] { loop(); });
+    for (auto& t : threads_) t.detach();  // lives for the process
+  }
+  void drain() {
+    for (int i = next_.fetch_add(1); i < n_jobs_; i = next_.fetch_add(1)) (*job_)(i);
+  }
+  void loop() {
+    uint64_t seen = 0;
+    for (;;) {
+      {
+        std::unique_lock<std::mutex> g(mu_);
+        cv_.wait(g, [&] { return gen_ != seen; });
+        seen = gen_;
+      }
+      drain();
+      std::lock_guard<std::mutex> g(mu_);
+      if (--active_ == 0) done_.notify_one();
+    }
+  }
+  pid_t pid_;
+  std::vector<std::thread> threads_;
+  std::mutex batch_mu_, mu_;
+  std::condition_variable cv_, done_;
+  const std::function<void(int)>* job_ = nullptr;
+  int n_jobs_ = 0, active_ = 0;
+  std::atomic<int> next_{0};
+  uint64_t gen_ = 0;
+};
 
 struct NameId {
   const char* name;
@@ -68,6 +140,11 @@ struct TreeCompiler {
   std::vector<int32_t> const_slot;  // pre-order constant index of constant leaves
   std::vector<int32_t> need;
   std::vector<SrIns<T>> code;
+  struct Slot {
+    int32_t parent;
+    int which;
+  };
+  std::vector<Slot> pending;  // parse() work stack (kept across trees: no per-tree allocation)
   bool bad = false;
   int err = SR_OK;
   std::string msg;
@@ -114,13 +191,9 @@ struct TreeCompiler {
     }
     t.l.assign(n, -1);
     t.r.assign(n, -1);
-    // iterative: stack of (node, children filled)
-    std::vector<int32_t> stk;
-    stk.reserve(64);
     int64_t pos = 0;
-    // recursive descent with explicit stack of pending child slots
-    struct Slot { int32_t parent; int which; };
-    std::vector<Slot> pending;
+    // recursive descent with an explicit stack of pending child slots
+    pending.clear();
     pending.push_back({-1, 0});
     while (!pending.empty()) {
       Slot s = pending.back();
@@ -270,7 +343,9 @@ struct TreeCompiler {
 
   SrIns<T> leaf_ins(int i) {
     SrIns<T> in{};
-    in.meta = kNoSlot;
+    // a constant's index: its slot in gradient programs, else 0 (the interpreter reads the X row
+    // named by every instruction's index before dispatching on the opcode)
+    in.meta = with_const_index ? kNoSlot : 0u;
     if (folded[i]) {
       in.op = SR_OP_LOAD_CONST;
       in.set_value(fold_val[i]);
@@ -413,7 +488,21 @@ struct TreeCompiler {
     n_consts = k;
   }
 
-  bool run() {
+  // Compile tree `tree` (the vectors keep their capacity from the previous tree).
+  bool run(const Tree<T>& tree) {
+    t.degree = tree.degree;
+    t.op = tree.op;
+    t.feature = tree.feature;
+    t.constant = tree.constant;
+    t.val = tree.val;
+    t.n = tree.n;
+    code.clear();
+    bad = false;
+    err = SR_OK;
+    msg.clear();
+    depth = max_depth = 0;
+    n_checks = n_consts = 0;
+    n_ops = 0;
     if (!parse()) return false;
     const int64_t n = t.n;
     folded.assign(n, 0);
@@ -494,8 +583,10 @@ int sr_compile_batch(const sr_tree_batch& trees, const SrOpset& ops, int64_t n_r
     *err = "sr_tree_batch has NULL arrays";
     return SR_ERR_INVALID_ARG;
   }
+  // per tree: where its code sits in its thread's buffer, and its summary
   struct PerTree {
-    std::vector<SrIns<T>> code;
+    int thread;
+    uint32_t begin, len;
     uint8_t bad;
     uint32_t checks, consts, cost;
     int depth;
@@ -503,24 +594,31 @@ int sr_compile_batch(const sr_tree_batch& trees, const SrOpset& ops, int64_t n_r
   };
   std::vector<PerTree> per(size_t(nt > 0 ? nt : 0));
   std::vector<int> errs(size_t(nt > 0 ? nt : 0), SR_OK);
-  std::vector<std::string> msgs;
   const T* vals = static_cast<const T*>(trees.val);
+  // work split: ~256-tree pieces over the persistent workers (small batches: the caller alone)
+  const int64_t kPiece = 256;
+  const int n_pieces = int(nt <= kPiece ? 1 : (nt + kPiece - 1) / kPiece);
+  const int nthreads = n_pieces;  // one code buffer per piece
+  std::vector<std::vector<SrIns<T>>> bufs(static_cast<size_t>(nthreads));
 
-  auto work = [&](int64_t lo, int64_t hi) {
+  auto work = [&](int w, int64_t lo, int64_t hi) {
+    TreeCompiler<T> tc(ops, n_rows, nfeatures, with_const_index);  // one per thread, reused
+    std::vector<SrIns<T>>& buf = bufs[size_t(w)];
+    buf.reserve(size_t(trees.offsets[hi] - trees.offsets[lo]));
     for (int64_t k = lo; k < hi; ++k) {
       const int64_t b = trees.offsets[k], e = trees.offsets[k + 1];
-      TreeCompiler<T> tc(ops, n_rows, nfeatures, with_const_index);
-      tc.t.degree = trees.degree + b;
-      tc.t.op = trees.op + b;
-      tc.t.feature = trees.feature + b;
-      tc.t.constant = trees.constant + b;
-      tc.t.val = vals + b;
-      tc.t.n = e - b;
       if (e < b) {
         errs[k] = SR_ERR_BAD_TREE;
         continue;
       }
-      tc.run();
+      Tree<T> tree;
+      tree.degree = trees.degree + b;
+      tree.op = trees.op + b;
+      tree.feature = trees.feature + b;
+      tree.constant = trees.constant + b;
+      tree.val = vals + b;
+      tree.n = e - b;
+      tc.run(tree);
       if (tc.err != SR_OK) {
         errs[k] = tc.err;
         continue;
@@ -528,9 +626,12 @@ int sr_compile_batch(const sr_tree_batch& trees, const SrOpset& ops, int64_t n_r
       uint32_t cost = 0;
       for (const auto& in : tc.code) cost += sr_instruction_cost(in.op);
       PerTree& p = per[k];
+      p.thread = w;
+      p.begin = uint32_t(buf.size());
+      p.len = uint32_t(tc.code.size());
+      buf.insert(buf.end(), tc.code.begin(), tc.code.end());
       p.cost = cost;
-      p.code.swap(tc.code);
-      p.bad = (tc.bad || p.code.empty()) ? 1 : 0;
+      p.bad = (tc.bad || tc.code.empty()) ? 1 : 0;
       p.checks = tc.n_checks;
       p.consts = tc.n_consts;
       p.depth = tc.max_depth;
@@ -539,22 +640,13 @@ int sr_compile_batch(const sr_tree_batch& trees, const SrOpset& ops, int64_t n_r
       for (int64_t i = b; i < e; ++i) p.ops += trees.degree[i] > 0 ? 1 : 0;
     }
   };
-  int nthreads = 1;
-  if (nt >= 4096) {
-    unsigned hc = std::thread::hardware_concurrency();
-    nthreads = int(hc == 0 ? 4 : (hc > 16 ? 16 : hc));
-  }
-  if (nthreads <= 1) {
-    work(0, nt);
+  if (n_pieces <= 1) {
+    work(0, 0, nt);
   } else {
-    std::vector<std::thread> th;
-    const int64_t chunk = (nt + nthreads - 1) / nthreads;
-    for (int w = 0; w < nthreads; ++w) {
-      const int64_t lo = w * chunk, hi = (lo + chunk < nt) ? lo + chunk : nt;
-      if (lo >= hi) break;
-      th.emplace_back(work, lo, hi);
-    }
-    for (auto& x : th) x.join();
+    WorkerPool::get().run(n_pieces, [&](int w) {
+      const int64_t lo = int64_t(w) * kPiece, hi = (lo + kPiece < nt) ? lo + kPiece : nt;
+      if (lo < hi) work(w, lo, hi);
+    });
   }
   for (int64_t k = 0; k < nt; ++k)
     if (errs[k] != SR_OK) {
@@ -573,12 +665,14 @@ int sr_compile_batch(const sr_tree_batch& trees, const SrOpset& ops, int64_t n_r
   out->total_nodes = 0;
   out->total_ops = 0;
   size_t total = 0;
-  for (int64_t k = 0; k < nt; ++k) total += per[k].code.size();
-  out->code.reserve(total);
+  for (int64_t k = 0; k < nt; ++k) total += per[k].len;
+  out->code.resize(total);
+  size_t at = 0;
   for (int64_t k = 0; k < nt; ++k) {
     const PerTree& p = per[k];
-    out->offsets[k] = uint32_t(out->code.size());
-    out->code.insert(out->code.end(), p.code.begin(), p.code.end());
+    out->offsets[k] = uint32_t(at);
+    if (p.len) std::memcpy(out->code.data() + at, bufs[size_t(p.thread)].data() + p.begin, size_t(p.len) * sizeof(SrIns<T>));
+    at += p.len;
     out->static_bad[k] = p.bad;
     out->cost[k] = p.bad ? 0u : p.cost;
     out->n_checks[k] = p.checks;

@@ -70,7 +70,7 @@ enum SrLossKind : int32_t {
 //         + and * never use CF (commuted to FC)
 //   c0 (, c1) : constant bits (C variants, LOAD_CONST*): f32 in c0, f64 in c0 | c1 << 32
 //   meta bits  0-15 : operand index: feature f (F variants, LOAD_FEAT*), stack slot k (S variants),
-//                     pre-order constant slot of a constant leaf (gradient programs; else 0xffff)
+//                     pre-order constant slot of a constant leaf (gradient programs; else 0)
 //   meta bits 24-29 : push slot + 1 (LOAD_*_PUSH)
 //   meta bit  31    : CHECK   this node's output array is validity-checked (DE early exit)
 //   (bits 16-23 stay 0, so `meta << s` with s >= 8 is the operand's byte offset for a row stride

@@ -38,6 +38,18 @@ template <int W>
 struct SrMinWaves {
   static constexpr int value = W >= 16 ? 8 : (W >= 8 ? 6 : 1);
 };
+// The f32 BASIC 8-rows/lane kernels fit 96 VGPRs (5 waves per SIMD; the interpreter loop is
+// latency-bound, so the fifth wave is worth it: C2 -4 %, arithmetic-only populations -10 %); the
+// few spills this forces sit in the tile-staging code, not in the interpreter loop.  The other
+// variants would spill inside the loop at that bound.
+#ifndef SR_MIN_WAVES_W4
+#define SR_MIN_WAVES_W4 5
+#endif
+template <typename T, int R, int TIER, int W>
+struct SrMinWavesFor {
+  static constexpr int value = (sizeof(T) == 4 && R == 8 && TIER == SR_TIER_BASIC && W == 4) ? SR_MIN_WAVES_W4
+                                                                                              : SrMinWaves<W>::value;
+};
 
 // 16-byte chunks of C values.
 template <typename T>
@@ -359,7 +371,7 @@ __device__ __forceinline__ uint4 sr_window(const void* code, uint32_t base, uint
 // lane j, the non-finite / suspicious bits in scalar masks.
 // LK: elementwise loss fixed at compile time (SR_LOSS_L2 / SR_LOSS_L1), or -1 = a.loss_kind.
 template <typename T, int R, int MODE, bool GATHER, int TIER, int W, int LK>
-__global__ void __launch_bounds__(W * 64, SrMinWaves<W>::value) sr_tile_kernel(const SrEvalArgs<T> a) {
+__global__ void __launch_bounds__(W * 64, (SrMinWavesFor<T, R, TIER, W>::value)) sr_tile_kernel(const SrEvalArgs<T> a) {
   constexpr int SR_WAVES = W;
   constexpr int SR_BLOCK = W * 64;
   using L = SrLane<T, R>;

@@ -53,6 +53,7 @@ EXPORTED_SYMBOLS = (
     "sr_eval_grad_batch",
     "sr_compile_info",
     "sr_last_kernel_ms",
+    "sr_last_phase_ms",
 )
 
 
@@ -130,6 +131,7 @@ def _load():
              c_int64, P, P, POINTER(c_int), P, c_int64],
         ),
         "sr_last_kernel_ms": (c_int, [P, POINTER(c_double), POINTER(c_double)]),
+        "sr_last_phase_ms": (c_int, [P, POINTER(c_double), c_int]),
     }
     for name, (res, args) in proto.items():
         fn = getattr(lib, name)

@@ -40,6 +40,12 @@ class DeviceContext:
         _lib.check(_lib.lib.sr_last_kernel_ms(self.handle, ctypes.byref(a), ctypes.byref(b)))
         return float(a.value), float(b.value)
 
+    def last_phase_ms(self):
+        """Host phases of the last eval_loss call: compile, upload+launch, wait, exact pass, finalize."""
+        out = (ctypes.c_double * 5)()
+        _lib.check(_lib.lib.sr_last_phase_ms(self.handle, out, 5))
+        return [float(v) for v in out]
+
     def close(self):
         if self.handle:
             _lib.lib.sr_shutdown(self.handle)

@@ -286,6 +286,35 @@ def test_ragged_sizes_and_determinism():
         assert np.max(_rel(l1[good], ol[good]), initial=0.0) < 1e-4, n
 
 
+def test_chunked_batch_matches_pieces(monkeypatch):
+    """With SR_AMD_CHUNKS, >= 4096 trees are compiled and launched in chunks (the host compiles chunk
+    c+1 while the device runs chunk c): per-tree results must not depend on the chunking —
+    bit-identical to evaluating each piece alone — and an error names the tree's index in the whole
+    batch."""
+    monkeypatch.setenv("SR_AMD_CHUNKS", "4")
+    ctx = sr_amd.device.DeviceContext(0)  # reads the environment at creation
+    opts = Options(**C2_OPTS)
+    X, y = _c2_data(3000, seed=71)
+    d = Dataset(X, y)
+    trees = gen_random_population(9000, opts, 5, max_size=30, seed=71)
+    loss, comp = eval_loss_batch(flatten_trees(trees, np.float32), d, opts, ctx=ctx)
+    parts = [eval_loss_batch(flatten_trees(trees[i:i + 1500], np.float32), d, opts, ctx=ctx) for i in range(0, 9000, 1500)]
+    assert np.array_equal(comp, np.concatenate([p[1] for p in parts]))
+    assert np.array_equal(loss, np.concatenate([p[0] for p in parts]))
+    sub = flatten_trees(trees[6500:7300], np.float32)  # straddles a chunk boundary
+    good, ol, oc = well_conditioned(Oracle.from_options(opts), sub, X, y)
+    assert np.array_equal(comp[6500:7300], oc)
+    assert np.max(_rel(loss[6500:7300][good], ol[good])) < 1e-4
+    bad = list(trees)
+    bad[8500] = Node(feature=9)  # feature out of range, in the last chunk
+    with pytest.raises(sr_amd.SRError, match="tree 8500"):
+        eval_loss_batch(bad, d, opts, ctx=ctx)
+    l2, c2 = eval_loss_batch(flatten_trees(trees, np.float32), d, opts, ctx=ctx)  # the context still works
+    assert np.array_equal(l2, loss)
+    d.free_device()
+    ctx.close()
+
+
 def test_empty_batch_and_errors():
     opts = Options(**C2_OPTS)
     X, y = _c2_data(100)

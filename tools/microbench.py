@@ -27,13 +27,16 @@ for name, kw in mixes.items():
     opts = Options(**kw)
     tb = flatten_trees(gen_random_population(10000, opts, 5, seed=1), np.float32)
     eval_loss_batch(tb, ds, opts)
-    ks, ts = [], []
+    ks, ts, ph = [], [], []
     for _ in range(5):
         t0 = time.perf_counter()
         l, c = eval_loss_batch(tb, ds, opts)
         ts.append(time.perf_counter() - t0)
         ks.append(ctx.last_kernel_ms()[0])
+        ph.append(ctx.last_phase_ms())
     k = float(np.median(ks)); t = float(np.median(ts)) * 1e3
     ne = tb.n_nodes * n
     print(f"{name:24s} nodes={tb.n_nodes:7d} ops={tb.n_operator_nodes:6d} complete={c.mean():.3f} "
-          f"kernel={k:7.3f}ms step={t:7.3f}ms  {ne / k / 1e9:8.1f} Gnode/s(kernel)  {ne / t / 1e9:8.1f} Gnode/s(step)", flush=True)
+          f"kernel={k:7.3f}ms step={t:7.3f}ms  {ne / k / 1e9:8.1f} Gnode/s(kernel)  {ne / t / 1e9:8.1f} Gnode/s(step)"
+          f"  phases(compile/launch/wait/exact/final)=" + "/".join(f"{v:.2f}" for v in np.median(np.array(ph), 0)),
+          flush=True)
