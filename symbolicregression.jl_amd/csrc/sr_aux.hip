@@ -94,11 +94,11 @@ size_t sr_tile_lds_bytes(int elem_size, int nf, int rows_per_lane, int stack_dep
          size_t(waves) * stack_depth * rows * elem_size + size_t(trees_per_block) * size_t(max_checks) * 8;
 }
 
-// Waves per workgroup: the f32 BASIC loss kernel has 4- and 16-wave builds (SR_AMD_WAVES selects);
+// Waves per workgroup: the f32 BASIC loss kernel has 4- and 8-wave (L2) builds (SR_AMD_WAVES selects);
 // every other kernel runs 4 waves.
 int sr_waves_per_block(int elem_size, int mode, int tier, int rows_per_lane, int requested) {
-  if (elem_size == 4 && mode == SR_MODE_LOSS && tier == SR_TIER_BASIC && rows_per_lane == 8 && requested == 16)
-    return 16;
+  if (elem_size == 4 && mode == SR_MODE_LOSS && tier == SR_TIER_BASIC && rows_per_lane == 8 && requested == 8)
+    return 8;
   return 4;
 }
 
@@ -119,7 +119,8 @@ hipError_t sr_launch_eval(const SrEvalArgs<T>& a, int mode, bool gather, int tie
         if (gather) return sr_launch_basic_loss<T, 8, true>(a, n_blocks, s);
         if (R == 16) return sr_launch_tile<T, 16, SR_MODE_LOSS, false, SR_TIER_BASIC>(a, n_blocks, s);
         if (R == 4) return sr_launch_tile<T, 4, SR_MODE_LOSS, false, SR_TIER_BASIC>(a, n_blocks, s);
-        if (waves == 16) return sr_launch_tile<T, 8, SR_MODE_LOSS, false, SR_TIER_BASIC, 16>(a, n_blocks, s);
+        if (waves == 8 && a.loss_kind == SR_LOSS_L2)
+          return sr_launch_tile<T, 8, SR_MODE_LOSS, false, SR_TIER_BASIC, 8, SR_LOSS_L2>(a, n_blocks, s);
         return sr_launch_basic_loss<T, 8, false>(a, n_blocks, s);
       }
       return gather ? sr_launch_tile<T, 4, SR_MODE_LOSS, true, SR_TIER_FULL>(a, n_blocks, s)

@@ -127,7 +127,7 @@ struct sr_ctx {
   int cu_count = 256;
   int rows_override = 0;    // SR_AMD_ROWS_PER_LANE (tuning): 4 selects the f32 BASIC 4-rows/lane kernel
   int tree_group = 0;       // SR_AMD_TREES_PER_BLOCK override (0 = heuristic)
-  int waves_override = 0;   // SR_AMD_WAVES (tuning): 16 selects the 16-wave f32 BASIC loss kernel
+  int waves_override = 0;   // SR_AMD_WAVES (tuning): 8 selects the 8-wave f32 BASIC L2 loss kernel
   bool cost_order = true;   // launch trees in decreasing estimated cost (SR_AMD_NO_SORT=1 disables)
   bool dead_hints = true;   // share dead-tree hints across row blocks (SR_AMD_NO_HINT=1 disables)
   int chunks = 1;           // SR_AMD_CHUNKS: pipeline compile/launch over up to this many tree chunks

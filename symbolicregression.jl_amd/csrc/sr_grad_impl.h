@@ -106,7 +106,7 @@ __global__ void __launch_bounds__(W * 64) sr_grad_kernel(const SrGradArgs<T> a) 
         const uint32_t n_here = __builtin_amdgcn_readfirstlane((pe - base < 64u) ? pe - base : 64u);
         for (uint32_t k = 0; k < n_here; ++k) {
           const uint32_t opc = uint32_t(__builtin_amdgcn_readlane(int(cw.x), int(k)));
-          const uint32_t meta = uint32_t(__builtin_amdgcn_readlane(int(cw.w), int(k)));
+          const uint32_t meta = uint32_t(__builtin_amdgcn_readlane(int(cw.y), int(k)));
           const uint32_t idx = meta & SR_M_INDEX;  // feature / stack slot / constant slot
           // operand (value + tangents): feature / stack slot / constant
           T ov = T(0);

@@ -69,6 +69,7 @@ enum SrLossKind : int32_t {
 //           + SR_P_PUSH: the old tos is first stored to stack slot `push` (a subtree's first instruction)
 //         + and * never use CF (commuted to FC)
 //   c0 (, c1) : constant bits (C variants, LOAD_CONST*): f32 in c0, f64 in c0 | c1 << 32
+//   (word order in memory: op, meta, c0, c1)
 //   meta bits  0-15 : operand index: feature f (F variants, LOAD_FEAT*), stack slot k (S variants),
 //                     pre-order constant slot of a constant leaf (gradient programs; else 0)
 //   meta bits 24-29 : push slot + 1 (LOAD_*_PUSH)
@@ -96,8 +97,8 @@ static_assert(SR_OP_BINARY0 + 6 * SR_B_COUNT <= SR_OP_PAIR0, "binary opcode rang
 template <typename T>
 struct alignas(16) SrIns {
   uint32_t op;
-  uint32_t c0, c1;
   uint32_t meta;
+  uint32_t c0, c1;  // (f32 programs use c0 only: the interpreter loads 12 of the 16 bytes)
   SR_HD inline uint32_t operand() const { return meta & SR_M_INDEX; }
   SR_HD inline int push_slot() const { return int((meta >> SR_M_PUSH_SHIFT) & 0x3fu) - 1; }
   SR_HD inline T value() const {

@@ -45,10 +45,15 @@ struct SrMinWaves {
 #ifndef SR_MIN_WAVES_W4
 #define SR_MIN_WAVES_W4 5
 #endif
+#ifndef SR_MIN_WAVES_R16
+#define SR_MIN_WAVES_R16 4
+#endif
 template <typename T, int R, int TIER, int W>
 struct SrMinWavesFor {
-  static constexpr int value = (sizeof(T) == 4 && R == 8 && TIER == SR_TIER_BASIC && W == 4) ? SR_MIN_WAVES_W4
-                                                                                              : SrMinWaves<W>::value;
+  static constexpr bool f32_basic = sizeof(T) == 4 && TIER == SR_TIER_BASIC && W == 4;
+  static constexpr int value = (f32_basic && R == 8)    ? SR_MIN_WAVES_W4
+                               : (f32_basic && R == 16) ? SR_MIN_WAVES_R16
+                                                        : SrMinWaves<W>::value;
 };
 
 // 16-byte chunks of C values.
@@ -351,13 +356,33 @@ __device__ __forceinline__ uint4 sr_load_window(const void* code, uint32_t at) {
   return *reinterpret_cast<const uint4*>(static_cast<const unsigned char*>(code) + size_t(at) * 16u);
 }
 
-// The tile interpreter's program window: instructions base .. base+SR_WIN-1 (those before `end`).
+// The tile interpreter's program window: instructions base .. base+SR_WIN-1 (those before `end`),
+// one per lane.  f32 programs load only the words they use (op, meta, c0): a loaded-but-dead c1
+// register would be reused as a temporary while the prefetch is in flight, which makes the
+// interpreter wait for the prefetch (vmcnt) at its first use of that register.
 // (An end-of-window opcode handled inside the switch would give the interpreter loop a second exit,
 // which the AMDGPU structurizer turns into per-iteration register copies: the trip count stays.)
 constexpr uint32_t SR_WIN = 64u;
-__device__ __forceinline__ uint4 sr_window(const void* code, uint32_t base, uint32_t end, int lane) {
-  uint4 w = make_uint4(0u, 0u, 0u, 0u);
-  if (base + uint32_t(lane) < end) w = sr_load_window(code, base + uint32_t(lane));
+template <typename T>
+struct SrWindow {
+  using type = uint4;
+  __device__ static __forceinline__ type load(const void* code, uint32_t at) { return sr_load_window(code, at); }
+  __device__ static __forceinline__ uint32_t c1(const type& w) { return w.w; }
+};
+template <>
+struct SrWindow<float> {
+  using type = uint3;
+  __device__ static __forceinline__ type load(const void* code, uint32_t at) {
+    const uint32_t* p = reinterpret_cast<const uint32_t*>(static_cast<const unsigned char*>(code) + size_t(at) * 16u);
+    return make_uint3(p[0], p[1], p[2]);
+  }
+  __device__ static __forceinline__ uint32_t c1(const type&) { return 0u; }
+};
+template <typename T>
+__device__ __forceinline__ typename SrWindow<T>::type sr_window(const void* code, uint32_t base, uint32_t end,
+                                                                int lane) {
+  typename SrWindow<T>::type w{};
+  if (base + uint32_t(lane) < end) w = SrWindow<T>::load(code, base + uint32_t(lane));
   return w;
 }
 
@@ -475,7 +500,7 @@ __global__ void __launch_bounds__(W * 64, (SrMinWavesFor<T, R, TIER, W>::value))
     todo &= todo - 1u;
     uint32_t nb = uint32_t(__builtin_amdgcn_readlane(int(my_pb), nj));
     uint32_t ne = uint32_t(__builtin_amdgcn_readlane(int(my_pe), nj));
-    uint4 nx = sr_window(a.code, nb, ne, lane);
+    typename SrWindow<T>::type nx = sr_window<T>(a.code, nb, ne, lane);
     int j = -1;
     uint32_t tpe = 0u;
     T tos[R];
@@ -487,7 +512,7 @@ __global__ void __launch_bounds__(W * 64, (SrMinWavesFor<T, R, TIER, W>::value))
     T mrun = T(0), mrun1 = T(0);  // FAST_CHECK: running max |v| over this lane's rows (2 chains)
     bool more = true;
     while (more) {
-      const uint4 cw = nx;
+      const typename SrWindow<T>::type cw = nx;
       const uint32_t base = nb;
       if (nj != j) {  // a new tree starts (its first instruction is a LOAD: tos needs no reset)
         j = nj;
@@ -508,11 +533,11 @@ __global__ void __launch_bounds__(W * 64, (SrMinWavesFor<T, R, TIER, W>::value))
       } else {
         more = false;
       }
-      if (more) nx = sr_window(a.code, nb, ne, lane);
+      if (more) nx = sr_window<T>(a.code, nb, ne, lane);
       const int g = wave + SR_WAVES * j;
 
       if (!dead) {
-        const uint32_t wop = cw.x, wc0 = cw.y, wc1 = cw.z, wmeta = cw.w;
+        const uint32_t wop = cw.x, wmeta = cw.y, wc0 = cw.z, wc1 = SrWindow<T>::c1(cw);
         const uint32_t n_here = __builtin_amdgcn_readfirstlane((tpe - base < SR_WIN) ? tpe - base : SR_WIN);
         // single-exit loop (a dead tree sets k past the window): a second loop exit would make
         // LLVM add an exit-selector block to every iteration
@@ -595,8 +620,8 @@ __global__ void __launch_bounds__(W * 64, (SrMinWavesFor<T, R, TIER, W>::value))
       if (base + SR_WIN >= tpe) {  // tree j is done on this tile
         const uint64_t bit = uint64_t(1) << j;
         if (MODE == SR_MODE_LOSS) {
-          T l[R];
           if (!dead) {
+            T l[R];
             T yv[R];
             L::load(y_lane, yv);
             if (weighted) {
@@ -608,54 +633,50 @@ __global__ void __launch_bounds__(W * 64, (SrMinWavesFor<T, R, TIER, W>::value))
 #pragma unroll
               for (int r = 0; r < R; ++r) l[r] = sr_elem_loss<T>(lk, tos[r], yv[r]);
             }
-          }
-          if (FAST_CHECK) {
-            // the root is always checked; a checked value was +-Inf -> incomplete; NaN anywhere
-            // reaches the root (BASIC operators propagate NaN) and shows in its loss terms (or, with
-            // weights, in the root values); a large finite one: the array-sum check may overflow
+            if (!full_tile) {  // rows past the end of the view (padding) do not count
 #pragma unroll
-            for (int r = 0; r < R; r += 4) {
-              mrun = SrMaxAbs<T>::step(mrun, tos[r], tos[r + 1]);
-              if (r + 3 < R) mrun1 = SrMaxAbs<T>::step(mrun1, tos[r + 2], tos[r + 3]);
+              for (int r = 0; r < R; ++r) l[r] = (row0 + L::row(lane, r) < a.n_rows) ? l[r] : T(0);
             }
-            mrun = SrMaxAbs<T>::step(mrun, mrun1, T(0));
-            bool nan_root = false;
-            if (weighted) {
+            // pairwise over the lane's rows (packed adds); the wave sum follows
 #pragma unroll
-              for (int r = 0; r < R; ++r) nan_root |= sr_isnan(tos[r]);
-            } else {
-              T q0 = l[0], q1 = l[1];
+            for (int h = 1; h < R; h *= 2) {
 #pragma unroll
-              for (int r = 2; r < R; r += 2) {
-                q0 += l[r];
-                q1 += l[r + 1];
+              for (int r = 0; r + h < R; r += 2 * h) l[r] += l[r + h];
+            }
+            if (FAST_CHECK) {
+              // the root is always checked; a checked value was +-Inf -> incomplete; NaN anywhere
+              // reaches the root (BASIC operators propagate NaN) and shows in the lane's loss sum
+              // (padded rows replicate a real row: masking them hides no NaN), or, with weights,
+              // in the root values; a large finite one: the array-sum check may overflow
+#pragma unroll
+              for (int r = 0; r < R; r += 4) {
+                mrun = SrMaxAbs<T>::step(mrun, tos[r], tos[r + 1]);
+                if (r + 3 < R) mrun1 = SrMaxAbs<T>::step(mrun1, tos[r + 2], tos[r + 3]);
               }
-              nan_root = sr_isnan(q0 + q1);
+              mrun = SrMaxAbs<T>::step(mrun, mrun1, T(0));
+              bool nan_root = false;
+              if (weighted) {
+#pragma unroll
+                for (int r = 0; r < R; ++r) nan_root |= sr_isnan(tos[r]);
+              } else {
+                nan_root = sr_isnan(l[0]);
+              }
+              if (sr_ballot(nan_root || !(mrun <= SrM<T>::big))) {
+                dead = true;
+              } else if (sr_ballot(!(mrun < a.tbig))) {
+                susp_any = true;
+              }
             }
-            if (sr_ballot(nan_root || !(mrun <= SrM<T>::big))) {
-              dead = true;
-            } else if (sr_ballot(!(mrun < a.tbig))) {
-              susp_any = true;
+            if (!dead) {
+              const T s = sr_wave_sum<T>(l[0]);
+              accv += (lane == j) ? double(s) : 0.0;
+              if (susp_any) bmask |= bit;
             }
           }
           if (dead) {
             dmask |= bit;
             if (use_hint && lane == 0)
               __hip_atomic_fetch_or(a.hint + tree0 + g, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          } else {
-            if (!full_tile) {  // rows past the end of the view (padding) do not count
-#pragma unroll
-              for (int r = 0; r < R; ++r) l[r] = (row0 + L::row(lane, r) < a.n_rows) ? l[r] : T(0);
-            }
-            // pairwise over the lane's rows (packed adds), then the wave
-#pragma unroll
-            for (int h = 1; h < R; h *= 2) {
-#pragma unroll
-              for (int r = 0; r + h < R; r += 2 * h) l[r] += l[r + h];
-            }
-            const T s = sr_wave_sum<T>(l[0]);
-            accv += (lane == j) ? double(s) : 0.0;
-            if (susp_any) bmask |= bit;
           }
         } else if (MODE == SR_MODE_PRED) {
           const uint32_t tree = a.perm ? a.perm[tree0 + g] : uint32_t(tree0 + g);

@@ -28,8 +28,8 @@ def compile_info(options, tb, n_rows, nfeatures, dtype):
     s = tb.to_struct()
     dt = _lib.SR_DTYPE_F32 if dtype == np.float32 else _lib.SR_DTYPE_F64
     cap = int(tb.n_nodes) + 16
-    rec = np.dtype([("op", "<u4"), ("val", "<f4"), ("c1", "<u4"), ("meta", "<u4")]) if dtype == np.float32 else \
-        np.dtype([("op", "<u4"), ("val", "<f8"), ("meta", "<u4")], align=False)
+    rec = np.dtype([("op", "<u4"), ("meta", "<u4"), ("val", "<f4"), ("c1", "<u4")]) if dtype == np.float32 else \
+        np.dtype([("op", "<u4"), ("meta", "<u4"), ("val", "<f8")], align=False)
     code = np.zeros(cap, dtype=rec)
     _lib.check(_lib.lib.sr_compile_info(dt, len(options.operators.unaops), un, len(options.operators.binops), bi,
                                         ctypes.byref(s), n_rows, nfeatures, lens.ctypes.data_as(ctypes.c_void_p),
