@@ -50,6 +50,8 @@ def main():
     ap.add_argument("--trees", type=int, default=10000)
     ap.add_argument("--cpu-trees", type=int, default=0, help="CPU-baseline tree sample (0 = auto)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--search-iters", type=int, default=2,
+                    help="iterations of the C1 search for the secondary 'search iterations/sec' figure (0 = skip)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -136,6 +138,9 @@ def main():
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         cpu = cpu_baseline(opts, tb, X, y, args.cpu_trees)
+    search = None
+    if rank == 0 and world == 1 and args.search_iters > 0:
+        search = search_throughput(args.search_iters)
 
     if rank == 0:
         line = {
@@ -179,10 +184,32 @@ def main():
                 "bytes_convention": "ceil(n_trees/G) passes x (nf+1) x n_rows x 4 B; X/y re-reads are served from L2/MALL",
             },
             "cpu_baseline": cpu,
+            "search": search,
         }
         print(json.dumps(line), flush=True)
     if dist is not None:
         dist.destroy_process_group()
+
+
+def search_throughput(niterations):
+    """BASELINE.json metric, second half: search iterations/sec on C1 (README example: X = randn(2, 100)
+    f64, ops + * / - cos exp, 20 populations, default options), lock-step islands with one batched
+    device scoring call per evolution round (sr_amd.search.equation_search).  Iterations/sec counts
+    completed s_r_cycles (one per island per iteration, src/SymbolicRegression.jl:1091) per wall s."""
+    from sr_amd import equation_search
+
+    rng = np.random.default_rng(0)
+    Xs = rng.standard_normal((2, 100))
+    ys = 2 * np.cos(Xs[1]) + Xs[0] ** 2 - 2
+    sopts = Options(binary_operators=["+", "*", "/", "-"], unary_operators=["cos", "exp"], populations=20)
+    t0 = time.perf_counter()
+    res = equation_search(Xs, ys, niterations=niterations, options=sopts, seed=0)
+    wall = time.perf_counter() - t0
+    return {"metric": "search iterations/sec", "value": res.s_r_cycles / wall, "unit": "s_r_cycles/s",
+            "iterations_per_s": niterations / wall, "islands": sopts.populations, "iterations": niterations,
+            "wall_s": wall, "device_calls": res.device_calls,
+            "best_loss": float(min(m.loss for m in res.pareto_frontier)),
+            "config": "C1 README example, X=randn(2,100) f64, 20 populations, default options"}
 
 
 def measured_traffic():
