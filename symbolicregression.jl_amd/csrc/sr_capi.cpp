@@ -427,8 +427,12 @@ int run_exact(sr_ctx* ctx, const sr_dataset* ds, const SrProgramBatch<T>& prog, 
   const int64_t n_eval = gather ? n_idx : ds->n;
   hipStream_t s = ctx->stream;
   const int depth = prog.max_depth > 0 ? prog.max_depth : 1;
-  Grid g = make_grid<T>(n_eval, 1, sr_rows_per_lane<T>(SR_MODE_EXACT, SR_TIER_FULL, 0), 4, int(ds->nf), depth,
-                        max_checks, ds->w != nullptr, 1);
+  // several listed trees per workgroup share one staged row tile (the heuristic G: >= 4096 workgroups)
+  Grid g = make_grid<T>(n_eval, n_list, sr_rows_per_lane<T>(SR_MODE_EXACT, SR_TIER_FULL, 0), 4, int(ds->nf), depth,
+                        max_checks, ds->w != nullptr, 0);
+  if (g.lds > kLdsMax)  // many checks: one tree per workgroup
+    g = make_grid<T>(n_eval, n_list, sr_rows_per_lane<T>(SR_MODE_EXACT, SR_TIER_FULL, 0), 4, int(ds->nf), depth,
+                     max_checks, ds->w != nullptr, 1);
   if (g.lds > kLdsMax) return set_error(SR_ERR_TOO_DEEP, "exact-sum pass needs more LDS than 160 KiB");
   std::vector<uint32_t> list32(static_cast<size_t>(n_list));
   for (int64_t i = 0; i < n_list; ++i) list32[size_t(i)] = uint32_t(list[i]);
@@ -443,7 +447,7 @@ int run_exact(sr_ctx* ctx, const sr_dataset* ds, const SrProgramBatch<T>& prog, 
   a.code = ctx->code.as<SrIns<T>>();
   a.offsets = ctx->offsets.as<uint32_t>();
   a.n_trees = int(n_list);
-  a.trees_per_block = 1;
+  a.trees_per_block = g.G;
   a.X = static_cast<const T*>(ds->X);
   a.y = static_cast<const T*>(ds->y);
   a.w = static_cast<const T*>(ds->w);
@@ -453,7 +457,7 @@ int run_exact(sr_ctx* ctx, const sr_dataset* ds, const SrProgramBatch<T>& prog, 
   a.nf = int(ds->nf);
   a.tiles_per_block = g.tiles;
   a.n_row_blocks = g.n_row_blocks;
-  a.n_groups = int(n_list);
+  a.n_groups = g.n_groups;
   a.stack_depth = depth;
   a.tbig = T(0);
   a.part_sum = ctx->part_sum.as<double>();
@@ -463,7 +467,7 @@ int run_exact(sr_ctx* ctx, const sr_dataset* ds, const SrProgramBatch<T>& prog, 
   a.check_sums = ctx->check_sums.as<double>();
   // f64 sums can overflow f64 itself: scale by 2^-64 (the threshold is scaled identically)
   a.scale = sizeof(T) == 8 ? std::ldexp(1.0, -64) : 1.0;
-  const int64_t blocks = int64_t(g.n_row_blocks) * n_list;
+  const int64_t blocks = g.n_blocks;
   if (blocks > 0x7fffffff) return set_error(SR_ERR_INVALID_ARG, "grid too large");
   SR_HIP_CHECK(sr_launch_eval<T>(a, SR_MODE_EXACT, gather, SR_TIER_FULL, 0, 4, int(blocks), s));
   SR_HIP_CHECK(hipMemcpyAsync(host_sums, ctx->check_sums.p, size_t(n_list) * max_checks * sizeof(double),
