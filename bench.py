@@ -75,6 +75,7 @@ def main():
     s = tb.to_struct()
     nt = tb.n_trees
 
+    launches = []
     if world == 1:
         losses = np.empty(nt, dtype=np.float32)
         comp = np.empty(nt, dtype=np.uint8)
@@ -83,6 +84,7 @@ def main():
             _lib.check(_lib.lib.sr_eval_loss_batch(ctx.handle, dsh, oid, ctypes.byref(s), None, 0, 0,
                                                    losses.ctypes.data_as(ctypes.c_void_p),
                                                    comp.ctypes.data_as(ctypes.c_void_p)))
+            launches.append(ctx.last_launches())
             return ctx.last_kernel_ms()[0]
 
         def barrier():
@@ -96,6 +98,7 @@ def main():
 
         def step():
             result["loss"], result["comp"] = eval_loss_sharded(tb, ds, opts, n_total)
+            launches.append(ctx.last_launches())
             return ctx.last_kernel_ms()[0]
 
         def barrier():
@@ -118,18 +121,20 @@ def main():
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         dt = float(tt.item())
 
-    grid_g = int(os.environ.get("SR_AMD_TREES_PER_BLOCK", "0")) or 128  # trees sharing one staged row tile
     nodes = int(tb.n_nodes)
     ops = int(tb.n_operator_nodes)
     node_evals = float(nodes) * float(n_total)            # all ranks
     value = node_evals * args.steps / dt
-    # roofline of the interpreter kernel on this GPU: algorithmic flops per launch / kernel time
-    flops_per_launch = float(args.rows) * (ops + 3 * nt)
+    # roofline of the interpreter kernel on this GPU: algorithmic flops of a step's interpreter work
+    # / the step's interpreter time (Σ of its launch durations: the batch is compiled and launched in
+    # `launches_per_step` chunks; a kernel trace's per-launch average x launches_per_step = kmean)
+    flops_per_step = float(args.rows) * (ops + 3 * nt)
     kmean = float(np.mean(kernel_ms))
-    achieved = flops_per_launch / (kmean * 1e-3) / 1e12
-    # algorithmic bytes of the interpreter launch: one pass of X + y per tree group
-    n_passes = -(-nt // min(grid_g, nt))
-    bytes_per_launch = float(n_passes) * (5 + 1) * float(args.rows) * 4.0
+    n_launch = int(round(float(np.mean(launches[-args.steps:])))) if launches else 1
+    achieved = flops_per_step / (kmean * 1e-3) / 1e12
+    # algorithmic bytes: one pass of X + y per tree group of every launch
+    n_passes = sum(-(-c // g) for c, g in chunk_groups(nt, args.rows, n_launch))
+    bytes_per_step = float(n_passes) * (5 + 1) * float(args.rows) * 4.0
     traffic = measured_traffic()
     if world > 1:
         comp = result["comp"]
@@ -173,14 +178,17 @@ def main():
                 "peak": PEAK_FP32_TFLOPS,
                 "unit": "TFLOP/s",
                 "frac": achieved / PEAK_FP32_TFLOPS,
-                "traffic": traffic.get("hbm_read_bytes_per_launch") if traffic else None,
+                "traffic": traffic.get("hbm_read_bytes_per_launch") * n_launch if traffic else None,
                 "traffic_source": traffic.get("source") if traffic else None,
                 "kernel": "sr_tile_kernel<float,8,LOSS,gather=false,BASIC>",
                 "kernel_ms_mean": kmean,
-                "flops_per_launch": flops_per_launch,
+                "launches_per_step": n_launch,
+                "kernel_ms_convention": "per step: sum of the interpreter launches' HIP-event durations (library stream)",
+                "flops_per_step": flops_per_step,
                 "flop_convention": "n_rows * sum_t(n_op(t) + 3), 1 flop per operator incl. transcendentals (SURVEY 8d)",
-                "algorithmic_bytes_per_launch": bytes_per_launch,
-                "algorithmic_GBps": bytes_per_launch / (kmean * 1e-3) / 1e9,
+                "algorithmic_bytes_per_step": bytes_per_step,
+                "algorithmic_GBps": bytes_per_step / (kmean * 1e-3) / 1e9,
+                "per_step": "achieved, traffic and bytes are per step (all launches of the step)",
                 "bytes_convention": "ceil(n_trees/G) passes x (nf+1) x n_rows x 4 B; X/y re-reads are served from L2/MALL",
             },
             "cpu_baseline": cpu,
@@ -189,6 +197,24 @@ def main():
         print(json.dumps(line), flush=True)
     if dist is not None:
         dist.destroy_process_group()
+
+
+def chunk_groups(nt, rows, n_launch):
+    """(trees, trees per workgroup) of each interpreter launch of a step, as csrc/sr_capi.cpp's
+    run_batch / make_grid split them (2 launches: a first chunk of nt/6 trees)."""
+    tiles = -(-rows // 512)
+    n_rb = -(-tiles // (-(-tiles // 256)))
+    bounds = [0, nt // 6, nt] if n_launch == 2 else [nt * k // n_launch for k in range(n_launch + 1)]
+    out = []
+    for a, b in zip(bounds[:-1], bounds[1:]):
+        c = b - a
+        g = int(os.environ.get("SR_AMD_TREES_PER_BLOCK", "0"))
+        if not g:
+            g = 128
+            while g > 4 and n_rb * (-(-c // g)) < 4096:
+                g //= 2
+        out.append((c, max(1, min(g, c))))
+    return out
 
 
 def search_throughput(niterations):

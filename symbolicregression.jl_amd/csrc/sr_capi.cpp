@@ -101,6 +101,8 @@ constexpr int kMaxChunks = 4;
 struct sr_ctx {
   int device = 0;
   hipStream_t stream = nullptr;
+  hipStream_t stream2 = nullptr;  // second stream of the chunked pipeline (odd chunks)
+  hipEvent_t ev_join = nullptr;
   hipEvent_t ev_start = nullptr, ev_k0 = nullptr, ev_k1 = nullptr, ev_end = nullptr;
   hipEvent_t ev_c0[kMaxChunks] = {}, ev_c1[kMaxChunks] = {};  // per-chunk interpreter launches
   int n_chunks_last = 0;
@@ -130,7 +132,7 @@ struct sr_ctx {
   int waves_override = 0;   // SR_AMD_WAVES (tuning): 8 selects the 8-wave f32 BASIC L2 loss kernel
   bool cost_order = true;   // launch trees in decreasing estimated cost (SR_AMD_NO_SORT=1 disables)
   bool dead_hints = true;   // share dead-tree hints across row blocks (SR_AMD_NO_HINT=1 disables)
-  int chunks = 1;           // SR_AMD_CHUNKS: pipeline compile/launch over up to this many tree chunks
+  int chunks = 2;           // SR_AMD_CHUNKS: pipeline compile/launch over this many tree chunks (1 = off)
   std::vector<uint32_t> perm_host;
 };
 
@@ -237,13 +239,21 @@ int run_batch(sr_ctx* ctx, const sr_dataset* ds, int opset_id, const sr_tree_bat
   const int R = sr_rows_per_lane<T>(mode, tier, ctx->rows_override);
   const int W = sr_waves_per_block(int(sizeof(T)), mode, tier, R, ctx->waves_override);
   hipStream_t s = ctx->stream;
+  // error exits while chunks are in flight: no DMA may still read the staging buffers
+  auto sync_both = [&] {
+    (void)hipStreamSynchronize(s);
+    (void)hipStreamSynchronize(ctx->stream2);
+  };
 
-  // chunking (SR_AMD_CHUNKS, default 1): LOSS mode only (PRED writes rows by caller tree index),
-  // >= kChunkTrees trees each.  Measured on the C2 population: 4 chunks cost more kernel time (each
-  // launch drains its own tail) than they hide once compiling is ~0.5 ms.
+  // chunking (SR_AMD_CHUNKS, default 2; LOSS mode only — PRED writes rows by caller tree index).
+  // Default: a first chunk of 1/6 of the trees runs while the host compiles the rest (exposed compile
+  // 0.72 -> 0.27 ms on C2, every test population's step faster).  k > 2 equal chunks (>= 2048 trees
+  // each) alternate over the two streams; they cost kernel time on complete-heavy populations.
   constexpr int64_t kChunkTrees = 2048;
   int n_chunks = 1;
-  if (mode == SR_MODE_LOSS && ctx->chunks > 1) {
+  if (mode == SR_MODE_LOSS && ctx->chunks == 2) {
+    n_chunks = nt / 6 >= kChunkTrees / 2 ? 2 : 1;  // the small first chunk holds >= 1024 trees
+  } else if (mode == SR_MODE_LOSS && ctx->chunks > 2) {
     const int64_t k = nt / kChunkTrees;
     const int64_t cap = ctx->chunks < kMaxChunks ? ctx->chunks : kMaxChunks;
     n_chunks = int(k < 1 ? 1 : (k > cap ? cap : k));
@@ -293,19 +303,32 @@ int run_batch(sr_ctx* ctx, const sr_dataset* ds, int opset_id, const sr_tree_bat
   if (gather)
     SR_HIP_CHECK(hipMemcpyAsync(ctx->row_idx.p, row_idx, size_t(n_idx) * sizeof(int64_t), hipMemcpyHostToDevice, s));
   if (use_hint) SR_HIP_CHECK(hipMemsetAsync(ctx->hint.p, 0, size_t(nt) * sizeof(uint32_t), s));
+  if (n_chunks > 1) {  // odd chunks run on the second stream, after the shared setup above
+    SR_HIP_CHECK(hipEventRecord(ctx->ev_join, s));
+    SR_HIP_CHECK(hipStreamWaitEvent(ctx->stream2, ctx->ev_join, 0));
+  }
 
   uint32_t code_base = 0;
   Grid glast = g0;
   std::string err;
   for (int c = 0; c < n_chunks && nt > 0; ++c) {
-    const int64_t t0 = nt * c / n_chunks, t1 = nt * (c + 1) / n_chunks, nc = t1 - t0;
+    // two chunks: a small first one (1/6) runs while the host compiles the rest, so the exposed
+    // compile time is the small chunk's; more chunks: equal pieces
+    auto bound = [&](int k) -> int64_t {
+      if (k <= 0) return 0;
+      if (k >= n_chunks) return nt;
+      return n_chunks == 2 ? nt / 6 : nt * k / n_chunks;
+    };
+    const int64_t t0 = bound(c), t1 = bound(c + 1), nc = t1 - t0;
+    // chunks alternate between two streams: chunk c+1's workgroups fill the GPU while chunk c drains
+    const hipStream_t cs = (c & 1) ? ctx->stream2 : s;
     sr_tree_batch sub = *trees;
     sub.n_trees = nc;
     sub.offsets = trees->offsets + t0;  // node arrays stay indexed by absolute offsets
     SrProgramBatch<T> pc;
     int rc = sr_compile_batch<T>(sub, ctx->opsets[opset_id], n_total, ds->nf, false, &pc, &err);
     if (rc != SR_OK) {
-      (void)hipStreamSynchronize(s);  // earlier chunks may still read the staging buffers
+      sync_both();  // earlier chunks may still read the staging buffers
       if (rc == SR_ERR_BAD_TREE || rc == SR_ERR_INVALID_ARG) {
         // report the tree index of the whole batch
         const size_t at = err.find("tree ");
@@ -320,7 +343,7 @@ int run_batch(sr_ctx* ctx, const sr_dataset* ds, int opset_id, const sr_tree_bat
     const int depth = pc.max_depth > 0 ? pc.max_depth : 1;
     Grid g = make_grid<T>(n_eval, nc, R, W, int(ds->nf), depth, 0, ds->w != nullptr, ctx->tree_group);
     if (g.lds > kLdsMax) {
-      (void)hipStreamSynchronize(s);
+      sync_both();
       return set_error(SR_ERR_TOO_DEEP, "the row tile (" + std::to_string(ds->nf) + " features, " +
                                             std::to_string(depth) + " stack slots) needs " + std::to_string(g.lds) +
                                             " bytes of LDS; the limit is 160 KiB");
@@ -329,7 +352,7 @@ int run_batch(sr_ctx* ctx, const sr_dataset* ds, int opset_id, const sr_tree_bat
     // stage: code at code_base, offsets made absolute, static_bad, launch order (chunk-local)
     const size_t ncode = pc.code.size();
     if (code_base + ncode > code_cap) {
-      (void)hipStreamSynchronize(s);
+      sync_both();
       return set_error(SR_ERR_INVALID_ARG, "program longer than its node count");
     }
     if (ncode) std::memcpy(h_code + code_base, pc.code.data(), ncode * sizeof(SrIns<T>));
@@ -349,12 +372,12 @@ int run_batch(sr_ctx* ctx, const sr_dataset* ds, int opset_id, const sr_tree_bat
     }
     if (ncode)
       SR_HIP_CHECK(hipMemcpyAsync(ctx->code.as<SrIns<T>>() + code_base, h_code + code_base, ncode * sizeof(SrIns<T>),
-                                  hipMemcpyHostToDevice, s));
+                                  hipMemcpyHostToDevice, cs));
     SR_HIP_CHECK(hipMemcpyAsync(ctx->offsets.as<uint32_t>() + t0, h_off + t0, size_t(nc + 1) * sizeof(uint32_t),
-                                hipMemcpyHostToDevice, s));
-    SR_HIP_CHECK(hipMemcpyAsync(ctx->static_bad.as<uint8_t>() + t0, h_bad + t0, size_t(nc), hipMemcpyHostToDevice, s));
+                                hipMemcpyHostToDevice, cs));
+    SR_HIP_CHECK(hipMemcpyAsync(ctx->static_bad.as<uint8_t>() + t0, h_bad + t0, size_t(nc), hipMemcpyHostToDevice, cs));
     SR_HIP_CHECK(hipMemcpyAsync(ctx->perm.as<uint32_t>() + t0, h_perm + t0, size_t(nc) * sizeof(uint32_t),
-                                hipMemcpyHostToDevice, s));
+                                hipMemcpyHostToDevice, cs));
     // merged summary
     for (int64_t i = 0; i <= nc; ++i) prog->offsets[size_t(t0 + i)] = h_off[t0 + i];
     std::memcpy(prog->static_bad.data() + t0, pc.static_bad.data(), size_t(nc));
@@ -390,16 +413,20 @@ int run_batch(sr_ctx* ctx, const sr_dataset* ds, int opset_id, const sr_tree_bat
     a.pred_ld = n_eval;
     a.scale = 1.0;
     if (g.n_blocks > 0x7fffffff || g.n_row_blocks != n_rb) {
-      (void)hipStreamSynchronize(s);
+      sync_both();
       return set_error(SR_ERR_INVALID_ARG, "grid too large");
     }
-    SR_HIP_CHECK(hipEventRecord(ctx->ev_c0[c], s));
-    SR_HIP_CHECK(sr_launch_eval<T>(a, mode, gather, tier, ctx->rows_override, g.W, int(g.n_blocks), s));
-    SR_HIP_CHECK(hipEventRecord(ctx->ev_c1[c], s));
+    SR_HIP_CHECK(hipEventRecord(ctx->ev_c0[c], cs));
+    SR_HIP_CHECK(sr_launch_eval<T>(a, mode, gather, tier, ctx->rows_override, g.W, int(g.n_blocks), cs));
+    SR_HIP_CHECK(hipEventRecord(ctx->ev_c1[c], cs));
     SR_HIP_CHECK(sr_launch_reduce(a.part_sum, a.part_flag, int(nc), n_rb, a.perm, ctx->static_bad.as<uint8_t>() + t0,
-                                  ctx->out_sum.as<double>() + t0, ctx->out_flag.as<uint32_t>() + t0, s));
+                                  ctx->out_sum.as<double>() + t0, ctx->out_flag.as<uint32_t>() + t0, cs));
     ctx->n_chunks_last = c + 1;
     code_base += uint32_t(ncode);
+  }
+  if (n_chunks > 1) {  // the caller continues on the first stream: join the second
+    SR_HIP_CHECK(hipEventRecord(ctx->ev_join, ctx->stream2));
+    SR_HIP_CHECK(hipStreamWaitEvent(s, ctx->ev_join, 0));
   }
   if (nt == 0) ctx->mark_phase(0);
   *grid_out = glast;
@@ -407,7 +434,8 @@ int run_batch(sr_ctx* ctx, const sr_dataset* ds, int opset_id, const sr_tree_bat
   return SR_OK;
 }
 
-// Σ of the interpreter launch times of the last run_batch (ms).
+// Interpreter time of the last run_batch (ms): Σ of its launches' durations (as a kernel trace sums
+// them; chunks on the two streams may overlap, so this can exceed the wall time they span).
 inline double chunk_kernel_ms(sr_ctx* ctx) {
   double ms = 0.0;
   for (int c = 0; c < ctx->n_chunks_last; ++c) {
@@ -826,6 +854,8 @@ int sr_init(int device, sr_ctx** out) {
   if (const char* v = std::getenv("SR_AMD_NO_HINT")) ctx->dead_hints = std::atoi(v) == 0;
   if (const char* v = std::getenv("SR_AMD_CHUNKS")) ctx->chunks = std::atoi(v);
   hipError_t e = hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking);
+  if (e == hipSuccess) e = hipStreamCreateWithFlags(&ctx->stream2, hipStreamNonBlocking);
+  if (e == hipSuccess) e = hipEventCreateWithFlags(&ctx->ev_join, hipEventDisableTiming);
   if (e == hipSuccess) e = hipEventCreate(&ctx->ev_start);
   if (e == hipSuccess) e = hipEventCreate(&ctx->ev_k0);
   if (e == hipSuccess) e = hipEventCreate(&ctx->ev_k1);
@@ -858,6 +888,9 @@ int sr_shutdown(sr_ctx* ctx) {
       (void)hipEventDestroy(ctx->ev_c0[c]);
       (void)hipEventDestroy(ctx->ev_c1[c]);
     }
+    (void)hipStreamSynchronize(ctx->stream2);
+    (void)hipEventDestroy(ctx->ev_join);
+    (void)hipStreamDestroy(ctx->stream2);
     (void)hipEventDestroy(ctx->ev_start);
     (void)hipEventDestroy(ctx->ev_k0);
     (void)hipEventDestroy(ctx->ev_k1);
@@ -1108,6 +1141,7 @@ int sr_compile_info(int dtype, int n_unary, const char* const* unary_names, int 
 int sr_last_phase_ms(sr_ctx* ctx, double* out, int n) {
   if (check_ctx(ctx) != SR_OK) return SR_ERR_INVALID_ARG;
   for (int i = 0; i < n && i < 5; ++i) out[i] = ctx->phase_ms[i];
+  if (n > 5) out[5] = double(ctx->n_chunks_last);
   return SR_OK;
 }
 

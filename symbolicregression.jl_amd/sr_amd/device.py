@@ -42,9 +42,15 @@ class DeviceContext:
 
     def last_phase_ms(self):
         """Host phases of the last eval_loss call: compile, upload+launch, wait, exact pass, finalize."""
-        out = (ctypes.c_double * 5)()
-        _lib.check(_lib.lib.sr_last_phase_ms(self.handle, out, 5))
-        return [float(v) for v in out]
+        out = (ctypes.c_double * 6)()
+        _lib.check(_lib.lib.sr_last_phase_ms(self.handle, out, 6))
+        return [float(v) for v in out[:5]]
+
+    def last_launches(self):
+        """Interpreter launches of the last eval_loss call (chunked compile/launch pipeline)."""
+        out = (ctypes.c_double * 6)()
+        _lib.check(_lib.lib.sr_last_phase_ms(self.handle, out, 6))
+        return int(out[5])
 
     def close(self):
         if self.handle:

@@ -313,6 +313,10 @@ def test_chunked_batch_matches_pieces(monkeypatch):
     assert np.array_equal(l2, loss)
     d.free_device()
     ctx.close()
+    # the default context: two chunks (a small first one while the rest compiles)
+    d2 = Dataset(X, y)
+    l3, c3 = eval_loss_batch(flatten_trees(trees, np.float32), d2, opts)
+    assert np.array_equal(l3, loss) and np.array_equal(c3, comp)
 
 
 def test_empty_batch_and_errors():
