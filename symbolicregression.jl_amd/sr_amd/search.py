@@ -88,12 +88,12 @@ class PopMember:
     """src/PopMember.jl: tree, cost, loss, birth order, complexity, ref / parent."""
     __slots__ = ("tree", "cost", "loss", "birth", "complexity", "ref", "parent")
 
-    def __init__(self, tree, cost, loss, complexity, parent=-1):
+    def __init__(self, tree, cost, loss, complexity, parent=-1, birth=None):
         self.tree = tree
         self.cost = float(cost)
         self.loss = float(loss)
         self.complexity = int(complexity)
-        self.birth = _next_birth()
+        self.birth = _next_birth() if birth is None else birth
         self.ref = _next_ref()
         self.parent = parent
 
@@ -407,13 +407,13 @@ def replace_oldest(pop, babies):
         pop[oldest] = b
 
 
-def migrate(candidates, pop, frac, rng):
-    """migrate! (src/Migration.jl:15-37): Poisson(n * frac) members replaced by copies."""
+def migrate(candidates, pop, frac, rng, birth=_next_birth):
+    """migrate! (src/Migration.jl:15-37): Poisson(n * frac) members replaced by copies (newest birth)."""
     n = len(pop)
     k = min(int(rng.poisson(n * frac)), len(candidates), n)
     for loc in rng.integers(0, n, size=max(k, 0)):
         m = candidates[int(rng.integers(0, len(candidates)))].copy()
-        m.birth = _next_birth()
+        m.birth = birth()
         pop[int(loc)] = m
 
 
@@ -472,18 +472,58 @@ def _accept(pl, after_cost, new_size, snap, maxsize, so, rng):
     return not (prob < rng.random())
 
 
+def _torch_comm():
+    """(rank, world, allgather_object) of the default torch.distributed group, or None."""
+    try:
+        import torch.distributed as tdist
+    except ImportError:  # pragma: no cover
+        return None
+    if not (tdist.is_available() and tdist.is_initialized()) or tdist.get_world_size() == 1:
+        return None
+    world = tdist.get_world_size()
+
+    def allgather(obj):
+        out = [None] * world
+        tdist.all_gather_object(out, obj)
+        return out
+
+    return tdist.get_rank(), world, allgather
+
+
 def equation_search(X=None, y=None, *, niterations=10, options, weights=None, search_options=None, seed=0,
-                    verbosity=0, dataset=None):
-    """Batched-island ``equation_search`` on the device scoring path -> SearchResult."""
+                    verbosity=0, dataset=None, distributed=False, _score_fn=None):
+    """Batched-island ``equation_search`` on the device scoring path -> SearchResult.
+
+    distributed=True (torch.distributed initialised, one process per GPU; SURVEY §8(e) island
+    sharding): island i lives on rank i % world; every rank scores only its islands' children (one
+    batched launch per round on its own GPU) and after each iteration the ranks all-gather their
+    islands (members + best-seen) and replay the head node's island-by-island bookkeeping — running
+    statistics, hall of fame, Pareto frontier — identically; migration into island i is done by its
+    owner with the island's own random stream.  Random streams and birth counters are per island, so
+    with constant optimisation off the result equals the single-process search's (tested); the
+    constant-optimisation perturbations come from a per-rank stream.
+    ``_score_fn(trees, dataset) -> (costs, losses)`` replaces the device scorer (CPU tests only)."""
     so = search_options or SearchOptions()
+    comm = _torch_comm() if distributed else None
+    rank, world, allgather = comm if comm else (0, 1, None)
     if dataset is None:
         dataset = Dataset(np.asarray(X), np.asarray(y), weights=weights)
-    update_baseline_loss_(dataset, options)
+    if _score_fn is None:
+        update_baseline_loss_(dataset, options)
+    else:  # update_baseline_loss! through the injected scorer
+        dataset.use_baseline, dataset.baseline_loss = True, dataset.dtype.type(1)
+        bl = _score_fn([Node(val=dataset.dtype.type(0))], dataset)[1][0]
+        if np.isfinite(bl):
+            dataset.baseline_loss = dataset.dtype.type(bl)
+        else:
+            dataset.use_baseline, dataset.baseline_loss = False, dataset.dtype.type(1)
     T = dataset.dtype.type
     nfeatures = dataset.nfeatures
     npop = options.populations
+    owned = [i for i in range(npop) if i % world == rank]
     rngs = [np.random.default_rng([seed, i]) for i in range(npop)]
-    head_rng = np.random.default_rng([seed, 1_000_003])
+    births = [_Counter() for _ in range(npop)]  # birth order per island (replace_oldest compares within one)
+    head_rng = np.random.default_rng([seed, 1_000_003, rank])
     maxsize = options.maxsize
     tweights = tournament_selection_weights(options)
     calls = [0]
@@ -493,19 +533,36 @@ def equation_search(X=None, y=None, *, niterations=10, options, weights=None, se
         if not trees:
             return np.zeros(0), np.zeros(0)
         calls[0] += 1
+        if _score_fn is not None:
+            return _score_fn(trees, ds)
         return eval_cost_batch(trees, ds, options, complexities=[t.count_nodes() for t in trees])
 
-    # initial populations: one batched scoring launch for every island
-    init = [random_population_trees(options.population_size, options, nfeatures, T, rngs[i]) for i in range(npop)]
-    flat = [t for pop in init for t in pop]
+    def exchange(pops, best_seen=None):
+        """All-gather the owned islands (members, best-seen) so every rank holds all of them."""
+        if world == 1:
+            return
+        mine = {i: (pops[i], None if best_seen is None else (best_seen[i].members, best_seen[i].exists))
+                for i in owned}
+        for part in allgather(mine):
+            for i, (members, bs) in part.items():
+                if i % world == rank:
+                    continue
+                pops[i] = members
+                if best_seen is not None:
+                    best_seen[i].members, best_seen[i].exists = bs
+
+    # initial populations: one batched scoring launch for every (owned) island
+    init = {i: random_population_trees(options.population_size, options, nfeatures, T, rngs[i]) for i in owned}
+    flat = [t for i in owned for t in init[i]]
     c, l = score(flat, dataset)
-    pops, k = [], 0
-    for i in range(npop):
+    pops, k = [None] * npop, 0
+    for i in owned:
         pop = []
         for t in init[i]:
-            pop.append(PopMember(t, c[k], l[k], t.count_nodes()))
+            pop.append(PopMember(t, c[k], l[k], t.count_nodes(), birth=births[i]()))
             k += 1
-        pops.append(pop)
+        pops[i] = pop
+    exchange(pops)
     stats = RunningSearchStatistics(maxsize)
     hof = HallOfFame(maxsize)
     best_sub_pops = [sorted(p, key=lambda m: m.cost)[: so.topn] for p in pops]
@@ -528,7 +585,7 @@ def equation_search(X=None, y=None, *, niterations=10, options, weights=None, se
         for temperature in temps:
             for _ in range(n_evol):
                 plans, pending = [], []
-                for i in range(npop):  # host: every island selects and mutates (or crosses over)
+                for i in owned:  # host: every island selects and mutates (or crosses over)
                     rng, pop = rngs[i], pops[i]
                     if rng.random() > so.crossover_probability:
                         allstar = best_of_sample(pop, snap, options, so, rng, tweights)
@@ -567,38 +624,42 @@ def equation_search(X=None, y=None, *, niterations=10, options, weights=None, se
                 costs, losses = score(pending, ds_iter)  # device: ONE batched eval_cost for all islands
                 num_evals += len(pending) * ds_iter.dataset_fraction()
                 for pl in plans:  # host: per-island acceptance, replacing the oldest member(s)
-                    rng, pop = rngs[pl.island], pops[pl.island]
+                    i = pl.island
+                    rng, pop, born = rngs[i], pops[i], births[i]
                     if pl.kind == "reject":
                         if not so.skip_mutation_failures:
                             baby = pl.parent.copy()
-                            baby.birth, baby.parent = _next_birth(), pl.parent.ref
+                            baby.birth, baby.parent = born(), pl.parent.ref
                             replace_oldest(pop, [baby])
                         continue
                     if pl.kind == "keep":
                         p = pl.parent
-                        replace_oldest(pop, [PopMember(p.tree.copy(), p.cost, p.loss, p.complexity, parent=p.ref)])
+                        replace_oldest(pop, [PopMember(p.tree.copy(), p.cost, p.loss, p.complexity, parent=p.ref,
+                                                       birth=born())])
                         continue
                     if pl.kind == "cross":
                         j = pl.slot
-                        b1 = PopMember(pl.tree, costs[j], losses[j], pl.tree.count_nodes(), parent=pl.parent.ref)
+                        b1 = PopMember(pl.tree, costs[j], losses[j], pl.tree.count_nodes(), parent=pl.parent.ref,
+                                       birth=born())
                         b2 = PopMember(pl.tree2, costs[j + 1], losses[j + 1], pl.tree2.count_nodes(),
-                                       parent=pl.parent2.ref)
+                                       parent=pl.parent2.ref, birth=born())
                         replace_oldest(pop, [b1, b2])
                         continue
                     j = pl.slot
                     new_size = pl.tree.count_nodes()
                     if _accept(pl, float(costs[j]), new_size, snap, maxsize, so, rng):
-                        replace_oldest(pop, [PopMember(pl.tree, costs[j], losses[j], new_size, parent=pl.parent.ref)])
+                        replace_oldest(pop, [PopMember(pl.tree, costs[j], losses[j], new_size, parent=pl.parent.ref,
+                                                       birth=born())])
                     elif not so.skip_mutation_failures:
                         baby = pl.parent.copy()
-                        baby.birth, baby.parent = _next_birth(), pl.parent.ref
+                        baby.birth, baby.parent = born(), pl.parent.ref
                         replace_oldest(pop, [baby])
-            for i in range(npop):
+            for i in owned:
                 best_seen[i].update(pops[i], options, maxsize)
-        # optimize_and_simplify_population: one batched constant optimisation for all islands
+        # optimize_and_simplify_population: one batched constant optimisation for all (owned) islands
         if options.should_optimize_constants:
             sel = []
-            for i in range(npop):
+            for i in owned:
                 do_opt = rngs[i].random(len(pops[i])) < options.optimizer_probability
                 sel.extend((i, j) for j in np.nonzero(do_opt)[0] if pops[i][j].tree.count_constants() > 0)
             if sel:
@@ -618,30 +679,36 @@ def equation_search(X=None, y=None, *, niterations=10, options, weights=None, se
                     m.loss = float(new_losses[k])
                     m.cost = float(loss_to_cost(T(new_losses[k]), dataset.use_baseline, dataset.baseline_loss,
                                                 m.tree, options, m.complexity))
-                    m.birth = _next_birth()
+                    m.birth = births[i]()
         if options.batching:  # finalize_costs (src/Population.jl:182-196): re-score on the full data
-            flat = [m for p in pops for m in p]
+            flat = [m for i in owned for m in pops[i]]
             c, l = score([m.tree for m in flat], dataset)
             for m, cc, ll in zip(flat, c, l):
                 m.cost, m.loss = float(cc), float(ll)
-        for p in pops:
-            for m in p:
+        for i in owned:
+            for m in pops[i]:
                 m.parent, m.ref = m.ref, _next_ref()
-        for i in range(npop):  # head node, island by island (the reference's order)
+        exchange(pops, best_seen)  # every rank now holds every island of this iteration
+        for i in range(npop):  # head node, island by island (the reference's order), on every rank
             best_sub_pops[i] = sorted(pops[i], key=lambda m: m.cost)[: so.topn]
             for m in pops[i]:
                 stats.update_frequencies(m.complexity)
             hof.update(pops[i], options, maxsize)
             hof.update([m for m, e in zip(best_seen[i].members, best_seen[i].exists) if e], options, maxsize)
             dominating = hof.pareto_frontier()
-            if so.migration:
-                migrate([m for p in best_sub_pops for m in p], pops[i], so.fraction_replaced, rngs[i])
-            if so.hof_migration and dominating:
-                migrate(dominating, pops[i], so.fraction_replaced_hof, rngs[i])
+            if i % world == rank:  # the owner migrates with the island's own stream
+                if so.migration:
+                    migrate([m for p in best_sub_pops for m in p], pops[i], so.fraction_replaced, rngs[i],
+                            births[i])
+                if so.hof_migration and dominating:
+                    migrate(dominating, pops[i], so.fraction_replaced_hof, rngs[i], births[i])
             cycles_done += 1
             stats.move_window()
-        if verbosity:
+        if verbosity and rank == 0:
             best = min((m for m in hof.members if m is not None), key=lambda m: m.loss)
             print(f"iteration {it + 1}/{niterations}: best loss {best.loss:.4g} (complexity {best.complexity})")
+    exchange(pops)  # the final migrations
+    if world > 1:
+        num_evals = float(sum(allgather(num_evals)))
     wall = time.perf_counter() - t0
     return SearchResult(hof, hof.pareto_frontier(), pops, niterations, wall, niterations * npop, num_evals, calls[0])
