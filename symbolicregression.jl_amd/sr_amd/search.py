@@ -34,7 +34,7 @@ import numpy as np
 
 from .constant_optimization import optimize_constants_batch
 from .dataset import Dataset, batch
-from .loss import eval_cost_batch, loss_to_cost, update_baseline_loss_
+from .loss import eval_cost_batch, eval_loss_batch, loss_to_cost, update_baseline_loss_
 from .mutation import gen_random_tree_fixed_size, make_random_leaf
 from .node import Node, flatten_trees
 
@@ -146,9 +146,10 @@ class RunningSearchStatistics:
 
 def check_constraints(tree, options, maxsize, size=None):
     """check_constraints (src/CheckConstraints.jl:75-92): size and depth limits."""
-    if (size if size is not None else tree.count_nodes()) > maxsize:
+    size = size if size is not None else tree.count_nodes()
+    if size > maxsize:
         return False
-    return tree.count_depth() <= options.maxdepth
+    return size <= options.maxdepth or tree.count_depth() <= options.maxdepth  # depth <= node count
 
 
 class HallOfFame:
@@ -354,9 +355,10 @@ def condition_mutation_weights(w, member, so, curmaxsize, nfeatures):
         else:
             w["mutate_feature"] = 0.0
         return w
-    if not any(n.degree == 2 for n in tree.preorder()):
+    nodes = tree.preorder()  # one traversal for both counts
+    if not any(n.degree == 2 for n in nodes):
         w["swap_operands"] = 0.0
-    w["mutate_constant"] *= min(8, tree.count_constants()) / 8.0
+    w["mutate_constant"] *= min(8, sum(1 for n in nodes if n.degree == 0 and n.constant)) / 8.0
     if nfeatures <= 1:
         w["mutate_feature"] = 0.0
     if member.complexity >= curmaxsize:
@@ -368,9 +370,15 @@ def condition_mutation_weights(w, member, so, curmaxsize, nfeatures):
 
 
 def sample_mutation(w, rng):
+    """sample_mutation (src/MutationWeights.jl): one draw ∝ the conditioned weights."""
     keys = [k for k in MUTATIONS if k in w]
-    p = np.array([w[k] for k in keys], dtype=np.float64)
-    return keys[int(rng.choice(len(keys), p=p / p.sum()))]
+    total = sum(w[k] for k in keys)
+    r, acc = rng.random() * total, 0.0
+    for k in keys:
+        acc += w[k]
+        if r < acc:
+            return k
+    return next(k for k in reversed(keys) if w[k] > 0)
 
 
 def tournament_selection_weights(options):
@@ -395,8 +403,14 @@ def best_of_sample(pop, stats, options, so, rng, tweights):
     else:
         costs = [m.cost for m in members]
     ranked = sorted((i for i in range(n) if costs[i] < math.inf), key=lambda i: (costs[i], i))
-    place = 0 if options.tournament_selection_p == 1.0 else int(rng.choice(len(tweights), p=tweights))
+    place = 0 if options.tournament_selection_p == 1.0 else _draw(tweights, rng)
     return members[ranked[place]] if place < len(ranked) else members[0]
+
+
+def _draw(weights, rng):
+    """Index drawn with probability weights[i] (weights sum to 1): inverse CDF of one uniform."""
+    cdf = np.cumsum(weights)
+    return min(int(np.searchsorted(cdf, rng.random() * cdf[-1], side="right")), len(weights) - 1)
 
 
 def replace_oldest(pop, babies):
@@ -449,6 +463,18 @@ class _Plan:
     def __init__(self, kind, island, parent=None, parent2=None, tree=None, tree2=None, slot=-1, temperature=1.0):
         self.kind, self.island, self.parent, self.parent2 = kind, island, parent, parent2
         self.tree, self.tree2, self.slot, self.temperature = tree, tree2, slot, temperature
+
+
+def _costs(losses, sizes, ds, options):
+    """loss_to_cost (src/LossFunctions.jl:170-190) over a batch: loss / normalization +
+    L(size * parsimony::Float32), in the loss type as the scalar version computes it."""
+    full = getattr(ds, "full", ds)
+    L = losses.dtype.type
+    base = L(full.baseline_loss)
+    norm = base if (base >= L(0.01) and full.use_baseline) else L(0.01)
+    pars = (np.asarray(sizes, dtype=np.float32) * np.float32(options.parsimony)).astype(losses.dtype)
+    with np.errstate(over="ignore", invalid="ignore"):
+        return (losses / norm + pars).astype(np.float64)
 
 
 def _accept(pl, after_cost, new_size, snap, maxsize, so, rng):
@@ -535,7 +561,9 @@ def equation_search(X=None, y=None, *, niterations=10, options, weights=None, se
         calls[0] += 1
         if _score_fn is not None:
             return _score_fn(trees, ds)
-        return eval_cost_batch(trees, ds, options, complexities=[t.count_nodes() for t in trees])
+        tb = flatten_trees(trees, dataset.dtype)  # one flattening: the batch and the complexities
+        losses, _ = eval_loss_batch(tb, ds, options)
+        return _costs(losses, tb.tree_sizes(), ds, options), losses
 
     def exchange(pops, best_seen=None):
         """All-gather the owned islands (members, best-seen) so every rank holds all of them."""

@@ -120,3 +120,21 @@ def test_replace_oldest():
     oldest = pop[0]
     replace_oldest(pop, [_member(t[0].copy(), 0.0)])
     assert oldest not in pop and len(pop) == 3
+
+
+def test_vectorised_costs_match_loss_to_cost():
+    """search._costs (the batched loss_to_cost the search uses) == loss_to_cost tree by tree."""
+    from sr_amd import Dataset, Node, Options, loss_to_cost
+    from sr_amd.search import _costs
+
+    opts = Options(binary_operators=["+", "*"], unary_operators=["cos"], parsimony=0.0032)
+    for dt in (np.float32, np.float64):
+        ds = Dataset(np.zeros((2, 10), dtype=dt), np.zeros(10, dtype=dt))
+        for use, base in ((True, 3.7), (True, 0.001), (False, 5.0)):
+            ds.use_baseline, ds.baseline_loss = use, dt(base)
+            losses = np.array([0.0, 1.5, 1e-7, np.inf, 123.25], dtype=dt)
+            sizes = np.array([1, 3, 30, 7, 12])
+            got = _costs(losses, sizes, ds, opts)
+            want = [float(loss_to_cost(losses[k], ds.use_baseline, ds.baseline_loss, Node(val=dt(0)), opts,
+                                       int(sizes[k]))) for k in range(len(sizes))]
+            assert got.tolist() == want
