@@ -37,9 +37,28 @@ extern "C" {
 #define SR_DTYPE_F32 0
 #define SR_DTYPE_F64 1
 
-/* elementwise losses (Options.elementwise_loss) */
-#define SR_LOSS_L2DIST 0 /* L2DistLoss() — the default (src/Options.jl:772) */
-#define SR_LOSS_L1DIST 1 /* L1DistLoss() */
+/* elementwise losses (Options.elementwise_loss; the LossFunctions.jl catalog of src/Options.jl:301-328).
+ * The parameter-free ones are passed as `loss_kind` directly; a parametric one (and HuberLoss with
+ * delta != 1) is registered with sr_register_loss, which returns the code to pass instead. */
+#define SR_LOSS_L2DIST 0            /* L2DistLoss() — the default (src/Options.jl:772) */
+#define SR_LOSS_L1DIST 1            /* L1DistLoss() */
+#define SR_LOSS_LPDIST 2            /* LPDistLoss{P}()          param P */
+#define SR_LOSS_LOGITDIST 3         /* LogitDistLoss() */
+#define SR_LOSS_HUBERLOSS 4         /* HuberLoss(d)             param d (direct code: d = 1) */
+#define SR_LOSS_L1EPSINS 5          /* L1EpsilonInsLoss(eps)    param eps */
+#define SR_LOSS_L2EPSINS 6          /* L2EpsilonInsLoss(eps)    param eps */
+#define SR_LOSS_PERIODICLOSS 7      /* PeriodicLoss(circ)       param circ */
+#define SR_LOSS_QUANTILELOSS 8      /* QuantileLoss(tau)        param tau */
+#define SR_LOSS_ZEROONE 9           /* ZeroOneLoss() */
+#define SR_LOSS_PERCEPTRONLOSS 10   /* PerceptronLoss() */
+#define SR_LOSS_L1HINGE 11          /* L1HingeLoss() */
+#define SR_LOSS_L2HINGE 12          /* L2HingeLoss() */
+#define SR_LOSS_SMOOTHEDL1HINGE 13  /* SmoothedL1HingeLoss(gamma) param gamma */
+#define SR_LOSS_MODIFIEDHUBER 14    /* ModifiedHuberLoss() */
+#define SR_LOSS_L2MARGIN 15         /* L2MarginLoss() */
+#define SR_LOSS_EXPLOSS 16          /* ExpLoss() */
+#define SR_LOSS_SIGMOIDLOSS 17      /* SigmoidLoss() */
+#define SR_LOSS_DWDMARGIN 18        /* DWDMarginLoss(q)         param q */
 
 /* per-tree partial flag bits (sr_eval_loss_partials) */
 #define SR_FLAG_NONFINITE 1u /* some checked intermediate array holds NaN/Inf: complete = false */
@@ -82,6 +101,12 @@ int sr_shutdown(sr_ctx* ctx);
  */
 int sr_register_opset(sr_ctx* ctx, int n_unary, const char* const* unary_names, int n_binary,
                       const char* const* binary_names, int* opset_id);
+
+/*
+ * Register an elementwise loss with its parameter (Options.elementwise_loss, e.g. HuberLoss(1.5) =
+ * {SR_LOSS_HUBERLOSS, 1.5}); *loss_code is what the eval calls take as `loss_kind`.
+ */
+int sr_register_loss(sr_ctx* ctx, int kind, double param, int* loss_code);
 
 /*
  * Upload a dataset (src/Dataset.jl:131-246).  X is Julia's column-major [nfeatures, n] matrix

@@ -390,11 +390,48 @@ int FN(oracle_eval_tree)(int64_t n_nodes, const uint8_t* degree, const uint8_t* 
   return 1;
 }
 
+/* LossFunctions.jl 0.11 SupervisedLoss values (not vendored; published definitions restated):
+ * d = output - target, a = target * output, p = the loss's parameter.  Julia's max(0, x) propagates
+ * NaN.  Kinds as SrLossKind (csrc/sr_ops.h). */
+static inline T FN(pos)(T x) { return (x != x) ? x : (x > (T)0 ? x : (T)0); }
+static inline T FN(elem_loss)(int kind, double pd, T pred, T target) {
+  const T p = (T)pd, d = pred - target, ad = M_FABS(d), a = target * pred;
+  T e;
+  switch (kind) {
+    case 1: return ad;                                                     /* L1DistLoss */
+    case 2: return M_POW(ad, p);                                           /* LPDistLoss{P} */
+    case 3: return -M_LOG((T)4) - d + (T)2 * M_LOG((T)1 + M_EXP(d));       /* LogitDistLoss */
+    case 4: return ad <= p ? d * d / (T)2 : p * (ad - p / (T)2);           /* HuberLoss(d) */
+    case 5: return FN(pos)(ad - p);                                        /* L1EpsilonInsLoss */
+    case 6: e = FN(pos)(ad - p); return e * e;                             /* L2EpsilonInsLoss */
+    case 7: return (T)1 - M_COS(d * ((T)2 * (T)3.14159265358979323846 / p)); /* PeriodicLoss(circ) */
+    case 8: return d * ((d > (T)0 ? (T)1 : (T)0) - p);                     /* QuantileLoss(tau) */
+    case 9: return a < (T)0 ? (T)1 : (T)0;                                 /* ZeroOneLoss */
+    case 10: return FN(pos)(-a);                                           /* PerceptronLoss */
+    case 11: return FN(pos)((T)1 - a);                                     /* L1HingeLoss */
+    case 12: e = FN(pos)((T)1 - a); return e * e;                          /* L2HingeLoss */
+    case 13:                                                               /* SmoothedL1HingeLoss(g) */
+      if (a >= (T)1 - p) { e = FN(pos)((T)1 - a); return e * e / ((T)2 * p); }
+      return (T)1 - p / (T)2 - a;
+    case 14:                                                               /* ModifiedHuberLoss */
+      if (a >= (T)-1) { e = FN(pos)((T)1 - a); return e * e; }
+      return (T)-4 * a;
+    case 15: e = (T)1 - a; return e * e;                                   /* L2MarginLoss */
+    case 16: return M_EXP(-a);                                             /* ExpLoss */
+    case 17: return (T)1 - M_TANH(a);                                      /* SigmoidLoss */
+    case 18:                                                               /* DWDMarginLoss(q) */
+      if (a <= p / (p + (T)1)) return (T)1 - a;
+      return (M_POW(p, p) / M_POW(p + (T)1, p + (T)1)) / M_POW(a, p);
+    default: return d * d;                                                 /* L2DistLoss */
+  }
+}
+
 /* _eval_loss: L(Inf) if incomplete; accum 0 = sequential T fold ("ref"), 1 = f64 fold. */
 int FN(oracle_eval_loss)(int64_t n_nodes, const uint8_t* degree, const uint8_t* op, const uint16_t* feature,
                          const uint8_t* constant, const T* val, const int32_t* un_ids, int n_un,
                          const int32_t* bin_ids, int n_bin, const T* X, int64_t nf, int64_t n, const T* y,
-                         const T* w, int loss_kind, int accum, T* loss, int* complete, int perturb) {
+                         const T* w, int loss_kind, double loss_param, int accum, T* loss, int* complete,
+                         int perturb) {
   T* pred = FN(alloc)(n);
   if (!FN(oracle_eval_tree)(n_nodes, degree, op, feature, constant, val, un_ids, n_un, bin_ids, n_bin, X, nf, n,
                             pred, complete, perturb)) {
@@ -409,8 +446,7 @@ int FN(oracle_eval_loss)(int64_t n_nodes, const uint8_t* degree, const uint8_t* 
   if (accum == 0) {
     T s = (T)0, ws = (T)0;
     for (int64_t j = 0; j < n; ++j) {
-      const T d = pred[j] - y[j];
-      T l = loss_kind == 1 ? M_FABS(d) : d * d;
+      T l = FN(elem_loss)(loss_kind, loss_param, pred[j], y[j]);
       if (w) { l = w[j] * l; ws = ws + w[j]; }
       s = s + l;
     }
@@ -418,8 +454,7 @@ int FN(oracle_eval_loss)(int64_t n_nodes, const uint8_t* degree, const uint8_t* 
   } else {
     double s = 0.0, ws = 0.0;
     for (int64_t j = 0; j < n; ++j) {
-      const T d = pred[j] - y[j];
-      T l = loss_kind == 1 ? M_FABS(d) : d * d;
+      T l = FN(elem_loss)(loss_kind, loss_param, pred[j], y[j]);
       if (w) { l = w[j] * l; ws += (double)w[j]; }
       s += (double)l;
     }
@@ -434,15 +469,15 @@ int FN(oracle_eval_loss)(int64_t n_nodes, const uint8_t* degree, const uint8_t* 
 int FN(oracle_eval_loss_batch)(int64_t n_trees, const int64_t* offsets, const uint8_t* degree, const uint8_t* op,
                                const uint16_t* feature, const uint8_t* constant, const T* val,
                                const int32_t* un_ids, int n_un, const int32_t* bin_ids, int n_bin, const T* X,
-                               int64_t nf, int64_t n, const T* y, const T* w, int loss_kind, int accum,
-                               int n_threads, T* loss, int* complete, int perturb) {
+                               int64_t nf, int64_t n, const T* y, const T* w, int loss_kind, double loss_param,
+                               int accum, int n_threads, T* loss, int* complete, int perturb) {
   int bad = 0;
 #pragma omp parallel for schedule(dynamic, 1) num_threads(n_threads) reduction(| : bad)
   for (int64_t k = 0; k < n_trees; ++k) {
     const int64_t b = offsets[k], e = offsets[k + 1];
     int c = 0;
     if (!FN(oracle_eval_loss)(e - b, degree + b, op + b, feature + b, constant + b, val + b, un_ids, n_un, bin_ids,
-                              n_bin, X, nf, n, y, w, loss_kind, accum, loss + k, &c, perturb))
+                              n_bin, X, nf, n, y, w, loss_kind, loss_param, accum, loss + k, &c, perturb))
       bad |= 1;
     complete[k] = c;
   }

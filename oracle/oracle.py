@@ -26,6 +26,7 @@ def _load():
     P = ctypes.c_void_p
     I64 = ctypes.c_int64
     I = ctypes.c_int
+    D = ctypes.c_double
     lib.oracle_op_id.restype = I
     lib.oracle_op_id.argtypes = [ctypes.c_char_p, I]
     for sfx in ("f32", "f64"):
@@ -34,10 +35,10 @@ def _load():
         f.argtypes = [I64, P, P, P, P, P, P, I, P, I, P, I64, I64, P, P, I]
         f = getattr(lib, f"oracle_eval_loss_{sfx}")
         f.restype = I
-        f.argtypes = [I64, P, P, P, P, P, P, I, P, I, P, I64, I64, P, P, I, I, P, P, I]
+        f.argtypes = [I64, P, P, P, P, P, P, I, P, I, P, I64, I64, P, P, I, D, I, P, P, I]
         f = getattr(lib, f"oracle_eval_loss_batch_{sfx}")
         f.restype = I
-        f.argtypes = [I64, P, P, P, P, P, P, P, I, P, I, P, I64, I64, P, P, I, I, I, P, P, I]
+        f.argtypes = [I64, P, P, P, P, P, P, P, I, P, I, P, I64, I64, P, P, I, D, I, I, P, P, I]
     return lib
 
 
@@ -99,7 +100,7 @@ class Oracle:
             raise ValueError("oracle: malformed tree")
         return out, bool(comp.value)
 
-    def eval_loss_batch(self, tb, X, y, w=None, loss_kind=0, accum="f64", n_threads=1, perturb=0):
+    def eval_loss_batch(self, tb, X, y, w=None, loss_kind=0, accum="f64", n_threads=1, perturb=0, loss_param=0.0):
         X = np.asarray(X)
         dtype = X.dtype
         Xj = np.ascontiguousarray(X.T)
@@ -113,30 +114,31 @@ class Oracle:
         ok = f(n_trees, _p(np.ascontiguousarray(tb.offsets, dtype=np.int64)), _p(tb.degree), _p(tb.op),
                _p(tb.feature), _p(tb.constant), _p(val), _p(self.un), len(self.unaops), _p(self.bi),
                len(self.binops), _p(Xj), X.shape[0], X.shape[1], _p(y), _p(w), int(loss_kind),
-               0 if accum == "ref" else 1, int(n_threads), _p(loss), _p(comp), int(perturb))
+               float(loss_param), 0 if accum == "ref" else 1, int(n_threads), _p(loss), _p(comp), int(perturb))
         if not ok:
             raise ValueError("oracle: malformed tree")
         return loss, comp.astype(bool)
 
-    def loss_grad_fd(self, tb, X, y, w=None, loss_kind=0, rel_step=1e-5, n_threads=8, with_error=False):
+    def loss_grad_fd(self, tb, X, y, w=None, loss_kind=0, rel_step=1e-5, n_threads=8, with_error=False, loss_param=0.0):
         """Central finite differences of the f64 loss with respect to every tree's constants
         (pre-order, get_scalar_constants), the gradient-free objective the reference's Optim BFGS
         differentiates (src/ConstantOptimization.jl:77-116), Richardson-extrapolated over steps h
         and h/2.  Returns (grads, loss, complete) in the layout of ``sr_amd.eval_grad_batch``
         (plus |D(h) - D(h/2)|, a truncation-error estimate, with ``with_error``)."""
-        g1, loss0, comp0 = self._fd(tb, X, y, w, loss_kind, rel_step, n_threads)
-        g2, _, _ = self._fd(tb, X, y, w, loss_kind, rel_step / 2, n_threads)
+        g1, loss0, comp0 = self._fd(tb, X, y, w, loss_kind, rel_step, n_threads, loss_param)
+        g2, _, _ = self._fd(tb, X, y, w, loss_kind, rel_step / 2, n_threads, loss_param)
         g = (4 * g2 - g1) / 3
         if with_error:
             return g, loss0, comp0, np.abs(g2 - g1)
         return g, loss0, comp0
 
-    def _fd(self, tb, X, y, w, loss_kind, rel_step, n_threads):
+    def _fd(self, tb, X, y, w, loss_kind, rel_step, n_threads, loss_param=0.0):
         X = np.asarray(X, dtype=np.float64)
         mask = (tb.degree == 0) & (tb.constant != 0)
         cpos = np.nonzero(mask)[0]
         base_val = tb.val.astype(np.float64)
-        loss0, comp0 = self.eval_loss_batch(tb, X, y, w, loss_kind, accum="f64", n_threads=n_threads)
+        loss0, comp0 = self.eval_loss_batch(tb, X, y, w, loss_kind, accum="f64", n_threads=n_threads,
+                                            loss_param=loss_param)
         if len(cpos) == 0:
             return np.zeros(0), loss0, comp0
         tree_of = np.searchsorted(tb.offsets, cpos, side="right") - 1
@@ -157,6 +159,6 @@ class Oracle:
         b = _B()
         b.offsets, b.degree, b.op = offs, tb.degree[sel], tb.op[sel]
         b.feature, b.constant, b.val = tb.feature[sel], tb.constant[sel], val
-        lp, _ = self.eval_loss_batch(b, X, y, w, loss_kind, accum="f64", n_threads=n_threads)
+        lp, _ = self.eval_loss_batch(b, X, y, w, loss_kind, accum="f64", n_threads=n_threads, loss_param=loss_param)
         g = (lp[0::2] - lp[1::2]) / (2 * h)
         return g, loss0, comp0

@@ -106,7 +106,8 @@ int sr_waves_per_block(int elem_size, int mode, int tier, int rows_per_lane, int
 template <typename T, int R, bool GATHER>
 hipError_t sr_launch_basic_loss(const SrEvalArgs<T>& a, int n_blocks, hipStream_t s) {
   if (a.loss_kind == SR_LOSS_L1) return sr_launch_tile<T, R, SR_MODE_LOSS, GATHER, SR_TIER_BASIC, 4, SR_LOSS_L1>(a, n_blocks, s);
-  return sr_launch_tile<T, R, SR_MODE_LOSS, GATHER, SR_TIER_BASIC, 4, SR_LOSS_L2>(a, n_blocks, s);
+  if (a.loss_kind == SR_LOSS_L2) return sr_launch_tile<T, R, SR_MODE_LOSS, GATHER, SR_TIER_BASIC, 4, SR_LOSS_L2>(a, n_blocks, s);
+  return sr_launch_tile<T, R, SR_MODE_LOSS, GATHER, SR_TIER_BASIC, 4, -1>(a, n_blocks, s);  // the other losses
 }
 
 template <typename T>

@@ -95,6 +95,18 @@ struct HostBuf {
 };
 
 constexpr int kMaxChunks = 4;
+constexpr int kLossCodeBase = 256;
+
+// Parameter-free losses (and HuberLoss with its default delta = 1) may be passed by kind.
+inline bool loss_direct_ok(int kind) {
+  switch (kind) {
+    case SR_LOSS_LP: case SR_LOSS_L1_EPS_INS: case SR_LOSS_L2_EPS_INS: case SR_LOSS_PERIODIC:
+    case SR_LOSS_QUANTILE: case SR_LOSS_SMOOTH_L1_HINGE: case SR_LOSS_DWD_MARGIN:
+      return false;
+    default:
+      return kind >= 0 && kind < SR_LOSS_COUNT;
+  }
+}
 
 }  // namespace
 
@@ -110,6 +122,7 @@ struct sr_ctx {
   std::mutex mu;
   std::vector<SrOpset> opsets;
   std::vector<int> tiers;
+  std::vector<std::pair<int, double>> losses;  // registered (kind, param); code = kLossCodeBase + index
   DevBuf code, offsets, static_bad, part_sum, part_flag, out_sum, out_flag, pred, row_idx, tree_list,
       check_sums, perm, hint, g_code, g_offsets, g_consts, g_const_off, g_items, g_part, g_out;
   double last_eval_ms = 0.0, last_total_ms = 0.0;
@@ -213,6 +226,23 @@ int validate_common(sr_ctx* ctx, const sr_dataset* ds, int opset_id, const sr_tr
   return SR_OK;
 }
 
+// loss_kind as passed to the eval calls -> (SrLossKind, parameter).
+int decode_loss(sr_ctx* ctx, int code, int* kind, double* param) {
+  if (code >= kLossCodeBase) {
+    const size_t i = size_t(code - kLossCodeBase);
+    if (i >= ctx->losses.size()) return set_error(SR_ERR_INVALID_ARG, "unknown registered loss code " + std::to_string(code));
+    *kind = ctx->losses[i].first;
+    *param = ctx->losses[i].second;
+    return SR_OK;
+  }
+  if (!loss_direct_ok(code))
+    return set_error(SR_ERR_INVALID_ARG, "loss kind " + std::to_string(code) +
+                                             " is unknown or needs a parameter: register it with sr_register_loss");
+  *kind = code;
+  *param = code == SR_LOSS_HUBER ? 1.0 : 0.0;
+  return SR_OK;
+}
+
 // Shared engine: compile + upload + interpreter(+reduce).  Leaves per-tree {sum, flag} in
 // ctx->out_sum / ctx->out_flag (device).  n_eval rows (full dataset or row_idx view).
 //
@@ -227,8 +257,9 @@ int run_batch(sr_ctx* ctx, const sr_dataset* ds, int opset_id, const sr_tree_bat
   const bool gather = row_idx != nullptr && n_idx > 0;
   const int64_t n_eval = gather ? n_idx : ds->n;
   if (n_eval <= 0) return set_error(SR_ERR_INVALID_ARG, "no rows to evaluate");
-  if (loss_kind != SR_LOSS_L2DIST && loss_kind != SR_LOSS_L1DIST)
-    return set_error(SR_ERR_INVALID_ARG, "unsupported loss kind");
+  int lkind = 0;
+  double lparam = 0.0;
+  if (decode_loss(ctx, loss_kind, &lkind, &lparam) != SR_OK) return SR_ERR_INVALID_ARG;
   const int64_t nt = trees->n_trees;
   if (nt < 0) return set_error(SR_ERR_INVALID_ARG, "negative tree count");
   if (nt > 0 && !trees->offsets) return set_error(SR_ERR_INVALID_ARG, "sr_tree_batch has NULL arrays");
@@ -406,7 +437,8 @@ int run_batch(sr_ctx* ctx, const sr_dataset* ds, int opset_id, const sr_tree_bat
     a.stack_depth = depth;
     // Σ over n_total rows of values below tbig cannot overflow T, even with rounding slack.
     a.tbig = T(t_max<T>() / (2.0 * double(n_total > 0 ? n_total : 1)));
-    a.loss_kind = loss_kind;
+    a.loss_kind = lkind;
+    a.loss_param = T(lparam);
     a.part_sum = ctx->part_sum.as<double>() + size_t(n_rb) * size_t(t0);
     a.part_flag = ctx->part_flag.as<uint32_t>() + size_t(n_rb) * size_t(t0);
     a.pred = ctx->pred.as<T>();
@@ -695,6 +727,9 @@ int eval_grad_impl(sr_ctx* ctx, const sr_dataset* ds, int opset_id, const sr_tre
     if (!sr_unary_grad_supported(u)) return set_error(SR_ERR_UNSUPPORTED_OP, "operator without a gradient rule");
   for (uint32_t b : ops.binary)
     if (!sr_binary_grad_supported(b)) return set_error(SR_ERR_UNSUPPORTED_OP, "operator without a gradient rule");
+  int lkind = 0;
+  double lparam = 0.0;
+  if (decode_loss(ctx, loss_kind, &lkind, &lparam) != SR_OK) return SR_ERR_INVALID_ARG;
   int rc = eval_loss_impl<T>(ctx, ds, opset_id, trees, row_idx, n_idx, loss_kind, out_loss, out_complete);
   if (rc != SR_OK) return rc;
   const int64_t nt = trees->n_trees;
@@ -783,7 +818,8 @@ int eval_grad_impl(sr_ctx* ctx, const sr_dataset* ds, int opset_id, const sr_tre
     a.n_row_blocks = int(n_rb);
     a.n_groups = int(n_groups);
     a.stack_depth = depth;
-    a.loss_kind = loss_kind;
+    a.loss_kind = lkind;
+    a.loss_param = T(lparam);
     a.part = ctx->g_part.as<double>();
     const size_t lds = (size_t(a.nf) + 1 + (a.w ? 1 : 0)) * kRowsPerTile * sizeof(T) +
                        size_t(kWaves) * depth * (1 + kt) * 64 * sizeof(T);
@@ -924,6 +960,21 @@ int sr_register_opset(sr_ctx* ctx, int n_unary, const char* const* unary_names, 
   ctx->opsets.push_back(o);
   ctx->tiers.push_back(tier_of(o));
   *opset_id = int(ctx->opsets.size()) - 1;
+  return SR_OK;
+}
+
+int sr_register_loss(sr_ctx* ctx, int kind, double param, int* loss_code) {
+  if (check_ctx(ctx) != SR_OK) return SR_ERR_INVALID_ARG;
+  if (!loss_code || kind < 0 || kind >= SR_LOSS_COUNT) return set_error(SR_ERR_INVALID_ARG, "unknown loss kind");
+  if (!std::isfinite(param)) return set_error(SR_ERR_INVALID_ARG, "loss parameter must be finite");
+  Lock l(ctx);
+  for (size_t i = 0; i < ctx->losses.size(); ++i)
+    if (ctx->losses[i].first == kind && ctx->losses[i].second == param) {
+      *loss_code = kLossCodeBase + int(i);
+      return SR_OK;
+    }
+  ctx->losses.emplace_back(kind, param);
+  *loss_code = kLossCodeBase + int(ctx->losses.size()) - 1;
   return SR_OK;
 }
 

@@ -30,7 +30,8 @@ struct SrEvalArgs {
   int n_groups;                // tree groups (blockIdx = row_block * n_groups + group)
   int stack_depth;             // LDS operand-stack slots per wave (>= 1)
   T tbig;                      // |v| >= tbig may overflow the array-sum check
-  int loss_kind;
+  int loss_kind;               // SrLossKind
+  T loss_param;                // its parameter (HuberLoss delta, QuantileLoss tau, ...)
   // outputs
   double* part_sum;            // [n_row_blocks][n_trees], per launch position
   uint32_t* part_flag;         // [n_row_blocks][n_trees], per launch position
@@ -86,6 +87,7 @@ struct SrGradArgs {
   int n_groups;
   int stack_depth;
   int loss_kind;
+  T loss_param;
   double* part;              // [n_row_blocks][n_items][KT]
 };
 

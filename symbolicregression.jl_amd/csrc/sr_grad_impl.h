@@ -169,7 +169,7 @@ __global__ void __launch_bounds__(W * 64) sr_grad_kernel(const SrGradArgs<T> a) 
         }
       }
       // d loss / d constant: (d loss / d pred) * d pred / d constant, padded rows excluded
-      T coef = sr_elem_loss_deriv<T>(a.loss_kind, v, ys[r]);
+      T coef = sr_elem_loss_deriv<T>(a.loss_kind, v, ys[r], a.loss_param);
       if (weighted) coef *= wsv[r];
       if (row0 + r >= a.n_rows) coef = T(0);
 #pragma unroll

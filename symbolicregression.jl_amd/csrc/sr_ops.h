@@ -42,11 +42,36 @@ enum SrBinaryOp : uint32_t {
   SR_B_COUNT
 };
 
-// Elementwise losses (LossFunctions.jl SupervisedLoss value at (output, target)).
+// Elementwise losses: the SupervisedLoss catalog src/Options.jl:301-328 lists (LossFunctions.jl 0.11,
+// not vendored: the published definitions are restated in sr_elem_loss below; d = output - target,
+// a = target * output).  Parametric ones take one parameter (P, d, eps, circ, tau, gamma, q).
 enum SrLossKind : int32_t {
-  SR_LOSS_L2 = 0,   // L2DistLoss: abs2(output - target)   (default, src/Options.jl:772)
-  SR_LOSS_L1 = 1,   // L1DistLoss: abs(output - target)
+  SR_LOSS_L2 = 0,              // L2DistLoss: abs2(d)   (default, src/Options.jl:772)
+  SR_LOSS_L1 = 1,              // L1DistLoss: abs(d)
+  SR_LOSS_LP = 2,              // LPDistLoss{P}: abs(d)^P
+  SR_LOSS_LOGIT = 3,           // LogitDistLoss: -log(4) - d + 2 log(1 + exp(d))
+  SR_LOSS_HUBER = 4,           // HuberLoss(delta): abs(d) <= delta ? d^2/2 : delta (abs(d) - delta/2)
+  SR_LOSS_L1_EPS_INS = 5,      // L1EpsilonInsLoss(eps): max(0, abs(d) - eps)
+  SR_LOSS_L2_EPS_INS = 6,      // L2EpsilonInsLoss(eps): max(0, abs(d) - eps)^2
+  SR_LOSS_PERIODIC = 7,        // PeriodicLoss(circ): 1 - cos(d * 2pi/circ)
+  SR_LOSS_QUANTILE = 8,        // QuantileLoss(tau): d * ((d > 0) - tau)
+  SR_LOSS_ZERO_ONE = 9,        // ZeroOneLoss: sign(a) < 0 ? 1 : 0
+  SR_LOSS_PERCEPTRON = 10,     // PerceptronLoss: max(0, -a)
+  SR_LOSS_L1_HINGE = 11,       // L1HingeLoss: max(0, 1 - a)
+  SR_LOSS_L2_HINGE = 12,       // L2HingeLoss: max(0, 1 - a)^2
+  SR_LOSS_SMOOTH_L1_HINGE = 13,  // SmoothedL1HingeLoss(gamma): a >= 1 - gamma ? max(0, 1-a)^2/(2 gamma) : 1 - gamma/2 - a
+  SR_LOSS_MODIFIED_HUBER = 14,   // ModifiedHuberLoss: a >= -1 ? max(0, 1 - a)^2 : -4a
+  SR_LOSS_L2_MARGIN = 15,      // L2MarginLoss: (1 - a)^2
+  SR_LOSS_EXP = 16,            // ExpLoss: exp(-a)
+  SR_LOSS_SIGMOID = 17,        // SigmoidLoss: 1 - tanh(a)
+  SR_LOSS_DWD_MARGIN = 18,     // DWDMarginLoss(q): a <= q/(q+1) ? 1 - a : (q^q/(q+1)^(q+1)) / a^q
+  SR_LOSS_COUNT
 };
+// Losses whose value is NaN whenever the prediction is (the deferred NaN test may read the loss sum)
+SR_HD inline bool sr_loss_propagates_nan(int32_t kind) {
+  return kind == SR_LOSS_L2 || kind == SR_LOSS_L1 || kind == SR_LOSS_LP || kind == SR_LOSS_LOGIT ||
+         kind == SR_LOSS_HUBER || kind == SR_LOSS_L2_MARGIN || kind == SR_LOSS_EXP || kind == SR_LOSS_SIGMOID;
+}
 
 // ---------------------------------------------------------------------------------------
 // Program instruction: one per evaluated node (a leaf that is a binary node's operand is folded into
@@ -380,17 +405,84 @@ SR_HD inline void sr_binary_partials(uint32_t op, T a, T b, T r, T* pa, T* pb) {
   }
 }
 
-// Elementwise loss value.
+// Julia's max(0, x): NaN propagates.
 template <typename T>
-SR_HD inline T sr_elem_loss(int32_t kind, T pred, T target) {
-  const T d = pred - target;
-  if (kind == SR_LOSS_L1) return d < T(0) ? -d : d;
-  return d * d;
+SR_HD inline T sr_pos(T x) {
+  return (x != x) ? x : (x > T(0) ? x : T(0));
 }
-// d loss / d pred
+
+// Elementwise loss value (LossFunctions.jl restated; `p` = the loss's parameter).
 template <typename T>
-SR_HD inline T sr_elem_loss_deriv(int32_t kind, T pred, T target) {
+SR_HD inline T sr_elem_loss(int32_t kind, T pred, T target, T p = T(0)) {
+  using M = SrM<T>;
   const T d = pred - target;
-  if (kind == SR_LOSS_L1) return d > T(0) ? T(1) : (d < T(0) ? T(-1) : T(0));
-  return T(2) * d;
+  const T ad = d < T(0) ? -d : d;
+  const T a = target * pred;
+  switch (kind) {
+    case SR_LOSS_L1: return ad;
+    case SR_LOSS_LP: return M::pow(ad, p);
+    case SR_LOSS_LOGIT: return -M::log(T(4)) - d + T(2) * M::log(T(1) + M::exp(d));
+    case SR_LOSS_HUBER: return ad <= p ? d * d / T(2) : p * (ad - p / T(2));
+    case SR_LOSS_L1_EPS_INS: return sr_pos<T>(ad - p);
+    case SR_LOSS_L2_EPS_INS: { const T e = sr_pos<T>(ad - p); return e * e; }
+    case SR_LOSS_PERIODIC: return T(1) - M::cos(d * (T(2) * T(3.14159265358979323846) / p));
+    case SR_LOSS_QUANTILE: return d * ((d > T(0) ? T(1) : T(0)) - p);
+    case SR_LOSS_ZERO_ONE: return (a < T(0)) ? T(1) : T(0);
+    case SR_LOSS_PERCEPTRON: return sr_pos<T>(-a);
+    case SR_LOSS_L1_HINGE: return sr_pos<T>(T(1) - a);
+    case SR_LOSS_L2_HINGE: { const T e = sr_pos<T>(T(1) - a); return e * e; }
+    case SR_LOSS_SMOOTH_L1_HINGE: {
+      if (a >= T(1) - p) { const T e = sr_pos<T>(T(1) - a); return e * e / (T(2) * p); }
+      return T(1) - p / T(2) - a;
+    }
+    case SR_LOSS_MODIFIED_HUBER: {
+      if (a >= T(-1)) { const T e = sr_pos<T>(T(1) - a); return e * e; }
+      return T(-4) * a;
+    }
+    case SR_LOSS_L2_MARGIN: { const T e = T(1) - a; return e * e; }
+    case SR_LOSS_EXP: return M::exp(-a);
+    case SR_LOSS_SIGMOID: return T(1) - M::tanh(a);
+    case SR_LOSS_DWD_MARGIN: {
+      if (a <= p / (p + T(1))) return T(1) - a;
+      return (M::pow(p, p) / M::pow(p + T(1), p + T(1))) / M::pow(a, p);
+    }
+    default: return d * d;  // SR_LOSS_L2
+  }
+}
+// d loss / d pred (a = target * pred: d/dpred = target * dL/da); kinks take the one-sided value
+// LossFunctions' `deriv` takes there
+template <typename T>
+SR_HD inline T sr_elem_loss_deriv(int32_t kind, T pred, T target, T p = T(0)) {
+  using M = SrM<T>;
+  const T d = pred - target;
+  const T ad = d < T(0) ? -d : d;
+  const T sd = d > T(0) ? T(1) : (d < T(0) ? T(-1) : T(0));
+  const T a = target * pred;
+  switch (kind) {
+    case SR_LOSS_L1: return sd;
+    case SR_LOSS_LP: return ad == T(0) ? T(0) : p * M::pow(ad, p - T(1)) * sd;
+    case SR_LOSS_LOGIT: return M::tanh(d / T(2));
+    case SR_LOSS_HUBER: return ad <= p ? d : p * sd;
+    case SR_LOSS_L1_EPS_INS: return ad > p ? sd : T(0);
+    case SR_LOSS_L2_EPS_INS: return ad > p ? T(2) * (ad - p) * sd : T(0);
+    case SR_LOSS_PERIODIC: { const T k = T(2) * T(3.14159265358979323846) / p; return k * M::sin(d * k); }
+    case SR_LOSS_QUANTILE: return (d > T(0) ? T(1) : T(0)) - p;
+    case SR_LOSS_ZERO_ONE: return T(0);
+    case SR_LOSS_PERCEPTRON: return a < T(0) ? -target : T(0);
+    case SR_LOSS_L1_HINGE: return a < T(1) ? -target : T(0);
+    case SR_LOSS_L2_HINGE: return a < T(1) ? T(-2) * (T(1) - a) * target : T(0);
+    case SR_LOSS_SMOOTH_L1_HINGE:
+      if (a >= T(1) - p) return a < T(1) ? -(T(1) - a) / p * target : T(0);
+      return -target;
+    case SR_LOSS_MODIFIED_HUBER:
+      if (a >= T(-1)) return a < T(1) ? T(-2) * (T(1) - a) * target : T(0);
+      return T(-4) * target;
+    case SR_LOSS_L2_MARGIN: return T(-2) * (T(1) - a) * target;
+    case SR_LOSS_EXP: return -M::exp(-a) * target;
+    case SR_LOSS_SIGMOID: { const T t = M::tanh(a); return -(T(1) - t * t) * target; }
+    case SR_LOSS_DWD_MARGIN:
+      if (a <= p / (p + T(1))) return -target;
+      return -(M::pow(p, p + T(1)) / M::pow(p + T(1), p + T(1))) / M::pow(a, p + T(1)) * target;
+    default: return T(2) * d;  // SR_LOSS_L2
+  }
 }

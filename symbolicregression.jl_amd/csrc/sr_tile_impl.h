@@ -628,10 +628,10 @@ __global__ void __launch_bounds__(W * 64, (SrMinWavesFor<T, R, TIER, W>::value))
               T wv[R];
               L::load(w_lane, wv);
 #pragma unroll
-              for (int r = 0; r < R; ++r) l[r] = sr_elem_loss<T>(lk, tos[r], yv[r]) * wv[r];
+              for (int r = 0; r < R; ++r) l[r] = sr_elem_loss<T>(lk, tos[r], yv[r], a.loss_param) * wv[r];
             } else {
 #pragma unroll
-              for (int r = 0; r < R; ++r) l[r] = sr_elem_loss<T>(lk, tos[r], yv[r]);
+              for (int r = 0; r < R; ++r) l[r] = sr_elem_loss<T>(lk, tos[r], yv[r], a.loss_param);
             }
             if (!full_tile) {  // rows past the end of the view (padding) do not count
 #pragma unroll
@@ -646,8 +646,9 @@ __global__ void __launch_bounds__(W * 64, (SrMinWavesFor<T, R, TIER, W>::value))
             if (FAST_CHECK) {
               // the root is always checked; a checked value was +-Inf -> incomplete; NaN anywhere
               // reaches the root (BASIC operators propagate NaN) and shows in the lane's loss sum
-              // (padded rows replicate a real row: masking them hides no NaN), or, with weights,
-              // in the root values; a large finite one: the array-sum check may overflow
+              // (padded rows replicate a real row: masking them hides no NaN), or, with weights or a
+              // loss that can map NaN to a number (margin losses), in the root values; a large
+              // finite one: the array-sum check may overflow
 #pragma unroll
               for (int r = 0; r < R; r += 4) {
                 mrun = SrMaxAbs<T>::step(mrun, tos[r], tos[r + 1]);
@@ -655,7 +656,7 @@ __global__ void __launch_bounds__(W * 64, (SrMinWavesFor<T, R, TIER, W>::value))
               }
               mrun = SrMaxAbs<T>::step(mrun, mrun1, T(0));
               bool nan_root = false;
-              if (weighted) {
+              if (weighted || !sr_loss_propagates_nan(lk)) {
 #pragma unroll
                 for (int r = 0; r < R; ++r) nan_root |= sr_isnan(tos[r]);
               } else {
@@ -732,4 +733,5 @@ hipError_t sr_launch_tile(const SrEvalArgs<T>& a, int n_blocks, hipStream_t s) {
 // BASIC-tier loss kernels: one instantiation per elementwise loss
 #define SR_INSTANTIATE_LOSS(T, R, GATHER)                                   \
   SR_INSTANTIATE_WL(T, R, SR_MODE_LOSS, GATHER, SR_TIER_BASIC, 4, SR_LOSS_L2) \
-  SR_INSTANTIATE_WL(T, R, SR_MODE_LOSS, GATHER, SR_TIER_BASIC, 4, SR_LOSS_L1)
+  SR_INSTANTIATE_WL(T, R, SR_MODE_LOSS, GATHER, SR_TIER_BASIC, 4, SR_LOSS_L1) \
+  SR_INSTANTIATE_WL(T, R, SR_MODE_LOSS, GATHER, SR_TIER_BASIC, 4, -1)

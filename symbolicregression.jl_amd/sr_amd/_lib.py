@@ -40,6 +40,7 @@ EXPORTED_SYMBOLS = (
     "sr_init",
     "sr_shutdown",
     "sr_register_opset",
+    "sr_register_loss",
     "sr_dataset_upload",
     "sr_dataset_free",
     "sr_dataset_info",
@@ -99,6 +100,7 @@ def _load():
             c_int,
             [P, c_int, POINTER(c_char_p), c_int, POINTER(c_char_p), POINTER(c_int)],
         ),
+        "sr_register_loss": (c_int, [P, c_int, c_double, POINTER(c_int)]),
         "sr_dataset_upload": (c_int, [P, c_int, P, c_int64, c_int64, P, P, POINTER(P)]),
         "sr_dataset_free": (c_int, [P]),
         "sr_dataset_info": (c_int, [P, POINTER(c_int), POINTER(c_int64), POINTER(c_int64)]),

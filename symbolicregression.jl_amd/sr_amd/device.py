@@ -35,6 +35,20 @@ class DeviceContext:
             self._opsets[key] = oid
         return oid
 
+    def loss_code(self, options) -> int:
+        """The `loss_kind` the C ABI takes for options' elementwise loss: the kind itself for the
+        parameter-free losses (and HuberLoss(1)), else the code sr_register_loss returns."""
+        kind, param = options.loss_kind, float(getattr(options, "loss_param", 0.0))
+        if kind in (0, 1, 3, 9, 10, 11, 12, 14, 15, 16, 17) or (kind == 4 and param == 1.0):
+            return kind
+        key = (kind, param)
+        codes = self.__dict__.setdefault("_loss_codes", {})
+        if key not in codes:
+            out = ctypes.c_int()
+            _lib.check(_lib.lib.sr_register_loss(self.handle, kind, param, ctypes.byref(out)))
+            codes[key] = int(out.value)
+        return codes[key]
+
     def last_kernel_ms(self):
         a, b = ctypes.c_double(), ctypes.c_double()
         _lib.check(_lib.lib.sr_last_kernel_ms(self.handle, ctypes.byref(a), ctypes.byref(b)))

@@ -32,7 +32,7 @@ def gpu_partials(tb, shard, options, n_total, ctx=None):
     s = tb.to_struct()
     _lib.check(_lib.lib.sr_eval_loss_partials(
         ctx.handle, shard.device_handle(ctx), ctx.opset_id(options.operators), ctypes.byref(s), int(n_total),
-        options.loss_kind, sums.ctypes.data_as(ctypes.c_void_p), flags.ctypes.data_as(ctypes.c_void_p), 0))
+        ctx.loss_code(options), sums.ctypes.data_as(ctypes.c_void_p), flags.ctypes.data_as(ctypes.c_void_p), 0))
     return sums, flags
 
 

@@ -54,7 +54,7 @@ def eval_loss_batch(trees, dataset, options, *, ctx=None):
             ctypes.byref(s),
             None if idx is None else idx.ctypes.data_as(ctypes.c_void_p),
             0 if idx is None else int(idx.size),
-            options.loss_kind,
+            ctx.loss_code(options),
             losses.ctypes.data_as(ctypes.c_void_p),
             complete.ctypes.data_as(ctypes.c_void_p),
         )
@@ -92,7 +92,7 @@ def eval_grad_batch(trees, dataset, options, *, ctx=None):
             ctypes.byref(s),
             None if idx is None else idx.ctypes.data_as(ctypes.c_void_p),
             0 if idx is None else int(idx.size),
-            options.loss_kind,
+            ctx.loss_code(options),
             losses.ctypes.data_as(ctypes.c_void_p),
             grads.ctypes.data_as(ctypes.c_void_p),
             complete.ctypes.data_as(ctypes.c_void_p),

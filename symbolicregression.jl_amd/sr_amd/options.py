@@ -9,11 +9,47 @@ src/OptionsStruct.jl:186-187).
 """
 from __future__ import annotations
 
+import re
+
 import numpy as np
 
 from .operators import OperatorEnum
 
-LOSSES = {"L2DistLoss": 0, "L2DistLoss()": 0, "l2": 0, "L1DistLoss": 1, "L1DistLoss()": 1, "l1": 1}
+# Elementwise losses the device evaluates: the LossFunctions.jl catalog src/Options.jl:301-328 lists,
+# as (SrLossKind, parameter name or None).  Kinds match include/sr_amd.h SR_LOSS_*.
+LOSS_KINDS = {
+    "L2DistLoss": (0, None), "L1DistLoss": (1, None), "LPDistLoss": (2, "P"), "LogitDistLoss": (3, None),
+    "HuberLoss": (4, "d"), "L1EpsilonInsLoss": (5, "eps"), "L2EpsilonInsLoss": (6, "eps"),
+    "PeriodicLoss": (7, "circ"), "QuantileLoss": (8, "tau"), "ZeroOneLoss": (9, None),
+    "PerceptronLoss": (10, None), "L1HingeLoss": (11, None), "L2HingeLoss": (12, None),
+    "SmoothedL1HingeLoss": (13, "gamma"), "ModifiedHuberLoss": (14, None), "L2MarginLoss": (15, None),
+    "ExpLoss": (16, None), "SigmoidLoss": (17, None), "DWDMarginLoss": (18, "q"),
+}
+LOSS_DEFAULTS = {"HuberLoss": 1.0}  # LossFunctions' HuberLoss() default delta
+LOSSES = {"l2": 0, "l1": 1}  # short aliases
+
+
+def parse_loss(spec):
+    """'HuberLoss(1.5)', 'LPDistLoss{3}()', 'QuantileLoss(0.3)', 'L2DistLoss()', ... -> (kind, param)."""
+    if isinstance(spec, str) and spec in LOSSES:
+        return LOSSES[spec], 0.0
+    if not isinstance(spec, str):
+        raise ValueError(f"elementwise_loss {spec!r} is not supported by the device path")
+    m = re.fullmatch(r"\s*([A-Za-z0-9]+)\s*(?:\{\s*([^}]*)\s*\})?\s*(?:\(\s*([^)]*)\s*\))?\s*", spec)
+    if not m or m.group(1) not in LOSS_KINDS:
+        raise ValueError(f"elementwise_loss {spec!r} is not supported by the device path")
+    name, curly, paren = m.group(1), m.group(2), m.group(3)
+    kind, pname = LOSS_KINDS[name]
+    arg = (curly or "").strip() or (paren or "").strip()
+    if pname is None:
+        if arg:
+            raise ValueError(f"{name} takes no parameter")
+        return kind, 0.0
+    if not arg:
+        if name not in LOSS_DEFAULTS:
+            raise ValueError(f"{name} needs its parameter {pname}, e.g. {name}(1.0)")
+        return kind, LOSS_DEFAULTS[name]
+    return kind, float(arg)
 
 
 class Options:
@@ -49,10 +85,8 @@ class Options:
         self.operators = operators if operators is not None else OperatorEnum(unary_operators, binary_operators)
         if callable(elementwise_loss) and not isinstance(elementwise_loss, str):
             raise ValueError("custom elementwise loss functions stay on the reference CPU path")
-        if elementwise_loss not in LOSSES:
-            raise ValueError(f"elementwise_loss {elementwise_loss!r} is not supported by the device path")
         self.elementwise_loss = elementwise_loss
-        self.loss_kind = LOSSES[elementwise_loss]
+        self.loss_kind, self.loss_param = parse_loss(elementwise_loss)
         self.loss_function = loss_function
         self.loss_function_expression = loss_function_expression
         self.parsimony = np.float32(parsimony)

@@ -13,7 +13,7 @@ def rel(a, b):
 PERTURB_SEEDS = (1, 2, 3, 4)
 
 
-def well_conditioned(orc, tb, X, y, w=None, loss_kind=0, tol=2e-5):
+def well_conditioned(orc, tb, X, y, w=None, loss_kind=0, tol=2e-5, loss_param=0.0):
     """Trees whose loss is determined by the data, not by how the libm rounds.
 
     The oracle evaluates every tree five times: as is, and four times with every libm result (exp,
@@ -25,7 +25,7 @@ def well_conditioned(orc, tb, X, y, w=None, loss_kind=0, tol=2e-5):
     loss bar (1e-4 relative) is applied to the well-conditioned trees; `complete` flags are
     compared on every tree.  Returns (mask, loss, complete) of the unperturbed oracle.
     """
-    kw = dict(w=w, loss_kind=loss_kind, accum="f64", n_threads=8)
+    kw = dict(w=w, loss_kind=loss_kind, accum="f64", n_threads=8, loss_param=loss_param)
     l0, c0 = orc.eval_loss_batch(tb, X, y, **kw)
     mask = c0.copy()
     for seed in PERTURB_SEEDS:  # one pattern of signs can cancel by chance; four rarely all do

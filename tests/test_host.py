@@ -21,7 +21,23 @@ def test_unsupported_operator_raises():
     with pytest.raises(ValueError):
         Options(binary_operators=["+"], unary_operators=["my_custom_op"])
     with pytest.raises(ValueError):
-        Options(elementwise_loss="HuberLoss")
+        Options(elementwise_loss="CrossEntropyLoss()")  # not in the device catalog
+    with pytest.raises(ValueError):
+        Options(elementwise_loss="QuantileLoss")  # needs its parameter
+
+
+def test_loss_catalog_parsing():
+    """The LossFunctions catalog of src/Options.jl:301-328, as the device's (kind, parameter)."""
+    cases = {"L2DistLoss()": (0, 0.0), "L1DistLoss": (1, 0.0), "LPDistLoss{3}()": (2, 3.0), "LPDistLoss(1.5)": (2, 1.5),
+             "LogitDistLoss()": (3, 0.0), "HuberLoss()": (4, 1.0), "HuberLoss(2.5)": (4, 2.5),
+             "L1EpsilonInsLoss(0.1)": (5, 0.1), "L2EpsilonInsLoss(0.2)": (6, 0.2), "PeriodicLoss(6.0)": (7, 6.0),
+             "QuantileLoss(0.3)": (8, 0.3), "ZeroOneLoss()": (9, 0.0), "PerceptronLoss()": (10, 0.0),
+             "L1HingeLoss()": (11, 0.0), "L2HingeLoss()": (12, 0.0), "SmoothedL1HingeLoss(0.5)": (13, 0.5),
+             "ModifiedHuberLoss()": (14, 0.0), "L2MarginLoss()": (15, 0.0), "ExpLoss()": (16, 0.0),
+             "SigmoidLoss()": (17, 0.0), "DWDMarginLoss(2)": (18, 2.0)}
+    for spec, want in cases.items():
+        o = Options(elementwise_loss=spec)
+        assert (o.loss_kind, o.loss_param) == want, spec
 
 
 def test_parse_print_roundtrip_and_preorder():

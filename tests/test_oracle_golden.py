@@ -129,3 +129,50 @@ def test_tree_construction_loss_and_cost(golden):
         assert float(cg) < float(cb)
         cb10 = loss_to_cost(loss[1], True, dt(10), bad, opts)
         assert float(cb10) < float(cb)
+
+
+def test_loss_catalog_known_answers():
+    """The oracle's LossFunctions restatement at hand-computed points (d = output - target,
+    a = target * output).  Constant trees over a dataset with y = target."""
+    import math
+
+    from oracle import Oracle
+    from sr_amd import Node, Options, flatten_trees
+
+    pts = [(0.5, 0.0), (3.0, 0.0), (-2.0, 0.0), (0.25, 1.0), (-0.5, 1.0), (2.0, -1.0)]  # (output, target)
+    k = 2 * math.pi / 6.0
+
+    def hinge(x):
+        return max(0.0, x)
+
+    spec = {  # elementwise_loss -> f(output, target)
+        "L2DistLoss()": lambda o, t: (o - t) ** 2,
+        "L1DistLoss()": lambda o, t: abs(o - t),
+        "LPDistLoss{3}()": lambda o, t: abs(o - t) ** 3,
+        "LogitDistLoss()": lambda o, t: -math.log(4 * math.exp(o - t) / (1 + math.exp(o - t)) ** 2),
+        "HuberLoss(1.0)": lambda o, t: 0.5 * (o - t) ** 2 if abs(o - t) <= 1 else abs(o - t) - 0.5,
+        "L1EpsilonInsLoss(0.3)": lambda o, t: hinge(abs(o - t) - 0.3),
+        "L2EpsilonInsLoss(0.3)": lambda o, t: hinge(abs(o - t) - 0.3) ** 2,
+        "PeriodicLoss(6.0)": lambda o, t: 1 - math.cos((o - t) * k),
+        "QuantileLoss(0.3)": lambda o, t: (o - t) * ((1.0 if o - t > 0 else 0.0) - 0.3),
+        "ZeroOneLoss()": lambda o, t: 1.0 if t * o < 0 else 0.0,
+        "PerceptronLoss()": lambda o, t: hinge(-t * o),
+        "L1HingeLoss()": lambda o, t: hinge(1 - t * o),
+        "L2HingeLoss()": lambda o, t: hinge(1 - t * o) ** 2,
+        "SmoothedL1HingeLoss(0.5)": lambda o, t: (hinge(1 - t * o) ** 2 / 1.0 if t * o >= 0.5 else 0.75 - t * o),
+        "ModifiedHuberLoss()": lambda o, t: hinge(1 - t * o) ** 2 if t * o >= -1 else -4 * t * o,
+        "L2MarginLoss()": lambda o, t: (1 - t * o) ** 2,
+        "ExpLoss()": lambda o, t: math.exp(-t * o),
+        "SigmoidLoss()": lambda o, t: 1 - math.tanh(t * o),
+        "DWDMarginLoss(2)": lambda o, t: 1 - t * o if t * o <= 2 / 3 else (4 / 27) / (t * o) ** 2,
+    }
+    X = np.zeros((1, 4))
+    for name, f in spec.items():
+        opts = Options(binary_operators=["+"], elementwise_loss=name)
+        orc = Oracle.from_options(opts)
+        for o, t in pts:
+            tb = flatten_trees([Node(val=np.float64(o))], np.float64)
+            loss, comp = orc.eval_loss_batch(tb, X, np.full(4, t), loss_kind=opts.loss_kind,
+                                             loss_param=opts.loss_param)
+            assert comp[0]
+            assert loss[0] == pytest.approx(f(o, t), rel=1e-12, abs=1e-15), (name, o, t)
