@@ -133,7 +133,62 @@ function eval_loss_batch(trees::AbstractVector, dataset::Dataset{T,L}, options::
     return L.(losses), complete .== 0x01
 end
 
-loss_kind(options) = options.elementwise_loss isa SymbolicRegression.L1DistLoss ? Cint(1) : Cint(0)
+# Options.elementwise_loss -> (SrLossKind, parameter) (include/sr_amd.h SR_LOSS_*; LossFunctions.jl types as
+# src/Options.jl:301-328 lists them); parametric losses are registered once per context.
+const LF = SymbolicRegression.LossFunctions
+loss_spec(l::LF.L2DistLoss) = (0, 0.0)
+loss_spec(l::LF.L1DistLoss) = (1, 0.0)
+loss_spec(l::LF.LPDistLoss{P}) where {P} = (2, Float64(P))
+loss_spec(l::LF.LogitDistLoss) = (3, 0.0)
+loss_spec(l::LF.HuberLoss) = (4, Float64(l.d))
+loss_spec(l::LF.L1EpsilonInsLoss) = (5, Float64(l.ε))
+loss_spec(l::LF.L2EpsilonInsLoss) = (6, Float64(l.ε))
+loss_spec(l::LF.PeriodicLoss) = (7, Float64(2π / l.k))
+loss_spec(l::LF.QuantileLoss) = (8, Float64(l.τ))
+loss_spec(l::LF.ZeroOneLoss) = (9, 0.0)
+loss_spec(l::LF.PerceptronLoss) = (10, 0.0)
+loss_spec(l::LF.L1HingeLoss) = (11, 0.0)
+loss_spec(l::LF.L2HingeLoss) = (12, 0.0)
+loss_spec(l::LF.SmoothedL1HingeLoss) = (13, Float64(l.gamma))
+loss_spec(l::LF.ModifiedHuberLoss) = (14, 0.0)
+loss_spec(l::LF.L2MarginLoss) = (15, 0.0)
+loss_spec(l::LF.ExpLoss) = (16, 0.0)
+loss_spec(l::LF.SigmoidLoss) = (17, 0.0)
+loss_spec(l::LF.DWDMarginLoss) = (18, Float64(l.q))
+loss_spec(l) = throw(ArgumentError("elementwise_loss $(typeof(l)) stays on the CPU path"))
+
+const LOSS_CODES = Dict{Tuple{Ptr{Cvoid},Int,Float64},Cint}()
+function loss_kind(options)
+    kind, param = loss_spec(options.elementwise_loss)
+    (kind in (0, 1, 3, 9, 10, 11, 12, 14, 15, 16, 17) || (kind == 4 && param == 1.0)) && return Cint(kind)
+    ctx = context()
+    get!(LOSS_CODES, (ctx.handle, kind, param)) do
+        code = Ref{Cint}(0)
+        check(ccall((:sr_register_loss, LIB), Cint, (Ptr{Cvoid}, Cint, Cdouble, Ref{Cint}),
+                    ctx.handle, kind, param, code))
+        code[]
+    end
+end
+
+"""Batched objective + forward-mode gradient for BFGS (src/ConstantOptimization.jl:126-167):
+losses, the gradient of every tree's loss w.r.t. its constants (pre-order, concatenated), complete."""
+function eval_grad_batch(trees::AbstractVector, dataset::Dataset{T,L}, options::AbstractOptions) where {T,L}
+    ctx = context()
+    ops = get_operators(first(trees), options)
+    f = flatten(trees, T)
+    losses = Vector{T}(undef, length(trees))
+    complete = Vector{UInt8}(undef, length(trees))
+    grads = zeros(T, count(==(0x01), f.constant) + 1)
+    GC.@preserve f begin
+        b = SrTreeBatch(length(trees), pointer(f.offsets), pointer(f.degree), pointer(f.op),
+                        pointer(f.feature), pointer(f.constant), Ptr{Cvoid}(pointer(f.val)))
+        check(ccall((:sr_eval_grad_batch, LIB), Cint,
+                    (Ptr{Cvoid}, Ptr{Cvoid}, Cint, Ref{SrTreeBatch}, Ptr{Int64}, Int64, Cint, Ptr{T}, Ptr{T}, Ptr{UInt8}),
+                    ctx.handle, device_dataset(ctx, dataset), opset_id(ctx, ops), b, C_NULL, 0,
+                    loss_kind(options), losses, grads, complete))
+    end
+    return L.(losses), grads[1:end-1], complete .== 0x01
+end
 
 """Batched `eval_cost` (src/LossFunctions.jl:193-209): fills `costs`, `losses` in place."""
 function eval_cost_batch!(costs::AbstractVector{L}, losses::AbstractVector{L}, dataset::Dataset{T,L}, members,
