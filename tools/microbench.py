@@ -7,9 +7,10 @@ import sr_amd
 from sr_amd import Options, Dataset, flatten_trees, gen_random_population, eval_loss_batch
 
 n = 1 << 20
+DT = np.float64 if os.environ.get("MB_DTYPE", "f32") == "f64" else np.float32
 rng = np.random.default_rng(2)
-X = rng.standard_normal((5, n)).astype(np.float32)
-y = (2 * np.cos(X[3]) + X[0] ** 2 - 2).astype(np.float32)
+X = rng.standard_normal((5, n)).astype(DT)
+y = (2 * np.cos(X[3]) + X[0] ** 2 - 2).astype(DT)
 ds = Dataset(X, y)
 ctx = sr_amd.get_context()
 mixes = {
@@ -25,7 +26,7 @@ for name, kw in mixes.items():
     if only and not any(name.startswith(o) for o in only):
         continue
     opts = Options(**kw)
-    tb = flatten_trees(gen_random_population(10000, opts, 5, seed=1), np.float32)
+    tb = flatten_trees(gen_random_population(10000, opts, 5, seed=1), DT)
     eval_loss_batch(tb, ds, opts)
     ks, ts, ph = [], [], []
     for _ in range(5):
