@@ -69,10 +69,11 @@ struct DevBuf {
 struct HostBuf {
   void* p = nullptr;
   size_t cap = 0;
-  hipError_t ensure(size_t bytes, hipStream_t s) {
+  hipError_t ensure(size_t bytes, hipStream_t s, hipStream_t s2) {
     if (bytes <= cap) return hipSuccess;
     if (p) {
       hipError_t e = hipStreamSynchronize(s);  // no DMA may still read the old buffer
+      if (e == hipSuccess) e = hipStreamSynchronize(s2);
       if (e == hipSuccess) e = hipHostFree(p);
       if (e != hipSuccess) return e;
       p = nullptr;
@@ -124,7 +125,7 @@ struct sr_ctx {
   std::vector<int> tiers;
   std::vector<std::pair<int, double>> losses;  // registered (kind, param); code = kLossCodeBase + index
   DevBuf code, offsets, static_bad, part_sum, part_flag, out_sum, out_flag, pred, row_idx, tree_list,
-      check_sums, perm, hint, g_code, g_offsets, g_consts, g_const_off, g_items, g_part, g_out;
+      check_sums, perm, hint, probe_sum, probe_flag, g_code, g_offsets, g_consts, g_const_off, g_items, g_part, g_out;
   double last_eval_ms = 0.0, last_total_ms = 0.0;
   // host-side phases of the last eval_loss call (ms): compile, upload+launch, wait, exact pass,
   // finalize (sr_last_phase_ms)
@@ -146,6 +147,7 @@ struct sr_ctx {
   bool cost_order = true;   // launch trees in decreasing estimated cost (SR_AMD_NO_SORT=1 disables)
   bool dead_hints = true;   // share dead-tree hints across row blocks (SR_AMD_NO_HINT=1 disables)
   int chunks = 2;           // SR_AMD_CHUNKS: pipeline compile/launch over this many tree chunks (1 = off)
+  bool probe = true;        // SR_AMD_NO_PROBE=1 disables the dead-tree probe launch
   std::vector<uint32_t> perm_host;
 };
 
@@ -299,10 +301,10 @@ int run_batch(sr_ctx* ctx, const sr_dataset* ds, int opset_id, const sr_tree_bat
   SR_HIP_CHECK(ctx->offsets.ensure((size_t(nt) + 1) * sizeof(uint32_t)));
   SR_HIP_CHECK(ctx->static_bad.ensure(size_t(nt) + 16));
   SR_HIP_CHECK(ctx->perm.ensure((size_t(nt) + 1) * sizeof(uint32_t)));
-  SR_HIP_CHECK(ctx->h_code.ensure(code_cap * sizeof(SrIns<T>), s));
-  SR_HIP_CHECK(ctx->h_offsets.ensure((size_t(nt) + 1) * sizeof(uint32_t), s));
-  SR_HIP_CHECK(ctx->h_static_bad.ensure(size_t(nt) + 16, s));
-  SR_HIP_CHECK(ctx->h_perm.ensure((size_t(nt) + 1) * sizeof(uint32_t), s));
+  SR_HIP_CHECK(ctx->h_code.ensure(code_cap * sizeof(SrIns<T>), s, ctx->stream2));
+  SR_HIP_CHECK(ctx->h_offsets.ensure((size_t(nt) + 1) * sizeof(uint32_t), s, ctx->stream2));
+  SR_HIP_CHECK(ctx->h_static_bad.ensure(size_t(nt) + 16, s, ctx->stream2));
+  SR_HIP_CHECK(ctx->h_perm.ensure((size_t(nt) + 1) * sizeof(uint32_t), s, ctx->stream2));
   const size_t n_part = size_t(nt) * size_t(n_rb);
   SR_HIP_CHECK(ctx->part_sum.ensure(n_part * sizeof(double) + 8));
   SR_HIP_CHECK(ctx->part_flag.ensure(n_part * sizeof(uint32_t) + 4));
@@ -311,6 +313,13 @@ int run_batch(sr_ctx* ctx, const sr_dataset* ds, int opset_id, const sr_tree_bat
   if (mode == SR_MODE_PRED) SR_HIP_CHECK(ctx->pred.ensure(size_t(nt) * size_t(n_eval) * sizeof(T) + 16));
   const bool use_hint = ctx->dead_hints && mode == SR_MODE_LOSS && n_rb > 1;
   if (use_hint) SR_HIP_CHECK(ctx->hint.ensure(size_t(nt) * sizeof(uint32_t) + 4));
+  // dead-tree probe: the first kProbeTiles row tiles of the view, hints only (scratch partials)
+  constexpr int kProbeTiles = 4;
+  const bool use_probe = use_hint && ctx->probe && n_rb >= 16;
+  if (use_probe) {
+    SR_HIP_CHECK(ctx->probe_sum.ensure(size_t(nt) * sizeof(double) + 8));
+    SR_HIP_CHECK(ctx->probe_flag.ensure(size_t(nt) * sizeof(uint32_t) + 4));
+  }
   if (gather) {
     for (int64_t i = 0; i < n_idx; ++i)
       if (row_idx[i] < 0 || row_idx[i] >= ds->n)
@@ -447,6 +456,19 @@ int run_batch(sr_ctx* ctx, const sr_dataset* ds, int opset_id, const sr_tree_bat
     if (g.n_blocks > 0x7fffffff || g.n_row_blocks != n_rb) {
       sync_both();
       return set_error(SR_ERR_INVALID_ARG, "grid too large");
+    }
+    if (use_probe) {
+      // Trees that are non-finite on the first rows are flagged before the main launch, so its
+      // workgroups skip them from their first tile (without the probe, the ~16 row blocks that
+      // start together evaluate every such tree in full before a hint exists).  Only hints come
+      // out of it: a tree non-finite on some rows of the view is incomplete on the whole view.
+      SrEvalArgs<T> pa = a;
+      pa.tiles_per_block = kProbeTiles;
+      pa.n_row_blocks = 1;
+      pa.n_rows = std::min<int64_t>(n_eval, int64_t(kProbeTiles) * 64 * R);
+      pa.part_sum = ctx->probe_sum.as<double>() + t0;
+      pa.part_flag = ctx->probe_flag.as<uint32_t>() + t0;
+      SR_HIP_CHECK(sr_launch_eval<T>(pa, mode, gather, tier, ctx->rows_override, g.W, g.n_groups, cs));
     }
     SR_HIP_CHECK(hipEventRecord(ctx->ev_c0[c], cs));
     SR_HIP_CHECK(sr_launch_eval<T>(a, mode, gather, tier, ctx->rows_override, g.W, int(g.n_blocks), cs));
@@ -889,6 +911,7 @@ int sr_init(int device, sr_ctx** out) {
   if (const char* v = std::getenv("SR_AMD_NO_SORT")) ctx->cost_order = std::atoi(v) == 0;
   if (const char* v = std::getenv("SR_AMD_NO_HINT")) ctx->dead_hints = std::atoi(v) == 0;
   if (const char* v = std::getenv("SR_AMD_CHUNKS")) ctx->chunks = std::atoi(v);
+  if (const char* v = std::getenv("SR_AMD_NO_PROBE")) ctx->probe = std::atoi(v) == 0;
   hipError_t e = hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking);
   if (e == hipSuccess) e = hipStreamCreateWithFlags(&ctx->stream2, hipStreamNonBlocking);
   if (e == hipSuccess) e = hipEventCreateWithFlags(&ctx->ev_join, hipEventDisableTiming);
@@ -916,7 +939,7 @@ int sr_shutdown(sr_ctx* ctx) {
     (void)hipStreamSynchronize(ctx->stream);
     for (DevBuf* b : {&ctx->code, &ctx->offsets, &ctx->static_bad, &ctx->part_sum, &ctx->part_flag, &ctx->out_sum,
                       &ctx->out_flag, &ctx->pred, &ctx->row_idx, &ctx->tree_list, &ctx->check_sums,
-                      &ctx->perm, &ctx->hint, &ctx->g_code, &ctx->g_offsets, &ctx->g_consts, &ctx->g_const_off,
+                      &ctx->perm, &ctx->hint, &ctx->probe_sum, &ctx->probe_flag, &ctx->g_code, &ctx->g_offsets, &ctx->g_consts, &ctx->g_const_off,
                       &ctx->g_items, &ctx->g_part, &ctx->g_out})
       b->release();
     for (HostBuf* b : {&ctx->h_code, &ctx->h_offsets, &ctx->h_static_bad, &ctx->h_perm}) b->release();

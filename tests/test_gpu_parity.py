@@ -319,6 +319,25 @@ def test_chunked_batch_matches_pieces(monkeypatch):
     assert np.array_equal(l3, loss) and np.array_equal(c3, comp)
 
 
+def test_dead_tree_probe_is_invisible(monkeypatch):
+    """The dead-tree probe launch (first 4 row tiles, hints only) changes no result: a context
+    without it gives bit-identical losses and flags, and both equal the oracle's flags."""
+    opts = Options(**C2_OPTS)
+    X, y = _c2_data(40000, seed=81)
+    tb = flatten_trees(gen_random_population(3000, opts, 5, max_size=30, seed=81), np.float32)
+    loss, comp = eval_loss_batch(tb, Dataset(X, y), opts)
+    monkeypatch.setenv("SR_AMD_NO_PROBE", "1")
+    ctx = sr_amd.device.DeviceContext(0)
+    d2 = Dataset(X, y)
+    l2, c2 = eval_loss_batch(tb, d2, opts, ctx=ctx)
+    d2.free_device()
+    ctx.close()
+    assert np.array_equal(comp, c2) and np.array_equal(loss, l2)
+    _, oc = Oracle.from_options(opts).eval_loss_batch(tb, X, y, n_threads=8)
+    assert np.array_equal(comp, oc)
+    assert 0.2 < comp.mean() < 0.8  # the population has plenty of dead trees for the probe
+
+
 def test_empty_batch_and_errors():
     opts = Options(**C2_OPTS)
     X, y = _c2_data(100)
