@@ -317,8 +317,8 @@ int run_batch(sr_ctx* ctx, const sr_dataset* ds, int opset_id, const sr_tree_bat
   constexpr int kProbeTiles = 4;
   const bool use_probe = use_hint && ctx->probe && n_rb >= 16;
   if (use_probe) {
-    SR_HIP_CHECK(ctx->probe_sum.ensure(size_t(nt) * sizeof(double) + 8));
-    SR_HIP_CHECK(ctx->probe_flag.ensure(size_t(nt) * sizeof(uint32_t) + 4));
+    SR_HIP_CHECK(ctx->probe_sum.ensure(size_t(nt) * kProbeTiles * sizeof(double) + 8));
+    SR_HIP_CHECK(ctx->probe_flag.ensure(size_t(nt) * kProbeTiles * sizeof(uint32_t) + 4));
   }
   if (gather) {
     for (int64_t i = 0; i < n_idx; ++i)
@@ -462,13 +462,17 @@ int run_batch(sr_ctx* ctx, const sr_dataset* ds, int opset_id, const sr_tree_bat
       // workgroups skip them from their first tile (without the probe, the ~16 row blocks that
       // start together evaluate every such tree in full before a hint exists).  Only hints come
       // out of it: a tree non-finite on some rows of the view is incomplete on the whole view.
+      // a wide, short grid: 16 trees x 1 tile per workgroup, kProbeTiles row blocks
       SrEvalArgs<T> pa = a;
-      pa.tiles_per_block = kProbeTiles;
-      pa.n_row_blocks = 1;
+      pa.trees_per_block = std::max(16, g.W);
+      pa.n_groups = int((nc + pa.trees_per_block - 1) / pa.trees_per_block);
+      pa.tiles_per_block = 1;
+      pa.n_row_blocks = kProbeTiles;
       pa.n_rows = std::min<int64_t>(n_eval, int64_t(kProbeTiles) * 64 * R);
-      pa.part_sum = ctx->probe_sum.as<double>() + t0;
-      pa.part_flag = ctx->probe_flag.as<uint32_t>() + t0;
-      SR_HIP_CHECK(sr_launch_eval<T>(pa, mode, gather, tier, ctx->rows_override, g.W, g.n_groups, cs));
+      pa.part_sum = ctx->probe_sum.as<double>();
+      pa.part_flag = ctx->probe_flag.as<uint32_t>();
+      SR_HIP_CHECK(sr_launch_eval<T>(pa, mode, gather, tier, ctx->rows_override, g.W,
+                                     pa.n_groups * kProbeTiles, cs));
     }
     SR_HIP_CHECK(hipEventRecord(ctx->ev_c0[c], cs));
     SR_HIP_CHECK(sr_launch_eval<T>(a, mode, gather, tier, ctx->rows_override, g.W, int(g.n_blocks), cs));
