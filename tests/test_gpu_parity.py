@@ -320,13 +320,14 @@ def test_chunked_batch_matches_pieces(monkeypatch):
 
 
 def test_dead_tree_probe_is_invisible(monkeypatch):
-    """The dead-tree probe launch (first 4 row tiles, hints only) changes no result: a context
-    without it gives bit-identical losses and flags, and both equal the oracle's flags."""
+    """The dead-tree probe launch (first 4 row tiles, hints only; opt-in via SR_AMD_PROBE=1)
+    changes no result: a context with it gives bit-identical losses and flags, and both equal the
+    oracle's flags."""
     opts = Options(**C2_OPTS)
     X, y = _c2_data(40000, seed=81)
     tb = flatten_trees(gen_random_population(3000, opts, 5, max_size=30, seed=81), np.float32)
     loss, comp = eval_loss_batch(tb, Dataset(X, y), opts)
-    monkeypatch.setenv("SR_AMD_NO_PROBE", "1")
+    monkeypatch.setenv("SR_AMD_PROBE", "1")
     ctx = sr_amd.device.DeviceContext(0)
     d2 = Dataset(X, y)
     l2, c2 = eval_loss_batch(tb, d2, opts, ctx=ctx)
