@@ -77,13 +77,15 @@ class Node:
 
     def preorder(self) -> List["Node"]:
         out, stack = [], [self]
+        push, pop, emit = stack.append, stack.pop, out.append  # hot in the host search loop
         while stack:
-            n = stack.pop()
-            out.append(n)
-            if n.degree == 2:
-                stack.append(n.r)
-            if n.degree >= 1:
-                stack.append(n.l)
+            n = pop()
+            emit(n)
+            d = n.degree
+            if d:
+                if d == 2:
+                    push(n.r)
+                push(n.l)
         return out
 
     def count_nodes(self) -> int:
@@ -320,14 +322,14 @@ class TreeBatch:
 
 
 def flatten_trees(trees: Iterable[Node], dtype=np.float32) -> TreeBatch:
-    degree, op, feature, constant, val, offsets = [], [], [], [], [], [0]
+    nodes, offsets = [], [0]
     for t in trees:
         t = getattr(t, "tree", t)  # PopMember / Expression wrappers
-        for n in t.preorder():
-            degree.append(n.degree)
-            op.append(n.op)
-            feature.append(n.feature)
-            constant.append(1 if (n.degree == 0 and n.constant) else 0)
-            val.append(n.val if n.constant else 0.0)
-        offsets.append(len(degree))
+        nodes.extend(t.preorder())
+        offsets.append(len(nodes))
+    degree = [n.degree for n in nodes]
+    op = [n.op for n in nodes]
+    feature = [n.feature for n in nodes]
+    constant = [1 if (n.degree == 0 and n.constant) else 0 for n in nodes]
+    val = [n.val if n.constant else 0.0 for n in nodes]
     return TreeBatch(offsets, degree, op, feature, constant, np.array(val, dtype=dtype))
