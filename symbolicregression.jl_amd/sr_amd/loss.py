@@ -37,7 +37,6 @@ def eval_loss_batch(trees, dataset, options, *, ctx=None):
         raise NotImplementedError("custom objectives are evaluated by the reference CPU path")
     ctx = ctx or get_context()
     full = dataset.full
-    T = full.dtype.type
     tb = _as_batch(trees, full.dtype)
     nt = tb.n_trees
     losses = np.empty(nt, dtype=full.dtype)
@@ -59,7 +58,6 @@ def eval_loss_batch(trees, dataset, options, *, ctx=None):
             complete.ctypes.data_as(ctypes.c_void_p),
         )
     )
-    del T
     return losses, complete.astype(bool)
 
 
