@@ -175,6 +175,9 @@ struct Grid {
   size_t lds = 0;
 };
 constexpr size_t kLdsMax = 160 * 1024;
+// Upper bound on row blocks per tree (tuning knob SR_AMD_MAX_ROW_BLOCKS, read at sr_init).
+static int g_max_row_blocks = 256;
+
 template <typename T>
 Grid make_grid(int64_t n_rows, int64_t n_trees, int R, int W, int nf, int depth, int max_checks, bool weighted,
                int g_override = 0) {
@@ -183,7 +186,7 @@ Grid make_grid(int64_t n_rows, int64_t n_trees, int R, int W, int nf, int depth,
   g.R = R;
   g.W = W;
   const int64_t n_tiles = (n_rows + rows_per_tile - 1) / rows_per_tile;
-  int64_t tiles = (n_tiles + 255) / 256;  // keep <= 256 row blocks per tree
+  int64_t tiles = (n_tiles + g_max_row_blocks - 1) / g_max_row_blocks;  // keep <= max row blocks per tree
   if (tiles < 1) tiles = 1;
   g.tiles = int(tiles);
   g.n_row_blocks = int((n_tiles + tiles - 1) / tiles);
@@ -917,6 +920,7 @@ int sr_init(int device, sr_ctx** out) {
   if (const char* v = std::getenv("SR_AMD_NO_HINT")) ctx->dead_hints = std::atoi(v) == 0;
   if (const char* v = std::getenv("SR_AMD_CHUNKS")) ctx->chunks = std::atoi(v);
   if (const char* v = std::getenv("SR_AMD_PROBE")) ctx->probe = std::atoi(v) != 0;
+  if (const char* v = std::getenv("SR_AMD_MAX_ROW_BLOCKS")) g_max_row_blocks = std::max(1, std::atoi(v));
   hipError_t e = hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking);
   if (e == hipSuccess) e = hipStreamCreateWithFlags(&ctx->stream2, hipStreamNonBlocking);
   if (e == hipSuccess) e = hipEventCreateWithFlags(&ctx->ev_join, hipEventDisableTiming);
