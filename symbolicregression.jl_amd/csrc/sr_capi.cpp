@@ -146,6 +146,7 @@ struct sr_ctx {
   int waves_override = 0;   // SR_AMD_WAVES (tuning): 8 selects the 8-wave f32 BASIC L2 loss kernel
   bool cost_order = true;   // launch trees in decreasing estimated cost (SR_AMD_NO_SORT=1 disables)
   bool dead_hints = true;   // share dead-tree hints across row blocks (SR_AMD_NO_HINT=1 disables)
+  int max_row_blocks = 256; // SR_AMD_MAX_ROW_BLOCKS (tuning): upper bound on row blocks per tree
   int chunks = 2;           // SR_AMD_CHUNKS: pipeline compile/launch over this many tree chunks (1 = off)
   bool probe = false;       // SR_AMD_PROBE=1 enables the dead-tree probe launch (off: it saves
                             // ~0.4 ms of C2 kernel time but costs more step time than it saves)
@@ -175,18 +176,15 @@ struct Grid {
   size_t lds = 0;
 };
 constexpr size_t kLdsMax = 160 * 1024;
-// Upper bound on row blocks per tree (tuning knob SR_AMD_MAX_ROW_BLOCKS, read at sr_init).
-static int g_max_row_blocks = 256;
-
 template <typename T>
 Grid make_grid(int64_t n_rows, int64_t n_trees, int R, int W, int nf, int depth, int max_checks, bool weighted,
-               int g_override = 0) {
+               int g_override = 0, int max_row_blocks = 256) {
   const int64_t rows_per_tile = 64 * int64_t(R);
   Grid g;
   g.R = R;
   g.W = W;
   const int64_t n_tiles = (n_rows + rows_per_tile - 1) / rows_per_tile;
-  int64_t tiles = (n_tiles + g_max_row_blocks - 1) / g_max_row_blocks;  // keep <= max row blocks per tree
+  int64_t tiles = (n_tiles + max_row_blocks - 1) / max_row_blocks;  // keep <= max row blocks per tree
   if (tiles < 1) tiles = 1;
   g.tiles = int(tiles);
   g.n_row_blocks = int((n_tiles + tiles - 1) / tiles);
@@ -298,7 +296,8 @@ int run_batch(sr_ctx* ctx, const sr_dataset* ds, int opset_id, const sr_tree_bat
 
   // device + pinned buffers sized for the whole batch up front (a chunk's kernel may still run while
   // the next one is staged): a program has at most one instruction per node
-  Grid g0 = make_grid<T>(n_eval, nt > 0 ? nt : 1, R, W, int(ds->nf), 1, 0, ds->w != nullptr, ctx->tree_group);
+  Grid g0 = make_grid<T>(n_eval, nt > 0 ? nt : 1, R, W, int(ds->nf), 1, 0, ds->w != nullptr, ctx->tree_group,
+                         ctx->max_row_blocks);
   const int n_rb = g0.n_row_blocks;
   const size_t code_cap = size_t(total_nodes) + 16;
   SR_HIP_CHECK(ctx->code.ensure(code_cap * sizeof(SrIns<T>)));
@@ -385,7 +384,8 @@ int run_batch(sr_ctx* ctx, const sr_dataset* ds, int opset_id, const sr_tree_bat
     }
     if (c == 0) ctx->mark_phase(0);
     const int depth = pc.max_depth > 0 ? pc.max_depth : 1;
-    Grid g = make_grid<T>(n_eval, nc, R, W, int(ds->nf), depth, 0, ds->w != nullptr, ctx->tree_group);
+    Grid g = make_grid<T>(n_eval, nc, R, W, int(ds->nf), depth, 0, ds->w != nullptr, ctx->tree_group,
+                         ctx->max_row_blocks);
     if (g.lds > kLdsMax) {
       sync_both();
       return set_error(SR_ERR_TOO_DEEP, "the row tile (" + std::to_string(ds->nf) + " features, " +
@@ -519,10 +519,10 @@ int run_exact(sr_ctx* ctx, const sr_dataset* ds, const SrProgramBatch<T>& prog, 
   const int depth = prog.max_depth > 0 ? prog.max_depth : 1;
   // several listed trees per workgroup share one staged row tile (the heuristic G: >= 4096 workgroups)
   Grid g = make_grid<T>(n_eval, n_list, sr_rows_per_lane<T>(SR_MODE_EXACT, SR_TIER_FULL, 0), 4, int(ds->nf), depth,
-                        max_checks, ds->w != nullptr, 0);
+                        max_checks, ds->w != nullptr, 0, ctx->max_row_blocks);
   if (g.lds > kLdsMax)  // many checks: one tree per workgroup
     g = make_grid<T>(n_eval, n_list, sr_rows_per_lane<T>(SR_MODE_EXACT, SR_TIER_FULL, 0), 4, int(ds->nf), depth,
-                     max_checks, ds->w != nullptr, 1);
+                     max_checks, ds->w != nullptr, 1, ctx->max_row_blocks);
   if (g.lds > kLdsMax) return set_error(SR_ERR_TOO_DEEP, "exact-sum pass needs more LDS than 160 KiB");
   std::vector<uint32_t> list32(static_cast<size_t>(n_list));
   for (int64_t i = 0; i < n_list; ++i) list32[size_t(i)] = uint32_t(list[i]);
@@ -920,7 +920,7 @@ int sr_init(int device, sr_ctx** out) {
   if (const char* v = std::getenv("SR_AMD_NO_HINT")) ctx->dead_hints = std::atoi(v) == 0;
   if (const char* v = std::getenv("SR_AMD_CHUNKS")) ctx->chunks = std::atoi(v);
   if (const char* v = std::getenv("SR_AMD_PROBE")) ctx->probe = std::atoi(v) != 0;
-  if (const char* v = std::getenv("SR_AMD_MAX_ROW_BLOCKS")) g_max_row_blocks = std::max(1, std::atoi(v));
+  if (const char* v = std::getenv("SR_AMD_MAX_ROW_BLOCKS")) ctx->max_row_blocks = std::max(1, std::atoi(v));
   hipError_t e = hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking);
   if (e == hipSuccess) e = hipStreamCreateWithFlags(&ctx->stream2, hipStreamNonBlocking);
   if (e == hipSuccess) e = hipEventCreateWithFlags(&ctx->ev_join, hipEventDisableTiming);

@@ -403,3 +403,30 @@ def test_row_sharded_partials_match_single():
                                            out.ctypes.data_as(ctypes.c_void_p), comp.ctypes.data_as(ctypes.c_void_p)))
     assert np.array_equal(comp.astype(bool), full_comp)
     assert np.max(_rel(out[full_comp], full_loss[full_comp])) < 1e-6
+
+
+@pytest.mark.parametrize("max_rb", [1, 7, 1000])
+def test_row_block_bound_keeps_results(monkeypatch, max_rb):
+    """SR_AMD_MAX_ROW_BLOCKS only regroups rows into workgroups (one tile per block up to every tile
+    in one block): flags stay bit-identical to the default grid and to the oracle, losses move only
+    by the f64 partial-sum grouping."""
+    opts = Options(**C2_OPTS)
+    X, y = _c2_data(100_000, seed=83)
+    trees = flatten_trees(gen_random_population(1500, opts, 5, max_size=30, seed=83), np.float32)
+    d = Dataset(X, y)
+    ref_loss, ref_comp = eval_loss_batch(trees, d, opts)
+    monkeypatch.setenv("SR_AMD_MAX_ROW_BLOCKS", str(max_rb))
+    ctx = sr_amd.device.DeviceContext(0)  # reads the environment at creation
+    d2 = Dataset(X, y)  # a device dataset belongs to one context
+    loss, comp = eval_loss_batch(trees, d2, opts, ctx=ctx)
+    assert np.array_equal(comp, ref_comp)
+    fin = np.isfinite(ref_loss)
+    assert np.array_equal(fin, np.isfinite(loss))
+    assert np.max(_rel(loss[fin], ref_loss[fin]), initial=0.0) < 1e-6
+    sub = flatten_trees([trees.tree(i) for i in range(0, 1500, 15)], np.float32)
+    good, ol, oc = well_conditioned(Oracle.from_options(opts), sub, X, y)
+    assert np.array_equal(comp[::15], oc)
+    assert np.max(_rel(loss[::15][good], ol[good]), initial=0.0) < 1e-4
+    d2.free_device()
+    d.free_device()
+    ctx.close()
