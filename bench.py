@@ -178,7 +178,7 @@ def main():
                 "peak": PEAK_FP32_TFLOPS,
                 "unit": "TFLOP/s",
                 "frac": achieved / PEAK_FP32_TFLOPS,
-                "traffic": traffic.get("hbm_read_bytes_per_launch") * n_launch if traffic else None,
+                "traffic": traffic.get("hbm_read_bytes_per_step") if traffic else None,
                 "traffic_source": traffic.get("source") if traffic else None,
                 "kernel": "sr_tile_kernel<float,8,LOSS,gather=false,BASIC>",
                 "kernel_ms_mean": kmean,
@@ -238,6 +238,9 @@ def search_throughput(niterations):
             "config": "C1 README example, X=randn(2,100) f64, 20 populations, default options"}
 
 
+PROFILED_STEPS = 6  # steps + warmup of the bench command tools/profile.sh profiles
+
+
 def measured_traffic():
     """Per-launch HBM bytes of the interpreter kernel from the committed rocprofv3 PMC pass of this
     same command (profiles/traffic.json, written by tools/profile.sh: FETCH_SIZE x2, gfx950)."""
@@ -247,6 +250,9 @@ def measured_traffic():
             t = json.load(f)
     except (OSError, ValueError):
         return None
+    # per step: every interpreter launch of the profiled run (chunks and dead-tree probes) over its
+    # steps (tools/profile.sh runs bench.py --steps 5 --warmup 1)
+    t["hbm_read_bytes_per_step"] = t["hbm_read_bytes_per_launch"] * t["calls"] / PROFILED_STEPS
     t["source"] = "profiles/traffic.json (rocprofv3 --pmc FETCH_SIZE of bench.py)"
     return t
 

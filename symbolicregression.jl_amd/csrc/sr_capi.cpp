@@ -148,8 +148,9 @@ struct sr_ctx {
   bool dead_hints = true;   // share dead-tree hints across row blocks (SR_AMD_NO_HINT=1 disables)
   int max_row_blocks = 256; // SR_AMD_MAX_ROW_BLOCKS (tuning): upper bound on row blocks per tree
   int chunks = 2;           // SR_AMD_CHUNKS: pipeline compile/launch over this many tree chunks (1 = off)
-  bool probe = false;       // SR_AMD_PROBE=1 enables the dead-tree probe launch (off: it saves
-                            // ~0.4 ms of C2 kernel time but costs more step time than it saves)
+  int probe = 2;            // dead-tree probe launch (SR_AMD_PROBE): 0 off, 1 before every chunk,
+                            // 2 (default) only before the chunks after the first, whose probe
+                            // overlaps the first chunk's kernel (profiles/r01_ab_probe_modes.txt)
   std::vector<uint32_t> perm_host;
 };
 
@@ -461,7 +462,8 @@ int run_batch(sr_ctx* ctx, const sr_dataset* ds, int opset_id, const sr_tree_bat
       sync_both();
       return set_error(SR_ERR_INVALID_ARG, "grid too large");
     }
-    if (use_probe) {
+    SR_HIP_CHECK(hipEventRecord(ctx->ev_c0[c], cs));  // the chunk's kernel time includes its probe
+    if (use_probe && (ctx->probe != 2 || c > 0)) {
       // Trees that are non-finite on the first rows are flagged before the main launch, so its
       // workgroups skip them from their first tile (without the probe, the ~16 row blocks that
       // start together evaluate every such tree in full before a hint exists).  Only hints come
@@ -478,7 +480,6 @@ int run_batch(sr_ctx* ctx, const sr_dataset* ds, int opset_id, const sr_tree_bat
       SR_HIP_CHECK(sr_launch_eval<T>(pa, mode, gather, tier, ctx->rows_override, g.W,
                                      pa.n_groups * kProbeTiles, cs));
     }
-    SR_HIP_CHECK(hipEventRecord(ctx->ev_c0[c], cs));
     SR_HIP_CHECK(sr_launch_eval<T>(a, mode, gather, tier, ctx->rows_override, g.W, int(g.n_blocks), cs));
     SR_HIP_CHECK(hipEventRecord(ctx->ev_c1[c], cs));
     SR_HIP_CHECK(sr_launch_reduce(a.part_sum, a.part_flag, int(nc), n_rb, a.perm, ctx->static_bad.as<uint8_t>() + t0,
@@ -919,7 +920,7 @@ int sr_init(int device, sr_ctx** out) {
   if (const char* v = std::getenv("SR_AMD_NO_SORT")) ctx->cost_order = std::atoi(v) == 0;
   if (const char* v = std::getenv("SR_AMD_NO_HINT")) ctx->dead_hints = std::atoi(v) == 0;
   if (const char* v = std::getenv("SR_AMD_CHUNKS")) ctx->chunks = std::atoi(v);
-  if (const char* v = std::getenv("SR_AMD_PROBE")) ctx->probe = std::atoi(v) != 0;
+  if (const char* v = std::getenv("SR_AMD_PROBE")) ctx->probe = std::atoi(v);
   if (const char* v = std::getenv("SR_AMD_MAX_ROW_BLOCKS")) ctx->max_row_blocks = std::max(1, std::atoi(v));
   hipError_t e = hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking);
   if (e == hipSuccess) e = hipStreamCreateWithFlags(&ctx->stream2, hipStreamNonBlocking);

@@ -319,15 +319,17 @@ def test_chunked_batch_matches_pieces(monkeypatch):
     assert np.array_equal(l3, loss) and np.array_equal(c3, comp)
 
 
-def test_dead_tree_probe_is_invisible(monkeypatch):
-    """The dead-tree probe launch (first 4 row tiles, hints only; opt-in via SR_AMD_PROBE=1)
-    changes no result: a context with it gives bit-identical losses and flags, and both equal the
-    oracle's flags."""
+@pytest.mark.parametrize("mode", ["0", "1"])
+def test_dead_tree_probe_is_invisible(monkeypatch, mode):
+    """The dead-tree probe launch (first 4 row tiles, hints only; SR_AMD_PROBE: 0 off, 1 every
+    chunk, 2 = default, the chunks after the first) changes no result: contexts in every mode give
+    bit-identical losses and flags, and all equal the oracle's flags.  6600 trees -> two chunks."""
     opts = Options(**C2_OPTS)
     X, y = _c2_data(40000, seed=81)
-    tb = flatten_trees(gen_random_population(3000, opts, 5, max_size=30, seed=81), np.float32)
+    tb = flatten_trees(gen_random_population(6600, opts, 5, max_size=30, seed=81), np.float32)
     loss, comp = eval_loss_batch(tb, Dataset(X, y), opts)
-    monkeypatch.setenv("SR_AMD_PROBE", "1")
+    assert sr_amd.device.get_context().last_launches() == 2
+    monkeypatch.setenv("SR_AMD_PROBE", mode)
     ctx = sr_amd.device.DeviceContext(0)
     d2 = Dataset(X, y)
     l2, c2 = eval_loss_batch(tb, d2, opts, ctx=ctx)
