@@ -44,8 +44,8 @@ def c2_workload(n_rows, n_trees, rank, nf=5):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=10)
-    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=8)
     ap.add_argument("--rows", type=int, default=1 << 20, help="rows per GPU")
     ap.add_argument("--trees", type=int, default=10000)
     ap.add_argument("--cpu-trees", type=int, default=0, help="CPU-baseline tree sample (0 = auto)")
@@ -108,12 +108,14 @@ def main():
     for _ in range(args.warmup):
         step()
     barrier()
-    kernel_ms = []
+    kernel_ms, step_t = [], []
     t0 = time.perf_counter()
     for _ in range(args.steps):
         kernel_ms.append(step())
+        step_t.append(time.perf_counter())
     barrier()
     dt = time.perf_counter() - t0
+    step_ms = np.diff(np.array([t0] + step_t)) * 1e3  # per-step wall (rank-local), jitter diagnostics
     if dist is not None:
         import torch
 
@@ -156,6 +158,7 @@ def main():
             "steps": args.steps,
             "warmup": args.warmup,
             "ms_per_step": dt / args.steps * 1e3,
+            "step_ms_min_median_max": [float(step_ms.min()), float(np.median(step_ms)), float(step_ms.max())],
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
