@@ -140,28 +140,50 @@ int sr_eval_tree_array(sr_ctx* ctx, const sr_dataset* ds, int opset_id, const sr
  * rows; n_total is the number of rows over ALL shards (it sets the overflow-check threshold).
  * Writes per-tree partial Σ w·loss (f64) and flag bits (SR_FLAG_*).  With out_on_device = 1 the
  * two output pointers are device pointers (e.g. a torch tensor to all-reduce with RCCL).
- * Combine across ranks: sums add, flags OR; then call sr_exact_check_partials for trees whose
- * combined flags == SR_FLAG_BIG and sr_finalize_losses.
+ * Combine across ranks: sums add, flags OR; trees whose combined flags == SR_FLAG_BIG get the exact
+ * verdict from sr_jsum_partials + sr_jsum_finite; then sr_finalize_losses.
  */
 int sr_eval_loss_partials(sr_ctx* ctx, const sr_dataset* ds, int opset_id, const sr_tree_batch* trees,
                           int64_t n_total, int loss_kind, double* out_sum, uint32_t* out_flags,
                           int out_on_device);
-/* Maximum number of checked nodes per tree for `trees` (sizes sr_exact_check_partials output). */
+/*
+ * The same partials packed for ONE all-reduce (SUM): out[4][n_trees] f64 = Σ w·loss, then the
+ * SR_FLAG_NONFINITE, SR_FLAG_BIG and SR_FLAG_STATIC bits as 0/1 (summed over ranks: > 0 means set).
+ * out_on_device = 1: `out` is a device pointer on this context's GPU (no host round trip).
+ */
+int sr_eval_loss_partials_packed(sr_ctx* ctx, const sr_dataset* ds, int opset_id, const sr_tree_batch* trees,
+                                 int64_t n_total, int loss_kind, double* out, int out_on_device);
+/* Maximum number of checked nodes per tree for `trees` (sizes the sr_jsum_partials output). */
 int sr_max_checks(sr_ctx* ctx, int opset_id, const sr_tree_batch* trees, int* max_checks);
 /*
- * Exact array-sum validity check (DynamicExpressions' isfinite(sum(x)) on every checked node)
- * for the trees listed in tree_list[n_list]; out_sums[n_list][max_checks] receive this shard's
- * f64 sums (scaled by 2^-64 for f64 data).  Sum across ranks, then pass to sr_finalize_losses.
+ * Exact validity check, DynamicExpressions' isfinite(sum(x)) on every checked node with Base's
+ * pairwise `sum` in T (Base.mapreduce_impl: halves split at lo + (hi-lo)>>1 down to blocks of < 1024
+ * elements folded sequentially).  This dataset holds global rows [row_offset, row_offset + n) of
+ * n_total.  sr_jsum_range_count gives the number of row ranges this shard folds (the global leaf
+ * blocks it holds, and one-row ranges continuing a block that starts in an earlier shard);
+ * sr_jsum_partials writes, for the listed trees, out_vals[n_list][max_checks][n_ranges] (T: the
+ * fold of each checked array over each range).  sr_jsum_finite combines every shard's values
+ * (row_offsets[n_ranks + 1] bounds the shards, rank_vals[r] = shard r's out_vals) into
+ * out_finite[n_arrays] (n_arrays = n_list * max_checks): a tree is complete iff all its arrays are.
  */
-int sr_exact_check_partials(sr_ctx* ctx, const sr_dataset* ds, int opset_id, const sr_tree_batch* trees,
-                            const int64_t* tree_list, int64_t n_list, int max_checks, double* out_sums);
+int sr_jsum_range_count(int64_t row_offset, int64_t n_local, int64_t n_total, int64_t* out_n_ranges);
+/* The ranges themselves (each output may be NULL): local rows [lo, hi], global leaf index, and
+ * head = 1 for a one-row range continuing a leaf that starts in an earlier shard. */
+int sr_jsum_ranges(int64_t row_offset, int64_t n_local, int64_t n_total, int64_t* lo, int64_t* hi, int64_t* leaf,
+                   uint8_t* head);
+int sr_jsum_partials(sr_ctx* ctx, const sr_dataset* ds, int opset_id, const sr_tree_batch* trees,
+                     const int64_t* tree_list, int64_t n_list, int max_checks, int64_t row_offset, int64_t n_total,
+                     void* out_vals);
+int sr_jsum_finite(int dtype, int64_t n_total, int n_ranks, const int64_t* row_offsets, const void* const* rank_vals,
+                   int64_t n_arrays, uint8_t* out_finite);
 /*
  * Host-side combine: loss = sum / denom (denom = n_total, or Σweights), +Inf when incomplete.
- * check_sums may be NULL when no tree carries SR_FLAG_BIG alone.
+ * Trees flagged SR_FLAG_BIG alone are listed in tree_list with their exact verdict list_ok
+ * (1 = every checked array's Julia sum is finite); list may be empty (NULL, 0).
  */
 int sr_finalize_losses(int dtype, int64_t n_trees, const double* sums, const uint32_t* flags, double denom,
-                       const int64_t* tree_list, int64_t n_list, int max_checks, const double* check_sums,
-                       void* out_loss, uint8_t* out_complete);
+                       const int64_t* tree_list, int64_t n_list, const uint8_t* list_ok, void* out_loss,
+                       uint8_t* out_complete);
 /* Σ weights of this shard (f64), or the row count when unweighted. */
 int sr_dataset_denominator(const sr_dataset* ds, double* denom);
 

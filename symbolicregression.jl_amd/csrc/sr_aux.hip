@@ -30,6 +30,26 @@ __global__ void __launch_bounds__(256) sr_reduce_partials_kernel(const double* _
   out_flag[tree] = f;
 }
 
+// Packed row-shard partials for one all-reduce (sr_eval_loss_partials_packed): [4][n] f64 = Σ loss,
+// then the NONFINITE / BIG / STATIC flag bits as 0 / 1.
+__global__ void __launch_bounds__(256) sr_pack_partials_kernel(const double* __restrict__ sum,
+                                                                const uint32_t* __restrict__ flag, int n,
+                                                                double* __restrict__ out) {
+  const int t = int(int64_t(blockIdx.x) * blockDim.x + threadIdx.x);
+  if (t >= n) return;
+  const uint32_t f = flag[t];
+  out[t] = sum[t];
+  out[size_t(n) + t] = (f & SR_FLAG_NONFINITE) ? 1.0 : 0.0;
+  out[2 * size_t(n) + t] = (f & SR_FLAG_BIG) ? 1.0 : 0.0;
+  out[3 * size_t(n) + t] = (f & SR_FLAG_STATIC) ? 1.0 : 0.0;
+}
+
+hipError_t sr_launch_pack_partials(const double* sum, const uint32_t* flag, int n, double* out, hipStream_t s) {
+  if (n <= 0) return hipSuccess;
+  hipLaunchKernelGGL(sr_pack_partials_kernel, dim3(unsigned((n + 255) / 256)), dim3(256), 0, s, sum, flag, n, out);
+  return hipGetLastError();
+}
+
 // Julia [nf, n] column-major -> per-feature rows [nf][ld]; padded rows replicate row 0 so that the
 // interpreter's validity checks never see a value that is not in the dataset.
 template <typename T>
@@ -89,9 +109,11 @@ template int sr_rows_per_lane<double>(int, int, int);
 
 size_t sr_tile_lds_bytes(int elem_size, int nf, int rows_per_lane, int stack_depth, int trees_per_block,
                          int max_checks, int waves, bool weighted) {
+  // = SrLdsPlan (sr_tile_impl.h): X tile, y (+ w), LDS stack, EXACT checked values + running sums
   const size_t rows = size_t(64) * rows_per_lane;
   return size_t(nf) * rows * elem_size + (weighted ? 2 : 1) * rows * elem_size +
-         size_t(waves) * stack_depth * rows * elem_size + size_t(trees_per_block) * size_t(max_checks) * 8;
+         size_t(waves) * stack_depth * rows * elem_size + size_t(waves) * size_t(max_checks) * rows * elem_size +
+         (size_t(trees_per_block) * size_t(max_checks) * elem_size + 15) / 16 * 16;
 }
 
 // Waves per workgroup: the f32 BASIC loss kernel has 4- and 8-wave (L2) builds (SR_AMD_WAVES selects);
@@ -103,18 +125,38 @@ int sr_waves_per_block(int elem_size, int mode, int tier, int rows_per_lane, int
 }
 
 // BASIC-tier loss kernels are built per elementwise loss (the loss code folds away).
-template <typename T, int R, bool GATHER>
+template <typename T, int R, bool GATHER, bool VSTK = false>
 hipError_t sr_launch_basic_loss(const SrEvalArgs<T>& a, int n_blocks, hipStream_t s) {
-  if (a.loss_kind == SR_LOSS_L1) return sr_launch_tile<T, R, SR_MODE_LOSS, GATHER, SR_TIER_BASIC, 4, SR_LOSS_L1>(a, n_blocks, s);
-  if (a.loss_kind == SR_LOSS_L2) return sr_launch_tile<T, R, SR_MODE_LOSS, GATHER, SR_TIER_BASIC, 4, SR_LOSS_L2>(a, n_blocks, s);
-  return sr_launch_tile<T, R, SR_MODE_LOSS, GATHER, SR_TIER_BASIC, 4, -1>(a, n_blocks, s);  // the other losses
+  if (a.loss_kind == SR_LOSS_L1)
+    return sr_launch_tile<T, R, SR_MODE_LOSS, GATHER, SR_TIER_BASIC, 4, SR_LOSS_L1, VSTK>(a, n_blocks, s);
+  if (a.loss_kind == SR_LOSS_L2)
+    return sr_launch_tile<T, R, SR_MODE_LOSS, GATHER, SR_TIER_BASIC, 4, SR_LOSS_L2, VSTK>(a, n_blocks, s);
+  return sr_launch_tile<T, R, SR_MODE_LOSS, GATHER, SR_TIER_BASIC, 4, -1, VSTK>(a, n_blocks, s);  // other losses
+}
+
+// Register-stack kernels (f32 BASIC loss over the full dataset, operand stack in VGPRs): rows per
+// lane for a view of n rows, or 0 when the classic LDS-stack kernel should run.  Larger tiles
+// amortise the per-instruction dispatch over more rows; below a few tiles the
+// padding and the loss of parallelism cost more.  requested: SR_AMD_ROWS_PER_LANE (16 / 32 force a
+// register-stack kernel, 4 / 8 the classic one).
+int sr_vstk_rows(int64_t n_rows, int requested) {
+  if (requested == 16 || requested == 32) return requested;
+  if (requested != 0) return 0;
+  if (n_rows >= 65536) return 32;
+  if (n_rows >= 8192) return 16;
+  return 0;
 }
 
 template <typename T>
-hipError_t sr_launch_eval(const SrEvalArgs<T>& a, int mode, bool gather, int tier, int rows_per_lane, int waves,
+hipError_t sr_launch_eval(const SrEvalArgs<T>& a, int mode, bool gather, int tier, int R, int waves, bool vstk,
                           int n_blocks, hipStream_t s) {
-  const int R = sr_rows_per_lane<T>(mode, tier, rows_per_lane);
   if constexpr (sizeof(T) == 4) {
+    if (vstk) {
+      if (mode != SR_MODE_LOSS || tier != SR_TIER_BASIC || gather) return hipErrorInvalidValue;
+      if (R == 32) return sr_launch_basic_loss<T, 32, false, true>(a, n_blocks, s);
+      if (R == 16) return sr_launch_basic_loss<T, 16, false, true>(a, n_blocks, s);
+      return hipErrorInvalidValue;
+    }
     if (mode == SR_MODE_LOSS) {
       if (tier == SR_TIER_BASIC) {
         if (gather) return sr_launch_basic_loss<T, 8, true>(a, n_blocks, s);
@@ -130,11 +172,12 @@ hipError_t sr_launch_eval(const SrEvalArgs<T>& a, int mode, bool gather, int tie
     if (mode == SR_MODE_PRED)
       return gather ? sr_launch_tile<T, 4, SR_MODE_PRED, true, SR_TIER_FULL>(a, n_blocks, s)
                     : sr_launch_tile<T, 4, SR_MODE_PRED, false, SR_TIER_FULL>(a, n_blocks, s);
-    return gather ? sr_launch_tile<T, 4, SR_MODE_EXACT, true, SR_TIER_FULL>(a, n_blocks, s)
-                  : sr_launch_tile<T, 4, SR_MODE_EXACT, false, SR_TIER_FULL>(a, n_blocks, s);
+    return gather ? sr_launch_tile<T, 4, SR_MODE_EXACT, true, SR_TIER_FULL, 1>(a, n_blocks, s)
+                  : sr_launch_tile<T, 4, SR_MODE_EXACT, false, SR_TIER_FULL, 1>(a, n_blocks, s);
   } else {
     (void)R;
     (void)waves;
+    if (vstk) return hipErrorInvalidValue;
     if (mode == SR_MODE_LOSS) {
       if (tier == SR_TIER_BASIC)
         return gather ? sr_launch_basic_loss<T, 4, true>(a, n_blocks, s) : sr_launch_basic_loss<T, 4, false>(a, n_blocks, s);
@@ -144,13 +187,12 @@ hipError_t sr_launch_eval(const SrEvalArgs<T>& a, int mode, bool gather, int tie
     if (mode == SR_MODE_PRED)
       return gather ? sr_launch_tile<T, 2, SR_MODE_PRED, true, SR_TIER_FULL>(a, n_blocks, s)
                     : sr_launch_tile<T, 2, SR_MODE_PRED, false, SR_TIER_FULL>(a, n_blocks, s);
-    return gather ? sr_launch_tile<T, 2, SR_MODE_EXACT, true, SR_TIER_FULL>(a, n_blocks, s)
-                  : sr_launch_tile<T, 2, SR_MODE_EXACT, false, SR_TIER_FULL>(a, n_blocks, s);
+    return gather ? sr_launch_tile<T, 2, SR_MODE_EXACT, true, SR_TIER_FULL, 1>(a, n_blocks, s)
+                  : sr_launch_tile<T, 2, SR_MODE_EXACT, false, SR_TIER_FULL, 1>(a, n_blocks, s);
   }
 }
-
-template hipError_t sr_launch_eval<float>(const SrEvalArgs<float>&, int, bool, int, int, int, int, hipStream_t);
-template hipError_t sr_launch_eval<double>(const SrEvalArgs<double>&, int, bool, int, int, int, int, hipStream_t);
+template hipError_t sr_launch_eval<float>(const SrEvalArgs<float>&, int, bool, int, int, int, bool, int, hipStream_t);
+template hipError_t sr_launch_eval<double>(const SrEvalArgs<double>&, int, bool, int, int, int, bool, int, hipStream_t);
 template hipError_t sr_launch_transpose<float>(const float*, int64_t, int64_t, int64_t, float*, hipStream_t);
 template hipError_t sr_launch_transpose<double>(const double*, int64_t, int64_t, int64_t, double*, hipStream_t);
 template hipError_t sr_launch_pad<float>(float*, int64_t, int64_t, float, int, hipStream_t);

@@ -125,7 +125,7 @@ struct sr_ctx {
   std::vector<int> tiers;
   std::vector<std::pair<int, double>> losses;  // registered (kind, param); code = kLossCodeBase + index
   DevBuf code, offsets, static_bad, part_sum, part_flag, out_sum, out_flag, pred, row_idx, tree_list,
-      check_sums, perm, hint, probe_sum, probe_flag, g_code, g_offsets, g_consts, g_const_off, g_items, g_part, g_out;
+      range_lo, range_hi, range_sums, packed, perm, hint, probe_sum, probe_flag, g_code, g_offsets, g_consts, g_const_off, g_items, g_part, g_out;
   double last_eval_ms = 0.0, last_total_ms = 0.0;
   // host-side phases of the last eval_loss call (ms): compile, upload+launch, wait, exact pass,
   // finalize (sr_last_phase_ms)
@@ -274,6 +274,12 @@ int run_batch(sr_ctx* ctx, const sr_dataset* ds, int opset_id, const sr_tree_bat
   const int tier = ctx->tiers[opset_id];
   const int R = sr_rows_per_lane<T>(mode, tier, ctx->rows_override);
   const int W = sr_waves_per_block(int(sizeof(T)), mode, tier, R, ctx->waves_override);
+  // register-stack kernel (f32 BASIC loss over the full dataset): Rv rows per lane, used for every
+  // chunk whose programs need <= 2 operand-stack slots (all trees of <= 30 nodes); other chunks run
+  // the LDS-stack kernel at R rows per lane
+  const int Rv = (sizeof(T) == 4 && mode == SR_MODE_LOSS && tier == SR_TIER_BASIC && !gather)
+                     ? sr_vstk_rows(n_eval, ctx->rows_override)
+                     : 0;
   hipStream_t s = ctx->stream;
   // error exits while chunks are in flight: no DMA may still read the staging buffers
   auto sync_both = [&] {
@@ -299,7 +305,10 @@ int run_batch(sr_ctx* ctx, const sr_dataset* ds, int opset_id, const sr_tree_bat
   // the next one is staged): a program has at most one instruction per node
   Grid g0 = make_grid<T>(n_eval, nt > 0 ? nt : 1, R, W, int(ds->nf), 1, 0, ds->w != nullptr, ctx->tree_group,
                          ctx->max_row_blocks);
-  const int n_rb = g0.n_row_blocks;
+  int n_rb = g0.n_row_blocks;  // row blocks the partial buffers hold per tree (the most any kernel uses)
+  if (Rv > 0)
+    n_rb = std::max(n_rb, make_grid<T>(n_eval, nt > 0 ? nt : 1, Rv, W, int(ds->nf), 0, 0, ds->w != nullptr,
+                                       ctx->tree_group, ctx->max_row_blocks).n_row_blocks);
   const size_t code_cap = size_t(total_nodes) + 16;
   SR_HIP_CHECK(ctx->code.ensure(code_cap * sizeof(SrIns<T>)));
   SR_HIP_CHECK(ctx->offsets.ensure((size_t(nt) + 1) * sizeof(uint32_t)));
@@ -319,7 +328,7 @@ int run_batch(sr_ctx* ctx, const sr_dataset* ds, int opset_id, const sr_tree_bat
   if (use_hint) SR_HIP_CHECK(ctx->hint.ensure(size_t(nt) * sizeof(uint32_t) + 4));
   // dead-tree probe: the first kProbeTiles row tiles of the view, hints only (scratch partials)
   constexpr int kProbeTiles = 4;
-  const bool use_probe = use_hint && ctx->probe && n_rb >= 16;
+  const bool use_probe = use_hint && ctx->probe && n_rb >= 16;  // (per chunk: its grid has >= 16 row blocks)
   if (use_probe) {
     SR_HIP_CHECK(ctx->probe_sum.ensure(size_t(nt) * kProbeTiles * sizeof(double) + 8));
     SR_HIP_CHECK(ctx->probe_flag.ensure(size_t(nt) * kProbeTiles * sizeof(uint32_t) + 4));
@@ -385,15 +394,12 @@ int run_batch(sr_ctx* ctx, const sr_dataset* ds, int opset_id, const sr_tree_bat
     }
     if (c == 0) ctx->mark_phase(0);
     const int depth = pc.max_depth > 0 ? pc.max_depth : 1;
-    Grid g = make_grid<T>(n_eval, nc, R, W, int(ds->nf), depth, 0, ds->w != nullptr, ctx->tree_group,
-                         ctx->max_row_blocks);
-    if (g.lds > kLdsMax) {
-      sync_both();
-      return set_error(SR_ERR_TOO_DEEP, "the row tile (" + std::to_string(ds->nf) + " features, " +
-                                            std::to_string(depth) + " stack slots) needs " + std::to_string(g.lds) +
-                                            " bytes of LDS; the limit is 160 KiB");
-    }
-    glast = g;
+    // Trees whose programs fit the register stack (<= 2 slots: every tree of < 23 nodes, most of the
+    // rest) run on the register-stack kernel; the few deeper ones follow in a second launch of the
+    // LDS-stack kernel over the tail of the launch order.
+    int64_t n_vs = 0;  // launch positions [0, n_vs) -> register-stack kernel
+    if (Rv > 0)
+      for (int64_t i = 0; i < nc; ++i) n_vs += pc.depth[size_t(i)] <= 2 ? 1 : 0;
     // stage: code at code_base, offsets made absolute, static_bad, launch order (chunk-local)
     const size_t ncode = pc.code.size();
     if (code_base + ncode > code_cap) {
@@ -403,17 +409,23 @@ int run_batch(sr_ctx* ctx, const sr_dataset* ds, int opset_id, const sr_tree_bat
     if (ncode) std::memcpy(h_code + code_base, pc.code.data(), ncode * sizeof(SrIns<T>));
     for (int64_t i = 0; i <= nc; ++i) h_off[t0 + i] = code_base + pc.offsets[size_t(i)];
     std::memcpy(h_bad + t0, pc.static_bad.data(), size_t(nc));
-    for (int64_t i = 0; i < nc; ++i) h_perm[t0 + i] = uint32_t(i);
-    if (ctx->cost_order && nc > 1) {
-      // decreasing estimated cost, so every block's waves get similar work (counting sort: costs
-      // are small integers; ties keep tree order)
+    {
+      // launch order: register-stack trees first, each class in decreasing estimated cost so every
+      // block's waves get similar work (counting sort: costs are small integers; ties keep order)
       const std::vector<uint32_t>& cost = pc.cost;
+      const bool sort = ctx->cost_order && nc > 1;
       uint32_t cmax = 0;
-      for (uint32_t v : cost) cmax = v > cmax ? v : cmax;
-      std::vector<uint32_t> start(size_t(cmax) + 2, 0);
-      for (uint32_t v : cost) ++start[size_t(cmax - v) + 1];
+      if (sort)
+        for (uint32_t v : cost) cmax = v > cmax ? v : cmax;
+      const size_t nkey = size_t(cmax) + 1;
+      std::vector<uint32_t> start(2 * nkey + 1, 0);
+      auto key = [&](int64_t i) -> size_t {
+        const size_t cls = (Rv > 0 && pc.depth[size_t(i)] > 2) ? 1 : 0;
+        return cls * nkey + (sort ? size_t(cmax - cost[size_t(i)]) : 0);
+      };
+      for (int64_t i = 0; i < nc; ++i) ++start[key(i) + 1];
       for (size_t k = 1; k < start.size(); ++k) start[k] += start[k - 1];
-      for (int64_t i = 0; i < nc; ++i) h_perm[t0 + start[size_t(cmax - cost[size_t(i)])]++] = uint32_t(i);
+      for (int64_t i = 0; i < nc; ++i) h_perm[t0 + start[key(i)]++] = uint32_t(i);
     }
     if (ncode)
       SR_HIP_CHECK(hipMemcpyAsync(ctx->code.as<SrIns<T>>() + code_base, h_code + code_base, ncode * sizeof(SrIns<T>),
@@ -431,59 +443,75 @@ int run_batch(sr_ctx* ctx, const sr_dataset* ds, int opset_id, const sr_tree_bat
     prog->total_nodes += pc.total_nodes;
     prog->total_ops += pc.total_ops;
 
-    SrEvalArgs<T> a{};
-    a.code = ctx->code.as<SrIns<T>>();
-    a.offsets = ctx->offsets.as<uint32_t>() + t0;
-    a.perm = ctx->perm.as<uint32_t>() + t0;
-    a.hint = use_hint ? ctx->hint.as<uint32_t>() + t0 : nullptr;
-    a.n_trees = int(nc);
-    a.trees_per_block = g.G;
-    a.X = static_cast<const T*>(ds->X);
-    a.y = static_cast<const T*>(ds->y);
-    a.w = static_cast<const T*>(ds->w);
-    a.row_idx = gather ? ctx->row_idx.as<int64_t>() : nullptr;
-    a.ld = ds->ld;
-    a.n_rows = n_eval;
-    a.nf = int(ds->nf);
-    a.tiles_per_block = g.tiles;
-    a.n_row_blocks = g.n_row_blocks;
-    a.n_groups = g.n_groups;
-    a.stack_depth = depth;
-    // Σ over n_total rows of values below tbig cannot overflow T, even with rounding slack.
-    a.tbig = T(t_max<T>() / (2.0 * double(n_total > 0 ? n_total : 1)));
-    a.loss_kind = lkind;
-    a.loss_param = T(lparam);
-    a.part_sum = ctx->part_sum.as<double>() + size_t(n_rb) * size_t(t0);
-    a.part_flag = ctx->part_flag.as<uint32_t>() + size_t(n_rb) * size_t(t0);
-    a.pred = ctx->pred.as<T>();
-    a.pred_ld = n_eval;
-    a.scale = 1.0;
-    if (g.n_blocks > 0x7fffffff || g.n_row_blocks != n_rb) {
-      sync_both();
-      return set_error(SR_ERR_INVALID_ARG, "grid too large");
-    }
     SR_HIP_CHECK(hipEventRecord(ctx->ev_c0[c], cs));  // the chunk's kernel time includes its probe
-    if (use_probe && (ctx->probe != 2 || c > 0)) {
-      // Trees that are non-finite on the first rows are flagged before the main launch, so its
-      // workgroups skip them from their first tile (without the probe, the ~16 row blocks that
-      // start together evaluate every such tree in full before a hint exists).  Only hints come
-      // out of it: a tree non-finite on some rows of the view is incomplete on the whole view.
-      // a wide, short grid: 16 trees x 1 tile per workgroup, kProbeTiles row blocks
-      SrEvalArgs<T> pa = a;
-      pa.trees_per_block = std::max(16, g.W);
-      pa.n_groups = int((nc + pa.trees_per_block - 1) / pa.trees_per_block);
-      pa.tiles_per_block = 1;
-      pa.n_row_blocks = kProbeTiles;
-      pa.n_rows = std::min<int64_t>(n_eval, int64_t(kProbeTiles) * 64 * R);
-      pa.part_sum = ctx->probe_sum.as<double>();
-      pa.part_flag = ctx->probe_flag.as<uint32_t>();
-      SR_HIP_CHECK(sr_launch_eval<T>(pa, mode, gather, tier, ctx->rows_override, g.W,
-                                     pa.n_groups * kProbeTiles, cs));
+    // one launch over launch positions [p0, p0 + np) of the chunk; its partials occupy
+    // [n_rb][np] words from p0 * n_rb (the chunk's region holds n_rb rows for every position)
+    auto launch = [&](int64_t p0, int64_t np, bool vstk) -> int {
+      const int Rc = vstk ? Rv : R;
+      Grid g = make_grid<T>(n_eval, np, Rc, W, int(ds->nf), vstk ? 0 : depth, 0, ds->w != nullptr, ctx->tree_group,
+                           ctx->max_row_blocks);
+      if (g.lds > kLdsMax)
+        return set_error(SR_ERR_TOO_DEEP, "the row tile (" + std::to_string(ds->nf) + " features, " +
+                                              std::to_string(depth) + " stack slots) needs " + std::to_string(g.lds) +
+                                              " bytes of LDS; the limit is 160 KiB");
+      if (g.n_blocks > 0x7fffffff || g.n_row_blocks > n_rb) return set_error(SR_ERR_INVALID_ARG, "grid too large");
+      glast = g;
+      SrEvalArgs<T> a{};
+      a.code = ctx->code.as<SrIns<T>>();
+      a.offsets = ctx->offsets.as<uint32_t>() + t0;
+      a.perm = ctx->perm.as<uint32_t>() + t0 + p0;
+      a.hint = use_hint ? ctx->hint.as<uint32_t>() + t0 + p0 : nullptr;
+      a.n_trees = int(np);
+      a.trees_per_block = g.G;
+      a.X = static_cast<const T*>(ds->X);
+      a.y = static_cast<const T*>(ds->y);
+      a.w = static_cast<const T*>(ds->w);
+      a.row_idx = gather ? ctx->row_idx.as<int64_t>() : nullptr;
+      a.ld = ds->ld;
+      a.n_rows = n_eval;
+      a.nf = int(ds->nf);
+      a.tiles_per_block = g.tiles;
+      a.n_row_blocks = g.n_row_blocks;
+      a.n_groups = g.n_groups;
+      a.stack_depth = vstk ? std::min(depth, 2) : depth;  // (the register-stack trees need <= 2)
+      // Σ over n_total rows of values below tbig cannot overflow T, even with rounding slack.
+      a.tbig = T(t_max<T>() / (2.0 * double(n_total > 0 ? n_total : 1)));
+      a.loss_kind = lkind;
+      a.loss_param = T(lparam);
+      a.part_sum = ctx->part_sum.as<double>() + size_t(n_rb) * size_t(t0 + p0);
+      a.part_flag = ctx->part_flag.as<uint32_t>() + size_t(n_rb) * size_t(t0 + p0);
+      a.pred = ctx->pred.as<T>();
+      a.pred_ld = n_eval;
+      if (use_probe && p0 == 0 && g.n_row_blocks >= 16 && (ctx->probe != 2 || c > 0)) {
+        // Trees that are non-finite on the first rows are flagged before the main launch, so its
+        // workgroups skip them from their first tile (without the probe, the ~16 row blocks that
+        // start together evaluate every such tree in full before a hint exists).  Only hints come
+        // out of it: a tree non-finite on some rows of the view is incomplete on the whole view.
+        // a wide, short grid: 16 trees x 1 tile per workgroup, kProbeTiles row blocks
+        SrEvalArgs<T> pa = a;
+        pa.trees_per_block = std::max(16, g.W);
+        pa.n_groups = int((np + pa.trees_per_block - 1) / pa.trees_per_block);
+        pa.tiles_per_block = 1;
+        pa.n_row_blocks = kProbeTiles;
+        pa.n_rows = std::min<int64_t>(n_eval, int64_t(kProbeTiles) * 64 * Rc);
+        pa.part_sum = ctx->probe_sum.as<double>();
+        pa.part_flag = ctx->probe_flag.as<uint32_t>();
+        SR_HIP_CHECK(sr_launch_eval<T>(pa, mode, gather, tier, Rc, g.W, vstk, pa.n_groups * kProbeTiles, cs));
+      }
+      SR_HIP_CHECK(sr_launch_eval<T>(a, mode, gather, tier, Rc, g.W, vstk, int(g.n_blocks), cs));
+      SR_HIP_CHECK(sr_launch_reduce(a.part_sum, a.part_flag, int(np), g.n_row_blocks, a.perm,
+                                    ctx->static_bad.as<uint8_t>() + t0, ctx->out_sum.as<double>() + t0,
+                                    ctx->out_flag.as<uint32_t>() + t0, cs));
+      return SR_OK;
+    };
+    int lrc = SR_OK;
+    if (n_vs > 0) lrc = launch(0, n_vs, true);
+    if (lrc == SR_OK && n_vs < nc) lrc = launch(n_vs, nc - n_vs, false);
+    if (lrc != SR_OK) {
+      sync_both();
+      return lrc;
     }
-    SR_HIP_CHECK(sr_launch_eval<T>(a, mode, gather, tier, ctx->rows_override, g.W, int(g.n_blocks), cs));
     SR_HIP_CHECK(hipEventRecord(ctx->ev_c1[c], cs));
-    SR_HIP_CHECK(sr_launch_reduce(a.part_sum, a.part_flag, int(nc), n_rb, a.perm, ctx->static_bad.as<uint8_t>() + t0,
-                                  ctx->out_sum.as<double>() + t0, ctx->out_flag.as<uint32_t>() + t0, cs));
     ctx->n_chunks_last = c + 1;
     code_base += uint32_t(ncode);
   }
@@ -508,90 +536,203 @@ inline double chunk_kernel_ms(sr_ctx* ctx) {
   return ms;
 }
 
-// Exact isfinite(sum(array)) check of every CHECK node of the listed trees.  Writes this dataset
-// view's sums to host_sums[n_list][max_checks].
+// ---------------------------------------------------------------- Julia's pairwise `sum`
+// DynamicExpressions decides a checked array with isfinite(sum(x)); Base's `sum` over an Array runs
+// Base.mapreduce_impl: [lo, hi] splits at lo + (hi - lo) >> 1 until hi - lo < 1024
+// (pairwise_blocksize), each leaf block is folded sequentially (v = a[lo]; v = v + a[i]) in T, and
+// the halves are added back in the same recursion (arrays of < 16 elements: one sequential fold,
+// which is the same thing).  The kernel's EXACT mode computes the leaf folds over row ranges; the
+// host adds them in recursion order.  Row sharding: the global leaves are intersected with each
+// shard; a leaf that starts in an earlier shard is carried by its first shard's prefix fold and
+// continued, row by row, with this shard's values ("head" ranges of one row each).
+struct JlRange {
+  int64_t lo, hi;  // local rows of this view / shard (inclusive)
+  int64_t leaf;    // global leaf index
+  bool head;       // a single row continuing a leaf that starts in an earlier shard
+};
+
+std::vector<std::pair<int64_t, int64_t>> jl_leaves(int64_t n) {
+  std::vector<std::pair<int64_t, int64_t>> out, st;
+  if (n <= 0) return out;
+  st.push_back({0, n - 1});
+  while (!st.empty()) {
+    const auto [lo, hi] = st.back();
+    st.pop_back();
+    if (hi - lo < 1024) {
+      out.push_back({lo, hi});
+    } else {
+      const int64_t mid = lo + ((hi - lo) >> 1);
+      st.push_back({mid + 1, hi});
+      st.push_back({lo, mid});
+    }
+  }
+  return out;
+}
+
+// The ranges a shard holding global rows [off, off + n) of n_total sums (in this order).
+std::vector<JlRange> jl_ranges(int64_t off, int64_t n, int64_t n_total) {
+  std::vector<JlRange> out;
+  const auto leaves = jl_leaves(n_total);
+  const int64_t last = off + n - 1;
+  for (size_t k = 0; k < leaves.size(); ++k) {
+    const auto [L, H] = leaves[k];
+    if (H < off || L > last) continue;
+    const int64_t h = H < last ? H : last;
+    if (L >= off) {
+      out.push_back({L - off, h - off, int64_t(k), false});
+    } else {
+      for (int64_t r = off; r <= h; ++r) out.push_back({r - off, r - off, int64_t(k), true});
+    }
+  }
+  return out;
+}
+
+template <typename T>
+T jl_reduce(const std::vector<T>& leafval, int64_t lo, int64_t hi, size_t* idx) {
+  if (hi - lo < 1024) return leafval[(*idx)++];
+  const int64_t mid = lo + ((hi - lo) >> 1);
+  const T a = jl_reduce<T>(leafval, lo, mid, idx);
+  const T b = jl_reduce<T>(leafval, mid + 1, hi, idx);
+  return a + b;
+}
+
+// isfinite(Julia sum) of n_arrays arrays of n_total rows from every shard's range folds:
+// rank_vals[r] = [n_arrays][ranges of shard r] (T), shards r = [offs[r], offs[r + 1]).
+template <typename T>
+void jl_finite(int64_t n_total, int n_ranks, const int64_t* offs, const T* const* rank_vals, int64_t n_arrays,
+               uint8_t* out_finite) {
+  const size_t n_leaves = jl_leaves(n_total).size();
+  std::vector<std::vector<JlRange>> ranges(static_cast<size_t>(n_ranks));
+  for (int r = 0; r < n_ranks; ++r) ranges[size_t(r)] = jl_ranges(offs[r], offs[r + 1] - offs[r], n_total);
+  std::vector<T> leafval(n_leaves);
+  for (int64_t a = 0; a < n_arrays; ++a) {
+    for (int r = 0; r < n_ranks; ++r) {
+      const std::vector<JlRange>& rg = ranges[size_t(r)];
+      const T* v = rank_vals[r] + size_t(a) * rg.size();
+      for (size_t i = 0; i < rg.size(); ++i) {
+        T& dst = leafval[size_t(rg[i].leaf)];
+        dst = rg[i].head ? T(dst + v[i]) : v[i];
+      }
+    }
+    size_t idx = 0;
+    const T sum = n_total > 0 ? jl_reduce<T>(leafval, 0, n_total - 1, &idx) : T(0);
+    out_finite[a] = std::isfinite(sum) ? 1 : 0;
+  }
+}
+
+// EXACT pass: the Julia-order fold of every checked array of the listed trees over `ranges` of this
+// view -> host_vals[n_list][max_checks][ranges] (T; a tree's unused check slots hold 0).
 template <typename T>
 int run_exact(sr_ctx* ctx, const sr_dataset* ds, const SrProgramBatch<T>& prog, const int64_t* row_idx,
-              int64_t n_idx, const int64_t* list, int64_t n_list, int max_checks, double* host_sums) {
-  if (n_list == 0 || max_checks == 0) return SR_OK;
+              int64_t n_idx, const int64_t* list, int64_t n_list, int max_checks, const std::vector<JlRange>& ranges,
+              T* host_vals) {
+  if (n_list == 0 || max_checks == 0 || ranges.empty()) return SR_OK;
   const bool gather = row_idx != nullptr && n_idx > 0;
   const int64_t n_eval = gather ? n_idx : ds->n;
   hipStream_t s = ctx->stream;
   const int depth = prog.max_depth > 0 ? prog.max_depth : 1;
-  // several listed trees per workgroup share one staged row tile (the heuristic G: >= 4096 workgroups)
-  Grid g = make_grid<T>(n_eval, n_list, sr_rows_per_lane<T>(SR_MODE_EXACT, SR_TIER_FULL, 0), 4, int(ds->nf), depth,
-                        max_checks, ds->w != nullptr, 0, ctx->max_row_blocks);
-  if (g.lds > kLdsMax)  // many checks: one tree per workgroup
-    g = make_grid<T>(n_eval, n_list, sr_rows_per_lane<T>(SR_MODE_EXACT, SR_TIER_FULL, 0), 4, int(ds->nf), depth,
-                     max_checks, ds->w != nullptr, 1, ctx->max_row_blocks);
-  if (g.lds > kLdsMax) return set_error(SR_ERR_TOO_DEEP, "exact-sum pass needs more LDS than 160 KiB");
-  std::vector<uint32_t> list32(static_cast<size_t>(n_list));
-  for (int64_t i = 0; i < n_list; ++i) list32[size_t(i)] = uint32_t(list[i]);
-  SR_HIP_CHECK(ctx->tree_list.ensure(size_t(n_list) * sizeof(uint32_t)));
-  SR_HIP_CHECK(ctx->check_sums.ensure(size_t(n_list) * max_checks * sizeof(double)));
-  SR_HIP_CHECK(hipMemcpyAsync(ctx->tree_list.p, list32.data(), size_t(n_list) * sizeof(uint32_t),
-                              hipMemcpyHostToDevice, s));
-  SR_HIP_CHECK(hipMemsetAsync(ctx->check_sums.p, 0, size_t(n_list) * max_checks * sizeof(double), s));
-  SR_HIP_CHECK(ctx->part_sum.ensure(size_t(g.n_row_blocks) * sizeof(double) * size_t(n_list)));
-  SR_HIP_CHECK(ctx->part_flag.ensure(size_t(g.n_row_blocks) * sizeof(uint32_t) * size_t(n_list)));
-  SrEvalArgs<T> a{};
-  a.code = ctx->code.as<SrIns<T>>();
-  a.offsets = ctx->offsets.as<uint32_t>();
-  a.n_trees = int(n_list);
-  a.trees_per_block = g.G;
-  a.X = static_cast<const T*>(ds->X);
-  a.y = static_cast<const T*>(ds->y);
-  a.w = static_cast<const T*>(ds->w);
-  a.row_idx = gather ? ctx->row_idx.as<int64_t>() : nullptr;
-  a.ld = ds->ld;
-  a.n_rows = n_eval;
-  a.nf = int(ds->nf);
-  a.tiles_per_block = g.tiles;
-  a.n_row_blocks = g.n_row_blocks;
-  a.n_groups = g.n_groups;
-  a.stack_depth = depth;
-  a.tbig = T(0);
-  a.part_sum = ctx->part_sum.as<double>();
-  a.part_flag = ctx->part_flag.as<uint32_t>();
-  a.perm = ctx->tree_list.as<uint32_t>();
-  a.max_checks = max_checks;
-  a.check_sums = ctx->check_sums.as<double>();
-  // f64 sums can overflow f64 itself: scale by 2^-64 (the threshold is scaled identically)
-  a.scale = sizeof(T) == 8 ? std::ldexp(1.0, -64) : 1.0;
-  const int64_t blocks = g.n_blocks;
-  if (blocks > 0x7fffffff) return set_error(SR_ERR_INVALID_ARG, "grid too large");
-  SR_HIP_CHECK(sr_launch_eval<T>(a, SR_MODE_EXACT, gather, SR_TIER_FULL, 0, 4, int(blocks), s));
-  SR_HIP_CHECK(hipMemcpyAsync(host_sums, ctx->check_sums.p, size_t(n_list) * max_checks * sizeof(double),
-                              hipMemcpyDeviceToHost, s));
-  SR_HIP_CHECK(hipStreamSynchronize(s));
+  const int R = sr_rows_per_lane<T>(SR_MODE_EXACT, SR_TIER_FULL, 0);
+  const int64_t rows = 64 * int64_t(R);
+  const int64_t n_ranges = int64_t(ranges.size());
+  int64_t max_len = 1;
+  std::vector<int64_t> lo(static_cast<size_t>(n_ranges)), hi(static_cast<size_t>(n_ranges));
+  for (int64_t i = 0; i < n_ranges; ++i) {
+    lo[size_t(i)] = ranges[size_t(i)].lo;
+    hi[size_t(i)] = ranges[size_t(i)].hi;
+    if (hi[size_t(i)] < lo[size_t(i)] || hi[size_t(i)] >= n_eval) return set_error(SR_ERR_INVALID_ARG, "bad row range");
+    max_len = std::max(max_len, hi[size_t(i)] - lo[size_t(i)] + 1);
+  }
+  SR_HIP_CHECK(ctx->range_lo.ensure(size_t(n_ranges) * sizeof(int64_t)));
+  SR_HIP_CHECK(ctx->range_hi.ensure(size_t(n_ranges) * sizeof(int64_t)));
+  SR_HIP_CHECK(hipMemcpyAsync(ctx->range_lo.p, lo.data(), size_t(n_ranges) * sizeof(int64_t), hipMemcpyHostToDevice, s));
+  SR_HIP_CHECK(hipMemcpyAsync(ctx->range_hi.p, hi.data(), size_t(n_ranges) * sizeof(int64_t), hipMemcpyHostToDevice, s));
+  // listed trees in batches whose range folds fit a bounded scratch buffer
+  const size_t per_tree = size_t(max_checks) * size_t(n_ranges) * sizeof(T);
+  const int64_t batch = std::max<int64_t>(1, int64_t((size_t(256) << 20) / per_tree));
+  for (int64_t b0 = 0; b0 < n_list; b0 += batch) {
+    const int64_t nb = std::min(batch, n_list - b0);
+    // one wave per workgroup, G listed trees per workgroup (LDS: X tile + one wave's checked
+    // values [max_checks][rows] + running sums [G][max_checks])
+    int G = int(std::min<int64_t>(nb, 16));
+    size_t lds = 0;
+    for (;;) {
+      lds = sr_tile_lds_bytes(int(sizeof(T)), int(ds->nf), R, depth, G, max_checks, 1, false);
+      if (lds <= kLdsMax || G == 1) break;
+      G /= 2;
+    }
+    if (lds > kLdsMax) return set_error(SR_ERR_TOO_DEEP, "exact-sum pass needs more LDS than 160 KiB");
+    std::vector<uint32_t> list32(static_cast<size_t>(nb));
+    for (int64_t i = 0; i < nb; ++i) list32[size_t(i)] = uint32_t(list[b0 + i]);
+    SR_HIP_CHECK(ctx->tree_list.ensure(size_t(nb) * sizeof(uint32_t)));
+    SR_HIP_CHECK(hipMemcpyAsync(ctx->tree_list.p, list32.data(), size_t(nb) * sizeof(uint32_t), hipMemcpyHostToDevice, s));
+    SR_HIP_CHECK(ctx->range_sums.ensure(size_t(nb) * per_tree));
+    SrEvalArgs<T> a{};
+    a.code = ctx->code.as<SrIns<T>>();
+    a.offsets = ctx->offsets.as<uint32_t>();
+    a.perm = ctx->tree_list.as<uint32_t>();
+    a.n_trees = int(nb);
+    a.trees_per_block = G;
+    a.X = static_cast<const T*>(ds->X);
+    a.row_idx = gather ? ctx->row_idx.as<int64_t>() : nullptr;
+    a.ld = ds->ld;
+    a.n_rows = n_eval;
+    a.nf = int(ds->nf);
+    a.tiles_per_block = int((max_len + rows - 1) / rows);
+    a.n_row_blocks = int(n_ranges);
+    a.n_groups = int((nb + G - 1) / G);
+    a.stack_depth = depth;
+    a.tbig = T(0);
+    a.max_checks = max_checks;
+    a.range_lo = ctx->range_lo.as<int64_t>();
+    a.range_hi = ctx->range_hi.as<int64_t>();
+    a.range_sums = ctx->range_sums.p;
+    const int64_t blocks = int64_t(a.n_groups) * n_ranges;
+    if (blocks > 0x7fffffff) return set_error(SR_ERR_INVALID_ARG, "grid too large");
+    SR_HIP_CHECK(sr_launch_eval<T>(a, SR_MODE_EXACT, gather, SR_TIER_FULL, R, 1, false, int(blocks), s));
+    SR_HIP_CHECK(hipMemcpyAsync(host_vals + size_t(b0) * max_checks * size_t(n_ranges), ctx->range_sums.p,
+                                size_t(nb) * per_tree, hipMemcpyDeviceToHost, s));
+    SR_HIP_CHECK(hipStreamSynchronize(s));
+  }
   return SR_OK;
 }
 
+// EXACT pass over the whole view on this GPU -> list_ok[i] = every checked array of tree list[i]
+// passes isfinite(Julia sum).
 template <typename T>
-double exact_threshold() {
-  return sizeof(T) == 8 ? std::ldexp(t_max<T>(), -64) : t_max<T>();
+int exact_list_ok(sr_ctx* ctx, const sr_dataset* ds, const SrProgramBatch<T>& prog, const int64_t* row_idx,
+                  int64_t n_idx, const std::vector<int64_t>& list, std::vector<uint8_t>* list_ok) {
+  list_ok->assign(list.size(), 1);
+  if (list.empty() || prog.max_checks == 0) return SR_OK;
+  const bool gather = row_idx != nullptr && n_idx > 0;
+  const int64_t n_eval = gather ? n_idx : ds->n;
+  const std::vector<JlRange> ranges = jl_ranges(0, n_eval, n_eval);
+  const int mc = prog.max_checks;
+  std::vector<T> vals(list.size() * size_t(mc) * ranges.size());
+  int rc = run_exact<T>(ctx, ds, prog, row_idx, n_idx, list.data(), int64_t(list.size()), mc, ranges, vals.data());
+  if (rc != SR_OK) return rc;
+  std::vector<uint8_t> fin(list.size() * size_t(mc));
+  const int64_t offs[2] = {0, n_eval};
+  const T* pv = vals.data();
+  jl_finite<T>(n_eval, 1, offs, &pv, int64_t(fin.size()), fin.data());
+  for (size_t i = 0; i < list.size(); ++i)
+    for (int k = 0; k < mc; ++k) (*list_ok)[i] &= fin[i * size_t(mc) + size_t(k)];
+  return SR_OK;
 }
 
-// Finalize one tree: complete unless flagged; BIG-only trees look up their exact check sums.
+// Finalize one tree: complete unless flagged; BIG-only trees take their exact verdict (list_ok).
 template <typename T>
 void finalize(int64_t nt, const double* sums, const uint32_t* flags, double denom, const int64_t* list,
-              int64_t n_list, int max_checks, const double* check_sums, T* out_loss, uint8_t* out_complete) {
+              int64_t n_list, const uint8_t* list_ok, T* out_loss, uint8_t* out_complete) {
   std::vector<int64_t> pos;
   if (n_list > 0) {
     pos.assign(size_t(nt), -1);
     for (int64_t i = 0; i < n_list; ++i) pos[size_t(list[i])] = i;
   }
-  const double thr = exact_threshold<T>();
   for (int64_t t = 0; t < nt; ++t) {
     bool ok = (flags[t] & (SR_FLAG_NONFINITE | SR_FLAG_STATIC)) == 0;
     if (ok && (flags[t] & SR_FLAG_BIG)) {
       const int64_t p = pos.empty() ? -1 : pos[size_t(t)];
-      if (p >= 0 && check_sums) {
-        for (int k = 0; k < max_checks; ++k) {
-          const double v = check_sums[size_t(p) * max_checks + k];
-          if (!(std::fabs(v) <= thr)) ok = false;
-        }
-      }
+      if (p >= 0 && list_ok && !list_ok[p]) ok = false;
     }
     out_complete[t] = ok ? 1 : 0;
     out_loss[t] = ok ? T(sums[t] / denom) : T(INFINITY);
@@ -634,17 +775,13 @@ int eval_loss_impl(sr_ctx* ctx, const sr_dataset* ds, int opset_id, const sr_tre
   std::vector<int64_t> list;
   for (int64_t t = 0; t < nt; ++t)
     if ((flags[t] & (SR_FLAG_NONFINITE | SR_FLAG_STATIC)) == 0 && (flags[t] & SR_FLAG_BIG)) list.push_back(t);
-  std::vector<double> check_sums;
-  if (!list.empty()) {
-    check_sums.assign(list.size() * size_t(prog.max_checks), 0.0);
-    rc = run_exact<T>(ctx, ds, prog, row_idx, n_idx, list.data(), int64_t(list.size()), prog.max_checks,
-                      check_sums.data());
-    if (rc != SR_OK) return rc;
-  }
+  std::vector<uint8_t> list_ok;
+  rc = exact_list_ok<T>(ctx, ds, prog, row_idx, n_idx, list, &list_ok);
+  if (rc != SR_OK) return rc;
   ctx->mark_phase(3);
   const double denom = view_denominator<T>(ds, row_idx, n_idx);
-  finalize<T>(nt, sums.data(), flags.data(), denom, list.data(), int64_t(list.size()), prog.max_checks,
-              check_sums.empty() ? nullptr : check_sums.data(), static_cast<T*>(out_loss), out_complete);
+  finalize<T>(nt, sums.data(), flags.data(), denom, list.data(), int64_t(list.size()), list_ok.data(),
+              static_cast<T*>(out_loss), out_complete);
   ctx->mark_phase(4);
   auto t1 = std::chrono::steady_clock::now();
   ctx->last_total_ms = std::chrono::duration<double, std::milli>(t1 - t0).count();
@@ -673,16 +810,12 @@ int eval_pred_impl(sr_ctx* ctx, const sr_dataset* ds, int opset_id, const sr_tre
   std::vector<int64_t> list;
   for (int64_t t = 0; t < nt; ++t)
     if ((flags[t] & (SR_FLAG_NONFINITE | SR_FLAG_STATIC)) == 0 && (flags[t] & SR_FLAG_BIG)) list.push_back(t);
-  std::vector<double> check_sums;
-  if (!list.empty()) {
-    check_sums.assign(list.size() * size_t(prog.max_checks), 0.0);
-    rc = run_exact<T>(ctx, ds, prog, row_idx, n_idx, list.data(), int64_t(list.size()), prog.max_checks,
-                      check_sums.data());
-    if (rc != SR_OK) return rc;
-  }
+  std::vector<uint8_t> list_ok;
+  rc = exact_list_ok<T>(ctx, ds, prog, row_idx, n_idx, list, &list_ok);
+  if (rc != SR_OK) return rc;
   std::vector<T> dummy(static_cast<size_t>(nt));
-  finalize<T>(nt, sums.data(), flags.data(), 1.0, list.data(), int64_t(list.size()), prog.max_checks,
-              check_sums.empty() ? nullptr : check_sums.data(), dummy.data(), out_complete);
+  finalize<T>(nt, sums.data(), flags.data(), 1.0, list.data(), int64_t(list.size()), list_ok.data(), dummy.data(),
+              out_complete);
   // statically incomplete trees have no program: fill their rows with NaN
   T* p = static_cast<T*>(out_pred);
   for (int64_t t = 0; t < nt; ++t)
@@ -948,7 +1081,7 @@ int sr_shutdown(sr_ctx* ctx) {
     (void)hipSetDevice(ctx->device);
     (void)hipStreamSynchronize(ctx->stream);
     for (DevBuf* b : {&ctx->code, &ctx->offsets, &ctx->static_bad, &ctx->part_sum, &ctx->part_flag, &ctx->out_sum,
-                      &ctx->out_flag, &ctx->pred, &ctx->row_idx, &ctx->tree_list, &ctx->check_sums,
+                      &ctx->out_flag, &ctx->pred, &ctx->row_idx, &ctx->tree_list, &ctx->range_lo, &ctx->range_hi, &ctx->range_sums, &ctx->packed,
                       &ctx->perm, &ctx->hint, &ctx->probe_sum, &ctx->probe_flag, &ctx->g_code, &ctx->g_offsets, &ctx->g_consts, &ctx->g_const_off,
                       &ctx->g_items, &ctx->g_part, &ctx->g_out})
       b->release();
@@ -1102,6 +1235,40 @@ int sr_eval_loss_partials(sr_ctx* ctx, const sr_dataset* ds, int opset_id, const
   return SR_OK;
 }
 
+int sr_eval_loss_partials_packed(sr_ctx* ctx, const sr_dataset* ds, int opset_id, const sr_tree_batch* trees,
+                                 int64_t n_total, int loss_kind, double* out, int out_on_device) {
+  int rc = validate_common(ctx, ds, opset_id, trees);
+  if (rc != SR_OK) return rc;
+  const int64_t nt = trees->n_trees;
+  if (nt > 0 && !out) return set_error(SR_ERR_INVALID_ARG, "NULL output buffer");
+  if (n_total < ds->n) return set_error(SR_ERR_INVALID_ARG, "n_total smaller than this shard");
+  Lock l(ctx);
+  SR_HIP_CHECK(hipSetDevice(ctx->device));
+  Grid g;
+  auto t0 = std::chrono::steady_clock::now();
+  if (ds->dtype == SR_DTYPE_F32) {
+    SrProgramBatch<float> prog;
+    rc = run_batch<float>(ctx, ds, opset_id, trees, nullptr, 0, n_total, loss_kind, SR_MODE_LOSS, &prog, &g);
+  } else {
+    SrProgramBatch<double> prog;
+    rc = run_batch<double>(ctx, ds, opset_id, trees, nullptr, 0, n_total, loss_kind, SR_MODE_LOSS, &prog, &g);
+  }
+  if (rc != SR_OK || nt == 0) return rc;
+  hipStream_t s = ctx->stream;
+  const size_t bytes = size_t(4) * size_t(nt) * sizeof(double);
+  double* dst = out;
+  if (!out_on_device) {
+    SR_HIP_CHECK(ctx->packed.ensure(bytes));
+    dst = ctx->packed.as<double>();
+  }
+  SR_HIP_CHECK(sr_launch_pack_partials(ctx->out_sum.as<double>(), ctx->out_flag.as<uint32_t>(), int(nt), dst, s));
+  if (!out_on_device) SR_HIP_CHECK(hipMemcpyAsync(out, dst, bytes, hipMemcpyDeviceToHost, s));
+  SR_HIP_CHECK(hipStreamSynchronize(s));
+  ctx->last_eval_ms = chunk_kernel_ms(ctx);
+  ctx->last_total_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+  return SR_OK;
+}
+
 int sr_max_checks(sr_ctx* ctx, int opset_id, const sr_tree_batch* trees, int* max_checks) {
   if (check_ctx(ctx) != SR_OK) return SR_ERR_INVALID_ARG;
   if (!trees || !max_checks || opset_id < 0 || opset_id >= int(ctx->opsets.size()))
@@ -1114,46 +1281,83 @@ int sr_max_checks(sr_ctx* ctx, int opset_id, const sr_tree_batch* trees, int* ma
   return SR_OK;
 }
 
-int sr_exact_check_partials(sr_ctx* ctx, const sr_dataset* ds, int opset_id, const sr_tree_batch* trees,
-                            const int64_t* tree_list, int64_t n_list, int max_checks, double* out_sums) {
+int sr_jsum_range_count(int64_t row_offset, int64_t n_local, int64_t n_total, int64_t* out_n_ranges) {
+  if (!out_n_ranges || row_offset < 0 || n_local < 1 || row_offset + n_local > n_total)
+    return set_error(SR_ERR_INVALID_ARG, "bad shard bounds");
+  *out_n_ranges = int64_t(jl_ranges(row_offset, n_local, n_total).size());
+  return SR_OK;
+}
+
+int sr_jsum_ranges(int64_t row_offset, int64_t n_local, int64_t n_total, int64_t* lo, int64_t* hi, int64_t* leaf,
+                   uint8_t* head) {
+  if (row_offset < 0 || n_local < 1 || row_offset + n_local > n_total) return set_error(SR_ERR_INVALID_ARG, "bad shard bounds");
+  const std::vector<JlRange> r = jl_ranges(row_offset, n_local, n_total);
+  for (size_t i = 0; i < r.size(); ++i) {
+    if (lo) lo[i] = r[i].lo;
+    if (hi) hi[i] = r[i].hi;
+    if (leaf) leaf[i] = r[i].leaf;
+    if (head) head[i] = r[i].head ? 1 : 0;
+  }
+  return SR_OK;
+}
+
+int sr_jsum_partials(sr_ctx* ctx, const sr_dataset* ds, int opset_id, const sr_tree_batch* trees,
+                     const int64_t* tree_list, int64_t n_list, int max_checks, int64_t row_offset, int64_t n_total,
+                     void* out_vals) {
   int rc = validate_common(ctx, ds, opset_id, trees);
   if (rc != SR_OK) return rc;
-  if (n_list < 0 || (n_list > 0 && (!tree_list || !out_sums)) || max_checks < 0)
+  if (n_list < 0 || (n_list > 0 && (!tree_list || !out_vals)) || max_checks < 0)
     return set_error(SR_ERR_INVALID_ARG, "bad tree list");
+  if (row_offset < 0 || row_offset + ds->n > n_total) return set_error(SR_ERR_INVALID_ARG, "bad shard bounds");
   for (int64_t i = 0; i < n_list; ++i)
     if (tree_list[i] < 0 || tree_list[i] >= trees->n_trees) return set_error(SR_ERR_INVALID_ARG, "tree index out of range");
-  if (n_list == 0) return SR_OK;
+  if (n_list == 0 || max_checks == 0) return SR_OK;
   Lock l(ctx);
   SR_HIP_CHECK(hipSetDevice(ctx->device));
   Grid g;
-  if (ds->dtype == SR_DTYPE_F32) {
-    SrProgramBatch<float> prog;
-    rc = run_batch<float>(ctx, ds, opset_id, trees, nullptr, 0, ds->n, SR_LOSS_L2DIST, SR_MODE_LOSS, &prog, &g);
-    if (rc != SR_OK) return rc;
+  const std::vector<JlRange> ranges = jl_ranges(row_offset, ds->n, n_total);
+  auto go = [&](auto tag) -> int {
+    using T = decltype(tag);
+    SrProgramBatch<T> prog;
+    int r = run_batch<T>(ctx, ds, opset_id, trees, nullptr, 0, n_total, SR_LOSS_L2DIST, SR_MODE_LOSS, &prog, &g);
+    if (r != SR_OK) return r;
+    SR_HIP_CHECK(hipStreamSynchronize(ctx->stream));
     if (prog.max_checks > max_checks) return set_error(SR_ERR_INVALID_ARG, "max_checks too small");
-    return run_exact<float>(ctx, ds, prog, nullptr, 0, tree_list, n_list, max_checks, out_sums);
-  }
-  SrProgramBatch<double> prog;
-  rc = run_batch<double>(ctx, ds, opset_id, trees, nullptr, 0, ds->n, SR_LOSS_L2DIST, SR_MODE_LOSS, &prog, &g);
-  if (rc != SR_OK) return rc;
-  if (prog.max_checks > max_checks) return set_error(SR_ERR_INVALID_ARG, "max_checks too small");
-  return run_exact<double>(ctx, ds, prog, nullptr, 0, tree_list, n_list, max_checks, out_sums);
+    return run_exact<T>(ctx, ds, prog, nullptr, 0, tree_list, n_list, max_checks, ranges, static_cast<T*>(out_vals));
+  };
+  return ds->dtype == SR_DTYPE_F32 ? go(float{}) : go(double{});
+}
+
+int sr_jsum_finite(int dtype, int64_t n_total, int n_ranks, const int64_t* row_offsets, const void* const* rank_vals,
+                   int64_t n_arrays, uint8_t* out_finite) {
+  if (n_total < 1 || n_ranks < 1 || !row_offsets || !rank_vals || n_arrays < 0 || (n_arrays > 0 && !out_finite))
+    return set_error(SR_ERR_INVALID_ARG, "bad arguments");
+  if (row_offsets[0] != 0 || row_offsets[n_ranks] != n_total) return set_error(SR_ERR_INVALID_ARG, "shards must cover [0, n_total)");
+  for (int r = 0; r < n_ranks; ++r)
+    if (row_offsets[r + 1] <= row_offsets[r] || !rank_vals[r]) return set_error(SR_ERR_INVALID_ARG, "bad shard bounds");
+  if (dtype == SR_DTYPE_F32)
+    jl_finite<float>(n_total, n_ranks, row_offsets, reinterpret_cast<const float* const*>(rank_vals), n_arrays, out_finite);
+  else if (dtype == SR_DTYPE_F64)
+    jl_finite<double>(n_total, n_ranks, row_offsets, reinterpret_cast<const double* const*>(rank_vals), n_arrays,
+                      out_finite);
+  else
+    return set_error(SR_ERR_INVALID_ARG, "unknown dtype");
+  return SR_OK;
 }
 
 int sr_finalize_losses(int dtype, int64_t n_trees, const double* sums, const uint32_t* flags, double denom,
-                       const int64_t* tree_list, int64_t n_list, int max_checks, const double* check_sums,
-                       void* out_loss, uint8_t* out_complete) {
+                       const int64_t* tree_list, int64_t n_list, const uint8_t* list_ok, void* out_loss,
+                       uint8_t* out_complete) {
   if (n_trees < 0 || (n_trees > 0 && (!sums || !flags || !out_loss || !out_complete)))
     return set_error(SR_ERR_INVALID_ARG, "bad arguments");
-  if (n_list > 0 && !tree_list) return set_error(SR_ERR_INVALID_ARG, "NULL tree list");
+  if (n_list > 0 && (!tree_list || !list_ok)) return set_error(SR_ERR_INVALID_ARG, "NULL tree list");
   for (int64_t i = 0; i < n_list; ++i)
     if (tree_list[i] < 0 || tree_list[i] >= n_trees) return set_error(SR_ERR_INVALID_ARG, "tree index out of range");
   if (dtype == SR_DTYPE_F32)
-    finalize<float>(n_trees, sums, flags, denom, tree_list, n_list, max_checks, check_sums,
-                    static_cast<float*>(out_loss), out_complete);
+    finalize<float>(n_trees, sums, flags, denom, tree_list, n_list, list_ok, static_cast<float*>(out_loss), out_complete);
   else if (dtype == SR_DTYPE_F64)
-    finalize<double>(n_trees, sums, flags, denom, tree_list, n_list, max_checks, check_sums,
-                     static_cast<double*>(out_loss), out_complete);
+    finalize<double>(n_trees, sums, flags, denom, tree_list, n_list, list_ok, static_cast<double*>(out_loss),
+                     out_complete);
   else
     return set_error(SR_ERR_INVALID_ARG, "unknown dtype");
   return SR_OK;

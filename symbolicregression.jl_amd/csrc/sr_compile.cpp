@@ -660,6 +660,7 @@ int sr_compile_batch(const sr_tree_batch& trees, const SrOpset& ops, int64_t n_r
   out->n_consts.assign(size_t(nt), 0);
   out->const_off.assign(size_t(nt + 1), 0);
   out->cost.assign(size_t(nt), 0);
+  out->depth.assign(size_t(nt), 0);
   out->max_depth = 0;
   out->max_checks = 0;
   out->total_nodes = 0;
@@ -675,6 +676,7 @@ int sr_compile_batch(const sr_tree_batch& trees, const SrOpset& ops, int64_t n_r
     at += p.len;
     out->static_bad[k] = p.bad;
     out->cost[k] = p.bad ? 0u : p.cost;
+    out->depth[k] = uint8_t(p.bad ? 0 : (p.depth > 255 ? 255 : p.depth));
     out->n_checks[k] = p.checks;
     out->n_consts[k] = p.consts;
     out->const_off[k + 1] = out->const_off[k] + p.consts;

@@ -37,6 +37,7 @@ struct SrProgramBatch {
   std::vector<uint32_t> n_consts;   // constants per tree (pre-order, for gradients)
   std::vector<uint32_t> const_off;  // [n_trees + 1] prefix sum of n_consts
   std::vector<uint32_t> cost;       // estimated device cost per tree (launch ordering / balancing)
+  std::vector<uint8_t> depth;       // operand-stack slots each tree needs
   int max_depth = 0;                // operand-stack slots needed (below top-of-stack)
   int max_checks = 0;
   int64_t total_nodes = 0;          // Σ count_nodes (metric unit)

@@ -37,13 +37,15 @@ struct SrEvalArgs {
   uint32_t* part_flag;         // [n_row_blocks][n_trees], per launch position
   T* pred;                     // PRED: [n_trees][pred_ld]
   int64_t pred_ld;
-  // EXACT mode (perm = listed trees; check_sums row = position in the list)
+  // EXACT mode (perm = listed trees): row block rb = row range [range_lo[rb], range_hi[rb]] of the
+  // view; range_sums[list position][check][rb] (T) = Julia-order sum of the checked array over it
   int max_checks;
-  double* check_sums;          // [n_list][max_checks]
-  double scale;
+  const int64_t* range_lo;
+  const int64_t* range_hi;
+  void* range_sums;
 };
 
-template <typename T, int R, int MODE, bool GATHER, int TIER, int W = 4, int LK = -1>
+template <typename T, int R, int MODE, bool GATHER, int TIER, int W = 4, int LK = -1, bool VSTK = false>
 hipError_t sr_launch_tile(const SrEvalArgs<T>& a, int n_blocks, hipStream_t s);
 // LDS bytes one workgroup (W waves) of the tile kernel needs.
 size_t sr_tile_lds_bytes(int elem_size, int nf, int rows_per_lane, int stack_depth, int trees_per_block,
@@ -53,13 +55,17 @@ int sr_waves_per_block(int elem_size, int mode, int tier, int rows_per_lane, int
 // Rows per lane the dispatcher uses for (mode, tier); `requested` 4 selects the f32 BASIC tuning kernel.
 template <typename T>
 int sr_rows_per_lane(int mode, int tier, int requested);
-// Runtime dispatch over the instantiated kernels.
+// Rows per lane of the register-stack f32 BASIC loss kernel for n rows (0: use the LDS-stack kernel).
+int sr_vstk_rows(int64_t n_rows, int requested);
+// Runtime dispatch over the instantiated kernels: R rows per lane (sr_rows_per_lane, or
+// sr_vstk_rows with vstk = true: operand stack in VGPRs, programs of <= 2 stack slots).
 template <typename T>
-hipError_t sr_launch_eval(const SrEvalArgs<T>& a, int mode, bool gather, int tier, int rows_per_lane, int waves,
+hipError_t sr_launch_eval(const SrEvalArgs<T>& a, int mode, bool gather, int tier, int R, int waves, bool vstk,
                           int n_blocks, hipStream_t s);
 hipError_t sr_launch_reduce(const double* part_sum, const uint32_t* part_flag, int n_trees, int n_row_blocks,
                             const uint32_t* perm, const uint8_t* static_bad, double* out_sum, uint32_t* out_flag,
                             hipStream_t s);
+hipError_t sr_launch_pack_partials(const double* sum, const uint32_t* flag, int n, double* out, hipStream_t s);
 template <typename T>
 hipError_t sr_launch_transpose(const T* Xh_dev, int64_t nf, int64_t n, int64_t ld, T* Xd, hipStream_t s);
 template <typename T>

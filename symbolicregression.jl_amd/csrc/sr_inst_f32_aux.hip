@@ -1,6 +1,6 @@
-// f32 prediction and exact-check-sum kernels (FULL tier, 4 rows/lane).
+// f32 prediction and exact-check (Julia-order range sum) kernels (FULL tier, 4 rows/lane).
 #include "sr_tile_impl.h"
 SR_INSTANTIATE(float, 4, SR_MODE_PRED, false, SR_TIER_FULL)
 SR_INSTANTIATE(float, 4, SR_MODE_PRED, true, SR_TIER_FULL)
-SR_INSTANTIATE(float, 4, SR_MODE_EXACT, false, SR_TIER_FULL)
-SR_INSTANTIATE(float, 4, SR_MODE_EXACT, true, SR_TIER_FULL)
+SR_INSTANTIATE_W(float, 4, SR_MODE_EXACT, false, SR_TIER_FULL, 1)
+SR_INSTANTIATE_W(float, 4, SR_MODE_EXACT, true, SR_TIER_FULL, 1)

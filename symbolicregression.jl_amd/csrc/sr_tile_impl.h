@@ -48,12 +48,20 @@ struct SrMinWaves {
 #ifndef SR_MIN_WAVES_R16
 #define SR_MIN_WAVES_R16 4
 #endif
-template <typename T, int R, int TIER, int W>
+#ifndef SR_MIN_WAVES_VSTK16
+#define SR_MIN_WAVES_VSTK16 4
+#endif
+#ifndef SR_MIN_WAVES_VSTK32
+#define SR_MIN_WAVES_VSTK32 3
+#endif
+template <typename T, int R, int TIER, int W, bool VSTK = false>
 struct SrMinWavesFor {
   static constexpr bool f32_basic = sizeof(T) == 4 && TIER == SR_TIER_BASIC && W == 4;
-  static constexpr int value = (f32_basic && R == 8)    ? SR_MIN_WAVES_W4
-                               : (f32_basic && R == 16) ? SR_MIN_WAVES_R16
-                                                        : SrMinWaves<W>::value;
+  static constexpr int value = (f32_basic && VSTK && R == 16)   ? SR_MIN_WAVES_VSTK16
+                               : (f32_basic && VSTK && R == 32) ? SR_MIN_WAVES_VSTK32
+                               : (f32_basic && R == 8)          ? SR_MIN_WAVES_W4
+                               : (f32_basic && R == 16)         ? SR_MIN_WAVES_R16
+                                                                : SrMinWaves<W>::value;
 };
 
 // 16-byte chunks of C values.
@@ -236,12 +244,24 @@ __device__ __forceinline__ P* sr_row_at(P* base, uint32_t meta) {
 // flag bits above the index shift out of the 32-bit byte offset); constants from the c words
 #define SR_OPND_STK() sr_row_at<ROWS>(stk_lane, SR_META())
 #define SR_OPND_X() sr_row_at<ROWS>(x_lane, SR_META())
+// stack operand: VSTK kernels keep the (at most two) operand-stack slots in VGPRs (s0, s1; the slot
+// is the operand index); the others read the slot's rows from the wave's LDS stack area
+#define SR_STK_BIN(ID, LEFT)                                          \
+  if constexpr (VSTK) {                                               \
+    if ((SR_META() & SR_M_INDEX) == 0u) {                             \
+      SR_BIN_EACH((LEFT) ? s0[r] : tos[r], (LEFT) ? tos[r] : s0[r], ID); \
+    } else {                                                          \
+      SR_BIN_EACH((LEFT) ? s1[r] : tos[r], (LEFT) ? tos[r] : s1[r], ID); \
+    }                                                                 \
+  } else {                                                            \
+    T o[R];                                                           \
+    L::load(SR_OPND_STK(), o);                                        \
+    SR_BIN_EACH((LEFT) ? o[r] : tos[r], (LEFT) ? tos[r] : o[r], ID);  \
+  }
 #define SR_BCASE_R(ID, ENABLED)        \
   case SR_BIN_OPC(ID, SR_V_SR): {      \
     if (ENABLED) {                     \
-      T o[R];                          \
-      L::load(SR_OPND_STK(), o);       \
-      SR_BIN_EACH(tos[r], o[r], ID);   \
+      SR_STK_BIN(ID, false);           \
       SR_TRACK();                      \
     }                                  \
     break;                             \
@@ -266,9 +286,7 @@ __device__ __forceinline__ P* sr_row_at(P* base, uint32_t meta) {
 #define SR_BCASE_L(ID, ENABLED)        \
   case SR_BIN_OPC(ID, SR_V_SL): {      \
     if (ENABLED) {                     \
-      T o[R];                          \
-      L::load(SR_OPND_STK(), o);       \
-      SR_BIN_EACH(o[r], tos[r], ID);   \
+      SR_STK_BIN(ID, true);            \
       SR_TRACK();                      \
     }                                  \
     break;                             \
@@ -332,10 +350,11 @@ __device__ __forceinline__ P* sr_row_at(P* base, uint32_t meta) {
   SR_BCASE_R(ID, TIER == SR_TIER_FULL) SR_BCASE_L(ID, TIER == SR_TIER_FULL) SR_PCASES(ID, TIER == SR_TIER_FULL)
 
 // LDS carve, in bytes, 16-aligned: X tile [nf][ROWS] T | y [ROWS] | w [ROWS] (weighted) | stack
-// [W][depth][ROWS] T | xacc [G][max_checks] f64 (EXACT mode)
+// [W][depth][ROWS] T | EXACT mode: checked values [W][max_checks][ROWS] T and the running Julia-order
+// sums [G][max_checks] T
 template <typename T>
 struct SrLdsPlan {
-  size_t x, y, w, stk, xacc, total;
+  size_t x, y, w, stk, chk, jst, total;
   __host__ __device__ SrLdsPlan(int nf, int rows, int depth, int G, int max_checks, int waves, bool weighted) {
     size_t o = 0;
     x = o;
@@ -346,8 +365,10 @@ struct SrLdsPlan {
     if (weighted) o += size_t(rows) * sizeof(T);
     stk = o;
     o += size_t(waves) * size_t(depth) * rows * sizeof(T);
-    xacc = o;
-    o += size_t(G) * size_t(max_checks) * 8;
+    chk = o;
+    o += size_t(waves) * size_t(max_checks) * rows * sizeof(T);
+    jst = o;
+    o += (size_t(G) * size_t(max_checks) * sizeof(T) + 15) / 16 * 16;
     total = o;
   }
 };
@@ -387,7 +408,9 @@ __device__ __forceinline__ typename SrWindow<T>::type sr_window(const void* code
 }
 
 // ------------------------------------------------------------------ the interpreter kernel
-// MODE: SR_MODE_LOSS (partials), SR_MODE_PRED (write predictions), SR_MODE_EXACT (check sums).
+// MODE: SR_MODE_LOSS (partials), SR_MODE_PRED (write predictions), SR_MODE_EXACT (Julia-order sums of
+// the checked arrays over row ranges: DynamicExpressions' isfinite(sum(x)) decided exactly as Base's
+// pairwise `sum` computes it in T; a "row block" is one range of a.range_lo/range_hi).
 //
 // Tree ownership: the block's G trees are positions tree0 .. tree0+G-1 of the launch order
 // (a.perm maps a position to the caller's tree index: the host orders trees by estimated cost so
@@ -395,8 +418,9 @@ __device__ __forceinline__ typename SrWindow<T>::type sr_window(const void* code
 // everything per tree lives in that wave: program bounds in lane j's VGPRs, the loss accumulator in
 // lane j, the non-finite / suspicious bits in scalar masks.
 // LK: elementwise loss fixed at compile time (SR_LOSS_L2 / SR_LOSS_L1), or -1 = a.loss_kind.
-template <typename T, int R, int MODE, bool GATHER, int TIER, int W, int LK>
-__global__ void __launch_bounds__(W * 64, (SrMinWavesFor<T, R, TIER, W>::value)) sr_tile_kernel(const SrEvalArgs<T> a) {
+// VSTK: the operand stack (<= 2 slots: every tree of <= 30 nodes) lives in VGPRs.
+template <typename T, int R, int MODE, bool GATHER, int TIER, int W, int LK, bool VSTK>
+__global__ void __launch_bounds__(W * 64, (SrMinWavesFor<T, R, TIER, W, VSTK>::value)) sr_tile_kernel(const SrEvalArgs<T> a) {
   constexpr int SR_WAVES = W;
   constexpr int SR_BLOCK = W * 64;
   using L = SrLane<T, R>;
@@ -412,11 +436,12 @@ __global__ void __launch_bounds__(W * 64, (SrMinWavesFor<T, R, TIER, W>::value))
   const int lane = tid & 63;
   const int G = a.trees_per_block;
   const int MC = (MODE == SR_MODE_EXACT) ? a.max_checks : 0;
-  const SrLdsPlan<T> plan(a.nf, ROWS, a.stack_depth, G, MC, W, a.w != nullptr);
+  const SrLdsPlan<T> plan(a.nf, ROWS, VSTK ? 0 : a.stack_depth, G, MC, W, a.w != nullptr);
   T* xs = reinterpret_cast<T*>(sr_smem + plan.x);
   T* ys = reinterpret_cast<T*>(sr_smem + plan.y);
   T* wsv = reinterpret_cast<T*>(sr_smem + plan.w);
-  double* xacc = reinterpret_cast<double*>(sr_smem + plan.xacc);
+  T* chk = reinterpret_cast<T*>(sr_smem + plan.chk);  // EXACT: [W][MC][ROWS] checked values of a tile
+  T* jst = reinterpret_cast<T*>(sr_smem + plan.jst);  // EXACT: [G][MC] running sums
   const T* x_lane = xs + lane * C;
   const T* y_lane = ys + lane * C;
   const T* w_lane = wsv + lane * C;
@@ -451,16 +476,28 @@ __global__ void __launch_bounds__(W * 64, (SrMinWavesFor<T, R, TIER, W>::value))
   uint32_t hintv = 0u;
   if (use_hint && lane < S) hintv = __hip_atomic_load(a.hint + my_pos, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 
-  for (int i = tid; i < G * MC; i += SR_BLOCK) xacc[i] = 0.0;
+  for (int i = tid; i < G * MC; i += SR_BLOCK) jst[i] = T(0);
+  // EXACT: this block's row range [rlo, rhi] of the view (one leaf block of Julia's pairwise sum)
+  const int64_t rlo = (MODE == SR_MODE_EXACT) ? a.range_lo[rb] : 0;
+  const int64_t rhi = (MODE == SR_MODE_EXACT) ? a.range_hi[rb] : 0;
 
   for (int tile = 0; tile < a.tiles_per_block; ++tile) {
-    const int64_t row0 = (int64_t(rb) * a.tiles_per_block + tile) * ROWS;
-    if (row0 >= a.n_rows) break;  // uniform over the block
+    const int64_t row0 = (MODE == SR_MODE_EXACT) ? rlo + int64_t(tile) * ROWS
+                                                 : (int64_t(rb) * a.tiles_per_block + tile) * ROWS;
+    if (MODE == SR_MODE_EXACT ? row0 > rhi : row0 >= a.n_rows) break;  // uniform over the block
     const bool full_tile = row0 + ROWS <= a.n_rows;
+    const int n_valid = (MODE == SR_MODE_EXACT) ? int(rhi - row0 + 1 < ROWS ? rhi - row0 + 1 : ROWS) : ROWS;
     __syncthreads();              // previous tile's readers are done with the LDS image
     // ---- stage the tile: X rows of every feature, y, w (a plain copy; padded rows replicate
     // row 0 of the view, so every program sees finite, in-range data there)
-    if (!GATHER) {
+    if (MODE == SR_MODE_EXACT) {
+      // a range starts anywhere: element-wise loads; rows past the range replicate its first row
+      for (int i = tid; i < ROWS; i += SR_BLOCK) {
+        const int64_t v = (i < n_valid) ? row0 + i : rlo;
+        const int64_t src = GATHER ? a.row_idx[v] : v;
+        for (int f = 0; f < a.nf; ++f) xs[f * ROWS + i] = a.X[int64_t(f) * a.ld + src];
+      }
+    } else if (!GATHER) {
       constexpr int CPR = ROWS / C;  // 16-byte chunks per feature row
       using V = typename SrChunk<T>::V;
       const int n_chunks = a.nf * CPR;
@@ -504,8 +541,9 @@ __global__ void __launch_bounds__(W * 64, (SrMinWavesFor<T, R, TIER, W>::value))
     int j = -1;
     uint32_t tpe = 0u;
     T tos[R];
+    T s0[R], s1[R];  // VSTK operand-stack slots
 #pragma unroll
-    for (int r = 0; r < R; ++r) tos[r] = T(0);
+    for (int r = 0; r < R; ++r) tos[r] = s0[r] = s1[r] = T(0);
     bool dead = false;
     bool susp_any = false;
     int check_k = 0;
@@ -545,8 +583,16 @@ __global__ void __launch_bounds__(W * 64, (SrMinWavesFor<T, R, TIER, W>::value))
           const uint32_t op = uint32_t(__builtin_amdgcn_readlane(int(wop), int(k)));
 #define SR_CVAL() sr_lane_value<T>(wc0, wc1, k)
 #define SR_META() uint32_t(__builtin_amdgcn_readlane(int(wmeta), int(k)))
-#define SR_PUSH_TOS()                                                                      \
-  L::store(sr_row_at<ROWS>(stk_lane, ((SR_META() >> SR_M_PUSH_SHIFT) & 0x3fu) - 1u), tos)
+#define SR_PUSH_TOS()                                                                        \
+  if constexpr (VSTK) {                                                                      \
+    if (((SR_META() >> SR_M_PUSH_SHIFT) & 0x3fu) == 1u) {                                    \
+      _Pragma("unroll") for (int r = 0; r < R; ++r) s0[r] = tos[r];                          \
+    } else {                                                                                 \
+      _Pragma("unroll") for (int r = 0; r < R; ++r) s1[r] = tos[r];                          \
+    }                                                                                        \
+  } else {                                                                                   \
+    L::store(sr_row_at<ROWS>(stk_lane, ((SR_META() >> SR_M_PUSH_SHIFT) & 0x3fu) - 1u), tos); \
+  }
           switch (op) {
             case SR_OP_LOAD_FEAT_PUSH:
               SR_PUSH_TOS();
@@ -589,12 +635,8 @@ __global__ void __launch_bounds__(W * 64, (SrMinWavesFor<T, R, TIER, W>::value))
 #undef SR_PUSH_TOS
           if (!FAST_CHECK && (SR_META() & SR_M_CHECK)) {
             if (MODE == SR_MODE_EXACT) {
-              double s = 0.0;
-#pragma unroll
-              for (int r = 0; r < R; ++r)
-                s += (row0 + L::row(lane, r) < a.n_rows) ? double(tos[r]) * a.scale : 0.0;
-              s = sr_wave_sum<double>(s);
-              if (lane == 0) xacc[g * MC + check_k] += s;
+              // the checked array's rows of this tile, in row order, for the Julia-order fold below
+              if (check_k < MC) L::store(chk + (size_t(wave) * MC + check_k) * ROWS + lane * C, tos);
               ++check_k;
             } else {
               // |v| >= tbig (or NaN / Inf) in any row: one integer max per lane + one ballot;
@@ -619,7 +661,19 @@ __global__ void __launch_bounds__(W * 64, (SrMinWavesFor<T, R, TIER, W>::value))
 
       if (base + SR_WIN >= tpe) {  // tree j is done on this tile
         const uint64_t bit = uint64_t(1) << j;
-        if (MODE == SR_MODE_LOSS) {
+        if (MODE == SR_MODE_EXACT) {
+          // Base.mapreduce_impl's sequential leaf loop, v = v + a[i] in T, continued across the
+          // range's tiles (lane k folds check k; the first row of the range starts the fold)
+          __builtin_amdgcn_wave_barrier();
+          const int nk = check_k < MC ? check_k : MC;
+          for (int k = lane; k < nk; k += 64) {
+            const T* cb = chk + (size_t(wave) * MC + k) * ROWS;
+            T v = (tile == 0) ? cb[0] : jst[g * MC + k];
+            for (int i = (tile == 0) ? 1 : 0; i < n_valid; ++i) v = v + cb[i];
+            jst[g * MC + k] = v;
+          }
+          __builtin_amdgcn_wave_barrier();
+        } else if (MODE == SR_MODE_LOSS) {
           if (!dead) {
             T l[R];
             T yv[R];
@@ -696,11 +750,9 @@ __global__ void __launch_bounds__(W * 64, (SrMinWavesFor<T, R, TIER, W>::value))
 
   if (MODE == SR_MODE_EXACT) {
     __syncthreads();
-    // one device-scope add per (block, tree, check)
-    for (int i = tid; i < gcount * MC; i += SR_BLOCK) {
-      const double v = xacc[i];
-      if (v != 0.0) atomicAdd(a.check_sums + size_t(tree0) * MC + i, v);
-    }
+    // this range's sum of every checked array: [list position][check][range]
+    T* out = static_cast<T*>(a.range_sums);
+    for (int i = tid; i < gcount * MC; i += SR_BLOCK) out[(size_t(tree0) * MC + i) * size_t(a.n_row_blocks) + rb] = jst[i];
     return;
   }
   if (lane < S) {
@@ -711,23 +763,25 @@ __global__ void __launch_bounds__(W * 64, (SrMinWavesFor<T, R, TIER, W>::value))
 }
 
 // ------------------------------------------------------------------ launch helpers
-template <typename T, int R, int MODE, bool GATHER, int TIER, int W, int LK>
+template <typename T, int R, int MODE, bool GATHER, int TIER, int W, int LK, bool VSTK>
 hipError_t sr_launch_tile(const SrEvalArgs<T>& a, int n_blocks, hipStream_t s) {
-  const SrLdsPlan<T> plan(a.nf, 64 * R, a.stack_depth, a.trees_per_block, MODE == SR_MODE_EXACT ? a.max_checks : 0, W,
-                          a.w != nullptr);
-  const void* fn = reinterpret_cast<const void*>(&sr_tile_kernel<T, R, MODE, GATHER, TIER, W, LK>);
+  if (VSTK && a.stack_depth > 2) return hipErrorInvalidValue;  // host checks: VSTK holds two slots
+  const SrLdsPlan<T> plan(a.nf, 64 * R, VSTK ? 0 : a.stack_depth, a.trees_per_block,
+                          MODE == SR_MODE_EXACT ? a.max_checks : 0, W, a.w != nullptr);
+  const void* fn = reinterpret_cast<const void*>(&sr_tile_kernel<T, R, MODE, GATHER, TIER, W, LK, VSTK>);
   if (plan.total > 65536) {  // many features / a deep stack: opt in to the full 160 KiB of LDS
     const hipError_t e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, int(plan.total));
     if (e != hipSuccess) return e;
   }
-  hipLaunchKernelGGL((sr_tile_kernel<T, R, MODE, GATHER, TIER, W, LK>), dim3(n_blocks), dim3(W * 64), plan.total, s, a);
+  hipLaunchKernelGGL((sr_tile_kernel<T, R, MODE, GATHER, TIER, W, LK, VSTK>), dim3(n_blocks), dim3(W * 64), plan.total, s, a);
   return hipGetLastError();
 }
 
 // Explicit instantiations are spread over several translation units (sr_inst_*.hip, one per
 // element type / mode) so the build compiles them in parallel; see the Makefile.
-#define SR_INSTANTIATE_WL(T, R, MODE, GATHER, TIER, W, LK) \
-  template hipError_t sr_launch_tile<T, R, MODE, GATHER, TIER, W, LK>(const SrEvalArgs<T>&, int, hipStream_t);
+#define SR_INSTANTIATE_WLV(T, R, MODE, GATHER, TIER, W, LK, VSTK) \
+  template hipError_t sr_launch_tile<T, R, MODE, GATHER, TIER, W, LK, VSTK>(const SrEvalArgs<T>&, int, hipStream_t);
+#define SR_INSTANTIATE_WL(T, R, MODE, GATHER, TIER, W, LK) SR_INSTANTIATE_WLV(T, R, MODE, GATHER, TIER, W, LK, false)
 #define SR_INSTANTIATE_W(T, R, MODE, GATHER, TIER, W) SR_INSTANTIATE_WL(T, R, MODE, GATHER, TIER, W, -1)
 #define SR_INSTANTIATE(T, R, MODE, GATHER, TIER) SR_INSTANTIATE_WL(T, R, MODE, GATHER, TIER, 4, -1)
 // BASIC-tier loss kernels: one instantiation per elementwise loss
@@ -735,3 +789,8 @@ hipError_t sr_launch_tile(const SrEvalArgs<T>& a, int n_blocks, hipStream_t s) {
   SR_INSTANTIATE_WL(T, R, SR_MODE_LOSS, GATHER, SR_TIER_BASIC, 4, SR_LOSS_L2) \
   SR_INSTANTIATE_WL(T, R, SR_MODE_LOSS, GATHER, SR_TIER_BASIC, 4, SR_LOSS_L1) \
   SR_INSTANTIATE_WL(T, R, SR_MODE_LOSS, GATHER, SR_TIER_BASIC, 4, -1)
+// register-stack BASIC-tier loss kernels (f32, 16 / 32 rows per lane)
+#define SR_INSTANTIATE_LOSS_VSTK(T, R, GATHER)                                     \
+  SR_INSTANTIATE_WLV(T, R, SR_MODE_LOSS, GATHER, SR_TIER_BASIC, 4, SR_LOSS_L2, true) \
+  SR_INSTANTIATE_WLV(T, R, SR_MODE_LOSS, GATHER, SR_TIER_BASIC, 4, SR_LOSS_L1, true) \
+  SR_INSTANTIATE_WLV(T, R, SR_MODE_LOSS, GATHER, SR_TIER_BASIC, 4, -1, true)

@@ -47,8 +47,12 @@ EXPORTED_SYMBOLS = (
     "sr_eval_loss_batch",
     "sr_eval_tree_array",
     "sr_eval_loss_partials",
+    "sr_eval_loss_partials_packed",
     "sr_max_checks",
-    "sr_exact_check_partials",
+    "sr_jsum_range_count",
+    "sr_jsum_ranges",
+    "sr_jsum_partials",
+    "sr_jsum_finite",
     "sr_finalize_losses",
     "sr_dataset_denominator",
     "sr_eval_grad_batch",
@@ -114,13 +118,20 @@ def _load():
             [P, P, c_int, POINTER(SrTreeBatch), c_int64, c_int, P, P, c_int],
         ),
         "sr_max_checks": (c_int, [P, c_int, POINTER(SrTreeBatch), POINTER(c_int)]),
-        "sr_exact_check_partials": (
+        "sr_eval_loss_partials_packed": (
             c_int,
-            [P, P, c_int, POINTER(SrTreeBatch), P, c_int64, c_int, P],
+            [P, P, c_int, POINTER(SrTreeBatch), c_int64, c_int, P, c_int],
         ),
+        "sr_jsum_range_count": (c_int, [c_int64, c_int64, c_int64, POINTER(c_int64)]),
+        "sr_jsum_ranges": (c_int, [c_int64, c_int64, c_int64, P, P, P, P]),
+        "sr_jsum_partials": (
+            c_int,
+            [P, P, c_int, POINTER(SrTreeBatch), P, c_int64, c_int, c_int64, c_int64, P],
+        ),
+        "sr_jsum_finite": (c_int, [c_int, c_int64, c_int, P, P, c_int64, P]),
         "sr_finalize_losses": (
             c_int,
-            [c_int, c_int64, P, P, c_double, P, c_int64, c_int, P, P, P],
+            [c_int, c_int64, P, P, c_double, P, c_int64, P, P, P],
         ),
         "sr_dataset_denominator": (c_int, [P, POINTER(c_double)]),
         "sr_eval_grad_batch": (

@@ -1,11 +1,13 @@
 """Row-sharded scoring across GPUs (one process per GPU, torch.distributed over RCCL).
 
-Each rank holds one row shard of the dataset (HBM-resident), scores every tree on it
-(`sr_eval_loss_partials`: per-tree f64 Σ loss and flag bits), and the ranks combine the partials
-with all-reduces — SUM for the sums, MAX per flag bit — before `sr_finalize_losses` turns them into
-losses.  Trees that came close to overflowing a checked array sum (BIG only) need the exact per-check
-sums of every shard: one more all-reduce of `sr_exact_check_partials`.  This is the path's only
-exchange step; at 10k trees it moves 8 B + 12 B per tree.
+Each rank holds one row shard of the dataset (HBM-resident), scores every tree on it and packs its
+per-tree partials into one [4, n_trees] float64 device tensor (`sr_eval_loss_partials_packed`:
+Σ loss, then the NONFINITE / BIG / STATIC flag bits as 0/1), which ONE all-reduce (SUM) combines —
+the partials never leave the GPU.  Trees that came close to overflowing a checked array sum (BIG
+only: rare) get the exact verdict of DynamicExpressions' isfinite(sum(x)) in Julia's pairwise order
+over the GLOBAL row range: each rank folds the leaf blocks it holds (`sr_jsum_partials`), the folds
+are all-gathered, and `sr_jsum_finite` adds them in Base.mapreduce_impl's recursion order
+(DESIGN.md §7).  `sr_finalize_losses` then turns sums and verdicts into losses.
 
 `partials_fn` / `exact_fn` default to the GPU calls; tests inject CPU stand-ins to exercise the
 combine logic with the gloo backend.
@@ -20,40 +22,79 @@ from . import _lib
 from .device import get_context
 from .loss import _as_batch
 
-FLAG_BITS = (_lib.SR_FLAG_NONFINITE, _lib.SR_FLAG_BIG, _lib.SR_FLAG_STATIC)
+
+def _dtype_code(dtype):
+    return _lib.SR_DTYPE_F32 if np.dtype(dtype) == np.float32 else _lib.SR_DTYPE_F64
 
 
-def gpu_partials(tb, shard, options, n_total, ctx=None):
-    """This rank's per-tree (Σ loss f64, flags u32) on its row shard (GPU)."""
+def gpu_partials_packed(tb, shard, options, n_total, *, device_tensor=False, ctx=None):
+    """This rank's packed partials [4, n_trees] f64 on its row shard (GPU).  device_tensor=True
+    returns a torch tensor on this rank's GPU written by the library in place (no host copy)."""
     ctx = ctx or get_context()
     nt = tb.n_trees
-    sums = np.zeros(nt, dtype=np.float64)
-    flags = np.zeros(nt, dtype=np.uint32)
     s = tb.to_struct()
-    _lib.check(_lib.lib.sr_eval_loss_partials(
-        ctx.handle, shard.device_handle(ctx), ctx.opset_id(options.operators), ctypes.byref(s), int(n_total),
-        ctx.loss_code(options), sums.ctypes.data_as(ctypes.c_void_p), flags.ctypes.data_as(ctypes.c_void_p), 0))
-    return sums, flags
+    args = (ctx.handle, shard.device_handle(ctx), ctx.opset_id(options.operators), ctypes.byref(s), int(n_total),
+            ctx.loss_code(options))
+    if device_tensor:
+        import torch
 
-
-def gpu_exact(tb, shard, options, tree_list, ctx=None):
-    """This rank's exact per-check array sums for the listed trees (GPU): [n_list, max_checks]."""
-    ctx = ctx or get_context()
-    oid = ctx.opset_id(options.operators)
-    s = tb.to_struct()
-    m = ctypes.c_int()
-    _lib.check(_lib.lib.sr_max_checks(ctx.handle, oid, ctypes.byref(s), ctypes.byref(m)))
-    mc = int(m.value)
-    lst = np.ascontiguousarray(tree_list, dtype=np.int64)
-    out = np.zeros((lst.size, mc), dtype=np.float64)
-    if lst.size and mc:
-        _lib.check(_lib.lib.sr_exact_check_partials(
-            ctx.handle, shard.device_handle(ctx), oid, ctypes.byref(s), lst.ctypes.data_as(ctypes.c_void_p),
-            lst.size, mc, out.ctypes.data_as(ctypes.c_void_p)))
+        out = torch.empty((4, max(nt, 1)), dtype=torch.float64, device=torch.device("cuda", ctx.device))
+        _lib.check(_lib.lib.sr_eval_loss_partials_packed(*args, ctypes.c_void_p(out.data_ptr()), 1))
+        return out[:, :nt]
+    out = np.zeros((4, nt), dtype=np.float64)
+    _lib.check(_lib.lib.sr_eval_loss_partials_packed(*args, out.ctypes.data_as(ctypes.c_void_p), 0))
     return out
 
 
-def finalize(dtype, sums, flags, denom, tree_list=None, check_sums=None):
+def jsum_ranges(row_offset, n_local, n_total):
+    """(lo, hi, leaf, head) of the row ranges a shard folds for the exact check (C ABI)."""
+    n = ctypes.c_int64()
+    _lib.check(_lib.lib.sr_jsum_range_count(int(row_offset), int(n_local), int(n_total), ctypes.byref(n)))
+    lo, hi, leaf = (np.zeros(n.value, dtype=np.int64) for _ in range(3))
+    head = np.zeros(n.value, dtype=np.uint8)
+    p = lambda a: a.ctypes.data_as(ctypes.c_void_p)  # noqa: E731
+    _lib.check(_lib.lib.sr_jsum_ranges(int(row_offset), int(n_local), int(n_total), p(lo), p(hi), p(leaf), p(head)))
+    return lo, hi, leaf, head.astype(bool)
+
+
+def gpu_jsum(tb, shard, options, tree_list, max_checks, row_offset, n_total, ctx=None):
+    """This rank's Julia-order folds of every checked array of the listed trees over its ranges:
+    [n_list, max_checks, n_ranges] (dataset dtype)."""
+    ctx = ctx or get_context()
+    oid = ctx.opset_id(options.operators)
+    s = tb.to_struct()
+    lst = np.ascontiguousarray(tree_list, dtype=np.int64)
+    n_ranges = len(jsum_ranges(row_offset, shard.n, n_total)[0])
+    out = np.zeros((lst.size, max_checks, n_ranges), dtype=shard.full.dtype)
+    if lst.size and max_checks:
+        _lib.check(_lib.lib.sr_jsum_partials(
+            ctx.handle, shard.device_handle(ctx), oid, ctypes.byref(s), lst.ctypes.data_as(ctypes.c_void_p),
+            lst.size, max_checks, int(row_offset), int(n_total), out.ctypes.data_as(ctypes.c_void_p)))
+    return out
+
+
+def gpu_max_checks(tb, options, ctx=None):
+    ctx = ctx or get_context()
+    s = tb.to_struct()
+    m = ctypes.c_int()
+    _lib.check(_lib.lib.sr_max_checks(ctx.handle, ctx.opset_id(options.operators), ctypes.byref(s), ctypes.byref(m)))
+    return int(m.value)
+
+
+def jsum_finite(dtype, n_total, row_offsets, rank_vals):
+    """isfinite(Julia sum) per array from every shard's folds (C ABI sr_jsum_finite).
+    rank_vals[r]: [n_arrays, n_ranges_r] of shard r = [row_offsets[r], row_offsets[r + 1])."""
+    offs = np.ascontiguousarray(row_offsets, dtype=np.int64)
+    vals = [np.ascontiguousarray(v, dtype=dtype) for v in rank_vals]
+    n_arrays = int(vals[0].shape[0]) if vals else 0
+    ptrs = (ctypes.c_void_p * len(vals))(*[v.ctypes.data_as(ctypes.c_void_p) for v in vals])
+    out = np.zeros(n_arrays, dtype=np.uint8)
+    _lib.check(_lib.lib.sr_jsum_finite(_dtype_code(dtype), int(n_total), len(vals), offs.ctypes.data_as(ctypes.c_void_p),
+                                       ptrs, n_arrays, out.ctypes.data_as(ctypes.c_void_p)))
+    return out.astype(bool)
+
+
+def finalize(dtype, sums, flags, denom, tree_list=None, list_ok=None):
     """Host combine (C ABI `sr_finalize_losses`): losses[T], complete[bool]."""
     nt = len(sums)
     sums = np.ascontiguousarray(sums, dtype=np.float64)
@@ -62,60 +103,68 @@ def finalize(dtype, sums, flags, denom, tree_list=None, check_sums=None):
     comp = np.empty(nt, dtype=np.uint8)
     p = lambda a: None if a is None else a.ctypes.data_as(ctypes.c_void_p)  # noqa: E731
     lst = None if tree_list is None or len(tree_list) == 0 else np.ascontiguousarray(tree_list, dtype=np.int64)
-    cs = None if lst is None else np.ascontiguousarray(check_sums, dtype=np.float64)
-    mc = 0 if cs is None else int(cs.shape[1])
-    _lib.check(_lib.lib.sr_finalize_losses(
-        _lib.SR_DTYPE_F32 if np.dtype(dtype) == np.float32 else _lib.SR_DTYPE_F64, nt, p(sums), p(flags),
-        float(denom), p(lst), 0 if lst is None else lst.size, mc, p(cs), p(out), p(comp)))
+    ok = None if lst is None else np.ascontiguousarray(list_ok, dtype=np.uint8)
+    _lib.check(_lib.lib.sr_finalize_losses(_dtype_code(dtype), nt, p(sums), p(flags), float(denom), p(lst),
+                                           0 if lst is None else lst.size, p(ok), p(out), p(comp)))
     return out, comp.astype(bool)
 
 
-def _all_reduce_np(dist, arr, op, group):
-    import torch
-
-    t = torch.from_numpy(np.ascontiguousarray(arr))
-    dev = _reduce_device(dist, group)
-    if dev is not None:
-        t = t.to(dev)
-    dist.all_reduce(t, op=op, group=group)
-    return t.cpu().numpy()
-
-
-def _reduce_device(dist, group):
-    # RCCL ("nccl") reduces device tensors; gloo reduces host tensors
-    if dist.get_backend(group) == "nccl":
-        import torch
-
-        return torch.device("cuda", torch.cuda.current_device())
-    return None
+def unpack_flags(packed):
+    """[4, n] summed partials -> (Σ loss f64, flag words u32): a bit is set if any rank set it."""
+    packed = np.asarray(packed, dtype=np.float64)
+    flags = np.zeros(packed.shape[1], dtype=np.uint32)
+    for row, bit in ((1, _lib.SR_FLAG_NONFINITE), (2, _lib.SR_FLAG_BIG), (3, _lib.SR_FLAG_STATIC)):
+        flags |= np.where(packed[row] > 0, np.uint32(bit), np.uint32(0))
+    return packed[0].copy(), flags
 
 
 def eval_loss_sharded(trees, shard, options, n_total, *, denom=None, group=None, partials_fn=None, exact_fn=None):
     """Losses of every tree over the union of all ranks' row shards -> (losses[T], complete[bool]).
 
     `denom`: global denominator (Σ rows, or Σ weights); defaults to `n_total` for unweighted data.
+    `partials_fn(tb)` -> packed [4, n_trees] partials (numpy, or a torch tensor on this rank's GPU);
+    `exact_fn(tb, tree_list, max_checks, row_offset)` -> [n_list, max_checks, n_ranges] folds.
     """
+    import torch
     import torch.distributed as dist
 
     full = shard.full
     tb = _as_batch(trees, full.dtype)
-    partials_fn = partials_fn or (lambda tb_: gpu_partials(tb_, shard, options, n_total))
-    exact_fn = exact_fn or (lambda tb_, lst: gpu_exact(tb_, shard, options, lst))
-    sums, flags = partials_fn(tb)
-    sums = _all_reduce_np(dist, sums, dist.ReduceOp.SUM, group)
-    bits = np.stack([(flags & b) != 0 for b in FLAG_BITS]).astype(np.int32)
-    bits = _all_reduce_np(dist, bits, dist.ReduceOp.MAX, group)
-    flags = np.zeros(tb.n_trees, dtype=np.uint32)
-    for k, b in enumerate(FLAG_BITS):
-        flags |= np.where(bits[k] != 0, np.uint32(b), np.uint32(0))
-    big = np.nonzero(((flags & (_lib.SR_FLAG_NONFINITE | _lib.SR_FLAG_STATIC)) == 0) & ((flags & _lib.SR_FLAG_BIG) != 0))[0]
-    cs = None
+    on_gpu = dist.get_backend(group) == "nccl"
+    partials_fn = partials_fn or (lambda tb_: gpu_partials_packed(tb_, shard, options, n_total, device_tensor=on_gpu))
+    packed = partials_fn(tb)
+    t = packed if isinstance(packed, torch.Tensor) else torch.from_numpy(np.ascontiguousarray(packed))
+    if on_gpu and not t.is_cuda:
+        t = t.cuda()
+    t = t.contiguous()
+    # the path's one exchange step: every rank's [4, n_trees] partials, summed
+    dist.all_reduce(t, op=dist.ReduceOp.SUM, group=group)
+    sums, flags = unpack_flags(t.cpu().numpy())
+    big = np.nonzero(((flags & (_lib.SR_FLAG_NONFINITE | _lib.SR_FLAG_STATIC)) == 0) &
+                     ((flags & _lib.SR_FLAG_BIG) != 0))[0]
+    ok = None
     if big.size:
-        cs = _all_reduce_np(dist, exact_fn(tb, big), dist.ReduceOp.SUM, group)
+        # rare: exact Julia-order verdict over the global rows
+        world = dist.get_world_size(group)
+        sizes = [None] * world
+        dist.all_gather_object(sizes, int(shard.n), group=group)
+        offs = np.concatenate([[0], np.cumsum(sizes)]).astype(np.int64)
+        rank = dist.get_rank(group)
+        mc = gpu_max_checks(tb, options) if exact_fn is None else 1
+        exact_fn = exact_fn or (lambda tb_, lst, m, off: gpu_jsum(tb_, shard, options, lst, m, off, n_total))
+        mine = np.ascontiguousarray(exact_fn(tb, big, mc, int(offs[rank])))
+        mc = mine.shape[1]
+        every = [None] * world
+        dist.all_gather_object(every, mine, group=group)
+        fin = jsum_finite(full.dtype, n_total, offs, [v.reshape(big.size * mc, -1) for v in every])
+        ok = fin.reshape(big.size, mc).all(axis=1).astype(np.uint8)
     if denom is None:
         if full.weights is not None:
-            local = np.array([float(np.sum(full.weights, dtype=np.float64))])
-            denom = float(_all_reduce_np(dist, local, dist.ReduceOp.SUM, group)[0])
+            local = torch.tensor([float(np.sum(full.weights, dtype=np.float64))], dtype=torch.float64)
+            if on_gpu:
+                local = local.cuda()
+            dist.all_reduce(local, op=dist.ReduceOp.SUM, group=group)
+            denom = float(local.cpu()[0])
         else:
             denom = float(n_total)
-    return finalize(full.dtype, sums, flags, denom, big, cs)
+    return finalize(full.dtype, sums, flags, denom, big, ok)

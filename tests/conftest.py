@@ -16,12 +16,14 @@ for p in (ROOT, PKG, os.path.join(ROOT, "oracle")):
 
 
 def _ensure_built():
-    lib = os.path.join(PKG, "lib", "libsr_amd.so")
-    if not os.path.exists(lib):
-        subprocess.run(["make", "-s", "-j8", "-C", PKG], check=True)
-    orc = os.path.join(ROOT, "oracle", "build", "liboracle.so")
-    if not os.path.exists(orc):
-        subprocess.run(["make", "-s", "-C", os.path.join(ROOT, "oracle")], check=True)
+    """Always run the (incremental) builds: a stale shipped .so must never stand in for HEAD's
+    sources.  make is a no-op when nothing changed.  Where no compiler exists (a GPU box without
+    hipcc never happens on this pool) the prebuilt libraries are used as they are."""
+    for d, jobs in ((PKG, "-j8"), (os.path.join(ROOT, "oracle"), "-j1")):
+        try:
+            subprocess.run(["make", "-s", jobs, "-C", d], check=True)
+        except FileNotFoundError:
+            pass
 
 
 _ensure_built()

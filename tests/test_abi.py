@@ -47,27 +47,27 @@ def test_init_without_gpu_fails_cleanly():
     assert not h.value
 
 
-def _finalize(dtype, sums, flags, denom, lst=None, max_checks=0, check_sums=None):
+def _finalize(dtype, sums, flags, denom, lst=None, list_ok=None):
     nt = len(sums)
     sums = np.ascontiguousarray(sums, dtype=np.float64)
     flags = np.ascontiguousarray(flags, dtype=np.uint32)
     out = np.empty(nt, dtype=np.float32 if dtype == _lib.SR_DTYPE_F32 else np.float64)
     comp = np.empty(nt, dtype=np.uint8)
     lst = None if lst is None else np.ascontiguousarray(lst, dtype=np.int64)
-    cs = None if check_sums is None else np.ascontiguousarray(check_sums, dtype=np.float64)
+    ok = None if list_ok is None else np.ascontiguousarray(list_ok, dtype=np.uint8)
     p = lambda a: None if a is None else a.ctypes.data_as(ctypes.c_void_p)
     _lib.check(_lib.lib.sr_finalize_losses(dtype, nt, p(sums), p(flags), denom, p(lst),
-                                           0 if lst is None else len(lst), max_checks, p(cs), p(out), p(comp)))
+                                           0 if lst is None else len(lst), p(ok), p(out), p(comp)))
     return out, comp.astype(bool)
 
 
 def test_finalize_combines_partials():
-    # tree0 fine, tree1 non-finite, tree2 static-bad, tree3 "big" but sums fine, tree4 big and overflowing
+    # tree0 fine, tree1 non-finite, tree2 static-bad, tree3 "big" but its Julia sums are finite,
+    # tree4 big and one Julia sum overflows
     sums = [10.0, 5.0, 0.0, 8.0, 8.0]
     flags = [0, _lib.SR_FLAG_NONFINITE, _lib.SR_FLAG_STATIC | _lib.SR_FLAG_NONFINITE, _lib.SR_FLAG_BIG,
              _lib.SR_FLAG_BIG]
-    cs = [[1e30, 2e30], [1e38, 4e38]]  # per listed tree, per checked node
-    loss, comp = _finalize(_lib.SR_DTYPE_F32, sums, flags, 4.0, lst=[3, 4], max_checks=2, check_sums=cs)
+    loss, comp = _finalize(_lib.SR_DTYPE_F32, sums, flags, 4.0, lst=[3, 4], list_ok=[1, 0])
     assert list(comp) == [True, False, False, True, False]
     assert loss[0] == np.float32(2.5)
     assert np.isinf(loss[1]) and np.isinf(loss[2]) and np.isinf(loss[4])
@@ -80,8 +80,9 @@ def test_finalize_rejects_bad_list():
     out = np.empty(2, dtype=np.float32)
     comp = np.empty(2, dtype=np.uint8)
     lst = np.array([5], dtype=np.int64)
+    ok = np.ones(1, dtype=np.uint8)
     rc = _lib.lib.sr_finalize_losses(_lib.SR_DTYPE_F32, 2, sums.ctypes.data_as(ctypes.c_void_p),
                                      flags.ctypes.data_as(ctypes.c_void_p), 1.0, lst.ctypes.data_as(ctypes.c_void_p),
-                                     1, 1, None, out.ctypes.data_as(ctypes.c_void_p),
+                                     1, ok.ctypes.data_as(ctypes.c_void_p), out.ctypes.data_as(ctypes.c_void_p),
                                      comp.ctypes.data_as(ctypes.c_void_p))
     assert rc == _lib.SR_ERR_INVALID_ARG

@@ -1,9 +1,10 @@
 """CPU, world_size 2 (gloo): the multi-GPU combine of row-sharded partials.
 
 `sr_amd.distributed.eval_loss_sharded` is run by two processes over two row shards with CPU
-stand-ins for the two GPU calls (per-shard partial sums / flags from the oracle's predictions, and
-per-shard exact array sums); the all-reduces, the BIG-tree exact path and `sr_finalize_losses`
-(host C ABI) are the product code.  The result must equal the oracle on the unsharded data.
+stand-ins for the two GPU calls (per-shard packed partials — Σ loss + flag bits — from the oracle's
+predictions, and per-shard Julia-order folds of the checked arrays); the single packed all-reduce,
+the BIG-tree exact path (all-gather + `sr_jsum_finite`) and `sr_finalize_losses` (host C ABI) are
+the product code.  The result must equal the oracle on the unsharded data.
 """
 import os
 import socket
@@ -41,7 +42,9 @@ def _worker(rank, world, port, q):
     from oracle import Oracle
     from sr_amd import Dataset, Options, flatten_trees, parse_expression
     from sr_amd import _lib
-    from sr_amd.distributed import eval_loss_sharded
+    from sr_amd.distributed import eval_loss_sharded, jsum_ranges
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    from test_jsum import jl_sum
 
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
@@ -56,19 +59,24 @@ def _worker(rank, world, port, q):
         tbig = np.float32(3.4028235e38 / (2.0 * n))
 
         def partials(tb_):
-            sums = np.zeros(tb_.n_trees)
-            flags = np.zeros(tb_.n_trees, dtype=np.uint32)
+            packed = np.zeros((4, tb_.n_trees))
             for k in range(tb_.n_trees):
                 out, _ = orc.eval_tree_array(tb_, k, Xs)
                 if not np.all(np.isfinite(out)):
-                    flags[k] |= _lib.SR_FLAG_NONFINITE
+                    packed[1, k] = 1.0  # SR_FLAG_NONFINITE
                 elif np.any(np.abs(out) >= tbig):
-                    flags[k] |= _lib.SR_FLAG_BIG
-                sums[k] = np.sum((out.astype(np.float64) - ys) ** 2)
-            return sums, flags
+                    packed[2, k] = 1.0  # SR_FLAG_BIG
+                packed[0, k] = np.sum((out.astype(np.float64) - ys) ** 2)
+            return packed
 
-        def exact(tb_, lst):
-            return np.array([[np.sum(orc.eval_tree_array(tb_, int(k), Xs)[0].astype(np.float64))] for k in lst])
+        def exact(tb_, lst, max_checks, row_offset):
+            # these trees' only checked array is the root: its Julia-order folds over this shard's ranges
+            lo_, hi_, _, _ = jsum_ranges(row_offset, Xs.shape[1], n)
+            out = np.zeros((len(lst), 1, len(lo_)), dtype=np.float32)
+            for i, k in enumerate(lst):
+                a = orc.eval_tree_array(tb_, int(k), Xs)[0].astype(np.float32)
+                out[i, 0] = [jl_sum(a, int(l), int(h)) for l, h in zip(lo_, hi_)]
+            return out
 
         loss, comp = eval_loss_sharded(tb, shard, opts, n, partials_fn=partials, exact_fn=exact)
         q.put((rank, loss.tolist(), comp.tolist()))

@@ -1,0 +1,86 @@
+"""Device libm vs correctly rounded values (tests/golden/libm_ulp.json, mpmath 400-bit).
+
+The reference evaluates exp / safe_log / cos / sin / safe_sqrt with Julia's Base.Math, whose
+Float32/Float64 kernels are accurate to < 1 ulp.  No Julia runtime exists here (SURVEY.md §8(c):
+bitwise libm parity is unpinned), so the device is held to the correctly rounded value itself:
+<= 1 ulp of T on every fixture point (including the reduction worst cases near multiples of pi/2,
+huge arguments, exp's overflow threshold and log near 1), and sqrt exactly rounded (IEEE, as Julia).
+The CPU test pins the fixture: glibc's float64 libm (numpy) sits within 1 ulp of it.
+"""
+import json
+import os
+
+import numpy as np
+import pytest
+
+from sr_amd import Options, eval_tree_array, parse_expression
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+FNS = ("exp", "log", "cos", "sin", "sqrt")
+
+
+@pytest.fixture(scope="module")
+def ulp_fixture():
+    with open(os.path.join(HERE, "golden", "libm_ulp.json")) as f:
+        return json.load(f)
+
+
+def ulp_errors(dtype, xs_out, entries):
+    """|device - exact| in ulps of dtype (exact = hi + lo); inf entries must match exactly."""
+    e = np.array(entries, dtype=np.float64)
+    hi, lo = e[:, 1], e[:, 2]
+    dev = np.asarray(xs_out, dtype=np.float64)
+    inf = np.isinf(hi)
+    assert np.array_equal(dev[inf], hi[inf]), "overflowing results must be +-Inf"
+    fin = ~inf
+    ulp = np.spacing(np.abs(hi[fin]).astype(dtype)).astype(np.float64)
+    # the spacing below a power of two is half the one above: use the smaller (stricter) one
+    ulp = np.minimum(ulp, np.spacing(np.nextafter(np.abs(hi[fin]).astype(dtype), dtype(0))).astype(np.float64))
+    ulp = np.maximum(ulp, float(np.finfo(dtype).smallest_subnormal))
+    with np.errstate(invalid="ignore"):
+        err = np.abs((dev[fin] - hi[fin]) - lo[fin]) / ulp
+    return err
+
+
+def test_fixture_pinned_by_glibc_f64(ulp_fixture):
+    """CPU: glibc (numpy float64) exp/log/cos/sin/sqrt are within 1 ulp of the fixture."""
+    g = ulp_fixture["float64"]
+    for fn in FNS:
+        e = np.array(g[fn], dtype=np.float64)
+        with np.errstate(over="ignore"):
+            out = getattr(np, fn)(e[:, 0])
+        err = ulp_errors(np.float64, out, g[fn])
+        assert np.all(err <= 1.0), (fn, float(np.max(err)))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("dtype_name", ["float32", "float64"])
+@pytest.mark.parametrize("fn", FNS)
+def test_device_libm_within_one_ulp(ulp_fixture, dtype_name, fn):
+    dtype = np.float32 if dtype_name == "float32" else np.float64
+    opts = Options(binary_operators=["+"], unary_operators=[fn])
+    tree = parse_expression(f"{fn}(x1)", opts)
+    everything = ulp_fixture[dtype_name][fn]
+    # DE's validity check is isfinite(sum(array)): a non-finite value, or values so large that their
+    # sum overflows, make the whole tree incomplete (and its array is not returned).  Points whose
+    # value could do that are evaluated one by one; overflowing ones must come back incomplete.
+    big = float(np.finfo(dtype).max) / (4 * len(everything))
+    single = [e for e in everything if not abs(e[1]) <= big]
+    entries = [e for e in everything if abs(e[1]) <= big]
+    outs = []
+    for e in single:
+        o, complete = eval_tree_array(tree, np.array([[e[0]]], dtype=dtype), opts)
+        assert complete is bool(np.isfinite(e[1])), (fn, e[0])
+        if complete:
+            entries.append(e)
+            outs.append(float(o[0]))
+    xs = np.array([e[0] for e in entries[:len(entries) - len(outs)]], dtype=dtype)
+    out, complete = eval_tree_array(tree, xs[None, :], opts)
+    assert complete, fn
+    out = np.concatenate([np.asarray(out, dtype=np.float64), np.array(outs, dtype=np.float64)])
+    err = ulp_errors(dtype, out, entries)
+    worst = int(np.argmax(err))
+    fin = entries
+    print(f"{dtype_name} {fn}: n={len(entries)} max_ulp={float(err.max()):.3f} "
+          f"correctly_rounded={float(np.mean(err <= 0.5)):.4f}")
+    assert float(err.max()) <= (0.5 if fn == "sqrt" else 1.0), (fn, fin[worst][0], float(out[worst]), float(err.max()))

@@ -13,7 +13,8 @@ from oracle import Oracle
 from sr_amd import (Dataset, Node, Options, batch, eval_loss, eval_loss_batch, eval_tree_array, eval_tree_array_batch,
                     flatten_trees, gen_random_population, parse_expression)
 from sr_amd import _lib
-from parity_util import PERTURB_SEEDS, well_conditioned
+from parity_util import PERTURB_SEEDS, assert_losses_within, loss_tolerance
+
 
 pytestmark = pytest.mark.gpu
 
@@ -144,17 +145,17 @@ def test_population_f32_vs_oracle(opts_kw, n, n_trees, seed):
     tb = flatten_trees(trees, np.float32)
     loss, comp = eval_loss_batch(tb, Dataset(X, y), opts)
     orc = Oracle.from_options(opts)
-    good, o_loss, o_comp = well_conditioned(orc, tb, X, y)
+    tol, o_loss, o_comp, n_wide = loss_tolerance(orc, tb, X, y)
     mism = np.nonzero(comp != o_comp)[0]
     assert len(mism) == 0, [(int(k), sr_amd.string_tree(tb.tree(int(k)), opts.operators)) for k in mism[:5]]
     assert np.all(np.isinf(loss[~comp]))
-    assert good.sum() > 0.8 * comp.sum()
-    r = _rel(loss[good], o_loss[good])
-    assert np.max(r) < 1e-4, (np.argmax(r), np.max(r))
-    assert np.median(r) < 1e-6
+    # every complete tree, no exclusions: the 1e-4 bar, or 4x the tree's own libm spread
+    assert_losses_within(loss, o_loss, comp, tol)
+    assert n_wide < 0.2 * comp.sum()
+    assert np.median(_rel(loss[comp], o_loss[comp])) < 1e-6
     # against the reference-order accumulation (sequential f32 fold) too
     ref_loss, _ = orc.eval_loss_batch(tb, X, y, accum="ref", n_threads=8)
-    assert np.max(_rel(loss[good], ref_loss[good])) < 1e-4
+    assert_losses_within(loss, ref_loss, comp, np.maximum(tol, 1e-4 * np.abs(ref_loss.astype(np.float64))))
 
 
 def test_population_f64_vs_oracle():
@@ -182,17 +183,25 @@ def test_predictions_vs_oracle():
         o, c = orc.eval_tree_array(tb, k, X)
         assert comp[k] == c, (k, sr_amd.string_tree(tb.tree(k), opts.operators))
         if c:
-            # rows whose value moves under +-1-ulp libm perturbations are rounding-dominated
-            # (cancellation, or a floor/sign/comparison sitting on its threshold): excluded
-            scale = np.maximum(np.abs(o.astype(np.float64)), 1e-3)
-            okrow = np.ones(o.shape, dtype=bool)
+            # every row: 1e-4 relative (1e-6 absolute near zero), or 4x the row's own spread under
+            # +-1-ulp libm perturbations (cancellation, or a floor/sign/comparison sitting on its
+            # threshold, amplifies last-bit libm differences)
+            o64 = o.astype(np.float64)
+            spread = np.zeros(o.shape)
             for seed in PERTURB_SEEDS:
                 p, _ = orc.eval_tree_array(tb, k, X, perturb=seed)
-                okrow &= np.abs(p - o) <= 2e-5 * scale
-            compared += int(okrow.sum())
-            total += okrow.size
-            np.testing.assert_allclose(out[k][okrow], o[okrow], rtol=1e-4, atol=1e-6)
-    assert compared > 0.8 * total  # most rows of complete trees are well-conditioned
+                with np.errstate(invalid="ignore"):
+                    d = np.abs(p.astype(np.float64) - o64)
+                spread = np.maximum(spread, np.where(np.isfinite(d), d, np.inf))
+            tol = np.maximum(1e-4 * np.abs(o64) + 1e-6, 4 * spread)
+            dev = out[k].astype(np.float64)
+            same_nonfinite = (~np.isfinite(dev)) & (~np.isfinite(o64)) & ((dev == o64) | (np.isnan(dev) & np.isnan(o64)))
+            with np.errstate(invalid="ignore"):
+                ok = same_nonfinite | (np.abs(dev - o64) <= tol)
+            compared += int(np.sum(spread <= 2e-5 * np.maximum(np.abs(o64), 1e-3)))
+            total += o.size
+            assert ok.all(), (k, sr_amd.string_tree(tb.tree(k), opts.operators), np.nonzero(~ok)[0][:5])
+    assert compared > 0.8 * total  # most rows of complete trees are well-conditioned (plain bar)
 
 
 def test_weighted_and_gather_vs_oracle():
@@ -204,16 +213,16 @@ def test_weighted_and_gather_vs_oracle():
     tb = flatten_trees(trees, np.float32)
     orc = Oracle.from_options(opts)
     loss, comp = eval_loss_batch(tb, d, opts)
-    good, ol, oc = well_conditioned(orc, tb, X, y, w=w)
+    tol, ol, oc, _ = loss_tolerance(orc, tb, X, y, w=w)
     assert np.array_equal(comp, oc)
-    assert np.max(_rel(loss[good], ol[good])) < 1e-4
+    assert_losses_within(loss, ol, comp, tol)
     # SubDataset (minibatch with replacement): gather path
     idx = np.random.default_rng(15).integers(0, 6000, size=1500)
     sub = batch(d, idx)
     loss, comp = eval_loss_batch(tb, sub, opts)
-    good, ol, oc = well_conditioned(orc, tb, X[:, idx], y[idx], w=w[idx])
+    tol, ol, oc, _ = loss_tolerance(orc, tb, X[:, idx], y[idx], w=w[idx])
     assert np.array_equal(comp, oc)
-    assert np.max(_rel(loss[good], ol[good])) < 1e-4
+    assert_losses_within(loss, ol, comp, tol)
 
 
 def test_l1_loss_vs_oracle():
@@ -221,9 +230,9 @@ def test_l1_loss_vs_oracle():
     X, y = _c2_data(2048, seed=21)
     tb = flatten_trees(gen_random_population(600, opts, 5, seed=21), np.float32)
     loss, comp = eval_loss_batch(tb, Dataset(X, y), opts)
-    good, ol, oc = well_conditioned(Oracle.from_options(opts), tb, X, y, loss_kind=1)
+    tol, ol, oc, _ = loss_tolerance(Oracle.from_options(opts), tb, X, y, loss_kind=1)
     assert np.array_equal(comp, oc)
-    assert np.max(_rel(loss[good], ol[good])) < 1e-4
+    assert_losses_within(loss, ol, comp, tol)
 
 
 # ------------------------------------------------------------------ edge cases
@@ -281,9 +290,9 @@ def test_ragged_sizes_and_determinism():
         l1, c1 = eval_loss_batch(tb, d, opts)
         l2, c2 = eval_loss_batch(tb, d, opts)
         assert np.array_equal(l1, l2) and np.array_equal(c1, c2)  # bit-reproducible
-        good, ol, oc = well_conditioned(orc, tb, X, y)
+        tol, ol, oc, _ = loss_tolerance(orc, tb, X, y)
         assert np.array_equal(c1, oc), n
-        assert np.max(_rel(l1[good], ol[good]), initial=0.0) < 1e-4, n
+        assert_losses_within(l1, ol, c1, tol, n)
 
 
 def test_chunked_batch_matches_pieces(monkeypatch):
@@ -302,9 +311,9 @@ def test_chunked_batch_matches_pieces(monkeypatch):
     assert np.array_equal(comp, np.concatenate([p[1] for p in parts]))
     assert np.array_equal(loss, np.concatenate([p[0] for p in parts]))
     sub = flatten_trees(trees[6500:7300], np.float32)  # straddles a chunk boundary
-    good, ol, oc = well_conditioned(Oracle.from_options(opts), sub, X, y)
+    tol, ol, oc, _ = loss_tolerance(Oracle.from_options(opts), sub, X, y)
     assert np.array_equal(comp[6500:7300], oc)
-    assert np.max(_rel(loss[6500:7300][good], ol[good])) < 1e-4
+    assert_losses_within(loss[6500:7300], ol, oc, tol)
     bad = list(trees)
     bad[8500] = Node(feature=9)  # feature out of range, in the last chunk
     with pytest.raises(sr_amd.SRError, match="tree 8500"):
@@ -401,7 +410,7 @@ def test_row_sharded_partials_match_single():
     out = np.empty(tb.n_trees, dtype=np.float32)
     comp = np.empty(tb.n_trees, dtype=np.uint8)
     _lib.check(_lib.lib.sr_finalize_losses(_lib.SR_DTYPE_F32, tb.n_trees, sums.ctypes.data_as(ctypes.c_void_p),
-                                           flags.ctypes.data_as(ctypes.c_void_p), float(n), None, 0, 0, None,
+                                           flags.ctypes.data_as(ctypes.c_void_p), float(n), None, 0, None,
                                            out.ctypes.data_as(ctypes.c_void_p), comp.ctypes.data_as(ctypes.c_void_p)))
     assert np.array_equal(comp.astype(bool), full_comp)
     assert np.max(_rel(out[full_comp], full_loss[full_comp])) < 1e-6
@@ -426,9 +435,68 @@ def test_row_block_bound_keeps_results(monkeypatch, max_rb):
     assert np.array_equal(fin, np.isfinite(loss))
     assert np.max(_rel(loss[fin], ref_loss[fin]), initial=0.0) < 1e-6
     sub = flatten_trees([trees.tree(i) for i in range(0, 1500, 15)], np.float32)
-    good, ol, oc = well_conditioned(Oracle.from_options(opts), sub, X, y)
+    tol, ol, oc, _ = loss_tolerance(Oracle.from_options(opts), sub, X, y)
     assert np.array_equal(comp[::15], oc)
-    assert np.max(_rel(loss[::15][good], ol[good]), initial=0.0) < 1e-4
+    assert_losses_within(loss[::15], ol, oc, tol)
     d2.free_device()
     d.free_device()
     ctx.close()
+
+
+# ------------------------------------------------------------------ exact validity path (Julia order)
+def _adversarial_columns():
+    """Checked arrays on which an exact (f64) sum and Julia's T-precision pairwise sum disagree
+    (tests/test_jsum.py pins the verdicts on the CPU)."""
+    from test_jsum import cases
+
+    return {k: v for k, v in cases().items() if k not in ("one", "fifteen")}
+
+
+@pytest.mark.parametrize("name", list(_adversarial_columns()))
+def test_exact_path_follows_julia_sum_order(name):
+    """Flags of trees whose checked arrays are the adversarial columns: the device (deferred checks
+    -> BIG -> EXACT pass) must agree with the oracle's isfinite(Julia sum) bit for bit."""
+    col = _adversarial_columns()[name]
+    n = len(col)
+    X = np.stack([col, np.zeros(n, np.float32), np.ones(n, np.float32)]).astype(np.float32)
+    y = np.zeros(n, dtype=np.float32)
+    opts = Options(binary_operators=["+", "-", "*", "/"], unary_operators=["cos"])
+    exprs = ["x1 * 1.0", "(x1 * 1.0) + (x2 * 0.0)", "cos(x2) * (x1 * x3)", "(x1 - x2) / (x3 * 1.0)", "x1 + x2"]
+    tb = flatten_trees([parse_expression(e, opts) for e in exprs], np.float32)
+    _, comp = eval_loss_batch(tb, Dataset(X, y), opts)
+    _, oc = Oracle.from_options(opts).eval_loss_batch(tb, X, y, n_threads=4)
+    assert list(comp) == list(oc), (name, list(zip(exprs, comp, oc)))
+
+
+def test_row_sharded_packed_with_exact_path():
+    """Two row shards on one GPU through the multi-GPU building blocks — packed partials (one
+    all-reduce's worth), Julia-order folds per shard (the boundary falls inside a leaf block),
+    sr_jsum_finite, sr_finalize_losses — equal the single-GPU result bit for bit in the flags."""
+    from sr_amd.distributed import finalize, gpu_jsum, gpu_max_checks, gpu_partials_packed, jsum_finite, unpack_flags
+    from test_jsum import cases
+
+    opts = Options(**C2_OPTS)
+    n = 9000
+    X, y = _c2_data(n, seed=91)
+    X[2] = np.resize(cases()["mixed_overflow_pairwise"], n)  # x3 carries +-2e35 blocks
+    X[4, :4000] = 3e38 / 4000 * 1.3                           # x5's array sums just past FLT_MAX
+    trees = gen_random_population(600, opts, 5, seed=91)
+    trees += [parse_expression(e, opts) for e in ("x3 * 1.0", "x3 + x1", "x5 * 1.0", "(x5 * 0.5) + (x1 * 1.0)")]
+    tb = flatten_trees(trees, np.float32)
+    full_loss, full_comp = eval_loss_batch(tb, Dataset(X, y), opts)
+    cut = 4321
+    shards = [Dataset(np.ascontiguousarray(X[:, :cut]), np.ascontiguousarray(y[:cut])),
+              Dataset(np.ascontiguousarray(X[:, cut:]), np.ascontiguousarray(y[cut:]))]
+    packed = sum(gpu_partials_packed(tb, sh, opts, n) for sh in shards)
+    sums, flags = unpack_flags(packed)
+    big = np.nonzero(((flags & (_lib.SR_FLAG_NONFINITE | _lib.SR_FLAG_STATIC)) == 0) & ((flags & _lib.SR_FLAG_BIG) != 0))[0]
+    assert big.size >= 2
+    mc = gpu_max_checks(tb, opts)
+    folds = [gpu_jsum(tb, sh, opts, big, mc, off, n) for sh, off in zip(shards, (0, cut))]
+    fin = jsum_finite(np.float32, n, [0, cut, n], [f.reshape(big.size * mc, -1) for f in folds])
+    ok = fin.reshape(big.size, mc).all(axis=1)
+    loss, comp = finalize(np.float32, sums, flags, float(n), big, ok)
+    assert np.array_equal(comp, full_comp)
+    assert np.max(_rel(loss[full_comp], full_loss[full_comp]), initial=0.0) < 1e-6
+    _, oc = Oracle.from_options(opts).eval_loss_batch(tb, X, y, n_threads=8)
+    assert np.array_equal(comp, oc)
