@@ -209,6 +209,12 @@ int sr_compile_info(int dtype, int n_unary, const char* const* unary_names, int 
                     int64_t nfeatures, int32_t* out_len, uint8_t* out_static_bad, int32_t* out_max_depth,
                     void* out_code, int64_t code_capacity);
 
+/*
+ * Host-side evaluation of one unary operator (the code constant folding uses; the device runs the
+ * same functions): out[i] = op(x[i]) for n values of dtype.  For testing host/device agreement.
+ */
+int sr_host_unary(int dtype, const char* name, int64_t n, const void* x, void* out);
+
 /* Timing of the last device call on this context (ms): kernel-only, via HIP events. */
 int sr_last_kernel_ms(sr_ctx* ctx, double* eval_ms, double* total_ms);
 

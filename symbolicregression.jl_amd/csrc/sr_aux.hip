@@ -141,9 +141,7 @@ hipError_t sr_launch_basic_loss(const SrEvalArgs<T>& a, int n_blocks, hipStream_
 // register-stack kernel, 4 / 8 the classic one).
 int sr_vstk_rows(int64_t n_rows, int requested) {
   if (requested == 16 || requested == 32) return requested;
-  if (requested != 0) return 0;
-  if (n_rows >= 65536) return 32;
-  if (n_rows >= 8192) return 16;
+  (void)n_rows;  // off by default: see DESIGN.md §4 (register pressure of the two VGPR slots)
   return 0;
 }
 

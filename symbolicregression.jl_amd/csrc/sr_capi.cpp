@@ -163,6 +163,7 @@ struct sr_dataset {
   void* w = nullptr;  // [ld] or NULL
   std::vector<double> w_host;  // weights (for Σw of SubDataset views)
   double wsum = 0.0;
+  double max_abs_x = 0.0;  // max |X| over the data (NaN / Inf if any value is non-finite)
 };
 
 namespace {
@@ -476,6 +477,7 @@ int run_batch(sr_ctx* ctx, const sr_dataset* ds, int opset_id, const sr_tree_bat
       a.stack_depth = vstk ? std::min(depth, 2) : depth;  // (the register-stack trees need <= 2)
       // Σ over n_total rows of values below tbig cannot overflow T, even with rounding slack.
       a.tbig = T(t_max<T>() / (2.0 * double(n_total > 0 ? n_total : 1)));
+      a.track_x = !(ds->max_abs_x < double(a.tbig)) ? 1 : 0;
       a.loss_kind = lkind;
       a.loss_param = T(lparam);
       a.part_sum = ctx->part_sum.as<double>() + size_t(n_rb) * size_t(t0 + p0);
@@ -840,6 +842,17 @@ int upload_impl(sr_ctx* ctx, const void* X, int64_t nf, int64_t n, const void* y
     delete ds;
     return set_error(SR_ERR_HIP, std::string(what) + ": " + hipGetErrorString(e));
   };
+  {
+    const T* xh = static_cast<const T*>(X);
+    double m = 0.0;
+    bool bad = false;
+    for (int64_t i = 0; i < nf * n; ++i) {
+      const double v = std::fabs(double(xh[i]));
+      bad |= !std::isfinite(v);
+      m = v > m ? v : m;
+    }
+    ds->max_abs_x = bad ? double(INFINITY) : m;
+  }
   hipError_t e;
   if ((e = hipMalloc(&ds->X, size_t(nf) * size_t(ds->ld) * sizeof(T))) != hipSuccess) return fail(e, "hipMalloc X");
   void* tmp = nullptr;
@@ -1424,6 +1437,20 @@ int sr_compile_info(int dtype, int n_unary, const char* const* unary_names, int 
     return report(prog);
   }
   return set_error(SR_ERR_INVALID_ARG, "unknown dtype");
+}
+
+int sr_host_unary(int dtype, const char* name, int64_t n, const void* x, void* out) {
+  const uint32_t id = name ? sr_unary_id(name) : 0;
+  if (!id) return set_error(SR_ERR_UNSUPPORTED_OP, std::string("unsupported unary operator: ") + (name ? name : "(null)"));
+  if (n < 0 || (n > 0 && (!x || !out))) return set_error(SR_ERR_INVALID_ARG, "bad arguments");
+  if (dtype == SR_DTYPE_F32) {
+    for (int64_t i = 0; i < n; ++i) static_cast<float*>(out)[i] = sr_unary<float>(id, static_cast<const float*>(x)[i]);
+  } else if (dtype == SR_DTYPE_F64) {
+    for (int64_t i = 0; i < n; ++i) static_cast<double*>(out)[i] = sr_unary<double>(id, static_cast<const double*>(x)[i]);
+  } else {
+    return set_error(SR_ERR_INVALID_ARG, "unknown dtype");
+  }
+  return SR_OK;
 }
 
 int sr_last_phase_ms(sr_ctx* ctx, double* out, int n) {

@@ -30,6 +30,8 @@ struct SrEvalArgs {
   int n_groups;                // tree groups (blockIdx = row_block * n_groups + group)
   int stack_depth;             // LDS operand-stack slots per wave (>= 1)
   T tbig;                      // |v| >= tbig may overflow the array-sum check
+  int track_x;                 // the data holds |x| >= tbig or non-finite values: checked feature
+                               // loads join the deferred checks (FAST path)
   int loss_kind;               // SrLossKind
   T loss_param;                // its parameter (HuberLoss delta, QuantileLoss tau, ...)
   // outputs

@@ -21,6 +21,8 @@
 #define SR_HD
 #endif
 
+#include "sr_libm.h"
+
 // ---------------------------------------------------------------------------------------
 // Operator ids (semantic; independent of the position inside options.operators).
 // ---------------------------------------------------------------------------------------
@@ -152,11 +154,12 @@ static_assert(sizeof(SrIns<double>) == 16, "f64 instruction must be 16 bytes");
 // ---------------------------------------------------------------------------------------
 template <typename T> struct SrM;
 template <> struct SrM<float> {
-  static SR_HD inline float exp(float x) { return ::expf(x); }
-  static SR_HD inline float cos(float x) { return ::cosf(x); }
-  static SR_HD inline float sin(float x) { return ::sinf(x); }
+  // exp / cos / sin / log: computed in double and rounded once (sr_libm.h; <= 0.5 + 2^-16 ulp)
+  static SR_HD inline float exp(float x) { return sr_expf(x); }
+  static SR_HD inline float cos(float x) { return sr_cosf(x); }
+  static SR_HD inline float sin(float x) { return sr_sinf(x); }
   static SR_HD inline float tan(float x) { return ::tanf(x); }
-  static SR_HD inline float log(float x) { return ::logf(x); }
+  static SR_HD inline float log(float x) { return sr_logf(x); }
   static SR_HD inline float log2(float x) { return ::log2f(x); }
   static SR_HD inline float log10(float x) { return ::log10f(x); }
   static SR_HD inline float log1p(float x) { return ::log1pf(x); }

@@ -203,6 +203,24 @@ __device__ __forceinline__ P* sr_row_at(P* base, uint32_t meta) {
   return reinterpret_cast<P*>(reinterpret_cast<B*>(base) + (meta << sh));
 }
 
+// A unary operator over a lane's R rows.  Float32 cos / sin take the Cody-Waite fast path for all
+// rows unless some lane holds |x| >= 2^20 (one ballot: the Payne-Hanek path stays out of the loop).
+template <typename T, uint32_t ID, int R>
+__device__ __forceinline__ void sr_unary_rows(T (&v)[R]) {
+  if constexpr (sizeof(T) == 4 && (ID == SR_U_COS || ID == SR_U_SIN)) {
+    bool slow = false;
+#pragma unroll
+    for (int r = 0; r < R; ++r) slow |= !(__builtin_fabsf(v[r]) < srl::kTrigFastLimit);
+    if (__builtin_amdgcn_ballot_w64(slow) == 0) {
+#pragma unroll
+      for (int r = 0; r < R; ++r) v[r] = (ID == SR_U_COS) ? sr_cosf_fast(v[r]) : sr_sinf_fast(v[r]);
+      return;
+    }
+  }
+#pragma unroll
+  for (int r = 0; r < R; ++r) v[r] = sr_unary<T>(ID, v[r]);
+}
+
 // ------------------------------------------------------------------ dispatch cases
 #define SR_EACH(EXPR)                             \
   _Pragma("unroll") for (int r = 0; r < R; ++r) { \
@@ -223,20 +241,26 @@ __device__ __forceinline__ P* sr_row_at(P* base, uint32_t meta) {
       if (r + 3 < R) mrun1 = SrMaxAbs<T>::step(mrun1, tos[r + 2], tos[r + 3]); \
     }                                                                     \
   }
-#define SR_UCASE_GEN(ID, ENABLED)                                 \
-  case SR_OP_UNARY0 + ID: {                                       \
-    if (ENABLED) {                                                \
-      SR_EACH(sr_unary<T>(ID, x));                                \
-      SR_TRACK();                                                 \
-    }                                                             \
-    break;                                                        \
-  }                                                               \
-  case SR_OP_UNARY_INF0 + ID: {                                   \
-    if (ENABLED) {                                                \
-      SR_EACH(sr_isfinite(x) ? sr_unary<T>(ID, x) : sr_inf<T>()); \
-      SR_TRACK();                                                 \
-    }                                                             \
-    break;                                                        \
+// The fused unary (UNARY_INF: non-finite input -> +Inf) needs its own body only where checks are
+// per node: under the deferred checks (FAST_CHECK) the fused node's input is itself a tracked
+// operator output, so a non-finite input already marks the tree incomplete and the fused node's
+// value no longer matters — both opcodes share one body (half the transcendental code).
+#define SR_UCASE_GEN(ID, ENABLED)                                   \
+  case SR_OP_UNARY_INF0 + ID:                                       \
+    if constexpr (!FAST_CHECK) {                                    \
+      if (ENABLED) {                                                \
+        SR_EACH(sr_isfinite(x) ? sr_unary<T>(ID, x) : sr_inf<T>()); \
+        SR_TRACK();                                                 \
+      }                                                             \
+      break;                                                        \
+    }                                                               \
+    [[fallthrough]];                                                \
+  case SR_OP_UNARY0 + ID: {                                         \
+    if (ENABLED) {                                                  \
+      sr_unary_rows<T, ID, R>(tos);                                 \
+      SR_TRACK();                                                   \
+    }                                                               \
+    break;                                                          \
   }
 #define SR_UCASE(ID) SR_UCASE_GEN(ID, true)
 #define SR_UCASE_FULL(ID) SR_UCASE_GEN(ID, TIER == SR_TIER_FULL)
@@ -599,6 +623,11 @@ __global__ void __launch_bounds__(W * 64, (SrMinWavesFor<T, R, TIER, W, VSTK>::v
               [[fallthrough]];
             case SR_OP_LOAD_FEAT: {
               L::load(SR_OPND_X(), tos);
+              // a checked feature array (the child of a general unary node) joins the deferred checks
+              // when the data itself can be non-finite or huge (uniform: a dataset property)
+              if (FAST_CHECK && a.track_x && (SR_META() & SR_M_CHECK)) {
+                SR_TRACK();
+              }
               break;
             }
             case SR_OP_LOAD_CONST_PUSH:

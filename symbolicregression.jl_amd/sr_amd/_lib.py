@@ -57,6 +57,7 @@ EXPORTED_SYMBOLS = (
     "sr_dataset_denominator",
     "sr_eval_grad_batch",
     "sr_compile_info",
+    "sr_host_unary",
     "sr_last_kernel_ms",
     "sr_last_phase_ms",
 )
@@ -143,6 +144,7 @@ def _load():
             [c_int, c_int, POINTER(c_char_p), c_int, POINTER(c_char_p), POINTER(SrTreeBatch), c_int64,
              c_int64, P, P, POINTER(c_int), P, c_int64],
         ),
+        "sr_host_unary": (c_int, [c_int, c_char_p, c_int64, P, P]),
         "sr_last_kernel_ms": (c_int, [P, POINTER(c_double), POINTER(c_double)]),
         "sr_last_phase_ms": (c_int, [P, POINTER(c_double), c_int]),
     }

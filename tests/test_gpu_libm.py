@@ -65,8 +65,9 @@ def test_device_libm_within_one_ulp(ulp_fixture, dtype_name, fn):
     # sum overflows, make the whole tree incomplete (and its array is not returned).  Points whose
     # value could do that are evaluated one by one; overflowing ones must come back incomplete.
     big = float(np.finfo(dtype).max) / (4 * len(everything))
-    single = [e for e in everything if not abs(e[1]) <= big]
-    entries = [e for e in everything if abs(e[1]) <= big]
+    small = [abs(e[1]) <= big and abs(e[0]) <= big for e in everything]  # (the input array is checked too)
+    single = [e for e, ok in zip(everything, small) if not ok]
+    entries = [e for e, ok in zip(everything, small) if ok]
     outs = []
     for e in single:
         o, complete = eval_tree_array(tree, np.array([[e[0]]], dtype=dtype), opts)
@@ -84,3 +85,56 @@ def test_device_libm_within_one_ulp(ulp_fixture, dtype_name, fn):
     print(f"{dtype_name} {fn}: n={len(entries)} max_ulp={float(err.max()):.3f} "
           f"correctly_rounded={float(np.mean(err <= 0.5)):.4f}")
     assert float(err.max()) <= (0.5 if fn == "sqrt" else 1.0), (fn, fin[worst][0], float(out[worst]), float(err.max()))
+
+
+def host_unary(dtype, fn, xs):
+    import ctypes
+
+    from sr_amd import _lib
+
+    xs = np.ascontiguousarray(xs, dtype=dtype)
+    out = np.empty_like(xs)
+    _lib.check(_lib.lib.sr_host_unary(_lib.SR_DTYPE_F32 if dtype == np.float32 else _lib.SR_DTYPE_F64, fn.encode(),
+                                      xs.size, xs.ctypes.data_as(ctypes.c_void_p), out.ctypes.data_as(ctypes.c_void_p)))
+    return out
+
+
+@pytest.mark.parametrize("fn", ["exp", "log", "cos", "sin"])
+def test_host_libm_f32_within_half_ulp_plus(ulp_fixture, fn):
+    """CPU: the library's Float32 exp/log/cos/sin (sr_libm.h; the device runs the same code) are
+    within 0.5 + 2^-16 ulp of the exact value on every fixture point."""
+    entries = ulp_fixture["float32"][fn]
+    xs = np.array([e[0] for e in entries], dtype=np.float32)
+    with np.errstate(all="ignore"):
+        out = host_unary(np.float32, fn, xs)
+    hi = np.array([e[1] for e in entries])
+    fin = np.isfinite(hi)
+    if fn == "exp":
+        assert np.all(np.isinf(out[~fin]))
+    err = ulp_errors(np.float32, out[fin], [e for e, f in zip(entries, fin) if f])
+    assert float(err.max()) <= 0.5 + 2 ** -16, (fn, float(err.max()))
+
+
+@pytest.mark.parametrize("fn", ["exp", "log", "cos", "sin"])
+def test_host_libm_f32_random_vs_glibc(fn):
+    """CPU, 400k random Float32 points per function: equal to glibc's float64 result rounded to
+    Float32 except where that value sits within 2^-30 of a rounding midpoint (then <= 1 ulp apart)."""
+    rng = np.random.default_rng(7)
+    if fn == "exp":
+        xs = rng.uniform(-103, 88.7, 400_000)
+    elif fn == "log":
+        xs = np.exp(rng.uniform(-87, 88, 400_000))
+    else:
+        xs = np.concatenate([rng.uniform(-20, 20, 200_000), np.exp(rng.uniform(0, 88, 200_000)) * rng.choice([-1, 1], 200_000)])
+    xs = xs.astype(np.float32)
+    with np.errstate(all="ignore"):
+        out = host_unary(np.float32, fn, xs).astype(np.float64)
+        ref64 = getattr(np, fn)(xs.astype(np.float64))
+    ref = ref64.astype(np.float32).astype(np.float64)
+    diff = out != ref
+    ulp = np.spacing(np.abs(ref).astype(np.float32)).astype(np.float64)
+    # glibc double results are within 1 double ulp: a Float32 rounding of it can only differ from the
+    # correctly rounded value when the exact value is that close to a midpoint
+    mid = np.abs(np.abs(ref64 - ref) - ulp / 2) <= np.abs(ref64) * 2.0 ** -30
+    assert np.all(np.abs(out - ref)[diff] <= ulp[diff]), fn
+    assert np.all(mid[diff]), (fn, int(diff.sum()), xs[diff & ~mid][:5])

@@ -20,13 +20,23 @@ mixes = {
     "cos-only": dict(binary_operators=["+", "*"], unary_operators=["cos"]),
     "exp-only": dict(binary_operators=["+", "*"], unary_operators=["exp"]),
     "sin-only": dict(binary_operators=["+", "*"], unary_operators=["sin"]),
+    "log-only": dict(binary_operators=["+", "*"], unary_operators=["log"]),
+    "C2-complete": "C2(+-*/ cos exp log)",
+    "C2-dead": "C2(+-*/ cos exp log)",
 }
 only = sys.argv[1:]  # optional: mix names to run (profiling one population at a time)
 for name, kw in mixes.items():
     if only and not any(name.startswith(o) for o in only):
         continue
-    opts = Options(**kw)
-    tb = flatten_trees(gen_random_population(10000, opts, 5, seed=1), DT)
+    if isinstance(kw, str):  # a subset of another population: its complete or its dead trees
+        opts = Options(**mixes[kw])
+        full = gen_random_population(10000, opts, 5, seed=1)
+        _, c0 = eval_loss_batch(flatten_trees(full, DT), ds, opts)
+        keep = c0 if name.endswith("complete") else ~c0
+        tb = flatten_trees([t for t, k in zip(full, keep) if k], DT)
+    else:
+        opts = Options(**kw)
+        tb = flatten_trees(gen_random_population(10000, opts, 5, seed=1), DT)
     eval_loss_batch(tb, ds, opts)
     ks, ts, ph = [], [], []
     for _ in range(5):
