@@ -4,9 +4,19 @@
 Julia side of the drop-in: binds `libsr_amd.so` (include/sr_amd.h) with `ccall` and routes
 SymbolicRegression's scoring (`_eval_loss`, src/LossFunctions.jl:90-117) through it when the
 options are wrapped in `MI355XOptions` — the `AbstractOptions` extension mechanism the reference
-documents (src/OptionsStruct.jl:124-175).  Batched entry points (`eval_loss_batch`,
-`eval_cost_batch!`) score a whole population per launch for the `Population` / `finalize_costs`
-call sites (src/Population.jl:35-61, 182-196).
+documents (src/OptionsStruct.jl:124-175).
+
+Batching without touching the reference's search code:
+* `finalize_costs` (src/Population.jl:182-196) is overridden for `MI355XOptions`: one launch per
+  population;
+* every other scoring call site (`Population` init src/Population.jl:35-61, `next_generation`
+  src/Mutate.jl:270, `crossover_generation` :699-705, constant optimisation, the reload sites) calls
+  `_eval_loss` for one tree.  Under `parallelism=:multithreading` the islands run as concurrent
+  tasks (src/SearchUtils.jl:289-308) whose calls arrive together: the `BatchScorer` below holds each
+  call for a short window and scores everything that arrived in ONE launch, so the islands advance
+  in lock-step while each island keeps its serial semantics (it waits for its own result).
+* an operator, loss or expression type outside the device catalog keeps the reference's own CPU
+  path (`SR_ERR_UNSUPPORTED_OP` -> `_eval_loss(…, options.base, …)`), as INTEGRATION.md states.
 
 Not exercised in this repository's CI (no Julia runtime in the build image); the Python mirror in
 `../sr_amd` makes the same calls and is what the tests run.
@@ -14,8 +24,8 @@ Not exercised in this repository's CI (no Julia runtime in the build image); the
 module SymbolicRegressionMI355X
 
 using SymbolicRegression
-using SymbolicRegression: AbstractOptions, Dataset, LossFunctionsModule
-using DynamicExpressions: AbstractExpressionNode, AbstractExpression, get_tree, get_operators
+using SymbolicRegression: AbstractOptions, Dataset, LossFunctionsModule, PopulationModule
+using DynamicExpressions: AbstractExpressionNode, AbstractExpression, Expression, Node, get_tree, get_operators
 
 const LIB = get(ENV, "SR_AMD_LIB", joinpath(@__DIR__, "..", "lib", "libsr_amd.so"))
 
@@ -40,8 +50,9 @@ check(rc) = rc == SR_OK || error("libsr_amd error $(rc): $(last_error())")
 
 mutable struct DeviceContext
     handle::Ptr{Cvoid}
-    opsets::Dict{Any,Cint}
+    opsets::Dict{Any,Union{Cint,Nothing}}   # nothing: an operator outside the device catalog
     datasets::IdDict{Any,Ptr{Cvoid}}
+    lock::ReentrantLock
 end
 
 const CONTEXT = Ref{Union{DeviceContext,Nothing}}(nothing)
@@ -51,40 +62,53 @@ function context()
         dev = parse(Int, get(ENV, "LOCAL_RANK", "0"))   # one process per GPU
         h = Ref{Ptr{Cvoid}}(C_NULL)
         check(ccall((:sr_init, LIB), Cint, (Cint, Ref{Ptr{Cvoid}}), dev, h))
-        CONTEXT[] = DeviceContext(h[], Dict{Any,Cint}(), IdDict{Any,Ptr{Cvoid}}())
+        CONTEXT[] = DeviceContext(h[], Dict{Any,Union{Cint,Nothing}}(), IdDict{Any,Ptr{Cvoid}}(), ReentrantLock())
     end
     return CONTEXT[]::DeviceContext
 end
 
-"""Register `options.operators` once (names as DynamicExpressions prints them)."""
+"""Register `options.operators` once (names as DynamicExpressions prints them); `nothing` when an
+operator is outside the device catalog (the caller keeps the CPU path)."""
 function opset_id(ctx::DeviceContext, operators)
     key = (operators.unaops, operators.binops)
-    get!(ctx.opsets, key) do
-        un = [string(nameof(f)) for f in operators.unaops]
-        bi = [string(nameof(f)) for f in operators.binops]
-        id = Ref{Cint}(0)
-        rc = ccall((:sr_register_opset, LIB), Cint,
-                   (Ptr{Cvoid}, Cint, Ptr{Cstring}, Cint, Ptr{Cstring}, Ref{Cint}),
-                   ctx.handle, length(un), un, length(bi), bi, id)
-        rc == SR_ERR_UNSUPPORTED_OP && throw(ArgumentError(last_error()))
-        check(rc)
-        id[]
+    lock(ctx.lock) do
+        get!(ctx.opsets, key) do
+            un = [string(nameof(f)) for f in operators.unaops]
+            bi = [string(nameof(f)) for f in operators.binops]
+            id = Ref{Cint}(0)
+            rc = ccall((:sr_register_opset, LIB), Cint,
+                       (Ptr{Cvoid}, Cint, Ptr{Cstring}, Cint, Ptr{Cstring}, Ref{Cint}),
+                       ctx.handle, length(un), un, length(bi), bi, id)
+            rc == SR_ERR_UNSUPPORTED_OP && return nothing
+            check(rc)
+            id[]
+        end
     end
 end
 
 """Upload `dataset.X` ([nfeatures, n], column-major: exactly the ABI layout), y, weights once."""
 function device_dataset(ctx::DeviceContext, dataset::Dataset{T}) where {T}
-    get!(ctx.datasets, dataset) do
-        X = Matrix{T}(dataset.X)
-        out = Ref{Ptr{Cvoid}}(C_NULL)
-        w = dataset.weights === nothing ? C_NULL : pointer(Vector{T}(dataset.weights))
-        check(ccall((:sr_dataset_upload, LIB), Cint,
-                    (Ptr{Cvoid}, Cint, Ptr{T}, Int64, Int64, Ptr{T}, Ptr{Cvoid}, Ref{Ptr{Cvoid}}),
-                    ctx.handle, T === Float32 ? SR_DTYPE_F32 : SR_DTYPE_F64, X, size(X, 1), size(X, 2),
-                    Vector{T}(dataset.y), w, out))
-        out[]
+    lock(ctx.lock) do
+        get!(ctx.datasets, dataset) do
+            X = Matrix{T}(dataset.X)
+            y = Vector{T}(dataset.y)
+            w = dataset.weights === nothing ? nothing : Vector{T}(dataset.weights)
+            out = Ref{Ptr{Cvoid}}(C_NULL)
+            # every host buffer stays rooted for the whole call (the library copies them)
+            GC.@preserve X y w begin
+                check(ccall((:sr_dataset_upload, LIB), Cint,
+                            (Ptr{Cvoid}, Cint, Ptr{T}, Int64, Int64, Ptr{T}, Ptr{Cvoid}, Ref{Ptr{Cvoid}}),
+                            ctx.handle, T === Float32 ? SR_DTYPE_F32 : SR_DTYPE_F64, X, size(X, 1), size(X, 2),
+                            y, w === nothing ? C_NULL : Ptr{Cvoid}(pointer(w)), out))
+            end
+            out[]
+        end
     end
 end
+
+"""Trees the device evaluates: plain `Expression{T,Node{T,2}}` / `Node` (parametric and template
+expressions keep their own evaluators on the CPU)."""
+device_tree(t) = t isa Node || (t isa Expression && get_tree(t) isa Node)
 
 """Pre-order struct-of-arrays of many `Node{T,2}` trees (get_scalar_constants order)."""
 function flatten(trees::AbstractVector, ::Type{T}) where {T}
@@ -112,23 +136,31 @@ function flatten(trees::AbstractVector, ::Type{T}) where {T}
     return (; offsets, degree, op, feature, constant, val)
 end
 
-"""Batched `_eval_loss`: losses::Vector{T} and complete::Vector{Bool} for every tree."""
+"""Batched `_eval_loss`: (losses::Vector{L}, complete::Vector{Bool}) for every tree, or `nothing`
+when the device cannot evaluate them (operator, loss or expression type outside its catalog: the
+caller keeps the reference's CPU path)."""
 function eval_loss_batch(trees::AbstractVector, dataset::Dataset{T,L}, options::AbstractOptions;
                          idx::Union{Nothing,AbstractVector{Int}}=nothing) where {T,L}
+    isempty(trees) && return (L[], Bool[])
+    all(device_tree, trees) || return nothing
     ctx = context()
-    ops = get_operators(first(trees), options)
+    oid = opset_id(ctx, get_operators(first(trees), options))
+    lk = loss_kind(options)
+    (oid === nothing || lk === nothing) && return nothing
     f = flatten(trees, T)
     losses = Vector{T}(undef, length(trees))
     complete = Vector{UInt8}(undef, length(trees))
     rows = idx === nothing ? nothing : Int64.(idx .- 1)   # 0-based SubDataset view
-    GC.@preserve f rows begin
+    dsh = device_dataset(ctx, dataset)
+    GC.@preserve f rows losses complete begin
         b = SrTreeBatch(length(trees), pointer(f.offsets), pointer(f.degree), pointer(f.op),
                         pointer(f.feature), pointer(f.constant), Ptr{Cvoid}(pointer(f.val)))
-        check(ccall((:sr_eval_loss_batch, LIB), Cint,
-                    (Ptr{Cvoid}, Ptr{Cvoid}, Cint, Ref{SrTreeBatch}, Ptr{Int64}, Int64, Cint, Ptr{T}, Ptr{UInt8}),
-                    ctx.handle, device_dataset(ctx, dataset), opset_id(ctx, ops), b,
-                    rows === nothing ? C_NULL : pointer(rows), rows === nothing ? 0 : length(rows),
-                    loss_kind(options), losses, complete))
+        rc = ccall((:sr_eval_loss_batch, LIB), Cint,
+                   (Ptr{Cvoid}, Ptr{Cvoid}, Cint, Ref{SrTreeBatch}, Ptr{Int64}, Int64, Cint, Ptr{T}, Ptr{UInt8}),
+                   ctx.handle, dsh, oid, b, rows === nothing ? C_NULL : pointer(rows),
+                   rows === nothing ? 0 : length(rows), lk, losses, complete)
+        rc == SR_ERR_UNSUPPORTED_OP && return nothing
+        check(rc)
     end
     return L.(losses), complete .== 0x01
 end
@@ -155,73 +187,168 @@ loss_spec(l::LF.L2MarginLoss) = (15, 0.0)
 loss_spec(l::LF.ExpLoss) = (16, 0.0)
 loss_spec(l::LF.SigmoidLoss) = (17, 0.0)
 loss_spec(l::LF.DWDMarginLoss) = (18, Float64(l.q))
-loss_spec(l) = throw(ArgumentError("elementwise_loss $(typeof(l)) stays on the CPU path"))
+loss_spec(l) = nothing  # any other elementwise loss (or a custom function) stays on the CPU path
 
 const LOSS_CODES = Dict{Tuple{Ptr{Cvoid},Int,Float64},Cint}()
 function loss_kind(options)
-    kind, param = loss_spec(options.elementwise_loss)
+    spec = loss_spec(options.elementwise_loss)
+    spec === nothing && return nothing
+    kind, param = spec
     (kind in (0, 1, 3, 9, 10, 11, 12, 14, 15, 16, 17) || (kind == 4 && param == 1.0)) && return Cint(kind)
     ctx = context()
-    get!(LOSS_CODES, (ctx.handle, kind, param)) do
+    lock(ctx.lock) do; get!(LOSS_CODES, (ctx.handle, kind, param)) do
         code = Ref{Cint}(0)
         check(ccall((:sr_register_loss, LIB), Cint, (Ptr{Cvoid}, Cint, Cdouble, Ref{Cint}),
                     ctx.handle, kind, param, code))
         code[]
-    end
+    end end
 end
 
 """Batched objective + forward-mode gradient for BFGS (src/ConstantOptimization.jl:126-167):
 losses, the gradient of every tree's loss w.r.t. its constants (pre-order, concatenated), complete."""
 function eval_grad_batch(trees::AbstractVector, dataset::Dataset{T,L}, options::AbstractOptions) where {T,L}
+    all(device_tree, trees) || return nothing
     ctx = context()
-    ops = get_operators(first(trees), options)
+    oid = opset_id(ctx, get_operators(first(trees), options))
+    lk = loss_kind(options)
+    (oid === nothing || lk === nothing) && return nothing
     f = flatten(trees, T)
     losses = Vector{T}(undef, length(trees))
     complete = Vector{UInt8}(undef, length(trees))
     grads = zeros(T, count(==(0x01), f.constant) + 1)
-    GC.@preserve f begin
+    dsh = device_dataset(ctx, dataset)
+    GC.@preserve f losses grads complete begin
         b = SrTreeBatch(length(trees), pointer(f.offsets), pointer(f.degree), pointer(f.op),
                         pointer(f.feature), pointer(f.constant), Ptr{Cvoid}(pointer(f.val)))
-        check(ccall((:sr_eval_grad_batch, LIB), Cint,
-                    (Ptr{Cvoid}, Ptr{Cvoid}, Cint, Ref{SrTreeBatch}, Ptr{Int64}, Int64, Cint, Ptr{T}, Ptr{T}, Ptr{UInt8}),
-                    ctx.handle, device_dataset(ctx, dataset), opset_id(ctx, ops), b, C_NULL, 0,
-                    loss_kind(options), losses, grads, complete))
+        rc = ccall((:sr_eval_grad_batch, LIB), Cint,
+                   (Ptr{Cvoid}, Ptr{Cvoid}, Cint, Ref{SrTreeBatch}, Ptr{Int64}, Int64, Cint, Ptr{T}, Ptr{T}, Ptr{UInt8}),
+                   ctx.handle, dsh, oid, b, C_NULL, 0, lk, losses, grads, complete)
+        rc == SR_ERR_UNSUPPORTED_OP && return nothing
+        check(rc)
     end
     return L.(losses), grads[1:end-1], complete .== 0x01
 end
 
-"""Batched `eval_cost` (src/LossFunctions.jl:193-209): fills `costs`, `losses` in place."""
+"""Batched `eval_cost` (src/LossFunctions.jl:193-209): fills `costs`, `losses` in place
+(`loss_to_cost` on the host, exactly as the reference).  Falls back to the reference's own
+`eval_cost` per member when the device cannot evaluate the trees."""
 function eval_cost_batch!(costs::AbstractVector{L}, losses::AbstractVector{L}, dataset::Dataset{T,L}, members,
                           options::AbstractOptions) where {T,L}
-    trees = [m.tree for m in members]
-    l, _ = eval_loss_batch(trees, dataset, options)
+    base = options isa MI355XOptions ? options.base : options
+    idx = SymbolicRegression.CoreModule.get_indices(dataset)
+    full = SymbolicRegression.CoreModule.get_full_dataset(dataset)
+    r = eval_loss_batch([m.tree for m in members], full, options; idx=idx)
     for (i, m) in enumerate(members)
-        losses[i] = l[i]
-        costs[i] = LossFunctionsModule.loss_to_cost(l[i], dataset.use_baseline, dataset.baseline_loss, m, options,
-                                                    m.complexity)
+        if r === nothing
+            costs[i], losses[i] = LossFunctionsModule.eval_cost(dataset, m, base)
+        else
+            l = r[1][i] + LossFunctionsModule.dimensional_regularization(m.tree, dataset, base)
+            losses[i] = l
+            costs[i] = LossFunctionsModule.loss_to_cost(l, dataset.use_baseline, dataset.baseline_loss, m, base,
+                                                        m.complexity)
+        end
     end
     return costs, losses
 end
 
-"""Options wrapper selecting the device path: every property forwards to the wrapped options."""
+"""Options wrapper selecting the device path: every property forwards to the wrapped options.
+`coalesce = true` routes single-tree scoring through the `BatchScorer` (lock-step islands)."""
 struct MI355XOptions{O<:AbstractOptions} <: AbstractOptions
     base::O
+    coalesce::Bool
 end
-Base.getproperty(o::MI355XOptions, s::Symbol) = s === :base ? getfield(o, :base) : getproperty(getfield(o, :base), s)
+MI355XOptions(base::AbstractOptions; coalesce::Bool=Threads.nthreads() > 1) = MI355XOptions(base, coalesce)
+Base.getproperty(o::MI355XOptions, s::Symbol) =
+    s === :base ? getfield(o, :base) : s === :coalesce ? getfield(o, :coalesce) : getproperty(getfield(o, :base), s)
 Base.propertynames(o::MI355XOptions) = propertynames(getfield(o, :base))
 
-# Single-tree scoring (every eval_cost call site) routed through the batch kernel.
+# ---------------------------------------------------------------- lock-step coalescing
+# One request per `_eval_loss` call; the scorer task collects every request that arrives within
+# WINDOW_NS of the first (the concurrently running islands reach their next evaluation together),
+# groups them by (dataset, row view, options) and scores each group with ONE launch.
+struct ScoreRequest
+    tree::Any
+    dataset::Any          # the full dataset
+    idx::Any              # row view (SubDataset indices) or nothing
+    options::MI355XOptions
+    reply::Channel{Any}   # Vector{L}-element result, or :fallback
+end
+const QUEUE = Channel{ScoreRequest}(1 << 16)
+const SCORER = Ref{Union{Task,Nothing}}(nothing)
+const WINDOW_NS = Ref{UInt64}(30_000)
+const SCORER_LOCK = ReentrantLock()
+
+function scorer_loop()
+    pending = ScoreRequest[]
+    while true
+        push!(pending, take!(QUEUE))
+        t0 = time_ns()
+        while time_ns() - t0 < WINDOW_NS[]
+            isready(QUEUE) ? push!(pending, take!(QUEUE)) : yield()
+        end
+        groups = Dict{Any,Vector{ScoreRequest}}()
+        for r in pending
+            push!(get!(groups, (objectid(r.dataset), r.idx, objectid(r.options.base)), ScoreRequest[]), r)
+        end
+        for (_, g) in groups
+            res = try
+                eval_loss_batch([r.tree for r in g], g[1].dataset, g[1].options; idx=g[1].idx)
+            catch err
+                err
+            end
+            for (i, r) in enumerate(g)
+                put!(r.reply, res === nothing ? :fallback : res isa Exception ? res : res[1][i])
+            end
+        end
+        empty!(pending)
+    end
+end
+
+function scored_by_batch(tree, full, idx, options::MI355XOptions)
+    lock(SCORER_LOCK) do
+        if SCORER[] === nothing
+            SCORER[] = Threads.@spawn scorer_loop()
+        end
+    end
+    req = ScoreRequest(tree, full, idx, options, Channel{Any}(1))
+    put!(QUEUE, req)
+    r = take!(req.reply)
+    r isa Exception && throw(r)
+    return r
+end
+
+# Single-tree scoring (every eval_cost call site): the device batch kernel, coalesced across
+# concurrently running islands; the reference's own CPU path when the device cannot evaluate it.
 function LossFunctionsModule._eval_loss(tree::Union{AbstractExpression{T},AbstractExpressionNode{T}},
                                         dataset::Dataset{T,L}, options::MI355XOptions,
                                         regularization::Bool)::L where {T,L}
     idx = SymbolicRegression.CoreModule.get_indices(dataset)
     full = SymbolicRegression.CoreModule.get_full_dataset(dataset)
-    l, _ = eval_loss_batch([tree], full, options; idx=idx)
-    loss = l[1]
+    loss = if options.coalesce
+        scored_by_batch(tree, full, idx, options)
+    else
+        r = eval_loss_batch([tree], full, options; idx=idx)
+        r === nothing ? :fallback : r[1][1]
+    end
+    loss === :fallback && return LossFunctionsModule._eval_loss(tree, dataset, options.base, regularization)
     if regularization
         loss += LossFunctionsModule.dimensional_regularization(tree, dataset, options)
     end
     return loss
+end
+
+# `finalize_costs` (src/Population.jl:182-196): one launch for the whole population.
+function PopulationModule.finalize_costs(dataset::Dataset{T,L}, pop::P, options::MI355XOptions
+                                         )::Tuple{P,Float64} where {T,L,P<:PopulationModule.Population{T,L}}
+    options.batching || return (pop, 0.0)
+    costs = Vector{L}(undef, pop.n)
+    losses = Vector{L}(undef, pop.n)
+    eval_cost_batch!(costs, losses, dataset, pop.members, options)
+    for (m, c, l) in zip(pop.members, costs, losses)
+        m.cost = c
+        m.loss = l
+    end
+    return (pop, Float64(pop.n))
 end
 
 end # module

@@ -32,6 +32,8 @@ from dataclasses import dataclass, field
 
 import numpy as np
 
+from . import _lib
+
 from .constant_optimization import optimize_constants_batch
 from .dataset import Dataset, batch
 from .loss import eval_cost_batch, eval_loss_batch, loss_to_cost, update_baseline_loss_
@@ -395,16 +397,33 @@ def best_of_sample(pop, stats, options, so, rng, tweights):
     n = min(options.tournament_selection_n, len(pop))
     members = [pop[i] for i in rng.choice(len(pop), size=n, replace=False)]
     if so.use_frequency_in_tournament:
-        costs = []
-        for m in members:
-            size = m.complexity
-            freq = stats.normalized_frequencies[size - 1] if 0 < size <= options.maxsize else 0.0
-            costs.append(m.cost * math.exp(so.adaptive_parsimony_scaling * freq))
+        # adjusted_costs::Vector{L} (src/Population.jl:124-139): cost * exp(L(scaling) * L(freq)),
+        # every operation in the loss type L (Float32 for Float32 data)
+        L = type(members[0].cost) if isinstance(members[0].cost, np.floating) else np.float64
+        scaling = L(so.adaptive_parsimony_scaling)
+        arg = np.array([scaling * L(stats.normalized_frequencies[m.complexity - 1]
+                                    if 0 < m.complexity <= options.maxsize else 0.0) for m in members], dtype=L)
+        factor = host_exp(arg)
+        costs = [L(m.cost) * factor[i] for i, m in enumerate(members)]
     else:
         costs = [m.cost for m in members]
     ranked = sorted((i for i in range(n) if costs[i] < math.inf), key=lambda i: (costs[i], i))
     place = 0 if options.tournament_selection_p == 1.0 else _draw(tweights, rng)
     return members[ranked[place]] if place < len(ranked) else members[0]
+
+
+def host_exp(x):
+    """exp in the array's own precision with the library's host code (src/Population.jl computes the
+    tournament weights with Julia's exp in L; the library's Float32 exp is correctly rounded but for
+    2^-40-close midpoints, as Julia's Float32 exp)."""
+    import ctypes
+
+    x = np.ascontiguousarray(x)
+    out = np.empty_like(x)
+    dt = _lib.SR_DTYPE_F32 if x.dtype == np.float32 else _lib.SR_DTYPE_F64
+    _lib.check(_lib.lib.sr_host_unary(dt, b"exp", x.size, x.ctypes.data_as(ctypes.c_void_p),
+                                      out.ctypes.data_as(ctypes.c_void_p)))
+    return out
 
 
 def _draw(weights, rng):

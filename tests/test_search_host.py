@@ -138,3 +138,27 @@ def test_vectorised_costs_match_loss_to_cost():
             want = [float(loss_to_cost(losses[k], ds.use_baseline, ds.baseline_loss, Node(val=dt(0)), opts,
                                        int(sizes[k]))) for k in range(len(sizes))]
             assert got.tolist() == want
+
+
+def test_tournament_adjusted_costs_in_loss_type():
+    """src/Population.jl:124-139 computes adjusted_costs::Vector{L} = cost * exp(L(scaling) * L(freq))
+    in L (Float32 for Float32 data).  Two members whose Float32 adjusted costs tie but whose float64
+    ones do not: the tie keeps the first member of the sample (argmin_fast: strict <)."""
+    from types import SimpleNamespace
+
+    from sr_amd.search import best_of_sample
+
+    c = np.float32(1.0320923328399658)
+    f1, f2 = 0.11347446513971259, 0.11347445643963802  # L(f1) != L(f2); exp products tie in Float32
+    m1 = SimpleNamespace(cost=c, complexity=3, name="m1")
+    m2 = SimpleNamespace(cost=c, complexity=4, name="m2")
+    freqs = np.zeros(30)
+    freqs[2], freqs[3] = f1, f2
+    stats = SimpleNamespace(normalized_frequencies=freqs)
+    options = SimpleNamespace(tournament_selection_n=2, tournament_selection_p=1.0, maxsize=30)
+    so = SimpleNamespace(use_frequency_in_tournament=True, adaptive_parsimony_scaling=20.0)
+    assert float(c) * np.exp(20.0 * f2) < float(c) * np.exp(20.0 * f1)  # float64 would pick m2
+    for seed in range(6):
+        order = np.random.default_rng(seed).choice(2, size=2, replace=False)
+        won = best_of_sample([m1, m2], stats, options, so, np.random.default_rng(seed), None)
+        assert won is [m1, m2][order[0]], seed  # Float32 tie: the first sampled member wins
