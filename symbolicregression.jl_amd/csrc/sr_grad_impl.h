@@ -78,6 +78,7 @@ __global__ void __launch_bounds__(W * 64) sr_grad_kernel(const SrGradArgs<T> a) 
 #pragma unroll
   for (int k = 0; k < KT; ++k) acc[k] = 0.0;
   const bool weighted = a.w != nullptr;
+  sr_libm_lds_fill(tid, W * 64);  // libm tables (visible after the first tile's barrier)
 
   for (int tile = 0; tile < a.tiles_per_block; ++tile) {
     const int64_t row0 = (int64_t(rb) * a.tiles_per_block + tile) * ROWS;

@@ -1,20 +1,24 @@
-// sr_libm.h — Float32 exp / log / cos / sin for the evaluator (host + device), computed in double
-// and rounded once.
+// sr_libm.h — Float32 exp / log / cos / sin for the evaluator (host + device).
 //
 // The reference evaluates these with Julia's Base.Math, accurate to < 1 ulp (its Float32 trig and
-// log kernels work in Float64, as these do).  ROCm's OCML Float32 versions measured 1.26-1.75 ulp
-// on the fixture points of tests/golden/libm_ulp.json (profiles/r02_libm_ocml.txt), so the device
-// uses these instead: every fast-path result is within 2^-40 relative of the exact value before the
-// final rounding (polynomial fits and bounds: tools/gen_libm_coeffs.py), i.e. correctly rounded
-// unless the exact value lies within 2^-40 of a rounding midpoint, and never more than
-// 0.5 + 2^-16 ulp off.  MI355X runs FP64 FMA at the FP32 (non-packed) rate, so the double work
-// costs about what OCML's Float32 range reductions and slow-path branches do.
+// log kernels work in Float64).  ROCm's OCML Float32 log / cos / sin measured 1.75 / 1.26 / 1.49 ulp
+// on the fixture points of tests/golden/libm_ulp.json (profiles/r02_libm_ocml.txt), so those three
+// are computed here in double and rounded once, table-driven so the work per value stays close to
+// OCML's: log from a 128-cell table of [1, 2) and a degree-5 log1p, cos / sin from (sin, cos)(k pi/64)
+// and degree-5/4 polynomials on |r| <= pi/128.  Every fast-path result is within 2^-38 relative of
+// the exact value before the final rounding (tools/gen_libm_coeffs.py prints the bounds), i.e.
+// correctly rounded unless the exact value sits that close to a midpoint.  OCML's Float32 exp
+// measured 0.675 ulp and is kept on the device (sr_expf below, also correctly rounded but for
+// 2^-46-close midpoints, serves the host's constant folding).
 //
-// The same functions run on the host (constant folding in sr_compile.cpp, tools/libm_check.cpp):
-// IEEE double with fused multiply-adds and no contraction, so host and device agree bit for bit.
+// The device reads the tables from a per-workgroup LDS copy (sr_libm_lds_fill, every kernel that
+// evaluates operators runs it before its first barrier); the host reads them from constant memory.
+// Host and device run the same double arithmetic (fused multiply-adds, no contraction).
 #pragma once
 #include <math.h>
 #include <stdint.h>
+
+#include "sr_libm_tables.h"
 
 #if defined(__HIPCC__)
 #include <hip/hip_runtime.h>
@@ -48,6 +52,8 @@ constexpr double kLn2Hi = 0x1.62e42fefa39efp-1, kLn2Lo = 0x1.abc9e3b39803fp-56;
 constexpr double kTwoOverPi = 0x1.45f306dc9c883p-1;
 constexpr double kPio2_1 = 0x1.921fb54442d18p+0, kPio2_2 = 0x1.1a62633145c07p-54, kPio2_3 = -0x1.f1976b7ed8fbcp-110;
 constexpr double kSqrtHalf = 0x1.6a09e667f3bcdp-1;
+constexpr double k64OverPi = 0x1.45f306dc9c883p+4;
+constexpr double kPi64_1 = 0x1.921fb54442d18p-5, kPi64_2 = 0x1.1a62633145c07p-59, kPi64_3 = -0x1.f1976b7ed8fbcp-115;
 // 2/pi in 32-bit words: bit 1 of word 0 is the 2^-1 bit (Payne-Hanek reduction of huge arguments)
 constexpr uint32_t kTwoOverPiBits[12] = {0xA2F9836Eu, 0x4E441529u, 0xFC2757D1u, 0xF534DDC0u, 0xDB629599u, 0x3C439041u,
                                          0xFE5163ABu, 0xDEBBC561u, 0xB7246E3Au, 0x424DD2E0u, 0x06492EEAu, 0x09D1921Cu};
@@ -78,17 +84,26 @@ SRL_HD inline float sr_expf(float x) {
   return tiny ? 0.0f : v;
 }
 
-// log(x): x = 2^e m, m in [sqrt(1/2), sqrt(2)), log = e ln2 + log1p(m - 1).
-SRL_HD inline float sr_logf(float x) {
-  int e = 0;
-  double m = frexp(double(x), &e);  // [0.5, 1)
-  const bool lo = m < srl::kSqrtHalf;
-  m = lo ? m * 2.0 : m;
-  const double ed = double(lo ? e - 1 : e);
-  const double f = m - 1.0;  // exact (Sterbenz)
-  const double f2 = f * f;
-  const double l = fma(f2 * f, srl::horner(srl::kLog, f), fma(-0.5, f2, f));
-  const float v = float(fma(ed, srl::kLn2Hi, fma(ed, srl::kLn2Lo, l)));
+// log(x) = e ln2 + logc_k + log1p(m invc_k - 1): x = 2^e m, m in [0.75, 1.5) from the Float32 bits
+// (subnormals scaled by 2^24 first), cell k = the top 7 mantissa bits, |m invc_k - 1| < 2^-7.
+SRL_HD inline float sr_logf_tab(float x, const double* tab) {
+  uint32_t b;
+  __builtin_memcpy(&b, &x, 4);
+  const bool sub = b < 0x00800000u;  // zero / subnormal (x >= 0 here)
+  float xs = sub ? x * 0x1p24f : x;
+  __builtin_memcpy(&b, &xs, 4);
+  const int e = int(b >> 23) - 127 - (sub ? 24 : 0);
+  const uint32_t k = (b >> 16) & 127u;
+  const bool hi = k >= 64u;  // m in [1.5, 2): use m / 2 and e + 1 (x just below 1 keeps e = 0)
+  const uint32_t mb = (b & 0x007fffffu) | (hi ? 0x3f000000u : 0x3f800000u);
+  float mf;
+  __builtin_memcpy(&mf, &mb, 4);
+  const double invc = tab[2 * k], logc = tab[2 * k + 1];
+  const double r = fma(double(mf), invc, -1.0);
+  // log1p(r) = r - r^2/2 + r^3/3 - r^4/4 + r^5/5 (|r| < 2^-8: error < 2^-42 |r|)
+  const double p = fma(r * r, fma(r, fma(r, fma(r, 0.2, -0.25), 0x1.5555555555555p-2), -0.5), r);
+  const double ed = double(hi ? e + 1 : e);
+  const float v = float(fma(ed, srl::kLn2Hi, fma(ed, srl::kLn2Lo, logc + p)));
   // (+Inf -> +Inf; outside safe_log's domain as Base.log: 0 -> -Inf, x < 0 or NaN -> NaN)
   return x == __builtin_inff() ? x : (x > 0.0f ? v : (x == 0.0f ? -__builtin_inff() : __builtin_nanf("")));
 }
@@ -143,38 +158,67 @@ SRL_HD inline double sr_rem_pio2f_fast(float x, int* q) {
   return y;
 }
 
-// fast path only: |x| < 2^20 (the kernel checks the whole wave once and takes sr_sinf / sr_cosf
-// otherwise)
-SRL_HD inline float sr_sinf_fast(float x) {
-  int q = 0;
-  const double y = sr_rem_pio2f_fast(x, &q);
-  return sr_trig_kernel(y, q);
-}
-SRL_HD inline float sr_cosf_fast(float x) {
-  int q = 0;
-  const double y = sr_rem_pio2f_fast(x, &q);
-  return sr_trig_kernel(y, q + 1);
+// |x| < 2^20: x = n pi/64 + r (three-part Cody-Waite in double), |r| <= pi/128; with
+// (s_k, c_k) = (sin, cos)(k pi/64), k = n mod 128: sin x = s_k cos r + c_k sin r,
+// cos x = c_k cos r - s_k sin r; sin r = r - r^3/6 + r^5/120, cos r = 1 - r^2/2 + r^4/24.
+template <bool COS>
+SRL_HD inline float sr_sincosf_tab(float x, const double* tab) {
+  const double xd = double(x);
+  const double n = rint(xd * srl::k64OverPi);
+  double r = fma(-n, srl::kPi64_1, xd);
+  r = fma(-n, srl::kPi64_2, r);
+  r = fma(-n, srl::kPi64_3, r);
+  const int k = srl::to_int(n) & 127;
+  const double sk = tab[2 * k], ck = tab[2 * k + 1];
+  const double z = r * r;
+  const double sr = fma(z * r, fma(z, 0x1.1111111111111p-7, -0x1.5555555555555p-3), r);
+  const double cr = fma(z, fma(z, 0x1.5555555555555p-5, -0.5), 1.0);
+  return COS ? float(fma(ck, cr, -(sk * sr))) : float(fma(sk, cr, ck * sr));
 }
 
 // Full range, branch-free (selects: no divergent control flow in the interpreter's unrolled rows).
-SRL_HD inline float sr_sinf(float x) {
+template <bool COS>
+SRL_HD inline float sr_sincosf_full(float x, const double* tab) {
   const float ax = fabsf(x);
   const bool fast = ax < srl::kTrigFastLimit;
   const float xl = (fast || !(ax <= 3.4028235e38f)) ? 0x1p20f : ax;  // (a finite stand-in)
-  int ql = 0, qf = 0;
+  int ql = 0;
   const double yl = sr_rem_pio2f_large(xl, &ql);
-  const double yf = sr_rem_pio2f_fast(fast ? x : 0.0f, &qf);
-  const float vl = sr_trig_kernel(yl, ql);
-  const float v = fast ? sr_trig_kernel(yf, qf) : (x < 0.0f ? -vl : vl);
-  return ax <= 3.4028235e38f ? v : __builtin_nanf("");  // sin(+-Inf), NaN -> NaN
+  const float vf = sr_sincosf_tab<COS>(fast ? x : 0.0f, tab);
+  const float vl = COS ? sr_trig_kernel(yl, ql + 1) : sr_trig_kernel(yl, ql);
+  const float v = fast ? vf : ((!COS && x < 0.0f) ? -vl : vl);
+  return ax <= 3.4028235e38f ? v : __builtin_nanf("");  // sin/cos(+-Inf), NaN -> NaN
 }
-SRL_HD inline float sr_cosf(float x) {
-  const float ax = fabsf(x);
-  const bool fast = ax < srl::kTrigFastLimit;
-  const float xl = (fast || !(ax <= 3.4028235e38f)) ? 0x1p20f : ax;
-  int ql = 0, qf = 0;
-  const double yl = sr_rem_pio2f_large(xl, &ql);
-  const double yf = sr_rem_pio2f_fast(fast ? x : 0.0f, &qf);
-  const float v = fast ? sr_trig_kernel(yf, qf + 1) : sr_trig_kernel(yl, ql + 1);
-  return ax <= 3.4028235e38f ? v : __builtin_nanf("");
+
+// ---------------------------------------------------------------- tables: host / device
+#if defined(__HIPCC__)
+// per-workgroup LDS copy of the tables (trig then log; 4 KiB)
+static __shared__ double sr_lds_libm[512];
+// Copy the tables into LDS: every thread of the block calls this before the block's first barrier.
+__device__ inline void sr_libm_lds_fill(int tid, int nthreads) {
+  for (int i = tid; i < 256; i += nthreads) {
+    sr_lds_libm[i] = srl::kTrigTab[i];
+    sr_lds_libm[256 + i] = srl::kLogTab[i];
+  }
 }
+#endif
+SRL_HD inline const double* sr_trig_tab() {
+#if defined(__HIP_DEVICE_COMPILE__)
+  return sr_lds_libm;
+#else
+  return srl::kTrigTab;
+#endif
+}
+SRL_HD inline const double* sr_log_tab() {
+#if defined(__HIP_DEVICE_COMPILE__)
+  return sr_lds_libm + 256;
+#else
+  return srl::kLogTab;
+#endif
+}
+
+SRL_HD inline float sr_sinf(float x) { return sr_sincosf_full<false>(x, sr_trig_tab()); }
+SRL_HD inline float sr_cosf(float x) { return sr_sincosf_full<true>(x, sr_trig_tab()); }
+SRL_HD inline float sr_sinf_fast(float x) { return sr_sincosf_tab<false>(x, sr_trig_tab()); }
+SRL_HD inline float sr_cosf_fast(float x) { return sr_sincosf_tab<true>(x, sr_trig_tab()); }
+SRL_HD inline float sr_logf(float x) { return sr_logf_tab(x, sr_log_tab()); }

@@ -203,7 +203,7 @@ __device__ __forceinline__ P* sr_row_at(P* base, uint32_t meta) {
   return reinterpret_cast<P*>(reinterpret_cast<B*>(base) + (meta << sh));
 }
 
-// The double-precision Float32 libm (exp / log / cos / sin, sr_libm.h) over a lane's R rows, as a real
+// The double-precision Float32 libm (log / cos / sin, sr_libm.h) over a lane's R rows, as a real
 // call: its polynomial constants and f64 temporaries live in the callee's own registers instead of
 // being hoisted out of the interpreter loop and spilled, and each body exists once per kernel.
 // Float32 cos / sin take the Cody-Waite fast path for all rows unless some lane holds |x| >= 2^20
@@ -230,7 +230,7 @@ __device__ __attribute__((noinline)) SrRowVec<R> sr_libm_rows(SrRowVec<R> v) {
 // A unary operator over a lane's R rows.
 template <typename T, uint32_t ID, int R>
 __device__ __forceinline__ void sr_unary_rows(T (&v)[R]) {
-  if constexpr (sizeof(T) == 4 && (ID == SR_U_EXP || ID == SR_U_LOG || ID == SR_U_COS || ID == SR_U_SIN)) {
+  if constexpr (sizeof(T) == 4 && (ID == SR_U_LOG || ID == SR_U_COS || ID == SR_U_SIN)) {
     SrRowVec<R> x;
 #pragma unroll
     for (int r = 0; r < R; ++r) x[r] = v[r];
@@ -523,6 +523,7 @@ __global__ void __launch_bounds__(W * 64, (SrMinWavesFor<T, R, TIER, W, VSTK>::v
   if (use_hint && lane < S) hintv = __hip_atomic_load(a.hint + my_pos, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 
   for (int i = tid; i < G * MC; i += SR_BLOCK) jst[i] = T(0);
+  sr_libm_lds_fill(tid, SR_BLOCK);  // (visible after the first tile's barrier)
   // EXACT: this block's row range [rlo, rhi] of the view (one leaf block of Julia's pairwise sum)
   const int64_t rlo = (MODE == SR_MODE_EXACT) ? a.range_lo[rb] : 0;
   const int64_t rhi = (MODE == SR_MODE_EXACT) ? a.range_hi[rb] : 0;

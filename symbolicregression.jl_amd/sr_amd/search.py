@@ -493,7 +493,7 @@ def _costs(losses, sizes, ds, options):
     norm = base if (base >= L(0.01) and full.use_baseline) else L(0.01)
     pars = (np.asarray(sizes, dtype=np.float32) * np.float32(options.parsimony)).astype(losses.dtype)
     with np.errstate(over="ignore", invalid="ignore"):
-        return (losses / norm + pars).astype(np.float64)
+        return (losses / norm + pars).astype(losses.dtype)  # costs are L, as PopMember.cost
 
 
 def _accept(pl, after_cost, new_size, snap, maxsize, so, rng):
@@ -503,7 +503,10 @@ def _accept(pl, after_cost, new_size, snap, maxsize, so, rng):
         return False
     prob = 1.0
     if so.annealing:
-        delta = after_cost - pl.parent.cost
+        # delta = after_cost - before_cost in L, then promoted against the Float64 temperature
+        L = type(pl.parent.cost) if isinstance(pl.parent.cost, np.floating) else np.float64
+        with np.errstate(over="ignore", invalid="ignore"):
+            delta = float(L(after_cost) - L(pl.parent.cost))
         if pl.temperature > 0:
             with np.errstate(over="ignore", invalid="ignore"):
                 prob *= float(np.exp(-delta / (pl.temperature * so.alpha)))
@@ -694,7 +697,7 @@ def equation_search(X=None, y=None, *, niterations=10, options, weights=None, se
                         continue
                     j = pl.slot
                     new_size = pl.tree.count_nodes()
-                    if _accept(pl, float(costs[j]), new_size, snap, maxsize, so, rng):
+                    if _accept(pl, costs[j], new_size, snap, maxsize, so, rng):
                         replace_oldest(pop, [PopMember(pl.tree, costs[j], losses[j], new_size, parent=pl.parent.ref,
                                                        birth=born())])
                     elif not so.skip_mutation_failures:

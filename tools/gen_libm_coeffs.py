@@ -58,3 +58,38 @@ def split(v, k):
 
 if __name__ == "__main__":
     main()
+
+
+def tables():
+    """Tables of csrc/sr_libm.h: sin/cos(k pi/64), k = 0..127; log: for the 128 mantissa cells of
+    [1, 2), invc = 1 / (cell centre) rounded to double and logc = -log(invc) (so that
+    log(m) = logc + log1p(m * invc - 1) holds exactly in real arithmetic); cells of [1.5, 2) serve
+    m/2 (centre halved), cell 0 has centre 1."""
+    trig = [(float(mp.sin(k * mp.pi / 64)), float(mp.cos(k * mp.pi / 64))) for k in range(128)]
+    logt = []
+    for k in range(128):
+        c = 1 + (mp.mpf(k) + mp.mpf(1) / 2) / 128
+        if k == 0:  # cell [1, 1 + 1/128): centre 1 exactly, so log(1) = 0 exactly
+            c = mp.mpf(1)
+        elif k >= 64:  # m in [1.5, 2) is taken as m/2 in [0.75, 1) with e + 1 (no cancellation near 1-)
+            c = c / 2
+        invc = float(1 / c)
+        logt.append((invc, float(-mp.log(mp.mpf(invc)))))
+    return trig, logt
+
+
+def emit_tables():
+    trig, logt = tables()
+    print("constexpr double kTrigTab[256] = {" + ", ".join(float.hex(v) for p in trig for v in p) + "};")
+    print("constexpr double kLogTab[256] = {" + ", ".join(float.hex(v) for p in logt for v in p) + "};")
+    h = mp.pi / 64
+    print("pi/64 split:", [float.hex(float(x)) for x in split(h, 3)], " 64/pi:", float.hex(float(64 / mp.pi)))
+    # polynomial bounds on |r| <= pi/128 (trig) and |r| <= 1/256 (log)
+    r = mp.pi / 128
+    print("trig s err:", float(r ** 7 / 5040 / r), " c err:", float(r ** 6 / 720))
+    r = mp.mpf(1) / 256
+    print("log err (deg 5):", float(r ** 6 / 6 / r))
+
+
+if __name__ == "__main__" and len(__import__("sys").argv) > 1:
+    emit_tables()
