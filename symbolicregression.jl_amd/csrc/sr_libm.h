@@ -4,8 +4,8 @@
 // log kernels work in Float64).  ROCm's OCML Float32 log / cos / sin measured 1.75 / 1.26 / 1.49 ulp
 // on the fixture points of tests/golden/libm_ulp.json (profiles/r02_libm_ocml.txt), so those three
 // are computed here in double and rounded once, table-driven so the work per value stays close to
-// OCML's: log from a 128-cell table of [1, 2) and a degree-5 log1p, cos / sin from (sin, cos)(k pi/64)
-// and degree-5/4 polynomials on |r| <= pi/128.  Every fast-path result is within 2^-38 relative of
+// OCML's: log from a 32-cell table of [1, 2) and a degree-8 log1p, cos / sin from (sin, cos)(k pi/16)
+// and degree-7/6 polynomials on |r| <= pi/32.  Every fast-path result is within 2^-38 relative of
 // the exact value before the final rounding (tools/gen_libm_coeffs.py prints the bounds), i.e.
 // correctly rounded unless the exact value sits that close to a midpoint.  OCML's Float32 exp
 // measured 0.675 ulp and is kept on the device (sr_expf below, also correctly rounded but for
@@ -52,8 +52,8 @@ constexpr double kLn2Hi = 0x1.62e42fefa39efp-1, kLn2Lo = 0x1.abc9e3b39803fp-56;
 constexpr double kTwoOverPi = 0x1.45f306dc9c883p-1;
 constexpr double kPio2_1 = 0x1.921fb54442d18p+0, kPio2_2 = 0x1.1a62633145c07p-54, kPio2_3 = -0x1.f1976b7ed8fbcp-110;
 constexpr double kSqrtHalf = 0x1.6a09e667f3bcdp-1;
-constexpr double k64OverPi = 0x1.45f306dc9c883p+4;
-constexpr double kPi64_1 = 0x1.921fb54442d18p-5, kPi64_2 = 0x1.1a62633145c07p-59, kPi64_3 = -0x1.f1976b7ed8fbcp-115;
+constexpr double k16OverPi = 0x1.45f306dc9c883p+2;
+constexpr double kPi16_1 = 0x1.921fb54442d18p-3, kPi16_2 = 0x1.1a62633145c07p-57, kPi16_3 = -0x1.f1976b7ed8fbcp-113;
 // 2/pi in 32-bit words: bit 1 of word 0 is the 2^-1 bit (Payne-Hanek reduction of huge arguments)
 constexpr uint32_t kTwoOverPiBits[12] = {0xA2F9836Eu, 0x4E441529u, 0xFC2757D1u, 0xF534DDC0u, 0xDB629599u, 0x3C439041u,
                                          0xFE5163ABu, 0xDEBBC561u, 0xB7246E3Au, 0x424DD2E0u, 0x06492EEAu, 0x09D1921Cu};
@@ -85,7 +85,7 @@ SRL_HD inline float sr_expf(float x) {
 }
 
 // log(x) = e ln2 + logc_k + log1p(m invc_k - 1): x = 2^e m, m in [0.75, 1.5) from the Float32 bits
-// (subnormals scaled by 2^24 first), cell k = the top 7 mantissa bits, |m invc_k - 1| < 2^-7.
+// (subnormals scaled by 2^24 first), cell k = the top 5 mantissa bits, |m invc_k - 1| <= 2^-5.
 SRL_HD inline float sr_logf_tab(float x, const double* tab) {
   uint32_t b;
   __builtin_memcpy(&b, &x, 4);
@@ -93,15 +93,21 @@ SRL_HD inline float sr_logf_tab(float x, const double* tab) {
   float xs = sub ? x * 0x1p24f : x;
   __builtin_memcpy(&b, &xs, 4);
   const int e = int(b >> 23) - 127 - (sub ? 24 : 0);
-  const uint32_t k = (b >> 16) & 127u;
-  const bool hi = k >= 64u;  // m in [1.5, 2): use m / 2 and e + 1 (x just below 1 keeps e = 0)
+  const uint32_t k = (b >> 18) & 31u;
+  const bool hi = k >= 16u;  // m in [1.5, 2): use m / 2 and e + 1 (x just below 1 keeps e = 0)
   const uint32_t mb = (b & 0x007fffffu) | (hi ? 0x3f000000u : 0x3f800000u);
   float mf;
   __builtin_memcpy(&mf, &mb, 4);
   const double invc = tab[2 * k], logc = tab[2 * k + 1];
   const double r = fma(double(mf), invc, -1.0);
-  // log1p(r) = r - r^2/2 + r^3/3 - r^4/4 + r^5/5 (|r| < 2^-8: error < 2^-42 |r|)
-  const double p = fma(r * r, fma(r, fma(r, fma(r, 0.2, -0.25), 0x1.5555555555555p-2), -0.5), r);
+  // log1p(r) = r - r^2/2 + r^3/3 - ... - r^8/8 (|r| <= 2^-5: error < 2^-43 |r|)
+  double q = fma(r, -0.125, 0x1.2492492492492p-3);   // -1/8 r + 1/7
+  q = fma(r, q, -0x1.5555555555555p-3);               // -1/6
+  q = fma(r, q, 0.2);
+  q = fma(r, q, -0.25);
+  q = fma(r, q, 0x1.5555555555555p-2);                // 1/3
+  q = fma(r, q, -0.5);
+  const double p = fma(r * r, q, r);
   const double ed = double(hi ? e + 1 : e);
   const float v = float(fma(ed, srl::kLn2Hi, fma(ed, srl::kLn2Lo, logc + p)));
   // (+Inf -> +Inf; outside safe_log's domain as Base.log: 0 -> -Inf, x < 0 or NaN -> NaN)
@@ -158,21 +164,23 @@ SRL_HD inline double sr_rem_pio2f_fast(float x, int* q) {
   return y;
 }
 
-// |x| < 2^20: x = n pi/64 + r (three-part Cody-Waite in double), |r| <= pi/128; with
-// (s_k, c_k) = (sin, cos)(k pi/64), k = n mod 128: sin x = s_k cos r + c_k sin r,
-// cos x = c_k cos r - s_k sin r; sin r = r - r^3/6 + r^5/120, cos r = 1 - r^2/2 + r^4/24.
+// |x| < 2^20: x = n pi/16 + r (three-part Cody-Waite in double), |r| <= pi/32; with
+// (s_k, c_k) = (sin, cos)(k pi/16), k = n mod 32: sin x = s_k cos r + c_k sin r,
+// cos x = c_k cos r - s_k sin r; sin r and cos r by Taylor to r^7 / r^6 (errors < 2^-42).
 template <bool COS>
 SRL_HD inline float sr_sincosf_tab(float x, const double* tab) {
   const double xd = double(x);
-  const double n = rint(xd * srl::k64OverPi);
-  double r = fma(-n, srl::kPi64_1, xd);
-  r = fma(-n, srl::kPi64_2, r);
-  r = fma(-n, srl::kPi64_3, r);
-  const int k = srl::to_int(n) & 127;
+  const double n = rint(xd * srl::k16OverPi);
+  double r = fma(-n, srl::kPi16_1, xd);
+  r = fma(-n, srl::kPi16_2, r);
+  r = fma(-n, srl::kPi16_3, r);
+  const int k = srl::to_int(n) & 31;
   const double sk = tab[2 * k], ck = tab[2 * k + 1];
   const double z = r * r;
-  const double sr = fma(z * r, fma(z, 0x1.1111111111111p-7, -0x1.5555555555555p-3), r);
-  const double cr = fma(z, fma(z, 0x1.5555555555555p-5, -0.5), 1.0);
+  const double sp = fma(z, fma(z, -0x1.a01a01a01a01ap-13, 0x1.1111111111111p-7), -0x1.5555555555555p-3);
+  const double sr = fma(z * r, sp, r);
+  const double cp = fma(z, fma(z, -0x1.6c16c16c16c17p-10, 0x1.5555555555555p-5), -0.5);
+  const double cr = fma(z, cp, 1.0);
   return COS ? float(fma(ck, cr, -(sk * sr))) : float(fma(sk, cr, ck * sr));
 }
 
@@ -192,13 +200,14 @@ SRL_HD inline float sr_sincosf_full(float x, const double* tab) {
 
 // ---------------------------------------------------------------- tables: host / device
 #if defined(__HIPCC__)
-// per-workgroup LDS copy of the tables (trig then log; 4 KiB)
-static __shared__ double sr_lds_libm[512];
+// per-workgroup LDS copy of the tables (trig then log; 1 KiB: it must not cost the interpreter a
+// workgroup per CU)
+static __shared__ double sr_lds_libm[128];
 // Copy the tables into LDS: every thread of the block calls this before the block's first barrier.
 __device__ inline void sr_libm_lds_fill(int tid, int nthreads) {
-  for (int i = tid; i < 256; i += nthreads) {
+  for (int i = tid; i < 64; i += nthreads) {
     sr_lds_libm[i] = srl::kTrigTab[i];
-    sr_lds_libm[256 + i] = srl::kLogTab[i];
+    sr_lds_libm[64 + i] = srl::kLogTab[i];
   }
 }
 #endif
@@ -211,7 +220,7 @@ SRL_HD inline const double* sr_trig_tab() {
 }
 SRL_HD inline const double* sr_log_tab() {
 #if defined(__HIP_DEVICE_COMPILE__)
-  return sr_lds_libm + 256;
+  return sr_lds_libm + 64;
 #else
   return srl::kLogTab;
 #endif

@@ -206,35 +206,48 @@ __device__ __forceinline__ P* sr_row_at(P* base, uint32_t meta) {
 // The double-precision Float32 libm (log / cos / sin, sr_libm.h) over a lane's R rows, as a real
 // call: its polynomial constants and f64 temporaries live in the callee's own registers instead of
 // being hoisted out of the interpreter loop and spilled, and each body exists once per kernel.
-// Float32 cos / sin take the Cody-Waite fast path for all rows unless some lane holds |x| >= 2^20
-// (one ballot: the Payne-Hanek path stays out of the common case).
 template <int R>
 using SrRowVec = float __attribute__((ext_vector_type(R)));
+// every row through the full-range function (Float32 log / cos / sin)
 template <uint32_t ID, int R>
 __device__ __attribute__((noinline)) SrRowVec<R> sr_libm_rows(SrRowVec<R> v) {
-  if constexpr (ID == SR_U_COS || ID == SR_U_SIN) {
-    bool slow = false;
 #pragma unroll
-    for (int r = 0; r < R; ++r) slow |= !(__builtin_fabsf(v[r]) < srl::kTrigFastLimit);
-    if (__builtin_amdgcn_ballot_w64(slow) == 0) {
-#pragma unroll
-      for (int r = 0; r < R; ++r) v[r] = (ID == SR_U_COS) ? sr_cosf_fast(v[r]) : sr_sinf_fast(v[r]);
-      return v;
-    }
+  for (int r = 0; r < R; ++r) {
+    v[r] = sr_unary<float>(ID, v[r]);
+    __builtin_amdgcn_sched_barrier(0);  // row by row: few live registers
   }
+  return v;
+}
+// cos / sin when every row of the wave has |x| < 2^20 (a separate function: its few registers are
+// all caller-saved, so the common call saves nothing)
+template <uint32_t ID, int R>
+__device__ __attribute__((noinline)) SrRowVec<R> sr_trig_rows_fast(SrRowVec<R> v) {
 #pragma unroll
-  for (int r = 0; r < R; ++r) v[r] = sr_unary<float>(ID, v[r]);
+  for (int r = 0; r < R; ++r) {
+    v[r] = (ID == SR_U_COS) ? sr_cosf_fast(v[r]) : sr_sinf_fast(v[r]);
+    __builtin_amdgcn_sched_barrier(0);
+  }
   return v;
 }
 
-// A unary operator over a lane's R rows.
+// A unary operator over a lane's R rows.  Float32 cos / sin take the Cody-Waite fast path for all
+// rows unless some lane holds |x| >= 2^20 (one ballot: the Payne-Hanek path stays out of the
+// common case).
 template <typename T, uint32_t ID, int R>
 __device__ __forceinline__ void sr_unary_rows(T (&v)[R]) {
   if constexpr (sizeof(T) == 4 && (ID == SR_U_LOG || ID == SR_U_COS || ID == SR_U_SIN)) {
     SrRowVec<R> x;
 #pragma unroll
     for (int r = 0; r < R; ++r) x[r] = v[r];
-    x = sr_libm_rows<ID, R>(x);
+    bool slow = false;
+    if constexpr (ID == SR_U_COS || ID == SR_U_SIN) {
+#pragma unroll
+      for (int r = 0; r < R; ++r) slow |= !(__builtin_fabsf(v[r]) < srl::kTrigFastLimit);
+    }
+    if ((ID == SR_U_COS || ID == SR_U_SIN) && __builtin_amdgcn_ballot_w64(slow) == 0)
+      x = sr_trig_rows_fast<ID, R>(x);
+    else
+      x = sr_libm_rows<ID, R>(x);
 #pragma unroll
     for (int r = 0; r < R; ++r) v[r] = x[r];
   } else {

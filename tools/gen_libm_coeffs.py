@@ -61,17 +61,17 @@ if __name__ == "__main__":
 
 
 def tables():
-    """Tables of csrc/sr_libm.h: sin/cos(k pi/64), k = 0..127; log: for the 128 mantissa cells of
+    """Tables of csrc/sr_libm.h: sin/cos(k pi/16), k = 0..31; log: for the 32 mantissa cells of
     [1, 2), invc = 1 / (cell centre) rounded to double and logc = -log(invc) (so that
     log(m) = logc + log1p(m * invc - 1) holds exactly in real arithmetic); cells of [1.5, 2) serve
     m/2 (centre halved), cell 0 has centre 1."""
-    trig = [(float(mp.sin(k * mp.pi / 64)), float(mp.cos(k * mp.pi / 64))) for k in range(128)]
+    trig = [(float(mp.sin(k * mp.pi / 16)), float(mp.cos(k * mp.pi / 16))) for k in range(32)]
     logt = []
-    for k in range(128):
-        c = 1 + (mp.mpf(k) + mp.mpf(1) / 2) / 128
-        if k == 0:  # cell [1, 1 + 1/128): centre 1 exactly, so log(1) = 0 exactly
+    for k in range(32):
+        c = 1 + (mp.mpf(k) + mp.mpf(1) / 2) / 32
+        if k == 0:  # cell [1, 1 + 1/32): centre 1 exactly, so log(1) = 0 exactly
             c = mp.mpf(1)
-        elif k >= 64:  # m in [1.5, 2) is taken as m/2 in [0.75, 1) with e + 1 (no cancellation near 1-)
+        elif k >= 16:  # m in [1.5, 2) is taken as m/2 in [0.75, 1) with e + 1 (no cancellation near 1-)
             c = c / 2
         invc = float(1 / c)
         logt.append((invc, float(-mp.log(mp.mpf(invc)))))
@@ -80,15 +80,15 @@ def tables():
 
 def emit_tables():
     trig, logt = tables()
-    print("constexpr double kTrigTab[256] = {" + ", ".join(float.hex(v) for p in trig for v in p) + "};")
-    print("constexpr double kLogTab[256] = {" + ", ".join(float.hex(v) for p in logt for v in p) + "};")
-    h = mp.pi / 64
-    print("pi/64 split:", [float.hex(float(x)) for x in split(h, 3)], " 64/pi:", float.hex(float(64 / mp.pi)))
-    # polynomial bounds on |r| <= pi/128 (trig) and |r| <= 1/256 (log)
-    r = mp.pi / 128
-    print("trig s err:", float(r ** 7 / 5040 / r), " c err:", float(r ** 6 / 720))
-    r = mp.mpf(1) / 256
-    print("log err (deg 5):", float(r ** 6 / 6 / r))
+    print("constexpr double kTrigTab[64] = {" + ", ".join(float.hex(v) for p in trig for v in p) + "};")
+    print("constexpr double kLogTab[64] = {" + ", ".join(float.hex(v) for p in logt for v in p) + "};")
+    h = mp.pi / 16
+    print("pi/16 split:", [float.hex(float(x)) for x in split(h, 3)], " 16/pi:", float.hex(float(16 / mp.pi)))
+    # polynomial bounds on |r| <= pi/32 (trig, Taylor to r^7 / r^6) and |r| <= 1/32 (log, to r^7)
+    r = mp.pi / 32
+    print("trig s rel err:", float(r ** 8 / mp.factorial(9)), " c err:", float(r ** 8 / mp.factorial(8)))
+    r = mp.mpf(1) / 32
+    print("log rel err (deg 7):", float(r ** 7 / 8))
 
 
 if __name__ == "__main__" and len(__import__("sys").argv) > 1:
