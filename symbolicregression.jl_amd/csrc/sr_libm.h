@@ -184,18 +184,17 @@ SRL_HD inline float sr_sincosf_tab(float x, const double* tab) {
   return COS ? float(fma(ck, cr, -(sk * sr))) : float(fma(sk, cr, ck * sr));
 }
 
-// Full range, branch-free (selects: no divergent control flow in the interpreter's unrolled rows).
+// Full range: the table path below 2^20, Payne-Hanek above (the device only comes here when some
+// lane of the wave holds a huge argument, so the branch costs nothing in the common case).
 template <bool COS>
 SRL_HD inline float sr_sincosf_full(float x, const double* tab) {
   const float ax = fabsf(x);
-  const bool fast = ax < srl::kTrigFastLimit;
-  const float xl = (fast || !(ax <= 3.4028235e38f)) ? 0x1p20f : ax;  // (a finite stand-in)
-  int ql = 0;
-  const double yl = sr_rem_pio2f_large(xl, &ql);
-  const float vf = sr_sincosf_tab<COS>(fast ? x : 0.0f, tab);
-  const float vl = COS ? sr_trig_kernel(yl, ql + 1) : sr_trig_kernel(yl, ql);
-  const float v = fast ? vf : ((!COS && x < 0.0f) ? -vl : vl);
-  return ax <= 3.4028235e38f ? v : __builtin_nanf("");  // sin/cos(+-Inf), NaN -> NaN
+  if (ax < srl::kTrigFastLimit) return sr_sincosf_tab<COS>(x, tab);
+  if (!(ax <= 3.4028235e38f)) return __builtin_nanf("");  // sin/cos(+-Inf), NaN -> NaN
+  int q = 0;
+  const double y = sr_rem_pio2f_large(ax, &q);
+  const float v = COS ? sr_trig_kernel(y, q + 1) : sr_trig_kernel(y, q);
+  return (!COS && x < 0.0f) ? -v : v;
 }
 
 // ---------------------------------------------------------------- tables: host / device
