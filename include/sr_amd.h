@@ -215,6 +215,96 @@ int sr_compile_info(int dtype, int n_unary, const char* const* unary_names, int 
  */
 int sr_host_unary(int dtype, const char* name, int64_t n, const void* x, void* out);
 
+/* ------------------------------------------------------------------ native search engine
+ * equation_search's inner loop (s_r_cycle, optimize_and_simplify_population, the head's per-island
+ * bookkeeping: src/SingleIteration.jl, src/RegularizedEvolution.jl, src/Mutate.jl,
+ * src/MutationFunctions.jl, src/Population.jl, src/SymbolicRegression.jl:1040-1140) in C++, with
+ * every island's children of a regularised-evolution round scored by ONE sr_eval_loss_batch call.
+ * Islands shard over ranks (island i on rank i % world_size); per iteration a rank runs
+ * sr_search_iterate on its islands, the ranks exchange sr_search_export buffers (all-gather) and
+ * sr_search_import them, and every rank runs sr_search_head (identical bookkeeping, migration into
+ * an island by its owner).  Single process: start, then (iterate, head) per iteration.
+ */
+typedef struct sr_search sr_search;
+
+/* mutation kinds, the order of sr_search_options.mutation_weights (src/MutationWeights.jl) */
+#define SR_MUT_MUTATE_CONSTANT 0
+#define SR_MUT_MUTATE_OPERATOR 1
+#define SR_MUT_MUTATE_FEATURE 2
+#define SR_MUT_SWAP_OPERANDS 3
+#define SR_MUT_ROTATE_TREE 4
+#define SR_MUT_ADD_NODE 5
+#define SR_MUT_INSERT_NODE 6
+#define SR_MUT_DELETE_NODE 7
+#define SR_MUT_SIMPLIFY 8
+#define SR_MUT_RANDOMIZE 9
+#define SR_MUT_DO_NOTHING 10
+#define SR_MUT_OPTIMIZE 11
+#define SR_N_MUTATIONS 12
+
+/* member sets of sr_search_member_count / sr_search_members (>= 0: that island) */
+#define SR_SEARCH_HALL_OF_FAME (-1)
+#define SR_SEARCH_PARETO (-2)
+
+/* Options fields the search reads (src/OptionsStruct.jl types: Float32 fields are float) */
+typedef struct sr_search_options {
+  int populations, population_size, ncycles_per_iteration, tournament_selection_n;
+  float tournament_selection_p;
+  int maxsize, maxdepth;
+  float parsimony;
+  float crossover_probability;
+  int annealing;
+  float alpha, perturbation_factor, probability_negate_constant;
+  int use_frequency, use_frequency_in_tournament;
+  double adaptive_parsimony_scaling;
+  float fraction_replaced, fraction_replaced_hof;
+  int topn, migration, hof_migration, skip_mutation_failures, should_simplify;
+  int should_optimize_constants;
+  float optimizer_probability;
+  int optimizer_iterations, optimizer_nrestarts;
+  int batching;
+  int64_t batch_size;
+  float warmup_maxsize_by;
+  double mutation_weights[SR_N_MUTATIONS];
+} sr_search_options;
+
+typedef struct sr_search_info {
+  int64_t iterations, s_r_cycles, device_calls;
+  double num_evals;
+  double device_ms; /* wall time inside the scoring calls (device launches + their host sides) */
+  double host_ms;   /* selection, mutation and acceptance */
+  double baseline_loss;
+  int use_baseline;
+} sr_search_info;
+
+/* CPU scorers for tests (the library's own device path when not set): sr_eval_loss_batch /
+ * sr_eval_grad_batch semantics over the search's dataset; return SR_OK or an error code. */
+typedef int (*sr_loss_fn)(void* user, const sr_tree_batch* trees, const int64_t* row_idx, int64_t n_idx,
+                          void* out_loss, uint8_t* out_complete);
+typedef int (*sr_grad_fn)(void* user, const sr_tree_batch* trees, const int64_t* row_idx, int64_t n_idx,
+                          void* out_loss, void* out_grad, uint8_t* out_complete);
+
+int sr_search_create(int dtype, int64_t nfeatures, int64_t n_rows, int n_unary, const char* const* unary_names,
+                     int n_binary, const char* const* binary_names, const sr_search_options* opts, uint64_t seed,
+                     int rank, int world_size, sr_search** out);
+int sr_search_free(sr_search* s);
+/* score on the device: `ds` must match the search's dtype / features / rows */
+int sr_search_use_device(sr_search* s, sr_ctx* ctx, const sr_dataset* ds, int opset_id, int loss_code);
+int sr_search_use_callbacks(sr_search* s, sr_loss_fn loss, sr_grad_fn grad, void* user);
+/* update_baseline_loss! and the initial populations of this rank's islands */
+int sr_search_start(sr_search* s, int niterations);
+int sr_search_iterate(sr_search* s);
+int sr_search_head(sr_search* s);
+/* this rank's islands (members + best-seen) as bytes: call with buf = NULL for the size */
+int sr_search_export(sr_search* s, void* buf, int64_t capacity, int64_t* size);
+int sr_search_import(sr_search* s, const void* buf, int64_t size);
+int sr_search_get_info(sr_search* s, sr_search_info* out);
+int sr_search_member_count(sr_search* s, int which, int64_t* n_members, int64_t* n_nodes);
+/* members as pre-order node arrays (offsets[n_members + 1]) + cost / loss (dtype) and bookkeeping */
+int sr_search_members(sr_search* s, int which, int64_t* offsets, uint8_t* degree, uint8_t* op, uint16_t* feature,
+                      uint8_t* constant, void* val, void* cost, void* loss, int64_t* birth, int64_t* ref,
+                      int64_t* parent, int32_t* complexity);
+
 /* Timing of the last device call on this context (ms): kernel-only, via HIP events. */
 int sr_last_kernel_ms(sr_ctx* ctx, double* eval_ms, double* total_ms);
 

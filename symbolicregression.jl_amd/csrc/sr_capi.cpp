@@ -111,6 +111,9 @@ inline bool loss_direct_ok(int kind) {
 
 }  // namespace
 
+// the thread-local error message, for the other translation units of the library (sr_search.cpp)
+int sr_set_error(int code, const std::string& msg) { return set_error(code, msg); }
+
 struct sr_ctx {
   int device = 0;
   hipStream_t stream = nullptr;

@@ -1,0 +1,1260 @@
+// sr_search.cpp — native equation_search engine: lock-step islands scored by batched device calls.
+//
+// Restates the reference's search around the scoring path:
+//   * s_r_cycle (src/SingleIteration.jl:19-66): ncycles_per_iteration annealing temperatures
+//     LinRange(1, 0), one reg_evol_cycle each, best-seen members per complexity;
+//   * reg_evol_cycle (src/RegularizedEvolution.jl:12-160): ceil(n / tournament_selection_n) rounds of
+//     tournament selection (best_of_sample, src/Population.jl:109-159 with argmin_fast / bottomk_fast,
+//     src/Utils.jl:96-147), next_generation (src/Mutate.jl:174-356) or crossover_generation
+//     (:661-733), replacing the oldest member(s);
+//   * optimize_and_simplify_population (src/SingleIteration.jl:68-139) and finalize_costs
+//     (src/Population.jl:182-196); _dispatch_s_r_cycle's best-seen re-scoring under batching
+//     (src/SymbolicRegression.jl:1253-1296);
+//   * the head node's per-island bookkeeping of _main_search_loop! (src/SymbolicRegression.jl:
+//     1040-1140): running statistics (src/AdaptiveParsimony.jl), hall of fame (update_hall_of_fame!,
+//     src/SearchUtils.jl:717-736; calculate_pareto_frontier, src/HallOfFame.jl:96-124), migration
+//     (migrate!, src/Migration.jl:15-37 with poisson_sample, src/Utils.jl:149-157), get_cur_maxsize
+//     (src/SearchUtils.jl:656-671).
+//
+// MI355X-first change: the islands advance in LOCK-STEP.  At every regularised-evolution round each
+// owned island selects and mutates on the host, and the children of ALL islands are scored by ONE
+// batched device call; each island's serial semantics (its next round sees its own replacements)
+// are kept.  Constant optimisation runs batched over every island's selected members.  Islands shard
+// across ranks (island i on rank i % world): a rank runs its islands' cycles, the ranks exchange
+// islands (sr_search_export / sr_search_import over torch.distributed) and every rank replays the
+// head's island-by-island bookkeeping identically; migration into an island is done by its owner
+// with the island's own stream.  Random streams and birth counters are per island (sr_rng.h), so a
+// sharded search equals the single-process one.
+#include <math.h>
+#include <stdint.h>
+#include <string.h>
+
+#include <algorithm>
+#include <chrono>
+#include <memory>
+#include <string>
+#include <type_traits>
+#include <vector>
+
+#include "../../include/sr_amd.h"
+#include "sr_compile.h"
+#include "sr_constopt.h"
+#include "sr_libm.h"
+#include "sr_search_tree.h"
+
+int sr_set_error(int code, const std::string& msg);  // sr_capi.cpp
+
+namespace {
+
+using Clock = std::chrono::steady_clock;
+inline double ms_since(Clock::time_point t0) {
+  return std::chrono::duration<double, std::milli>(Clock::now() - t0).count();
+}
+
+template <typename T>
+struct Member {
+  SrTree<T> tree;
+  T cost = T(0), loss = T(0);  // L == T
+  int64_t birth = 0, ref = 0, parent = -1;
+  int complexity = 0;
+};
+
+template <typename T>
+struct Hof {
+  std::vector<Member<T>> m;
+  std::vector<uint8_t> exists;
+  void reset(int maxsize) {
+    m.assign(size_t(maxsize), Member<T>());
+    exists.assign(size_t(maxsize), 0);
+  }
+};
+
+// Julia isless on floats: NaN sorts last
+template <typename T>
+inline bool jl_isless(T a, T b) {
+  if (a != a) return false;
+  if (b != b) return true;
+  return a < b;
+}
+
+struct Flat {
+  std::vector<int64_t> offsets;
+  std::vector<uint8_t> degree, op, constant;
+  std::vector<uint16_t> feature;
+  std::vector<double> vd;
+  std::vector<float> vf;
+  void clear() {
+    offsets.assign(1, 0);
+    degree.clear();
+    op.clear();
+    constant.clear();
+    feature.clear();
+    vd.clear();
+    vf.clear();
+  }
+  template <typename T>
+  void add(const SrTree<T>& t, const std::vector<double>* consts = nullptr) {
+    size_t k = 0;
+    for (const auto& n : t) {
+      degree.push_back(n.degree);
+      op.push_back(n.op);
+      constant.push_back(n.constant);
+      feature.push_back(n.feature);
+      T v = n.val;
+      if (consts && n.degree == 0 && n.constant) v = T((*consts)[k++]);
+      if constexpr (sizeof(T) == 4)
+        vf.push_back(v);
+      else
+        vd.push_back(v);
+    }
+    offsets.push_back(offsets.back() + int64_t(t.size()));
+  }
+  template <typename T>
+  sr_tree_batch batch() const {
+    sr_tree_batch b{};
+    b.n_trees = int64_t(offsets.size()) - 1;
+    b.offsets = offsets.data();
+    b.degree = degree.data();
+    b.op = op.data();
+    b.feature = feature.data();
+    b.constant = constant.data();
+    if constexpr (sizeof(T) == 4)
+      b.val = vf.data();
+    else
+      b.val = vd.data();
+    return b;
+  }
+};
+
+// ---------------------------------------------------------------- byte stream (island exchange)
+struct Writer {
+  std::vector<uint8_t> buf;
+  template <typename V>
+  void put(const V& v) {
+    const uint8_t* p = reinterpret_cast<const uint8_t*>(&v);
+    buf.insert(buf.end(), p, p + sizeof(V));
+  }
+};
+struct Reader {
+  const uint8_t* p;
+  const uint8_t* end;
+  bool ok = true;
+  template <typename V>
+  V get() {
+    V v{};
+    if (p + sizeof(V) > end) {
+      ok = false;
+      return v;
+    }
+    memcpy(&v, p, sizeof(V));
+    p += sizeof(V);
+    return v;
+  }
+};
+
+}  // namespace
+
+struct sr_search_base {
+  virtual ~sr_search_base() = default;
+  int dtype = SR_DTYPE_F32;
+};
+
+namespace {
+
+template <typename T>
+struct Engine : sr_search_base {
+  sr_search_options o{};
+  SrTreeSpec sp;
+  int64_t n_rows = 0;
+  uint64_t seed = 0;
+  int rank = 0, world = 1;
+  std::vector<int> owned;
+  // scorer
+  sr_ctx* ctx = nullptr;
+  const sr_dataset* ds = nullptr;
+  int opset_id = -1, loss_code = 0;
+  sr_loss_fn loss_cb = nullptr;
+  sr_grad_fn grad_cb = nullptr;
+  void* cb_user = nullptr;
+  // dataset-level state (update_baseline_loss!)
+  T baseline = T(1);
+  bool use_baseline = false;
+  // islands
+  std::vector<std::vector<Member<T>>> pops;
+  std::vector<SrRng> rngs;
+  std::vector<int64_t> births, refs;
+  std::vector<Hof<T>> best_seen;
+  std::vector<std::vector<Member<T>>> best_sub;
+  std::vector<std::vector<double>> snap;  // normalized frequencies handed to each island's next cycle
+  std::vector<int> cur_maxsize;           // maxsize handed to each island's next cycle
+  // head
+  std::vector<double> freq;
+  Hof<T> hof;
+  int64_t total_cycles = 1, cycles_remaining = 1;
+  int head_maxsize = 1;  // state.cur_maxsizes[j]
+  int iteration = 0;
+  // accounting
+  double num_evals = 0.0;
+  int64_t device_calls = 0, s_r_cycles = 0;
+  double device_ms = 0.0, host_ms = 0.0;
+  std::vector<int64_t> batch_idx;  // this iteration's minibatch (batching)
+  Flat flat;
+
+  bool owns(int i) const { return i % world == rank; }
+  int64_t new_birth(int i) { return ++births[size_t(i)]; }
+  int64_t new_ref(int i) { return (int64_t(i + 1) << 40) | ++refs[size_t(i)]; }
+
+  // ------------------------------------------------------------ scoring
+  int score_flat(const int64_t* rows, int64_t n_idx, std::vector<T>* loss) {
+    const sr_tree_batch b = flat.batch<T>();
+    const int64_t nt = b.n_trees;
+    loss->assign(size_t(nt), T(0));
+    if (nt == 0) return SR_OK;
+    std::vector<uint8_t> comp(static_cast<size_t>(nt));
+    auto t0 = Clock::now();
+    int rc = loss_cb ? loss_cb(cb_user, &b, rows, n_idx, loss->data(), comp.data())
+                     : sr_eval_loss_batch(ctx, ds, opset_id, &b, rows, n_idx, loss_code, loss->data(), comp.data());
+    device_ms += ms_since(t0);
+    ++device_calls;
+    if (rc != SR_OK) return rc == SR_ERR_INVALID_ARG || rc < 0 ? rc : SR_ERR_INVALID_ARG;
+    for (int64_t k = 0; k < nt; ++k)
+      if (!comp[size_t(k)]) (*loss)[size_t(k)] = T(INFINITY);
+    return SR_OK;
+  }
+  // loss_to_cost (src/LossFunctions.jl:169-190) in L
+  T cost_of(T loss, int complexity) const {
+    const T norm = (baseline >= T(0.01) && use_baseline) ? baseline : T(0.01);
+    T v = loss / norm;
+    v = v + T(float(complexity) * o.parsimony);
+    return v;
+  }
+  int score_trees(const std::vector<const SrTree<T>*>& trees, const std::vector<int64_t>& rows,
+                  std::vector<T>* loss, std::vector<T>* cost) {
+    flat.clear();
+    for (auto* t : trees) flat.add(*t);
+    int rc = score_flat(rows.empty() ? nullptr : rows.data(), int64_t(rows.size()), loss);
+    if (rc) return rc;
+    cost->resize(loss->size());
+    for (size_t k = 0; k < loss->size(); ++k) (*cost)[k] = cost_of((*loss)[k], int(trees[k]->size()));
+    return SR_OK;
+  }
+  double fraction(const std::vector<int64_t>& rows) const {
+    return rows.empty() ? 1.0 : double(rows.size()) / double(n_rows);
+  }
+
+  // ------------------------------------------------------------ constant optimisation
+  struct Obj : SrObjective {
+    Engine* e;
+    const std::vector<const SrTree<T>*>* trees;
+    const std::vector<int64_t>* rows;
+    std::vector<int64_t> f_calls;
+    int f(const std::vector<int>& items, const std::vector<std::vector<double>>& xs, std::vector<double>* out) override {
+      e->flat.clear();
+      for (size_t j = 0; j < items.size(); ++j) {
+        e->flat.add(*(*trees)[size_t(items[j])], &xs[j]);
+        ++f_calls[size_t(items[j])];
+      }
+      std::vector<T> loss;
+      int rc = e->score_flat(rows->empty() ? nullptr : rows->data(), int64_t(rows->size()), &loss);
+      if (rc) return rc;
+      out->resize(loss.size());
+      for (size_t j = 0; j < loss.size(); ++j) (*out)[j] = double(loss[j]);
+      return SR_OK;
+    }
+    int fg(const std::vector<int>& items, const std::vector<std::vector<double>>& xs, std::vector<double>* out,
+           std::vector<std::vector<double>>* grads) override {
+      e->flat.clear();
+      size_t nc = 0;
+      for (size_t j = 0; j < items.size(); ++j) {
+        e->flat.add(*(*trees)[size_t(items[j])], &xs[j]);
+        ++f_calls[size_t(items[j])];
+        nc += xs[j].size();
+      }
+      const sr_tree_batch b = e->flat.template batch<T>();
+      std::vector<T> loss(items.size()), g(nc + 1);
+      std::vector<uint8_t> comp(items.size());
+      const int64_t* r = rows->empty() ? nullptr : rows->data();
+      auto t0 = Clock::now();
+      int rc = e->grad_cb ? e->grad_cb(e->cb_user, &b, r, int64_t(rows->size()), loss.data(), g.data(), comp.data())
+                          : sr_eval_grad_batch(e->ctx, e->ds, e->opset_id, &b, r, int64_t(rows->size()), e->loss_code,
+                                               loss.data(), g.data(), comp.data());
+      e->device_ms += ms_since(t0);
+      ++e->device_calls;
+      if (rc != SR_OK) return rc;
+      out->resize(items.size());
+      grads->resize(items.size());
+      size_t at = 0;
+      for (size_t j = 0; j < items.size(); ++j) {
+        (*out)[j] = comp[j] ? double(loss[j]) : INFINITY;
+        (*grads)[j].assign(xs[j].size(), 0.0);
+        for (size_t q = 0; q < xs[j].size(); ++q) (*grads)[j][q] = double(g[at + q]);
+        at += xs[j].size();
+      }
+      return SR_OK;
+    }
+  };
+
+  // optimize_constants over members (pointers); perturbation draws come from each member's island
+  // stream, in member order (deterministic whatever the batch composition)
+  int optimize_members(const std::vector<Member<T>*>& ms, const std::vector<int>& island,
+                       const std::vector<int64_t>& rows, std::vector<uint8_t>* improved_out) {
+    const size_t n = ms.size();
+    improved_out->assign(n, 0);
+    if (n == 0) return SR_OK;
+    if (!ctx && !grad_cb) return sr_set_error(SR_ERR_INVALID_ARG, "constant optimisation needs a gradient scorer");
+    std::vector<const SrTree<T>*> trees(n);
+    std::vector<std::vector<double>> x0(n);
+    for (size_t k = 0; k < n; ++k) {
+      trees[k] = &ms[k]->tree;
+      for (const auto& nd : ms[k]->tree)
+        if (nd.degree == 0 && nd.constant) x0[k].push_back(double(nd.val));
+    }
+    std::vector<std::vector<std::vector<double>>> restarts(size_t(o.optimizer_nrestarts),
+                                                           std::vector<std::vector<double>>(n));
+    for (size_t k = 0; k < n; ++k) {
+      SrRng& rng = rngs[size_t(island[k])];
+      for (int r = 0; r < o.optimizer_nrestarts; ++r) {
+        std::vector<double>& xt = restarts[size_t(r)][k];
+        xt.resize(x0[k].size());
+        for (size_t q = 0; q < x0[k].size(); ++q) {
+          const T eps = T(rng.normal());
+          xt[q] = double(T(x0[k][q]) * (T(1) + T(0.5) * eps));  // x0 .* (1 + eps/2) in T
+        }
+      }
+    }
+    Obj obj;
+    obj.e = this;
+    obj.trees = &trees;
+    obj.rows = &rows;
+    obj.f_calls.assign(n, 0);
+    std::vector<std::vector<double>> bx;
+    std::vector<double> bf, base;
+    int rc = sr_optimize_batch(obj, x0, restarts, o.optimizer_iterations, &bx, &bf, &base);
+    if (rc) return rc;
+    const double frac = fraction(rows);
+    std::vector<size_t> better;
+    for (size_t k = 0; k < n; ++k) {
+      num_evals += double(obj.f_calls[k]) * frac;
+      if (bf[k] < base[k]) better.push_back(k);
+    }
+    if (better.empty()) return SR_OK;
+    // adopt: constants, then the loss at the minimiser (f(result.minimizer)), cost, birth
+    flat.clear();
+    for (size_t k : better) flat.add(ms[k]->tree, &bx[k]);
+    std::vector<T> loss;
+    if ((rc = score_flat(rows.empty() ? nullptr : rows.data(), int64_t(rows.size()), &loss))) return rc;
+    for (size_t j = 0; j < better.size(); ++j) {
+      const size_t k = better[j];
+      Member<T>& m = *ms[k];
+      size_t q = 0;
+      for (auto& nd : m.tree)
+        if (nd.degree == 0 && nd.constant) nd.val = T(bx[k][q++]);
+      m.loss = loss[j];
+      m.cost = cost_of(m.loss, m.complexity);
+      m.birth = new_birth(island[k]);
+      num_evals += frac;
+      (*improved_out)[k] = 1;
+    }
+    return SR_OK;
+  }
+
+  // ------------------------------------------------------------ selection
+  std::vector<float> tweights;
+  void make_tournament_weights() {
+    const float p = o.tournament_selection_p;
+    tweights.resize(size_t(o.tournament_selection_n));
+    for (int k = 0; k < o.tournament_selection_n; ++k) tweights[size_t(k)] = p * float(pow(double(1.0f - p), k));
+  }
+  // StatsBase.sample(Weights): first index whose running Float32 sum reaches rand() * sum
+  int draw_place(SrRng& rng) {
+    float total = 0.0f;
+    for (float w : tweights) total += w;
+    const double t = rng.uniform() * double(total);
+    size_t i = 0;
+    float cw = tweights[0];
+    while (double(cw) < t && i + 1 < tweights.size()) {
+      ++i;
+      cw += tweights[i];
+    }
+    return int(i);
+  }
+  // best_of_sample (a copy of the winner)
+  Member<T> best_of_sample(int i) {
+    SrRng& rng = rngs[size_t(i)];
+    const auto& pop = pops[size_t(i)];
+    const int64_t np = int64_t(pop.size());
+    const int64_t n = std::min<int64_t>(o.tournament_selection_n, np);
+    std::vector<int64_t> idx(static_cast<size_t>(np));
+    for (int64_t k = 0; k < np; ++k) idx[size_t(k)] = k;
+    for (int64_t k = 0; k < n; ++k) std::swap(idx[size_t(k)], idx[size_t(k + rng.below(np - k))]);
+    std::vector<T> adj(static_cast<size_t>(n));
+    const std::vector<double>& nf = snap[size_t(i)];
+    for (int64_t k = 0; k < n; ++k) {
+      const Member<T>& m = pop[size_t(idx[size_t(k)])];
+      if (o.use_frequency_in_tournament) {
+        const T scaling = T(o.adaptive_parsimony_scaling);
+        const T f = (m.complexity > 0 && m.complexity <= o.maxsize) ? T(nf[size_t(m.complexity - 1)]) : T(0);
+        T e;
+        if constexpr (sizeof(T) == 4)
+          e = sr_expf(scaling * f);
+        else
+          e = exp(scaling * f);
+        adj[size_t(k)] = m.cost * e;
+      } else {
+        adj[size_t(k)] = m.cost;
+      }
+    }
+    const int place = o.tournament_selection_p == 1.0f ? 0 : draw_place(rng);
+    // bottomk_fast / argmin_fast: strict <, values must beat typemax (Inf), the initial index 1
+    // stays when fewer than place + 1 values qualify
+    const int K = place + 1;
+    std::vector<T> mv(static_cast<size_t>(K), T(INFINITY));
+    std::vector<int64_t> mi(static_cast<size_t>(K), 0);
+    for (int64_t k = 0; k < n; ++k) {
+      if (adj[size_t(k)] < mv[size_t(K - 1)]) {
+        mv[size_t(K - 1)] = adj[size_t(k)];
+        mi[size_t(K - 1)] = k;
+        for (int q = K - 1; q > 0; --q)
+          if (mv[size_t(q)] < mv[size_t(q - 1)]) {
+            std::swap(mv[size_t(q)], mv[size_t(q - 1)]);
+            std::swap(mi[size_t(q)], mi[size_t(q - 1)]);
+          }
+      }
+    }
+    return pop[size_t(idx[size_t(mi[size_t(K - 1)])])];
+  }
+
+  // ------------------------------------------------------------ mutation choice
+  void condition_weights(const Member<T>& m, int curmax, double* w) const {
+    const SrTree<T>& t = m.tree;
+    if (t[0].degree == 0) {
+      w[SR_MUT_MUTATE_OPERATOR] = w[SR_MUT_SWAP_OPERANDS] = w[SR_MUT_DELETE_NODE] = w[SR_MUT_SIMPLIFY] = 0.0;
+      if (!t[0].constant) {
+        w[SR_MUT_OPTIMIZE] = 0.0;
+        w[SR_MUT_MUTATE_CONSTANT] = 0.0;
+      } else {
+        w[SR_MUT_MUTATE_FEATURE] = 0.0;
+      }
+      return;
+    }
+    bool bin = false;
+    for (const auto& n : t) bin |= n.degree == 2;
+    if (!bin) w[SR_MUT_SWAP_OPERANDS] = 0.0;
+    w[SR_MUT_MUTATE_CONSTANT] *= double(std::min(8, sr_count_constants(t))) / 8.0;
+    if (sp.nfeatures <= 1) w[SR_MUT_MUTATE_FEATURE] = 0.0;
+    if (m.complexity >= curmax) w[SR_MUT_ADD_NODE] = w[SR_MUT_INSERT_NODE] = 0.0;
+    if (!o.should_simplify) w[SR_MUT_SIMPLIFY] = 0.0;
+  }
+  // sample_mutation: one draw proportional to the conditioned weights
+  int sample_mutation(const double* w, SrRng& rng) const {
+    double total = 0.0;
+    for (int k = 0; k < SR_N_MUTATIONS; ++k) total += w[k];
+    const double r = rng.uniform() * total;
+    double acc = 0.0;
+    for (int k = 0; k < SR_N_MUTATIONS; ++k) {
+      acc += w[k];
+      if (r < acc) return k;
+    }
+    for (int k = SR_N_MUTATIONS - 1; k >= 0; --k)
+      if (w[k] > 0) return k;
+    return SR_MUT_DO_NOTHING;
+  }
+  void apply_mutation(int choice, SrTree<T>& t, double temperature, int curmax, SrRng& rng) const {
+    switch (choice) {
+      case SR_MUT_MUTATE_CONSTANT: sr_mutate_constant(t, sp, temperature, rng); break;
+      case SR_MUT_MUTATE_OPERATOR: sr_mutate_operator(t, sp, rng); break;
+      case SR_MUT_MUTATE_FEATURE: sr_mutate_feature(t, sp, rng); break;
+      case SR_MUT_SWAP_OPERANDS: sr_swap_operands(t, rng); break;
+      case SR_MUT_ROTATE_TREE: sr_rotate_tree(t, rng); break;
+      case SR_MUT_ADD_NODE:
+        if (rng.uniform() < 0.5)
+          sr_append_random_op(t, sp, rng);
+        else
+          sr_prepend_random_op(t, sp, rng);
+        break;
+      case SR_MUT_INSERT_NODE: sr_insert_random_op(t, sp, rng); break;
+      case SR_MUT_DELETE_NODE: sr_delete_random_op(t, rng); break;
+      case SR_MUT_RANDOMIZE: t = sr_gen_random_tree_fixed_size<T>(int(1 + rng.below(curmax)), sp, rng); break;
+      default: break;
+    }
+  }
+
+  // replace the oldest member (argmin_fast over births: first minimum)
+  void replace_oldest(int i, Member<T>&& b) {
+    auto& pop = pops[size_t(i)];
+    size_t k = 0;
+    for (size_t j = 1; j < pop.size(); ++j)
+      if (pop[j].birth < pop[k].birth) k = j;
+    pop[k] = std::move(b);
+  }
+  void replace_two_oldest(int i, Member<T>&& b1, Member<T>&& b2) {
+    auto& pop = pops[size_t(i)];
+    size_t k1 = 0;
+    for (size_t j = 1; j < pop.size(); ++j)
+      if (pop[j].birth < pop[k1].birth) k1 = j;
+    size_t k2 = k1 == 0 ? 1 : 0;
+    for (size_t j = 0; j < pop.size(); ++j)
+      if (j != k1 && pop[j].birth < pop[k2].birth) k2 = j;
+    pop[k1] = std::move(b1);
+    pop[k2] = std::move(b2);
+  }
+
+  // ------------------------------------------------------------ one lock-step round
+  enum Kind { K_MUT, K_CROSS, K_KEEP, K_REJECT, K_CROSS_FAIL, K_OPT, K_SIMPLIFIED };
+  struct Plan {
+    Kind kind;
+    int island;
+    Member<T> parent, parent2;
+    SrTree<T> tree, tree2;
+    size_t slot = 0;
+  };
+
+  int round(double temperature, const std::vector<int64_t>& rows) {
+    std::vector<Plan> plans;
+    plans.reserve(owned.size());
+    std::vector<const SrTree<T>*> pending;
+    auto tp = Clock::now();
+    for (int i : owned) {
+      SrRng& rng = rngs[size_t(i)];
+      const int curmax = cur_maxsize[size_t(i)];
+      Plan pl;
+      pl.island = i;
+      if (rng.uniform() > double(o.crossover_probability)) {
+        pl.parent = best_of_sample(i);
+        double w[SR_N_MUTATIONS];
+        for (int k = 0; k < SR_N_MUTATIONS; ++k) w[k] = o.mutation_weights[k];
+        condition_weights(pl.parent, curmax, w);
+        const int choice = sample_mutation(w, rng);
+        if (choice == SR_MUT_DO_NOTHING) {
+          pl.kind = K_KEEP;
+        } else if (choice == SR_MUT_SIMPLIFY) {
+          pl.kind = K_SIMPLIFIED;
+          pl.tree = pl.parent.tree;
+          sr_simplify_tree(pl.tree, sp);
+        } else if (choice == SR_MUT_OPTIMIZE) {
+          pl.kind = K_OPT;
+        } else {
+          bool ok = false;
+          for (int attempt = 0; attempt < 10 && !ok; ++attempt) {
+            pl.tree = pl.parent.tree;
+            apply_mutation(choice, pl.tree, temperature, curmax, rng);
+            ok = sr_check_constraints(pl.tree, sp, curmax);
+          }
+          pl.kind = ok ? K_MUT : K_REJECT;
+        }
+      } else {
+        pl.parent = best_of_sample(i);
+        pl.parent2 = best_of_sample(i);
+        bool ok = false;
+        for (int tries = 1; tries <= 11 && !ok; ++tries) {
+          sr_crossover_trees(pl.parent.tree, pl.parent2.tree, rng, &pl.tree, &pl.tree2);
+          ok = sr_check_constraints(pl.tree, sp, curmax) && sr_check_constraints(pl.tree2, sp, curmax);
+        }
+        pl.kind = ok ? K_CROSS : K_CROSS_FAIL;
+      }
+      plans.push_back(std::move(pl));
+    }
+    for (auto& pl : plans) {
+      if (pl.kind == K_MUT || pl.kind == K_CROSS) {
+        pl.slot = pending.size();
+        pending.push_back(&pl.tree);
+        if (pl.kind == K_CROSS) pending.push_back(&pl.tree2);
+      }
+    }
+    host_ms += ms_since(tp);
+    // device: ONE batched eval_cost for every island's children
+    std::vector<T> loss, cost;
+    int rc = score_trees(pending, rows, &loss, &cost);
+    if (rc) return rc;
+    const double frac = fraction(rows);
+    num_evals += double(pending.size()) * frac;
+    // batched optimize mutations (rare: weight 0 by default)
+    {
+      std::vector<Member<T>*> om;
+      std::vector<int> oi;
+      for (auto& pl : plans)
+        if (pl.kind == K_OPT && sr_count_constants(pl.parent.tree) > 0) {
+          om.push_back(&pl.parent);
+          oi.push_back(pl.island);
+        }
+      std::vector<uint8_t> imp;
+      if ((rc = optimize_members(om, oi, rows, &imp))) return rc;
+    }
+    tp = Clock::now();
+    for (auto& pl : plans) {
+      const int i = pl.island;
+      SrRng& rng = rngs[size_t(i)];
+      switch (pl.kind) {
+        case K_KEEP: {  // do_nothing: a new member with the parent's tree, cost and loss
+          Member<T> b = pl.parent;
+          b.parent = pl.parent.ref;
+          b.ref = new_ref(i);
+          b.birth = new_birth(i);
+          replace_oldest(i, std::move(b));
+          break;
+        }
+        case K_SIMPLIFIED: {
+          Member<T> b = pl.parent;
+          b.tree = std::move(pl.tree);
+          b.complexity = int(b.tree.size());
+          b.parent = pl.parent.ref;
+          b.ref = new_ref(i);
+          b.birth = new_birth(i);
+          replace_oldest(i, std::move(b));
+          break;
+        }
+        case K_OPT:  // optimize: the (possibly re-fitted) copy replaces the oldest as it is
+          replace_oldest(i, std::move(pl.parent));
+          break;
+        case K_REJECT: {
+          if (o.skip_mutation_failures) break;
+          Member<T> b = pl.parent;
+          b.parent = pl.parent.ref;
+          b.ref = new_ref(i);
+          b.birth = new_birth(i);
+          replace_oldest(i, std::move(b));
+          break;
+        }
+        case K_CROSS_FAIL:  // the two sampled copies themselves (same births)
+          if (!o.skip_mutation_failures) replace_two_oldest(i, std::move(pl.parent), std::move(pl.parent2));
+          break;
+        case K_CROSS: {
+          Member<T> b1, b2;
+          b1.tree = std::move(pl.tree);
+          b1.complexity = int(b1.tree.size());
+          b1.loss = loss[pl.slot];
+          b1.cost = cost[pl.slot];
+          b1.parent = pl.parent.ref;
+          b1.ref = new_ref(i);
+          b1.birth = new_birth(i);
+          b2.tree = std::move(pl.tree2);
+          b2.complexity = int(b2.tree.size());
+          b2.loss = loss[pl.slot + 1];
+          b2.cost = cost[pl.slot + 1];
+          b2.parent = pl.parent2.ref;
+          b2.ref = new_ref(i);
+          b2.birth = new_birth(i);
+          replace_two_oldest(i, std::move(b1), std::move(b2));
+          break;
+        }
+        case K_MUT: {
+          const T after = cost[pl.slot];
+          bool accept = !(after != after);  // NaN cost: rejected
+          if (accept) {
+            double prob = 1.0;
+            if (o.annealing) {
+              const T delta = after - pl.parent.cost;
+              prob *= exp(-double(delta) / (temperature * double(o.alpha)));
+            }
+            const int new_size = int(pl.tree.size());
+            if (o.use_frequency) {
+              const std::vector<double>& nf = snap[size_t(i)];
+              const int old_size = pl.parent.complexity;
+              const double of = (old_size > 0 && old_size <= o.maxsize) ? nf[size_t(old_size - 1)] : 1e-6;
+              const double nw = (new_size > 0 && new_size <= o.maxsize) ? nf[size_t(new_size - 1)] : 1e-6;
+              prob *= of / nw;
+            }
+            accept = !(prob < rng.uniform());
+          }
+          if (accept) {
+            Member<T> b;
+            b.tree = std::move(pl.tree);
+            b.complexity = int(b.tree.size());
+            b.loss = loss[pl.slot];
+            b.cost = after;
+            b.parent = pl.parent.ref;
+            b.ref = new_ref(i);
+            b.birth = new_birth(i);
+            replace_oldest(i, std::move(b));
+          } else if (!o.skip_mutation_failures) {
+            Member<T> b = pl.parent;
+            b.parent = pl.parent.ref;
+            b.ref = new_ref(i);
+            b.birth = new_birth(i);
+            replace_oldest(i, std::move(b));
+          }
+          break;
+        }
+      }
+    }
+    host_ms += ms_since(tp);
+    return SR_OK;
+  }
+
+  // ------------------------------------------------------------ minibatches
+  // batch(dataset, batch_size): rows drawn with replacement.  One minibatch per iteration shared by
+  // every island, from a stream keyed by (seed, iteration) so all ranks draw the same one (the
+  // reference draws one per island's s_r_cycle; sharing it lets one launch score all islands).
+  std::vector<int64_t> draw_batch(uint64_t salt) const {
+    std::vector<int64_t> rows;
+    if (!o.batching) return rows;
+    SrRng r;
+    r.seed(seed ^ 0x6261746368ull, uint64_t(iteration) * 4 + salt);
+    rows.resize(size_t(o.batch_size));
+    for (auto& v : rows) v = r.below(n_rows);
+    return rows;
+  }
+
+  // ------------------------------------------------------------ public steps
+  int start(int niterations) {
+    const int np = o.populations;
+    pops.assign(size_t(np), {});
+    rngs.assign(size_t(np), SrRng());
+    births.assign(size_t(np), 0);
+    refs.assign(size_t(np), 0);
+    best_seen.assign(size_t(np), Hof<T>());
+    for (auto& h : best_seen) h.reset(o.maxsize);
+    best_sub.assign(size_t(np), {});
+    owned.clear();
+    for (int i = 0; i < np; ++i) {
+      rngs[size_t(i)].seed(seed, uint64_t(i));
+      if (owns(i)) owned.push_back(i);
+    }
+    freq.assign(size_t(o.maxsize), 1.0);
+    hof.reset(o.maxsize);
+    total_cycles = int64_t(niterations) * np;
+    if (total_cycles < 1) total_cycles = 1;
+    cycles_remaining = total_cycles;
+    iteration = 0;
+    snap.assign(size_t(np), normalized());
+    head_maxsize = get_cur_maxsize();
+    cur_maxsize.assign(size_t(np), head_maxsize);
+    make_tournament_weights();
+    // update_baseline_loss!: the constant init_value(T) = 0 tree
+    {
+      SrTree<T> zero(1);
+      zero[0].constant = 1;
+      std::vector<T> l, c;
+      const std::vector<const SrTree<T>*> one{&zero};
+      int rc = score_trees(one, {}, &l, &c);
+      if (rc) return rc;
+      if (std::isfinite(double(l[0]))) {
+        baseline = l[0];
+        use_baseline = true;
+      } else {
+        baseline = T(1);
+        use_baseline = false;
+      }
+    }
+    // Population(dataset; population_size, nlength = 3): gen_random_tree(3) per member, one launch
+    std::vector<SrTree<T>> init;
+    std::vector<int> who;
+    for (int i : owned)
+      for (int k = 0; k < o.population_size; ++k) {
+        init.push_back(sr_gen_random_tree<T>(3, sp, rngs[size_t(i)]));
+        who.push_back(i);
+      }
+    std::vector<const SrTree<T>*> ptr;
+    for (auto& t : init) ptr.push_back(&t);
+    std::vector<T> l, c;
+    int rc = score_trees(ptr, {}, &l, &c);
+    if (rc) return rc;
+    num_evals += double(init.size());
+    for (size_t k = 0; k < init.size(); ++k) {
+      const int i = who[k];
+      Member<T> m;
+      m.tree = std::move(init[k]);
+      m.complexity = int(m.tree.size());
+      m.loss = l[k];
+      m.cost = c[k];
+      m.birth = new_birth(i);
+      m.ref = new_ref(i);
+      pops[size_t(i)].push_back(std::move(m));
+    }
+    for (int i : owned) best_sub[size_t(i)] = best_sub_pop(pops[size_t(i)]);
+    return SR_OK;
+  }
+
+  std::vector<double> normalized() const {
+    double s = 0.0;
+    for (double f : freq) s += f;
+    std::vector<double> out(freq.size());
+    for (size_t k = 0; k < freq.size(); ++k) out[k] = freq[k] / s;
+    return out;
+  }
+  int get_cur_maxsize() const {
+    const int64_t elapsed = total_cycles - cycles_remaining;
+    const float frac = float(elapsed) / float(total_cycles);
+    if (o.warmup_maxsize_by > 0.0f && frac <= o.warmup_maxsize_by)
+      return 3 + int(floorf(float(o.maxsize - 3) * frac / o.warmup_maxsize_by));
+    return o.maxsize;
+  }
+  std::vector<Member<T>> best_sub_pop(const std::vector<Member<T>>& pop) const {
+    std::vector<size_t> idx(pop.size());
+    for (size_t k = 0; k < idx.size(); ++k) idx[k] = k;
+    std::stable_sort(idx.begin(), idx.end(), [&](size_t a, size_t b) { return jl_isless(pop[a].cost, pop[b].cost); });
+    std::vector<Member<T>> out;
+    for (size_t k = 0; k < idx.size() && int(k) < o.topn; ++k) out.push_back(pop[idx[k]]);
+    return out;
+  }
+
+  // s_r_cycle + optimize_and_simplify_population (+ finalize_costs) of every owned island
+  int iterate() {
+    const std::vector<int64_t> rows = draw_batch(0);
+    for (int i : owned) best_seen[size_t(i)].reset(o.maxsize);
+    const int ncyc = o.ncycles_per_iteration;
+    const int n_evol = (o.population_size + o.tournament_selection_n - 1) / o.tournament_selection_n;
+    for (int c = 0; c < ncyc; ++c) {
+      const double temperature =
+          ncyc > 1 ? (o.annealing ? 1.0 - double(c) / double(ncyc - 1) : 1.0) : 1.0;  // LinRange(1, 0, ncyc)
+      for (int r = 0; r < n_evol; ++r) {
+        int rc = round(temperature, rows);
+        if (rc) return rc;
+      }
+      for (int i : owned)
+        for (const auto& m : pops[size_t(i)]) {
+          const int s = m.complexity;
+          auto& h = best_seen[size_t(i)];
+          if (s > 0 && s <= o.maxsize && (!h.exists[size_t(s - 1)] || m.cost < h.m[size_t(s - 1)].cost)) {
+            h.exists[size_t(s - 1)] = 1;
+            h.m[size_t(s - 1)] = m;
+          }
+        }
+    }
+    // optimize_and_simplify_population: the simplification of every member, then one batched
+    // constant optimisation over every island's selected members
+    const std::vector<int64_t> orows = draw_batch(1);
+    std::vector<Member<T>*> sel;
+    std::vector<int> sel_island;
+    for (int i : owned) {
+      auto& pop = pops[size_t(i)];
+      std::vector<uint8_t> doopt(pop.size());
+      for (size_t j = 0; j < pop.size(); ++j) doopt[j] = rngs[size_t(i)].uniform() < double(o.optimizer_probability);
+      for (size_t j = 0; j < pop.size(); ++j) {
+        if (o.should_simplify) {  // cost and loss kept; setting the tree resets the cached complexity
+          sr_simplify_tree(pop[j].tree, sp);
+          pop[j].complexity = int(pop[j].tree.size());
+        }
+        if (o.should_optimize_constants && doopt[j] && sr_count_constants(pop[j].tree) > 0) {
+          sel.push_back(&pop[j]);
+          sel_island.push_back(i);
+        }
+      }
+    }
+    std::vector<uint8_t> imp;
+    int rc = optimize_members(sel, sel_island, orows, &imp);
+    if (rc) return rc;
+    if (o.batching) {  // finalize_costs + best-seen re-scoring on the full data
+      std::vector<Member<T>*> ms;
+      for (int i : owned) {
+        for (auto& m : pops[size_t(i)]) ms.push_back(&m);
+        auto& h = best_seen[size_t(i)];
+        for (size_t s = 0; s < h.m.size(); ++s)
+          if (h.exists[s]) ms.push_back(&h.m[s]);
+      }
+      std::vector<const SrTree<T>*> tr;
+      for (auto* m : ms) tr.push_back(&m->tree);
+      std::vector<T> l, c;
+      if ((rc = score_trees(tr, {}, &l, &c))) return rc;
+      for (size_t k = 0; k < ms.size(); ++k) {
+        ms[k]->loss = l[k];
+        ms[k]->cost = cost_of(l[k], ms[k]->complexity);
+      }
+      num_evals += double(ms.size());
+    }
+    for (int i : owned)
+      for (auto& m : pops[size_t(i)]) {
+        m.parent = m.ref;
+        m.ref = new_ref(i);
+      }
+    s_r_cycles += int64_t(owned.size());
+    return SR_OK;
+  }
+
+  void hof_update(const Member<T>& m) {
+    const int s = m.complexity;
+    if (!(s > 0 && s <= o.maxsize)) return;
+    if (!sr_check_constraints(m.tree, sp, o.maxsize)) return;
+    if (!hof.exists[size_t(s - 1)] || m.cost < hof.m[size_t(s - 1)].cost) {
+      hof.m[size_t(s - 1)] = m;
+      hof.exists[size_t(s - 1)] = 1;
+    }
+  }
+  std::vector<const Member<T>*> pareto() const {
+    std::vector<const Member<T>*> out;
+    for (size_t s = 0; s < hof.m.size(); ++s) {
+      if (!hof.exists[s]) continue;
+      bool better = true;
+      for (size_t q = 0; q < s && better; ++q)
+        if (hof.exists[q] && hof.m[s].loss >= hof.m[q].loss) better = false;  // (a NaN loss stays 'better')
+      if (better) out.push_back(&hof.m[s]);
+    }
+    return out;
+  }
+  void migrate(const std::vector<const Member<T>*>& cands, int i, float frac) {
+    auto& pop = pops[size_t(i)];
+    SrRng& rng = rngs[size_t(i)];
+    const int64_t n = int64_t(pop.size());
+    const float lam = float(n) * frac;
+    int64_t k = 0;
+    if (lam != 0.0f) {  // poisson_sample in Float32
+      const float L = sr_expf(-lam);
+      float p = 1.0f;
+      while (p > L) {
+        ++k;
+        p *= rng.uniform_f32();
+      }
+      --k;
+    }
+    k = std::min<int64_t>(k, int64_t(cands.size()));
+    k = std::min<int64_t>(k, n);
+    if (k <= 0) return;
+    std::vector<int64_t> loc(static_cast<size_t>(k)), mig(static_cast<size_t>(k));
+    for (auto& v : loc) v = rng.below(n);
+    for (auto& v : mig) v = rng.below(int64_t(cands.size()));
+    for (int64_t q = 0; q < k; ++q) {
+      pop[size_t(loc[size_t(q)])] = *cands[size_t(mig[size_t(q)])];
+      pop[size_t(loc[size_t(q)])].birth = new_birth(i);
+    }
+  }
+  // the head's island-by-island bookkeeping (every rank, identically)
+  int head() {
+    for (int i = 0; i < o.populations; ++i) {
+      // the island's next cycle gets the maxsize current when its output arrives
+      cur_maxsize[size_t(i)] = head_maxsize;
+      best_sub[size_t(i)] = best_sub_pop(pops[size_t(i)]);
+      for (const auto& m : pops[size_t(i)])
+        if (m.complexity > 0 && m.complexity <= int(freq.size())) freq[size_t(m.complexity - 1)] += 1.0;
+      for (const auto& m : pops[size_t(i)]) hof_update(m);
+      const auto& bs = best_seen[size_t(i)];
+      for (size_t s = 0; s < bs.m.size(); ++s)
+        if (bs.exists[s]) hof_update(bs.m[s]);
+      const std::vector<const Member<T>*> dom = pareto();
+      if (owns(i)) {
+        if (o.migration) {
+          std::vector<const Member<T>*> c;
+          for (const auto& p : best_sub)
+            for (const auto& m : p) c.push_back(&m);
+          migrate(c, i, o.fraction_replaced);
+        }
+        if (o.hof_migration && !dom.empty()) migrate(dom, i, o.fraction_replaced_hof);
+      }
+      --cycles_remaining;
+      snap[size_t(i)] = normalized();  // the copy the island's next s_r_cycle gets
+      head_maxsize = get_cur_maxsize();
+      move_window();
+    }
+    ++iteration;
+    return SR_OK;
+  }
+  void move_window() {
+    const double window = 100000.0, smallest = 1.0;
+    double s = 0.0;
+    for (double f : freq) s += f;
+    if (s <= window) return;
+    double diff = s - window;
+    int loops = 0;
+    while (diff > 0) {
+      std::vector<size_t> idx;
+      double mn = INFINITY;
+      for (size_t k = 0; k < freq.size(); ++k)
+        if (freq[k] > smallest) {
+          idx.push_back(k);
+          mn = std::min(mn, freq[k]);
+        }
+      if (idx.empty()) break;
+      const double amount = std::min(diff / double(idx.size()), mn - smallest);
+      for (size_t k : idx) freq[k] -= amount;
+      const double total = amount * double(idx.size());
+      diff -= total;
+      ++loops;
+      if (loops > 1000 || total < 1e-6) break;
+    }
+  }
+
+  // ------------------------------------------------------------ exchange / export
+  static void put_member(Writer& w, const Member<T>& m) {
+    w.put(double(m.cost));
+    w.put(double(m.loss));
+    w.put(m.birth);
+    w.put(m.ref);
+    w.put(m.parent);
+    w.put(int32_t(m.complexity));
+    w.put(int32_t(m.tree.size()));
+    for (const auto& n : m.tree) {
+      w.put(n.degree);
+      w.put(n.op);
+      w.put(n.constant);
+      w.put(n.feature);
+      w.put(n.val);
+    }
+  }
+  static bool get_member(Reader& r, Member<T>* m) {
+    m->cost = T(r.get<double>());
+    m->loss = T(r.get<double>());
+    m->birth = r.get<int64_t>();
+    m->ref = r.get<int64_t>();
+    m->parent = r.get<int64_t>();
+    m->complexity = r.get<int32_t>();
+    const int32_t nn = r.get<int32_t>();
+    if (!r.ok || nn < 1 || nn > (1 << 20)) return false;
+    m->tree.resize(size_t(nn));
+    for (auto& n : m->tree) {
+      n.degree = r.get<uint8_t>();
+      n.op = r.get<uint8_t>();
+      n.constant = r.get<uint8_t>();
+      n.feature = r.get<uint16_t>();
+      n.val = r.get<T>();
+    }
+    return r.ok;
+  }
+  std::vector<uint8_t> export_owned() const {
+    Writer w;
+    w.put(int32_t(owned.size()));
+    for (int i : owned) {
+      w.put(int32_t(i));
+      w.put(int32_t(pops[size_t(i)].size()));
+      for (const auto& m : pops[size_t(i)]) put_member(w, m);
+      const auto& h = best_seen[size_t(i)];
+      w.put(int32_t(h.m.size()));
+      for (size_t s = 0; s < h.m.size(); ++s) {
+        w.put(h.exists[s]);
+        if (h.exists[s]) put_member(w, h.m[s]);
+      }
+    }
+    return w.buf;
+  }
+  int import_islands(const uint8_t* p, int64_t n) {
+    Reader r{p, p + n};
+    const int32_t k = r.get<int32_t>();
+    for (int32_t q = 0; q < k && r.ok; ++q) {
+      const int32_t i = r.get<int32_t>();
+      if (i < 0 || i >= o.populations) return sr_set_error(SR_ERR_INVALID_ARG, "island index out of range");
+      const int32_t nm = r.get<int32_t>();
+      std::vector<Member<T>> pop(static_cast<size_t>(std::max(nm, 0)));
+      for (auto& m : pop)
+        if (!get_member(r, &m)) return sr_set_error(SR_ERR_INVALID_ARG, "truncated island buffer");
+      Hof<T> h;
+      const int32_t ns = r.get<int32_t>();
+      h.reset(ns);
+      for (int32_t s = 0; s < ns && r.ok; ++s) {
+        h.exists[size_t(s)] = r.get<uint8_t>();
+        if (h.exists[size_t(s)] && !get_member(r, &h.m[size_t(s)]))
+          return sr_set_error(SR_ERR_INVALID_ARG, "truncated island buffer");
+      }
+      if (!r.ok) return sr_set_error(SR_ERR_INVALID_ARG, "truncated island buffer");
+      if (owns(i)) continue;  // this rank's own islands are authoritative here
+      pops[size_t(i)] = std::move(pop);
+      best_seen[size_t(i)] = std::move(h);
+    }
+    return r.ok ? SR_OK : sr_set_error(SR_ERR_INVALID_ARG, "truncated island buffer");
+  }
+  std::vector<const Member<T>*> members_of(int which) const {
+    std::vector<const Member<T>*> out;
+    if (which >= 0) {
+      for (const auto& m : pops[size_t(which)]) out.push_back(&m);
+    } else if (which == SR_SEARCH_HALL_OF_FAME) {
+      for (size_t s = 0; s < hof.m.size(); ++s)
+        if (hof.exists[s]) out.push_back(&hof.m[s]);
+    } else if (which == SR_SEARCH_PARETO) {
+      out = pareto();
+    }
+    return out;
+  }
+};
+
+template <typename T>
+Engine<T>* as_engine(sr_search* s) {
+  return static_cast<Engine<T>*>(reinterpret_cast<sr_search_base*>(s));
+}
+
+template <typename R, typename F>
+int dispatch(sr_search* s, F f) {
+  if (!s) return sr_set_error(SR_ERR_INVALID_ARG, "NULL search handle");
+  auto* b = reinterpret_cast<sr_search_base*>(s);
+  if (b->dtype == SR_DTYPE_F32) return f(as_engine<float>(s));
+  return f(as_engine<double>(s));
+}
+
+}  // namespace
+
+extern "C" {
+
+int sr_search_create(int dtype, int64_t nfeatures, int64_t n_rows, int n_unary, const char* const* unary_names,
+                     int n_binary, const char* const* binary_names, const sr_search_options* opts, uint64_t seed,
+                     int rank, int world_size, sr_search** out) {
+  if (!opts || !out) return sr_set_error(SR_ERR_INVALID_ARG, "NULL options or output handle");
+  if (dtype != SR_DTYPE_F32 && dtype != SR_DTYPE_F64) return sr_set_error(SR_ERR_INVALID_ARG, "unknown dtype");
+  if (nfeatures < 1 || nfeatures > 65535 || n_rows < 1) return sr_set_error(SR_ERR_INVALID_ARG, "bad dataset shape");
+  if (world_size < 1 || rank < 0 || rank >= world_size) return sr_set_error(SR_ERR_INVALID_ARG, "bad rank / world size");
+  const sr_search_options& o = *opts;
+  // (tournament_selection_n > population_size samples the whole island: min(n, pop) as Population.jl)
+  if (o.populations < 1 || o.population_size < 2 || o.tournament_selection_n < 1 || o.maxsize < 1 || o.ncycles_per_iteration < 1 ||
+      o.optimizer_nrestarts < 0 || o.optimizer_iterations < 0 || (o.batching && o.batch_size < 1))
+    return sr_set_error(SR_ERR_INVALID_ARG, "invalid search options");
+  if (n_unary < 0 || n_binary < 0 || n_unary + n_binary == 0 || n_unary > 255 || n_binary > 255)
+    return sr_set_error(SR_ERR_INVALID_ARG, "bad operator counts");
+  SrTreeSpec sp;
+  sp.nfeatures = int(nfeatures);
+  sp.nops[0] = n_unary;
+  sp.nops[1] = n_binary;
+  for (int k = 0; k < n_unary; ++k) {
+    const uint32_t id = unary_names && unary_names[k] ? sr_unary_id(unary_names[k]) : 0;
+    if (!id) return sr_set_error(SR_ERR_UNSUPPORTED_OP, "unsupported unary operator");
+    sp.unary_ids.push_back(id);
+  }
+  for (int k = 0; k < n_binary; ++k) {
+    const uint32_t id = binary_names && binary_names[k] ? sr_binary_id(binary_names[k]) : 0;
+    if (!id) return sr_set_error(SR_ERR_UNSUPPORTED_OP, "unsupported binary operator");
+    sp.binary_ids.push_back(id);
+  }
+  sp.maxdepth = o.maxdepth > 0 ? o.maxdepth : o.maxsize;
+  sp.perturbation_factor = double(o.perturbation_factor);
+  sp.probability_negate_constant = double(o.probability_negate_constant);
+  auto make = [&](auto* e) {
+    e->dtype = dtype;
+    e->o = o;
+    e->sp = sp;
+    e->n_rows = n_rows;
+    e->seed = seed;
+    e->rank = rank;
+    e->world = world_size;
+    *out = reinterpret_cast<sr_search*>(static_cast<sr_search_base*>(e));
+    return SR_OK;
+  };
+  if (dtype == SR_DTYPE_F32) return make(new Engine<float>());
+  return make(new Engine<double>());
+}
+
+int sr_search_free(sr_search* s) {
+  if (s) delete reinterpret_cast<sr_search_base*>(s);
+  return SR_OK;
+}
+
+int sr_search_use_device(sr_search* s, sr_ctx* ctx, const sr_dataset* ds, int opset_id, int loss_code) {
+  return dispatch<int>(s, [&](auto* e) {
+    if (!ctx || !ds) return sr_set_error(SR_ERR_INVALID_ARG, "NULL context or dataset");
+    int dt = 0;
+    int64_t nf = 0, n = 0;
+    int rc = sr_dataset_info(ds, &dt, &nf, &n);
+    if (rc) return rc;
+    if (dt != e->dtype || nf != e->sp.nfeatures || n != e->n_rows)
+      return sr_set_error(SR_ERR_INVALID_ARG, "dataset does not match the search (dtype, features, rows)");
+    e->ctx = ctx;
+    e->ds = ds;
+    e->opset_id = opset_id;
+    e->loss_code = loss_code;
+    e->loss_cb = nullptr;
+    e->grad_cb = nullptr;
+    return SR_OK;
+  });
+}
+
+int sr_search_use_callbacks(sr_search* s, sr_loss_fn loss, sr_grad_fn grad, void* user) {
+  return dispatch<int>(s, [&](auto* e) {
+    if (!loss) return sr_set_error(SR_ERR_INVALID_ARG, "NULL loss callback");
+    e->loss_cb = loss;
+    e->grad_cb = grad;
+    e->cb_user = user;
+    e->ctx = nullptr;
+    e->ds = nullptr;
+    return SR_OK;
+  });
+}
+
+int sr_search_start(sr_search* s, int niterations) {
+  return dispatch<int>(s, [&](auto* e) {
+    if (!e->ctx && !e->loss_cb) return sr_set_error(SR_ERR_INVALID_ARG, "no scorer: call sr_search_use_device first");
+    if (niterations < 0) return sr_set_error(SR_ERR_INVALID_ARG, "negative iteration count");
+    return e->start(niterations);
+  });
+}
+
+int sr_search_iterate(sr_search* s) {
+  return dispatch<int>(s, [&](auto* e) {
+    if (e->pops.empty()) return sr_set_error(SR_ERR_INVALID_ARG, "search not started");
+    return e->iterate();
+  });
+}
+
+int sr_search_head(sr_search* s) {
+  return dispatch<int>(s, [&](auto* e) {
+    if (e->pops.empty()) return sr_set_error(SR_ERR_INVALID_ARG, "search not started");
+    for (int i = 0; i < e->o.populations; ++i)
+      if (e->pops[size_t(i)].empty()) return sr_set_error(SR_ERR_INVALID_ARG, "island missing: import every rank's islands first");
+    return e->head();
+  });
+}
+
+int sr_search_export(sr_search* s, void* buf, int64_t capacity, int64_t* size) {
+  return dispatch<int>(s, [&](auto* e) {
+    if (!size) return sr_set_error(SR_ERR_INVALID_ARG, "NULL size");
+    const std::vector<uint8_t> b = e->export_owned();
+    *size = int64_t(b.size());
+    if (buf && capacity >= int64_t(b.size())) memcpy(buf, b.data(), b.size());
+    return SR_OK;
+  });
+}
+
+int sr_search_import(sr_search* s, const void* buf, int64_t size) {
+  return dispatch<int>(s, [&](auto* e) {
+    if (!buf || size < 4) return sr_set_error(SR_ERR_INVALID_ARG, "empty island buffer");
+    return e->import_islands(static_cast<const uint8_t*>(buf), size);
+  });
+}
+
+int sr_search_get_info(sr_search* s, sr_search_info* out) {
+  return dispatch<int>(s, [&](auto* e) {
+    if (!out) return sr_set_error(SR_ERR_INVALID_ARG, "NULL output");
+    out->iterations = e->iteration;
+    out->s_r_cycles = e->s_r_cycles;
+    out->num_evals = e->num_evals;
+    out->device_calls = e->device_calls;
+    out->device_ms = e->device_ms;
+    out->host_ms = e->host_ms;
+    out->baseline_loss = double(e->baseline);
+    out->use_baseline = e->use_baseline ? 1 : 0;
+    return SR_OK;
+  });
+}
+
+int sr_search_member_count(sr_search* s, int which, int64_t* n_members, int64_t* n_nodes) {
+  return dispatch<int>(s, [&](auto* e) {
+    if (!n_members || !n_nodes) return sr_set_error(SR_ERR_INVALID_ARG, "NULL output");
+    if (which >= e->o.populations || which < SR_SEARCH_PARETO || (which >= 0 && e->pops.empty()))
+      return sr_set_error(SR_ERR_INVALID_ARG, "bad member set");
+    const auto ms = e->members_of(which);
+    *n_members = int64_t(ms.size());
+    int64_t nn = 0;
+    for (auto* m : ms) nn += int64_t(m->tree.size());
+    *n_nodes = nn;
+    return SR_OK;
+  });
+}
+
+int sr_search_members(sr_search* s, int which, int64_t* offsets, uint8_t* degree, uint8_t* op, uint16_t* feature,
+                      uint8_t* constant, void* val, void* cost, void* loss, int64_t* birth, int64_t* ref,
+                      int64_t* parent, int32_t* complexity) {
+  return dispatch<int>(s, [&](auto* e) {
+    using T = std::remove_reference_t<decltype(e->baseline)>;
+    if (which >= e->o.populations || which < SR_SEARCH_PARETO || (which >= 0 && e->pops.empty()))
+      return sr_set_error(SR_ERR_INVALID_ARG, "bad member set");
+    if (!offsets || !degree || !op || !feature || !constant || !val || !cost || !loss || !birth || !ref || !parent ||
+        !complexity)
+      return sr_set_error(SR_ERR_INVALID_ARG, "NULL output array");
+    const auto ms = e->members_of(which);
+    int64_t at = 0;
+    offsets[0] = 0;
+    for (size_t k = 0; k < ms.size(); ++k) {
+      const auto* m = ms[k];
+      for (const auto& n : m->tree) {
+        degree[at] = n.degree;
+        op[at] = n.op;
+        feature[at] = n.feature;
+        constant[at] = n.constant;
+        static_cast<T*>(val)[at] = n.val;
+        ++at;
+      }
+      offsets[k + 1] = at;
+      static_cast<T*>(cost)[k] = m->cost;
+      static_cast<T*>(loss)[k] = m->loss;
+      birth[k] = m->birth;
+      ref[k] = m->ref;
+      parent[k] = m->parent;
+      complexity[k] = m->complexity;
+    }
+    return SR_OK;
+  });
+}
+
+}  // extern "C"

@@ -38,7 +38,7 @@ from .node import (
 )
 from .operators import OperatorEnum
 from .options import Options
-from .search import HallOfFame, PopMember, RunningSearchStatistics, SearchOptions, equation_search
+from .search import HallOfFame, PopMember, SearchOptions, equation_search
 
 __all__ = [
     "Options", "OperatorEnum", "Dataset", "SubDataset", "batch", "Node", "TreeBatch", "flatten_trees",
@@ -48,5 +48,5 @@ __all__ = [
     "update_baseline_loss_", "score_func", "compute_complexity", "gen_random_tree_fixed_size",
     "gen_random_population", "make_random_leaf", "get_context", "device_available", "DeviceContext",
     "SRError", "UnsupportedOperatorError", "optimize_constants_batch", "equation_search", "SearchOptions",
-    "PopMember", "HallOfFame", "RunningSearchStatistics",
+    "PopMember", "HallOfFame",
 ]

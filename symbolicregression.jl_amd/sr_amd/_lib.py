@@ -60,7 +60,25 @@ EXPORTED_SYMBOLS = (
     "sr_host_unary",
     "sr_last_kernel_ms",
     "sr_last_phase_ms",
+    "sr_search_create",
+    "sr_search_free",
+    "sr_search_use_device",
+    "sr_search_use_callbacks",
+    "sr_search_start",
+    "sr_search_iterate",
+    "sr_search_head",
+    "sr_search_export",
+    "sr_search_import",
+    "sr_search_get_info",
+    "sr_search_member_count",
+    "sr_search_members",
 )
+
+# mutation kinds in sr_search_options.mutation_weights order (SR_MUT_*)
+MUTATIONS = ("mutate_constant", "mutate_operator", "mutate_feature", "swap_operands", "rotate_tree", "add_node",
+             "insert_node", "delete_node", "simplify", "randomize", "do_nothing", "optimize")
+SR_SEARCH_HALL_OF_FAME = -1
+SR_SEARCH_PARETO = -2
 
 
 class SRError(RuntimeError):
@@ -85,6 +103,36 @@ class SrTreeBatch(ctypes.Structure):
         ("constant", POINTER(c_uint8)),
         ("val", c_void_p),
     ]
+
+
+c_float = ctypes.c_float
+
+
+class SrSearchOptions(ctypes.Structure):
+    _fields_ = [
+        ("populations", c_int), ("population_size", c_int), ("ncycles_per_iteration", c_int),
+        ("tournament_selection_n", c_int), ("tournament_selection_p", c_float),
+        ("maxsize", c_int), ("maxdepth", c_int), ("parsimony", c_float), ("crossover_probability", c_float),
+        ("annealing", c_int), ("alpha", c_float), ("perturbation_factor", c_float),
+        ("probability_negate_constant", c_float), ("use_frequency", c_int), ("use_frequency_in_tournament", c_int),
+        ("adaptive_parsimony_scaling", c_double), ("fraction_replaced", c_float), ("fraction_replaced_hof", c_float),
+        ("topn", c_int), ("migration", c_int), ("hof_migration", c_int), ("skip_mutation_failures", c_int),
+        ("should_simplify", c_int), ("should_optimize_constants", c_int), ("optimizer_probability", c_float),
+        ("optimizer_iterations", c_int), ("optimizer_nrestarts", c_int), ("batching", c_int),
+        ("batch_size", c_int64), ("warmup_maxsize_by", c_float), ("mutation_weights", c_double * len(MUTATIONS)),
+    ]
+
+
+class SrSearchInfo(ctypes.Structure):
+    _fields_ = [
+        ("iterations", c_int64), ("s_r_cycles", c_int64), ("device_calls", c_int64), ("num_evals", c_double),
+        ("device_ms", c_double), ("host_ms", c_double), ("baseline_loss", c_double), ("use_baseline", c_int),
+    ]
+
+
+# CPU scorer callbacks (tests): sr_loss_fn / sr_grad_fn
+LOSS_FN = ctypes.CFUNCTYPE(c_int, c_void_p, POINTER(SrTreeBatch), c_void_p, c_int64, c_void_p, c_void_p)
+GRAD_FN = ctypes.CFUNCTYPE(c_int, c_void_p, POINTER(SrTreeBatch), c_void_p, c_int64, c_void_p, c_void_p, c_void_p)
 
 
 def _load():
@@ -147,6 +195,22 @@ def _load():
         "sr_host_unary": (c_int, [c_int, c_char_p, c_int64, P, P]),
         "sr_last_kernel_ms": (c_int, [P, POINTER(c_double), POINTER(c_double)]),
         "sr_last_phase_ms": (c_int, [P, POINTER(c_double), c_int]),
+        "sr_search_create": (
+            c_int,
+            [c_int, c_int64, c_int64, c_int, POINTER(c_char_p), c_int, POINTER(c_char_p), POINTER(SrSearchOptions),
+             ctypes.c_uint64, c_int, c_int, POINTER(P)],
+        ),
+        "sr_search_free": (c_int, [P]),
+        "sr_search_use_device": (c_int, [P, P, P, c_int, c_int]),
+        "sr_search_use_callbacks": (c_int, [P, LOSS_FN, GRAD_FN, P]),
+        "sr_search_start": (c_int, [P, c_int]),
+        "sr_search_iterate": (c_int, [P]),
+        "sr_search_head": (c_int, [P]),
+        "sr_search_export": (c_int, [P, P, c_int64, POINTER(c_int64)]),
+        "sr_search_import": (c_int, [P, P, c_int64]),
+        "sr_search_get_info": (c_int, [P, POINTER(SrSearchInfo)]),
+        "sr_search_member_count": (c_int, [P, c_int, POINTER(c_int64), POINTER(c_int64)]),
+        "sr_search_members": (c_int, [P, c_int, P, P, P, P, P, P, P, P, P, P, P, P]),
     }
     for name, (res, args) in proto.items():
         fn = getattr(lib, name)

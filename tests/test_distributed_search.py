@@ -3,7 +3,7 @@
 Two processes each own half of the islands (island i on rank i % 2), score only their islands'
 children, all-gather the islands after every iteration and replay the head node's bookkeeping
 (statistics, hall of fame, Pareto frontier, migration by the owner).  The scorer is the oracle
-(CPU test stand-in for the device call, injected through ``_score_fn``); the search logic and the
+(CPU test stand-in for the device call, injected through ``_loss_fn``); the search engine and the
 exchange are the product code.  Random streams and birth counters are per island, so the sharded
 search must reproduce the single-process search exactly: same hall of fame, same populations.
 """
@@ -25,7 +25,7 @@ def _free_port():
 def _setup():
     sys.path[:0] = [os.path.join(ROOT, "symbolicregression.jl_amd"), os.path.join(ROOT, "oracle")]
     from oracle import Oracle
-    from sr_amd import Options, flatten_trees, loss_to_cost
+    from sr_amd import Options
 
     opts = Options(binary_operators=["+", "*", "/", "-"], unary_operators=["cos", "exp"], populations=4,
                    population_size=12, ncycles_per_iteration=25, maxsize=15, should_optimize_constants=False)
@@ -34,13 +34,10 @@ def _setup():
     y = 2 * np.cos(X[1]) + X[0] ** 2 - 2
     orc = Oracle.from_options(opts)
 
-    def score(trees, ds):
-        tb = flatten_trees(trees, ds.dtype)
-        losses, comp = orc.eval_loss_batch(tb, ds.X, ds.y, accum="ref")
-        losses = np.where(comp, losses, np.inf)
-        costs = np.array([loss_to_cost(losses[k], ds.use_baseline, ds.baseline_loss, trees[k], opts,
-                                       trees[k].count_nodes()) for k in range(len(trees))])
-        return costs, losses
+    def score(tb, rows):
+        Xv, yv = (X, y) if rows is None else (X[:, rows], y[rows])
+        losses, comp = orc.eval_loss_batch(tb, Xv, yv, accum="ref")
+        return np.where(comp, losses, np.inf)
 
     return opts, X, y, score
 
@@ -63,7 +60,7 @@ def _worker(rank, world, port, q):
 
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
-        res = equation_search(X, y, niterations=3, options=opts, seed=5, distributed=True, _score_fn=score)
+        res = equation_search(X, y, niterations=3, options=opts, seed=5, distributed=True, _loss_fn=score)
         q.put((rank, _summary(res), res.num_evals))
     finally:
         dist.destroy_process_group()
@@ -75,7 +72,7 @@ def test_island_sharded_search_equals_single_process():
     opts, X, y, score = _setup()
     from sr_amd import equation_search
 
-    single = equation_search(X, y, niterations=3, options=opts, seed=5, _score_fn=score)
+    single = equation_search(X, y, niterations=3, options=opts, seed=5, _loss_fn=score)
     ref = _summary(single)
 
     ctx = mp.get_context("spawn")

@@ -70,22 +70,18 @@ def test_c3_search_device_equals_oracle_scored_search():
     not happen on this run (the test would show it)."""
     from oracle import Oracle
 
-    from sr_amd.search import _costs
-
     X, y = _c3_data()
     opts = Options(binary_operators=["+", "-", "*", "/"], unary_operators=["cos", "exp", "log"], populations=4,
                    population_size=20, ncycles_per_iteration=12, maxsize=20, should_optimize_constants=False)
     orc = Oracle.from_options(opts)
 
-    def oracle_score(trees, ds):
-        tb = flatten_trees(trees, np.float32)
-        idx = getattr(ds, "indices", None)
-        Xv, yv = (X, y) if idx is None else (X[:, idx], y[idx])
-        losses, _ = orc.eval_loss_batch(tb, Xv, yv, accum="f64", n_threads=8)
-        return _costs(losses, tb.tree_sizes(), ds, opts), losses
+    def oracle_loss(tb, rows):
+        Xv, yv = (X, y) if rows is None else (X[:, rows], y[rows])
+        losses, comp = orc.eval_loss_batch(tb, Xv, yv, accum="f64", n_threads=8)
+        return np.where(comp, losses, np.inf)
 
     dev = equation_search(X, y, niterations=2, options=opts, seed=5)
-    ref = equation_search(X, y, niterations=2, options=opts, seed=5, _score_fn=oracle_score)
+    ref = equation_search(X, y, niterations=2, options=opts, seed=5, _loss_fn=oracle_loss)
 
     def trees(res):
         return [[string_tree(m.tree, opts.operators) for m in p] for p in res.populations]

@@ -21,7 +21,8 @@ def run(name, X, y, opts, niterations):
     print(json.dumps({"config": name, "islands": opts.populations, "iterations": niterations,
                       "s_r_cycles": res.s_r_cycles, "wall_s": wall,
                       "s_r_cycles_per_s": res.s_r_cycles / wall, "iterations_per_s": niterations / wall,
-                      "device_calls": res.device_calls, "num_evals": res.num_evals, "best_loss": best.loss}),
+                      "device_calls": res.device_calls, "device_s": res.device_s, "host_s": res.host_s,
+                      "device_fraction": res.device_s / wall, "num_evals": res.num_evals, "best_loss": float(best.loss)}),
           flush=True)
 
 
@@ -33,11 +34,11 @@ if __name__ == "__main__":
         y = 2 * np.cos(X[1]) + X[0] ** 2 - 2
         opts = Options(binary_operators=["+", "*", "/", "-"], unary_operators=["cos", "exp"], populations=20)
         run("C1 README example (X=randn(2,100) f64, 20 populations, default options)", X, y, opts,
-            int(os.environ.get("C1_ITERS", "2")))
+            int(os.environ.get("C1_ITERS", "40")))
     if "C3" in which:
         rng = np.random.default_rng(1)
         X = rng.uniform(1, 5, size=(5, 100_000)).astype(np.float32)
         y = (X[0] * X[1] * X[2] / (X[3] * X[4] ** 2 + 1)).astype(np.float32)
         opts = Options(binary_operators=["+", "-", "*", "/"], unary_operators=["cos", "exp"])
         run("C3 Feynman-style 5 features x 100k rows f32 (31 populations, default options)", X, y, opts,
-            int(os.environ.get("C3_ITERS", "1")))
+            int(os.environ.get("C3_ITERS", "5")))
