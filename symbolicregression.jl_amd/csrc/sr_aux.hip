@@ -9,6 +9,9 @@
 // One thread per launch position: Σ over row blocks in row-block order (bit-reproducible), OR of
 // flags (partials are laid out [row block][position], so neighbouring threads read neighbouring
 // words); the result goes to the caller's tree index perm[position].
+// One wave per tree: lane l folds row blocks l, l + 64, ... in order, then a fixed butterfly adds the
+// 64 lane sums (deterministic: the same tree gives the same bits whatever the batch).  A thread per
+// tree walking every row block serialises its loads (C3's 196 row blocks: 47 us per call).
 __global__ void __launch_bounds__(256) sr_reduce_partials_kernel(const double* __restrict__ part_sum,
                                                                   const uint32_t* __restrict__ part_flag,
                                                                   int n_trees, int n_row_blocks,
@@ -16,18 +19,26 @@ __global__ void __launch_bounds__(256) sr_reduce_partials_kernel(const double* _
                                                                   const uint8_t* __restrict__ static_bad,
                                                                   double* __restrict__ out_sum,
                                                                   uint32_t* __restrict__ out_flag) {
-  const int pos = int(int64_t(blockIdx.x) * blockDim.x + threadIdx.x);
-  if (pos >= n_trees) return;
-  const int tree = perm ? int(perm[pos]) : pos;
+  const int lane = int(threadIdx.x) & 63;
+  const int pos = int(int64_t(blockIdx.x) * (blockDim.x / 64) + threadIdx.x / 64);
+  if (pos >= n_trees) return;  // wave-uniform
   double s = 0.0;
   uint32_t f = 0u;
-  for (int i = 0; i < n_row_blocks; ++i) {
+  for (int i = lane; i < n_row_blocks; i += 64) {
     s += part_sum[size_t(i) * n_trees + pos];
     f |= part_flag[size_t(i) * n_trees + pos];
   }
-  if (static_bad && static_bad[tree]) f |= SR_FLAG_STATIC | SR_FLAG_NONFINITE;
-  out_sum[tree] = s;
-  out_flag[tree] = f;
+#pragma unroll
+  for (int off = 32; off >= 1; off >>= 1) {
+    s += __shfl_xor(s, off, 64);
+    f |= __shfl_xor(f, off, 64);
+  }
+  if (lane == 0) {
+    const int tree = perm ? int(perm[pos]) : pos;
+    if (static_bad && static_bad[tree]) f |= SR_FLAG_STATIC | SR_FLAG_NONFINITE;
+    out_sum[tree] = s;
+    out_flag[tree] = f;
+  }
 }
 
 // Packed row-shard partials for one all-reduce (sr_eval_loss_partials_packed): [4][n] f64 = Σ loss,
@@ -72,7 +83,7 @@ hipError_t sr_launch_reduce(const double* part_sum, const uint32_t* part_flag, i
                             const uint32_t* perm, const uint8_t* static_bad, double* out_sum, uint32_t* out_flag,
                             hipStream_t s) {
   if (n_trees <= 0) return hipSuccess;
-  const int64_t blocks = (int64_t(n_trees) + 255) / 256;
+  const int64_t blocks = (int64_t(n_trees) + 3) / 4;  // 4 waves (trees) per block
   hipLaunchKernelGGL(sr_reduce_partials_kernel, dim3(unsigned(blocks)), dim3(256), 0, s, part_sum, part_flag,
                      n_trees, n_row_blocks, perm, static_bad, out_sum, out_flag);
   return hipGetLastError();

@@ -122,13 +122,35 @@ struct sr_ctx {
   hipEvent_t ev_start = nullptr, ev_k0 = nullptr, ev_k1 = nullptr, ev_end = nullptr;
   hipEvent_t ev_c0[kMaxChunks] = {}, ev_c1[kMaxChunks] = {};  // per-chunk interpreter launches
   int n_chunks_last = 0;
-  HostBuf h_code, h_offsets, h_static_bad, h_perm;
+  // programs + per-tree metadata of the last run_batch: ONE device allocation and ONE pinned staging
+  // buffer with the same layout (code | offsets | static_bad | launch order), so a single-chunk call
+  // uploads with one DMA; per-tree {Σ loss, flags} likewise share one allocation (one DMA back)
+  HostBuf h_prog, h_outs;
+  void* d_code = nullptr;
+  uint32_t* d_off = nullptr;
+  uint8_t* d_bad = nullptr;
+  uint32_t* d_perm = nullptr;
+  double* d_out_sum = nullptr;
+  uint32_t* d_out_flag = nullptr;
+  size_t outs_flag_off = 0;
+  // Small single-chunk LOSS calls (the search's regime: tens of trees, ~100 rows) are latency-bound:
+  // SR_AMD_HOST_IO = 1 (default) lets the kernel write the per-tree results straight into pinned
+  // host memory (no copy back), 2 also lets it read the programs from the pinned staging buffer (no
+  // upload), 0 keeps both copies.
+  int host_io = 1;
+  bool want_host_out = false;  // set by eval_loss_impl around its run_batch
+  bool outs_on_host = false;   // the last run_batch wrote {Σ, flags} to h_outs
+  // SR_AMD_SPIN = 1: small calls wait by polling hipStreamQuery instead of hipStreamSynchronize
+  // (measured slower on the box: 61 vs 50 us per 20-tree call, the polling slows the runtime's other
+  // threads; off by default)
+  int spin = 0;
+  uint32_t hint_epoch = 0;  // dead-tree hint epoch of the current call
   std::mutex mu;
   std::vector<SrOpset> opsets;
   std::vector<int> tiers;
   std::vector<std::pair<int, double>> losses;  // registered (kind, param); code = kLossCodeBase + index
-  DevBuf code, offsets, static_bad, part_sum, part_flag, out_sum, out_flag, pred, row_idx, tree_list,
-      range_lo, range_hi, range_sums, packed, perm, hint, probe_sum, probe_flag, g_code, g_offsets, g_consts, g_const_off, g_items, g_part, g_out;
+  DevBuf prog, outs, part_sum, part_flag, pred, row_idx, tree_list,
+      range_lo, range_hi, range_sums, packed, hint, probe_sum, probe_flag, g_code, g_offsets, g_consts, g_const_off, g_items, g_part, g_out;
   double last_eval_ms = 0.0, last_total_ms = 0.0;
   // host-side phases of the last eval_loss call (ms): compile, upload+launch, wait, exact pass,
   // finalize (sr_last_phase_ms)
@@ -253,7 +275,7 @@ int decode_loss(sr_ctx* ctx, int code, int* kind, double* param) {
 }
 
 // Shared engine: compile + upload + interpreter(+reduce).  Leaves per-tree {sum, flag} in
-// ctx->out_sum / ctx->out_flag (device).  n_eval rows (full dataset or row_idx view).
+// ctx->d_out_sum / ctx->d_out_flag (device).  n_eval rows (full dataset or row_idx view).
 //
 // Large LOSS batches are pipelined in up to kMaxChunks tree chunks: the host compiles chunk c+1
 // while the device runs chunk c (programs staged through pinned memory, async DMA).  Every chunk is
@@ -314,22 +336,46 @@ int run_batch(sr_ctx* ctx, const sr_dataset* ds, int opset_id, const sr_tree_bat
     n_rb = std::max(n_rb, make_grid<T>(n_eval, nt > 0 ? nt : 1, Rv, W, int(ds->nf), 0, 0, ds->w != nullptr,
                                        ctx->tree_group, ctx->max_row_blocks).n_row_blocks);
   const size_t code_cap = size_t(total_nodes) + 16;
-  SR_HIP_CHECK(ctx->code.ensure(code_cap * sizeof(SrIns<T>)));
-  SR_HIP_CHECK(ctx->offsets.ensure((size_t(nt) + 1) * sizeof(uint32_t)));
-  SR_HIP_CHECK(ctx->static_bad.ensure(size_t(nt) + 16));
-  SR_HIP_CHECK(ctx->perm.ensure((size_t(nt) + 1) * sizeof(uint32_t)));
-  SR_HIP_CHECK(ctx->h_code.ensure(code_cap * sizeof(SrIns<T>), s, ctx->stream2));
-  SR_HIP_CHECK(ctx->h_offsets.ensure((size_t(nt) + 1) * sizeof(uint32_t), s, ctx->stream2));
-  SR_HIP_CHECK(ctx->h_static_bad.ensure(size_t(nt) + 16, s, ctx->stream2));
-  SR_HIP_CHECK(ctx->h_perm.ensure((size_t(nt) + 1) * sizeof(uint32_t), s, ctx->stream2));
+  auto align256 = [](size_t x) { return (x + 255) & ~size_t(255); };
+  const size_t o_off = align256(code_cap * sizeof(SrIns<T>));
+  const size_t o_bad = align256(o_off + (size_t(nt) + 1) * sizeof(uint32_t));
+  const size_t o_perm = align256(o_bad + size_t(nt) + 16);
+  const size_t prog_bytes = o_perm + (size_t(nt) + 1) * sizeof(uint32_t);
+  SR_HIP_CHECK(ctx->prog.ensure(prog_bytes));
+  SR_HIP_CHECK(ctx->h_prog.ensure(prog_bytes, s, ctx->stream2));
+  char* const dprog = ctx->prog.as<char>();  // (re-pointed at the staging buffer below for host_prog)
+  ctx->d_code = dprog;
+  ctx->d_off = reinterpret_cast<uint32_t*>(dprog + o_off);
+  ctx->d_bad = reinterpret_cast<uint8_t*>(dprog + o_bad);
+  ctx->d_perm = reinterpret_cast<uint32_t*>(dprog + o_perm);
   const size_t n_part = size_t(nt) * size_t(n_rb);
   SR_HIP_CHECK(ctx->part_sum.ensure(n_part * sizeof(double) + 8));
   SR_HIP_CHECK(ctx->part_flag.ensure(n_part * sizeof(uint32_t) + 4));
-  SR_HIP_CHECK(ctx->out_sum.ensure(size_t(nt) * sizeof(double) + 8));
-  SR_HIP_CHECK(ctx->out_flag.ensure(size_t(nt) * sizeof(uint32_t) + 4));
+  ctx->outs_flag_off = align256(size_t(nt) * sizeof(double) + 8);
+  const size_t outs_bytes = ctx->outs_flag_off + size_t(nt) * sizeof(uint32_t) + 4;
+  SR_HIP_CHECK(ctx->outs.ensure(outs_bytes));
+  // latency path (see host_io): results written to pinned host memory, programs read from it
+  const bool small_call = n_chunks == 1 && mode == SR_MODE_LOSS;
+  const bool host_out = small_call && ctx->host_io >= 1 && ctx->want_host_out;
+  const bool host_prog = small_call && ctx->host_io >= 2;
+  if (host_out) SR_HIP_CHECK(ctx->h_outs.ensure(outs_bytes, s, ctx->stream2));
+  ctx->outs_on_host = host_out;
+  ctx->d_out_sum = reinterpret_cast<double*>(host_out ? ctx->h_outs.as<char>() : ctx->outs.as<char>());
+  ctx->d_out_flag = reinterpret_cast<uint32_t*>((host_out ? ctx->h_outs.as<char>() : ctx->outs.as<char>()) +
+                                                ctx->outs_flag_off);
   if (mode == SR_MODE_PRED) SR_HIP_CHECK(ctx->pred.ensure(size_t(nt) * size_t(n_eval) * sizeof(T) + 16));
   const bool use_hint = ctx->dead_hints && mode == SR_MODE_LOSS && n_rb > 1;
-  if (use_hint) SR_HIP_CHECK(ctx->hint.ensure(size_t(nt) * sizeof(uint32_t) + 4));
+  if (use_hint) {
+    // epoch-tagged hints: each call marks dead positions with its own epoch, so the array needs a
+    // reset only when (re)allocated or when the epoch counter wraps
+    void* const before = ctx->hint.p;
+    SR_HIP_CHECK(ctx->hint.ensure(size_t(nt) * sizeof(uint32_t) + 4));
+    if (ctx->hint.p != before || ctx->hint_epoch == 0xffffffffu) {
+      SR_HIP_CHECK(hipMemsetAsync(ctx->hint.p, 0, ctx->hint.cap, s));
+      ctx->hint_epoch = 0;
+    }
+    ++ctx->hint_epoch;
+  }
   // dead-tree probe: the first kProbeTiles row tiles of the view, hints only (scratch partials)
   constexpr int kProbeTiles = 4;
   const bool use_probe = use_hint && ctx->probe && n_rb >= 16;  // (per chunk: its grid has >= 16 row blocks)
@@ -351,15 +397,21 @@ int run_batch(sr_ctx* ctx, const sr_dataset* ds, int opset_id, const sr_tree_bat
   prog->max_checks = 0;
   prog->total_nodes = 0;
   prog->total_ops = 0;
-  SrIns<T>* h_code = ctx->h_code.as<SrIns<T>>();
-  uint32_t* h_off = ctx->h_offsets.as<uint32_t>();
-  uint8_t* h_bad = ctx->h_static_bad.as<uint8_t>();
-  uint32_t* h_perm = ctx->h_perm.as<uint32_t>();
+  char* const hprog = ctx->h_prog.as<char>();
+  if (host_prog) {
+    ctx->d_code = hprog;
+    ctx->d_off = reinterpret_cast<uint32_t*>(hprog + o_off);
+    ctx->d_bad = reinterpret_cast<uint8_t*>(hprog + o_bad);
+    ctx->d_perm = reinterpret_cast<uint32_t*>(hprog + o_perm);
+  }
+  SrIns<T>* h_code = reinterpret_cast<SrIns<T>*>(hprog);
+  uint32_t* h_off = reinterpret_cast<uint32_t*>(hprog + o_off);
+  uint8_t* h_bad = reinterpret_cast<uint8_t*>(hprog + o_bad);
+  uint32_t* h_perm = reinterpret_cast<uint32_t*>(hprog + o_perm);
   ctx->n_chunks_last = 0;
   SR_HIP_CHECK(hipEventRecord(ctx->ev_start, s));
   if (gather)
     SR_HIP_CHECK(hipMemcpyAsync(ctx->row_idx.p, row_idx, size_t(n_idx) * sizeof(int64_t), hipMemcpyHostToDevice, s));
-  if (use_hint) SR_HIP_CHECK(hipMemsetAsync(ctx->hint.p, 0, size_t(nt) * sizeof(uint32_t), s));
   if (n_chunks > 1) {  // odd chunks run on the second stream, after the shared setup above
     SR_HIP_CHECK(hipEventRecord(ctx->ev_join, s));
     SR_HIP_CHECK(hipStreamWaitEvent(ctx->stream2, ctx->ev_join, 0));
@@ -431,14 +483,18 @@ int run_batch(sr_ctx* ctx, const sr_dataset* ds, int opset_id, const sr_tree_bat
       for (size_t k = 1; k < start.size(); ++k) start[k] += start[k - 1];
       for (int64_t i = 0; i < nc; ++i) h_perm[t0 + start[key(i)]++] = uint32_t(i);
     }
-    if (ncode)
-      SR_HIP_CHECK(hipMemcpyAsync(ctx->code.as<SrIns<T>>() + code_base, h_code + code_base, ncode * sizeof(SrIns<T>),
-                                  hipMemcpyHostToDevice, cs));
-    SR_HIP_CHECK(hipMemcpyAsync(ctx->offsets.as<uint32_t>() + t0, h_off + t0, size_t(nc + 1) * sizeof(uint32_t),
-                                hipMemcpyHostToDevice, cs));
-    SR_HIP_CHECK(hipMemcpyAsync(ctx->static_bad.as<uint8_t>() + t0, h_bad + t0, size_t(nc), hipMemcpyHostToDevice, cs));
-    SR_HIP_CHECK(hipMemcpyAsync(ctx->perm.as<uint32_t>() + t0, h_perm + t0, size_t(nc) * sizeof(uint32_t),
-                                hipMemcpyHostToDevice, cs));
+    if (host_prog) {
+      // the kernel reads the staging image itself
+    } else if (n_chunks == 1) {  // the whole staging image (code, offsets, static_bad, order): one DMA
+      SR_HIP_CHECK(hipMemcpyAsync(dprog, hprog, o_perm + size_t(nc) * sizeof(uint32_t), hipMemcpyHostToDevice, cs));
+    } else {
+      if (ncode)
+        SR_HIP_CHECK(hipMemcpyAsync(static_cast<SrIns<T>*>(ctx->d_code) + code_base, h_code + code_base,
+                                    ncode * sizeof(SrIns<T>), hipMemcpyHostToDevice, cs));
+      SR_HIP_CHECK(hipMemcpyAsync(ctx->d_off + t0, h_off + t0, size_t(nc + 1) * sizeof(uint32_t), hipMemcpyHostToDevice, cs));
+      SR_HIP_CHECK(hipMemcpyAsync(ctx->d_bad + t0, h_bad + t0, size_t(nc), hipMemcpyHostToDevice, cs));
+      SR_HIP_CHECK(hipMemcpyAsync(ctx->d_perm + t0, h_perm + t0, size_t(nc) * sizeof(uint32_t), hipMemcpyHostToDevice, cs));
+    }
     // merged summary
     for (int64_t i = 0; i <= nc; ++i) prog->offsets[size_t(t0 + i)] = h_off[t0 + i];
     std::memcpy(prog->static_bad.data() + t0, pc.static_bad.data(), size_t(nc));
@@ -461,10 +517,11 @@ int run_batch(sr_ctx* ctx, const sr_dataset* ds, int opset_id, const sr_tree_bat
       if (g.n_blocks > 0x7fffffff || g.n_row_blocks > n_rb) return set_error(SR_ERR_INVALID_ARG, "grid too large");
       glast = g;
       SrEvalArgs<T> a{};
-      a.code = ctx->code.as<SrIns<T>>();
-      a.offsets = ctx->offsets.as<uint32_t>() + t0;
-      a.perm = ctx->perm.as<uint32_t>() + t0 + p0;
+      a.code = static_cast<const SrIns<T>*>(ctx->d_code);
+      a.offsets = ctx->d_off + t0;
+      a.perm = ctx->d_perm + t0 + p0;
       a.hint = use_hint ? ctx->hint.as<uint32_t>() + t0 + p0 : nullptr;
+      a.hint_epoch = ctx->hint_epoch;
       a.n_trees = int(np);
       a.trees_per_block = g.G;
       a.X = static_cast<const T*>(ds->X);
@@ -487,6 +544,12 @@ int run_batch(sr_ctx* ctx, const sr_dataset* ds, int opset_id, const sr_tree_bat
       a.part_flag = ctx->part_flag.as<uint32_t>() + size_t(n_rb) * size_t(t0 + p0);
       a.pred = ctx->pred.as<T>();
       a.pred_ld = n_eval;
+      const bool direct = mode == SR_MODE_LOSS && g.n_row_blocks == 1;
+      if (direct) {  // the interpreter writes the final per-tree values; no reduce launch
+        a.out_sum = ctx->d_out_sum + t0;
+        a.out_flag = ctx->d_out_flag + t0;
+        a.static_bad = ctx->d_bad + t0;
+      }
       if (use_probe && p0 == 0 && g.n_row_blocks >= 16 && (ctx->probe != 2 || c > 0)) {
         // Trees that are non-finite on the first rows are flagged before the main launch, so its
         // workgroups skip them from their first tile (without the probe, the ~16 row blocks that
@@ -494,6 +557,8 @@ int run_batch(sr_ctx* ctx, const sr_dataset* ds, int opset_id, const sr_tree_bat
         // out of it: a tree non-finite on some rows of the view is incomplete on the whole view.
         // a wide, short grid: 16 trees x 1 tile per workgroup, kProbeTiles row blocks
         SrEvalArgs<T> pa = a;
+        pa.out_sum = nullptr;
+        pa.out_flag = nullptr;
         pa.trees_per_block = std::max(16, g.W);
         pa.n_groups = int((np + pa.trees_per_block - 1) / pa.trees_per_block);
         pa.tiles_per_block = 1;
@@ -504,9 +569,9 @@ int run_batch(sr_ctx* ctx, const sr_dataset* ds, int opset_id, const sr_tree_bat
         SR_HIP_CHECK(sr_launch_eval<T>(pa, mode, gather, tier, Rc, g.W, vstk, pa.n_groups * kProbeTiles, cs));
       }
       SR_HIP_CHECK(sr_launch_eval<T>(a, mode, gather, tier, Rc, g.W, vstk, int(g.n_blocks), cs));
-      SR_HIP_CHECK(sr_launch_reduce(a.part_sum, a.part_flag, int(np), g.n_row_blocks, a.perm,
-                                    ctx->static_bad.as<uint8_t>() + t0, ctx->out_sum.as<double>() + t0,
-                                    ctx->out_flag.as<uint32_t>() + t0, cs));
+      if (!direct)
+        SR_HIP_CHECK(sr_launch_reduce(a.part_sum, a.part_flag, int(np), g.n_row_blocks, a.perm,
+                                    ctx->d_bad + t0, ctx->d_out_sum + t0, ctx->d_out_flag + t0, cs));
       return SR_OK;
     };
     int lrc = SR_OK;
@@ -672,8 +737,8 @@ int run_exact(sr_ctx* ctx, const sr_dataset* ds, const SrProgramBatch<T>& prog, 
     SR_HIP_CHECK(hipMemcpyAsync(ctx->tree_list.p, list32.data(), size_t(nb) * sizeof(uint32_t), hipMemcpyHostToDevice, s));
     SR_HIP_CHECK(ctx->range_sums.ensure(size_t(nb) * per_tree));
     SrEvalArgs<T> a{};
-    a.code = ctx->code.as<SrIns<T>>();
-    a.offsets = ctx->offsets.as<uint32_t>();
+    a.code = static_cast<const SrIns<T>*>(ctx->d_code);
+    a.offsets = ctx->d_off;
     a.perm = ctx->tree_list.as<uint32_t>();
     a.n_trees = int(nb);
     a.trees_per_block = G;
@@ -765,16 +830,31 @@ int eval_loss_impl(sr_ctx* ctx, const sr_dataset* ds, int opset_id, const sr_tre
   ctx->start_phases(t0);
   SrProgramBatch<T> prog;
   Grid g;
+  ctx->want_host_out = true;
   int rc = run_batch<T>(ctx, ds, opset_id, trees, row_idx, n_idx, n_eval, loss_kind, SR_MODE_LOSS, &prog, &g);
+  ctx->want_host_out = false;
   if (rc != SR_OK) return rc;
   if (nt == 0) return SR_OK;
-  std::vector<double> sums(static_cast<size_t>(nt));
-  std::vector<uint32_t> flags(static_cast<size_t>(nt));
   hipStream_t s = ctx->stream;
-  SR_HIP_CHECK(hipMemcpyAsync(sums.data(), ctx->out_sum.p, size_t(nt) * sizeof(double), hipMemcpyDeviceToHost, s));
-  SR_HIP_CHECK(hipMemcpyAsync(flags.data(), ctx->out_flag.p, size_t(nt) * sizeof(uint32_t), hipMemcpyDeviceToHost, s));
+  // {Σ loss, flags} of every tree: already in pinned memory (host_io), or one DMA there
+  if (!ctx->outs_on_host) {
+    const size_t out_bytes = ctx->outs_flag_off + size_t(nt) * sizeof(uint32_t);
+    SR_HIP_CHECK(ctx->h_outs.ensure(out_bytes, s, ctx->stream2));
+    SR_HIP_CHECK(hipMemcpyAsync(ctx->h_outs.p, ctx->outs.p, out_bytes, hipMemcpyDeviceToHost, s));
+  }
   SR_HIP_CHECK(hipEventRecord(ctx->ev_end, s));
-  SR_HIP_CHECK(hipStreamSynchronize(s));
+  if (ctx->spin && ctx->outs_on_host) {
+    hipError_t e;
+    while ((e = hipStreamQuery(s)) == hipErrorNotReady) {
+    }
+    SR_HIP_CHECK(e);
+  } else {
+    SR_HIP_CHECK(hipStreamSynchronize(s));
+  }
+  const double* hs = ctx->h_outs.as<double>();
+  const uint32_t* hf = reinterpret_cast<const uint32_t*>(ctx->h_outs.as<char>() + ctx->outs_flag_off);
+  std::vector<double> sums(hs, hs + nt);
+  std::vector<uint32_t> flags(hf, hf + nt);
   ctx->last_eval_ms = chunk_kernel_ms(ctx);
   ctx->mark_phase(2);
   std::vector<int64_t> list;
@@ -810,7 +890,7 @@ int eval_pred_impl(sr_ctx* ctx, const sr_dataset* ds, int opset_id, const sr_tre
   std::vector<double> sums(static_cast<size_t>(nt));
   std::vector<uint32_t> flags(static_cast<size_t>(nt));
   SR_HIP_CHECK(hipMemcpyAsync(out_pred, ctx->pred.p, size_t(nt) * size_t(n_eval) * sizeof(T), hipMemcpyDeviceToHost, s));
-  SR_HIP_CHECK(hipMemcpyAsync(flags.data(), ctx->out_flag.p, size_t(nt) * sizeof(uint32_t), hipMemcpyDeviceToHost, s));
+  SR_HIP_CHECK(hipMemcpyAsync(flags.data(), ctx->d_out_flag, size_t(nt) * sizeof(uint32_t), hipMemcpyDeviceToHost, s));
   SR_HIP_CHECK(hipStreamSynchronize(s));
   std::vector<int64_t> list;
   for (int64_t t = 0; t < nt; ++t)
@@ -1070,6 +1150,8 @@ int sr_init(int device, sr_ctx** out) {
   if (const char* v = std::getenv("SR_AMD_NO_HINT")) ctx->dead_hints = std::atoi(v) == 0;
   if (const char* v = std::getenv("SR_AMD_CHUNKS")) ctx->chunks = std::atoi(v);
   if (const char* v = std::getenv("SR_AMD_PROBE")) ctx->probe = std::atoi(v);
+  if (const char* v = std::getenv("SR_AMD_HOST_IO")) ctx->host_io = std::atoi(v);
+  if (const char* v = std::getenv("SR_AMD_SPIN")) ctx->spin = std::atoi(v);
   if (const char* v = std::getenv("SR_AMD_MAX_ROW_BLOCKS")) ctx->max_row_blocks = std::max(1, std::atoi(v));
   hipError_t e = hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking);
   if (e == hipSuccess) e = hipStreamCreateWithFlags(&ctx->stream2, hipStreamNonBlocking);
@@ -1096,12 +1178,11 @@ int sr_shutdown(sr_ctx* ctx) {
     Lock l(ctx);
     (void)hipSetDevice(ctx->device);
     (void)hipStreamSynchronize(ctx->stream);
-    for (DevBuf* b : {&ctx->code, &ctx->offsets, &ctx->static_bad, &ctx->part_sum, &ctx->part_flag, &ctx->out_sum,
-                      &ctx->out_flag, &ctx->pred, &ctx->row_idx, &ctx->tree_list, &ctx->range_lo, &ctx->range_hi, &ctx->range_sums, &ctx->packed,
-                      &ctx->perm, &ctx->hint, &ctx->probe_sum, &ctx->probe_flag, &ctx->g_code, &ctx->g_offsets, &ctx->g_consts, &ctx->g_const_off,
+    for (DevBuf* b : {&ctx->prog, &ctx->outs, &ctx->part_sum, &ctx->part_flag, &ctx->pred, &ctx->row_idx, &ctx->tree_list, &ctx->range_lo, &ctx->range_hi, &ctx->range_sums, &ctx->packed,
+                      &ctx->hint, &ctx->probe_sum, &ctx->probe_flag, &ctx->g_code, &ctx->g_offsets, &ctx->g_consts, &ctx->g_const_off,
                       &ctx->g_items, &ctx->g_part, &ctx->g_out})
       b->release();
-    for (HostBuf* b : {&ctx->h_code, &ctx->h_offsets, &ctx->h_static_bad, &ctx->h_perm}) b->release();
+    for (HostBuf* b : {&ctx->h_prog, &ctx->h_outs}) b->release();
     for (int c = 0; c < kMaxChunks; ++c) {
       (void)hipEventDestroy(ctx->ev_c0[c]);
       (void)hipEventDestroy(ctx->ev_c1[c]);
@@ -1243,8 +1324,8 @@ int sr_eval_loss_partials(sr_ctx* ctx, const sr_dataset* ds, int opset_id, const
   if (rc != SR_OK || nt == 0) return rc;
   hipStream_t s = ctx->stream;
   const hipMemcpyKind kind = out_on_device ? hipMemcpyDeviceToDevice : hipMemcpyDeviceToHost;
-  SR_HIP_CHECK(hipMemcpyAsync(out_sum, ctx->out_sum.p, size_t(nt) * sizeof(double), kind, s));
-  SR_HIP_CHECK(hipMemcpyAsync(out_flags, ctx->out_flag.p, size_t(nt) * sizeof(uint32_t), kind, s));
+  SR_HIP_CHECK(hipMemcpyAsync(out_sum, ctx->d_out_sum, size_t(nt) * sizeof(double), kind, s));
+  SR_HIP_CHECK(hipMemcpyAsync(out_flags, ctx->d_out_flag, size_t(nt) * sizeof(uint32_t), kind, s));
   SR_HIP_CHECK(hipStreamSynchronize(s));
   ctx->last_eval_ms = chunk_kernel_ms(ctx);
   ctx->last_total_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
@@ -1277,7 +1358,7 @@ int sr_eval_loss_partials_packed(sr_ctx* ctx, const sr_dataset* ds, int opset_id
     SR_HIP_CHECK(ctx->packed.ensure(bytes));
     dst = ctx->packed.as<double>();
   }
-  SR_HIP_CHECK(sr_launch_pack_partials(ctx->out_sum.as<double>(), ctx->out_flag.as<uint32_t>(), int(nt), dst, s));
+  SR_HIP_CHECK(sr_launch_pack_partials(ctx->d_out_sum, ctx->d_out_flag, int(nt), dst, s));
   if (!out_on_device) SR_HIP_CHECK(hipMemcpyAsync(out, dst, bytes, hipMemcpyDeviceToHost, s));
   SR_HIP_CHECK(hipStreamSynchronize(s));
   ctx->last_eval_ms = chunk_kernel_ms(ctx);

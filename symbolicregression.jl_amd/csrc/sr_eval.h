@@ -15,6 +15,7 @@ struct SrEvalArgs {
   const uint32_t* offsets;     // [n_trees + 1], indexed by the caller's tree index
   const uint32_t* perm;        // launch position -> caller's tree index (NULL: identity); EXACT: tree list
   uint32_t* hint;              // [n_trees] per position: dead-tree hints across row blocks (LOSS; may be NULL)
+  uint32_t hint_epoch;         // a position is dead when its hint equals this call's epoch (no reset pass)
   int n_trees;                 // trees (or listed trees in EXACT mode)
   int trees_per_block;         // G
   // data (per-feature rows, leading dimension ld; padded rows replicate row 0)
@@ -37,6 +38,11 @@ struct SrEvalArgs {
   // outputs
   double* part_sum;            // [n_row_blocks][n_trees], per launch position
   uint32_t* part_flag;         // [n_row_blocks][n_trees], per launch position
+  // single row block (n_row_blocks == 1): the per-tree results go straight to out_sum / out_flag
+  // (tree order, static_bad ORed in) and no reduce launch follows; NULL otherwise
+  double* out_sum;
+  uint32_t* out_flag;
+  const uint8_t* static_bad;
   T* pred;                     // PRED: [n_trees][pred_ld]
   int64_t pred_ld;
   // EXACT mode (perm = listed trees): row block rb = row range [range_lo[rb], range_hi[rb]] of the

@@ -585,7 +585,7 @@ __global__ void __launch_bounds__(W * 64, (SrMinWavesFor<T, R, TIER, W, VSTK>::v
     __syncthreads();
 
     if (use_hint) {
-      dmask |= sr_ballot(hintv != 0u) & live;
+      dmask |= sr_ballot(hintv == a.hint_epoch) & live;
       if (lane < S) hintv = __hip_atomic_load(a.hint + my_pos, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
     uint64_t todo = (MODE == SR_MODE_LOSS) ? (live & ~dmask) : live;
@@ -796,7 +796,7 @@ __global__ void __launch_bounds__(W * 64, (SrMinWavesFor<T, R, TIER, W, VSTK>::v
           if (dead) {
             dmask |= bit;
             if (use_hint && lane == 0)
-              __hip_atomic_fetch_or(a.hint + tree0 + g, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+              __hip_atomic_fetch_max(a.hint + tree0 + g, a.hint_epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
           }
         } else if (MODE == SR_MODE_PRED) {
           const uint32_t tree = a.perm ? a.perm[tree0 + g] : uint32_t(tree0 + g);
@@ -821,9 +821,17 @@ __global__ void __launch_bounds__(W * 64, (SrMinWavesFor<T, R, TIER, W, VSTK>::v
     return;
   }
   if (lane < S) {
-    const size_t o = size_t(rb) * a.n_trees + my_pos;  // [row block][position]: a block writes one run
-    a.part_sum[o] = accv;
-    a.part_flag[o] = (((dmask >> lane) & 1u) ? SR_FLAG_NONFINITE : 0u) | (((bmask >> lane) & 1u) ? SR_FLAG_BIG : 0u);
+    uint32_t f = (((dmask >> lane) & 1u) ? SR_FLAG_NONFINITE : 0u) | (((bmask >> lane) & 1u) ? SR_FLAG_BIG : 0u);
+    if (MODE == SR_MODE_LOSS && a.out_sum) {  // one row block: final per-tree values, tree order
+      const uint32_t tree = a.perm ? a.perm[my_pos] : uint32_t(my_pos);
+      if (a.static_bad[tree]) f |= SR_FLAG_STATIC | SR_FLAG_NONFINITE;
+      a.out_sum[tree] = accv;
+      a.out_flag[tree] = f;
+    } else {
+      const size_t o = size_t(rb) * a.n_trees + my_pos;  // [row block][position]: a block writes one run
+      a.part_sum[o] = accv;
+      a.part_flag[o] = f;
+    }
   }
 }
 
