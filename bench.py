@@ -339,17 +339,17 @@ def search_throughput(niterations):
 
 def measured_traffic(workload):
     """Per-step HBM bytes of the interpreter from the committed rocprofv3 PMC pass of this same
-    command (profiles/traffic.json, tools/profile.sh: FETCH_SIZE x2, gfx950)."""
+    command (profiles/traffic.json, written by tools/trace_frac.py)."""
     p = os.path.join(ROOT, "profiles", "traffic.json")
     try:
         with open(p) as f:
             t = json.load(f)
     except (OSError, ValueError):
         return None
-    if t.get("workload", "c2") != workload:
+    if t.get("workload") != workload or "hbm_read_bytes_per_step" not in t:
         return None
-    t["hbm_read_bytes_per_step"] = t["hbm_read_bytes_per_launch"] * t["calls"] / t.get("profiled_steps", 6)
-    t["source"] = "profiles/traffic.json (rocprofv3 --pmc FETCH_SIZE of bench.py)"
+    t["source"] = ("profiles/traffic.json (tools/bench_evidence.sh: rocprofv3 --pmc FETCH_SIZE of this bench "
+                   "command, x1024 B x2 gfx950, the timed steps' interpreter launches)")
     return t
 
 

@@ -305,6 +305,20 @@ int sr_search_members(sr_search* s, int which, int64_t* offsets, uint8_t* degree
                       uint8_t* constant, void* val, void* cost, void* loss, int64_t* birth, int64_t* ref,
                       int64_t* parent, int32_t* complexity);
 
+/*
+ * Batched constant optimisation (optimize_constants, src/ConstantOptimization.jl:29-116) of every
+ * tree: BFGS with BackTracking (Newton for one constant, its curvature from the device gradient)
+ * from the tree's constants and from `nrestarts` starts x0 .* (1 + eps/2), eps ~ randn(T) from the
+ * stream `seed`; each round of line-search trials is one batched loss call, each gradient one
+ * sr_eval_grad_batch call.  Out: the constants (pre-order per tree, concatenated; unchanged where
+ * not improved), the loss at them, improved = the minimum beat the start, and the objective
+ * evaluations per tree (num_evals = (f_calls + improved) x dataset fraction).
+ */
+int sr_optimize_constants_batch(sr_ctx* ctx, const sr_dataset* ds, int opset_id, const sr_tree_batch* trees,
+                                const int64_t* row_idx, int64_t n_idx, int loss_kind, int iterations, int nrestarts,
+                                uint64_t seed, void* out_consts, void* out_loss, uint8_t* out_improved,
+                                int64_t* out_f_calls);
+
 /* Timing of the last device call on this context (ms): kernel-only, via HIP events. */
 int sr_last_kernel_ms(sr_ctx* ctx, double* eval_ms, double* total_ms);
 

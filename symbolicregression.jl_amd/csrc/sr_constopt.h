@@ -261,7 +261,8 @@ inline int sr_optimize_batch(SrObjective& obj, const std::vector<std::vector<dou
   *best_x = x0;
   best_f->assign(n, INFINITY);
   std::vector<int> multi, single;
-  for (size_t k = 0; k < n; ++k) (x0[k].size() > 1 ? multi : single).push_back(int(k));
+  for (size_t k = 0; k < n; ++k)
+    if (!x0[k].empty()) (x0[k].size() > 1 ? multi : single).push_back(int(k));  // (no constants: nothing to do)
   for (size_t r = 0; r <= restarts.size(); ++r) {
     for (int g = 0; g < 2; ++g) {
       const std::vector<int>& grp = g == 0 ? multi : single;

@@ -53,7 +53,7 @@ constexpr double kTwoOverPi = 0x1.45f306dc9c883p-1;
 constexpr double kPio2_1 = 0x1.921fb54442d18p+0, kPio2_2 = 0x1.1a62633145c07p-54, kPio2_3 = -0x1.f1976b7ed8fbcp-110;
 constexpr double kSqrtHalf = 0x1.6a09e667f3bcdp-1;
 constexpr double k16OverPi = 0x1.45f306dc9c883p+2;
-constexpr double kPi16_1 = 0x1.921fb54442d18p-3, kPi16_2 = 0x1.1a62633145c07p-57, kPi16_3 = -0x1.f1976b7ed8fbcp-113;
+constexpr double kPi16_1 = 0x1.921fb54442d18p-3, kPi16_2 = 0x1.1a62633145c07p-57;
 // 2/pi in 32-bit words: bit 1 of word 0 is the 2^-1 bit (Payne-Hanek reduction of huge arguments)
 constexpr uint32_t kTwoOverPiBits[12] = {0xA2F9836Eu, 0x4E441529u, 0xFC2757D1u, 0xF534DDC0u, 0xDB629599u, 0x3C439041u,
                                          0xFE5163ABu, 0xDEBBC561u, 0xB7246E3Au, 0x424DD2E0u, 0x06492EEAu, 0x09D1921Cu};
@@ -86,13 +86,35 @@ SRL_HD inline float sr_expf(float x) {
 
 // log(x) = e ln2 + logc_k + log1p(m invc_k - 1): x = 2^e m, m in [0.75, 1.5) from the Float32 bits
 // (subnormals scaled by 2^24 first), cell k = the top 5 mantissa bits, |m invc_k - 1| <= 2^-5.
-SRL_HD inline float sr_logf_tab(float x, const double* tab) {
+// The f64 polynomial coefficients come in `c` (the device row function materialises them once per
+// call in scalar registers: 64-bit constants cannot be VOP3 literals, and rematerialising them
+// costs two v_mov per use and row).
+struct SrLogC {
+  double c8, c7, c6, c5, c4, c3, ln2hi, ln2lo;
+};
+constexpr SrLogC kSrLogC = {-0.125, 0x1.2492492492492p-3, -0x1.5555555555555p-3, 0.2, -0.25,
+                            0x1.5555555555555p-2, 0x1.62e42fefa39efp-1, 0x1.abc9e3b39803fp-56};
+
+#if defined(__HIP_DEVICE_COMPILE__)
+#define SRL_OPAQUE(v) asm volatile("" : "+v"(v))
+#else
+#define SRL_OPAQUE(v) (void)0
+#endif
+
+SRL_HD inline float sr_logf_core(float x, const double* tab, const SrLogC& c) {
   uint32_t b;
+#if defined(__HIP_DEVICE_COMPILE__)
+  // the hardware frexp normalises subnormals itself: x = mant 2^ex, mant in [0.5, 1)
+  const float mant = __builtin_amdgcn_frexp_mantf(x);
+  __builtin_memcpy(&b, &mant, 4);
+  const int e = __builtin_amdgcn_frexp_expf(x) - 1;
+#else
   __builtin_memcpy(&b, &x, 4);
   const bool sub = b < 0x00800000u;  // zero / subnormal (x >= 0 here)
   float xs = sub ? x * 0x1p24f : x;
   __builtin_memcpy(&b, &xs, 4);
   const int e = int(b >> 23) - 127 - (sub ? 24 : 0);
+#endif
   const uint32_t k = (b >> 18) & 31u;
   const bool hi = k >= 16u;  // m in [1.5, 2): use m / 2 and e + 1 (x just below 1 keeps e = 0)
   const uint32_t mb = (b & 0x007fffffu) | (hi ? 0x3f000000u : 0x3f800000u);
@@ -101,18 +123,61 @@ SRL_HD inline float sr_logf_tab(float x, const double* tab) {
   const double invc = tab[2 * k], logc = tab[2 * k + 1];
   const double r = fma(double(mf), invc, -1.0);
   // log1p(r) = r - r^2/2 + r^3/3 - ... - r^8/8 (|r| <= 2^-5: error < 2^-43 |r|)
-  double q = fma(r, -0.125, 0x1.2492492492492p-3);   // -1/8 r + 1/7
-  q = fma(r, q, -0x1.5555555555555p-3);               // -1/6
-  q = fma(r, q, 0.2);
-  q = fma(r, q, -0.25);
-  q = fma(r, q, 0x1.5555555555555p-2);                // 1/3
+  double q = fma(r, c.c8, c.c7);  // -1/8 r + 1/7
+  q = fma(r, q, c.c6);            // -1/6
+  q = fma(r, q, c.c5);            // 1/5
+  q = fma(r, q, c.c4);            // -1/4
+  q = fma(r, q, c.c3);            // 1/3
   q = fma(r, q, -0.5);
   const double p = fma(r * r, q, r);
   const double ed = double(hi ? e + 1 : e);
-  const float v = float(fma(ed, srl::kLn2Hi, fma(ed, srl::kLn2Lo, logc + p)));
-  // (+Inf -> +Inf; outside safe_log's domain as Base.log: 0 -> -Inf, x < 0 or NaN -> NaN)
-  return x == __builtin_inff() ? x : (x > 0.0f ? v : (x == 0.0f ? -__builtin_inff() : __builtin_nanf("")));
+  const float v = float(fma(ed, c.ln2hi, fma(ed, c.ln2lo, logc + p)));
+  // (+Inf -> +Inf; outside safe_log's domain as Base.log: 0 -> -Inf, x < 0 or NaN -> NaN).  Merged
+  // with an opaque bit mask, so the compiler cannot turn the merge into a divergent branch around
+  // the main path.
+#if defined(__HIP_DEVICE_COMPILE__)
+  // the hardware log2 has exactly these specials (+Inf -> +Inf, +-0 -> -Inf, x < 0 / NaN -> NaN);
+  // class 0x180 = positive normal or subnormal
+  const float special = __builtin_amdgcn_logf(x);
+  uint32_t keep = __builtin_amdgcn_class(x, 0x180) ? 0xffffffffu : 0u;
+#else
+  const float special = x == __builtin_inff() ? x : (x == 0.0f ? -__builtin_inff() : __builtin_nanf(""));
+  uint32_t keep = (x > 0.0f && x != __builtin_inff()) ? 0xffffffffu : 0u;
+#endif
+  SRL_OPAQUE(keep);
+  uint32_t vb, sb;
+  __builtin_memcpy(&vb, &v, 4);
+  __builtin_memcpy(&sb, &special, 4);
+#if defined(__HIP_DEVICE_COMPILE__)
+  uint32_t rb;
+  asm("v_bfi_b32 %0, %1, %2, %3" : "=v"(rb) : "v"(keep), "v"(vb), "v"(sb));
+#else
+  const uint32_t rb = (vb & keep) | (sb & ~keep);
+#endif
+  float out;
+  __builtin_memcpy(&out, &rb, 4);
+  return out;
 }
+SRL_HD inline float sr_logf_tab(float x, const double* tab) { return sr_logf_core(x, tab, kSrLogC); }
+
+#if defined(__HIP_DEVICE_COMPILE__)
+// a double constant in a scalar register pair (opaque to constant folding, so it stays there)
+template <uint64_t B>
+__device__ inline double srl_sconst() {
+  uint32_t lo, hi;
+  asm volatile("s_mov_b32 %0, %1" : "=s"(lo) : "i"(uint32_t(B & 0xffffffffu)));
+  asm volatile("s_mov_b32 %0, %1" : "=s"(hi) : "i"(uint32_t(B >> 32)));
+  return __builtin_bit_cast(double, (uint64_t(hi) << 32) | lo);
+}
+#define SRL_SCONST(v) srl_sconst<__builtin_bit_cast(uint64_t, double(v))>()
+__device__ inline SrLogC sr_logc_sgpr() {
+  return SrLogC{SRL_SCONST(kSrLogC.c8), SRL_SCONST(kSrLogC.c7), SRL_SCONST(kSrLogC.c6), SRL_SCONST(kSrLogC.c5),
+                SRL_SCONST(kSrLogC.c4), SRL_SCONST(kSrLogC.c3), SRL_SCONST(kSrLogC.ln2hi), SRL_SCONST(kSrLogC.ln2lo)};
+}
+#elif defined(__HIPCC__)
+// (host pass of device code: never executed)
+__device__ inline SrLogC sr_logc_sgpr() { return kSrLogC; }
+#endif
 
 // sin / cos of the reduced argument y (|y| <= pi/4 + tiny) in quadrant q: sin(x) = (q & 1 ? cos : sin)
 // with the sign of q & 2; cos(x) = the sin case of quadrant q + 1.
@@ -170,11 +235,16 @@ SRL_HD inline double sr_rem_pio2f_fast(float x, int* q) {
 template <bool COS>
 SRL_HD inline float sr_sincosf_tab(float x, const double* tab) {
   const double xd = double(x);
-  const double n = rint(xd * srl::k16OverPi);
+  // n = x 16/pi rounded to an integer by the 1.5 * 2^52 shifter: k = n mod 32 is the shifter's low
+  // bits (no conversions; a NaN x only yields a NaN result).  Two-part Cody-Waite with fused
+  // multiply-adds: |n| < 2^23, so the dropped third part (n * 2^-113 < 2^-90) is far below |r|'s ulp.
+  const double t = fma(xd, srl::k16OverPi, 0x1.8p52);
+  const double n = t - 0x1.8p52;
   double r = fma(-n, srl::kPi16_1, xd);
   r = fma(-n, srl::kPi16_2, r);
-  r = fma(-n, srl::kPi16_3, r);
-  const int k = srl::to_int(n) & 31;
+  uint64_t tb;
+  __builtin_memcpy(&tb, &t, 8);
+  const int k = int(uint32_t(tb) & 31u);
   const double sk = tab[2 * k], ck = tab[2 * k + 1];
   const double z = r * r;
   const double sp = fma(z, fma(z, -0x1.a01a01a01a01ap-13, 0x1.1111111111111p-7), -0x1.5555555555555p-3);

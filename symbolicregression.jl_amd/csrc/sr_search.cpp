@@ -152,6 +152,155 @@ struct Reader {
   }
 };
 
+// The scoring calls of the search: the library's own device path, or CPU callbacks (tests).
+template <typename T>
+struct Scorer {
+  sr_ctx* ctx = nullptr;
+  const sr_dataset* ds = nullptr;
+  int opset_id = -1, loss_code = 0;
+  sr_loss_fn loss_cb = nullptr;
+  sr_grad_fn grad_cb = nullptr;
+  void* cb_user = nullptr;
+  int64_t calls = 0;
+  double ms = 0.0;  // wall time inside the calls
+  bool ready() const { return ctx != nullptr || loss_cb != nullptr; }
+  bool has_grad() const { return ctx != nullptr || grad_cb != nullptr; }
+  // losses of `flat`'s trees (+Inf where incomplete)
+  int loss(const Flat& flat, const std::vector<int64_t>& rows, std::vector<T>* out) {
+    const sr_tree_batch b = flat.batch<T>();
+    const int64_t nt = b.n_trees;
+    out->assign(size_t(nt), T(0));
+    if (nt == 0) return SR_OK;
+    std::vector<uint8_t> comp(static_cast<size_t>(nt));
+    const int64_t* r = rows.empty() ? nullptr : rows.data();
+    const auto t0 = Clock::now();
+    const int rc = loss_cb ? loss_cb(cb_user, &b, r, int64_t(rows.size()), out->data(), comp.data())
+                           : sr_eval_loss_batch(ctx, ds, opset_id, &b, r, int64_t(rows.size()), loss_code, out->data(),
+                                                comp.data());
+    ms += ms_since(t0);
+    ++calls;
+    if (rc != SR_OK) return rc;
+    for (int64_t k = 0; k < nt; ++k)
+      if (!comp[size_t(k)]) (*out)[size_t(k)] = T(INFINITY);
+    return SR_OK;
+  }
+  // losses and d loss / d constants (pre-order per tree, concatenated)
+  int grad(const Flat& flat, const std::vector<int64_t>& rows, size_t n_consts, std::vector<T>* out,
+           std::vector<T>* g, std::vector<uint8_t>* comp) {
+    const sr_tree_batch b = flat.batch<T>();
+    out->assign(size_t(b.n_trees), T(0));
+    g->assign(n_consts + 1, T(0));
+    comp->assign(size_t(b.n_trees), 0);
+    if (b.n_trees == 0) return SR_OK;
+    const int64_t* r = rows.empty() ? nullptr : rows.data();
+    const auto t0 = Clock::now();
+    const int rc = grad_cb ? grad_cb(cb_user, &b, r, int64_t(rows.size()), out->data(), g->data(), comp->data())
+                           : sr_eval_grad_batch(ctx, ds, opset_id, &b, r, int64_t(rows.size()), loss_code, out->data(),
+                                                g->data(), comp->data());
+    ms += ms_since(t0);
+    ++calls;
+    return rc;
+  }
+};
+
+// The BFGS objective over a batch of trees: f / grad f of item k = tree k with constants xs[k]
+// (rounded to T), one batched device call per evaluation round.
+template <typename T>
+struct TreeObjective : SrObjective {
+  Scorer<T>* sc;
+  Flat* flat;
+  const std::vector<const SrTree<T>*>* trees;
+  const std::vector<int64_t>* rows;
+  std::vector<int64_t> f_calls;
+  int f(const std::vector<int>& items, const std::vector<std::vector<double>>& xs, std::vector<double>* out) override {
+    flat->clear();
+    for (size_t j = 0; j < items.size(); ++j) {
+      flat->add(*(*trees)[size_t(items[j])], &xs[j]);
+      ++f_calls[size_t(items[j])];
+    }
+    std::vector<T> loss;
+    const int rc = sc->loss(*flat, *rows, &loss);
+    if (rc) return rc;
+    out->resize(loss.size());
+    for (size_t j = 0; j < loss.size(); ++j) (*out)[j] = double(loss[j]);
+    return SR_OK;
+  }
+  int fg(const std::vector<int>& items, const std::vector<std::vector<double>>& xs, std::vector<double>* out,
+         std::vector<std::vector<double>>* grads) override {
+    flat->clear();
+    size_t nc = 0;
+    for (size_t j = 0; j < items.size(); ++j) {
+      flat->add(*(*trees)[size_t(items[j])], &xs[j]);
+      ++f_calls[size_t(items[j])];
+      nc += xs[j].size();
+    }
+    std::vector<T> loss, g;
+    std::vector<uint8_t> comp;
+    const int rc = sc->grad(*flat, *rows, nc, &loss, &g, &comp);
+    if (rc != SR_OK) return rc;
+    out->resize(items.size());
+    grads->resize(items.size());
+    size_t at = 0;
+    for (size_t j = 0; j < items.size(); ++j) {
+      (*out)[j] = comp[j] ? double(loss[j]) : INFINITY;
+      (*grads)[j].assign(xs[j].size(), 0.0);
+      for (size_t q = 0; q < xs[j].size(); ++q) (*grads)[j][q] = double(g[at + q]);
+      at += xs[j].size();
+    }
+    return SR_OK;
+  }
+};
+
+// optimize_constants (src/ConstantOptimization.jl:29-116) for a batch of trees with the perturbed
+// restart points already drawn: best constants per tree, whether the minimum beat the start, the
+// loss at the adopted constants (one more batched call, f(result.minimizer)) and f_calls per tree.
+template <typename T>
+int optimize_trees(Scorer<T>& sc, Flat& flat, const std::vector<const SrTree<T>*>& trees,
+                   const std::vector<std::vector<double>>& x0,
+                   const std::vector<std::vector<std::vector<double>>>& restarts, int iterations,
+                   const std::vector<int64_t>& rows, std::vector<std::vector<double>>* best_x,
+                   std::vector<uint8_t>* improved, std::vector<T>* adopted_loss, std::vector<int64_t>* f_calls) {
+  const size_t n = trees.size();
+  TreeObjective<T> obj;
+  obj.sc = &sc;
+  obj.flat = &flat;
+  obj.trees = &trees;
+  obj.rows = &rows;
+  obj.f_calls.assign(n, 0);
+  std::vector<double> bf, base;
+  int rc = sr_optimize_batch(obj, x0, restarts, iterations, best_x, &bf, &base);
+  if (rc) return rc;
+  improved->assign(n, 0);
+  adopted_loss->assign(n, T(0));
+  std::vector<size_t> better;
+  for (size_t k = 0; k < n; ++k)
+    if (bf[k] < base[k]) {
+      (*improved)[k] = 1;
+      better.push_back(k);
+    } else {
+      (*adopted_loss)[k] = T(base[k]);
+    }
+  if (!better.empty()) {
+    flat.clear();
+    for (size_t k : better) flat.add(*trees[k], &(*best_x)[k]);
+    std::vector<T> loss;
+    if ((rc = sc.loss(flat, rows, &loss))) return rc;
+    for (size_t j = 0; j < better.size(); ++j) (*adopted_loss)[better[j]] = loss[j];
+  }
+  *f_calls = obj.f_calls;
+  return SR_OK;
+}
+
+// one restart point x0 .* (1 + eps/2), eps ~ randn(T), in T (src/ConstantOptimization.jl:95-97)
+template <typename T>
+void draw_restart(SrRng& rng, const std::vector<double>& x0, std::vector<double>* xt) {
+  xt->resize(x0.size());
+  for (size_t q = 0; q < x0.size(); ++q) {
+    const T eps = T(rng.normal());
+    (*xt)[q] = double(T(x0[q]) * (T(1) + T(0.5) * eps));
+  }
+}
+
 }  // namespace
 
 struct sr_search_base {
@@ -169,13 +318,7 @@ struct Engine : sr_search_base {
   uint64_t seed = 0;
   int rank = 0, world = 1;
   std::vector<int> owned;
-  // scorer
-  sr_ctx* ctx = nullptr;
-  const sr_dataset* ds = nullptr;
-  int opset_id = -1, loss_code = 0;
-  sr_loss_fn loss_cb = nullptr;
-  sr_grad_fn grad_cb = nullptr;
-  void* cb_user = nullptr;
+  Scorer<T> sc;
   // dataset-level state (update_baseline_loss!)
   T baseline = T(1);
   bool use_baseline = false;
@@ -195,8 +338,8 @@ struct Engine : sr_search_base {
   int iteration = 0;
   // accounting
   double num_evals = 0.0;
-  int64_t device_calls = 0, s_r_cycles = 0;
-  double device_ms = 0.0, host_ms = 0.0;
+  int64_t s_r_cycles = 0;
+  double host_ms = 0.0;
   std::vector<int64_t> batch_idx;  // this iteration's minibatch (batching)
   Flat flat;
 
@@ -205,22 +348,6 @@ struct Engine : sr_search_base {
   int64_t new_ref(int i) { return (int64_t(i + 1) << 40) | ++refs[size_t(i)]; }
 
   // ------------------------------------------------------------ scoring
-  int score_flat(const int64_t* rows, int64_t n_idx, std::vector<T>* loss) {
-    const sr_tree_batch b = flat.batch<T>();
-    const int64_t nt = b.n_trees;
-    loss->assign(size_t(nt), T(0));
-    if (nt == 0) return SR_OK;
-    std::vector<uint8_t> comp(static_cast<size_t>(nt));
-    auto t0 = Clock::now();
-    int rc = loss_cb ? loss_cb(cb_user, &b, rows, n_idx, loss->data(), comp.data())
-                     : sr_eval_loss_batch(ctx, ds, opset_id, &b, rows, n_idx, loss_code, loss->data(), comp.data());
-    device_ms += ms_since(t0);
-    ++device_calls;
-    if (rc != SR_OK) return rc == SR_ERR_INVALID_ARG || rc < 0 ? rc : SR_ERR_INVALID_ARG;
-    for (int64_t k = 0; k < nt; ++k)
-      if (!comp[size_t(k)]) (*loss)[size_t(k)] = T(INFINITY);
-    return SR_OK;
-  }
   // loss_to_cost (src/LossFunctions.jl:169-190) in L
   T cost_of(T loss, int complexity) const {
     const T norm = (baseline >= T(0.01) && use_baseline) ? baseline : T(0.01);
@@ -232,7 +359,7 @@ struct Engine : sr_search_base {
                   std::vector<T>* loss, std::vector<T>* cost) {
     flat.clear();
     for (auto* t : trees) flat.add(*t);
-    int rc = score_flat(rows.empty() ? nullptr : rows.data(), int64_t(rows.size()), loss);
+    int rc = sc.loss(flat, rows, loss);
     if (rc) return rc;
     cost->resize(loss->size());
     for (size_t k = 0; k < loss->size(); ++k) (*cost)[k] = cost_of((*loss)[k], int(trees[k]->size()));
@@ -243,57 +370,6 @@ struct Engine : sr_search_base {
   }
 
   // ------------------------------------------------------------ constant optimisation
-  struct Obj : SrObjective {
-    Engine* e;
-    const std::vector<const SrTree<T>*>* trees;
-    const std::vector<int64_t>* rows;
-    std::vector<int64_t> f_calls;
-    int f(const std::vector<int>& items, const std::vector<std::vector<double>>& xs, std::vector<double>* out) override {
-      e->flat.clear();
-      for (size_t j = 0; j < items.size(); ++j) {
-        e->flat.add(*(*trees)[size_t(items[j])], &xs[j]);
-        ++f_calls[size_t(items[j])];
-      }
-      std::vector<T> loss;
-      int rc = e->score_flat(rows->empty() ? nullptr : rows->data(), int64_t(rows->size()), &loss);
-      if (rc) return rc;
-      out->resize(loss.size());
-      for (size_t j = 0; j < loss.size(); ++j) (*out)[j] = double(loss[j]);
-      return SR_OK;
-    }
-    int fg(const std::vector<int>& items, const std::vector<std::vector<double>>& xs, std::vector<double>* out,
-           std::vector<std::vector<double>>* grads) override {
-      e->flat.clear();
-      size_t nc = 0;
-      for (size_t j = 0; j < items.size(); ++j) {
-        e->flat.add(*(*trees)[size_t(items[j])], &xs[j]);
-        ++f_calls[size_t(items[j])];
-        nc += xs[j].size();
-      }
-      const sr_tree_batch b = e->flat.template batch<T>();
-      std::vector<T> loss(items.size()), g(nc + 1);
-      std::vector<uint8_t> comp(items.size());
-      const int64_t* r = rows->empty() ? nullptr : rows->data();
-      auto t0 = Clock::now();
-      int rc = e->grad_cb ? e->grad_cb(e->cb_user, &b, r, int64_t(rows->size()), loss.data(), g.data(), comp.data())
-                          : sr_eval_grad_batch(e->ctx, e->ds, e->opset_id, &b, r, int64_t(rows->size()), e->loss_code,
-                                               loss.data(), g.data(), comp.data());
-      e->device_ms += ms_since(t0);
-      ++e->device_calls;
-      if (rc != SR_OK) return rc;
-      out->resize(items.size());
-      grads->resize(items.size());
-      size_t at = 0;
-      for (size_t j = 0; j < items.size(); ++j) {
-        (*out)[j] = comp[j] ? double(loss[j]) : INFINITY;
-        (*grads)[j].assign(xs[j].size(), 0.0);
-        for (size_t q = 0; q < xs[j].size(); ++q) (*grads)[j][q] = double(g[at + q]);
-        at += xs[j].size();
-      }
-      return SR_OK;
-    }
-  };
-
   // optimize_constants over members (pointers); perturbation draws come from each member's island
   // stream, in member order (deterministic whatever the batch composition)
   int optimize_members(const std::vector<Member<T>*>& ms, const std::vector<int>& island,
@@ -301,7 +377,7 @@ struct Engine : sr_search_base {
     const size_t n = ms.size();
     improved_out->assign(n, 0);
     if (n == 0) return SR_OK;
-    if (!ctx && !grad_cb) return sr_set_error(SR_ERR_INVALID_ARG, "constant optimisation needs a gradient scorer");
+    if (!sc.has_grad()) return sr_set_error(SR_ERR_INVALID_ARG, "constant optimisation needs a gradient scorer");
     std::vector<const SrTree<T>*> trees(n);
     std::vector<std::vector<double>> x0(n);
     for (size_t k = 0; k < n; ++k) {
@@ -311,45 +387,24 @@ struct Engine : sr_search_base {
     }
     std::vector<std::vector<std::vector<double>>> restarts(size_t(o.optimizer_nrestarts),
                                                            std::vector<std::vector<double>>(n));
-    for (size_t k = 0; k < n; ++k) {
-      SrRng& rng = rngs[size_t(island[k])];
-      for (int r = 0; r < o.optimizer_nrestarts; ++r) {
-        std::vector<double>& xt = restarts[size_t(r)][k];
-        xt.resize(x0[k].size());
-        for (size_t q = 0; q < x0[k].size(); ++q) {
-          const T eps = T(rng.normal());
-          xt[q] = double(T(x0[k][q]) * (T(1) + T(0.5) * eps));  // x0 .* (1 + eps/2) in T
-        }
-      }
-    }
-    Obj obj;
-    obj.e = this;
-    obj.trees = &trees;
-    obj.rows = &rows;
-    obj.f_calls.assign(n, 0);
+    for (size_t k = 0; k < n; ++k)
+      for (int r = 0; r < o.optimizer_nrestarts; ++r) draw_restart<T>(rngs[size_t(island[k])], x0[k], &restarts[size_t(r)][k]);
     std::vector<std::vector<double>> bx;
-    std::vector<double> bf, base;
-    int rc = sr_optimize_batch(obj, x0, restarts, o.optimizer_iterations, &bx, &bf, &base);
+    std::vector<uint8_t> imp;
+    std::vector<T> loss;
+    std::vector<int64_t> f_calls;
+    const int rc = optimize_trees<T>(sc, flat, trees, x0, restarts, o.optimizer_iterations, rows, &bx, &imp, &loss, &f_calls);
     if (rc) return rc;
     const double frac = fraction(rows);
-    std::vector<size_t> better;
     for (size_t k = 0; k < n; ++k) {
-      num_evals += double(obj.f_calls[k]) * frac;
-      if (bf[k] < base[k]) better.push_back(k);
-    }
-    if (better.empty()) return SR_OK;
-    // adopt: constants, then the loss at the minimiser (f(result.minimizer)), cost, birth
-    flat.clear();
-    for (size_t k : better) flat.add(ms[k]->tree, &bx[k]);
-    std::vector<T> loss;
-    if ((rc = score_flat(rows.empty() ? nullptr : rows.data(), int64_t(rows.size()), &loss))) return rc;
-    for (size_t j = 0; j < better.size(); ++j) {
-      const size_t k = better[j];
+      num_evals += double(f_calls[k]) * frac;
+      if (!imp[k]) continue;
+      // adopt: constants, the loss at the minimiser, cost, birth
       Member<T>& m = *ms[k];
       size_t q = 0;
       for (auto& nd : m.tree)
         if (nd.degree == 0 && nd.constant) nd.val = T(bx[k][q++]);
-      m.loss = loss[j];
+      m.loss = loss[k];
       m.cost = cost_of(m.loss, m.complexity);
       m.birth = new_birth(island[k]);
       num_evals += frac;
@@ -1130,12 +1185,12 @@ int sr_search_use_device(sr_search* s, sr_ctx* ctx, const sr_dataset* ds, int op
     if (rc) return rc;
     if (dt != e->dtype || nf != e->sp.nfeatures || n != e->n_rows)
       return sr_set_error(SR_ERR_INVALID_ARG, "dataset does not match the search (dtype, features, rows)");
-    e->ctx = ctx;
-    e->ds = ds;
-    e->opset_id = opset_id;
-    e->loss_code = loss_code;
-    e->loss_cb = nullptr;
-    e->grad_cb = nullptr;
+    e->sc.ctx = ctx;
+    e->sc.ds = ds;
+    e->sc.opset_id = opset_id;
+    e->sc.loss_code = loss_code;
+    e->sc.loss_cb = nullptr;
+    e->sc.grad_cb = nullptr;
     return SR_OK;
   });
 }
@@ -1143,18 +1198,18 @@ int sr_search_use_device(sr_search* s, sr_ctx* ctx, const sr_dataset* ds, int op
 int sr_search_use_callbacks(sr_search* s, sr_loss_fn loss, sr_grad_fn grad, void* user) {
   return dispatch<int>(s, [&](auto* e) {
     if (!loss) return sr_set_error(SR_ERR_INVALID_ARG, "NULL loss callback");
-    e->loss_cb = loss;
-    e->grad_cb = grad;
-    e->cb_user = user;
-    e->ctx = nullptr;
-    e->ds = nullptr;
+    e->sc.loss_cb = loss;
+    e->sc.grad_cb = grad;
+    e->sc.cb_user = user;
+    e->sc.ctx = nullptr;
+    e->sc.ds = nullptr;
     return SR_OK;
   });
 }
 
 int sr_search_start(sr_search* s, int niterations) {
   return dispatch<int>(s, [&](auto* e) {
-    if (!e->ctx && !e->loss_cb) return sr_set_error(SR_ERR_INVALID_ARG, "no scorer: call sr_search_use_device first");
+    if (!e->sc.ready()) return sr_set_error(SR_ERR_INVALID_ARG, "no scorer: call sr_search_use_device first");
     if (niterations < 0) return sr_set_error(SR_ERR_INVALID_ARG, "negative iteration count");
     return e->start(niterations);
   });
@@ -1199,8 +1254,8 @@ int sr_search_get_info(sr_search* s, sr_search_info* out) {
     out->iterations = e->iteration;
     out->s_r_cycles = e->s_r_cycles;
     out->num_evals = e->num_evals;
-    out->device_calls = e->device_calls;
-    out->device_ms = e->device_ms;
+    out->device_calls = e->sc.calls;
+    out->device_ms = e->sc.ms;
     out->host_ms = e->host_ms;
     out->baseline_loss = double(e->baseline);
     out->use_baseline = e->use_baseline ? 1 : 0;
@@ -1255,6 +1310,73 @@ int sr_search_members(sr_search* s, int which, int64_t* offsets, uint8_t* degree
     }
     return SR_OK;
   });
+}
+
+int sr_optimize_constants_batch(sr_ctx* ctx, const sr_dataset* ds, int opset_id, const sr_tree_batch* trees,
+                                const int64_t* row_idx, int64_t n_idx, int loss_kind, int iterations, int nrestarts,
+                                uint64_t seed, void* out_consts, void* out_loss, uint8_t* out_improved,
+                                int64_t* out_f_calls) {
+  if (!ctx || !ds || !trees) return sr_set_error(SR_ERR_INVALID_ARG, "NULL context, dataset or trees");
+  if (iterations < 0 || nrestarts < 0) return sr_set_error(SR_ERR_INVALID_ARG, "negative iterations / restarts");
+  const int64_t nt = trees->n_trees;
+  if (nt < 0) return sr_set_error(SR_ERR_INVALID_ARG, "negative tree count");
+  if (nt > 0 && (!trees->offsets || !trees->degree || !trees->op || !trees->feature || !trees->constant ||
+                 !trees->val || !out_consts || !out_loss || !out_improved || !out_f_calls))
+    return sr_set_error(SR_ERR_INVALID_ARG, "NULL arrays");
+  int dt = 0;
+  int64_t nf = 0, n = 0;
+  int rc = sr_dataset_info(ds, &dt, &nf, &n);
+  if (rc) return rc;
+  auto run = [&](auto zero) -> int {
+    using T = decltype(zero);
+    std::vector<SrTree<T>> tv(static_cast<size_t>(nt));
+    std::vector<std::vector<double>> x0(static_cast<size_t>(nt));
+    const T* vals = static_cast<const T*>(trees->val);
+    for (int64_t t = 0; t < nt; ++t)
+      for (int64_t i = trees->offsets[t]; i < trees->offsets[t + 1]; ++i) {
+        SrNode<T> nd;
+        nd.degree = trees->degree[i];
+        nd.op = trees->op[i];
+        nd.feature = trees->feature[i];
+        nd.constant = trees->constant[i];
+        nd.val = vals[i];
+        tv[size_t(t)].push_back(nd);
+        if (nd.degree == 0 && nd.constant) x0[size_t(t)].push_back(double(nd.val));
+      }
+    SrRng rng;
+    rng.seed(seed, 0x6f7074696d697a65ull);
+    std::vector<std::vector<std::vector<double>>> restarts(static_cast<size_t>(nrestarts),
+                                                           std::vector<std::vector<double>>(static_cast<size_t>(nt)));
+    for (int64_t t = 0; t < nt; ++t)
+      for (int r = 0; r < nrestarts; ++r) draw_restart<T>(rng, x0[size_t(t)], &restarts[size_t(r)][size_t(t)]);
+    std::vector<const SrTree<T>*> ptr;
+    for (auto& t : tv) ptr.push_back(&t);
+    Scorer<T> sc;
+    sc.ctx = ctx;
+    sc.ds = ds;
+    sc.opset_id = opset_id;
+    sc.loss_code = loss_kind;
+    Flat flat;
+    const std::vector<int64_t> rows(row_idx && n_idx > 0 ? row_idx : nullptr,
+                                    row_idx && n_idx > 0 ? row_idx + n_idx : nullptr);
+    std::vector<std::vector<double>> bx;
+    std::vector<uint8_t> imp;
+    std::vector<T> loss;
+    std::vector<int64_t> f_calls;
+    int e = optimize_trees<T>(sc, flat, ptr, x0, restarts, iterations, rows, &bx, &imp, &loss, &f_calls);
+    if (e) return e;
+    size_t at = 0;
+    for (int64_t t = 0; t < nt; ++t) {
+      for (size_t q = 0; q < x0[size_t(t)].size(); ++q)
+        static_cast<T*>(out_consts)[at++] = imp[size_t(t)] ? T(bx[size_t(t)][q]) : T(x0[size_t(t)][q]);
+      static_cast<T*>(out_loss)[t] = loss[size_t(t)];
+      out_improved[t] = imp[size_t(t)];
+      out_f_calls[t] = f_calls[size_t(t)];
+    }
+    return SR_OK;
+  };
+  if (nt == 0) return SR_OK;
+  return dt == SR_DTYPE_F32 ? run(0.0f) : run(0.0);
 }
 
 }  // extern "C"

@@ -218,6 +218,18 @@ __device__ __attribute__((noinline)) SrRowVec<R> sr_libm_rows(SrRowVec<R> v) {
   }
   return v;
 }
+// Float32 log over the rows, its coefficients in scalar registers for the whole call
+template <int R>
+__device__ __attribute__((noinline)) SrRowVec<R> sr_log_rows(SrRowVec<R> v) {
+  const SrLogC c = sr_logc_sgpr();
+  const double* tab = sr_log_tab();
+#pragma unroll
+  for (int r = 0; r < R; ++r) {
+    v[r] = sr_logf_core(v[r], tab, c);
+    __builtin_amdgcn_sched_barrier(0);
+  }
+  return v;
+}
 // cos / sin when every row of the wave has |x| < 2^20 (a separate function: its few registers are
 // all caller-saved, so the common call saves nothing)
 template <uint32_t ID, int R>
@@ -244,7 +256,9 @@ __device__ __forceinline__ void sr_unary_rows(T (&v)[R]) {
 #pragma unroll
       for (int r = 0; r < R; ++r) slow |= !(__builtin_fabsf(v[r]) < srl::kTrigFastLimit);
     }
-    if ((ID == SR_U_COS || ID == SR_U_SIN) && __builtin_amdgcn_ballot_w64(slow) == 0)
+    if constexpr (ID == SR_U_LOG)
+      x = sr_log_rows<R>(x);
+    else if (__builtin_amdgcn_ballot_w64(slow) == 0)
       x = sr_trig_rows_fast<ID, R>(x);
     else
       x = sr_libm_rows<ID, R>(x);

@@ -72,6 +72,7 @@ EXPORTED_SYMBOLS = (
     "sr_search_get_info",
     "sr_search_member_count",
     "sr_search_members",
+    "sr_optimize_constants_batch",
 )
 
 # mutation kinds in sr_search_options.mutation_weights order (SR_MUT_*)
@@ -211,6 +212,10 @@ def _load():
         "sr_search_get_info": (c_int, [P, POINTER(SrSearchInfo)]),
         "sr_search_member_count": (c_int, [P, c_int, POINTER(c_int64), POINTER(c_int64)]),
         "sr_search_members": (c_int, [P, c_int, P, P, P, P, P, P, P, P, P, P, P, P]),
+        "sr_optimize_constants_batch": (
+            c_int,
+            [P, P, c_int, POINTER(SrTreeBatch), P, c_int64, c_int, c_int, c_int, ctypes.c_uint64, P, P, P, P],
+        ),
     }
     for name, (res, args) in proto.items():
         fn = getattr(lib, name)

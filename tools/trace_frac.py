@@ -1,0 +1,58 @@
+"""Recompute bench.py's roofline from a rocprofv3 kernel trace of the same command.
+
+  python3 tools/trace_frac.py OUTDIR      (OUTDIR from tools/bench_evidence.sh)
+
+Reads OUTDIR/kt/kt_kernel_trace.csv and OUTDIR/bench_traced.json (the bench line printed by the
+traced run).  The interpreter launches of the C2 step are the f32 BASIC loss kernel
+(sr_tile_kernel<float, 8, 0, ...>, probes included: the bench's HIP events bracket them too); the
+last steps x launches_per_step of them are the timed region.  Prints the per-step kernel time and
+roofline fraction from the trace next to the bench's own (HIP-event) values, and, when the PMC pass
+ran, the HBM bytes per step from FETCH_SIZE (x 1024 B/KiB x 2, the gfx950 correction of
+MI355X_MICROARCH.md)."""
+import csv
+import glob
+import json
+import os
+import sys
+
+
+def main(out):
+    line = json.loads(open(os.path.join(out, "bench_traced.json")).read().strip().splitlines()[-1])
+    rf = line["roofline"]
+    steps, per_step = line["steps"], rf["launches_per_step"]
+    rows = list(csv.DictReader(open(glob.glob(os.path.join(out, "kt", "*kernel_trace.csv"))[0])))
+    interp = [r for r in rows if r["Kernel_Name"].startswith("void sr_tile_kernel<float, 8, 0,")]
+    interp.sort(key=lambda r: int(r["Start_Timestamp"]))
+    # probes: each step after the first chunk adds one probe launch (same kernel, tiny grid)
+    probes_per_step = 1 if per_step == 2 else 0
+    k = steps * (per_step + probes_per_step)
+    timed = interp[-k:]
+    ns = sum(int(r["End_Timestamp"]) - int(r["Start_Timestamp"]) for r in timed)
+    trace_ms = ns / 1e6 / steps
+    achieved = rf["flops_per_step"] / (trace_ms * 1e-3) / 1e12
+    print(f"bench (traced run) : kernel {rf['kernel_ms_per_step']:.3f} ms/step (HIP events), frac {rf['frac']:.4f}")
+    print(f"kernel trace       : {len(interp)} interpreter launches, last {k} = {steps} timed steps x "
+          f"({per_step} + {probes_per_step} probe)")
+    print(f"                     kernel {trace_ms:.3f} ms/step, achieved {achieved:.2f} TFLOP/s, "
+          f"frac {achieved / rf['peak']:.4f} (peak {rf['peak']})")
+    print(f"agreement          : trace / events = {trace_ms / rf['kernel_ms_per_step']:.4f}")
+    pm = glob.glob(os.path.join(out, "pmc", "*counter_collection.csv"))
+    if pm:
+        fetch = {}
+        for r in csv.DictReader(open(pm[0])):
+            if r.get("Counter_Name") == "FETCH_SIZE" and r["Kernel_Name"].startswith("void sr_tile_kernel<float, 8, 0,"):
+                fetch[r["Dispatch_Id"]] = fetch.get(r["Dispatch_Id"], 0.0) + float(r["Counter_Value"])
+        vals = [fetch[d] for d in sorted(fetch, key=int)][-k:]
+        if vals:
+            per_step_bytes = sum(vals) * 1024 * 2 / steps
+            print(f"HBM (FETCH_SIZE)   : {per_step_bytes / 1e6:.1f} MB/step over the timed launches "
+                  f"(algorithmic {rf['algorithmic_bytes_per_step'] / 1e6:.1f} MB)")
+            json.dump({"workload": "c2", "kernel": "sr_tile_kernel<float, 8, 0, ...> (probes included)",
+                       "profiled_steps": steps, "launches": len(vals),
+                       "hbm_read_bytes_per_step": per_step_bytes,
+                       "source_cmd": "tools/bench_evidence.sh"},
+                      open(os.path.join(out, "traffic.json"), "w"))
+
+
+if __name__ == "__main__":
+    main(sys.argv[1])
