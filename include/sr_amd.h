@@ -153,8 +153,9 @@ int sr_eval_loss_partials(sr_ctx* ctx, const sr_dataset* ds, int opset_id, const
  */
 int sr_eval_loss_partials_packed(sr_ctx* ctx, const sr_dataset* ds, int opset_id, const sr_tree_batch* trees,
                                  int64_t n_total, int loss_kind, double* out, int out_on_device);
-/* Maximum number of checked nodes per tree for `trees` (sizes the sr_jsum_partials output). */
-int sr_max_checks(sr_ctx* ctx, int opset_id, const sr_tree_batch* trees, int* max_checks);
+/* Maximum number of checked nodes per tree for `trees` (element type dtype; sizes the
+ * sr_jsum_partials output). */
+int sr_max_checks(sr_ctx* ctx, int dtype, int opset_id, const sr_tree_batch* trees, int* max_checks);
 /*
  * Exact validity check, DynamicExpressions' isfinite(sum(x)) on every checked node with Base's
  * pairwise `sum` in T (Base.mapreduce_impl: halves split at lo + (hi-lo)>>1 down to blocks of < 1024

@@ -722,7 +722,8 @@ int run_exact(sr_ctx* ctx, const sr_dataset* ds, const SrProgramBatch<T>& prog, 
   for (int64_t b0 = 0; b0 < n_list; b0 += batch) {
     const int64_t nb = std::min(batch, n_list - b0);
     // one wave per workgroup, G listed trees per workgroup (LDS: X tile + one wave's checked
-    // values [max_checks][rows] + running sums [G][max_checks])
+    // values [max_checks][rows] + running sums [G][max_checks]); G = 16 amortises the tile staging
+    // (one tree per workgroup measured slower on C2's pass: 1.32 vs 0.97 ms)
     int G = int(std::min<int64_t>(nb, 16));
     size_t lds = 0;
     for (;;) {
@@ -1366,16 +1367,22 @@ int sr_eval_loss_partials_packed(sr_ctx* ctx, const sr_dataset* ds, int opset_id
   return SR_OK;
 }
 
-int sr_max_checks(sr_ctx* ctx, int opset_id, const sr_tree_batch* trees, int* max_checks) {
+int sr_max_checks(sr_ctx* ctx, int dtype, int opset_id, const sr_tree_batch* trees, int* max_checks) {
   if (check_ctx(ctx) != SR_OK) return SR_ERR_INVALID_ARG;
-  if (!trees || !max_checks || opset_id < 0 || opset_id >= int(ctx->opsets.size()))
+  if (!trees || !max_checks || opset_id < 0 || opset_id >= int(ctx->opsets.size()) ||
+      (dtype != SR_DTYPE_F32 && dtype != SR_DTYPE_F64))
     return set_error(SR_ERR_INVALID_ARG, "bad arguments");
-  SrProgramBatch<double> prog;
+  // compiled in the batch's own element type (`val` holds T): the same programs the eval calls build
   std::string err;
-  int rc = sr_compile_batch<double>(*trees, ctx->opsets[opset_id], 1, 65535, false, &prog, &err);
-  if (rc != SR_OK) return set_error(rc, err);
-  *max_checks = prog.max_checks;
-  return SR_OK;
+  auto go = [&](auto tag) -> int {
+    using T = decltype(tag);
+    SrProgramBatch<T> prog;
+    const int rc = sr_compile_batch<T>(*trees, ctx->opsets[opset_id], 1, 65535, false, &prog, &err);
+    if (rc != SR_OK) return set_error(rc, err);
+    *max_checks = prog.max_checks;
+    return SR_OK;
+  };
+  return dtype == SR_DTYPE_F32 ? go(0.0f) : go(0.0);
 }
 
 int sr_jsum_range_count(int64_t row_offset, int64_t n_local, int64_t n_total, int64_t* out_n_ranges) {

@@ -167,7 +167,7 @@ def _load():
             c_int,
             [P, P, c_int, POINTER(SrTreeBatch), c_int64, c_int, P, P, c_int],
         ),
-        "sr_max_checks": (c_int, [P, c_int, POINTER(SrTreeBatch), POINTER(c_int)]),
+        "sr_max_checks": (c_int, [P, c_int, c_int, POINTER(SrTreeBatch), POINTER(c_int)]),
         "sr_eval_loss_partials_packed": (
             c_int,
             [P, P, c_int, POINTER(SrTreeBatch), c_int64, c_int, P, c_int],

@@ -77,7 +77,8 @@ def gpu_max_checks(tb, options, ctx=None):
     ctx = ctx or get_context()
     s = tb.to_struct()
     m = ctypes.c_int()
-    _lib.check(_lib.lib.sr_max_checks(ctx.handle, ctx.opset_id(options.operators), ctypes.byref(s), ctypes.byref(m)))
+    _lib.check(_lib.lib.sr_max_checks(ctx.handle, _dtype_code(tb.val.dtype), ctx.opset_id(options.operators),
+                                      ctypes.byref(s), ctypes.byref(m)))
     return int(m.value)
 
 
