@@ -41,6 +41,41 @@ __global__ void __launch_bounds__(256) sr_reduce_partials_kernel(const double* _
   }
 }
 
+// Julia's pairwise `sum` of one view, from its leaf folds: every thread combines one array's
+// n_leaves folds by the shared post-order program (leaf index: push it; -1: add the top two, in T),
+// the order of Base.mapreduce_impl's recursion; out[a] = isfinite(total).
+template <typename T>
+__global__ void __launch_bounds__(256) sr_jsum_combine_kernel(const T* __restrict__ leaf_sums, int64_t n_arrays,
+                                                              int n_leaves, const int32_t* __restrict__ prog,
+                                                              int prog_len, uint8_t* __restrict__ out) {
+  const int64_t a = int64_t(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (a >= n_arrays) return;
+  T st[48];  // kJsumMaxDepth
+  int sp = 0;
+  const T* v = leaf_sums + a * n_leaves;
+  for (int i = 0; i < prog_len; ++i) {
+    const int c = prog[i];
+    if (c >= 0) {
+      st[sp++] = v[c];
+    } else {
+      const T b = st[--sp];
+      st[sp - 1] = st[sp - 1] + b;
+    }
+  }
+  out[a] = __builtin_isfinite(st[0]) ? 1 : 0;
+}
+
+template <typename T>
+hipError_t sr_launch_jsum_combine(const T* leaf_sums, int64_t n_arrays, int n_leaves, const int32_t* prog,
+                                  int prog_len, uint8_t* out, hipStream_t s) {
+  if (n_arrays <= 0) return hipSuccess;
+  hipLaunchKernelGGL(sr_jsum_combine_kernel<T>, dim3(unsigned((n_arrays + 255) / 256)), dim3(256), 0, s, leaf_sums,
+                     n_arrays, n_leaves, prog, prog_len, out);
+  return hipGetLastError();
+}
+template hipError_t sr_launch_jsum_combine<float>(const float*, int64_t, int, const int32_t*, int, uint8_t*, hipStream_t);
+template hipError_t sr_launch_jsum_combine<double>(const double*, int64_t, int, const int32_t*, int, uint8_t*, hipStream_t);
+
 // Packed row-shard partials for one all-reduce (sr_eval_loss_partials_packed): [4][n] f64 = Σ loss,
 // then the NONFINITE / BIG / STATIC flag bits as 0 / 1.
 __global__ void __launch_bounds__(256) sr_pack_partials_kernel(const double* __restrict__ sum,

@@ -96,6 +96,7 @@ struct HostBuf {
 };
 
 constexpr int kMaxChunks = 4;
+constexpr int kJsumMaxDepth = 48;  // stack of the device-side Julia-sum combine (2^26 rows need 17)
 constexpr int kLossCodeBase = 256;
 
 // Parameter-free losses (and HuberLoss with its default delta = 1) may be passed by kind.
@@ -145,12 +146,13 @@ struct sr_ctx {
   // threads; off by default)
   int spin = 0;
   uint32_t hint_epoch = 0;  // dead-tree hint epoch of the current call
+  int exact_g = 0;          // SR_AMD_EXACT_G (tuning): listed trees per workgroup of the EXACT pass
   std::mutex mu;
   std::vector<SrOpset> opsets;
   std::vector<int> tiers;
   std::vector<std::pair<int, double>> losses;  // registered (kind, param); code = kLossCodeBase + index
   DevBuf prog, outs, part_sum, part_flag, pred, row_idx, tree_list,
-      range_lo, range_hi, range_sums, packed, hint, probe_sum, probe_flag, g_code, g_offsets, g_consts, g_const_off, g_items, g_part, g_out;
+      range_lo, range_hi, range_sums, packed, hint, jsum_prog, jsum_fin, probe_sum, probe_flag, g_code, g_offsets, g_consts, g_const_off, g_items, g_part, g_out;
   double last_eval_ms = 0.0, last_total_ms = 0.0;
   // host-side phases of the last eval_loss call (ms): compile, upload+launch, wait, exact pass,
   // finalize (sr_last_phase_ms)
@@ -393,6 +395,7 @@ int run_batch(sr_ctx* ctx, const sr_dataset* ds, int opset_id, const sr_tree_bat
   prog->code.clear();
   prog->offsets.assign(size_t(nt) + 1, 0);
   prog->static_bad.assign(size_t(nt), 0);
+  prog->n_checks.assign(size_t(nt), 0);
   prog->max_depth = 0;
   prog->max_checks = 0;
   prog->total_nodes = 0;
@@ -498,6 +501,7 @@ int run_batch(sr_ctx* ctx, const sr_dataset* ds, int opset_id, const sr_tree_bat
     // merged summary
     for (int64_t i = 0; i <= nc; ++i) prog->offsets[size_t(t0 + i)] = h_off[t0 + i];
     std::memcpy(prog->static_bad.data() + t0, pc.static_bad.data(), size_t(nc));
+    std::copy(pc.n_checks.begin(), pc.n_checks.end(), prog->n_checks.begin() + t0);
     if (pc.max_depth > prog->max_depth) prog->max_depth = pc.max_depth;
     if (pc.max_checks > prog->max_checks) prog->max_checks = pc.max_checks;
     prog->total_nodes += pc.total_nodes;
@@ -690,12 +694,29 @@ void jl_finite(int64_t n_total, int n_ranks, const int64_t* offs, const T* const
   }
 }
 
+// Base.mapreduce_impl's combine of one view's leaf folds as a post-order program (leaf k: push
+// k; -1: add the top two), shared by every array; the stack it needs in *max_depth (`depth` = the
+// stack size after pushing a leaf at this point).
+void jl_program(int64_t lo, int64_t hi, int32_t* idx, std::vector<int32_t>* prog, int depth, int* max_depth) {
+  if (depth > *max_depth) *max_depth = depth;
+  if (hi - lo < 1024) {
+    prog->push_back((*idx)++);
+    return;
+  }
+  const int64_t mid = lo + ((hi - lo) >> 1);
+  jl_program(lo, mid, idx, prog, depth, max_depth);          // (the left half starts on the same stack)
+  jl_program(mid + 1, hi, idx, prog, depth + 1, max_depth);  // (above the left half's result)
+  prog->push_back(-1);
+}
+
 // EXACT pass: the Julia-order fold of every checked array of the listed trees over `ranges` of this
-// view -> host_vals[n_list][max_checks][ranges] (T; a tree's unused check slots hold 0).
+// view -> host_vals[n_list][max_checks][ranges] (T; a tree's unused check slots hold 0).  With
+// host_finite (single view: the ranges are the view's leaves in order) the leaves are combined on
+// the device in recursion order and only isfinite(sum) per array comes back: host_finite[n_list][max_checks].
 template <typename T>
 int run_exact(sr_ctx* ctx, const sr_dataset* ds, const SrProgramBatch<T>& prog, const int64_t* row_idx,
               int64_t n_idx, const int64_t* list, int64_t n_list, int max_checks, const std::vector<JlRange>& ranges,
-              T* host_vals) {
+              T* host_vals, uint8_t* host_finite = nullptr) {
   if (n_list == 0 || max_checks == 0 || ranges.empty()) return SR_OK;
   const bool gather = row_idx != nullptr && n_idx > 0;
   const int64_t n_eval = gather ? n_idx : ds->n;
@@ -716,6 +737,16 @@ int run_exact(sr_ctx* ctx, const sr_dataset* ds, const SrProgramBatch<T>& prog, 
   SR_HIP_CHECK(ctx->range_hi.ensure(size_t(n_ranges) * sizeof(int64_t)));
   SR_HIP_CHECK(hipMemcpyAsync(ctx->range_lo.p, lo.data(), size_t(n_ranges) * sizeof(int64_t), hipMemcpyHostToDevice, s));
   SR_HIP_CHECK(hipMemcpyAsync(ctx->range_hi.p, hi.data(), size_t(n_ranges) * sizeof(int64_t), hipMemcpyHostToDevice, s));
+  int comb_len = 0, comb_depth = 0;
+  if (host_finite) {
+    std::vector<int32_t> comb;
+    int32_t idx = 0;
+    jl_program(0, n_eval - 1, &idx, &comb, 1, &comb_depth);
+    if (idx != n_ranges || comb_depth > kJsumMaxDepth) return set_error(SR_ERR_INVALID_ARG, "bad leaf structure");
+    comb_len = int(comb.size());
+    SR_HIP_CHECK(ctx->jsum_prog.ensure(comb.size() * sizeof(int32_t)));
+    SR_HIP_CHECK(hipMemcpyAsync(ctx->jsum_prog.p, comb.data(), comb.size() * sizeof(int32_t), hipMemcpyHostToDevice, s));
+  }
   // listed trees in batches whose range folds fit a bounded scratch buffer
   const size_t per_tree = size_t(max_checks) * size_t(n_ranges) * sizeof(T);
   const int64_t batch = std::max<int64_t>(1, int64_t((size_t(256) << 20) / per_tree));
@@ -724,7 +755,7 @@ int run_exact(sr_ctx* ctx, const sr_dataset* ds, const SrProgramBatch<T>& prog, 
     // one wave per workgroup, G listed trees per workgroup (LDS: X tile + one wave's checked
     // values [max_checks][rows] + running sums [G][max_checks]); G = 16 amortises the tile staging
     // (one tree per workgroup measured slower on C2's pass: 1.32 vs 0.97 ms)
-    int G = int(std::min<int64_t>(nb, 16));
+    int G = int(std::min<int64_t>(nb, ctx->exact_g > 0 ? ctx->exact_g : 16));
     size_t lds = 0;
     for (;;) {
       lds = sr_tile_lds_bytes(int(sizeof(T)), int(ds->nf), R, depth, G, max_checks, 1, false);
@@ -760,8 +791,17 @@ int run_exact(sr_ctx* ctx, const sr_dataset* ds, const SrProgramBatch<T>& prog, 
     const int64_t blocks = int64_t(a.n_groups) * n_ranges;
     if (blocks > 0x7fffffff) return set_error(SR_ERR_INVALID_ARG, "grid too large");
     SR_HIP_CHECK(sr_launch_eval<T>(a, SR_MODE_EXACT, gather, SR_TIER_FULL, R, 1, false, int(blocks), s));
-    SR_HIP_CHECK(hipMemcpyAsync(host_vals + size_t(b0) * max_checks * size_t(n_ranges), ctx->range_sums.p,
-                                size_t(nb) * per_tree, hipMemcpyDeviceToHost, s));
+    if (host_finite) {
+      const int64_t n_arrays = nb * max_checks;
+      SR_HIP_CHECK(ctx->jsum_fin.ensure(size_t(n_arrays) + 16));
+      SR_HIP_CHECK(sr_launch_jsum_combine<T>(static_cast<const T*>(ctx->range_sums.p), n_arrays, int(n_ranges),
+                                             ctx->jsum_prog.as<int32_t>(), comb_len, ctx->jsum_fin.as<uint8_t>(), s));
+      SR_HIP_CHECK(hipMemcpyAsync(host_finite + size_t(b0) * max_checks, ctx->jsum_fin.p, size_t(n_arrays),
+                                  hipMemcpyDeviceToHost, s));
+    } else {
+      SR_HIP_CHECK(hipMemcpyAsync(host_vals + size_t(b0) * max_checks * size_t(n_ranges), ctx->range_sums.p,
+                                  size_t(nb) * per_tree, hipMemcpyDeviceToHost, s));
+    }
     SR_HIP_CHECK(hipStreamSynchronize(s));
   }
   return SR_OK;
@@ -777,14 +817,15 @@ int exact_list_ok(sr_ctx* ctx, const sr_dataset* ds, const SrProgramBatch<T>& pr
   const bool gather = row_idx != nullptr && n_idx > 0;
   const int64_t n_eval = gather ? n_idx : ds->n;
   const std::vector<JlRange> ranges = jl_ranges(0, n_eval, n_eval);
-  const int mc = prog.max_checks;
-  std::vector<T> vals(list.size() * size_t(mc) * ranges.size());
-  int rc = run_exact<T>(ctx, ds, prog, row_idx, n_idx, list.data(), int64_t(list.size()), mc, ranges, vals.data());
-  if (rc != SR_OK) return rc;
+  // check slots: the most any LISTED tree has (the LDS image and the fold buffers scale with it)
+  int mc = 0;
+  for (int64_t t : list) mc = std::max(mc, int(prog.n_checks[size_t(t)]));
+  if (mc == 0) return SR_OK;
+  // leaf folds combined in recursion order on the device: only the verdicts come back
   std::vector<uint8_t> fin(list.size() * size_t(mc));
-  const int64_t offs[2] = {0, n_eval};
-  const T* pv = vals.data();
-  jl_finite<T>(n_eval, 1, offs, &pv, int64_t(fin.size()), fin.data());
+  int rc = run_exact<T>(ctx, ds, prog, row_idx, n_idx, list.data(), int64_t(list.size()), mc, ranges, nullptr,
+                        fin.data());
+  if (rc != SR_OK) return rc;
   for (size_t i = 0; i < list.size(); ++i)
     for (int k = 0; k < mc; ++k) (*list_ok)[i] &= fin[i * size_t(mc) + size_t(k)];
   return SR_OK;
@@ -1153,6 +1194,7 @@ int sr_init(int device, sr_ctx** out) {
   if (const char* v = std::getenv("SR_AMD_PROBE")) ctx->probe = std::atoi(v);
   if (const char* v = std::getenv("SR_AMD_HOST_IO")) ctx->host_io = std::atoi(v);
   if (const char* v = std::getenv("SR_AMD_SPIN")) ctx->spin = std::atoi(v);
+  if (const char* v = std::getenv("SR_AMD_EXACT_G")) ctx->exact_g = std::atoi(v);
   if (const char* v = std::getenv("SR_AMD_MAX_ROW_BLOCKS")) ctx->max_row_blocks = std::max(1, std::atoi(v));
   hipError_t e = hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking);
   if (e == hipSuccess) e = hipStreamCreateWithFlags(&ctx->stream2, hipStreamNonBlocking);
@@ -1180,7 +1222,7 @@ int sr_shutdown(sr_ctx* ctx) {
     (void)hipSetDevice(ctx->device);
     (void)hipStreamSynchronize(ctx->stream);
     for (DevBuf* b : {&ctx->prog, &ctx->outs, &ctx->part_sum, &ctx->part_flag, &ctx->pred, &ctx->row_idx, &ctx->tree_list, &ctx->range_lo, &ctx->range_hi, &ctx->range_sums, &ctx->packed,
-                      &ctx->hint, &ctx->probe_sum, &ctx->probe_flag, &ctx->g_code, &ctx->g_offsets, &ctx->g_consts, &ctx->g_const_off,
+                      &ctx->hint, &ctx->jsum_prog, &ctx->jsum_fin, &ctx->probe_sum, &ctx->probe_flag, &ctx->g_code, &ctx->g_offsets, &ctx->g_consts, &ctx->g_const_off,
                       &ctx->g_items, &ctx->g_part, &ctx->g_out})
       b->release();
     for (HostBuf* b : {&ctx->h_prog, &ctx->h_outs}) b->release();

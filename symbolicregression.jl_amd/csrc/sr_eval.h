@@ -73,6 +73,11 @@ hipError_t sr_launch_eval(const SrEvalArgs<T>& a, int mode, bool gather, int tie
 hipError_t sr_launch_reduce(const double* part_sum, const uint32_t* part_flag, int n_trees, int n_row_blocks,
                             const uint32_t* perm, const uint8_t* static_bad, double* out_sum, uint32_t* out_flag,
                             hipStream_t s);
+// isfinite(Julia pairwise sum) of n_arrays arrays from their leaf folds [n_arrays][n_leaves] (T),
+// combined by the post-order program `prog` (leaf index: push; -1: add the top two).
+template <typename T>
+hipError_t sr_launch_jsum_combine(const T* leaf_sums, int64_t n_arrays, int n_leaves, const int32_t* prog,
+                                  int prog_len, uint8_t* out, hipStream_t s);
 hipError_t sr_launch_pack_partials(const double* sum, const uint32_t* flag, int n, double* out, hipStream_t s);
 template <typename T>
 hipError_t sr_launch_transpose(const T* Xh_dev, int64_t nf, int64_t n, int64_t ld, T* Xd, hipStream_t s);
