@@ -329,6 +329,13 @@ int sr_last_kernel_ms(sr_ctx* ctx, double* eval_ms, double* total_ms);
  * sr_last_kernel_ms's eval_ms is the sum of those launches' durations. */
 int sr_last_phase_ms(sr_ctx* ctx, double* out, int n);
 
+/* Run-time tuning of a context (the SR_AMD_* environment variables are read once at sr_init):
+ * "derived" (0 / 1: derived columns for unary(feature) nodes of large LOSS calls).  Results do not
+ * depend on any knob.  SR_ERR_INVALID_ARG for an unknown name.  *used_derived_columns (optional
+ * query): sr_tuning_info reports how many derived columns the last sr_eval_loss_batch used. */
+int sr_set_tuning(sr_ctx* ctx, const char* name, int64_t value);
+int sr_tuning_info(sr_ctx* ctx, int* used_derived_columns);
+
 #ifdef __cplusplus
 }
 #endif

@@ -122,7 +122,10 @@ struct sr_ctx {
   hipEvent_t ev_join = nullptr;
   hipEvent_t ev_start = nullptr, ev_k0 = nullptr, ev_k1 = nullptr, ev_end = nullptr;
   hipEvent_t ev_c0[kMaxChunks] = {}, ev_c1[kMaxChunks] = {};  // per-chunk interpreter launches
+  hipEvent_t ev_d0 = nullptr, ev_d1 = nullptr;                 // the derived-column launch
   int n_chunks_last = 0;
+  bool derived_last = false;  // the last run_batch launched derived columns (timed by ev_d0/ev_d1)
+  int n_derived_last = 0;
   // programs + per-tree metadata of the last run_batch: ONE device allocation and ONE pinned staging
   // buffer with the same layout (code | offsets | static_bad | launch order), so a single-chunk call
   // uploads with one DMA; per-tree {Σ loss, flags} likewise share one allocation (one DMA back)
@@ -147,12 +150,16 @@ struct sr_ctx {
   int spin = 0;
   uint32_t hint_epoch = 0;  // dead-tree hint epoch of the current call
   int exact_g = 0;          // SR_AMD_EXACT_G (tuning): listed trees per workgroup of the EXACT pass
+  // SR_AMD_DERIVED (default 1): nodes unary(feature) shared by several trees of a large LOSS call
+  // are evaluated once per call into derived columns (LOAD_DERIVED); 0 disables
+  int derived = 1;
   std::mutex mu;
   std::vector<SrOpset> opsets;
   std::vector<int> tiers;
   std::vector<std::pair<int, double>> losses;  // registered (kind, param); code = kLossCodeBase + index
   DevBuf prog, outs, part_sum, part_flag, pred, row_idx, tree_list,
-      range_lo, range_hi, range_sums, packed, hint, jsum_prog, jsum_fin, probe_sum, probe_flag, g_code, g_offsets, g_consts, g_const_off, g_items, g_part, g_out;
+      range_lo, range_hi, range_sums, packed, hint, jsum_prog, jsum_fin, probe_sum, probe_flag, g_code, g_offsets, g_consts, g_const_off, g_items, g_part, g_out,
+      derived_cols;
   double last_eval_ms = 0.0, last_total_ms = 0.0;
   // host-side phases of the last eval_loss call (ms): compile, upload+launch, wait, exact pass,
   // finalize (sr_last_phase_ms)
@@ -284,9 +291,50 @@ int decode_loss(sr_ctx* ctx, int code, int* kind, double* param) {
 // an independent launch over its own slice of the per-tree device arrays; `prog` receives the merged
 // per-tree summary (offsets into the device code buffer, static_bad, max_depth, max_checks) that
 // the exact-sum pass and the callers use — its `code` stays empty.
+// Derived columns of a LOSS call: the unary(feature) nodes of the batch's transcendental operators
+// (exp / cos / sin / safe_log / safe_sqrt) that at least kDerivedMinUses trees of a sample share,
+// most used first, at most SR_MAX_DERIVED.  dmap: [SR_U_COUNT][nf] -> column or -1.
+constexpr int64_t kDerivedMinRows = 16384;  // below this the per-call column pass does not pay
+constexpr int kDerivedMinUses = 4;
+constexpr int64_t kDerivedSample = 4096;    // trees scanned
+void choose_derived(const sr_tree_batch& trees, const SrOpset& ops, int64_t nf, SrDerivedSpec* spec,
+                    std::vector<int16_t>* dmap) {
+  spec->n = 0;
+  dmap->assign(size_t(SR_U_COUNT) * size_t(nf), int16_t(-1));
+  auto eligible = [](uint32_t u) {
+    return u == SR_U_EXP || u == SR_U_COS || u == SR_U_SIN || u == SR_U_LOG || u == SR_U_SQRT;
+  };
+  std::vector<int32_t> uses(size_t(SR_U_COUNT) * size_t(nf), 0);
+  const int64_t ns = trees.n_trees < kDerivedSample ? trees.n_trees : kDerivedSample;
+  for (int64_t k = 0; k < ns; ++k) {
+    const int64_t b = trees.offsets[k], e = trees.offsets[k + 1];
+    // pre-order: node i (degree 1) has its child at i + 1
+    for (int64_t i = b; i + 1 < e; ++i) {
+      if (trees.degree[i] != 1 || trees.degree[i + 1] != 0 || trees.constant[i + 1]) continue;
+      const int oi = int(trees.op[i]) - 1;
+      const int f = int(trees.feature[i + 1]) - 1;
+      if (oi < 0 || oi >= int(ops.unary.size()) || f < 0 || f >= nf) continue;
+      const uint32_t u = ops.unary[size_t(oi)];
+      if (eligible(u)) ++uses[size_t(u) * size_t(nf) + size_t(f)];
+    }
+  }
+  std::vector<std::pair<int32_t, size_t>> cand;
+  for (size_t q = 0; q < uses.size(); ++q)
+    if (uses[q] >= kDerivedMinUses) cand.push_back({uses[q], q});
+  std::stable_sort(cand.begin(), cand.end(), [](const auto& x, const auto& y) { return x.first > y.first; });
+  for (const auto& c : cand) {
+    if (spec->n >= SR_MAX_DERIVED) break;
+    const int k = spec->n++;
+    spec->op[k] = uint8_t(c.second / size_t(nf));
+    spec->feat[k] = uint16_t(c.second % size_t(nf));
+    (*dmap)[c.second] = int16_t(k);
+  }
+}
+
 template <typename T>
 int run_batch(sr_ctx* ctx, const sr_dataset* ds, int opset_id, const sr_tree_batch* trees, const int64_t* row_idx,
-              int64_t n_idx, int64_t n_total, int loss_kind, int mode, SrProgramBatch<T>* prog, Grid* grid_out) {
+              int64_t n_idx, int64_t n_total, int loss_kind, int mode, SrProgramBatch<T>* prog, Grid* grid_out,
+              bool allow_derived = false) {
   const bool gather = row_idx != nullptr && n_idx > 0;
   const int64_t n_eval = gather ? n_idx : ds->n;
   if (n_eval <= 0) return set_error(SR_ERR_INVALID_ARG, "no rows to evaluate");
@@ -412,9 +460,34 @@ int run_batch(sr_ctx* ctx, const sr_dataset* ds, int opset_id, const sr_tree_bat
   uint8_t* h_bad = reinterpret_cast<uint8_t*>(hprog + o_bad);
   uint32_t* h_perm = reinterpret_cast<uint32_t*>(hprog + o_perm);
   ctx->n_chunks_last = 0;
+  ctx->derived_last = false;
+  ctx->n_derived_last = 0;
   SR_HIP_CHECK(hipEventRecord(ctx->ev_start, s));
   if (gather)
     SR_HIP_CHECK(hipMemcpyAsync(ctx->row_idx.p, row_idx, size_t(n_idx) * sizeof(int64_t), hipMemcpyHostToDevice, s));
+  // derived columns (LOAD_DERIVED): for the BASIC-tier deferred-check loss kernels over many rows,
+  // every unary(feature) node of a transcendental shared by several trees is evaluated once for the
+  // call.  Chosen from a sample of the batch; not when the data itself needs tracked feature loads.
+  std::vector<int16_t> dmap;
+  const int64_t dld = (n_eval + kRowAlign - 1) / kRowAlign * kRowAlign;
+  // (single-view calls only: row-sharded partials number their checked arrays identically on every
+  // rank, and a rank's choice of columns depends on its shard)
+  if (allow_derived && ctx->derived && mode == SR_MODE_LOSS && tier == SR_TIER_BASIC && n_eval >= kDerivedMinRows && nt >= 64 &&
+      ds->max_abs_x < double(T(t_max<T>() / (2.0 * double(n_total > 0 ? n_total : 1))))) {  // (track_x off)
+    SrDerivedSpec spec{};
+    choose_derived(*trees, ctx->opsets[opset_id], ds->nf, &spec, &dmap);
+    if (spec.n > 0) {
+      SR_HIP_CHECK(ctx->derived_cols.ensure(size_t(spec.n) * size_t(dld) * sizeof(T)));
+      SR_HIP_CHECK(hipEventRecord(ctx->ev_d0, s));
+      SR_HIP_CHECK(sr_launch_derived<T>(static_cast<const T*>(ds->X), ds->ld, gather ? ctx->row_idx.as<int64_t>() : nullptr,
+                                        n_eval, dld, spec, ctx->derived_cols.as<T>(), dld, s));
+      SR_HIP_CHECK(hipEventRecord(ctx->ev_d1, s));
+      ctx->derived_last = true;
+      ctx->n_derived_last = spec.n;
+    } else {
+      dmap.clear();
+    }
+  }
   if (n_chunks > 1) {  // odd chunks run on the second stream, after the shared setup above
     SR_HIP_CHECK(hipEventRecord(ctx->ev_join, s));
     SR_HIP_CHECK(hipStreamWaitEvent(ctx->stream2, ctx->ev_join, 0));
@@ -438,7 +511,8 @@ int run_batch(sr_ctx* ctx, const sr_dataset* ds, int opset_id, const sr_tree_bat
     sub.n_trees = nc;
     sub.offsets = trees->offsets + t0;  // node arrays stay indexed by absolute offsets
     SrProgramBatch<T> pc;
-    int rc = sr_compile_batch<T>(sub, ctx->opsets[opset_id], n_total, ds->nf, false, &pc, &err);
+    int rc = sr_compile_batch<T>(sub, ctx->opsets[opset_id], n_total, ds->nf, false, &pc, &err,
+                                 dmap.empty() ? nullptr : dmap.data());
     if (rc != SR_OK) {
       sync_both();  // earlier chunks may still read the staging buffers
       if (rc == SR_ERR_BAD_TREE || rc == SR_ERR_INVALID_ARG) {
@@ -533,6 +607,8 @@ int run_batch(sr_ctx* ctx, const sr_dataset* ds, int opset_id, const sr_tree_bat
       a.w = static_cast<const T*>(ds->w);
       a.row_idx = gather ? ctx->row_idx.as<int64_t>() : nullptr;
       a.ld = ds->ld;
+      a.derived = dmap.empty() ? nullptr : ctx->derived_cols.as<T>();
+      a.dld = dld;
       a.n_rows = n_eval;
       a.nf = int(ds->nf);
       a.tiles_per_block = g.tiles;
@@ -606,6 +682,10 @@ inline double chunk_kernel_ms(sr_ctx* ctx) {
   for (int c = 0; c < ctx->n_chunks_last; ++c) {
     float m = 0.f;
     if (hipEventElapsedTime(&m, ctx->ev_c0[c], ctx->ev_c1[c]) == hipSuccess) ms += double(m);
+  }
+  if (ctx->derived_last) {  // the derived columns are part of the call's interpreter work
+    float m = 0.f;
+    if (hipEventElapsedTime(&m, ctx->ev_d0, ctx->ev_d1) == hipSuccess) ms += double(m);
   }
   return ms;
 }
@@ -873,7 +953,7 @@ int eval_loss_impl(sr_ctx* ctx, const sr_dataset* ds, int opset_id, const sr_tre
   SrProgramBatch<T> prog;
   Grid g;
   ctx->want_host_out = true;
-  int rc = run_batch<T>(ctx, ds, opset_id, trees, row_idx, n_idx, n_eval, loss_kind, SR_MODE_LOSS, &prog, &g);
+  int rc = run_batch<T>(ctx, ds, opset_id, trees, row_idx, n_idx, n_eval, loss_kind, SR_MODE_LOSS, &prog, &g, true);
   ctx->want_host_out = false;
   if (rc != SR_OK) return rc;
   if (nt == 0) return SR_OK;
@@ -1195,6 +1275,7 @@ int sr_init(int device, sr_ctx** out) {
   if (const char* v = std::getenv("SR_AMD_HOST_IO")) ctx->host_io = std::atoi(v);
   if (const char* v = std::getenv("SR_AMD_SPIN")) ctx->spin = std::atoi(v);
   if (const char* v = std::getenv("SR_AMD_EXACT_G")) ctx->exact_g = std::atoi(v);
+  if (const char* v = std::getenv("SR_AMD_DERIVED")) ctx->derived = std::atoi(v);
   if (const char* v = std::getenv("SR_AMD_MAX_ROW_BLOCKS")) ctx->max_row_blocks = std::max(1, std::atoi(v));
   hipError_t e = hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking);
   if (e == hipSuccess) e = hipStreamCreateWithFlags(&ctx->stream2, hipStreamNonBlocking);
@@ -1203,6 +1284,8 @@ int sr_init(int device, sr_ctx** out) {
   if (e == hipSuccess) e = hipEventCreate(&ctx->ev_k0);
   if (e == hipSuccess) e = hipEventCreate(&ctx->ev_k1);
   if (e == hipSuccess) e = hipEventCreate(&ctx->ev_end);
+  if (e == hipSuccess) e = hipEventCreate(&ctx->ev_d0);
+  if (e == hipSuccess) e = hipEventCreate(&ctx->ev_d1);
   for (int c = 0; c < kMaxChunks; ++c) {
     if (e == hipSuccess) e = hipEventCreate(&ctx->ev_c0[c]);
     if (e == hipSuccess) e = hipEventCreate(&ctx->ev_c1[c]);
@@ -1223,7 +1306,7 @@ int sr_shutdown(sr_ctx* ctx) {
     (void)hipStreamSynchronize(ctx->stream);
     for (DevBuf* b : {&ctx->prog, &ctx->outs, &ctx->part_sum, &ctx->part_flag, &ctx->pred, &ctx->row_idx, &ctx->tree_list, &ctx->range_lo, &ctx->range_hi, &ctx->range_sums, &ctx->packed,
                       &ctx->hint, &ctx->jsum_prog, &ctx->jsum_fin, &ctx->probe_sum, &ctx->probe_flag, &ctx->g_code, &ctx->g_offsets, &ctx->g_consts, &ctx->g_const_off,
-                      &ctx->g_items, &ctx->g_part, &ctx->g_out})
+                      &ctx->g_items, &ctx->g_part, &ctx->g_out, &ctx->derived_cols})
       b->release();
     for (HostBuf* b : {&ctx->h_prog, &ctx->h_outs}) b->release();
     for (int c = 0; c < kMaxChunks; ++c) {
@@ -1237,6 +1320,8 @@ int sr_shutdown(sr_ctx* ctx) {
     (void)hipEventDestroy(ctx->ev_k0);
     (void)hipEventDestroy(ctx->ev_k1);
     (void)hipEventDestroy(ctx->ev_end);
+    (void)hipEventDestroy(ctx->ev_d0);
+    (void)hipEventDestroy(ctx->ev_d1);
     (void)hipStreamDestroy(ctx->stream);
   }
   delete ctx;
@@ -1590,6 +1675,23 @@ int sr_last_phase_ms(sr_ctx* ctx, double* out, int n) {
   if (check_ctx(ctx) != SR_OK) return SR_ERR_INVALID_ARG;
   for (int i = 0; i < n && i < 5; ++i) out[i] = ctx->phase_ms[i];
   if (n > 5) out[5] = double(ctx->n_chunks_last);
+  return SR_OK;
+}
+
+int sr_set_tuning(sr_ctx* ctx, const char* name, int64_t value) {
+  if (check_ctx(ctx) != SR_OK) return SR_ERR_INVALID_ARG;
+  if (!name) return set_error(SR_ERR_INVALID_ARG, "tuning knob name is NULL");
+  Lock l(ctx);
+  if (std::strcmp(name, "derived") == 0) {
+    ctx->derived = value != 0 ? 1 : 0;
+    return SR_OK;
+  }
+  return set_error(SR_ERR_INVALID_ARG, std::string("unknown tuning knob '") + name + "'");
+}
+
+int sr_tuning_info(sr_ctx* ctx, int* used_derived_columns) {
+  if (check_ctx(ctx) != SR_OK) return SR_ERR_INVALID_ARG;
+  if (used_derived_columns) *used_derived_columns = ctx->n_derived_last;
   return SR_OK;
 }
 

@@ -153,8 +153,21 @@ struct TreeCompiler {
   uint32_t n_consts = 0;
   int64_t n_ops = 0;
 
-  TreeCompiler(const SrOpset& o, int64_t nr, int64_t nf, bool wci)
-      : ops(o), n_rows(nr), nfeatures(nf), with_const_index(wci) {}
+  const int16_t* derived = nullptr;  // [SR_U_COUNT][nfeatures]: derived column of unary(feature), -1 none
+
+  TreeCompiler(const SrOpset& o, int64_t nr, int64_t nf, bool wci, const int16_t* dm = nullptr)
+      : ops(o), n_rows(nr), nfeatures(nf), with_const_index(wci), derived(dm) {}
+
+  // The derived column holding node i = unary(feature leaf) for the whole view, or -1.  (Such a node
+  // is a general deg1 node: its child is an unfused leaf, never constant here.)
+  int derived_col(int i) {
+    if (!derived || t.degree[i] != 1) return -1;
+    const int c = t.l[i];
+    if (t.degree[c] != 0 || t.constant[c]) return -1;
+    const uint32_t u = unary_id(i);
+    if (u == SR_U_NONE || u >= SR_U_COUNT) return -1;
+    return derived[size_t(u) * size_t(nfeatures) + size_t(t.feature[c] - 1)];
+  }
 
   bool leaf(int i) const { return t.degree[i] == 0; }
   bool effleaf(int i) const { return t.degree[i] == 0 || folded[i]; }
@@ -394,6 +407,7 @@ struct TreeCompiler {
       return;
     }
     if (in.op >= SR_OP_PAIR0) in.op += SR_P_PUSH;                    // PAIR v -> PAIR v + PUSH
+    else if (in.op == SR_OP_LOAD_DERIVED) in.op = SR_OP_LOAD_DERIVED_PUSH;
     else in.op += SR_OP_LOAD_FEAT_PUSH - SR_OP_LOAD_FEAT;            // LOAD_x -> LOAD_x_PUSH
     in.meta |= uint32_t(slot + 1) << SR_M_PUSH_SHIFT;
   }
@@ -445,6 +459,17 @@ struct TreeCompiler {
     const int d = t.degree[i];
     ++n_ops;
     if (d == 1) {
+      const int dc = infsub[i] ? -1 : derived_col(i);
+      if (dc >= 0) {  // the whole node from the call's derived column
+        SrIns<T> in{};
+        in.op = SR_OP_LOAD_DERIVED;
+        in.meta = uint32_t(dc);
+        // (op, feature) for kernels that recompute the node in place (the exact-sum pass)
+        in.c0 = (unary_id(i) << 16) | uint32_t(t.feature[t.l[i]] - 1);
+        code.push_back(in);
+        emit_check(i);
+        return;
+      }
       emit(t.l[i]);
       SrIns<T> in{};
       // fused unary: non-finite input -> +Inf
@@ -536,14 +561,15 @@ struct TreeCompiler {
 
 uint32_t sr_instruction_cost(uint32_t code) {
   uint32_t c = 6;  // dispatch + operand fetch + validity tracking
-  if (code == SR_OP_LOAD_FEAT_PUSH || code == SR_OP_LOAD_CONST_PUSH) c += 2;
+  if (code == SR_OP_LOAD_FEAT_PUSH || code == SR_OP_LOAD_CONST_PUSH || code == SR_OP_LOAD_DERIVED_PUSH) c += 2;
+  if (code == SR_OP_LOAD_DERIVED || code == SR_OP_LOAD_DERIVED_PUSH) return c + 3;
   if (code >= SR_OP_PAIR0) {
     c += ((code - SR_OP_PAIR0) % 6u >= SR_P_PUSH) ? 3 : 1;  // second operand (+ push)
     code = SR_OP_BINARY0 + (code - SR_OP_PAIR0) / 6u * 6u;  // priced as its binary operator
   }
   if (code >= SR_OP_BINARY0) {
     const uint32_t b = (code - SR_OP_BINARY0) / 6u + 1u;
-    if (b == SR_B_DIV) c += 10;
+    if (b == SR_B_DIV) c += 6;
     else if (b == SR_B_ADD || b == SR_B_SUB || b == SR_B_MUL) c += 1;
     else c += 20;
   } else if (code > SR_OP_UNARY0) {
@@ -551,7 +577,7 @@ uint32_t sr_instruction_cost(uint32_t code) {
     if (code >= SR_OP_UNARY_INF0) c += 2;
     switch (u) {
       case SR_U_NEG: case SR_U_SQUARE: case SR_U_CUBE: case SR_U_ABS: c += 2; break;
-      case SR_U_EXP: c += 14; break;
+      case SR_U_EXP: c += 9; break;
       case SR_U_LOG: c += 16; break;
       case SR_U_SQRT: c += 8; break;
       case SR_U_COS: case SR_U_SIN: c += 32; break;
@@ -576,7 +602,7 @@ uint32_t sr_binary_id(const char* name) {
 
 template <typename T>
 int sr_compile_batch(const sr_tree_batch& trees, const SrOpset& ops, int64_t n_rows, int64_t nfeatures,
-                     bool with_const_index, SrProgramBatch<T>* out, std::string* err) {
+                     bool with_const_index, SrProgramBatch<T>* out, std::string* err, const int16_t* derived) {
   const int64_t nt = trees.n_trees;
   if (nt < 0 || (nt > 0 && (!trees.offsets || !trees.degree || !trees.op || !trees.feature ||
                             !trees.constant || !trees.val))) {
@@ -602,7 +628,7 @@ int sr_compile_batch(const sr_tree_batch& trees, const SrOpset& ops, int64_t n_r
   std::vector<std::vector<SrIns<T>>> bufs(static_cast<size_t>(nthreads));
 
   auto work = [&](int w, int64_t lo, int64_t hi) {
-    TreeCompiler<T> tc(ops, n_rows, nfeatures, with_const_index);  // one per thread, reused
+    TreeCompiler<T> tc(ops, n_rows, nfeatures, with_const_index, with_const_index ? nullptr : derived);
     std::vector<SrIns<T>>& buf = bufs[size_t(w)];
     buf.reserve(size_t(trees.offsets[hi] - trees.offsets[lo]));
     for (int64_t k = lo; k < hi; ++k) {
@@ -690,6 +716,6 @@ int sr_compile_batch(const sr_tree_batch& trees, const SrOpset& ops, int64_t n_r
 }
 
 template int sr_compile_batch<float>(const sr_tree_batch&, const SrOpset&, int64_t, int64_t, bool,
-                                     SrProgramBatch<float>*, std::string*);
+                                     SrProgramBatch<float>*, std::string*, const int16_t*);
 template int sr_compile_batch<double>(const sr_tree_batch&, const SrOpset&, int64_t, int64_t, bool,
-                                      SrProgramBatch<double>*, std::string*);
+                                      SrProgramBatch<double>*, std::string*, const int16_t*);

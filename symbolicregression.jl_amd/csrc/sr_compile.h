@@ -51,6 +51,10 @@ struct SrProgramBatch {
 // step (dispatch overhead included): used only to order trees for load balance.
 uint32_t sr_instruction_cost(uint32_t opcode);
 
+// derived: optional [SR_U_COUNT][nfeatures] map (-1 = none) of the call's derived columns; nodes
+// unary(feature) with a column become one LOAD_DERIVED (BASIC-tier LOSS programs only; ignored with
+// with_const_index).
 template <typename T>
 int sr_compile_batch(const sr_tree_batch& trees, const SrOpset& ops, int64_t n_rows, int64_t nfeatures,
-                     bool with_const_index, SrProgramBatch<T>* out, std::string* err);
+                     bool with_const_index, SrProgramBatch<T>* out, std::string* err,
+                     const int16_t* derived = nullptr);

@@ -24,6 +24,8 @@ struct SrEvalArgs {
   const T* w;                  // NULL -> unweighted
   const int64_t* row_idx;      // GATHER mode: rows of the SubDataset
   int64_t ld;
+  const T* derived;            // LOAD_DERIVED columns [k][dld] over the rows of the view (NULL: none)
+  int64_t dld;
   int64_t n_rows;              // rows evaluated
   int nf;
   int tiles_per_block;
@@ -70,6 +72,17 @@ int sr_vstk_rows(int64_t n_rows, int requested);
 template <typename T>
 hipError_t sr_launch_eval(const SrEvalArgs<T>& a, int mode, bool gather, int tier, int R, int waves, bool vstk,
                           int n_blocks, hipStream_t s);
+// Derived columns of a call (LOAD_DERIVED): column k = op[k](X[feat[k]]) over the view's rows.
+constexpr int SR_MAX_DERIVED = 32;
+struct SrDerivedSpec {
+  int n;
+  uint8_t op[SR_MAX_DERIVED];
+  uint16_t feat[SR_MAX_DERIVED];  // 0-based feature
+};
+template <typename T>
+hipError_t sr_launch_derived(const T* X, int64_t ld, const int64_t* row_idx, int64_t n_view, int64_t n_pad,
+                             const SrDerivedSpec& spec, T* out, int64_t dld, hipStream_t s);
+
 hipError_t sr_launch_reduce(const double* part_sum, const uint32_t* part_flag, int n_trees, int n_row_blocks,
                             const uint32_t* perm, const uint8_t* static_bad, double* out_sum, uint32_t* out_flag,
                             hipStream_t s);

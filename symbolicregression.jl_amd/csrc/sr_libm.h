@@ -52,8 +52,8 @@ constexpr double kLn2Hi = 0x1.62e42fefa39efp-1, kLn2Lo = 0x1.abc9e3b39803fp-56;
 constexpr double kTwoOverPi = 0x1.45f306dc9c883p-1;
 constexpr double kPio2_1 = 0x1.921fb54442d18p+0, kPio2_2 = 0x1.1a62633145c07p-54, kPio2_3 = -0x1.f1976b7ed8fbcp-110;
 constexpr double kSqrtHalf = 0x1.6a09e667f3bcdp-1;
-constexpr double k16OverPi = 0x1.45f306dc9c883p+2;
-constexpr double kPi16_1 = 0x1.921fb54442d18p-3, kPi16_2 = 0x1.1a62633145c07p-57;
+constexpr double k64OverPi = 0x1.45f306dc9c883p+4;
+constexpr double kPi64_1 = 0x1.921fb54442d18p-5, kPi64_2 = 0x1.1a62633145c07p-59;
 // 2/pi in 32-bit words: bit 1 of word 0 is the 2^-1 bit (Payne-Hanek reduction of huge arguments)
 constexpr uint32_t kTwoOverPiBits[12] = {0xA2F9836Eu, 0x4E441529u, 0xFC2757D1u, 0xF534DDC0u, 0xDB629599u, 0x3C439041u,
                                          0xFE5163ABu, 0xDEBBC561u, 0xB7246E3Au, 0x424DD2E0u, 0x06492EEAu, 0x09D1921Cu};
@@ -229,28 +229,27 @@ SRL_HD inline double sr_rem_pio2f_fast(float x, int* q) {
   return y;
 }
 
-// |x| < 2^20: x = n pi/16 + r (three-part Cody-Waite in double), |r| <= pi/32; with
-// (s_k, c_k) = (sin, cos)(k pi/16), k = n mod 32: sin x = s_k cos r + c_k sin r,
-// cos x = c_k cos r - s_k sin r; sin r and cos r by Taylor to r^7 / r^6 (errors < 2^-42).
+// |x| < 2^20: x = n pi/64 + r (Cody-Waite in double), |r| <= pi/128; with (s_k, c_k) =
+// (sin, cos)(k pi/64), k = n mod 128: sin x = s_k cos r + c_k sin r, cos x = c_k cos r - s_k sin r;
+// sin r and cos r by Taylor to r^5 / r^4 (relative errors < 2^-44 / 2^-41).
 template <bool COS>
 SRL_HD inline float sr_sincosf_tab(float x, const double* tab) {
   const double xd = double(x);
-  // n = x 16/pi rounded to an integer by the 1.5 * 2^52 shifter: k = n mod 32 is the shifter's low
-  // bits (no conversions; a NaN x only yields a NaN result).  Two-part Cody-Waite with fused
-  // multiply-adds: |n| < 2^23, so the dropped third part (n * 2^-113 < 2^-90) is far below |r|'s ulp.
-  const double t = fma(xd, srl::k16OverPi, 0x1.8p52);
+  // n = x 64/pi rounded to an integer by the 1.5 * 2^52 shifter: k = n mod 128 is the shifter's
+  // low bits (no conversions; a NaN x only yields a NaN result).  Two-part Cody-Waite with fused
+  // multiply-adds: |n| < 2^25, so the dropped third part (n * 2^-115 < 2^-90) is far below |r|'s ulp.
+  const double t = fma(xd, srl::k64OverPi, 0x1.8p52);
   const double n = t - 0x1.8p52;
-  double r = fma(-n, srl::kPi16_1, xd);
-  r = fma(-n, srl::kPi16_2, r);
+  double r = fma(-n, srl::kPi64_1, xd);
+  r = fma(-n, srl::kPi64_2, r);
   uint64_t tb;
   __builtin_memcpy(&tb, &t, 8);
-  const int k = int(uint32_t(tb) & 31u);
-  const double sk = tab[2 * k], ck = tab[2 * k + 1];
+  // entry k = 16 bytes at byte offset 16 k
+  const double* e = reinterpret_cast<const double*>(reinterpret_cast<const char*>(tab) + ((uint32_t(tb) << 4) & 0x7f0u));
+  const double sk = e[0], ck = e[1];
   const double z = r * r;
-  const double sp = fma(z, fma(z, -0x1.a01a01a01a01ap-13, 0x1.1111111111111p-7), -0x1.5555555555555p-3);
-  const double sr = fma(z * r, sp, r);
-  const double cp = fma(z, fma(z, -0x1.6c16c16c16c17p-10, 0x1.5555555555555p-5), -0.5);
-  const double cr = fma(z, cp, 1.0);
+  const double sr = fma(z * r, fma(z, 0x1.1111111111111p-7, -0x1.5555555555555p-3), r);
+  const double cr = fma(z, fma(z, 0x1.5555555555555p-5, -0.5), 1.0);
   return COS ? float(fma(ck, cr, -(sk * sr))) : float(fma(sk, cr, ck * sr));
 }
 
@@ -269,15 +268,13 @@ SRL_HD inline float sr_sincosf_full(float x, const double* tab) {
 
 // ---------------------------------------------------------------- tables: host / device
 #if defined(__HIPCC__)
-// per-workgroup LDS copy of the tables (trig then log; 1 KiB: it must not cost the interpreter a
+// per-workgroup LDS copy of the tables (trig then log; 2.5 KiB: it must not cost the interpreter a
 // workgroup per CU)
-static __shared__ double sr_lds_libm[128];
+static __shared__ __attribute__((aligned(16))) double sr_lds_libm[256 + 64];
 // Copy the tables into LDS: every thread of the block calls this before the block's first barrier.
 __device__ inline void sr_libm_lds_fill(int tid, int nthreads) {
-  for (int i = tid; i < 64; i += nthreads) {
-    sr_lds_libm[i] = srl::kTrigTab[i];
-    sr_lds_libm[64 + i] = srl::kLogTab[i];
-  }
+  for (int i = tid; i < 256; i += nthreads) sr_lds_libm[i] = srl::kTrigTab[i];
+  for (int i = tid; i < 64; i += nthreads) sr_lds_libm[256 + i] = srl::kLogTab[i];
 }
 #endif
 SRL_HD inline const double* sr_trig_tab() {
@@ -289,7 +286,7 @@ SRL_HD inline const double* sr_trig_tab() {
 }
 SRL_HD inline const double* sr_log_tab() {
 #if defined(__HIP_DEVICE_COMPILE__)
-  return sr_lds_libm + 64;
+  return sr_lds_libm + 256;
 #else
   return srl::kLogTab;
 #endif

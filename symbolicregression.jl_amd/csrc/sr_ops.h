@@ -95,6 +95,9 @@ SR_HD inline bool sr_loss_propagates_nan(int32_t kind) {
 //           SR_P_FF: op(X[f], X[g])  SR_P_FC: op(X[f], c)  SR_P_CF: op(c, X[f])   (f in meta, g in c0)
 //           + SR_P_PUSH: the old tos is first stored to stack slot `push` (a subtree's first instruction)
 //         + and * never use CF (commuted to FC)
+//       SR_OP_LOAD_DERIVED (_PUSH)  tos <- D[k]: a derived column op_u(X[f]) computed once per call
+//                             for the whole batch (LOSS programs of BASIC-tier kernels only: the
+//                             node unary(feature), shared by many trees of a population)
 //   c0 (, c1) : constant bits (C variants, LOAD_CONST*): f32 in c0, f64 in c0 | c1 << 32
 //   (word order in memory: op, meta, c0, c1)
 //   meta bits  0-15 : operand index: feature f (F variants, LOAD_FEAT*), stack slot k (S variants),
@@ -109,6 +112,7 @@ enum : uint32_t {
   SR_OP_UNARY0 = 4u,       // opcode = SR_OP_UNARY0 + SrUnaryOp (1..)
   SR_OP_UNARY_INF0 = 40u,  // opcode = SR_OP_UNARY_INF0 + SrUnaryOp (fused: non-finite input -> +Inf)
   SR_OP_BINARY0 = 80u,     // opcode = SR_OP_BINARY0 + 6*(SrBinaryOp-1) + variant
+  SR_OP_LOAD_DERIVED = 78u, SR_OP_LOAD_DERIVED_PUSH = 79u,  // (between the unary-inf and binary ranges)
   SR_OP_PAIR0 = 256u,      // opcode = SR_OP_PAIR0 + 6*(SrBinaryOp-1) + pair variant
   SR_V_SL = 0u, SR_V_SR = 1u, SR_V_FL = 2u, SR_V_FR = 3u, SR_V_CL = 4u, SR_V_CR = 5u,
   SR_P_FF = 0u, SR_P_FC = 1u, SR_P_CF = 2u, SR_P_PUSH = 3u,
@@ -116,7 +120,8 @@ enum : uint32_t {
   SR_MAX_STACK_SLOTS = 62u,
 };
 static_assert(SR_OP_UNARY0 + SR_U_COUNT <= SR_OP_UNARY_INF0, "unary opcode ranges overlap");
-static_assert(SR_OP_UNARY_INF0 + SR_U_COUNT <= SR_OP_BINARY0, "unary opcode range overlaps the binary range");
+static_assert(SR_OP_UNARY_INF0 + SR_U_COUNT <= SR_OP_LOAD_DERIVED, "unary opcode range overlaps LOAD_DERIVED");
+static_assert(SR_OP_LOAD_DERIVED_PUSH < SR_OP_BINARY0, "LOAD_DERIVED overlaps the binary range");
 static_assert(SR_OP_BINARY0 + 6 * SR_B_COUNT <= SR_OP_PAIR0, "binary opcode range overlaps the pair range");
 #define SR_BIN_OPC(b, v) (SR_OP_BINARY0 + 6u * ((b) - 1u) + (v))
 #define SR_PAIR_OPC(b, v) (SR_OP_PAIR0 + 6u * ((b) - 1u) + (v))

@@ -208,6 +208,11 @@ __device__ __forceinline__ P* sr_row_at(P* base, uint32_t meta) {
 // being hoisted out of the interpreter loop and spilled, and each body exists once per kernel.
 template <int R>
 using SrRowVec = float __attribute__((ext_vector_type(R)));
+#ifdef SR_LIBM_INLINE
+#define SR_LIBM_CALL __attribute__((always_inline))
+#else
+#define SR_LIBM_CALL __attribute__((noinline))
+#endif
 // every row through the full-range function (Float32 log / cos / sin)
 template <uint32_t ID, int R>
 __device__ __attribute__((noinline)) SrRowVec<R> sr_libm_rows(SrRowVec<R> v) {
@@ -220,7 +225,7 @@ __device__ __attribute__((noinline)) SrRowVec<R> sr_libm_rows(SrRowVec<R> v) {
 }
 // Float32 log over the rows, its coefficients in scalar registers for the whole call
 template <int R>
-__device__ __attribute__((noinline)) SrRowVec<R> sr_log_rows(SrRowVec<R> v) {
+__device__ SR_LIBM_CALL SrRowVec<R> sr_log_rows(SrRowVec<R> v) {
   const SrLogC c = sr_logc_sgpr();
   const double* tab = sr_log_tab();
 #pragma unroll
@@ -233,7 +238,7 @@ __device__ __attribute__((noinline)) SrRowVec<R> sr_log_rows(SrRowVec<R> v) {
 // cos / sin when every row of the wave has |x| < 2^20 (a separate function: its few registers are
 // all caller-saved, so the common call saves nothing)
 template <uint32_t ID, int R>
-__device__ __attribute__((noinline)) SrRowVec<R> sr_trig_rows_fast(SrRowVec<R> v) {
+__device__ SR_LIBM_CALL SrRowVec<R> sr_trig_rows_fast(SrRowVec<R> v) {
 #pragma unroll
   for (int r = 0; r < R; ++r) {
     v[r] = (ID == SR_U_COS) ? sr_cosf_fast(v[r]) : sr_sinf_fast(v[r]);
@@ -242,19 +247,108 @@ __device__ __attribute__((noinline)) SrRowVec<R> sr_trig_rows_fast(SrRowVec<R> v
   return v;
 }
 
+// Two rows per v_pk_* instruction (gfx950 packed fp32: v_pk_fma / v_pk_mul / v_pk_add).
+using SrF2 = float __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ SrF2 sr_pk_fma(SrF2 a, SrF2 b, SrF2 c) { return __builtin_elementwise_fma(a, b, c); }
+__device__ __forceinline__ float sr_min3_abs(float m, float a, float b) {
+  float r;
+  asm("v_min3_f32 %0, %1, |%2|, |%3|" : "=v"(r) : "v"(m), "v"(a), "v"(b));
+  return r;
+}
+
+// Float32 exp over the rows.  When every row of the wave has |x| <= 88 (one ballot) this is the
+// OCML expf sequence itself — ph = x*log2e, pl = fma(x, log2e_lo, fma(x, log2e, -ph)),
+// exp2((ph - rint(ph)) + pl) * 2^rint(ph) — without its range selects, which are no-ops there (and
+// without the evaluator's x > MAX_EXP test), with the rounding steps two rows per packed
+// instruction and rint by the 1.5*2^23 shifter (exact for |ph| < 2^22): bit-identical results at
+// about half the VALU issue.  Otherwise every row takes the full function.
+template <int R>
+__device__ __forceinline__ void sr_exp_rows_f32(float (&v)[R]) {
+  static_assert(R % 2 == 0, "pairs of rows");
+  float m = 0.0f;
+#pragma unroll
+  for (int r = 0; r < R; r += 2) m = SrMaxAbs<float>::step(m, v[r], v[r + 1]);
+  if (__builtin_amdgcn_ballot_w64(!(m <= 88.0f)) == 0) {
+    const SrF2 c = __builtin_bit_cast(float, 0x3fb8aa3bu);    // log2(e) rounded
+    const SrF2 cc = __builtin_bit_cast(float, 0x32a5705fu);   // log2(e) - c
+    const SrF2 sh = 0x1.8p23f;
+#pragma unroll
+    for (int r = 0; r < R; r += 2) {
+      const SrF2 x = {v[r], v[r + 1]};
+      const SrF2 ph = x * c;
+      const SrF2 pl = sr_pk_fma(x, cc, sr_pk_fma(x, c, -ph));
+      const SrF2 t = ph + sh;
+      const SrF2 e = t - sh;
+      const SrF2 f = (ph - e) + pl;
+#pragma unroll
+      for (int q = 0; q < 2; ++q) {
+        const int k = int(e[q]);  // rint(ph), exact
+        v[r + q] = __builtin_amdgcn_ldexpf(__builtin_amdgcn_exp2f(f[q]), k);
+      }
+    }
+  } else {
+#pragma unroll
+    for (int r = 0; r < R; ++r) v[r] = sr_unary<float>(SR_U_EXP, v[r]);
+  }
+}
+
+// Float32 a / b over the rows (IEEE, as Julia's `/`).  The library's correctly rounded division
+// scales its operands (v_div_scale) and fixes up special cases (v_div_fixup) around a Newton /
+// Markstein core: y = rcp(b) refined once, q = a*y corrected twice by the exact remainder
+// fma(-b, q, a).  When |a| and |b| lie in [2^-40, 2^40] in every row of the wave the scaling is the
+// identity and no intermediate over- or underflows (1/b and q within 2^+-80, remainders exact), so
+// the bare core — its fma / mul steps two rows per packed instruction — returns the same correctly
+// rounded quotient.  The range test is one max3 and one min3 per row and one ballot (a NaN operand
+// is ignored by both and yields NaN through the core, as it must); a wave with any row outside it
+// (zeros, infinities, huge or tiny values) takes the full division in every row.
+template <int R>
+__device__ __forceinline__ void sr_div_rows_f32(float (&out)[R], const float (&a)[R], const float (&b)[R]) {
+  static_assert(R % 2 == 0, "pairs of rows");
+  float hi = 0.0f, lo = 0x1p40f;
+#pragma unroll
+  for (int r = 0; r < R; ++r) {
+    hi = SrMaxAbs<float>::step(hi, a[r], b[r]);
+    lo = sr_min3_abs(lo, a[r], b[r]);
+  }
+  if (__builtin_amdgcn_ballot_w64(!(hi <= 0x1p40f) || !(lo >= 0x1p-40f)) == 0) {
+    const SrF2 one = 1.0f;
+#pragma unroll
+    for (int r = 0; r < R; r += 2) {
+      const SrF2 A = {a[r], a[r + 1]};
+      const SrF2 B = {b[r], b[r + 1]};
+      SrF2 y = {__builtin_amdgcn_rcpf(b[r]), __builtin_amdgcn_rcpf(b[r + 1])};
+      y = sr_pk_fma(sr_pk_fma(-B, y, one), y, y);
+      SrF2 Q = A * y;
+      Q = sr_pk_fma(sr_pk_fma(-B, Q, A), y, Q);
+      Q = sr_pk_fma(sr_pk_fma(-B, Q, A), y, Q);
+      out[r] = Q[0];
+      out[r + 1] = Q[1];
+    }
+  } else {
+#pragma unroll
+    for (int r = 0; r < R; ++r) out[r] = a[r] / b[r];
+  }
+}
+
 // A unary operator over a lane's R rows.  Float32 cos / sin take the Cody-Waite fast path for all
 // rows unless some lane holds |x| >= 2^20 (one ballot: the Payne-Hanek path stays out of the
 // common case).
 template <typename T, uint32_t ID, int R>
 __device__ __forceinline__ void sr_unary_rows(T (&v)[R]) {
-  if constexpr (sizeof(T) == 4 && (ID == SR_U_LOG || ID == SR_U_COS || ID == SR_U_SIN)) {
+  if constexpr (sizeof(T) == 4 && ID == SR_U_EXP && R % 2 == 0) {
+    sr_exp_rows_f32<R>(v);
+  } else if constexpr (sizeof(T) == 4 && (ID == SR_U_LOG || ID == SR_U_COS || ID == SR_U_SIN)) {
     SrRowVec<R> x;
 #pragma unroll
     for (int r = 0; r < R; ++r) x[r] = v[r];
     bool slow = false;
     if constexpr (ID == SR_U_COS || ID == SR_U_SIN) {
+      // max |x| over the rows (v_max3 ignores NaN, which the fast path maps to NaN itself)
+      float m = 0.0f;
 #pragma unroll
-      for (int r = 0; r < R; ++r) slow |= !(__builtin_fabsf(v[r]) < srl::kTrigFastLimit);
+      for (int r = 0; r + 1 < R; r += 2) m = SrMaxAbs<float>::step(m, v[r], v[r + 1]);
+      if constexpr (R % 2 != 0) m = SrMaxAbs<float>::step(m, v[R - 1], v[R - 1]);
+      slow = !(m < srl::kTrigFastLimit);
     }
     if constexpr (ID == SR_U_LOG)
       x = sr_log_rows<R>(x);
@@ -276,11 +370,22 @@ __device__ __forceinline__ void sr_unary_rows(T (&v)[R]) {
     const T x = tos[r];                           \
     tos[r] = (EXPR);                              \
   }
-#define SR_BIN_EACH(AEXPR, BEXPR, ID)             \
-  _Pragma("unroll") for (int r = 0; r < R; ++r) { \
-    const T aa = (AEXPR);                         \
-    const T bb = (BEXPR);                         \
-    tos[r] = sr_binary<T>(ID, aa, bb);            \
+#define SR_BIN_EACH(AEXPR, BEXPR, ID)                                     \
+  if constexpr (sizeof(T) == 4 && (ID) == SR_B_DIV && R % 2 == 0) {       \
+    T aa_[R], bb_[R];                                                     \
+    _Pragma("unroll") for (int r = 0; r < R; ++r) {                       \
+      aa_[r] = (AEXPR);                                                   \
+      bb_[r] = (BEXPR);                                                   \
+    }                                                                     \
+    sr_div_rows_f32<R>(reinterpret_cast<float(&)[R]>(tos),                \
+                       reinterpret_cast<const float(&)[R]>(aa_),          \
+                       reinterpret_cast<const float(&)[R]>(bb_));         \
+  } else {                                                                \
+    _Pragma("unroll") for (int r = 0; r < R; ++r) {                       \
+      const T aa = (AEXPR);                                               \
+      const T bb = (BEXPR);                                               \
+      tos[r] = sr_binary<T>(ID, aa, bb);                                  \
+    }                                                                     \
   }
 // FAST_CHECK: every operator output joins the running max |v| of the tree
 #define SR_TRACK()                                                        \
@@ -680,6 +785,31 @@ __global__ void __launch_bounds__(W * 64, (SrMinWavesFor<T, R, TIER, W, VSTK>::v
               }
               break;
             }
+            case SR_OP_LOAD_DERIVED_PUSH:
+              SR_PUSH_TOS();
+              [[fallthrough]];
+            case SR_OP_LOAD_DERIVED: {
+              // unary(feature) from the call's derived columns (same chunk layout as the LDS tile,
+              // read straight from global memory); the node is an operator output: tracked
+              if constexpr (FAST_CHECK) {
+                L::load(a.derived + size_t(SR_META() & SR_M_INDEX) * size_t(a.dld) + size_t(row0) + size_t(lane * C), tos);
+                SR_TRACK();
+              } else {
+                // other kernels running a LOSS program (the exact-sum pass): the node in place,
+                // op_u(X[f]) with (u, f) from c0, exactly as the column was computed
+                const uint32_t uf = uint32_t(__builtin_amdgcn_readlane(int(wc0), int(k)));
+                L::load(sr_row_at<ROWS>(x_lane, uf & 0xffffu), tos);
+                switch (uf >> 16) {
+                  case SR_U_EXP: sr_unary_rows<T, SR_U_EXP, R>(tos); break;
+                  case SR_U_COS: sr_unary_rows<T, SR_U_COS, R>(tos); break;
+                  case SR_U_SIN: sr_unary_rows<T, SR_U_SIN, R>(tos); break;
+                  case SR_U_LOG: sr_unary_rows<T, SR_U_LOG, R>(tos); break;
+                  case SR_U_SQRT: sr_unary_rows<T, SR_U_SQRT, R>(tos); break;
+                  default: break;
+                }
+              }
+              break;
+            }
             case SR_OP_LOAD_CONST_PUSH:
               SR_PUSH_TOS();
               [[fallthrough]];
@@ -863,6 +993,53 @@ hipError_t sr_launch_tile(const SrEvalArgs<T>& a, int n_blocks, hipStream_t s) {
   hipLaunchKernelGGL((sr_tile_kernel<T, R, MODE, GATHER, TIER, W, LK, VSTK>), dim3(n_blocks), dim3(W * 64), plan.total, s, a);
   return hipGetLastError();
 }
+
+// ------------------------------------------------------------------ derived columns
+// Column k = op_k(X[f_k]) over rows [0, n_pad) of the view (gathered rows through row_idx; rows past
+// the view replicate its first row, as the tile staging does), computed with the interpreter's own
+// unary bodies, so a LOAD_DERIVED reads exactly the values UNARY0 + op_k would produce in place.
+template <typename T, int R>
+__global__ void __launch_bounds__(256) sr_derived_kernel(const T* __restrict__ X, int64_t ld, const int64_t* row_idx,
+                                                         int64_t n_view, int64_t n_pad, SrDerivedSpec spec,
+                                                         T* __restrict__ out, int64_t dld) {
+  sr_libm_lds_fill(int(threadIdx.x), 256);
+  __syncthreads();
+  const int k = int(blockIdx.y);
+  const int64_t v0 = (int64_t(blockIdx.x) * 256 + threadIdx.x) * R;
+  if (v0 >= n_pad) return;
+  const T* xf = X + int64_t(spec.feat[k]) * ld;
+  T v[R];
+#pragma unroll
+  for (int r = 0; r < R; ++r) {
+    const int64_t q = v0 + r;
+    v[r] = xf[row_idx ? row_idx[q < n_view ? q : 0] : q];
+  }
+  switch (spec.op[k]) {
+    case SR_U_EXP: sr_unary_rows<T, SR_U_EXP, R>(v); break;
+    case SR_U_COS: sr_unary_rows<T, SR_U_COS, R>(v); break;
+    case SR_U_SIN: sr_unary_rows<T, SR_U_SIN, R>(v); break;
+    case SR_U_LOG: sr_unary_rows<T, SR_U_LOG, R>(v); break;
+    case SR_U_SQRT: sr_unary_rows<T, SR_U_SQRT, R>(v); break;
+    default: break;
+  }
+  T* o = out + size_t(k) * size_t(dld) + size_t(v0);
+#pragma unroll
+  for (int r = 0; r < R; ++r) o[r] = v[r];
+}
+
+template <typename T>
+hipError_t sr_launch_derived(const T* X, int64_t ld, const int64_t* row_idx, int64_t n_view, int64_t n_pad,
+                             const SrDerivedSpec& spec, T* out, int64_t dld, hipStream_t s) {
+  constexpr int R = 8;
+  if (spec.n <= 0) return hipSuccess;
+  const int64_t per_block = 256 * R;
+  const dim3 grid(unsigned((n_pad + per_block - 1) / per_block), unsigned(spec.n));
+  hipLaunchKernelGGL((sr_derived_kernel<T, R>), grid, dim3(256), 0, s, X, ld, row_idx, n_view, n_pad, spec, out, dld);
+  return hipGetLastError();
+}
+#define SR_INSTANTIATE_DERIVED(T)                                                                            \
+  template hipError_t sr_launch_derived<T>(const T*, int64_t, const int64_t*, int64_t, int64_t, const SrDerivedSpec&, \
+                                           T*, int64_t, hipStream_t);
 
 // Explicit instantiations are spread over several translation units (sr_inst_*.hip, one per
 // element type / mode) so the build compiles them in parallel; see the Makefile.

@@ -60,6 +60,8 @@ EXPORTED_SYMBOLS = (
     "sr_host_unary",
     "sr_last_kernel_ms",
     "sr_last_phase_ms",
+    "sr_set_tuning",
+    "sr_tuning_info",
     "sr_search_create",
     "sr_search_free",
     "sr_search_use_device",
@@ -196,6 +198,8 @@ def _load():
         "sr_host_unary": (c_int, [c_int, c_char_p, c_int64, P, P]),
         "sr_last_kernel_ms": (c_int, [P, POINTER(c_double), POINTER(c_double)]),
         "sr_last_phase_ms": (c_int, [P, POINTER(c_double), c_int]),
+        "sr_set_tuning": (c_int, [P, ctypes.c_char_p, ctypes.c_int64]),
+        "sr_tuning_info": (c_int, [P, POINTER(c_int)]),
         "sr_search_create": (
             c_int,
             [c_int, c_int64, c_int64, c_int, POINTER(c_char_p), c_int, POINTER(c_char_p), POINTER(SrSearchOptions),

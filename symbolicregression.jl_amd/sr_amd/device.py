@@ -60,6 +60,16 @@ class DeviceContext:
         _lib.check(_lib.lib.sr_last_phase_ms(self.handle, out, 6))
         return [float(v) for v in out[:5]]
 
+    def set_tuning(self, name, value):
+        """Run-time tuning knob (results never depend on one): "derived" = 0 / 1."""
+        _lib.check(_lib.lib.sr_set_tuning(self.handle, name.encode(), int(value)))
+
+    def last_derived_columns(self):
+        """Derived columns (unary(feature) nodes evaluated once) used by the last eval_loss call."""
+        n = ctypes.c_int(0)
+        _lib.check(_lib.lib.sr_tuning_info(self.handle, ctypes.byref(n)))
+        return int(n.value)
+
     def last_launches(self):
         """Interpreter launches of the last eval_loss call (chunked compile/launch pipeline)."""
         out = (ctypes.c_double * 6)()
