@@ -61,11 +61,11 @@ if __name__ == "__main__":
 
 
 def tables():
-    """Tables of csrc/sr_libm.h: sin/cos(k pi/16), k = 0..31; log: for the 32 mantissa cells of
+    """Tables of csrc/sr_libm.h: sin/cos(k pi/64), k = 0..127; log: for the 32 mantissa cells of
     [1, 2), invc = 1 / (cell centre) rounded to double and logc = -log(invc) (so that
     log(m) = logc + log1p(m * invc - 1) holds exactly in real arithmetic); cells of [1.5, 2) serve
     m/2 (centre halved), cell 0 has centre 1."""
-    trig = [(float(mp.sin(k * mp.pi / 16)), float(mp.cos(k * mp.pi / 16))) for k in range(32)]
+    trig = [(float(mp.sin(k * mp.pi / 64)), float(mp.cos(k * mp.pi / 64))) for k in range(128)]
     logt = []
     for k in range(32):
         c = 1 + (mp.mpf(k) + mp.mpf(1) / 2) / 32
@@ -80,13 +80,13 @@ def tables():
 
 def emit_tables():
     trig, logt = tables()
-    print("constexpr double kTrigTab[64] = {" + ", ".join(float.hex(v) for p in trig for v in p) + "};")
+    print("constexpr double kTrigTab[256] = {" + ", ".join(float.hex(v) for p in trig for v in p) + "};")
     print("constexpr double kLogTab[64] = {" + ", ".join(float.hex(v) for p in logt for v in p) + "};")
-    h = mp.pi / 16
-    print("pi/16 split:", [float.hex(float(x)) for x in split(h, 3)], " 16/pi:", float.hex(float(16 / mp.pi)))
-    # polynomial bounds on |r| <= pi/32 (trig, Taylor to r^7 / r^6) and |r| <= 1/32 (log, to r^7)
-    r = mp.pi / 32
-    print("trig s rel err:", float(r ** 8 / mp.factorial(9)), " c err:", float(r ** 8 / mp.factorial(8)))
+    h = mp.pi / 1024  # reduction by 16 n' (pi / 1024) = n' pi / 64: the shifter's low word is 16 n'
+    print("pi/1024 split:", [float.hex(float(x)) for x in split(h, 3)], " 1024/pi:", float.hex(float(1024 / mp.pi)))
+    # polynomial bounds on |r| <= pi/128 (trig, Taylor to r^5 / r^4) and |r| <= 1/32 (log, to r^7)
+    r = mp.pi / 128
+    print("trig s rel err:", float(r ** 6 / mp.factorial(7)), " c err:", float(r ** 6 / mp.factorial(6)))
     r = mp.mpf(1) / 32
     print("log rel err (deg 7):", float(r ** 7 / 8))
 
