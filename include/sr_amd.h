@@ -291,6 +291,12 @@ int sr_search_create(int dtype, int64_t nfeatures, int64_t n_rows, int n_unary, 
 int sr_search_free(sr_search* s);
 /* score on the device: `ds` must match the search's dtype / features / rows */
 int sr_search_use_device(sr_search* s, sr_ctx* ctx, const sr_dataset* ds, int opset_id, int loss_code);
+/* an extra scoring lane (before sr_search_start): its own context and dataset copy on the same or
+ * another GPU.  sr_search_iterate then splits this rank's islands over the lanes, one host thread
+ * per lane, so one lane's device round trips overlap the others' work.  Results do not depend on
+ * the number of lanes (every draw comes from the islands' own streams); num_evals is summed per
+ * lane, so its last bits can differ. */
+int sr_search_add_device(sr_search* s, sr_ctx* ctx, const sr_dataset* ds, int opset_id, int loss_code);
 int sr_search_use_callbacks(sr_search* s, sr_loss_fn loss, sr_grad_fn grad, void* user);
 /* update_baseline_loss! and the initial populations of this rank's islands */
 int sr_search_start(sr_search* s, int niterations);
@@ -325,16 +331,18 @@ int sr_last_kernel_ms(sr_ctx* ctx, double* eval_ms, double* total_ms);
 
 /* Host-side phases of the last sr_eval_loss_batch call (ms, wall clock), up to n of: compile,
  * upload + launch, wait for the interpreter + reduction, exact-sum pass, finalize; out[5] (n >= 6)
- * = the number of interpreter launches of the call (the batch is compiled and launched in chunks).
+ * = the number of interpreter launches of the call (the batch is compiled and launched in chunks),
+ * out[6] (n >= 7) = device time of the exact-sum pass (ms).
  * sr_last_kernel_ms's eval_ms is the sum of those launches' durations. */
 int sr_last_phase_ms(sr_ctx* ctx, double* out, int n);
 
 /* Run-time tuning of a context (the SR_AMD_* environment variables are read once at sr_init):
  * "derived" (0 / 1: derived columns for unary(feature) nodes of large LOSS calls).  Results do not
- * depend on any knob.  SR_ERR_INVALID_ARG for an unknown name.  *used_derived_columns (optional
- * query): sr_tuning_info reports how many derived columns the last sr_eval_loss_batch used. */
+ * depend on any knob.  SR_ERR_INVALID_ARG for an unknown name.  sr_tuning_info (optional outputs)
+ * reports how many derived columns the last sr_eval_loss_batch used and how many of its trees went
+ * through the exact-sum pass (flagged BIG). */
 int sr_set_tuning(sr_ctx* ctx, const char* name, int64_t value);
-int sr_tuning_info(sr_ctx* ctx, int* used_derived_columns);
+int sr_tuning_info(sr_ctx* ctx, int* used_derived_columns, int64_t* exact_trees);
 
 #ifdef __cplusplus
 }

@@ -126,6 +126,8 @@ struct sr_ctx {
   int n_chunks_last = 0;
   bool derived_last = false;  // the last run_batch launched derived columns (timed by ev_d0/ev_d1)
   int n_derived_last = 0;
+  int64_t n_exact_last = 0;  // trees of the last eval_loss call sent through the exact-sum pass
+  double exact_kernel_ms = 0.0;  // device time of that pass (its interpreter + combine launches)
   // programs + per-tree metadata of the last run_batch: ONE device allocation and ONE pinned staging
   // buffer with the same layout (code | offsets | static_bad | launch order), so a single-chunk call
   // uploads with one DMA; per-tree {Σ loss, flags} likewise share one allocation (one DMA back)
@@ -296,7 +298,7 @@ int decode_loss(sr_ctx* ctx, int code, int* kind, double* param) {
 // most used first, at most SR_MAX_DERIVED.  dmap: [SR_U_COUNT][nf] -> column or -1.
 constexpr int64_t kDerivedMinRows = 16384;  // below this the per-call column pass does not pay
 constexpr int kDerivedMinUses = 4;
-constexpr int64_t kDerivedSample = 4096;    // trees scanned
+constexpr int64_t kDerivedSample = 1024;    // trees scanned
 void choose_derived(const sr_tree_batch& trees, const SrOpset& ops, int64_t nf, SrDerivedSpec* spec,
                     std::vector<int16_t>* dmap) {
   spec->n = 0;
@@ -833,9 +835,10 @@ int run_exact(sr_ctx* ctx, const sr_dataset* ds, const SrProgramBatch<T>& prog, 
   for (int64_t b0 = 0; b0 < n_list; b0 += batch) {
     const int64_t nb = std::min(batch, n_list - b0);
     // one wave per workgroup, G listed trees per workgroup (LDS: X tile + one wave's checked
-    // values [max_checks][rows] + running sums [G][max_checks]); G = 16 amortises the tile staging
-    // (one tree per workgroup measured slower on C2's pass: 1.32 vs 0.97 ms)
-    int G = int(std::min<int64_t>(nb, ctx->exact_g > 0 ? ctx->exact_g : 16));
+    // values [max_checks][rows] + running sums [G][max_checks]): G amortises the tile staging over
+    // trees, small G spreads few trees over more waves; aim at >= 8192 waves, G <= 16
+    const int64_t g_fill = (nb * n_ranges + 8191) / 8192;
+    int G = int(std::min<int64_t>(nb, ctx->exact_g > 0 ? ctx->exact_g : std::max<int64_t>(1, std::min<int64_t>(16, g_fill))));
     size_t lds = 0;
     for (;;) {
       lds = sr_tile_lds_bytes(int(sizeof(T)), int(ds->nf), R, depth, G, max_checks, 1, false);
@@ -870,6 +873,7 @@ int run_exact(sr_ctx* ctx, const sr_dataset* ds, const SrProgramBatch<T>& prog, 
     a.range_sums = ctx->range_sums.p;
     const int64_t blocks = int64_t(a.n_groups) * n_ranges;
     if (blocks > 0x7fffffff) return set_error(SR_ERR_INVALID_ARG, "grid too large");
+    SR_HIP_CHECK(hipEventRecord(ctx->ev_k0, s));
     SR_HIP_CHECK(sr_launch_eval<T>(a, SR_MODE_EXACT, gather, SR_TIER_FULL, R, 1, false, int(blocks), s));
     if (host_finite) {
       const int64_t n_arrays = nb * max_checks;
@@ -882,7 +886,10 @@ int run_exact(sr_ctx* ctx, const sr_dataset* ds, const SrProgramBatch<T>& prog, 
       SR_HIP_CHECK(hipMemcpyAsync(host_vals + size_t(b0) * max_checks * size_t(n_ranges), ctx->range_sums.p,
                                   size_t(nb) * per_tree, hipMemcpyDeviceToHost, s));
     }
+    SR_HIP_CHECK(hipEventRecord(ctx->ev_k1, s));
     SR_HIP_CHECK(hipStreamSynchronize(s));
+    float km = 0.f;
+    if (hipEventElapsedTime(&km, ctx->ev_k0, ctx->ev_k1) == hipSuccess) ctx->exact_kernel_ms += double(km);
   }
   return SR_OK;
 }
@@ -983,6 +990,8 @@ int eval_loss_impl(sr_ctx* ctx, const sr_dataset* ds, int opset_id, const sr_tre
   for (int64_t t = 0; t < nt; ++t)
     if ((flags[t] & (SR_FLAG_NONFINITE | SR_FLAG_STATIC)) == 0 && (flags[t] & SR_FLAG_BIG)) list.push_back(t);
   std::vector<uint8_t> list_ok;
+  ctx->n_exact_last = int64_t(list.size());
+  ctx->exact_kernel_ms = 0.0;
   rc = exact_list_ok<T>(ctx, ds, prog, row_idx, n_idx, list, &list_ok);
   if (rc != SR_OK) return rc;
   ctx->mark_phase(3);
@@ -1675,6 +1684,7 @@ int sr_last_phase_ms(sr_ctx* ctx, double* out, int n) {
   if (check_ctx(ctx) != SR_OK) return SR_ERR_INVALID_ARG;
   for (int i = 0; i < n && i < 5; ++i) out[i] = ctx->phase_ms[i];
   if (n > 5) out[5] = double(ctx->n_chunks_last);
+  if (n > 6) out[6] = ctx->exact_kernel_ms;
   return SR_OK;
 }
 
@@ -1689,9 +1699,10 @@ int sr_set_tuning(sr_ctx* ctx, const char* name, int64_t value) {
   return set_error(SR_ERR_INVALID_ARG, std::string("unknown tuning knob '") + name + "'");
 }
 
-int sr_tuning_info(sr_ctx* ctx, int* used_derived_columns) {
+int sr_tuning_info(sr_ctx* ctx, int* used_derived_columns, int64_t* exact_trees) {
   if (check_ctx(ctx) != SR_OK) return SR_ERR_INVALID_ARG;
   if (used_derived_columns) *used_derived_columns = ctx->n_derived_last;
+  if (exact_trees) *exact_trees = ctx->n_exact_last;
   return SR_OK;
 }
 

@@ -33,6 +33,7 @@
 #include <chrono>
 #include <memory>
 #include <string>
+#include <thread>
 #include <type_traits>
 #include <vector>
 
@@ -342,6 +343,27 @@ struct Engine : sr_search_base {
   double host_ms = 0.0;
   std::vector<int64_t> batch_idx;  // this iteration's minibatch (batching)
   Flat flat;
+  // Scoring lanes: lane 0 is (sc, flat, num_evals, host_ms); further lanes (sr_search_add_device:
+  // their own context and dataset copy) each run a share of the owned islands' iteration on their
+  // own host thread, so one lane's device round trip overlaps the others' host work and calls.
+  struct Lane {
+    Scorer<T>* sc;
+    Flat* flat;
+    double* num_evals;
+    double* host_ms;
+  };
+  struct ExtraLane {
+    Scorer<T> sc;
+    Flat flat;
+    double num_evals = 0.0, host_ms = 0.0;
+  };
+  std::vector<std::unique_ptr<ExtraLane>> extra;
+  Lane lane0() { return Lane{&sc, &flat, &num_evals, &host_ms}; }
+  double total_num_evals() const {
+    double v = num_evals;
+    for (const auto& x : extra) v += x->num_evals;
+    return v;
+  }
 
   bool owns(int i) const { return i % world == rank; }
   int64_t new_birth(int i) { return ++births[size_t(i)]; }
@@ -355,11 +377,11 @@ struct Engine : sr_search_base {
     v = v + T(float(complexity) * o.parsimony);
     return v;
   }
-  int score_trees(const std::vector<const SrTree<T>*>& trees, const std::vector<int64_t>& rows,
+  int score_trees(Lane L, const std::vector<const SrTree<T>*>& trees, const std::vector<int64_t>& rows,
                   std::vector<T>* loss, std::vector<T>* cost) {
-    flat.clear();
-    for (auto* t : trees) flat.add(*t);
-    int rc = sc.loss(flat, rows, loss);
+    L.flat->clear();
+    for (auto* t : trees) L.flat->add(*t);
+    int rc = L.sc->loss(*L.flat, rows, loss);
     if (rc) return rc;
     cost->resize(loss->size());
     for (size_t k = 0; k < loss->size(); ++k) (*cost)[k] = cost_of((*loss)[k], int(trees[k]->size()));
@@ -372,12 +394,12 @@ struct Engine : sr_search_base {
   // ------------------------------------------------------------ constant optimisation
   // optimize_constants over members (pointers); perturbation draws come from each member's island
   // stream, in member order (deterministic whatever the batch composition)
-  int optimize_members(const std::vector<Member<T>*>& ms, const std::vector<int>& island,
+  int optimize_members(Lane L, const std::vector<Member<T>*>& ms, const std::vector<int>& island,
                        const std::vector<int64_t>& rows, std::vector<uint8_t>* improved_out) {
     const size_t n = ms.size();
     improved_out->assign(n, 0);
     if (n == 0) return SR_OK;
-    if (!sc.has_grad()) return sr_set_error(SR_ERR_INVALID_ARG, "constant optimisation needs a gradient scorer");
+    if (!L.sc->has_grad()) return sr_set_error(SR_ERR_INVALID_ARG, "constant optimisation needs a gradient scorer");
     std::vector<const SrTree<T>*> trees(n);
     std::vector<std::vector<double>> x0(n);
     for (size_t k = 0; k < n; ++k) {
@@ -393,11 +415,11 @@ struct Engine : sr_search_base {
     std::vector<uint8_t> imp;
     std::vector<T> loss;
     std::vector<int64_t> f_calls;
-    const int rc = optimize_trees<T>(sc, flat, trees, x0, restarts, o.optimizer_iterations, rows, &bx, &imp, &loss, &f_calls);
+    const int rc = optimize_trees<T>(*L.sc, *L.flat, trees, x0, restarts, o.optimizer_iterations, rows, &bx, &imp, &loss, &f_calls);
     if (rc) return rc;
     const double frac = fraction(rows);
     for (size_t k = 0; k < n; ++k) {
-      num_evals += double(f_calls[k]) * frac;
+      *L.num_evals += double(f_calls[k]) * frac;
       if (!imp[k]) continue;
       // adopt: constants, the loss at the minimiser, cost, birth
       Member<T>& m = *ms[k];
@@ -407,7 +429,7 @@ struct Engine : sr_search_base {
       m.loss = loss[k];
       m.cost = cost_of(m.loss, m.complexity);
       m.birth = new_birth(island[k]);
-      num_evals += frac;
+      *L.num_evals += frac;
       (*improved_out)[k] = 1;
     }
     return SR_OK;
@@ -564,12 +586,12 @@ struct Engine : sr_search_base {
     size_t slot = 0;
   };
 
-  int round(double temperature, const std::vector<int64_t>& rows) {
+  int round(Lane L, const std::vector<int>& islands, double temperature, const std::vector<int64_t>& rows) {
     std::vector<Plan> plans;
-    plans.reserve(owned.size());
+    plans.reserve(islands.size());
     std::vector<const SrTree<T>*> pending;
     auto tp = Clock::now();
-    for (int i : owned) {
+    for (int i : islands) {
       SrRng& rng = rngs[size_t(i)];
       const int curmax = cur_maxsize[size_t(i)];
       Plan pl;
@@ -616,13 +638,13 @@ struct Engine : sr_search_base {
         if (pl.kind == K_CROSS) pending.push_back(&pl.tree2);
       }
     }
-    host_ms += ms_since(tp);
+    *L.host_ms += ms_since(tp);
     // device: ONE batched eval_cost for every island's children
     std::vector<T> loss, cost;
-    int rc = score_trees(pending, rows, &loss, &cost);
+    int rc = score_trees(L, pending, rows, &loss, &cost);
     if (rc) return rc;
     const double frac = fraction(rows);
-    num_evals += double(pending.size()) * frac;
+    *L.num_evals += double(pending.size()) * frac;
     // batched optimize mutations (rare: weight 0 by default)
     {
       std::vector<Member<T>*> om;
@@ -633,7 +655,7 @@ struct Engine : sr_search_base {
           oi.push_back(pl.island);
         }
       std::vector<uint8_t> imp;
-      if ((rc = optimize_members(om, oi, rows, &imp))) return rc;
+      if ((rc = optimize_members(L, om, oi, rows, &imp))) return rc;
     }
     tp = Clock::now();
     for (auto& pl : plans) {
@@ -732,7 +754,7 @@ struct Engine : sr_search_base {
         }
       }
     }
-    host_ms += ms_since(tp);
+    *L.host_ms += ms_since(tp);
     return SR_OK;
   }
 
@@ -781,7 +803,7 @@ struct Engine : sr_search_base {
       zero[0].constant = 1;
       std::vector<T> l, c;
       const std::vector<const SrTree<T>*> one{&zero};
-      int rc = score_trees(one, {}, &l, &c);
+      int rc = score_trees(lane0(), one, {}, &l, &c);
       if (rc) return rc;
       if (std::isfinite(double(l[0]))) {
         baseline = l[0];
@@ -802,7 +824,7 @@ struct Engine : sr_search_base {
     std::vector<const SrTree<T>*> ptr;
     for (auto& t : init) ptr.push_back(&t);
     std::vector<T> l, c;
-    int rc = score_trees(ptr, {}, &l, &c);
+    int rc = score_trees(lane0(), ptr, {}, &l, &c);
     if (rc) return rc;
     num_evals += double(init.size());
     for (size_t k = 0; k < init.size(); ++k) {
@@ -843,20 +865,21 @@ struct Engine : sr_search_base {
     return out;
   }
 
-  // s_r_cycle + optimize_and_simplify_population (+ finalize_costs) of every owned island
-  int iterate() {
-    const std::vector<int64_t> rows = draw_batch(0);
-    for (int i : owned) best_seen[size_t(i)].reset(o.maxsize);
+  // s_r_cycle + optimize_and_simplify_population (+ finalize_costs) of a set of islands, scored on
+  // one lane (every draw comes from the islands' own streams: the result does not depend on how the
+  // owned islands are split over lanes)
+  int iterate_islands(Lane L, const std::vector<int>& islands, const std::vector<int64_t>& rows,
+                      const std::vector<int64_t>& orows) {
     const int ncyc = o.ncycles_per_iteration;
     const int n_evol = (o.population_size + o.tournament_selection_n - 1) / o.tournament_selection_n;
     for (int c = 0; c < ncyc; ++c) {
       const double temperature =
           ncyc > 1 ? (o.annealing ? 1.0 - double(c) / double(ncyc - 1) : 1.0) : 1.0;  // LinRange(1, 0, ncyc)
       for (int r = 0; r < n_evol; ++r) {
-        int rc = round(temperature, rows);
+        int rc = round(L, islands, temperature, rows);
         if (rc) return rc;
       }
-      for (int i : owned)
+      for (int i : islands)
         for (const auto& m : pops[size_t(i)]) {
           const int s = m.complexity;
           auto& h = best_seen[size_t(i)];
@@ -868,10 +891,9 @@ struct Engine : sr_search_base {
     }
     // optimize_and_simplify_population: the simplification of every member, then one batched
     // constant optimisation over every island's selected members
-    const std::vector<int64_t> orows = draw_batch(1);
     std::vector<Member<T>*> sel;
     std::vector<int> sel_island;
-    for (int i : owned) {
+    for (int i : islands) {
       auto& pop = pops[size_t(i)];
       std::vector<uint8_t> doopt(pop.size());
       for (size_t j = 0; j < pop.size(); ++j) doopt[j] = rngs[size_t(i)].uniform() < double(o.optimizer_probability);
@@ -887,11 +909,11 @@ struct Engine : sr_search_base {
       }
     }
     std::vector<uint8_t> imp;
-    int rc = optimize_members(sel, sel_island, orows, &imp);
+    int rc = optimize_members(L, sel, sel_island, orows, &imp);
     if (rc) return rc;
     if (o.batching) {  // finalize_costs + best-seen re-scoring on the full data
       std::vector<Member<T>*> ms;
-      for (int i : owned) {
+      for (int i : islands) {
         for (auto& m : pops[size_t(i)]) ms.push_back(&m);
         auto& h = best_seen[size_t(i)];
         for (size_t s = 0; s < h.m.size(); ++s)
@@ -900,18 +922,48 @@ struct Engine : sr_search_base {
       std::vector<const SrTree<T>*> tr;
       for (auto* m : ms) tr.push_back(&m->tree);
       std::vector<T> l, c;
-      if ((rc = score_trees(tr, {}, &l, &c))) return rc;
+      if ((rc = score_trees(L, tr, {}, &l, &c))) return rc;
       for (size_t k = 0; k < ms.size(); ++k) {
         ms[k]->loss = l[k];
         ms[k]->cost = cost_of(l[k], ms[k]->complexity);
       }
-      num_evals += double(ms.size());
+      *L.num_evals += double(ms.size());
     }
-    for (int i : owned)
+    for (int i : islands)
       for (auto& m : pops[size_t(i)]) {
         m.parent = m.ref;
         m.ref = new_ref(i);
       }
+    return SR_OK;
+  }
+
+  int iterate() {
+    const std::vector<int64_t> rows = draw_batch(0);
+    const std::vector<int64_t> orows = draw_batch(1);
+    for (int i : owned) best_seen[size_t(i)].reset(o.maxsize);
+    const size_t nl = std::min(owned.size(), extra.size() + 1);
+    if (nl <= 1) {
+      const int rc = iterate_islands(lane0(), owned, rows, orows);
+      if (rc) return rc;
+    } else {
+      // contiguous shares of the owned islands, one host thread per extra lane
+      std::vector<std::vector<int>> share(nl);
+      for (size_t k = 0; k < owned.size(); ++k) share[k * nl / owned.size()].push_back(owned[k]);
+      std::vector<int> rcs(nl, SR_OK);
+      std::vector<std::string> msgs(nl);
+      std::vector<std::thread> th;
+      for (size_t q = 1; q < nl; ++q)
+        th.emplace_back([&, q] {
+          ExtraLane& x = *extra[q - 1];
+          rcs[q] = iterate_islands(Lane{&x.sc, &x.flat, &x.num_evals, &x.host_ms}, share[q], rows, orows);
+          if (rcs[q]) msgs[q] = sr_last_error();
+        });
+      rcs[0] = iterate_islands(lane0(), share[0], rows, orows);
+      if (rcs[0]) msgs[0] = sr_last_error();
+      for (auto& t : th) t.join();
+      for (size_t q = 0; q < nl; ++q)
+        if (rcs[q]) return sr_set_error(rcs[q], msgs[q]);
+    }
     s_r_cycles += int64_t(owned.size());
     return SR_OK;
   }
@@ -1195,6 +1247,28 @@ int sr_search_use_device(sr_search* s, sr_ctx* ctx, const sr_dataset* ds, int op
   });
 }
 
+int sr_search_add_device(sr_search* s, sr_ctx* ctx, const sr_dataset* ds, int opset_id, int loss_code) {
+  return dispatch<int>(s, [&](auto* e) {
+    if (!ctx || !ds) return sr_set_error(SR_ERR_INVALID_ARG, "NULL context or dataset");
+    if (!e->sc.ctx) return sr_set_error(SR_ERR_INVALID_ARG, "sr_search_use_device first (lane 0)");
+    if (!e->pops.empty()) return sr_set_error(SR_ERR_INVALID_ARG, "lanes must be added before sr_search_start");
+    int dt = 0;
+    int64_t nf = 0, n = 0;
+    int rc = sr_dataset_info(ds, &dt, &nf, &n);
+    if (rc) return rc;
+    if (dt != e->dtype || nf != e->sp.nfeatures || n != e->n_rows)
+      return sr_set_error(SR_ERR_INVALID_ARG, "dataset does not match the search (dtype, features, rows)");
+    using E = std::remove_reference_t<decltype(*e)>;
+    auto x = std::make_unique<typename E::ExtraLane>();
+    x->sc.ctx = ctx;
+    x->sc.ds = ds;
+    x->sc.opset_id = opset_id;
+    x->sc.loss_code = loss_code;
+    e->extra.push_back(std::move(x));
+    return SR_OK;
+  });
+}
+
 int sr_search_use_callbacks(sr_search* s, sr_loss_fn loss, sr_grad_fn grad, void* user) {
   return dispatch<int>(s, [&](auto* e) {
     if (!loss) return sr_set_error(SR_ERR_INVALID_ARG, "NULL loss callback");
@@ -1203,6 +1277,7 @@ int sr_search_use_callbacks(sr_search* s, sr_loss_fn loss, sr_grad_fn grad, void
     e->sc.cb_user = user;
     e->sc.ctx = nullptr;
     e->sc.ds = nullptr;
+    e->extra.clear();
     return SR_OK;
   });
 }
@@ -1253,10 +1328,15 @@ int sr_search_get_info(sr_search* s, sr_search_info* out) {
     if (!out) return sr_set_error(SR_ERR_INVALID_ARG, "NULL output");
     out->iterations = e->iteration;
     out->s_r_cycles = e->s_r_cycles;
-    out->num_evals = e->num_evals;
+    out->num_evals = e->total_num_evals();
     out->device_calls = e->sc.calls;
     out->device_ms = e->sc.ms;
     out->host_ms = e->host_ms;
+    for (const auto& x : e->extra) {  // (summed over lanes: lanes run concurrently)
+      out->device_calls += x->sc.calls;
+      out->device_ms += x->sc.ms;
+      out->host_ms += x->host_ms;
+    }
     out->baseline_loss = double(e->baseline);
     out->use_baseline = e->use_baseline ? 1 : 0;
     return SR_OK;

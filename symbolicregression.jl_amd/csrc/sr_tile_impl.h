@@ -878,7 +878,20 @@ __global__ void __launch_bounds__(W * 64, (SrMinWavesFor<T, R, TIER, W, VSTK>::v
           for (int k = lane; k < nk; k += 64) {
             const T* cb = chk + (size_t(wave) * MC + k) * ROWS;
             T v = (tile == 0) ? cb[0] : jst[g * MC + k];
-            for (int i = (tile == 0) ? 1 : 0; i < n_valid; ++i) v = v + cb[i];
+            int i = (tile == 0) ? 1 : 0;
+            // the adds stay sequential in row order; the LDS reads go 16 rows at a time (16-byte
+            // reads all in flight before the adds) instead of one latency per row
+            for (; i < n_valid && (i & 3); ++i) v = v + cb[i];
+            for (; i + 16 <= n_valid; i += 16) {
+              using V = typename SrChunk<T>::V;
+              constexpr int CH = SrChunk<T>::N;
+              T blk[16];
+#pragma unroll
+              for (int q = 0; q < 16; q += CH) SrChunk<T>::get(*reinterpret_cast<const V*>(cb + i + q), blk + q);
+#pragma unroll
+              for (int q = 0; q < 16; ++q) v = v + blk[q];
+            }
+            for (; i < n_valid; ++i) v = v + cb[i];
             jst[g * MC + k] = v;
           }
           __builtin_amdgcn_wave_barrier();

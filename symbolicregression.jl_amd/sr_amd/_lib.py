@@ -65,6 +65,7 @@ EXPORTED_SYMBOLS = (
     "sr_search_create",
     "sr_search_free",
     "sr_search_use_device",
+    "sr_search_add_device",
     "sr_search_use_callbacks",
     "sr_search_start",
     "sr_search_iterate",
@@ -199,7 +200,7 @@ def _load():
         "sr_last_kernel_ms": (c_int, [P, POINTER(c_double), POINTER(c_double)]),
         "sr_last_phase_ms": (c_int, [P, POINTER(c_double), c_int]),
         "sr_set_tuning": (c_int, [P, ctypes.c_char_p, ctypes.c_int64]),
-        "sr_tuning_info": (c_int, [P, POINTER(c_int)]),
+        "sr_tuning_info": (c_int, [P, POINTER(c_int), POINTER(c_int64)]),
         "sr_search_create": (
             c_int,
             [c_int, c_int64, c_int64, c_int, POINTER(c_char_p), c_int, POINTER(c_char_p), POINTER(SrSearchOptions),
@@ -207,6 +208,7 @@ def _load():
         ),
         "sr_search_free": (c_int, [P]),
         "sr_search_use_device": (c_int, [P, P, P, c_int, c_int]),
+        "sr_search_add_device": (c_int, [P, P, P, c_int, c_int]),
         "sr_search_use_callbacks": (c_int, [P, LOSS_FN, GRAD_FN, P]),
         "sr_search_start": (c_int, [P, c_int]),
         "sr_search_iterate": (c_int, [P]),

@@ -52,7 +52,8 @@ class Dataset:
     # ---------------------------------------------------------------- device residency
     def device_handle(self, ctx=None):
         ctx = ctx or get_context()
-        h = self._device.get(ctx.device)
+        key = ctx.handle.value  # one copy per context (a search's scoring lanes each hold one)
+        h = self._device.get(key)
         if h is None:
             Xj = np.ascontiguousarray(self.X.T)  # Julia column-major [nf, n]: address f + nf*i
             y = None if self.y is None else np.ascontiguousarray(self.y)
@@ -71,7 +72,7 @@ class Dataset:
                 )
             )
             h = out
-            self._device[ctx.device] = h
+            self._device[key] = h
         return h
 
     def free_device(self):

@@ -9,6 +9,7 @@ from . import _lib
 
 _lock = threading.Lock()
 _contexts: dict = {}
+_lane_contexts: dict = {}
 
 
 class DeviceContext:
@@ -67,8 +68,20 @@ class DeviceContext:
     def last_derived_columns(self):
         """Derived columns (unary(feature) nodes evaluated once) used by the last eval_loss call."""
         n = ctypes.c_int(0)
-        _lib.check(_lib.lib.sr_tuning_info(self.handle, ctypes.byref(n)))
+        _lib.check(_lib.lib.sr_tuning_info(self.handle, ctypes.byref(n), None))
         return int(n.value)
+
+    def last_exact_trees(self):
+        """Trees of the last eval_loss call that went through the exact-sum pass (flagged BIG)."""
+        n = ctypes.c_int64(0)
+        _lib.check(_lib.lib.sr_tuning_info(self.handle, None, ctypes.byref(n)))
+        return int(n.value)
+
+    def last_exact_kernel_ms(self):
+        """Device time of the last eval_loss call's exact-sum pass (ms)."""
+        out = (ctypes.c_double * 7)()
+        _lib.check(_lib.lib.sr_last_phase_ms(self.handle, out, 7))
+        return float(out[6])
 
     def last_launches(self):
         """Interpreter launches of the last eval_loss call (chunked compile/launch pipeline)."""
@@ -84,6 +97,20 @@ class DeviceContext:
 
 def default_device() -> int:
     return int(os.environ.get("SR_AMD_DEVICE", os.environ.get("LOCAL_RANK", "0")))
+
+
+def get_lane_context(lane: int, device: int | None = None) -> DeviceContext:
+    """Scoring lane ``lane`` of a device: lane 0 is get_context(device); further lanes are contexts
+    of their own (own streams and staging buffers), cached for the process."""
+    if lane == 0:
+        return get_context(device)
+    dev = default_device() if device is None else int(device)
+    with _lock:
+        ctx = _lane_contexts.get((dev, lane))
+        if ctx is None:
+            ctx = DeviceContext(dev)
+            _lane_contexts[(dev, lane)] = ctx
+        return ctx
 
 
 def get_context(device: int | None = None) -> DeviceContext:

@@ -186,6 +186,13 @@ class NativeSearch:
         _lib.check(_lib.lib.sr_search_use_device(self.h, ctx.handle, dataset.device_handle(ctx),
                                                  ctx.opset_id(self.options.operators), ctx.loss_code(self.options)))
 
+    def add_device(self, dataset, ctx):
+        """An extra scoring lane (its own context and dataset copy): iterate() splits this rank's
+        islands over the lanes, one host thread each."""
+        self._keep.append(dataset)
+        _lib.check(_lib.lib.sr_search_add_device(self.h, ctx.handle, dataset.device_handle(ctx),
+                                                 ctx.opset_id(self.options.operators), ctx.loss_code(self.options)))
+
     def use_callbacks(self, loss_fn, grad_fn=None):
         """CPU scorers (tests): loss_fn(TreeBatch, rows or None) -> losses (Inf where incomplete);
         grad_fn(TreeBatch, rows) -> (losses, gradients over the batch's constants)."""
@@ -306,13 +313,15 @@ def _torch_comm():
 
 
 def equation_search(X=None, y=None, *, niterations=10, options, weights=None, search_options=None, seed=0,
-                    verbosity=0, dataset=None, distributed=False, _loss_fn=None, _grad_fn=None):
+                    verbosity=0, dataset=None, distributed=False, scoring_lanes=2, _loss_fn=None, _grad_fn=None):
     """Batched-island ``equation_search`` (src/SymbolicRegression.jl:967-1216) -> SearchResult.
 
     distributed=True (torch.distributed initialised, one process per GPU; SURVEY §8(e) island
     sharding): island i lives on rank i % world; every rank scores only its islands' children (one
     batched launch per round on its own GPU); after each iteration the ranks all-gather their islands
     and every rank replays the head's island-by-island bookkeeping identically.
+    scoring_lanes: device contexts (streams) the rank's islands are split over, one host thread each,
+    so device round trips overlap; results do not depend on it (num_evals up to rounding).
     ``_loss_fn`` / ``_grad_fn`` replace the device scorer with CPU callbacks (tests only)."""
     so = search_options or SearchOptions()
     comm = _torch_comm() if distributed else None
@@ -323,7 +332,12 @@ def equation_search(X=None, y=None, *, niterations=10, options, weights=None, se
     if _loss_fn is not None:
         eng.use_callbacks(_loss_fn, _grad_fn)
     else:
+        from .device import get_lane_context
+
         eng.use_device(dataset)
+        n_own = len(range(rank, options.populations, world))
+        for lane in range(1, max(1, min(int(scoring_lanes), n_own))):
+            eng.add_device(dataset, get_lane_context(lane))
 
     def exchange():
         if world == 1:

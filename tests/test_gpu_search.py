@@ -96,3 +96,23 @@ def test_c3_search_device_equals_oracle_scored_search():
     assert ([string_tree(m.tree, opts.operators) for m in dev.pareto_frontier] ==
             [string_tree(m.tree, opts.operators) for m in ref.pareto_frontier])
     assert dev.device_calls == ref.device_calls > 40
+
+
+@pytest.mark.parametrize("batching", [False, True])
+def test_scoring_lanes_change_nothing(batching):
+    """Islands split over 1, 2 and 3 scoring lanes (own contexts and streams, one host thread each)
+    evolve identically: same populations, costs and losses bit for bit; num_evals up to rounding."""
+    X, y = _readme_data(300, seed=5)
+    opts = Options(binary_operators=["+", "*", "-", "/"], unary_operators=["cos", "exp"], populations=6,
+                   population_size=20, ncycles_per_iteration=15, maxsize=15, batching=batching, batch_size=64,
+                   optimizer_probability=0.3)
+    runs = []
+    for lanes in (1, 2, 3):
+        res = equation_search(X, y, niterations=3, options=opts, seed=9, scoring_lanes=lanes)
+        pops = [[(string_tree(m.tree, opts.operators), np.float32(m.cost).tobytes(), np.float32(m.loss).tobytes(),
+                  m.birth, m.ref, m.parent) for m in p] for p in res.populations]
+        runs.append((pops, res.num_evals, res.device_calls))
+    assert runs[1][0] == runs[0][0]
+    assert runs[2][0] == runs[0][0]
+    assert runs[1][1] == pytest.approx(runs[0][1], rel=1e-12)
+    assert runs[2][2] > runs[0][2]  # the islands' rounds went through several lanes

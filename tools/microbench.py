@@ -49,5 +49,7 @@ for name, kw in mixes.items():
     ne = tb.n_nodes * n
     print(f"{name:24s} nodes={tb.n_nodes:7d} ops={tb.n_operator_nodes:6d} complete={c.mean():.3f} "
           f"kernel={k:7.3f}ms step={t:7.3f}ms  {ne / k / 1e9:8.1f} Gnode/s(kernel)  {ne / t / 1e9:8.1f} Gnode/s(step)"
-          f"  phases(compile/launch/wait/exact/final)=" + "/".join(f"{v:.2f}" for v in np.median(np.array(ph), 0)),
+          f"  phases(compile/launch/wait/exact/final)=" + "/".join(f"{v:.2f}" for v in np.median(np.array(ph), 0))
+          + f"  derived={ctx.last_derived_columns()} exact_trees={ctx.last_exact_trees()}"
+          f" exact_kernel={ctx.last_exact_kernel_ms():.3f}ms",
           flush=True)
