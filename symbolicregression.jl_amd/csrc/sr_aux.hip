@@ -44,37 +44,43 @@ __global__ void __launch_bounds__(256) sr_reduce_partials_kernel(const double* _
 // Julia's pairwise `sum` of one view, from its leaf folds: every thread combines one array's
 // n_leaves folds by the shared post-order program (leaf index: push it; -1: add the top two, in T),
 // the order of Base.mapreduce_impl's recursion; out[a] = isfinite(total).
+// Base.mapreduce_impl's combine of one view's leaf folds, level by level: `nodes` holds the
+// internal nodes of the recursion tree grouped by height (level_off), each as (left, right) with
+// c >= 0 = leaf c and c < 0 = internal node -c-1; a node's two children are always of lower height,
+// so a level's nodes are independent.  One workgroup per array; the internal sums go to `scratch`
+// ([n_arrays][n_internal], global: the workgroup barrier orders them); the root's isfinite -> out.
 template <typename T>
-__global__ void __launch_bounds__(256) sr_jsum_combine_kernel(const T* __restrict__ leaf_sums, int64_t n_arrays,
-                                                              int n_leaves, const int32_t* __restrict__ prog,
-                                                              int prog_len, uint8_t* __restrict__ out) {
-  const int64_t a = int64_t(blockIdx.x) * blockDim.x + threadIdx.x;
-  if (a >= n_arrays) return;
-  T st[48];  // kJsumMaxDepth
-  int sp = 0;
-  const T* v = leaf_sums + a * n_leaves;
-  for (int i = 0; i < prog_len; ++i) {
-    const int c = prog[i];
-    if (c >= 0) {
-      st[sp++] = v[c];
-    } else {
-      const T b = st[--sp];
-      st[sp - 1] = st[sp - 1] + b;
+__global__ void __launch_bounds__(256) sr_jsum_levels_kernel(const T* __restrict__ leaf_sums, int n_leaves,
+                                                             const int2* __restrict__ nodes, int n_internal,
+                                                             const int32_t* __restrict__ level_off, int n_levels,
+                                                             T* __restrict__ scratch, uint8_t* __restrict__ out) {
+  const int64_t a = blockIdx.x;
+  const T* leaf = leaf_sums + a * n_leaves;
+  T* in = scratch + a * n_internal;
+  for (int lv = 0; lv < n_levels; ++lv) {
+    for (int m = level_off[lv] + int(threadIdx.x); m < level_off[lv + 1]; m += int(blockDim.x)) {
+      const int2 c = nodes[m];
+      const T x = c.x >= 0 ? leaf[c.x] : in[-c.x - 1];
+      const T y = c.y >= 0 ? leaf[c.y] : in[-c.y - 1];
+      in[m] = x + y;
     }
+    __syncthreads();
   }
-  out[a] = __builtin_isfinite(st[0]) ? 1 : 0;
+  if (threadIdx.x == 0) out[a] = __builtin_isfinite(n_internal > 0 ? in[n_internal - 1] : leaf[0]) ? 1 : 0;
 }
 
 template <typename T>
-hipError_t sr_launch_jsum_combine(const T* leaf_sums, int64_t n_arrays, int n_leaves, const int32_t* prog,
-                                  int prog_len, uint8_t* out, hipStream_t s) {
+hipError_t sr_launch_jsum_levels(const T* leaf_sums, int64_t n_arrays, int n_leaves, const int2* nodes, int n_internal,
+                                 const int32_t* level_off, int n_levels, T* scratch, uint8_t* out, hipStream_t s) {
   if (n_arrays <= 0) return hipSuccess;
-  hipLaunchKernelGGL(sr_jsum_combine_kernel<T>, dim3(unsigned((n_arrays + 255) / 256)), dim3(256), 0, s, leaf_sums,
-                     n_arrays, n_leaves, prog, prog_len, out);
+  hipLaunchKernelGGL(sr_jsum_levels_kernel<T>, dim3(unsigned(n_arrays)), dim3(256), 0, s, leaf_sums, n_leaves, nodes,
+                     n_internal, level_off, n_levels, scratch, out);
   return hipGetLastError();
 }
-template hipError_t sr_launch_jsum_combine<float>(const float*, int64_t, int, const int32_t*, int, uint8_t*, hipStream_t);
-template hipError_t sr_launch_jsum_combine<double>(const double*, int64_t, int, const int32_t*, int, uint8_t*, hipStream_t);
+template hipError_t sr_launch_jsum_levels<float>(const float*, int64_t, int, const int2*, int, const int32_t*, int, float*,
+                                                 uint8_t*, hipStream_t);
+template hipError_t sr_launch_jsum_levels<double>(const double*, int64_t, int, const int2*, int, const int32_t*, int,
+                                                  double*, uint8_t*, hipStream_t);
 
 // Packed row-shard partials for one all-reduce (sr_eval_loss_partials_packed): [4][n] f64 = Σ loss,
 // then the NONFINITE / BIG / STATIC flag bits as 0 / 1.

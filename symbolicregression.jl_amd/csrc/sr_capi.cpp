@@ -13,6 +13,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <functional>
 #include <mutex>
 #include <string>
 #include <vector>
@@ -96,7 +97,6 @@ struct HostBuf {
 };
 
 constexpr int kMaxChunks = 4;
-constexpr int kJsumMaxDepth = 48;  // stack of the device-side Julia-sum combine (2^26 rows need 17)
 constexpr int kLossCodeBase = 256;
 
 // Parameter-free losses (and HuberLoss with its default delta = 1) may be passed by kind.
@@ -160,7 +160,7 @@ struct sr_ctx {
   std::vector<int> tiers;
   std::vector<std::pair<int, double>> losses;  // registered (kind, param); code = kLossCodeBase + index
   DevBuf prog, outs, part_sum, part_flag, pred, row_idx, tree_list,
-      range_lo, range_hi, range_sums, packed, hint, jsum_prog, jsum_fin, probe_sum, probe_flag, g_code, g_offsets, g_consts, g_const_off, g_items, g_part, g_out,
+      range_lo, range_hi, range_sums, packed, hint, jsum_prog, jsum_fin, jsum_scratch, probe_sum, probe_flag, g_code, g_offsets, g_consts, g_const_off, g_items, g_part, g_out,
       derived_cols;
   double last_eval_ms = 0.0, last_total_ms = 0.0;
   // host-side phases of the last eval_loss call (ms): compile, upload+launch, wait, exact pass,
@@ -776,19 +776,47 @@ void jl_finite(int64_t n_total, int n_ranks, const int64_t* offs, const T* const
   }
 }
 
-// Base.mapreduce_impl's combine of one view's leaf folds as a post-order program (leaf k: push
-// k; -1: add the top two), shared by every array; the stack it needs in *max_depth (`depth` = the
-// stack size after pushing a leaf at this point).
-void jl_program(int64_t lo, int64_t hi, int32_t* idx, std::vector<int32_t>* prog, int depth, int* max_depth) {
-  if (depth > *max_depth) *max_depth = depth;
-  if (hi - lo < 1024) {
-    prog->push_back((*idx)++);
-    return;
+// Base.mapreduce_impl's combine of one view's leaf folds as a level-ordered node list: internal
+// node m = (left, right) with c >= 0 = leaf c (leaves numbered in row order) and c < 0 = internal
+// node -c-1; nodes are grouped by height (level_off), so every node's children lie in earlier levels.
+struct JlLevels {
+  std::vector<int32_t> nodes;      // 2 per internal node
+  std::vector<int32_t> level_off;  // n_levels + 1
+};
+JlLevels jl_levels(int64_t n) {
+  struct Tmp {
+    int64_t l, r;  // >= 0 leaf, < 0 temporary internal id -x-1
+    int h;
+  };
+  std::vector<Tmp> tmp;
+  int64_t n_leaf = 0;
+  // returns (code, height)
+  std::function<std::pair<int64_t, int>(int64_t, int64_t)> rec = [&](int64_t lo, int64_t hi) -> std::pair<int64_t, int> {
+    if (hi - lo < 1024) return {n_leaf++, 0};
+    const int64_t mid = lo + ((hi - lo) >> 1);
+    const auto L = rec(lo, mid);
+    const auto R = rec(mid + 1, hi);
+    const int h = 1 + std::max(L.second, R.second);
+    tmp.push_back(Tmp{L.first, R.first, h});
+    return {-int64_t(tmp.size()), h};
+  };
+  JlLevels out;
+  if (n > 0) rec(0, n - 1);
+  int max_h = 0;
+  for (const Tmp& t : tmp) max_h = std::max(max_h, t.h);
+  std::vector<int64_t> final_id(tmp.size());
+  out.level_off.assign(size_t(max_h) + 1, 0);
+  for (const Tmp& t : tmp) out.level_off[size_t(t.h)]++;  // counts at heights 1..max_h
+  for (int h = 1; h <= max_h; ++h) out.level_off[size_t(h)] += out.level_off[size_t(h - 1)];
+  std::vector<int64_t> fill(out.level_off.begin(), out.level_off.end() - 1);  // level h-1 starts at level_off[h-1]
+  for (size_t i = 0; i < tmp.size(); ++i) final_id[i] = fill[size_t(tmp[i].h - 1)]++;
+  out.nodes.resize(2 * tmp.size());
+  auto code = [&](int64_t c) -> int32_t { return c >= 0 ? int32_t(c) : int32_t(-final_id[size_t(-c - 1)] - 1); };
+  for (size_t i = 0; i < tmp.size(); ++i) {
+    out.nodes[2 * size_t(final_id[i])] = code(tmp[i].l);
+    out.nodes[2 * size_t(final_id[i]) + 1] = code(tmp[i].r);
   }
-  const int64_t mid = lo + ((hi - lo) >> 1);
-  jl_program(lo, mid, idx, prog, depth, max_depth);          // (the left half starts on the same stack)
-  jl_program(mid + 1, hi, idx, prog, depth + 1, max_depth);  // (above the left half's result)
-  prog->push_back(-1);
+  return out;
 }
 
 // EXACT pass: the Julia-order fold of every checked array of the listed trees over `ranges` of this
@@ -819,15 +847,18 @@ int run_exact(sr_ctx* ctx, const sr_dataset* ds, const SrProgramBatch<T>& prog, 
   SR_HIP_CHECK(ctx->range_hi.ensure(size_t(n_ranges) * sizeof(int64_t)));
   SR_HIP_CHECK(hipMemcpyAsync(ctx->range_lo.p, lo.data(), size_t(n_ranges) * sizeof(int64_t), hipMemcpyHostToDevice, s));
   SR_HIP_CHECK(hipMemcpyAsync(ctx->range_hi.p, hi.data(), size_t(n_ranges) * sizeof(int64_t), hipMemcpyHostToDevice, s));
-  int comb_len = 0, comb_depth = 0;
+  int n_internal = 0, n_levels = 0;
   if (host_finite) {
-    std::vector<int32_t> comb;
-    int32_t idx = 0;
-    jl_program(0, n_eval - 1, &idx, &comb, 1, &comb_depth);
-    if (idx != n_ranges || comb_depth > kJsumMaxDepth) return set_error(SR_ERR_INVALID_ARG, "bad leaf structure");
-    comb_len = int(comb.size());
-    SR_HIP_CHECK(ctx->jsum_prog.ensure(comb.size() * sizeof(int32_t)));
-    SR_HIP_CHECK(hipMemcpyAsync(ctx->jsum_prog.p, comb.data(), comb.size() * sizeof(int32_t), hipMemcpyHostToDevice, s));
+    const JlLevels lv = jl_levels(n_eval);
+    n_internal = int(lv.nodes.size() / 2);
+    n_levels = int(lv.level_off.size()) - 1;
+    if (n_internal != n_ranges - 1 && !(n_ranges == 1 && n_internal == 0))
+      return set_error(SR_ERR_INVALID_ARG, "bad leaf structure");
+    // nodes then level offsets, one upload
+    std::vector<int32_t> buf(lv.nodes);
+    buf.insert(buf.end(), lv.level_off.begin(), lv.level_off.end());
+    SR_HIP_CHECK(ctx->jsum_prog.ensure(buf.size() * sizeof(int32_t)));
+    SR_HIP_CHECK(hipMemcpyAsync(ctx->jsum_prog.p, buf.data(), buf.size() * sizeof(int32_t), hipMemcpyHostToDevice, s));
   }
   // listed trees in batches whose range folds fit a bounded scratch buffer
   const size_t per_tree = size_t(max_checks) * size_t(n_ranges) * sizeof(T);
@@ -878,8 +909,11 @@ int run_exact(sr_ctx* ctx, const sr_dataset* ds, const SrProgramBatch<T>& prog, 
     if (host_finite) {
       const int64_t n_arrays = nb * max_checks;
       SR_HIP_CHECK(ctx->jsum_fin.ensure(size_t(n_arrays) + 16));
-      SR_HIP_CHECK(sr_launch_jsum_combine<T>(static_cast<const T*>(ctx->range_sums.p), n_arrays, int(n_ranges),
-                                             ctx->jsum_prog.as<int32_t>(), comb_len, ctx->jsum_fin.as<uint8_t>(), s));
+      SR_HIP_CHECK(ctx->jsum_scratch.ensure(size_t(std::max<int64_t>(1, n_arrays * n_internal)) * sizeof(T)));
+      const int32_t* lvp = ctx->jsum_prog.as<int32_t>();
+      SR_HIP_CHECK(sr_launch_jsum_levels<T>(static_cast<const T*>(ctx->range_sums.p), n_arrays, int(n_ranges),
+                                            reinterpret_cast<const int2*>(lvp), n_internal, lvp + 2 * n_internal,
+                                            n_levels, ctx->jsum_scratch.as<T>(), ctx->jsum_fin.as<uint8_t>(), s));
       SR_HIP_CHECK(hipMemcpyAsync(host_finite + size_t(b0) * max_checks, ctx->jsum_fin.p, size_t(n_arrays),
                                   hipMemcpyDeviceToHost, s));
     } else {
@@ -1314,7 +1348,7 @@ int sr_shutdown(sr_ctx* ctx) {
     (void)hipSetDevice(ctx->device);
     (void)hipStreamSynchronize(ctx->stream);
     for (DevBuf* b : {&ctx->prog, &ctx->outs, &ctx->part_sum, &ctx->part_flag, &ctx->pred, &ctx->row_idx, &ctx->tree_list, &ctx->range_lo, &ctx->range_hi, &ctx->range_sums, &ctx->packed,
-                      &ctx->hint, &ctx->jsum_prog, &ctx->jsum_fin, &ctx->probe_sum, &ctx->probe_flag, &ctx->g_code, &ctx->g_offsets, &ctx->g_consts, &ctx->g_const_off,
+                      &ctx->hint, &ctx->jsum_prog, &ctx->jsum_fin, &ctx->jsum_scratch, &ctx->probe_sum, &ctx->probe_flag, &ctx->g_code, &ctx->g_offsets, &ctx->g_consts, &ctx->g_const_off,
                       &ctx->g_items, &ctx->g_part, &ctx->g_out, &ctx->derived_cols})
       b->release();
     for (HostBuf* b : {&ctx->h_prog, &ctx->h_outs}) b->release();

@@ -89,8 +89,8 @@ hipError_t sr_launch_reduce(const double* part_sum, const uint32_t* part_flag, i
 // isfinite(Julia pairwise sum) of n_arrays arrays from their leaf folds [n_arrays][n_leaves] (T),
 // combined by the post-order program `prog` (leaf index: push; -1: add the top two).
 template <typename T>
-hipError_t sr_launch_jsum_combine(const T* leaf_sums, int64_t n_arrays, int n_leaves, const int32_t* prog,
-                                  int prog_len, uint8_t* out, hipStream_t s);
+hipError_t sr_launch_jsum_levels(const T* leaf_sums, int64_t n_arrays, int n_leaves, const int2* nodes, int n_internal,
+                                 const int32_t* level_off, int n_levels, T* scratch, uint8_t* out, hipStream_t s);
 hipError_t sr_launch_pack_partials(const double* sum, const uint32_t* flag, int n, double* out, hipStream_t s);
 template <typename T>
 hipError_t sr_launch_transpose(const T* Xh_dev, int64_t nf, int64_t n, int64_t ld, T* Xd, hipStream_t s);

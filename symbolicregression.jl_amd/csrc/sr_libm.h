@@ -4,7 +4,7 @@
 // log kernels work in Float64).  ROCm's OCML Float32 log / cos / sin measured 1.75 / 1.26 / 1.49 ulp
 // on the fixture points of tests/golden/libm_ulp.json (profiles/r02_libm_ocml.txt), so those three
 // are computed here in double and rounded once, table-driven so the work per value stays close to
-// OCML's: log from a 32-cell table of [1, 2) and a degree-8 log1p, cos / sin from (sin, cos)(k pi/16)
+// OCML's: log from a 64-cell table of an offset octave and a degree-6 log1p, cos / sin from (sin, cos)(k pi/16)
 // and degree-7/6 polynomials on |r| <= pi/32.  Every fast-path result is within 2^-38 relative of
 // the exact value before the final rounding (tools/gen_libm_coeffs.py prints the bounds), i.e.
 // correctly rounded unless the exact value sits that close to a midpoint.  OCML's Float32 exp
@@ -84,79 +84,52 @@ SRL_HD inline float sr_expf(float x) {
   return tiny ? 0.0f : v;
 }
 
-// log(x) = e ln2 + logc_k + log1p(m invc_k - 1): x = 2^e m, m in [0.75, 1.5) from the Float32 bits
-// (subnormals scaled by 2^24 first), cell k = the top 5 mantissa bits, |m invc_k - 1| <= 2^-5.
+// log(x) = k ln2 + logc_i + log1p(z invc_i - 1) for x = 2^k z with z's Float32 bits in
+// [0x3f330000, 0x3fb30000) (z ~ [0.699, 1.398): an offset octave, so x just below 1 keeps k = 0 with
+// no branch), cell i = the 6 bits below the offset (64 cells, |z invc_i - 1| <= 2^-7), log1p by
+// Taylor to r^6 (error <= 2^-51.8 absolute, <= 2^-43.8 relative to the result).  Every step but the
+// last rounding is exact or double: the result is within 2^-43 relative before rounding to Float32.
 // The f64 polynomial coefficients come in `c` (the device row function materialises them once per
-// call in scalar registers: 64-bit constants cannot be VOP3 literals, and rematerialising them
-// costs two v_mov per use and row).
+// call in scalar registers: 64-bit constants cannot be VOP3 literals, and rematerialising them costs
+// two v_mov per use and row).
 struct SrLogC {
-  double c8, c7, c6, c5, c4, c3, ln2hi, ln2lo;
+  double c3, c4, c5, c6, ln2;
 };
-constexpr SrLogC kSrLogC = {-0.125, 0x1.2492492492492p-3, -0x1.5555555555555p-3, 0.2, -0.25,
-                            0x1.5555555555555p-2, 0x1.62e42fefa39efp-1, 0x1.abc9e3b39803fp-56};
+constexpr SrLogC kSrLogC = {0x1.5555555555555p-2, -0.25, 0.2, -0x1.5555555555555p-3, 0x1.62e42fefa39efp-1};
+constexpr uint32_t kLogOff = 0x3f330000u;
 
-#if defined(__HIP_DEVICE_COMPILE__)
-#define SRL_OPAQUE(v) asm volatile("" : "+v"(v))
-#else
-#define SRL_OPAQUE(v) (void)0
-#endif
+// positive normal finite x (Float32 bits ix), scaled by 2^-kadj
+SRL_HD inline double sr_log_normal(uint32_t ix, int kadj, const double* tab, const SrLogC& c) {
+  const uint32_t tmp = ix - kLogOff;
+  const uint32_t i = (tmp >> 17) & 63u;
+  const int k = int32_t(tmp) >> 23;
+  const uint32_t iz = ix - (tmp & 0xff800000u);
+  float z;
+  __builtin_memcpy(&z, &iz, 4);
+  const double invc = tab[2 * i], logc = tab[2 * i + 1];
+  const double r = fma(double(z), invc, -1.0);
+  const double r2 = r * r;
+  // log1p(r) = r + r^2 ((-1/2 + r/3) + r^2 ((-1/4 + r/5) - r^2/6))
+  const double a = fma(r, c.c3, -0.5);
+  const double b = fma(r2, c.c6, fma(r, c.c5, c.c4));
+  const double p = fma(r2, b, a);
+  const double y = fma(double(k + kadj), c.ln2, logc) + r;
+  return fma(r2, p, y);
+}
 
+// Base.log over every Float32: +Inf -> +Inf, +-0 -> -Inf, x < 0 or NaN -> NaN; subnormals scaled by
+// 2^23 (exact) first.  (The evaluator's safe_log maps x <= 0 to NaN before calling.)
 SRL_HD inline float sr_logf_core(float x, const double* tab, const SrLogC& c) {
-  uint32_t b;
-#if defined(__HIP_DEVICE_COMPILE__)
-  // the hardware frexp normalises subnormals itself: x = mant 2^ex, mant in [0.5, 1)
-  const float mant = __builtin_amdgcn_frexp_mantf(x);
-  __builtin_memcpy(&b, &mant, 4);
-  const int e = __builtin_amdgcn_frexp_expf(x) - 1;
-#else
-  __builtin_memcpy(&b, &x, 4);
-  const bool sub = b < 0x00800000u;  // zero / subnormal (x >= 0 here)
-  float xs = sub ? x * 0x1p24f : x;
-  __builtin_memcpy(&b, &xs, 4);
-  const int e = int(b >> 23) - 127 - (sub ? 24 : 0);
-#endif
-  const uint32_t k = (b >> 18) & 31u;
-  const bool hi = k >= 16u;  // m in [1.5, 2): use m / 2 and e + 1 (x just below 1 keeps e = 0)
-  const uint32_t mb = (b & 0x007fffffu) | (hi ? 0x3f000000u : 0x3f800000u);
-  float mf;
-  __builtin_memcpy(&mf, &mb, 4);
-  const double invc = tab[2 * k], logc = tab[2 * k + 1];
-  const double r = fma(double(mf), invc, -1.0);
-  // log1p(r) = r - r^2/2 + r^3/3 - ... - r^8/8 (|r| <= 2^-5: error < 2^-43 |r|)
-  double q = fma(r, c.c8, c.c7);  // -1/8 r + 1/7
-  q = fma(r, q, c.c6);            // -1/6
-  q = fma(r, q, c.c5);            // 1/5
-  q = fma(r, q, c.c4);            // -1/4
-  q = fma(r, q, c.c3);            // 1/3
-  q = fma(r, q, -0.5);
-  const double p = fma(r * r, q, r);
-  const double ed = double(hi ? e + 1 : e);
-  const float v = float(fma(ed, c.ln2hi, fma(ed, c.ln2lo, logc + p)));
-  // (+Inf -> +Inf; outside safe_log's domain as Base.log: 0 -> -Inf, x < 0 or NaN -> NaN).  Merged
-  // with an opaque bit mask, so the compiler cannot turn the merge into a divergent branch around
-  // the main path.
-#if defined(__HIP_DEVICE_COMPILE__)
-  // the hardware log2 has exactly these specials (+Inf -> +Inf, +-0 -> -Inf, x < 0 / NaN -> NaN);
-  // class 0x180 = positive normal or subnormal
-  const float special = __builtin_amdgcn_logf(x);
-  uint32_t keep = __builtin_amdgcn_class(x, 0x180) ? 0xffffffffu : 0u;
-#else
-  const float special = x == __builtin_inff() ? x : (x == 0.0f ? -__builtin_inff() : __builtin_nanf(""));
-  uint32_t keep = (x > 0.0f && x != __builtin_inff()) ? 0xffffffffu : 0u;
-#endif
-  SRL_OPAQUE(keep);
-  uint32_t vb, sb;
-  __builtin_memcpy(&vb, &v, 4);
-  __builtin_memcpy(&sb, &special, 4);
-#if defined(__HIP_DEVICE_COMPILE__)
-  uint32_t rb;
-  asm("v_bfi_b32 %0, %1, %2, %3" : "=v"(rb) : "v"(keep), "v"(vb), "v"(sb));
-#else
-  const uint32_t rb = (vb & keep) | (sb & ~keep);
-#endif
-  float out;
-  __builtin_memcpy(&out, &rb, 4);
-  return out;
+  uint32_t ix;
+  __builtin_memcpy(&ix, &x, 4);
+  if (ix - 0x00800000u < 0x7f000000u) return float(sr_log_normal(ix, 0, tab, c));  // positive normal
+  if ((ix & 0x7fffffffu) == 0u) return -__builtin_inff();
+  if (ix > 0x7f800000u) return __builtin_nanf("");  // negative (sign bit set) or NaN
+  if (ix == 0x7f800000u) return x;
+  const float xs = x * 0x1p23f;  // positive subnormal
+  uint32_t is;
+  __builtin_memcpy(&is, &xs, 4);
+  return float(sr_log_normal(is, -23, tab, c));
 }
 SRL_HD inline float sr_logf_tab(float x, const double* tab) { return sr_logf_core(x, tab, kSrLogC); }
 
@@ -171,8 +144,8 @@ __device__ inline double srl_sconst() {
 }
 #define SRL_SCONST(v) srl_sconst<__builtin_bit_cast(uint64_t, double(v))>()
 __device__ inline SrLogC sr_logc_sgpr() {
-  return SrLogC{SRL_SCONST(kSrLogC.c8), SRL_SCONST(kSrLogC.c7), SRL_SCONST(kSrLogC.c6), SRL_SCONST(kSrLogC.c5),
-                SRL_SCONST(kSrLogC.c4), SRL_SCONST(kSrLogC.c3), SRL_SCONST(kSrLogC.ln2hi), SRL_SCONST(kSrLogC.ln2lo)};
+  return SrLogC{SRL_SCONST(kSrLogC.c3), SRL_SCONST(kSrLogC.c4), SRL_SCONST(kSrLogC.c5), SRL_SCONST(kSrLogC.c6),
+                SRL_SCONST(kSrLogC.ln2)};
 }
 #elif defined(__HIPCC__)
 // (host pass of device code: never executed)
@@ -268,13 +241,13 @@ SRL_HD inline float sr_sincosf_full(float x, const double* tab) {
 
 // ---------------------------------------------------------------- tables: host / device
 #if defined(__HIPCC__)
-// per-workgroup LDS copy of the tables (trig then log; 2.5 KiB: it must not cost the interpreter a
+// per-workgroup LDS copy of the tables (trig then log; 3 KiB: it must not cost the interpreter a
 // workgroup per CU)
-static __shared__ __attribute__((aligned(16))) double sr_lds_libm[256 + 64];
+static __shared__ __attribute__((aligned(16))) double sr_lds_libm[256 + 128];
 // Copy the tables into LDS: every thread of the block calls this before the block's first barrier.
 __device__ inline void sr_libm_lds_fill(int tid, int nthreads) {
   for (int i = tid; i < 256; i += nthreads) sr_lds_libm[i] = srl::kTrigTab[i];
-  for (int i = tid; i < 64; i += nthreads) sr_lds_libm[256 + i] = srl::kLogTab[i];
+  for (int i = tid; i < 128; i += nthreads) sr_lds_libm[256 + i] = srl::kLogTab[i];
 }
 #endif
 SRL_HD inline const double* sr_trig_tab() {

@@ -223,15 +223,33 @@ __device__ __attribute__((noinline)) SrRowVec<R> sr_libm_rows(SrRowVec<R> v) {
   }
   return v;
 }
-// Float32 log over the rows, its coefficients in scalar registers for the whole call
+// Float32 log over the rows, its coefficients in scalar registers for the whole call.  When every row
+// of the wave is a positive normal finite value (unsigned bits in [2^23, 0x7f7fffff]: one max and one
+// min per row, one ballot) the rows take the bare reduction + polynomial; otherwise every row takes
+// the full function (same arithmetic for those values, plus zeros, subnormals, Inf, NaN, negatives).
 template <int R>
 __device__ SR_LIBM_CALL SrRowVec<R> sr_log_rows(SrRowVec<R> v) {
   const SrLogC c = sr_logc_sgpr();
   const double* tab = sr_log_tab();
+  uint32_t hi = 0u, lo = 0xffffffffu;
 #pragma unroll
   for (int r = 0; r < R; ++r) {
-    v[r] = sr_logf_core(v[r], tab, c);
-    __builtin_amdgcn_sched_barrier(0);
+    const uint32_t b = __float_as_uint(v[r]);
+    hi = b > hi ? b : hi;
+    lo = b < lo ? b : lo;
+  }
+  if (__builtin_amdgcn_ballot_w64(hi > 0x7f7fffffu || lo < 0x00800000u) == 0) {
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+      v[r] = float(sr_log_normal(__float_as_uint(v[r]), 0, tab, c));
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  } else {
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+      v[r] = sr_logf_core(v[r], tab, c);
+      __builtin_amdgcn_sched_barrier(0);
+    }
   }
   return v;
 }

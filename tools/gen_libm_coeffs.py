@@ -61,34 +61,44 @@ if __name__ == "__main__":
 
 
 def tables():
-    """Tables of csrc/sr_libm.h: sin/cos(k pi/64), k = 0..127; log: for the 32 mantissa cells of
-    [1, 2), invc = 1 / (cell centre) rounded to double and logc = -log(invc) (so that
-    log(m) = logc + log1p(m * invc - 1) holds exactly in real arithmetic); cells of [1.5, 2) serve
-    m/2 (centre halved), cell 0 has centre 1."""
+    """Tables of csrc/sr_libm.h: sin/cos(k pi/64), k = 0..127; log: 64 cells of the offset octave
+    z in [0x3f330000, 0x3fb30000) (Float32 bits; x = 2^k z with z ~ [0.699, 1.398), so no branch
+    between the halves of the octave), cell i = bits [OFF + i 2^17, OFF + (i+1) 2^17):
+    invc = 1 / (cell centre) rounded to double and logc = -log(invc) (so that
+    log(z) = logc + log1p(z * invc - 1) holds exactly in real arithmetic); the cell holding 1
+    (i = 38) has centre 1, so log(1) = 0 exactly.  |z invc - 1| <= 2^-7 in every cell."""
+    import struct
+
+    def f32(bits):
+        return mp.mpf(struct.unpack("<f", struct.pack("<I", bits))[0])
+
     trig = [(float(mp.sin(k * mp.pi / 64)), float(mp.cos(k * mp.pi / 64))) for k in range(128)]
-    logt = []
-    for k in range(32):
-        c = 1 + (mp.mpf(k) + mp.mpf(1) / 2) / 32
-        if k == 0:  # cell [1, 1 + 1/32): centre 1 exactly, so log(1) = 0 exactly
-            c = mp.mpf(1)
-        elif k >= 16:  # m in [1.5, 2) is taken as m/2 in [0.75, 1) with e + 1 (no cancellation near 1-)
-            c = c / 2
+    logt, rmax = [], mp.mpf(0)
+    for i in range(64):
+        lo, hi = f32(LOG_OFF + (i << 17)), f32(LOG_OFF + ((i + 1) << 17))
+        c = mp.mpf(1) if lo <= 1 < hi else (lo + hi) / 2
         invc = float(1 / c)
+        rmax = max(rmax, abs(lo * invc - 1), abs(hi * invc - 1))
         logt.append((invc, float(-mp.log(mp.mpf(invc)))))
-    return trig, logt
+    return trig, logt, rmax
+
+
+LOG_OFF = 0x3F330000
 
 
 def emit_tables():
-    trig, logt = tables()
+    trig, logt, rmax = tables()
     print("constexpr double kTrigTab[256] = {" + ", ".join(float.hex(v) for p in trig for v in p) + "};")
-    print("constexpr double kLogTab[64] = {" + ", ".join(float.hex(v) for p in logt for v in p) + "};")
+    print("constexpr double kLogTab[128] = {" + ", ".join(float.hex(v) for p in logt for v in p) + "};")
     h = mp.pi / 1024  # reduction by 16 n' (pi / 1024) = n' pi / 64: the shifter's low word is 16 n'
     print("pi/1024 split:", [float.hex(float(x)) for x in split(h, 3)], " 1024/pi:", float.hex(float(1024 / mp.pi)))
     # polynomial bounds on |r| <= pi/128 (trig, Taylor to r^5 / r^4) and |r| <= 1/32 (log, to r^7)
     r = mp.pi / 128
     print("trig s rel err:", float(r ** 6 / mp.factorial(7)), " c err:", float(r ** 6 / mp.factorial(6)))
-    r = mp.mpf(1) / 32
-    print("log rel err (deg 7):", float(r ** 7 / 8))
+    # log1p(r) by Taylor to r^6: |error| <= |r|^7 / 7 absolute, relative to |log x| >= |log(0.99609375)|
+    # outside the centre-1 cell and to |r| inside it
+    print("log |r| max:", float(rmax), " abs err:", float(rmax ** 7 / 7),
+          " rel err (worst cell):", float(rmax ** 7 / 7 / abs(mp.log(mp.mpf(0.99609375)))))
 
 
 if __name__ == "__main__" and len(__import__("sys").argv) > 1:
