@@ -210,7 +210,7 @@ hipError_t sr_launch_eval(const SrEvalArgs<T>& a, int mode, bool gather, int tie
     if (mode == SR_MODE_LOSS) {
       if (tier == SR_TIER_BASIC) {
         if (gather) return sr_launch_basic_loss<T, 8, true>(a, n_blocks, s);
-        if (R == 16) return sr_launch_tile<T, 16, SR_MODE_LOSS, false, SR_TIER_BASIC>(a, n_blocks, s);
+        if (R == 16) return sr_launch_basic_loss<T, 16, false>(a, n_blocks, s);
         if (R == 4) return sr_launch_tile<T, 4, SR_MODE_LOSS, false, SR_TIER_BASIC>(a, n_blocks, s);
         if (waves == 8 && a.loss_kind == SR_LOSS_L2)
           return sr_launch_tile<T, 8, SR_MODE_LOSS, false, SR_TIER_BASIC, 8, SR_LOSS_L2>(a, n_blocks, s);

@@ -406,9 +406,10 @@ struct TreeCompiler {
       fail(SR_ERR_TOO_DEEP, "tree needs more operand-stack slots than the encoding holds");
       return;
     }
-    if (in.op >= SR_OP_PAIR0) in.op += SR_P_PUSH;                    // PAIR v -> PAIR v + PUSH
-    else if (in.op == SR_OP_LOAD_DERIVED) in.op = SR_OP_LOAD_DERIVED_PUSH;
-    else in.op += SR_OP_LOAD_FEAT_PUSH - SR_OP_LOAD_FEAT;            // LOAD_x -> LOAD_x_PUSH
+    const uint32_t base = in.op & SR_OP_MASK;  // (a fused POST unary sits above the opcode)
+    if (base >= SR_OP_PAIR0) in.op += SR_P_PUSH;                     // PAIR v -> PAIR v + PUSH
+    else if (base == SR_OP_LOAD_DERIVED) in.op += SR_OP_LOAD_DERIVED_PUSH - SR_OP_LOAD_DERIVED;
+    else in.op += SR_OP_LOAD_FEAT_PUSH - SR_OP_LOAD_FEAT;             // LOAD_x -> LOAD_x_PUSH
     in.meta |= uint32_t(slot + 1) << SR_M_PUSH_SHIFT;
   }
 
@@ -471,6 +472,17 @@ struct TreeCompiler {
         return;
       }
       emit(t.l[i]);
+      // the child's code ends with the instruction computing it: the unary rides on it as its POST
+      // operator (one dispatch for both), unless that instruction carries one already; gradient
+      // programs keep the plain form (their kernel has no post operators)
+      if (!with_const_index && !code.empty() && (code.back().op >> SR_OP_POST_SHIFT) == 0u) {
+        code.back().op |= (unary_id(i) << SR_OP_POST_SHIFT) | (infsub[i] ? SR_OP_POST_INF : 0u);
+        if (arr_check[i]) {
+          code.back().op |= SR_OP_POST_CHECK;
+          ++n_checks;
+        }
+        return;
+      }
       SrIns<T> in{};
       // fused unary: non-finite input -> +Inf
       in.op = (infsub[i] ? SR_OP_UNARY_INF0 : SR_OP_UNARY0) + unary_id(i);
@@ -559,8 +571,22 @@ struct TreeCompiler {
 
 }  // namespace
 
+static uint32_t sr_unary_cost(uint32_t u) {
+  switch (u) {
+    case SR_U_NEG: case SR_U_SQUARE: case SR_U_CUBE: case SR_U_ABS: return 2;
+    case SR_U_EXP: return 9;
+    case SR_U_LOG: return 16;
+    case SR_U_SQRT: return 8;
+    case SR_U_COS: case SR_U_SIN: return 32;
+    default: return 30;
+  }
+}
+
 uint32_t sr_instruction_cost(uint32_t code) {
+  const uint32_t post = (code >> SR_OP_POST_SHIFT) & 0x3fu;
   uint32_t c = 6;  // dispatch + operand fetch + validity tracking
+  if (post) c += 2 + sr_unary_cost(post) + ((code & SR_OP_POST_INF) ? 2u : 0u);
+  code &= SR_OP_MASK;
   if (code == SR_OP_LOAD_FEAT_PUSH || code == SR_OP_LOAD_CONST_PUSH || code == SR_OP_LOAD_DERIVED_PUSH) c += 2;
   if (code == SR_OP_LOAD_DERIVED || code == SR_OP_LOAD_DERIVED_PUSH) return c + 3;
   if (code >= SR_OP_PAIR0) {
@@ -575,14 +601,7 @@ uint32_t sr_instruction_cost(uint32_t code) {
   } else if (code > SR_OP_UNARY0) {
     const uint32_t u = code >= SR_OP_UNARY_INF0 ? code - SR_OP_UNARY_INF0 : code - SR_OP_UNARY0;
     if (code >= SR_OP_UNARY_INF0) c += 2;
-    switch (u) {
-      case SR_U_NEG: case SR_U_SQUARE: case SR_U_CUBE: case SR_U_ABS: c += 2; break;
-      case SR_U_EXP: c += 9; break;
-      case SR_U_LOG: c += 16; break;
-      case SR_U_SQRT: c += 8; break;
-      case SR_U_COS: case SR_U_SIN: c += 32; break;
-      default: c += 30; break;
-    }
+    c += sr_unary_cost(u);
   } else {
     c += 1;
   }

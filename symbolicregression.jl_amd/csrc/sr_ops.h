@@ -100,6 +100,11 @@ SR_HD inline bool sr_loss_propagates_nan(int32_t kind) {
 //                             node unary(feature), shared by many trees of a population)
 //   c0 (, c1) : constant bits (C variants, LOAD_CONST*): f32 in c0, f64 in c0 | c1 << 32
 //   (word order in memory: op, meta, c0, c1)
+//   op bits  0-8    : the opcode (below 512)
+//   op bits 16-21   : POST  unary operator applied to tos after the opcode (0 = none): a unary node
+//                     fused into the instruction computing its child (one dispatch for both)
+//   op bit  22      : POST_INF  the post unary is DynamicExpressions' fused form (non-finite -> +Inf)
+//   op bit  23      : POST_CHECK  the post unary's output array is validity-checked
 //   meta bits  0-15 : operand index: feature f (F variants, LOAD_FEAT*), stack slot k (S variants),
 //                     pre-order constant slot of a constant leaf (gradient programs; else 0)
 //   meta bits 24-29 : push slot + 1 (LOAD_*_PUSH)
@@ -116,6 +121,7 @@ enum : uint32_t {
   SR_OP_PAIR0 = 256u,      // opcode = SR_OP_PAIR0 + 6*(SrBinaryOp-1) + pair variant
   SR_V_SL = 0u, SR_V_SR = 1u, SR_V_FL = 2u, SR_V_FR = 3u, SR_V_CL = 4u, SR_V_CR = 5u,
   SR_P_FF = 0u, SR_P_FC = 1u, SR_P_CF = 2u, SR_P_PUSH = 3u,
+  SR_OP_MASK = 0x1ffu, SR_OP_POST_SHIFT = 16u, SR_OP_POST_INF = 1u << 22, SR_OP_POST_CHECK = 1u << 23,
   SR_M_INDEX = 0xffffu, SR_M_PUSH_SHIFT = 24u, SR_M_PUSH_MASK = 0x3fu << 24, SR_M_CHECK = 1u << 31,
   SR_MAX_STACK_SLOTS = 62u,
 };
@@ -123,6 +129,8 @@ static_assert(SR_OP_UNARY0 + SR_U_COUNT <= SR_OP_UNARY_INF0, "unary opcode range
 static_assert(SR_OP_UNARY_INF0 + SR_U_COUNT <= SR_OP_LOAD_DERIVED, "unary opcode range overlaps LOAD_DERIVED");
 static_assert(SR_OP_LOAD_DERIVED_PUSH < SR_OP_BINARY0, "LOAD_DERIVED overlaps the binary range");
 static_assert(SR_OP_BINARY0 + 6 * SR_B_COUNT <= SR_OP_PAIR0, "binary opcode range overlaps the pair range");
+static_assert(SR_OP_PAIR0 + 6 * SR_B_COUNT <= SR_OP_MASK + 1, "opcodes must fit the op word's low 9 bits");
+static_assert(SR_U_COUNT <= 64, "post-unary ids must fit 6 bits");
 #define SR_BIN_OPC(b, v) (SR_OP_BINARY0 + 6u * ((b) - 1u) + (v))
 #define SR_PAIR_OPC(b, v) (SR_OP_PAIR0 + 6u * ((b) - 1u) + (v))
 

@@ -46,7 +46,7 @@ struct SrMinWaves {
 #define SR_MIN_WAVES_W4 5
 #endif
 #ifndef SR_MIN_WAVES_R16
-#define SR_MIN_WAVES_R16 4
+#define SR_MIN_WAVES_R16 2
 #endif
 #ifndef SR_MIN_WAVES_VSTK16
 #define SR_MIN_WAVES_VSTK16 4
@@ -206,6 +206,13 @@ __device__ __forceinline__ P* sr_row_at(P* base, uint32_t meta) {
 // The double-precision Float32 libm (log / cos / sin, sr_libm.h) over a lane's R rows, as a real
 // call: its polynomial constants and f64 temporaries live in the callee's own registers instead of
 // being hoisted out of the interpreter loop and spilled, and each body exists once per kernel.
+// Rows per scheduling group inside the libm row callees: a sched_barrier after every group keeps
+// the callee's live registers to that many rows' temporaries (1 = row by row).
+#ifndef SR_LIBM_ILP
+#define SR_LIBM_ILP 1
+#endif
+#define SR_LIBM_ROW_END(r) \
+  if (((r) + 1) % SR_LIBM_ILP == 0) __builtin_amdgcn_sched_barrier(0)
 template <int R>
 using SrRowVec = float __attribute__((ext_vector_type(R)));
 #ifdef SR_LIBM_INLINE
@@ -242,7 +249,7 @@ __device__ SR_LIBM_CALL SrRowVec<R> sr_log_rows(SrRowVec<R> v) {
 #pragma unroll
     for (int r = 0; r < R; ++r) {
       v[r] = float(sr_log_normal(__float_as_uint(v[r]), 0, tab, c));
-      __builtin_amdgcn_sched_barrier(0);
+      SR_LIBM_ROW_END(r);
     }
   } else {
 #pragma unroll
@@ -260,7 +267,7 @@ __device__ SR_LIBM_CALL SrRowVec<R> sr_trig_rows_fast(SrRowVec<R> v) {
 #pragma unroll
   for (int r = 0; r < R; ++r) {
     v[r] = (ID == SR_U_COS) ? sr_cosf_fast(v[r]) : sr_sinf_fast(v[r]);
-    __builtin_amdgcn_sched_barrier(0);
+    SR_LIBM_ROW_END(r);
   }
   return v;
 }
@@ -381,6 +388,50 @@ __device__ __forceinline__ void sr_unary_rows(T (&v)[R]) {
     for (int r = 0; r < R; ++r) v[r] = sr_unary<T>(ID, v[r]);
   }
 }
+
+// A unary operator fused into the instruction computing its child (the POST field of the op word):
+// the same row bodies as the UNARY opcodes; INF = DynamicExpressions' fused form (non-finite input ->
+// +Inf), which only the per-node-check kernels distinguish (under deferred checks the input is a
+// tracked operator output, so a non-finite input already decides the tree).
+#define SR_POST_CASE(ID) \
+  case ID:               \
+    sr_unary_rows<T, ID, R>(tos); \
+    break;
+template <typename T, int R, int TIER, bool FAST>
+__device__ __forceinline__ void sr_post_unary(uint32_t u, bool inf, T (&tos)[R]) {
+  uint32_t nonfin = 0u;
+  if constexpr (!FAST) {
+    if (inf) {
+#pragma unroll
+      for (int r = 0; r < R; ++r) nonfin |= sr_isfinite(tos[r]) ? 0u : (1u << r);
+    }
+  }
+  switch (u) {
+    SR_POST_CASE(SR_U_NEG) SR_POST_CASE(SR_U_SQUARE) SR_POST_CASE(SR_U_CUBE) SR_POST_CASE(SR_U_EXP)
+    SR_POST_CASE(SR_U_COS) SR_POST_CASE(SR_U_SIN) SR_POST_CASE(SR_U_LOG) SR_POST_CASE(SR_U_SQRT)
+    SR_POST_CASE(SR_U_ABS)
+    default:
+      if constexpr (TIER == SR_TIER_FULL) {
+        switch (u) {
+          SR_POST_CASE(SR_U_TAN) SR_POST_CASE(SR_U_LOG2) SR_POST_CASE(SR_U_LOG10) SR_POST_CASE(SR_U_LOG1P)
+          SR_POST_CASE(SR_U_SIGN) SR_POST_CASE(SR_U_TANH) SR_POST_CASE(SR_U_SINH) SR_POST_CASE(SR_U_COSH)
+          SR_POST_CASE(SR_U_ATAN) SR_POST_CASE(SR_U_ASIN) SR_POST_CASE(SR_U_ACOS) SR_POST_CASE(SR_U_ACOSH)
+          SR_POST_CASE(SR_U_ATANH) SR_POST_CASE(SR_U_ASINH) SR_POST_CASE(SR_U_RELU) SR_POST_CASE(SR_U_INV)
+          SR_POST_CASE(SR_U_ERF) SR_POST_CASE(SR_U_ERFC) SR_POST_CASE(SR_U_GAMMA) SR_POST_CASE(SR_U_ROUND)
+          SR_POST_CASE(SR_U_FLOOR) SR_POST_CASE(SR_U_CEIL) SR_POST_CASE(SR_U_EXP2) SR_POST_CASE(SR_U_EXPM1)
+          default: break;
+        }
+      }
+      break;
+  }
+  if constexpr (!FAST) {
+    if (inf) {
+#pragma unroll
+      for (int r = 0; r < R; ++r) tos[r] = ((nonfin >> r) & 1u) ? sr_inf<T>() : tos[r];
+    }
+  }
+}
+#undef SR_POST_CASE
 
 // ------------------------------------------------------------------ dispatch cases
 #define SR_EACH(EXPR)                             \
@@ -790,7 +841,7 @@ __global__ void __launch_bounds__(W * 64, (SrMinWavesFor<T, R, TIER, W, VSTK>::v
   } else {                                                                                   \
     L::store(sr_row_at<ROWS>(stk_lane, ((SR_META() >> SR_M_PUSH_SHIFT) & 0x3fu) - 1u), tos); \
   }
-          switch (op) {
+          switch (op & SR_OP_MASK) {
             case SR_OP_LOAD_FEAT_PUSH:
               SR_PUSH_TOS();
               [[fallthrough]];
@@ -860,29 +911,40 @@ __global__ void __launch_bounds__(W * 64, (SrMinWavesFor<T, R, TIER, W, VSTK>::v
           }
 #undef SR_CVAL
 #undef SR_PUSH_TOS
+          // DynamicExpressions' check of a node's output array (per node: FULL tier, PRED, EXACT)
+#define SR_CHECK_NODE()                                                                                      \
+  if (MODE == SR_MODE_EXACT) {                                                                               \
+    /* the checked array's rows of this tile, in row order, for the Julia-order fold below */                \
+    if (check_k < MC) L::store(chk + (size_t(wave) * MC + check_k) * ROWS + lane * C, tos);                  \
+    ++check_k;                                                                                               \
+  } else {                                                                                                   \
+    /* |v| >= tbig (or NaN / Inf) in any row: one integer max per lane + one ballot; padded rows */          \
+    /* replicate row 0 of the view, so no row mask is needed here */                                         \
+    uint32_t m = SrBits<T>::mag(tos[0]);                                                                     \
+    _Pragma("unroll") for (int r = 1; r < R; ++r) m = max(m, SrBits<T>::mag(tos[r]));                       \
+    if (sr_ballot(m >= thr)) {                                                                               \
+      susp_any = true;                                                                                       \
+      bool nonfin = false;                                                                                   \
+      _Pragma("unroll") for (int r = 0; r < R; ++r) nonfin |= !sr_isfinite(tos[r]);                         \
+      if (sr_ballot(nonfin)) {                                                                               \
+        dead = true;                                                                                         \
+        k = SR_WIN;                                                                                          \
+      }                                                                                                      \
+    }                                                                                                        \
+  }
           if (!FAST_CHECK && (SR_META() & SR_M_CHECK)) {
-            if (MODE == SR_MODE_EXACT) {
-              // the checked array's rows of this tile, in row order, for the Julia-order fold below
-              if (check_k < MC) L::store(chk + (size_t(wave) * MC + check_k) * ROWS + lane * C, tos);
-              ++check_k;
-            } else {
-              // |v| >= tbig (or NaN / Inf) in any row: one integer max per lane + one ballot;
-              // padded rows replicate row 0 of the view, so no row mask is needed here
-              uint32_t m = SrBits<T>::mag(tos[0]);
-#pragma unroll
-              for (int r = 1; r < R; ++r) m = max(m, SrBits<T>::mag(tos[r]));
-              if (sr_ballot(m >= thr)) {
-                susp_any = true;
-                bool nonfin = false;
-#pragma unroll
-                for (int r = 0; r < R; ++r) nonfin |= !sr_isfinite(tos[r]);
-                if (sr_ballot(nonfin)) {
-                  dead = true;
-                  k = SR_WIN;
-                }
-              }
+            SR_CHECK_NODE();
+          }
+          // the POST unary fused into this instruction (the node whose child it computed)
+          const uint32_t post = (op >> SR_OP_POST_SHIFT) & 0x3fu;
+          if (post != 0u && !dead) {
+            sr_post_unary<T, R, TIER, FAST_CHECK>(post, (op & SR_OP_POST_INF) != 0u, tos);
+            SR_TRACK();
+            if (!FAST_CHECK && (op & SR_OP_POST_CHECK)) {
+              SR_CHECK_NODE();
             }
           }
+#undef SR_CHECK_NODE
         }
       }
 

@@ -79,6 +79,7 @@ def _binary(bid, a, b):
 LOAD_FEAT, LOAD_CONST, LOAD_FEAT_PUSH, LOAD_CONST_PUSH = 0, 1, 2, 3
 UNARY0, UNARY_INF0, BINARY0, PAIR0 = 4, 40, 80, 256
 CHECK = 1 << 31
+OP_MASK, POST_SHIFT, POST_INF, POST_CHECK = 0x1FF, 16, 1 << 22, 1 << 23
 
 
 def operand(meta):
@@ -104,8 +105,13 @@ def run_program(code, lo, hi, X, T):
     slots = {}
     complete = True
     big = T(np.finfo(T).max)
+    def checked(v):  # isfinite(sum(array)) (f64 sum)
+        s = np.sum(v.astype(np.float64))
+        return np.isfinite(v).all() and abs(s) <= float(big)
+
     for pc in range(lo, hi):
-        opc = int(code["op"][pc])
+        word = int(code["op"][pc])
+        opc = word & OP_MASK
         meta = int(code["meta"][pc])
         val = T(code["val"][pc])
         if opc < UNARY0:  # LOAD_FEAT / LOAD_CONST, the _PUSH forms storing the old tos first
@@ -148,9 +154,15 @@ def run_program(code, lo, hi, X, T):
                 o = np.full(n, val, dtype=T)
             a, b = (o, tos) if v in (0, 2, 4) else (tos, o)
             tos = _binary(bid, a, b).astype(T)
-        if is_check(meta):  # isfinite(sum(array)) (f64 sum)
-            s = np.sum(tos.astype(np.float64))
-            if not np.isfinite(tos).all() or not abs(s) <= float(big):
+        if is_check(meta) and not checked(tos):
+            complete = False
+        post = (word >> POST_SHIFT) & 0x3F  # a unary node fused into this instruction
+        if post:
+            v = _unary(post, tos, T).astype(T)
+            if word & POST_INF:  # fused form: non-finite input -> +Inf
+                v = np.where(np.isfinite(tos), v, T(np.inf)).astype(T)
+            tos = v
+            if (word & POST_CHECK) and not checked(tos):
                 complete = False
     return tos, complete
 

@@ -49,7 +49,7 @@ def test_program_shapes():
         "x1": 1,                          # LOAD
         "x1 * 3.0": 1,                    # PAIR MUL FC
         "cos(3.0 * 2.0)": 1,              # folded constant tree
-        "cos(x1) + cos(x2)": 5,           # LOAD,COS, LOAD+PUSH,COS, ADD stack
+        "cos(x1) + cos(x2)": 3,           # LOAD+cos, LOAD+PUSH+cos, ADD stack (unaries fused as POST)
         "(x1 * 2.0) * (3.0 * 4.0)": 2,    # PAIR, then the folded right child as constant operand
     }
     trees = [parse_expression(e, opts) for e in cases]
@@ -61,18 +61,26 @@ def test_program_shapes():
     k = list(cases).index("cos(x1) + cos(x2)")
     ops = [int(v) for v in code["op"][offs[k]:offs[k + 1]]]
     meta = [int(v) for v in code["meta"][offs[k]:offs[k + 1]]]
-    assert [vm.is_check(m) for m in meta] == [1, 1, 1, 1, 1]
-    # LOAD x1, COS, LOAD_PUSH x2 (cos(x1) to slot 0), COS, ADD with slot 0 (commuted: R variant)
-    assert ops == [0, 4 + 5, 2, 4 + 5, 80 + 1]
-    assert [vm.push_slot(m) for m in meta] == [-1, -1, 0, -1, -1]
-    assert vm.operand(meta[4]) == 0 and vm.operand(meta[2]) == 1
-    # fused unary: cos(x1 * 2.0) -> PAIR MUL FC, INF-COS; no CHECK on the inner product
+    assert [vm.is_check(m) for m in meta] == [1, 1, 1]
+    # LOAD x1 + POST cos, LOAD_PUSH x2 (cos(x1) to slot 0) + POST cos, ADD with slot 0 (commuted: R
+    # variant); each cos output is checked (child of a general binary): POST_CHECK
+    post_cos = (5 << vm.POST_SHIFT) | vm.POST_CHECK
+    assert ops == [0 | post_cos, 2 | post_cos, 80 + 1]
+    assert [vm.push_slot(m) for m in meta] == [-1, 0, -1]
+    assert vm.operand(meta[2]) == 0 and vm.operand(meta[1]) == 1
+    # fused unary: cos(x1 * 2.0) -> PAIR MUL FC with POST INF-cos (the root: POST_CHECK); no CHECK on
+    # the inner product
     tb2 = flatten_trees([parse_expression("cos(x1 * 2.0)", opts)], np.float32)
     code2, offs2, _, depth2 = vm.compile_info(opts, tb2, 100, 5, np.float32)
     ops2 = [int(v) for v in code2["op"][:offs2[1]]]
     meta2 = [int(v) for v in code2["meta"][:offs2[1]]]
-    assert ops2 == [256 + 6 * 2 + 1, 40 + 5]
-    assert [vm.is_check(m) for m in meta2] == [0, 1]
+    assert ops2 == [(256 + 6 * 2 + 1) | (5 << vm.POST_SHIFT) | vm.POST_INF | vm.POST_CHECK]
+    assert [vm.is_check(m) for m in meta2] == [0]
+    # a unary of a unary: the inner one rides on the LOAD, the outer one is its own instruction
+    tb5 = flatten_trees([parse_expression("exp(cos(x1))", opts)], np.float32)
+    code5, offs5, _, _ = vm.compile_info(opts, tb5, 100, 5, np.float32)
+    assert [int(v) & vm.OP_MASK for v in code5["op"][:offs5[1]]] == [0, 40 + 4]  # (DE fused form: INF-exp)
+    assert (int(code5["op"][0]) >> vm.POST_SHIFT) & 0x3F == 5
     assert depth2 == 0  # the fused unary needs no stack slot
     # non-commutative stack operand keeps its side: (x1 - cos(x2)) - exp(x3) style trees
     tb3 = flatten_trees([parse_expression("cos(x1) - exp(x2)", opts)], np.float32)

@@ -1,7 +1,8 @@
 #!/bin/bash
-# Operator-mix microbenchmark under each listed library ("-" = the in-tree lib/libsr_amd.so, else
-# ab/<name>/libsr_amd.so built by tools/ab_lib.sh), alternating A/B twice.
-# usage: bash tools/ab_libs.sh "mixes" - base ...
+# Operator-mix microbenchmark under each listed variant, alternating A/B twice.  A variant is
+# "<lib>[+ENV=VAL...]": <lib> "-" = the in-tree lib/libsr_amd.so, else ab/<lib>/libsr_amd.so built
+# by tools/ab_lib.sh; the ENV settings apply to that run.
+# usage: bash tools/ab_libs.sh "mixes" - base -+SR_AMD_ROWS_PER_LANE=16 ...
 set -o pipefail
 cd $GRAFT_REPO_ROOT
 mkdir -p gpurun_out
@@ -9,12 +10,11 @@ mixes=$1; shift
 : > gpurun_out/ab_libs.txt
 for pass in 1 2; do
   for v in "$@"; do
+    IFS='+' read -r lib envs <<< "$v"
+    e="${envs//+/ }"
+    [ "$lib" = "-" ] || e="SR_AMD_LIB=ab/$lib/libsr_amd.so $e"
     echo "== $v (pass $pass)" >> gpurun_out/ab_libs.txt
-    if [ "$v" = "-" ]; then
-      timeout -k 10 300 python3 -u tools/microbench.py $mixes >> gpurun_out/ab_libs.txt 2>&1 || exit $?
-    else
-      SR_AMD_LIB=ab/$v/libsr_amd.so timeout -k 10 300 python3 -u tools/microbench.py $mixes >> gpurun_out/ab_libs.txt 2>&1 || exit $?
-    fi
+    env $e timeout -k 10 300 python3 -u tools/microbench.py $mixes >> gpurun_out/ab_libs.txt 2>&1 || exit $?
   done
 done
 cat gpurun_out/ab_libs.txt
