@@ -190,6 +190,7 @@ def main():
     n_launch = int(round(float(np.mean(state["launches"][-args.steps:])))) if state["launches"] else 1
     flops_per_step = float(n_local) * (ops + 3 * nt)  # this GPU's interpreter work per step
     traffic = measured_traffic(args.workload)
+    rpl = ctx.last_rows_per_lane()  # the interpreter build the library picked for this view
     frac_complete = float(np.mean(np.asarray(comp).astype(bool)))
 
     extra = {}
@@ -239,12 +240,13 @@ def main():
                 flops_per_step, kmean, PEAK_FP32_TFLOPS,
                 traffic=traffic.get("hbm_read_bytes_per_step") if traffic else None,
                 traffic_source=traffic.get("source") if traffic else None,
-                kernel="sr_tile_kernel<float,8,LOSS,gather=false,BASIC,W=4,L2>",
+                kernel=(f"sr_tile_kernel<float,{rpl},LOSS,gather=false,BASIC,W=4,L2"
+                        + (",register stack>" if rpl >= 16 else ">")),
                 launches_per_step=n_launch,
                 kernel_ms_convention=("per step: sum of the interpreter launches' HIP-event durations on the "
                                       "library's streams (= the kernel-trace sum: overlapping chunks count fully)"),
                 flop_convention="n_rows * sum_t(n_op(t) + 3), 1 flop per operator incl. transcendentals (SURVEY 8d)",
-                algorithmic_bytes_per_step=algorithmic_bytes(nt, n_local, n_launch),
+                algorithmic_bytes_per_step=algorithmic_bytes(nt, n_local, n_launch, rpl),
                 bytes_convention="ceil(n_trees/G) passes x (nf+1) x n_rows x 4 B; X/y re-reads are served from L2/MALL",
             ),
             "cpu_baseline": cpu,
@@ -290,15 +292,15 @@ def extra_lines(ctx, opts, trees, comp, X, y, args):
     return out
 
 
-def algorithmic_bytes(nt, rows, n_launch):
-    n_passes = sum(-(-c // g) for c, g in chunk_groups(nt, rows, n_launch))
+def algorithmic_bytes(nt, rows, n_launch, rows_per_lane=8):
+    n_passes = sum(-(-c // g) for c, g in chunk_groups(nt, rows, n_launch, rows_per_lane))
     return float(n_passes) * (5 + 1) * float(rows) * 4.0
 
 
-def chunk_groups(nt, rows, n_launch):
+def chunk_groups(nt, rows, n_launch, rows_per_lane=8):
     """(trees, trees per workgroup) of each interpreter launch of a step, as csrc/sr_capi.cpp's
     run_batch / make_grid split them (2 launches: a first chunk of nt/6 trees)."""
-    tiles = -(-rows // 512)
+    tiles = -(-rows // (64 * rows_per_lane))
     n_rb = -(-tiles // (-(-tiles // 256)))
     bounds = [0, nt // 6, nt] if n_launch == 2 else [nt * k // n_launch for k in range(n_launch + 1)]
     out = []

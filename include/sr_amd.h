@@ -332,7 +332,8 @@ int sr_last_kernel_ms(sr_ctx* ctx, double* eval_ms, double* total_ms);
 /* Host-side phases of the last sr_eval_loss_batch call (ms, wall clock), up to n of: compile,
  * upload + launch, wait for the interpreter + reduction, exact-sum pass, finalize; out[5] (n >= 6)
  * = the number of interpreter launches of the call (the batch is compiled and launched in chunks),
- * out[6] (n >= 7) = device time of the exact-sum pass (ms).
+ * out[6] (n >= 7) = device time of the exact-sum pass (ms), out[7] (n >= 8) = rows per lane of its
+ * interpreter kernel.
  * sr_last_kernel_ms's eval_ms is the sum of those launches' durations. */
 int sr_last_phase_ms(sr_ctx* ctx, double* out, int n);
 

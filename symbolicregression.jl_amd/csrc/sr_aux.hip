@@ -187,14 +187,15 @@ hipError_t sr_launch_basic_loss(const SrEvalArgs<T>& a, int n_blocks, hipStream_
 }
 
 // Register-stack kernels (f32 BASIC loss over the full dataset, operand stack in VGPRs): rows per
-// lane for a view of n rows, or 0 when the classic LDS-stack kernel should run.  Larger tiles
-// amortise the per-instruction dispatch over more rows; below a few tiles the
-// padding and the loss of parallelism cost more.  requested: SR_AMD_ROWS_PER_LANE (16 / 32 force a
-// register-stack kernel, 4 / 8 the classic one).
+// lane for a view of n rows, or 0 when the classic LDS-stack kernel should run.  Larger tiles halve
+// the per-tree epilogues and dispatches per row and, with no LDS stack, keep the workgroup's LDS at
+// the X tile (C2 kernel -5 %, its complete trees -12 %, arithmetic-only -18 %); below
+// 2^17 rows the padding and the loss of parallelism cost more.  requested: SR_AMD_ROWS_PER_LANE
+// (16 / 32 force a register-stack kernel, 4 / 8 the classic one).
 int sr_vstk_rows(int64_t n_rows, int requested) {
   if (requested == 16 || requested == 32) return requested;
-  (void)n_rows;  // off by default: see DESIGN.md §4 (register pressure of the two VGPR slots)
-  return 0;
+  if (requested == 4 || requested == 8) return 0;
+  return n_rows >= (int64_t(1) << 17) ? 16 : 0;
 }
 
 template <typename T>

@@ -179,6 +179,7 @@ struct sr_ctx {
   int cu_count = 256;
   int rows_override = 0;    // SR_AMD_ROWS_PER_LANE (tuning): 4 selects the f32 BASIC 4-rows/lane kernel
   int tree_group = 0;       // SR_AMD_TREES_PER_BLOCK override (0 = heuristic)
+  int rows_last = 0;        // rows per lane of the last interpreter call (sr_last_phase_ms out[7])
   int waves_override = 0;   // SR_AMD_WAVES (tuning): 8 selects the 8-wave f32 BASIC L2 loss kernel
   bool cost_order = true;   // launch trees in decreasing estimated cost (SR_AMD_NO_SORT=1 disables)
   bool dead_hints = true;   // share dead-tree hints across row blocks (SR_AMD_NO_HINT=1 disables)
@@ -358,6 +359,7 @@ int run_batch(sr_ctx* ctx, const sr_dataset* ds, int opset_id, const sr_tree_bat
   const int Rv = (sizeof(T) == 4 && mode == SR_MODE_LOSS && tier == SR_TIER_BASIC && !gather)
                      ? sr_vstk_rows(n_eval, ctx->rows_override)
                      : 0;
+  ctx->rows_last = Rv > 0 ? Rv : R;  // (every C2-like tree fits the register stack)
   hipStream_t s = ctx->stream;
   // error exits while chunks are in flight: no DMA may still read the staging buffers
   auto sync_both = [&] {
@@ -1719,6 +1721,7 @@ int sr_last_phase_ms(sr_ctx* ctx, double* out, int n) {
   for (int i = 0; i < n && i < 5; ++i) out[i] = ctx->phase_ms[i];
   if (n > 5) out[5] = double(ctx->n_chunks_last);
   if (n > 6) out[6] = ctx->exact_kernel_ms;
+  if (n > 7) out[7] = double(ctx->rows_last);
   return SR_OK;
 }
 

@@ -702,6 +702,10 @@ __global__ void __launch_bounds__(W * 64, (SrMinWavesFor<T, R, TIER, W, VSTK>::v
   if (gcount > G) gcount = G;
   const bool weighted = a.w != nullptr;
   const uint32_t thr = SrBits<T>::mag(a.tbig);
+  // tbig held in a register for the whole kernel: left as a kernel argument, the per-tree epilogue
+  // re-reads it with a scalar load and a full lgkmcnt wait under the kernel's SGPR pressure
+  T tbig = a.tbig;
+  asm volatile("" : "+v"(tbig));
   const int lk = LK >= 0 ? LK : a.loss_kind;
 
   // this wave's slots
@@ -1020,7 +1024,7 @@ __global__ void __launch_bounds__(W * 64, (SrMinWavesFor<T, R, TIER, W, VSTK>::v
               }
               if (sr_ballot(nan_root || !(mrun <= SrM<T>::big))) {
                 dead = true;
-              } else if (sr_ballot(!(mrun < a.tbig))) {
+              } else if (sr_ballot(!(mrun < tbig))) {
                 susp_any = true;
               }
             }

@@ -83,6 +83,12 @@ class DeviceContext:
         _lib.check(_lib.lib.sr_last_phase_ms(self.handle, out, 7))
         return float(out[6])
 
+    def last_rows_per_lane(self):
+        """Rows per lane of the last call's interpreter kernel (8 or 16 for f32 BASIC loss)."""
+        out = (ctypes.c_double * 8)()
+        _lib.check(_lib.lib.sr_last_phase_ms(self.handle, out, 8))
+        return int(out[7])
+
     def last_launches(self):
         """Interpreter launches of the last eval_loss call (chunked compile/launch pipeline)."""
         out = (ctypes.c_double * 6)()

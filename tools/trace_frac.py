@@ -4,7 +4,7 @@
 
 Reads OUTDIR/kt/kt_kernel_trace.csv and OUTDIR/bench_traced.json (the bench line printed by the
 traced run).  The interpreter launches of the C2 step are the f32 BASIC loss kernel
-(sr_tile_kernel<float, 8, 0, ...>, probes included: the bench's HIP events bracket them too); the
+(sr_tile_kernel<float, R, 0, ...> with the bench line's R, probes included: the bench's HIP events bracket them too); the
 last steps x launches_per_step of them are the timed region.  Prints the per-step kernel time and
 roofline fraction from the trace next to the bench's own (HIP-event) values, and, when the PMC pass
 ran, the HBM bytes per step from FETCH_SIZE (x 1024 B/KiB x 2, the gfx950 correction of
@@ -21,7 +21,9 @@ def main(out):
     rf = line["roofline"]
     steps, per_step = line["steps"], rf["launches_per_step"]
     rows = list(csv.DictReader(open(glob.glob(os.path.join(out, "kt", "*kernel_trace.csv"))[0])))
-    interp = [r for r in rows if r["Kernel_Name"].startswith("void sr_tile_kernel<float, 8, 0,")]
+    rpl = rf["kernel"].split("<float,")[1].split(",")[0]  # rows per lane of the build the bench ran
+    prefix = f"void sr_tile_kernel<float, {rpl}, 0,"
+    interp = [r for r in rows if r["Kernel_Name"].startswith(prefix)]
     interp.sort(key=lambda r: int(r["Start_Timestamp"]))
     # probes: each step after the first chunk adds one probe launch (same kernel, tiny grid)
     probes_per_step = 1 if per_step == 2 else 0
@@ -40,14 +42,14 @@ def main(out):
     if pm:
         fetch = {}
         for r in csv.DictReader(open(pm[0])):
-            if r.get("Counter_Name") == "FETCH_SIZE" and r["Kernel_Name"].startswith("void sr_tile_kernel<float, 8, 0,"):
+            if r.get("Counter_Name") == "FETCH_SIZE" and r["Kernel_Name"].startswith(prefix):
                 fetch[r["Dispatch_Id"]] = fetch.get(r["Dispatch_Id"], 0.0) + float(r["Counter_Value"])
         vals = [fetch[d] for d in sorted(fetch, key=int)][-k:]
         if vals:
             per_step_bytes = sum(vals) * 1024 * 2 / steps
             print(f"HBM (FETCH_SIZE)   : {per_step_bytes / 1e6:.1f} MB/step over the timed launches "
                   f"(algorithmic {rf['algorithmic_bytes_per_step'] / 1e6:.1f} MB)")
-            json.dump({"workload": "c2", "kernel": "sr_tile_kernel<float, 8, 0, ...> (probes included)",
+            json.dump({"workload": "c2", "kernel": f"sr_tile_kernel<float, {rpl}, 0, ...> (probes included)",
                        "profiled_steps": steps, "launches": len(vals),
                        "hbm_read_bytes_per_step": per_step_bytes,
                        "source_cmd": "tools/bench_evidence.sh"},
