@@ -191,8 +191,12 @@ hipError_t sr_launch_basic_loss(const SrEvalArgs<T>& a, int n_blocks, hipStream_
 // the per-tree epilogues and dispatches per row and, with no LDS stack, keep the workgroup's LDS at
 // the X tile (C2 kernel -5 %, its complete trees -12 %, arithmetic-only -18 %); below
 // 2^17 rows the padding and the loss of parallelism cost more.  requested: SR_AMD_ROWS_PER_LANE
-// (16 / 32 force a register-stack kernel, 4 / 8 the classic one).
-int sr_vstk_rows(int64_t n_rows, int requested) {
+// (16 / 32 force a register-stack kernel, 4 / 8 the classic one; f64: 8 selects its register-stack
+// build).
+int sr_vstk_rows(int elem_size, int64_t n_rows, int requested) {
+  // f64: the 8-rows/lane register-stack build needs 181 VGPRs (2 waves per SIMD) and measured no
+  // better than the classic 4-rows/lane build at 100 (5 waves): only on request (tuning)
+  if (elem_size == 8) return requested == 8 ? 8 : 0;
   if (requested == 16 || requested == 32) return requested;
   if (requested == 4 || requested == 8) return 0;
   return n_rows >= (int64_t(1) << 17) ? 16 : 0;
@@ -226,9 +230,11 @@ hipError_t sr_launch_eval(const SrEvalArgs<T>& a, int mode, bool gather, int tie
     return gather ? sr_launch_tile<T, 4, SR_MODE_EXACT, true, SR_TIER_FULL, 1>(a, n_blocks, s)
                   : sr_launch_tile<T, 4, SR_MODE_EXACT, false, SR_TIER_FULL, 1>(a, n_blocks, s);
   } else {
-    (void)R;
     (void)waves;
-    if (vstk) return hipErrorInvalidValue;
+    if (vstk) {
+      if (mode != SR_MODE_LOSS || tier != SR_TIER_BASIC || gather || R != 8) return hipErrorInvalidValue;
+      return sr_launch_basic_loss<T, 8, false, true>(a, n_blocks, s);
+    }
     if (mode == SR_MODE_LOSS) {
       if (tier == SR_TIER_BASIC)
         return gather ? sr_launch_basic_loss<T, 4, true>(a, n_blocks, s) : sr_launch_basic_loss<T, 4, false>(a, n_blocks, s);

@@ -356,8 +356,8 @@ int run_batch(sr_ctx* ctx, const sr_dataset* ds, int opset_id, const sr_tree_bat
   // register-stack kernel (f32 BASIC loss over the full dataset): Rv rows per lane, used for every
   // chunk whose programs need <= 2 operand-stack slots (all trees of <= 30 nodes); other chunks run
   // the LDS-stack kernel at R rows per lane
-  const int Rv = (sizeof(T) == 4 && mode == SR_MODE_LOSS && tier == SR_TIER_BASIC && !gather)
-                     ? sr_vstk_rows(n_eval, ctx->rows_override)
+  const int Rv = (mode == SR_MODE_LOSS && tier == SR_TIER_BASIC && !gather)
+                     ? sr_vstk_rows(int(sizeof(T)), n_eval, ctx->rows_override)
                      : 0;
   ctx->rows_last = Rv > 0 ? Rv : R;  // (every C2-like tree fits the register stack)
   hipStream_t s = ctx->stream;
@@ -639,18 +639,21 @@ int run_batch(sr_ctx* ctx, const sr_dataset* ds, int opset_id, const sr_tree_bat
         // workgroups skip them from their first tile (without the probe, the ~16 row blocks that
         // start together evaluate every such tree in full before a hint exists).  Only hints come
         // out of it: a tree non-finite on some rows of the view is incomplete on the whole view.
-        // a wide, short grid: 16 trees x 1 tile per workgroup, kProbeTiles row blocks
+        // a wide, short grid: 16 trees x 1 tile per workgroup, kProbeTiles row blocks; always the
+        // classic kernel at R rows per lane (a register-stack launch's 2x longer tiles would double the
+        // probe's work for the same verdicts: C2's dead trees 0.88 -> 0.6x ms)
         SrEvalArgs<T> pa = a;
+        pa.stack_depth = depth;
         pa.out_sum = nullptr;
         pa.out_flag = nullptr;
         pa.trees_per_block = std::max(16, g.W);
         pa.n_groups = int((np + pa.trees_per_block - 1) / pa.trees_per_block);
         pa.tiles_per_block = 1;
         pa.n_row_blocks = kProbeTiles;
-        pa.n_rows = std::min<int64_t>(n_eval, int64_t(kProbeTiles) * 64 * Rc);
+        pa.n_rows = std::min<int64_t>(n_eval, int64_t(kProbeTiles) * 64 * R);
         pa.part_sum = ctx->probe_sum.as<double>();
         pa.part_flag = ctx->probe_flag.as<uint32_t>();
-        SR_HIP_CHECK(sr_launch_eval<T>(pa, mode, gather, tier, Rc, g.W, vstk, pa.n_groups * kProbeTiles, cs));
+        SR_HIP_CHECK(sr_launch_eval<T>(pa, mode, gather, tier, R, W, false, pa.n_groups * kProbeTiles, cs));
       }
       SR_HIP_CHECK(sr_launch_eval<T>(a, mode, gather, tier, Rc, g.W, vstk, int(g.n_blocks), cs));
       if (!direct)

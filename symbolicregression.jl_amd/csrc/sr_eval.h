@@ -66,7 +66,7 @@ int sr_waves_per_block(int elem_size, int mode, int tier, int rows_per_lane, int
 template <typename T>
 int sr_rows_per_lane(int mode, int tier, int requested);
 // Rows per lane of the register-stack f32 BASIC loss kernel for n rows (0: use the LDS-stack kernel).
-int sr_vstk_rows(int64_t n_rows, int requested);
+int sr_vstk_rows(int elem_size, int64_t n_rows, int requested);
 // Runtime dispatch over the instantiated kernels: R rows per lane (sr_rows_per_lane, or
 // sr_vstk_rows with vstk = true: operand stack in VGPRs, programs of <= 2 stack slots).
 template <typename T>

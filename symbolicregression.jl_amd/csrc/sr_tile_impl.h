@@ -51,13 +51,18 @@ struct SrMinWaves {
 #ifndef SR_MIN_WAVES_VSTK16
 #define SR_MIN_WAVES_VSTK16 4
 #endif
+#ifndef SR_MIN_WAVES_VSTK_F64
+#define SR_MIN_WAVES_VSTK_F64 2
+#endif
 #ifndef SR_MIN_WAVES_VSTK32
 #define SR_MIN_WAVES_VSTK32 3
 #endif
 template <typename T, int R, int TIER, int W, bool VSTK = false>
 struct SrMinWavesFor {
   static constexpr bool f32_basic = sizeof(T) == 4 && TIER == SR_TIER_BASIC && W == 4;
-  static constexpr int value = (f32_basic && VSTK && R == 16)   ? SR_MIN_WAVES_VSTK16
+  static constexpr bool f64_basic = sizeof(T) == 8 && TIER == SR_TIER_BASIC && W == 4;
+  static constexpr int value = (f64_basic && VSTK)               ? SR_MIN_WAVES_VSTK_F64
+                               : (f32_basic && VSTK && R == 16)   ? SR_MIN_WAVES_VSTK16
                                : (f32_basic && VSTK && R == 32) ? SR_MIN_WAVES_VSTK32
                                : (f32_basic && R == 8)          ? SR_MIN_WAVES_W4
                                : (f32_basic && R == 16)         ? SR_MIN_WAVES_R16
@@ -230,6 +235,19 @@ __device__ __attribute__((noinline)) SrRowVec<R> sr_libm_rows(SrRowVec<R> v) {
   }
   return v;
 }
+// Float64 transcendentals (OCML) over the rows, as a real call: inlined into the interpreter's
+// switch their temporaries set the kernel's VGPR count (143 at 4 rows per lane: 3 waves per SIMD).
+template <uint32_t ID, int R>
+using SrRowVecD = double __attribute__((ext_vector_type(R)));
+template <uint32_t ID, int R>
+__device__ __attribute__((noinline)) SrRowVecD<ID, R> sr_libm_rows_f64(SrRowVecD<ID, R> v) {
+#pragma unroll
+  for (int r = 0; r < R; ++r) {
+    v[r] = sr_unary<double>(ID, v[r]);
+    __builtin_amdgcn_sched_barrier(0);
+  }
+  return v;
+}
 // Float32 log over the rows, its coefficients in scalar registers for the whole call.  When every row
 // of the wave is a positive normal finite value (unsigned bits in [2^23, 0x7f7fffff]: one max and one
 // min per row, one ballot) the rows take the bare reduction + polynomial; otherwise every row takes
@@ -381,6 +399,13 @@ __device__ __forceinline__ void sr_unary_rows(T (&v)[R]) {
       x = sr_trig_rows_fast<ID, R>(x);
     else
       x = sr_libm_rows<ID, R>(x);
+#pragma unroll
+    for (int r = 0; r < R; ++r) v[r] = x[r];
+  } else if constexpr (sizeof(T) == 8 && (ID == SR_U_EXP || ID == SR_U_LOG || ID == SR_U_COS || ID == SR_U_SIN)) {
+    SrRowVecD<ID, R> x;
+#pragma unroll
+    for (int r = 0; r < R; ++r) x[r] = v[r];
+    x = sr_libm_rows_f64<ID, R>(x);
 #pragma unroll
     for (int r = 0; r < R; ++r) v[r] = x[r];
   } else {
