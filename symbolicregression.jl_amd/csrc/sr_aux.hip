@@ -193,13 +193,16 @@ hipError_t sr_launch_basic_loss(const SrEvalArgs<T>& a, int n_blocks, hipStream_
 // 2^17 rows the padding and the loss of parallelism cost more.  requested: SR_AMD_ROWS_PER_LANE
 // (16 / 32 force a register-stack kernel, 4 / 8 the classic one; f64: 8 selects its register-stack
 // build).
+#ifndef SR_VSTK_DEFAULT_ROWS
+#define SR_VSTK_DEFAULT_ROWS 16
+#endif
 int sr_vstk_rows(int elem_size, int64_t n_rows, int requested) {
   // f64: the 8-rows/lane register-stack build needs 181 VGPRs (2 waves per SIMD) and measured no
   // better than the classic 4-rows/lane build at 100 (5 waves): only on request (tuning)
   if (elem_size == 8) return requested == 8 ? 8 : 0;
   if (requested == 16 || requested == 32) return requested;
   if (requested == 4 || requested == 8) return 0;
-  return n_rows >= (int64_t(1) << 17) ? 16 : 0;
+  return n_rows >= (int64_t(1) << 17) ? SR_VSTK_DEFAULT_ROWS : 0;
 }
 
 template <typename T>
@@ -210,6 +213,7 @@ hipError_t sr_launch_eval(const SrEvalArgs<T>& a, int mode, bool gather, int tie
       if (mode != SR_MODE_LOSS || tier != SR_TIER_BASIC || gather) return hipErrorInvalidValue;
       if (R == 32) return sr_launch_basic_loss<T, 32, false, true>(a, n_blocks, s);
       if (R == 16) return sr_launch_basic_loss<T, 16, false, true>(a, n_blocks, s);
+      if (R == 8) return sr_launch_basic_loss<T, 8, false, true>(a, n_blocks, s);
       return hipErrorInvalidValue;
     }
     if (mode == SR_MODE_LOSS) {

@@ -51,6 +51,9 @@ struct SrMinWaves {
 #ifndef SR_MIN_WAVES_VSTK16
 #define SR_MIN_WAVES_VSTK16 4
 #endif
+#ifndef SR_MIN_WAVES_VSTK8
+#define SR_MIN_WAVES_VSTK8 6
+#endif
 #ifndef SR_MIN_WAVES_VSTK_F64
 #define SR_MIN_WAVES_VSTK_F64 2
 #endif
@@ -62,6 +65,7 @@ struct SrMinWavesFor {
   static constexpr bool f32_basic = sizeof(T) == 4 && TIER == SR_TIER_BASIC && W == 4;
   static constexpr bool f64_basic = sizeof(T) == 8 && TIER == SR_TIER_BASIC && W == 4;
   static constexpr int value = (f64_basic && VSTK)               ? SR_MIN_WAVES_VSTK_F64
+                               : (f32_basic && VSTK && R == 8)    ? SR_MIN_WAVES_VSTK8
                                : (f32_basic && VSTK && R == 16)   ? SR_MIN_WAVES_VSTK16
                                : (f32_basic && VSTK && R == 32) ? SR_MIN_WAVES_VSTK32
                                : (f32_basic && R == 8)          ? SR_MIN_WAVES_W4
