@@ -13,6 +13,7 @@ import csv
 import glob
 import json
 import os
+import re
 import sys
 
 
@@ -22,10 +23,13 @@ def main(out):
     steps, per_step = line["steps"], rf["launches_per_step"]
     rows = list(csv.DictReader(open(glob.glob(os.path.join(out, "kt", "*kernel_trace.csv"))[0])))
     rpl = rf["kernel"].split("<float,")[1].split(",")[0]  # rows per lane of the build the bench ran
+    # every f32 BASIC-tier LOSS launch (mode 0, no gather, tier 0, 4 waves): the bench's build and the
+    # dead-tree probe, which runs on the classic 8-rows/lane build whatever the main launches use
+    pat = re.compile(r"void sr_tile_kernel<float, \d+, 0, false, 0, 4, ")
     prefix = f"void sr_tile_kernel<float, {rpl}, 0,"
-    interp = [r for r in rows if r["Kernel_Name"].startswith(prefix)]
+    interp = [r for r in rows if pat.match(r["Kernel_Name"])]
     interp.sort(key=lambda r: int(r["Start_Timestamp"]))
-    # probes: each step after the first chunk adds one probe launch (same kernel, tiny grid)
+    # probes: each step after the first chunk adds one probe launch (small grid)
     probes_per_step = 1 if per_step == 2 else 0
     k = steps * (per_step + probes_per_step)
     timed = interp[-k:]
@@ -42,14 +46,14 @@ def main(out):
     if pm:
         fetch = {}
         for r in csv.DictReader(open(pm[0])):
-            if r.get("Counter_Name") == "FETCH_SIZE" and r["Kernel_Name"].startswith(prefix):
+            if r.get("Counter_Name") == "FETCH_SIZE" and pat.match(r["Kernel_Name"]):
                 fetch[r["Dispatch_Id"]] = fetch.get(r["Dispatch_Id"], 0.0) + float(r["Counter_Value"])
         vals = [fetch[d] for d in sorted(fetch, key=int)][-k:]
         if vals:
             per_step_bytes = sum(vals) * 1024 * 2 / steps
             print(f"HBM (FETCH_SIZE)   : {per_step_bytes / 1e6:.1f} MB/step over the timed launches "
                   f"(algorithmic {rf['algorithmic_bytes_per_step'] / 1e6:.1f} MB)")
-            json.dump({"workload": "c2", "kernel": f"sr_tile_kernel<float, {rpl}, 0, ...> (probes included)",
+            json.dump({"workload": "c2", "kernel": f"sr_tile_kernel<float, {rpl}, 0, ...> + the probe launches",
                        "profiled_steps": steps, "launches": len(vals),
                        "hbm_read_bytes_per_step": per_step_bytes,
                        "source_cmd": "tools/bench_evidence.sh"},
