@@ -161,7 +161,8 @@ struct sr_ctx {
   std::vector<std::pair<int, double>> losses;  // registered (kind, param); code = kLossCodeBase + index
   DevBuf prog, outs, part_sum, part_flag, pred, row_idx, tree_list,
       range_lo, range_hi, range_sums, packed, hint, jsum_prog, jsum_fin, jsum_scratch, probe_sum, probe_flag, g_code, g_offsets, g_consts, g_const_off, g_items, g_part, g_out,
-      derived_cols;
+      derived_cols, probe_derived;
+  int stress_probe = 1;     // SR_AMD_STRESS_PROBE: the probe runs the dataset's stress rows (below)
   double last_eval_ms = 0.0, last_total_ms = 0.0;
   // host-side phases of the last eval_loss call (ms): compile, upload+launch, wait, exact pass,
   // finalize (sr_last_phase_ms)
@@ -201,11 +202,17 @@ struct sr_dataset {
   std::vector<double> w_host;  // weights (for Σw of SubDataset views)
   double wsum = 0.0;
   double max_abs_x = 0.0;  // max |X| over the data (NaN / Inf if any value is non-finite)
+  // dead-tree probe rows (large datasets): the "stress rows" — per feature the K largest, K smallest
+  // and K smallest-magnitude values, where exp overflows, logs and divisions blow up — then rows 0, 1,
+  // ... up to kProbeRows; int64 row indices on the device (NULL for small datasets)
+  void* probe_rows = nullptr;
+  int64_t n_probe = 0;
 };
 
 namespace {
 
 constexpr int64_t kRowAlign = 2048;  // a multiple of every kernel's row tile (64 lanes x R rows)
+constexpr int64_t kProbeRows = 2048;  // the dead-tree probe's rows: 4 tiles of the classic f32 build
 
 // Work decomposition: row tiles of 64*R rows (one LDS image each), `tiles` per block; trees grouped G
 // per block (the block's 4 waves share the G trees of a tile).
@@ -473,12 +480,12 @@ int run_batch(sr_ctx* ctx, const sr_dataset* ds, int opset_id, const sr_tree_bat
   // every unary(feature) node of a transcendental shared by several trees is evaluated once for the
   // call.  Chosen from a sample of the batch; not when the data itself needs tracked feature loads.
   std::vector<int16_t> dmap;
+  SrDerivedSpec spec{};
   const int64_t dld = (n_eval + kRowAlign - 1) / kRowAlign * kRowAlign;
   // (single-view calls only: row-sharded partials number their checked arrays identically on every
   // rank, and a rank's choice of columns depends on its shard)
   if (allow_derived && ctx->derived && mode == SR_MODE_LOSS && tier == SR_TIER_BASIC && n_eval >= kDerivedMinRows && nt >= 64 &&
       ds->max_abs_x < double(T(t_max<T>() / (2.0 * double(n_total > 0 ? n_total : 1))))) {  // (track_x off)
-    SrDerivedSpec spec{};
     choose_derived(*trees, ctx->opsets[opset_id], ds->nf, &spec, &dmap);
     if (spec.n > 0) {
       SR_HIP_CHECK(ctx->derived_cols.ensure(size_t(spec.n) * size_t(dld) * sizeof(T)));
@@ -491,6 +498,14 @@ int run_batch(sr_ctx* ctx, const sr_dataset* ds, int opset_id, const sr_tree_bat
     } else {
       dmap.clear();
     }
+  }
+  // the probe over the dataset's stress rows (full views only: a gathered view's rows are its own);
+  // its LOAD_DERIVED nodes read columns computed over those rows
+  const bool stress_probe = use_probe && !gather && ds->probe_rows != nullptr && ctx->stress_probe;
+  if (stress_probe && !dmap.empty()) {
+    SR_HIP_CHECK(ctx->probe_derived.ensure(size_t(spec.n) * size_t(kProbeRows) * sizeof(T)));
+    SR_HIP_CHECK(sr_launch_derived<T>(static_cast<const T*>(ds->X), ds->ld, static_cast<const int64_t*>(ds->probe_rows),
+                                      ds->n_probe, kProbeRows, spec, ctx->probe_derived.as<T>(), kProbeRows, s));
   }
   if (n_chunks > 1) {  // odd chunks run on the second stream, after the shared setup above
     SR_HIP_CHECK(hipEventRecord(ctx->ev_join, s));
@@ -653,7 +668,15 @@ int run_batch(sr_ctx* ctx, const sr_dataset* ds, int opset_id, const sr_tree_bat
         pa.n_rows = std::min<int64_t>(n_eval, int64_t(kProbeTiles) * 64 * R);
         pa.part_sum = ctx->probe_sum.as<double>();
         pa.part_flag = ctx->probe_flag.as<uint32_t>();
-        SR_HIP_CHECK(sr_launch_eval<T>(pa, mode, gather, tier, R, W, false, pa.n_groups * kProbeTiles, cs));
+        if (stress_probe) {  // the stress rows first (sr_dataset::probe_rows), through the gather build
+          pa.row_idx = static_cast<const int64_t*>(ds->probe_rows);
+          pa.n_rows = std::min<int64_t>(ds->n_probe, int64_t(kProbeTiles) * 64 * R);
+          if (!dmap.empty()) {
+            pa.derived = ctx->probe_derived.as<T>();
+            pa.dld = kProbeRows;
+          }
+        }
+        SR_HIP_CHECK(sr_launch_eval<T>(pa, mode, gather || stress_probe, tier, R, W, false, pa.n_groups * kProbeTiles, cs));
       }
       SR_HIP_CHECK(sr_launch_eval<T>(a, mode, gather, tier, Rc, g.W, vstk, int(g.n_blocks), cs));
       if (!direct)
@@ -1079,6 +1102,35 @@ int eval_pred_impl(sr_ctx* ctx, const sr_dataset* ds, int opset_id, const sr_tre
   return SR_OK;
 }
 
+// The dead-tree probe's rows (sr_dataset::probe_rows): a tree that is non-finite on some row of the
+// data is incomplete, and random trees go non-finite first on extreme inputs (exp of the largest
+// values, division by and log of the values nearest zero), so those rows lead the probe.  X is
+// Julia's column-major [nf, n] on the host.
+template <typename T>
+std::vector<int64_t> stress_rows(const T* X, int64_t nf, int64_t n) {
+  const int64_t K = std::max<int64_t>(1, std::min<int64_t>(100, (kProbeRows * 3 / 4) / (3 * std::max<int64_t>(nf, 1))));
+  std::vector<int64_t> pick;
+  std::vector<int64_t> idx(static_cast<size_t>(n));
+  for (int64_t f = 0; f < nf; ++f) {
+    auto val = [&](int64_t i) { return double(X[size_t(i) * size_t(nf) + size_t(f)]); };
+    auto mag = [&](int64_t i) { return std::fabs(val(i)); };
+    auto take = [&](auto less) {
+      for (int64_t i = 0; i < n; ++i) idx[size_t(i)] = i;
+      std::nth_element(idx.begin(), idx.begin() + K, idx.end(), less);
+      pick.insert(pick.end(), idx.begin(), idx.begin() + K);
+    };
+    // (NaN values order arbitrarily here; any row is a valid probe row)
+    take([&](int64_t a, int64_t b) { return val(a) > val(b); });
+    take([&](int64_t a, int64_t b) { return val(a) < val(b); });
+    take([&](int64_t a, int64_t b) { return mag(a) < mag(b); });
+  }
+  std::sort(pick.begin(), pick.end());
+  pick.erase(std::unique(pick.begin(), pick.end()), pick.end());
+  if (int64_t(pick.size()) > kProbeRows) pick.resize(size_t(kProbeRows));
+  for (int64_t i = 0; int64_t(pick.size()) < kProbeRows && i < n; ++i) pick.push_back(i);
+  return pick;
+}
+
 template <typename T>
 int upload_impl(sr_ctx* ctx, const void* X, int64_t nf, int64_t n, const void* y, const void* w, sr_dataset** out) {
   auto* ds = new sr_dataset();
@@ -1092,6 +1144,7 @@ int upload_impl(sr_ctx* ctx, const void* X, int64_t nf, int64_t n, const void* y
     if (ds->X) (void)hipFree(ds->X);
     if (ds->y) (void)hipFree(ds->y);
     if (ds->w) (void)hipFree(ds->w);
+    if (ds->probe_rows) (void)hipFree(ds->probe_rows);
     delete ds;
     return set_error(SR_ERR_HIP, std::string(what) + ": " + hipGetErrorString(e));
   };
@@ -1140,6 +1193,13 @@ int upload_impl(sr_ctx* ctx, const void* X, int64_t nf, int64_t n, const void* y
     if ((e = hipMalloc(&ds->w, size_t(ds->ld) * sizeof(T))) != hipSuccess) return fail(e, "hipMalloc w");
     if ((e = hipMemcpyAsync(ds->w, w, size_t(n) * sizeof(T), hipMemcpyHostToDevice, s)) != hipSuccess) return fail(e, "copy w");
     if ((e = sr_launch_pad<T>(static_cast<T*>(ds->w), n, ds->ld, T(0), 0, s)) != hipSuccess) return fail(e, "pad w");
+  }
+  if (n >= 4 * kProbeRows) {
+    const std::vector<int64_t> rows = stress_rows<T>(static_cast<const T*>(X), nf, n);
+    if ((e = hipMalloc(&ds->probe_rows, rows.size() * sizeof(int64_t))) != hipSuccess) return fail(e, "hipMalloc probe rows");
+    if ((e = hipMemcpy(ds->probe_rows, rows.data(), rows.size() * sizeof(int64_t), hipMemcpyHostToDevice)) != hipSuccess)
+      return fail(e, "copy probe rows");
+    ds->n_probe = int64_t(rows.size());
   }
   if ((e = hipStreamSynchronize(s)) != hipSuccess) return fail(e, "sync");
   *out = ds;
@@ -1320,6 +1380,7 @@ int sr_init(int device, sr_ctx** out) {
   if (const char* v = std::getenv("SR_AMD_NO_HINT")) ctx->dead_hints = std::atoi(v) == 0;
   if (const char* v = std::getenv("SR_AMD_CHUNKS")) ctx->chunks = std::atoi(v);
   if (const char* v = std::getenv("SR_AMD_PROBE")) ctx->probe = std::atoi(v);
+  if (const char* v = std::getenv("SR_AMD_STRESS_PROBE")) ctx->stress_probe = std::atoi(v);
   if (const char* v = std::getenv("SR_AMD_HOST_IO")) ctx->host_io = std::atoi(v);
   if (const char* v = std::getenv("SR_AMD_SPIN")) ctx->spin = std::atoi(v);
   if (const char* v = std::getenv("SR_AMD_EXACT_G")) ctx->exact_g = std::atoi(v);
@@ -1354,7 +1415,7 @@ int sr_shutdown(sr_ctx* ctx) {
     (void)hipStreamSynchronize(ctx->stream);
     for (DevBuf* b : {&ctx->prog, &ctx->outs, &ctx->part_sum, &ctx->part_flag, &ctx->pred, &ctx->row_idx, &ctx->tree_list, &ctx->range_lo, &ctx->range_hi, &ctx->range_sums, &ctx->packed,
                       &ctx->hint, &ctx->jsum_prog, &ctx->jsum_fin, &ctx->jsum_scratch, &ctx->probe_sum, &ctx->probe_flag, &ctx->g_code, &ctx->g_offsets, &ctx->g_consts, &ctx->g_const_off,
-                      &ctx->g_items, &ctx->g_part, &ctx->g_out, &ctx->derived_cols})
+                      &ctx->g_items, &ctx->g_part, &ctx->g_out, &ctx->derived_cols, &ctx->probe_derived})
       b->release();
     for (HostBuf* b : {&ctx->h_prog, &ctx->h_outs}) b->release();
     for (int c = 0; c < kMaxChunks; ++c) {
@@ -1438,6 +1499,7 @@ int sr_dataset_free(sr_dataset* ds) {
     if (ds->X) (void)hipFree(ds->X);
     if (ds->y) (void)hipFree(ds->y);
     if (ds->w) (void)hipFree(ds->w);
+    if (ds->probe_rows) (void)hipFree(ds->probe_rows);
   }
   delete ds;
   return SR_OK;
@@ -1734,6 +1796,14 @@ int sr_set_tuning(sr_ctx* ctx, const char* name, int64_t value) {
   Lock l(ctx);
   if (std::strcmp(name, "derived") == 0) {
     ctx->derived = value != 0 ? 1 : 0;
+    return SR_OK;
+  }
+  if (std::strcmp(name, "probe") == 0) {  // dead-tree probe mode (SR_AMD_PROBE)
+    ctx->probe = int(value);
+    return SR_OK;
+  }
+  if (std::strcmp(name, "stress_probe") == 0) {  // the probe over the stress rows (SR_AMD_STRESS_PROBE)
+    ctx->stress_probe = value != 0 ? 1 : 0;
     return SR_OK;
   }
   return set_error(SR_ERR_INVALID_ARG, std::string("unknown tuning knob '") + name + "'");

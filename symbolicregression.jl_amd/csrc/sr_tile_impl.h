@@ -772,11 +772,33 @@ __global__ void __launch_bounds__(W * 64, (SrMinWavesFor<T, R, TIER, W, VSTK>::v
     // ---- stage the tile: X rows of every feature, y, w (a plain copy; padded rows replicate
     // row 0 of the view, so every program sees finite, in-range data there)
     if (MODE == SR_MODE_EXACT) {
-      // a range starts anywhere: element-wise loads; rows past the range replicate its first row
-      for (int i = tid; i < ROWS; i += SR_BLOCK) {
+      // a range starts anywhere: element-wise loads; rows past the range replicate its first row.
+      // The thread's rows' sources first, then the loads of up to 4 features at a time, all in
+      // flight before the LDS stores (one memory latency per 4 features, not one per element)
+      constexpr int PER = (ROWS + SR_BLOCK - 1) / SR_BLOCK;
+      int64_t src[PER];
+#pragma unroll
+      for (int q = 0; q < PER; ++q) {
+        const int i = tid + q * SR_BLOCK;
         const int64_t v = (i < n_valid) ? row0 + i : rlo;
-        const int64_t src = GATHER ? a.row_idx[v] : v;
-        for (int f = 0; f < a.nf; ++f) xs[f * ROWS + i] = a.X[int64_t(f) * a.ld + src];
+        src[q] = (i < ROWS) ? (GATHER ? a.row_idx[v] : v) : rlo;
+      }
+      for (int f0 = 0; f0 < a.nf; f0 += 4) {
+        T v[4][PER];
+#pragma unroll
+        for (int df = 0; df < 4; ++df) {
+          const int f = f0 + df < a.nf ? f0 + df : f0;
+#pragma unroll
+          for (int q = 0; q < PER; ++q) v[df][q] = a.X[int64_t(f) * a.ld + src[q]];
+        }
+#pragma unroll
+        for (int df = 0; df < 4; ++df) {
+#pragma unroll
+          for (int q = 0; q < PER; ++q) {
+            const int i = tid + q * SR_BLOCK;
+            if (f0 + df < a.nf && i < ROWS) xs[(f0 + df) * ROWS + i] = v[df][q];
+          }
+        }
       }
     } else if (!GATHER) {
       constexpr int CPR = ROWS / C;  // 16-byte chunks per feature row

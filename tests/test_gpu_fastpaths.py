@@ -154,3 +154,40 @@ def test_derived_columns_change_nothing(dtype, batching):
     assert 0.1 < c1.mean() < 0.9
     assert np.array_equal(np.asarray(l1)[c1].view(np.uint64 if dtype == np.float64 else np.uint32),
                           np.asarray(l0)[c0].view(np.uint64 if dtype == np.float64 else np.uint32))
+
+
+@pytest.mark.parametrize("dtype", [np.float32, np.float64])
+def test_probe_modes_change_nothing(dtype):
+    """The dead-tree probe only sets hints: with no probe, the first-rows probe, the stress-row probe
+    (extreme and nearest-zero rows of each feature, through the gather build and derived columns
+    computed over those rows) and a probe before every chunk, losses and flags are identical bit for
+    bit.  The data holds rare overflow rows past the first tiles, so the stress rows find trees the
+    first rows do not."""
+    import sr_amd
+    from sr_amd import Dataset, eval_loss_batch, flatten_trees, gen_random_population
+
+    rng = np.random.default_rng(12)
+    n = 1 << 18
+    X = rng.standard_normal((5, n)).astype(dtype)
+    X[1, 200_001] = dtype(95.0)   # exp overflows on one row far from the first tiles
+    X[3, 150_003] = dtype(0.0)    # division by zero on one row
+    y = (2 * np.cos(X[3]) + X[0] ** 2 - 2).astype(dtype)
+    ds = Dataset(X, y)
+    opts = Options(binary_operators=["+", "-", "*", "/"], unary_operators=["cos", "exp", "log"])
+    tb = flatten_trees(gen_random_population(4000, opts, 5, seed=6), dtype)
+    ctx = sr_amd.get_context()
+    res = []
+    try:
+        for probe, stress in ((0, 0), (2, 0), (2, 1), (1, 1)):
+            ctx.set_tuning("probe", probe)
+            ctx.set_tuning("stress_probe", stress)
+            res.append(eval_loss_batch(tb, ds, opts))
+    finally:
+        ctx.set_tuning("probe", 2)
+        ctx.set_tuning("stress_probe", 1)
+    l0, c0 = res[0]
+    assert 0.1 < c0.mean() < 0.9
+    u = np.uint64 if dtype == np.float64 else np.uint32
+    for l1, c1 in res[1:]:
+        assert np.array_equal(c1, c0)
+        assert np.array_equal(np.asarray(l1)[c1].view(u), np.asarray(l0)[c0].view(u))
