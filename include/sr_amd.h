@@ -341,7 +341,8 @@ int sr_last_phase_ms(sr_ctx* ctx, double* out, int n);
  * "derived" (0 / 1: derived columns for unary(feature) nodes of large LOSS calls), "probe" (dead-tree
  * probe: 0 off, 1 before every chunk, 2 before the chunks after the first), "stress_probe" (0 / 1: the
  * probe runs the dataset's stress rows — per feature the extreme and nearest-zero values — instead of
- * its first rows).  Results do not depend on any knob.  SR_ERR_INVALID_ARG for an unknown name.  sr_tuning_info (optional outputs)
+ * its first rows), "code_cache" (0 / 1: register-stack launches copy each tree group's programs into
+ * LDS once instead of streaming them per tile from global memory).  Results do not depend on any knob.  SR_ERR_INVALID_ARG for an unknown name.  sr_tuning_info (optional outputs)
  * reports how many derived columns the last sr_eval_loss_batch used and how many of its trees went
  * through the exact-sum pass (flagged BIG). */
 int sr_set_tuning(sr_ctx* ctx, const char* name, int64_t value);

@@ -160,12 +160,13 @@ template int sr_rows_per_lane<float>(int, int, int);
 template int sr_rows_per_lane<double>(int, int, int);
 
 size_t sr_tile_lds_bytes(int elem_size, int nf, int rows_per_lane, int stack_depth, int trees_per_block,
-                         int max_checks, int waves, bool weighted) {
-  // = SrLdsPlan (sr_tile_impl.h): X tile, y (+ w), LDS stack, EXACT checked values + running sums
+                         int max_checks, int waves, bool weighted, int code_lds) {
+  // = SrLdsPlan (sr_tile_impl.h): X tile, y (+ w), LDS stack, EXACT checked values + running sums,
+  // program cache (16-byte instructions)
   const size_t rows = size_t(64) * rows_per_lane;
   return size_t(nf) * rows * elem_size + (weighted ? 2 : 1) * rows * elem_size +
          size_t(waves) * stack_depth * rows * elem_size + size_t(waves) * size_t(max_checks) * rows * elem_size +
-         (size_t(trees_per_block) * size_t(max_checks) * elem_size + 15) / 16 * 16;
+         (size_t(trees_per_block) * size_t(max_checks) * elem_size + 15) / 16 * 16 + size_t(code_lds) * 16;
 }
 
 // Waves per workgroup: the f32 BASIC loss kernel has 4- and 8-wave (L2) builds (SR_AMD_WAVES selects);

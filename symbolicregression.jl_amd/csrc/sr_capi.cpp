@@ -136,6 +136,7 @@ struct sr_ctx {
   uint32_t* d_off = nullptr;
   uint8_t* d_bad = nullptr;
   uint32_t* d_perm = nullptr;
+  uint32_t* d_end = nullptr;  // [nt] end of each tree's program (code is staged in launch order)
   double* d_out_sum = nullptr;
   uint32_t* d_out_flag = nullptr;
   size_t outs_flag_off = 0;
@@ -162,7 +163,8 @@ struct sr_ctx {
   DevBuf prog, outs, part_sum, part_flag, pred, row_idx, tree_list,
       range_lo, range_hi, range_sums, packed, hint, jsum_prog, jsum_fin, jsum_scratch, probe_sum, probe_flag, g_code, g_offsets, g_consts, g_const_off, g_items, g_part, g_out,
       derived_cols, probe_derived;
-  int stress_probe = 1;     // SR_AMD_STRESS_PROBE: the probe runs the dataset's stress rows (below)
+  int stress_probe = 1;
+  int code_cache = 1;       // SR_AMD_CODE_CACHE: LDS program cache of the register-stack launches     // SR_AMD_STRESS_PROBE: the probe runs the dataset's stress rows (below)
   double last_eval_ms = 0.0, last_total_ms = 0.0;
   // host-side phases of the last eval_loss call (ms): compile, upload+launch, wait, exact pass,
   // finalize (sr_last_phase_ms)
@@ -212,7 +214,8 @@ struct sr_dataset {
 namespace {
 
 constexpr int64_t kRowAlign = 2048;  // a multiple of every kernel's row tile (64 lanes x R rows)
-constexpr int64_t kProbeRows = 2048;  // the dead-tree probe's rows: 4 tiles of the classic f32 build
+constexpr int64_t kProbeRows = 2048;
+constexpr size_t kCodeCacheLds = 36 * 1024;  // dynamic LDS a register-stack workgroup may use with its program cache  // the dead-tree probe's rows: 4 tiles of the classic f32 build
 
 // Work decomposition: row tiles of 64*R rows (one LDS image each), `tiles` per block; trees grouped G
 // per block (the block's 4 waves share the G trees of a tile).
@@ -401,7 +404,8 @@ int run_batch(sr_ctx* ctx, const sr_dataset* ds, int opset_id, const sr_tree_bat
   const size_t o_off = align256(code_cap * sizeof(SrIns<T>));
   const size_t o_bad = align256(o_off + (size_t(nt) + 1) * sizeof(uint32_t));
   const size_t o_perm = align256(o_bad + size_t(nt) + 16);
-  const size_t prog_bytes = o_perm + (size_t(nt) + 1) * sizeof(uint32_t);
+  const size_t o_end = align256(o_perm + (size_t(nt) + 1) * sizeof(uint32_t));
+  const size_t prog_bytes = o_end + (size_t(nt) + 1) * sizeof(uint32_t);
   SR_HIP_CHECK(ctx->prog.ensure(prog_bytes));
   SR_HIP_CHECK(ctx->h_prog.ensure(prog_bytes, s, ctx->stream2));
   char* const dprog = ctx->prog.as<char>();  // (re-pointed at the staging buffer below for host_prog)
@@ -409,6 +413,7 @@ int run_batch(sr_ctx* ctx, const sr_dataset* ds, int opset_id, const sr_tree_bat
   ctx->d_off = reinterpret_cast<uint32_t*>(dprog + o_off);
   ctx->d_bad = reinterpret_cast<uint8_t*>(dprog + o_bad);
   ctx->d_perm = reinterpret_cast<uint32_t*>(dprog + o_perm);
+  ctx->d_end = reinterpret_cast<uint32_t*>(dprog + o_end);
   const size_t n_part = size_t(nt) * size_t(n_rb);
   SR_HIP_CHECK(ctx->part_sum.ensure(n_part * sizeof(double) + 8));
   SR_HIP_CHECK(ctx->part_flag.ensure(n_part * sizeof(uint32_t) + 4));
@@ -465,11 +470,13 @@ int run_batch(sr_ctx* ctx, const sr_dataset* ds, int opset_id, const sr_tree_bat
     ctx->d_off = reinterpret_cast<uint32_t*>(hprog + o_off);
     ctx->d_bad = reinterpret_cast<uint8_t*>(hprog + o_bad);
     ctx->d_perm = reinterpret_cast<uint32_t*>(hprog + o_perm);
+    ctx->d_end = reinterpret_cast<uint32_t*>(hprog + o_end);
   }
   SrIns<T>* h_code = reinterpret_cast<SrIns<T>*>(hprog);
   uint32_t* h_off = reinterpret_cast<uint32_t*>(hprog + o_off);
   uint8_t* h_bad = reinterpret_cast<uint8_t*>(hprog + o_bad);
   uint32_t* h_perm = reinterpret_cast<uint32_t*>(hprog + o_perm);
+  uint32_t* h_end = reinterpret_cast<uint32_t*>(hprog + o_end);
   ctx->n_chunks_last = 0;
   ctx->derived_last = false;
   ctx->n_derived_last = 0;
@@ -558,8 +565,6 @@ int run_batch(sr_ctx* ctx, const sr_dataset* ds, int opset_id, const sr_tree_bat
       sync_both();
       return set_error(SR_ERR_INVALID_ARG, "program longer than its node count");
     }
-    if (ncode) std::memcpy(h_code + code_base, pc.code.data(), ncode * sizeof(SrIns<T>));
-    for (int64_t i = 0; i <= nc; ++i) h_off[t0 + i] = code_base + pc.offsets[size_t(i)];
     std::memcpy(h_bad + t0, pc.static_bad.data(), size_t(nc));
     {
       // launch order: register-stack trees first, each class in decreasing estimated cost so every
@@ -579,20 +584,34 @@ int run_batch(sr_ctx* ctx, const sr_dataset* ds, int opset_id, const sr_tree_bat
       for (size_t k = 1; k < start.size(); ++k) start[k] += start[k - 1];
       for (int64_t i = 0; i < nc; ++i) h_perm[t0 + start[key(i)]++] = uint32_t(i);
     }
+    {
+      // programs in launch order: a tree group's code is one contiguous span (the kernel's LDS program
+      // cache copies it in one pass); offsets / ends stay indexed by tree
+      uint32_t at = code_base;
+      for (int64_t p = 0; p < nc; ++p) {
+        const uint32_t i = h_perm[t0 + p];
+        const uint32_t b = pc.offsets[size_t(i)], e = pc.offsets[size_t(i) + 1];
+        if (e > b) std::memcpy(h_code + at, pc.code.data() + b, size_t(e - b) * sizeof(SrIns<T>));
+        h_off[t0 + i] = at;
+        h_end[t0 + i] = at + (e - b);
+        at += e - b;
+      }
+    }
     if (host_prog) {
       // the kernel reads the staging image itself
     } else if (n_chunks == 1) {  // the whole staging image (code, offsets, static_bad, order): one DMA
-      SR_HIP_CHECK(hipMemcpyAsync(dprog, hprog, o_perm + size_t(nc) * sizeof(uint32_t), hipMemcpyHostToDevice, cs));
+      SR_HIP_CHECK(hipMemcpyAsync(dprog, hprog, o_end + size_t(nc) * sizeof(uint32_t), hipMemcpyHostToDevice, cs));
     } else {
       if (ncode)
         SR_HIP_CHECK(hipMemcpyAsync(static_cast<SrIns<T>*>(ctx->d_code) + code_base, h_code + code_base,
                                     ncode * sizeof(SrIns<T>), hipMemcpyHostToDevice, cs));
-      SR_HIP_CHECK(hipMemcpyAsync(ctx->d_off + t0, h_off + t0, size_t(nc + 1) * sizeof(uint32_t), hipMemcpyHostToDevice, cs));
+      SR_HIP_CHECK(hipMemcpyAsync(ctx->d_off + t0, h_off + t0, size_t(nc) * sizeof(uint32_t), hipMemcpyHostToDevice, cs));
+      SR_HIP_CHECK(hipMemcpyAsync(ctx->d_end + t0, h_end + t0, size_t(nc) * sizeof(uint32_t), hipMemcpyHostToDevice, cs));
       SR_HIP_CHECK(hipMemcpyAsync(ctx->d_bad + t0, h_bad + t0, size_t(nc), hipMemcpyHostToDevice, cs));
       SR_HIP_CHECK(hipMemcpyAsync(ctx->d_perm + t0, h_perm + t0, size_t(nc) * sizeof(uint32_t), hipMemcpyHostToDevice, cs));
     }
     // merged summary
-    for (int64_t i = 0; i <= nc; ++i) prog->offsets[size_t(t0 + i)] = h_off[t0 + i];
+    for (int64_t i = 0; i < nc; ++i) prog->offsets[size_t(t0 + i)] = h_off[t0 + i];  // (starts; ends: h_end)
     std::memcpy(prog->static_bad.data() + t0, pc.static_bad.data(), size_t(nc));
     std::copy(pc.n_checks.begin(), pc.n_checks.end(), prog->n_checks.begin() + t0);
     if (pc.max_depth > prog->max_depth) prog->max_depth = pc.max_depth;
@@ -616,6 +635,7 @@ int run_batch(sr_ctx* ctx, const sr_dataset* ds, int opset_id, const sr_tree_bat
       SrEvalArgs<T> a{};
       a.code = static_cast<const SrIns<T>*>(ctx->d_code);
       a.offsets = ctx->d_off + t0;
+      a.ends = ctx->d_end + t0;
       a.perm = ctx->d_perm + t0 + p0;
       a.hint = use_hint ? ctx->hint.as<uint32_t>() + t0 + p0 : nullptr;
       a.hint_epoch = ctx->hint_epoch;
@@ -643,6 +663,21 @@ int run_batch(sr_ctx* ctx, const sr_dataset* ds, int opset_id, const sr_tree_bat
       a.part_flag = ctx->part_flag.as<uint32_t>() + size_t(n_rb) * size_t(t0 + p0);
       a.pred = ctx->pred.as<T>();
       a.pred_ld = n_eval;
+      // LDS program cache (register-stack launches: 4 workgroups per CU leave ~36 KiB of dynamic LDS
+      // each): sized for the longest group span of this launch, capped by that budget (groups longer
+      // than the cap stream their windows from global memory)
+      a.code_lds = 0;
+      if (vstk && mode == SR_MODE_LOSS && ctx->code_cache && size_t(g.lds) < kCodeCacheLds) {
+        int64_t maxspan = 0;
+        for (int64_t q = 0; q < g.n_groups; ++q) {
+          const int64_t pf = p0 + q * g.G, pl = std::min<int64_t>(p0 + np, pf + g.G) - 1;
+          const int64_t sp = int64_t(h_end[t0 + h_perm[t0 + pl]]) - int64_t(h_off[t0 + h_perm[t0 + pf]]);
+          maxspan = std::max(maxspan, sp);
+        }
+        const int64_t cap = int64_t((kCodeCacheLds - size_t(g.lds)) / 16);
+        a.code_lds = int(std::min(maxspan, cap));
+        if (a.code_lds < 64) a.code_lds = 0;
+      }
       const bool direct = mode == SR_MODE_LOSS && g.n_row_blocks == 1;
       if (direct) {  // the interpreter writes the final per-tree values; no reduce launch
         a.out_sum = ctx->d_out_sum + t0;
@@ -661,6 +696,7 @@ int run_batch(sr_ctx* ctx, const sr_dataset* ds, int opset_id, const sr_tree_bat
         pa.stack_depth = depth;
         pa.out_sum = nullptr;
         pa.out_flag = nullptr;
+        pa.code_lds = 0;  // (its groups differ from the main launch's)
         pa.trees_per_block = std::max(16, g.W);
         pa.n_groups = int((np + pa.trees_per_block - 1) / pa.trees_per_block);
         pa.tiles_per_block = 1;
@@ -913,6 +949,7 @@ int run_exact(sr_ctx* ctx, const sr_dataset* ds, const SrProgramBatch<T>& prog, 
     SrEvalArgs<T> a{};
     a.code = static_cast<const SrIns<T>*>(ctx->d_code);
     a.offsets = ctx->d_off;
+    a.ends = ctx->d_end;
     a.perm = ctx->tree_list.as<uint32_t>();
     a.n_trees = int(nb);
     a.trees_per_block = G;
@@ -1381,6 +1418,7 @@ int sr_init(int device, sr_ctx** out) {
   if (const char* v = std::getenv("SR_AMD_CHUNKS")) ctx->chunks = std::atoi(v);
   if (const char* v = std::getenv("SR_AMD_PROBE")) ctx->probe = std::atoi(v);
   if (const char* v = std::getenv("SR_AMD_STRESS_PROBE")) ctx->stress_probe = std::atoi(v);
+  if (const char* v = std::getenv("SR_AMD_CODE_CACHE")) ctx->code_cache = std::atoi(v);
   if (const char* v = std::getenv("SR_AMD_HOST_IO")) ctx->host_io = std::atoi(v);
   if (const char* v = std::getenv("SR_AMD_SPIN")) ctx->spin = std::atoi(v);
   if (const char* v = std::getenv("SR_AMD_EXACT_G")) ctx->exact_g = std::atoi(v);
@@ -1800,6 +1838,10 @@ int sr_set_tuning(sr_ctx* ctx, const char* name, int64_t value) {
   }
   if (std::strcmp(name, "probe") == 0) {  // dead-tree probe mode (SR_AMD_PROBE)
     ctx->probe = int(value);
+    return SR_OK;
+  }
+  if (std::strcmp(name, "code_cache") == 0) {  // LDS program cache (SR_AMD_CODE_CACHE)
+    ctx->code_cache = value != 0 ? 1 : 0;
     return SR_OK;
   }
   if (std::strcmp(name, "stress_probe") == 0) {  // the probe over the stress rows (SR_AMD_STRESS_PROBE)

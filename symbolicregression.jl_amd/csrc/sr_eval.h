@@ -13,6 +13,8 @@ struct SrEvalArgs {
   // programs
   const SrIns<T>* code;
   const uint32_t* offsets;     // [n_trees + 1], indexed by the caller's tree index
+  const uint32_t* ends;        // [n_trees] end of each tree's program (NULL: offsets[t + 1]); programs are
+                               // staged in launch order, so a tree group's code is one contiguous span
   const uint32_t* perm;        // launch position -> caller's tree index (NULL: identity); EXACT: tree list
   uint32_t* hint;              // [n_trees] per position: dead-tree hints across row blocks (LOSS; may be NULL)
   uint32_t hint_epoch;         // a position is dead when its hint equals this call's epoch (no reset pass)
@@ -32,6 +34,8 @@ struct SrEvalArgs {
   int n_row_blocks;
   int n_groups;                // tree groups (blockIdx = row_block * n_groups + group)
   int stack_depth;             // LDS operand-stack slots per wave (>= 1)
+  int code_lds;                // LOSS: instructions of LDS program cache per workgroup (0: windows
+                               // stream from global memory); a group whose span exceeds it streams too
   T tbig;                      // |v| >= tbig may overflow the array-sum check
   int track_x;                 // the data holds |x| >= tbig or non-finite values: checked feature
                                // loads join the deferred checks (FAST path)
@@ -59,7 +63,7 @@ template <typename T, int R, int MODE, bool GATHER, int TIER, int W = 4, int LK 
 hipError_t sr_launch_tile(const SrEvalArgs<T>& a, int n_blocks, hipStream_t s);
 // LDS bytes one workgroup (W waves) of the tile kernel needs.
 size_t sr_tile_lds_bytes(int elem_size, int nf, int rows_per_lane, int stack_depth, int trees_per_block,
-                         int max_checks, int waves, bool weighted);
+                         int max_checks, int waves, bool weighted, int code_lds = 0);
 // Waves per workgroup the dispatcher uses for (mode, tier, rows per lane); `requested` overrides.
 int sr_waves_per_block(int elem_size, int mode, int tier, int rows_per_lane, int requested);
 // Rows per lane the dispatcher uses for (mode, tier); `requested` 4 selects the f32 BASIC tuning kernel.

@@ -627,11 +627,12 @@ __device__ __forceinline__ void sr_post_unary(uint32_t u, bool inf, T (&tos)[R])
 
 // LDS carve, in bytes, 16-aligned: X tile [nf][ROWS] T | y [ROWS] | w [ROWS] (weighted) | stack
 // [W][depth][ROWS] T | EXACT mode: checked values [W][max_checks][ROWS] T and the running Julia-order
-// sums [G][max_checks] T
+// sums [G][max_checks] T | program cache [code_lds] 16-byte instructions (LOSS)
 template <typename T>
 struct SrLdsPlan {
-  size_t x, y, w, stk, chk, jst, total;
-  __host__ __device__ SrLdsPlan(int nf, int rows, int depth, int G, int max_checks, int waves, bool weighted) {
+  size_t x, y, w, stk, chk, jst, code, total;
+  __host__ __device__ SrLdsPlan(int nf, int rows, int depth, int G, int max_checks, int waves, bool weighted,
+                                int code_lds = 0) {
     size_t o = 0;
     x = o;
     o += size_t(nf) * rows * sizeof(T);
@@ -645,6 +646,8 @@ struct SrLdsPlan {
     o += size_t(waves) * size_t(max_checks) * rows * sizeof(T);
     jst = o;
     o += (size_t(G) * size_t(max_checks) * sizeof(T) + 15) / 16 * 16;
+    code = o;
+    o += size_t(code_lds) * 16;
     total = o;
   }
 };
@@ -682,6 +685,19 @@ __device__ __forceinline__ typename SrWindow<T>::type sr_window(const void* code
   if (base + uint32_t(lane) < end) w = SrWindow<T>::load(code, base + uint32_t(lane));
   return w;
 }
+// the same window from the workgroup's LDS program cache (ds_read instead of a global load: the next
+// tree's window arrives within the current short tree's run)
+template <typename T>
+__device__ __forceinline__ typename SrWindow<T>::type sr_window_lds(const uint4* lcode, uint32_t base, uint32_t end,
+                                                                    int lane) {
+  typename SrWindow<T>::type w{};
+  if (base + uint32_t(lane) < end) {
+    const uint4 v = lcode[base + uint32_t(lane)];
+    if constexpr (sizeof(T) == 4) w = make_uint3(v.x, v.y, v.z);
+    else w = v;
+  }
+  return w;
+}
 
 // ------------------------------------------------------------------ the interpreter kernel
 // MODE: SR_MODE_LOSS (partials), SR_MODE_PRED (write predictions), SR_MODE_EXACT (Julia-order sums of
@@ -712,7 +728,8 @@ __global__ void __launch_bounds__(W * 64, (SrMinWavesFor<T, R, TIER, W, VSTK>::v
   const int lane = tid & 63;
   const int G = a.trees_per_block;
   const int MC = (MODE == SR_MODE_EXACT) ? a.max_checks : 0;
-  const SrLdsPlan<T> plan(a.nf, ROWS, VSTK ? 0 : a.stack_depth, G, MC, W, a.w != nullptr);
+  const SrLdsPlan<T> plan(a.nf, ROWS, VSTK ? 0 : a.stack_depth, G, MC, W, a.w != nullptr,
+                          MODE == SR_MODE_LOSS ? a.code_lds : 0);
   T* xs = reinterpret_cast<T*>(sr_smem + plan.x);
   T* ys = reinterpret_cast<T*>(sr_smem + plan.y);
   T* wsv = reinterpret_cast<T*>(sr_smem + plan.w);
@@ -744,7 +761,27 @@ __global__ void __launch_bounds__(W * 64, (SrMinWavesFor<T, R, TIER, W, VSTK>::v
   if (lane < S) {
     const uint32_t t = a.perm ? a.perm[my_pos] : uint32_t(my_pos);
     my_pb = a.offsets[t];
-    my_pe = a.offsets[t + 1];
+    my_pe = a.ends ? a.ends[t] : a.offsets[t + 1];
+  }
+  // LDS program cache (LOSS): the group's programs are one contiguous span of the launch-ordered code
+  // (first position's start .. last position's end); copied once, read by every tile's windows
+  const uint4* lcode = reinterpret_cast<const uint4*>(sr_smem + plan.code);
+  bool lds_code = false;
+  if (MODE == SR_MODE_LOSS && a.code_lds > 0 && a.ends != nullptr && gcount > 0) {
+    const uint32_t t_first = a.perm ? a.perm[tree0] : uint32_t(tree0);
+    const uint32_t t_last = a.perm ? a.perm[tree0 + gcount - 1] : uint32_t(tree0 + gcount - 1);
+    const uint32_t gbase = __builtin_amdgcn_readfirstlane(a.offsets[t_first]);
+    const uint32_t gend = __builtin_amdgcn_readfirstlane(a.ends[t_last]);
+    if (gend >= gbase && gend - gbase <= uint32_t(a.code_lds)) {
+      lds_code = true;
+      const uint4* src = reinterpret_cast<const uint4*>(a.code) + gbase;
+      uint4* dst = reinterpret_cast<uint4*>(sr_smem + plan.code);
+      for (uint32_t i = uint32_t(tid); i < gend - gbase; i += uint32_t(SR_BLOCK)) dst[i] = src[i];
+      if (lane < S) {
+        my_pb -= gbase;
+        my_pe -= gbase;
+      }
+    }
   }
   const uint64_t live = sr_ballot(lane < S && my_pe > my_pb);  // empty program: statically incomplete
   uint64_t dmask = 0u, bmask = 0u;
@@ -840,7 +877,7 @@ __global__ void __launch_bounds__(W * 64, (SrMinWavesFor<T, R, TIER, W, VSTK>::v
     todo &= todo - 1u;
     uint32_t nb = uint32_t(__builtin_amdgcn_readlane(int(my_pb), nj));
     uint32_t ne = uint32_t(__builtin_amdgcn_readlane(int(my_pe), nj));
-    typename SrWindow<T>::type nx = sr_window<T>(a.code, nb, ne, lane);
+    typename SrWindow<T>::type nx = lds_code ? sr_window_lds<T>(lcode, nb, ne, lane) : sr_window<T>(a.code, nb, ne, lane);
     int j = -1;
     uint32_t tpe = 0u;
     T tos[R];
@@ -874,7 +911,7 @@ __global__ void __launch_bounds__(W * 64, (SrMinWavesFor<T, R, TIER, W, VSTK>::v
       } else {
         more = false;
       }
-      if (more) nx = sr_window<T>(a.code, nb, ne, lane);
+      if (more) nx = lds_code ? sr_window_lds<T>(lcode, nb, ne, lane) : sr_window<T>(a.code, nb, ne, lane);
       const int g = wave + SR_WAVES * j;
 
       if (!dead) {
@@ -941,6 +978,9 @@ __global__ void __launch_bounds__(W * 64, (SrMinWavesFor<T, R, TIER, W, VSTK>::v
               const T cv = SR_CVAL();
 #pragma unroll
               for (int r = 0; r < R; ++r) tos[r] = cv;
+              // (a constant leaf is an operand of its parent: LOAD_CONST is only ever a constant
+              // tree's root, which the deferred checks must see like every other root)
+              SR_TRACK();
               break;
             }
             // BASIC tier
@@ -1048,23 +1088,21 @@ __global__ void __launch_bounds__(W * 64, (SrMinWavesFor<T, R, TIER, W, VSTK>::v
 #pragma unroll
               for (int r = 0; r < R; ++r) l[r] = (row0 + L::row(lane, r) < a.n_rows) ? l[r] : T(0);
             }
-            // pairwise over the lane's rows (packed adds); the wave sum follows
+            // pairwise over the lane's rows by halves (rows r and r + h: adjacent pairs of rows add as
+            // one packed instruction, R - 1 adds in R / 2 instructions); the wave sum follows
 #pragma unroll
-            for (int h = 1; h < R; h *= 2) {
+            for (int h = R / 2; h >= 1; h /= 2) {
 #pragma unroll
-              for (int r = 0; r + h < R; r += 2 * h) l[r] += l[r + h];
+              for (int r = 0; r < h; ++r) l[r] += l[r + h];
             }
             if (FAST_CHECK) {
-              // the root is always checked; a checked value was +-Inf -> incomplete; NaN anywhere
-              // reaches the root (BASIC operators propagate NaN) and shows in the lane's loss sum
-              // (padded rows replicate a real row: masking them hides no NaN), or, with weights or a
-              // loss that can map NaN to a number (margin losses), in the root values; a large
-              // finite one: the array-sum check may overflow
-#pragma unroll
-              for (int r = 0; r < R; r += 4) {
-                mrun = SrMaxAbs<T>::step(mrun, tos[r], tos[r + 1]);
-                if (r + 3 < R) mrun1 = SrMaxAbs<T>::step(mrun1, tos[r + 2], tos[r + 3]);
-              }
+              // the root is always checked, and already in the running max: every operator output and
+              // constant root joins it, a feature root when the data needs it (track_x: otherwise
+              // the data is finite and below tbig); a checked value was +-Inf -> incomplete; NaN
+              // anywhere reaches the root (BASIC operators propagate NaN) and shows in the lane's
+              // loss sum (padded rows replicate a real row: masking them hides no NaN), or, with
+              // weights or a loss that can map NaN to a number (margin losses), in the root values;
+              // a large finite one: the array-sum check may overflow
               mrun = SrMaxAbs<T>::step(mrun, mrun1, T(0));
               bool nan_root = false;
               if (weighted || !sr_loss_propagates_nan(lk)) {
@@ -1132,7 +1170,8 @@ template <typename T, int R, int MODE, bool GATHER, int TIER, int W, int LK, boo
 hipError_t sr_launch_tile(const SrEvalArgs<T>& a, int n_blocks, hipStream_t s) {
   if (VSTK && a.stack_depth > 2) return hipErrorInvalidValue;  // host checks: VSTK holds two slots
   const SrLdsPlan<T> plan(a.nf, 64 * R, VSTK ? 0 : a.stack_depth, a.trees_per_block,
-                          MODE == SR_MODE_EXACT ? a.max_checks : 0, W, a.w != nullptr);
+                          MODE == SR_MODE_EXACT ? a.max_checks : 0, W, a.w != nullptr,
+                          MODE == SR_MODE_LOSS ? a.code_lds : 0);
   const void* fn = reinterpret_cast<const void*>(&sr_tile_kernel<T, R, MODE, GATHER, TIER, W, LK, VSTK>);
   if (plan.total > 65536) {  // many features / a deep stack: opt in to the full 160 KiB of LDS
     const hipError_t e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, int(plan.total));

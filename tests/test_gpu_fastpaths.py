@@ -158,7 +158,7 @@ def test_derived_columns_change_nothing(dtype, batching):
 
 @pytest.mark.parametrize("dtype", [np.float32, np.float64])
 def test_probe_modes_change_nothing(dtype):
-    """The dead-tree probe only sets hints: with no probe, the first-rows probe, the stress-row probe
+    """The LDS program cache on or off, and the dead-tree probe, which only sets hints: with no probe, the first-rows probe, the stress-row probe
     (extreme and nearest-zero rows of each feature, through the gather build and derived columns
     computed over those rows) and a probe before every chunk, losses and flags are identical bit for
     bit.  The data holds rare overflow rows past the first tiles, so the stress rows find trees the
@@ -178,13 +178,15 @@ def test_probe_modes_change_nothing(dtype):
     ctx = sr_amd.get_context()
     res = []
     try:
-        for probe, stress in ((0, 0), (2, 0), (2, 1), (1, 1)):
+        for probe, stress, cache in ((0, 0, 1), (2, 0, 1), (2, 1, 1), (1, 1, 1), (2, 1, 0)):
             ctx.set_tuning("probe", probe)
             ctx.set_tuning("stress_probe", stress)
+            ctx.set_tuning("code_cache", cache)
             res.append(eval_loss_batch(tb, ds, opts))
     finally:
         ctx.set_tuning("probe", 2)
         ctx.set_tuning("stress_probe", 1)
+        ctx.set_tuning("code_cache", 1)
     l0, c0 = res[0]
     assert 0.1 < c0.mean() < 0.9
     u = np.uint64 if dtype == np.float64 else np.uint32
