@@ -931,8 +931,10 @@ int run_exact(sr_ctx* ctx, const sr_dataset* ds, const SrProgramBatch<T>& prog, 
     const int64_t nb = std::min(batch, n_list - b0);
     // one wave per workgroup, G listed trees per workgroup (LDS: X tile + one wave's checked
     // values [max_checks][rows] + running sums [G][max_checks]): G amortises the tile staging over
-    // trees, small G spreads few trees over more waves; aim at >= 8192 waves, G <= 16
-    const int64_t g_fill = (nb * n_ranges + 8191) / 8192;
+    // trees, small G spreads few trees over more waves; aim at >= 1024 waves (one per SIMD), G <= 16
+    // (C2's 8 listed trees x 1024 leaf ranges: G 1 -> 8, exact pass 0.28 -> 0.21 ms;
+    // profiles/r02_ab_exact_g.txt)
+    const int64_t g_fill = (nb * n_ranges + 1023) / 1024;
     int G = int(std::min<int64_t>(nb, ctx->exact_g > 0 ? ctx->exact_g : std::max<int64_t>(1, std::min<int64_t>(16, g_fill))));
     size_t lds = 0;
     for (;;) {
