@@ -522,11 +522,16 @@ __device__ __forceinline__ void sr_post_unary(uint32_t u, bool inf, T (&tos)[R])
 #define SR_OPND_X() sr_row_at<ROWS>(x_lane, SR_META())
 // stack operand: VSTK kernels keep the (at most two) operand-stack slots in VGPRs (s0, s1; the slot
 // is the operand index); the others read the slot's rows from the wave's LDS stack area
+// (SR_KEEP_BRANCH: an empty volatile asm in each arm keeps the wave-uniform slot choice a scalar
+// branch; if-converted, LLVM selects every row of both slots with v_cndmask)
+#define SR_KEEP_BRANCH() asm volatile("")
 #define SR_STK_BIN(ID, LEFT)                                          \
   if constexpr (VSTK) {                                               \
     if ((SR_META() & SR_M_INDEX) == 0u) {                             \
+      SR_KEEP_BRANCH();                                               \
       SR_BIN_EACH((LEFT) ? s0[r] : tos[r], (LEFT) ? tos[r] : s0[r], ID); \
     } else {                                                          \
+      SR_KEEP_BRANCH();                                               \
       SR_BIN_EACH((LEFT) ? s1[r] : tos[r], (LEFT) ? tos[r] : s1[r], ID); \
     }                                                                 \
   } else {                                                            \
@@ -926,8 +931,10 @@ __global__ void __launch_bounds__(W * 64, (SrMinWavesFor<T, R, TIER, W, VSTK>::v
 #define SR_PUSH_TOS()                                                                        \
   if constexpr (VSTK) {                                                                      \
     if (((SR_META() >> SR_M_PUSH_SHIFT) & 0x3fu) == 1u) {                                    \
+      SR_KEEP_BRANCH();                                                                      \
       _Pragma("unroll") for (int r = 0; r < R; ++r) s0[r] = tos[r];                          \
     } else {                                                                                 \
+      SR_KEEP_BRANCH();                                                                      \
       _Pragma("unroll") for (int r = 0; r < R; ++r) s1[r] = tos[r];                          \
     }                                                                                        \
   } else {                                                                                   \
