@@ -25,7 +25,7 @@ def main(out):
     rpl = rf["kernel"].split("<float,")[1].split(",")[0]  # rows per lane of the build the bench ran
     # every f32 BASIC-tier LOSS launch (mode 0, no gather, tier 0, 4 waves): the bench's build and the
     # dead-tree probe, which runs on the classic 8-rows/lane build whatever the main launches use
-    pat = re.compile(r"void sr_tile_kernel<float, \d+, 0, false, 0, 4, ")
+    pat = re.compile(r"void sr_tile_kernel<float, \d+, 0, (false|true), 0, 4, ")
     prefix = f"void sr_tile_kernel<float, {rpl}, 0,"
     interp = [r for r in rows if pat.match(r["Kernel_Name"])]
     interp.sort(key=lambda r: int(r["Start_Timestamp"]))
