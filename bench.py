@@ -125,12 +125,15 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     dist = None
-    if world > 1:
-        import torch
+    # SR_BENCH_FORCE_DIST=1 (under torch.distributed.run): the multi-GPU code path at world size 1
+    # (rehearses the scaling run's rendezvous, RCCL communicator and sharded step on one GPU)
+    if world > 1 or os.environ.get("SR_BENCH_FORCE_DIST") == "1":
         import torch.distributed as tdist
 
-        torch.cuda.set_device(local_rank)
-        tdist.init_process_group(backend="nccl")
+        # gloo (CPU) for the rendezvous, the barrier and the max-over-ranks timing; the data path's
+        # exchange is the library's own RCCL all-reduce over xGMI (sr_comm_*): torch's bundled HIP
+        # runtime cannot share a GPU with the library's in one process, so torch never touches it
+        tdist.init_process_group(backend="gloo")
         dist = tdist
     c4 = args.workload == "c4"
     if c4 and args.steps == 20 and args.warmup == 8:  # a C4 step is ~2 s on one GPU: fewer by default
@@ -150,17 +153,19 @@ def main():
         X, y = c2_data(rows_total // world, rank)
     n_local = X.shape[1]
     ctx = sr_amd.get_context(local_rank)
+    if dist is not None:
+        from sr_amd.distributed import init_device_comm
+
+        init_device_comm(ctx=ctx)
     ds = Dataset(X, y)
     ds.device_handle(ctx)  # upload before timing
 
-    if world == 1:
+    if dist is None:
         step, losses, comp, state = single_gpu_step(ctx, tb, ds, opts)
 
         def barrier():
             pass
     else:
-        import torch
-
         from sr_amd.distributed import eval_loss_sharded
 
         result, state = {}, {"launches": []}
@@ -171,14 +176,14 @@ def main():
             return ctx.last_kernel_ms()[0]
 
         def barrier():
+            # every library call returns after its stream has drained (device synchronised)
             dist.barrier()
-            torch.cuda.synchronize()
 
     dt, step_ms, kernel_ms = timed(step, args.steps, args.warmup, barrier)
     if dist is not None:
         import torch
 
-        tt = torch.tensor([dt], dtype=torch.float64, device=torch.device("cuda", local_rank))
+        tt = torch.tensor([dt], dtype=torch.float64)
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         dt = float(tt.item())
         comp = result["comp"]

@@ -153,6 +153,20 @@ int sr_eval_loss_partials(sr_ctx* ctx, const sr_dataset* ds, int opset_id, const
  */
 int sr_eval_loss_partials_packed(sr_ctx* ctx, const sr_dataset* ds, int opset_id, const sr_tree_batch* trees,
                                  int64_t n_total, int loss_kind, double* out, int out_on_device);
+/* RCCL for the row-sharded path, on the library's own HIP runtime: rank 0 calls
+ * sr_comm_unique_id, the caller broadcasts the SR_COMM_ID_BYTES bytes (any CPU channel: MPI, a TCP
+ * store, torch.distributed's gloo group), every rank calls sr_comm_init with them.
+ * sr_eval_loss_partials_allreduce = sr_eval_loss_partials_packed on this shard, then ONE in-place
+ * ncclAllReduce (sum) of the [4, n_trees] f64 buffer on the device over xGMI, then the global
+ * partials to out_host (what sr_finalize_losses / the exact path take).  Every rank must call it
+ * with the same trees.  (Replaces the Julia-side Distributed reduction of the reference's
+ * per-worker losses for one batched call.) */
+#define SR_COMM_ID_BYTES 128
+int sr_comm_unique_id(void* out_id);
+int sr_comm_init(sr_ctx* ctx, int nranks, int rank, const void* id_bytes);
+int sr_comm_destroy(sr_ctx* ctx);
+int sr_eval_loss_partials_allreduce(sr_ctx* ctx, const sr_dataset* ds, int opset_id, const sr_tree_batch* trees,
+                                    int64_t n_total, int loss_kind, double* out_host);
 /* Maximum number of checked nodes per tree for `trees` (element type dtype; sizes the
  * sr_jsum_partials output). */
 int sr_max_checks(sr_ctx* ctx, int dtype, int opset_id, const sr_tree_batch* trees, int* max_checks);

@@ -6,6 +6,7 @@
 //   check for trees whose checked values came close to overflowing -> loss = Σ / denominator.
 // Mirrors reference src/LossFunctions.jl:90-117 (`_eval_loss`) for each tree of the batch.
 #include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
 
 #include <algorithm>
 #include <chrono>
@@ -164,7 +165,12 @@ struct sr_ctx {
       range_lo, range_hi, range_sums, packed, hint, jsum_prog, jsum_fin, jsum_scratch, probe_sum, probe_flag, g_code, g_offsets, g_consts, g_const_off, g_items, g_part, g_out,
       derived_cols, probe_derived;
   int stress_probe = 1;
-  int code_cache = 1;       // SR_AMD_CODE_CACHE: LDS program cache of the register-stack launches     // SR_AMD_STRESS_PROBE: the probe runs the dataset's stress rows (below)
+  int code_cache = 1;
+  int first_chunk = 6;
+  // RCCL communicator of the row-sharded path (sr_comm_init): the library's own RCCL over xGMI on
+  // its own HIP runtime (torch's bundled runtime cannot share the GPU with this one in a process)
+  ncclComm_t comm = nullptr;
+  int comm_ranks = 0;      // SR_AMD_FIRST_CHUNK: the two-chunk pipeline's first chunk is 1/first_chunk       // SR_AMD_CODE_CACHE: LDS program cache of the register-stack launches     // SR_AMD_STRESS_PROBE: the probe runs the dataset's stress rows (below)
   double last_eval_ms = 0.0, last_total_ms = 0.0;
   // host-side phases of the last eval_loss call (ms): compile, upload+launch, wait, exact pass,
   // finalize (sr_last_phase_ms)
@@ -384,7 +390,7 @@ int run_batch(sr_ctx* ctx, const sr_dataset* ds, int opset_id, const sr_tree_bat
   constexpr int64_t kChunkTrees = 2048;
   int n_chunks = 1;
   if (mode == SR_MODE_LOSS && ctx->chunks == 2) {
-    n_chunks = nt / 6 >= kChunkTrees / 2 ? 2 : 1;  // the small first chunk holds >= 1024 trees
+    n_chunks = nt / ctx->first_chunk >= kChunkTrees / 2 ? 2 : 1;  // the small first chunk holds >= 1024 trees
   } else if (mode == SR_MODE_LOSS && ctx->chunks > 2) {
     const int64_t k = nt / kChunkTrees;
     const int64_t cap = ctx->chunks < kMaxChunks ? ctx->chunks : kMaxChunks;
@@ -528,7 +534,7 @@ int run_batch(sr_ctx* ctx, const sr_dataset* ds, int opset_id, const sr_tree_bat
     auto bound = [&](int k) -> int64_t {
       if (k <= 0) return 0;
       if (k >= n_chunks) return nt;
-      return n_chunks == 2 ? nt / 6 : nt * k / n_chunks;
+      return n_chunks == 2 ? nt / ctx->first_chunk : nt * k / n_chunks;
     };
     const int64_t t0 = bound(c), t1 = bound(c + 1), nc = t1 - t0;
     // chunks alternate between two streams: chunk c+1's workgroups fill the GPU while chunk c drains
@@ -1421,6 +1427,7 @@ int sr_init(int device, sr_ctx** out) {
   if (const char* v = std::getenv("SR_AMD_PROBE")) ctx->probe = std::atoi(v);
   if (const char* v = std::getenv("SR_AMD_STRESS_PROBE")) ctx->stress_probe = std::atoi(v);
   if (const char* v = std::getenv("SR_AMD_CODE_CACHE")) ctx->code_cache = std::atoi(v);
+  if (const char* v = std::getenv("SR_AMD_FIRST_CHUNK")) ctx->first_chunk = std::max(2, std::atoi(v));
   if (const char* v = std::getenv("SR_AMD_HOST_IO")) ctx->host_io = std::atoi(v);
   if (const char* v = std::getenv("SR_AMD_SPIN")) ctx->spin = std::atoi(v);
   if (const char* v = std::getenv("SR_AMD_EXACT_G")) ctx->exact_g = std::atoi(v);
@@ -1453,6 +1460,8 @@ int sr_shutdown(sr_ctx* ctx) {
     Lock l(ctx);
     (void)hipSetDevice(ctx->device);
     (void)hipStreamSynchronize(ctx->stream);
+    if (ctx->comm) (void)ncclCommDestroy(ctx->comm);
+    ctx->comm = nullptr;
     for (DevBuf* b : {&ctx->prog, &ctx->outs, &ctx->part_sum, &ctx->part_flag, &ctx->pred, &ctx->row_idx, &ctx->tree_list, &ctx->range_lo, &ctx->range_hi, &ctx->range_sums, &ctx->packed,
                       &ctx->hint, &ctx->jsum_prog, &ctx->jsum_fin, &ctx->jsum_scratch, &ctx->probe_sum, &ctx->probe_flag, &ctx->g_code, &ctx->g_offsets, &ctx->g_consts, &ctx->g_const_off,
                       &ctx->g_items, &ctx->g_part, &ctx->g_out, &ctx->derived_cols, &ctx->probe_derived})
@@ -1638,6 +1647,85 @@ int sr_eval_loss_partials_packed(sr_ctx* ctx, const sr_dataset* ds, int opset_id
   }
   SR_HIP_CHECK(sr_launch_pack_partials(ctx->d_out_sum, ctx->d_out_flag, int(nt), dst, s));
   if (!out_on_device) SR_HIP_CHECK(hipMemcpyAsync(out, dst, bytes, hipMemcpyDeviceToHost, s));
+  SR_HIP_CHECK(hipStreamSynchronize(s));
+  ctx->last_eval_ms = chunk_kernel_ms(ctx);
+  ctx->last_total_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+  return SR_OK;
+}
+
+int sr_comm_unique_id(void* out_id) {
+  if (!out_id) return set_error(SR_ERR_INVALID_ARG, "NULL output");
+  ncclUniqueId id;
+  const ncclResult_t r = ncclGetUniqueId(&id);
+  if (r != ncclSuccess) return set_error(SR_ERR_HIP, std::string("ncclGetUniqueId: ") + ncclGetErrorString(r));
+  static_assert(sizeof(id) == SR_COMM_ID_BYTES, "RCCL unique id size");
+  std::memcpy(out_id, &id, sizeof(id));
+  return SR_OK;
+}
+
+int sr_comm_init(sr_ctx* ctx, int nranks, int rank, const void* id_bytes) {
+  if (check_ctx(ctx) != SR_OK) return SR_ERR_INVALID_ARG;
+  if (!id_bytes || nranks < 1 || rank < 0 || rank >= nranks) return set_error(SR_ERR_INVALID_ARG, "bad communicator arguments");
+  Lock l(ctx);
+  SR_HIP_CHECK(hipSetDevice(ctx->device));
+  if (ctx->comm) {
+    (void)ncclCommDestroy(ctx->comm);
+    ctx->comm = nullptr;
+    ctx->comm_ranks = 0;
+  }
+  ncclUniqueId id;
+  std::memcpy(&id, id_bytes, sizeof(id));
+  const ncclResult_t r = ncclCommInitRank(&ctx->comm, nranks, id, rank);
+  if (r != ncclSuccess) {
+    ctx->comm = nullptr;
+    return set_error(SR_ERR_HIP, std::string("ncclCommInitRank: ") + ncclGetErrorString(r));
+  }
+  ctx->comm_ranks = nranks;
+  return SR_OK;
+}
+
+int sr_comm_destroy(sr_ctx* ctx) {
+  if (check_ctx(ctx) != SR_OK) return SR_ERR_INVALID_ARG;
+  Lock l(ctx);
+  if (ctx->comm) (void)ncclCommDestroy(ctx->comm);
+  ctx->comm = nullptr;
+  ctx->comm_ranks = 0;
+  return SR_OK;
+}
+
+// Row-sharded step with the exchange on the device: this shard's packed [4, n_trees] partials
+// (sr_eval_loss_partials_packed) summed over every rank by ONE RCCL all-reduce in place on the
+// library's stream, then copied to out_host (every rank gets the global sums and flag counts).
+int sr_eval_loss_partials_allreduce(sr_ctx* ctx, const sr_dataset* ds, int opset_id, const sr_tree_batch* trees,
+                                    int64_t n_total, int loss_kind, double* out_host) {
+  if (check_ctx(ctx) != SR_OK) return SR_ERR_INVALID_ARG;
+  if (!ctx->comm) return set_error(SR_ERR_INVALID_ARG, "no communicator: call sr_comm_init first");
+  int rc = validate_common(ctx, ds, opset_id, trees);
+  if (rc != SR_OK) return rc;
+  const int64_t nt = trees->n_trees;
+  if (nt > 0 && !out_host) return set_error(SR_ERR_INVALID_ARG, "NULL output buffer");
+  if (n_total < ds->n) return set_error(SR_ERR_INVALID_ARG, "n_total smaller than this shard");
+  Lock l(ctx);
+  SR_HIP_CHECK(hipSetDevice(ctx->device));
+  Grid g;
+  auto t0 = std::chrono::steady_clock::now();
+  if (ds->dtype == SR_DTYPE_F32) {
+    SrProgramBatch<float> prog;
+    rc = run_batch<float>(ctx, ds, opset_id, trees, nullptr, 0, n_total, loss_kind, SR_MODE_LOSS, &prog, &g);
+  } else {
+    SrProgramBatch<double> prog;
+    rc = run_batch<double>(ctx, ds, opset_id, trees, nullptr, 0, n_total, loss_kind, SR_MODE_LOSS, &prog, &g);
+  }
+  if (rc != SR_OK) return rc;
+  hipStream_t s = ctx->stream;
+  const size_t n = size_t(4) * size_t(nt > 0 ? nt : 0);
+  SR_HIP_CHECK(ctx->packed.ensure(n * sizeof(double) + 8));
+  double* dst = ctx->packed.as<double>();
+  if (nt > 0) SR_HIP_CHECK(sr_launch_pack_partials(ctx->d_out_sum, ctx->d_out_flag, int(nt), dst, s));
+  // every rank enters the collective, also with an empty batch (the counts agree: same trees)
+  const ncclResult_t r = ncclAllReduce(dst, dst, n, ncclDouble, ncclSum, ctx->comm, s);
+  if (r != ncclSuccess) return set_error(SR_ERR_HIP, std::string("ncclAllReduce: ") + ncclGetErrorString(r));
+  if (nt > 0) SR_HIP_CHECK(hipMemcpyAsync(out_host, dst, n * sizeof(double), hipMemcpyDeviceToHost, s));
   SR_HIP_CHECK(hipStreamSynchronize(s));
   ctx->last_eval_ms = chunk_kernel_ms(ctx);
   ctx->last_total_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();

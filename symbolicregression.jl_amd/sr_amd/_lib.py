@@ -48,6 +48,10 @@ EXPORTED_SYMBOLS = (
     "sr_eval_tree_array",
     "sr_eval_loss_partials",
     "sr_eval_loss_partials_packed",
+    "sr_comm_unique_id",
+    "sr_comm_init",
+    "sr_comm_destroy",
+    "sr_eval_loss_partials_allreduce",
     "sr_max_checks",
     "sr_jsum_range_count",
     "sr_jsum_ranges",
@@ -171,6 +175,10 @@ def _load():
             [P, P, c_int, POINTER(SrTreeBatch), c_int64, c_int, P, P, c_int],
         ),
         "sr_max_checks": (c_int, [P, c_int, c_int, POINTER(SrTreeBatch), POINTER(c_int)]),
+        "sr_comm_unique_id": (c_int, [P]),
+        "sr_comm_init": (c_int, [P, c_int, c_int, P]),
+        "sr_comm_destroy": (c_int, [P]),
+        "sr_eval_loss_partials_allreduce": (c_int, [P, P, c_int, POINTER(SrTreeBatch), c_int64, c_int, P]),
         "sr_eval_loss_partials_packed": (
             c_int,
             [P, P, c_int, POINTER(SrTreeBatch), c_int64, c_int, P, c_int],

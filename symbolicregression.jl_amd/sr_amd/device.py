@@ -19,6 +19,7 @@ class DeviceContext:
         _lib.check(_lib.lib.sr_init(device, ctypes.byref(h)))
         self.handle = h
         self._opsets: dict = {}
+        self.has_comm = False  # RCCL communicator created (sr_amd.distributed.init_device_comm)
 
     def opset_id(self, operators) -> int:
         key = operators.key()

@@ -46,6 +46,42 @@ def gpu_partials_packed(tb, shard, options, n_total, *, device_tensor=False, ctx
     return out
 
 
+SR_COMM_ID_BYTES = 128
+
+
+def init_device_comm(group=None, ctx=None):
+    """Create this rank's RCCL communicator inside the library (C ABI sr_comm_*), on the library's
+    own HIP runtime; `group` is any torch.distributed group used only to broadcast rank 0's unique
+    id (gloo: no torch GPU state, which could not share the device with the library's runtime).
+    After this, `eval_loss_sharded` sums the partials with one device all-reduce over xGMI."""
+    import torch.distributed as dist
+
+    ctx = ctx or get_context()
+    buf = ctypes.create_string_buffer(SR_COMM_ID_BYTES)
+    if dist.get_rank(group) == 0:
+        _lib.check(_lib.lib.sr_comm_unique_id(ctypes.cast(buf, ctypes.c_void_p)))
+    obj = [bytes(buf.raw)]
+    dist.broadcast_object_list(obj, src=0, group=group)
+    raw = ctypes.create_string_buffer(obj[0], SR_COMM_ID_BYTES)
+    _lib.check(_lib.lib.sr_comm_init(ctx.handle, dist.get_world_size(group), dist.get_rank(group),
+                                     ctypes.cast(raw, ctypes.c_void_p)))
+    ctx.has_comm = True
+    return ctx
+
+
+def gpu_partials_allreduce(tb, shard, options, n_total, ctx=None):
+    """Every rank's packed partials [4, n_trees], summed on the devices by the library's RCCL
+    communicator (init_device_comm) -> numpy on every rank."""
+    ctx = ctx or get_context()
+    nt = tb.n_trees
+    s = tb.to_struct()
+    out = np.zeros((4, max(nt, 1)), dtype=np.float64)
+    _lib.check(_lib.lib.sr_eval_loss_partials_allreduce(
+        ctx.handle, shard.device_handle(ctx), ctx.opset_id(options.operators), ctypes.byref(s), int(n_total),
+        ctx.loss_code(options), out.ctypes.data_as(ctypes.c_void_p)))
+    return out[:, :nt]
+
+
 def jsum_ranges(row_offset, n_local, n_total):
     """(lo, hi, leaf, head) of the row ranges a shard folds for the exact check (C ABI)."""
     n = ctypes.c_int64()
@@ -132,15 +168,20 @@ def eval_loss_sharded(trees, shard, options, n_total, *, denom=None, group=None,
     full = shard.full
     tb = _as_batch(trees, full.dtype)
     on_gpu = dist.get_backend(group) == "nccl"
-    partials_fn = partials_fn or (lambda tb_: gpu_partials_packed(tb_, shard, options, n_total, device_tensor=on_gpu))
-    packed = partials_fn(tb)
-    t = packed if isinstance(packed, torch.Tensor) else torch.from_numpy(np.ascontiguousarray(packed))
-    if on_gpu and not t.is_cuda:
-        t = t.cuda()
-    t = t.contiguous()
-    # the path's one exchange step: every rank's [4, n_trees] partials, summed
-    dist.all_reduce(t, op=dist.ReduceOp.SUM, group=group)
-    sums, flags = unpack_flags(t.cpu().numpy())
+    if partials_fn is None and getattr(get_context(), "has_comm", False):
+        # the path's one exchange step on the devices: the library's RCCL all-reduce (init_device_comm)
+        packed = gpu_partials_allreduce(tb, shard, options, n_total)
+    else:
+        partials_fn = partials_fn or (lambda tb_: gpu_partials_packed(tb_, shard, options, n_total, device_tensor=on_gpu))
+        packed = partials_fn(tb)
+        t = packed if isinstance(packed, torch.Tensor) else torch.from_numpy(np.ascontiguousarray(packed))
+        if on_gpu and not t.is_cuda:
+            t = t.cuda()
+        t = t.contiguous()
+        # the path's one exchange step: every rank's [4, n_trees] partials, summed
+        dist.all_reduce(t, op=dist.ReduceOp.SUM, group=group)
+        packed = t.cpu().numpy()
+    sums, flags = unpack_flags(packed)
     big = np.nonzero(((flags & (_lib.SR_FLAG_NONFINITE | _lib.SR_FLAG_STATIC)) == 0) &
                      ((flags & _lib.SR_FLAG_BIG) != 0))[0]
     ok = None
@@ -151,9 +192,13 @@ def eval_loss_sharded(trees, shard, options, n_total, *, denom=None, group=None,
         dist.all_gather_object(sizes, int(shard.n), group=group)
         offs = np.concatenate([[0], np.cumsum(sizes)]).astype(np.int64)
         rank = dist.get_rank(group)
-        mc = gpu_max_checks(tb, options) if exact_fn is None else 1
-        exact_fn = exact_fn or (lambda tb_, lst, m, off: gpu_jsum(tb_, shard, options, lst, m, off, n_total))
-        mine = np.ascontiguousarray(exact_fn(tb, big, mc, int(offs[rank])))
+        if exact_fn is None:
+            # only the BIG trees are compiled again (a sub-batch: the check numbering is per tree)
+            sub = tb.take(big)
+            mc = gpu_max_checks(sub, options)
+            mine = np.ascontiguousarray(gpu_jsum(sub, shard, options, np.arange(big.size), mc, int(offs[rank]), n_total))
+        else:
+            mine = np.ascontiguousarray(exact_fn(tb, big, 1, int(offs[rank])))
         mc = mine.shape[1]
         every = [None] * world
         dist.all_gather_object(every, mine, group=group)

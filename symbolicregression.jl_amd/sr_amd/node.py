@@ -260,6 +260,15 @@ class TreeBatch:
     def tree_sizes(self) -> np.ndarray:
         return np.diff(self.offsets)
 
+    def take(self, idx) -> "TreeBatch":
+        """The batch of trees idx (in that order): the node arrays of each, concatenated."""
+        idx = np.asarray(idx, dtype=np.int64)
+        b, e = self.offsets[idx], self.offsets[idx + 1]
+        nodes = np.concatenate([np.arange(x, y) for x, y in zip(b, e)]) if idx.size else np.zeros(0, np.int64)
+        offs = np.concatenate([[0], np.cumsum(e - b)])
+        return TreeBatch(offs, self.degree[nodes], self.op[nodes], self.feature[nodes], self.constant[nodes],
+                         self.val[nodes])
+
     def to_struct(self) -> _lib.SrTreeBatch:
         def ptr(a, t):
             return a.ctypes.data_as(ctypes.POINTER(t))
