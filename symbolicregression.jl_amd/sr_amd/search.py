@@ -302,6 +302,10 @@ def _torch_comm():
         return None
     if not (tdist.is_available() and tdist.is_initialized()) or tdist.get_world_size() == 1:
         return None
+    if tdist.get_backend() != "gloo":
+        # the exchange is a few KB of host objects; an "nccl" group would make torch initialise its
+        # own HIP runtime on the GPU, which cannot share the device with the library's
+        raise RuntimeError("equation_search(distributed=True) needs a gloo process group (CPU objects only)")
     world = tdist.get_world_size()
 
     def allgather(obj):
