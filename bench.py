@@ -1,28 +1,36 @@
 #!/usr/bin/env python3
-"""Benchmark: batched eval_loss throughput (BASELINE.json metric) on C2 (default) or C4.
+"""Benchmark: batched eval_loss throughput (BASELINE.json metric) on C2, with C4, tree sharding and the
+search-iterations half of the metric as sub-objects.
 
 One step = score the whole population once: compile the trees into device programs, upload, run
 the interpreter over all rows, reduce, copy losses back, exact re-check when needed, finalize (the
 full cost of one `eval_cost_batch` call of a search iteration).  Trees and data are synthetic
 (seeded), generated before timing; the dataset is resident in HBM when the timed region starts.
 
-  python bench.py [--gpus N] [--steps K] [--warmup W] [--workload c2|c4]
+  python bench.py [--gpus N] [--steps K] [--warmup W]
 
-c2 (default): BASELINE config 2, 10k trees x 1M rows x 5 features per GPU.  N > 1 (launched by
-  torch.distributed.run): weak scaling — every rank holds its own 1M-row shard of one N x 1M-row
-  dataset; the ranks combine per-tree partials with ONE all-reduce of a packed device buffer.
-c4: BASELINE config 4, 100k trees x 64M rows (2^26) x 5 features, FIXED total rows sharded n/N
-  over the N ranks (strong scaling: the configuration the 85 % scaling target is quoted on).
+--gpus N without a launcher (WORLD_SIZE unset) starts N rank processes itself (fresh children of a
+parent that makes no GPU call; rank 0 prints).  Under torch.distributed.run the launcher's ranks are
+used.  One process per GPU (LOCAL_RANK); a gloo group is the CPU channel (unique id, barriers,
+max-over-ranks timing); every data-path exchange is the library's own RCCL over xGMI.
 
-Rank 0 prints one JSON line.  Beside the headline it reports the interpreter's roofline (HIP-event
-kernel time on the library's streams), the same population restricted to its complete trees
-(no dead-tree skipping can flatter it), the population in Float64 (C5's type, against the FP64
-peak), the CPU baseline (the C oracle on the host's cores) and the C1 search throughput.
+Headline, C2 (BASELINE config 2): 10k trees x 1M rows x 5 features PER GPU, weak scaling.  N = 1:
+  the single-GPU call (sr_eval_loss_batch).  N > 1: rank r holds its own 1M-row shard of an N x 1M-row
+  dataset, and the step is the row-sharded call (sr_eval_loss_sharded: ONE RCCL all-reduce of packed
+  per-tree partials).  `c2_sharded_path` (N = 1) times the same step through the row-sharded call at
+  world size 1, so the scaling denominator's code path is on record.
+Sub-objects measured at every N, each through the same code path at every N:
+  c4            BASELINE config 4: 100k trees x 64M (2^26) rows, rows sharded n/N (strong scaling).
+  tree_sharded  the C2 population over a replicated 1M-row dataset, trees dealt over the N ranks.
+Rank 0 at N = 1 also reports: the interpreter roofline, the complete-trees-only and Float64 lines,
+the CPU baseline (the C oracle on the host cores) and the parity of the timed step against it, and
+the search throughput (C1 and C3) with the same engine scored by the C port as its CPU baseline.
 """
 import argparse
-import ctypes
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -32,13 +40,63 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(ROOT, "symbolicregression.jl_amd"))
 sys.path.insert(0, os.path.join(ROOT, "oracle"))
 
-import sr_amd  # noqa: E402
-from sr_amd import Dataset, Options, _lib, flatten_trees, gen_random_population  # noqa: E402
-
-PEAK_FP32_TFLOPS = 157.3  # MI355X FP32 vector dense peak (packed FMA), MI355X_MICROARCH.md
+PEAK_FP32_TFLOPS = 157.3  # MI355X FP32 vector dense peak, MI355X_MICROARCH.md
 PEAK_FP64_TFLOPS = 78.6   # MI355X FP64 vector dense peak
+PEAK_HBM_GBPS = 8000.0
 C2_OPS = dict(binary_operators=["+", "-", "*", "/"], unary_operators=["cos", "exp", "log"])
 BLOCK = 1 << 20           # C4 data is generated in seeded 1M-row blocks (shards are whole blocks)
+
+
+def parse_args(argv=None):
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=8)
+    ap.add_argument("--rows", type=int, default=0, help="C2 rows per GPU (default 2^20)")
+    ap.add_argument("--trees", type=int, default=0, help="C2 trees (default 10k)")
+    ap.add_argument("--c4-rows", type=int, default=1 << 26, help="C4 total rows (multiple of 2^20 x N)")
+    ap.add_argument("--c4-trees", type=int, default=100_000)
+    ap.add_argument("--c4-steps", type=int, default=3)
+    ap.add_argument("--no-c4", action="store_true")
+    ap.add_argument("--no-tree-sharded", action="store_true")
+    ap.add_argument("--cpu-trees", type=int, default=0, help="CPU-baseline tree sample (0 = auto, ~15 s)")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-extra", action="store_true", help="skip the complete-only and Float64 lines")
+    ap.add_argument("--search-iters", type=int, default=40, help="iterations of the C1 / C3 searches (0 = skip)")
+    ap.add_argument("--search-cpu-iters", type=int, default=0,
+                    help="iterations of the CPU-port searches (0 = C1: all, C3: 2, a bounded sample)")
+    return ap.parse_args(argv)
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def spawn_ranks(n):
+    """`--gpus N` without a launcher: N fresh rank processes (this parent has made no GPU call and
+    never re-execs); each inherits stdout, rank 0 prints the line.  A failed rank stops the others."""
+    port = _free_port()
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env))
+    rc = 0
+    alive = set(range(n))
+    while alive:
+        for r in list(alive):
+            code = procs[r].poll()
+            if code is None:
+                continue
+            alive.discard(r)
+            if code != 0:
+                rc = rc or code
+                for q in alive:
+                    procs[q].terminate()
+        time.sleep(0.05)
+    return rc
 
 
 def c2_data(n_rows, rank, nf=5, dtype=np.float32):
@@ -60,11 +118,38 @@ def c4_shard(rank, world, rows_total, nf=5):
         xb = rng.standard_normal((nf, BLOCK), dtype=np.float32)
         X[:, j * BLOCK:(j + 1) * BLOCK] = xb
         y[j * BLOCK:(j + 1) * BLOCK] = 2 * np.cos(xb[3]) + xb[0] ** 2 - 2 + 0.1 * rng.standard_normal(BLOCK, dtype=np.float32)
-    return X, y, b0 * BLOCK
+    return X, y
+
+
+class Comm:
+    """The CPU channel: a gloo group (world 1 too, so the sharded code path is the same at every N)."""
+
+    def __init__(self, world, rank):
+        import torch.distributed as tdist
+
+        self.d = tdist
+        self.world, self.rank = world, rank
+        addr = os.environ.get("MASTER_ADDR", "127.0.0.1")
+        port = os.environ.get("MASTER_PORT") or str(_free_port())
+        tdist.init_process_group("gloo", init_method=f"tcp://{addr}:{port}", rank=rank, world_size=world)
+
+    def barrier(self):
+        self.d.barrier()
+
+    def max(self, v):
+        import torch
+
+        t = torch.tensor([float(v)], dtype=torch.float64)
+        self.d.all_reduce(t, op=self.d.ReduceOp.MAX)
+        return float(t.item())
+
+    def close(self):
+        self.d.destroy_process_group()
 
 
 def timed(step, steps, warmup, barrier):
-    """W untimed steps, then K timed steps between barriers (+ device sync)."""
+    """W untimed steps, then K timed steps between barriers (every library call returns after its
+    streams have drained: the device is synchronised on both sides)."""
     for _ in range(warmup):
         step()
     barrier()
@@ -79,23 +164,32 @@ def timed(step, steps, warmup, barrier):
     return dt, step_ms, kernel_ms
 
 
-def single_gpu_step(ctx, tb, ds, opts, dtype=np.float32):
-    """One sr_eval_loss_batch over the whole population -> its interpreter time (ms)."""
+def lib_step(ctx, fn, state):
+    """Wrap one library call: its interpreter kernel time (sum of launches), busy time (union) and launches."""
+    def step():
+        fn()
+        k, _ = ctx.last_kernel_ms()
+        state.setdefault("busy", []).append(ctx.last_busy_ms())
+        state.setdefault("launches", []).append(ctx.last_launches())
+        return k
+    return step
+
+
+def single_gpu_call(ctx, tb, ds, opts, dtype=np.float32):
+    import ctypes
+
+    from sr_amd import _lib
+
     dsh = ds.device_handle(ctx)
     oid = ctx.opset_id(opts.operators)
     s = tb.to_struct()
-    losses = np.empty(tb.n_trees, dtype=dtype)
-    comp = np.empty(tb.n_trees, dtype=np.uint8)
-    state = {"launches": []}
+    out = {"loss": np.empty(tb.n_trees, dtype=dtype), "comp": np.empty(tb.n_trees, dtype=np.uint8)}
 
-    def step():
+    def call():
         _lib.check(_lib.lib.sr_eval_loss_batch(ctx.handle, dsh, oid, ctypes.byref(s), None, 0, 0,
-                                               losses.ctypes.data_as(ctypes.c_void_p),
-                                               comp.ctypes.data_as(ctypes.c_void_p)))
-        state["launches"].append(ctx.last_launches())
-        return ctx.last_kernel_ms()[0]
-
-    return step, losses, comp, state
+                                               out["loss"].ctypes.data_as(ctypes.c_void_p),
+                                               out["comp"].ctypes.data_as(ctypes.c_void_p)))
+    return call, out
 
 
 def roofline(flops, kernel_ms, peak, **extra):
@@ -107,204 +201,267 @@ def roofline(flops, kernel_ms, peak, **extra):
 
 
 def main():
-    ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=8)
-    ap.add_argument("--workload", choices=["c2", "c4"], default="c2")
-    ap.add_argument("--rows", type=int, default=0, help="c2: rows per GPU (default 2^20); c4: total rows (2^26)")
-    ap.add_argument("--trees", type=int, default=0, help="default 10k (c2) / 100k (c4)")
-    ap.add_argument("--cpu-trees", type=int, default=0, help="CPU-baseline tree sample (0 = auto)")
-    ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--no-extra", action="store_true", help="skip the complete-only and Float64 lines")
-    ap.add_argument("--search-iters", type=int, default=40,
-                    help="iterations of the C1 search for the 'search iterations/sec' figure (0 = skip)")
-    args = ap.parse_args()
-
+    args = parse_args()
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        sys.exit(spawn_ranks(args.gpus))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
-    dist = None
-    # SR_BENCH_FORCE_DIST=1 (under torch.distributed.run): the multi-GPU code path at world size 1
-    # (rehearses the scaling run's rendezvous, RCCL communicator and sharded step on one GPU)
-    if world > 1 or os.environ.get("SR_BENCH_FORCE_DIST") == "1":
-        import torch.distributed as tdist
 
-        # gloo (CPU) for the rendezvous, the barrier and the max-over-ranks timing; the data path's
-        # exchange is the library's own RCCL all-reduce over xGMI (sr_comm_*): torch's bundled HIP
-        # runtime cannot share a GPU with the library's in one process, so torch never touches it
-        tdist.init_process_group(backend="gloo")
-        dist = tdist
-    c4 = args.workload == "c4"
-    if c4 and args.steps == 20 and args.warmup == 8:  # a C4 step is ~2 s on one GPU: fewer by default
-        args.steps, args.warmup = 5, 2
+    import sr_amd  # noqa: E402  (after the spawn decision: the parent never loads the HIP runtime)
+    from sr_amd import Dataset, Options, flatten_trees, gen_random_batch, gen_random_population
+    from sr_amd.distributed import comm_info, eval_loss_sharded, eval_loss_tree_sharded, init_device_comm
+
+    comm = Comm(world, rank)
+    ctx = sr_amd.get_context(local_rank)
+    init_device_comm(ctx=ctx)
+    cinfo = comm_info(ctx)
 
     opts = Options(**C2_OPS)
-    nt = args.trees or (100_000 if c4 else 10_000)
-    trees = gen_random_population(nt, opts, 5, max_size=30, seed=4 if c4 else 1)
+    nt = args.trees or 10_000
+    trees = gen_random_population(nt, opts, 5, max_size=30, seed=1)
     tb = flatten_trees(trees, np.float32)
-    if c4:
-        rows_total = args.rows or (1 << 26)
-        if rows_total % (BLOCK * world):
-            raise SystemExit("c4: total rows must be a multiple of 2^20 x N")
-        X, y, _ = c4_shard(rank, world, rows_total)
-    else:
-        rows_total = (args.rows or (1 << 20)) * world
-        X, y = c2_data(rows_total // world, rank)
-    n_local = X.shape[1]
-    ctx = sr_amd.get_context(local_rank)
-    if dist is not None:
-        from sr_amd.distributed import init_device_comm
-
-        init_device_comm(ctx=ctx)
+    rows = args.rows or (1 << 20)
+    rows_total = rows * world
+    X, y = c2_data(rows, rank)
     ds = Dataset(X, y)
     ds.device_handle(ctx)  # upload before timing
-
-    if dist is None:
-        step, losses, comp, state = single_gpu_step(ctx, tb, ds, opts)
-
-        def barrier():
-            pass
-    else:
-        from sr_amd.distributed import eval_loss_sharded
-
-        result, state = {}, {"launches": []}
-
-        def step():
-            result["loss"], result["comp"] = eval_loss_sharded(tb, ds, opts, rows_total)
-            state["launches"].append(ctx.last_launches())
-            return ctx.last_kernel_ms()[0]
-
-        def barrier():
-            # every library call returns after its stream has drained (device synchronised)
-            dist.barrier()
-
-    dt, step_ms, kernel_ms = timed(step, args.steps, args.warmup, barrier)
-    if dist is not None:
-        import torch
-
-        tt = torch.tensor([dt], dtype=torch.float64)
-        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-        dt = float(tt.item())
-        comp = result["comp"]
-
     nodes, ops = int(tb.n_nodes), int(tb.n_operator_nodes)
-    node_evals = float(nodes) * float(rows_total)  # all ranks
-    value = node_evals * args.steps / dt
+
+    # ---- headline: C2, weak scaling
+    state = {}
+    if world == 1:
+        call, out = single_gpu_call(ctx, tb, ds, opts)
+        path = "single-GPU sr_eval_loss_batch"
+    else:
+        out = {}
+
+        def call():
+            out["loss"], out["comp"] = eval_loss_sharded(tb, ds, opts)
+        path = "row-sharded sr_eval_loss_sharded (one RCCL all-reduce of packed [4, n_trees] partials per step)"
+    dt, step_ms, kernel_ms = timed(lib_step(ctx, call, state), args.steps, args.warmup, comm.barrier)
+    dt = comm.max(dt)
+    comp = np.asarray(out["comp"]).astype(bool)
+    loss = np.asarray(out["loss"]).copy()
+    value = float(nodes) * float(rows_total) * args.steps / dt
     kmean = float(np.mean(kernel_ms))
-    n_launch = int(round(float(np.mean(state["launches"][-args.steps:])))) if state["launches"] else 1
-    flops_per_step = float(n_local) * (ops + 3 * nt)  # this GPU's interpreter work per step
-    traffic = measured_traffic(args.workload)
-    rpl = ctx.last_rows_per_lane()  # the interpreter build the library picked for this view
-    frac_complete = float(np.mean(np.asarray(comp).astype(bool)))
+    busy = float(np.mean(state["busy"][-args.steps:]))
+    n_launch = int(round(float(np.mean(state["launches"][-args.steps:]))))
+    flops_per_step = float(rows) * (ops + 3 * nt)  # this GPU's interpreter work per step
+    traffic = measured_traffic("c2")
+    rpl = ctx.last_rows_per_lane()
+
+    subs = {}
+    if world == 1:
+        subs["c2_sharded_path"] = sharded_path_line(ctx, tb, ds, opts, eval_loss_sharded, args, comm, nodes, rows)
+    if not args.no_tree_sharded:
+        subs["tree_sharded"] = tree_sharded_line(ctx, tb, opts, eval_loss_tree_sharded, args, comm, world, rank,
+                                                 nodes, rows, loss if world == 1 else None, comp if world == 1 else None)
+    if not args.no_c4:
+        subs["c4"] = c4_line(ctx, opts, eval_loss_sharded, gen_random_batch, Dataset, args, comm, world, rank)
 
     extra = {}
-    if rank == 0 and world == 1 and not args.no_extra and not c4:
-        extra = extra_lines(ctx, opts, trees, np.asarray(comp).astype(bool), X, y, args)
-    cpu = None
+    if rank == 0 and world == 1 and not args.no_extra:
+        extra = extra_lines(ctx, opts, trees, comp, X, y, args)
+    cpu, parity = None, None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        cpu = cpu_baseline(opts, tb, X[:, :min(n_local, 1 << 20)], y[:min(n_local, 1 << 20)], args.cpu_trees)
+        cpu, parity = cpu_baseline_and_parity(opts, tb, X, y, args.cpu_trees, loss, comp)
     search = None
-    if rank == 0 and world == 1 and args.search_iters > 0 and not c4:
-        search = search_throughput(args.search_iters)
+    if rank == 0 and world == 1 and args.search_iters > 0:
+        search = search_lines(args)
 
     if rank == 0:
-        if c4:
-            workload = (f"C4 row-sharded eval_loss: {nt // 1000}k random trees (size U{{1..30}}; +,-,*,/,cos,exp,"
-                        f"safe_log) x {rows_total >> 20}M rows x 5 features, rows sharded n/{world}")
-        else:
-            workload = (f"C2 batched eval_loss: {nt // 1000}k random trees (size U{{1..30}}; +,-,*,/,cos,exp,safe_log)"
-                        f" x {n_local >> 20}M rows x 5 features per GPU")
+        algo_bytes = algorithmic_bytes(nt, rows, n_launch, rpl)
         line = {
             "metric": "tree-node x row evals/sec (batched eval_loss, fp32)",
             "value": value,
             "unit": "node-evals/s",
             "n_gpus": world,
+            "world_size_rccl": cinfo["nranks"],
             "steps": args.steps,
             "warmup": args.warmup,
             "ms_per_step": dt / args.steps * 1e3,
             "step_ms_min_median_max": [float(step_ms.min()), float(np.median(step_ms)), float(step_ms.max())],
             "higher_is_better": True,
-            "scaling": "strong" if c4 else "weak",
+            "scaling": "weak",
             "vs_baseline": None,
             "dtype": "f32",
             "data": "synthetic (seeded): gen_random_tree_fixed_size population, X~N(0,1), y=2cos(x4)+x1^2-2+0.1N",
             "config": {
-                "workload": workload,
+                "workload": (f"C2 batched eval_loss: {nt // 1000}k random trees (size U{{1..30}}; +,-,*,/,cos,exp,"
+                             f"safe_log) x {rows >> 20}M rows x 5 features per GPU"),
                 "n_trees": nt,
                 "tree_nodes": nodes,
                 "operator_nodes": ops,
-                "rows_per_gpu": n_local,
+                "rows_per_gpu": rows,
                 "rows_total": rows_total,
                 "nfeatures": 5,
                 "parallelism": (f"rows sharded x{world}; one RCCL all-reduce of packed [4, n_trees] per-tree partials"
                                 if world > 1 else "single GPU"),
-                "fraction_complete": frac_complete,
+                "code_path": path,
+                "fraction_complete": float(np.mean(comp)),
+                "runtime": {"hip": cinfo.get("hip"), "rccl": cinfo.get("rccl")},
             },
             "roofline": roofline(
                 flops_per_step, kmean, PEAK_FP32_TFLOPS,
+                busy_ms_per_step=busy,
                 traffic=traffic.get("hbm_read_bytes_per_step") if traffic else None,
                 traffic_source=traffic.get("source") if traffic else None,
                 kernel=(f"sr_tile_kernel<float,{rpl},LOSS,gather=false,BASIC,W=4,L2"
                         + (",register stack>" if rpl >= 16 else ">")),
                 launches_per_step=n_launch,
                 kernel_ms_convention=("per step: sum of the interpreter launches' HIP-event durations on the "
-                                      "library's streams (= the kernel-trace sum: overlapping chunks count fully)"),
+                                      "library's streams (= the kernel-trace sum); busy_ms_per_step = the union "
+                                      "of those intervals (the two pipeline streams overlap)"),
                 flop_convention="n_rows * sum_t(n_op(t) + 3), 1 flop per operator incl. transcendentals (SURVEY 8d)",
-                algorithmic_bytes_per_step=algorithmic_bytes(nt, n_local, n_launch, rpl),
+                algorithmic_bytes_per_step=algo_bytes,
+                algorithmic_GBps=algo_bytes / (kmean * 1e-3) / 1e9,
                 bytes_convention="ceil(n_trees/G) passes x (nf+1) x n_rows x 4 B; X/y re-reads are served from L2/MALL",
             ),
             "cpu_baseline": cpu,
+            "parity": parity,
             "search": search,
         }
-        line["roofline"]["algorithmic_GBps"] = line["roofline"]["algorithmic_bytes_per_step"] / (kmean * 1e-3) / 1e9
+        line.update(subs)
         line.update(extra)
         print(json.dumps(line), flush=True)
-    if dist is not None:
-        dist.destroy_process_group()
+    comm.close()
+
+
+def sharded_path_line(ctx, tb, ds, opts, eval_loss_sharded, args, comm, nodes, rows):
+    """The C2 step through the row-sharded call at world size 1 (the code path every N > 1 runs)."""
+    st = {}
+    res = {}
+
+    def call():
+        res["l"], res["c"] = eval_loss_sharded(tb, ds, opts)
+    dt, step_ms, kms = timed(lib_step(ctx, call, st), args.steps, args.warmup, comm.barrier)
+    return {"ms_per_step": dt / args.steps * 1e3, "value": float(nodes) * rows * args.steps / dt,
+            "kernel_ms_per_step": float(np.mean(kms)), "busy_ms_per_step": float(np.mean(st["busy"][-args.steps:])),
+            "derived_columns": ctx.last_derived_columns(), "exact_trees": ctx.last_exact_trees(),
+            "what": "C2 through sr_eval_loss_sharded at world size 1 (the N > 1 code path)"}
+
+
+def tree_sharded_line(ctx, tb, opts, eval_loss_tree_sharded, args, comm, world, rank, nodes, rows, ref_loss, ref_comp):
+    """The C2 population over one replicated 1M-row dataset (rank 0's data on every rank), trees dealt
+    over the ranks: strong scaling of tree sharding."""
+    from sr_amd import Dataset
+
+    X, y = c2_data(rows, 0)
+    ds = Dataset(X, y)
+    ds.device_handle(ctx)
+    res = {}
+
+    def step():
+        t = time.perf_counter()
+        res["l"], res["c"] = eval_loss_tree_sharded(tb, ds, opts)
+        return (time.perf_counter() - t) * 1e3
+    steps, warm = max(5, args.steps // 2), 3
+    dt, step_ms, _ = timed(step, steps, warm, comm.barrier)
+    dt = comm.max(dt)
+    out = {"value": float(nodes) * rows * steps / dt, "unit": "node-evals/s", "ms_per_step": dt / steps * 1e3,
+           "scaling": "strong", "n_gpus": world,
+           "workload": f"C2 population ({tb.n_trees} trees) x {rows >> 20}M rows replicated, trees dealt over {world} ranks"}
+    if ref_comp is not None:  # N = 1: the same answer as the single-GPU call
+        out["equals_single_gpu"] = bool(np.array_equal(res["c"], ref_comp) and
+                                        np.array_equal(res["l"][ref_comp], ref_loss[ref_comp]))
+    ds.free_device()
+    return out
+
+
+def c4_line(ctx, opts, eval_loss_sharded, gen_random_batch, Dataset, args, comm, world, rank):
+    """BASELINE config 4: 100k trees x 64M rows sharded n/N, through sr_eval_loss_sharded at every N."""
+    rows_total = args.c4_rows
+    if rows_total % (BLOCK * world):
+        return {"skipped": f"C4 total rows {rows_total} is not a multiple of 2^20 x {world}"}
+    tb = gen_random_batch(args.c4_trees, opts, 5, max_size=30, seed=4)
+    X, y = c4_shard(rank, world, rows_total)
+    ds = Dataset(X, y)
+    ds.device_handle(ctx)
+    del X, y
+    st = {}
+    res = {}
+
+    def call():
+        res["l"], res["c"] = eval_loss_sharded(tb, ds, opts)
+    dt, step_ms, kms = timed(lib_step(ctx, call, st), args.c4_steps, 1, comm.barrier)
+    dt = comm.max(dt)
+    n_local = rows_total // world
+    kmean, busy = float(np.mean(kms)), float(np.mean(st["busy"][-args.c4_steps:]))
+    flops = float(n_local) * (tb.n_operator_nodes + 3 * tb.n_trees)
+    traffic = measured_traffic("c4")
+    nl = int(round(float(np.mean(st["launches"][-args.c4_steps:]))))
+    algo = algorithmic_bytes(tb.n_trees, n_local, nl, ctx.last_rows_per_lane())
+    out = {"metric": "tree-node x row evals/sec (batched eval_loss, fp32)",
+           "value": float(tb.n_nodes) * rows_total * args.c4_steps / dt, "unit": "node-evals/s",
+           "ms_per_step": dt / args.c4_steps * 1e3, "steps": args.c4_steps, "warmup": 1, "n_gpus": world,
+           "scaling": "strong",
+           "workload": (f"C4 row-sharded eval_loss: {tb.n_trees // 1000}k random trees (size U{{1..30}}; native "
+                        f"generator, seed 4) x {rows_total >> 20}M rows x 5 features, rows sharded n/{world}"),
+           "code_path": "sr_eval_loss_sharded (same at every N)", "rows_per_gpu": n_local,
+           "fraction_complete": float(np.mean(res["c"])),
+           "roofline": roofline(flops, kmean, PEAK_FP32_TFLOPS, busy_ms_per_step=busy,
+                                algorithmic_bytes_per_step=algo, algorithmic_GBps=algo / (kmean * 1e-3) / 1e9,
+                                traffic=traffic.get("hbm_read_bytes_per_step") if traffic else None,
+                                traffic_source=traffic.get("source") if traffic else None,
+                                hbm_GBps=(traffic["hbm_read_bytes_per_step"] / (kmean * 1e-3) / 1e9
+                                          if traffic else None), hbm_peak_GBps=PEAK_HBM_GBPS)}
+    ds.free_device()
+    return out
 
 
 def extra_lines(ctx, opts, trees, comp, X, y, args):
     """The same C2 population (i) restricted to its complete trees — the interpreter's roofline
-    without dead-tree skipping — and (ii) in Float64 against the FP64 vector peak."""
+    without dead-tree skipping — and (ii) in Float64 against the FP64 peak, each with its per-launch
+    breakdown (trees per workgroup G, workgroups, per-chunk time)."""
+    from sr_amd import Dataset, flatten_trees
+
     out = {}
     steps, warm = max(5, args.steps // 2), 3
     live = [t for t, c in zip(trees, comp) if c]
     tbc = flatten_trees(live, np.float32)
     dsc = Dataset(X, y)
-    step, _, _, _ = single_gpu_step(ctx, tbc, dsc, opts)
-    dt, _, kms = timed(step, steps, warm, lambda: None)
+    call, _ = single_gpu_call(ctx, tbc, dsc, opts)
+    st = {}
+    dt, _, kms = timed(lib_step(ctx, call, st), steps, warm, lambda: None)
     km = float(np.mean(kms))
     out["roofline_complete_only"] = roofline(
         float(X.shape[1]) * (tbc.n_operator_nodes + 3 * tbc.n_trees), km, PEAK_FP32_TFLOPS,
+        busy_ms_per_step=float(np.mean(st["busy"][-steps:])),
         n_trees=tbc.n_trees, ms_per_step=dt / steps * 1e3,
         node_evals_per_s=float(tbc.n_nodes) * X.shape[1] * steps / dt,
+        launches=chunk_groups(tbc.n_trees, X.shape[1], int(round(np.mean(st["launches"][-steps:]))),
+                              ctx.last_rows_per_lane()),
         what="the C2 population's complete trees only (every tree runs every row)")
     dsc.free_device()
     X64, y64 = X.astype(np.float64), y.astype(np.float64)
     tb64 = flatten_trees(trees, np.float64)
     ds64 = Dataset(X64, y64)
-    step, _, c64, _ = single_gpu_step(ctx, tb64, ds64, opts, np.float64)
-    dt, _, kms = timed(step, steps, warm, lambda: None)
+    call, o64 = single_gpu_call(ctx, tb64, ds64, opts, np.float64)
+    st = {}
+    dt, _, kms = timed(lib_step(ctx, call, st), steps, warm, lambda: None)
     km = float(np.mean(kms))
+    busy = float(np.mean(st["busy"][-steps:]))
     out["f64"] = roofline(
-        float(X.shape[1]) * (tb64.n_operator_nodes + 3 * tb64.n_trees), km, PEAK_FP64_TFLOPS,
-        kernel="sr_tile_kernel<double,4,LOSS,gather=false,BASIC>", ms_per_step=dt / steps * 1e3,
+        float(X.shape[1]) * (tb64.n_operator_nodes + 3 * tb64.n_trees), busy, PEAK_FP64_TFLOPS,
+        kernel_sum_ms_per_step=km, ms_per_step=dt / steps * 1e3,
+        kernel="sr_tile_kernel<double,4,LOSS,gather=false,BASIC>",
         node_evals_per_s=float(tb64.n_nodes) * X.shape[1] * steps / dt,
-        fraction_complete=float(np.mean(c64.astype(bool))),
+        fraction_complete=float(np.mean(o64["comp"].astype(bool))),
+        convention="achieved / frac from the device-busy time (union of the launch intervals), which fits in the step",
         what="the C2 population and data in Float64 (C5's element type)")
     ds64.free_device()
     return out
 
 
 def algorithmic_bytes(nt, rows, n_launch, rows_per_lane=8):
-    n_passes = sum(-(-c // g) for c, g in chunk_groups(nt, rows, n_launch, rows_per_lane))
+    n_passes = sum(-(-c // g) for c, g, _ in chunk_groups(nt, rows, n_launch, rows_per_lane))
     return float(n_passes) * (5 + 1) * float(rows) * 4.0
 
 
 def chunk_groups(nt, rows, n_launch, rows_per_lane=8):
-    """(trees, trees per workgroup) of each interpreter launch of a step, as csrc/sr_capi.cpp's
-    run_batch / make_grid split them (2 launches: a first chunk of nt/6 trees)."""
+    """(trees, trees per workgroup G, workgroups) of each interpreter launch of a step, as
+    csrc/sr_capi.cpp's run_batch / make_grid split them (2 launches: a first chunk of nt/6 trees)."""
     tiles = -(-rows // (64 * rows_per_lane))
     n_rb = -(-tiles // (-(-tiles // 256)))
     bounds = [0, nt // 6, nt] if n_launch == 2 else [nt * k // n_launch for k in range(n_launch + 1)]
@@ -316,38 +473,62 @@ def chunk_groups(nt, rows, n_launch, rows_per_lane=8):
             g = 128
             while g > 4 and n_rb * (-(-c // g)) < 4096:
                 g //= 2
-        out.append((c, max(1, min(g, c))))
+        g = max(1, min(g, c))
+        out.append((c, g, n_rb * (-(-c // g))))
     return out
 
 
-def search_throughput(niterations):
-    """BASELINE.json metric, second half: search iterations/sec on C1 (README example: X = randn(2, 100)
-    f64, ops + * / - cos exp, 20 populations, default options, 40 iterations), lock-step islands with
-    one batched device scoring call per evolution round (sr_amd.search.equation_search).
-    Iterations/sec counts completed s_r_cycles (one per island per iteration,
-    src/SymbolicRegression.jl:1091) per wall second."""
-    from sr_amd import equation_search
+def search_lines(args):
+    """BASELINE.json metric, second half: search iterations/sec of C1 (the README example) and C3
+    (Feynman-style 5-feature target, 100k rows, f32), device-scored, each beside the same engine with
+    the same seeds scored by the C port on the host cores (`sr_search_use_callbacks` with the
+    oracle's C scorers: a "port" CPU baseline)."""
+    from oracle import Oracle, SearchScorer
 
+    from sr_amd import Options, equation_search
+
+    threads = min(int(os.environ.get("OMP_NUM_THREADS", "0")) or (os.cpu_count() or 1), 16)
+    out = {}
     rng = np.random.default_rng(0)
-    Xs = rng.standard_normal((2, 100))
-    ys = 2 * np.cos(Xs[1]) + Xs[0] ** 2 - 2
-    sopts = Options(binary_operators=["+", "*", "/", "-"], unary_operators=["cos", "exp"], populations=20)
-    t0 = time.perf_counter()
-    res = equation_search(Xs, ys, niterations=niterations, options=sopts, seed=0)
-    wall = time.perf_counter() - t0
-    return {"metric": "search iterations/sec", "value": res.s_r_cycles / wall, "unit": "s_r_cycles/s",
-            "iterations_per_s": niterations / wall, "islands": sopts.populations, "iterations": niterations,
-            "wall_s": wall, "device_calls": res.device_calls,
-            "best_loss": float(min(m.loss for m in res.pareto_frontier)),
-            "config": "C1 README example, X=randn(2,100) f64, 20 populations, default options",
-            "cpu_baseline": None,
-            "cpu_baseline_note": "the reference's Julia search cannot run here (no Julia runtime in the image)"}
+    X1 = rng.standard_normal((2, 100))
+    y1 = 2 * np.cos(X1[1]) + X1[0] ** 2 - 2
+    o1 = Options(binary_operators=["+", "*", "/", "-"], unary_operators=["cos", "exp"], populations=20)
+    rng = np.random.default_rng(11)
+    X3 = rng.uniform(0.5, 2.0, (5, 100_000)).astype(np.float32)
+    y3 = (X3[0] * X3[1] * X3[2] / (X3[3] * X3[4] ** 2 + 1)).astype(np.float32)
+    o3 = Options(binary_operators=["+", "-", "*", "/"], unary_operators=["cos", "exp", "log"], populations=31)
+    for name, X, y, o, cpu_iters, cpu_threads, desc in (
+            ("c1", X1, y1, o1, args.search_cpu_iters or args.search_iters, 1,
+             "C1 README example: X=randn(2,100) f64, ops + * / - cos exp, 20 populations, default options"),
+            ("c3", X3, y3, o3, args.search_cpu_iters or 2, threads,
+             "C3: y = x1 x2 x3 / (x4 x5^2 + 1), X ~ U(0.5, 2) 5 x 100k f32, 31 populations, default options")):
+        t0 = time.perf_counter()
+        res = equation_search(X, y, niterations=args.search_iters, options=o, seed=0)
+        wall = time.perf_counter() - t0
+        line = {"metric": "search iterations/sec", "value": res.s_r_cycles / wall, "unit": "s_r_cycles/s",
+                "iterations_per_s": args.search_iters / wall, "islands": o.populations,
+                "iterations": args.search_iters, "wall_s": wall, "device_calls": res.device_calls,
+                "device_wall_s": res.device_s, "host_s": res.host_s,
+                "device_wall_per_call_us": res.device_s / max(res.device_calls, 1) * 1e6,
+                "best_loss": float(min(m.loss for m in res.pareto_frontier)), "config": desc}
+        sc = SearchScorer(Oracle.from_options(o), X, y, n_threads=cpu_threads)
+        t0 = time.perf_counter()
+        cres = equation_search(X, y, niterations=cpu_iters, options=o, seed=0, _native_scorer=sc)
+        cwall = time.perf_counter() - t0
+        line["cpu_baseline"] = {
+            "value": cres.s_r_cycles / cwall, "unit": "s_r_cycles/s", "iterations_per_s": cpu_iters / cwall,
+            "cores": cpu_threads, "kind": "port",
+            "sample": (f"the same engine and seeds, every scoring call answered by the C oracle on {cpu_threads} host "
+                       f"core(s) (loss folded in T; gradients by central differences as the reference's Optim "
+                       f"BFGS), {cpu_iters} iteration(s), {cwall:.1f} s, {cres.device_calls} scoring calls")}
+        out[name] = line
+    return out
 
 
 def measured_traffic(workload):
     """Per-step HBM bytes of the interpreter from the committed rocprofv3 PMC pass of this same
-    command (profiles/traffic.json, written by tools/trace_frac.py)."""
-    p = os.path.join(ROOT, "profiles", "traffic.json")
+    command (profiles/traffic.json / traffic_c4.json, written by tools/trace_frac.py)."""
+    p = os.path.join(ROOT, "profiles", "traffic.json" if workload == "c2" else f"traffic_{workload}.json")
     try:
         with open(p) as f:
             t = json.load(f)
@@ -355,39 +536,82 @@ def measured_traffic(workload):
         return None
     if t.get("workload") != workload or "hbm_read_bytes_per_step" not in t:
         return None
-    t["source"] = ("profiles/traffic.json (tools/bench_evidence.sh: rocprofv3 --pmc FETCH_SIZE of this bench "
-                   "command, x1024 B x2 gfx950, the timed steps' interpreter launches)")
+    t["source"] = (f"profiles/{os.path.basename(p)} (rocprofv3 --pmc FETCH_SIZE of the bench command, "
+                   "x1024 B x2 gfx950, the timed steps' interpreter launches)")
     return t
 
 
-def cpu_baseline(opts, tb, X, y, n_sample):
-    """Oracle (C port of DE's array-at-a-time evaluator, OpenMP over trees) on a bounded sample:
-    a strided subset of the same trees over the first <= 1M rows (~10-30 s on 16 host cores)."""
+def cpu_baseline_and_parity(opts, tb, X, y, n_sample, dev_loss, dev_comp):
+    """CPU baseline: the oracle (C port of DE's array-at-a-time evaluator, OpenMP over trees) on a
+    bounded sample — a strided subset of the same trees over the same 1M rows (~15 s on <= 16 host
+    cores), timed with the reference's sequential Float32 loss fold.
+    Parity of the TIMED step on that sample: flags bit-exact; every complete tree's loss within the
+    per-tree bar (1e-4 relative, or 4x the tree's own spread under +-1-ulp libm perturbations — the
+    tests' rule) against BOTH the oracle's f64 accumulation and the reference's sequential f32 fold."""
     from oracle import Oracle
 
     threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or min(os.cpu_count() or 1, 16)
     threads = min(threads, 16)
     orc = Oracle.from_options(opts)
 
-    def run(n):
+    def pick(n):
         step = max(1, tb.n_trees // n)
-        sub = tb.subset(np.arange(0, tb.n_trees, step)[:n])
+        idx = np.arange(0, tb.n_trees, step)[:n]
+        return idx, tb.take(idx), step
+
+    def run(n):
+        idx, sub, step = pick(n)
         t0 = time.perf_counter()
-        orc.eval_loss_batch(sub, X, y, accum="ref", n_threads=threads)
-        return sub, step, time.perf_counter() - t0
+        l, c = orc.eval_loss_batch(sub, X, y, accum="ref", n_threads=threads)
+        return idx, sub, step, time.perf_counter() - t0, l, c
 
     if n_sample <= 0:  # pilot, then size the sample for ~15 s of CPU work
-        sub, step, dt = run(2 * threads)
+        _, _, _, dt, _, _ = run(2 * threads)
         n_sample = int(min(tb.n_trees, max(2 * threads, 2 * threads * 15.0 / max(dt, 1e-3))))
-    sub, step, dt = run(n_sample)
+    idx, sub, step, dt, l_ref, c_ref = run(n_sample)
     rate = float(sub.n_nodes) * X.shape[1] / dt
-    return {
-        "value": rate,
-        "unit": "node-evals/s",
-        "cores": threads,
-        "kind": "port",
-        "sample": f"{sub.n_trees} of {tb.n_trees} trees (every {step}th), {X.shape[1]} rows, {dt:.1f} s",
-    }
+    cpu = {"value": rate, "unit": "node-evals/s", "cores": threads, "kind": "port",
+           "sample": f"{sub.n_trees} of {tb.n_trees} trees (every {step}th), {X.shape[1]} rows, {dt:.1f} s"}
+
+    l_f64, c_f64 = orc.eval_loss_batch(sub, X, y, accum="f64", n_threads=threads)
+    d_loss, d_comp = dev_loss[idx].astype(np.float64), dev_comp[idx]
+    flag_mismatch = int(np.sum(d_comp != c_f64)) + int(np.sum(c_ref != c_f64))
+    ok = d_comp & c_f64
+
+    def rel(a, b):
+        with np.errstate(invalid="ignore", divide="ignore"):
+            return np.where(a == b, 0.0, np.abs(a - b) / np.maximum(np.abs(b), 1e-30))
+    r64 = rel(d_loss, l_f64.astype(np.float64))
+    rref = rel(d_loss, l_ref.astype(np.float64))
+    worst = np.nonzero(ok & ((r64 > 1e-4) | (rref > 1e-4)))[0]
+    n_widened, fail = 0, 0
+    if worst.size:  # the per-tree bar: 4x the tree's own libm spread (only for the trees that need it)
+        wsub = sub.take(worst)
+        l0, c0 = orc.eval_loss_batch(wsub, X, y, accum="f64", n_threads=threads)
+        spread = np.zeros(worst.size)
+        for seed in (1, 2, 3, 4):
+            lp, cp = orc.eval_loss_batch(wsub, X, y, accum="f64", n_threads=threads, perturb=seed)
+            with np.errstate(invalid="ignore"):
+                d = np.abs(lp.astype(np.float64) - l0.astype(np.float64))
+            spread = np.maximum(spread, np.where(cp & c0 & np.isfinite(d), d, 0.0))
+        for k, i in enumerate(worst):
+            bar = max(1e-4 * abs(float(l_f64[i])), 4 * spread[k])
+            bar_ref = max(bar, 1e-4 * abs(float(l_ref[i])))
+            n_widened += 1
+            if not (abs(d_loss[i] - l_f64[i]) <= bar and abs(d_loss[i] - l_ref[i]) <= bar_ref):
+                fail += 1
+    parity = {"sample": cpu["sample"], "trees": int(sub.n_trees), "rows": int(X.shape[1]),
+              "flags_bit_exact": flag_mismatch == 0, "flag_mismatches": flag_mismatch,
+              "complete": int(ok.sum()),
+              "max_rel_vs_f64_accum": float(np.max(r64[ok], initial=0.0)),
+              "median_rel_vs_f64_accum": float(np.median(r64[ok])) if ok.any() else 0.0,
+              "max_rel_vs_ref_f32_fold": float(np.max(rref[ok], initial=0.0)),
+              "median_rel_vs_ref_f32_fold": float(np.median(rref[ok])) if ok.any() else 0.0,
+              "trees_over_1e-4_given_libm_spread_bar": n_widened, "loss_failures": fail,
+              "pass": flag_mismatch == 0 and fail == 0,
+              "rule": ("flags bit-exact; losses within max(1e-4 |oracle|, 4 x the tree's libm spread) of both the "
+                       "f64-accumulated and the sequential-f32 oracle (tests/parity_util.py)")}
+    return cpu, parity
 
 
 if __name__ == "__main__":

@@ -167,6 +167,36 @@ int sr_comm_init(sr_ctx* ctx, int nranks, int rank, const void* id_bytes);
 int sr_comm_destroy(sr_ctx* ctx);
 int sr_eval_loss_partials_allreduce(sr_ctx* ctx, const sr_dataset* ds, int opset_id, const sr_tree_batch* trees,
                                     int64_t n_total, int loss_kind, double* out_host);
+/*
+ * The whole row-sharded step of batched eval_loss (SURVEY §8(e) row sharding, config C4) in one call:
+ * rank r's `ds` holds global rows [Σ_{q<r} n_q, Σ_{q<=r} n_q) (shards in rank order; their sizes, Σw
+ * and max|X| are exchanged over the communicator at the first call per dataset).  This shard runs
+ * the single-GPU launch pipeline, the packed [4, n_trees] partials are summed by ONE in-place RCCL
+ * all-reduce over xGMI, losses are finalized on the device (Σ / global n or Σw), and trees flagged BIG
+ * get DynamicExpressions' exact isfinite(sum) verdict over the GLOBAL rows (leaf folds all-gathered).
+ * out_loss / out_complete as sr_eval_loss_batch over the union of the shards, on every rank.
+ * Collective: every rank calls it with the same trees.  A failure on one rank (HIP error, bad tree)
+ * still enters the collectives with its error word set, and every rank then returns an error.
+ * (Replaces SymbolicRegression's per-worker scoring over a distributed dataset for one batched call.)
+ */
+int sr_eval_loss_sharded(sr_ctx* ctx, const sr_dataset* ds, int opset_id, const sr_tree_batch* trees, int loss_kind,
+                         void* out_loss, uint8_t* out_complete);
+/*
+ * Tree-sharded batched eval_loss (SURVEY §8(e) tree sharding): `ds` is the whole dataset on every
+ * rank; the trees are dealt over the ranks by size (snake order over the sorted batch), each rank
+ * scores its share with sr_eval_loss_batch, and ONE all-reduce hands every rank every (loss, complete).
+ * Serves the member-parallel scoring sites (src/Population.jl:49-60, src/SingleIteration.jl:79-92).
+ * Collective, same trees on every rank, same error rule as sr_eval_loss_sharded.
+ */
+int sr_eval_loss_tree_sharded(sr_ctx* ctx, const sr_dataset* ds, int opset_id, const sr_tree_batch* trees,
+                              int loss_kind, void* out_loss, uint8_t* out_complete);
+/* The communicator's size and this rank as RCCL reports them (ncclCommCount / ncclCommUserRank; may be
+ * NULL), and "hip=<file>;rccl=<file>": the HIP runtime and the RCCL this library's calls bind to
+ * (`paths` may be NULL).  sr_comm_unique_id / sr_comm_init fail if the two come from different ROCm
+ * trees (RCCL would then run this library's streams on another HIP runtime). */
+int sr_comm_info(sr_ctx* ctx, int* nranks, int* rank, char* paths, int64_t capacity);
+/* The same "hip=...;rccl=..." string without a context (no device needed). */
+int sr_runtime_info(char* paths, int64_t capacity);
 /* Maximum number of checked nodes per tree for `trees` (element type dtype; sizes the
  * sr_jsum_partials output). */
 int sr_max_checks(sr_ctx* ctx, int dtype, int opset_id, const sr_tree_batch* trees, int* max_checks);
@@ -327,6 +357,16 @@ int sr_search_members(sr_search* s, int which, int64_t* offsets, uint8_t* degree
                       int64_t* parent, int32_t* complexity);
 
 /*
+ * A population of n_trees random trees from gen_random_tree_fixed_size (src/MutationFunctions.jl:441-471;
+ * the engine's generator and draws) with node_count ~ U{1..max_size}, one xoshiro256** stream keyed by
+ * `seed` (Population init at scale, and the benchmark populations).  Pre-order node arrays of at most
+ * `capacity` nodes (n_trees * max_size always suffices); offsets[n_trees + 1]; val has the dtype.
+ */
+int sr_gen_random_population(int dtype, int64_t n_trees, int64_t nfeatures, int n_unary, int n_binary, int max_size,
+                              uint64_t seed, int64_t capacity, int64_t* offsets, uint8_t* degree, uint8_t* op,
+                              uint16_t* feature, uint8_t* constant, void* val);
+
+/*
  * Batched constant optimisation (optimize_constants, src/ConstantOptimization.jl:29-116) of every
  * tree: BFGS with BackTracking (Newton for one constant, its curvature from the device gradient)
  * from the tree's constants and from `nrestarts` starts x0 .* (1 + eps/2), eps ~ randn(T) from the
@@ -340,6 +380,13 @@ int sr_optimize_constants_batch(sr_ctx* ctx, const sr_dataset* ds, int opset_id,
                                 uint64_t seed, void* out_consts, void* out_loss, uint8_t* out_improved,
                                 int64_t* out_f_calls);
 
+/* The same optimiser with the scoring calls answered by CPU callbacks (sr_loss_fn / sr_grad_fn, as
+ * sr_search_use_callbacks): a test seam and the host-port baseline.  dtype = the trees' element type. */
+int sr_optimize_constants_callbacks(int dtype, const sr_tree_batch* trees, const int64_t* row_idx, int64_t n_idx,
+                                    int iterations, int nrestarts, uint64_t seed, sr_loss_fn loss, sr_grad_fn grad,
+                                    void* user, void* out_consts, void* out_loss, uint8_t* out_improved,
+                                    int64_t* out_f_calls);
+
 /* Timing of the last device call on this context (ms): kernel-only, via HIP events. */
 int sr_last_kernel_ms(sr_ctx* ctx, double* eval_ms, double* total_ms);
 
@@ -347,7 +394,8 @@ int sr_last_kernel_ms(sr_ctx* ctx, double* eval_ms, double* total_ms);
  * upload + launch, wait for the interpreter + reduction, exact-sum pass, finalize; out[5] (n >= 6)
  * = the number of interpreter launches of the call (the batch is compiled and launched in chunks),
  * out[6] (n >= 7) = device time of the exact-sum pass (ms), out[7] (n >= 8) = rows per lane of its
- * interpreter kernel.
+ * interpreter kernel, out[8] (n >= 9) = the device-busy time of those launches: the UNION of their
+ * intervals (launches on the two pipeline streams overlap, so their summed durations can exceed it).
  * sr_last_kernel_ms's eval_ms is the sum of those launches' durations. */
 int sr_last_phase_ms(sr_ctx* ctx, double* out, int n);
 

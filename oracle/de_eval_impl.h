@@ -484,4 +484,117 @@ int FN(oracle_eval_loss_batch)(int64_t n_trees, const int64_t* offsets, const ui
   return bad ? 0 : 1;
 }
 
+/* The search engine's CPU scorers (sr_search_use_callbacks): the same engine, seeds and draws as a
+ * device-scored search, with every batched scoring call answered by this port on the host cores —
+ * the "port" CPU baseline of the search-throughput metric (bench.py).  The loss folds sequentially in
+ * T (the reference's order).  The gradient is what the reference's Optim BFGS uses by default
+ * (src/ConstantOptimization.jl:77-116, autodiff_backend = nothing): central finite differences of
+ * that loss, step cbrt(eps(T)) * max(1, |c|) per constant (FiniteDiff.jl's central rule). */
+typedef struct {
+  const void* X;  /* Julia layout [n][nf] (row j's features contiguous) */
+  int64_t nf, n;
+  const void* y;
+  const void* w;  /* NULL: unweighted */
+  const int32_t* un;
+  int n_un;
+  const int32_t* bi;
+  int n_bi;
+  int loss_kind;
+  double loss_param;
+  int n_threads;
+} FN(oscorer);
+
+static int FN(view_gather)(const FN(oscorer) * sc, const int64_t* row_idx, int64_t n_idx, T** Xv, T** yv, T** wv) {
+  *Xv = NULL; *yv = NULL; *wv = NULL;
+  if (!row_idx || n_idx <= 0) return 0;
+  *Xv = FN(alloc)(n_idx * sc->nf);
+  *yv = FN(alloc)(n_idx);
+  if (sc->w) *wv = FN(alloc)(n_idx);
+  for (int64_t i = 0; i < n_idx; ++i) {
+    const int64_t r = row_idx[i];
+    memcpy(*Xv + i * sc->nf, (const T*)sc->X + r * sc->nf, sizeof(T) * (size_t)sc->nf);
+    (*yv)[i] = ((const T*)sc->y)[r];
+    if (sc->w) (*wv)[i] = ((const T*)sc->w)[r];
+  }
+  return 1;
+}
+
+int FN(oracle_search_loss)(void* user, const oracle_tree_batch* tb, const int64_t* row_idx, int64_t n_idx,
+                           void* out_loss, uint8_t* out_complete) {
+  const FN(oscorer)* sc = (const FN(oscorer)*)user;
+  T *Xv, *yv, *wv;
+  const int g = FN(view_gather)(sc, row_idx, n_idx, &Xv, &yv, &wv);
+  const int64_t n = g ? n_idx : sc->n;
+  int* comp = (int*)malloc(sizeof(int) * (size_t)(tb->n_trees > 0 ? tb->n_trees : 1));
+  const int ok = FN(oracle_eval_loss_batch)(tb->n_trees, tb->offsets, tb->degree, tb->op, tb->feature, tb->constant,
+                                            (const T*)tb->val, sc->un, sc->n_un, sc->bi, sc->n_bi,
+                                            g ? Xv : (const T*)sc->X, sc->nf, n, g ? yv : (const T*)sc->y,
+                                            g ? wv : (const T*)sc->w, sc->loss_kind, sc->loss_param, 0,
+                                            sc->n_threads, (T*)out_loss, comp, 0);
+  for (int64_t k = 0; k < tb->n_trees; ++k) out_complete[k] = comp[k] ? 1 : 0;
+  free(comp); free(Xv); free(yv); free(wv);
+  return ok ? 0 : -4;
+}
+
+int FN(oracle_search_grad)(void* user, const oracle_tree_batch* tb, const int64_t* row_idx, int64_t n_idx,
+                           void* out_loss, void* out_grad, uint8_t* out_complete) {
+  const FN(oscorer)* sc = (const FN(oscorer)*)user;
+  T *Xv, *yv, *wv;
+  const int g = FN(view_gather)(sc, row_idx, n_idx, &Xv, &yv, &wv);
+  const int64_t n = g ? n_idx : sc->n;
+  const T* X = g ? Xv : (const T*)sc->X;
+  const T* y = g ? yv : (const T*)sc->y;
+  const T* w = g ? wv : (const T*)sc->w;
+  const T* val = (const T*)tb->val;
+  /* first gradient slot of each tree (constants in pre-order, trees concatenated) */
+  int64_t* goff = (int64_t*)malloc(sizeof(int64_t) * (size_t)(tb->n_trees + 1));
+  goff[0] = 0;
+  for (int64_t k = 0; k < tb->n_trees; ++k) {
+    int64_t c = 0;
+    for (int64_t i = tb->offsets[k]; i < tb->offsets[k + 1]; ++i) c += (tb->degree[i] == 0 && tb->constant[i]) ? 1 : 0;
+    goff[k + 1] = goff[k] + c;
+  }
+  int bad = 0;
+  const T h0 = (T)(sizeof(T) == 4 ? 4.921566601151848e-03 : 6.055454452393343e-06); /* cbrt(eps(T)) */
+#pragma omp parallel for schedule(dynamic, 1) num_threads(sc->n_threads) reduction(| : bad)
+  for (int64_t k = 0; k < tb->n_trees; ++k) {
+    const int64_t b = tb->offsets[k], e = tb->offsets[k + 1];
+    T* v = FN(alloc)(e - b);
+    memcpy(v, val + b, sizeof(T) * (size_t)(e - b));
+    int c = 0;
+    T l0;
+    if (!FN(oracle_eval_loss)(e - b, tb->degree + b, tb->op + b, tb->feature + b, tb->constant + b, v, sc->un,
+                              sc->n_un, sc->bi, sc->n_bi, X, sc->nf, n, y, w, sc->loss_kind, sc->loss_param, 0, &l0,
+                              &c, 0))
+      bad |= 1;
+    ((T*)out_loss)[k] = l0;
+    out_complete[k] = c ? 1 : 0;
+    int64_t slot = goff[k];
+    for (int64_t i = 0; i < e - b; ++i) {
+      if (!(tb->degree[b + i] == 0 && tb->constant[b + i])) continue;
+      T gi = (T)0;
+      if (c) {
+        const T x0 = v[i];
+        const T h = h0 * (M_FABS(x0) > (T)1 ? M_FABS(x0) : (T)1);
+        T lp, lm;
+        int cp = 0, cm = 0;
+        v[i] = x0 + h;
+        bad |= !FN(oracle_eval_loss)(e - b, tb->degree + b, tb->op + b, tb->feature + b, tb->constant + b, v, sc->un,
+                                     sc->n_un, sc->bi, sc->n_bi, X, sc->nf, n, y, w, sc->loss_kind, sc->loss_param,
+                                     0, &lp, &cp, 0);
+        v[i] = x0 - h;
+        bad |= !FN(oracle_eval_loss)(e - b, tb->degree + b, tb->op + b, tb->feature + b, tb->constant + b, v, sc->un,
+                                     sc->n_un, sc->bi, sc->n_bi, X, sc->nf, n, y, w, sc->loss_kind, sc->loss_param,
+                                     0, &lm, &cm, 0);
+        v[i] = x0;
+        gi = (lp - lm) / ((x0 + h) - (x0 - h));
+      }
+      ((T*)out_grad)[slot++] = gi;
+    }
+    free(v);
+  }
+  free(goff); free(Xv); free(yv); free(wv);
+  return bad ? -4 : 0;
+}
+
 #undef FN

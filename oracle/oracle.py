@@ -162,3 +162,123 @@ class Oracle:
         lp, _ = self.eval_loss_batch(b, X, y, w, loss_kind, accum="f64", n_threads=n_threads, loss_param=loss_param)
         g = (lp[0::2] - lp[1::2]) / (2 * h)
         return g, loss0, comp0
+
+
+class _Scorer(ctypes.Structure):
+    _fields_ = [("X", ctypes.c_void_p), ("nf", ctypes.c_int64), ("n", ctypes.c_int64), ("y", ctypes.c_void_p),
+                ("w", ctypes.c_void_p), ("un", ctypes.c_void_p), ("n_un", ctypes.c_int), ("bi", ctypes.c_void_p),
+                ("n_bi", ctypes.c_int), ("loss_kind", ctypes.c_int), ("loss_param", ctypes.c_double),
+                ("n_threads", ctypes.c_int)]
+
+
+class SearchScorer:
+    """The oracle as the search engine's CPU scorer (C callbacks `oracle_search_loss` /
+    `oracle_search_grad` for ``sr_search_use_callbacks``): the same engine, seeds and draws as a
+    device-scored search, every scoring call answered on the host cores by this port (loss folded in
+    T as the reference does; gradients by central finite differences, as the reference's Optim BFGS
+    uses by default).  bench.py's search CPU baseline ("port")."""
+
+    def __init__(self, orc, X, y, w=None, loss_kind=0, loss_param=0.0, n_threads=1):
+        X = np.asarray(X)
+        dt = X.dtype
+        sfx = Oracle._sfx(dt)
+        self._keep = [np.ascontiguousarray(X.T), np.ascontiguousarray(y, dtype=dt),
+                      None if w is None else np.ascontiguousarray(w, dtype=dt), orc.un, orc.bi]
+        Xj, yy, ww = self._keep[:3]
+        self.st = _Scorer(_p(Xj), X.shape[0], X.shape[1], _p(yy), _p(ww), _p(orc.un), len(orc.unaops), _p(orc.bi),
+                          len(orc.binops), int(loss_kind), float(loss_param), int(n_threads))
+        self.user = ctypes.cast(ctypes.pointer(self.st), ctypes.c_void_p)
+        L = lib()
+        self.loss_addr = ctypes.cast(getattr(L, f"oracle_search_loss_{sfx}"), ctypes.c_void_p).value
+        self.grad_addr = ctypes.cast(getattr(L, f"oracle_search_grad_{sfx}"), ctypes.c_void_p).value
+
+
+def _fwd_unary(name, x, y):
+    """d op(x) / dx of the device's derivative rules (csrc/sr_ops.h sr_unary_deriv)."""
+    if name == "cos":
+        return -np.sin(x)
+    if name == "sin":
+        return np.cos(x)
+    if name == "exp":
+        return y
+    if name in ("log", "safe_log"):
+        return 1.0 / x
+    if name in ("sqrt", "safe_sqrt"):
+        return 0.5 / y
+    if name == "square":
+        return 2.0 * x
+    if name == "cube":
+        return 3.0 * x * x
+    if name == "neg":
+        return -np.ones_like(x)
+    if name == "abs":
+        return np.sign(x)
+    raise ValueError(f"no forward-mode rule for {name!r}")
+
+
+_UNARY_FN = {"cos": np.cos, "sin": np.sin, "exp": np.exp, "log": np.log, "safe_log": np.log, "sqrt": np.sqrt,
+             "safe_sqrt": np.sqrt, "square": np.square, "cube": lambda x: x * x * x, "neg": np.negative,
+             "abs": np.abs}
+
+
+def loss_grad_forward(orc, tb, X, y, w=None, loss_kind=0):
+    """Forward-mode (dual-number) gradient of the Float64 L2 loss with respect to every tree's constants
+    (pre-order, get_scalar_constants) — the restatement of the device's forward-mode kernel
+    (csrc/sr_grad_impl.h: d loss / d pred = 2(pred - y), times the weight, / n or / Σw) with numpy's
+    libm.  Only complete trees are differentiated (zeros otherwise), as the device does.  Returns
+    (grads, loss, complete) in the layout of ``sr_amd.eval_grad_batch``."""
+    if loss_kind != 0:
+        raise ValueError("loss_grad_forward restates L2DistLoss only")
+    X = np.asarray(X, dtype=np.float64)
+    y = np.asarray(y, dtype=np.float64)
+    loss, comp = orc.eval_loss_batch(tb, X, y, w, accum="f64", n_threads=8)
+    denom = float(np.sum(w)) if w is not None else float(X.shape[1])
+    grads = []
+    for k in range(len(tb.offsets) - 1):
+        b, e = int(tb.offsets[k]), int(tb.offsets[k + 1])
+        deg, op, feat = tb.degree[b:e], tb.op[b:e], tb.feature[b:e]
+        con, val = tb.constant[b:e], tb.val[b:e].astype(np.float64)
+        cidx = np.cumsum((deg == 0) & (con != 0)) - 1
+        nc = int(np.count_nonzero((deg == 0) & (con != 0)))
+        if nc == 0:
+            continue
+        if not comp[k]:
+            grads.append(np.zeros(nc))
+            continue
+        pos = [0]
+
+        def ev():
+            i = pos[0]
+            pos[0] += 1
+            if deg[i] == 0:
+                if con[i]:
+                    d = np.zeros((nc, X.shape[1]))
+                    d[cidx[i]] = 1.0
+                    return np.full(X.shape[1], val[i]), d
+                return X[int(feat[i]) - 1].copy(), np.zeros((nc, X.shape[1]))
+            if deg[i] == 1:
+                name = orc.unaops[int(op[i]) - 1]
+                xv, dx = ev()
+                yv = _UNARY_FN[name](xv)
+                return yv, _fwd_unary(name, xv, yv) * dx
+            name = orc.binops[int(op[i]) - 1]
+            av, da = ev()
+            bv, db = ev()
+            if name == "+":
+                return av + bv, da + db
+            if name == "-":
+                return av - bv, da - db
+            if name == "*":
+                return av * bv, bv * da + av * db
+            if name == "/":
+                r = av / bv
+                return r, (1.0 / bv) * da + (-r / bv) * db
+            raise ValueError(f"no forward-mode rule for {name!r}")
+
+        pred, dpred = ev()
+        coef = 2.0 * (pred - y)
+        if w is not None:
+            coef = coef * np.asarray(w, dtype=np.float64)
+        grads.append(dpred @ coef / denom)
+    g = np.concatenate(grads) if grads else np.zeros(0)
+    return g, loss, comp

@@ -102,6 +102,34 @@ hipError_t sr_launch_pack_partials(const double* sum, const uint32_t* flag, int 
   return hipGetLastError();
 }
 
+// Row-sharded finalize on the device (sr_eval_loss_sharded): the partials [4][n] summed over every
+// rank -> loss[t] = Σ / denom (f64 division, rounded once to T) or +Inf, and comp[t] = 1 complete,
+// 0 incomplete, 2 flagged BIG only (the exact Julia-order check over the global rows decides; its
+// loss slot holds the finite value).  The same rules as the host's finalize (sr_capi.cpp).
+template <typename T>
+__global__ void __launch_bounds__(256) sr_finalize_packed_kernel(const double* __restrict__ packed, int n,
+                                                                 double denom, T* __restrict__ loss,
+                                                                 uint8_t* __restrict__ comp) {
+  const int t = int(int64_t(blockIdx.x) * blockDim.x + threadIdx.x);
+  if (t >= n) return;
+  const bool nonfinite = packed[size_t(n) + t] > 0.0;
+  const bool big = packed[2 * size_t(n) + t] > 0.0;
+  const bool stat = packed[3 * size_t(n) + t] > 0.0;
+  const bool ok = !nonfinite && !stat;
+  loss[t] = ok ? T(packed[t] / denom) : T(INFINITY);
+  comp[t] = ok ? (big ? uint8_t(2) : uint8_t(1)) : uint8_t(0);
+}
+
+template <typename T>
+hipError_t sr_launch_finalize_packed(const double* packed, int n, double denom, T* loss, uint8_t* comp, hipStream_t s) {
+  if (n <= 0) return hipSuccess;
+  hipLaunchKernelGGL(sr_finalize_packed_kernel<T>, dim3(unsigned((n + 255) / 256)), dim3(256), 0, s, packed, n, denom,
+                     loss, comp);
+  return hipGetLastError();
+}
+template hipError_t sr_launch_finalize_packed<float>(const double*, int, double, float*, uint8_t*, hipStream_t);
+template hipError_t sr_launch_finalize_packed<double>(const double*, int, double, double*, uint8_t*, hipStream_t);
+
 // Julia [nf, n] column-major -> per-feature rows [nf][ld]; padded rows replicate row 0 so that the
 // interpreter's validity checks never see a value that is not in the dataset.
 template <typename T>

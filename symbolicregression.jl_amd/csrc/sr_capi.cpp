@@ -7,8 +7,12 @@
 // Mirrors reference src/LossFunctions.jl:90-117 (`_eval_loss`) for each tree of the batch.
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
+#include <dlfcn.h>
+#include <limits.h>
+#include <stdlib.h>
 
 #include <algorithm>
+#include <atomic>
 #include <chrono>
 #include <cmath>
 #include <cstdio>
@@ -170,8 +174,12 @@ struct sr_ctx {
   // RCCL communicator of the row-sharded path (sr_comm_init): the library's own RCCL over xGMI on
   // its own HIP runtime (torch's bundled runtime cannot share the GPU with this one in a process)
   ncclComm_t comm = nullptr;
-  int comm_ranks = 0;      // SR_AMD_FIRST_CHUNK: the two-chunk pipeline's first chunk is 1/first_chunk       // SR_AMD_CODE_CACHE: LDS program cache of the register-stack launches     // SR_AMD_STRESS_PROBE: the probe runs the dataset's stress rows (below)
+  int comm_ranks = 0;
+  int comm_rank = 0;
+  uint64_t comm_gen = 0;  // process-unique id of the current communicator (shard layouts are cached per id)
+  DevBuf shard_buf;       // collectives of the sharded calls (shard layout, exact-pass folds, tree results)      // SR_AMD_FIRST_CHUNK: the two-chunk pipeline's first chunk is 1/first_chunk       // SR_AMD_CODE_CACHE: LDS program cache of the register-stack launches     // SR_AMD_STRESS_PROBE: the probe runs the dataset's stress rows (below)
   double last_eval_ms = 0.0, last_total_ms = 0.0;
+  double last_busy_ms = 0.0;  // union of the last call's interpreter launch intervals (sr_last_phase_ms out[8])
   // host-side phases of the last eval_loss call (ms): compile, upload+launch, wait, exact pass,
   // finalize (sr_last_phase_ms)
   double phase_ms[5] = {0, 0, 0, 0, 0};
@@ -215,6 +223,12 @@ struct sr_dataset {
   // ... up to kProbeRows; int64 row indices on the device (NULL for small datasets)
   void* probe_rows = nullptr;
   int64_t n_probe = 0;
+  // row-sharded calls (sr_eval_loss_sharded): every shard's rows, Σw and max|X|, exchanged once per
+  // communicator (shard_gen = its sr_ctx::comm_gen; rank r holds global rows [offs[r], offs[r + 1]))
+  mutable uint64_t shard_gen = 0;
+  mutable std::vector<int64_t> shard_offs;
+  mutable double shard_wsum = 0.0, shard_max_abs_x = 0.0;
+  mutable int64_t shard_min_rows = 0;
 };
 
 namespace {
@@ -350,10 +364,18 @@ void choose_derived(const sr_tree_batch& trees, const SrOpset& ops, int64_t nf, 
   }
 }
 
+// Row-sharded calls decide data-dependent launch choices from the statistics of ALL shards, so every
+// rank compiles identical programs (same derived columns: the exact path numbers checked arrays the
+// same on every rank): max|X| over every shard and the smallest shard's row count.
+struct ShardCtl {
+  double max_abs_x;
+  int64_t min_rows;
+};
+
 template <typename T>
 int run_batch(sr_ctx* ctx, const sr_dataset* ds, int opset_id, const sr_tree_batch* trees, const int64_t* row_idx,
               int64_t n_idx, int64_t n_total, int loss_kind, int mode, SrProgramBatch<T>* prog, Grid* grid_out,
-              bool allow_derived = false) {
+              bool allow_derived = false, const ShardCtl* shard = nullptr) {
   const bool gather = row_idx != nullptr && n_idx > 0;
   const int64_t n_eval = gather ? n_idx : ds->n;
   if (n_eval <= 0) return set_error(SR_ERR_INVALID_ARG, "no rows to evaluate");
@@ -495,10 +517,12 @@ int run_batch(sr_ctx* ctx, const sr_dataset* ds, int opset_id, const sr_tree_bat
   std::vector<int16_t> dmap;
   SrDerivedSpec spec{};
   const int64_t dld = (n_eval + kRowAlign - 1) / kRowAlign * kRowAlign;
-  // (single-view calls only: row-sharded partials number their checked arrays identically on every
-  // rank, and a rank's choice of columns depends on its shard)
-  if (allow_derived && ctx->derived && mode == SR_MODE_LOSS && tier == SR_TIER_BASIC && n_eval >= kDerivedMinRows && nt >= 64 &&
-      ds->max_abs_x < double(T(t_max<T>() / (2.0 * double(n_total > 0 ? n_total : 1))))) {  // (track_x off)
+  // (row-sharded calls pass `shard`: the choice then depends only on the trees and on statistics of
+  // every shard, so all ranks compile the same programs and number their checked arrays alike)
+  const double max_abs_x = shard ? shard->max_abs_x : ds->max_abs_x;
+  const int64_t derived_rows = shard ? shard->min_rows : n_eval;
+  if (allow_derived && ctx->derived && mode == SR_MODE_LOSS && tier == SR_TIER_BASIC && derived_rows >= kDerivedMinRows &&
+      nt >= 64 && max_abs_x < double(T(t_max<T>() / (2.0 * double(n_total > 0 ? n_total : 1))))) {  // (track_x off)
     choose_derived(*trees, ctx->opsets[opset_id], ds->nf, &spec, &dmap);
     if (spec.n > 0) {
       SR_HIP_CHECK(ctx->derived_cols.ensure(size_t(spec.n) * size_t(dld) * sizeof(T)));
@@ -662,7 +686,7 @@ int run_batch(sr_ctx* ctx, const sr_dataset* ds, int opset_id, const sr_tree_bat
       a.stack_depth = vstk ? std::min(depth, 2) : depth;  // (the register-stack trees need <= 2)
       // Σ over n_total rows of values below tbig cannot overflow T, even with rounding slack.
       a.tbig = T(t_max<T>() / (2.0 * double(n_total > 0 ? n_total : 1)));
-      a.track_x = !(ds->max_abs_x < double(a.tbig)) ? 1 : 0;
+      a.track_x = !(max_abs_x < double(a.tbig)) ? 1 : 0;
       a.loss_kind = lkind;
       a.loss_param = T(lparam);
       a.part_sum = ctx->part_sum.as<double>() + size_t(n_rb) * size_t(t0 + p0);
@@ -760,6 +784,32 @@ inline double chunk_kernel_ms(sr_ctx* ctx) {
     if (hipEventElapsedTime(&m, ctx->ev_d0, ctx->ev_d1) == hipSuccess) ms += double(m);
   }
   return ms;
+}
+
+// The same launches' device-busy time: the UNION of their [start, end] intervals (chunks on the two
+// streams overlap, so the sum above can exceed the wall time they span; this cannot).
+inline double chunk_busy_ms(sr_ctx* ctx) {
+  std::vector<std::pair<double, double>> iv;
+  auto add = [&](hipEvent_t a, hipEvent_t b) {
+    float t0 = 0.f, t1 = 0.f;
+    if (hipEventElapsedTime(&t0, ctx->ev_start, a) == hipSuccess && hipEventElapsedTime(&t1, ctx->ev_start, b) == hipSuccess)
+      iv.push_back({double(t0), double(t1)});
+  };
+  for (int c = 0; c < ctx->n_chunks_last; ++c) add(ctx->ev_c0[c], ctx->ev_c1[c]);
+  if (ctx->derived_last) add(ctx->ev_d0, ctx->ev_d1);
+  std::sort(iv.begin(), iv.end());
+  double busy = 0.0, lo = 0.0, hi = -1.0;
+  for (const auto& [a, b] : iv) {
+    if (a > hi) {
+      if (hi > lo) busy += hi - lo;
+      lo = a;
+      hi = b;
+    } else {
+      hi = std::max(hi, b);
+    }
+  }
+  if (hi > lo) busy += hi - lo;
+  return busy;
 }
 
 // ---------------------------------------------------------------- Julia's pairwise `sum`
@@ -1092,6 +1142,7 @@ int eval_loss_impl(sr_ctx* ctx, const sr_dataset* ds, int opset_id, const sr_tre
   std::vector<double> sums(hs, hs + nt);
   std::vector<uint32_t> flags(hf, hf + nt);
   ctx->last_eval_ms = chunk_kernel_ms(ctx);
+  ctx->last_busy_ms = chunk_busy_ms(ctx);
   ctx->mark_phase(2);
   std::vector<int64_t> list;
   for (int64_t t = 0; t < nt; ++t)
@@ -1387,6 +1438,270 @@ int tier_of(const SrOpset& o) {
   return SR_TIER_BASIC;
 }
 
+// ---------------------------------------------------------------- multi-GPU
+std::atomic<uint64_t> g_comm_gen{0};
+
+#define SR_NCCL_CHECK(expr)                                                                         \
+  do {                                                                                              \
+    const ncclResult_t _r = (expr);                                                                 \
+    if (_r != ncclSuccess) return set_error(SR_ERR_HIP, std::string(#expr) + ": " + ncclGetErrorString(_r)); \
+  } while (0)
+
+// The file a symbol was loaded from (dladdr), with symlinks resolved.
+std::string so_path(const void* sym) {
+  Dl_info info{};
+  if (!dladdr(sym, &info) || !info.dli_fname) return "?";
+  char buf[PATH_MAX];
+  return realpath(info.dli_fname, buf) ? std::string(buf) : std::string(info.dli_fname);
+}
+std::string dir_of(const std::string& p) {
+  const size_t k = p.rfind('/');
+  return k == std::string::npos ? std::string() : p.substr(0, k);
+}
+// The HIP runtime and the RCCL this library's calls bind to.  The dynamic loader reuses an already
+// loaded soname, so when a process loaded torch's bundled ROCm first, the library runs on torch's
+// HIP and RCCL, otherwise on /opt/rocm's: either way the two must come from ONE tree, because RCCL
+// is handed this library's streams and device buffers.
+std::string runtime_paths() {
+  return "hip=" + so_path(reinterpret_cast<const void*>(&hipStreamSynchronize)) +
+         ";rccl=" + so_path(reinterpret_cast<const void*>(&ncclAllReduce));
+}
+int check_runtime_pair() {
+  const std::string hip = so_path(reinterpret_cast<const void*>(&hipStreamSynchronize));
+  const std::string rccl = so_path(reinterpret_cast<const void*>(&ncclAllReduce));
+  if (dir_of(hip) != dir_of(rccl))
+    return set_error(SR_ERR_HIP, "the HIP runtime (" + hip + ") and RCCL (" + rccl +
+                                     ") come from different ROCm trees: RCCL would run this library's streams "
+                                     "on another runtime; load libsr_amd before anything else that loads HIP");
+  return SR_OK;
+}
+
+// Every shard's rows, Σw and max|X| (one all-gather per dataset and communicator).  Collective.
+int shard_layout(sr_ctx* ctx, const sr_dataset* ds) {
+  if (ds->shard_gen == ctx->comm_gen && !ds->shard_offs.empty()) return SR_OK;
+  const int nr = ctx->comm_ranks;
+  hipStream_t s = ctx->stream;
+  const double mine[4] = {double(ds->n), ds->w ? ds->wsum : 0.0, ds->max_abs_x, ds->w ? 1.0 : 0.0};
+  SR_HIP_CHECK(ctx->shard_buf.ensure(sizeof(double) * 4 * size_t(nr + 1)));
+  double* d = ctx->shard_buf.as<double>();
+  SR_HIP_CHECK(hipMemcpyAsync(d, mine, sizeof(mine), hipMemcpyHostToDevice, s));
+  SR_NCCL_CHECK(ncclAllGather(d, d + 4, 4, ncclDouble, ctx->comm, s));
+  std::vector<double> all(size_t(4) * size_t(nr));
+  SR_HIP_CHECK(hipMemcpyAsync(all.data(), d + 4, all.size() * sizeof(double), hipMemcpyDeviceToHost, s));
+  SR_HIP_CHECK(hipStreamSynchronize(s));
+  std::vector<int64_t> offs(size_t(nr) + 1, 0);
+  double wsum = 0.0, mx = 0.0;
+  int64_t mn = INT64_MAX;
+  int weighted = 0;
+  for (int r = 0; r < nr; ++r) {
+    const int64_t n = int64_t(all[size_t(4 * r)]);
+    offs[size_t(r) + 1] = offs[size_t(r)] + n;
+    wsum += all[size_t(4 * r + 1)];
+    const double m = all[size_t(4 * r + 2)];
+    mx = (m > mx || m != m) ? m : mx;  // NaN / Inf (non-finite data) propagate
+    mn = std::min(mn, n);
+    weighted += all[size_t(4 * r + 3)] != 0.0 ? 1 : 0;
+  }
+  if (weighted != 0 && weighted != nr) return set_error(SR_ERR_INVALID_ARG, "some shards have weights and some do not");
+  if (int64_t(all[size_t(4 * ctx->comm_rank)]) != ds->n) return set_error(SR_ERR_INVALID_ARG, "shard layout exchange failed");
+  ds->shard_offs = offs;
+  ds->shard_wsum = wsum;
+  ds->shard_max_abs_x = (mx != mx) ? double(INFINITY) : mx;
+  ds->shard_min_rows = mn;
+  ds->shard_gen = ctx->comm_gen;
+  return SR_OK;
+}
+
+// EXACT verdicts of the listed (BIG-only) trees over the GLOBAL rows of a row-sharded call: each rank
+// folds the Julia leaf blocks it holds (sr_jsum_partials' ranges), the folds are all-gathered over
+// the communicator, and every rank adds them in Base.mapreduce_impl's recursion order.  Collective
+// (the list is the same on every rank: it comes from the all-reduced flags).
+template <typename T>
+int exact_sharded(sr_ctx* ctx, const sr_dataset* ds, const SrProgramBatch<T>& prog, const std::vector<int64_t>& list,
+                  std::vector<uint8_t>* list_ok) {
+  list_ok->assign(list.size(), 1);
+  int mc = 0;
+  for (int64_t t : list) mc = std::max(mc, int(prog.n_checks[size_t(t)]));
+  if (list.empty() || mc == 0) return SR_OK;
+  const int nr = ctx->comm_ranks, me = ctx->comm_rank;
+  const std::vector<int64_t>& offs = ds->shard_offs;
+  const int64_t n_total = offs[size_t(nr)];
+  if (nr == 1) return exact_list_ok<T>(ctx, ds, prog, nullptr, 0, list, list_ok);  // one shard = the whole view
+  std::vector<std::vector<JlRange>> ranges(static_cast<size_t>(nr));
+  size_t max_r = 0;
+  for (int r = 0; r < nr; ++r) {
+    ranges[size_t(r)] = jl_ranges(offs[size_t(r)], offs[size_t(r) + 1] - offs[size_t(r)], n_total);
+    max_r = std::max(max_r, ranges[size_t(r)].size());
+  }
+  const size_t n_arrays = list.size() * size_t(mc);
+  // per rank: [n_arrays][its own range count] folds, then an error word (bytes of one double)
+  const size_t payload = n_arrays * max_r * sizeof(T);
+  const size_t slot = (payload + sizeof(double) + 255) & ~size_t(255);
+  std::vector<char> mine(slot, 0);
+  int local = run_exact<T>(ctx, ds, prog, nullptr, 0, list.data(), int64_t(list.size()), mc, ranges[size_t(me)],
+                           reinterpret_cast<T*>(mine.data()));
+  if (local != SR_OK) std::fill(mine.begin(), mine.end(), 0);
+  const double err = local != SR_OK ? 1.0 : 0.0;
+  std::memcpy(mine.data() + payload, &err, sizeof(double));
+  hipStream_t s = ctx->stream;
+  SR_HIP_CHECK(ctx->shard_buf.ensure(slot * size_t(nr + 1)));
+  char* d = ctx->shard_buf.as<char>();
+  SR_HIP_CHECK(hipMemcpyAsync(d, mine.data(), slot, hipMemcpyHostToDevice, s));
+  SR_NCCL_CHECK(ncclAllGather(d, d + slot, slot, ncclChar, ctx->comm, s));
+  std::vector<char> every(slot * size_t(nr));
+  SR_HIP_CHECK(hipMemcpyAsync(every.data(), d + slot, every.size(), hipMemcpyDeviceToHost, s));
+  SR_HIP_CHECK(hipStreamSynchronize(s));
+  for (int r = 0; r < nr; ++r) {
+    double e = 0.0;
+    std::memcpy(&e, every.data() + slot * size_t(r) + payload, sizeof(double));
+    if (e != 0.0) return local != SR_OK ? local : set_error(SR_ERR_HIP, "the exact-sum pass failed on rank " + std::to_string(r));
+  }
+  std::vector<const T*> rank_vals(static_cast<size_t>(nr));
+  for (int r = 0; r < nr; ++r) rank_vals[size_t(r)] = reinterpret_cast<const T*>(every.data() + slot * size_t(r));
+  std::vector<uint8_t> fin(n_arrays);
+  jl_finite<T>(n_total, nr, offs.data(), rank_vals.data(), int64_t(n_arrays), fin.data());
+  for (size_t i = 0; i < list.size(); ++i)
+    for (int k = 0; k < mc; ++k) (*list_ok)[i] &= fin[i * size_t(mc) + size_t(k)];
+  return SR_OK;
+}
+
+// The row-sharded step (sr_eval_loss_sharded): this rank's shard through the same launch pipeline as
+// a single-GPU call (derived columns, dead-tree probe, two-chunk compile/launch overlap), the packed
+// [4, n_trees] partials plus an error word summed by ONE in-place all-reduce on the device, losses
+// finalized on the device (Σ / global denominator), and the rare BIG-only trees decided by the exact
+// pass over the global rows.  Every rank enters every collective, also after a local failure (its
+// partials zeroed, its error word set), and then every rank returns an error.
+template <typename T>
+int eval_sharded_impl(sr_ctx* ctx, const sr_dataset* ds, int opset_id, const sr_tree_batch* trees, int loss_kind,
+                      T* out_loss, uint8_t* out_complete) {
+  const int64_t nt = trees->n_trees;
+  int rc = shard_layout(ctx, ds);
+  if (rc != SR_OK) return rc;
+  const int nr = ctx->comm_ranks;
+  const int64_t n_total = ds->shard_offs[size_t(nr)];
+  const ShardCtl sc{ds->shard_max_abs_x, ds->shard_min_rows};
+  auto t0 = std::chrono::steady_clock::now();
+  ctx->start_phases(t0);
+  SrProgramBatch<T> prog;
+  Grid g;
+  int local = nt > 0 ? run_batch<T>(ctx, ds, opset_id, trees, nullptr, 0, n_total, loss_kind, SR_MODE_LOSS, &prog, &g,
+                                    true, &sc)
+                     : SR_OK;
+  hipStream_t s = ctx->stream;
+  const size_t n4 = size_t(4) * size_t(nt);
+  // [4][nt] partials | error word, then the finalized losses (T) and complete bytes
+  const size_t o_loss = ((n4 + 1) * sizeof(double) + 255) & ~size_t(255);
+  const size_t o_comp = o_loss + ((size_t(nt) * sizeof(T) + 255) & ~size_t(255));
+  SR_HIP_CHECK(ctx->packed.ensure(o_comp + size_t(nt) + 16));
+  char* base = ctx->packed.as<char>();
+  double* dst = reinterpret_cast<double*>(base);
+  if (local == SR_OK && nt > 0) {
+    const hipError_t e = sr_launch_pack_partials(ctx->d_out_sum, ctx->d_out_flag, int(nt), dst, s);
+    if (e != hipSuccess) local = set_error(SR_ERR_HIP, std::string("pack partials: ") + hipGetErrorString(e));
+  }
+  const double err_word = local != SR_OK ? 1.0 : 0.0;
+  if (local != SR_OK) SR_HIP_CHECK(hipMemsetAsync(dst, 0, n4 * sizeof(double), s));
+  SR_HIP_CHECK(hipMemcpyAsync(dst + n4, &err_word, sizeof(double), hipMemcpyHostToDevice, s));
+  ctx->mark_phase(1);
+  // the path's one exchange step: every rank's partials (and error words), summed in place over xGMI
+  SR_NCCL_CHECK(ncclAllReduce(dst, dst, n4 + 1, ncclDouble, ncclSum, ctx->comm, s));
+  const double denom = ds->w ? ds->shard_wsum : double(n_total);
+  T* d_loss = reinterpret_cast<T*>(base + o_loss);
+  uint8_t* d_comp = reinterpret_cast<uint8_t*>(base + o_comp);
+  SR_HIP_CHECK(sr_launch_finalize_packed<T>(dst, int(nt), denom, d_loss, d_comp, s));
+  double err_sum = 0.0;
+  SR_HIP_CHECK(hipMemcpyAsync(&err_sum, dst + n4, sizeof(double), hipMemcpyDeviceToHost, s));
+  if (nt > 0) {
+    SR_HIP_CHECK(hipMemcpyAsync(out_loss, d_loss, size_t(nt) * sizeof(T), hipMemcpyDeviceToHost, s));
+    SR_HIP_CHECK(hipMemcpyAsync(out_complete, d_comp, size_t(nt), hipMemcpyDeviceToHost, s));
+  }
+  SR_HIP_CHECK(hipStreamSynchronize(s));
+  ctx->last_eval_ms = local == SR_OK && nt > 0 ? chunk_kernel_ms(ctx) : 0.0;
+  ctx->last_busy_ms = local == SR_OK && nt > 0 ? chunk_busy_ms(ctx) : 0.0;
+  ctx->mark_phase(2);
+  if (err_sum != 0.0) return local != SR_OK ? local : set_error(SR_ERR_HIP, "the row-sharded step failed on a peer rank");
+  std::vector<int64_t> list;
+  for (int64_t t = 0; t < nt; ++t)
+    if (out_complete[t] == 2) list.push_back(t);
+  std::vector<uint8_t> list_ok;
+  ctx->n_exact_last = int64_t(list.size());
+  ctx->exact_kernel_ms = 0.0;
+  rc = exact_sharded<T>(ctx, ds, prog, list, &list_ok);
+  if (rc != SR_OK) return rc;
+  for (size_t i = 0; i < list.size(); ++i) {
+    const int64_t t = list[i];
+    out_complete[t] = list_ok[i] ? 1 : 0;
+    if (!list_ok[i]) out_loss[t] = T(INFINITY);
+  }
+  ctx->mark_phase(3);
+  ctx->last_total_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+  return SR_OK;
+}
+
+// Tree-sharded scoring (sr_eval_loss_tree_sharded): the dataset is replicated, the trees are split over
+// the ranks by estimated cost (node count; sorted, dealt in snake order so every rank gets a similar
+// share), each rank scores its own trees with the single-GPU call, and ONE all-reduce of a
+// [loss | complete | error] buffer (each tree's slots written by its owner only) hands every rank
+// every result.
+template <typename T>
+int eval_tree_sharded_impl(sr_ctx* ctx, const sr_dataset* ds, int opset_id, const sr_tree_batch* trees, int loss_kind,
+                           T* out_loss, uint8_t* out_complete) {
+  const int64_t nt = trees->n_trees;
+  const int nr = ctx->comm_ranks, me = ctx->comm_rank;
+  std::vector<int64_t> order(static_cast<size_t>(nt));
+  for (int64_t t = 0; t < nt; ++t) order[size_t(t)] = t;
+  auto size_of = [&](int64_t t) { return trees->offsets[t + 1] - trees->offsets[t]; };
+  std::stable_sort(order.begin(), order.end(), [&](int64_t a, int64_t b) { return size_of(a) > size_of(b); });
+  std::vector<int64_t> mine;
+  for (int64_t k = 0; k < nt; ++k) {
+    const int64_t round = k / nr, pos = k % nr;
+    const int owner = int((round & 1) ? (nr - 1 - pos) : pos);
+    if (owner == me) mine.push_back(order[size_t(k)]);
+  }
+  std::sort(mine.begin(), mine.end());  // this rank's trees in the caller's order
+  // this rank's sub-batch (node arrays copied: a batch's trees are contiguous ranges)
+  std::vector<int64_t> offs(mine.size() + 1, 0);
+  for (size_t i = 0; i < mine.size(); ++i) offs[i + 1] = offs[i] + size_of(mine[i]);
+  const size_t nn = size_t(offs.back());
+  std::vector<uint8_t> deg(nn), op(nn), con(nn);
+  std::vector<uint16_t> feat(nn);
+  std::vector<T> val(nn);
+  const T* vals = static_cast<const T*>(trees->val);
+  for (size_t i = 0; i < mine.size(); ++i) {
+    const int64_t b = trees->offsets[mine[i]], n = size_of(mine[i]), o = offs[i];
+    std::memcpy(deg.data() + o, trees->degree + b, size_t(n));
+    std::memcpy(op.data() + o, trees->op + b, size_t(n));
+    std::memcpy(con.data() + o, trees->constant + b, size_t(n));
+    std::memcpy(feat.data() + o, trees->feature + b, size_t(n) * sizeof(uint16_t));
+    std::memcpy(val.data() + o, vals + b, size_t(n) * sizeof(T));
+  }
+  sr_tree_batch sub{int64_t(mine.size()), offs.data(), deg.data(), op.data(), feat.data(), con.data(), val.data()};
+  std::vector<T> l(mine.size());
+  std::vector<uint8_t> c(mine.size());
+  int local = eval_loss_impl<T>(ctx, ds, opset_id, &sub, nullptr, 0, loss_kind, l.data(), c.data());
+  std::vector<double> buf(2 * size_t(nt) + 1, 0.0);
+  if (local == SR_OK) {
+    for (size_t i = 0; i < mine.size(); ++i) {
+      buf[size_t(mine[i])] = double(l[i]);
+      buf[size_t(nt) + size_t(mine[i])] = double(c[i]);
+    }
+  }
+  buf[2 * size_t(nt)] = local != SR_OK ? 1.0 : 0.0;
+  hipStream_t s = ctx->stream;
+  SR_HIP_CHECK(ctx->shard_buf.ensure(buf.size() * sizeof(double)));
+  double* d = ctx->shard_buf.as<double>();
+  SR_HIP_CHECK(hipMemcpyAsync(d, buf.data(), buf.size() * sizeof(double), hipMemcpyHostToDevice, s));
+  SR_NCCL_CHECK(ncclAllReduce(d, d, buf.size(), ncclDouble, ncclSum, ctx->comm, s));
+  SR_HIP_CHECK(hipMemcpyAsync(buf.data(), d, buf.size() * sizeof(double), hipMemcpyDeviceToHost, s));
+  SR_HIP_CHECK(hipStreamSynchronize(s));
+  if (buf[2 * size_t(nt)] != 0.0) return local != SR_OK ? local : set_error(SR_ERR_HIP, "tree-sharded scoring failed on a peer rank");
+  for (int64_t t = 0; t < nt; ++t) {
+    out_loss[t] = T(buf[size_t(t)]);
+    out_complete[t] = buf[size_t(nt) + size_t(t)] != 0.0 ? 1 : 0;
+  }
+  return SR_OK;
+}
+
 }  // namespace
 
 // ====================================================================== C ABI
@@ -1464,7 +1779,7 @@ int sr_shutdown(sr_ctx* ctx) {
     ctx->comm = nullptr;
     for (DevBuf* b : {&ctx->prog, &ctx->outs, &ctx->part_sum, &ctx->part_flag, &ctx->pred, &ctx->row_idx, &ctx->tree_list, &ctx->range_lo, &ctx->range_hi, &ctx->range_sums, &ctx->packed,
                       &ctx->hint, &ctx->jsum_prog, &ctx->jsum_fin, &ctx->jsum_scratch, &ctx->probe_sum, &ctx->probe_flag, &ctx->g_code, &ctx->g_offsets, &ctx->g_consts, &ctx->g_const_off,
-                      &ctx->g_items, &ctx->g_part, &ctx->g_out, &ctx->derived_cols, &ctx->probe_derived})
+                      &ctx->g_items, &ctx->g_part, &ctx->g_out, &ctx->derived_cols, &ctx->probe_derived, &ctx->shard_buf})
       b->release();
     for (HostBuf* b : {&ctx->h_prog, &ctx->h_outs}) b->release();
     for (int c = 0; c < kMaxChunks; ++c) {
@@ -1615,6 +1930,7 @@ int sr_eval_loss_partials(sr_ctx* ctx, const sr_dataset* ds, int opset_id, const
   SR_HIP_CHECK(hipMemcpyAsync(out_flags, ctx->d_out_flag, size_t(nt) * sizeof(uint32_t), kind, s));
   SR_HIP_CHECK(hipStreamSynchronize(s));
   ctx->last_eval_ms = chunk_kernel_ms(ctx);
+  ctx->last_busy_ms = chunk_busy_ms(ctx);
   ctx->last_total_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
   return SR_OK;
 }
@@ -1649,12 +1965,14 @@ int sr_eval_loss_partials_packed(sr_ctx* ctx, const sr_dataset* ds, int opset_id
   if (!out_on_device) SR_HIP_CHECK(hipMemcpyAsync(out, dst, bytes, hipMemcpyDeviceToHost, s));
   SR_HIP_CHECK(hipStreamSynchronize(s));
   ctx->last_eval_ms = chunk_kernel_ms(ctx);
+  ctx->last_busy_ms = chunk_busy_ms(ctx);
   ctx->last_total_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
   return SR_OK;
 }
 
 int sr_comm_unique_id(void* out_id) {
   if (!out_id) return set_error(SR_ERR_INVALID_ARG, "NULL output");
+  if (check_runtime_pair() != SR_OK) return SR_ERR_HIP;
   ncclUniqueId id;
   const ncclResult_t r = ncclGetUniqueId(&id);
   if (r != ncclSuccess) return set_error(SR_ERR_HIP, std::string("ncclGetUniqueId: ") + ncclGetErrorString(r));
@@ -1673,6 +1991,7 @@ int sr_comm_init(sr_ctx* ctx, int nranks, int rank, const void* id_bytes) {
     ctx->comm = nullptr;
     ctx->comm_ranks = 0;
   }
+  if (check_runtime_pair() != SR_OK) return SR_ERR_HIP;
   ncclUniqueId id;
   std::memcpy(&id, id_bytes, sizeof(id));
   const ncclResult_t r = ncclCommInitRank(&ctx->comm, nranks, id, rank);
@@ -1681,6 +2000,8 @@ int sr_comm_init(sr_ctx* ctx, int nranks, int rank, const void* id_bytes) {
     return set_error(SR_ERR_HIP, std::string("ncclCommInitRank: ") + ncclGetErrorString(r));
   }
   ctx->comm_ranks = nranks;
+  ctx->comm_rank = rank;
+  ctx->comm_gen = ++g_comm_gen;
   return SR_OK;
 }
 
@@ -1716,19 +2037,80 @@ int sr_eval_loss_partials_allreduce(sr_ctx* ctx, const sr_dataset* ds, int opset
     SrProgramBatch<double> prog;
     rc = run_batch<double>(ctx, ds, opset_id, trees, nullptr, 0, n_total, loss_kind, SR_MODE_LOSS, &prog, &g);
   }
-  if (rc != SR_OK) return rc;
+  const int local = rc;
   hipStream_t s = ctx->stream;
   const size_t n = size_t(4) * size_t(nt > 0 ? nt : 0);
   SR_HIP_CHECK(ctx->packed.ensure(n * sizeof(double) + 8));
   double* dst = ctx->packed.as<double>();
-  if (nt > 0) SR_HIP_CHECK(sr_launch_pack_partials(ctx->d_out_sum, ctx->d_out_flag, int(nt), dst, s));
-  // every rank enters the collective, also with an empty batch (the counts agree: same trees)
-  const ncclResult_t r = ncclAllReduce(dst, dst, n, ncclDouble, ncclSum, ctx->comm, s);
+  if (local == SR_OK && nt > 0) SR_HIP_CHECK(sr_launch_pack_partials(ctx->d_out_sum, ctx->d_out_flag, int(nt), dst, s));
+  // every rank enters the collective, also with an empty batch (the counts agree: same trees) and
+  // after a local failure (partials zeroed, the error word after them set): then every rank fails
+  const double err_word = local != SR_OK ? 1.0 : 0.0;
+  if (local != SR_OK) SR_HIP_CHECK(hipMemsetAsync(dst, 0, n * sizeof(double), s));
+  SR_HIP_CHECK(hipMemcpyAsync(dst + n, &err_word, sizeof(double), hipMemcpyHostToDevice, s));
+  const ncclResult_t r = ncclAllReduce(dst, dst, n + 1, ncclDouble, ncclSum, ctx->comm, s);
   if (r != ncclSuccess) return set_error(SR_ERR_HIP, std::string("ncclAllReduce: ") + ncclGetErrorString(r));
+  double err_sum = 0.0;
+  SR_HIP_CHECK(hipMemcpyAsync(&err_sum, dst + n, sizeof(double), hipMemcpyDeviceToHost, s));
   if (nt > 0) SR_HIP_CHECK(hipMemcpyAsync(out_host, dst, n * sizeof(double), hipMemcpyDeviceToHost, s));
   SR_HIP_CHECK(hipStreamSynchronize(s));
+  if (err_sum != 0.0) return local != SR_OK ? local : set_error(SR_ERR_HIP, "the row-sharded step failed on a peer rank");
   ctx->last_eval_ms = chunk_kernel_ms(ctx);
+  ctx->last_busy_ms = chunk_busy_ms(ctx);
   ctx->last_total_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+  return SR_OK;
+}
+
+int sr_eval_loss_sharded(sr_ctx* ctx, const sr_dataset* ds, int opset_id, const sr_tree_batch* trees, int loss_kind,
+                         void* out_loss, uint8_t* out_complete) {
+  if (check_ctx(ctx) != SR_OK) return SR_ERR_INVALID_ARG;
+  if (!ctx->comm) return set_error(SR_ERR_INVALID_ARG, "no communicator: call sr_comm_init first");
+  int rc = validate_common(ctx, ds, opset_id, trees);
+  if (rc != SR_OK) return rc;
+  if (trees->n_trees > 0 && (!out_loss || !out_complete)) return set_error(SR_ERR_INVALID_ARG, "NULL output buffers");
+  if (!ds->y) return set_error(SR_ERR_INVALID_ARG, "dataset has no y");
+  Lock l(ctx);
+  SR_HIP_CHECK(hipSetDevice(ctx->device));
+  if (ds->dtype == SR_DTYPE_F32)
+    return eval_sharded_impl<float>(ctx, ds, opset_id, trees, loss_kind, static_cast<float*>(out_loss), out_complete);
+  return eval_sharded_impl<double>(ctx, ds, opset_id, trees, loss_kind, static_cast<double*>(out_loss), out_complete);
+}
+
+int sr_eval_loss_tree_sharded(sr_ctx* ctx, const sr_dataset* ds, int opset_id, const sr_tree_batch* trees,
+                              int loss_kind, void* out_loss, uint8_t* out_complete) {
+  if (check_ctx(ctx) != SR_OK) return SR_ERR_INVALID_ARG;
+  if (!ctx->comm) return set_error(SR_ERR_INVALID_ARG, "no communicator: call sr_comm_init first");
+  int rc = validate_common(ctx, ds, opset_id, trees);
+  if (rc != SR_OK) return rc;
+  if (trees->n_trees > 0 && (!out_loss || !out_complete)) return set_error(SR_ERR_INVALID_ARG, "NULL output buffers");
+  if (trees->n_trees > 0 && !trees->offsets) return set_error(SR_ERR_INVALID_ARG, "sr_tree_batch has NULL arrays");
+  Lock l(ctx);
+  SR_HIP_CHECK(hipSetDevice(ctx->device));
+  if (ds->dtype == SR_DTYPE_F32)
+    return eval_tree_sharded_impl<float>(ctx, ds, opset_id, trees, loss_kind, static_cast<float*>(out_loss), out_complete);
+  return eval_tree_sharded_impl<double>(ctx, ds, opset_id, trees, loss_kind, static_cast<double*>(out_loss), out_complete);
+}
+
+int sr_comm_info(sr_ctx* ctx, int* nranks, int* rank, char* paths, int64_t capacity) {
+  if (check_ctx(ctx) != SR_OK) return SR_ERR_INVALID_ARG;
+  Lock l(ctx);
+  if (nranks || rank) {
+    if (!ctx->comm) return set_error(SR_ERR_INVALID_ARG, "no communicator: call sr_comm_init first");
+    int c = 0, r = 0;
+    SR_NCCL_CHECK(ncclCommCount(ctx->comm, &c));
+    SR_NCCL_CHECK(ncclCommUserRank(ctx->comm, &r));
+    if (nranks) *nranks = c;
+    if (rank) *rank = r;
+  }
+  return sr_runtime_info(paths, capacity);
+}
+
+int sr_runtime_info(char* paths, int64_t capacity) {
+  if (!paths || capacity <= 0) return SR_OK;
+  const std::string p = runtime_paths();
+  const size_t n = std::min(p.size(), size_t(capacity - 1));
+  std::memcpy(paths, p.data(), n);
+  paths[n] = '\0';
   return SR_OK;
 }
 
@@ -1915,6 +2297,7 @@ int sr_last_phase_ms(sr_ctx* ctx, double* out, int n) {
   if (n > 5) out[5] = double(ctx->n_chunks_last);
   if (n > 6) out[6] = ctx->exact_kernel_ms;
   if (n > 7) out[7] = double(ctx->rows_last);
+  if (n > 8) out[8] = ctx->last_busy_ms;
   return SR_OK;
 }
 

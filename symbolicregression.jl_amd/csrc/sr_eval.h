@@ -97,6 +97,8 @@ hipError_t sr_launch_jsum_levels(const T* leaf_sums, int64_t n_arrays, int n_lea
                                  const int32_t* level_off, int n_levels, T* scratch, uint8_t* out, hipStream_t s);
 hipError_t sr_launch_pack_partials(const double* sum, const uint32_t* flag, int n, double* out, hipStream_t s);
 template <typename T>
+hipError_t sr_launch_finalize_packed(const double* packed, int n, double denom, T* loss, uint8_t* comp, hipStream_t s);
+template <typename T>
 hipError_t sr_launch_transpose(const T* Xh_dev, int64_t nf, int64_t n, int64_t ld, T* Xd, hipStream_t s);
 template <typename T>
 hipError_t sr_launch_pad(T* v, int64_t n, int64_t ld, T pad_value, int replicate_first, hipStream_t s);

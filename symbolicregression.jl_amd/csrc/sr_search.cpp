@@ -1173,6 +1173,60 @@ int dispatch(sr_search* s, F f) {
   return f(as_engine<double>(s));
 }
 
+// The batched constant optimiser over `trees` with a ready scorer (device or CPU callbacks): the
+// reference's optimize_constants per tree (src/ConstantOptimization.jl:29-116), all trees in lock-step.
+template <typename T>
+int optimize_common(Scorer<T>& sc, const sr_tree_batch* trees, const int64_t* row_idx, int64_t n_idx, int iterations,
+                    int nrestarts, uint64_t seed, void* out_consts, void* out_loss, uint8_t* out_improved,
+                    int64_t* out_f_calls) {
+  if (iterations < 0 || nrestarts < 0) return sr_set_error(SR_ERR_INVALID_ARG, "negative iterations / restarts");
+  const int64_t nt = trees->n_trees;
+  if (nt < 0) return sr_set_error(SR_ERR_INVALID_ARG, "negative tree count");
+  if (nt == 0) return SR_OK;
+  if (!trees->offsets || !trees->degree || !trees->op || !trees->feature || !trees->constant || !trees->val ||
+      !out_consts || !out_loss || !out_improved || !out_f_calls)
+    return sr_set_error(SR_ERR_INVALID_ARG, "NULL arrays");
+  std::vector<SrTree<T>> tv(static_cast<size_t>(nt));
+  std::vector<std::vector<double>> x0(static_cast<size_t>(nt));
+  const T* vals = static_cast<const T*>(trees->val);
+  for (int64_t t = 0; t < nt; ++t)
+    for (int64_t i = trees->offsets[t]; i < trees->offsets[t + 1]; ++i) {
+      SrNode<T> nd;
+      nd.degree = trees->degree[i];
+      nd.op = trees->op[i];
+      nd.feature = trees->feature[i];
+      nd.constant = trees->constant[i];
+      nd.val = vals[i];
+      tv[size_t(t)].push_back(nd);
+      if (nd.degree == 0 && nd.constant) x0[size_t(t)].push_back(double(nd.val));
+    }
+  SrRng rng;
+  rng.seed(seed, 0x6f7074696d697a65ull);
+  std::vector<std::vector<std::vector<double>>> restarts(static_cast<size_t>(nrestarts),
+                                                         std::vector<std::vector<double>>(static_cast<size_t>(nt)));
+  for (int64_t t = 0; t < nt; ++t)
+    for (int r = 0; r < nrestarts; ++r) draw_restart<T>(rng, x0[size_t(t)], &restarts[size_t(r)][size_t(t)]);
+  std::vector<const SrTree<T>*> ptr;
+  for (auto& t : tv) ptr.push_back(&t);
+  Flat flat;
+  const std::vector<int64_t> rows(row_idx && n_idx > 0 ? row_idx : nullptr, row_idx && n_idx > 0 ? row_idx + n_idx : nullptr);
+  std::vector<std::vector<double>> bx;
+  std::vector<uint8_t> imp;
+  std::vector<T> loss;
+  std::vector<int64_t> f_calls;
+  const int e = optimize_trees<T>(sc, flat, ptr, x0, restarts, iterations, rows, &bx, &imp, &loss, &f_calls);
+  if (e) return e;
+  size_t at = 0;
+  for (int64_t t = 0; t < nt; ++t) {
+    for (size_t q = 0; q < x0[size_t(t)].size(); ++q)
+      static_cast<T*>(out_consts)[at++] = imp[size_t(t)] ? T(bx[size_t(t)][q]) : T(x0[size_t(t)][q]);
+    static_cast<T*>(out_loss)[t] = loss[size_t(t)];
+    out_improved[t] = imp[size_t(t)];
+    out_f_calls[t] = f_calls[size_t(t)];
+  }
+  return SR_OK;
+}
+
 }  // namespace
 
 extern "C" {
@@ -1221,6 +1275,43 @@ int sr_search_create(int dtype, int64_t nfeatures, int64_t n_rows, int n_unary, 
   };
   if (dtype == SR_DTYPE_F32) return make(new Engine<float>());
   return make(new Engine<double>());
+}
+
+int sr_gen_random_population(int dtype, int64_t n_trees, int64_t nfeatures, int n_unary, int n_binary, int max_size,
+                              uint64_t seed, int64_t capacity, int64_t* offsets, uint8_t* degree, uint8_t* op,
+                              uint16_t* feature, uint8_t* constant, void* val) {
+  if (dtype != SR_DTYPE_F32 && dtype != SR_DTYPE_F64) return sr_set_error(SR_ERR_INVALID_ARG, "unknown dtype");
+  if (n_trees < 0 || nfeatures < 1 || nfeatures > 65535 || max_size < 1 || n_unary < 0 || n_binary < 0 ||
+      n_unary > 255 || n_binary > 255 || !offsets || !degree || !op || !feature || !constant || !val)
+    return sr_set_error(SR_ERR_INVALID_ARG, "bad arguments");
+  SrTreeSpec sp;
+  sp.nfeatures = int(nfeatures);
+  sp.nops[0] = n_unary;
+  sp.nops[1] = n_binary;
+  SrRng rng;
+  rng.seed(seed, 0x9e11ull);
+  auto go = [&](auto tag) -> int {
+    using T = decltype(tag);
+    T* v = static_cast<T*>(val);
+    int64_t at = 0;
+    offsets[0] = 0;
+    for (int64_t k = 0; k < n_trees; ++k) {
+      const int size = int(1 + rng.below(max_size));
+      const SrTree<T> t = sr_gen_random_tree_fixed_size<T>(size, sp, rng);
+      if (at + int64_t(t.size()) > capacity) return sr_set_error(SR_ERR_INVALID_ARG, "node capacity too small");
+      for (const SrNode<T>& nd : t) {
+        degree[at] = nd.degree;
+        op[at] = nd.op;
+        feature[at] = nd.feature;
+        constant[at] = nd.constant;
+        v[at] = nd.val;
+        ++at;
+      }
+      offsets[k + 1] = at;
+    }
+    return SR_OK;
+  };
+  return dtype == SR_DTYPE_F32 ? go(0.0f) : go(0.0);
 }
 
 int sr_search_free(sr_search* s) {
@@ -1397,66 +1488,39 @@ int sr_optimize_constants_batch(sr_ctx* ctx, const sr_dataset* ds, int opset_id,
                                 uint64_t seed, void* out_consts, void* out_loss, uint8_t* out_improved,
                                 int64_t* out_f_calls) {
   if (!ctx || !ds || !trees) return sr_set_error(SR_ERR_INVALID_ARG, "NULL context, dataset or trees");
-  if (iterations < 0 || nrestarts < 0) return sr_set_error(SR_ERR_INVALID_ARG, "negative iterations / restarts");
-  const int64_t nt = trees->n_trees;
-  if (nt < 0) return sr_set_error(SR_ERR_INVALID_ARG, "negative tree count");
-  if (nt > 0 && (!trees->offsets || !trees->degree || !trees->op || !trees->feature || !trees->constant ||
-                 !trees->val || !out_consts || !out_loss || !out_improved || !out_f_calls))
-    return sr_set_error(SR_ERR_INVALID_ARG, "NULL arrays");
   int dt = 0;
   int64_t nf = 0, n = 0;
   int rc = sr_dataset_info(ds, &dt, &nf, &n);
   if (rc) return rc;
   auto run = [&](auto zero) -> int {
     using T = decltype(zero);
-    std::vector<SrTree<T>> tv(static_cast<size_t>(nt));
-    std::vector<std::vector<double>> x0(static_cast<size_t>(nt));
-    const T* vals = static_cast<const T*>(trees->val);
-    for (int64_t t = 0; t < nt; ++t)
-      for (int64_t i = trees->offsets[t]; i < trees->offsets[t + 1]; ++i) {
-        SrNode<T> nd;
-        nd.degree = trees->degree[i];
-        nd.op = trees->op[i];
-        nd.feature = trees->feature[i];
-        nd.constant = trees->constant[i];
-        nd.val = vals[i];
-        tv[size_t(t)].push_back(nd);
-        if (nd.degree == 0 && nd.constant) x0[size_t(t)].push_back(double(nd.val));
-      }
-    SrRng rng;
-    rng.seed(seed, 0x6f7074696d697a65ull);
-    std::vector<std::vector<std::vector<double>>> restarts(static_cast<size_t>(nrestarts),
-                                                           std::vector<std::vector<double>>(static_cast<size_t>(nt)));
-    for (int64_t t = 0; t < nt; ++t)
-      for (int r = 0; r < nrestarts; ++r) draw_restart<T>(rng, x0[size_t(t)], &restarts[size_t(r)][size_t(t)]);
-    std::vector<const SrTree<T>*> ptr;
-    for (auto& t : tv) ptr.push_back(&t);
     Scorer<T> sc;
     sc.ctx = ctx;
     sc.ds = ds;
     sc.opset_id = opset_id;
     sc.loss_code = loss_kind;
-    Flat flat;
-    const std::vector<int64_t> rows(row_idx && n_idx > 0 ? row_idx : nullptr,
-                                    row_idx && n_idx > 0 ? row_idx + n_idx : nullptr);
-    std::vector<std::vector<double>> bx;
-    std::vector<uint8_t> imp;
-    std::vector<T> loss;
-    std::vector<int64_t> f_calls;
-    int e = optimize_trees<T>(sc, flat, ptr, x0, restarts, iterations, rows, &bx, &imp, &loss, &f_calls);
-    if (e) return e;
-    size_t at = 0;
-    for (int64_t t = 0; t < nt; ++t) {
-      for (size_t q = 0; q < x0[size_t(t)].size(); ++q)
-        static_cast<T*>(out_consts)[at++] = imp[size_t(t)] ? T(bx[size_t(t)][q]) : T(x0[size_t(t)][q]);
-      static_cast<T*>(out_loss)[t] = loss[size_t(t)];
-      out_improved[t] = imp[size_t(t)];
-      out_f_calls[t] = f_calls[size_t(t)];
-    }
-    return SR_OK;
+    return optimize_common<T>(sc, trees, row_idx, n_idx, iterations, nrestarts, seed, out_consts, out_loss,
+                              out_improved, out_f_calls);
   };
-  if (nt == 0) return SR_OK;
   return dt == SR_DTYPE_F32 ? run(0.0f) : run(0.0);
+}
+
+int sr_optimize_constants_callbacks(int dtype, const sr_tree_batch* trees, const int64_t* row_idx, int64_t n_idx,
+                                    int iterations, int nrestarts, uint64_t seed, sr_loss_fn loss, sr_grad_fn grad,
+                                    void* user, void* out_consts, void* out_loss, uint8_t* out_improved,
+                                    int64_t* out_f_calls) {
+  if (!trees || !loss || !grad) return sr_set_error(SR_ERR_INVALID_ARG, "NULL trees or scorer callbacks");
+  if (dtype != SR_DTYPE_F32 && dtype != SR_DTYPE_F64) return sr_set_error(SR_ERR_INVALID_ARG, "unknown dtype");
+  auto run = [&](auto zero) -> int {
+    using T = decltype(zero);
+    Scorer<T> sc;
+    sc.loss_cb = loss;
+    sc.grad_cb = grad;
+    sc.cb_user = user;
+    return optimize_common<T>(sc, trees, row_idx, n_idx, iterations, nrestarts, seed, out_consts, out_loss,
+                              out_improved, out_f_calls);
+  };
+  return dtype == SR_DTYPE_F32 ? run(0.0f) : run(0.0);
 }
 
 }  // extern "C"

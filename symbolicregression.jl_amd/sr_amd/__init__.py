@@ -23,7 +23,7 @@ from .loss import (
     score_func,
     update_baseline_loss_,
 )
-from .mutation import gen_random_population, gen_random_tree_fixed_size, make_random_leaf
+from .mutation import gen_random_batch, gen_random_population, gen_random_tree_fixed_size, make_random_leaf
 from .node import (
     Node,
     TreeBatch,
@@ -46,7 +46,7 @@ __all__ = [
     "get_scalar_constants", "set_scalar_constants", "eval_tree_array", "eval_tree_array_batch",
     "eval_loss", "eval_loss_batch", "eval_grad_batch", "eval_cost", "eval_cost_batch", "loss_to_cost",
     "update_baseline_loss_", "score_func", "compute_complexity", "gen_random_tree_fixed_size",
-    "gen_random_population", "make_random_leaf", "get_context", "device_available", "DeviceContext",
+    "gen_random_population", "gen_random_batch", "make_random_leaf", "get_context", "device_available", "DeviceContext",
     "SRError", "UnsupportedOperatorError", "optimize_constants_batch", "equation_search", "SearchOptions",
     "PopMember", "HallOfFame",
 ]

@@ -52,6 +52,10 @@ EXPORTED_SYMBOLS = (
     "sr_comm_init",
     "sr_comm_destroy",
     "sr_eval_loss_partials_allreduce",
+    "sr_eval_loss_sharded",
+    "sr_eval_loss_tree_sharded",
+    "sr_comm_info",
+    "sr_runtime_info",
     "sr_max_checks",
     "sr_jsum_range_count",
     "sr_jsum_ranges",
@@ -80,6 +84,8 @@ EXPORTED_SYMBOLS = (
     "sr_search_member_count",
     "sr_search_members",
     "sr_optimize_constants_batch",
+    "sr_gen_random_population",
+    "sr_optimize_constants_callbacks",
 )
 
 # mutation kinds in sr_search_options.mutation_weights order (SR_MUT_*)
@@ -179,6 +185,10 @@ def _load():
         "sr_comm_init": (c_int, [P, c_int, c_int, P]),
         "sr_comm_destroy": (c_int, [P]),
         "sr_eval_loss_partials_allreduce": (c_int, [P, P, c_int, POINTER(SrTreeBatch), c_int64, c_int, P]),
+        "sr_eval_loss_sharded": (c_int, [P, P, c_int, POINTER(SrTreeBatch), c_int, P, P]),
+        "sr_eval_loss_tree_sharded": (c_int, [P, P, c_int, POINTER(SrTreeBatch), c_int, P, P]),
+        "sr_comm_info": (c_int, [P, POINTER(c_int), POINTER(c_int), c_char_p, c_int64]),
+        "sr_runtime_info": (c_int, [c_char_p, c_int64]),
         "sr_eval_loss_partials_packed": (
             c_int,
             [P, P, c_int, POINTER(SrTreeBatch), c_int64, c_int, P, c_int],
@@ -226,6 +236,14 @@ def _load():
         "sr_search_get_info": (c_int, [P, POINTER(SrSearchInfo)]),
         "sr_search_member_count": (c_int, [P, c_int, POINTER(c_int64), POINTER(c_int64)]),
         "sr_search_members": (c_int, [P, c_int, P, P, P, P, P, P, P, P, P, P, P, P]),
+        "sr_optimize_constants_callbacks": (
+            c_int,
+            [c_int, POINTER(SrTreeBatch), P, c_int64, c_int, c_int, ctypes.c_uint64, LOSS_FN, GRAD_FN, P, P, P, P, P],
+        ),
+        "sr_gen_random_population": (
+            c_int,
+            [c_int, c_int64, c_int64, c_int, c_int, c_int, ctypes.c_uint64, c_int64, P, P, P, P, P, P],
+        ),
         "sr_optimize_constants_batch": (
             c_int,
             [P, P, c_int, POINTER(SrTreeBatch), P, c_int64, c_int, c_int, c_int, ctypes.c_uint64, P, P, P, P],
@@ -253,6 +271,13 @@ def check(rc: int) -> None:
     if rc == SR_ERR_UNSUPPORTED_OP:
         raise UnsupportedOperatorError(rc, msg)
     raise SRError(rc, msg)
+
+
+def runtime_info() -> dict:
+    """{"hip": file, "rccl": file}: the HIP runtime and RCCL the library's calls bind to (no device needed)."""
+    buf = ctypes.create_string_buffer(4096)
+    check(lib.sr_runtime_info(buf, len(buf)))
+    return dict(kv.split("=", 1) for kv in buf.value.decode().split(";") if "=" in kv)
 
 
 def device_count() -> int:

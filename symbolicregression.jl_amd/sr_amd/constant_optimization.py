@@ -55,3 +55,30 @@ def optimize_constants_batch(trees, dataset, options, rng=None, *, iterations=No
     imp = improved[:nt].astype(bool)
     num_evals = (f_calls[:nt] + imp.astype(np.int64)) * dataset.dataset_fraction()
     return new_tb, losses[:nt].copy(), imp, num_evals
+
+
+def optimize_constants_callbacks(trees, loss_fn, grad_fn, *, dtype=np.float64, seed=0, iterations=8, nrestarts=2,
+                                 rows=None):
+    """The same batched optimiser with CPU scorers (``sr_optimize_constants_callbacks``; test seam):
+    loss_fn(TreeBatch, rows) -> losses, grad_fn(TreeBatch, rows) -> (losses, gradients).  The restart
+    draws come from ``seed`` exactly as ``optimize_constants_batch``'s.  Returns (new_batch, losses,
+    improved, f_calls)."""
+    from .loss import _as_batch
+    from .search import make_callbacks
+
+    tb = _as_batch(trees, dtype)
+    nt = tb.n_trees
+    n_const = int(np.count_nonzero(tb.constant_mask()))
+    consts = np.zeros(max(1, n_const), dtype=dtype)
+    losses = np.zeros(max(1, nt), dtype=dtype)
+    improved = np.zeros(max(1, nt), dtype=np.uint8)
+    f_calls = np.zeros(max(1, nt), dtype=np.int64)
+    cbs = make_callbacks(dtype, loss_fn, grad_fn)
+    r = None if rows is None else np.ascontiguousarray(rows, dtype=np.int64)
+    p = lambda a: None if a is None else a.ctypes.data_as(ctypes.c_void_p)  # noqa: E731
+    s = tb.to_struct()
+    _lib.check(_lib.lib.sr_optimize_constants_callbacks(
+        _lib.SR_DTYPE_F32 if np.dtype(dtype) == np.float32 else _lib.SR_DTYPE_F64, ctypes.byref(s), p(r),
+        0 if r is None else r.size, int(iterations), int(nrestarts), ctypes.c_uint64(int(seed)), cbs[0], cbs[1], None,
+        p(consts), p(losses), p(improved), p(f_calls)))
+    return tb.with_constants(consts[:n_const]), losses[:nt].copy(), improved[:nt].astype(bool), f_calls[:nt].copy()

@@ -90,6 +90,12 @@ class DeviceContext:
         _lib.check(_lib.lib.sr_last_phase_ms(self.handle, out, 8))
         return int(out[7])
 
+    def last_busy_ms(self):
+        """Device-busy time of the last call's interpreter launches: the union of their intervals (ms)."""
+        out = (ctypes.c_double * 9)()
+        _lib.check(_lib.lib.sr_last_phase_ms(self.handle, out, 9))
+        return float(out[8])
+
     def last_launches(self):
         """Interpreter launches of the last eval_loss call (chunked compile/launch pipeline)."""
         out = (ctypes.c_double * 6)()
@@ -128,6 +134,13 @@ def get_context(device: int | None = None) -> DeviceContext:
             ctx = DeviceContext(dev)
             _contexts[dev] = ctx
         return ctx
+
+
+def peek_context(device: int | None = None):
+    """This process's context for `device` if one exists (no device call otherwise), else None."""
+    dev = default_device() if device is None else int(device)
+    with _lock:
+        return _contexts.get(dev)
 
 
 def device_available() -> bool:

@@ -1,16 +1,24 @@
-"""Row-sharded scoring across GPUs (one process per GPU, torch.distributed over RCCL).
+"""Multi-GPU scoring: rows sharded (C4) and trees sharded, one process per GPU.
 
-Each rank holds one row shard of the dataset (HBM-resident), scores every tree on it and packs its
-per-tree partials into one [4, n_trees] float64 device tensor (`sr_eval_loss_partials_packed`:
-Σ loss, then the NONFINITE / BIG / STATIC flag bits as 0/1), which ONE all-reduce (SUM) combines —
-the partials never leave the GPU.  Trees that came close to overflowing a checked array sum (BIG
-only: rare) get the exact verdict of DynamicExpressions' isfinite(sum(x)) in Julia's pairwise order
-over the GLOBAL row range: each rank folds the leaf blocks it holds (`sr_jsum_partials`), the folds
-are all-gathered, and `sr_jsum_finite` adds them in Base.mapreduce_impl's recursion order
-(DESIGN.md §7).  `sr_finalize_losses` then turns sums and verdicts into losses.
+The data path's exchanges run inside the library on its own RCCL communicator over xGMI
+(`init_device_comm` → C ABI `sr_comm_*`); torch.distributed is used only as a CPU channel (a gloo
+group: the 128-byte RCCL unique id, barriers, small host objects).  torch never touches the GPU:
+its bundled HIP runtime cannot share the device with the library's in one process.
 
-`partials_fn` / `exact_fn` default to the GPU calls; tests inject CPU stand-ins to exercise the
-combine logic with the gloo backend.
+Row sharding, `eval_loss_sharded`: rank r holds global rows [Σ_{q<r} n_q, Σ_{q<=r} n_q).  With a
+device communicator the whole step is ONE library call (`sr_eval_loss_sharded`): the shard runs
+the single-GPU launch pipeline, its packed [4, n_trees] partials (Σ loss, then the NONFINITE / BIG /
+STATIC flag bits as 0/1) are summed by one in-place RCCL all-reduce, losses are finalized on the
+device, and the rare BIG trees get DynamicExpressions' exact isfinite(sum(x)) verdict in Julia's
+pairwise order over the GLOBAL rows (each rank folds the leaf blocks it holds; the folds are
+all-gathered; `sr_jsum_finite`'s recursion-order combine).
+
+Tree sharding, `eval_loss_tree_sharded`: the dataset is replicated, the trees are dealt over the
+ranks by size, each rank scores its share, one all-reduce hands every rank every result
+(`sr_eval_loss_tree_sharded`).
+
+Without a device communicator (tests on CPU: `partials_fn` / `exact_fn` / `score_fn` stand-ins for
+the GPU calls) the same protocols run over the gloo group on host arrays.
 """
 from __future__ import annotations
 
@@ -19,7 +27,7 @@ import ctypes
 import numpy as np
 
 from . import _lib
-from .device import get_context
+from .device import get_context, peek_context
 from .loss import _as_batch
 
 
@@ -27,22 +35,26 @@ def _dtype_code(dtype):
     return _lib.SR_DTYPE_F32 if np.dtype(dtype) == np.float32 else _lib.SR_DTYPE_F64
 
 
-def gpu_partials_packed(tb, shard, options, n_total, *, device_tensor=False, ctx=None):
-    """This rank's packed partials [4, n_trees] f64 on its row shard (GPU).  device_tensor=True
-    returns a torch tensor on this rank's GPU written by the library in place (no host copy)."""
+def _require_gloo(group):
+    import torch.distributed as dist
+
+    backend = dist.get_backend(group)
+    if backend != "gloo":
+        # an "nccl" group would make torch initialise its own HIP runtime on the GPU, which cannot share
+        # the device with the library's; the data path's collectives are the library's own RCCL
+        raise RuntimeError(f"sr_amd.distributed needs a gloo process group as its CPU channel (got {backend!r}); "
+                           "the device collectives run on the library's RCCL communicator (init_device_comm)")
+
+
+def gpu_partials_packed(tb, shard, options, n_total, ctx=None):
+    """This rank's packed partials [4, n_trees] f64 on its row shard (GPU), on the host."""
     ctx = ctx or get_context()
     nt = tb.n_trees
     s = tb.to_struct()
-    args = (ctx.handle, shard.device_handle(ctx), ctx.opset_id(options.operators), ctypes.byref(s), int(n_total),
-            ctx.loss_code(options))
-    if device_tensor:
-        import torch
-
-        out = torch.empty((4, max(nt, 1)), dtype=torch.float64, device=torch.device("cuda", ctx.device))
-        _lib.check(_lib.lib.sr_eval_loss_partials_packed(*args, ctypes.c_void_p(out.data_ptr()), 1))
-        return out[:, :nt]
     out = np.zeros((4, nt), dtype=np.float64)
-    _lib.check(_lib.lib.sr_eval_loss_partials_packed(*args, out.ctypes.data_as(ctypes.c_void_p), 0))
+    _lib.check(_lib.lib.sr_eval_loss_partials_packed(
+        ctx.handle, shard.device_handle(ctx), ctx.opset_id(options.operators), ctypes.byref(s), int(n_total),
+        ctx.loss_code(options), out.ctypes.data_as(ctypes.c_void_p), 0))
     return out
 
 
@@ -50,12 +62,12 @@ SR_COMM_ID_BYTES = 128
 
 
 def init_device_comm(group=None, ctx=None):
-    """Create this rank's RCCL communicator inside the library (C ABI sr_comm_*), on the library's
-    own HIP runtime; `group` is any torch.distributed group used only to broadcast rank 0's unique
-    id (gloo: no torch GPU state, which could not share the device with the library's runtime).
-    After this, `eval_loss_sharded` sums the partials with one device all-reduce over xGMI."""
+    """Create this rank's RCCL communicator inside the library (C ABI sr_comm_*) over the ranks of
+    `group` (a gloo group: it only broadcasts rank 0's unique id).  The communicator's size and rank
+    must equal the group's; after this the sharded calls exchange on the devices over xGMI."""
     import torch.distributed as dist
 
+    _require_gloo(group)
     ctx = ctx or get_context()
     buf = ctypes.create_string_buffer(SR_COMM_ID_BYTES)
     if dist.get_rank(group) == 0:
@@ -63,15 +75,46 @@ def init_device_comm(group=None, ctx=None):
     obj = [bytes(buf.raw)]
     dist.broadcast_object_list(obj, src=0, group=group)
     raw = ctypes.create_string_buffer(obj[0], SR_COMM_ID_BYTES)
-    _lib.check(_lib.lib.sr_comm_init(ctx.handle, dist.get_world_size(group), dist.get_rank(group),
-                                     ctypes.cast(raw, ctypes.c_void_p)))
+    world, rank = dist.get_world_size(group), dist.get_rank(group)
+    _lib.check(_lib.lib.sr_comm_init(ctx.handle, world, rank, ctypes.cast(raw, ctypes.c_void_p)))
+    info = comm_info(ctx)
+    if (info["nranks"], info["rank"]) != (world, rank):
+        raise RuntimeError(f"RCCL communicator is rank {info['rank']} of {info['nranks']}, group says {rank} of {world}")
     ctx.has_comm = True
+    ctx.comm_world, ctx.comm_rank = world, rank
     return ctx
+
+
+def destroy_device_comm(ctx=None):
+    ctx = ctx or get_context()
+    _lib.check(_lib.lib.sr_comm_destroy(ctx.handle))
+    ctx.has_comm = False
+
+
+def comm_info(ctx=None):
+    """{"nranks", "rank"} as RCCL reports them, and the files of the HIP runtime / RCCL in use."""
+    ctx = ctx or get_context()
+    n, r = ctypes.c_int(), ctypes.c_int()
+    buf = ctypes.create_string_buffer(4096)
+    _lib.check(_lib.lib.sr_comm_info(ctx.handle, ctypes.byref(n), ctypes.byref(r), buf, len(buf)))
+    out = dict(kv.split("=", 1) for kv in buf.value.decode().split(";") if "=" in kv)
+    out.update(nranks=int(n.value), rank=int(r.value))
+    return out
+
+
+def _check_group(ctx, group):
+    """The device communicator must span exactly the ranks of `group` (else the sums and the host-side
+    verdicts would come from different sets of ranks)."""
+    import torch.distributed as dist
+
+    if (getattr(ctx, "comm_world", None), getattr(ctx, "comm_rank", None)) != (dist.get_world_size(group),
+                                                                              dist.get_rank(group)):
+        raise RuntimeError("the device communicator was created over another group of ranks")
 
 
 def gpu_partials_allreduce(tb, shard, options, n_total, ctx=None):
     """Every rank's packed partials [4, n_trees], summed on the devices by the library's RCCL
-    communicator (init_device_comm) -> numpy on every rank."""
+    communicator (`sr_eval_loss_partials_allreduce`) -> numpy on every rank."""
     ctx = ctx or get_context()
     nt = tb.n_trees
     s = tb.to_struct()
@@ -155,62 +198,162 @@ def unpack_flags(packed):
     return packed[0].copy(), flags
 
 
-def eval_loss_sharded(trees, shard, options, n_total, *, denom=None, group=None, partials_fn=None, exact_fn=None):
-    """Losses of every tree over the union of all ranks' row shards -> (losses[T], complete[bool]).
-
-    `denom`: global denominator (Σ rows, or Σ weights); defaults to `n_total` for unweighted data.
-    `partials_fn(tb)` -> packed [4, n_trees] partials (numpy, or a torch tensor on this rank's GPU);
-    `exact_fn(tb, tree_list, max_checks, row_offset)` -> [n_list, max_checks, n_ranges] folds.
-    """
+def _allreduce_host(arr, group, op="sum"):
     import torch
+    import torch.distributed as dist
+
+    t = torch.from_numpy(np.ascontiguousarray(arr))
+    dist.all_reduce(t, op=dist.ReduceOp.SUM if op == "sum" else dist.ReduceOp.MAX, group=group)
+    return t.numpy()
+
+
+def eval_loss_sharded(trees, shard, options, n_total=None, *, denom=None, group=None, partials_fn=None,
+                      exact_fn=None):
+    """Losses of every tree over the union of all ranks' row shards -> (losses[T], complete[bool]),
+    the same on every rank.  Collective: every rank calls it with the same trees.
+
+    With a device communicator (init_device_comm) this is one `sr_eval_loss_sharded` call.  Otherwise
+    the protocol runs over the gloo `group` on host arrays: `partials_fn(tb)` -> this shard's packed
+    [4, n_trees] partials (default: the GPU call), `exact_fn(tb, tree_list, max_checks, row_offset)`
+    -> [n_list, max_checks, n_ranges] folds (default: the GPU call).  A failure on one rank is
+    all-reduced as an error word, so every rank raises instead of waiting in a collective."""
     import torch.distributed as dist
 
     full = shard.full
     tb = _as_batch(trees, full.dtype)
-    on_gpu = dist.get_backend(group) == "nccl"
-    if partials_fn is None and getattr(get_context(), "has_comm", False):
-        # the path's one exchange step on the devices: the library's RCCL all-reduce (init_device_comm)
-        packed = gpu_partials_allreduce(tb, shard, options, n_total)
-    else:
-        partials_fn = partials_fn or (lambda tb_: gpu_partials_packed(tb_, shard, options, n_total, device_tensor=on_gpu))
-        packed = partials_fn(tb)
-        t = packed if isinstance(packed, torch.Tensor) else torch.from_numpy(np.ascontiguousarray(packed))
-        if on_gpu and not t.is_cuda:
-            t = t.cuda()
-        t = t.contiguous()
-        # the path's one exchange step: every rank's [4, n_trees] partials, summed
-        dist.all_reduce(t, op=dist.ReduceOp.SUM, group=group)
-        packed = t.cpu().numpy()
-    sums, flags = unpack_flags(packed)
+    ctx = peek_context()
+    if partials_fn is None and exact_fn is None and getattr(ctx, "has_comm", False):
+        _check_group(ctx, group)
+        nt = tb.n_trees
+        s = tb.to_struct()
+        loss = np.empty(nt, dtype=full.dtype)
+        comp = np.empty(nt, dtype=np.uint8)
+        _lib.check(_lib.lib.sr_eval_loss_sharded(
+            ctx.handle, shard.device_handle(ctx), ctx.opset_id(options.operators), ctypes.byref(s),
+            ctx.loss_code(options), loss.ctypes.data_as(ctypes.c_void_p), comp.ctypes.data_as(ctypes.c_void_p)))
+        if n_total is not None:
+            sizes = [None] * dist.get_world_size(group)
+            dist.all_gather_object(sizes, int(shard.n), group=group)
+            if sum(sizes) != int(n_total):
+                raise ValueError(f"n_total {n_total} != the shards' {sum(sizes)} rows")
+        return loss, comp.astype(bool)
+
+    _require_gloo(group)
+    world, rank = dist.get_world_size(group), dist.get_rank(group)
+    sizes = [None] * world
+    dist.all_gather_object(sizes, int(shard.n), group=group)
+    offs = np.concatenate([[0], np.cumsum(sizes)]).astype(np.int64)
+    if n_total is None:
+        n_total = int(offs[-1])
+    elif int(offs[-1]) != int(n_total):
+        raise ValueError(f"n_total {n_total} != the shards' {int(offs[-1])} rows")
+    partials_fn = partials_fn or (lambda tb_: gpu_partials_packed(tb_, shard, options, n_total))
+    nt = tb.n_trees
+    buf = np.zeros(4 * nt + 1, dtype=np.float64)
+    err = None
+    try:
+        buf[:4 * nt] = np.asarray(partials_fn(tb), dtype=np.float64).reshape(-1)
+    except Exception as e:  # noqa: BLE001 - every rank must still enter the collective
+        err = e
+        buf[:] = 0.0
+        buf[-1] = 1.0
+    # the path's one exchange step: every rank's [4, n_trees] partials (and error words), summed
+    buf = _allreduce_host(buf, group)
+    if err is not None:
+        raise err
+    if buf[-1] != 0.0:
+        raise RuntimeError("the row-sharded step failed on a peer rank")
+    sums, flags = unpack_flags(buf[:4 * nt].reshape(4, nt))
     big = np.nonzero(((flags & (_lib.SR_FLAG_NONFINITE | _lib.SR_FLAG_STATIC)) == 0) &
                      ((flags & _lib.SR_FLAG_BIG) != 0))[0]
     ok = None
     if big.size:
         # rare: exact Julia-order verdict over the global rows
-        world = dist.get_world_size(group)
-        sizes = [None] * world
-        dist.all_gather_object(sizes, int(shard.n), group=group)
-        offs = np.concatenate([[0], np.cumsum(sizes)]).astype(np.int64)
-        rank = dist.get_rank(group)
-        if exact_fn is None:
-            # only the BIG trees are compiled again (a sub-batch: the check numbering is per tree)
-            sub = tb.take(big)
-            mc = gpu_max_checks(sub, options)
-            mine = np.ascontiguousarray(gpu_jsum(sub, shard, options, np.arange(big.size), mc, int(offs[rank]), n_total))
-        else:
-            mine = np.ascontiguousarray(exact_fn(tb, big, 1, int(offs[rank])))
-        mc = mine.shape[1]
+        try:
+            if exact_fn is None:
+                # only the BIG trees are compiled again (a sub-batch: the check numbering is per tree)
+                sub = tb.take(big)
+                mc = gpu_max_checks(sub, options)
+                mine = np.ascontiguousarray(gpu_jsum(sub, shard, options, np.arange(big.size), mc, int(offs[rank]),
+                                                     n_total))
+            else:
+                mine = np.ascontiguousarray(exact_fn(tb, big, 1, int(offs[rank])))
+            payload = (None, mine)
+        except Exception as e:  # noqa: BLE001
+            payload = (repr(e), None)
         every = [None] * world
-        dist.all_gather_object(every, mine, group=group)
-        fin = jsum_finite(full.dtype, n_total, offs, [v.reshape(big.size * mc, -1) for v in every])
+        dist.all_gather_object(every, payload, group=group)
+        bad = [r for r, (e, _) in enumerate(every) if e is not None]
+        if bad:
+            raise RuntimeError(f"the exact-sum pass failed on rank(s) {bad}: {every[bad[0]][0]}")
+        mc = every[0][1].shape[1]
+        fin = jsum_finite(full.dtype, n_total, offs, [v.reshape(big.size * mc, -1) for _, v in every])
         ok = fin.reshape(big.size, mc).all(axis=1).astype(np.uint8)
     if denom is None:
         if full.weights is not None:
-            local = torch.tensor([float(np.sum(full.weights, dtype=np.float64))], dtype=torch.float64)
-            if on_gpu:
-                local = local.cuda()
-            dist.all_reduce(local, op=dist.ReduceOp.SUM, group=group)
-            denom = float(local.cpu()[0])
+            denom = float(_allreduce_host(np.array([np.sum(full.weights, dtype=np.float64)]), group)[0])
         else:
             denom = float(n_total)
     return finalize(full.dtype, sums, flags, denom, big, ok)
+
+
+def tree_owners(tb, world):
+    """Owner rank of every tree for tree sharding (the library's rule, sr_eval_loss_tree_sharded):
+    trees sorted by node count (largest first, stable), dealt in snake order 0..N-1, N-1..0, ..."""
+    sizes = np.diff(np.asarray(tb.offsets, dtype=np.int64))
+    order = np.argsort(-sizes, kind="stable")
+    k = np.arange(len(order))
+    rnd, pos = k // world, k % world
+    owner = np.where(rnd % 2 == 1, world - 1 - pos, pos)
+    out = np.empty(len(order), dtype=np.int64)
+    out[order] = owner
+    return out
+
+
+def eval_loss_tree_sharded(trees, dataset, options, *, group=None, score_fn=None):
+    """Tree-sharded batched eval_loss: every rank holds the whole dataset; each scores
+    the trees `tree_owners` gives it and every rank gets every (loss, complete).  Collective.
+    With a device communicator: one `sr_eval_loss_tree_sharded` call (RCCL all-reduce of the results);
+    otherwise over the gloo group with `score_fn(sub_batch) -> (losses, complete)` (default: the
+    single-GPU `eval_loss_batch`)."""
+    import torch.distributed as dist
+
+    full = getattr(dataset, "full", dataset)
+    tb = _as_batch(trees, full.dtype)
+    ctx = peek_context()
+    if score_fn is None and getattr(ctx, "has_comm", False):
+        _check_group(ctx, group)
+        nt = tb.n_trees
+        s = tb.to_struct()
+        loss = np.empty(nt, dtype=full.dtype)
+        comp = np.empty(nt, dtype=np.uint8)
+        _lib.check(_lib.lib.sr_eval_loss_tree_sharded(
+            ctx.handle, dataset.device_handle(ctx), ctx.opset_id(options.operators), ctypes.byref(s),
+            ctx.loss_code(options), loss.ctypes.data_as(ctypes.c_void_p), comp.ctypes.data_as(ctypes.c_void_p)))
+        return loss, comp.astype(bool)
+
+    _require_gloo(group)
+    world, rank = dist.get_world_size(group), dist.get_rank(group)
+    if score_fn is None:
+        from .loss import eval_loss_batch
+
+        def score_fn(sub):
+            return eval_loss_batch(sub, dataset, options)
+    mine = np.nonzero(tree_owners(tb, world) == rank)[0]
+    nt = tb.n_trees
+    buf = np.zeros(2 * nt + 1, dtype=np.float64)
+    err = None
+    try:
+        l, c = score_fn(tb.take(mine))
+        buf[mine] = np.asarray(l, dtype=np.float64)
+        buf[nt + mine] = np.asarray(c, dtype=np.float64)
+    except Exception as e:  # noqa: BLE001 - every rank must still enter the collective
+        err = e
+        buf[:] = 0.0
+        buf[-1] = 1.0
+    buf = _allreduce_host(buf, group)
+    if err is not None:
+        raise err
+    if buf[-1] != 0.0:
+        raise RuntimeError("tree-sharded scoring failed on a peer rank")
+    return buf[:nt].astype(full.dtype), buf[nt:2 * nt] != 0.0

@@ -78,3 +78,26 @@ def gen_random_population(n_trees: int, options, nfeatures: int, *, max_size: in
     rng = np.random.default_rng(seed)
     sizes = rng.integers(1, max_size + 1, size=n_trees)
     return [gen_random_tree_fixed_size(int(s), options, nfeatures, dtype, rng) for s in sizes]
+
+
+def gen_random_batch(n_trees: int, options, nfeatures: int, *, max_size: int = 30, dtype=np.float32, seed: int = 1):
+    """A TreeBatch of ``n_trees`` random trees (``node_count ~ U{1..max_size}``) from the library's native
+    gen_random_tree_fixed_size (C ABI ``sr_gen_random_population``; the engine's generator and draws,
+    one stream keyed by ``seed``) — the same distribution as ``gen_random_population`` at C speed."""
+    import ctypes
+
+    from . import _lib
+    from .node import TreeBatch
+
+    cap = int(n_trees) * int(max_size)
+    offs = np.zeros(n_trees + 1, np.int64)
+    deg, op, con = (np.zeros(max(cap, 1), np.uint8) for _ in range(3))
+    feat = np.zeros(max(cap, 1), np.uint16)
+    val = np.zeros(max(cap, 1), dtype)
+    p = lambda a: a.ctypes.data_as(ctypes.c_void_p)  # noqa: E731
+    _lib.check(_lib.lib.sr_gen_random_population(
+        _lib.SR_DTYPE_F32 if np.dtype(dtype) == np.float32 else _lib.SR_DTYPE_F64, int(n_trees), int(nfeatures),
+        len(options.operators.unaops), len(options.operators.binops), int(max_size), int(seed), cap, p(offs), p(deg),
+        p(op), p(feat), p(con), p(val)))
+    nn = int(offs[-1])
+    return TreeBatch(offs, deg[:nn].copy(), op[:nn].copy(), feat[:nn].copy(), con[:nn].copy(), val[:nn].copy())

@@ -108,6 +108,66 @@ class SearchResult:
     host_s: float = 0.0
 
 
+def make_callbacks(dtype, loss_fn, grad_fn=None):
+    """(sr_loss_fn, sr_grad_fn) ctypes callbacks around Python scorers: loss_fn(TreeBatch, rows or None)
+    -> losses (Inf where incomplete); grad_fn(TreeBatch, rows) -> (losses, gradients over the batch's
+    constants).  Keep the returned objects alive while the library may call them."""
+    dtype = np.dtype(dtype)
+
+    def batch_of(p):
+        s = p.contents
+        nt = int(s.n_trees)
+        offs = np.ctypeslib.as_array(s.offsets, shape=(nt + 1,)).copy()
+        nn = int(offs[-1])
+
+        def arr(ptr, t):
+            return np.ctypeslib.as_array(ptr, shape=(nn,)).copy() if nn else np.zeros(0, t)
+        val = np.ctypeslib.as_array(ctypes.cast(s.val, ctypes.POINTER(
+            ctypes.c_float if dtype == np.float32 else ctypes.c_double)), shape=(nn,)).copy()
+        return TreeBatch(offs, arr(s.degree, np.uint8), arr(s.op, np.uint8), arr(s.feature, np.uint16),
+                         arr(s.constant, np.uint8), val)
+
+    def rows_of(p, n):
+        if not p or n <= 0:
+            return None
+        return np.ctypeslib.as_array(ctypes.cast(p, ctypes.POINTER(ctypes.c_int64)), shape=(n,)).copy()
+
+    def out_arr(p, n, t):
+        return np.ctypeslib.as_array(ctypes.cast(p, ctypes.POINTER(t)), shape=(n,))
+
+    ct = ctypes.c_float if dtype == np.float32 else ctypes.c_double
+
+    def loss_cb(user, trees, rows, n_idx, out_loss, out_complete):
+        try:
+            tb = batch_of(trees)
+            losses = np.asarray(loss_fn(tb, rows_of(rows, n_idx)), dtype=dtype)
+            out_arr(out_loss, tb.n_trees, ct)[:] = losses
+            out_arr(out_complete, tb.n_trees, ctypes.c_uint8)[:] = np.isfinite(losses)
+            return 0
+        except Exception:  # pragma: no cover - surfaced as an error code
+            import traceback
+            traceback.print_exc()
+            return _lib.SR_ERR_INVALID_ARG
+
+    def grad_cb(user, trees, rows, n_idx, out_loss, out_grad, out_complete):
+        try:
+            tb = batch_of(trees)
+            losses, g = grad_fn(tb, rows_of(rows, n_idx))
+            losses = np.asarray(losses, dtype=dtype)
+            out_arr(out_loss, tb.n_trees, ct)[:] = losses
+            nc = int(np.count_nonzero(tb.constant_mask()))
+            if nc:
+                out_arr(out_grad, nc, ct)[:] = np.asarray(g, dtype=dtype)
+            out_arr(out_complete, tb.n_trees, ctypes.c_uint8)[:] = np.isfinite(losses)
+            return 0
+        except Exception:  # pragma: no cover
+            import traceback
+            traceback.print_exc()
+            return _lib.SR_ERR_INVALID_ARG
+
+    return _lib.LOSS_FN(loss_cb), (_lib.GRAD_FN(grad_cb) if grad_fn else _lib.GRAD_FN())
+
+
 def search_options_struct(options, so: SearchOptions) -> _lib.SrSearchOptions:
     """Options + SearchOptions -> sr_search_options (Float32 fields as the reference stores them)."""
     o = _lib.SrSearchOptions()
@@ -196,60 +256,14 @@ class NativeSearch:
     def use_callbacks(self, loss_fn, grad_fn=None):
         """CPU scorers (tests): loss_fn(TreeBatch, rows or None) -> losses (Inf where incomplete);
         grad_fn(TreeBatch, rows) -> (losses, gradients over the batch's constants)."""
-        dtype = self.dtype
-
-        def batch_of(p):
-            s = p.contents
-            nt = int(s.n_trees)
-            offs = np.ctypeslib.as_array(s.offsets, shape=(nt + 1,)).copy()
-            nn = int(offs[-1])
-            def arr(ptr, t):
-                return np.ctypeslib.as_array(ptr, shape=(nn,)).copy() if nn else np.zeros(0, t)
-            val = np.ctypeslib.as_array(ctypes.cast(s.val, ctypes.POINTER(
-                ctypes.c_float if dtype == np.float32 else ctypes.c_double)), shape=(nn,)).copy()
-            return TreeBatch(offs, arr(s.degree, np.uint8), arr(s.op, np.uint8), arr(s.feature, np.uint16),
-                             arr(s.constant, np.uint8), val)
-
-        def rows_of(p, n):
-            if not p or n <= 0:
-                return None
-            return np.ctypeslib.as_array(ctypes.cast(p, ctypes.POINTER(ctypes.c_int64)), shape=(n,)).copy()
-
-        def out_arr(p, n, t):
-            return np.ctypeslib.as_array(ctypes.cast(p, ctypes.POINTER(t)), shape=(n,))
-
-        ct = ctypes.c_float if dtype == np.float32 else ctypes.c_double
-
-        def loss_cb(user, trees, rows, n_idx, out_loss, out_complete):
-            try:
-                tb = batch_of(trees)
-                losses = np.asarray(loss_fn(tb, rows_of(rows, n_idx)), dtype=dtype)
-                out_arr(out_loss, tb.n_trees, ct)[:] = losses
-                out_arr(out_complete, tb.n_trees, ctypes.c_uint8)[:] = np.isfinite(losses)
-                return 0
-            except Exception:  # pragma: no cover - surfaced as an error code
-                import traceback
-                traceback.print_exc()
-                return _lib.SR_ERR_INVALID_ARG
-
-        def grad_cb(user, trees, rows, n_idx, out_loss, out_grad, out_complete):
-            try:
-                tb = batch_of(trees)
-                losses, g = grad_fn(tb, rows_of(rows, n_idx))
-                losses = np.asarray(losses, dtype=dtype)
-                out_arr(out_loss, tb.n_trees, ct)[:] = losses
-                nc = int(np.count_nonzero(tb.constant_mask()))
-                if nc:
-                    out_arr(out_grad, nc, ct)[:] = np.asarray(g, dtype=dtype)
-                out_arr(out_complete, tb.n_trees, ctypes.c_uint8)[:] = np.isfinite(losses)
-                return 0
-            except Exception:  # pragma: no cover
-                import traceback
-                traceback.print_exc()
-                return _lib.SR_ERR_INVALID_ARG
-
-        self._cbs = (_lib.LOSS_FN(loss_cb), _lib.GRAD_FN(grad_cb) if grad_fn else _lib.GRAD_FN())
+        self._cbs = make_callbacks(self.dtype, loss_fn, grad_fn)
         _lib.check(_lib.lib.sr_search_use_callbacks(self.h, self._cbs[0], self._cbs[1], None))
+
+    def use_native_callbacks(self, loss_addr, grad_addr, user):
+        """C scorers given as raw function addresses (sr_loss_fn / sr_grad_fn) and their user pointer:
+        a host port answering every scoring call without Python in the loop (bench's CPU baseline)."""
+        self._cbs = (_lib.LOSS_FN(loss_addr), _lib.GRAD_FN(grad_addr) if grad_addr else _lib.GRAD_FN(), user)
+        _lib.check(_lib.lib.sr_search_use_callbacks(self.h, self._cbs[0], self._cbs[1], user))
 
     def start(self, niterations):
         _lib.check(_lib.lib.sr_search_start(self.h, int(niterations)))
@@ -317,7 +331,8 @@ def _torch_comm():
 
 
 def equation_search(X=None, y=None, *, niterations=10, options, weights=None, search_options=None, seed=0,
-                    verbosity=0, dataset=None, distributed=False, scoring_lanes=2, _loss_fn=None, _grad_fn=None):
+                    verbosity=0, dataset=None, distributed=False, scoring_lanes=2, _loss_fn=None, _grad_fn=None,
+                    _native_scorer=None):
     """Batched-island ``equation_search`` (src/SymbolicRegression.jl:967-1216) -> SearchResult.
 
     distributed=True (torch.distributed initialised, one process per GPU; SURVEY §8(e) island
@@ -326,14 +341,18 @@ def equation_search(X=None, y=None, *, niterations=10, options, weights=None, se
     and every rank replays the head's island-by-island bookkeeping identically.
     scoring_lanes: device contexts (streams) the rank's islands are split over, one host thread each,
     so device round trips overlap; results do not depend on it (num_evals up to rounding).
-    ``_loss_fn`` / ``_grad_fn`` replace the device scorer with CPU callbacks (tests only)."""
+    ``_loss_fn`` / ``_grad_fn`` replace the device scorer with CPU callbacks (tests only);
+    ``_native_scorer`` (an object with ``loss_addr``, ``grad_addr``, ``user``: C callbacks) likewise,
+    without Python in the loop (bench.py's CPU baseline)."""
     so = search_options or SearchOptions()
     comm = _torch_comm() if distributed else None
     rank, world, allgather = comm if comm else (0, 1, None)
     if dataset is None:
         dataset = Dataset(np.asarray(X), np.asarray(y), weights=weights)
     eng = NativeSearch(dataset, options, so, seed, rank, world)
-    if _loss_fn is not None:
+    if _native_scorer is not None:
+        eng.use_native_callbacks(_native_scorer.loss_addr, _native_scorer.grad_addr, _native_scorer.user)
+    elif _loss_fn is not None:
         eng.use_callbacks(_loss_fn, _grad_fn)
     else:
         from .device import get_lane_context

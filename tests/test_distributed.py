@@ -1,10 +1,12 @@
-"""CPU, world_size 2 (gloo): the multi-GPU combine of row-sharded partials.
+"""CPU, world_size 2 (gloo): the multi-GPU protocols of row sharding and tree sharding.
 
 `sr_amd.distributed.eval_loss_sharded` is run by two processes over two row shards with CPU
 stand-ins for the two GPU calls (per-shard packed partials — Σ loss + flag bits — from the oracle's
 predictions, and per-shard Julia-order folds of the checked arrays); the single packed all-reduce,
 the BIG-tree exact path (all-gather + `sr_jsum_finite`) and `sr_finalize_losses` (host C ABI) are
-the product code.  The result must equal the oracle on the unsharded data.
+the product code.  The result must equal the oracle on the unsharded data.  Tree sharding deals the
+trees over the ranks (`tree_owners`, the library's rule) and one all-reduce hands every rank every
+result.  A failure on one rank is all-reduced as an error word: every rank raises, none hangs.
 """
 import os
 import socket
@@ -34,7 +36,7 @@ def _data():
 EXPRS = ["cos(x2) + x3", "x2 * x3 - 1.5", "log(x2)", "x1 * 1e35", "x1 * 1e34", "cos(x1) * x2 / x3"]
 
 
-def _worker(rank, world, port, q):
+def _worker(rank, world, port, q, mode="rows"):
     sys.path[:0] = [os.path.join(ROOT, "symbolicregression.jl_amd"), os.path.join(ROOT, "oracle")]
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     import torch.distributed as dist
@@ -78,23 +80,39 @@ def _worker(rank, world, port, q):
                 out[i, 0] = [jl_sum(a, int(l), int(h)) for l, h in zip(lo_, hi_)]
             return out
 
-        loss, comp = eval_loss_sharded(tb, shard, opts, n, partials_fn=partials, exact_fn=exact)
+        if mode == "rows":
+            loss, comp = eval_loss_sharded(tb, shard, opts, n, partials_fn=partials, exact_fn=exact)
+        elif mode == "trees":
+            from sr_amd.distributed import eval_loss_tree_sharded
+
+            # replicated dataset; this rank scores only its share (the oracle stands in for the GPU)
+            def score(sub):
+                assert sub.n_trees < tb.n_trees
+                return orc.eval_loss_batch(sub, X, y)
+            loss, comp = eval_loss_tree_sharded(tb, Dataset(X, y), opts, score_fn=score)
+        else:  # "fail": rank 1's GPU call fails; both ranks must raise instead of waiting for each other
+            def failing(tb_):
+                if rank == 1:
+                    raise RuntimeError("injected failure")
+                return partials(tb_)
+            try:
+                eval_loss_sharded(tb, shard, opts, n, partials_fn=failing, exact_fn=exact)
+                q.put((rank, "no error", None))
+            except RuntimeError as e:
+                q.put((rank, str(e), None))
+            return
         q.put((rank, loss.tolist(), comp.tolist()))
     finally:
         dist.destroy_process_group()
 
 
-def test_sharded_combine_gloo_world2():
+def _run(mode):
     import torch.multiprocessing as mp
-
-    sys.path[:0] = [os.path.join(ROOT, "symbolicregression.jl_amd"), os.path.join(ROOT, "oracle")]
-    from oracle import Oracle
-    from sr_amd import Options, flatten_trees, parse_expression
 
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, 2, port, q)) for r in range(2)]
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, q, mode)) for r in range(2)]
     for p in procs:
         p.start()
     res = [q.get(timeout=240) for _ in range(2)]
@@ -102,6 +120,16 @@ def test_sharded_combine_gloo_world2():
         p.join(timeout=60)
         assert p.exitcode == 0
     res.sort()
+    return res
+
+
+@pytest.mark.parametrize("mode", ["rows", "trees"])
+def test_sharded_combine_gloo_world2(mode):
+    sys.path[:0] = [os.path.join(ROOT, "symbolicregression.jl_amd"), os.path.join(ROOT, "oracle")]
+    from oracle import Oracle
+    from sr_amd import Options, flatten_trees, parse_expression
+
+    res = _run(mode)
     assert res[0][1:] == res[1][1:]  # every rank finalizes the same answer
     loss, comp = np.array(res[0][1], dtype=np.float32), np.array(res[0][2])
 
@@ -116,3 +144,24 @@ def test_sharded_combine_gloo_world2():
             assert loss[k] == pytest.approx(float(ol[k]), rel=1e-6), EXPRS[k]
         else:
             assert np.isinf(loss[k])
+
+
+def test_failure_on_one_rank_fails_every_rank():
+    res = _run("fail")
+    assert res[0][1] == "the row-sharded step failed on a peer rank"
+    assert res[1][1] == "injected failure"
+
+
+def test_tree_owners_balanced():
+    sys.path[:0] = [os.path.join(ROOT, "symbolicregression.jl_amd")]
+    from sr_amd import Options, flatten_trees, gen_random_population
+    from sr_amd.distributed import tree_owners
+
+    opts = Options(binary_operators=["+", "-", "*", "/"], unary_operators=["cos", "exp", "log"])
+    tb = flatten_trees(gen_random_population(10_000, opts, 5, seed=1), np.float32)
+    sizes = np.diff(tb.offsets)
+    for world in (1, 2, 3, 8):
+        own = tree_owners(tb, world)
+        assert set(own.tolist()) == set(range(world))
+        load = np.array([sizes[own == r].sum() for r in range(world)])
+        assert load.max() - load.min() <= sizes.max(), (world, load)
