@@ -63,6 +63,8 @@ def parse_args(argv=None):
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-extra", action="store_true", help="skip the complete-only and Float64 lines")
     ap.add_argument("--search-iters", type=int, default=40, help="iterations of the C1 / C3 searches (0 = skip)")
+    ap.add_argument("--dry-run", action="store_true",
+                    help="launcher + CPU channel only (no device): rehearses --gpus N on a CPU host")
     ap.add_argument("--search-cpu-iters", type=int, default=0,
                     help="iterations of the CPU-port searches (0 = C1: all, C3: 2, a bounded sample)")
     return ap.parse_args(argv)
@@ -81,7 +83,7 @@ def spawn_ranks(n):
     procs = []
     for r in range(n):
         env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
-                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), SR_BENCH_SPAWNED="1")
         procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env))
     rc = 0
     alive = set(range(n))
@@ -207,6 +209,17 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+
+    if args.dry_run:
+        comm = Comm(world, rank)
+        dt, step_ms, _ = timed(lambda: time.sleep(0.001 * (1 + rank)), args.steps, args.warmup, comm.barrier)
+        dt = comm.max(dt)
+        if rank == 0:
+            print(json.dumps({"dry_run": True, "n_gpus": world, "steps": args.steps, "ms_per_step": dt / args.steps * 1e3,
+                              "ranks_launched_by": "bench.py" if os.environ.get("SR_BENCH_SPAWNED") else "launcher"}),
+                  flush=True)
+        comm.close()
+        return
 
     import sr_amd  # noqa: E402  (after the spawn decision: the parent never loads the HIP runtime)
     from sr_amd import Dataset, Options, flatten_trees, gen_random_batch, gen_random_population
@@ -510,6 +523,8 @@ def search_lines(args):
                 "iterations": args.search_iters, "wall_s": wall, "device_calls": res.device_calls,
                 "device_wall_s": res.device_s, "host_s": res.host_s,
                 "device_wall_per_call_us": res.device_s / max(res.device_calls, 1) * 1e6,
+                "kernel_busy_s": res.kernel_s,
+                "kernel_busy_per_call_us": res.kernel_s / max(res.device_calls, 1) * 1e6,
                 "best_loss": float(min(m.loss for m in res.pareto_frontier)), "config": desc}
         sc = SearchScorer(Oracle.from_options(o), X, y, n_threads=cpu_threads)
         t0 = time.perf_counter()

@@ -320,6 +320,7 @@ typedef struct sr_search_info {
   double host_ms;   /* selection, mutation and acceptance */
   double baseline_loss;
   int use_baseline;
+  double kernel_ms; /* device-busy time of the scoring calls' interpreter launches (loss calls) */
 } sr_search_info;
 
 /* CPU scorers for tests (the library's own device path when not set): sr_eval_loss_batch /

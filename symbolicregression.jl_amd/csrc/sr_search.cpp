@@ -164,6 +164,7 @@ struct Scorer {
   void* cb_user = nullptr;
   int64_t calls = 0;
   double ms = 0.0;  // wall time inside the calls
+  double kernel_ms = 0.0;  // device-busy time of the loss calls' interpreter launches
   bool ready() const { return ctx != nullptr || loss_cb != nullptr; }
   bool has_grad() const { return ctx != nullptr || grad_cb != nullptr; }
   // losses of `flat`'s trees (+Inf where incomplete)
@@ -181,6 +182,10 @@ struct Scorer {
     ms += ms_since(t0);
     ++calls;
     if (rc != SR_OK) return rc;
+    if (!loss_cb) {  // the interpreter launches' device-busy time of this call
+      double ph[9] = {0};
+      if (sr_last_phase_ms(ctx, ph, 9) == SR_OK) kernel_ms += ph[8];
+    }
     for (int64_t k = 0; k < nt; ++k)
       if (!comp[size_t(k)]) (*out)[size_t(k)] = T(INFINITY);
     return SR_OK;
@@ -1422,10 +1427,12 @@ int sr_search_get_info(sr_search* s, sr_search_info* out) {
     out->num_evals = e->total_num_evals();
     out->device_calls = e->sc.calls;
     out->device_ms = e->sc.ms;
+    out->kernel_ms = e->sc.kernel_ms;
     out->host_ms = e->host_ms;
     for (const auto& x : e->extra) {  // (summed over lanes: lanes run concurrently)
       out->device_calls += x->sc.calls;
       out->device_ms += x->sc.ms;
+      out->kernel_ms += x->sc.kernel_ms;
       out->host_ms += x->host_ms;
     }
     out->baseline_loss = double(e->baseline);

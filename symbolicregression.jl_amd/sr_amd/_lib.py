@@ -141,6 +141,7 @@ class SrSearchInfo(ctypes.Structure):
     _fields_ = [
         ("iterations", c_int64), ("s_r_cycles", c_int64), ("device_calls", c_int64), ("num_evals", c_double),
         ("device_ms", c_double), ("host_ms", c_double), ("baseline_loss", c_double), ("use_baseline", c_int),
+        ("kernel_ms", c_double),
     ]
 
 

@@ -106,6 +106,7 @@ class SearchResult:
     device_calls: int
     device_s: float = 0.0
     host_s: float = 0.0
+    kernel_s: float = 0.0  # device-busy time of the scoring launches (interpreter), inside device_s
 
 
 def make_callbacks(dtype, loss_fn, grad_fn=None):
@@ -383,7 +384,8 @@ def equation_search(X=None, y=None, *, niterations=10, options, weights=None, se
     exchange()  # the final migrations
     wall = time.perf_counter() - t0
     inf = eng.info()
-    info = dict(num_evals=inf.num_evals, calls=inf.device_calls, dev=inf.device_ms, host=inf.host_ms)
+    info = dict(num_evals=inf.num_evals, calls=inf.device_calls, dev=inf.device_ms, host=inf.host_ms,
+                kernel=inf.kernel_ms)
     if world > 1:
         parts = allgather(info)
         info = {k: sum(p[k] for p in parts) for k in info}
@@ -396,4 +398,5 @@ def equation_search(X=None, y=None, *, niterations=10, options, weights=None, se
         hof.exists[m.complexity - 1] = True
     pops = [eng.members(i) for i in range(options.populations)]
     return SearchResult(hof, hof.pareto_frontier(), pops, niterations, wall, niterations * options.populations,
-                        float(info["num_evals"]), int(info["calls"]), info["dev"] / 1e3, info["host"] / 1e3)
+                        float(info["num_evals"]), int(info["calls"]), info["dev"] / 1e3, info["host"] / 1e3,
+                        info["kernel"] / 1e3)
