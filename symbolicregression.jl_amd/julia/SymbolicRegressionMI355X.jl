@@ -24,8 +24,10 @@ Not exercised in this repository's CI (no Julia runtime in the build image); the
 module SymbolicRegressionMI355X
 
 using SymbolicRegression
-using SymbolicRegression: AbstractOptions, Dataset, LossFunctionsModule, PopulationModule
-using DynamicExpressions: AbstractExpressionNode, AbstractExpression, Expression, Node, get_tree, get_operators
+using SymbolicRegression: AbstractOptions, Dataset, LossFunctionsModule, PopulationModule, PopMemberModule,
+                          SingleIterationModule, ConstantOptimizationModule
+using DynamicExpressions: AbstractExpressionNode, AbstractExpression, Expression, Node, get_tree, get_operators,
+                          get_scalar_constants, set_scalar_constants!, simplify_tree!, combine_operators
 
 const LIB = get(ENV, "SR_AMD_LIB", joinpath(@__DIR__, "..", "lib", "libsr_amd.so"))
 
@@ -335,6 +337,109 @@ function LossFunctionsModule._eval_loss(tree::Union{AbstractExpression{T},Abstra
         loss += LossFunctionsModule.dimensional_regularization(tree, dataset, options)
     end
     return loss
+end
+
+# ---------------------------------------------------------------- batched constant optimisation
+"""Batched `optimize_constants` (src/ConstantOptimization.jl:29-116) of `members` on `dataset` (a full
+dataset or a SubDataset view): ONE `sr_optimize_constants_batch` call runs the reference's algorithm
+for every member in lock-step on the device (BFGS + BackTracking, Newton for one constant, from the
+constants and `optimizer_nrestarts` perturbed starts, the minimum adopted only if it beats the start;
+each line-search round one batched loss launch, each gradient one forward-mode launch).  Updates the
+improved members' constants, loss, cost and birth like `_optimize_constants_inner` and returns their
+`num_evals` (objective calls x dataset fraction, +1 per improved member), or `nothing` when the device
+cannot take these trees (the caller then keeps the reference's per-member path)."""
+function optimize_constants_batch!(dataset::Dataset{T,L}, members::AbstractVector, options::MI355XOptions
+                                   ) where {T,L}
+    isempty(members) && return Float64[]
+    trees = [m.tree for m in members]
+    all(device_tree, trees) || return nothing
+    ctx = context()
+    oid = opset_id(ctx, get_operators(first(trees), options))
+    lk = loss_kind(options)
+    (oid === nothing || lk === nothing) && return nothing
+    idx = SymbolicRegression.CoreModule.get_indices(dataset)
+    full = SymbolicRegression.CoreModule.get_full_dataset(dataset)
+    f = flatten(trees, T)
+    n = length(trees)
+    consts = Vector{T}(undef, max(1, count(==(0x01), f.constant)))
+    losses = Vector{T}(undef, n)
+    improved = Vector{UInt8}(undef, n)
+    f_calls = Vector{Int64}(undef, n)
+    rows = idx === nothing ? nothing : Int64.(idx .- 1)
+    dsh = device_dataset(ctx, full)
+    seed = rand(UInt64)   # the restart draws (x0 .* (1 + eps/2), eps ~ randn) come from this stream
+    GC.@preserve f rows consts losses improved f_calls begin
+        b = SrTreeBatch(n, pointer(f.offsets), pointer(f.degree), pointer(f.op), pointer(f.feature),
+                        pointer(f.constant), Ptr{Cvoid}(pointer(f.val)))
+        rc = ccall((:sr_optimize_constants_batch, LIB), Cint,
+                   (Ptr{Cvoid}, Ptr{Cvoid}, Cint, Ref{SrTreeBatch}, Ptr{Int64}, Int64, Cint, Cint, Cint, UInt64,
+                    Ptr{T}, Ptr{T}, Ptr{UInt8}, Ptr{Int64}),
+                   ctx.handle, dsh, oid, b, rows === nothing ? C_NULL : pointer(rows),
+                   rows === nothing ? 0 : length(rows), lk, options.optimizer_iterations,
+                   options.optimizer_nrestarts, seed, consts, losses, improved, f_calls)
+        rc == SR_ERR_UNSUPPORTED_OP && return nothing
+        check(rc)
+    end
+    base = options.base
+    frac = SymbolicRegression.CoreModule.dataset_fraction(dataset)
+    num_evals = zeros(Float64, n)
+    at = 0
+    for (k, m) in enumerate(members)
+        x0, refs = get_scalar_constants(m.tree)   # pre-order: the order the library returned them in
+        nk = length(x0)
+        num_evals[k] = f_calls[k] * frac
+        if improved[k] == 0x01
+            set_scalar_constants!(m.tree, consts[at+1:at+nk], refs)
+            m.loss = L(losses[k]) + LossFunctionsModule.dimensional_regularization(m.tree, dataset, base)
+            m.cost = LossFunctionsModule.loss_to_cost(m.loss, dataset.use_baseline, dataset.baseline_loss, m, base)
+            m.birth = SymbolicRegression.UtilsModule.get_birth_order(; deterministic=base.deterministic)
+            num_evals[k] += frac
+        end
+        at += nk
+    end
+    return num_evals
+end
+
+# `optimize_and_simplify_population` (src/SingleIteration.jl:68-139): simplification per member as the
+# reference, then the selected members' constants optimised in ONE batched device call instead of one
+# Optim run per member (:79-92), then `finalize_costs` and the new references.  With the recorder on
+# (or trees the device cannot take) the reference's own function runs.
+function SingleIterationModule.optimize_and_simplify_population(
+    dataset::D, pop::P, options::MI355XOptions, curmaxsize::Int, record::SymbolicRegression.RecordType
+)::Tuple{P,Float64} where {T,L,D<:Dataset{T,L},P<:PopulationModule.Population{T,L}}
+    base = options.base
+    base.use_recorder && return SingleIterationModule.optimize_and_simplify_population(dataset, pop, base,
+                                                                                       curmaxsize, record)
+    do_optimization = rand(pop.n) .< options.optimizer_probability
+    batched_dataset = options.batching ? SymbolicRegression.CoreModule.batch(dataset, options.batch_size) : dataset
+    if options.should_simplify
+        for m in pop.members
+            tree = simplify_tree!(m.tree, options.operators)
+            m.tree = combine_operators(tree, options.operators)
+        end
+    end
+    num_evals = 0.0
+    if options.should_optimize_constants
+        sel = [m for (m, d) in zip(pop.members, do_optimization) if d &&
+               ConstantOptimizationModule.count_constants_for_optimization(m.tree) > 0]
+        ev = optimize_constants_batch!(batched_dataset, sel, options)
+        if ev === nothing  # the reference's per-member optimiser
+            for m in sel
+                _, e = ConstantOptimizationModule.optimize_constants(batched_dataset, m, base)
+                num_evals += e
+            end
+        else
+            num_evals += sum(ev; init=0.0)
+        end
+    end
+    pop, tmp_num_evals = PopulationModule.finalize_costs(dataset, pop, options)
+    num_evals += tmp_num_evals
+    for m in pop.members
+        old_ref = m.ref
+        m.parent = old_ref
+        m.ref = PopMemberModule.generate_reference()
+    end
+    return (pop, num_evals)
 end
 
 # `finalize_costs` (src/Population.jl:182-196): one launch for the whole population.
