@@ -235,7 +235,9 @@ namespace {
 
 constexpr int64_t kRowAlign = 2048;  // a multiple of every kernel's row tile (64 lanes x R rows)
 constexpr int64_t kProbeRows = 2048;
-constexpr size_t kCodeCacheLds = 36 * 1024;  // dynamic LDS a register-stack workgroup may use with its program cache  // the dead-tree probe's rows: 4 tiles of the classic f32 build
+// dynamic LDS a register-stack workgroup may use with its program cache: with the 5 KiB of static
+// libm tables, 4 workgroups still fit a CU's 160 KiB
+constexpr size_t kCodeCacheLds = 34 * 1024;
 
 // Work decomposition: row tiles of 64*R rows (one LDS image each), `tiles` per block; trees grouped G
 // per block (the block's 4 waves share the G trees of a tile).

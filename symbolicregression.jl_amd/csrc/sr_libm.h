@@ -4,10 +4,11 @@
 // log kernels work in Float64).  ROCm's OCML Float32 log / cos / sin measured 1.75 / 1.26 / 1.49 ulp
 // on the fixture points of tests/golden/libm_ulp.json (profiles/r02_libm_ocml.txt), so those three
 // are computed here in double and rounded once, table-driven so the work per value stays close to
-// OCML's: log from a 64-cell table of an offset octave and a degree-6 log1p, cos / sin from (sin, cos)(k pi/16)
-// and degree-7/6 polynomials on |r| <= pi/32.  Every fast-path result is within 2^-38 relative of
-// the exact value before the final rounding (tools/gen_libm_coeffs.py prints the bounds), i.e.
-// correctly rounded unless the exact value sits that close to a midpoint.  OCML's Float32 exp
+// OCML's: log from a 64-cell table of an offset octave and a degree-6 log1p (within 2^-43 relative
+// before the final rounding: correctly rounded unless the exact value sits that close to a
+// midpoint), cos / sin from (sin, cos)(k pi/128) and degree-3/2 polynomials on |r| <= pi/256 (within
+// 2^-28 relative before the final rounding: <= 0.5223 ulp over every Float32 |x| < 2^20, checked
+// exhaustively by tools/libm_exhaustive.cpp; profiles/r03_libm_exhaustive.txt).  OCML's Float32 exp
 // measured 0.675 ulp and is kept on the device (sr_expf below, also correctly rounded but for
 // 2^-46-close midpoints, serves the host's constant folding).
 //
@@ -52,8 +53,8 @@ constexpr double kLn2Hi = 0x1.62e42fefa39efp-1, kLn2Lo = 0x1.abc9e3b39803fp-56;
 constexpr double kTwoOverPi = 0x1.45f306dc9c883p-1;
 constexpr double kPio2_1 = 0x1.921fb54442d18p+0, kPio2_2 = 0x1.1a62633145c07p-54, kPio2_3 = -0x1.f1976b7ed8fbcp-110;
 constexpr double kSqrtHalf = 0x1.6a09e667f3bcdp-1;
-constexpr double k64OverPi = 0x1.45f306dc9c883p+4;
-constexpr double kPi64_1 = 0x1.921fb54442d18p-5, kPi64_2 = 0x1.1a62633145c07p-59;
+constexpr double k128OverPi = 0x1.45f306dc9c883p+5;
+constexpr double kPi128_1 = 0x1.921fb54442d18p-6, kPi128_2 = 0x1.1a62633145c07p-60;
 // 2/pi in 32-bit words: bit 1 of word 0 is the 2^-1 bit (Payne-Hanek reduction of huge arguments)
 constexpr uint32_t kTwoOverPiBits[12] = {0xA2F9836Eu, 0x4E441529u, 0xFC2757D1u, 0xF534DDC0u, 0xDB629599u, 0x3C439041u,
                                          0xFE5163ABu, 0xDEBBC561u, 0xB7246E3Au, 0x424DD2E0u, 0x06492EEAu, 0x09D1921Cu};
@@ -202,27 +203,31 @@ SRL_HD inline double sr_rem_pio2f_fast(float x, int* q) {
   return y;
 }
 
-// |x| < 2^20: x = n pi/64 + r (Cody-Waite in double), |r| <= pi/128; with (s_k, c_k) =
-// (sin, cos)(k pi/64), k = n mod 128: sin x = s_k cos r + c_k sin r, cos x = c_k cos r - s_k sin r;
-// sin r and cos r by Taylor to r^5 / r^4 (relative errors < 2^-44 / 2^-41).
+// |x| < 2^20: x = n pi/128 + r (Cody-Waite in double), |r| <= pi/256; with (s_k, c_k) =
+// (sin, cos)(k pi/128), k = n mod 256: sin x = s_k cos r + c_k sin r, cos x = c_k cos r - s_k sin r,
+// with cos r = 1 - r^2/2 and sin r = r (1 - r^2/6).  The dropped Taylor terms (r^4/24 <= 2^-30 of c_k,
+// r^5/120 <= 2^-38) stay below 2^-28 of the result wherever it is (|result| >= |c_k| / 2 next to a
+// zero of the function, where c_k = 0 exactly and the result is -s_k sin r itself): <= 0.5 + 2^-4
+// ulp after the final rounding (tools/libm_exhaustive.cpp: every Float32 |x| < 2^20).  Six f64
+// operations after the reduction (eight with the degree-5/4 polynomials of a 128-entry table).
 template <bool COS>
 SRL_HD inline float sr_sincosf_tab(float x, const double* tab) {
   const double xd = double(x);
-  // n = x 64/pi rounded to an integer by the 1.5 * 2^52 shifter: k = n mod 128 is the shifter's
+  // n = x 128/pi rounded to an integer by the 1.5 * 2^52 shifter: k = n mod 256 is the shifter's
   // low bits (no conversions; a NaN x only yields a NaN result).  Two-part Cody-Waite with fused
-  // multiply-adds: |n| < 2^25, so the dropped third part (n * 2^-115 < 2^-90) is far below |r|'s ulp.
-  const double t = fma(xd, srl::k64OverPi, 0x1.8p52);
+  // multiply-adds: |n| < 2^26, so the dropped third part (n * 2^-114 < 2^-88) is far below |r|'s ulp.
+  const double t = fma(xd, srl::k128OverPi, 0x1.8p52);
   const double n = t - 0x1.8p52;
-  double r = fma(-n, srl::kPi64_1, xd);
-  r = fma(-n, srl::kPi64_2, r);
+  double r = fma(-n, srl::kPi128_1, xd);
+  r = fma(-n, srl::kPi128_2, r);
   uint64_t tb;
   __builtin_memcpy(&tb, &t, 8);
   // entry k = 16 bytes at byte offset 16 k
-  const double* e = reinterpret_cast<const double*>(reinterpret_cast<const char*>(tab) + ((uint32_t(tb) << 4) & 0x7f0u));
+  const double* e = reinterpret_cast<const double*>(reinterpret_cast<const char*>(tab) + ((uint32_t(tb) << 4) & 0xff0u));
   const double sk = e[0], ck = e[1];
   const double z = r * r;
-  const double sr = fma(z * r, fma(z, 0x1.1111111111111p-7, -0x1.5555555555555p-3), r);
-  const double cr = fma(z, fma(z, 0x1.5555555555555p-5, -0.5), 1.0);
+  const double sr = r * fma(z, -0x1.5555555555555p-3, 1.0);
+  const double cr = fma(z, -0.5, 1.0);
   return COS ? float(fma(ck, cr, -(sk * sr))) : float(fma(sk, cr, ck * sr));
 }
 
@@ -241,13 +246,13 @@ SRL_HD inline float sr_sincosf_full(float x, const double* tab) {
 
 // ---------------------------------------------------------------- tables: host / device
 #if defined(__HIPCC__)
-// per-workgroup LDS copy of the tables (trig then log; 3 KiB: it must not cost the interpreter a
+// per-workgroup LDS copy of the tables (trig then log; 5 KiB: it must not cost the interpreter a
 // workgroup per CU)
-static __shared__ __attribute__((aligned(16))) double sr_lds_libm[256 + 128];
+static __shared__ __attribute__((aligned(16))) double sr_lds_libm[512 + 128];
 // Copy the tables into LDS: every thread of the block calls this before the block's first barrier.
 __device__ inline void sr_libm_lds_fill(int tid, int nthreads) {
-  for (int i = tid; i < 256; i += nthreads) sr_lds_libm[i] = srl::kTrigTab[i];
-  for (int i = tid; i < 128; i += nthreads) sr_lds_libm[256 + i] = srl::kLogTab[i];
+  for (int i = tid; i < 512; i += nthreads) sr_lds_libm[i] = srl::kTrigTab[i];
+  for (int i = tid; i < 128; i += nthreads) sr_lds_libm[512 + i] = srl::kLogTab[i];
 }
 #endif
 SRL_HD inline const double* sr_trig_tab() {
@@ -259,7 +264,7 @@ SRL_HD inline const double* sr_trig_tab() {
 }
 SRL_HD inline const double* sr_log_tab() {
 #if defined(__HIP_DEVICE_COMPILE__)
-  return sr_lds_libm + 256;
+  return sr_lds_libm + 512;
 #else
   return srl::kLogTab;
 #endif

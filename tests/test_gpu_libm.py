@@ -99,10 +99,17 @@ def host_unary(dtype, fn, xs):
     return out
 
 
+# Float32 bars of the library's own functions (sr_libm.h): exp and log are correctly rounded but for
+# values within 2^-38 of a midpoint; cos / sin (128-entry (sin, cos)(k pi/128) table, degree-3/2
+# polynomials) are within 0.5223 ulp over EVERY Float32 |x| < 2^20 (tools/libm_exhaustive.cpp,
+# profiles/r03_libm_exhaustive.txt) and use the exact reduction above.
+F32_BAR = {"exp": 0.5 + 2 ** -16, "log": 0.5 + 2 ** -16, "cos": 0.5224, "sin": 0.5224}
+
+
 @pytest.mark.parametrize("fn", ["exp", "log", "cos", "sin"])
 def test_host_libm_f32_within_half_ulp_plus(ulp_fixture, fn):
     """CPU: the library's Float32 exp/log/cos/sin (sr_libm.h; the device runs the same code) are
-    within 0.5 + 2^-16 ulp of the exact value on every fixture point."""
+    within their bar (F32_BAR) of the exact value on every fixture point."""
     entries = ulp_fixture["float32"][fn]
     xs = np.array([e[0] for e in entries], dtype=np.float32)
     with np.errstate(all="ignore"):
@@ -112,13 +119,14 @@ def test_host_libm_f32_within_half_ulp_plus(ulp_fixture, fn):
     if fn == "exp":
         assert np.all(np.isinf(out[~fin]))
     err = ulp_errors(np.float32, out[fin], [e for e, f in zip(entries, fin) if f])
-    assert float(err.max()) <= 0.5 + 2 ** -16, (fn, float(err.max()))
+    assert float(err.max()) <= F32_BAR[fn], (fn, float(err.max()))
 
 
 @pytest.mark.parametrize("fn", ["exp", "log", "cos", "sin"])
 def test_host_libm_f32_random_vs_glibc(fn):
-    """CPU, 400k random Float32 points per function: equal to glibc's float64 result rounded to
-    Float32 except where that value sits within 2^-30 of a rounding midpoint (then <= 1 ulp apart)."""
+    """CPU, 400k random Float32 points per function: within F32_BAR of glibc's float64 result; exp
+    and log equal to it rounded to Float32 except where that value sits within 2^-30 of a rounding
+    midpoint (then <= 1 ulp apart)."""
     rng = np.random.default_rng(7)
     if fn == "exp":
         xs = rng.uniform(-103, 88.7, 400_000)
@@ -137,4 +145,9 @@ def test_host_libm_f32_random_vs_glibc(fn):
     # correctly rounded value when the exact value is that close to a midpoint
     mid = np.abs(np.abs(ref64 - ref) - ulp / 2) <= np.abs(ref64) * 2.0 ** -30
     assert np.all(np.abs(out - ref)[diff] <= ulp[diff]), fn
-    assert np.all(mid[diff]), (fn, int(diff.sum()), xs[diff & ~mid][:5])
+    # error in ulps of the result's binade (the smaller spacing at a power of two)
+    u = np.minimum(ulp, np.spacing(np.nextafter(np.abs(ref).astype(np.float32), np.float32(0))).astype(np.float64))
+    fin = np.isfinite(ref64) & (u > 0)
+    assert float(np.max(np.abs(out - ref64)[fin] / u[fin])) <= F32_BAR[fn] + 2 ** -20, fn
+    if fn in ("exp", "log"):
+        assert np.all(mid[diff]), (fn, int(diff.sum()), xs[diff & ~mid][:5])
