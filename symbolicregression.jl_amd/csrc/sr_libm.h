@@ -4,9 +4,8 @@
 // log kernels work in Float64).  ROCm's OCML Float32 log / cos / sin measured 1.75 / 1.26 / 1.49 ulp
 // on the fixture points of tests/golden/libm_ulp.json (profiles/r02_libm_ocml.txt), so those three
 // are computed here in double and rounded once, table-driven so the work per value stays close to
-// OCML's: log from a 64-cell table of an offset octave and a degree-6 log1p (within 2^-43 relative
-// before the final rounding: correctly rounded unless the exact value sits that close to a
-// midpoint), cos / sin from (sin, cos)(k pi/128) and degree-3/2 polynomials on |r| <= pi/256 (within
+// OCML's: log from a 64-cell table of an offset octave and a degree-4 log1p (within 2^-30 relative
+// before the final rounding: <= 0.5101 ulp), cos / sin from (sin, cos)(k pi/128) and degree-3/2 polynomials on |r| <= pi/256 (within
 // 2^-28 relative before the final rounding: <= 0.5223 ulp over every Float32 |x| < 2^20, checked
 // exhaustively by tools/libm_exhaustive.cpp; profiles/r03_libm_exhaustive.txt).  OCML's Float32 exp
 // measured 0.675 ulp and is kept on the device (sr_expf below, also correctly rounded but for
@@ -88,15 +87,16 @@ SRL_HD inline float sr_expf(float x) {
 // log(x) = k ln2 + logc_i + log1p(z invc_i - 1) for x = 2^k z with z's Float32 bits in
 // [0x3f330000, 0x3fb30000) (z ~ [0.699, 1.398): an offset octave, so x just below 1 keeps k = 0 with
 // no branch), cell i = the 6 bits below the offset (64 cells, |z invc_i - 1| <= 2^-7), log1p by
-// Taylor to r^6 (error <= 2^-51.8 absolute, <= 2^-43.8 relative to the result).  Every step but the
-// last rounding is exact or double: the result is within 2^-43 relative before rounding to Float32.
+// Taylor to r^4 (error <= 2^-37.3 absolute, <= 2^-30 relative to the result).  Every other step is
+// exact or double: <= 0.5101 ulp after the final rounding (every positive normal Float32 checked,
+// tools/libm_exhaustive.cpp).
 // The f64 polynomial coefficients come in `c` (the device row function materialises them once per
 // call in scalar registers: 64-bit constants cannot be VOP3 literals, and rematerialising them costs
 // two v_mov per use and row).
 struct SrLogC {
-  double c3, c4, c5, c6, ln2;
+  double c3, c4, ln2;
 };
-constexpr SrLogC kSrLogC = {0x1.5555555555555p-2, -0.25, 0.2, -0x1.5555555555555p-3, 0x1.62e42fefa39efp-1};
+constexpr SrLogC kSrLogC = {0x1.5555555555555p-2, -0.25, 0x1.62e42fefa39efp-1};
 constexpr uint32_t kLogOff = 0x3f330000u;
 
 // positive normal finite x (Float32 bits ix), scaled by 2^-kadj
@@ -110,10 +110,10 @@ SRL_HD inline double sr_log_normal(uint32_t ix, int kadj, const double* tab, con
   const double invc = tab[2 * i], logc = tab[2 * i + 1];
   const double r = fma(double(z), invc, -1.0);
   const double r2 = r * r;
-  // log1p(r) = r + r^2 ((-1/2 + r/3) + r^2 ((-1/4 + r/5) - r^2/6))
+  // log1p(r) = r + r^2 ((-1/2 + r/3) - r^2/4): the dropped r^5/5 is <= 2^-37.3 absolute, <= 2^-30 of the
+  // result (|log x| >= 2^-7.4 outside the cell of 1; |r| inside it)
   const double a = fma(r, c.c3, -0.5);
-  const double b = fma(r2, c.c6, fma(r, c.c5, c.c4));
-  const double p = fma(r2, b, a);
+  const double p = fma(r2, c.c4, a);
   const double y = fma(double(k + kadj), c.ln2, logc) + r;
   return fma(r2, p, y);
 }
@@ -145,8 +145,7 @@ __device__ inline double srl_sconst() {
 }
 #define SRL_SCONST(v) srl_sconst<__builtin_bit_cast(uint64_t, double(v))>()
 __device__ inline SrLogC sr_logc_sgpr() {
-  return SrLogC{SRL_SCONST(kSrLogC.c3), SRL_SCONST(kSrLogC.c4), SRL_SCONST(kSrLogC.c5), SRL_SCONST(kSrLogC.c6),
-                SRL_SCONST(kSrLogC.ln2)};
+  return SrLogC{SRL_SCONST(kSrLogC.c3), SRL_SCONST(kSrLogC.c4), SRL_SCONST(kSrLogC.ln2)};
 }
 #elif defined(__HIPCC__)
 // (host pass of device code: never executed)

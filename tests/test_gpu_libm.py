@@ -99,11 +99,11 @@ def host_unary(dtype, fn, xs):
     return out
 
 
-# Float32 bars of the library's own functions (sr_libm.h): exp and log are correctly rounded but for
-# values within 2^-38 of a midpoint; cos / sin (128-entry (sin, cos)(k pi/128) table, degree-3/2
-# polynomials) are within 0.5223 ulp over EVERY Float32 |x| < 2^20 (tools/libm_exhaustive.cpp,
-# profiles/r03_libm_exhaustive.txt) and use the exact reduction above.
-F32_BAR = {"exp": 0.5 + 2 ** -16, "log": 0.5 + 2 ** -16, "cos": 0.5224, "sin": 0.5224}
+# Float32 bars of the library's own functions (sr_libm.h): exp is correctly rounded but for values
+# within 2^-38 of a midpoint; cos / sin (256-entry (sin, cos)(k pi/128) table, degree-3/2 polynomials)
+# are within 0.5223 ulp over EVERY Float32 |x| < 2^20 and log (degree-4 log1p) within 0.5101 over every
+# positive normal Float32 (tools/libm_exhaustive.cpp, profiles/r03_libm_exhaustive.txt).
+F32_BAR = {"exp": 0.5 + 2 ** -16, "log": 0.5101, "cos": 0.5224, "sin": 0.5224}
 
 
 @pytest.mark.parametrize("fn", ["exp", "log", "cos", "sin"])
@@ -125,8 +125,8 @@ def test_host_libm_f32_within_half_ulp_plus(ulp_fixture, fn):
 @pytest.mark.parametrize("fn", ["exp", "log", "cos", "sin"])
 def test_host_libm_f32_random_vs_glibc(fn):
     """CPU, 400k random Float32 points per function: within F32_BAR of glibc's float64 result; exp
-    and log equal to it rounded to Float32 except where that value sits within 2^-30 of a rounding
-    midpoint (then <= 1 ulp apart)."""
+    equal to it rounded to Float32 except where that value sits within 2^-30 of a rounding midpoint
+    (then <= 1 ulp apart)."""
     rng = np.random.default_rng(7)
     if fn == "exp":
         xs = rng.uniform(-103, 88.7, 400_000)
@@ -149,5 +149,5 @@ def test_host_libm_f32_random_vs_glibc(fn):
     u = np.minimum(ulp, np.spacing(np.nextafter(np.abs(ref).astype(np.float32), np.float32(0))).astype(np.float64))
     fin = np.isfinite(ref64) & (u > 0)
     assert float(np.max(np.abs(out - ref64)[fin] / u[fin])) <= F32_BAR[fn] + 2 ** -20, fn
-    if fn in ("exp", "log"):
+    if fn == "exp":
         assert np.all(mid[diff]), (fn, int(diff.sum()), xs[diff & ~mid][:5])
