@@ -518,13 +518,20 @@ def search_lines(args):
         t0 = time.perf_counter()
         res = equation_search(X, y, niterations=args.search_iters, options=o, seed=0)
         wall = time.perf_counter() - t0
+        # per-call breakdown from a short second run with the kernel timing on (reading the events
+        # costs every call their queries, so the timed run above goes without)
+        os.environ["SR_AMD_SEARCH_KERNEL_TIMES"] = "1"
+        diag = equation_search(X, y, niterations=min(5, args.search_iters), options=o, seed=0)
+        del os.environ["SR_AMD_SEARCH_KERNEL_TIMES"]
         line = {"metric": "search iterations/sec", "value": res.s_r_cycles / wall, "unit": "s_r_cycles/s",
                 "iterations_per_s": args.search_iters / wall, "islands": o.populations,
                 "iterations": args.search_iters, "wall_s": wall, "device_calls": res.device_calls,
                 "device_wall_s": res.device_s, "host_s": res.host_s,
                 "device_wall_per_call_us": res.device_s / max(res.device_calls, 1) * 1e6,
-                "kernel_busy_s": res.kernel_s,
-                "kernel_busy_per_call_us": res.kernel_s / max(res.device_calls, 1) * 1e6,
+                "kernel_busy_per_call_us": diag.kernel_s / max(diag.device_calls, 1) * 1e6,
+                "per_call_note": ("device_wall = wall time inside the scoring calls (two scoring lanes overlap); "
+                                  "kernel_busy = the interpreter launches' device-busy time (a 5-iteration run "
+                                  "with SR_AMD_SEARCH_KERNEL_TIMES=1)"),
                 "best_loss": float(min(m.loss for m in res.pareto_frontier)), "config": desc}
         sc = SearchScorer(Oracle.from_options(o), X, y, n_threads=cpu_threads)
         t0 = time.perf_counter()

@@ -180,6 +180,9 @@ struct sr_ctx {
   DevBuf shard_buf;       // collectives of the sharded calls (shard layout, exact-pass folds, tree results)      // SR_AMD_FIRST_CHUNK: the two-chunk pipeline's first chunk is 1/first_chunk       // SR_AMD_CODE_CACHE: LDS program cache of the register-stack launches     // SR_AMD_STRESS_PROBE: the probe runs the dataset's stress rows (below)
   double last_eval_ms = 0.0, last_total_ms = 0.0;
   double last_busy_ms = 0.0;  // union of the last call's interpreter launch intervals (sr_last_phase_ms out[8])
+  // the two above are read from the last call's events lazily, when asked for (sr_last_kernel_ms /
+  // sr_last_phase_ms): a small call (the search's) does not pay the event queries it never reads
+  bool timing_pending = false;
   // host-side phases of the last eval_loss call (ms): compile, upload+launch, wait, exact pass,
   // finalize (sr_last_phase_ms)
   double phase_ms[5] = {0, 0, 0, 0, 0};
@@ -1143,8 +1146,7 @@ int eval_loss_impl(sr_ctx* ctx, const sr_dataset* ds, int opset_id, const sr_tre
   const uint32_t* hf = reinterpret_cast<const uint32_t*>(ctx->h_outs.as<char>() + ctx->outs_flag_off);
   std::vector<double> sums(hs, hs + nt);
   std::vector<uint32_t> flags(hf, hf + nt);
-  ctx->last_eval_ms = chunk_kernel_ms(ctx);
-  ctx->last_busy_ms = chunk_busy_ms(ctx);
+  ctx->timing_pending = true;
   ctx->mark_phase(2);
   std::vector<int64_t> list;
   for (int64_t t = 0; t < nt; ++t)
@@ -1618,8 +1620,8 @@ int eval_sharded_impl(sr_ctx* ctx, const sr_dataset* ds, int opset_id, const sr_
     SR_HIP_CHECK(hipMemcpyAsync(out_complete, d_comp, size_t(nt), hipMemcpyDeviceToHost, s));
   }
   SR_HIP_CHECK(hipStreamSynchronize(s));
-  ctx->last_eval_ms = local == SR_OK && nt > 0 ? chunk_kernel_ms(ctx) : 0.0;
-  ctx->last_busy_ms = local == SR_OK && nt > 0 ? chunk_busy_ms(ctx) : 0.0;
+  ctx->timing_pending = local == SR_OK && nt > 0;
+  if (!ctx->timing_pending) ctx->last_eval_ms = ctx->last_busy_ms = 0.0;
   ctx->mark_phase(2);
   if (err_sum != 0.0) return local != SR_OK ? local : set_error(SR_ERR_HIP, "the row-sharded step failed on a peer rank");
   std::vector<int64_t> list;
@@ -1931,8 +1933,7 @@ int sr_eval_loss_partials(sr_ctx* ctx, const sr_dataset* ds, int opset_id, const
   SR_HIP_CHECK(hipMemcpyAsync(out_sum, ctx->d_out_sum, size_t(nt) * sizeof(double), kind, s));
   SR_HIP_CHECK(hipMemcpyAsync(out_flags, ctx->d_out_flag, size_t(nt) * sizeof(uint32_t), kind, s));
   SR_HIP_CHECK(hipStreamSynchronize(s));
-  ctx->last_eval_ms = chunk_kernel_ms(ctx);
-  ctx->last_busy_ms = chunk_busy_ms(ctx);
+  ctx->timing_pending = true;
   ctx->last_total_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
   return SR_OK;
 }
@@ -1966,8 +1967,7 @@ int sr_eval_loss_partials_packed(sr_ctx* ctx, const sr_dataset* ds, int opset_id
   SR_HIP_CHECK(sr_launch_pack_partials(ctx->d_out_sum, ctx->d_out_flag, int(nt), dst, s));
   if (!out_on_device) SR_HIP_CHECK(hipMemcpyAsync(out, dst, bytes, hipMemcpyDeviceToHost, s));
   SR_HIP_CHECK(hipStreamSynchronize(s));
-  ctx->last_eval_ms = chunk_kernel_ms(ctx);
-  ctx->last_busy_ms = chunk_busy_ms(ctx);
+  ctx->timing_pending = true;
   ctx->last_total_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
   return SR_OK;
 }
@@ -2057,8 +2057,7 @@ int sr_eval_loss_partials_allreduce(sr_ctx* ctx, const sr_dataset* ds, int opset
   if (nt > 0) SR_HIP_CHECK(hipMemcpyAsync(out_host, dst, n * sizeof(double), hipMemcpyDeviceToHost, s));
   SR_HIP_CHECK(hipStreamSynchronize(s));
   if (err_sum != 0.0) return local != SR_OK ? local : set_error(SR_ERR_HIP, "the row-sharded step failed on a peer rank");
-  ctx->last_eval_ms = chunk_kernel_ms(ctx);
-  ctx->last_busy_ms = chunk_busy_ms(ctx);
+  ctx->timing_pending = true;
   ctx->last_total_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
   return SR_OK;
 }
@@ -2293,8 +2292,17 @@ int sr_host_unary(int dtype, const char* name, int64_t n, const void* x, void* o
   return SR_OK;
 }
 
+// the last call's kernel / busy times from its events (computed on first request)
+static void settle_timing(sr_ctx* ctx) {
+  if (!ctx->timing_pending) return;
+  ctx->timing_pending = false;
+  ctx->last_eval_ms = chunk_kernel_ms(ctx);
+  ctx->last_busy_ms = chunk_busy_ms(ctx);
+}
+
 int sr_last_phase_ms(sr_ctx* ctx, double* out, int n) {
   if (check_ctx(ctx) != SR_OK) return SR_ERR_INVALID_ARG;
+  if (n > 8) settle_timing(ctx);
   for (int i = 0; i < n && i < 5; ++i) out[i] = ctx->phase_ms[i];
   if (n > 5) out[5] = double(ctx->n_chunks_last);
   if (n > 6) out[6] = ctx->exact_kernel_ms;
@@ -2335,6 +2343,7 @@ int sr_tuning_info(sr_ctx* ctx, int* used_derived_columns, int64_t* exact_trees)
 
 int sr_last_kernel_ms(sr_ctx* ctx, double* eval_ms, double* total_ms) {
   if (check_ctx(ctx) != SR_OK) return SR_ERR_INVALID_ARG;
+  settle_timing(ctx);
   if (eval_ms) *eval_ms = ctx->last_eval_ms;
   if (total_ms) *total_ms = ctx->last_total_ms;
   return SR_OK;

@@ -30,6 +30,7 @@
 #include <string.h>
 
 #include <algorithm>
+#include <cstdlib>
 #include <chrono>
 #include <memory>
 #include <string>
@@ -165,6 +166,11 @@ struct Scorer {
   int64_t calls = 0;
   double ms = 0.0;  // wall time inside the calls
   double kernel_ms = 0.0;  // device-busy time of the loss calls' interpreter launches
+  // (SR_AMD_SEARCH_KERNEL_TIMES=1: reading it costs every call its event queries, so off by default)
+  bool time_kernels = [] {
+    const char* v = std::getenv("SR_AMD_SEARCH_KERNEL_TIMES");
+    return v && std::atoi(v) != 0;
+  }();
   bool ready() const { return ctx != nullptr || loss_cb != nullptr; }
   bool has_grad() const { return ctx != nullptr || grad_cb != nullptr; }
   // losses of `flat`'s trees (+Inf where incomplete)
@@ -182,7 +188,7 @@ struct Scorer {
     ms += ms_since(t0);
     ++calls;
     if (rc != SR_OK) return rc;
-    if (!loss_cb) {  // the interpreter launches' device-busy time of this call
+    if (!loss_cb && time_kernels) {  // the interpreter launches' device-busy time of this call
       double ph[9] = {0};
       if (sr_last_phase_ms(ctx, ph, 9) == SR_OK) kernel_ms += ph[8];
     }

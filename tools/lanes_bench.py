@@ -6,6 +6,8 @@ import sys
 import time
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+if os.environ.get("LANES_KERNEL_TIMES") == "1":
+    os.environ["SR_AMD_SEARCH_KERNEL_TIMES"] = "1"
 sys.path[:0] = [os.path.join(ROOT, "symbolicregression.jl_amd")]
 import numpy as np  # noqa: E402
 
