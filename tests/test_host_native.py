@@ -1,0 +1,70 @@
+"""CPU: host-side native pieces that need no device — the library's random-population generator
+(`sr_gen_random_population`, C4's 100k trees) and the batched constant optimiser driven by CPU
+scorers (`sr_optimize_constants_callbacks`: the same BFGS / Newton code the device path runs,
+src/ConstantOptimization.jl:29-116), scored by the oracle."""
+import numpy as np
+import pytest
+
+from oracle import Oracle, loss_grad_forward
+from sr_amd import Options, flatten_trees, gen_random_batch, gen_random_population, parse_expression, string_tree
+from sr_amd.constant_optimization import optimize_constants_callbacks
+
+OPS = dict(binary_operators=["+", "-", "*", "/"], unary_operators=["cos", "exp", "log"])
+
+
+def test_native_population_matches_generator_distribution():
+    """gen_random_tree_fixed_size (src/MutationFunctions.jl:441-471) with node_count ~ U{1..30}: the
+    native generator's population has the Python generator's statistics (mean size, unary : binary
+    ratio = nuna : nbin = 3 : 4, leaves half constants), is seeded, and every tree parses back."""
+    opts = Options(**OPS)
+    a = gen_random_batch(20_000, opts, 5, seed=4)
+    b = gen_random_batch(20_000, opts, 5, seed=4)
+    assert np.array_equal(a.offsets, b.offsets) and np.array_equal(a.val, b.val)
+    ref = flatten_trees(gen_random_population(5_000, opts, 5, seed=9), np.float32)
+    for tb in (a, ref):
+        sizes = np.diff(tb.offsets)
+        assert 14.5 < sizes.mean() < 16.5
+        assert sizes.min() >= 1 and sizes.max() <= 30
+        un, bi = np.sum(tb.degree == 1), np.sum(tb.degree == 2)
+        assert 0.6 < un / bi < 0.9
+        leaves = tb.degree == 0
+        assert 0.45 < tb.constant[leaves].mean() < 0.55
+        assert np.all((tb.feature[leaves & (tb.constant == 0)] >= 1) & (tb.feature[leaves & (tb.constant == 0)] <= 5))
+    for k in range(50):
+        assert string_tree(a.tree(k), opts.operators)
+
+
+def _scorers(opts, X, y):
+    orc = Oracle.from_options(opts)
+
+    def lossf(b, rows):
+        l, c = orc.eval_loss_batch(b, X, y, accum="f64", n_threads=4)
+        return np.where(c, l, np.inf)
+
+    def gradf(b, rows):
+        g, l, c = loss_grad_forward(orc, b, X, y)
+        return np.where(c, l, np.inf), g
+    return lossf, gradf
+
+
+def test_callback_optimiser_reaches_known_optima():
+    """BFGS (several constants) and Newton (one constant) from perturbed starts approach the exact
+    optimum; the start loss is never made worse; the restarts are seeded (same seed, same result)."""
+    rng = np.random.default_rng(3)
+    X = rng.uniform(0.5, 2.0, (3, 500))
+    opts = Options(**OPS)
+    cases = [(2.5 * X[0] * X[1] / (X[2] + 0.75), "1.9 * x1 * x2 / (x3 + 0.5)", [2.5, 0.75], 1e-5),     # BFGS
+             (2.5 * X[0] * X[1] / (X[2] + 0.75), "x1 * x2 / (x3 * 0.5 + 0.2)", [0.4, 0.3], 1e-12),    # BFGS
+             (2.5 * X[0] * X[1] / X[2], "1.3 * x1 * x2 / x3", [2.5], 1e-12)]                           # Newton
+    for y, expr, want, bar in cases:
+        lossf, gradf = _scorers(opts, X, y)
+        tb = flatten_trees([parse_expression(expr, opts), parse_expression("cos(x1) + 0.3", opts)], np.float64)
+        start = lossf(tb, None)
+        out, loss, improved, f_calls = optimize_constants_callbacks(tb, lossf, gradf, seed=11)
+        assert np.all(loss <= start) and improved[0] and f_calls[0] > 0, expr
+        # 8 iterations (the reference's default optimizer_iterations)
+        assert loss[0] < bar * start[0], (expr, loss[0], start[0])
+        c0 = out.val[out.offsets[0]:out.offsets[1]][out.constant_mask()[out.offsets[0]:out.offsets[1]]]
+        np.testing.assert_allclose(c0, want, rtol=1e-3)
+        again = optimize_constants_callbacks(tb, lossf, gradf, seed=11)
+        assert np.array_equal(again[1], loss) and np.array_equal(again[0].val, out.val)
