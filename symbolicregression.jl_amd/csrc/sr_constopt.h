@@ -21,6 +21,9 @@
 // Batched objective over (item, x) pairs: f -> losses, fg -> losses + gradients.  Items index the
 // batch being optimised; calls return an SR_* status.
 struct SrObjective {
+  // false around evaluations the reference's Optim does not count in f_calls (Newton's curvature
+  // probes: there the Hessian comes from its own differencing, not from objective calls)
+  bool counting = true;
   virtual ~SrObjective() = default;
   virtual int f(const std::vector<int>& items, const std::vector<std::vector<double>>& xs, std::vector<double>* out) = 0;
   virtual int fg(const std::vector<int>& items, const std::vector<std::vector<double>>& xs, std::vector<double>* out,
@@ -163,8 +166,11 @@ inline int minimize(SrObjective& obj, const std::vector<int>& items, std::vector
       }
       std::vector<double> fp, fm;
       std::vector<std::vector<double>> gp, gm;
-      if ((rc = obj.fg(sub, xp, &fp, &gp))) return rc;
-      if ((rc = obj.fg(sub, xm, &fm, &gm))) return rc;
+      obj.counting = false;  // (num_evals follows Optim's f_calls: the curvature probes are not in it)
+      rc = obj.fg(sub, xp, &fp, &gp);
+      if (!rc) rc = obj.fg(sub, xm, &fm, &gm);
+      obj.counting = true;
+      if (rc) return rc;
       for (size_t j = 0; j < act.size(); ++j) {
         const size_t k = size_t(act[j]);
         double H = (gp[j][0] - gm[j][0]) / (2.0 * h[j]);

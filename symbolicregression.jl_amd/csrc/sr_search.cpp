@@ -228,7 +228,7 @@ struct TreeObjective : SrObjective {
     flat->clear();
     for (size_t j = 0; j < items.size(); ++j) {
       flat->add(*(*trees)[size_t(items[j])], &xs[j]);
-      ++f_calls[size_t(items[j])];
+      if (counting) ++f_calls[size_t(items[j])];
     }
     std::vector<T> loss;
     const int rc = sc->loss(*flat, *rows, &loss);
@@ -243,7 +243,7 @@ struct TreeObjective : SrObjective {
     size_t nc = 0;
     for (size_t j = 0; j < items.size(); ++j) {
       flat->add(*(*trees)[size_t(items[j])], &xs[j]);
-      ++f_calls[size_t(items[j])];
+      if (counting) ++f_calls[size_t(items[j])];
       nc += xs[j].size();
     }
     std::vector<T> loss, g;
