@@ -183,6 +183,8 @@ struct sr_ctx {
   // the two above are read from the last call's events lazily, when asked for (sr_last_kernel_ms /
   // sr_last_phase_ms): a small call (the search's) does not pay the event queries it never reads
   bool timing_pending = false;
+  int timing = 1;           // 0: no timing events at all (sr_set_tuning "timing"; the search engine's calls)
+  bool timed_last = false;  // the last run_batch recorded its events
   // host-side phases of the last eval_loss call (ms): compile, upload+launch, wait, exact pass,
   // finalize (sr_last_phase_ms)
   double phase_ms[5] = {0, 0, 0, 0, 0};
@@ -334,6 +336,7 @@ int decode_loss(sr_ctx* ctx, int code, int* kind, double* param) {
 // most used first, at most SR_MAX_DERIVED.  dmap: [SR_U_COUNT][nf] -> column or -1.
 constexpr int64_t kDerivedMinRows = 16384;  // below this the per-call column pass does not pay
 constexpr int kDerivedMinUses = 4;
+constexpr double kDerivedMinWork = 33554432.0;  // trees x rows (2^25) below which the column pass does not pay
 constexpr int64_t kDerivedSample = 1024;    // trees scanned
 void choose_derived(const sr_tree_batch& trees, const SrOpset& ops, int64_t nf, SrDerivedSpec* spec,
                     std::vector<int16_t>* dmap) {
@@ -513,7 +516,8 @@ int run_batch(sr_ctx* ctx, const sr_dataset* ds, int opset_id, const sr_tree_bat
   ctx->n_chunks_last = 0;
   ctx->derived_last = false;
   ctx->n_derived_last = 0;
-  SR_HIP_CHECK(hipEventRecord(ctx->ev_start, s));
+  ctx->timed_last = ctx->timing != 0;
+  if (ctx->timed_last) SR_HIP_CHECK(hipEventRecord(ctx->ev_start, s));
   if (gather)
     SR_HIP_CHECK(hipMemcpyAsync(ctx->row_idx.p, row_idx, size_t(n_idx) * sizeof(int64_t), hipMemcpyHostToDevice, s));
   // derived columns (LOAD_DERIVED): for the BASIC-tier deferred-check loss kernels over many rows,
@@ -526,15 +530,18 @@ int run_batch(sr_ctx* ctx, const sr_dataset* ds, int opset_id, const sr_tree_bat
   // every shard, so all ranks compile the same programs and number their checked arrays alike)
   const double max_abs_x = shard ? shard->max_abs_x : ds->max_abs_x;
   const int64_t derived_rows = shard ? shard->min_rows : n_eval;
+  // (and only for calls with enough work: the column pass is one more launch, which a search's small
+  // calls — tens of trees x 1e5 rows — would pay in latency for nothing)
   if (allow_derived && ctx->derived && mode == SR_MODE_LOSS && tier == SR_TIER_BASIC && derived_rows >= kDerivedMinRows &&
-      nt >= 64 && max_abs_x < double(T(t_max<T>() / (2.0 * double(n_total > 0 ? n_total : 1))))) {  // (track_x off)
+      nt >= 64 && double(nt) * double(derived_rows) >= kDerivedMinWork &&
+      max_abs_x < double(T(t_max<T>() / (2.0 * double(n_total > 0 ? n_total : 1))))) {  // (track_x off)
     choose_derived(*trees, ctx->opsets[opset_id], ds->nf, &spec, &dmap);
     if (spec.n > 0) {
       SR_HIP_CHECK(ctx->derived_cols.ensure(size_t(spec.n) * size_t(dld) * sizeof(T)));
-      SR_HIP_CHECK(hipEventRecord(ctx->ev_d0, s));
+      if (ctx->timed_last) SR_HIP_CHECK(hipEventRecord(ctx->ev_d0, s));
       SR_HIP_CHECK(sr_launch_derived<T>(static_cast<const T*>(ds->X), ds->ld, gather ? ctx->row_idx.as<int64_t>() : nullptr,
                                         n_eval, dld, spec, ctx->derived_cols.as<T>(), dld, s));
-      SR_HIP_CHECK(hipEventRecord(ctx->ev_d1, s));
+      if (ctx->timed_last) SR_HIP_CHECK(hipEventRecord(ctx->ev_d1, s));
       ctx->derived_last = true;
       ctx->n_derived_last = spec.n;
     } else {
@@ -654,7 +661,7 @@ int run_batch(sr_ctx* ctx, const sr_dataset* ds, int opset_id, const sr_tree_bat
     prog->total_nodes += pc.total_nodes;
     prog->total_ops += pc.total_ops;
 
-    SR_HIP_CHECK(hipEventRecord(ctx->ev_c0[c], cs));  // the chunk's kernel time includes its probe
+    if (ctx->timed_last) SR_HIP_CHECK(hipEventRecord(ctx->ev_c0[c], cs));  // the chunk's kernel time includes its probe
     // one launch over launch positions [p0, p0 + np) of the chunk; its partials occupy
     // [n_rb][np] words from p0 * n_rb (the chunk's region holds n_rb rows for every position)
     auto launch = [&](int64_t p0, int64_t np, bool vstk) -> int {
@@ -762,7 +769,7 @@ int run_batch(sr_ctx* ctx, const sr_dataset* ds, int opset_id, const sr_tree_bat
       sync_both();
       return lrc;
     }
-    SR_HIP_CHECK(hipEventRecord(ctx->ev_c1[c], cs));
+    if (ctx->timed_last) SR_HIP_CHECK(hipEventRecord(ctx->ev_c1[c], cs));
     ctx->n_chunks_last = c + 1;
     code_base += uint32_t(ncode);
   }
@@ -780,6 +787,7 @@ int run_batch(sr_ctx* ctx, const sr_dataset* ds, int opset_id, const sr_tree_bat
 // them; chunks on the two streams may overlap, so this can exceed the wall time they span).
 inline double chunk_kernel_ms(sr_ctx* ctx) {
   double ms = 0.0;
+  if (!ctx->timed_last) return 0.0;
   for (int c = 0; c < ctx->n_chunks_last; ++c) {
     float m = 0.f;
     if (hipEventElapsedTime(&m, ctx->ev_c0[c], ctx->ev_c1[c]) == hipSuccess) ms += double(m);
@@ -795,6 +803,7 @@ inline double chunk_kernel_ms(sr_ctx* ctx) {
 // streams overlap, so the sum above can exceed the wall time they span; this cannot).
 inline double chunk_busy_ms(sr_ctx* ctx) {
   std::vector<std::pair<double, double>> iv;
+  if (!ctx->timed_last) return 0.0;
   auto add = [&](hipEvent_t a, hipEvent_t b) {
     float t0 = 0.f, t1 = 0.f;
     if (hipEventElapsedTime(&t0, ctx->ev_start, a) == hipSuccess && hipEventElapsedTime(&t1, ctx->ev_start, b) == hipSuccess)
@@ -1133,7 +1142,6 @@ int eval_loss_impl(sr_ctx* ctx, const sr_dataset* ds, int opset_id, const sr_tre
     SR_HIP_CHECK(ctx->h_outs.ensure(out_bytes, s, ctx->stream2));
     SR_HIP_CHECK(hipMemcpyAsync(ctx->h_outs.p, ctx->outs.p, out_bytes, hipMemcpyDeviceToHost, s));
   }
-  SR_HIP_CHECK(hipEventRecord(ctx->ev_end, s));
   if (ctx->spin && ctx->outs_on_host) {
     hipError_t e;
     while ((e = hipStreamQuery(s)) == hipErrorNotReady) {
@@ -2325,6 +2333,10 @@ int sr_set_tuning(sr_ctx* ctx, const char* name, int64_t value) {
   }
   if (std::strcmp(name, "code_cache") == 0) {  // LDS program cache (SR_AMD_CODE_CACHE)
     ctx->code_cache = value != 0 ? 1 : 0;
+    return SR_OK;
+  }
+  if (std::strcmp(name, "timing") == 0) {  // 0: record no timing events (kernel times read as 0)
+    ctx->timing = value != 0 ? 1 : 0;
     return SR_OK;
   }
   if (std::strcmp(name, "stress_probe") == 0) {  // the probe over the stress rows (SR_AMD_STRESS_PROBE)
