@@ -59,6 +59,7 @@ def parse_args(argv=None):
     ap.add_argument("--c4-steps", type=int, default=3)
     ap.add_argument("--no-c4", action="store_true")
     ap.add_argument("--no-tree-sharded", action="store_true")
+    ap.add_argument("--no-sharded-path", action="store_true", help="skip the N = 1 c2_sharded_path line")
     ap.add_argument("--cpu-trees", type=int, default=0, help="CPU-baseline tree sample (0 = auto, ~15 s)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-extra", action="store_true", help="skip the complete-only and Float64 lines")
@@ -265,7 +266,7 @@ def main():
     rpl = ctx.last_rows_per_lane()
 
     subs = {}
-    if world == 1:
+    if world == 1 and not args.no_sharded_path:
         subs["c2_sharded_path"] = sharded_path_line(ctx, tb, ds, opts, eval_loss_sharded, args, comm, nodes, rows)
     if not args.no_tree_sharded:
         subs["tree_sharded"] = tree_sharded_line(ctx, tb, opts, eval_loss_tree_sharded, args, comm, world, rank,
@@ -413,7 +414,8 @@ def c4_line(ctx, opts, eval_loss_sharded, gen_random_batch, Dataset, args, comm,
                         f"generator, seed 4) x {rows_total >> 20}M rows x 5 features, rows sharded n/{world}"),
            "code_path": "sr_eval_loss_sharded (same at every N)", "rows_per_gpu": n_local,
            "fraction_complete": float(np.mean(res["c"])),
-           "roofline": roofline(flops, kmean, PEAK_FP32_TFLOPS, busy_ms_per_step=busy,
+           "roofline": roofline(flops, kmean, PEAK_FP32_TFLOPS, busy_ms_per_step=busy, launches_per_step=nl,
+                                kernel=f"sr_tile_kernel<float,{ctx.last_rows_per_lane()},LOSS,gather=false,BASIC,W=4,L2>",
                                 algorithmic_bytes_per_step=algo, algorithmic_GBps=algo / (kmean * 1e-3) / 1e9,
                                 traffic=traffic.get("hbm_read_bytes_per_step") if traffic else None,
                                 traffic_source=traffic.get("source") if traffic else None,

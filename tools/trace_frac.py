@@ -17,8 +17,10 @@ import re
 import sys
 
 
-def main(out):
+def main(out, workload="c2"):
     line = json.loads(open(os.path.join(out, "bench_traced.json")).read().strip().splitlines()[-1])
+    if workload == "c4":  # the c4 sub-object: its launches are the last ones of the run
+        line = line["c4"]
     rf = line["roofline"]
     steps, per_step = line["steps"], rf["launches_per_step"]
     rows = list(csv.DictReader(open(glob.glob(os.path.join(out, "kt", "*kernel_trace.csv"))[0])))
@@ -53,12 +55,12 @@ def main(out):
             per_step_bytes = sum(vals) * 1024 * 2 / steps
             print(f"HBM (FETCH_SIZE)   : {per_step_bytes / 1e6:.1f} MB/step over the timed launches "
                   f"(algorithmic {rf['algorithmic_bytes_per_step'] / 1e6:.1f} MB)")
-            json.dump({"workload": "c2", "kernel": f"sr_tile_kernel<float, {rpl}, 0, ...> + the probe launches",
+            json.dump({"workload": workload, "kernel": f"sr_tile_kernel<float, {rpl}, 0, ...> + the probe launches",
                        "profiled_steps": steps, "launches": len(vals),
                        "hbm_read_bytes_per_step": per_step_bytes,
                        "source_cmd": "tools/bench_evidence.sh"},
-                      open(os.path.join(out, "traffic.json"), "w"))
+                      open(os.path.join(out, "traffic.json" if workload == "c2" else f"traffic_{workload}.json"), "w"))
 
 
 if __name__ == "__main__":
-    main(sys.argv[1])
+    main(sys.argv[1], sys.argv[2] if len(sys.argv) > 2 else "c2")
