@@ -14,8 +14,10 @@ import sr_amd  # noqa: E402
 from sr_amd import Dataset, Options, eval_loss_batch, flatten_trees, gen_random_population  # noqa: E402
 
 ctx = sr_amd.get_context()
-for dt, n_rows, n_trees in ((np.float64, 100, 20), (np.float64, 100, 40), (np.float32, 100_000, 31),
-                            (np.float64, 100, 280)):
+CONFIGS = ((np.float64, 100, 20), (np.float64, 100, 40), (np.float32, 100_000, 31), (np.float64, 100, 280))
+# SMALL_CONFIGS=2 (comma-separated indices) runs a subset
+_pick = os.environ.get("SMALL_CONFIGS")
+for dt, n_rows, n_trees in ([CONFIGS[int(i)] for i in _pick.split(",")] if _pick else CONFIGS):
     rng = np.random.default_rng(0)
     X = rng.standard_normal((2, n_rows)).astype(dt)
     y = (2 * np.cos(X[1]) + X[0] ** 2 - 2).astype(dt)
