@@ -168,6 +168,10 @@ struct sr_ctx {
   DevBuf prog, outs, part_sum, part_flag, pred, row_idx, tree_list,
       range_lo, range_hi, range_sums, packed, hint, jsum_prog, jsum_fin, jsum_scratch, probe_sum, probe_flag, g_code, g_offsets, g_consts, g_const_off, g_items, g_part, g_out,
       derived_cols, probe_derived;
+#ifdef SR_STAMPS
+  DevBuf stamps;  // latency-analysis builds: the last main launch's per-wave stamps (sr_debug_stamps)
+  int64_t n_stamps = 0;
+#endif
   int stress_probe = 1;
   int code_cache = 1;
   int first_chunk = 6;
@@ -739,6 +743,7 @@ int run_batch(sr_ctx* ctx, const sr_dataset* ds, int opset_id, const sr_tree_bat
         pa.out_sum = nullptr;
         pa.out_flag = nullptr;
         pa.code_lds = 0;  // (its groups differ from the main launch's)
+        pa.stamps = nullptr;
         pa.trees_per_block = std::max(16, g.W);
         pa.n_groups = int((np + pa.trees_per_block - 1) / pa.trees_per_block);
         pa.tiles_per_block = 1;
@@ -756,6 +761,12 @@ int run_batch(sr_ctx* ctx, const sr_dataset* ds, int opset_id, const sr_tree_bat
         }
         SR_HIP_CHECK(sr_launch_eval<T>(pa, mode, gather || stress_probe, tier, R, W, false, pa.n_groups * kProbeTiles, cs));
       }
+#ifdef SR_STAMPS
+      ctx->n_stamps = g.n_blocks * g.W * SR_NSTAMPS;
+      SR_HIP_CHECK(ctx->stamps.ensure(size_t(ctx->n_stamps) * sizeof(uint64_t)));
+      SR_HIP_CHECK(hipMemsetAsync(ctx->stamps.p, 0, size_t(ctx->n_stamps) * sizeof(uint64_t), cs));
+      a.stamps = ctx->stamps.as<uint64_t>();
+#endif
       SR_HIP_CHECK(sr_launch_eval<T>(a, mode, gather, tier, Rc, g.W, vstk, int(g.n_blocks), cs));
       if (!direct)
         SR_HIP_CHECK(sr_launch_reduce(a.part_sum, a.part_flag, int(np), g.n_row_blocks, a.perm,
@@ -2352,6 +2363,21 @@ int sr_tuning_info(sr_ctx* ctx, int* used_derived_columns, int64_t* exact_trees)
   if (exact_trees) *exact_trees = ctx->n_exact_last;
   return SR_OK;
 }
+
+#ifdef SR_STAMPS
+// latency-analysis builds only (not in include/sr_amd.h): the last main launch's stamps
+// [block][wave][SR_NSTAMPS] (wall clock, 100 MHz) and their count
+int sr_debug_stamps(sr_ctx* ctx, uint64_t* out, int64_t cap, int64_t* n) {
+  if (check_ctx(ctx) != SR_OK) return SR_ERR_INVALID_ARG;
+  Lock lk(ctx);
+  *n = ctx->n_stamps;
+  if (ctx->n_stamps > 0 && out && cap >= ctx->n_stamps) {
+    SR_HIP_CHECK(hipStreamSynchronize(ctx->stream));
+    SR_HIP_CHECK(hipMemcpy(out, ctx->stamps.p, size_t(ctx->n_stamps) * sizeof(uint64_t), hipMemcpyDeviceToHost));
+  }
+  return SR_OK;
+}
+#endif
 
 int sr_last_kernel_ms(sr_ctx* ctx, double* eval_ms, double* total_ms) {
   if (check_ctx(ctx) != SR_OK) return SR_ERR_INVALID_ARG;

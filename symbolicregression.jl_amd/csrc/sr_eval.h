@@ -57,7 +57,11 @@ struct SrEvalArgs {
   const int64_t* range_lo;
   const int64_t* range_hi;
   void* range_sums;
+  // -DSR_STAMPS builds only (latency analysis, tools/stamps.py): per wave, SR_NSTAMPS wall-clock
+  // stamps at fixed points of the kernel, [block][wave][SR_NSTAMPS]; NULL otherwise
+  uint64_t* stamps;
 };
+constexpr int SR_NSTAMPS = 8;
 
 template <typename T, int R, int MODE, bool GATHER, int TIER, int W = 4, int LK = -1, bool VSTK = false>
 hipError_t sr_launch_tile(const SrEvalArgs<T>& a, int n_blocks, hipStream_t s);

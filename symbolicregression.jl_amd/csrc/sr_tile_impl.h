@@ -705,6 +705,18 @@ __device__ __forceinline__ typename SrWindow<T>::type sr_window_lds(const uint4*
 }
 
 // ------------------------------------------------------------------ the interpreter kernel
+// SR_STAMP(k): latency-analysis builds only (-DSR_STAMPS, tools/stamps.py): lane 0 of each wave
+// records the wall clock at point k (0 entry, 1 prologue issued, 2 first tile staged, 3 first window
+// consumed, 4 first tile's trees done, 5 all tiles done, 6 results written)
+#ifdef SR_STAMPS
+#define SR_STAMP(k)                                                                              \
+  do {                                                                                           \
+    if (a.stamps && lane == 0)                                                                   \
+      a.stamps[(size_t(blockIdx.x) * size_t(W) + size_t(wave)) * SR_NSTAMPS + (k)] = wall_clock64(); \
+  } while (0)
+#else
+#define SR_STAMP(k) ((void)0)
+#endif
 // MODE: SR_MODE_LOSS (partials), SR_MODE_PRED (write predictions), SR_MODE_EXACT (Julia-order sums of
 // the checked arrays over row ranges: DynamicExpressions' isfinite(sum(x)) decided exactly as Base's
 // pairwise `sum` computes it in T; a "row block" is one range of a.range_lo/range_hi).
@@ -731,6 +743,7 @@ __global__ void __launch_bounds__(W * 64, (SrMinWavesFor<T, R, TIER, W, VSTK>::v
   const int tid = threadIdx.x;
   const int wave = tid >> 6;
   const int lane = tid & 63;
+  SR_STAMP(0);
   const int G = a.trees_per_block;
   const int MC = (MODE == SR_MODE_EXACT) ? a.max_checks : 0;
   const SrLdsPlan<T> plan(a.nf, ROWS, VSTK ? 0 : a.stack_depth, G, MC, W, a.w != nullptr,
@@ -803,6 +816,7 @@ __global__ void __launch_bounds__(W * 64, (SrMinWavesFor<T, R, TIER, W, VSTK>::v
   // EXACT: this block's row range [rlo, rhi] of the view (one leaf block of Julia's pairwise sum)
   const int64_t rlo = (MODE == SR_MODE_EXACT) ? a.range_lo[rb] : 0;
   const int64_t rhi = (MODE == SR_MODE_EXACT) ? a.range_hi[rb] : 0;
+  SR_STAMP(1);
 
   for (int tile = 0; tile < a.tiles_per_block; ++tile) {
     const int64_t row0 = (MODE == SR_MODE_EXACT) ? rlo + int64_t(tile) * ROWS
@@ -868,6 +882,7 @@ __global__ void __launch_bounds__(W * 64, (SrMinWavesFor<T, R, TIER, W, VSTK>::v
       }
     }
     __syncthreads();
+    if (tile == 0) SR_STAMP(2);
 
     if (use_hint) {
       dmask |= sr_ballot(hintv == a.hint_epoch) & live;
@@ -885,6 +900,9 @@ __global__ void __launch_bounds__(W * 64, (SrMinWavesFor<T, R, TIER, W, VSTK>::v
     typename SrWindow<T>::type nx = lds_code ? sr_window_lds<T>(lcode, nb, ne, lane) : sr_window<T>(a.code, nb, ne, lane);
     int j = -1;
     uint32_t tpe = 0u;
+#ifdef SR_STAMPS
+    const uint32_t nb0 = nb;
+#endif
     T tos[R];
     T s0[R], s1[R];  // VSTK operand-stack slots
 #pragma unroll
@@ -924,6 +942,9 @@ __global__ void __launch_bounds__(W * 64, (SrMinWavesFor<T, R, TIER, W, VSTK>::v
         const uint32_t n_here = __builtin_amdgcn_readfirstlane((tpe - base < SR_WIN) ? tpe - base : SR_WIN);
         // single-exit loop (a dead tree sets k past the window): a second loop exit would make
         // LLVM add an exit-selector block to every iteration
+#ifdef SR_STAMPS
+        if (tile == 0 && base == nb0) SR_STAMP(3);
+#endif
         for (uint32_t k = 0; k < n_here; ++k) {
           const uint32_t op = uint32_t(__builtin_amdgcn_readlane(int(wop), int(k)));
 #define SR_CVAL() sr_lane_value<T>(wc0, wc1, k)
@@ -1148,7 +1169,9 @@ __global__ void __launch_bounds__(W * 64, (SrMinWavesFor<T, R, TIER, W, VSTK>::v
         }
       }
     }
+    if (tile == 0) SR_STAMP(4);
   }
+  SR_STAMP(5);
 
   if (MODE == SR_MODE_EXACT) {
     __syncthreads();
@@ -1170,6 +1193,7 @@ __global__ void __launch_bounds__(W * 64, (SrMinWavesFor<T, R, TIER, W, VSTK>::v
       a.part_flag[o] = f;
     }
   }
+  SR_STAMP(6);
 }
 
 // ------------------------------------------------------------------ launch helpers
