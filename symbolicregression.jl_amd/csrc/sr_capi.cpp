@@ -208,6 +208,7 @@ struct sr_ctx {
   int rows_last = 0;        // rows per lane of the last interpreter call (sr_last_phase_ms out[7])
   int waves_override = 0;   // SR_AMD_WAVES (tuning): 8 selects the 8-wave f32 BASIC L2 loss kernel
   bool cost_order = true;   // launch trees in decreasing estimated cost (SR_AMD_NO_SORT=1 disables)
+  bool balance_groups = true;  // deal the cost order round-robin over tree groups (SR_AMD_BALANCE=0: contiguous)
   bool dead_hints = true;   // share dead-tree hints across row blocks (SR_AMD_NO_HINT=1 disables)
   int max_row_blocks = 256; // SR_AMD_MAX_ROW_BLOCKS (tuning): upper bound on row blocks per tree
   int chunks = 2;           // SR_AMD_CHUNKS: pipeline compile/launch over this many tree chunks (1 = off)
@@ -629,6 +630,29 @@ int run_batch(sr_ctx* ctx, const sr_dataset* ds, int opset_id, const sr_tree_bat
       for (int64_t i = 0; i < nc; ++i) ++start[key(i) + 1];
       for (size_t k = 1; k < start.size(); ++k) start[k] += start[k - 1];
       for (int64_t i = 0; i < nc; ++i) h_perm[t0 + start[key(i)]++] = uint32_t(i);
+      // Deal the cost-ordered trees of each class round-robin over that launch's tree groups (group
+      // g takes ranks g, g + n_groups, ...; each group's positions stay in decreasing cost, so its
+      // waves still get equal work).  Contiguous cost ranks made the first groups' workgroups several
+      // times longer than the last groups' and the launch ended on a tail of heavy workgroups (C2's
+      // complete trees: 4.36 ms with contiguous groups of 128, 3.32 unsorted).
+      if (sort && ctx->balance_groups) {
+        auto deal = [&](int64_t p0, int64_t np, int Rc, int depth_c) {
+          if (np <= 1) return;
+          const Grid gc = make_grid<T>(n_eval, np, Rc, W, int(ds->nf), depth_c, 0, ds->w != nullptr, ctx->tree_group,
+                                       ctx->max_row_blocks);
+          const int64_t G = gc.G, ng = gc.n_groups;
+          if (ng <= 1) return;
+          std::vector<uint32_t> ranked(h_perm + t0 + p0, h_perm + t0 + p0 + np);
+          int64_t k = 0;
+          for (int64_t j = 0; j < G; ++j)
+            for (int64_t gi = 0; gi < ng; ++gi) {
+              const int64_t size = gi + 1 < ng ? G : np - (ng - 1) * G;
+              if (j < size) h_perm[t0 + p0 + gi * G + j] = ranked[size_t(k++)];
+            }
+        };
+        if (n_vs > 0) deal(0, n_vs, Rv, 0);
+        if (n_vs < nc) deal(n_vs, nc - n_vs, R, depth);
+      }
     }
     {
       // programs in launch order: a tree group's code is one contiguous span (the kernel's LDS program
@@ -1760,6 +1784,7 @@ int sr_init(int device, sr_ctx** out) {
   if (const char* v = std::getenv("SR_AMD_TREES_PER_BLOCK")) ctx->tree_group = std::atoi(v);
   if (const char* v = std::getenv("SR_AMD_WAVES")) ctx->waves_override = std::atoi(v);
   if (const char* v = std::getenv("SR_AMD_NO_SORT")) ctx->cost_order = std::atoi(v) == 0;
+  if (const char* v = std::getenv("SR_AMD_BALANCE")) ctx->balance_groups = std::atoi(v) != 0;
   if (const char* v = std::getenv("SR_AMD_NO_HINT")) ctx->dead_hints = std::atoi(v) == 0;
   if (const char* v = std::getenv("SR_AMD_CHUNKS")) ctx->chunks = std::atoi(v);
   if (const char* v = std::getenv("SR_AMD_PROBE")) ctx->probe = std::atoi(v);

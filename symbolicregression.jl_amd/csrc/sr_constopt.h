@@ -128,9 +128,13 @@ inline int line_search(SrObjective& obj, const std::vector<int>& items, const st
   return 0;
 }
 
-// batched BFGS (n >= 2 constants) or 1-D Newton (one constant) from x0s; minimisers and minima out
+// batched BFGS (newton[k] = 0: n >= 2 constants) or 1-D Newton (newton[k] = 1: one constant) from
+// x0s; minimisers and minima out.  Every item runs its own algorithm on its own values: the batch only
+// decides which items share a call (each item's k-th line-search trial is in round k whatever the
+// others do), so the restarts and both groups of a batch run in one lock-step pass.
 inline int minimize(SrObjective& obj, const std::vector<int>& items, std::vector<std::vector<double>> xs,
-                    int iterations, bool newton, std::vector<std::vector<double>>* x_out, std::vector<double>* f_out) {
+                    int iterations, const std::vector<uint8_t>& newton, std::vector<std::vector<double>>* x_out,
+                    std::vector<double>* f_out) {
   const double g_tol = 1e-8;
   const size_t n = items.size();
   std::vector<double> fs;
@@ -138,8 +142,8 @@ inline int minimize(SrObjective& obj, const std::vector<int>& items, std::vector
   int rc = obj.fg(items, xs, &fs, &gs);
   if (rc) return rc;
   std::vector<std::vector<double>> invH(n);
-  if (!newton)
-    for (size_t k = 0; k < n; ++k) {
+  for (size_t k = 0; k < n; ++k)
+    if (!newton[k]) {
       const size_t d = xs[k].size();
       invH[k].assign(d * d, 0.0);
       for (size_t i = 0; i < d; ++i) invH[k][i * d + i] = 1.0;
@@ -155,39 +159,47 @@ inline int minimize(SrObjective& obj, const std::vector<int>& items, std::vector
     std::vector<std::vector<double>> sx, sg, dirs;
     std::vector<double> sf;
     for (int k : act) sub.push_back(items[size_t(k)]);
-    if (newton) {
-      std::vector<std::vector<double>> xp, xm;
-      std::vector<double> h;
-      for (int k : act) {
+    // Newton items: curvature from a central difference of the gradient, both probes of every such
+    // item in ONE gradient call (x + h then x - h)
+    std::vector<int> nsub;
+    std::vector<std::vector<double>> probes, xm;
+    std::vector<double> h;
+    for (int k : act)
+      if (newton[size_t(k)]) {
         const double hk = 1e-4 * std::max(1.0, fabs(xs[size_t(k)][0]));
         h.push_back(hk);
-        xp.push_back({xs[size_t(k)][0] + hk});
+        nsub.push_back(items[size_t(k)]);
+        probes.push_back({xs[size_t(k)][0] + hk});
         xm.push_back({xs[size_t(k)][0] - hk});
       }
-      std::vector<double> fp, fm;
-      std::vector<std::vector<double>> gp, gm;
+    const size_t nn = nsub.size();
+    std::vector<std::vector<double>> gpm;
+    if (nn > 0) {
+      for (size_t j = 0; j < nn; ++j) nsub.push_back(nsub[j]);
+      probes.insert(probes.end(), xm.begin(), xm.end());
+      std::vector<double> fpm;
       obj.counting = false;  // (num_evals follows Optim's f_calls: the curvature probes are not in it)
-      rc = obj.fg(sub, xp, &fp, &gp);
-      if (!rc) rc = obj.fg(sub, xm, &fm, &gm);
+      rc = obj.fg(nsub, probes, &fpm, &gpm);
       obj.counting = true;
       if (rc) return rc;
-      for (size_t j = 0; j < act.size(); ++j) {
-        const size_t k = size_t(act[j]);
-        double H = (gp[j][0] - gm[j][0]) / (2.0 * h[j]);
+    }
+    size_t q = 0;
+    for (int k : act) {
+      if (newton[size_t(k)]) {
+        double H = (gpm[q][0] - gpm[nn + q][0]) / (2.0 * h[q]);
         H = isfinite(H) ? (H > 1e-12 ? H : std::max(fabs(H), 1.0)) : 1.0;
-        dirs.push_back({-gs[k][0] / H});
+        dirs.push_back({-gs[size_t(k)][0] / H});
+        ++q;
+        continue;
       }
-    } else {
-      for (int k : act) {
-        const size_t d = xs[size_t(k)].size();
-        std::vector<double> dd(d, 0.0);
-        for (size_t i = 0; i < d; ++i) {
-          double s = 0.0;
-          for (size_t j = 0; j < d; ++j) s += invH[size_t(k)][i * d + j] * gs[size_t(k)][j];
-          dd[i] = -s;
-        }
-        dirs.push_back(dd);
+      const size_t d = xs[size_t(k)].size();
+      std::vector<double> dd(d, 0.0);
+      for (size_t i = 0; i < d; ++i) {
+        double s = 0.0;
+        for (size_t j = 0; j < d; ++j) s += invH[size_t(k)][i * d + j] * gs[size_t(k)][j];
+        dd[i] = -s;
       }
+      dirs.push_back(dd);
     }
     for (int k : act) {
       sx.push_back(xs[size_t(k)]);
@@ -225,7 +237,7 @@ inline int minimize(SrObjective& obj, const std::vector<int>& items, std::vector
       xs[k] = xnew[m];
       fs[k] = f2[m];
       gs[k] = g2[m];
-      if (newton) {
+      if (newton[k]) {
         if (!isfinite(fs[k]) || fabs(gs[k][0]) <= g_tol) active[k] = 0;
         continue;
       }
@@ -266,25 +278,28 @@ inline int sr_optimize_batch(SrObjective& obj, const std::vector<std::vector<dou
   if (rc) return rc;
   *best_x = x0;
   best_f->assign(n, INFINITY);
-  std::vector<int> multi, single;
-  for (size_t k = 0; k < n; ++k)
-    if (!x0[k].empty()) (x0[k].size() > 1 ? multi : single).push_back(int(k));  // (no constants: nothing to do)
-  for (size_t r = 0; r <= restarts.size(); ++r) {
-    for (int g = 0; g < 2; ++g) {
-      const std::vector<int>& grp = g == 0 ? multi : single;
-      if (grp.empty()) continue;
-      std::vector<std::vector<double>> starts;
-      for (int k : grp) starts.push_back(r == 0 ? x0[size_t(k)] : restarts[r - 1][size_t(k)]);
-      std::vector<std::vector<double>> xs;
-      std::vector<double> fs;
-      if ((rc = srco::minimize(obj, grp, starts, iterations, g == 1, &xs, &fs))) return rc;
-      for (size_t j = 0; j < grp.size(); ++j) {
-        const size_t k = size_t(grp[j]);
-        if (fs[j] < (*best_f)[k]) {
-          (*best_f)[k] = fs[j];
-          (*best_x)[k] = xs[j];
-        }
+  // every (start, member) pair with constants, in the reference's order (the member's own constants
+  // first, then each restart; per start BFGS members before Newton ones): one lock-step pass
+  std::vector<int> items;
+  std::vector<std::vector<double>> starts;
+  std::vector<uint8_t> newton;
+  for (size_t r = 0; r <= restarts.size(); ++r)
+    for (int g = 0; g < 2; ++g)
+      for (size_t k = 0; k < n; ++k) {
+        if (x0[k].empty() || (x0[k].size() > 1) != (g == 0)) continue;  // (no constants: nothing to do)
+        items.push_back(int(k));
+        starts.push_back(r == 0 ? x0[k] : restarts[r - 1][k]);
+        newton.push_back(g == 1 ? 1 : 0);
       }
+  if (items.empty()) return 0;
+  std::vector<std::vector<double>> xs;
+  std::vector<double> fs;
+  if ((rc = srco::minimize(obj, items, starts, iterations, newton, &xs, &fs))) return rc;
+  for (size_t j = 0; j < items.size(); ++j) {  // the best over starts, earlier starts winning ties
+    const size_t k = size_t(items[j]);
+    if (fs[j] < (*best_f)[k]) {
+      (*best_f)[k] = fs[j];
+      (*best_x)[k] = xs[j];
     }
   }
   return 0;
