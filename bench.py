@@ -264,6 +264,7 @@ def main():
     flops_per_step = float(rows) * (ops + 3 * nt)  # this GPU's interpreter work per step
     traffic = measured_traffic("c2")
     rpl = ctx.last_rows_per_lane()
+    n_derived = ctx.last_derived_columns()
 
     subs = {}
     if world == 1 and not args.no_sharded_path:
@@ -286,6 +287,7 @@ def main():
 
     if rank == 0:
         algo_bytes = algorithmic_bytes(nt, rows, n_launch, rpl)
+        algo_bytes_d = algorithmic_bytes(nt, rows, n_launch, rpl, n_derived)
         line = {
             "metric": "tree-node x row evals/sec (batched eval_loss, fp32)",
             "value": value,
@@ -330,7 +332,10 @@ def main():
                 flop_convention="n_rows * sum_t(n_op(t) + 3), 1 flop per operator incl. transcendentals (SURVEY 8d)",
                 algorithmic_bytes_per_step=algo_bytes,
                 algorithmic_GBps=algo_bytes / (kmean * 1e-3) / 1e9,
-                bytes_convention="ceil(n_trees/G) passes x (nf+1) x n_rows x 4 B; X/y re-reads are served from L2/MALL",
+                algorithmic_bytes_with_derived_per_step=algo_bytes_d,
+                n_derived_columns=n_derived,
+                bytes_convention=("ceil(n_trees/G) passes x (nf+1) x n_rows x 4 B; X/y re-reads are served from "
+                                  "L2/MALL; _with_derived adds the derived columns (n_derived x n_rows x 4 B per pass)"),
             ),
             "cpu_baseline": cpu,
             "parity": parity,
@@ -406,6 +411,8 @@ def c4_line(ctx, opts, eval_loss_sharded, gen_random_batch, Dataset, args, comm,
     traffic = measured_traffic("c4")
     nl = int(round(float(np.mean(st["launches"][-args.c4_steps:]))))
     algo = algorithmic_bytes(tb.n_trees, n_local, nl, ctx.last_rows_per_lane())
+    n_derived = ctx.last_derived_columns()
+    algo_d = algorithmic_bytes(tb.n_trees, n_local, nl, ctx.last_rows_per_lane(), n_derived)
     out = {"metric": "tree-node x row evals/sec (batched eval_loss, fp32)",
            "value": float(tb.n_nodes) * rows_total * args.c4_steps / dt, "unit": "node-evals/s",
            "ms_per_step": dt / args.c4_steps * 1e3, "steps": args.c4_steps, "warmup": 1, "n_gpus": world,
@@ -417,6 +424,7 @@ def c4_line(ctx, opts, eval_loss_sharded, gen_random_batch, Dataset, args, comm,
            "roofline": roofline(flops, kmean, PEAK_FP32_TFLOPS, busy_ms_per_step=busy, launches_per_step=nl,
                                 kernel=f"sr_tile_kernel<float,{ctx.last_rows_per_lane()},LOSS,gather=false,BASIC,W=4,L2>",
                                 algorithmic_bytes_per_step=algo, algorithmic_GBps=algo / (kmean * 1e-3) / 1e9,
+                                algorithmic_bytes_with_derived_per_step=algo_d, n_derived_columns=n_derived,
                                 traffic=traffic.get("hbm_read_bytes_per_step") if traffic else None,
                                 traffic_source=traffic.get("source") if traffic else None,
                                 hbm_GBps=(traffic["hbm_read_bytes_per_step"] / (kmean * 1e-3) / 1e9
@@ -469,9 +477,12 @@ def extra_lines(ctx, opts, trees, comp, X, y, args):
     return out
 
 
-def algorithmic_bytes(nt, rows, n_launch, rows_per_lane=8):
+def algorithmic_bytes(nt, rows, n_launch, rows_per_lane=8, n_derived=0):
+    """Bytes the interpreter launches of a step must read: every tree-group pass streams the X rows
+    (5 features) and y, plus the derived columns (LOAD_DERIVED inputs, read from HBM by the trees that
+    use them: with tree groups dealt round-robin every group holds users of nearly every column)."""
     n_passes = sum(-(-c // g) for c, g, _ in chunk_groups(nt, rows, n_launch, rows_per_lane))
-    return float(n_passes) * (5 + 1) * float(rows) * 4.0
+    return float(n_passes) * (5 + 1 + n_derived) * float(rows) * 4.0
 
 
 def chunk_groups(nt, rows, n_launch, rows_per_lane=8):

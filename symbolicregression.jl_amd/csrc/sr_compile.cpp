@@ -20,8 +20,12 @@
 namespace {
 
 // Persistent compile workers: spawning threads per batch cost more than compiling 10k trees.
-// run(n, fn) calls fn(0..n-1) on the workers and the caller; one batch at a time.  A forked child
-// (no threads of its own) gets a fresh pool.
+// run(n, fn) calls fn(0..n-1) on the caller and whichever workers wake in time; one batch at a time.
+// The caller never waits for a worker to wake up: it takes jobs itself from the start and waits only
+// for jobs a worker has already taken (a search's small batches finish before a sleeping worker is
+// scheduled: waiting for every worker to check in cost ~40 us per call).  Jobs are handed out by
+// tickets (generation << 32 | index), so a worker that wakes late never runs a finished batch's job.
+// A forked child (no threads of its own) gets a fresh pool.
 class WorkerPool {
  public:
   static WorkerPool& get() {
@@ -34,19 +38,18 @@ class WorkerPool {
   int size() const { return int(threads_.size()) + 1; }
   void run(int n, const std::function<void(int)>& fn) {
     std::lock_guard<std::mutex> batch(batch_mu_);
+    uint64_t g;
     {
-      std::lock_guard<std::mutex> g(mu_);
+      std::lock_guard<std::mutex> lk(mu_);
+      g = ++gen_;
       job_ = &fn;
       n_jobs_ = n;
-      next_.store(0);
-      active_ = int(threads_.size());
-      ++gen_;
+      done_.store(0);
+      ticket_.store(g << 32);
     }
-    cv_.notify_all();
-    drain();
-    std::unique_lock<std::mutex> g(mu_);
-    done_.wait(g, [&] { return active_ == 0; });
-    job_ = nullptr;
+    if (n > 1 && !threads_.empty()) cv_.notify_all();
+    drain(g, &fn, n);
+    while (done_.load(std::memory_order_acquire) < n) std::this_thread::yield();  // (jobs already taken)
   }
 
  private:
@@ -58,29 +61,41 @@ class WorkerPool {
     for (int i = 0; i < n; ++i) threads_.emplace_back([this] { loop(); });
     for (auto& t : threads_) t.detach();  // lives for the process
   }
-  void drain() {
-    for (int i = next_.fetch_add(1); i < n_jobs_; i = next_.fetch_add(1)) (*job_)(i);
+  // take jobs of generation g until none is left (a ticket of another generation ends the loop)
+  void drain(uint64_t g, const std::function<void(int)>* job, int n) {
+    uint64_t t = ticket_.load();
+    for (;;) {
+      if ((t >> 32) != g || int(t & 0xffffffffu) >= n) return;
+      if (!ticket_.compare_exchange_weak(t, t + 1)) continue;  // (t reloaded)
+      (*job)(int(t & 0xffffffffu));
+      done_.fetch_add(1, std::memory_order_release);
+      t = ticket_.load();
+    }
   }
   void loop() {
     uint64_t seen = 0;
     for (;;) {
+      uint64_t g;
+      const std::function<void(int)>* job;
+      int n;
       {
-        std::unique_lock<std::mutex> g(mu_);
-        cv_.wait(g, [&] { return gen_ != seen; });
-        seen = gen_;
+        std::unique_lock<std::mutex> lk(mu_);
+        cv_.wait(lk, [&] { return gen_ != seen; });
+        seen = g = gen_;
+        job = job_;
+        n = n_jobs_;
       }
-      drain();
-      std::lock_guard<std::mutex> g(mu_);
-      if (--active_ == 0) done_.notify_one();
+      drain(g, job, n);
     }
   }
   pid_t pid_;
   std::vector<std::thread> threads_;
   std::mutex batch_mu_, mu_;
-  std::condition_variable cv_, done_;
+  std::condition_variable cv_;
   const std::function<void(int)>* job_ = nullptr;
-  int n_jobs_ = 0, active_ = 0;
-  std::atomic<int> next_{0};
+  int n_jobs_ = 0;
+  std::atomic<uint64_t> ticket_{0};
+  std::atomic<int> done_{0};
   uint64_t gen_ = 0;
 };
 
