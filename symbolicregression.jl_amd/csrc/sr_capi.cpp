@@ -605,7 +605,7 @@ int run_batch(sr_ctx* ctx, const sr_dataset* ds, int opset_id, const sr_tree_bat
     // LDS-stack kernel over the tail of the launch order.
     int64_t n_vs = 0;  // launch positions [0, n_vs) -> register-stack kernel
     if (Rv > 0)
-      for (int64_t i = 0; i < nc; ++i) n_vs += pc.depth[size_t(i)] <= 2 ? 1 : 0;
+      for (int64_t i = 0; i < nc; ++i) n_vs += pc.depth[size_t(i)] <= SR_VSTK_SLOTS ? 1 : 0;
     // stage: code at code_base, offsets made absolute, static_bad, launch order (chunk-local)
     const size_t ncode = pc.code.size();
     if (code_base + ncode > code_cap) {
@@ -624,7 +624,7 @@ int run_batch(sr_ctx* ctx, const sr_dataset* ds, int opset_id, const sr_tree_bat
       const size_t nkey = size_t(cmax) + 1;
       std::vector<uint32_t> start(2 * nkey + 1, 0);
       auto key = [&](int64_t i) -> size_t {
-        const size_t cls = (Rv > 0 && pc.depth[size_t(i)] > 2) ? 1 : 0;
+        const size_t cls = (Rv > 0 && pc.depth[size_t(i)] > SR_VSTK_SLOTS) ? 1 : 0;
         return cls * nkey + (sort ? size_t(cmax - cost[size_t(i)]) : 0);
       };
       for (int64_t i = 0; i < nc; ++i) ++start[key(i) + 1];
@@ -723,7 +723,7 @@ int run_batch(sr_ctx* ctx, const sr_dataset* ds, int opset_id, const sr_tree_bat
       a.tiles_per_block = g.tiles;
       a.n_row_blocks = g.n_row_blocks;
       a.n_groups = g.n_groups;
-      a.stack_depth = vstk ? std::min(depth, 2) : depth;  // (the register-stack trees need <= 2)
+      a.stack_depth = vstk ? std::min(depth, SR_VSTK_SLOTS) : depth;  // (the register-stack trees need <= SR_VSTK_SLOTS)
       // Σ over n_total rows of values below tbig cannot overflow T, even with rounding slack.
       a.tbig = T(t_max<T>() / (2.0 * double(n_total > 0 ? n_total : 1)));
       a.track_x = !(max_abs_x < double(a.tbig)) ? 1 : 0;

@@ -6,6 +6,11 @@
 #include "../../include/sr_amd.h"
 
 enum { SR_MODE_LOSS = 0, SR_MODE_PRED = 1, SR_MODE_EXACT = 2 };
+// operand-stack slots the register-stack kernels hold in VGPRs (1: trees needing a second slot —
+// 6 % of C2's — run on the LDS-stack kernel instead)
+#ifndef SR_VSTK_SLOTS
+#define SR_VSTK_SLOTS 2
+#endif
 enum { SR_TIER_BASIC = 0, SR_TIER_FULL = 1 };
 
 template <typename T>

@@ -51,6 +51,7 @@ struct SrMinWaves {
 #ifndef SR_MIN_WAVES_VSTK16
 #define SR_MIN_WAVES_VSTK16 4
 #endif
+
 #ifndef SR_MIN_WAVES_VSTK8
 #define SR_MIN_WAVES_VSTK8 6
 #endif
@@ -527,7 +528,7 @@ __device__ __forceinline__ void sr_post_unary(uint32_t u, bool inf, T (&tos)[R])
 #define SR_KEEP_BRANCH() asm volatile("")
 #define SR_STK_BIN(ID, LEFT)                                          \
   if constexpr (VSTK) {                                               \
-    if ((SR_META() & SR_M_INDEX) == 0u) {                             \
+    if (SR_VSTK_SLOTS == 1 || (SR_META() & SR_M_INDEX) == 0u) {       \
       SR_KEEP_BRANCH();                                               \
       SR_BIN_EACH((LEFT) ? s0[r] : tos[r], (LEFT) ? tos[r] : s0[r], ID); \
     } else {                                                          \
@@ -904,9 +905,18 @@ __global__ void __launch_bounds__(W * 64, (SrMinWavesFor<T, R, TIER, W, VSTK>::v
     const uint32_t nb0 = nb;
 #endif
     T tos[R];
-    T s0[R], s1[R];  // VSTK operand-stack slots
+    T s0[R];  // VSTK operand-stack slots
+#if SR_VSTK_SLOTS > 1
+    T s1[R];
+#else
+    T* const s1 = s0;  // (never selected: one-slot kernels take no second-slot programs)
+#endif
 #pragma unroll
-    for (int r = 0; r < R; ++r) tos[r] = s0[r] = s1[r] = T(0);
+    for (int r = 0; r < R; ++r) tos[r] = s0[r] = T(0);
+#if SR_VSTK_SLOTS > 1
+#pragma unroll
+    for (int r = 0; r < R; ++r) s1[r] = T(0);
+#endif
     bool dead = false;
     bool susp_any = false;
     int check_k = 0;
@@ -945,13 +955,24 @@ __global__ void __launch_bounds__(W * 64, (SrMinWavesFor<T, R, TIER, W, VSTK>::v
 #ifdef SR_STAMPS
         if (tile == 0 && base == nb0) SR_STAMP(3);
 #endif
+#ifdef SR_OP_PREFETCH
+        // the next instruction's op word read one iteration ahead (lane k + 1 of the window; the
+        // read of lane 64 wraps to lane 0 and is never used): the scalar dispatch chain starts
+        // without waiting on the VALU -> SGPR read of its own op
+        uint32_t op_next = uint32_t(__builtin_amdgcn_readlane(int(wop), 0));
+#endif
         for (uint32_t k = 0; k < n_here; ++k) {
+#ifdef SR_OP_PREFETCH
+          const uint32_t op = op_next;
+          op_next = uint32_t(__builtin_amdgcn_readlane(int(wop), int((k + 1u) & 63u)));
+#else
           const uint32_t op = uint32_t(__builtin_amdgcn_readlane(int(wop), int(k)));
+#endif
 #define SR_CVAL() sr_lane_value<T>(wc0, wc1, k)
 #define SR_META() uint32_t(__builtin_amdgcn_readlane(int(wmeta), int(k)))
 #define SR_PUSH_TOS()                                                                        \
   if constexpr (VSTK) {                                                                      \
-    if (((SR_META() >> SR_M_PUSH_SHIFT) & 0x3fu) == 1u) {                                    \
+    if (SR_VSTK_SLOTS == 1 || ((SR_META() >> SR_M_PUSH_SHIFT) & 0x3fu) == 1u) {              \
       SR_KEEP_BRANCH();                                                                      \
       _Pragma("unroll") for (int r = 0; r < R; ++r) s0[r] = tos[r];                          \
     } else {                                                                                 \
@@ -1199,7 +1220,7 @@ __global__ void __launch_bounds__(W * 64, (SrMinWavesFor<T, R, TIER, W, VSTK>::v
 // ------------------------------------------------------------------ launch helpers
 template <typename T, int R, int MODE, bool GATHER, int TIER, int W, int LK, bool VSTK>
 hipError_t sr_launch_tile(const SrEvalArgs<T>& a, int n_blocks, hipStream_t s) {
-  if (VSTK && a.stack_depth > 2) return hipErrorInvalidValue;  // host checks: VSTK holds two slots
+  if (VSTK && a.stack_depth > SR_VSTK_SLOTS) return hipErrorInvalidValue;  // host routes deeper programs elsewhere
   const SrLdsPlan<T> plan(a.nf, 64 * R, VSTK ? 0 : a.stack_depth, a.trees_per_block,
                           MODE == SR_MODE_EXACT ? a.max_checks : 0, W, a.w != nullptr,
                           MODE == SR_MODE_LOSS ? a.code_lds : 0);
