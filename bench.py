@@ -465,10 +465,11 @@ def extra_lines(ctx, opts, trees, comp, X, y, args):
     dt, _, kms = timed(lib_step(ctx, call, st), steps, warm, lambda: None)
     km = float(np.mean(kms))
     busy = float(np.mean(st["busy"][-steps:]))
+    rpl64 = ctx.last_rows_per_lane()
     out["f64"] = roofline(
         float(X.shape[1]) * (tb64.n_operator_nodes + 3 * tb64.n_trees), busy, PEAK_FP64_TFLOPS,
         kernel_sum_ms_per_step=km, ms_per_step=dt / steps * 1e3,
-        kernel="sr_tile_kernel<double,4,LOSS,gather=false,BASIC>",
+        kernel=(f"sr_tile_kernel<double,{rpl64},LOSS,gather=false,BASIC" + (",register stack>" if rpl64 == 8 else ">")),
         node_evals_per_s=float(tb64.n_nodes) * X.shape[1] * steps / dt,
         fraction_complete=float(np.mean(o64["comp"].astype(bool))),
         convention="achieved / frac from the device-busy time (union of the launch intervals), which fits in the step",
@@ -542,7 +543,7 @@ def search_lines(args):
                 "device_wall_s": res.device_s, "host_s": res.host_s,
                 "device_wall_per_call_us": res.device_s / max(res.device_calls, 1) * 1e6,
                 "kernel_busy_per_call_us": diag.kernel_s / max(diag.device_calls, 1) * 1e6,
-                "per_call_note": ("device_wall = wall time inside the scoring calls (two scoring lanes overlap); "
+                "per_call_note": ("device_wall = wall time inside the scoring calls (the default four scoring lanes overlap); "
                                   "kernel_busy = the interpreter launches' device-busy time (a 5-iteration run "
                                   "with SR_AMD_SEARCH_KERNEL_TIMES=1)"),
                 "best_loss": float(min(m.loss for m in res.pareto_frontier)), "config": desc}

@@ -405,7 +405,11 @@ int sr_last_phase_ms(sr_ctx* ctx, double* out, int n);
  * probe: 0 off, 1 before every chunk, 2 before the chunks after the first), "stress_probe" (0 / 1: the
  * probe runs the dataset's stress rows — per feature the extreme and nearest-zero values — instead of
  * its first rows), "code_cache" (0 / 1: register-stack launches copy each tree group's programs into
- * LDS once instead of streaming them per tile from global memory).  Results do not depend on any knob.  SR_ERR_INVALID_ARG for an unknown name.  sr_tuning_info (optional outputs)
+ * LDS once instead of streaming them per tile from global memory), "timing" (0 / 1: record the HIP
+ * events behind sr_last_kernel_ms / sr_last_phase_ms), "rows_per_lane" (0: the default kernel per
+ * call; Float32 16 / 32 force the register-stack kernel and 4 / 8 the LDS-stack one, Float64 8 / 4
+ * likewise), "balance" (0 / 1: deal the cost-ordered trees round-robin over tree groups).  Results do
+ * not depend on any knob.  SR_ERR_INVALID_ARG for an unknown name.  sr_tuning_info (optional outputs)
  * reports how many derived columns the last sr_eval_loss_batch used and how many of its trees went
  * through the exact-sum pass (flagged BIG). */
 int sr_set_tuning(sr_ctx* ctx, const char* name, int64_t value);

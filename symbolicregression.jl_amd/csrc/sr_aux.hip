@@ -226,9 +226,15 @@ hipError_t sr_launch_basic_loss(const SrEvalArgs<T>& a, int n_blocks, hipStream_
 #define SR_VSTK_DEFAULT_ROWS 16
 #endif
 int sr_vstk_rows(int elem_size, int64_t n_rows, int requested) {
-  // f64: the 8-rows/lane register-stack build needs 181 VGPRs (2 waves per SIMD) and measured no
-  // better than the classic 4-rows/lane build at 100 (5 waves): only on request (tuning)
-  if (elem_size == 8) return requested == 8 ? 8 : 0;
+  // f64: the 8-rows/lane register-stack build (181 VGPRs, 2 waves per SIMD) against the classic
+  // 4-rows/lane build (100, 5 waves): round 2 measured it 3 % slower; with the launch order dealt over
+  // tree groups it is faster (C2 in f64 13.45 -> 12.69 ms per step, arithmetic-only -19 %,
+  // profiles/r03_ab_f64_vstk.txt), so it is the default for large views too
+  if (elem_size == 8) {
+    if (requested == 8) return 8;
+    if (requested == 4 || requested == 2) return 0;
+    return n_rows >= (int64_t(1) << 17) ? 8 : 0;
+  }
   if (requested == 16 || requested == 32) return requested;
   if (requested == 4 || requested == 8) return 0;
   return n_rows >= (int64_t(1) << 17) ? SR_VSTK_DEFAULT_ROWS : 0;

@@ -2379,6 +2379,14 @@ int sr_set_tuning(sr_ctx* ctx, const char* name, int64_t value) {
     ctx->stress_probe = value != 0 ? 1 : 0;
     return SR_OK;
   }
+  if (std::strcmp(name, "rows_per_lane") == 0) {  // kernel build per call (SR_AMD_ROWS_PER_LANE; 0 = default)
+    ctx->rows_override = int(value);
+    return SR_OK;
+  }
+  if (std::strcmp(name, "balance") == 0) {  // launch order dealt over tree groups (SR_AMD_BALANCE)
+    ctx->balance_groups = value != 0;
+    return SR_OK;
+  }
   return set_error(SR_ERR_INVALID_ARG, std::string("unknown tuning knob '") + name + "'");
 }
 

@@ -109,13 +109,13 @@ SRL_HD inline double sr_log_normal(uint32_t ix, int kadj, const double* tab, con
   __builtin_memcpy(&z, &iz, 4);
   const double invc = tab[2 * i], logc = tab[2 * i + 1];
   const double r = fma(double(z), invc, -1.0);
-  const double r2 = r * r;
-  // log1p(r) = r + r^2 ((-1/2 + r/3) - r^2/4): the dropped r^5/5 is <= 2^-37.3 absolute, <= 2^-30 of the
-  // result (|log x| >= 2^-7.4 outside the cell of 1; |r| inside it)
-  const double a = fma(r, c.c3, -0.5);
-  const double p = fma(r2, c.c4, a);
-  const double y = fma(double(k + kadj), c.ln2, logc) + r;
-  return fma(r2, p, y);
+  // log1p(r) = r (1 + r (-1/2 + r (1/3 - r/4))) in Horner form, added to k ln2 + log c by the last
+  // fused multiply-add: the dropped r^5/5 is <= 2^-37.3 absolute, <= 2^-30 of the result (|log x| >=
+  // 2^-7.4 outside the cell of 1; |r| inside it).  Six f64 operations (round 3; was seven)
+  double q = fma(r, c.c4, c.c3);
+  q = fma(r, q, -0.5);
+  q = fma(r, q, 1.0);
+  return fma(r, q, fma(double(k + kadj), c.ln2, logc));
 }
 
 // Base.log over every Float32: +Inf -> +Inf, +-0 -> -Inf, x < 0 or NaN -> NaN; subnormals scaled by
@@ -207,8 +207,9 @@ SRL_HD inline double sr_rem_pio2f_fast(float x, int* q) {
 // with cos r = 1 - r^2/2 and sin r = r (1 - r^2/6).  The dropped Taylor terms (r^4/24 <= 2^-30 of c_k,
 // r^5/120 <= 2^-38) stay below 2^-28 of the result wherever it is (|result| >= |c_k| / 2 next to a
 // zero of the function, where c_k = 0 exactly and the result is -s_k sin r itself): <= 0.5 + 2^-4
-// ulp after the final rounding (tools/libm_exhaustive.cpp: every Float32 |x| < 2^20).  Six f64
-// operations after the reduction (eight with the degree-5/4 polynomials of a 128-entry table).
+// ulp after the final rounding (tools/libm_exhaustive.cpp: every Float32 |x| < 2^20).  Five f64
+// operations after the reduction, the terms in Horner form in r (six as (c_k cos r - s_k sin r) in
+// round 3's first version, eight with the degree-5/4 polynomials of a 128-entry table).
 template <bool COS>
 SRL_HD inline float sr_sincosf_tab(float x, const double* tab) {
   const double xd = double(x);
@@ -224,10 +225,11 @@ SRL_HD inline float sr_sincosf_tab(float x, const double* tab) {
   // entry k = 16 bytes at byte offset 16 k
   const double* e = reinterpret_cast<const double*>(reinterpret_cast<const char*>(tab) + ((uint32_t(tb) << 4) & 0xff0u));
   const double sk = e[0], ck = e[1];
-  const double z = r * r;
-  const double sr = r * fma(z, -0x1.5555555555555p-3, 1.0);
-  const double cr = fma(z, -0.5, 1.0);
-  return COS ? float(fma(ck, cr, -(sk * sr))) : float(fma(sk, cr, ck * sr));
+  // cos x = ck + r (-sk + r (-ck/2 + r sk/6)), sin x = sk + r (ck + r (-sk/2 - r ck/6)): the same
+  // Taylor terms in Horner form, five f64 operations (round 3; was six)
+  const double a = COS ? ck : sk, b = COS ? -sk : ck;
+  const double c2 = -0.5 * a, c3 = b * -0x1.5555555555555p-3;
+  return float(fma(r, fma(r, fma(r, c3, c2), b), a));
 }
 
 // Full range: the table path below 2^20, Payne-Hanek above (the device only comes here when some

@@ -355,6 +355,10 @@ struct Engine : sr_search_base {
   int iteration = 0;
   // accounting
   double num_evals = 0.0;
+  const bool profile_lanes = [] {
+    const char* v = std::getenv("SR_AMD_SEARCH_PROFILE");
+    return v && std::atoi(v) != 0;
+  }();
   int64_t s_r_cycles = 0;
   double host_ms = 0.0;
   std::vector<int64_t> batch_idx;  // this iteration's minibatch (batching)
@@ -886,6 +890,8 @@ struct Engine : sr_search_base {
   // owned islands are split over lanes)
   int iterate_islands(Lane L, const std::vector<int>& islands, const std::vector<int64_t>& rows,
                       const std::vector<int64_t>& orows) {
+    const auto t_start = Clock::now();
+    const int64_t calls0 = L.sc->calls;
     const int ncyc = o.ncycles_per_iteration;
     const int n_evol = (o.population_size + o.tournament_selection_n - 1) / o.tournament_selection_n;
     for (int c = 0; c < ncyc; ++c) {
@@ -924,9 +930,15 @@ struct Engine : sr_search_base {
         }
       }
     }
+    const double cyc_ms = ms_since(t_start);
+    const int64_t calls1 = L.sc->calls;
     std::vector<uint8_t> imp;
     int rc = optimize_members(L, sel, sel_island, orows, &imp);
     if (rc) return rc;
+    if (profile_lanes)  // SR_AMD_SEARCH_PROFILE=1: per lane and iteration, to stderr
+      std::fprintf(stderr, "[sr_search] iteration %d lane islands %zu: cycles %.2f ms (%lld calls), optimise %.2f ms (%lld calls, %zu members)\n",
+                   iteration, islands.size(), cyc_ms, (long long)(calls1 - calls0), ms_since(t_start) - cyc_ms,
+                   (long long)(L.sc->calls - calls1), sel.size());
     if (o.batching) {  // finalize_costs + best-seen re-scoring on the full data
       std::vector<Member<T>*> ms;
       for (int i : islands) {

@@ -63,7 +63,8 @@ class DeviceContext:
         return [float(v) for v in out[:5]]
 
     def set_tuning(self, name, value):
-        """Run-time tuning knob (results never depend on one): "derived" = 0 / 1."""
+        """Run-time tuning knob (results never depend on one; include/sr_amd.h lists them): "derived",
+        "probe", "stress_probe", "code_cache", "timing", "rows_per_lane", "balance"."""
         _lib.check(_lib.lib.sr_set_tuning(self.handle, name.encode(), int(value)))
 
     def last_derived_columns(self):

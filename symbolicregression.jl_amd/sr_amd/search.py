@@ -332,7 +332,7 @@ def _torch_comm():
 
 
 def equation_search(X=None, y=None, *, niterations=10, options, weights=None, search_options=None, seed=0,
-                    verbosity=0, dataset=None, distributed=False, scoring_lanes=2, _loss_fn=None, _grad_fn=None,
+                    verbosity=0, dataset=None, distributed=False, scoring_lanes=4, _loss_fn=None, _grad_fn=None,
                     _native_scorer=None):
     """Batched-island ``equation_search`` (src/SymbolicRegression.jl:967-1216) -> SearchResult.
 

@@ -174,6 +174,35 @@ def test_population_f64_vs_oracle():
     assert np.median(_rel(loss[comp], o_loss[comp])) < 1e-13
 
 
+@pytest.mark.parametrize("dtype,builds", [(np.float32, (0, 16, 8)), (np.float64, (0, 8, 4))])
+def test_kernel_builds_and_launch_orders_agree(dtype, builds):
+    """Every interpreter build a call can pick (register-stack or LDS-stack operand stack, rows per
+    lane) and both launch orders (cost ranks dealt over tree groups, or contiguous) against the oracle;
+    one build's results are bit-identical whatever the launch order."""
+    opts = Options(**C2_OPTS)
+    X, y = _c2_data(20000, dtype=dtype, seed=17)
+    tb = flatten_trees(gen_random_population(1200, opts, 5, max_size=30, dtype=dtype, seed=17), dtype)
+    d = Dataset(X, y)
+    orc = Oracle.from_options(opts)
+    rel_bar = 1e-10 if dtype == np.float64 else 1e-4
+    tol, o_loss, o_comp, _ = loss_tolerance(orc, tb, X, y, rel_bar=rel_bar)
+    ctx = sr_amd.get_context()
+    try:
+        for rpl in builds:
+            ctx.set_tuning("rows_per_lane", rpl)
+            runs = []
+            for bal in (1, 0):
+                ctx.set_tuning("balance", bal)
+                loss, comp = eval_loss_batch(tb, d, opts)
+                assert np.array_equal(comp, o_comp), (rpl, bal)
+                assert_losses_within(loss, o_loss, comp, tol, f"rows_per_lane={rpl} balance={bal}")
+                runs.append(loss)
+            assert np.array_equal(runs[0], runs[1]), rpl
+    finally:
+        ctx.set_tuning("rows_per_lane", 0)
+        ctx.set_tuning("balance", 1)
+
+
 def test_predictions_vs_oracle():
     opts = Options(**FULL_OPTS)
     X, _ = _c2_data(777, seed=9)
