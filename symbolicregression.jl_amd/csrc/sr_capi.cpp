@@ -136,7 +136,7 @@ struct sr_ctx {
   // programs + per-tree metadata of the last run_batch: ONE device allocation and ONE pinned staging
   // buffer with the same layout (code | offsets | static_bad | launch order), so a single-chunk call
   // uploads with one DMA; per-tree {Σ loss, flags} likewise share one allocation (one DMA back)
-  HostBuf h_prog, h_outs;
+  HostBuf h_prog, h_outs, h_grad;  // (h_grad: the gradient call's staging image, then its results)
   void* d_code = nullptr;
   uint32_t* d_off = nullptr;
   uint8_t* d_bad = nullptr;
@@ -1397,31 +1397,50 @@ int eval_grad_impl(sr_ctx* ctx, const sr_dataset* ds, int opset_id, const sr_tre
   }
   hipStream_t s = ctx->stream;
   const int depth = prog.max_depth > 0 ? prog.max_depth : 1;
-  SR_HIP_CHECK(ctx->g_code.ensure(prog.code.size() * sizeof(SrIns<T>) + 16));
-  SR_HIP_CHECK(ctx->g_offsets.ensure(prog.offsets.size() * sizeof(uint32_t)));
-  SR_HIP_CHECK(ctx->g_consts.ensure(consts.size() * sizeof(T) + 16));
-  SR_HIP_CHECK(ctx->g_const_off.ensure(prog.const_off.size() * sizeof(uint32_t)));
-  if (!prog.code.empty())
-    SR_HIP_CHECK(hipMemcpyAsync(ctx->g_code.p, prog.code.data(), prog.code.size() * sizeof(SrIns<T>),
-                                hipMemcpyHostToDevice, s));
-  SR_HIP_CHECK(hipMemcpyAsync(ctx->g_offsets.p, prog.offsets.data(), prog.offsets.size() * sizeof(uint32_t),
-                              hipMemcpyHostToDevice, s));
-  if (!consts.empty())
-    SR_HIP_CHECK(hipMemcpyAsync(ctx->g_consts.p, consts.data(), consts.size() * sizeof(T), hipMemcpyHostToDevice, s));
-  SR_HIP_CHECK(hipMemcpyAsync(ctx->g_const_off.p, prog.const_off.data(), prog.const_off.size() * sizeof(uint32_t),
-                              hipMemcpyHostToDevice, s));
+  // one pinned staging image (programs, offsets, constants, constant offsets, every bucket's work
+  // items) -> ONE upload; every bucket's kernel and reduce go out back to back, their results come
+  // back in ONE copy, and the host waits once (round 3: four uploads, then per bucket an upload, a
+  // copy back and a wait)
+  auto al = [](size_t x) { return (x + 255) & ~size_t(255); };
+  const size_t o_code = 0;
+  const size_t o_offs = al(o_code + prog.code.size() * sizeof(SrIns<T>));
+  const size_t o_cons = al(o_offs + prog.offsets.size() * sizeof(uint32_t));
+  const size_t o_coff = al(o_cons + consts.size() * sizeof(T));
+  size_t o_items[3], o_vals[3];
+  size_t at = al(o_coff + prog.const_off.size() * sizeof(uint32_t)), n_vals_all = 0;
+  for (int b = 0; b < 3; ++b) {
+    o_items[b] = at;
+    at = al(at + 2 * items[b].size() * sizeof(uint32_t));
+    o_vals[b] = n_vals_all;
+    n_vals_all += items[b].size() * size_t(kts[b]);
+  }
+  const size_t stage_bytes = at;
+  SR_HIP_CHECK(ctx->g_code.ensure(stage_bytes + 16));
+  SR_HIP_CHECK(ctx->h_grad.ensure(std::max(stage_bytes, n_vals_all * sizeof(double)) + 16, s, ctx->stream2));
+  char* hs = ctx->h_grad.as<char>();
+  if (!prog.code.empty()) std::memcpy(hs + o_code, prog.code.data(), prog.code.size() * sizeof(SrIns<T>));
+  std::memcpy(hs + o_offs, prog.offsets.data(), prog.offsets.size() * sizeof(uint32_t));
+  if (!consts.empty()) std::memcpy(hs + o_cons, consts.data(), consts.size() * sizeof(T));
+  std::memcpy(hs + o_coff, prog.const_off.data(), prog.const_off.size() * sizeof(uint32_t));
+  for (int b = 0; b < 3; ++b) {
+    uint32_t* d = reinterpret_cast<uint32_t*>(hs + o_items[b]);
+    std::copy(items[b].begin(), items[b].end(), d);
+    std::copy(k0s[b].begin(), k0s[b].end(), d + items[b].size());
+  }
+  char* ds_ = ctx->g_code.as<char>();
+  SR_HIP_CHECK(hipMemcpyAsync(ds_, hs, stage_bytes, hipMemcpyHostToDevice, s));
+  SR_HIP_CHECK(ctx->g_out.ensure(n_vals_all * sizeof(double) + 16));
   const double denom = view_denominator<T>(ds, row_idx, n_idx);
-  constexpr int kWaves = 4, kRowsPerTile = 256;
-  const int64_t n_tiles = (n_eval + kRowsPerTile - 1) / kRowsPerTile;
+  constexpr int kWaves = 4;
+  size_t part_need = 0;
+  struct Launch { int64_t n_rb, tiles_per_block, n_groups; };
+  Launch lc[3] = {};
   for (int b = 0; b < 3; ++b) {
     const int64_t ni = int64_t(items[b].size());
     if (ni == 0) continue;
     const int kt = kts[b];
-    std::vector<uint32_t> packed(items[b]);
-    packed.insert(packed.end(), k0s[b].begin(), k0s[b].end());
-    SR_HIP_CHECK(ctx->g_items.ensure(packed.size() * sizeof(uint32_t)));
-    SR_HIP_CHECK(hipMemcpyAsync(ctx->g_items.p, packed.data(), packed.size() * sizeof(uint32_t),
-                                hipMemcpyHostToDevice, s));
+    const int64_t rows_per_tile = 64 * int64_t(sr_grad_rows_per_lane(kt));
+    const int64_t n_tiles = (n_eval + rows_per_tile - 1) / rows_per_tile;
     const int64_t n_groups = (ni + kWaves - 1) / kWaves;
     int64_t n_rb = (4096 + n_groups - 1) / n_groups;
     if (n_rb > n_tiles) n_rb = n_tiles;
@@ -1429,16 +1448,25 @@ int eval_grad_impl(sr_ctx* ctx, const sr_dataset* ds, int opset_id, const sr_tre
     const int64_t tiles_per_block = (n_tiles + n_rb - 1) / n_rb;
     n_rb = (n_tiles + tiles_per_block - 1) / tiles_per_block;
     if (n_rb * n_groups > 0x7fffffff) return set_error(SR_ERR_INVALID_ARG, "grid too large");
-    const size_t n_vals = size_t(ni) * size_t(kt);
-    SR_HIP_CHECK(ctx->g_part.ensure(size_t(n_rb) * n_vals * sizeof(double)));
-    SR_HIP_CHECK(ctx->g_out.ensure(n_vals * sizeof(double)));
+    const size_t lds = (size_t(ds->nf) + 1 + (ds->w ? 1 : 0)) * size_t(rows_per_tile) * sizeof(T) +
+                       size_t(kWaves) * depth * (1 + kt) * size_t(rows_per_tile) * sizeof(T);
+    if (lds > kLdsMax) return set_error(SR_ERR_TOO_DEEP, "gradient tile needs more than 160 KiB of LDS");
+    lc[b] = Launch{n_rb, tiles_per_block, n_groups};
+    part_need = std::max(part_need, size_t(n_rb) * size_t(ni) * size_t(kt));
+  }
+  // (buckets run one after another on the stream, so they share the partials buffer)
+  SR_HIP_CHECK(ctx->g_part.ensure(part_need * sizeof(double) + 16));
+  for (int b = 0; b < 3; ++b) {
+    const int64_t ni = int64_t(items[b].size());
+    if (ni == 0) continue;
+    const int kt = kts[b];
     SrGradArgs<T> a{};
-    a.code = ctx->g_code.as<SrIns<T>>();
-    a.offsets = ctx->g_offsets.as<uint32_t>();
-    a.consts = ctx->g_consts.as<T>();
-    a.const_off = ctx->g_const_off.as<uint32_t>();
-    a.item_tree = ctx->g_items.as<uint32_t>();
-    a.item_k0 = ctx->g_items.as<uint32_t>() + ni;
+    a.code = reinterpret_cast<const SrIns<T>*>(ds_ + o_code);
+    a.offsets = reinterpret_cast<const uint32_t*>(ds_ + o_offs);
+    a.consts = reinterpret_cast<const T*>(ds_ + o_cons);
+    a.const_off = reinterpret_cast<const uint32_t*>(ds_ + o_coff);
+    a.item_tree = reinterpret_cast<const uint32_t*>(ds_ + o_items[b]);
+    a.item_k0 = a.item_tree + ni;
     a.n_items = int(ni);
     a.X = static_cast<const T*>(ds->X);
     a.y = static_cast<const T*>(ds->y);
@@ -1447,26 +1475,26 @@ int eval_grad_impl(sr_ctx* ctx, const sr_dataset* ds, int opset_id, const sr_tre
     a.ld = ds->ld;
     a.n_rows = n_eval;
     a.nf = int(ds->nf);
-    a.tiles_per_block = int(tiles_per_block);
-    a.n_row_blocks = int(n_rb);
-    a.n_groups = int(n_groups);
+    a.tiles_per_block = int(lc[b].tiles_per_block);
+    a.n_row_blocks = int(lc[b].n_rb);
+    a.n_groups = int(lc[b].n_groups);
     a.stack_depth = depth;
     a.loss_kind = lkind;
     a.loss_param = T(lparam);
     a.part = ctx->g_part.as<double>();
-    const size_t lds = (size_t(a.nf) + 1 + (a.w ? 1 : 0)) * kRowsPerTile * sizeof(T) +
-                       size_t(kWaves) * depth * (1 + kt) * 64 * sizeof(T);
-    if (lds > kLdsMax) return set_error(SR_ERR_TOO_DEEP, "gradient tile needs more than 160 KiB of LDS");
-    SR_HIP_CHECK(sr_launch_grad_any<T>(a, kt, gather, int(n_rb * n_groups), s));
-    SR_HIP_CHECK(sr_launch_grad_reduce(a.part, int(n_rb), int(n_vals), ctx->g_out.as<double>(), s));
-    std::vector<double> out(n_vals);
-    SR_HIP_CHECK(hipMemcpyAsync(out.data(), ctx->g_out.p, n_vals * sizeof(double), hipMemcpyDeviceToHost, s));
-    SR_HIP_CHECK(hipStreamSynchronize(s));
-    for (int64_t i = 0; i < ni; ++i) {
-      const uint32_t t = items[b][size_t(i)], k0 = k0s[b][size_t(i)];
+    SR_HIP_CHECK(sr_launch_grad_any<T>(a, kt, gather, int(lc[b].n_rb * lc[b].n_groups), s));
+    SR_HIP_CHECK(sr_launch_grad_reduce(a.part, int(lc[b].n_rb), int(size_t(ni) * kt), ctx->g_out.as<double>() + o_vals[b], s));
+  }
+  double* out = ctx->h_grad.as<double>();  // (the staging image is no longer needed: the upload is done)
+  SR_HIP_CHECK(hipMemcpyAsync(out, ctx->g_out.p, n_vals_all * sizeof(double), hipMemcpyDeviceToHost, s));
+  SR_HIP_CHECK(hipStreamSynchronize(s));
+  for (int b = 0; b < 3; ++b) {
+    const int kt = kts[b];
+    for (size_t i = 0; i < items[b].size(); ++i) {
+      const uint32_t t = items[b][i], k0 = k0s[b][i];
       const uint32_t nc = prog.n_consts[t];
       for (int q = 0; q < kt && k0 + uint32_t(q) < nc; ++q)
-        g[prog.const_off[t] + k0 + uint32_t(q)] = T(out[size_t(i) * kt + size_t(q)] / denom);
+        g[prog.const_off[t] + k0 + uint32_t(q)] = T(out[o_vals[b] + i * size_t(kt) + size_t(q)] / denom);
     }
   }
   return SR_OK;
@@ -1829,7 +1857,7 @@ int sr_shutdown(sr_ctx* ctx) {
                       &ctx->hint, &ctx->jsum_prog, &ctx->jsum_fin, &ctx->jsum_scratch, &ctx->probe_sum, &ctx->probe_flag, &ctx->g_code, &ctx->g_offsets, &ctx->g_consts, &ctx->g_const_off,
                       &ctx->g_items, &ctx->g_part, &ctx->g_out, &ctx->derived_cols, &ctx->probe_derived, &ctx->shard_buf})
       b->release();
-    for (HostBuf* b : {&ctx->h_prog, &ctx->h_outs}) b->release();
+    for (HostBuf* b : {&ctx->h_prog, &ctx->h_outs, &ctx->h_grad}) b->release();
     for (int c = 0; c < kMaxChunks; ++c) {
       (void)hipEventDestroy(ctx->ev_c0[c]);
       (void)hipEventDestroy(ctx->ev_c1[c]);

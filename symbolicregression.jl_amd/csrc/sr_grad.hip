@@ -16,8 +16,8 @@ hipError_t sr_launch_grad_any(const SrGradArgs<T>& a, int kt, bool gather, int n
 
 hipError_t sr_launch_grad_reduce(const double* part, int n_row_blocks, int n_vals, double* out, hipStream_t s) {
   if (n_vals <= 0) return hipSuccess;
-  hipLaunchKernelGGL(sr_grad_reduce_kernel, dim3(unsigned((n_vals + 255) / 256)), dim3(256), 0, s, part, n_row_blocks,
-                     n_vals, out);
+  hipLaunchKernelGGL(sr_grad_reduce_kernel, dim3(unsigned((n_vals + 3) / 4)), dim3(256), 0, s, part, n_row_blocks,
+                     n_vals, out);  // (4 waves per block, one value per wave)
   return hipGetLastError();
 }
 

@@ -40,11 +40,19 @@ __device__ __forceinline__ T sr_readlane_val(T v, uint32_t l) {
   }
 }
 
+// Rows per lane by tangent width: the value and its KT tangents of R rows stay in VGPRs, so one
+// dispatch of an instruction covers R x 64 rows (round 3: one row per lane made every dispatch and
+// operand decode cover 64 rows only; C3's gradient launches 0.61 ms each).
+template <int KT>
+struct SrGradRows {
+  static constexpr int value = sr_grad_rows_per_lane(KT);
+};
+
 template <typename T, int KT, int W, bool GATHER>
 __global__ void __launch_bounds__(W * 64) sr_grad_kernel(const SrGradArgs<T> a) {
-  constexpr int SUB = 4;             // 64-row sub-tiles per staged tile
-  constexpr int ROWS = 64 * SUB;
-  constexpr int NV = 1 + KT;         // value + tangents
+  constexpr int R = SrGradRows<KT>::value;  // rows per lane: lane + 64 j, j < R
+  constexpr int ROWS = 64 * R;               // rows per staged tile
+  constexpr int NV = 1 + KT;                 // value + tangents
   extern __shared__ __attribute__((aligned(16))) unsigned char sr_smem[];
   const int tid = threadIdx.x;
   const int wave = tid >> 6;
@@ -52,8 +60,8 @@ __global__ void __launch_bounds__(W * 64) sr_grad_kernel(const SrGradArgs<T> a) 
   T* xs = reinterpret_cast<T*>(sr_smem);                       // [nf][ROWS]
   T* ys = xs + size_t(a.nf) * ROWS;                            // [ROWS]
   T* wsv = ys + ROWS;                                          // [ROWS] (weighted)
-  T* stk = wsv + (a.w ? ROWS : 0);                             // [W][depth][NV][64]
-  T* my_stk = stk + size_t(wave) * a.stack_depth * NV * 64 + lane;
+  T* stk = wsv + (a.w ? ROWS : 0);                             // [W][depth][NV][R][64]
+  T* my_stk = stk + size_t(wave) * a.stack_depth * NV * R * 64 + lane;
 
   const int tg = blockIdx.x % a.n_groups;
   const int rb = blockIdx.x / a.n_groups;
@@ -94,87 +102,108 @@ __global__ void __launch_bounds__(W * 64) sr_grad_kernel(const SrGradArgs<T> a) 
     __syncthreads();
     if (!active || pe == pb) continue;
 
-    for (int sub = 0; sub < SUB; ++sub) {
-      const int r = sub * 64 + lane;
-      if (row0 + sub * 64 >= a.n_rows) break;  // uniform
-      T v = T(0);
-      T dv[KT];
+    T v[R];
+    T dv[R][KT];
 #pragma unroll
-      for (int k = 0; k < KT; ++k) dv[k] = T(0);
-      for (uint32_t base = pb; base < pe; base += 64u) {
-        uint4 cw = make_uint4(0u, 0u, 0u, 0u);
-        if (base + lane < pe) cw = sr_load_window(a.code, base + lane);
-        const uint32_t n_here = __builtin_amdgcn_readfirstlane((pe - base < 64u) ? pe - base : 64u);
-        for (uint32_t k = 0; k < n_here; ++k) {
-          const uint32_t opc = uint32_t(__builtin_amdgcn_readlane(int(cw.x), int(k)));
-          const uint32_t meta = uint32_t(__builtin_amdgcn_readlane(int(cw.y), int(k)));
-          const uint32_t idx = meta & SR_M_INDEX;  // feature / stack slot / constant slot
-          // operand (value + tangents): feature / stack slot / constant
-          T ov = T(0);
-          T od[KT];
+    for (int j = 0; j < R; ++j) {
+      v[j] = T(0);
 #pragma unroll
-          for (int q = 0; q < KT; ++q) od[q] = T(0);
-          uint32_t variant = 6u;
-          if (opc >= SR_OP_BINARY0) variant = (opc - SR_OP_BINARY0) % 6u;
-          const bool load = opc <= SR_OP_LOAD_CONST_PUSH;
-          const bool load_feat = opc == SR_OP_LOAD_FEAT || opc == SR_OP_LOAD_FEAT_PUSH;
-          if ((load && load_feat) || variant == SR_V_FL || variant == SR_V_FR) {
-            ov = xs[idx * ROWS + r];
-          } else if (load || variant == SR_V_CL || variant == SR_V_CR) {
-            // constant slot idx: value from the tree's constant array, tangent e_{idx-k0}
-            ov = idx < 64u ? sr_readlane_val<T>(cval0, idx) : sr_readlane_val<T>(cval1, idx - 64u);
-            const int jj = int(idx) - int(k0);
+      for (int q = 0; q < KT; ++q) dv[j][q] = T(0);
+    }
+    for (uint32_t base = pb; base < pe; base += 64u) {
+      uint4 cw = make_uint4(0u, 0u, 0u, 0u);
+      if (base + lane < pe) cw = sr_load_window(a.code, base + lane);
+      const uint32_t n_here = __builtin_amdgcn_readfirstlane((pe - base < 64u) ? pe - base : 64u);
+      for (uint32_t k = 0; k < n_here; ++k) {
+        const uint32_t opc = uint32_t(__builtin_amdgcn_readlane(int(cw.x), int(k)));
+        const uint32_t meta = uint32_t(__builtin_amdgcn_readlane(int(cw.y), int(k)));
+        const uint32_t idx = meta & SR_M_INDEX;  // feature / stack slot / constant slot
+        uint32_t variant = 6u;
+        if (opc >= SR_OP_BINARY0) variant = (opc - SR_OP_BINARY0) % 6u;
+        const bool load = opc <= SR_OP_LOAD_CONST_PUSH;
+        const bool from_feat = (load && (opc == SR_OP_LOAD_FEAT || opc == SR_OP_LOAD_FEAT_PUSH)) ||
+                               variant == SR_V_FL || variant == SR_V_FR;
+        const bool from_stack = variant == SR_V_SL || variant == SR_V_SR;
+        // a constant operand: its value (wave-uniform) and its one-hot tangent e_{idx-k0}
+        T cv = T(0);
+        const int jj = int(idx) - int(k0);
+        if (!from_feat && !from_stack)
+          cv = idx < 64u ? sr_readlane_val<T>(cval0, idx) : sr_readlane_val<T>(cval1, idx - 64u);
+        const T* xrow = xs + size_t(idx) * ROWS + lane;
+        const T* sp = my_stk + size_t(idx) * NV * R * 64;
+        if (load) {
+          if (opc >= SR_OP_LOAD_FEAT_PUSH) {
+            T* pp = my_stk + size_t(((meta >> SR_M_PUSH_SHIFT) & 0x3fu) - 1u) * NV * R * 64;
 #pragma unroll
-            for (int q = 0; q < KT; ++q) od[q] = (q == jj) ? T(1) : T(0);
-          } else if (variant == SR_V_SL || variant == SR_V_SR) {
-            const T* sp = my_stk + size_t(idx) * NV * 64;
-            ov = sp[0];
+            for (int j = 0; j < R; ++j) {
+              pp[j * 64] = v[j];
 #pragma unroll
-            for (int q = 0; q < KT; ++q) od[q] = sp[(q + 1) * 64];
-          }
-          if (load) {
-            if (opc >= SR_OP_LOAD_FEAT_PUSH) {
-              T* sp = my_stk + size_t(((meta >> SR_M_PUSH_SHIFT) & 0x3fu) - 1u) * NV * 64;
-              sp[0] = v;
-#pragma unroll
-              for (int q = 0; q < KT; ++q) sp[(q + 1) * 64] = dv[q];
+              for (int q = 0; q < KT; ++q) pp[((q + 1) * R + j) * 64] = dv[j][q];
             }
-            v = ov;
+          }
 #pragma unroll
-            for (int q = 0; q < KT; ++q) dv[q] = od[q];
-          } else if (opc < SR_OP_BINARY0) {
-            const uint32_t u = opc >= SR_OP_UNARY_INF0 ? opc - SR_OP_UNARY_INF0 : opc - SR_OP_UNARY0;
-            const T x = v;
+          for (int j = 0; j < R; ++j) {
+            v[j] = from_feat ? xrow[j * 64] : cv;
+#pragma unroll
+            for (int q = 0; q < KT; ++q) dv[j][q] = (!from_feat && q == jj) ? T(1) : T(0);
+          }
+        } else if (opc < SR_OP_BINARY0) {
+          const uint32_t u = opc >= SR_OP_UNARY_INF0 ? opc - SR_OP_UNARY_INF0 : opc - SR_OP_UNARY0;
+#pragma unroll
+          for (int j = 0; j < R; ++j) {
+            const T x = v[j];
             const T yv = sr_unary<T>(u, x);
             // (fused unaries: complete trees have finite inner values, so INFSUB never fires)
             const T dfx = sr_unary_deriv<T>(u, x, yv);
-            v = yv;
+            v[j] = yv;
 #pragma unroll
-            for (int q = 0; q < KT; ++q) dv[q] = dfx * dv[q];
-          } else {
-            const uint32_t b = (opc - SR_OP_BINARY0) / 6u + 1u;
-            const bool left = variant == SR_V_SL || variant == SR_V_FL || variant == SR_V_CL;
-            const T av = left ? ov : v, bv = left ? v : ov;
+            for (int q = 0; q < KT; ++q) dv[j][q] = dfx * dv[j][q];
+          }
+        } else {
+          const uint32_t b = (opc - SR_OP_BINARY0) / 6u + 1u;
+          const bool left = variant == SR_V_SL || variant == SR_V_FL || variant == SR_V_CL;
+#pragma unroll
+          for (int j = 0; j < R; ++j) {
+            // operand (value + tangents) of row j: feature / stack slot / constant
+            T ov, od[KT];
+            if (from_feat) {
+              ov = xrow[j * 64];
+#pragma unroll
+              for (int q = 0; q < KT; ++q) od[q] = T(0);
+            } else if (from_stack) {
+              ov = sp[j * 64];
+#pragma unroll
+              for (int q = 0; q < KT; ++q) od[q] = sp[((q + 1) * R + j) * 64];
+            } else {
+              ov = cv;
+#pragma unroll
+              for (int q = 0; q < KT; ++q) od[q] = q == jj ? T(1) : T(0);
+            }
+            const T av = left ? ov : v[j], bv = left ? v[j] : ov;
             const T rv = sr_binary<T>(b, av, bv);
             T pa, pbv;
             sr_binary_partials<T>(b, av, bv, rv, &pa, &pbv);
-            v = rv;
+            v[j] = rv;
             if (left) {
 #pragma unroll
-              for (int q = 0; q < KT; ++q) dv[q] = __builtin_fma(pa, od[q], pbv * dv[q]);
+              for (int q = 0; q < KT; ++q) dv[j][q] = __builtin_fma(pa, od[q], pbv * dv[j][q]);
             } else {
 #pragma unroll
-              for (int q = 0; q < KT; ++q) dv[q] = __builtin_fma(pa, dv[q], pbv * od[q]);
+              for (int q = 0; q < KT; ++q) dv[j][q] = __builtin_fma(pa, dv[j][q], pbv * od[q]);
             }
           }
         }
       }
-      // d loss / d constant: (d loss / d pred) * d pred / d constant, padded rows excluded
-      T coef = sr_elem_loss_deriv<T>(a.loss_kind, v, ys[r], a.loss_param);
+    }
+    // d loss / d constant: (d loss / d pred) * d pred / d constant, padded rows excluded
+#pragma unroll
+    for (int j = 0; j < R; ++j) {
+      const int r = j * 64 + lane;
+      T coef = sr_elem_loss_deriv<T>(a.loss_kind, v[j], ys[r], a.loss_param);
       if (weighted) coef *= wsv[r];
       if (row0 + r >= a.n_rows) coef = T(0);
 #pragma unroll
-      for (int q = 0; q < KT; ++q) acc[q] = __builtin_fma(double(coef), double(dv[q]), acc[q]);
+      for (int q = 0; q < KT; ++q) acc[q] = __builtin_fma(double(coef), double(dv[j][q]), acc[q]);
     }
   }
   if (!active) return;
@@ -185,10 +214,17 @@ __global__ void __launch_bounds__(W * 64) sr_grad_kernel(const SrGradArgs<T> a) 
   }
 }
 
+// LDS of one workgroup: the X / y / w tile and the waves' operand stacks (value + tangents per row)
+template <typename T, int KT, int W>
+size_t sr_grad_lds(int nf, bool weighted, int stack_depth) {
+  constexpr int R = SrGradRows<KT>::value;
+  return (size_t(nf) + 1 + (weighted ? 1 : 0)) * 64 * R * sizeof(T) +
+         size_t(W) * size_t(stack_depth) * (1 + KT) * R * 64 * sizeof(T);
+}
+
 template <typename T, int KT, int W, bool GATHER>
 hipError_t sr_launch_grad(const SrGradArgs<T>& a, int n_blocks, hipStream_t s) {
-  const size_t lds = (size_t(a.nf) + 1 + (a.w ? 1 : 0)) * 256 * sizeof(T) +
-                     size_t(W) * a.stack_depth * (1 + KT) * 64 * sizeof(T);
+  const size_t lds = sr_grad_lds<T, KT, W>(a.nf, a.w != nullptr, a.stack_depth);
   const void* fn = reinterpret_cast<const void*>(&sr_grad_kernel<T, KT, W, GATHER>);
   if (lds > 65536) {
     const hipError_t e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, int(lds));
@@ -198,12 +234,17 @@ hipError_t sr_launch_grad(const SrGradArgs<T>& a, int n_blocks, hipStream_t s) {
   return hipGetLastError();
 }
 
-// Σ over row blocks (fixed order) of the [row block][item][KT] partials -> out[item][KT].
+// Σ over row blocks of the [row block][item][KT] partials -> out[item][KT], one wave per value: lane
+// l folds row blocks l, l + 64, ... in order and a fixed butterfly adds the lanes (deterministic; a
+// thread per value walking ~160 row blocks serially took 46 us per launch in C3's searches).
 __global__ void __launch_bounds__(256) sr_grad_reduce_kernel(const double* __restrict__ part, int n_row_blocks,
                                                               int n_vals, double* __restrict__ out) {
-  const int i = int(int64_t(blockIdx.x) * blockDim.x + threadIdx.x);
-  if (i >= n_vals) return;
+  const int lane = int(threadIdx.x) & 63;
+  const int i = int(int64_t(blockIdx.x) * (blockDim.x / 64) + threadIdx.x / 64);
+  if (i >= n_vals) return;  // wave-uniform
   double s = 0.0;
-  for (int b = 0; b < n_row_blocks; ++b) s += part[size_t(b) * n_vals + i];
-  out[i] = s;
+  for (int b = lane; b < n_row_blocks; b += 64) s += part[size_t(b) * n_vals + i];
+#pragma unroll
+  for (int off = 32; off >= 1; off >>= 1) s += __shfl_xor(s, off, 64);
+  if (lane == 0) out[i] = s;
 }
