@@ -524,11 +524,19 @@ def search_lines(args):
     X3 = rng.uniform(0.5, 2.0, (5, 100_000)).astype(np.float32)
     y3 = (X3[0] * X3[1] * X3[2] / (X3[3] * X3[4] ** 2 + 1)).astype(np.float32)
     o3 = Options(binary_operators=["+", "-", "*", "/"], unary_operators=["cos", "exp", "log"], populations=31)
+    # C5: the C3 data in Float64, constant optimisation on (BFGS / Newton with the device's forward-mode
+    # gradients; it is on by default, optimizer_probability 0.14), populations a multiple of 8
+    X5, y5 = X3.astype(np.float64), y3.astype(np.float64)
+    o5 = Options(binary_operators=["+", "-", "*", "/"], unary_operators=["cos", "exp", "log"], populations=32,
+                 should_optimize_constants=True)
     for name, X, y, o, cpu_iters, cpu_threads, desc in (
             ("c1", X1, y1, o1, args.search_cpu_iters or args.search_iters, 1,
              "C1 README example: X=randn(2,100) f64, ops + * / - cos exp, 20 populations, default options"),
             ("c3", X3, y3, o3, args.search_cpu_iters or 2, threads,
-             "C3: y = x1 x2 x3 / (x4 x5^2 + 1), X ~ U(0.5, 2) 5 x 100k f32, 31 populations, default options")):
+             "C3: y = x1 x2 x3 / (x4 x5^2 + 1), X ~ U(0.5, 2) 5 x 100k f32, 31 populations, default options"),
+            ("c5", X5, y5, o5, args.search_cpu_iters or 1, threads,
+             "C5: the C3 data in f64, constant optimisation (BFGS / Newton, device forward-mode gradients), "
+             "32 populations, default options")):
         t0 = time.perf_counter()
         res = equation_search(X, y, niterations=args.search_iters, options=o, seed=0)
         wall = time.perf_counter() - t0

@@ -1383,13 +1383,16 @@ int eval_grad_impl(sr_ctx* ctx, const sr_dataset* ds, int opset_id, const sr_tre
   T* g = static_cast<T*>(out_grad);
   std::fill(g, g + consts.size(), T(0));
   // work items per tangent width: (tree, first constant)
-  std::vector<uint32_t> items[3], k0s[3];
-  const int kts[3] = {4, 8, 16};
+  // tangent buckets: a tree runs with the narrowest width that holds its constants (1, 2, 4, 8; more
+  // than 8: passes of 16), so a one-constant tree carries one tangent, not four
+  constexpr int kNB = 5;
+  std::vector<uint32_t> items[kNB], k0s[kNB];
+  const int kts[kNB] = {1, 2, 4, 8, 16};
   for (int64_t t = 0; t < nt; ++t) {
     const uint32_t nc = prog.n_consts[size_t(t)];
     if (nc == 0 || !out_complete[t]) continue;
     if (nc > 128) return set_error(SR_ERR_TOO_DEEP, "more than 128 constants in one tree");
-    const int b = nc <= 4 ? 0 : (nc <= 8 ? 1 : 2);
+    const int b = nc <= 1 ? 0 : (nc <= 2 ? 1 : (nc <= 4 ? 2 : (nc <= 8 ? 3 : 4)));
     for (uint32_t k0 = 0; k0 < nc; k0 += uint32_t(kts[b])) {
       items[b].push_back(uint32_t(t));
       k0s[b].push_back(k0);
@@ -1406,9 +1409,9 @@ int eval_grad_impl(sr_ctx* ctx, const sr_dataset* ds, int opset_id, const sr_tre
   const size_t o_offs = al(o_code + prog.code.size() * sizeof(SrIns<T>));
   const size_t o_cons = al(o_offs + prog.offsets.size() * sizeof(uint32_t));
   const size_t o_coff = al(o_cons + consts.size() * sizeof(T));
-  size_t o_items[3], o_vals[3];
+  size_t o_items[kNB], o_vals[kNB];
   size_t at = al(o_coff + prog.const_off.size() * sizeof(uint32_t)), n_vals_all = 0;
-  for (int b = 0; b < 3; ++b) {
+  for (int b = 0; b < kNB; ++b) {
     o_items[b] = at;
     at = al(at + 2 * items[b].size() * sizeof(uint32_t));
     o_vals[b] = n_vals_all;
@@ -1422,7 +1425,7 @@ int eval_grad_impl(sr_ctx* ctx, const sr_dataset* ds, int opset_id, const sr_tre
   std::memcpy(hs + o_offs, prog.offsets.data(), prog.offsets.size() * sizeof(uint32_t));
   if (!consts.empty()) std::memcpy(hs + o_cons, consts.data(), consts.size() * sizeof(T));
   std::memcpy(hs + o_coff, prog.const_off.data(), prog.const_off.size() * sizeof(uint32_t));
-  for (int b = 0; b < 3; ++b) {
+  for (int b = 0; b < kNB; ++b) {
     uint32_t* d = reinterpret_cast<uint32_t*>(hs + o_items[b]);
     std::copy(items[b].begin(), items[b].end(), d);
     std::copy(k0s[b].begin(), k0s[b].end(), d + items[b].size());
@@ -1434,8 +1437,8 @@ int eval_grad_impl(sr_ctx* ctx, const sr_dataset* ds, int opset_id, const sr_tre
   constexpr int kWaves = 4;
   size_t part_need = 0;
   struct Launch { int64_t n_rb, tiles_per_block, n_groups; };
-  Launch lc[3] = {};
-  for (int b = 0; b < 3; ++b) {
+  Launch lc[kNB] = {};
+  for (int b = 0; b < kNB; ++b) {
     const int64_t ni = int64_t(items[b].size());
     if (ni == 0) continue;
     const int kt = kts[b];
@@ -1456,7 +1459,7 @@ int eval_grad_impl(sr_ctx* ctx, const sr_dataset* ds, int opset_id, const sr_tre
   }
   // (buckets run one after another on the stream, so they share the partials buffer)
   SR_HIP_CHECK(ctx->g_part.ensure(part_need * sizeof(double) + 16));
-  for (int b = 0; b < 3; ++b) {
+  for (int b = 0; b < kNB; ++b) {
     const int64_t ni = int64_t(items[b].size());
     if (ni == 0) continue;
     const int kt = kts[b];
@@ -1488,7 +1491,7 @@ int eval_grad_impl(sr_ctx* ctx, const sr_dataset* ds, int opset_id, const sr_tre
   double* out = ctx->h_grad.as<double>();  // (the staging image is no longer needed: the upload is done)
   SR_HIP_CHECK(hipMemcpyAsync(out, ctx->g_out.p, n_vals_all * sizeof(double), hipMemcpyDeviceToHost, s));
   SR_HIP_CHECK(hipStreamSynchronize(s));
-  for (int b = 0; b < 3; ++b) {
+  for (int b = 0; b < kNB; ++b) {
     const int kt = kts[b];
     for (size_t i = 0; i < items[b].size(); ++i) {
       const uint32_t t = items[b][i], k0 = k0s[b][i];

@@ -40,7 +40,8 @@ __device__ __forceinline__ T sr_readlane_val(T v, uint32_t l) {
   }
 }
 
-// Rows per lane by tangent width: the value and its KT tangents of R rows stay in VGPRs, so one
+// Rows per lane by tangent width (8 for 1-2 tangents, 4 for 4, 2 for 8, 1 for 16): the value and its
+// KT tangents of R rows stay in VGPRs, so one
 // dispatch of an instruction covers R x 64 rows (round 3: one row per lane made every dispatch and
 // operand decode cover 64 rows only; C3's gradient launches 0.61 ms each).
 template <int KT>
