@@ -1,0 +1,7 @@
+#!/bin/bash
+set -o pipefail
+cd $GRAFT_REPO_ROOT
+mkdir -p gpurun_out/exp15
+timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > gpurun_out/exp15/pytest_gpu.log 2>&1 || exit $?
+bash tools/ab_libs.sh "C2 cos arith" - trackall || exit $?
+cp gpurun_out/ab_libs.txt gpurun_out/exp15/ab_track.txt
