@@ -228,8 +228,25 @@ def main():
 
     comm = Comm(world, rank)
     ctx = sr_amd.get_context(local_rank)
-    init_device_comm(ctx=ctx)
-    cinfo = comm_info(ctx)
+    # the library's RCCL communicator (every data-path exchange of the sharded calls); if it cannot be
+    # created on every rank, all ranks fall back to exchanging the same partials over gloo (host
+    # copies) and the line says so, rather than printing nothing
+    err = None
+    try:
+        init_device_comm(ctx=ctx)
+    except Exception as e:  # noqa: BLE001  (reported in the JSON line)
+        if world == 1:
+            raise
+        err = f"{type(e).__name__}: {e}"
+    if world > 1 and comm.max(1.0 if err else 0.0) > 0.0:
+        if ctx.has_comm:
+            from sr_amd.distributed import destroy_device_comm
+            destroy_device_comm(ctx)
+        print(f"[bench] rank {rank}: RCCL communicator unavailable ({err or 'failed on a peer rank'}); "
+              "the sharded calls exchange over gloo", file=sys.stderr, flush=True)
+        cinfo = {"nranks": None, "rccl_error": err or "failed on a peer rank"}
+    else:
+        cinfo = comm_info(ctx)
 
     opts = Options(**C2_OPS)
     nt = args.trees or 10_000
@@ -294,6 +311,7 @@ def main():
             "unit": "node-evals/s",
             "n_gpus": world,
             "world_size_rccl": cinfo["nranks"],
+            **({"rccl_error": cinfo["rccl_error"]} if cinfo.get("rccl_error") else {}),
             "steps": args.steps,
             "warmup": args.warmup,
             "ms_per_step": dt / args.steps * 1e3,
