@@ -68,3 +68,24 @@ def test_callback_optimiser_reaches_known_optima():
         np.testing.assert_allclose(c0, want, rtol=1e-3)
         again = optimize_constants_callbacks(tb, lossf, gradf, seed=11)
         assert np.array_equal(again[1], loss) and np.array_equal(again[0].val, out.val)
+
+
+def test_callback_optimiser_items_independent_of_batch():
+    """The batched optimiser runs every (tree, start) item on its own values: without
+    restarts (no random draws), each tree's constants, loss and f_calls are the same optimised alone
+    or in one batch with BFGS and Newton members of other shapes."""
+    rng = np.random.default_rng(5)
+    X = rng.uniform(0.5, 2.0, (3, 400))
+    y = 2.5 * X[0] * X[1] / (X[2] + 0.75)
+    opts = Options(**OPS)
+    lossf, gradf = _scorers(opts, X, y)
+    exprs = ["1.9 * x1 * x2 / (x3 + 0.5)", "1.3 * x1 * x2 / x3", "cos(x1 * 0.7) + x2 * 1.1",
+             "x1 * x2 / (x3 * 0.5 + 0.2)", "exp(x3 * -0.3) * 2.0"]
+    trees = [parse_expression(e, opts) for e in exprs]
+    tb = flatten_trees(trees, np.float64)
+    out, loss, improved, f_calls = optimize_constants_callbacks(tb, lossf, gradf, nrestarts=0)
+    for k, t in enumerate(trees):
+        one = flatten_trees([t], np.float64)
+        o1, l1, i1, f1 = optimize_constants_callbacks(one, lossf, gradf, nrestarts=0)
+        assert l1[0] == loss[k] and i1[0] == improved[k] and f1[0] == f_calls[k], exprs[k]
+        assert np.array_equal(o1.val, out.val[out.offsets[k]:out.offsets[k + 1]]), exprs[k]
