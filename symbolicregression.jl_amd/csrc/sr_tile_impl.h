@@ -423,18 +423,6 @@ __device__ __forceinline__ void sr_unary_rows(T (&v)[R]) {
 // the same row bodies as the UNARY opcodes; INF = DynamicExpressions' fused form (non-finite input ->
 // +Inf), which only the per-node-check kernels distinguish (under deferred checks the input is a
 // tracked operator output, so a non-finite input already decides the tree).
-// Unary outputs the deferred checks need not track: cos / sin are bounded by 1, log of a finite
-// positive value by 104 in magnitude, sqrt by max(x, 1), neg / abs keep |x|; a non-finite or huge
-// output needs a non-finite or huge input, and every input is itself tracked (operator outputs,
-// checked feature loads when the data needs it, derived columns), so the tree is already marked.
-// (NaN is decided at the root: BASIC operators propagate it.)  Off by default (A/B: SR_UNTRACKED_UNARY=1).
-#ifndef SR_UNTRACKED_UNARY
-#define SR_UNTRACKED_UNARY 0
-#endif
-__host__ __device__ constexpr bool sr_unary_keeps_bound(uint32_t u) {
-  return SR_UNTRACKED_UNARY && (u == SR_U_COS || u == SR_U_SIN || u == SR_U_LOG || u == SR_U_SQRT ||
-                                u == SR_U_NEG || u == SR_U_ABS);
-}
 #define SR_POST_CASE(ID) \
   case ID:               \
     sr_unary_rows<T, ID, R>(tos); \
@@ -523,9 +511,7 @@ __device__ __forceinline__ void sr_post_unary(uint32_t u, bool inf, T (&tos)[R])
   case SR_OP_UNARY0 + ID: {                                         \
     if (ENABLED) {                                                  \
       sr_unary_rows<T, ID, R>(tos);                                 \
-      if constexpr (!sr_unary_keeps_bound(ID)) {                    \
-        SR_TRACK();                                                 \
-      }                                                             \
+      SR_TRACK();                                                   \
     }                                                               \
     break;                                                          \
   }
@@ -1097,9 +1083,7 @@ __global__ void __launch_bounds__(W * 64, (SrMinWavesFor<T, R, TIER, W, VSTK>::v
           const uint32_t post = (op >> SR_OP_POST_SHIFT) & 0x3fu;
           if (post != 0u && !dead) {
             sr_post_unary<T, R, TIER, FAST_CHECK>(post, (op & SR_OP_POST_INF) != 0u, tos);
-            if (!sr_unary_keeps_bound(post)) {
-              SR_TRACK();
-            }
+            SR_TRACK();
             if (!FAST_CHECK && (op & SR_OP_POST_CHECK)) {
               SR_CHECK_NODE();
             }
