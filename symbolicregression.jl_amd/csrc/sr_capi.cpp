@@ -475,9 +475,12 @@ int run_batch(sr_ctx* ctx, const sr_dataset* ds, int opset_id, const sr_tree_bat
   if (use_hint) {
     // epoch-tagged hints: each call marks dead positions with its own epoch, so the array needs a
     // reset only when (re)allocated or when the epoch counter wraps
-    void* const before = ctx->hint.p;
+    // (a reallocation is detected by the capacity, not the address: the allocator may hand back the
+    // freed address for the larger buffer, whose new part then holds stale words — possibly equal to
+    // this call's epoch, which would mark live trees dead)
+    const size_t cap_before = ctx->hint.cap;
     SR_HIP_CHECK(ctx->hint.ensure(size_t(nt) * sizeof(uint32_t) + 4));
-    if (ctx->hint.p != before || ctx->hint_epoch == 0xffffffffu) {
+    if (ctx->hint.cap != cap_before || ctx->hint_epoch == 0xffffffffu) {
       SR_HIP_CHECK(hipMemsetAsync(ctx->hint.p, 0, ctx->hint.cap, s));
       ctx->hint_epoch = 0;
     }
@@ -1442,7 +1445,7 @@ int eval_grad_impl(sr_ctx* ctx, const sr_dataset* ds, int opset_id, const sr_tre
     const int64_t ni = int64_t(items[b].size());
     if (ni == 0) continue;
     const int kt = kts[b];
-    const int64_t rows_per_tile = 64 * int64_t(sr_grad_rows_per_lane(kt));
+    const int64_t rows_per_tile = 64 * int64_t(sr_grad_rows_per_lane(kt, int(sizeof(T))));
     const int64_t n_tiles = (n_eval + rows_per_tile - 1) / rows_per_tile;
     const int64_t n_groups = (ni + kWaves - 1) / kWaves;
     int64_t n_rb = (4096 + n_groups - 1) / n_groups;

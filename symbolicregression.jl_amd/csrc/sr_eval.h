@@ -141,5 +141,9 @@ struct SrGradArgs {
 template <typename T>
 hipError_t sr_launch_grad_any(const SrGradArgs<T>& a, int kt, bool gather, int n_blocks, hipStream_t s);
 // Rows per lane of the gradient kernel for KT tangents (a staged tile is 64 x that many rows).
-constexpr int sr_grad_rows_per_lane(int kt) { return kt <= 2 ? 8 : (kt <= 4 ? 4 : (kt <= 8 ? 2 : 1)); }
+// (the same for Float64: halving its rows, to bring its ~230-256 VGPRs down, changed the gradient
+// sums' row-block order and with it chaotic C5 optimiser trajectories; not kept)
+constexpr int sr_grad_rows_per_lane(int kt, int elem_size = 4) {
+  return (void)elem_size, kt <= 2 ? 8 : (kt <= 4 ? 4 : (kt <= 8 ? 2 : 1));
+}
 hipError_t sr_launch_grad_reduce(const double* part, int n_row_blocks, int n_vals, double* out, hipStream_t s);

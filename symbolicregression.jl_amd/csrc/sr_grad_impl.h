@@ -23,6 +23,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <type_traits>
+
 #include "sr_eval.h"
 #include "sr_ops.h"
 #include "sr_tile_impl.h"
@@ -44,14 +46,14 @@ __device__ __forceinline__ T sr_readlane_val(T v, uint32_t l) {
 // KT tangents of R rows stay in VGPRs, so one
 // dispatch of an instruction covers R x 64 rows (round 3: one row per lane made every dispatch and
 // operand decode cover 64 rows only; C3's gradient launches 0.61 ms each).
-template <int KT>
+template <typename T, int KT>
 struct SrGradRows {
-  static constexpr int value = sr_grad_rows_per_lane(KT);
+  static constexpr int value = sr_grad_rows_per_lane(KT, int(sizeof(T)));
 };
 
 template <typename T, int KT, int W, bool GATHER>
 __global__ void __launch_bounds__(W * 64) sr_grad_kernel(const SrGradArgs<T> a) {
-  constexpr int R = SrGradRows<KT>::value;  // rows per lane: lane + 64 j, j < R
+  constexpr int R = SrGradRows<T, KT>::value;  // rows per lane: lane + 64 j, j < R
   constexpr int ROWS = 64 * R;               // rows per staged tile
   constexpr int NV = 1 + KT;                 // value + tangents
   extern __shared__ __attribute__((aligned(16))) unsigned char sr_smem[];
@@ -150,48 +152,73 @@ __global__ void __launch_bounds__(W * 64) sr_grad_kernel(const SrGradArgs<T> a) 
           }
         } else if (opc < SR_OP_BINARY0) {
           const uint32_t u = opc >= SR_OP_UNARY_INF0 ? opc - SR_OP_UNARY_INF0 : opc - SR_OP_UNARY0;
+          // the operator chosen once per instruction (a compile-time operator inside the row loop),
+          // not once per row; operators outside the BASIC set take the generic loop
+          auto unary_rows = [&](auto op_c) {
+            constexpr uint32_t UID = decltype(op_c)::value;
+            const uint32_t uu = UID == 0xffffffffu ? u : UID;
 #pragma unroll
-          for (int j = 0; j < R; ++j) {
-            const T x = v[j];
-            const T yv = sr_unary<T>(u, x);
-            // (fused unaries: complete trees have finite inner values, so INFSUB never fires)
-            const T dfx = sr_unary_deriv<T>(u, x, yv);
-            v[j] = yv;
+            for (int j = 0; j < R; ++j) {
+              const T x = v[j];
+              const T yv = sr_unary<T>(uu, x);
+              // (fused unaries: complete trees have finite inner values, so INFSUB never fires)
+              const T dfx = sr_unary_deriv<T>(uu, x, yv);
+              v[j] = yv;
 #pragma unroll
-            for (int q = 0; q < KT; ++q) dv[j][q] = dfx * dv[j][q];
+              for (int q = 0; q < KT; ++q) dv[j][q] = dfx * dv[j][q];
+            }
+          };
+#define SR_GU(ID) \
+  case ID: unary_rows(std::integral_constant<uint32_t, ID>{}); break;
+          switch (u) {
+            SR_GU(SR_U_NEG) SR_GU(SR_U_SQUARE) SR_GU(SR_U_CUBE) SR_GU(SR_U_EXP) SR_GU(SR_U_COS)
+            SR_GU(SR_U_SIN) SR_GU(SR_U_LOG) SR_GU(SR_U_SQRT) SR_GU(SR_U_ABS)
+            default: unary_rows(std::integral_constant<uint32_t, 0xffffffffu>{}); break;
           }
+#undef SR_GU
         } else {
           const uint32_t b = (opc - SR_OP_BINARY0) / 6u + 1u;
           const bool left = variant == SR_V_SL || variant == SR_V_FL || variant == SR_V_CL;
+          auto binary_rows = [&](auto op_c) {
+            constexpr uint32_t BID = decltype(op_c)::value;
+            const uint32_t bb = BID == 0xffffffffu ? b : BID;
 #pragma unroll
-          for (int j = 0; j < R; ++j) {
-            // operand (value + tangents) of row j: feature / stack slot / constant
-            T ov, od[KT];
-            if (from_feat) {
-              ov = xrow[j * 64];
+            for (int j = 0; j < R; ++j) {
+              // operand (value + tangents) of row j: feature / stack slot / constant
+              T ov, od[KT];
+              if (from_feat) {
+                ov = xrow[j * 64];
 #pragma unroll
-              for (int q = 0; q < KT; ++q) od[q] = T(0);
-            } else if (from_stack) {
-              ov = sp[j * 64];
+                for (int q = 0; q < KT; ++q) od[q] = T(0);
+              } else if (from_stack) {
+                ov = sp[j * 64];
 #pragma unroll
-              for (int q = 0; q < KT; ++q) od[q] = sp[((q + 1) * R + j) * 64];
-            } else {
-              ov = cv;
+                for (int q = 0; q < KT; ++q) od[q] = sp[((q + 1) * R + j) * 64];
+              } else {
+                ov = cv;
 #pragma unroll
-              for (int q = 0; q < KT; ++q) od[q] = q == jj ? T(1) : T(0);
+                for (int q = 0; q < KT; ++q) od[q] = q == jj ? T(1) : T(0);
+              }
+              const T av = left ? ov : v[j], bv = left ? v[j] : ov;
+              const T rv = sr_binary<T>(bb, av, bv);
+              T pa, pbv;
+              sr_binary_partials<T>(bb, av, bv, rv, &pa, &pbv);
+              v[j] = rv;
+              if (left) {
+#pragma unroll
+                for (int q = 0; q < KT; ++q) dv[j][q] = __builtin_fma(pa, od[q], pbv * dv[j][q]);
+              } else {
+#pragma unroll
+                for (int q = 0; q < KT; ++q) dv[j][q] = __builtin_fma(pa, dv[j][q], pbv * od[q]);
+              }
             }
-            const T av = left ? ov : v[j], bv = left ? v[j] : ov;
-            const T rv = sr_binary<T>(b, av, bv);
-            T pa, pbv;
-            sr_binary_partials<T>(b, av, bv, rv, &pa, &pbv);
-            v[j] = rv;
-            if (left) {
-#pragma unroll
-              for (int q = 0; q < KT; ++q) dv[j][q] = __builtin_fma(pa, od[q], pbv * dv[j][q]);
-            } else {
-#pragma unroll
-              for (int q = 0; q < KT; ++q) dv[j][q] = __builtin_fma(pa, dv[j][q], pbv * od[q]);
-            }
+          };
+          switch (b) {
+            case SR_B_ADD: binary_rows(std::integral_constant<uint32_t, SR_B_ADD>{}); break;
+            case SR_B_SUB: binary_rows(std::integral_constant<uint32_t, SR_B_SUB>{}); break;
+            case SR_B_MUL: binary_rows(std::integral_constant<uint32_t, SR_B_MUL>{}); break;
+            case SR_B_DIV: binary_rows(std::integral_constant<uint32_t, SR_B_DIV>{}); break;
+            default: binary_rows(std::integral_constant<uint32_t, 0xffffffffu>{}); break;
           }
         }
       }
@@ -218,7 +245,7 @@ __global__ void __launch_bounds__(W * 64) sr_grad_kernel(const SrGradArgs<T> a) 
 // LDS of one workgroup: the X / y / w tile and the waves' operand stacks (value + tangents per row)
 template <typename T, int KT, int W>
 size_t sr_grad_lds(int nf, bool weighted, int stack_depth) {
-  constexpr int R = SrGradRows<KT>::value;
+  constexpr int R = SrGradRows<T, KT>::value;
   return (size_t(nf) + 1 + (weighted ? 1 : 0)) * 64 * R * sizeof(T) +
          size_t(W) * size_t(stack_depth) * (1 + KT) * R * 64 * sizeof(T);
 }
