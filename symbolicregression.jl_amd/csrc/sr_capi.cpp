@@ -172,16 +172,16 @@ struct sr_ctx {
   DevBuf stamps;  // latency-analysis builds: the last main launch's per-wave stamps (sr_debug_stamps)
   int64_t n_stamps = 0;
 #endif
-  int stress_probe = 1;
-  int code_cache = 1;
-  int first_chunk = 6;
+  int stress_probe = 1;  // SR_AMD_STRESS_PROBE: the probe runs the dataset's stress rows (below)
+  int code_cache = 1;    // SR_AMD_CODE_CACHE: LDS program cache of the register-stack launches
+  int first_chunk = 6;   // SR_AMD_FIRST_CHUNK: the two-chunk pipeline's first chunk is 1/first_chunk
   // RCCL communicator of the row-sharded path (sr_comm_init): the library's own RCCL over xGMI on
   // its own HIP runtime (torch's bundled runtime cannot share the GPU with this one in a process)
   ncclComm_t comm = nullptr;
   int comm_ranks = 0;
   int comm_rank = 0;
   uint64_t comm_gen = 0;  // process-unique id of the current communicator (shard layouts are cached per id)
-  DevBuf shard_buf;       // collectives of the sharded calls (shard layout, exact-pass folds, tree results)      // SR_AMD_FIRST_CHUNK: the two-chunk pipeline's first chunk is 1/first_chunk       // SR_AMD_CODE_CACHE: LDS program cache of the register-stack launches     // SR_AMD_STRESS_PROBE: the probe runs the dataset's stress rows (below)
+  DevBuf shard_buf;       // collectives of the sharded calls (shard layout, exact-pass folds, tree results)
   double last_eval_ms = 0.0, last_total_ms = 0.0;
   double last_busy_ms = 0.0;  // union of the last call's interpreter launch intervals (sr_last_phase_ms out[8])
   // the two above are read from the last call's events lazily, when asked for (sr_last_kernel_ms /
