@@ -269,7 +269,7 @@ def main():
 
         def call():
             out["loss"], out["comp"] = eval_loss_sharded(tb, ds, opts)
-        path = "row-sharded sr_eval_loss_sharded (one RCCL all-reduce of packed [4, n_trees] partials per step)"
+        path = "row-sharded sr_eval_loss_sharded (one RCCL all-reduce of packed [5, n_trees] partials per step)"
     dt, step_ms, kernel_ms = timed(lib_step(ctx, call, state), args.steps, args.warmup, comm.barrier)
     dt = comm.max(dt)
     comp = np.asarray(out["comp"]).astype(bool)
@@ -330,7 +330,7 @@ def main():
                 "rows_per_gpu": rows,
                 "rows_total": rows_total,
                 "nfeatures": 5,
-                "parallelism": (f"rows sharded x{world}; one RCCL all-reduce of packed [4, n_trees] per-tree partials"
+                "parallelism": (f"rows sharded x{world}; one RCCL all-reduce of packed [5, n_trees] per-tree partials"
                                 if world > 1 else "single GPU"),
                 "code_path": path,
                 "fraction_complete": float(np.mean(comp)),

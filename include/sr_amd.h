@@ -22,7 +22,7 @@
 extern "C" {
 #endif
 
-#define SR_AMD_VERSION 1
+#define SR_AMD_VERSION 2
 
 /* status codes */
 #define SR_OK 0
@@ -64,6 +64,8 @@ extern "C" {
 #define SR_FLAG_NONFINITE 1u /* some checked intermediate array holds NaN/Inf: complete = false */
 #define SR_FLAG_BIG 2u       /* some checked value is so large its array sum may overflow: exact check needed */
 #define SR_FLAG_STATIC 4u    /* tree is incomplete independent of X (constant checks, constant folding) */
+#define SR_FLAG_ELEMINF 8u   /* an elementwise loss, or the T sum of two, is +Inf: the reference's loss fold
+                                (LossFunctions' sequential sum in T, src/LossFunctions.jl:38-58) is +Inf */
 
 typedef struct sr_ctx sr_ctx;
 typedef struct sr_dataset sr_dataset;
@@ -147,8 +149,9 @@ int sr_eval_loss_partials(sr_ctx* ctx, const sr_dataset* ds, int opset_id, const
                           int64_t n_total, int loss_kind, double* out_sum, uint32_t* out_flags,
                           int out_on_device);
 /*
- * The same partials packed for ONE all-reduce (SUM): out[4][n_trees] f64 = Σ w·loss, then the
- * SR_FLAG_NONFINITE, SR_FLAG_BIG and SR_FLAG_STATIC bits as 0/1 (summed over ranks: > 0 means set).
+ * The same partials packed for ONE all-reduce (SUM): out[5][n_trees] f64 = Σ w·loss, then the
+ * SR_FLAG_NONFINITE, SR_FLAG_BIG, SR_FLAG_STATIC and SR_FLAG_ELEMINF bits as 0/1 (summed over ranks:
+ * > 0 means set).
  * out_on_device = 1: `out` is a device pointer on this context's GPU (no host round trip).
  */
 int sr_eval_loss_partials_packed(sr_ctx* ctx, const sr_dataset* ds, int opset_id, const sr_tree_batch* trees,
@@ -157,13 +160,22 @@ int sr_eval_loss_partials_packed(sr_ctx* ctx, const sr_dataset* ds, int opset_id
  * sr_comm_unique_id, the caller broadcasts the SR_COMM_ID_BYTES bytes (any CPU channel: MPI, a TCP
  * store, torch.distributed's gloo group), every rank calls sr_comm_init with them.
  * sr_eval_loss_partials_allreduce = sr_eval_loss_partials_packed on this shard, then ONE in-place
- * ncclAllReduce (sum) of the [4, n_trees] f64 buffer on the device over xGMI, then the global
+ * all-reduce (sum) of the [5, n_trees] f64 buffer on the device over xGMI, then the global
  * partials to out_host (what sr_finalize_losses / the exact path take).  Every rank must call it
  * with the same trees.  (Replaces the Julia-side Distributed reduction of the reference's
  * per-worker losses for one batched call.) */
 #define SR_COMM_ID_BYTES 128
 int sr_comm_unique_id(void* out_id);
 int sr_comm_init(sr_ctx* ctx, int nranks, int rank, const void* id_bytes);
+/* The same sharded calls over collectives the caller provides instead of RCCL (any transport: a gloo /
+ * MPI group on the host, a test harness; several ranks may then share one GPU).  Both callbacks are
+ * collective and return 0 on success: allreduce sums buf[n] over the ranks in place; allgather writes
+ * every rank's `bytes` send bytes into recv[nranks][bytes] in rank order.  The library calls them with
+ * host buffers, on the calling thread, in the same order on every rank. */
+typedef int (*sr_host_allreduce_fn)(void* user, double* buf, int64_t n);
+typedef int (*sr_host_allgather_fn)(void* user, const void* send, void* recv, int64_t bytes);
+int sr_comm_init_host(sr_ctx* ctx, int nranks, int rank, sr_host_allreduce_fn allreduce, sr_host_allgather_fn allgather,
+                      void* user);
 int sr_comm_destroy(sr_ctx* ctx);
 int sr_eval_loss_partials_allreduce(sr_ctx* ctx, const sr_dataset* ds, int opset_id, const sr_tree_batch* trees,
                                     int64_t n_total, int loss_kind, double* out_host);
@@ -171,9 +183,10 @@ int sr_eval_loss_partials_allreduce(sr_ctx* ctx, const sr_dataset* ds, int opset
  * The whole row-sharded step of batched eval_loss (SURVEY §8(e) row sharding, config C4) in one call:
  * rank r's `ds` holds global rows [Σ_{q<r} n_q, Σ_{q<=r} n_q) (shards in rank order; their sizes, Σw
  * and max|X| are exchanged over the communicator at the first call per dataset).  This shard runs
- * the single-GPU launch pipeline, the packed [4, n_trees] partials are summed by ONE in-place RCCL
- * all-reduce over xGMI, losses are finalized on the device (Σ / global n or Σw), and trees flagged BIG
- * get DynamicExpressions' exact isfinite(sum) verdict over the GLOBAL rows (leaf folds all-gathered).
+ * the single-GPU launch pipeline, the packed [5, n_trees] partials are summed by ONE in-place RCCL
+ * all-reduce over xGMI, losses are finalized on the device (Σ / global n or Σw), trees flagged BIG
+ * get DynamicExpressions' exact isfinite(sum) verdict over the GLOBAL rows (leaf folds all-gathered),
+ * and the rare trees whose T-precision loss fold may overflow are folded in row order across the shards.
  * out_loss / out_complete as sr_eval_loss_batch over the union of the shards, on every rank.
  * Collective: every rank calls it with the same trees.  A failure on one rank (HIP error, bad tree)
  * still enters the collectives with its error word set, and every rank then returns an error.
@@ -190,9 +203,9 @@ int sr_eval_loss_sharded(sr_ctx* ctx, const sr_dataset* ds, int opset_id, const 
  */
 int sr_eval_loss_tree_sharded(sr_ctx* ctx, const sr_dataset* ds, int opset_id, const sr_tree_batch* trees,
                               int loss_kind, void* out_loss, uint8_t* out_complete);
-/* The communicator's size and this rank as RCCL reports them (ncclCommCount / ncclCommUserRank; may be
- * NULL), and "hip=<file>;rccl=<file>": the HIP runtime and the RCCL this library's calls bind to
- * (`paths` may be NULL).  sr_comm_unique_id / sr_comm_init fail if the two come from different ROCm
+/* The communicator's size and this rank (as RCCL reports them: ncclCommCount / ncclCommUserRank; may be
+ * NULL), and "transport=rccl|host;hip=<file>;rccl=<file>": the transport and the HIP runtime and RCCL
+ * this library's calls bind to (`paths` may be NULL).  sr_comm_unique_id / sr_comm_init fail if the two come from different ROCm
  * trees (RCCL would then run this library's streams on another HIP runtime). */
 int sr_comm_info(sr_ctx* ctx, int* nranks, int* rank, char* paths, int64_t capacity);
 /* The same "hip=...;rccl=..." string without a context (no device needed). */
@@ -396,8 +409,10 @@ int sr_last_kernel_ms(sr_ctx* ctx, double* eval_ms, double* total_ms);
  * = the number of interpreter launches of the call (the batch is compiled and launched in chunks),
  * out[6] (n >= 7) = device time of the exact-sum pass (ms), out[7] (n >= 8) = rows per lane of its
  * interpreter kernel, out[8] (n >= 9) = the device-busy time of those launches: the UNION of their
- * intervals (launches on the two pipeline streams overlap, so their summed durations can exceed it).
- * sr_last_kernel_ms's eval_ms is the sum of those launches' durations. */
+ * intervals (launches on the two pipeline streams overlap, so their summed durations can exceed it),
+ * out[9] (n >= 10) = the number of trees whose loss fold was computed in row order (the overflow rule of
+ * the reference's T-precision fold: csrc/sr_fold.h).  sr_last_kernel_ms's eval_ms is the sum of those
+ * launches' durations. */
 int sr_last_phase_ms(sr_ctx* ctx, double* out, int n);
 
 /* Run-time tuning of a context (the SR_AMD_* environment variables are read once at sr_init):

@@ -452,13 +452,18 @@ int FN(oracle_eval_loss)(int64_t n_nodes, const uint8_t* degree, const uint8_t* 
     }
     *loss = w ? s / ws : s / (T)n;
   } else {
+    /* the value from an f64 accumulation (the device's arithmetic), the overflow verdict from the
+     * reference's own T fold (src/LossFunctions.jl:38-58: a fold that passes floatmax(T) is +Inf) */
     double s = 0.0, ws = 0.0;
+    T st = (T)0;
     for (int64_t j = 0; j < n; ++j) {
       T l = FN(elem_loss)(loss_kind, loss_param, pred[j], y[j]);
       if (w) { l = w[j] * l; ws += (double)w[j]; }
       s += (double)l;
+      st = j == 0 ? l : st + l;
     }
     *loss = (T)(w ? s / ws : s / (double)n);
+    if (st == (T)INFINITY) *loss = (T)INFINITY;
   }
   free(pred);
   return 1;

@@ -4,6 +4,7 @@
 #include <stdint.h>
 
 #include "sr_eval.h"
+#include "sr_fold.h"
 
 
 // One thread per launch position: Σ over row blocks in row-block order (bit-reproducible), OR of
@@ -82,8 +83,8 @@ template hipError_t sr_launch_jsum_levels<float>(const float*, int64_t, int, con
 template hipError_t sr_launch_jsum_levels<double>(const double*, int64_t, int, const int2*, int, const int32_t*, int,
                                                   double*, uint8_t*, hipStream_t);
 
-// Packed row-shard partials for one all-reduce (sr_eval_loss_partials_packed): [4][n] f64 = Σ loss,
-// then the NONFINITE / BIG / STATIC flag bits as 0 / 1.
+// Packed row-shard partials for one all-reduce (sr_eval_loss_partials_packed): [5][n] f64 = Σ loss,
+// then the NONFINITE / BIG / STATIC / ELEMINF flag bits as 0 / 1.
 __global__ void __launch_bounds__(256) sr_pack_partials_kernel(const double* __restrict__ sum,
                                                                 const uint32_t* __restrict__ flag, int n,
                                                                 double* __restrict__ out) {
@@ -94,6 +95,7 @@ __global__ void __launch_bounds__(256) sr_pack_partials_kernel(const double* __r
   out[size_t(n) + t] = (f & SR_FLAG_NONFINITE) ? 1.0 : 0.0;
   out[2 * size_t(n) + t] = (f & SR_FLAG_BIG) ? 1.0 : 0.0;
   out[3 * size_t(n) + t] = (f & SR_FLAG_STATIC) ? 1.0 : 0.0;
+  out[4 * size_t(n) + t] = (f & SR_FLAG_ELEMINF) ? 1.0 : 0.0;
 }
 
 hipError_t sr_launch_pack_partials(const double* sum, const uint32_t* flag, int n, double* out, hipStream_t s) {
@@ -102,33 +104,219 @@ hipError_t sr_launch_pack_partials(const double* sum, const uint32_t* flag, int 
   return hipGetLastError();
 }
 
-// Row-sharded finalize on the device (sr_eval_loss_sharded): the partials [4][n] summed over every
-// rank -> loss[t] = Σ / denom (f64 division, rounded once to T) or +Inf, and comp[t] = 1 complete,
-// 0 incomplete, 2 flagged BIG only (the exact Julia-order check over the global rows decides; its
-// loss slot holds the finite value).  The same rules as the host's finalize (sr_capi.cpp).
+// Row-sharded finalize on the device (sr_eval_loss_sharded): the partials [5][n] summed over every
+// rank -> loss[t] = Σ / denom (f64 division, rounded once to T) or +Inf, and comp[t] = 0 incomplete,
+// 1 complete, 2 flagged BIG only (the exact Julia-order check over the global rows decides; its loss
+// slot holds the finite value), plus SR_COMP_FOLD when the reference's loss fold over the n_terms global
+// rows must be computed in order (sr_fold.h).  The same rules as the host's finalize (sr_capi.cpp).
 template <typename T>
 __global__ void __launch_bounds__(256) sr_finalize_packed_kernel(const double* __restrict__ packed, int n,
-                                                                 double denom, T* __restrict__ loss,
+                                                                 double denom, int64_t n_terms, T* __restrict__ loss,
                                                                  uint8_t* __restrict__ comp) {
   const int t = int(int64_t(blockIdx.x) * blockDim.x + threadIdx.x);
   if (t >= n) return;
   const bool nonfinite = packed[size_t(n) + t] > 0.0;
   const bool big = packed[2 * size_t(n) + t] > 0.0;
   const bool stat = packed[3 * size_t(n) + t] > 0.0;
+  const bool elem_inf = packed[4 * size_t(n) + t] > 0.0;
   const bool ok = !nonfinite && !stat;
-  loss[t] = ok ? T(packed[t] / denom) : T(INFINITY);
-  comp[t] = ok ? (big ? uint8_t(2) : uint8_t(1)) : uint8_t(0);
+  T l = ok ? T(packed[t] / denom) : T(INFINITY);
+  uint8_t c = ok ? (big ? uint8_t(2) : uint8_t(1)) : uint8_t(0);
+  if (ok) {
+    const int cls = n_terms > 0 ? sr_fold_class<T>(packed[t], elem_inf, n_terms) : (elem_inf ? SR_FOLD_INF : SR_FOLD_FINITE);
+    if (cls == SR_FOLD_INF) l = T(INFINITY);
+    if (cls == SR_FOLD_EXACT) c |= uint8_t(SR_COMP_FOLD);
+  }
+  loss[t] = l;
+  comp[t] = c;
 }
 
 template <typename T>
-hipError_t sr_launch_finalize_packed(const double* packed, int n, double denom, T* loss, uint8_t* comp, hipStream_t s) {
+hipError_t sr_launch_finalize_packed(const double* packed, int n, double denom, int64_t n_terms, T* loss, uint8_t* comp,
+                                     hipStream_t s) {
   if (n <= 0) return hipSuccess;
   hipLaunchKernelGGL(sr_finalize_packed_kernel<T>, dim3(unsigned((n + 255) / 256)), dim3(256), 0, s, packed, n, denom,
-                     loss, comp);
+                     n_terms, loss, comp);
   return hipGetLastError();
 }
-template hipError_t sr_launch_finalize_packed<float>(const double*, int, double, float*, uint8_t*, hipStream_t);
-template hipError_t sr_launch_finalize_packed<double>(const double*, int, double, double*, uint8_t*, hipStream_t);
+template hipError_t sr_launch_finalize_packed<float>(const double*, int, double, int64_t, float*, uint8_t*, hipStream_t);
+template hipError_t sr_launch_finalize_packed<double>(const double*, int, double, int64_t, double*, uint8_t*, hipStream_t);
+
+// ---------------------------------------------------------------- the reference's loss fold, exactly
+// LossFunctions' mean / weighted sum fold the elementwise losses left to right in T
+// (src/LossFunctions.jl:38-58; sr_fold.h).  For the rare trees whose overflow the bounds of sr_fold.h
+// cannot decide, this kernel computes that fold bit for bit, in parallel: while the running value p
+// stays in one binade [2^e, 2^(e+1)), fl(p + l) = p + ulp * (m + r), where l / ulp = m + f (m integer)
+// and r rounds f half-to-even against the parity of p / ulp + m — so a step is a function of the
+// parity of the running value only, and chunks of steps compose (a scan over pairs: the increment from
+// an even and from an odd start).  The first step that would leave the binade is done with the
+// hardware add itself and the scan restarts there (p only grows: at most ~280 binades for Float32).
+// One workgroup per listed tree; pred[b][n] its predictions over the view; carry[b] (or NULL) the
+// value of the fold over the rows before this shard; out[b] = the fold (+Inf when it overflows).
+template <typename T>
+struct SrFoldStep {
+  int64_t m;
+  int kind;  // 0: f < 1/2, 1: f == 1/2 (tie), 2: f > 1/2
+};
+
+template <typename T>
+__device__ __forceinline__ SrFoldStep<T> sr_fold_step(T e, int q, int64_t cap) {
+  SrFoldStep<T> st{cap, 0};
+  const double t = ldexp(double(e), -q);  // exact: a power-of-two scaling of a T value
+  if (!(t < double(cap))) return st;      // (also NaN / Inf: a crossing, taken by the hardware add)
+  const double fl = floor(t);
+  const double f = t - fl;
+  st.m = int64_t(fl);
+  st.kind = f > 0.5 ? 2 : (f == 0.5 ? 1 : 0);
+  return st;
+}
+template <typename T>
+__device__ __forceinline__ int64_t sr_fold_inc(const SrFoldStep<T>& st, int64_t b) {
+  return st.m + (st.kind == 2 ? 1 : (st.kind == 1 ? ((b + st.m) & 1) : 0));
+}
+// (a0, a1): ulps added from an even / odd start; compose(x, y)(b) = x(b) + y((b + x(b)) & 1)
+__device__ __forceinline__ void sr_fold_compose(int64_t x0, int64_t x1, int64_t& y0, int64_t& y1, int64_t cap) {
+  const int64_t n0 = x0 + ((x0 & 1) ? y1 : y0);
+  const int64_t n1 = x1 + (((1 + x1) & 1) ? y1 : y0);
+  y0 = n0 < cap ? n0 : cap;
+  y1 = n1 < cap ? n1 : cap;
+}
+
+template <typename T, int R>
+__global__ void __launch_bounds__(1024) sr_fold_kernel(const T* __restrict__ pred, int64_t pred_ld,
+                                                       const T* __restrict__ y, const T* __restrict__ w,
+                                                       const int64_t* __restrict__ row_idx, int64_t n, int lk, T lp,
+                                                       const T* __restrict__ carry, T* __restrict__ out) {
+  using Tr = SrFoldTraits<T>;
+  constexpr int NT = 1024;
+  constexpr int64_t CHUNK = int64_t(NT) * R;
+  constexpr int64_t CAP = int64_t(1) << (Tr::mant + 3);
+  constexpr T MIN_NORMAL = sizeof(T) == 4 ? T(1.17549435e-38f) : T(2.2250738585072014e-308);
+  __shared__ T s_p;
+  __shared__ int64_t s_k;
+  __shared__ int64_t s_w0[NT / 64], s_w1[NT / 64];
+  const int tid = int(threadIdx.x), lane = tid & 63, wave = tid >> 6;
+  const T* pr = pred + int64_t(blockIdx.x) * pred_ld;
+  auto elem = [&](int64_t i) -> T {
+    const int64_t ri = row_idx ? row_idx[i] : i;
+    T e = sr_elem_loss<T>(lk, pr[i], y[ri], lp);
+    if (w) e *= w[ri];  // (the interpreter's product, in the same order)
+    return e;
+  };
+  if (tid == 0) {
+    if (carry) {
+      s_p = carry[blockIdx.x];
+      s_k = 0;
+    } else {  // Statistics.mean / Base.sum over a generator: the first loss starts the fold
+      s_p = n > 0 ? elem(0) : T(0);
+      s_k = 1;
+    }
+  }
+  for (;;) {
+    __syncthreads();
+    const T p = s_p;
+    const int64_t k = s_k;
+    __syncthreads();  // every thread has read the state before thread 0 may write it again
+    if (k >= n || !(p <= SrM<T>::big)) break;  // done, or +Inf / NaN (a fold that stays so)
+    // p = P 2^q, P < lim: the binade's spacing (subnormals: the fixed spacing up to the first normal)
+    int q;
+    int64_t lim;
+    if (p < MIN_NORMAL) {
+      q = Tr::qmin;
+      lim = int64_t(1) << Tr::mant;
+    } else {
+      int ex;
+      (void)frexp(double(p), &ex);
+      q = ex - 1 - Tr::mant;
+      lim = int64_t(1) << (Tr::mant + 1);
+    }
+    const int64_t P = int64_t(ldexp(double(p), -q));
+    // this thread's R consecutive losses and their composed step
+    const int64_t base = k + int64_t(tid) * R;
+    T ev[R];
+    int64_t a0 = 0, a1 = 0;
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+      ev[r] = (base + r < n) ? elem(base + r) : T(0);  // (a zero loss adds nothing)
+      const SrFoldStep<T> st = sr_fold_step<T>(ev[r], q, CAP);
+      int64_t e0 = sr_fold_inc<T>(st, (0 + a0) & 1), e1 = sr_fold_inc<T>(st, (1 + a1) & 1);
+      a0 = a0 + e0 < CAP ? a0 + e0 : CAP;
+      a1 = a1 + e1 < CAP ? a1 + e1 : CAP;
+    }
+    // inclusive scan over the wave's lanes (in row order), then over the waves
+    int64_t i0 = a0, i1 = a1;
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+      const int64_t l0 = __shfl_up(i0, off, 64), l1 = __shfl_up(i1, off, 64);
+      if (lane >= off) sr_fold_compose(l0, l1, i0, i1, CAP);
+    }
+    if (lane == 63) {
+      s_w0[wave] = i0;
+      s_w1[wave] = i1;
+    }
+    __syncthreads();
+    int64_t w0 = 0, w1 = 0;  // the waves before this one
+    for (int v = 0; v < wave; ++v) {
+      int64_t y0 = s_w0[v], y1 = s_w1[v];
+      sr_fold_compose(w0, w1, y0, y1, CAP);
+      w0 = y0;
+      w1 = y1;
+    }
+    int64_t t0 = 0, t1 = 0;  // the whole chunk
+    for (int v = 0; v < NT / 64; ++v) {
+      int64_t y0 = s_w0[v], y1 = s_w1[v];
+      sr_fold_compose(t0, t1, y0, y1, CAP);
+      t0 = y0;
+      t1 = y1;
+    }
+    const int64_t b0 = P & 1;
+    const int64_t tot = b0 ? t1 : t0;
+    if (P + tot < lim) {  // the whole chunk stays in this binade
+      if (tid == 0) {
+        s_p = T(ldexp(double(P + tot), q));
+        s_k = k + CHUNK < n ? k + CHUNK : n;
+      }
+      continue;
+    }
+    // the step leaving the binade: in the thread whose exclusive prefix is below lim and inclusive
+    // prefix is not (prefixes only grow, so exactly one thread)
+    int64_t e0 = __shfl_up(i0, 1, 64), e1 = __shfl_up(i1, 1, 64);
+    if (lane == 0) e0 = e1 = 0;
+    int64_t x0 = w0, x1 = w1;
+    sr_fold_compose(x0, x1, e0, e1, CAP);  // exclusive prefix of this thread
+    int64_t n0 = w0, n1 = w1, y0 = i0, y1 = i1;
+    sr_fold_compose(n0, n1, y0, y1, CAP);  // inclusive
+    const int64_t pre = P + (b0 ? e1 : e0), inc = P + (b0 ? y1 : y0);
+    if (pre < lim && inc >= lim) {
+      int64_t run = pre;
+#pragma unroll
+      for (int r = 0; r < R; ++r) {
+        if (base + r >= n) break;
+        const int64_t d = sr_fold_inc<T>(sr_fold_step<T>(ev[r], q, CAP), run & 1);
+        if (run + d >= lim) {
+          s_p = T(ldexp(double(run), q)) + ev[r];  // the hardware's own rounding of this step
+          s_k = base + r + 1;
+          break;
+        }
+        run += d;
+      }
+    }
+  }
+  if (tid == 0) out[blockIdx.x] = s_p;
+}
+
+template <typename T>
+hipError_t sr_launch_fold(const T* pred, int64_t pred_ld, int n_trees, const T* y, const T* w, const int64_t* row_idx,
+                          int64_t n, int loss_kind, T loss_param, const T* carry, T* out, hipStream_t s) {
+  if (n_trees <= 0) return hipSuccess;
+  hipLaunchKernelGGL((sr_fold_kernel<T, 8>), dim3(unsigned(n_trees)), dim3(1024), 0, s, pred, pred_ld, y, w, row_idx, n,
+                     loss_kind, loss_param, carry, out);
+  return hipGetLastError();
+}
+template hipError_t sr_launch_fold<float>(const float*, int64_t, int, const float*, const float*, const int64_t*, int64_t,
+                                          int, float, const float*, float*, hipStream_t);
+template hipError_t sr_launch_fold<double>(const double*, int64_t, int, const double*, const double*, const int64_t*,
+                                           int64_t, int, double, const double*, double*, hipStream_t);
 
 // Julia [nf, n] column-major -> per-feature rows [nf][ld]; padded rows replicate row 0 so that the
 // interpreter's validity checks never see a value that is not in the dataset.

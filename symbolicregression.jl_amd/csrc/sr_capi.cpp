@@ -19,6 +19,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <functional>
+#include <memory>
 #include <mutex>
 #include <string>
 #include <vector>
@@ -26,10 +27,12 @@
 #include "../../include/sr_amd.h"
 #include "sr_compile.h"
 #include "sr_eval.h"
+#include "sr_fold.h"
 
 namespace {
 
 thread_local std::string g_last_error;
+struct SrComm;  // the sharded calls' transport (multi-GPU section below)
 
 int set_error(int code, const std::string& msg) {
   g_last_error = msg;
@@ -132,6 +135,7 @@ struct sr_ctx {
   bool derived_last = false;  // the last run_batch launched derived columns (timed by ev_d0/ev_d1)
   int n_derived_last = 0;
   int64_t n_exact_last = 0;  // trees of the last eval_loss call sent through the exact-sum pass
+  int64_t n_fold_last = 0;   // trees of the last eval_loss call whose loss fold was computed in order (sr_fold.h)
   double exact_kernel_ms = 0.0;  // device time of that pass (its interpreter + combine launches)
   // programs + per-tree metadata of the last run_batch: ONE device allocation and ONE pinned staging
   // buffer with the same layout (code | offsets | static_bad | launch order), so a single-chunk call
@@ -167,7 +171,7 @@ struct sr_ctx {
   std::vector<std::pair<int, double>> losses;  // registered (kind, param); code = kLossCodeBase + index
   DevBuf prog, outs, part_sum, part_flag, pred, row_idx, tree_list,
       range_lo, range_hi, range_sums, packed, hint, jsum_prog, jsum_fin, jsum_scratch, probe_sum, probe_flag, g_code, g_offsets, g_consts, g_const_off, g_items, g_part, g_out,
-      derived_cols, probe_derived;
+      derived_cols, probe_derived, fold_io;
 #ifdef SR_STAMPS
   DevBuf stamps;  // latency-analysis builds: the last main launch's per-wave stamps (sr_debug_stamps)
   int64_t n_stamps = 0;
@@ -175,13 +179,18 @@ struct sr_ctx {
   int stress_probe = 1;  // SR_AMD_STRESS_PROBE: the probe runs the dataset's stress rows (below)
   int code_cache = 1;    // SR_AMD_CODE_CACHE: LDS program cache of the register-stack launches
   int first_chunk = 6;   // SR_AMD_FIRST_CHUNK: the two-chunk pipeline's first chunk is 1/first_chunk
-  // RCCL communicator of the row-sharded path (sr_comm_init): the library's own RCCL over xGMI on
-  // its own HIP runtime (torch's bundled runtime cannot share the GPU with this one in a process)
-  ncclComm_t comm = nullptr;
+  // data-path transport of the sharded calls: the library's own RCCL over xGMI on its own HIP runtime
+  // (sr_comm_init; torch's bundled runtime cannot share the GPU with this one in a process), or the
+  // caller's host collectives (sr_comm_init_host)
+  std::unique_ptr<SrComm> xport;
   int comm_ranks = 0;
   int comm_rank = 0;
   uint64_t comm_gen = 0;  // process-unique id of the current communicator (shard layouts are cached per id)
-  DevBuf shard_buf;       // collectives of the sharded calls (shard layout, exact-pass folds, tree results)
+  // buffers of the sharded calls' collectives only (their growth is identical on every rank: Prep):
+  // shard layout / exact-pass folds / loss-fold chain / tree results, the packed partials, the agree word
+  DevBuf coll_buf, coll_packed, ctl;
+  HostBuf h_coll;        // pinned staging of the tree-sharded results
+  int inject_fail = 0;   // tests (sr_set_tuning "inject_failure"): the next k collective-buffer growths fail
   double last_eval_ms = 0.0, last_total_ms = 0.0;
   double last_busy_ms = 0.0;  // union of the last call's interpreter launch intervals (sr_last_phase_ms out[8])
   // the two above are read from the last call's events lazily, when asked for (sr_last_kernel_ms /
@@ -218,6 +227,16 @@ struct sr_ctx {
   std::vector<uint32_t> perm_host;
 };
 
+// For the search engine (sr_search.cpp, not in the public header): set the context's "timing" knob
+// and return its previous value, under the context's lock (a caller's setting is restored after the
+// engine's calls).
+int sr_ctx_swap_timing(sr_ctx* ctx, int value) {
+  std::lock_guard<std::mutex> g(ctx->mu);
+  const int old = ctx->timing;
+  ctx->timing = value != 0 ? 1 : 0;
+  return old;
+}
+
 struct sr_dataset {
   sr_ctx* ctx = nullptr;
   int dtype = SR_DTYPE_F32;
@@ -227,6 +246,7 @@ struct sr_dataset {
   void* w = nullptr;  // [ld] or NULL
   std::vector<double> w_host;  // weights (for Σw of SubDataset views)
   double wsum = 0.0;
+  double w_min = 0.0;      // smallest weight (the loss-fold overflow rule needs w >= 0: sr_fold.h)
   double max_abs_x = 0.0;  // max |X| over the data (NaN / Inf if any value is non-finite)
   // dead-tree probe rows (large datasets): the "stress rows" — per feature the K largest, K smallest
   // and K smallest-magnitude values, where exp overflows, logs and divisions blow up — then rows 0, 1,
@@ -238,6 +258,7 @@ struct sr_dataset {
   mutable uint64_t shard_gen = 0;
   mutable std::vector<int64_t> shard_offs;
   mutable double shard_wsum = 0.0, shard_max_abs_x = 0.0;
+  mutable double shard_w_min = 0.0;  // smallest weight over every shard
   mutable int64_t shard_min_rows = 0;
 };
 
@@ -407,9 +428,14 @@ int run_batch(sr_ctx* ctx, const sr_dataset* ds, int opset_id, const sr_tree_bat
   // register-stack kernel (f32 BASIC loss over the full dataset): Rv rows per lane, used for every
   // chunk whose programs need <= 2 operand-stack slots (all trees of <= 30 nodes); other chunks run
   // the LDS-stack kernel at R rows per lane
-  const int Rv = (mode == SR_MODE_LOSS && tier == SR_TIER_BASIC && !gather)
-                     ? sr_vstk_rows(int(sizeof(T)), n_eval, ctx->rows_override)
-                     : 0;
+  int Rv = (mode == SR_MODE_LOSS && tier == SR_TIER_BASIC && !gather)
+               ? sr_vstk_rows(int(sizeof(T)), n_eval, ctx->rows_override)
+               : 0;
+  // a wide dataset whose register-stack tile (its rows per lane are twice the classic kernel's) would
+  // not fit the LDS runs the classic kernel instead (Float64 with ~40-75 features)
+  if (Rv > 0 && make_grid<T>(n_eval, nt > 0 ? nt : 1, Rv, W, int(ds->nf), 0, 0, ds->w != nullptr, ctx->tree_group,
+                             ctx->max_row_blocks).lds > kLdsMax)
+    Rv = 0;
   ctx->rows_last = Rv > 0 ? Rv : R;  // (every C2-like tree fits the register stack)
   hipStream_t s = ctx->stream;
   // error exits while chunks are in flight: no DMA may still read the staging buffers
@@ -1127,10 +1153,14 @@ int exact_list_ok(sr_ctx* ctx, const sr_dataset* ds, const SrProgramBatch<T>& pr
   return SR_OK;
 }
 
-// Finalize one tree: complete unless flagged; BIG-only trees take their exact verdict (list_ok).
+// Finalize one tree: complete unless flagged; BIG-only trees take their exact verdict (list_ok).  A
+// complete tree's loss is Σ / denom, or +Inf where the reference's T-precision fold of the losses
+// overflows (sr_fold.h; n_terms = rows of the fold, 0: only SR_FLAG_ELEMINF is applied).  Trees the
+// bounds cannot decide are appended to *fold_list (when given) for the exact in-order fold.
 template <typename T>
 void finalize(int64_t nt, const double* sums, const uint32_t* flags, double denom, const int64_t* list,
-              int64_t n_list, const uint8_t* list_ok, T* out_loss, uint8_t* out_complete) {
+              int64_t n_list, const uint8_t* list_ok, T* out_loss, uint8_t* out_complete, int64_t n_terms = 0,
+              std::vector<int64_t>* fold_list = nullptr) {
   std::vector<int64_t> pos;
   if (n_list > 0) {
     pos.assign(size_t(nt), -1);
@@ -1144,7 +1174,84 @@ void finalize(int64_t nt, const double* sums, const uint32_t* flags, double deno
     }
     out_complete[t] = ok ? 1 : 0;
     out_loss[t] = ok ? T(sums[t] / denom) : T(INFINITY);
+    if (!ok) continue;
+    const bool elem_inf = (flags[t] & SR_FLAG_ELEMINF) != 0;
+    const int cls = n_terms > 0 ? sr_fold_class<T>(sums[t], elem_inf, n_terms) : (elem_inf ? SR_FOLD_INF : SR_FOLD_FINITE);
+    if (cls == SR_FOLD_INF) {
+      out_loss[t] = T(INFINITY);
+    } else if (cls == SR_FOLD_EXACT && fold_list) {
+      fold_list->push_back(t);
+    }
   }
+}
+
+// The trees `idx` of a batch as a batch of their own (node arrays copied: a tree is a contiguous range).
+template <typename T>
+struct SubBatch {
+  std::vector<int64_t> offs;
+  std::vector<uint8_t> deg, op, con;
+  std::vector<uint16_t> feat;
+  std::vector<T> val;
+  sr_tree_batch b{};
+  SubBatch(const sr_tree_batch& trees, const int64_t* idx, size_t n) {
+    offs.assign(n + 1, 0);
+    for (size_t i = 0; i < n; ++i) offs[i + 1] = offs[i] + (trees.offsets[idx[i] + 1] - trees.offsets[idx[i]]);
+    const size_t nn = size_t(offs.back());
+    deg.resize(nn);
+    op.resize(nn);
+    con.resize(nn);
+    feat.resize(nn);
+    val.resize(nn);
+    const T* vals = static_cast<const T*>(trees.val);
+    for (size_t i = 0; i < n; ++i) {
+      const int64_t b0 = trees.offsets[idx[i]], len = offs[i + 1] - offs[i], o = offs[i];
+      std::memcpy(deg.data() + o, trees.degree + b0, size_t(len));
+      std::memcpy(op.data() + o, trees.op + b0, size_t(len));
+      std::memcpy(con.data() + o, trees.constant + b0, size_t(len));
+      std::memcpy(feat.data() + o, trees.feature + b0, size_t(len) * sizeof(uint16_t));
+      std::memcpy(val.data() + o, vals + b0, size_t(len) * sizeof(T));
+    }
+    b = sr_tree_batch{int64_t(n), offs.data(), deg.data(), op.data(), feat.data(), con.data(), val.data()};
+  }
+};
+
+// The reference's fold of the listed trees' losses over this view (or shard), exactly and in row order
+// (sr_fold_kernel): their predictions from the PRED interpreter (the values the LOSS kernels saw), then
+// one workgroup per tree.  carry (host, may be NULL): per listed tree the fold over the rows before this
+// shard.  out: the folds (T; +Inf where the fold overflows).  Runs after the call's other passes (it
+// reuses the context's program buffers).
+template <typename T>
+int fold_exact(sr_ctx* ctx, const sr_dataset* ds, int opset_id, const sr_tree_batch* trees, const int64_t* row_idx,
+               int64_t n_idx, int64_t n_total, int loss_kind, const std::vector<int64_t>& list, const T* carry,
+               std::vector<T>* out) {
+  out->assign(list.size(), T(0));
+  if (list.empty()) return SR_OK;
+  int lkind = 0;
+  double lparam = 0.0;
+  if (decode_loss(ctx, loss_kind, &lkind, &lparam) != SR_OK) return SR_ERR_INVALID_ARG;
+  const bool gather = row_idx != nullptr && n_idx > 0;
+  const int64_t n_eval = gather ? n_idx : ds->n;
+  hipStream_t s = ctx->stream;
+  // predictions of at most ~1 GiB per pass
+  const int64_t per = std::max<int64_t>(1, int64_t((size_t(1) << 30) / (size_t(n_eval) * sizeof(T))));
+  for (size_t b0 = 0; b0 < list.size(); b0 += size_t(per)) {
+    const size_t nb = std::min(list.size() - b0, size_t(per));
+    SubBatch<T> sub(*trees, list.data() + b0, nb);
+    SrProgramBatch<T> prog;
+    Grid g;
+    int rc = run_batch<T>(ctx, ds, opset_id, &sub.b, row_idx, n_idx, n_total, loss_kind, SR_MODE_PRED, &prog, &g);
+    if (rc != SR_OK) return rc;
+    SR_HIP_CHECK(ctx->fold_io.ensure(2 * nb * sizeof(T) + 16));
+    T* d_carry = ctx->fold_io.as<T>();
+    T* d_out = d_carry + nb;
+    if (carry) SR_HIP_CHECK(hipMemcpyAsync(d_carry, carry + b0, nb * sizeof(T), hipMemcpyHostToDevice, s));
+    SR_HIP_CHECK(sr_launch_fold<T>(ctx->pred.as<T>(), n_eval, int(nb), static_cast<const T*>(ds->y),
+                                   static_cast<const T*>(ds->w), gather ? ctx->row_idx.as<int64_t>() : nullptr, n_eval,
+                                   lkind, T(lparam), carry ? d_carry : nullptr, d_out, s));
+    SR_HIP_CHECK(hipMemcpyAsync(out->data() + b0, d_out, nb * sizeof(T), hipMemcpyDeviceToHost, s));
+    SR_HIP_CHECK(hipStreamSynchronize(s));
+  }
+  return SR_OK;
 }
 
 template <typename T>
@@ -1156,6 +1263,10 @@ double view_denominator(const sr_dataset* ds, const int64_t* row_idx, int64_t n_
   for (int64_t i = 0; i < n_idx; ++i) s += ds->w_host[size_t(row_idx[i])];
   return s;
 }
+
+// Rows of the reference's loss fold for the overflow rule (sr_fold.h), or 0 when the rule does not
+// apply (negative weights: the fold is not monotone).
+inline int64_t fold_terms(const sr_dataset* ds, int64_t n_rows) { return (ds->w && ds->w_min < 0.0) ? 0 : n_rows; }
 
 template <typename T>
 int eval_loss_impl(sr_ctx* ctx, const sr_dataset* ds, int opset_id, const sr_tree_batch* trees,
@@ -1204,8 +1315,17 @@ int eval_loss_impl(sr_ctx* ctx, const sr_dataset* ds, int opset_id, const sr_tre
   if (rc != SR_OK) return rc;
   ctx->mark_phase(3);
   const double denom = view_denominator<T>(ds, row_idx, n_idx);
+  std::vector<int64_t> fold_list;
   finalize<T>(nt, sums.data(), flags.data(), denom, list.data(), int64_t(list.size()), list_ok.data(),
-              static_cast<T*>(out_loss), out_complete);
+              static_cast<T*>(out_loss), out_complete, fold_terms(ds, n_eval), &fold_list);
+  ctx->n_fold_last = int64_t(fold_list.size());
+  if (!fold_list.empty()) {  // rare: the reference's own fold, in row order (sr_fold.h)
+    std::vector<T> fold;
+    rc = fold_exact<T>(ctx, ds, opset_id, trees, row_idx, n_idx, n_eval, loss_kind, fold_list, nullptr, &fold);
+    if (rc != SR_OK) return rc;
+    for (size_t i = 0; i < fold_list.size(); ++i)
+      static_cast<T*>(out_loss)[fold_list[i]] = T(fold[i] / T(denom));  // mean: total / count, in T
+  }
   ctx->mark_phase(4);
   auto t1 = std::chrono::steady_clock::now();
   ctx->last_total_ms = std::chrono::duration<double, std::milli>(t1 - t0).count();
@@ -1330,12 +1450,14 @@ int upload_impl(sr_ctx* ctx, const void* X, int64_t nf, int64_t n, const void* y
   if (w) {
     const T* wh = static_cast<const T*>(w);
     ds->w_host.resize(size_t(n));
-    double sum = 0.0;
+    double sum = 0.0, wmin = INFINITY;
     for (int64_t i = 0; i < n; ++i) {
       ds->w_host[size_t(i)] = double(wh[i]);
       sum += double(wh[i]);
+      wmin = std::min(wmin, double(wh[i]));
     }
     ds->wsum = sum;
+    ds->w_min = wmin;
     if ((e = hipMalloc(&ds->w, size_t(ds->ld) * sizeof(T))) != hipSuccess) return fail(e, "hipMalloc w");
     if ((e = hipMemcpyAsync(ds->w, w, size_t(n) * sizeof(T), hipMemcpyHostToDevice, s)) != hipSuccess) return fail(e, "copy w");
     if ((e = sr_launch_pad<T>(static_cast<T*>(ds->w), n, ds->ld, T(0), 0, s)) != hipSuccess) return fail(e, "pad w");
@@ -1402,7 +1524,6 @@ int eval_grad_impl(sr_ctx* ctx, const sr_dataset* ds, int opset_id, const sr_tre
     }
   }
   hipStream_t s = ctx->stream;
-  const int depth = prog.max_depth > 0 ? prog.max_depth : 1;
   // one pinned staging image (programs, offsets, constants, constant offsets, every bucket's work
   // items) -> ONE upload; every bucket's kernel and reduce go out back to back, their results come
   // back in ONE copy, and the host waits once (round 3: four uploads, then per bucket an upload, a
@@ -1439,13 +1560,19 @@ int eval_grad_impl(sr_ctx* ctx, const sr_dataset* ds, int opset_id, const sr_tre
   const double denom = view_denominator<T>(ds, row_idx, n_idx);
   constexpr int kWaves = 4;
   size_t part_need = 0;
-  struct Launch { int64_t n_rb, tiles_per_block, n_groups; };
+  struct Launch { int64_t n_rb, tiles_per_block, n_groups; int rows, depth; };
   Launch lc[kNB] = {};
   for (int b = 0; b < kNB; ++b) {
     const int64_t ni = int64_t(items[b].size());
     if (ni == 0) continue;
     const int kt = kts[b];
-    const int64_t rows_per_tile = 64 * int64_t(sr_grad_rows_per_lane(kt, int(sizeof(T))));
+    // the bucket's own deepest program sizes its LDS operand stacks; rows per lane drop to 1 when the
+    // default's tile + stacks would not fit (many features, Float64, deep trees: ADVICE r3)
+    int bdepth = 1;
+    for (uint32_t t : items[b]) bdepth = std::max(bdepth, int(prog.depth[t]));
+    const int rows = sr_grad_launch_rows(int(sizeof(T)), kt, int(ds->nf), ds->w != nullptr, bdepth, kWaves, kLdsMax);
+    if (rows == 0) return set_error(SR_ERR_TOO_DEEP, "gradient tile needs more than 160 KiB of LDS");
+    const int64_t rows_per_tile = 64 * int64_t(rows);
     const int64_t n_tiles = (n_eval + rows_per_tile - 1) / rows_per_tile;
     const int64_t n_groups = (ni + kWaves - 1) / kWaves;
     int64_t n_rb = (4096 + n_groups - 1) / n_groups;
@@ -1454,10 +1581,7 @@ int eval_grad_impl(sr_ctx* ctx, const sr_dataset* ds, int opset_id, const sr_tre
     const int64_t tiles_per_block = (n_tiles + n_rb - 1) / n_rb;
     n_rb = (n_tiles + tiles_per_block - 1) / tiles_per_block;
     if (n_rb * n_groups > 0x7fffffff) return set_error(SR_ERR_INVALID_ARG, "grid too large");
-    const size_t lds = (size_t(ds->nf) + 1 + (ds->w ? 1 : 0)) * size_t(rows_per_tile) * sizeof(T) +
-                       size_t(kWaves) * depth * (1 + kt) * size_t(rows_per_tile) * sizeof(T);
-    if (lds > kLdsMax) return set_error(SR_ERR_TOO_DEEP, "gradient tile needs more than 160 KiB of LDS");
-    lc[b] = Launch{n_rb, tiles_per_block, n_groups};
+    lc[b] = Launch{n_rb, tiles_per_block, n_groups, rows, bdepth};
     part_need = std::max(part_need, size_t(n_rb) * size_t(ni) * size_t(kt));
   }
   // (buckets run one after another on the stream, so they share the partials buffer)
@@ -1484,11 +1608,11 @@ int eval_grad_impl(sr_ctx* ctx, const sr_dataset* ds, int opset_id, const sr_tre
     a.tiles_per_block = int(lc[b].tiles_per_block);
     a.n_row_blocks = int(lc[b].n_rb);
     a.n_groups = int(lc[b].n_groups);
-    a.stack_depth = depth;
+    a.stack_depth = lc[b].depth;
     a.loss_kind = lkind;
     a.loss_param = T(lparam);
     a.part = ctx->g_part.as<double>();
-    SR_HIP_CHECK(sr_launch_grad_any<T>(a, kt, gather, int(lc[b].n_rb * lc[b].n_groups), s));
+    SR_HIP_CHECK(sr_launch_grad_any<T>(a, kt, gather, lc[b].rows, int(lc[b].n_rb * lc[b].n_groups), s));
     SR_HIP_CHECK(sr_launch_grad_reduce(a.part, int(lc[b].n_rb), int(size_t(ni) * kt), ctx->g_out.as<double>() + o_vals[b], s));
   }
   double* out = ctx->h_grad.as<double>();  // (the staging image is no longer needed: the upload is done)
@@ -1557,36 +1681,185 @@ int check_runtime_pair() {
   return SR_OK;
 }
 
-// Every shard's rows, Σw and max|X| (one all-gather per dataset and communicator).  Collective.
+// The sharded calls' data-path transport: the library's own RCCL communicator over xGMI
+// (sr_comm_init), or collectives the caller registers (sr_comm_init_host: host callbacks such as a gloo
+// group — several ranks can then share one GPU, and they run this same code).  Buffers are device
+// memory on the library's stream; a call returns once its result is usable on that stream.
+struct SrComm {
+  int nranks = 1, rank = 0;
+  virtual ~SrComm() = default;
+  virtual const char* kind() const = 0;
+  virtual int allreduce_sum(double* d, size_t n, hipStream_t s) = 0;                     // in place
+  virtual int allgather(const void* send, void* recv, size_t bytes, hipStream_t s) = 0;  // recv[nranks][bytes]
+};
+
+struct SrRcclComm final : SrComm {
+  ncclComm_t comm = nullptr;
+  ~SrRcclComm() override {
+    if (comm) (void)ncclCommDestroy(comm);
+  }
+  const char* kind() const override { return "rccl"; }
+  int allreduce_sum(double* d, size_t n, hipStream_t s) override {
+    SR_NCCL_CHECK(ncclAllReduce(d, d, n, ncclDouble, ncclSum, comm, s));
+    return SR_OK;
+  }
+  int allgather(const void* send, void* recv, size_t bytes, hipStream_t s) override {
+    SR_NCCL_CHECK(ncclAllGather(send, recv, bytes, ncclChar, comm, s));
+    return SR_OK;
+  }
+};
+
+// Host callbacks: the buffers are staged through host memory.  A failed staging copy still calls the
+// callback, with this rank's contribution poisoned (NaN bytes): every caller appends an error word to
+// its payload, which then reads non-zero on every rank.  A rank never skips a collective its peers
+// enter.
+struct SrHostComm final : SrComm {
+  sr_host_allreduce_fn ar = nullptr;
+  sr_host_allgather_fn ag = nullptr;
+  void* user = nullptr;
+  std::vector<char> h_send, h_recv;
+  const char* kind() const override { return "host"; }
+  int allreduce_sum(double* d, size_t n, hipStream_t s) override {
+    h_send.resize(n * sizeof(double));
+    const bool staged = hipMemcpyAsync(h_send.data(), d, h_send.size(), hipMemcpyDeviceToHost, s) == hipSuccess &&
+                        hipStreamSynchronize(s) == hipSuccess;
+    if (!staged) std::memset(h_send.data(), 0xff, h_send.size());
+    if (ar(user, reinterpret_cast<double*>(h_send.data()), int64_t(n)) != 0)
+      return set_error(SR_ERR_HIP, "the host all-reduce callback failed");
+    SR_HIP_CHECK(hipMemcpyAsync(d, h_send.data(), h_send.size(), hipMemcpyHostToDevice, s));
+    SR_HIP_CHECK(hipStreamSynchronize(s));
+    return staged ? SR_OK : set_error(SR_ERR_HIP, "staging the all-reduce buffer failed");
+  }
+  int allgather(const void* send, void* recv, size_t bytes, hipStream_t s) override {
+    h_send.resize(bytes);
+    h_recv.resize(bytes * size_t(nranks));
+    const bool staged = hipMemcpyAsync(h_send.data(), send, bytes, hipMemcpyDeviceToHost, s) == hipSuccess &&
+                        hipStreamSynchronize(s) == hipSuccess;
+    if (!staged) std::memset(h_send.data(), 0xff, bytes);
+    if (ag(user, h_send.data(), h_recv.data(), int64_t(bytes)) != 0)
+      return set_error(SR_ERR_HIP, "the host all-gather callback failed");
+    SR_HIP_CHECK(hipMemcpyAsync(recv, h_recv.data(), h_recv.size(), hipMemcpyHostToDevice, s));
+    SR_HIP_CHECK(hipStreamSynchronize(s));
+    return staged ? SR_OK : set_error(SR_ERR_HIP, "staging the all-gather buffer failed");
+  }
+};
+
+// A buffer of a sharded call's collectives, grown before the collective.  Growth happens on every rank
+// at the same call (the sizes depend only on the batch and the number of ranks, and the collective
+// buffers serve the collective calls alone), so whether a call grows a buffer is the same on every
+// rank; a call that grows one first agrees on the outcome (agree below).  ctx->inject_fail (tests,
+// sr_set_tuning "inject_failure") makes the next growths fail on this rank.
+struct Prep {
+  sr_ctx* ctx;
+  bool grew = false;
+  int rc = SR_OK;
+  std::vector<DevBuf*> touched;
+  std::vector<HostBuf*> touched_host;
+  bool inject() {
+    if (ctx->inject_fail <= 0) return false;
+    --ctx->inject_fail;
+    return true;
+  }
+  void fail(hipError_t e) {
+    if (e != hipSuccess && rc == SR_OK) rc = set_error(SR_ERR_HIP, std::string("collective buffer: ") + hipGetErrorString(e));
+  }
+  void need(DevBuf& b, size_t bytes) {
+    if (bytes <= b.cap) return;
+    grew = true;
+    touched.push_back(&b);
+    if (rc != SR_OK) return;
+    if (inject()) {
+      b.release();
+      fail(hipErrorOutOfMemory);
+    } else {
+      fail(b.ensure(bytes));
+    }
+  }
+  void need(HostBuf& b, size_t bytes) {  // (pinned staging of a collective's results)
+    if (bytes <= b.cap) return;
+    grew = true;
+    touched_host.push_back(&b);
+    if (rc != SR_OK) return;
+    if (inject()) {
+      b.release();
+      fail(hipErrorOutOfMemory);
+    } else {
+      fail(b.ensure(bytes, ctx->stream, ctx->stream2));
+    }
+  }
+};
+
+// Every rank's readiness before a collective: one Σ of error words (a rank whose preparation failed
+// still enters it), so either every rank proceeds or every rank returns an error.
+int agree(sr_ctx* ctx, int local) {
+  hipStream_t s = ctx->stream;
+  double* d = ctx->ctl.as<double>();
+  const double e = local != SR_OK ? 1.0 : 0.0;
+  double sum = 0.0;
+  const bool set = hipMemcpyAsync(d, &e, sizeof(double), hipMemcpyHostToDevice, s) == hipSuccess;
+  int rc = ctx->xport->allreduce_sum(d, 1, s);
+  if (rc == SR_OK) {
+    SR_HIP_CHECK(hipMemcpyAsync(&sum, d, sizeof(double), hipMemcpyDeviceToHost, s));
+    SR_HIP_CHECK(hipStreamSynchronize(s));
+  }
+  if (local != SR_OK) return local;
+  if (!set) return set_error(SR_ERR_HIP, "error word upload failed");
+  if (rc != SR_OK) return rc;
+  if (sum != 0.0) return set_error(SR_ERR_HIP, "a peer rank failed to prepare its collective buffers");
+  return SR_OK;
+}
+// Grown buffers are agreed on; after a failure every rank releases them, so the next call grows them
+// on every rank again (the ranks' buffer states stay identical).
+int agree_prep(sr_ctx* ctx, Prep& p) {
+  if (!p.grew) return SR_OK;
+  const int rc = agree(ctx, p.rc);
+  if (rc != SR_OK) {
+    for (DevBuf* b : p.touched) b->release();
+    for (HostBuf* b : p.touched_host) b->release();
+  }
+  return rc;
+}
+
+constexpr int kLayoutWords = 6;
+// Every shard's rows, Σw, max|X| and smallest weight (one all-gather per dataset and communicator; its buffer is
+// prepared and agreed on by the caller).  Collective: a local failure still enters the all-gather,
+// with its error word set.
 int shard_layout(sr_ctx* ctx, const sr_dataset* ds) {
-  if (ds->shard_gen == ctx->comm_gen && !ds->shard_offs.empty()) return SR_OK;
+  constexpr int K = kLayoutWords;
   const int nr = ctx->comm_ranks;
   hipStream_t s = ctx->stream;
-  const double mine[4] = {double(ds->n), ds->w ? ds->wsum : 0.0, ds->max_abs_x, ds->w ? 1.0 : 0.0};
-  SR_HIP_CHECK(ctx->shard_buf.ensure(sizeof(double) * 4 * size_t(nr + 1)));
-  double* d = ctx->shard_buf.as<double>();
-  SR_HIP_CHECK(hipMemcpyAsync(d, mine, sizeof(mine), hipMemcpyHostToDevice, s));
-  SR_NCCL_CHECK(ncclAllGather(d, d + 4, 4, ncclDouble, ctx->comm, s));
-  std::vector<double> all(size_t(4) * size_t(nr));
-  SR_HIP_CHECK(hipMemcpyAsync(all.data(), d + 4, all.size() * sizeof(double), hipMemcpyDeviceToHost, s));
+  // n, Σw, max|X|, weighted, min w, error word
+  double mine[K] = {double(ds->n), ds->w ? ds->wsum : 0.0, ds->max_abs_x, ds->w ? 1.0 : 0.0, ds->w ? ds->w_min : 0.0, 0.0};
+  double* d = ctx->coll_buf.as<double>();
+  if (hipMemcpyAsync(d, mine, sizeof(mine), hipMemcpyHostToDevice, s) != hipSuccess) {
+    mine[K - 1] = 1.0;
+    (void)hipMemcpy(d, mine, sizeof(mine), hipMemcpyHostToDevice);
+  }
+  int rc = ctx->xport->allgather(d, d + K, K * sizeof(double), s);
+  if (rc != SR_OK) return rc;
+  std::vector<double> all(size_t(K) * size_t(nr));
+  SR_HIP_CHECK(hipMemcpyAsync(all.data(), d + K, all.size() * sizeof(double), hipMemcpyDeviceToHost, s));
   SR_HIP_CHECK(hipStreamSynchronize(s));
   std::vector<int64_t> offs(size_t(nr) + 1, 0);
-  double wsum = 0.0, mx = 0.0;
+  double wsum = 0.0, mx = 0.0, wmin = INFINITY;
   int64_t mn = INT64_MAX;
   int weighted = 0;
   for (int r = 0; r < nr; ++r) {
-    const int64_t n = int64_t(all[size_t(4 * r)]);
+    const double* a = all.data() + size_t(K) * size_t(r);
+    if (a[K - 1] != 0.0) return set_error(SR_ERR_HIP, "the shard layout exchange failed on rank " + std::to_string(r));
+    const int64_t n = int64_t(a[0]);
     offs[size_t(r) + 1] = offs[size_t(r)] + n;
-    wsum += all[size_t(4 * r + 1)];
-    const double m = all[size_t(4 * r + 2)];
-    mx = (m > mx || m != m) ? m : mx;  // NaN / Inf (non-finite data) propagate
+    wsum += a[1];
+    mx = (a[2] > mx || a[2] != a[2]) ? a[2] : mx;  // NaN / Inf (non-finite data) propagate
     mn = std::min(mn, n);
-    weighted += all[size_t(4 * r + 3)] != 0.0 ? 1 : 0;
+    weighted += a[3] != 0.0 ? 1 : 0;
+    wmin = std::min(wmin, a[4]);
   }
   if (weighted != 0 && weighted != nr) return set_error(SR_ERR_INVALID_ARG, "some shards have weights and some do not");
-  if (int64_t(all[size_t(4 * ctx->comm_rank)]) != ds->n) return set_error(SR_ERR_INVALID_ARG, "shard layout exchange failed");
+  if (int64_t(all[size_t(K) * size_t(ctx->comm_rank)]) != ds->n) return set_error(SR_ERR_INVALID_ARG, "shard layout exchange failed");
   ds->shard_offs = offs;
   ds->shard_wsum = wsum;
+  ds->shard_w_min = weighted ? wmin : 0.0;
   ds->shard_max_abs_x = (mx != mx) ? double(INFINITY) : mx;
   ds->shard_min_rows = mn;
   ds->shard_gen = ctx->comm_gen;
@@ -1594,9 +1867,9 @@ int shard_layout(sr_ctx* ctx, const sr_dataset* ds) {
 }
 
 // EXACT verdicts of the listed (BIG-only) trees over the GLOBAL rows of a row-sharded call: each rank
-// folds the Julia leaf blocks it holds (sr_jsum_partials' ranges), the folds are all-gathered over
-// the communicator, and every rank adds them in Base.mapreduce_impl's recursion order.  Collective
-// (the list is the same on every rank: it comes from the all-reduced flags).
+// folds the Julia leaf blocks it holds (sr_jsum_partials' ranges), the folds are all-gathered, and
+// every rank adds them in Base.mapreduce_impl's recursion order.  Collective (the list is the same on
+// every rank: it comes from the all-reduced flags); a local failure travels in the error word.
 template <typename T>
 int exact_sharded(sr_ctx* ctx, const sr_dataset* ds, const SrProgramBatch<T>& prog, const std::vector<int64_t>& list,
                   std::vector<uint8_t>* list_ok) {
@@ -1625,10 +1898,17 @@ int exact_sharded(sr_ctx* ctx, const sr_dataset* ds, const SrProgramBatch<T>& pr
   const double err = local != SR_OK ? 1.0 : 0.0;
   std::memcpy(mine.data() + payload, &err, sizeof(double));
   hipStream_t s = ctx->stream;
-  SR_HIP_CHECK(ctx->shard_buf.ensure(slot * size_t(nr + 1)));
-  char* d = ctx->shard_buf.as<char>();
-  SR_HIP_CHECK(hipMemcpyAsync(d, mine.data(), slot, hipMemcpyHostToDevice, s));
-  SR_NCCL_CHECK(ncclAllGather(d, d + slot, slot, ncclChar, ctx->comm, s));
+  Prep prep{ctx};
+  prep.need(ctx->coll_buf, slot * size_t(nr + 1));
+  int rc = agree_prep(ctx, prep);
+  if (rc != SR_OK) return local != SR_OK ? local : rc;
+  char* d = ctx->coll_buf.as<char>();
+  if (hipMemcpyAsync(d, mine.data(), slot, hipMemcpyHostToDevice, s) != hipSuccess) {
+    std::memset(mine.data() + payload, 0xff, sizeof(double));  // (poisoned error word)
+    (void)hipMemcpy(d, mine.data(), slot, hipMemcpyHostToDevice);
+  }
+  rc = ctx->xport->allgather(d, d + slot, slot, s);
+  if (rc != SR_OK) return rc;
   std::vector<char> every(slot * size_t(nr));
   SR_HIP_CHECK(hipMemcpyAsync(every.data(), d + slot, every.size(), hipMemcpyDeviceToHost, s));
   SR_HIP_CHECK(hipStreamSynchronize(s));
@@ -1646,52 +1926,118 @@ int exact_sharded(sr_ctx* ctx, const sr_dataset* ds, const SrProgramBatch<T>& pr
   return SR_OK;
 }
 
+// The reference's loss fold of the listed trees over the GLOBAL rows, in row order: the shards fold in
+// rank order, each continuing from the previous shard's value (one all-gather per rank: the round's
+// folding rank broadcasts its values with an error word).  Collective; out = the folds (T).
+template <typename T>
+int fold_sharded(sr_ctx* ctx, const sr_dataset* ds, int opset_id, const sr_tree_batch* trees, int loss_kind,
+                 const std::vector<int64_t>& list, std::vector<T>* out) {
+  out->assign(list.size(), T(0));
+  if (list.empty()) return SR_OK;
+  const int nr = ctx->comm_ranks, me = ctx->comm_rank;
+  const int64_t n_total = ds->shard_offs[size_t(nr)];
+  if (nr == 1) return fold_exact<T>(ctx, ds, opset_id, trees, nullptr, 0, n_total, loss_kind, list, nullptr, out);
+  const size_t payload = list.size() * sizeof(T);
+  const size_t slot = (payload + sizeof(double) + 255) & ~size_t(255);
+  hipStream_t s = ctx->stream;
+  Prep prep{ctx};
+  prep.need(ctx->coll_buf, slot * size_t(nr + 1));
+  int rc = agree_prep(ctx, prep);
+  if (rc != SR_OK) return rc;
+  char* d = ctx->coll_buf.as<char>();
+  std::vector<T> carry;
+  std::vector<char> mine(slot, 0), every(slot * size_t(nr));
+  for (int r = 0; r < nr; ++r) {
+    int local = SR_OK;
+    std::fill(mine.begin(), mine.end(), 0);
+    if (me == r) {
+      std::vector<T> vals;
+      local = fold_exact<T>(ctx, ds, opset_id, trees, nullptr, 0, n_total, loss_kind, list, r == 0 ? nullptr : carry.data(),
+                            &vals);
+      if (local == SR_OK) std::memcpy(mine.data(), vals.data(), payload);
+      const double err = local != SR_OK ? 1.0 : 0.0;
+      std::memcpy(mine.data() + payload, &err, sizeof(double));
+    }
+    if (hipMemcpyAsync(d, mine.data(), slot, hipMemcpyHostToDevice, s) != hipSuccess) {
+      std::memset(mine.data() + payload, 0xff, sizeof(double));
+      (void)hipMemcpy(d, mine.data(), slot, hipMemcpyHostToDevice);
+    }
+    rc = ctx->xport->allgather(d, d + slot, slot, s);
+    if (rc != SR_OK) return rc;
+    SR_HIP_CHECK(hipMemcpyAsync(every.data(), d + slot, every.size(), hipMemcpyDeviceToHost, s));
+    SR_HIP_CHECK(hipStreamSynchronize(s));
+    for (int q = 0; q < nr; ++q) {
+      double e = 0.0;
+      std::memcpy(&e, every.data() + slot * size_t(q) + payload, sizeof(double));
+      if (e != 0.0) return local != SR_OK ? local : set_error(SR_ERR_HIP, "the loss fold failed on rank " + std::to_string(q));
+    }
+    carry.assign(reinterpret_cast<const T*>(every.data() + slot * size_t(r)),
+                 reinterpret_cast<const T*>(every.data() + slot * size_t(r)) + list.size());
+  }
+  *out = carry;
+  return SR_OK;
+}
+
 // The row-sharded step (sr_eval_loss_sharded): this rank's shard through the same launch pipeline as
 // a single-GPU call (derived columns, dead-tree probe, two-chunk compile/launch overlap), the packed
-// [4, n_trees] partials plus an error word summed by ONE in-place all-reduce on the device, losses
-// finalized on the device (Σ / global denominator), and the rare BIG-only trees decided by the exact
-// pass over the global rows.  Every rank enters every collective, also after a local failure (its
+// [5, n_trees] partials plus an error word summed by ONE in-place all-reduce on the device, losses
+// finalized on the device (Σ / global denominator), the rare BIG-only trees decided by the exact pass
+// over the global rows, and the rarer trees whose loss fold the bounds cannot decide folded in row
+// order across the shards.  Every rank enters every collective, also after a local failure (its
 // partials zeroed, its error word set), and then every rank returns an error.
 template <typename T>
 int eval_sharded_impl(sr_ctx* ctx, const sr_dataset* ds, int opset_id, const sr_tree_batch* trees, int loss_kind,
                       T* out_loss, uint8_t* out_complete) {
   const int64_t nt = trees->n_trees;
-  int rc = shard_layout(ctx, ds);
-  if (rc != SR_OK) return rc;
   const int nr = ctx->comm_ranks;
+  const size_t n5 = size_t(5) * size_t(nt);
+  // [5][nt] partials | error word, then the finalized losses (T) and complete codes
+  const size_t o_loss = ((n5 + 1) * sizeof(double) + 255) & ~size_t(255);
+  const size_t o_comp = o_loss + ((size_t(nt) * sizeof(T) + 255) & ~size_t(255));
+  // 1. every buffer this call's collectives use, grown (and agreed on) before the first of them
+  const bool need_layout = !(ds->shard_gen == ctx->comm_gen && !ds->shard_offs.empty());
+  Prep prep{ctx};
+  if (need_layout) prep.need(ctx->coll_buf, sizeof(double) * kLayoutWords * size_t(nr + 1));
+  prep.need(ctx->coll_packed, o_comp + size_t(nt) + 16);
+  int rc = agree_prep(ctx, prep);
+  if (rc != SR_OK) return rc;
+  // 2. the shards' layout (first call per dataset and communicator)
+  if (need_layout) {
+    rc = shard_layout(ctx, ds);
+    if (rc != SR_OK) return rc;
+  }
   const int64_t n_total = ds->shard_offs[size_t(nr)];
   const ShardCtl sc{ds->shard_max_abs_x, ds->shard_min_rows};
   auto t0 = std::chrono::steady_clock::now();
   ctx->start_phases(t0);
+  // 3. this shard
   SrProgramBatch<T> prog;
   Grid g;
   int local = nt > 0 ? run_batch<T>(ctx, ds, opset_id, trees, nullptr, 0, n_total, loss_kind, SR_MODE_LOSS, &prog, &g,
                                     true, &sc)
                      : SR_OK;
   hipStream_t s = ctx->stream;
-  const size_t n4 = size_t(4) * size_t(nt);
-  // [4][nt] partials | error word, then the finalized losses (T) and complete bytes
-  const size_t o_loss = ((n4 + 1) * sizeof(double) + 255) & ~size_t(255);
-  const size_t o_comp = o_loss + ((size_t(nt) * sizeof(T) + 255) & ~size_t(255));
-  SR_HIP_CHECK(ctx->packed.ensure(o_comp + size_t(nt) + 16));
-  char* base = ctx->packed.as<char>();
+  char* base = ctx->coll_packed.as<char>();
   double* dst = reinterpret_cast<double*>(base);
   if (local == SR_OK && nt > 0) {
     const hipError_t e = sr_launch_pack_partials(ctx->d_out_sum, ctx->d_out_flag, int(nt), dst, s);
     if (e != hipSuccess) local = set_error(SR_ERR_HIP, std::string("pack partials: ") + hipGetErrorString(e));
   }
-  const double err_word = local != SR_OK ? 1.0 : 0.0;
-  if (local != SR_OK) SR_HIP_CHECK(hipMemsetAsync(dst, 0, n4 * sizeof(double), s));
-  SR_HIP_CHECK(hipMemcpyAsync(dst + n4, &err_word, sizeof(double), hipMemcpyHostToDevice, s));
+  double err_word = local != SR_OK ? 1.0 : 0.0;
+  if (local != SR_OK && hipMemsetAsync(dst, 0, n5 * sizeof(double), s) != hipSuccess) err_word = NAN;
+  if (hipMemcpyAsync(dst + n5, &err_word, sizeof(double), hipMemcpyHostToDevice, s) != hipSuccess && local == SR_OK)
+    local = set_error(SR_ERR_HIP, "error word upload failed");
   ctx->mark_phase(1);
-  // the path's one exchange step: every rank's partials (and error words), summed in place over xGMI
-  SR_NCCL_CHECK(ncclAllReduce(dst, dst, n4 + 1, ncclDouble, ncclSum, ctx->comm, s));
+  // 4. the path's one exchange step: every rank's partials (and error words), summed in place
+  rc = ctx->xport->allreduce_sum(dst, n5 + 1, s);
+  if (rc != SR_OK) return local != SR_OK ? local : rc;
   const double denom = ds->w ? ds->shard_wsum : double(n_total);
   T* d_loss = reinterpret_cast<T*>(base + o_loss);
   uint8_t* d_comp = reinterpret_cast<uint8_t*>(base + o_comp);
-  SR_HIP_CHECK(sr_launch_finalize_packed<T>(dst, int(nt), denom, d_loss, d_comp, s));
   double err_sum = 0.0;
-  SR_HIP_CHECK(hipMemcpyAsync(&err_sum, dst + n4, sizeof(double), hipMemcpyDeviceToHost, s));
+  SR_HIP_CHECK(hipMemcpyAsync(&err_sum, dst + n5, sizeof(double), hipMemcpyDeviceToHost, s));
+  const int64_t n_terms = (ds->w && ds->shard_w_min < 0.0) ? 0 : n_total;
+  SR_HIP_CHECK(sr_launch_finalize_packed<T>(dst, int(nt), denom, n_terms, d_loss, d_comp, s));
   if (nt > 0) {
     SR_HIP_CHECK(hipMemcpyAsync(out_loss, d_loss, size_t(nt) * sizeof(T), hipMemcpyDeviceToHost, s));
     SR_HIP_CHECK(hipMemcpyAsync(out_complete, d_comp, size_t(nt), hipMemcpyDeviceToHost, s));
@@ -1701,9 +2047,10 @@ int eval_sharded_impl(sr_ctx* ctx, const sr_dataset* ds, int opset_id, const sr_
   if (!ctx->timing_pending) ctx->last_eval_ms = ctx->last_busy_ms = 0.0;
   ctx->mark_phase(2);
   if (err_sum != 0.0) return local != SR_OK ? local : set_error(SR_ERR_HIP, "the row-sharded step failed on a peer rank");
+  // 5. rare: BIG-only trees, DynamicExpressions' exact check over the global rows
   std::vector<int64_t> list;
   for (int64_t t = 0; t < nt; ++t)
-    if (out_complete[t] == 2) list.push_back(t);
+    if (out_complete[t] & 2) list.push_back(t);
   std::vector<uint8_t> list_ok;
   ctx->n_exact_last = int64_t(list.size());
   ctx->exact_kernel_ms = 0.0;
@@ -1711,74 +2058,103 @@ int eval_sharded_impl(sr_ctx* ctx, const sr_dataset* ds, int opset_id, const sr_
   if (rc != SR_OK) return rc;
   for (size_t i = 0; i < list.size(); ++i) {
     const int64_t t = list[i];
-    out_complete[t] = list_ok[i] ? 1 : 0;
+    out_complete[t] = uint8_t((out_complete[t] & ~3) | (list_ok[i] ? 1 : 0));
     if (!list_ok[i]) out_loss[t] = T(INFINITY);
   }
+  // 6. rarer: the loss fold in row order across the shards (sr_fold.h)
+  std::vector<int64_t> fold_list;
+  for (int64_t t = 0; t < nt; ++t)
+    if ((out_complete[t] & 1) && (out_complete[t] & SR_COMP_FOLD)) fold_list.push_back(t);
+  ctx->n_fold_last = int64_t(fold_list.size());
+  std::vector<T> fold;
+  rc = fold_sharded<T>(ctx, ds, opset_id, trees, loss_kind, fold_list, &fold);
+  if (rc != SR_OK) return rc;
+  for (size_t i = 0; i < fold_list.size(); ++i) out_loss[fold_list[i]] = T(fold[i] / T(denom));
+  for (int64_t t = 0; t < nt; ++t) out_complete[t] &= 1;
   ctx->mark_phase(3);
   ctx->last_total_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
   return SR_OK;
 }
 
+// Owner rank of every tree for tree sharding: sorted by node count (largest first, stable), dealt in
+// snake order 0..N-1, N-1..0, ... (sr_amd.distributed.tree_owners is the same rule).
+std::vector<int> tree_owners(const sr_tree_batch* trees, int nr) {
+  const int64_t nt = trees->n_trees;
+  std::vector<int64_t> order(static_cast<size_t>(nt));
+  for (int64_t t = 0; t < nt; ++t) order[size_t(t)] = t;
+  auto size_of = [&](int64_t t) { return trees->offsets[t + 1] - trees->offsets[t]; };
+  std::stable_sort(order.begin(), order.end(), [&](int64_t a, int64_t b) { return size_of(a) > size_of(b); });
+  std::vector<int> owner(static_cast<size_t>(nt));
+  for (int64_t k = 0; k < nt; ++k) {
+    const int64_t round = k / nr, pos = k % nr;
+    owner[size_t(order[size_t(k)])] = int((round & 1) ? (nr - 1 - pos) : pos);
+  }
+  return owner;
+}
+
 // Tree-sharded scoring (sr_eval_loss_tree_sharded): the dataset is replicated, the trees are split over
-// the ranks by estimated cost (node count; sorted, dealt in snake order so every rank gets a similar
-// share), each rank scores its own trees with the single-GPU call, and ONE all-reduce of a
-// [loss | complete | error] buffer (each tree's slots written by its owner only) hands every rank
-// every result.
+// the ranks by estimated cost (tree_owners), each rank scores its own trees with the single-GPU call,
+// and ONE all-gather of every rank's results ([loss (T) | complete] of its trees, in tree order, and
+// an error word) hands every rank every result.
 template <typename T>
 int eval_tree_sharded_impl(sr_ctx* ctx, const sr_dataset* ds, int opset_id, const sr_tree_batch* trees, int loss_kind,
                            T* out_loss, uint8_t* out_complete) {
   const int64_t nt = trees->n_trees;
   const int nr = ctx->comm_ranks, me = ctx->comm_rank;
-  std::vector<int64_t> order(static_cast<size_t>(nt));
-  for (int64_t t = 0; t < nt; ++t) order[size_t(t)] = t;
-  auto size_of = [&](int64_t t) { return trees->offsets[t + 1] - trees->offsets[t]; };
-  std::stable_sort(order.begin(), order.end(), [&](int64_t a, int64_t b) { return size_of(a) > size_of(b); });
-  std::vector<int64_t> mine;
-  for (int64_t k = 0; k < nt; ++k) {
-    const int64_t round = k / nr, pos = k % nr;
-    const int owner = int((round & 1) ? (nr - 1 - pos) : pos);
-    if (owner == me) mine.push_back(order[size_t(k)]);
-  }
-  std::sort(mine.begin(), mine.end());  // this rank's trees in the caller's order
-  // this rank's sub-batch (node arrays copied: a batch's trees are contiguous ranges)
-  std::vector<int64_t> offs(mine.size() + 1, 0);
-  for (size_t i = 0; i < mine.size(); ++i) offs[i + 1] = offs[i] + size_of(mine[i]);
-  const size_t nn = size_t(offs.back());
-  std::vector<uint8_t> deg(nn), op(nn), con(nn);
-  std::vector<uint16_t> feat(nn);
-  std::vector<T> val(nn);
-  const T* vals = static_cast<const T*>(trees->val);
-  for (size_t i = 0; i < mine.size(); ++i) {
-    const int64_t b = trees->offsets[mine[i]], n = size_of(mine[i]), o = offs[i];
-    std::memcpy(deg.data() + o, trees->degree + b, size_t(n));
-    std::memcpy(op.data() + o, trees->op + b, size_t(n));
-    std::memcpy(con.data() + o, trees->constant + b, size_t(n));
-    std::memcpy(feat.data() + o, trees->feature + b, size_t(n) * sizeof(uint16_t));
-    std::memcpy(val.data() + o, vals + b, size_t(n) * sizeof(T));
-  }
-  sr_tree_batch sub{int64_t(mine.size()), offs.data(), deg.data(), op.data(), feat.data(), con.data(), val.data()};
-  std::vector<T> l(mine.size());
-  std::vector<uint8_t> c(mine.size());
-  int local = eval_loss_impl<T>(ctx, ds, opset_id, &sub, nullptr, 0, loss_kind, l.data(), c.data());
-  std::vector<double> buf(2 * size_t(nt) + 1, 0.0);
-  if (local == SR_OK) {
-    for (size_t i = 0; i < mine.size(); ++i) {
-      buf[size_t(mine[i])] = double(l[i]);
-      buf[size_t(nt) + size_t(mine[i])] = double(c[i]);
+  const std::vector<int> owner = nr > 1 ? tree_owners(trees, nr) : std::vector<int>(size_t(nt), 0);
+  std::vector<std::vector<int64_t>> of(static_cast<size_t>(nr));
+  for (int64_t t = 0; t < nt; ++t) of[size_t(owner[size_t(t)])].push_back(t);
+  size_t max_cnt = 0;
+  for (const auto& v : of) max_cnt = std::max(max_cnt, v.size());
+  const size_t o_comp = max_cnt * sizeof(T);
+  const size_t o_err = (o_comp + max_cnt + 7) & ~size_t(7);
+  const size_t slot = (o_err + sizeof(double) + 255) & ~size_t(255);
+  Prep prep{ctx};
+  prep.need(ctx->h_coll, slot * size_t(nr + 1));
+  prep.need(ctx->coll_buf, slot * size_t(nr + 1));
+  int rc = agree_prep(ctx, prep);
+  if (rc != SR_OK) return rc;
+  const std::vector<int64_t>& mine = of[size_t(me)];
+  char* hm = ctx->h_coll.as<char>();  // pinned: this rank's slot, then every rank's
+  std::memset(hm, 0, slot);
+  int local = SR_OK;
+  if (!mine.empty()) {
+    T* l = reinterpret_cast<T*>(hm);
+    uint8_t* c = reinterpret_cast<uint8_t*>(hm + o_comp);
+    if (nr == 1) {  // (one rank owns every tree, in order: no sub-batch)
+      local = eval_loss_impl<T>(ctx, ds, opset_id, trees, nullptr, 0, loss_kind, l, c);
+    } else {
+      SubBatch<T> sub(*trees, mine.data(), mine.size());
+      local = eval_loss_impl<T>(ctx, ds, opset_id, &sub.b, nullptr, 0, loss_kind, l, c);
     }
   }
-  buf[2 * size_t(nt)] = local != SR_OK ? 1.0 : 0.0;
+  const double err = local != SR_OK ? 1.0 : 0.0;
+  if (local != SR_OK) std::memset(hm, 0, slot);
+  std::memcpy(hm + o_err, &err, sizeof(double));
   hipStream_t s = ctx->stream;
-  SR_HIP_CHECK(ctx->shard_buf.ensure(buf.size() * sizeof(double)));
-  double* d = ctx->shard_buf.as<double>();
-  SR_HIP_CHECK(hipMemcpyAsync(d, buf.data(), buf.size() * sizeof(double), hipMemcpyHostToDevice, s));
-  SR_NCCL_CHECK(ncclAllReduce(d, d, buf.size(), ncclDouble, ncclSum, ctx->comm, s));
-  SR_HIP_CHECK(hipMemcpyAsync(buf.data(), d, buf.size() * sizeof(double), hipMemcpyDeviceToHost, s));
+  char* d = ctx->coll_buf.as<char>();
+  if (hipMemcpyAsync(d, hm, slot, hipMemcpyHostToDevice, s) != hipSuccess) {
+    std::memset(hm + o_err, 0xff, sizeof(double));
+    (void)hipMemcpy(d, hm, slot, hipMemcpyHostToDevice);
+  }
+  rc = ctx->xport->allgather(d, d + slot, slot, s);
+  if (rc != SR_OK) return local != SR_OK ? local : rc;
+  char* every = hm + slot;
+  SR_HIP_CHECK(hipMemcpyAsync(every, d + slot, slot * size_t(nr), hipMemcpyDeviceToHost, s));
   SR_HIP_CHECK(hipStreamSynchronize(s));
-  if (buf[2 * size_t(nt)] != 0.0) return local != SR_OK ? local : set_error(SR_ERR_HIP, "tree-sharded scoring failed on a peer rank");
-  for (int64_t t = 0; t < nt; ++t) {
-    out_loss[t] = T(buf[size_t(t)]);
-    out_complete[t] = buf[size_t(nt) + size_t(t)] != 0.0 ? 1 : 0;
+  for (int r = 0; r < nr; ++r) {
+    double e = 0.0;
+    std::memcpy(&e, every + slot * size_t(r) + o_err, sizeof(double));
+    if (e != 0.0) return local != SR_OK ? local : set_error(SR_ERR_HIP, "tree-sharded scoring failed on rank " + std::to_string(r));
+  }
+  for (int r = 0; r < nr; ++r) {
+    const T* l = reinterpret_cast<const T*>(every + slot * size_t(r));
+    const uint8_t* c = reinterpret_cast<const uint8_t*>(every + slot * size_t(r) + o_comp);
+    const std::vector<int64_t>& v = of[size_t(r)];
+    for (size_t i = 0; i < v.size(); ++i) {
+      out_loss[v[i]] = l[i];
+      out_complete[v[i]] = c[i] ? 1 : 0;
+    }
   }
   return SR_OK;
 }
@@ -1857,13 +2233,12 @@ int sr_shutdown(sr_ctx* ctx) {
     Lock l(ctx);
     (void)hipSetDevice(ctx->device);
     (void)hipStreamSynchronize(ctx->stream);
-    if (ctx->comm) (void)ncclCommDestroy(ctx->comm);
-    ctx->comm = nullptr;
+    ctx->xport.reset();
     for (DevBuf* b : {&ctx->prog, &ctx->outs, &ctx->part_sum, &ctx->part_flag, &ctx->pred, &ctx->row_idx, &ctx->tree_list, &ctx->range_lo, &ctx->range_hi, &ctx->range_sums, &ctx->packed,
                       &ctx->hint, &ctx->jsum_prog, &ctx->jsum_fin, &ctx->jsum_scratch, &ctx->probe_sum, &ctx->probe_flag, &ctx->g_code, &ctx->g_offsets, &ctx->g_consts, &ctx->g_const_off,
-                      &ctx->g_items, &ctx->g_part, &ctx->g_out, &ctx->derived_cols, &ctx->probe_derived, &ctx->shard_buf})
+                      &ctx->g_items, &ctx->g_part, &ctx->g_out, &ctx->derived_cols, &ctx->probe_derived, &ctx->coll_buf, &ctx->coll_packed, &ctx->ctl, &ctx->fold_io})
       b->release();
-    for (HostBuf* b : {&ctx->h_prog, &ctx->h_outs, &ctx->h_grad}) b->release();
+    for (HostBuf* b : {&ctx->h_prog, &ctx->h_outs, &ctx->h_grad, &ctx->h_coll}) b->release();
     for (int c = 0; c < kMaxChunks; ++c) {
       (void)hipEventDestroy(ctx->ev_c0[c]);
       (void)hipEventDestroy(ctx->ev_c1[c]);
@@ -2036,7 +2411,7 @@ int sr_eval_loss_partials_packed(sr_ctx* ctx, const sr_dataset* ds, int opset_id
   }
   if (rc != SR_OK || nt == 0) return rc;
   hipStream_t s = ctx->stream;
-  const size_t bytes = size_t(4) * size_t(nt) * sizeof(double);
+  const size_t bytes = size_t(5) * size_t(nt) * sizeof(double);
   double* dst = out;
   if (!out_on_device) {
     SR_HIP_CHECK(ctx->packed.ensure(bytes));
@@ -2061,46 +2436,71 @@ int sr_comm_unique_id(void* out_id) {
   return SR_OK;
 }
 
-int sr_comm_init(sr_ctx* ctx, int nranks, int rank, const void* id_bytes) {
-  if (check_ctx(ctx) != SR_OK) return SR_ERR_INVALID_ARG;
-  if (!id_bytes || nranks < 1 || rank < 0 || rank >= nranks) return set_error(SR_ERR_INVALID_ARG, "bad communicator arguments");
-  Lock l(ctx);
-  SR_HIP_CHECK(hipSetDevice(ctx->device));
-  if (ctx->comm) {
-    (void)ncclCommDestroy(ctx->comm);
-    ctx->comm = nullptr;
-    ctx->comm_ranks = 0;
-  }
-  if (check_runtime_pair() != SR_OK) return SR_ERR_HIP;
-  ncclUniqueId id;
-  std::memcpy(&id, id_bytes, sizeof(id));
-  const ncclResult_t r = ncclCommInitRank(&ctx->comm, nranks, id, rank);
-  if (r != ncclSuccess) {
-    ctx->comm = nullptr;
-    return set_error(SR_ERR_HIP, std::string("ncclCommInitRank: ") + ncclGetErrorString(r));
-  }
+// A fresh transport: the collective buffers restart empty (every rank of the new group alike), shard
+// layouts are re-exchanged (new generation).
+static int install_comm(sr_ctx* ctx, std::unique_ptr<SrComm> x, int nranks, int rank) {
+  for (DevBuf* b : {&ctx->coll_buf, &ctx->coll_packed}) b->release();
+  ctx->h_coll.release();
+  SR_HIP_CHECK(ctx->ctl.ensure(256));
+  x->nranks = nranks;
+  x->rank = rank;
+  ctx->xport = std::move(x);
   ctx->comm_ranks = nranks;
   ctx->comm_rank = rank;
   ctx->comm_gen = ++g_comm_gen;
   return SR_OK;
 }
 
+int sr_comm_init(sr_ctx* ctx, int nranks, int rank, const void* id_bytes) {
+  if (check_ctx(ctx) != SR_OK) return SR_ERR_INVALID_ARG;
+  if (!id_bytes || nranks < 1 || rank < 0 || rank >= nranks) return set_error(SR_ERR_INVALID_ARG, "bad communicator arguments");
+  Lock l(ctx);
+  SR_HIP_CHECK(hipSetDevice(ctx->device));
+  ctx->xport.reset();
+  ctx->comm_ranks = 0;
+  if (check_runtime_pair() != SR_OK) return SR_ERR_HIP;
+  ncclUniqueId id;
+  std::memcpy(&id, id_bytes, sizeof(id));
+  auto x = std::make_unique<SrRcclComm>();
+  const ncclResult_t r = ncclCommInitRank(&x->comm, nranks, id, rank);
+  if (r != ncclSuccess) {
+    x->comm = nullptr;
+    return set_error(SR_ERR_HIP, std::string("ncclCommInitRank: ") + ncclGetErrorString(r));
+  }
+  return install_comm(ctx, std::move(x), nranks, rank);
+}
+
+int sr_comm_init_host(sr_ctx* ctx, int nranks, int rank, sr_host_allreduce_fn allreduce, sr_host_allgather_fn allgather,
+                      void* user) {
+  if (check_ctx(ctx) != SR_OK) return SR_ERR_INVALID_ARG;
+  if (!allreduce || !allgather || nranks < 1 || rank < 0 || rank >= nranks)
+    return set_error(SR_ERR_INVALID_ARG, "bad host communicator arguments");
+  Lock l(ctx);
+  SR_HIP_CHECK(hipSetDevice(ctx->device));
+  ctx->xport.reset();
+  ctx->comm_ranks = 0;
+  auto x = std::make_unique<SrHostComm>();
+  x->ar = allreduce;
+  x->ag = allgather;
+  x->user = user;
+  return install_comm(ctx, std::move(x), nranks, rank);
+}
+
 int sr_comm_destroy(sr_ctx* ctx) {
   if (check_ctx(ctx) != SR_OK) return SR_ERR_INVALID_ARG;
   Lock l(ctx);
-  if (ctx->comm) (void)ncclCommDestroy(ctx->comm);
-  ctx->comm = nullptr;
+  ctx->xport.reset();
   ctx->comm_ranks = 0;
   return SR_OK;
 }
 
-// Row-sharded step with the exchange on the device: this shard's packed [4, n_trees] partials
-// (sr_eval_loss_partials_packed) summed over every rank by ONE RCCL all-reduce in place on the
-// library's stream, then copied to out_host (every rank gets the global sums and flag counts).
+// Row-sharded step with the exchange on the device: this shard's packed [5, n_trees] partials
+// (sr_eval_loss_partials_packed) summed over every rank by ONE in-place all-reduce on the library's
+// stream, then copied to out_host (every rank gets the global sums and flag counts).
 int sr_eval_loss_partials_allreduce(sr_ctx* ctx, const sr_dataset* ds, int opset_id, const sr_tree_batch* trees,
                                     int64_t n_total, int loss_kind, double* out_host) {
   if (check_ctx(ctx) != SR_OK) return SR_ERR_INVALID_ARG;
-  if (!ctx->comm) return set_error(SR_ERR_INVALID_ARG, "no communicator: call sr_comm_init first");
+  if (!ctx->xport) return set_error(SR_ERR_INVALID_ARG, "no communicator: call sr_comm_init first");
   int rc = validate_common(ctx, ds, opset_id, trees);
   if (rc != SR_OK) return rc;
   const int64_t nt = trees->n_trees;
@@ -2108,6 +2508,11 @@ int sr_eval_loss_partials_allreduce(sr_ctx* ctx, const sr_dataset* ds, int opset
   if (n_total < ds->n) return set_error(SR_ERR_INVALID_ARG, "n_total smaller than this shard");
   Lock l(ctx);
   SR_HIP_CHECK(hipSetDevice(ctx->device));
+  const size_t n = size_t(5) * size_t(nt > 0 ? nt : 0);
+  Prep prep{ctx};
+  prep.need(ctx->coll_packed, (n + 1) * sizeof(double));
+  rc = agree_prep(ctx, prep);
+  if (rc != SR_OK) return rc;
   Grid g;
   auto t0 = std::chrono::steady_clock::now();
   if (ds->dtype == SR_DTYPE_F32) {
@@ -2117,19 +2522,18 @@ int sr_eval_loss_partials_allreduce(sr_ctx* ctx, const sr_dataset* ds, int opset
     SrProgramBatch<double> prog;
     rc = run_batch<double>(ctx, ds, opset_id, trees, nullptr, 0, n_total, loss_kind, SR_MODE_LOSS, &prog, &g);
   }
-  const int local = rc;
+  int local = rc;
   hipStream_t s = ctx->stream;
-  const size_t n = size_t(4) * size_t(nt > 0 ? nt : 0);
-  SR_HIP_CHECK(ctx->packed.ensure(n * sizeof(double) + 8));
-  double* dst = ctx->packed.as<double>();
-  if (local == SR_OK && nt > 0) SR_HIP_CHECK(sr_launch_pack_partials(ctx->d_out_sum, ctx->d_out_flag, int(nt), dst, s));
+  double* dst = ctx->coll_packed.as<double>();
+  if (local == SR_OK && nt > 0 && sr_launch_pack_partials(ctx->d_out_sum, ctx->d_out_flag, int(nt), dst, s) != hipSuccess)
+    local = set_error(SR_ERR_HIP, "pack partials failed");
   // every rank enters the collective, also with an empty batch (the counts agree: same trees) and
   // after a local failure (partials zeroed, the error word after them set): then every rank fails
-  const double err_word = local != SR_OK ? 1.0 : 0.0;
-  if (local != SR_OK) SR_HIP_CHECK(hipMemsetAsync(dst, 0, n * sizeof(double), s));
-  SR_HIP_CHECK(hipMemcpyAsync(dst + n, &err_word, sizeof(double), hipMemcpyHostToDevice, s));
-  const ncclResult_t r = ncclAllReduce(dst, dst, n + 1, ncclDouble, ncclSum, ctx->comm, s);
-  if (r != ncclSuccess) return set_error(SR_ERR_HIP, std::string("ncclAllReduce: ") + ncclGetErrorString(r));
+  double err_word = local != SR_OK ? 1.0 : 0.0;
+  if (local != SR_OK && hipMemsetAsync(dst, 0, n * sizeof(double), s) != hipSuccess) err_word = NAN;
+  (void)hipMemcpyAsync(dst + n, &err_word, sizeof(double), hipMemcpyHostToDevice, s);
+  rc = ctx->xport->allreduce_sum(dst, n + 1, s);
+  if (rc != SR_OK) return local != SR_OK ? local : rc;
   double err_sum = 0.0;
   SR_HIP_CHECK(hipMemcpyAsync(&err_sum, dst + n, sizeof(double), hipMemcpyDeviceToHost, s));
   if (nt > 0) SR_HIP_CHECK(hipMemcpyAsync(out_host, dst, n * sizeof(double), hipMemcpyDeviceToHost, s));
@@ -2143,7 +2547,7 @@ int sr_eval_loss_partials_allreduce(sr_ctx* ctx, const sr_dataset* ds, int opset
 int sr_eval_loss_sharded(sr_ctx* ctx, const sr_dataset* ds, int opset_id, const sr_tree_batch* trees, int loss_kind,
                          void* out_loss, uint8_t* out_complete) {
   if (check_ctx(ctx) != SR_OK) return SR_ERR_INVALID_ARG;
-  if (!ctx->comm) return set_error(SR_ERR_INVALID_ARG, "no communicator: call sr_comm_init first");
+  if (!ctx->xport) return set_error(SR_ERR_INVALID_ARG, "no communicator: call sr_comm_init first");
   int rc = validate_common(ctx, ds, opset_id, trees);
   if (rc != SR_OK) return rc;
   if (trees->n_trees > 0 && (!out_loss || !out_complete)) return set_error(SR_ERR_INVALID_ARG, "NULL output buffers");
@@ -2158,7 +2562,7 @@ int sr_eval_loss_sharded(sr_ctx* ctx, const sr_dataset* ds, int opset_id, const 
 int sr_eval_loss_tree_sharded(sr_ctx* ctx, const sr_dataset* ds, int opset_id, const sr_tree_batch* trees,
                               int loss_kind, void* out_loss, uint8_t* out_complete) {
   if (check_ctx(ctx) != SR_OK) return SR_ERR_INVALID_ARG;
-  if (!ctx->comm) return set_error(SR_ERR_INVALID_ARG, "no communicator: call sr_comm_init first");
+  if (!ctx->xport) return set_error(SR_ERR_INVALID_ARG, "no communicator: call sr_comm_init first");
   int rc = validate_common(ctx, ds, opset_id, trees);
   if (rc != SR_OK) return rc;
   if (trees->n_trees > 0 && (!out_loss || !out_complete)) return set_error(SR_ERR_INVALID_ARG, "NULL output buffers");
@@ -2174,12 +2578,21 @@ int sr_comm_info(sr_ctx* ctx, int* nranks, int* rank, char* paths, int64_t capac
   if (check_ctx(ctx) != SR_OK) return SR_ERR_INVALID_ARG;
   Lock l(ctx);
   if (nranks || rank) {
-    if (!ctx->comm) return set_error(SR_ERR_INVALID_ARG, "no communicator: call sr_comm_init first");
-    int c = 0, r = 0;
-    SR_NCCL_CHECK(ncclCommCount(ctx->comm, &c));
-    SR_NCCL_CHECK(ncclCommUserRank(ctx->comm, &r));
+    if (!ctx->xport) return set_error(SR_ERR_INVALID_ARG, "no communicator: call sr_comm_init first");
+    int c = ctx->comm_ranks, r = ctx->comm_rank;
+    if (auto* rc = dynamic_cast<SrRcclComm*>(ctx->xport.get())) {  // as RCCL itself reports them
+      SR_NCCL_CHECK(ncclCommCount(rc->comm, &c));
+      SR_NCCL_CHECK(ncclCommUserRank(rc->comm, &r));
+    }
     if (nranks) *nranks = c;
     if (rank) *rank = r;
+  }
+  if (paths && capacity > 0 && ctx->xport) {  // "transport=rccl|host;hip=...;rccl=..."
+    const std::string p = std::string("transport=") + ctx->xport->kind() + ";" + runtime_paths();
+    const size_t n = std::min(p.size(), size_t(capacity - 1));
+    std::memcpy(paths, p.data(), n);
+    paths[n] = '\0';
+    return SR_OK;
   }
   return sr_runtime_info(paths, capacity);
 }
@@ -2380,12 +2793,14 @@ static void settle_timing(sr_ctx* ctx) {
 
 int sr_last_phase_ms(sr_ctx* ctx, double* out, int n) {
   if (check_ctx(ctx) != SR_OK) return SR_ERR_INVALID_ARG;
+  Lock l(ctx);
   if (n > 8) settle_timing(ctx);
   for (int i = 0; i < n && i < 5; ++i) out[i] = ctx->phase_ms[i];
   if (n > 5) out[5] = double(ctx->n_chunks_last);
   if (n > 6) out[6] = ctx->exact_kernel_ms;
   if (n > 7) out[7] = double(ctx->rows_last);
   if (n > 8) out[8] = ctx->last_busy_ms;
+  if (n > 9) out[9] = double(ctx->n_fold_last);
   return SR_OK;
 }
 
@@ -2421,6 +2836,10 @@ int sr_set_tuning(sr_ctx* ctx, const char* name, int64_t value) {
     ctx->balance_groups = value != 0;
     return SR_OK;
   }
+  if (std::strcmp(name, "inject_failure") == 0) {  // tests: the next `value` collective-buffer growths fail
+    ctx->inject_fail = int(value);
+    return SR_OK;
+  }
   return set_error(SR_ERR_INVALID_ARG, std::string("unknown tuning knob '") + name + "'");
 }
 
@@ -2448,6 +2867,7 @@ int sr_debug_stamps(sr_ctx* ctx, uint64_t* out, int64_t cap, int64_t* n) {
 
 int sr_last_kernel_ms(sr_ctx* ctx, double* eval_ms, double* total_ms) {
   if (check_ctx(ctx) != SR_OK) return SR_ERR_INVALID_ARG;
+  Lock l(ctx);
   settle_timing(ctx);
   if (eval_ms) *eval_ms = ctx->last_eval_ms;
   if (total_ms) *total_ms = ctx->last_total_ms;

@@ -105,8 +105,12 @@ template <typename T>
 hipError_t sr_launch_jsum_levels(const T* leaf_sums, int64_t n_arrays, int n_leaves, const int2* nodes, int n_internal,
                                  const int32_t* level_off, int n_levels, T* scratch, uint8_t* out, hipStream_t s);
 hipError_t sr_launch_pack_partials(const double* sum, const uint32_t* flag, int n, double* out, hipStream_t s);
+// comp codes of the row-sharded finalize: 0 incomplete, 1 complete, 2 BIG only (exact check pending),
+// | SR_COMP_FOLD: the loss fold is computed in order (sr_fold.h)
+constexpr int SR_COMP_FOLD = 4;
 template <typename T>
-hipError_t sr_launch_finalize_packed(const double* packed, int n, double denom, T* loss, uint8_t* comp, hipStream_t s);
+hipError_t sr_launch_finalize_packed(const double* packed, int n, double denom, int64_t n_terms, T* loss, uint8_t* comp,
+                                     hipStream_t s);
 template <typename T>
 hipError_t sr_launch_transpose(const T* Xh_dev, int64_t nf, int64_t n, int64_t ld, T* Xd, hipStream_t s);
 template <typename T>
@@ -138,12 +142,34 @@ struct SrGradArgs {
   double* part;              // [n_row_blocks][n_items][KT]
 };
 
+// rows: rows per lane, sr_grad_rows_per_lane(kt) or 1 (sr_grad_launch_rows)
 template <typename T>
-hipError_t sr_launch_grad_any(const SrGradArgs<T>& a, int kt, bool gather, int n_blocks, hipStream_t s);
+hipError_t sr_launch_grad_any(const SrGradArgs<T>& a, int kt, bool gather, int rows, int n_blocks, hipStream_t s);
 // Rows per lane of the gradient kernel for KT tangents (a staged tile is 64 x that many rows).
 // (the same for Float64: halving its rows, to bring its ~230-256 VGPRs down, changed the gradient
 // sums' row-block order and with it chaotic C5 optimiser trajectories; not kept)
 constexpr int sr_grad_rows_per_lane(int kt, int elem_size = 4) {
   return (void)elem_size, kt <= 2 ? 8 : (kt <= 4 ? 4 : (kt <= 8 ? 2 : 1));
 }
+// LDS of one gradient workgroup (W waves): the X / y / w tile and the waves' operand stacks (value +
+// KT tangents per row, stack_depth slots)
+inline size_t sr_grad_lds_bytes(int elem_size, int kt, int rows, int nf, bool weighted, int stack_depth, int waves) {
+  return (size_t(nf) + 1 + (weighted ? 1 : 0)) * 64 * size_t(rows) * size_t(elem_size) +
+         size_t(waves) * size_t(stack_depth) * size_t(1 + kt) * size_t(rows) * 64 * size_t(elem_size);
+}
+// Rows per lane a bucket of KT tangents runs with: the default, or 1 when the default's tile and stack
+// (at the bucket's own deepest program) would pass `lds_max` (many features, Float64, deep stacks:
+// ADVICE r3); 0 when even one row per lane does not fit.
+inline int sr_grad_launch_rows(int elem_size, int kt, int nf, bool weighted, int stack_depth, int waves, size_t lds_max) {
+  const int rd = sr_grad_rows_per_lane(kt, elem_size);
+  if (sr_grad_lds_bytes(elem_size, kt, rd, nf, weighted, stack_depth, waves) <= lds_max) return rd;
+  if (sr_grad_lds_bytes(elem_size, kt, 1, nf, weighted, stack_depth, waves) <= lds_max) return 1;
+  return 0;
+}
 hipError_t sr_launch_grad_reduce(const double* part, int n_row_blocks, int n_vals, double* out, hipStream_t s);
+// The reference's loss fold in row order for listed trees (sr_fold.h; sr_aux.hip): predictions
+// pred[b][pred_ld] of n rows, losses against y (and w) at row_idx (or the row itself), carry[b] the fold
+// over earlier shards (NULL: none); out[b] = the fold in T (+Inf when it overflows).
+template <typename T>
+hipError_t sr_launch_fold(const T* pred, int64_t pred_ld, int n_trees, const T* y, const T* w, const int64_t* row_idx,
+                          int64_t n, int loss_kind, T loss_param, const T* carry, T* out, hipStream_t s);

@@ -51,9 +51,11 @@ struct SrGradRows {
   static constexpr int value = sr_grad_rows_per_lane(KT, int(sizeof(T)));
 };
 
-template <typename T, int KT, int W, bool GATHER>
+// R: rows per lane (SrGradRows' default, or 1 when the default's LDS operand stack would not fit:
+// sr_grad_launch_rows)
+template <typename T, int KT, int W, bool GATHER, int R>
 __global__ void __launch_bounds__(W * 64) sr_grad_kernel(const SrGradArgs<T> a) {
-  constexpr int R = SrGradRows<T, KT>::value;  // rows per lane: lane + 64 j, j < R
+  // rows per lane: lane + 64 j, j < R
   constexpr int ROWS = 64 * R;               // rows per staged tile
   constexpr int NV = 1 + KT;                 // value + tangents
   extern __shared__ __attribute__((aligned(16))) unsigned char sr_smem[];
@@ -242,23 +244,15 @@ __global__ void __launch_bounds__(W * 64) sr_grad_kernel(const SrGradArgs<T> a) 
   }
 }
 
-// LDS of one workgroup: the X / y / w tile and the waves' operand stacks (value + tangents per row)
-template <typename T, int KT, int W>
-size_t sr_grad_lds(int nf, bool weighted, int stack_depth) {
-  constexpr int R = SrGradRows<T, KT>::value;
-  return (size_t(nf) + 1 + (weighted ? 1 : 0)) * 64 * R * sizeof(T) +
-         size_t(W) * size_t(stack_depth) * (1 + KT) * R * 64 * sizeof(T);
-}
-
-template <typename T, int KT, int W, bool GATHER>
+template <typename T, int KT, int W, bool GATHER, int R>
 hipError_t sr_launch_grad(const SrGradArgs<T>& a, int n_blocks, hipStream_t s) {
-  const size_t lds = sr_grad_lds<T, KT, W>(a.nf, a.w != nullptr, a.stack_depth);
-  const void* fn = reinterpret_cast<const void*>(&sr_grad_kernel<T, KT, W, GATHER>);
+  const size_t lds = sr_grad_lds_bytes(int(sizeof(T)), KT, R, a.nf, a.w != nullptr, a.stack_depth, W);
+  const void* fn = reinterpret_cast<const void*>(&sr_grad_kernel<T, KT, W, GATHER, R>);
   if (lds > 65536) {
     const hipError_t e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, int(lds));
     if (e != hipSuccess) return e;
   }
-  hipLaunchKernelGGL((sr_grad_kernel<T, KT, W, GATHER>), dim3(n_blocks), dim3(W * 64), lds, s, a);
+  hipLaunchKernelGGL((sr_grad_kernel<T, KT, W, GATHER, R>), dim3(n_blocks), dim3(W * 64), lds, s, a);
   return hipGetLastError();
 }
 

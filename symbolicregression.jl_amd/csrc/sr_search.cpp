@@ -45,6 +45,7 @@
 #include "sr_search_tree.h"
 
 int sr_set_error(int code, const std::string& msg);  // sr_capi.cpp
+int sr_ctx_swap_timing(sr_ctx* ctx, int value);        // sr_capi.cpp: set "timing", return the old value
 
 namespace {
 
@@ -182,12 +183,13 @@ struct Scorer {
     std::vector<uint8_t> comp(static_cast<size_t>(nt));
     const int64_t* r = rows.empty() ? nullptr : rows.data();
     const auto t0 = Clock::now();
-    // (no timing events on the search's small calls unless their kernel times are wanted)
-    if (!loss_cb && !time_kernels) sr_set_tuning(ctx, "timing", 0);
+    // (no timing events on the search's small calls unless their kernel times are wanted; the
+    // context's own setting is restored afterwards)
+    const int timing_was = (!loss_cb && !time_kernels) ? sr_ctx_swap_timing(ctx, 0) : -1;
     const int rc = loss_cb ? loss_cb(cb_user, &b, r, int64_t(rows.size()), out->data(), comp.data())
                            : sr_eval_loss_batch(ctx, ds, opset_id, &b, r, int64_t(rows.size()), loss_code, out->data(),
                                                 comp.data());
-    if (!loss_cb && !time_kernels) sr_set_tuning(ctx, "timing", 1);
+    if (timing_was >= 0) sr_ctx_swap_timing(ctx, timing_was);
     ms += ms_since(t0);
     ++calls;
     if (rc != SR_OK) return rc;
@@ -209,11 +211,11 @@ struct Scorer {
     if (b.n_trees == 0) return SR_OK;
     const int64_t* r = rows.empty() ? nullptr : rows.data();
     const auto t0 = Clock::now();
-    if (!grad_cb && !time_kernels) sr_set_tuning(ctx, "timing", 0);
+    const int timing_was = (!grad_cb && !time_kernels) ? sr_ctx_swap_timing(ctx, 0) : -1;
     const int rc = grad_cb ? grad_cb(cb_user, &b, r, int64_t(rows.size()), out->data(), g->data(), comp->data())
                            : sr_eval_grad_batch(ctx, ds, opset_id, &b, r, int64_t(rows.size()), loss_code, out->data(),
                                                 g->data(), comp->data());
-    if (!grad_cb && !time_kernels) sr_set_tuning(ctx, "timing", 1);
+    if (timing_was >= 0) sr_ctx_swap_timing(ctx, timing_was);
     ms += ms_since(t0);
     ++calls;
     return rc;

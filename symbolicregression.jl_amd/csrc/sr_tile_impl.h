@@ -803,7 +803,7 @@ __global__ void __launch_bounds__(W * 64, (SrMinWavesFor<T, R, TIER, W, VSTK>::v
     }
   }
   const uint64_t live = sr_ballot(lane < S && my_pe > my_pb);  // empty program: statically incomplete
-  uint64_t dmask = 0u, bmask = 0u;
+  uint64_t dmask = 0u, bmask = 0u, emask = 0u;
   double accv = 0.0;
   // dead-tree hints shared across row blocks (LOSS mode): a tree found non-finite by any block is
   // skipped by blocks that start it later.  Loaded one tile ahead; only ever a hint (a skipped
@@ -1138,9 +1138,18 @@ __global__ void __launch_bounds__(W * 64, (SrMinWavesFor<T, R, TIER, W, VSTK>::v
               for (int r = 0; r < R; ++r) l[r] = (row0 + L::row(lane, r) < a.n_rows) ? l[r] : T(0);
             }
             // pairwise over the lane's rows by halves (rows r and r + h: adjacent pairs of rows add as
-            // one packed instruction, R - 1 adds in R / 2 instructions); the wave sum follows
+            // one packed instruction, R - 1 adds in R / 2 instructions); the wave sum follows.  The
+            // first level's sums are sums of TWO losses: one of them +Inf means an elementwise loss,
+            // or the T sum of two, is +Inf, and the reference's sequential fold of all the losses
+            // (each >= 0) is then +Inf too (it is at least the fold of those two).  Their max (one
+            // VGPR) decides that below, only when the tile's sum overflowed.
 #pragma unroll
-            for (int h = R / 2; h >= 1; h /= 2) {
+            for (int r = 0; r < R / 2; ++r) l[r] += l[r + R / 2];
+            T pair_max = l[0];
+#pragma unroll
+            for (int r = 1; r < R / 2; ++r) pair_max = pair_max > l[r] ? pair_max : l[r];
+#pragma unroll
+            for (int h = R / 4; h >= 1; h /= 2) {
 #pragma unroll
               for (int r = 0; r < h; ++r) l[r] += l[r + h];
             }
@@ -1170,6 +1179,10 @@ __global__ void __launch_bounds__(W * 64, (SrMinWavesFor<T, R, TIER, W, VSTK>::v
               const T s = sr_wave_sum<T>(l[0]);
               accv += (lane == j) ? double(s) : 0.0;
               if (susp_any) bmask |= bit;
+              // The tile's T sum of the losses is +Inf (rare; s is wave-uniform): SR_FLAG_ELEMINF when
+              // a loss or a pair sum is +Inf (the reference's fold is then +Inf); otherwise only the
+              // longer sums overflowed and the host decides the fold (sr_fold.h)
+              if (!(s <= SrM<T>::big) && sr_ballot(pair_max == T(INFINITY))) emask |= bit;
             }
           }
           if (dead) {
@@ -1202,7 +1215,8 @@ __global__ void __launch_bounds__(W * 64, (SrMinWavesFor<T, R, TIER, W, VSTK>::v
     return;
   }
   if (lane < S) {
-    uint32_t f = (((dmask >> lane) & 1u) ? SR_FLAG_NONFINITE : 0u) | (((bmask >> lane) & 1u) ? SR_FLAG_BIG : 0u);
+    uint32_t f = (((dmask >> lane) & 1u) ? SR_FLAG_NONFINITE : 0u) | (((bmask >> lane) & 1u) ? SR_FLAG_BIG : 0u) |
+                 (((emask >> lane) & 1u) ? SR_FLAG_ELEMINF : 0u);
     if (MODE == SR_MODE_LOSS && a.out_sum) {  // one row block: final per-tree values, tree order
       const uint32_t tree = a.perm ? a.perm[my_pos] : uint32_t(my_pos);
       if (a.static_bad[tree]) f |= SR_FLAG_STATIC | SR_FLAG_NONFINITE;

@@ -31,6 +31,7 @@ SR_LOSS_L1DIST = 1
 SR_FLAG_NONFINITE = 1
 SR_FLAG_BIG = 2
 SR_FLAG_STATIC = 4
+SR_FLAG_ELEMINF = 8
 
 # Every symbol include/sr_amd.h declares (checked by tests/test_abi.py).
 EXPORTED_SYMBOLS = (
@@ -50,6 +51,7 @@ EXPORTED_SYMBOLS = (
     "sr_eval_loss_partials_packed",
     "sr_comm_unique_id",
     "sr_comm_init",
+    "sr_comm_init_host",
     "sr_comm_destroy",
     "sr_eval_loss_partials_allreduce",
     "sr_eval_loss_sharded",
@@ -148,6 +150,9 @@ class SrSearchInfo(ctypes.Structure):
 # CPU scorer callbacks (tests): sr_loss_fn / sr_grad_fn
 LOSS_FN = ctypes.CFUNCTYPE(c_int, c_void_p, POINTER(SrTreeBatch), c_void_p, c_int64, c_void_p, c_void_p)
 GRAD_FN = ctypes.CFUNCTYPE(c_int, c_void_p, POINTER(SrTreeBatch), c_void_p, c_int64, c_void_p, c_void_p, c_void_p)
+# host collectives of sr_comm_init_host: sr_host_allreduce_fn / sr_host_allgather_fn
+HOST_ALLREDUCE_FN = ctypes.CFUNCTYPE(c_int, c_void_p, POINTER(c_double), c_int64)
+HOST_ALLGATHER_FN = ctypes.CFUNCTYPE(c_int, c_void_p, c_void_p, c_void_p, c_int64)
 
 
 def _load():
@@ -184,6 +189,7 @@ def _load():
         "sr_max_checks": (c_int, [P, c_int, c_int, POINTER(SrTreeBatch), POINTER(c_int)]),
         "sr_comm_unique_id": (c_int, [P]),
         "sr_comm_init": (c_int, [P, c_int, c_int, P]),
+        "sr_comm_init_host": (c_int, [P, c_int, c_int, HOST_ALLREDUCE_FN, HOST_ALLGATHER_FN, P]),
         "sr_comm_destroy": (c_int, [P]),
         "sr_eval_loss_partials_allreduce": (c_int, [P, P, c_int, POINTER(SrTreeBatch), c_int64, c_int, P]),
         "sr_eval_loss_sharded": (c_int, [P, P, c_int, POINTER(SrTreeBatch), c_int, P, P]),

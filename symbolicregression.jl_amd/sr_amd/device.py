@@ -64,7 +64,7 @@ class DeviceContext:
 
     def set_tuning(self, name, value):
         """Run-time tuning knob (results never depend on one; include/sr_amd.h lists them): "derived",
-        "probe", "stress_probe", "code_cache", "timing", "rows_per_lane", "balance"."""
+        "probe", "stress_probe", "code_cache", "timing", "rows_per_lane", "balance"; tests: "inject_failure"."""
         _lib.check(_lib.lib.sr_set_tuning(self.handle, name.encode(), int(value)))
 
     def last_derived_columns(self):
@@ -96,6 +96,13 @@ class DeviceContext:
         out = (ctypes.c_double * 9)()
         _lib.check(_lib.lib.sr_last_phase_ms(self.handle, out, 9))
         return float(out[8])
+
+    def last_fold_trees(self):
+        """Trees of the last eval_loss call whose loss fold was computed in row order (the reference's
+        T-precision fold near overflow: csrc/sr_fold.h)."""
+        out = (ctypes.c_double * 10)()
+        _lib.check(_lib.lib.sr_last_phase_ms(self.handle, out, 10))
+        return int(out[9])
 
     def last_launches(self):
         """Interpreter launches of the last eval_loss call (chunked compile/launch pipeline)."""

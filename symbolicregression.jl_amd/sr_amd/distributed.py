@@ -7,11 +7,16 @@ its bundled HIP runtime cannot share the device with the library's in one proces
 
 Row sharding, `eval_loss_sharded`: rank r holds global rows [Σ_{q<r} n_q, Σ_{q<=r} n_q).  With a
 device communicator the whole step is ONE library call (`sr_eval_loss_sharded`): the shard runs
-the single-GPU launch pipeline, its packed [4, n_trees] partials (Σ loss, then the NONFINITE / BIG /
-STATIC flag bits as 0/1) are summed by one in-place RCCL all-reduce, losses are finalized on the
-device, and the rare BIG trees get DynamicExpressions' exact isfinite(sum(x)) verdict in Julia's
+the single-GPU launch pipeline, its packed [5, n_trees] partials (Σ loss, then the NONFINITE / BIG /
+STATIC / ELEMINF flag bits as 0/1) are summed by one in-place RCCL all-reduce, losses are finalized on
+the device, the rare BIG trees get DynamicExpressions' exact isfinite(sum(x)) verdict in Julia's
 pairwise order over the GLOBAL rows (each rank folds the leaf blocks it holds; the folds are
-all-gathered; `sr_jsum_finite`'s recursion-order combine).
+all-gathered; `sr_jsum_finite`'s recursion-order combine), and the rarer trees whose T-precision loss
+fold may overflow are folded in row order across the shards.
+
+`init_host_comm` gives the library the same collectives over the gloo group instead of RCCL
+(`sr_comm_init_host`): the library's own sharded code then runs with several ranks on one GPU (the
+multi-rank tests on a one-GPU box).
 
 Tree sharding, `eval_loss_tree_sharded`: the dataset is replicated, the trees are dealt over the
 ranks by size, each rank scores its share, one all-reduce hands every rank every result
@@ -46,12 +51,15 @@ def _require_gloo(group):
                            "the device collectives run on the library's RCCL communicator (init_device_comm)")
 
 
+N_PACKED = 5  # rows of the packed partials: Σ loss, NONFINITE, BIG, STATIC, ELEMINF
+
+
 def gpu_partials_packed(tb, shard, options, n_total, ctx=None):
-    """This rank's packed partials [4, n_trees] f64 on its row shard (GPU), on the host."""
+    """This rank's packed partials [5, n_trees] f64 on its row shard (GPU), on the host."""
     ctx = ctx or get_context()
     nt = tb.n_trees
     s = tb.to_struct()
-    out = np.zeros((4, nt), dtype=np.float64)
+    out = np.zeros((N_PACKED, nt), dtype=np.float64)
     _lib.check(_lib.lib.sr_eval_loss_partials_packed(
         ctx.handle, shard.device_handle(ctx), ctx.opset_id(options.operators), ctypes.byref(s), int(n_total),
         ctx.loss_code(options), out.ctypes.data_as(ctypes.c_void_p), 0))
@@ -85,6 +93,51 @@ def init_device_comm(group=None, ctx=None):
     return ctx
 
 
+def init_host_comm(group=None, ctx=None):
+    """The library's sharded calls over the gloo `group` instead of RCCL (C ABI sr_comm_init_host): the
+    library stages each collective's buffer through host memory and calls back into torch.distributed
+    (all_reduce of float64 / all_gather of bytes).  The same C++ code path as with RCCL, so several
+    ranks can share one GPU (tests)."""
+    import torch
+    import torch.distributed as dist
+
+    _require_gloo(group)
+    ctx = ctx or get_context()
+    world, rank = dist.get_world_size(group), dist.get_rank(group)
+
+    def allreduce(_user, buf, n):
+        try:
+            a = np.ctypeslib.as_array(buf, shape=(int(n),))
+            t = torch.from_numpy(a.copy())
+            dist.all_reduce(t, op=dist.ReduceOp.SUM, group=group)
+            a[:] = t.numpy()
+            return 0
+        except Exception:  # noqa: BLE001 - reported to the library as a failed collective
+            return 1
+
+    def allgather(_user, send, recv, nbytes):
+        try:
+            nb = int(nbytes)
+            src = np.frombuffer((ctypes.c_char * nb).from_address(send), dtype=np.uint8).copy()
+            parts = [torch.empty(nb, dtype=torch.uint8) for _ in range(world)]
+            dist.all_gather(parts, torch.from_numpy(src), group=group)
+            dst = np.frombuffer((ctypes.c_char * (nb * world)).from_address(recv), dtype=np.uint8)
+            for r, part in enumerate(parts):
+                dst[r * nb:(r + 1) * nb] = part.numpy()
+            return 0
+        except Exception:  # noqa: BLE001
+            return 1
+
+    ctx._host_comm_cbs = (_lib.HOST_ALLREDUCE_FN(allreduce), _lib.HOST_ALLGATHER_FN(allgather))
+    _lib.check(_lib.lib.sr_comm_init_host(ctx.handle, world, rank, ctx._host_comm_cbs[0], ctx._host_comm_cbs[1], None))
+    info = comm_info(ctx)
+    if (info["nranks"], info["rank"], info.get("transport")) != (world, rank, "host"):
+        raise RuntimeError(f"host communicator is rank {info['rank']} of {info['nranks']}, group says {rank} of {world}")
+    ctx.has_comm = True
+    ctx.comm_world, ctx.comm_rank = world, rank
+    return ctx
+
+
 def destroy_device_comm(ctx=None):
     ctx = ctx or get_context()
     _lib.check(_lib.lib.sr_comm_destroy(ctx.handle))
@@ -113,12 +166,12 @@ def _check_group(ctx, group):
 
 
 def gpu_partials_allreduce(tb, shard, options, n_total, ctx=None):
-    """Every rank's packed partials [4, n_trees], summed on the devices by the library's RCCL
+    """Every rank's packed partials [5, n_trees], summed on the devices by the library's
     communicator (`sr_eval_loss_partials_allreduce`) -> numpy on every rank."""
     ctx = ctx or get_context()
     nt = tb.n_trees
     s = tb.to_struct()
-    out = np.zeros((4, max(nt, 1)), dtype=np.float64)
+    out = np.zeros((N_PACKED, max(nt, 1)), dtype=np.float64)
     _lib.check(_lib.lib.sr_eval_loss_partials_allreduce(
         ctx.handle, shard.device_handle(ctx), ctx.opset_id(options.operators), ctypes.byref(s), int(n_total),
         ctx.loss_code(options), out.ctypes.data_as(ctypes.c_void_p)))
@@ -190,10 +243,11 @@ def finalize(dtype, sums, flags, denom, tree_list=None, list_ok=None):
 
 
 def unpack_flags(packed):
-    """[4, n] summed partials -> (Σ loss f64, flag words u32): a bit is set if any rank set it."""
+    """[5, n] summed partials -> (Σ loss f64, flag words u32): a bit is set if any rank set it."""
     packed = np.asarray(packed, dtype=np.float64)
     flags = np.zeros(packed.shape[1], dtype=np.uint32)
-    for row, bit in ((1, _lib.SR_FLAG_NONFINITE), (2, _lib.SR_FLAG_BIG), (3, _lib.SR_FLAG_STATIC)):
+    for row, bit in ((1, _lib.SR_FLAG_NONFINITE), (2, _lib.SR_FLAG_BIG), (3, _lib.SR_FLAG_STATIC),
+                     (4, _lib.SR_FLAG_ELEMINF)):
         flags |= np.where(packed[row] > 0, np.uint32(bit), np.uint32(0))
     return packed[0].copy(), flags
 
@@ -212,17 +266,22 @@ def eval_loss_sharded(trees, shard, options, n_total=None, *, denom=None, group=
     """Losses of every tree over the union of all ranks' row shards -> (losses[T], complete[bool]),
     the same on every rank.  Collective: every rank calls it with the same trees.
 
-    With a device communicator (init_device_comm) this is one `sr_eval_loss_sharded` call.  Otherwise
-    the protocol runs over the gloo `group` on host arrays: `partials_fn(tb)` -> this shard's packed
-    [4, n_trees] partials (default: the GPU call), `exact_fn(tb, tree_list, max_checks, row_offset)`
-    -> [n_list, max_checks, n_ranges] folds (default: the GPU call).  A failure on one rank is
-    all-reduced as an error word, so every rank raises instead of waiting in a collective."""
+    With a library communicator (init_device_comm: RCCL; init_host_comm: gloo) this is one
+    `sr_eval_loss_sharded` call.  Otherwise (CPU tests of the protocol, stand-ins for the GPU calls)
+    the protocol runs here over the gloo `group` on host arrays: `partials_fn(tb)` -> this shard's
+    packed [5, n_trees] partials (default: the GPU call), `exact_fn(tb, tree_list, max_checks,
+    row_offset)` -> [n_list, max_checks, n_ranges] folds (default: the GPU call); this restatement
+    stops at the overflow rule's bounds (no in-order fold across shards).  A failure on one rank is
+    all-reduced as an error word, so every rank raises instead of waiting in a collective.  `denom`
+    applies to this restatement only (the library divides by the shards' n or Σw)."""
     import torch.distributed as dist
 
     full = shard.full
     tb = _as_batch(trees, full.dtype)
     ctx = peek_context()
     if partials_fn is None and exact_fn is None and getattr(ctx, "has_comm", False):
+        if denom is not None:
+            raise ValueError("the library's sharded call divides by the shards' own n or Σw; `denom` is not supported")
         _check_group(ctx, group)
         nt = tb.n_trees
         s = tb.to_struct()
@@ -249,21 +308,21 @@ def eval_loss_sharded(trees, shard, options, n_total=None, *, denom=None, group=
         raise ValueError(f"n_total {n_total} != the shards' {int(offs[-1])} rows")
     partials_fn = partials_fn or (lambda tb_: gpu_partials_packed(tb_, shard, options, n_total))
     nt = tb.n_trees
-    buf = np.zeros(4 * nt + 1, dtype=np.float64)
+    buf = np.zeros(N_PACKED * nt + 1, dtype=np.float64)
     err = None
     try:
-        buf[:4 * nt] = np.asarray(partials_fn(tb), dtype=np.float64).reshape(-1)
+        buf[:N_PACKED * nt] = np.asarray(partials_fn(tb), dtype=np.float64).reshape(-1)
     except Exception as e:  # noqa: BLE001 - every rank must still enter the collective
         err = e
         buf[:] = 0.0
         buf[-1] = 1.0
-    # the path's one exchange step: every rank's [4, n_trees] partials (and error words), summed
+    # the path's one exchange step: every rank's [5, n_trees] partials (and error words), summed
     buf = _allreduce_host(buf, group)
     if err is not None:
         raise err
     if buf[-1] != 0.0:
         raise RuntimeError("the row-sharded step failed on a peer rank")
-    sums, flags = unpack_flags(buf[:4 * nt].reshape(4, nt))
+    sums, flags = unpack_flags(buf[:N_PACKED * nt].reshape(N_PACKED, nt))
     big = np.nonzero(((flags & (_lib.SR_FLAG_NONFINITE | _lib.SR_FLAG_STATIC)) == 0) &
                      ((flags & _lib.SR_FLAG_BIG) != 0))[0]
     ok = None

@@ -15,11 +15,33 @@ for p in (ROOT, PKG, os.path.join(ROOT, "oracle")):
         sys.path.insert(0, p)
 
 
+def _lib_is_current():
+    """libsr_amd.so was built from exactly these sources: the hash its Makefile wrote beside it equals
+    the hash of the sources here (a GPU-box snapshot carries the library but no object files, so make
+    alone would rebuild everything)."""
+    import glob
+    import hashlib
+
+    stamp = os.path.join(PKG, "lib", "libsr_amd.so.srchash")
+    if not (os.path.exists(stamp) and os.path.exists(os.path.join(PKG, "lib", "libsr_amd.so"))):
+        return False
+    files = sorted(glob.glob("csrc/*", root_dir=PKG) + ["../include/sr_amd.h", "Makefile"])
+    h = hashlib.sha256()
+    for f in files:
+        with open(os.path.join(PKG, f), "rb") as fh:
+            h.update(fh.read())
+    with open(stamp) as fh:
+        return fh.read().strip() == h.hexdigest()
+
+
 def _ensure_built():
-    """Always run the (incremental) builds: a stale shipped .so must never stand in for HEAD's
-    sources.  make is a no-op when nothing changed.  Where no compiler exists (a GPU box without
-    hipcc never happens on this pool) the prebuilt libraries are used as they are."""
-    for d, jobs in ((PKG, "-j8"), (os.path.join(ROOT, "oracle"), "-j1")):
+    """Run the (incremental) builds unless the library provably matches the sources: a stale shipped
+    .so must never stand in for HEAD's sources.  Where no compiler exists (a GPU box without hipcc
+    never happens on this pool) the prebuilt libraries are used as they are."""
+    builds = [(os.path.join(ROOT, "oracle"), "-j1")]
+    if not _lib_is_current():
+        builds.insert(0, (PKG, "-j8"))
+    for d, jobs in builds:
         try:
             subprocess.run(["make", "-s", jobs, "-C", d], check=True)
         except FileNotFoundError:

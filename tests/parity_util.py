@@ -43,10 +43,13 @@ def loss_tolerance(orc, tb, X, y, w=None, loss_kind=0, loss_param=0.0, rel_bar=R
 
 
 def assert_losses_within(loss, ref_loss, comp, tol, what=""):
-    """Every complete tree: |device - oracle| <= tol (per tree)."""
+    """Every complete tree: |device - oracle| <= tol (per tree), and +Inf exactly where the oracle has
+    +Inf (a loss fold that overflows; an Inf oracle loss must not widen the bar to Inf)."""
     loss = np.asarray(loss, dtype=np.float64)
     ref = np.asarray(ref_loss, dtype=np.float64)
     comp = np.asarray(comp, dtype=bool)
+    inf_mism = np.nonzero(comp & (np.isinf(loss) != np.isinf(ref)))[0]
+    assert len(inf_mism) == 0, (what, "Inf mismatch", [(int(k), float(loss[k]), float(ref[k])) for k in inf_mism[:5]])
     with np.errstate(invalid="ignore"):
         err = np.where(loss == ref, 0.0, np.abs(loss - ref))  # equal infinities (a mean that overflows) agree
     bad = np.nonzero(comp & ~(err <= tol))[0]

@@ -28,7 +28,7 @@ def test_header_symbols_exported():
 
 
 def test_version_and_error_string():
-    assert _lib.lib.sr_version() == 1
+    assert _lib.lib.sr_version() == 2
     rc = _lib.lib.sr_shutdown(None)
     assert rc == 0
     h = ctypes.c_void_p()

@@ -61,7 +61,7 @@ def _worker(rank, world, port, q, mode="rows"):
         tbig = np.float32(3.4028235e38 / (2.0 * n))
 
         def partials(tb_):
-            packed = np.zeros((4, tb_.n_trees))
+            packed = np.zeros((5, tb_.n_trees))
             for k in range(tb_.n_trees):
                 out, _ = orc.eval_tree_array(tb_, k, Xs)
                 if not np.all(np.isfinite(out)):

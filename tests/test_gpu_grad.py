@@ -144,3 +144,35 @@ def test_bfgs_batch_recovers_constants():
     for k in np.nonzero(~improved)[0]:
         co = tb.constant_offsets()
         np.testing.assert_array_equal(new_tb.get_constants()[co[k]:co[k + 1]], tb.get_constants()[co[k]:co[k + 1]])
+
+
+def test_grad_f64_many_features_deep_trees_weighted():
+    """Float64 with 10 features, weights, maxsize 30 and unary operators — trees of
+    stack depth 3 and two-constant trees in one batch.  The 8-rows-per-lane buckets' LDS operand stacks
+    do not fit 160 KiB there; those buckets must fall back to one row per lane instead of failing, and
+    the gradient must still match central finite differences of the f64 oracle."""
+    opts = Options(binary_operators=["+", "-", "*", "/"], unary_operators=["cos", "exp", "sin"])
+    rng = np.random.default_rng(12)
+    nf = 10
+    X = rng.standard_normal((nf, 1500))
+    y = np.cos(X[0]) + X[1] * X[2]
+    w = rng.uniform(0.5, 2.0, 1500)
+    trees = gen_random_population(300, opts, nf, max_size=30, seed=13)
+    trees += [parse_expression("cos(cos(x1 * 1.5) + sin(x2 * 0.5)) * (x3 + (x4 - x5 * x6))", opts)]
+    tb = flatten_trees(trees, np.float64)
+    loss, g, comp = eval_grad_batch(tb, Dataset(X, y, weights=w), opts)
+    g_fd, _, comp_o, fd_err = Oracle.from_options(opts).loss_grad_fd(tb, X, y, w, with_error=True)
+    assert np.array_equal(comp, comp_o)
+    co = tb.constant_offsets()
+    checked = 0
+    for t in np.nonzero(comp)[0]:
+        a, b, e = g[co[t]:co[t + 1]], g_fd[co[t]:co[t + 1]], fd_err[co[t]:co[t + 1]]
+        if len(a) == 0:
+            continue
+        scale = max(1.0, float(np.abs(b).max()))
+        if e.max() > 1e-6 * scale:
+            continue
+        # (10 features and weights: the finite differences' own rounding error is ~1e-6 here)
+        assert np.all(np.abs(a - b) <= 2e-5 * scale), (t, a, b)
+        checked += 1
+    assert checked > 50

@@ -532,3 +532,20 @@ def test_row_sharded_packed_with_exact_path():
     assert np.max(_rel(loss[full_comp], full_loss[full_comp]), initial=0.0) < 1e-6
     _, oc = Oracle.from_options(opts).eval_loss_batch(tb, X, y, n_threads=8)
     assert np.array_equal(comp, oc)
+
+
+def test_wide_f64_dataset_large_view_falls_back_to_classic_kernel():
+    """Float64 over >= 2^17 rows defaults to the 8-rows/lane register-stack kernel,
+    whose X tile (4096 (nf + 1) bytes) passes 160 KiB at ~40 features; such a call must run the classic
+    kernel instead of failing, and agree with the oracle."""
+    opts = Options(**C2_OPTS)
+    nf, n = 48, 1 << 17
+    rng = np.random.default_rng(44)
+    X = rng.standard_normal((nf, n))
+    y = np.cos(X[3]) + X[40] ** 2
+    tb = flatten_trees(gen_random_population(200, opts, nf, max_size=20, dtype=np.float64, seed=44), np.float64)
+    loss, comp = eval_loss_batch(tb, Dataset(X, y), opts)
+    orc = Oracle.from_options(opts)
+    tol, o_loss, o_comp, _ = loss_tolerance(orc, tb, X, y, rel_bar=1e-10)
+    assert np.array_equal(comp, o_comp)
+    assert_losses_within(loss, o_loss, comp, tol, "wide f64")

@@ -61,7 +61,7 @@ def test_sharded_rccl_world1_matches_single_gpu():
         ds = Dataset(X, y)
 
         packed = gpu_partials_allreduce(tb, ds, opts, n)
-        assert packed.shape == (4, tb.n_trees)
+        assert packed.shape == (5, tb.n_trees)
         assert np.any(packed[2] > 0), "no tree took the BIG (exact-sum) path"
 
         ref_loss, ref_comp = eval_loss_batch(tb, ds, opts)
