@@ -131,6 +131,17 @@ int sr_eval_loss_batch(sr_ctx* ctx, const sr_dataset* ds, int opset_id, const sr
                        uint8_t* out_complete);
 
 /*
+ * The same for trees on different row views in ONE call: tree t is scored on the n_views x view_len
+ * row array's view tree_view[t] (rows view_rows[tree_view[t] * view_len + i], 0-based, may repeat).  This
+ * is SymbolicRegression's batching with one minibatch per island (src/SingleIteration.jl:40, 77;
+ * src/Dataset.jl:303-304): the children of every island in one launch, each on its own island's rows.
+ * Results equal sr_eval_loss_batch per view.
+ */
+int sr_eval_loss_batch_views(sr_ctx* ctx, const sr_dataset* ds, int opset_id, const sr_tree_batch* trees,
+                             const int32_t* tree_view, int n_views, const int64_t* view_rows, int64_t view_len,
+                             int loss_kind, void* out_loss, uint8_t* out_complete);
+
+/*
  * Batched eval_tree_array (src/InterfaceDynamicExpressions.jl:58-88): predictions
  * out_pred[n_trees][n_rows] (dataset dtype, row-major per tree) and complete flags.
  */
@@ -254,6 +265,12 @@ int sr_dataset_denominator(const sr_dataset* ds, double* denom);
 int sr_eval_grad_batch(sr_ctx* ctx, const sr_dataset* ds, int opset_id, const sr_tree_batch* trees,
                        const int64_t* row_idx, int64_t n_idx, int loss_kind, void* out_loss,
                        void* out_grad, uint8_t* out_complete);
+
+/* sr_eval_grad_batch over several row views (as sr_eval_loss_batch_views): the constant optimisation of
+ * every island's members in one lock-step pass, each on its island's minibatch. */
+int sr_eval_grad_batch_views(sr_ctx* ctx, const sr_dataset* ds, int opset_id, const sr_tree_batch* trees,
+                             const int32_t* tree_view, int n_views, const int64_t* view_rows, int64_t view_len,
+                             int loss_kind, void* out_loss, void* out_grad, uint8_t* out_complete);
 
 /*
  * Host-only dry run of the tree compiler (no device needed): compile `trees` for an operator set

@@ -12,8 +12,11 @@ function cites the reference code it restates:
   src/Population.jl:109-159             best_of_sample (bottomk_fast / argmin_fast, src/Utils.jl)
   src/SingleIteration.jl:19-139         s_r_cycle, optimize_and_simplify_population
   src/SymbolicRegression.jl:1040-1140   the head's per-island bookkeeping, migrate!, move_window!
-Scores come from a caller-supplied ``loss_fn(trees) -> losses`` (tests pass the C oracle).
-Constant optimisation is not restated here (the tests run with should_optimize_constants=False).
+Scores come from a caller-supplied ``loss_fn(trees, rows) -> losses`` (tests pass the C oracle): rows is
+None (the full dataset) or, with ``batching``, one array of row indices per tree — its island's
+minibatch, ``batch(dataset, batch_size)`` drawn per island per s_r_cycle (src/SingleIteration.jl:40;
+src/Dataset.jl:303-304: rows with replacement).  Constant optimisation is not restated here (the tests
+run with should_optimize_constants=False).
 Only ``tests/`` import this module.
 """
 from __future__ import annotations
@@ -454,6 +457,16 @@ MUTATIONS = ("mutate_constant", "mutate_operator", "mutate_feature", "swap_opera
              "insert_node", "delete_node", "simplify", "randomize", "do_nothing", "optimize")
 
 
+BATCH_KEY = 0x6261746368  # the minibatch streams' key (csrc/sr_search.cpp draw_batch)
+
+
+def draw_batch(seed, iteration, island, npop, salt, batch_size, n_rows):
+    """The rows of island `island`'s minibatch in iteration `iteration` (salt 0: its s_r_cycle, 1: its
+    constant optimisation): batch_size rows with replacement from their own xoshiro256** stream."""
+    r = Rng(seed ^ BATCH_KEY, (iteration * npop + island) * 2 + salt)
+    return np.array([r.below(n_rows) for _ in range(batch_size)], dtype=np.int64)
+
+
 class SearchOracle:
     def __init__(self, options, so, nfeatures, n_rows, T, seed, loss_fn):
         self.o, self.so, self.T = options, so, T
@@ -484,11 +497,11 @@ class SearchOracle:
             v = T(T(loss) / norm)
             return T(v + T(np.float32(np.float32(complexity) * np.float32(self.o.parsimony))))
 
-    def score(self, trees):
+    def score(self, trees, rows=None):
         if not trees:
             return [], []
         self.calls += 1
-        losses = np.asarray(self.loss_fn(trees), dtype=self.T)
+        losses = np.asarray(self.loss_fn(trees, rows), dtype=self.T)
         return list(losses), [self.cost_of(losses[k], trees[k].count_nodes()) for k in range(len(trees))]
 
     def normalized(self):
@@ -650,15 +663,20 @@ class SearchOracle:
                     if ok:
                         break
                 plans.append(["cross" if ok else "cross_fail", i, a1, a2, c1, c2])
+        prow = []  # each pending tree's island minibatch (batching)
         for pl in plans:
             if pl[0] == "mut":
                 pl.append(len(pending))
                 pending.append(pl[3])
+                prow.append(pl[1])
             elif pl[0] == "cross":
                 pl.append(len(pending))
                 pending.extend([pl[4], pl[5]])
-        losses, costs = self.score(pending)
-        self.num_evals += len(pending)
+                prow.extend([pl[1], pl[1]])
+        rows = [self.batch_rows[i] for i in prow] if self.o.batching else None
+        losses, costs = self.score(pending, rows)
+        frac = self.o.batch_size / self.n_rows if self.o.batching else 1.0
+        self.num_evals += len(pending) * frac
         for pl in plans:
             kind, i = pl[0], pl[1]
             rng = self.rngs[i]
@@ -729,7 +747,7 @@ class SearchOracle:
         self.head_maxsize = self.cur_maxsize_now()
         self.snap = [self.normalized() for _ in range(npop)]
         self.cur_maxsize = [self.head_maxsize] * npop
-        bl = np.asarray(self.loss_fn([Node(val=T(0))]), dtype=T)[0]
+        bl = np.asarray(self.loss_fn([Node(val=T(0))], None), dtype=T)[0]
         self.calls += 1
         self.baseline, self.use_baseline = (T(bl), True) if np.isfinite(bl) else (T(1), False)
         trees, who = [], []
@@ -755,6 +773,10 @@ class SearchOracle:
         o = self.o
         npop = o.populations
         self.best_seen = [[None] * o.maxsize for _ in range(npop)]
+        if self.o.batching:  # one minibatch per island for this iteration's s_r_cycle
+            it = getattr(self, "iteration", 0)
+            self.batch_rows = [draw_batch(self.seed, it, i, npop, 0, self.o.batch_size, self.n_rows)
+                               for i in range(npop)]
         ncyc = o.ncycles_per_iteration
         n_evol = -(-o.population_size // o.tournament_selection_n)
         for c in range(ncyc):
@@ -775,9 +797,22 @@ class SearchOracle:
                 if self.so.should_simplify:
                     m.tree = simplify(m.tree, self.sp)
                     m.complexity = m.tree.count_nodes()
+        if self.o.batching:
+            # finalize_costs on the full dataset (src/Population.jl:182-196), and the best-seen members
+            # re-scored likewise (_dispatch_s_r_cycle), in one call: every island's members, then its
+            # best-seen by size
+            ms = []
+            for i in range(npop):
+                ms.extend(self.pops[i])
+                ms.extend(m for m in self.best_seen[i] if m is not None)
+            losses, costs = self.score([m.tree for m in ms])
+            for m, l, c in zip(ms, losses, costs):
+                m.loss, m.cost = l, c
+            self.num_evals += len(ms)
         for i in range(npop):
             for m in self.pops[i]:
                 m.parent, m.ref = m.ref, self.ref(i)
+        self.iteration = getattr(self, "iteration", 0) + 1
 
     def hof_update(self, m):
         s = m.complexity

@@ -406,13 +406,25 @@ struct ShardCtl {
   int64_t min_rows;
 };
 
+// Several row views in one LOSS call (sr_eval_loss_batch_views): tree t is scored on the rows
+// view_rows[tree_view[t] * view_len ...] (the caller's row_idx array holds n_views views of view_len rows).
+struct ViewSpec {
+  const int32_t* tree_view;
+  int n_views;
+  int64_t view_len;
+};
+
 template <typename T>
 int run_batch(sr_ctx* ctx, const sr_dataset* ds, int opset_id, const sr_tree_batch* trees, const int64_t* row_idx,
               int64_t n_idx, int64_t n_total, int loss_kind, int mode, SrProgramBatch<T>* prog, Grid* grid_out,
-              bool allow_derived = false, const ShardCtl* shard = nullptr) {
+              bool allow_derived = false, const ShardCtl* shard = nullptr, const ViewSpec* views = nullptr) {
   const bool gather = row_idx != nullptr && n_idx > 0;
   const int64_t n_eval = gather ? n_idx : ds->n;
   if (n_eval <= 0) return set_error(SR_ERR_INVALID_ARG, "no rows to evaluate");
+  // several views: one launch, its tree groups view-pure (SrSegment); rows uploaded for every view
+  const bool multi = views != nullptr && gather && mode == SR_MODE_LOSS;
+  const int64_t n_rows_up = multi ? int64_t(views->n_views) * n_idx : n_idx;
+  if (multi) allow_derived = false;
   int lkind = 0;
   double lparam = 0.0;
   if (decode_loss(ctx, loss_kind, &lkind, &lparam) != SR_OK) return SR_ERR_INVALID_ARG;
@@ -450,7 +462,9 @@ int run_batch(sr_ctx* ctx, const sr_dataset* ds, int opset_id, const sr_tree_bat
   // each) alternate over the two streams; they cost kernel time on complete-heavy populations.
   constexpr int64_t kChunkTrees = 2048;
   int n_chunks = 1;
-  if (mode == SR_MODE_LOSS && ctx->chunks == 2) {
+  if (multi) {
+    // (one chunk: the segments cover the whole launch)
+  } else if (mode == SR_MODE_LOSS && ctx->chunks == 2) {
     n_chunks = nt / ctx->first_chunk >= kChunkTrees / 2 ? 2 : 1;  // the small first chunk holds >= 1024 trees
   } else if (mode == SR_MODE_LOSS && ctx->chunks > 2) {
     const int64_t k = nt / kChunkTrees;
@@ -472,7 +486,9 @@ int run_batch(sr_ctx* ctx, const sr_dataset* ds, int opset_id, const sr_tree_bat
   const size_t o_bad = align256(o_off + (size_t(nt) + 1) * sizeof(uint32_t));
   const size_t o_perm = align256(o_bad + size_t(nt) + 16);
   const size_t o_end = align256(o_perm + (size_t(nt) + 1) * sizeof(uint32_t));
-  const size_t prog_bytes = o_end + (size_t(nt) + 1) * sizeof(uint32_t);
+  const size_t o_seg = align256(o_end + (size_t(nt) + 1) * sizeof(uint32_t));
+  const size_t n_seg_cap = multi ? size_t(views->n_views) : 0;
+  const size_t prog_bytes = o_seg + n_seg_cap * sizeof(SrSegment);
   SR_HIP_CHECK(ctx->prog.ensure(prog_bytes));
   SR_HIP_CHECK(ctx->h_prog.ensure(prog_bytes, s, ctx->stream2));
   char* const dprog = ctx->prog.as<char>();  // (re-pointed at the staging buffer below for host_prog)
@@ -497,7 +513,7 @@ int run_batch(sr_ctx* ctx, const sr_dataset* ds, int opset_id, const sr_tree_bat
   ctx->d_out_flag = reinterpret_cast<uint32_t*>((host_out ? ctx->h_outs.as<char>() : ctx->outs.as<char>()) +
                                                 ctx->outs_flag_off);
   if (mode == SR_MODE_PRED) SR_HIP_CHECK(ctx->pred.ensure(size_t(nt) * size_t(n_eval) * sizeof(T) + 16));
-  const bool use_hint = ctx->dead_hints && mode == SR_MODE_LOSS && n_rb > 1;
+  const bool use_hint = ctx->dead_hints && mode == SR_MODE_LOSS && n_rb > 1;  // (hints are per position)
   if (use_hint) {
     // epoch-tagged hints: each call marks dead positions with its own epoch, so the array needs a
     // reset only when (re)allocated or when the epoch counter wraps
@@ -514,17 +530,21 @@ int run_batch(sr_ctx* ctx, const sr_dataset* ds, int opset_id, const sr_tree_bat
   }
   // dead-tree probe: the first kProbeTiles row tiles of the view, hints only (scratch partials)
   constexpr int kProbeTiles = 4;
-  const bool use_probe = use_hint && ctx->probe && n_rb >= 16;  // (per chunk: its grid has >= 16 row blocks)
+  const bool use_probe = use_hint && ctx->probe && n_rb >= 16 && !multi;  // (per chunk: its grid has >= 16 row blocks)
   if (use_probe) {
     SR_HIP_CHECK(ctx->probe_sum.ensure(size_t(nt) * kProbeTiles * sizeof(double) + 8));
     SR_HIP_CHECK(ctx->probe_flag.ensure(size_t(nt) * kProbeTiles * sizeof(uint32_t) + 4));
   }
   if (gather) {
-    for (int64_t i = 0; i < n_idx; ++i)
+    for (int64_t i = 0; i < n_rows_up; ++i)
       if (row_idx[i] < 0 || row_idx[i] >= ds->n)
         return set_error(SR_ERR_INVALID_ARG, "row index " + std::to_string(row_idx[i]) + " out of range");
-    SR_HIP_CHECK(ctx->row_idx.ensure(size_t(n_idx) * sizeof(int64_t)));
+    SR_HIP_CHECK(ctx->row_idx.ensure(size_t(n_rows_up) * sizeof(int64_t)));
   }
+  if (multi)
+    for (int64_t t = 0; t < nt; ++t)
+      if (views->tree_view[t] < 0 || views->tree_view[t] >= views->n_views)
+        return set_error(SR_ERR_INVALID_ARG, "tree " + std::to_string(t) + ": view index out of range");
 
   prog->code.clear();
   prog->offsets.assign(size_t(nt) + 1, 0);
@@ -553,7 +573,7 @@ int run_batch(sr_ctx* ctx, const sr_dataset* ds, int opset_id, const sr_tree_bat
   ctx->timed_last = ctx->timing != 0;
   if (ctx->timed_last) SR_HIP_CHECK(hipEventRecord(ctx->ev_start, s));
   if (gather)
-    SR_HIP_CHECK(hipMemcpyAsync(ctx->row_idx.p, row_idx, size_t(n_idx) * sizeof(int64_t), hipMemcpyHostToDevice, s));
+    SR_HIP_CHECK(hipMemcpyAsync(ctx->row_idx.p, row_idx, size_t(n_rows_up) * sizeof(int64_t), hipMemcpyHostToDevice, s));
   // derived columns (LOAD_DERIVED): for the BASIC-tier deferred-check loss kernels over many rows,
   // every unary(feature) node of a transcendental shared by several trees is evaluated once for the
   // call.  Chosen from a sample of the batch; not when the data itself needs tracked feature loads.
@@ -651,9 +671,12 @@ int run_batch(sr_ctx* ctx, const sr_dataset* ds, int opset_id, const sr_tree_bat
       if (sort)
         for (uint32_t v : cost) cmax = v > cmax ? v : cmax;
       const size_t nkey = size_t(cmax) + 1;
-      std::vector<uint32_t> start(2 * nkey + 1, 0);
+      // several views: the view first (each view's trees contiguous: its own segment of tree groups)
+      const size_t n_cls = multi ? size_t(views->n_views) : 2;
+      std::vector<uint32_t> start(n_cls * nkey + 1, 0);
       auto key = [&](int64_t i) -> size_t {
-        const size_t cls = (Rv > 0 && pc.depth[size_t(i)] > SR_VSTK_SLOTS) ? 1 : 0;
+        const size_t cls = multi ? size_t(views->tree_view[t0 + i])
+                                 : ((Rv > 0 && pc.depth[size_t(i)] > SR_VSTK_SLOTS) ? 1 : 0);
         return cls * nkey + (sort ? size_t(cmax - cost[size_t(i)]) : 0);
       };
       for (int64_t i = 0; i < nc; ++i) ++start[key(i) + 1];
@@ -664,7 +687,7 @@ int run_batch(sr_ctx* ctx, const sr_dataset* ds, int opset_id, const sr_tree_bat
       // waves still get equal work).  Contiguous cost ranks made the first groups' workgroups several
       // times longer than the last groups' and the launch ended on a tail of heavy workgroups (C2's
       // complete trees: 4.36 ms with contiguous groups of 128, 3.32 unsorted).
-      if (sort && ctx->balance_groups) {
+      if (sort && ctx->balance_groups && !multi) {
         auto deal = [&](int64_t p0, int64_t np, int Rc, int depth_c) {
           if (np <= 1) return;
           const Grid gc = make_grid<T>(n_eval, np, Rc, W, int(ds->nf), depth_c, 0, ds->w != nullptr, ctx->tree_group,
@@ -696,10 +719,34 @@ int run_batch(sr_ctx* ctx, const sr_dataset* ds, int opset_id, const sr_tree_bat
         at += e - b;
       }
     }
+    // several views: one segment per view present (launch positions in view order), tree groups of the
+    // launch's G, blocks in segment order
+    int n_seg = 0;
+    int64_t seg_blocks = 0;
+    if (multi && nc > 0) {
+      const Grid gm = make_grid<T>(n_eval, nc, R, W, int(ds->nf), depth, 0, ds->w != nullptr, ctx->tree_group,
+                                   ctx->max_row_blocks);
+      SrSegment* hs = reinterpret_cast<SrSegment*>(hprog + o_seg);
+      for (int64_t p = 0; p < nc;) {
+        const int v = views->tree_view[t0 + h_perm[t0 + p]];
+        int64_t q = p;
+        while (q < nc && views->tree_view[t0 + h_perm[t0 + q]] == v) ++q;
+        SrSegment sg{};
+        sg.block0 = int(seg_blocks);
+        sg.pos0 = int(p);
+        sg.n_pos = int(q - p);
+        sg.groups = int((q - p + gm.G - 1) / gm.G);
+        sg.row_off = int64_t(v) * n_idx;
+        hs[n_seg++] = sg;
+        seg_blocks += int64_t(sg.groups) * gm.n_row_blocks;
+        p = q;
+      }
+    }
     if (host_prog) {
       // the kernel reads the staging image itself
     } else if (n_chunks == 1) {  // the whole staging image (code, offsets, static_bad, order): one DMA
-      SR_HIP_CHECK(hipMemcpyAsync(dprog, hprog, o_end + size_t(nc) * sizeof(uint32_t), hipMemcpyHostToDevice, cs));
+      const size_t img = multi ? o_seg + size_t(n_seg) * sizeof(SrSegment) : o_end + size_t(nc) * sizeof(uint32_t);
+      SR_HIP_CHECK(hipMemcpyAsync(dprog, hprog, img, hipMemcpyHostToDevice, cs));
     } else {
       if (ncode)
         SR_HIP_CHECK(hipMemcpyAsync(static_cast<SrIns<T>*>(ctx->d_code) + code_base, h_code + code_base,
@@ -777,6 +824,13 @@ int run_batch(sr_ctx* ctx, const sr_dataset* ds, int opset_id, const sr_tree_bat
         a.code_lds = int(std::min(maxspan, cap));
         if (a.code_lds < 64) a.code_lds = 0;
       }
+      int64_t n_blocks = g.n_blocks;
+      if (multi) {  // (one launch over the whole chunk: the segments computed above)
+        a.segs = reinterpret_cast<const SrSegment*>((host_prog ? hprog : dprog) + o_seg);
+        a.n_segs = n_seg;
+        n_blocks = seg_blocks;
+        if (n_blocks > 0x7fffffff) return set_error(SR_ERR_INVALID_ARG, "grid too large");
+      }
       const bool direct = mode == SR_MODE_LOSS && g.n_row_blocks == 1;
       if (direct) {  // the interpreter writes the final per-tree values; no reduce launch
         a.out_sum = ctx->d_out_sum + t0;
@@ -820,7 +874,7 @@ int run_batch(sr_ctx* ctx, const sr_dataset* ds, int opset_id, const sr_tree_bat
       SR_HIP_CHECK(hipMemsetAsync(ctx->stamps.p, 0, size_t(ctx->n_stamps) * sizeof(uint64_t), cs));
       a.stamps = ctx->stamps.as<uint64_t>();
 #endif
-      SR_HIP_CHECK(sr_launch_eval<T>(a, mode, gather, tier, Rc, g.W, vstk, int(g.n_blocks), cs));
+      SR_HIP_CHECK(sr_launch_eval<T>(a, mode, gather, tier, Rc, g.W, vstk, int(n_blocks), cs));
       if (!direct)
         SR_HIP_CHECK(sr_launch_reduce(a.part_sum, a.part_flag, int(np), g.n_row_blocks, a.perm,
                                     ctx->d_bad + t0, ctx->d_out_sum + t0, ctx->d_out_flag + t0, cs));
@@ -1024,7 +1078,7 @@ JlLevels jl_levels(int64_t n) {
 template <typename T>
 int run_exact(sr_ctx* ctx, const sr_dataset* ds, const SrProgramBatch<T>& prog, const int64_t* row_idx,
               int64_t n_idx, const int64_t* list, int64_t n_list, int max_checks, const std::vector<JlRange>& ranges,
-              T* host_vals, uint8_t* host_finite = nullptr) {
+              T* host_vals, uint8_t* host_finite = nullptr, int64_t dev_row_off = 0) {
   if (n_list == 0 || max_checks == 0 || ranges.empty()) return SR_OK;
   const bool gather = row_idx != nullptr && n_idx > 0;
   const int64_t n_eval = gather ? n_idx : ds->n;
@@ -1090,7 +1144,7 @@ int run_exact(sr_ctx* ctx, const sr_dataset* ds, const SrProgramBatch<T>& prog, 
     a.n_trees = int(nb);
     a.trees_per_block = G;
     a.X = static_cast<const T*>(ds->X);
-    a.row_idx = gather ? ctx->row_idx.as<int64_t>() : nullptr;
+    a.row_idx = gather ? ctx->row_idx.as<int64_t>() + dev_row_off : nullptr;  // (this view's rows on the device)
     a.ld = ds->ld;
     a.n_rows = n_eval;
     a.nf = int(ds->nf);
@@ -1133,7 +1187,8 @@ int run_exact(sr_ctx* ctx, const sr_dataset* ds, const SrProgramBatch<T>& prog, 
 // passes isfinite(Julia sum).
 template <typename T>
 int exact_list_ok(sr_ctx* ctx, const sr_dataset* ds, const SrProgramBatch<T>& prog, const int64_t* row_idx,
-                  int64_t n_idx, const std::vector<int64_t>& list, std::vector<uint8_t>* list_ok) {
+                  int64_t n_idx, const std::vector<int64_t>& list, std::vector<uint8_t>* list_ok,
+                  int64_t dev_row_off = 0) {
   list_ok->assign(list.size(), 1);
   if (list.empty() || prog.max_checks == 0) return SR_OK;
   const bool gather = row_idx != nullptr && n_idx > 0;
@@ -1146,7 +1201,7 @@ int exact_list_ok(sr_ctx* ctx, const sr_dataset* ds, const SrProgramBatch<T>& pr
   // leaf folds combined in recursion order on the device: only the verdicts come back
   std::vector<uint8_t> fin(list.size() * size_t(mc));
   int rc = run_exact<T>(ctx, ds, prog, row_idx, n_idx, list.data(), int64_t(list.size()), mc, ranges, nullptr,
-                        fin.data());
+                        fin.data(), dev_row_off);
   if (rc != SR_OK) return rc;
   for (size_t i = 0; i < list.size(); ++i)
     for (int k = 0; k < mc; ++k) (*list_ok)[i] &= fin[i * size_t(mc) + size_t(k)];
@@ -1160,7 +1215,7 @@ int exact_list_ok(sr_ctx* ctx, const sr_dataset* ds, const SrProgramBatch<T>& pr
 template <typename T>
 void finalize(int64_t nt, const double* sums, const uint32_t* flags, double denom, const int64_t* list,
               int64_t n_list, const uint8_t* list_ok, T* out_loss, uint8_t* out_complete, int64_t n_terms = 0,
-              std::vector<int64_t>* fold_list = nullptr) {
+              std::vector<int64_t>* fold_list = nullptr, const double* denoms = nullptr) {
   std::vector<int64_t> pos;
   if (n_list > 0) {
     pos.assign(size_t(nt), -1);
@@ -1173,7 +1228,7 @@ void finalize(int64_t nt, const double* sums, const uint32_t* flags, double deno
       if (p >= 0 && list_ok && !list_ok[p]) ok = false;
     }
     out_complete[t] = ok ? 1 : 0;
-    out_loss[t] = ok ? T(sums[t] / denom) : T(INFINITY);
+    out_loss[t] = ok ? T(sums[t] / (denoms ? denoms[t] : denom)) : T(INFINITY);
     if (!ok) continue;
     const bool elem_inf = (flags[t] & SR_FLAG_ELEMINF) != 0;
     const int cls = n_terms > 0 ? sr_fold_class<T>(sums[t], elem_inf, n_terms) : (elem_inf ? SR_FOLD_INF : SR_FOLD_FINITE);
@@ -1268,19 +1323,26 @@ double view_denominator(const sr_dataset* ds, const int64_t* row_idx, int64_t n_
 // apply (negative weights: the fold is not monotone).
 inline int64_t fold_terms(const sr_dataset* ds, int64_t n_rows) { return (ds->w && ds->w_min < 0.0) ? 0 : n_rows; }
 
+// views (may be NULL): several row views in one call (sr_eval_loss_batch_views); row_idx then holds
+// views->n_views views of n_idx rows each.
 template <typename T>
 int eval_loss_impl(sr_ctx* ctx, const sr_dataset* ds, int opset_id, const sr_tree_batch* trees,
-                   const int64_t* row_idx, int64_t n_idx, int loss_kind, void* out_loss, uint8_t* out_complete) {
+                   const int64_t* row_idx, int64_t n_idx, int loss_kind, void* out_loss, uint8_t* out_complete,
+                   const ViewSpec* views = nullptr) {
   const int64_t nt = trees->n_trees;
   if (nt > 0 && (!out_loss || !out_complete)) return set_error(SR_ERR_INVALID_ARG, "NULL output buffers");
   const bool gather = row_idx != nullptr && n_idx > 0;
   const int64_t n_eval = gather ? n_idx : ds->n;
+  const int n_views = views ? views->n_views : 1;
+  auto view_of = [&](int64_t t) -> int { return views ? int(views->tree_view[t]) : 0; };
+  auto rows_of = [&](int v) -> const int64_t* { return gather ? row_idx + int64_t(v) * n_idx : nullptr; };
   auto t0 = std::chrono::steady_clock::now();
   ctx->start_phases(t0);
   SrProgramBatch<T> prog;
   Grid g;
   ctx->want_host_out = true;
-  int rc = run_batch<T>(ctx, ds, opset_id, trees, row_idx, n_idx, n_eval, loss_kind, SR_MODE_LOSS, &prog, &g, true);
+  int rc = run_batch<T>(ctx, ds, opset_id, trees, row_idx, n_idx, n_eval, loss_kind, SR_MODE_LOSS, &prog, &g, true,
+                        nullptr, views);
   ctx->want_host_out = false;
   if (rc != SR_OK) return rc;
   if (nt == 0) return SR_OK;
@@ -1308,23 +1370,45 @@ int eval_loss_impl(sr_ctx* ctx, const sr_dataset* ds, int opset_id, const sr_tre
   std::vector<int64_t> list;
   for (int64_t t = 0; t < nt; ++t)
     if ((flags[t] & (SR_FLAG_NONFINITE | SR_FLAG_STATIC)) == 0 && (flags[t] & SR_FLAG_BIG)) list.push_back(t);
-  std::vector<uint8_t> list_ok;
+  std::vector<uint8_t> list_ok(list.size(), 1);
   ctx->n_exact_last = int64_t(list.size());
   ctx->exact_kernel_ms = 0.0;
-  rc = exact_list_ok<T>(ctx, ds, prog, row_idx, n_idx, list, &list_ok);
-  if (rc != SR_OK) return rc;
-  ctx->mark_phase(3);
-  const double denom = view_denominator<T>(ds, row_idx, n_idx);
-  std::vector<int64_t> fold_list;
-  finalize<T>(nt, sums.data(), flags.data(), denom, list.data(), int64_t(list.size()), list_ok.data(),
-              static_cast<T*>(out_loss), out_complete, fold_terms(ds, n_eval), &fold_list);
-  ctx->n_fold_last = int64_t(fold_list.size());
-  if (!fold_list.empty()) {  // rare: the reference's own fold, in row order (sr_fold.h)
-    std::vector<T> fold;
-    rc = fold_exact<T>(ctx, ds, opset_id, trees, row_idx, n_idx, n_eval, loss_kind, fold_list, nullptr, &fold);
+  for (int v = 0; v < n_views && !list.empty(); ++v) {  // (each view's listed trees over its own rows)
+    std::vector<int64_t> lv;
+    std::vector<size_t> at;
+    for (size_t i = 0; i < list.size(); ++i)
+      if (view_of(list[i]) == v) {
+        lv.push_back(list[i]);
+        at.push_back(i);
+      }
+    if (lv.empty()) continue;
+    std::vector<uint8_t> ok;
+    rc = exact_list_ok<T>(ctx, ds, prog, rows_of(v), n_idx, lv, &ok, int64_t(v) * n_idx);
     if (rc != SR_OK) return rc;
-    for (size_t i = 0; i < fold_list.size(); ++i)
-      static_cast<T*>(out_loss)[fold_list[i]] = T(fold[i] / T(denom));  // mean: total / count, in T
+    for (size_t i = 0; i < lv.size(); ++i) list_ok[at[i]] = ok[i];
+  }
+  ctx->mark_phase(3);
+  std::vector<double> vden(static_cast<size_t>(n_views)), denoms;
+  for (int v = 0; v < n_views; ++v) vden[size_t(v)] = view_denominator<T>(ds, rows_of(v), n_idx);
+  if (views) {
+    denoms.resize(size_t(nt));
+    for (int64_t t = 0; t < nt; ++t) denoms[size_t(t)] = vden[size_t(view_of(t))];
+  }
+  std::vector<int64_t> fold_list;
+  finalize<T>(nt, sums.data(), flags.data(), vden[0], list.data(), int64_t(list.size()), list_ok.data(),
+              static_cast<T*>(out_loss), out_complete, fold_terms(ds, n_eval), &fold_list,
+              views ? denoms.data() : nullptr);
+  ctx->n_fold_last = int64_t(fold_list.size());
+  for (int v = 0; v < n_views && !fold_list.empty(); ++v) {  // rare: the reference's own fold, in row order (sr_fold.h)
+    std::vector<int64_t> fv;
+    for (int64_t t : fold_list)
+      if (view_of(t) == v) fv.push_back(t);
+    if (fv.empty()) continue;
+    std::vector<T> fold;
+    rc = fold_exact<T>(ctx, ds, opset_id, trees, rows_of(v), n_idx, n_eval, loss_kind, fv, nullptr, &fold);
+    if (rc != SR_OK) return rc;
+    for (size_t i = 0; i < fv.size(); ++i)
+      static_cast<T*>(out_loss)[fv[i]] = T(fold[i] / T(vden[size_t(v)]));  // mean: total / count, in T
   }
   ctx->mark_phase(4);
   auto t1 = std::chrono::steady_clock::now();
@@ -1476,10 +1560,11 @@ int upload_impl(sr_ctx* ctx, const void* X, int64_t nf, int64_t n, const void* y
 
 // Batched forward-mode gradient (sr_eval_grad_batch): exact loss + complete flags from the loss
 // kernel, then d loss / d constants of every complete tree from the tangent kernel.
+// views (may be NULL): several row views in one call (sr_eval_grad_batch_views), as eval_loss_impl.
 template <typename T>
 int eval_grad_impl(sr_ctx* ctx, const sr_dataset* ds, int opset_id, const sr_tree_batch* trees,
                    const int64_t* row_idx, int64_t n_idx, int loss_kind, void* out_loss, void* out_grad,
-                   uint8_t* out_complete) {
+                   uint8_t* out_complete, const ViewSpec* views = nullptr) {
   const SrOpset& ops = ctx->opsets[opset_id];
   for (uint32_t u : ops.unary)
     if (!sr_unary_grad_supported(u)) return set_error(SR_ERR_UNSUPPORTED_OP, "operator without a gradient rule");
@@ -1488,12 +1573,14 @@ int eval_grad_impl(sr_ctx* ctx, const sr_dataset* ds, int opset_id, const sr_tre
   int lkind = 0;
   double lparam = 0.0;
   if (decode_loss(ctx, loss_kind, &lkind, &lparam) != SR_OK) return SR_ERR_INVALID_ARG;
-  int rc = eval_loss_impl<T>(ctx, ds, opset_id, trees, row_idx, n_idx, loss_kind, out_loss, out_complete);
+  int rc = eval_loss_impl<T>(ctx, ds, opset_id, trees, row_idx, n_idx, loss_kind, out_loss, out_complete, views);
   if (rc != SR_OK) return rc;
   const int64_t nt = trees->n_trees;
   if (nt == 0) return SR_OK;
   const bool gather = row_idx != nullptr && n_idx > 0;
   const int64_t n_eval = gather ? n_idx : ds->n;
+  const int n_views = (views && gather) ? views->n_views : 1;
+  auto view_of = [&](int64_t t) -> int { return n_views > 1 ? int(views->tree_view[t]) : 0; };
   SrProgramBatch<T> prog;
   std::string err;
   rc = sr_compile_batch<T>(*trees, ops, n_eval, ds->nf, true, &prog, &err);
@@ -1524,20 +1611,57 @@ int eval_grad_impl(sr_ctx* ctx, const sr_dataset* ds, int opset_id, const sr_tre
     }
   }
   hipStream_t s = ctx->stream;
+  // the loss pass's in-order folds re-upload their own view's rows: put every view's rows back
+  if (gather && ctx->n_fold_last > 0) {
+    SR_HIP_CHECK(ctx->row_idx.ensure(size_t(n_views) * size_t(n_idx) * sizeof(int64_t)));
+    SR_HIP_CHECK(hipMemcpyAsync(ctx->row_idx.p, row_idx, size_t(n_views) * size_t(n_idx) * sizeof(int64_t),
+                                hipMemcpyHostToDevice, s));
+  }
+  // several views: each bucket's work items ordered by view (stable), one segment per view; the
+  // segments' tree groups (kWaves items each) and blocks are laid out below
+  constexpr int kWaves = 4;
+  std::vector<SrSegment> segs[kNB];
+  if (n_views > 1)
+    for (int b = 0; b < kNB; ++b) {
+      std::vector<size_t> ord(items[b].size());
+      for (size_t i = 0; i < ord.size(); ++i) ord[i] = i;
+      std::stable_sort(ord.begin(), ord.end(), [&](size_t x, size_t y) { return view_of(items[b][x]) < view_of(items[b][y]); });
+      std::vector<uint32_t> it2(ord.size()), k2(ord.size());
+      for (size_t i = 0; i < ord.size(); ++i) {
+        it2[i] = items[b][ord[i]];
+        k2[i] = k0s[b][ord[i]];
+      }
+      items[b].swap(it2);
+      k0s[b].swap(k2);
+      for (size_t p = 0; p < items[b].size();) {
+        const int v = view_of(items[b][p]);
+        size_t q = p;
+        while (q < items[b].size() && view_of(items[b][q]) == v) ++q;
+        SrSegment sg{};
+        sg.pos0 = int(p);
+        sg.n_pos = int(q - p);
+        sg.groups = int((q - p + kWaves - 1) / kWaves);
+        sg.row_off = int64_t(v) * n_idx;
+        segs[b].push_back(sg);
+        p = q;
+      }
+    }
   // one pinned staging image (programs, offsets, constants, constant offsets, every bucket's work
-  // items) -> ONE upload; every bucket's kernel and reduce go out back to back, their results come
-  // back in ONE copy, and the host waits once (round 3: four uploads, then per bucket an upload, a
-  // copy back and a wait)
+  // items and segments) -> ONE upload; every bucket's kernel and reduce go out back to back, their
+  // results come back in ONE copy, and the host waits once (round 3: four uploads, then per bucket an
+  // upload, a copy back and a wait)
   auto al = [](size_t x) { return (x + 255) & ~size_t(255); };
   const size_t o_code = 0;
   const size_t o_offs = al(o_code + prog.code.size() * sizeof(SrIns<T>));
   const size_t o_cons = al(o_offs + prog.offsets.size() * sizeof(uint32_t));
   const size_t o_coff = al(o_cons + consts.size() * sizeof(T));
-  size_t o_items[kNB], o_vals[kNB];
+  size_t o_items[kNB], o_vals[kNB], o_segs[kNB];
   size_t at = al(o_coff + prog.const_off.size() * sizeof(uint32_t)), n_vals_all = 0;
   for (int b = 0; b < kNB; ++b) {
     o_items[b] = at;
     at = al(at + 2 * items[b].size() * sizeof(uint32_t));
+    o_segs[b] = at;
+    at = al(at + segs[b].size() * sizeof(SrSegment));
     o_vals[b] = n_vals_all;
     n_vals_all += items[b].size() * size_t(kts[b]);
   }
@@ -1555,10 +1679,9 @@ int eval_grad_impl(sr_ctx* ctx, const sr_dataset* ds, int opset_id, const sr_tre
     std::copy(k0s[b].begin(), k0s[b].end(), d + items[b].size());
   }
   char* ds_ = ctx->g_code.as<char>();
-  SR_HIP_CHECK(hipMemcpyAsync(ds_, hs, stage_bytes, hipMemcpyHostToDevice, s));
   SR_HIP_CHECK(ctx->g_out.ensure(n_vals_all * sizeof(double) + 16));
-  const double denom = view_denominator<T>(ds, row_idx, n_idx);
-  constexpr int kWaves = 4;
+  std::vector<double> vden(static_cast<size_t>(n_views));
+  for (int v = 0; v < n_views; ++v) vden[size_t(v)] = view_denominator<T>(ds, gather ? row_idx + int64_t(v) * n_idx : nullptr, n_idx);
   size_t part_need = 0;
   struct Launch { int64_t n_rb, tiles_per_block, n_groups; int rows, depth; };
   Launch lc[kNB] = {};
@@ -1574,16 +1697,27 @@ int eval_grad_impl(sr_ctx* ctx, const sr_dataset* ds, int opset_id, const sr_tre
     if (rows == 0) return set_error(SR_ERR_TOO_DEEP, "gradient tile needs more than 160 KiB of LDS");
     const int64_t rows_per_tile = 64 * int64_t(rows);
     const int64_t n_tiles = (n_eval + rows_per_tile - 1) / rows_per_tile;
-    const int64_t n_groups = (ni + kWaves - 1) / kWaves;
+    int64_t n_groups = (ni + kWaves - 1) / kWaves;
+    if (!segs[b].empty()) {  // (view-pure groups: a few more than ni / kWaves)
+      n_groups = 0;
+      for (const SrSegment& sg : segs[b]) n_groups += sg.groups;
+    }
     int64_t n_rb = (4096 + n_groups - 1) / n_groups;
     if (n_rb > n_tiles) n_rb = n_tiles;
     if (n_rb < 1) n_rb = 1;
     const int64_t tiles_per_block = (n_tiles + n_rb - 1) / n_rb;
     n_rb = (n_tiles + tiles_per_block - 1) / tiles_per_block;
     if (n_rb * n_groups > 0x7fffffff) return set_error(SR_ERR_INVALID_ARG, "grid too large");
+    int64_t blk = 0;  // segments' first blocks
+    for (SrSegment& sg : segs[b]) {
+      sg.block0 = int(blk);
+      blk += int64_t(sg.groups) * n_rb;
+    }
+    if (!segs[b].empty()) std::memcpy(hs + o_segs[b], segs[b].data(), segs[b].size() * sizeof(SrSegment));
     lc[b] = Launch{n_rb, tiles_per_block, n_groups, rows, bdepth};
     part_need = std::max(part_need, size_t(n_rb) * size_t(ni) * size_t(kt));
   }
+  SR_HIP_CHECK(hipMemcpyAsync(ds_, hs, stage_bytes, hipMemcpyHostToDevice, s));
   // (buckets run one after another on the stream, so they share the partials buffer)
   SR_HIP_CHECK(ctx->g_part.ensure(part_need * sizeof(double) + 16));
   for (int b = 0; b < kNB; ++b) {
@@ -1612,6 +1746,10 @@ int eval_grad_impl(sr_ctx* ctx, const sr_dataset* ds, int opset_id, const sr_tre
     a.loss_kind = lkind;
     a.loss_param = T(lparam);
     a.part = ctx->g_part.as<double>();
+    if (!segs[b].empty()) {
+      a.segs = reinterpret_cast<const SrSegment*>(ds_ + o_segs[b]);
+      a.n_segs = int(segs[b].size());
+    }
     SR_HIP_CHECK(sr_launch_grad_any<T>(a, kt, gather, lc[b].rows, int(lc[b].n_rb * lc[b].n_groups), s));
     SR_HIP_CHECK(sr_launch_grad_reduce(a.part, int(lc[b].n_rb), int(size_t(ni) * kt), ctx->g_out.as<double>() + o_vals[b], s));
   }
@@ -1624,7 +1762,7 @@ int eval_grad_impl(sr_ctx* ctx, const sr_dataset* ds, int opset_id, const sr_tre
       const uint32_t t = items[b][i], k0 = k0s[b][i];
       const uint32_t nc = prog.n_consts[t];
       for (int q = 0; q < kt && k0 + uint32_t(q) < nc; ++q)
-        g[prog.const_off[t] + k0 + uint32_t(q)] = T(out[o_vals[b] + i * size_t(kt) + size_t(q)] / denom);
+        g[prog.const_off[t] + k0 + uint32_t(q)] = T(out[o_vals[b] + i * size_t(kt) + size_t(q)] / vden[size_t(view_of(t))]);
     }
   }
   return SR_OK;
@@ -2349,6 +2487,49 @@ int sr_eval_loss_batch(sr_ctx* ctx, const sr_dataset* ds, int opset_id, const sr
   if (ds->dtype == SR_DTYPE_F32)
     return eval_loss_impl<float>(ctx, ds, opset_id, trees, row_idx, n_idx, loss_kind, out_loss, out_complete);
   return eval_loss_impl<double>(ctx, ds, opset_id, trees, row_idx, n_idx, loss_kind, out_loss, out_complete);
+}
+
+// several row views in one call (per-island minibatches): validated here, ViewSpec below the ABI
+static int check_views(const sr_tree_batch* trees, const int32_t* tree_view, int n_views, const int64_t* view_rows,
+                       int64_t view_len) {
+  if (n_views < 1 || view_len < 1 || !view_rows || (trees->n_trees > 0 && !tree_view))
+    return set_error(SR_ERR_INVALID_ARG, "bad row views");
+  return SR_OK;
+}
+
+int sr_eval_loss_batch_views(sr_ctx* ctx, const sr_dataset* ds, int opset_id, const sr_tree_batch* trees,
+                             const int32_t* tree_view, int n_views, const int64_t* view_rows, int64_t view_len,
+                             int loss_kind, void* out_loss, uint8_t* out_complete) {
+  int rc = validate_common(ctx, ds, opset_id, trees);
+  if (rc != SR_OK) return rc;
+  if ((rc = check_views(trees, tree_view, n_views, view_rows, view_len)) != SR_OK) return rc;
+  Lock l(ctx);
+  SR_HIP_CHECK(hipSetDevice(ctx->device));
+  const ViewSpec vs{tree_view, n_views, view_len};
+  const ViewSpec* v = n_views > 1 ? &vs : nullptr;  // (one view: the plain gather path)
+  if (ds->dtype == SR_DTYPE_F32)
+    return eval_loss_impl<float>(ctx, ds, opset_id, trees, view_rows, view_len, loss_kind, out_loss, out_complete, v);
+  return eval_loss_impl<double>(ctx, ds, opset_id, trees, view_rows, view_len, loss_kind, out_loss, out_complete, v);
+}
+
+int sr_eval_grad_batch_views(sr_ctx* ctx, const sr_dataset* ds, int opset_id, const sr_tree_batch* trees,
+                             const int32_t* tree_view, int n_views, const int64_t* view_rows, int64_t view_len,
+                             int loss_kind, void* out_loss, void* out_grad, uint8_t* out_complete) {
+  int rc = validate_common(ctx, ds, opset_id, trees);
+  if (rc != SR_OK) return rc;
+  if ((rc = check_views(trees, tree_view, n_views, view_rows, view_len)) != SR_OK) return rc;
+  if (trees->n_trees > 0 && (!out_loss || !out_grad || !out_complete))
+    return set_error(SR_ERR_INVALID_ARG, "NULL output buffers");
+  if (!ds->y) return set_error(SR_ERR_INVALID_ARG, "dataset has no y");
+  Lock l(ctx);
+  SR_HIP_CHECK(hipSetDevice(ctx->device));
+  const ViewSpec vs{tree_view, n_views, view_len};
+  const ViewSpec* v = n_views > 1 ? &vs : nullptr;
+  if (ds->dtype == SR_DTYPE_F32)
+    return eval_grad_impl<float>(ctx, ds, opset_id, trees, view_rows, view_len, loss_kind, out_loss, out_grad,
+                                 out_complete, v);
+  return eval_grad_impl<double>(ctx, ds, opset_id, trees, view_rows, view_len, loss_kind, out_loss, out_grad,
+                                out_complete, v);
 }
 
 int sr_eval_tree_array(sr_ctx* ctx, const sr_dataset* ds, int opset_id, const sr_tree_batch* trees,

@@ -13,6 +13,14 @@ enum { SR_MODE_LOSS = 0, SR_MODE_PRED = 1, SR_MODE_EXACT = 2 };
 #endif
 enum { SR_TIER_BASIC = 0, SR_TIER_FULL = 1 };
 
+// One row view's launch positions in a several-view launch (sr_eval_loss_batch_views): positions
+// [pos0, pos0 + n_pos) in tree groups of trees_per_block, blocks [block0, block0 + groups x row blocks),
+// rows row_idx[row_off .. row_off + n_rows).
+struct SrSegment {
+  int block0, pos0, n_pos, groups;
+  int64_t row_off;
+};
+
 template <typename T>
 struct SrEvalArgs {
   // programs
@@ -62,6 +70,9 @@ struct SrEvalArgs {
   const int64_t* range_lo;
   const int64_t* range_hi;
   void* range_sums;
+  // several row views in one launch (GATHER LOSS; NULL: one view, blockIdx = row_block * n_groups + group)
+  const SrSegment* segs;
+  int n_segs;
   // -DSR_STAMPS builds only (latency analysis, tools/stamps.py): per wave, SR_NSTAMPS wall-clock
   // stamps at fixed points of the kernel, [block][wave][SR_NSTAMPS]; NULL otherwise
   uint64_t* stamps;
@@ -140,6 +151,8 @@ struct SrGradArgs {
   int loss_kind;
   T loss_param;
   double* part;              // [n_row_blocks][n_items][KT]
+  const SrSegment* segs;     // several row views (GATHER; positions = work items); NULL: one view
+  int n_segs;
 };
 
 // rows: rows per lane, sr_grad_rows_per_lane(kt) or 1 (sr_grad_launch_rows)

@@ -68,10 +68,29 @@ __global__ void __launch_bounds__(W * 64) sr_grad_kernel(const SrGradArgs<T> a) 
   T* stk = wsv + (a.w ? ROWS : 0);                             // [W][depth][NV][R][64]
   T* my_stk = stk + size_t(wave) * a.stack_depth * NV * R * 64 + lane;
 
-  const int tg = blockIdx.x % a.n_groups;
-  const int rb = blockIdx.x / a.n_groups;
-  const int item = tg * W + wave;
-  const bool active = item < a.n_items;
+  int tg, rb, item, item_end = a.n_items;
+  const int64_t* ridx = a.row_idx;  // GATHER: this block's row view
+  if (a.segs == nullptr) {
+    tg = int(blockIdx.x) % a.n_groups;
+    rb = int(blockIdx.x) / a.n_groups;
+    item = tg * W + wave;
+  } else {
+    // several row views in one launch (sr_eval_grad_batch_views): segment = one view's work items
+    int lo = 0, hi = a.n_segs - 1;
+    while (lo < hi) {
+      const int mid = (lo + hi + 1) >> 1;
+      if (a.segs[mid].block0 <= int(blockIdx.x)) lo = mid;
+      else hi = mid - 1;
+    }
+    const SrSegment sg = a.segs[lo];
+    const int local = int(blockIdx.x) - sg.block0;
+    tg = local % sg.groups;
+    rb = local / sg.groups;
+    item = sg.pos0 + tg * W + wave;
+    item_end = sg.pos0 + sg.n_pos;
+    ridx += sg.row_off;
+  }
+  const bool active = item < item_end;
   uint32_t pb = 0u, pe = 0u, k0 = 0u, cb = 0u, nconst = 0u;
   if (active) {
     const uint32_t t = a.item_tree[item];
@@ -99,7 +118,7 @@ __global__ void __launch_bounds__(W * 64) sr_grad_kernel(const SrGradArgs<T> a) 
     __syncthreads();
     for (int i = tid; i < ROWS; i += W * 64) {
       const int64_t v = row0 + i;
-      const int64_t src = GATHER ? a.row_idx[v < a.n_rows ? v : 0] : (v < a.n_rows ? v : 0);
+      const int64_t src = GATHER ? ridx[v < a.n_rows ? v : 0] : (v < a.n_rows ? v : 0);
       for (int f = 0; f < a.nf; ++f) xs[f * ROWS + i] = a.X[int64_t(f) * a.ld + src];
       ys[i] = a.y[src];
       if (weighted) wsv[i] = a.w[src];

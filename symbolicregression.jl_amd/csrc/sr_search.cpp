@@ -112,6 +112,22 @@ struct Flat {
     }
     offsets.push_back(offsets.back() + int64_t(t.size()));
   }
+  // the trees ks of this batch as a batch of their own (CPU scorers over several row views)
+  Flat take(const std::vector<size_t>& ks) const {
+    Flat f;
+    f.clear();
+    for (size_t k : ks) {
+      const int64_t b = offsets[k], e = offsets[k + 1];
+      f.degree.insert(f.degree.end(), degree.begin() + b, degree.begin() + e);
+      f.op.insert(f.op.end(), op.begin() + b, op.begin() + e);
+      f.constant.insert(f.constant.end(), constant.begin() + b, constant.begin() + e);
+      f.feature.insert(f.feature.end(), feature.begin() + b, feature.begin() + e);
+      if (!vf.empty()) f.vf.insert(f.vf.end(), vf.begin() + b, vf.begin() + e);
+      if (!vd.empty()) f.vd.insert(f.vd.end(), vd.begin() + b, vd.begin() + e);
+      f.offsets.push_back(f.offsets.back() + (e - b));
+    }
+    return f;
+  }
   template <typename T>
   sr_tree_batch batch() const {
     sr_tree_batch b{};
@@ -174,6 +190,119 @@ struct Scorer {
   }();
   bool ready() const { return ctx != nullptr || loss_cb != nullptr; }
   bool has_grad() const { return ctx != nullptr || grad_cb != nullptr; }
+  // Rows per tree (per-island minibatches): tree k on *rows[k] (all of one length); empty: every tree
+  // on the full dataset.  -> the distinct views (tree_view, their rows concatenated); false when the
+  // trees share one view (*one = it).
+  using TreeRows = std::vector<const std::vector<int64_t>*>;
+  static bool make_views(const TreeRows& tr, std::vector<int32_t>* tv, std::vector<int64_t>* cat, int* nv,
+                         int64_t* len, const std::vector<int64_t>** one) {
+    std::vector<const std::vector<int64_t>*> uniq;
+    tv->resize(tr.size());
+    for (size_t k = 0; k < tr.size(); ++k) {
+      size_t u = 0;
+      while (u < uniq.size() && uniq[u] != tr[k]) ++u;
+      if (u == uniq.size()) uniq.push_back(tr[k]);
+      (*tv)[k] = int32_t(u);
+    }
+    *one = uniq.empty() ? nullptr : uniq[0];
+    if (uniq.size() <= 1) return false;
+    *nv = int(uniq.size());
+    *len = int64_t(uniq[0]->size());
+    cat->clear();
+    for (auto* r : uniq) cat->insert(cat->end(), r->begin(), r->end());
+    return true;
+  }
+  int loss(const Flat& flat, const TreeRows& tr, std::vector<T>* out) {
+    static const std::vector<int64_t> kAll;
+    std::vector<int32_t> tv;
+    std::vector<int64_t> cat;
+    int nv = 1;
+    int64_t len = 0;
+    const std::vector<int64_t>* one = nullptr;
+    if (tr.empty() || !make_views(tr, &tv, &cat, &nv, &len, &one)) return loss(flat, one ? *one : kAll, out);
+    const int64_t nt = int64_t(flat.offsets.size()) - 1;
+    out->assign(size_t(nt), T(0));
+    const auto t0 = Clock::now();
+    int rc = SR_OK;
+    if (loss_cb) {  // CPU scorers: one callback per view over that view's trees
+      for (int v = 0; v < nv && rc == SR_OK; ++v) {
+        std::vector<size_t> ks;
+        for (int64_t k = 0; k < nt; ++k)
+          if (tv[size_t(k)] == v) ks.push_back(size_t(k));
+        const Flat sub = flat.take(ks);
+        const sr_tree_batch b = sub.batch<T>();
+        std::vector<T> l(ks.size());
+        std::vector<uint8_t> c(ks.size());
+        rc = loss_cb(cb_user, &b, cat.data() + int64_t(v) * len, len, l.data(), c.data());
+        for (size_t j = 0; j < ks.size(); ++j) (*out)[ks[j]] = c[j] ? l[j] : T(INFINITY);
+      }
+    } else {  // the device: every view in ONE call
+      const sr_tree_batch b = flat.batch<T>();
+      std::vector<uint8_t> comp(static_cast<size_t>(nt));
+      const int timing_was = !time_kernels ? sr_ctx_swap_timing(ctx, 0) : -1;
+      rc = sr_eval_loss_batch_views(ctx, ds, opset_id, &b, tv.data(), nv, cat.data(), len, loss_code, out->data(),
+                                    comp.data());
+      if (timing_was >= 0) sr_ctx_swap_timing(ctx, timing_was);
+      for (int64_t k = 0; k < nt; ++k)
+        if (!comp[size_t(k)]) (*out)[size_t(k)] = T(INFINITY);
+    }
+    ms += ms_since(t0);
+    ++calls;
+    return rc;
+  }
+  int grad(const Flat& flat, const TreeRows& tr, size_t n_consts, std::vector<T>* out, std::vector<T>* g,
+           std::vector<uint8_t>* comp) {
+    static const std::vector<int64_t> kAll;
+    std::vector<int32_t> tv;
+    std::vector<int64_t> cat;
+    int nv = 1;
+    int64_t len = 0;
+    const std::vector<int64_t>* one = nullptr;
+    if (tr.empty() || !make_views(tr, &tv, &cat, &nv, &len, &one)) return grad(flat, one ? *one : kAll, n_consts, out, g, comp);
+    const sr_tree_batch b = flat.batch<T>();
+    const int64_t nt = b.n_trees;
+    out->assign(size_t(nt), T(0));
+    g->assign(n_consts + 1, T(0));
+    comp->assign(size_t(nt), 0);
+    const auto t0 = Clock::now();
+    int rc = SR_OK;
+    if (grad_cb) {  // CPU scorers: one callback per view; the gradient slots scattered back per tree
+      std::vector<size_t> coff(size_t(nt) + 1, 0);
+      for (int64_t k = 0; k < nt; ++k) {
+        size_t c = 0;
+        for (int64_t i = b.offsets[k]; i < b.offsets[k + 1]; ++i) c += (b.degree[i] == 0 && b.constant[i]) ? 1 : 0;
+        coff[size_t(k) + 1] = coff[size_t(k)] + c;
+      }
+      for (int v = 0; v < nv && rc == SR_OK; ++v) {
+        std::vector<size_t> ks;
+        size_t nc = 0;
+        for (int64_t k = 0; k < nt; ++k)
+          if (tv[size_t(k)] == v) {
+            ks.push_back(size_t(k));
+            nc += coff[size_t(k) + 1] - coff[size_t(k)];
+          }
+        const Flat sub = flat.take(ks);
+        const sr_tree_batch sb = sub.batch<T>();
+        std::vector<T> l(ks.size()), gg(nc + 1);
+        std::vector<uint8_t> c(ks.size());
+        rc = grad_cb(cb_user, &sb, cat.data() + int64_t(v) * len, len, l.data(), gg.data(), c.data());
+        size_t at = 0;
+        for (size_t j = 0; j < ks.size(); ++j) {
+          (*out)[ks[j]] = l[j];
+          (*comp)[ks[j]] = c[j];
+          for (size_t q = coff[ks[j]]; q < coff[ks[j] + 1]; ++q) (*g)[q] = gg[at++];
+        }
+      }
+    } else {
+      const int timing_was = !time_kernels ? sr_ctx_swap_timing(ctx, 0) : -1;
+      rc = sr_eval_grad_batch_views(ctx, ds, opset_id, &b, tv.data(), nv, cat.data(), len, loss_code, out->data(),
+                                    g->data(), comp->data());
+      if (timing_was >= 0) sr_ctx_swap_timing(ctx, timing_was);
+    }
+    ms += ms_since(t0);
+    ++calls;
+    return rc;
+  }
   // losses of `flat`'s trees (+Inf where incomplete)
   int loss(const Flat& flat, const std::vector<int64_t>& rows, std::vector<T>* out) {
     const sr_tree_batch b = flat.batch<T>();
@@ -226,11 +355,18 @@ struct Scorer {
 // (rounded to T), one batched device call per evaluation round.
 template <typename T>
 struct TreeObjective : SrObjective {
+  using TreeRows = typename Scorer<T>::TreeRows;
   Scorer<T>* sc;
   Flat* flat;
   const std::vector<const SrTree<T>*>* trees;
-  const std::vector<int64_t>* rows;
+  const TreeRows* rows;  // per tree (its island's minibatch), or empty: the full dataset
   std::vector<int64_t> f_calls;
+  TreeRows rows_of(const std::vector<int>& items) const {
+    TreeRows r;
+    if (!rows->empty())
+      for (int k : items) r.push_back((*rows)[size_t(k)]);
+    return r;
+  }
   int f(const std::vector<int>& items, const std::vector<std::vector<double>>& xs, std::vector<double>* out) override {
     flat->clear();
     for (size_t j = 0; j < items.size(); ++j) {
@@ -238,7 +374,7 @@ struct TreeObjective : SrObjective {
       if (counting) ++f_calls[size_t(items[j])];
     }
     std::vector<T> loss;
-    const int rc = sc->loss(*flat, *rows, &loss);
+    const int rc = sc->loss(*flat, rows_of(items), &loss);
     if (rc) return rc;
     out->resize(loss.size());
     for (size_t j = 0; j < loss.size(); ++j) (*out)[j] = double(loss[j]);
@@ -255,7 +391,7 @@ struct TreeObjective : SrObjective {
     }
     std::vector<T> loss, g;
     std::vector<uint8_t> comp;
-    const int rc = sc->grad(*flat, *rows, nc, &loss, &g, &comp);
+    const int rc = sc->grad(*flat, rows_of(items), nc, &loss, &g, &comp);
     if (rc != SR_OK) return rc;
     out->resize(items.size());
     grads->resize(items.size());
@@ -277,7 +413,7 @@ template <typename T>
 int optimize_trees(Scorer<T>& sc, Flat& flat, const std::vector<const SrTree<T>*>& trees,
                    const std::vector<std::vector<double>>& x0,
                    const std::vector<std::vector<std::vector<double>>>& restarts, int iterations,
-                   const std::vector<int64_t>& rows, std::vector<std::vector<double>>* best_x,
+                   const typename Scorer<T>::TreeRows& rows, std::vector<std::vector<double>>* best_x,
                    std::vector<uint8_t>* improved, std::vector<T>* adopted_loss, std::vector<int64_t>* f_calls) {
   const size_t n = trees.size();
   TreeObjective<T> obj;
@@ -301,9 +437,13 @@ int optimize_trees(Scorer<T>& sc, Flat& flat, const std::vector<const SrTree<T>*
     }
   if (!better.empty()) {
     flat.clear();
-    for (size_t k : better) flat.add(*trees[k], &(*best_x)[k]);
+    typename Scorer<T>::TreeRows br;
+    for (size_t k : better) {
+      flat.add(*trees[k], &(*best_x)[k]);
+      if (!rows.empty()) br.push_back(rows[k]);
+    }
     std::vector<T> loss;
-    if ((rc = sc.loss(flat, rows, &loss))) return rc;
+    if ((rc = sc.loss(flat, br, &loss))) return rc;
     for (size_t j = 0; j < better.size(); ++j) (*adopted_loss)[better[j]] = loss[j];
   }
   *f_calls = obj.f_calls;
@@ -363,7 +503,6 @@ struct Engine : sr_search_base {
   }();
   int64_t s_r_cycles = 0;
   double host_ms = 0.0;
-  std::vector<int64_t> batch_idx;  // this iteration's minibatch (batching)
   Flat flat;
   // Scoring lanes: lane 0 is (sc, flat, num_evals, host_ms); further lanes (sr_search_add_device:
   // their own context and dataset copy) each run a share of the owned islands' iteration on their
@@ -399,7 +538,15 @@ struct Engine : sr_search_base {
     v = v + T(float(complexity) * o.parsimony);
     return v;
   }
-  int score_trees(Lane L, const std::vector<const SrTree<T>*>& trees, const std::vector<int64_t>& rows,
+  using TreeRows = typename Scorer<T>::TreeRows;
+  // each tree's rows: its island's minibatch (batching), or none (the full dataset)
+  TreeRows rows_for(const std::vector<int>& island, const std::vector<std::vector<int64_t>>& by_island) const {
+    TreeRows r;
+    if (o.batching)
+      for (int i : island) r.push_back(&by_island[size_t(i)]);
+    return r;
+  }
+  int score_trees(Lane L, const std::vector<const SrTree<T>*>& trees, const TreeRows& rows,
                   std::vector<T>* loss, std::vector<T>* cost) {
     L.flat->clear();
     for (auto* t : trees) L.flat->add(*t);
@@ -409,15 +556,16 @@ struct Engine : sr_search_base {
     for (size_t k = 0; k < loss->size(); ++k) (*cost)[k] = cost_of((*loss)[k], int(trees[k]->size()));
     return SR_OK;
   }
-  double fraction(const std::vector<int64_t>& rows) const {
-    return rows.empty() ? 1.0 : double(rows.size()) / double(n_rows);
+  double fraction(const TreeRows& rows) const {
+    return rows.empty() ? 1.0 : double(rows[0]->size()) / double(n_rows);
   }
 
   // ------------------------------------------------------------ constant optimisation
   // optimize_constants over members (pointers); perturbation draws come from each member's island
   // stream, in member order (deterministic whatever the batch composition)
   int optimize_members(Lane L, const std::vector<Member<T>*>& ms, const std::vector<int>& island,
-                       const std::vector<int64_t>& rows, std::vector<uint8_t>* improved_out) {
+                       const std::vector<std::vector<int64_t>>& rows_by_island, std::vector<uint8_t>* improved_out) {
+    const TreeRows rows = rows_for(island, rows_by_island);
     const size_t n = ms.size();
     improved_out->assign(n, 0);
     if (n == 0) return SR_OK;
@@ -608,7 +756,8 @@ struct Engine : sr_search_base {
     size_t slot = 0;
   };
 
-  int round(Lane L, const std::vector<int>& islands, double temperature, const std::vector<int64_t>& rows) {
+  int round(Lane L, const std::vector<int>& islands, double temperature,
+            const std::vector<std::vector<int64_t>>& rows_by_island) {
     std::vector<Plan> plans;
     plans.reserve(islands.size());
     std::vector<const SrTree<T>*> pending;
@@ -653,16 +802,22 @@ struct Engine : sr_search_base {
       }
       plans.push_back(std::move(pl));
     }
+    std::vector<int> pend_island;
     for (auto& pl : plans) {
       if (pl.kind == K_MUT || pl.kind == K_CROSS) {
         pl.slot = pending.size();
         pending.push_back(&pl.tree);
-        if (pl.kind == K_CROSS) pending.push_back(&pl.tree2);
+        pend_island.push_back(pl.island);
+        if (pl.kind == K_CROSS) {
+          pending.push_back(&pl.tree2);
+          pend_island.push_back(pl.island);
+        }
       }
     }
     *L.host_ms += ms_since(tp);
-    // device: ONE batched eval_cost for every island's children
+    // device: ONE batched eval_cost for every island's children (each on its island's minibatch)
     std::vector<T> loss, cost;
+    const TreeRows rows = rows_for(pend_island, rows_by_island);
     int rc = score_trees(L, pending, rows, &loss, &cost);
     if (rc) return rc;
     const double frac = fraction(rows);
@@ -677,7 +832,7 @@ struct Engine : sr_search_base {
           oi.push_back(pl.island);
         }
       std::vector<uint8_t> imp;
-      if ((rc = optimize_members(L, om, oi, rows, &imp))) return rc;
+      if ((rc = optimize_members(L, om, oi, rows_by_island, &imp))) return rc;
     }
     tp = Clock::now();
     for (auto& pl : plans) {
@@ -781,14 +936,16 @@ struct Engine : sr_search_base {
   }
 
   // ------------------------------------------------------------ minibatches
-  // batch(dataset, batch_size): rows drawn with replacement.  One minibatch per iteration shared by
-  // every island, from a stream keyed by (seed, iteration) so all ranks draw the same one (the
-  // reference draws one per island's s_r_cycle; sharing it lets one launch score all islands).
-  std::vector<int64_t> draw_batch(uint64_t salt) const {
+  // batch(dataset, batch_size): rows drawn with replacement (src/Dataset.jl:303-304), one minibatch
+  // per island per iteration for its s_r_cycle (salt 0, src/SingleIteration.jl:40) and one for its
+  // constant optimisation (salt 1, :77), each from its own stream keyed by (seed, iteration, island):
+  // independent of the island's other draws, of lanes and of which rank owns the island.  The device
+  // scores every island's trees on their own rows in one launch (sr_eval_loss_batch_views).
+  std::vector<int64_t> draw_batch(int island, uint64_t salt) const {
     std::vector<int64_t> rows;
     if (!o.batching) return rows;
     SrRng r;
-    r.seed(seed ^ 0x6261746368ull, uint64_t(iteration) * 4 + salt);
+    r.seed(seed ^ 0x6261746368ull, (uint64_t(iteration) * uint64_t(o.populations) + uint64_t(island)) * 2 + salt);
     rows.resize(size_t(o.batch_size));
     for (auto& v : rows) v = r.below(n_rows);
     return rows;
@@ -890,8 +1047,8 @@ struct Engine : sr_search_base {
   // s_r_cycle + optimize_and_simplify_population (+ finalize_costs) of a set of islands, scored on
   // one lane (every draw comes from the islands' own streams: the result does not depend on how the
   // owned islands are split over lanes)
-  int iterate_islands(Lane L, const std::vector<int>& islands, const std::vector<int64_t>& rows,
-                      const std::vector<int64_t>& orows) {
+  int iterate_islands(Lane L, const std::vector<int>& islands, const std::vector<std::vector<int64_t>>& rows,
+                      const std::vector<std::vector<int64_t>>& orows) {
     const auto t_start = Clock::now();
     const int64_t calls0 = L.sc->calls;
     const int ncyc = o.ncycles_per_iteration;
@@ -968,8 +1125,11 @@ struct Engine : sr_search_base {
   }
 
   int iterate() {
-    const std::vector<int64_t> rows = draw_batch(0);
-    const std::vector<int64_t> orows = draw_batch(1);
+    std::vector<std::vector<int64_t>> rows(size_t(o.populations)), orows(size_t(o.populations));
+    for (int i : owned) {
+      rows[size_t(i)] = draw_batch(i, 0);
+      orows[size_t(i)] = draw_batch(i, 1);
+    }
     for (int i : owned) best_seen[size_t(i)].reset(o.maxsize);
     const size_t nl = std::min(owned.size(), extra.size() + 1);
     if (nl <= 1) {
@@ -1239,7 +1399,9 @@ int optimize_common(Scorer<T>& sc, const sr_tree_batch* trees, const int64_t* ro
   std::vector<const SrTree<T>*> ptr;
   for (auto& t : tv) ptr.push_back(&t);
   Flat flat;
-  const std::vector<int64_t> rows(row_idx && n_idx > 0 ? row_idx : nullptr, row_idx && n_idx > 0 ? row_idx + n_idx : nullptr);
+  const std::vector<int64_t> view(row_idx && n_idx > 0 ? row_idx : nullptr, row_idx && n_idx > 0 ? row_idx + n_idx : nullptr);
+  typename Scorer<T>::TreeRows rows;  // (one view for every tree, or the full dataset)
+  if (!view.empty()) rows.assign(size_t(nt), &view);
   std::vector<std::vector<double>> bx;
   std::vector<uint8_t> imp;
   std::vector<T> loss;

@@ -760,10 +760,30 @@ __global__ void __launch_bounds__(W * 64, (SrMinWavesFor<T, R, TIER, W, VSTK>::v
   T* stk_lane = reinterpret_cast<T*>(sr_smem + plan.stk) + size_t(wave) * a.stack_depth * ROWS + lane * C;
 
   // tree group fastest: the blocks resident at one time share few row blocks (X stays in L2)
-  const int tg = blockIdx.x % a.n_groups;
-  const int rb = blockIdx.x / a.n_groups;
-  const int tree0 = tg * G;
-  int gcount = a.n_trees - tree0;
+  int tg, rb, tree0, gcount;
+  const int64_t* ridx = a.row_idx;  // GATHER: this block's row view
+  if (a.segs == nullptr) {
+    tg = int(blockIdx.x) % a.n_groups;
+    rb = int(blockIdx.x) / a.n_groups;
+    tree0 = tg * G;
+    gcount = a.n_trees - tree0;
+  } else {
+    // several row views in one launch (sr_eval_loss_batch_views): segment s = the launch positions
+    // of view s's trees, its own tree groups; its blocks follow the previous segments' (block0)
+    int lo = 0, hi = a.n_segs - 1;
+    while (lo < hi) {
+      const int mid = (lo + hi + 1) >> 1;
+      if (a.segs[mid].block0 <= int(blockIdx.x)) lo = mid;
+      else hi = mid - 1;
+    }
+    const SrSegment sg = a.segs[lo];
+    const int local = int(blockIdx.x) - sg.block0;
+    tg = local % sg.groups;
+    rb = local / sg.groups;
+    tree0 = sg.pos0 + tg * G;
+    gcount = sg.pos0 + sg.n_pos - tree0;
+    ridx += sg.row_off;
+  }
   if (gcount > G) gcount = G;
   const bool weighted = a.w != nullptr;
   const uint32_t thr = SrBits<T>::mag(a.tbig);
@@ -838,7 +858,7 @@ __global__ void __launch_bounds__(W * 64, (SrMinWavesFor<T, R, TIER, W, VSTK>::v
       for (int q = 0; q < PER; ++q) {
         const int i = tid + q * SR_BLOCK;
         const int64_t v = (i < n_valid) ? row0 + i : rlo;
-        src[q] = (i < ROWS) ? (GATHER ? a.row_idx[v] : v) : rlo;
+        src[q] = (i < ROWS) ? (GATHER ? ridx[v] : v) : rlo;
       }
       for (int f0 = 0; f0 < a.nf; f0 += 4) {
         T v[4][PER];
@@ -874,7 +894,7 @@ __global__ void __launch_bounds__(W * 64, (SrMinWavesFor<T, R, TIER, W, VSTK>::v
     } else {
       for (int i = tid; i < ROWS; i += SR_BLOCK) {
         const int64_t v = row0 + i;
-        const int64_t src = a.row_idx[v < a.n_rows ? v : 0];
+        const int64_t src = ridx[v < a.n_rows ? v : 0];
         for (int f = 0; f < a.nf; ++f) xs[f * ROWS + i] = a.X[int64_t(f) * a.ld + src];
         if (MODE != SR_MODE_EXACT && a.y) {
           ys[i] = a.y[src];

@@ -15,8 +15,10 @@ from .loss import (
     eval_cost,
     eval_cost_batch,
     eval_grad_batch,
+    eval_grad_batch_views,
     eval_loss,
     eval_loss_batch,
+    eval_loss_batch_views,
     eval_tree_array,
     eval_tree_array_batch,
     loss_to_cost,
@@ -44,7 +46,7 @@ __all__ = [
     "Options", "OperatorEnum", "Dataset", "SubDataset", "batch", "Node", "TreeBatch", "flatten_trees",
     "extend_operators", "apply_unary", "apply_binary", "parse_expression", "string_tree",
     "get_scalar_constants", "set_scalar_constants", "eval_tree_array", "eval_tree_array_batch",
-    "eval_loss", "eval_loss_batch", "eval_grad_batch", "eval_cost", "eval_cost_batch", "loss_to_cost",
+    "eval_loss", "eval_loss_batch", "eval_grad_batch", "eval_loss_batch_views", "eval_grad_batch_views", "eval_cost", "eval_cost_batch", "loss_to_cost",
     "update_baseline_loss_", "score_func", "compute_complexity", "gen_random_tree_fixed_size",
     "gen_random_population", "gen_random_batch", "make_random_leaf", "get_context", "device_available", "DeviceContext",
     "SRError", "UnsupportedOperatorError", "optimize_constants_batch", "equation_search", "SearchOptions",

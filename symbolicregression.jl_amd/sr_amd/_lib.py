@@ -46,6 +46,7 @@ EXPORTED_SYMBOLS = (
     "sr_dataset_free",
     "sr_dataset_info",
     "sr_eval_loss_batch",
+    "sr_eval_loss_batch_views",
     "sr_eval_tree_array",
     "sr_eval_loss_partials",
     "sr_eval_loss_partials_packed",
@@ -66,6 +67,7 @@ EXPORTED_SYMBOLS = (
     "sr_finalize_losses",
     "sr_dataset_denominator",
     "sr_eval_grad_batch",
+    "sr_eval_grad_batch_views",
     "sr_compile_info",
     "sr_host_unary",
     "sr_last_kernel_ms",
@@ -180,6 +182,14 @@ def _load():
         "sr_eval_loss_batch": (
             c_int,
             [P, P, c_int, POINTER(SrTreeBatch), P, c_int64, c_int, P, P],
+        ),
+        "sr_eval_loss_batch_views": (
+            c_int,
+            [P, P, c_int, POINTER(SrTreeBatch), P, c_int, P, c_int64, c_int, P, P],
+        ),
+        "sr_eval_grad_batch_views": (
+            c_int,
+            [P, P, c_int, POINTER(SrTreeBatch), P, c_int, P, c_int64, c_int, P, P, P],
         ),
         "sr_eval_tree_array": (c_int, [P, P, c_int, POINTER(SrTreeBatch), P, c_int64, P, P]),
         "sr_eval_loss_partials": (

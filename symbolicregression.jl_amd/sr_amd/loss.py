@@ -61,6 +61,50 @@ def eval_loss_batch(trees, dataset, options, *, ctx=None):
     return losses, complete.astype(bool)
 
 
+def _views(tree_view, view_rows, nt):
+    tv = np.ascontiguousarray(tree_view, dtype=np.int32)
+    vr = np.ascontiguousarray(view_rows, dtype=np.int64)
+    if vr.ndim != 2 or tv.shape != (nt,):
+        raise ValueError("view_rows must be [n_views, view_len] and tree_view one view per tree")
+    return tv, vr
+
+
+def eval_loss_batch_views(trees, dataset, options, tree_view, view_rows, *, ctx=None):
+    """``eval_loss_batch`` with tree t on the rows ``view_rows[tree_view[t]]`` of ``dataset`` (a Dataset):
+    every island's trees on its own minibatch (src/SingleIteration.jl:40) in ONE device call."""
+    ctx = ctx or get_context()
+    full = dataset.full
+    tb = _as_batch(trees, full.dtype)
+    nt = tb.n_trees
+    tv, vr = _views(tree_view, view_rows, nt)
+    losses = np.empty(nt, dtype=full.dtype)
+    complete = np.empty(nt, dtype=np.uint8)
+    s = tb.to_struct()
+    p = lambda a: a.ctypes.data_as(ctypes.c_void_p)  # noqa: E731
+    _lib.check(_lib.lib.sr_eval_loss_batch_views(
+        ctx.handle, full.device_handle(ctx), ctx.opset_id(options.operators), ctypes.byref(s), p(tv), int(vr.shape[0]),
+        p(vr), int(vr.shape[1]), ctx.loss_code(options), p(losses), p(complete)))
+    return losses, complete.astype(bool)
+
+
+def eval_grad_batch_views(trees, dataset, options, tree_view, view_rows, *, ctx=None):
+    """``eval_grad_batch`` over several row views in one call (as ``eval_loss_batch_views``)."""
+    ctx = ctx or get_context()
+    full = dataset.full
+    tb = _as_batch(trees, full.dtype)
+    nt = tb.n_trees
+    tv, vr = _views(tree_view, view_rows, nt)
+    losses = np.empty(nt, dtype=full.dtype)
+    complete = np.empty(nt, dtype=np.uint8)
+    grads = np.zeros(int(tb.constant_mask().sum()) + 1, dtype=full.dtype)
+    s = tb.to_struct()
+    p = lambda a: a.ctypes.data_as(ctypes.c_void_p)  # noqa: E731
+    _lib.check(_lib.lib.sr_eval_grad_batch_views(
+        ctx.handle, full.device_handle(ctx), ctx.opset_id(options.operators), ctypes.byref(s), p(tv), int(vr.shape[0]),
+        p(vr), int(vr.shape[1]), ctx.loss_code(options), p(losses), p(grads), p(complete)))
+    return losses, grads[:-1], complete.astype(bool)
+
+
 def eval_grad_batch(trees, dataset, options, *, ctx=None):
     """Loss and its gradient with respect to every tree's constants, for a whole batch.
 

@@ -170,7 +170,9 @@ def test_grad_f64_many_features_deep_trees_weighted():
         if len(a) == 0:
             continue
         scale = max(1.0, float(np.abs(b).max()))
-        if e.max() > 1e-6 * scale:
+        if e.max() > 1e-6 * scale or not loss[t] < 1e8:
+            # (finite differences of a loss of 1e25 — exp(exp(x)) terms — resolve nothing: both
+            # steps see the same loss bits and report a zero gradient with a zero error estimate)
             continue
         # (10 features and weights: the finite differences' own rounding error is ~1e-6 here)
         assert np.all(np.abs(a - b) <= 2e-5 * scale), (t, a, b)

@@ -87,13 +87,15 @@ def _worker(rank, world, port, q):
             out[key + "_ref"] = (ref_loss, ref_comp, ref_fold)
             tl, tc = eval_loss_tree_sharded(tb, full, opts)
             out[key + "_trees"] = (tl, tc)
-        # the failure protocol: a bigger batch grows the collective buffers on both ranks; rank 1's
-        # growth is made to fail -> both ranks raise, and the next call works on both
+        # the failure protocol: a fresh communicator starts with empty collective buffers, so the next
+        # call grows them on both ranks; rank 1's growth is made to fail -> both ranks raise, and the
+        # next call works on both
         X, y, _ = _data(False)
         shard = Dataset(np.ascontiguousarray(X[:, lo:hi]), np.ascontiguousarray(y[lo:hi]))
         big = tb.take(np.concatenate([np.arange(tb.n_trees)] * 3))
         errs = []
         for fn in (lambda: eval_loss_sharded(big, shard, opts), lambda: eval_loss_tree_sharded(big, Dataset(X, y), opts)):
+            init_host_comm(ctx=ctx)
             if rank == 1:
                 ctx.set_tuning("inject_failure", 1)
             try:

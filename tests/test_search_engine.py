@@ -36,6 +36,22 @@ def _loss_fn(opts, X, y):
     return lf
 
 
+def _restated_loss(lf, dtype):
+    """The restatement's loss_fn(trees, rows): rows None (full data) or one row array per tree (its
+    island's minibatch)."""
+    def f(trees, rows):
+        if rows is None:
+            return lf(flatten_trees(trees, dtype), None)
+        out = np.empty(len(trees))
+        groups = {}
+        for k, r in enumerate(rows):
+            groups.setdefault(id(r), (r, []))[1].append(k)
+        for r, ks in groups.values():
+            out[ks] = lf(flatten_trees([trees[k] for k in ks], dtype), r)
+        return out
+    return f
+
+
 def _key(t, dtype):
     tb = flatten_trees([t], dtype)
     return tuple(tb.degree), tuple(tb.op), tuple(tb.feature), tuple(float(v) for v in tb.val)
@@ -50,6 +66,9 @@ CASES = [
                                                       use_frequency_in_tournament=False), {}),
     ("tournament_p1_parsimony", np.float32, 6, {}, dict(tournament_selection_p=1.0, parsimony=0.01)),
     ("heavy_migration", np.float64, 7, dict(fraction_replaced=0.2, fraction_replaced_hof=0.3, topn=4), {}),
+    # per-island minibatches (src/SingleIteration.jl:40): each island's children on its own rows
+    ("batching_f32", np.float32, 8, {}, dict(batching=True, batch_size=17)),
+    ("batching_f64_crossover", np.float64, 9, dict(crossover_probability=0.3), dict(batching=True, batch_size=23)),
 ]
 
 
@@ -61,7 +80,7 @@ def test_engine_equals_restatement(name, dtype, seed, sokw, okw):
     X, y = _data(dtype)
     lf = _loss_fn(opts, X, y)
     res = equation_search(X, y, niterations=3, options=opts, seed=seed, search_options=so, _loss_fn=lf)
-    ref = SearchOracle(opts, so, 2, X.shape[1], dtype, seed, lambda trees: lf(flatten_trees(trees, dtype), None)).run(3)
+    ref = SearchOracle(opts, so, 2, X.shape[1], dtype, seed, _restated_loss(lf, dtype)).run(3)
     for i, (pa, pb) in enumerate(zip(res.populations, ref.pops)):
         for k, (a, b) in enumerate(zip(pa, pb)):
             assert (_key(a.tree, dtype), float(a.cost), a.birth, a.ref, a.parent) == \

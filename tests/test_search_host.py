@@ -19,7 +19,7 @@ OPTS = dict(binary_operators=["+", "-", "*", "/"], unary_operators=["cos", "sin"
 
 
 def _oracle(opts, so=None, T=np.float64, seed=0):
-    o = so_mod.SearchOracle(opts, so or SearchOptions(), 3, 10, T, seed, lambda trees: np.zeros(len(trees)))
+    o = so_mod.SearchOracle(opts, so or SearchOptions(), 3, 10, T, seed, lambda trees, rows=None: np.zeros(len(trees)))
     o.snap = [[1.0 / opts.maxsize] * opts.maxsize for _ in range(opts.populations)]
     o.baseline, o.use_baseline = T(1), True
     return o
