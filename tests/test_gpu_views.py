@@ -56,7 +56,7 @@ def test_grad_views_equal_per_view_calls():
         assert np.array_equal(loss[sel].view(np.uint8), lv.view(np.uint8))
         sub_co = tb.take(sel).constant_offsets()
         for j, t in enumerate(sel):
-            assert np.array_equal(g[co[t]:co[t + 1]], gv[sub_co[j]:sub_co[j + 1]]), (v, t)
+            assert np.array_equal(g[co[t]:co[t + 1]].view(np.uint8), gv[sub_co[j]:sub_co[j + 1]].view(np.uint8)), (v, t)
 
 
 @pytest.mark.parametrize("optimize", [False, True])
