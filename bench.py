@@ -58,6 +58,8 @@ def parse_args(argv=None):
     ap.add_argument("--c4-trees", type=int, default=100_000)
     ap.add_argument("--c4-steps", type=int, default=3)
     ap.add_argument("--no-c4", action="store_true")
+    ap.add_argument("--no-c4-parity", action="store_true", help="skip the C4 full-size parity sample (N = 1)")
+    ap.add_argument("--c4-parity-trees", type=int, default=64)
     ap.add_argument("--no-tree-sharded", action="store_true")
     ap.add_argument("--no-sharded-path", action="store_true", help="skip the N = 1 c2_sharded_path line")
     ap.add_argument("--cpu-trees", type=int, default=0, help="CPU-baseline tree sample (0 = auto, ~15 s)")
@@ -447,7 +449,83 @@ def c4_line(ctx, opts, eval_loss_sharded, gen_random_batch, Dataset, args, comm,
                                 traffic_source=traffic.get("source") if traffic else None,
                                 hbm_GBps=(traffic["hbm_read_bytes_per_step"] / (kmean * 1e-3) / 1e9
                                           if traffic else None), hbm_peak_GBps=PEAK_HBM_GBPS)}
+    if world == 1 and rank == 0 and not args.no_c4_parity:
+        out["parity"] = c4_parity(opts, tb, res, lambda t: eval_loss_sharded(t, ds, opts), rows_total,
+                                  args.c4_parity_trees)
     ds.free_device()
+    return out
+
+
+def per_tree_bar(orc, sub, X, y, d_loss, l64, ok, rel_bar, threads):
+    """The tests' per-tree loss bar (tests/parity_util.py): max(rel_bar |oracle|, 4 x the tree's spread
+    under +-1-ulp libm perturbations), the spread measured only for the trees the plain bar misses."""
+    with np.errstate(invalid="ignore", divide="ignore"):
+        r = np.where(d_loss == l64, 0.0, np.abs(d_loss - l64) / np.maximum(np.abs(l64), 1e-300))
+    worst = np.nonzero(ok & (r > rel_bar))[0]
+    spread = np.zeros(len(d_loss))
+    if worst.size:
+        wsub = sub.take(worst)
+        l0, c0 = orc.eval_loss_batch(wsub, X, y, accum="f64", n_threads=threads)
+        for seed in (1, 2, 3, 4):
+            lp, cp = orc.eval_loss_batch(wsub, X, y, accum="f64", n_threads=threads, perturb=seed)
+            with np.errstate(invalid="ignore"):
+                d = np.abs(lp.astype(np.float64) - l0.astype(np.float64))
+            spread[worst] = np.maximum(spread[worst], np.where(cp & c0 & np.isfinite(d), d, 0.0))
+    with np.errstate(invalid="ignore"):
+        bar = np.maximum(rel_bar * np.abs(l64), 4 * spread)
+        err = np.where(d_loss == l64, 0.0, np.abs(d_loss - l64))
+    return r, bar, err, int(worst.size)
+
+
+def c4_parity(opts, tb, res, device_call, rows_total, n_sample):
+    """C4 at full size against the oracle: a stratified sample of the timed step's trees (complete and
+    incomplete, every size) over all rows, plus planted trees whose values reach the exact-sum
+    threshold (max|v| >= floatmax / 2n: DynamicExpressions' isfinite(sum) decided in Julia's pairwise
+    order over 2^26 rows, BIG path) scored by the same sharded call; flags bit-exact, +Inf exactly where
+    the reference's Float32 fold is +Inf, losses within the per-tree bar."""
+    from oracle import Oracle
+    from sr_amd import flatten_trees, parse_expression
+
+    threads = min(int(os.environ.get("OMP_NUM_THREADS", "0")) or (os.cpu_count() or 1), 16)
+    t0 = time.perf_counter()
+    comp = np.asarray(res["c"]).astype(bool)
+    sizes = np.diff(np.asarray(tb.offsets))
+    pick = []
+    for want_comp, k in ((True, n_sample * 3 // 4), (False, n_sample - n_sample * 3 // 4)):
+        cand = np.nonzero(comp == want_comp)[0]
+        cand = cand[np.argsort(sizes[cand], kind="stable")]  # every size: evenly over the size order
+        pick.extend(cand[np.linspace(0, len(cand) - 1, k).astype(int)].tolist() if len(cand) else [])
+    idx = np.array(sorted(set(pick)), dtype=np.int64)
+    sub = tb.take(idx)
+    planted = flatten_trees([parse_expression(e, opts) for e in ("x1 * 1.0e30", "x1 * 5.0e34", "(x2 * 4.0e34) + x3",
+                                                                   "cos(x1) * 2.0e33")], np.float32)
+    pl_loss, pl_comp = device_call(planted)
+    X, y = c4_shard(0, 1, rows_total)
+    orc = Oracle.from_options(opts)
+    out = {}
+    for name, t, d_loss, d_comp in (("sample", sub, np.asarray(res["l"])[idx], comp[idx]),
+                                    ("planted_big", planted, pl_loss, pl_comp)):
+        l64, c64 = orc.eval_loss_batch(t, X, y, accum="f64", n_threads=threads)
+        lref, cref = orc.eval_loss_batch(t, X, y, accum="ref", n_threads=threads)
+        d_loss = np.asarray(d_loss, dtype=np.float64)
+        ok = d_comp & c64
+        r, bar, err, n_wide = per_tree_bar(orc, t, X, y, d_loss, l64.astype(np.float64), ok, 1e-4, threads)
+        fail = ok & ~(err <= bar)
+        inf_m = int(np.sum(ok & (np.isinf(d_loss) != np.isinf(lref))))
+        out[name] = {"trees": int(t.n_trees), "complete": int(ok.sum()),
+                     "flag_mismatches": int(np.sum(d_comp != c64)) + int(np.sum(cref != c64)),
+                     "ref_fold_inf_trees": int(np.sum(ok & np.isinf(lref))), "ref_fold_inf_mismatches": inf_m,
+                     "max_rel_vs_f64_accum": float(np.max(np.where(np.isfinite(r[ok]), r[ok], 0.0), initial=0.0)),
+                     "n_held_to_libm_spread_bar": n_wide, "loss_failures": int(fail.sum())}
+    out["rows"] = int(rows_total)
+    out["pass"] = all(v["flag_mismatches"] == 0 and v["loss_failures"] == 0 and v["ref_fold_inf_mismatches"] == 0
+                      for v in (out["sample"], out["planted_big"]))
+    out["rule"] = ("flags bit-exact vs the oracle over all rows; +Inf exactly where the reference's Float32 fold is; "
+                   "complete losses within max(1e-4 |oracle f64|, 4 x libm spread); sample = the timed step's own "
+                   "results for a stratified tree sample (3/4 complete, 1/4 incomplete, evenly over tree size); "
+                   "planted_big = trees over values >= floatmax/2n (the exact Julia-order isfinite(sum) pass), "
+                   "scored by the same sharded call")
+    out["cpu_s"] = time.perf_counter() - t0
     return out
 
 
@@ -484,8 +562,12 @@ def extra_lines(ctx, opts, trees, comp, X, y, args):
     km = float(np.mean(kms))
     busy = float(np.mean(st["busy"][-steps:]))
     rpl64 = ctx.last_rows_per_lane()
+    f64_parity = None
+    if not args.no_cpu_baseline:
+        f64_parity = f64_parity_sample(opts, tb64, X64, y64, o64)
     out["f64"] = roofline(
         float(X.shape[1]) * (tb64.n_operator_nodes + 3 * tb64.n_trees), busy, PEAK_FP64_TFLOPS,
+        parity=f64_parity,
         kernel_sum_ms_per_step=km, ms_per_step=dt / steps * 1e3,
         kernel=(f"sr_tile_kernel<double,{rpl64},LOSS,gather=false,BASIC" + (",register stack>" if rpl64 == 8 else ">")),
         node_evals_per_s=float(tb64.n_nodes) * X.shape[1] * steps / dt,
@@ -494,6 +576,33 @@ def extra_lines(ctx, opts, trees, comp, X, y, args):
         what="the C2 population and data in Float64 (C5's element type)")
     ds64.free_device()
     return out
+
+
+def f64_parity_sample(opts, tb64, X64, y64, o64, n=320):
+    """The timed Float64 step against the oracle at full size (2^20 rows): a strided tree sample, flags
+    bit-exact, every complete tree within the north-star f64 bar (1e-10 relative, or 4 x the tree's
+    libm spread: tests/parity_util.py)."""
+    from oracle import Oracle
+
+    threads = min(int(os.environ.get("OMP_NUM_THREADS", "0")) or (os.cpu_count() or 1), 16)
+    t0 = time.perf_counter()
+    step = max(1, tb64.n_trees // n)
+    idx = np.arange(0, tb64.n_trees, step)[:n]
+    sub = tb64.take(idx)
+    orc = Oracle.from_options(opts)
+    l64, c64 = orc.eval_loss_batch(sub, X64, y64, accum="f64", n_threads=threads)
+    d_loss = np.asarray(o64["loss"], dtype=np.float64)[idx]
+    d_comp = np.asarray(o64["comp"]).astype(bool)[idx]
+    ok = d_comp & c64
+    r, bar, err, n_wide = per_tree_bar(orc, sub, X64, y64, d_loss, l64, ok, 1e-10, threads)
+    fail = ok & ~(err <= bar)
+    fin = ok & np.isfinite(r)
+    return {"trees": int(sub.n_trees), "rows": int(X64.shape[1]), "complete": int(ok.sum()),
+            "flag_mismatches": int(np.sum(d_comp != c64)), "loss_failures": int(fail.sum()),
+            "max_rel": float(np.max(r[fin], initial=0.0)), "median_rel": float(np.median(r[fin])) if fin.any() else 0.0,
+            "n_held_to_libm_spread_bar": n_wide, "pass": bool(np.all(d_comp == c64) and not fail.any()),
+            "rule": "flags bit-exact; every complete tree within max(1e-10 |oracle|, 4 x libm spread)",
+            "cpu_s": time.perf_counter() - t0}
 
 
 def algorithmic_bytes(nt, rows, n_launch, rows_per_lane=8, n_derived=0):
@@ -573,6 +682,8 @@ def search_lines(args):
                                   "kernel_busy = the interpreter launches' device-busy time (a 5-iteration run "
                                   "with SR_AMD_SEARCH_KERNEL_TIMES=1)"),
                 "best_loss": float(min(m.loss for m in res.pareto_frontier)), "config": desc}
+        if name == "c5":
+            line["grad_roofline"] = grad_roofline(res, X, y, o)
         sc = SearchScorer(Oracle.from_options(o), X, y, n_threads=cpu_threads)
         t0 = time.perf_counter()
         cres = equation_search(X, y, niterations=cpu_iters, options=o, seed=0, _native_scorer=sc)
@@ -585,6 +696,48 @@ def search_lines(args):
                        f"BFGS), {cpu_iters} iteration(s), {cwall:.1f} s, {cres.device_calls} scoring calls")}
         out[name] = line
     return out
+
+
+def grad_roofline(res, X, y, opts, reps=5):
+    """The gradient kernel (sr_eval_grad_batch: BFGS's objective + gradient, src/ConstantOptimization.jl:
+    126-167) on the C5 search's final members with constants, over the full data: per tangent bucket the
+    tangent kernel's HIP-event time and its algorithmic flops (csrc sr_last_grad_info: per row and work
+    item, each unary node 2 + KT, binary node 3 + 2 KT, loss epilogue 3 + KT), against the FP64 peak."""
+    import sr_amd
+    from sr_amd import Dataset, eval_grad_batch, flatten_trees
+
+    trees = [m.tree for p in res.populations for m in p if m.tree.count_constants() > 0]
+    tb = flatten_trees(trees, np.float64)
+    ds = Dataset(X, y)
+    ctx = sr_amd.get_context()
+    for _ in range(2):
+        eval_grad_batch(tb, ds, opts)
+    per = None
+    for _ in range(reps):
+        eval_grad_batch(tb, ds, opts)
+        info = ctx.last_grad_info()
+        if per is None:
+            per = [dict(b, kernel_ms=0.0) for b in info]
+        for a, b in zip(per, info):
+            a["kernel_ms"] += b["kernel_ms"] / reps
+    buckets = []
+    for b in per:
+        if b["items"] == 0:
+            continue
+        ach = b["flops"] / (b["kernel_ms"] * 1e-3) / 1e12 if b["kernel_ms"] > 0 else 0.0
+        buckets.append(dict(b, achieved_TFLOPs=ach, frac=ach / PEAK_FP64_TFLOPS))
+    tot_ms = sum(b["kernel_ms"] for b in buckets)
+    tot_fl = sum(b["flops"] for b in buckets)
+    dom = max(buckets, key=lambda b: b["kernel_ms"]) if buckets else None
+    ach = tot_fl / (tot_ms * 1e-3) / 1e12 if tot_ms > 0 else 0.0
+    ds.free_device()
+    return {"bound": "valu", "achieved": ach, "peak": PEAK_FP64_TFLOPS, "unit": "TFLOP/s", "frac": ach / PEAK_FP64_TFLOPS,
+            "kernel_ms_per_call": tot_ms, "flops_per_call": tot_fl, "dominant_bucket": dom, "buckets": buckets,
+            "trees": int(tb.n_trees), "rows": int(X.shape[1]), "dtype": "f64",
+            "kernel": "sr_grad_kernel<double,KT,W=4,gather=false,R>",
+            "flop_convention": ("per row and (tree, first tangent) item: unary node 2 + KT, binary node 3 + 2 KT, "
+                                "loss epilogue 3 + KT; 1 flop per operator incl. transcendentals"),
+            "what": "sr_eval_grad_batch on the C5 search's final members with constants, full 100k rows, f64"}
 
 
 def measured_traffic(workload):
@@ -644,6 +797,10 @@ def cpu_baseline_and_parity(opts, tb, X, y, n_sample, dev_loss, dev_comp):
         with np.errstate(invalid="ignore", divide="ignore"):
             return np.where(a == b, 0.0, np.abs(a - b) / np.maximum(np.abs(b), 1e-30))
     l64 = l_f64.astype(np.float64)
+    # the reference's L(Inf) where its Float32 loss fold overflows (src/LossFunctions.jl:38-58): the
+    # device must be +Inf exactly there (the oracle's f64 accumulation takes the same verdict)
+    inf_mism = int(np.sum(ok & (np.isinf(d_loss) != np.isinf(l_ref))))
+    n_fold_inf = int(np.sum(ok & np.isinf(l_ref)))
     r64 = rel(d_loss, l64)
     rref = rel(d_loss, l_ref.astype(np.float64))
     # the reference's own accumulation error: its sequential Float32 fold against the f64-accumulated sum
@@ -680,11 +837,14 @@ def cpu_baseline_and_parity(opts, tb, X, y, n_sample, dev_loss, dev_comp):
               "ref_f32_fold_self_error_median_rel": float(np.median(rfold[fin])) if fin.any() else 0.0,
               "ref_f32_fold_self_error_max_rel": float(np.max(rfold[fin], initial=0.0)),
               "loss_failures_vs_ref_fold": int(failref.sum()),
-              "pass": flag_mismatch == 0 and not fail64.any() and not failref.any(),
-              "rule": ("flags bit-exact; every complete tree within max(1e-4 |oracle|, 4 x the tree's libm spread) of "
+              "ref_fold_inf_trees": n_fold_inf,
+              "ref_fold_inf_mismatches": inf_mism,
+              "pass": flag_mismatch == 0 and not fail64.any() and not failref.any() and inf_mism == 0,
+              "rule": ("flags bit-exact; +Inf exactly where the reference's sequential Float32 loss fold overflows; "
+                       "every complete tree within max(1e-4 |oracle|, 4 x the tree's libm spread) of "
                        "the f64-accumulated oracle (tests/parity_util.py), and no farther from the reference's "
                        "sequential Float32 fold than that fold is from the f64 sum, plus the same bar (at 2^20 rows "
-                       "the fold's own error exceeds 1e-4: ref_f32_fold_self_error_*)")}
+                       "the fold's own error exceeds 1e-4: ref_f32_fold_self_error_*; DESIGN §5)")}
     return cpu, parity
 
 

@@ -445,6 +445,12 @@ int sr_last_phase_ms(sr_ctx* ctx, double* out, int n);
  * reports how many derived columns the last sr_eval_loss_batch used and how many of its trees went
  * through the exact-sum pass (flagged BIG). */
 int sr_set_tuning(sr_ctx* ctx, const char* name, int64_t value);
+/* The last sr_eval_grad_batch(_views) call's tangent kernels, per tangent bucket b = 0..4 (1, 2, 4, 8,
+ * 16 tangents; up to n of each output, each may be NULL): device time (ms, HIP events; 0 when the
+ * context's "timing" is off or the bucket was empty), algorithmic flops (per row of a (tree, first
+ * tangent) work item: each unary node 2 + KT, each binary node 3 + 2 KT, the loss epilogue 3 + KT),
+ * work items and rows per lane. */
+int sr_last_grad_info(sr_ctx* ctx, int n, double* kernel_ms, double* flops, int64_t* items, int* rows_per_lane);
 int sr_tuning_info(sr_ctx* ctx, int* used_derived_columns, int64_t* exact_trees);
 
 #ifdef __cplusplus

@@ -131,6 +131,14 @@ struct sr_ctx {
   hipEvent_t ev_start = nullptr, ev_k0 = nullptr, ev_k1 = nullptr, ev_end = nullptr;
   hipEvent_t ev_c0[kMaxChunks] = {}, ev_c1[kMaxChunks] = {};  // per-chunk interpreter launches
   hipEvent_t ev_d0 = nullptr, ev_d1 = nullptr;                 // the derived-column launch
+  // the last gradient call's tangent-kernel launches, per tangent bucket (1, 2, 4, 8, 16): HIP events,
+  // algorithmic flops (sr_last_grad_info), work items, rows per lane
+  static constexpr int kGradBuckets = 5;
+  hipEvent_t ev_g0[kGradBuckets] = {}, ev_g1[kGradBuckets] = {};
+  bool grad_timed[kGradBuckets] = {};
+  double grad_flops[kGradBuckets] = {};
+  int64_t grad_items[kGradBuckets] = {};
+  int grad_rows[kGradBuckets] = {};
   int n_chunks_last = 0;
   bool derived_last = false;  // the last run_batch launched derived columns (timed by ev_d0/ev_d1)
   int n_derived_last = 0;
@@ -161,6 +169,8 @@ struct sr_ctx {
   // threads; off by default)
   int spin = 0;
   uint32_t hint_epoch = 0;  // dead-tree hint epoch of the current call
+  int debug_hint_regrow = 0;       // tests (sr_set_tuning "debug_hint_regrow"): grow the hint array in place
+  void* hint_reserve = nullptr;    // its fixed-address reservation
   int exact_g = 0;          // SR_AMD_EXACT_G (tuning): listed trees per workgroup of the EXACT pass
   // SR_AMD_DERIVED (default 1): nodes unary(feature) shared by several trees of a large LOSS call
   // are evaluated once per call into derived columns (LOAD_DERIVED); 0 disables
@@ -521,7 +531,30 @@ int run_batch(sr_ctx* ctx, const sr_dataset* ds, int opset_id, const sr_tree_bat
     // freed address for the larger buffer, whose new part then holds stale words — possibly equal to
     // this call's epoch, which would mark live trees dead)
     const size_t cap_before = ctx->hint.cap;
-    SR_HIP_CHECK(ctx->hint.ensure(size_t(nt) * sizeof(uint32_t) + 4));
+    const size_t hint_bytes = size_t(nt) * sizeof(uint32_t) + 4;
+    if (ctx->debug_hint_regrow && hint_bytes > ctx->hint.cap) {
+      // (tests: sr_set_tuning "debug_hint_regrow") the array grows IN PLACE, at the same address, its
+      // new words holding the epoch the next call would use without a reset — the conditions of the
+      // round-3 stale-hint bug (a reallocation that got the freed address back); only the capacity
+      // check below catches it
+      constexpr size_t kReserve = size_t(64) << 20;
+      if (hint_bytes + hint_bytes / 4 > kReserve) return set_error(SR_ERR_INVALID_ARG, "debug_hint_regrow: batch too large");
+      if (ctx->hint_reserve == nullptr) SR_HIP_CHECK(hipMalloc(&ctx->hint_reserve, kReserve));
+      if (ctx->hint.p != ctx->hint_reserve) {
+        ctx->hint.release();
+        ctx->hint.p = ctx->hint_reserve;
+      }
+      const size_t want = hint_bytes + hint_bytes / 4;
+      SR_HIP_CHECK(hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(static_cast<char*>(ctx->hint.p) + cap_before),
+                                     int(ctx->hint_epoch + 1), (want - cap_before) / 4, s));
+      ctx->hint.cap = want;
+    } else {
+      if (ctx->hint.p == ctx->hint_reserve && ctx->hint_reserve != nullptr) {  // (leaving the debug mode)
+        ctx->hint.p = nullptr;
+        ctx->hint.cap = 0;
+      }
+      SR_HIP_CHECK(ctx->hint.ensure(hint_bytes));
+    }
     if (ctx->hint.cap != cap_before || ctx->hint_epoch == 0xffffffffu) {
       SR_HIP_CHECK(hipMemsetAsync(ctx->hint.p, 0, ctx->hint.cap, s));
       ctx->hint_epoch = 0;
@@ -1720,6 +1753,28 @@ int eval_grad_impl(sr_ctx* ctx, const sr_dataset* ds, int opset_id, const sr_tre
   SR_HIP_CHECK(hipMemcpyAsync(ds_, hs, stage_bytes, hipMemcpyHostToDevice, s));
   // (buckets run one after another on the stream, so they share the partials buffer)
   SR_HIP_CHECK(ctx->g_part.ensure(part_need * sizeof(double) + 16));
+  // algorithmic flops of each bucket's tangent kernel (bench.py's gradient roofline), per row of an
+  // item (tree, first tangent) of KT tangents: each unary node 1 (value, transcendentals count 1) +
+  // 1 (its derivative) + KT (tangents scaled), each binary node 1 + 2 (partials) + 2 KT (the
+  // tangents' product and fused add), and the loss epilogue 3 (d loss / d pred, weight) + KT
+  // accumulations; loads move data only
+  static_assert(kNB == sr_ctx::kGradBuckets, "gradient buckets");
+  for (int b = 0; b < kNB; ++b) {
+    ctx->grad_timed[b] = false;
+    ctx->grad_items[b] = int64_t(items[b].size());
+    ctx->grad_rows[b] = lc[b].rows;
+    double per_row = 0.0;
+    const double kt = kts[b];
+    for (uint32_t t : items[b]) {
+      per_row += 3.0 + kt;
+      for (uint32_t i = prog.offsets[t]; i < prog.offsets[t + 1]; ++i) {
+        const uint32_t opc = prog.code[i].op & SR_OP_MASK;
+        if (opc >= SR_OP_BINARY0) per_row += 3.0 + 2.0 * kt;
+        else if (opc >= SR_OP_UNARY0 && opc < SR_OP_LOAD_DERIVED) per_row += 2.0 + kt;
+      }
+    }
+    ctx->grad_flops[b] = per_row * double(n_eval);
+  }
   for (int b = 0; b < kNB; ++b) {
     const int64_t ni = int64_t(items[b].size());
     if (ni == 0) continue;
@@ -1750,7 +1805,12 @@ int eval_grad_impl(sr_ctx* ctx, const sr_dataset* ds, int opset_id, const sr_tre
       a.segs = reinterpret_cast<const SrSegment*>(ds_ + o_segs[b]);
       a.n_segs = int(segs[b].size());
     }
+    if (ctx->timing) SR_HIP_CHECK(hipEventRecord(ctx->ev_g0[b], s));
     SR_HIP_CHECK(sr_launch_grad_any<T>(a, kt, gather, lc[b].rows, int(lc[b].n_rb * lc[b].n_groups), s));
+    if (ctx->timing) {
+      SR_HIP_CHECK(hipEventRecord(ctx->ev_g1[b], s));
+      ctx->grad_timed[b] = true;
+    }
     SR_HIP_CHECK(sr_launch_grad_reduce(a.part, int(lc[b].n_rb), int(size_t(ni) * kt), ctx->g_out.as<double>() + o_vals[b], s));
   }
   double* out = ctx->h_grad.as<double>();  // (the staging image is no longer needed: the upload is done)
@@ -2357,6 +2417,10 @@ int sr_init(int device, sr_ctx** out) {
     if (e == hipSuccess) e = hipEventCreate(&ctx->ev_c0[c]);
     if (e == hipSuccess) e = hipEventCreate(&ctx->ev_c1[c]);
   }
+  for (int b = 0; b < sr_ctx::kGradBuckets; ++b) {
+    if (e == hipSuccess) e = hipEventCreate(&ctx->ev_g0[b]);
+    if (e == hipSuccess) e = hipEventCreate(&ctx->ev_g1[b]);
+  }
   if (e != hipSuccess) {
     delete ctx;
     return set_error(SR_ERR_HIP, std::string("stream/event creation: ") + hipGetErrorString(e));
@@ -2372,6 +2436,12 @@ int sr_shutdown(sr_ctx* ctx) {
     (void)hipSetDevice(ctx->device);
     (void)hipStreamSynchronize(ctx->stream);
     ctx->xport.reset();
+    if (ctx->hint.p == ctx->hint_reserve) {
+      ctx->hint.p = nullptr;
+      ctx->hint.cap = 0;
+    }
+    if (ctx->hint_reserve) (void)hipFree(ctx->hint_reserve);
+    ctx->hint_reserve = nullptr;
     for (DevBuf* b : {&ctx->prog, &ctx->outs, &ctx->part_sum, &ctx->part_flag, &ctx->pred, &ctx->row_idx, &ctx->tree_list, &ctx->range_lo, &ctx->range_hi, &ctx->range_sums, &ctx->packed,
                       &ctx->hint, &ctx->jsum_prog, &ctx->jsum_fin, &ctx->jsum_scratch, &ctx->probe_sum, &ctx->probe_flag, &ctx->g_code, &ctx->g_offsets, &ctx->g_consts, &ctx->g_const_off,
                       &ctx->g_items, &ctx->g_part, &ctx->g_out, &ctx->derived_cols, &ctx->probe_derived, &ctx->coll_buf, &ctx->coll_packed, &ctx->ctl, &ctx->fold_io})
@@ -2380,6 +2450,10 @@ int sr_shutdown(sr_ctx* ctx) {
     for (int c = 0; c < kMaxChunks; ++c) {
       (void)hipEventDestroy(ctx->ev_c0[c]);
       (void)hipEventDestroy(ctx->ev_c1[c]);
+    }
+    for (int b = 0; b < sr_ctx::kGradBuckets; ++b) {
+      (void)hipEventDestroy(ctx->ev_g0[b]);
+      (void)hipEventDestroy(ctx->ev_g1[b]);
     }
     (void)hipStreamSynchronize(ctx->stream2);
     (void)hipEventDestroy(ctx->ev_join);
@@ -3017,11 +3091,29 @@ int sr_set_tuning(sr_ctx* ctx, const char* name, int64_t value) {
     ctx->balance_groups = value != 0;
     return SR_OK;
   }
+  if (std::strcmp(name, "debug_hint_regrow") == 0) {  // tests: hint-array growth in place, stale epochs in it
+    ctx->debug_hint_regrow = value != 0 ? 1 : 0;
+    return SR_OK;
+  }
   if (std::strcmp(name, "inject_failure") == 0) {  // tests: the next `value` collective-buffer growths fail
     ctx->inject_fail = int(value);
     return SR_OK;
   }
   return set_error(SR_ERR_INVALID_ARG, std::string("unknown tuning knob '") + name + "'");
+}
+
+int sr_last_grad_info(sr_ctx* ctx, int n, double* kernel_ms, double* flops, int64_t* items, int* rows_per_lane) {
+  if (check_ctx(ctx) != SR_OK) return SR_ERR_INVALID_ARG;
+  Lock l(ctx);
+  for (int b = 0; b < n && b < sr_ctx::kGradBuckets; ++b) {
+    float m = 0.f;
+    if (kernel_ms)
+      kernel_ms[b] = (ctx->grad_timed[b] && hipEventElapsedTime(&m, ctx->ev_g0[b], ctx->ev_g1[b]) == hipSuccess) ? double(m) : 0.0;
+    if (flops) flops[b] = ctx->grad_flops[b];
+    if (items) items[b] = ctx->grad_items[b];
+    if (rows_per_lane) rows_per_lane[b] = ctx->grad_rows[b];
+  }
+  return SR_OK;
 }
 
 int sr_tuning_info(sr_ctx* ctx, int* used_derived_columns, int64_t* exact_trees) {

@@ -74,6 +74,7 @@ EXPORTED_SYMBOLS = (
     "sr_last_phase_ms",
     "sr_set_tuning",
     "sr_tuning_info",
+    "sr_last_grad_info",
     "sr_search_create",
     "sr_search_free",
     "sr_search_use_device",
@@ -236,6 +237,7 @@ def _load():
         "sr_last_phase_ms": (c_int, [P, POINTER(c_double), c_int]),
         "sr_set_tuning": (c_int, [P, ctypes.c_char_p, ctypes.c_int64]),
         "sr_tuning_info": (c_int, [P, POINTER(c_int), POINTER(c_int64)]),
+        "sr_last_grad_info": (c_int, [P, c_int, P, P, P, P]),
         "sr_search_create": (
             c_int,
             [c_int, c_int64, c_int64, c_int, POINTER(c_char_p), c_int, POINTER(c_char_p), POINTER(SrSearchOptions),

@@ -104,6 +104,19 @@ class DeviceContext:
         _lib.check(_lib.lib.sr_last_phase_ms(self.handle, out, 10))
         return int(out[9])
 
+    def last_grad_info(self):
+        """The last gradient call's tangent kernels per bucket (1, 2, 4, 8, 16 tangents): list of dicts
+        {kt, kernel_ms, flops, items, rows_per_lane} (csrc: sr_last_grad_info)."""
+        import numpy as np
+
+        ms, fl = np.zeros(5), np.zeros(5)
+        it = np.zeros(5, dtype=np.int64)
+        rp = np.zeros(5, dtype=np.int32)
+        p = lambda a: a.ctypes.data_as(ctypes.c_void_p)  # noqa: E731
+        _lib.check(_lib.lib.sr_last_grad_info(self.handle, 5, p(ms), p(fl), p(it), p(rp)))
+        return [dict(kt=k, kernel_ms=float(ms[b]), flops=float(fl[b]), items=int(it[b]), rows_per_lane=int(rp[b]))
+                for b, k in enumerate((1, 2, 4, 8, 16))]
+
     def last_launches(self):
         """Interpreter launches of the last eval_loss call (chunked compile/launch pipeline)."""
         out = (ctypes.c_double * 6)()

@@ -549,3 +549,28 @@ def test_wide_f64_dataset_large_view_falls_back_to_classic_kernel():
     tol, o_loss, o_comp, _ = loss_tolerance(orc, tb, X, y, rel_bar=1e-10)
     assert np.array_equal(comp, o_comp)
     assert_losses_within(loss, o_loss, comp, tol, "wide f64")
+
+
+def test_dead_tree_hints_survive_in_place_regrowth():
+    """VERDICT r3 #9 (the bug fixed in 58818aa): the dead-tree hint array is epoch-tagged and never
+    cleared between calls, so a grown array whose new words happen to equal the next call's epoch marks
+    live trees dead.  The debug hook grows it IN PLACE (same address) with exactly those stale words —
+    the bug's conditions — and every call must still equal the oracle; with the reallocation detected by
+    address instead of capacity, the grown part would keep its stale epochs and this test fails."""
+    opts = Options(**C2_OPTS)
+    X, y = _c2_data(1 << 17, seed=23)
+    d = Dataset(X, y)
+    orc = Oracle.from_options(opts)
+    ctx = sr_amd.get_context()
+    ctx.set_tuning("debug_hint_regrow", 1)
+    try:
+        for k, n_trees in enumerate((300, 1200, 3500)):  # each call grows the array
+            tb = flatten_trees(gen_random_population(n_trees, opts, 5, max_size=30, seed=40 + k), np.float32)
+            loss, comp = eval_loss_batch(tb, d, opts)
+            o_loss, o_comp = orc.eval_loss_batch(tb, X, y, n_threads=8)
+            assert np.array_equal(comp, o_comp), (n_trees, int(np.sum(comp != o_comp)))
+            assert 0.2 < comp.mean() < 0.9
+            sel = comp & np.isfinite(o_loss)
+            assert np.median(_rel(loss[sel], o_loss[sel])) < 1e-6
+    finally:
+        ctx.set_tuning("debug_hint_regrow", 0)
