@@ -404,6 +404,32 @@ def tree_sharded_line(ctx, tb, opts, eval_loss_tree_sharded, args, comm, world, 
     if ref_comp is not None:  # N = 1: the same answer as the single-GPU call
         out["equals_single_gpu"] = bool(np.array_equal(res["c"], ref_comp) and
                                         np.array_equal(res["l"][ref_comp], ref_loss[ref_comp]))
+    if world == 1:
+        # the overhead of the tree-sharded call at world 1 (<= 1.05x the single call on the
+        # same dataset), and the 8-rank projection: rank 0's share under the owners rule, scored by the
+        # single-GPU call (the per-rank work at N = 8; the results all-gather is not included)
+        from sr_amd.distributed import tree_owners
+
+        call, _ = single_gpu_call(ctx, tb, ds, opts)
+
+        def single():
+            t = time.perf_counter()
+            call()
+            return (time.perf_counter() - t) * 1e3
+        dt1, _, _ = timed(single, steps, warm, comm.barrier)
+        share = tb.take(np.nonzero(tree_owners(tb, 8) == 0)[0])
+        call8, _ = single_gpu_call(ctx, share, ds, opts)
+
+        def single8():
+            t = time.perf_counter()
+            call8()
+            return (time.perf_counter() - t) * 1e3
+        dt8, _, _ = timed(single8, steps, warm, comm.barrier)
+        t1, t8 = dt1 / steps * 1e3, dt8 / steps * 1e3
+        out["single_call_ms_per_step"] = t1
+        out["overhead_vs_single_call"] = out["ms_per_step"] / t1
+        out["projection_8_ranks"] = {"rank0_share_trees": share.n_trees, "rank0_share_ms": t8,
+                                     "efficiency_excluding_allgather": t1 / (8 * t8)}
     ds.free_device()
     return out
 

@@ -7,10 +7,7 @@
 #include "sr_fold.h"
 
 
-// One thread per launch position: Σ over row blocks in row-block order (bit-reproducible), OR of
-// flags (partials are laid out [row block][position], so neighbouring threads read neighbouring
-// words); the result goes to the caller's tree index perm[position].
-// One wave per tree: lane l folds row blocks l, l + 64, ... in order, then a fixed butterfly adds the
+// The result goes to the caller's tree index perm[position].  One wave per tree: lane l folds row blocks l, l + 64, ... in order, then a fixed butterfly adds the
 // 64 lane sums (deterministic: the same tree gives the same bits whatever the batch).  A thread per
 // tree walking every row block serialises its loads (C3's 196 row blocks: 47 us per call).
 __global__ void __launch_bounds__(256) sr_reduce_partials_kernel(const double* __restrict__ part_sum,
@@ -23,23 +20,8 @@ __global__ void __launch_bounds__(256) sr_reduce_partials_kernel(const double* _
   const int lane = int(threadIdx.x) & 63;
   const int pos = int(int64_t(blockIdx.x) * (blockDim.x / 64) + threadIdx.x / 64);
   if (pos >= n_trees) return;  // wave-uniform
-  double s = 0.0;
-  uint32_t f = 0u;
-  for (int i = lane; i < n_row_blocks; i += 64) {
-    s += part_sum[size_t(i) * n_trees + pos];
-    f |= part_flag[size_t(i) * n_trees + pos];
-  }
-#pragma unroll
-  for (int off = 32; off >= 1; off >>= 1) {
-    s += __shfl_xor(s, off, 64);
-    f |= __shfl_xor(f, off, 64);
-  }
-  if (lane == 0) {
-    const int tree = perm ? int(perm[pos]) : pos;
-    if (static_bad && static_bad[tree]) f |= SR_FLAG_STATIC | SR_FLAG_NONFINITE;
-    out_sum[tree] = s;
-    out_flag[tree] = f;
-  }
+  sr_reduce_positions<1, false>(part_sum, part_flag, n_trees, n_row_blocks, pos, 1, 1, perm, static_bad, out_sum,
+                                out_flag, lane);
 }
 
 // Julia's pairwise `sum` of one view, from its leaf folds: every thread combines one array's

@@ -188,6 +188,10 @@ struct sr_ctx {
 #endif
   int stress_probe = 1;  // SR_AMD_STRESS_PROBE: the probe runs the dataset's stress rows (below)
   int code_cache = 1;    // SR_AMD_CODE_CACHE: LDS program cache of the register-stack launches
+  // SR_AMD_FUSED_REDUCE: multi-row-block LOSS launches reduce their partials in the launch (the last
+  // workgroup of a tree group) when the group holds at most this many partials (0: a reduce launch)
+  int64_t fused_reduce = int64_t(1) << 30;
+  DevBuf group_cnt;      // its per-group counters (zeroed at allocation; each launch leaves them zero)
   int first_chunk = 6;   // SR_AMD_FIRST_CHUNK: the two-chunk pipeline's first chunk is 1/first_chunk
   // data-path transport of the sharded calls: the library's own RCCL over xGMI on its own HIP runtime
   // (sr_comm_init; torch's bundled runtime cannot share the GPU with this one in a process), or the
@@ -510,6 +514,11 @@ int run_batch(sr_ctx* ctx, const sr_dataset* ds, int opset_id, const sr_tree_bat
   const size_t n_part = size_t(nt) * size_t(n_rb);
   SR_HIP_CHECK(ctx->part_sum.ensure(n_part * sizeof(double) + 8));
   SR_HIP_CHECK(ctx->part_flag.ensure(n_part * sizeof(uint32_t) + 4));
+  if (mode == SR_MODE_LOSS && ctx->fused_reduce > 0 && size_t(nt) * sizeof(uint32_t) + 4 > ctx->group_cnt.cap) {
+    SR_HIP_CHECK(hipStreamSynchronize(s));  // (the second stream runs only inside a call)
+    SR_HIP_CHECK(ctx->group_cnt.ensure(size_t(nt) * sizeof(uint32_t) + 4));
+    SR_HIP_CHECK(hipMemset(ctx->group_cnt.p, 0, ctx->group_cnt.cap));
+  }
   ctx->outs_flag_off = align256(size_t(nt) * sizeof(double) + 8);
   const size_t outs_bytes = ctx->outs_flag_off + size_t(nt) * sizeof(uint32_t) + 4;
   SR_HIP_CHECK(ctx->outs.ensure(outs_bytes));
@@ -544,9 +553,11 @@ int run_batch(sr_ctx* ctx, const sr_dataset* ds, int opset_id, const sr_tree_bat
         ctx->hint.release();
         ctx->hint.p = ctx->hint_reserve;
       }
-      const size_t want = hint_bytes + hint_bytes / 4;
-      SR_HIP_CHECK(hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(static_cast<char*>(ctx->hint.p) + cap_before),
-                                     int(ctx->hint_epoch + 1), (want - cap_before) / 4, s));
+      // (word-aligned: an earlier ordinary allocation may have left an odd capacity)
+      const size_t from = (cap_before + 3) & ~size_t(3);
+      const size_t want = (hint_bytes + hint_bytes / 4 + 255) & ~size_t(255);
+      SR_HIP_CHECK(hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(static_cast<char*>(ctx->hint.p) + from),
+                                     int(ctx->hint_epoch + 1), (want - from) / 4, s));
       ctx->hint.cap = want;
     } else {
       if (ctx->hint.p == ctx->hint_reserve && ctx->hint_reserve != nullptr) {  // (leaving the debug mode)
@@ -870,6 +881,15 @@ int run_batch(sr_ctx* ctx, const sr_dataset* ds, int opset_id, const sr_tree_bat
         a.out_flag = ctx->d_out_flag + t0;
         a.static_bad = ctx->d_bad + t0;
       }
+      // several row blocks: the last workgroup of each tree group reduces it (no reduce launch)
+      const bool fused = !direct && mode == SR_MODE_LOSS && ctx->fused_reduce > 0 &&
+                         int64_t(g.G) * int64_t(g.n_row_blocks) <= ctx->fused_reduce;
+      if (fused) {
+        a.group_cnt = ctx->group_cnt.as<uint32_t>() + t0 + p0;
+        a.fused_sum = ctx->d_out_sum + t0;
+        a.fused_flag = ctx->d_out_flag + t0;
+        a.static_bad = ctx->d_bad + t0;
+      }
       if (use_probe && p0 == 0 && g.n_row_blocks >= 16 && (ctx->probe != 2 || c > 0)) {
         // Trees that are non-finite on the first rows are flagged before the main launch, so its
         // workgroups skip them from their first tile (without the probe, the ~16 row blocks that
@@ -883,6 +903,7 @@ int run_batch(sr_ctx* ctx, const sr_dataset* ds, int opset_id, const sr_tree_bat
         pa.out_sum = nullptr;
         pa.out_flag = nullptr;
         pa.code_lds = 0;  // (its groups differ from the main launch's)
+        pa.group_cnt = nullptr;
         pa.stamps = nullptr;
         pa.trees_per_block = std::max(16, g.W);
         pa.n_groups = int((np + pa.trees_per_block - 1) / pa.trees_per_block);
@@ -908,7 +929,7 @@ int run_batch(sr_ctx* ctx, const sr_dataset* ds, int opset_id, const sr_tree_bat
       a.stamps = ctx->stamps.as<uint64_t>();
 #endif
       SR_HIP_CHECK(sr_launch_eval<T>(a, mode, gather, tier, Rc, g.W, vstk, int(n_blocks), cs));
-      if (!direct)
+      if (!direct && !fused)
         SR_HIP_CHECK(sr_launch_reduce(a.part_sum, a.part_flag, int(np), g.n_row_blocks, a.perm,
                                     ctx->d_bad + t0, ctx->d_out_sum + t0, ctx->d_out_flag + t0, cs));
       return SR_OK;
@@ -2398,6 +2419,7 @@ int sr_init(int device, sr_ctx** out) {
   if (const char* v = std::getenv("SR_AMD_PROBE")) ctx->probe = std::atoi(v);
   if (const char* v = std::getenv("SR_AMD_STRESS_PROBE")) ctx->stress_probe = std::atoi(v);
   if (const char* v = std::getenv("SR_AMD_CODE_CACHE")) ctx->code_cache = std::atoi(v);
+  if (const char* v = std::getenv("SR_AMD_FUSED_REDUCE")) ctx->fused_reduce = std::atoll(v);
   if (const char* v = std::getenv("SR_AMD_FIRST_CHUNK")) ctx->first_chunk = std::max(2, std::atoi(v));
   if (const char* v = std::getenv("SR_AMD_HOST_IO")) ctx->host_io = std::atoi(v);
   if (const char* v = std::getenv("SR_AMD_SPIN")) ctx->spin = std::atoi(v);
@@ -2444,7 +2466,7 @@ int sr_shutdown(sr_ctx* ctx) {
     ctx->hint_reserve = nullptr;
     for (DevBuf* b : {&ctx->prog, &ctx->outs, &ctx->part_sum, &ctx->part_flag, &ctx->pred, &ctx->row_idx, &ctx->tree_list, &ctx->range_lo, &ctx->range_hi, &ctx->range_sums, &ctx->packed,
                       &ctx->hint, &ctx->jsum_prog, &ctx->jsum_fin, &ctx->jsum_scratch, &ctx->probe_sum, &ctx->probe_flag, &ctx->g_code, &ctx->g_offsets, &ctx->g_consts, &ctx->g_const_off,
-                      &ctx->g_items, &ctx->g_part, &ctx->g_out, &ctx->derived_cols, &ctx->probe_derived, &ctx->coll_buf, &ctx->coll_packed, &ctx->ctl, &ctx->fold_io})
+                      &ctx->g_items, &ctx->g_part, &ctx->g_out, &ctx->derived_cols, &ctx->probe_derived, &ctx->coll_buf, &ctx->coll_packed, &ctx->ctl, &ctx->fold_io, &ctx->group_cnt})
       b->release();
     for (HostBuf* b : {&ctx->h_prog, &ctx->h_outs, &ctx->h_grad, &ctx->h_coll}) b->release();
     for (int c = 0; c < kMaxChunks; ++c) {
@@ -3069,6 +3091,10 @@ int sr_set_tuning(sr_ctx* ctx, const char* name, int64_t value) {
   }
   if (std::strcmp(name, "probe") == 0) {  // dead-tree probe mode (SR_AMD_PROBE)
     ctx->probe = int(value);
+    return SR_OK;
+  }
+  if (std::strcmp(name, "fused_reduce") == 0) {  // in-launch partial reduction bound (SR_AMD_FUSED_REDUCE)
+    ctx->fused_reduce = value;
     return SR_OK;
   }
   if (std::strcmp(name, "code_cache") == 0) {  // LDS program cache (SR_AMD_CODE_CACHE)

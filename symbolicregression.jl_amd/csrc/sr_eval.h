@@ -21,6 +21,67 @@ struct SrSegment {
   int64_t row_off;
 };
 
+// Per-tree reduction of [row block][position] partials, one wave per tree: lane l folds row blocks
+// l, l + 64, ... in order, then a fixed shfl_xor butterfly adds the 64 lane sums; lane 0 writes the
+// tree's Σ and OR of flags (static_bad ORed in) at perm[position].  The SAME arithmetic serves the
+// reduce launch and the in-launch reduction (bit-identical results).  The wave handles `count`
+// positions pos0, pos0 + step, ...; K of them at a time, so their loads are in flight together.
+// SC1: the partials were written by other workgroups in this launch (write-through `sc1` stores):
+// read them with `sc1` loads, which bypass this CU's L1.
+template <int K, bool SC1>
+__device__ inline void sr_reduce_positions(const double* part_sum, const uint32_t* part_flag, int n_trees,
+                                           int n_row_blocks, int pos0, int step, int count,
+                                           const uint32_t* perm, const uint8_t* static_bad, double* out_sum,
+                                           uint32_t* out_flag, int lane) {
+  for (int j0 = 0; j0 < count; j0 += K) {
+    double s[K];
+    uint32_t f[K];
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+      s[k] = 0.0;
+      f[k] = 0u;
+    }
+    for (int i = lane; i < n_row_blocks; i += 64) {
+#pragma unroll
+      for (int k = 0; k < K; ++k) {
+        if (j0 + k < count) {
+          const size_t o = size_t(i) * size_t(n_trees) + size_t(pos0 + (j0 + k) * step);
+          if (SC1) {
+            s[k] += __longlong_as_double(static_cast<long long>(__hip_atomic_load(
+                reinterpret_cast<unsigned long long*>(const_cast<double*>(part_sum + o)), __ATOMIC_RELAXED,
+                __HIP_MEMORY_SCOPE_AGENT)));
+            f[k] |= __hip_atomic_load(const_cast<uint32_t*>(part_flag + o), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          } else {
+            s[k] += part_sum[o];
+            f[k] |= part_flag[o];
+          }
+        }
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+#pragma unroll
+      for (int off = 32; off >= 1; off >>= 1) {
+        s[k] += __shfl_xor(s[k], off, 64);
+        f[k] |= __shfl_xor(f[k], off, 64);
+      }
+    }
+    if (lane == 0) {
+#pragma unroll
+      for (int k = 0; k < K; ++k) {
+        if (j0 + k < count) {
+          const int pos = pos0 + (j0 + k) * step;
+          const int tree = perm ? int(perm[pos]) : pos;
+          uint32_t fl = f[k];
+          if (static_bad && static_bad[tree]) fl |= SR_FLAG_STATIC | SR_FLAG_NONFINITE;
+          out_sum[tree] = s[k];
+          out_flag[tree] = fl;
+        }
+      }
+    }
+  }
+}
+
 template <typename T>
 struct SrEvalArgs {
   // programs
@@ -62,7 +123,14 @@ struct SrEvalArgs {
   double* out_sum;
   uint32_t* out_flag;
   const uint8_t* static_bad;
-  T* pred;                     // PRED: [n_trees][pred_ld]
+  // several row blocks, reduced in the launch (LOSS; NULL: a reduce launch follows): the last row
+  // block of a tree group to finish reduces the group's partials into fused_sum / fused_flag (tree
+  // order, static_bad ORed in), in sr_reduce_partials_kernel's order; group_cnt[first position of
+  // the group] counts the group's finished blocks (zero between launches: the last one resets it)
+  uint32_t* group_cnt;
+  double* fused_sum;
+  uint32_t* fused_flag;
+  T* pred;                   // PRED: [n_trees][pred_ld]
   int64_t pred_ld;
   // EXACT mode (perm = listed trees): row block rb = row range [range_lo[rb], range_hi[rb]] of the
   // view; range_sums[list position][check][rb] (T) = Julia-order sum of the checked array over it

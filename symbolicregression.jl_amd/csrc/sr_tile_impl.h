@@ -1242,11 +1242,36 @@ __global__ void __launch_bounds__(W * 64, (SrMinWavesFor<T, R, TIER, W, VSTK>::v
       if (a.static_bad[tree]) f |= SR_FLAG_STATIC | SR_FLAG_NONFINITE;
       a.out_sum[tree] = accv;
       a.out_flag[tree] = f;
+    } else if (MODE == SR_MODE_LOSS && a.group_cnt) {  // write-through (sc1): read by another workgroup
+      const size_t o = size_t(rb) * a.n_trees + my_pos;
+      __hip_atomic_store(reinterpret_cast<unsigned long long*>(a.part_sum + o),
+                         static_cast<unsigned long long>(__double_as_longlong(accv)), __ATOMIC_RELAXED,
+                         __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(a.part_flag + o, f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     } else {
       const size_t o = size_t(rb) * a.n_trees + my_pos;  // [row block][position]: a block writes one run
       a.part_sum[o] = accv;
       a.part_flag[o] = f;
     }
+  }
+  if (MODE == SR_MODE_LOSS && a.group_cnt && a.out_sum == nullptr) {
+    // In-launch reduction (the hand-off of MI355X_MICROARCH.md's visibility table, first row): every
+    // wave drains its sc1 stores, the workgroup barrier orders them before ONE agent-scope add per
+    // workgroup on the group's counter; the block whose add comes last reduces the group (sc1 loads)
+    // and resets the counter.  Each wave reduces its own positions, K at a time.
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    int* last_word = reinterpret_cast<int*>(sr_smem + plan.x);  // (the tiles are done with the LDS)
+    if (tid == 0) {
+      const uint32_t prev = __hip_atomic_fetch_add(a.group_cnt + tree0, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      const bool last = prev == uint32_t(a.n_row_blocks - 1);
+      if (last) __hip_atomic_store(a.group_cnt + tree0, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      *last_word = last ? 1 : 0;
+    }
+    __syncthreads();
+    if (*last_word)
+      sr_reduce_positions<8, true>(a.part_sum, a.part_flag, a.n_trees, a.n_row_blocks, tree0 + wave, SR_WAVES, S,
+                                   a.perm, a.static_bad, a.fused_sum, a.fused_flag, lane);
   }
   SR_STAMP(6);
 }

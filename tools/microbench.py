@@ -1,7 +1,9 @@
 """Kernel-time breakdown by operator mix (GPU box).  Prints one line per population."""
 import os, sys, time
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-sys.path[:0] = [os.path.join(ROOT, "symbolicregression.jl_amd")]
+# SR_AMD_PKG=ab/<name>: another revision's package + library (tools/ab_lib.sh)
+sys.path[:0] = [os.path.join(ROOT, os.environ["SR_AMD_PKG"]) if os.environ.get("SR_AMD_PKG")
+                else os.path.join(ROOT, "symbolicregression.jl_amd")]
 import numpy as np
 import sr_amd
 from sr_amd import Options, Dataset, flatten_trees, gen_random_population, eval_loss_batch
