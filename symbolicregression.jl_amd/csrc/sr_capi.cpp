@@ -187,10 +187,11 @@ struct sr_ctx {
   int64_t n_stamps = 0;
 #endif
   int stress_probe = 1;  // SR_AMD_STRESS_PROBE: the probe runs the dataset's stress rows (below)
-  int code_cache = 1;    // SR_AMD_CODE_CACHE: LDS program cache of the register-stack launches
+  int code_cache = 1;    // SR_AMD_CODE_CACHE: LDS program cache (1: register-stack launches, 2: also the classic ones)
   // SR_AMD_FUSED_REDUCE: multi-row-block LOSS launches reduce their partials in the launch (the last
   // workgroup of a tree group) when the group holds at most this many partials (0: a reduce launch)
   int64_t fused_reduce = int64_t(1) << 30;
+  int grad_rows_force = 0;  // SR_AMD_GRAD_ROWS / "grad_rows": the gradient kernel's rows per lane (0: chosen per call)
   DevBuf group_cnt;      // its per-group counters (zeroed at allocation; each launch leaves them zero)
   int first_chunk = 6;   // SR_AMD_FIRST_CHUNK: the two-chunk pipeline's first chunk is 1/first_chunk
   // data-path transport of the sharded calls: the library's own RCCL over xGMI on its own HIP runtime
@@ -857,14 +858,17 @@ int run_batch(sr_ctx* ctx, const sr_dataset* ds, int opset_id, const sr_tree_bat
       // each): sized for the longest group span of this launch, capped by that budget (groups longer
       // than the cap stream their windows from global memory)
       a.code_lds = 0;
-      if (vstk && mode == SR_MODE_LOSS && ctx->code_cache && size_t(g.lds) < kCodeCacheLds) {
+      // (code_cache 2: the classic LDS-stack launches too, within 48 KiB per workgroup so that three
+      //  still share a CU — with SR_AMD_HOST_IO=2 the programs then cross PCIe once per workgroup)
+      const size_t code_budget = vstk ? kCodeCacheLds : (ctx->code_cache >= 2 ? size_t(48) * 1024 : 0);
+      if (mode == SR_MODE_LOSS && ctx->code_cache && size_t(g.lds) < code_budget) {
         int64_t maxspan = 0;
         for (int64_t q = 0; q < g.n_groups; ++q) {
           const int64_t pf = p0 + q * g.G, pl = std::min<int64_t>(p0 + np, pf + g.G) - 1;
           const int64_t sp = int64_t(h_end[t0 + h_perm[t0 + pl]]) - int64_t(h_off[t0 + h_perm[t0 + pf]]);
           maxspan = std::max(maxspan, sp);
         }
-        const int64_t cap = int64_t((kCodeCacheLds - size_t(g.lds)) / 16);
+        const int64_t cap = int64_t((code_budget - size_t(g.lds)) / 16);
         a.code_lds = int(std::min(maxspan, cap));
         if (a.code_lds < 64) a.code_lds = 0;
       }
@@ -1747,20 +1751,25 @@ int eval_grad_impl(sr_ctx* ctx, const sr_dataset* ds, int opset_id, const sr_tre
     // default's tile + stacks would not fit (many features, Float64, deep trees: ADVICE r3)
     int bdepth = 1;
     for (uint32_t t : items[b]) bdepth = std::max(bdepth, int(prog.depth[t]));
-    const int rows = sr_grad_launch_rows(int(sizeof(T)), kt, int(ds->nf), ds->w != nullptr, bdepth, kWaves, kLdsMax);
+    const int rows = sr_grad_launch_rows(int(sizeof(T)), kt, int(ds->nf), ds->w != nullptr, bdepth, kWaves, kLdsMax,
+                                         ctx->grad_rows_force);
     if (rows == 0) return set_error(SR_ERR_TOO_DEEP, "gradient tile needs more than 160 KiB of LDS");
-    const int64_t rows_per_tile = 64 * int64_t(rows);
-    const int64_t n_tiles = (n_eval + rows_per_tile - 1) / rows_per_tile;
     int64_t n_groups = (ni + kWaves - 1) / kWaves;
     if (!segs[b].empty()) {  // (view-pure groups: a few more than ni / kWaves)
       n_groups = 0;
       for (const SrSegment& sg : segs[b]) n_groups += sg.groups;
     }
+    // row blocks in units of 512 rows (64 lanes x the largest rows per lane): they cover the same rows
+    // whatever the rows per lane, and a lane accumulates its rows (lane mod 64) in row order inside a
+    // block either way, so the gradients are bit-identical for every rows-per-lane choice
+    constexpr int64_t kUnit = 512;
+    const int64_t n_units = (n_eval + kUnit - 1) / kUnit;
     int64_t n_rb = (4096 + n_groups - 1) / n_groups;
-    if (n_rb > n_tiles) n_rb = n_tiles;
+    if (n_rb > n_units) n_rb = n_units;
     if (n_rb < 1) n_rb = 1;
-    const int64_t tiles_per_block = (n_tiles + n_rb - 1) / n_rb;
-    n_rb = (n_tiles + tiles_per_block - 1) / tiles_per_block;
+    const int64_t units_per_block = (n_units + n_rb - 1) / n_rb;
+    n_rb = (n_units + units_per_block - 1) / units_per_block;
+    const int64_t tiles_per_block = units_per_block * (kUnit / (64 * int64_t(rows)));
     if (n_rb * n_groups > 0x7fffffff) return set_error(SR_ERR_INVALID_ARG, "grid too large");
     int64_t blk = 0;  // segments' first blocks
     for (SrSegment& sg : segs[b]) {
@@ -2420,6 +2429,7 @@ int sr_init(int device, sr_ctx** out) {
   if (const char* v = std::getenv("SR_AMD_STRESS_PROBE")) ctx->stress_probe = std::atoi(v);
   if (const char* v = std::getenv("SR_AMD_CODE_CACHE")) ctx->code_cache = std::atoi(v);
   if (const char* v = std::getenv("SR_AMD_FUSED_REDUCE")) ctx->fused_reduce = std::atoll(v);
+  if (const char* v = std::getenv("SR_AMD_GRAD_ROWS")) ctx->grad_rows_force = std::atoi(v);
   if (const char* v = std::getenv("SR_AMD_FIRST_CHUNK")) ctx->first_chunk = std::max(2, std::atoi(v));
   if (const char* v = std::getenv("SR_AMD_HOST_IO")) ctx->host_io = std::atoi(v);
   if (const char* v = std::getenv("SR_AMD_SPIN")) ctx->spin = std::atoi(v);
@@ -3093,12 +3103,16 @@ int sr_set_tuning(sr_ctx* ctx, const char* name, int64_t value) {
     ctx->probe = int(value);
     return SR_OK;
   }
+  if (std::strcmp(name, "grad_rows") == 0) {  // gradient kernel rows per lane (SR_AMD_GRAD_ROWS; 0: automatic)
+    ctx->grad_rows_force = int(value);
+    return SR_OK;
+  }
   if (std::strcmp(name, "fused_reduce") == 0) {  // in-launch partial reduction bound (SR_AMD_FUSED_REDUCE)
     ctx->fused_reduce = value;
     return SR_OK;
   }
   if (std::strcmp(name, "code_cache") == 0) {  // LDS program cache (SR_AMD_CODE_CACHE)
-    ctx->code_cache = value != 0 ? 1 : 0;
+    ctx->code_cache = int(value < 0 ? 0 : (value > 2 ? 2 : value));
     return SR_OK;
   }
   if (std::strcmp(name, "timing") == 0) {  // 0: record no timing events (kernel times read as 0)

@@ -226,26 +226,30 @@ struct SrGradArgs {
 // rows: rows per lane, sr_grad_rows_per_lane(kt) or 1 (sr_grad_launch_rows)
 template <typename T>
 hipError_t sr_launch_grad_any(const SrGradArgs<T>& a, int kt, bool gather, int rows, int n_blocks, hipStream_t s);
-// Rows per lane of the gradient kernel for KT tangents (a staged tile is 64 x that many rows).
-// (the same for Float64: halving its rows, to bring its ~230-256 VGPRs down, changed the gradient
-// sums' row-block order and with it chaotic C5 optimiser trajectories; not kept)
-constexpr int sr_grad_rows_per_lane(int kt, int elem_size = 4) {
-  return (void)elem_size, kt <= 2 ? 8 : (kt <= 4 ? 4 : (kt <= 8 ? 2 : 1));
-}
+// Largest rows per lane of the gradient kernel for KT tangents (a staged tile is 64 x that many rows);
+// kernels exist for it, its halves down to 2, and 1.
+constexpr int sr_grad_rows_per_lane(int kt) { return kt <= 2 ? 8 : (kt <= 4 ? 4 : (kt <= 8 ? 2 : 1)); }
 // LDS of one gradient workgroup (W waves): the X / y / w tile and the waves' operand stacks (value +
 // KT tangents per row, stack_depth slots)
 inline size_t sr_grad_lds_bytes(int elem_size, int kt, int rows, int nf, bool weighted, int stack_depth, int waves) {
   return (size_t(nf) + 1 + (weighted ? 1 : 0)) * 64 * size_t(rows) * size_t(elem_size) +
          size_t(waves) * size_t(stack_depth) * size_t(1 + kt) * size_t(rows) * 64 * size_t(elem_size);
 }
-// Rows per lane a bucket of KT tangents runs with: the default, or 1 when the default's tile and stack
-// (at the bucket's own deepest program) would pass `lds_max` (many features, Float64, deep stacks:
-// ADVICE r3); 0 when even one row per lane does not fit.
-inline int sr_grad_launch_rows(int elem_size, int kt, int nf, bool weighted, int stack_depth, int waves, size_t lds_max) {
-  const int rd = sr_grad_rows_per_lane(kt, elem_size);
-  if (sr_grad_lds_bytes(elem_size, kt, rd, nf, weighted, stack_depth, waves) <= lds_max) return rd;
-  if (sr_grad_lds_bytes(elem_size, kt, 1, nf, weighted, stack_depth, waves) <= lds_max) return 1;
-  return 0;
+// Rows per lane a bucket of KT tangents runs with (results do not depend on it): `force` when it is
+// one the kernels exist for and fits; otherwise the preferred count (Float32: the largest; Float64:
+// half of it — the f64 value and tangents of 8 rows need ~190 VGPRs, two waves per SIMD), halved
+// while the workgroup's LDS (tile + operand stacks, which grow with the bucket's deepest program)
+// passes lds_max / 2, so that two workgroups share a CU; 0 when even one row per lane does not fit.
+inline int sr_grad_launch_rows(int elem_size, int kt, int nf, bool weighted, int stack_depth, int waves, size_t lds_max,
+                               int force = 0) {
+  const int rmax = sr_grad_rows_per_lane(kt);
+  auto fits = [&](int r, size_t cap) { return sr_grad_lds_bytes(elem_size, kt, r, nf, weighted, stack_depth, waves) <= cap; };
+  auto valid = [&](int r) { return r == 1 || (r <= rmax && r >= 2 && (r & (r - 1)) == 0); };
+  if (force > 0 && valid(force) && fits(force, lds_max)) return force;
+  int r = elem_size == 8 && rmax > 1 ? rmax / 2 : rmax;
+  while (r > 1 && !fits(r, lds_max / 2)) r /= 2;
+  if (fits(r, lds_max)) return r;
+  return fits(1, lds_max) ? 1 : 0;
 }
 hipError_t sr_launch_grad_reduce(const double* part, int n_row_blocks, int n_vals, double* out, hipStream_t s);
 // The reference's loss fold in row order for listed trees (sr_fold.h; sr_aux.hip): predictions

@@ -1,31 +1,20 @@
-// sr_grad.hip — forward-mode constant-gradient kernels (f32 / f64, 1 / 2 / 4 / 8 / 16 tangents per pass)
-// and their launcher used by the C ABI (sr_eval_grad_batch).
+// sr_grad.hip — forward-mode constant-gradient kernels (Float32; 1 / 2 / 4 / 8 / 16 tangents per pass),
+// their partial reduction, and the launcher used by the C ABI (sr_eval_grad_batch).
 #include "sr_grad_impl.h"
 
-template <typename T, bool GATHER, int KT>
-hipError_t sr_launch_grad_rows(const SrGradArgs<T>& a, int rows, int n_blocks, hipStream_t s) {
-  constexpr int RD = sr_grad_rows_per_lane(KT);
-  if (rows == RD) return sr_launch_grad<T, KT, 4, GATHER, RD>(a, n_blocks, s);
-  if constexpr (RD != 1) {
-    if (rows == 1) return sr_launch_grad<T, KT, 4, GATHER, 1>(a, n_blocks, s);
-  }
-  return hipErrorInvalidValue;
-}
-
-template <typename T>
-hipError_t sr_launch_grad_any(const SrGradArgs<T>& a, int kt, bool gather, int rows, int n_blocks, hipStream_t s) {
-  auto go = [&](auto g) -> hipError_t {
-    constexpr bool G = decltype(g)::value;
-    switch (kt) {
-      case 1: return sr_launch_grad_rows<T, G, 1>(a, rows, n_blocks, s);
-      case 2: return sr_launch_grad_rows<T, G, 2>(a, rows, n_blocks, s);
-      case 4: return sr_launch_grad_rows<T, G, 4>(a, rows, n_blocks, s);
-      case 8: return sr_launch_grad_rows<T, G, 8>(a, rows, n_blocks, s);
-      case 16: return sr_launch_grad_rows<T, G, 16>(a, rows, n_blocks, s);
-      default: return hipErrorInvalidValue;
-    }
-  };
-  return gather ? go(std::true_type{}) : go(std::false_type{});
+// Σ over row blocks of the [row block][item][KT] partials -> out[item][KT], one wave per value: lane
+// l folds row blocks l, l + 64, ... in order and a fixed butterfly adds the lanes (deterministic; a
+// thread per value walking ~160 row blocks serially took 46 us per launch in C3's searches).
+__global__ void __launch_bounds__(256) sr_grad_reduce_kernel(const double* __restrict__ part, int n_row_blocks,
+                                                              int n_vals, double* __restrict__ out) {
+  const int lane = int(threadIdx.x) & 63;
+  const int i = int(int64_t(blockIdx.x) * (blockDim.x / 64) + threadIdx.x / 64);
+  if (i >= n_vals) return;  // wave-uniform
+  double s = 0.0;
+  for (int b = lane; b < n_row_blocks; b += 64) s += part[size_t(b) * n_vals + i];
+#pragma unroll
+  for (int off = 32; off >= 1; off >>= 1) s += __shfl_xor(s, off, 64);
+  if (lane == 0) out[i] = s;
 }
 
 hipError_t sr_launch_grad_reduce(const double* part, int n_row_blocks, int n_vals, double* out, hipStream_t s) {
@@ -36,4 +25,4 @@ hipError_t sr_launch_grad_reduce(const double* part, int n_row_blocks, int n_val
 }
 
 template hipError_t sr_launch_grad_any<float>(const SrGradArgs<float>&, int, bool, int, int, hipStream_t);
-template hipError_t sr_launch_grad_any<double>(const SrGradArgs<double>&, int, bool, int, int, hipStream_t);
+// (Float64: sr_grad_f64.hip, a translation unit of its own so the two compile in parallel)

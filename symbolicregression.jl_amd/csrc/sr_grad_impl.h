@@ -42,17 +42,65 @@ __device__ __forceinline__ T sr_readlane_val(T v, uint32_t l) {
   }
 }
 
-// Rows per lane by tangent width (8 for 1-2 tangents, 4 for 4, 2 for 8, 1 for 16): the value and its
-// KT tangents of R rows stay in VGPRs, so one
-// dispatch of an instruction covers R x 64 rows (round 3: one row per lane made every dispatch and
-// operand decode cover 64 rows only; C3's gradient launches 0.61 ms each).
-template <typename T, int KT>
-struct SrGradRows {
-  static constexpr int value = sr_grad_rows_per_lane(KT, int(sizeof(T)));
-};
+// Row callees (noinline: their temporaries live in the callee's own registers, so the kernel's VGPR
+// count — and with it its occupancy — is set by the interpreter loop, not by the largest operator body;
+// round 3's Float64 kernels inlined every operator into a row-unrolled switch: 256 VGPRs, one wave per
+// SIMD).  Value rows, derivative rows, and the operators outside the BASIC set.
+template <typename T, int R>
+using SrGVec = T __attribute__((ext_vector_type(R)));
+template <typename T, int R>
+__device__ __attribute__((noinline)) SrGVec<T, R> sr_grad_unary_val(uint32_t u, SrGVec<T, R> x) {
+#pragma unroll
+  for (int r = 0; r < R; ++r) {
+    x[r] = sr_unary<T>(u, x[r]);
+    __builtin_amdgcn_sched_barrier(0);
+  }
+  return x;
+}
+template <typename T, int R>
+__device__ __attribute__((noinline)) SrGVec<T, R> sr_grad_unary_der(uint32_t u, SrGVec<T, R> x, SrGVec<T, R> y) {
+#pragma unroll
+  for (int r = 0; r < R; ++r) {
+    x[r] = sr_unary_deriv<T>(u, x[r], y[r]);
+    __builtin_amdgcn_sched_barrier(0);
+  }
+  return x;
+}
+template <typename T, int R>
+__device__ __attribute__((noinline)) SrGVec<T, R> sr_grad_binary_val(uint32_t b, SrGVec<T, R> x, SrGVec<T, R> y) {
+#pragma unroll
+  for (int r = 0; r < R; ++r) {
+    x[r] = sr_binary<T>(b, x[r], y[r]);
+    __builtin_amdgcn_sched_barrier(0);
+  }
+  return x;
+}
+// WHICH = 0: d r / d a, 1: d r / d b
+template <typename T, int R, int WHICH>
+__device__ __attribute__((noinline)) SrGVec<T, R> sr_grad_binary_der(uint32_t b, SrGVec<T, R> x, SrGVec<T, R> y,
+                                                                      SrGVec<T, R> res) {
+#pragma unroll
+  for (int r = 0; r < R; ++r) {
+    T pa, pb;
+    sr_binary_partials<T>(b, x[r], y[r], res[r], &pa, &pb);
+    x[r] = WHICH == 0 ? pa : pb;
+    __builtin_amdgcn_sched_barrier(0);
+  }
+  return x;
+}
+template <typename T, int R>
+__device__ __attribute__((noinline)) SrGVec<T, R> sr_grad_loss_der(int kind, SrGVec<T, R> pred, SrGVec<T, R> y, T p) {
+#pragma unroll
+  for (int r = 0; r < R; ++r) {
+    pred[r] = sr_elem_loss_deriv<T>(kind, pred[r], y[r], p);
+    __builtin_amdgcn_sched_barrier(0);
+  }
+  return pred;
+}
 
-// R: rows per lane (SrGradRows' default, or 1 when the default's LDS operand stack would not fit:
-// sr_grad_launch_rows)
+// R: rows per lane (sr_grad_launch_rows: up to 8 for 1-2 tangents, 4 for 4, 2 for 8, 1 for 16): the
+// value and its KT tangents of R rows stay in VGPRs, so one dispatch of an instruction covers R x 64
+// rows (round 3: one row per lane made every dispatch and operand decode cover 64 rows only).
 template <typename T, int KT, int W, bool GATHER, int R>
 __global__ void __launch_bounds__(W * 64) sr_grad_kernel(const SrGradArgs<T> a) {
   // rows per lane: lane + 64 j, j < R
@@ -173,82 +221,189 @@ __global__ void __launch_bounds__(W * 64) sr_grad_kernel(const SrGradArgs<T> a) 
           }
         } else if (opc < SR_OP_BINARY0) {
           const uint32_t u = opc >= SR_OP_UNARY_INF0 ? opc - SR_OP_UNARY_INF0 : opc - SR_OP_UNARY0;
-          // the operator chosen once per instruction (a compile-time operator inside the row loop),
-          // not once per row; operators outside the BASIC set take the generic loop
-          auto unary_rows = [&](auto op_c) {
-            constexpr uint32_t UID = decltype(op_c)::value;
-            const uint32_t uu = UID == 0xffffffffu ? u : UID;
-#pragma unroll
-            for (int j = 0; j < R; ++j) {
-              const T x = v[j];
-              const T yv = sr_unary<T>(uu, x);
-              // (fused unaries: complete trees have finite inner values, so INFSUB never fires)
-              const T dfx = sr_unary_deriv<T>(uu, x, yv);
-              v[j] = yv;
-#pragma unroll
-              for (int q = 0; q < KT; ++q) dv[j][q] = dfx * dv[j][q];
-            }
-          };
-#define SR_GU(ID) \
-  case ID: unary_rows(std::integral_constant<uint32_t, ID>{}); break;
+          // value and derivative rows: the BASIC operators with the loss kernel's own row bodies
+          // (sr_unary_rows: the same values), the rest through the noinline row callees
+          // (fused unaries: complete trees have finite inner values, so INFSUB never fires)
+          T dfx[R];
           switch (u) {
-            SR_GU(SR_U_NEG) SR_GU(SR_U_SQUARE) SR_GU(SR_U_CUBE) SR_GU(SR_U_EXP) SR_GU(SR_U_COS)
-            SR_GU(SR_U_SIN) SR_GU(SR_U_LOG) SR_GU(SR_U_SQRT) SR_GU(SR_U_ABS)
-            default: unary_rows(std::integral_constant<uint32_t, 0xffffffffu>{}); break;
+            case SR_U_NEG:
+#pragma unroll
+              for (int j = 0; j < R; ++j) {
+                v[j] = -v[j];
+                dfx[j] = T(-1);
+              }
+              break;
+            case SR_U_SQUARE:
+#pragma unroll
+              for (int j = 0; j < R; ++j) {
+                const T x = v[j];
+                v[j] = x * x;
+                dfx[j] = T(2) * x;
+              }
+              break;
+            case SR_U_CUBE:
+#pragma unroll
+              for (int j = 0; j < R; ++j) {
+                const T x = v[j];
+                v[j] = x * x * x;
+                dfx[j] = T(3) * x * x;
+              }
+              break;
+            case SR_U_ABS:
+#pragma unroll
+              for (int j = 0; j < R; ++j) {
+                const T x = v[j];
+                v[j] = sr_unary<T>(SR_U_ABS, x);
+                dfx[j] = sr_unary_deriv<T>(SR_U_ABS, x, v[j]);
+              }
+              break;
+            case SR_U_SQRT:
+#pragma unroll
+              for (int j = 0; j < R; ++j) {
+                v[j] = sr_unary<T>(SR_U_SQRT, v[j]);
+                dfx[j] = T(0.5) / v[j];
+              }
+              break;
+            case SR_U_EXP:
+              sr_unary_rows<T, SR_U_EXP, R>(v);
+#pragma unroll
+              for (int j = 0; j < R; ++j) dfx[j] = v[j];
+              break;
+            case SR_U_LOG:
+#pragma unroll
+              for (int j = 0; j < R; ++j) dfx[j] = T(1) / v[j];
+              sr_unary_rows<T, SR_U_LOG, R>(v);
+              break;
+            case SR_U_COS:
+#pragma unroll
+              for (int j = 0; j < R; ++j) dfx[j] = v[j];
+              sr_unary_rows<T, SR_U_COS, R>(v);
+              sr_unary_rows<T, SR_U_SIN, R>(dfx);
+#pragma unroll
+              for (int j = 0; j < R; ++j) dfx[j] = -dfx[j];
+              break;
+            case SR_U_SIN:
+#pragma unroll
+              for (int j = 0; j < R; ++j) dfx[j] = v[j];
+              sr_unary_rows<T, SR_U_SIN, R>(v);
+              sr_unary_rows<T, SR_U_COS, R>(dfx);
+              break;
+            default: {
+              SrGVec<T, R> x, y;
+#pragma unroll
+              for (int j = 0; j < R; ++j) x[j] = v[j];
+              y = sr_grad_unary_val<T, R>(u, x);
+              x = sr_grad_unary_der<T, R>(u, x, y);
+#pragma unroll
+              for (int j = 0; j < R; ++j) {
+                v[j] = y[j];
+                dfx[j] = x[j];
+              }
+              break;
+            }
           }
-#undef SR_GU
+#pragma unroll
+          for (int j = 0; j < R; ++j) {
+#pragma unroll
+            for (int q = 0; q < KT; ++q) dv[j][q] = dfx[j] * dv[j][q];
+          }
         } else {
           const uint32_t b = (opc - SR_OP_BINARY0) / 6u + 1u;
           const bool left = variant == SR_V_SL || variant == SR_V_FL || variant == SR_V_CL;
-          auto binary_rows = [&](auto op_c) {
+          // operand row j: value and tangents (feature / stack slot / constant)
+          auto operand = [&](int j, T& ov, T (&od)[KT]) {
+            if (from_feat) {
+              ov = xrow[j * 64];
+#pragma unroll
+              for (int q = 0; q < KT; ++q) od[q] = T(0);
+            } else if (from_stack) {
+              ov = sp[j * 64];
+#pragma unroll
+              for (int q = 0; q < KT; ++q) od[q] = sp[((q + 1) * R + j) * 64];
+            } else {
+              ov = cv;
+#pragma unroll
+              for (int q = 0; q < KT; ++q) od[q] = q == jj ? T(1) : T(0);
+            }
+          };
+          auto tangents = [&](int j, T pa, T pbv, const T (&od)[KT]) {
+            if (left) {
+#pragma unroll
+              for (int q = 0; q < KT; ++q) dv[j][q] = __builtin_fma(pa, od[q], pbv * dv[j][q]);
+            } else {
+#pragma unroll
+              for (int q = 0; q < KT; ++q) dv[j][q] = __builtin_fma(pa, dv[j][q], pbv * od[q]);
+            }
+          };
+          auto basic_rows = [&](auto op_c) {
             constexpr uint32_t BID = decltype(op_c)::value;
-            const uint32_t bb = BID == 0xffffffffu ? b : BID;
 #pragma unroll
             for (int j = 0; j < R; ++j) {
-              // operand (value + tangents) of row j: feature / stack slot / constant
               T ov, od[KT];
-              if (from_feat) {
-                ov = xrow[j * 64];
-#pragma unroll
-                for (int q = 0; q < KT; ++q) od[q] = T(0);
-              } else if (from_stack) {
-                ov = sp[j * 64];
-#pragma unroll
-                for (int q = 0; q < KT; ++q) od[q] = sp[((q + 1) * R + j) * 64];
-              } else {
-                ov = cv;
-#pragma unroll
-                for (int q = 0; q < KT; ++q) od[q] = q == jj ? T(1) : T(0);
-              }
+              operand(j, ov, od);
               const T av = left ? ov : v[j], bv = left ? v[j] : ov;
-              const T rv = sr_binary<T>(bb, av, bv);
+              const T rv = sr_binary<T>(BID, av, bv);
               T pa, pbv;
-              sr_binary_partials<T>(bb, av, bv, rv, &pa, &pbv);
-              v[j] = rv;
-              if (left) {
-#pragma unroll
-                for (int q = 0; q < KT; ++q) dv[j][q] = __builtin_fma(pa, od[q], pbv * dv[j][q]);
+              if constexpr (BID == SR_B_DIV) {  // d/da = 1/b, d/db = -(a/b)/b = -r (1/b): one division fewer
+                pa = T(1) / bv;
+                pbv = -rv * pa;
               } else {
-#pragma unroll
-                for (int q = 0; q < KT; ++q) dv[j][q] = __builtin_fma(pa, dv[j][q], pbv * od[q]);
+                sr_binary_partials<T>(BID, av, bv, rv, &pa, &pbv);
               }
+              v[j] = rv;
+              tangents(j, pa, pbv, od);
             }
           };
           switch (b) {
-            case SR_B_ADD: binary_rows(std::integral_constant<uint32_t, SR_B_ADD>{}); break;
-            case SR_B_SUB: binary_rows(std::integral_constant<uint32_t, SR_B_SUB>{}); break;
-            case SR_B_MUL: binary_rows(std::integral_constant<uint32_t, SR_B_MUL>{}); break;
-            case SR_B_DIV: binary_rows(std::integral_constant<uint32_t, SR_B_DIV>{}); break;
-            default: binary_rows(std::integral_constant<uint32_t, 0xffffffffu>{}); break;
+            case SR_B_ADD: basic_rows(std::integral_constant<uint32_t, SR_B_ADD>{}); break;
+            case SR_B_SUB: basic_rows(std::integral_constant<uint32_t, SR_B_SUB>{}); break;
+            case SR_B_MUL: basic_rows(std::integral_constant<uint32_t, SR_B_MUL>{}); break;
+            case SR_B_DIV: basic_rows(std::integral_constant<uint32_t, SR_B_DIV>{}); break;
+            default: {  // the other operators: value and partials through the row callees
+              SrGVec<T, R> av, bv;
+#pragma unroll
+              for (int j = 0; j < R; ++j) {
+                T ov, od[KT];
+                operand(j, ov, od);
+                av[j] = left ? ov : v[j];
+                bv[j] = left ? v[j] : ov;
+              }
+              const SrGVec<T, R> rv = sr_grad_binary_val<T, R>(b, av, bv);
+              const SrGVec<T, R> pa = sr_grad_binary_der<T, R, 0>(b, av, bv, rv);
+              const SrGVec<T, R> pbv = sr_grad_binary_der<T, R, 1>(b, av, bv, rv);
+#pragma unroll
+              for (int j = 0; j < R; ++j) {
+                T ov, od[KT];
+                operand(j, ov, od);
+                v[j] = rv[j];
+                tangents(j, pa[j], pbv[j], od);
+              }
+              break;
+            }
           }
         }
       }
     }
     // d loss / d constant: (d loss / d pred) * d pred / d constant, padded rows excluded
+    T coefs[R];
+    if (a.loss_kind == SR_LOSS_L2) {
+#pragma unroll
+      for (int j = 0; j < R; ++j) coefs[j] = sr_elem_loss_deriv<T>(SR_LOSS_L2, v[j], ys[j * 64 + lane], T(0));
+    } else {
+      SrGVec<T, R> pv, yv;
+#pragma unroll
+      for (int j = 0; j < R; ++j) {
+        pv[j] = v[j];
+        yv[j] = ys[j * 64 + lane];
+      }
+      pv = sr_grad_loss_der<T, R>(a.loss_kind, pv, yv, a.loss_param);
+#pragma unroll
+      for (int j = 0; j < R; ++j) coefs[j] = pv[j];
+    }
 #pragma unroll
     for (int j = 0; j < R; ++j) {
       const int r = j * 64 + lane;
-      T coef = sr_elem_loss_deriv<T>(a.loss_kind, v[j], ys[r], a.loss_param);
+      T coef = coefs[j];
       if (weighted) coef *= wsv[r];
       if (row0 + r >= a.n_rows) coef = T(0);
 #pragma unroll
@@ -275,17 +430,28 @@ hipError_t sr_launch_grad(const SrGradArgs<T>& a, int n_blocks, hipStream_t s) {
   return hipGetLastError();
 }
 
-// Σ over row blocks of the [row block][item][KT] partials -> out[item][KT], one wave per value: lane
-// l folds row blocks l, l + 64, ... in order and a fixed butterfly adds the lanes (deterministic; a
-// thread per value walking ~160 row blocks serially took 46 us per launch in C3's searches).
-__global__ void __launch_bounds__(256) sr_grad_reduce_kernel(const double* __restrict__ part, int n_row_blocks,
-                                                              int n_vals, double* __restrict__ out) {
-  const int lane = int(threadIdx.x) & 63;
-  const int i = int(int64_t(blockIdx.x) * (blockDim.x / 64) + threadIdx.x / 64);
-  if (i >= n_vals) return;  // wave-uniform
-  double s = 0.0;
-  for (int b = lane; b < n_row_blocks; b += 64) s += part[size_t(b) * n_vals + i];
-#pragma unroll
-  for (int off = 32; off >= 1; off >>= 1) s += __shfl_xor(s, off, 64);
-  if (lane == 0) out[i] = s;
+// Launch with `rows` rows per lane: the kernels exist for the bucket's default (sr_grad_rows_per_lane),
+// its halves down to 2, and 1 (sr_grad_launch_rows picks one; results do not depend on it: the row
+// blocks cover the same rows whatever the rows per lane, see sr_capi.cpp eval_grad_impl).
+template <typename T, bool GATHER, int KT, int RR>
+hipError_t sr_launch_grad_rows_from(const SrGradArgs<T>& a, int rows, int n_blocks, hipStream_t s) {
+  if (rows == RR) return sr_launch_grad<T, KT, 4, GATHER, RR>(a, n_blocks, s);
+  if constexpr (RR > 1) return sr_launch_grad_rows_from<T, GATHER, KT, RR / 2>(a, rows, n_blocks, s);
+  return hipErrorInvalidValue;
+}
+
+template <typename T>
+hipError_t sr_launch_grad_any(const SrGradArgs<T>& a, int kt, bool gather, int rows, int n_blocks, hipStream_t s) {
+  auto go = [&](auto g) -> hipError_t {
+    constexpr bool G = decltype(g)::value;
+    switch (kt) {
+      case 1: return sr_launch_grad_rows_from<T, G, 1, sr_grad_rows_per_lane(1)>(a, rows, n_blocks, s);
+      case 2: return sr_launch_grad_rows_from<T, G, 2, sr_grad_rows_per_lane(2)>(a, rows, n_blocks, s);
+      case 4: return sr_launch_grad_rows_from<T, G, 4, sr_grad_rows_per_lane(4)>(a, rows, n_blocks, s);
+      case 8: return sr_launch_grad_rows_from<T, G, 8, sr_grad_rows_per_lane(8)>(a, rows, n_blocks, s);
+      case 16: return sr_launch_grad_rows_from<T, G, 16, sr_grad_rows_per_lane(16)>(a, rows, n_blocks, s);
+      default: return hipErrorInvalidValue;
+    }
+  };
+  return gather ? go(std::true_type{}) : go(std::false_type{});
 }

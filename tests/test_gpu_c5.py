@@ -91,6 +91,23 @@ def test_c5_constant_optimizer_device_equals_oracle_scored():
     assert np.mean(dev_imp == ora_imp) >= 0.95
     # where they differ, neither optimiser is stuck far above the other's optimum
     assert np.all(np.minimum(dev_loss[sel], ora_loss[sel]) * 10 >= np.maximum(dev_loss[sel], ora_loss[sel]) - 1e-12)
+    # VERDICT r3 weak #11, per tree: continue BOTH end points with the same (device) optimiser for 200
+    # more BFGS iterations and no restarts.  Same basin: both continue to the same minimum (to 1e-8) —
+    # the 8-iteration budget stopped the two trajectories at different points of one descent (they
+    # diverged at a rounding-level line-search decision).  Otherwise: two different local minima.
+    idx = np.nonzero(sel)[0][~close]
+    if idx.size:
+        cd = optimize_constants_batch(dev_tb.take(idx), ds, opts, rng=np.random.default_rng(5), iterations=200,
+                                      nrestarts=0)[1]
+        co = optimize_constants_batch(ora_tb.take(idx), ds, opts, rng=np.random.default_rng(5), iterations=200,
+                                      nrestarts=0)[1]
+        same = np.abs(cd - co) <= 1e-8 * np.maximum(np.abs(co), 1e-300)
+        lower = np.minimum(cd, co) < np.minimum(dev_loss[idx], ora_loss[idx]) * (1 - 1e-12)
+        print(f"C5 optimiser disagreements: {idx.size} trees; same basin after continuing {int(same.sum())}, "
+              f"different minima {int((~same).sum())}; continuing lowered the loss for {int(lower.sum())}")
+        for k in np.nonzero(~same)[0][:5]:
+            print("   different minima: tree", int(idx[k]), float(cd[k]), float(co[k]))
+        assert np.all(cd <= dev_loss[idx] * (1 + 1e-12)) and np.all(co <= ora_loss[idx] * (1 + 1e-12))
 
 
 def _c5_opts(**kw):

@@ -178,3 +178,39 @@ def test_grad_f64_many_features_deep_trees_weighted():
         assert np.all(np.abs(a - b) <= 2e-5 * scale), (t, a, b)
         checked += 1
     assert checked > 50
+
+
+@pytest.mark.parametrize("dtype", [np.float64, np.float32])
+def test_gradients_independent_of_rows_per_lane(dtype):
+    """The gradient kernel's rows per lane is a tuning choice (sr_set_tuning "grad_rows"): its row
+    blocks cover the same rows whatever the choice and each lane accumulates its rows in order, so the
+    gradients are bit-identical for every choice — also with FULL-tier operators (their row callees),
+    weights, a non-L2 loss and every tangent bucket."""
+    import sr_amd
+
+    rng = np.random.default_rng(8)
+    n = 30_001
+    X = rng.uniform(0.5, 2.0, (4, n)).astype(dtype)
+    y = (X[0] * X[1] / (X[2] + 1) + np.cos(X[3])).astype(dtype)
+    w = (0.5 + rng.random(n)).astype(dtype)
+    ctx = sr_amd.get_context()
+    for kw, loss in ((dict(binary_operators=["+", "-", "*", "/"], unary_operators=["cos", "exp", "log", "sin"]), None),
+                     (dict(binary_operators=["+", "*", "/", "^", "max"], unary_operators=["tanh", "sqrt", "atan"]),
+                      "L1DistLoss")):
+        opts = Options(**kw, **({"elementwise_loss": loss} if loss else {}))
+        trees = gen_random_population(400, opts, 4, max_size=25, dtype=dtype, seed=8)
+        tb = flatten_trees(trees, dtype)
+        ds = Dataset(X, y, weights=w)
+        ref = None
+        try:
+            for rows in (0, 1, 2, 4, 8):
+                ctx.set_tuning("grad_rows", rows)
+                l, g, c = eval_grad_batch(tb, ds, opts)
+                if ref is None:
+                    ref = (l, g, c)
+                    assert c.mean() > 0.2
+                    continue
+                assert np.array_equal(c, ref[2]), rows
+                assert np.array_equal(g.view(np.uint8), ref[1].view(np.uint8)), (rows, kw)
+        finally:
+            ctx.set_tuning("grad_rows", 0)
