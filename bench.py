@@ -281,7 +281,7 @@ def main():
     busy = float(np.mean(state["busy"][-args.steps:]))
     n_launch = int(round(float(np.mean(state["launches"][-args.steps:]))))
     flops_per_step = float(rows) * (ops + 3 * nt)  # this GPU's interpreter work per step
-    traffic = measured_traffic("c2")
+    traffic = measured_traffic("c2", nt, rows)
     rpl = ctx.last_rows_per_lane()
     n_derived = ctx.last_derived_columns()
 
@@ -454,7 +454,7 @@ def c4_line(ctx, opts, eval_loss_sharded, gen_random_batch, Dataset, args, comm,
     n_local = rows_total // world
     kmean, busy = float(np.mean(kms)), float(np.mean(st["busy"][-args.c4_steps:]))
     flops = float(n_local) * (tb.n_operator_nodes + 3 * tb.n_trees)
-    traffic = measured_traffic("c4")
+    traffic = measured_traffic("c4", tb.n_trees, n_local)
     nl = int(round(float(np.mean(st["launches"][-args.c4_steps:]))))
     algo = algorithmic_bytes(tb.n_trees, n_local, nl, ctx.last_rows_per_lane())
     n_derived = ctx.last_derived_columns()
@@ -766,9 +766,10 @@ def grad_roofline(res, X, y, opts, reps=5):
             "what": "sr_eval_grad_batch on the C5 search's final members with constants, full 100k rows, f64"}
 
 
-def measured_traffic(workload):
+def measured_traffic(workload, n_trees, rows_per_gpu):
     """Per-step HBM bytes of the interpreter from the committed rocprofv3 PMC pass of this same
-    command (profiles/traffic.json / traffic_c4.json, written by tools/trace_frac.py)."""
+    command (profiles/traffic.json / traffic_c4.json, written by tools/trace_frac.py) — only when it
+    was measured on this configuration (files without the configuration: the default one)."""
     p = os.path.join(ROOT, "profiles", "traffic.json" if workload == "c2" else f"traffic_{workload}.json")
     try:
         with open(p) as f:
@@ -776,6 +777,9 @@ def measured_traffic(workload):
     except (OSError, ValueError):
         return None
     if t.get("workload") != workload or "hbm_read_bytes_per_step" not in t:
+        return None
+    default = (10_000, 1 << 20) if workload == "c2" else (100_000, 1 << 26)
+    if (t.get("n_trees", default[0]), t.get("rows_per_gpu", default[1])) != (n_trees, rows_per_gpu):
         return None
     t["source"] = (f"profiles/{os.path.basename(p)} (rocprofv3 --pmc FETCH_SIZE of the bench command, "
                    "x1024 B x2 gfx950, the timed steps' interpreter launches)")

@@ -349,6 +349,18 @@ __device__ __forceinline__ void sr_exp_rows_f32(float (&v)[R]) {
 // rounded quotient.  The range test is one max3 and one min3 per row and one ballot (a NaN operand
 // is ignored by both and yields NaN through the core, as it must); a wave with any row outside it
 // (zeros, infinities, huge or tiny values) takes the full division in every row.
+// The full division over the rows as a real call (SR_DIV_FULL_CALL builds): the rarely taken branch
+// of every division case then costs one call site instead of R inlined divisions (the 14 division
+// cases of the register-stack kernel carried ~18 KB of such cold code).
+template <int R>
+__device__ __attribute__((noinline)) SrRowVec<R> sr_div_rows_full(SrRowVec<R> a, SrRowVec<R> b) {
+#pragma unroll
+  for (int r = 0; r < R; ++r) {
+    a[r] = a[r] / b[r];
+    __builtin_amdgcn_sched_barrier(0);
+  }
+  return a;
+}
 template <int R>
 __device__ __forceinline__ void sr_div_rows_f32(float (&out)[R], const float (&a)[R], const float (&b)[R]) {
   static_assert(R % 2 == 0, "pairs of rows");
@@ -373,8 +385,20 @@ __device__ __forceinline__ void sr_div_rows_f32(float (&out)[R], const float (&a
       out[r + 1] = Q[1];
     }
   } else {
+#ifdef SR_DIV_FULL_CALL
+    SrRowVec<R> va, vb;
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+      va[r] = a[r];
+      vb[r] = b[r];
+    }
+    va = sr_div_rows_full<R>(va, vb);
+#pragma unroll
+    for (int r = 0; r < R; ++r) out[r] = va[r];
+#else
 #pragma unroll
     for (int r = 0; r < R; ++r) out[r] = a[r] / b[r];
+#endif
   }
 }
 

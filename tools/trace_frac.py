@@ -57,6 +57,8 @@ def main(out, workload="c2"):
                   f"(algorithmic {rf['algorithmic_bytes_per_step'] / 1e6:.1f} MB)")
             json.dump({"workload": workload, "kernel": f"sr_tile_kernel<float, {rpl}, 0, ...> + the probe launches",
                        "profiled_steps": steps, "launches": len(vals),
+                       "n_trees": line.get("config", line).get("n_trees", line.get("n_trees")),
+                       "rows_per_gpu": line.get("config", line).get("rows_per_gpu", line.get("rows_per_gpu")),
                        "hbm_read_bytes_per_step": per_step_bytes,
                        "source_cmd": "tools/bench_evidence.sh"},
                       open(os.path.join(out, "traffic.json" if workload == "c2" else f"traffic_{workload}.json"), "w"))
