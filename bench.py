@@ -729,11 +729,17 @@ def grad_roofline(res, X, y, opts, reps=5):
     126-167) on the C5 search's final members with constants, over the full data: per tangent bucket the
     tangent kernel's HIP-event time and its algorithmic flops (csrc sr_last_grad_info: per row and work
     item, each unary node 2 + KT, binary node 3 + 2 KT, loss epilogue 3 + KT), against the FP64 peak."""
-    import sr_amd
-    from sr_amd import Dataset, eval_grad_batch, flatten_trees
+    from sr_amd import flatten_trees
 
     trees = [m.tree for p in res.populations for m in p if m.tree.count_constants() > 0]
-    tb = flatten_trees(trees, np.float64)
+    return grad_roofline_batch(flatten_trees(trees, np.float64), X, y, opts, reps)
+
+
+def grad_roofline_batch(tb, X, y, opts, reps=5):
+    """grad_roofline's measurement on a flattened batch (tools/c5_grad_profile.py profiles it alone)."""
+    import sr_amd
+    from sr_amd import Dataset, eval_grad_batch
+
     ds = Dataset(X, y)
     ctx = sr_amd.get_context()
     for _ in range(2):
