@@ -401,7 +401,7 @@ int sr_vstk_rows(int elem_size, int64_t n_rows, int requested) {
   // tree groups it is faster (C2 in f64 13.45 -> 12.69 ms per step, arithmetic-only -19 %,
   // profiles/r03_ab_f64_vstk.txt), so it is the default for large views too
   if (elem_size == 8) {
-    if (requested == 8) return 8;
+    if (requested == 8 || requested == -4) return requested == 8 ? 8 : 4;  // (-4: the 4-row register-stack build)
     if (requested == 4 || requested == 2) return 0;
     return n_rows >= (int64_t(1) << 17) ? 8 : 0;
   }
@@ -441,8 +441,10 @@ hipError_t sr_launch_eval(const SrEvalArgs<T>& a, int mode, bool gather, int tie
   } else {
     (void)waves;
     if (vstk) {
-      if (mode != SR_MODE_LOSS || tier != SR_TIER_BASIC || gather || R != 8) return hipErrorInvalidValue;
-      return sr_launch_basic_loss<T, 8, false, true>(a, n_blocks, s);
+      if (mode != SR_MODE_LOSS || tier != SR_TIER_BASIC || gather) return hipErrorInvalidValue;
+      if (R == 8) return sr_launch_basic_loss<T, 8, false, true>(a, n_blocks, s);
+      if (R == 4) return sr_launch_basic_loss<T, 4, false, true>(a, n_blocks, s);
+      return hipErrorInvalidValue;
     }
     if (mode == SR_MODE_LOSS) {
       if (tier == SR_TIER_BASIC)

@@ -191,6 +191,7 @@ struct sr_ctx {
   // SR_AMD_FUSED_REDUCE: multi-row-block LOSS launches reduce their partials in the launch (the last
   // workgroup of a tree group) when the group holds at most this many partials (0: a reduce launch)
   int64_t fused_reduce = int64_t(1) << 30;
+  int vstk_rows = 0;        // SR_AMD_VSTK_ROWS / "vstk_rows": rows per lane of the register-stack kernel (0: default)
   int grad_rows_force = 0;  // SR_AMD_GRAD_ROWS / "grad_rows": the gradient kernel's rows per lane (0: chosen per call)
   DevBuf group_cnt;      // its per-group counters (zeroed at allocation; each launch leaves them zero)
   int first_chunk = 6;   // SR_AMD_FIRST_CHUNK: the two-chunk pipeline's first chunk is 1/first_chunk
@@ -456,7 +457,7 @@ int run_batch(sr_ctx* ctx, const sr_dataset* ds, int opset_id, const sr_tree_bat
   // chunk whose programs need <= 2 operand-stack slots (all trees of <= 30 nodes); other chunks run
   // the LDS-stack kernel at R rows per lane
   int Rv = (mode == SR_MODE_LOSS && tier == SR_TIER_BASIC && !gather)
-               ? sr_vstk_rows(int(sizeof(T)), n_eval, ctx->rows_override)
+               ? sr_vstk_rows(int(sizeof(T)), n_eval, ctx->vstk_rows ? ctx->vstk_rows : ctx->rows_override)
                : 0;
   // a wide dataset whose register-stack tile (its rows per lane are twice the classic kernel's) would
   // not fit the LDS runs the classic kernel instead (Float64 with ~40-75 features)
@@ -2430,6 +2431,7 @@ int sr_init(int device, sr_ctx** out) {
   if (const char* v = std::getenv("SR_AMD_CODE_CACHE")) ctx->code_cache = std::atoi(v);
   if (const char* v = std::getenv("SR_AMD_FUSED_REDUCE")) ctx->fused_reduce = std::atoll(v);
   if (const char* v = std::getenv("SR_AMD_GRAD_ROWS")) ctx->grad_rows_force = std::atoi(v);
+  if (const char* v = std::getenv("SR_AMD_VSTK_ROWS")) ctx->vstk_rows = std::atoi(v);
   if (const char* v = std::getenv("SR_AMD_FIRST_CHUNK")) ctx->first_chunk = std::max(2, std::atoi(v));
   if (const char* v = std::getenv("SR_AMD_HOST_IO")) ctx->host_io = std::atoi(v);
   if (const char* v = std::getenv("SR_AMD_SPIN")) ctx->spin = std::atoi(v);
@@ -3101,6 +3103,15 @@ int sr_set_tuning(sr_ctx* ctx, const char* name, int64_t value) {
   }
   if (std::strcmp(name, "probe") == 0) {  // dead-tree probe mode (SR_AMD_PROBE)
     ctx->probe = int(value);
+    return SR_OK;
+  }
+  if (std::strcmp(name, "host_io") == 0) {  // small-call host I/O (SR_AMD_HOST_IO: 0, 1, 2)
+    if (value < 0 || value > 2) return set_error(SR_ERR_INVALID_ARG, "host_io must be 0, 1 or 2");
+    ctx->host_io = int(value);
+    return SR_OK;
+  }
+  if (std::strcmp(name, "vstk_rows") == 0) {  // register-stack rows per lane (SR_AMD_VSTK_ROWS; 0: default)
+    ctx->vstk_rows = int(value);
     return SR_OK;
   }
   if (std::strcmp(name, "grad_rows") == 0) {  // gradient kernel rows per lane (SR_AMD_GRAD_ROWS; 0: automatic)

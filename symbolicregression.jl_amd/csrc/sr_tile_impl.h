@@ -58,6 +58,9 @@ struct SrMinWaves {
 #ifndef SR_MIN_WAVES_VSTK_F64
 #define SR_MIN_WAVES_VSTK_F64 2
 #endif
+#ifndef SR_MIN_WAVES_VSTK4_F64
+#define SR_MIN_WAVES_VSTK4_F64 4  // f64 register stack at 4 rows per lane: <= 128 VGPRs
+#endif
 #ifndef SR_MIN_WAVES_VSTK32
 #define SR_MIN_WAVES_VSTK32 3
 #endif
@@ -65,7 +68,8 @@ template <typename T, int R, int TIER, int W, bool VSTK = false>
 struct SrMinWavesFor {
   static constexpr bool f32_basic = sizeof(T) == 4 && TIER == SR_TIER_BASIC && W == 4;
   static constexpr bool f64_basic = sizeof(T) == 8 && TIER == SR_TIER_BASIC && W == 4;
-  static constexpr int value = (f64_basic && VSTK)               ? SR_MIN_WAVES_VSTK_F64
+  static constexpr int value = (f64_basic && VSTK && R == 4)     ? SR_MIN_WAVES_VSTK4_F64
+                               : (f64_basic && VSTK)               ? SR_MIN_WAVES_VSTK_F64
                                : (f32_basic && VSTK && R == 8)    ? SR_MIN_WAVES_VSTK8
                                : (f32_basic && VSTK && R == 16)   ? SR_MIN_WAVES_VSTK16
                                : (f32_basic && VSTK && R == 32) ? SR_MIN_WAVES_VSTK32

@@ -158,7 +158,7 @@ def test_derived_columns_change_nothing(dtype, batching):
 
 @pytest.mark.parametrize("dtype", [np.float32, np.float64])
 def test_probe_modes_change_nothing(dtype):
-    """The LDS program cache on or off, and the dead-tree probe, which only sets hints: with no probe, the first-rows probe, the stress-row probe
+    """The LDS program cache off, on, or on for the classic launches too, and the dead-tree probe, which only sets hints: with no probe, the first-rows probe, the stress-row probe
     (extreme and nearest-zero rows of each feature, through the gather build and derived columns
     computed over those rows) and a probe before every chunk, losses and flags are identical bit for
     bit.  The data holds rare overflow rows past the first tiles, so the stress rows find trees the
@@ -178,7 +178,7 @@ def test_probe_modes_change_nothing(dtype):
     ctx = sr_amd.get_context()
     res = []
     try:
-        for probe, stress, cache in ((0, 0, 1), (2, 0, 1), (2, 1, 1), (1, 1, 1), (2, 1, 0)):
+        for probe, stress, cache in ((0, 0, 1), (2, 0, 1), (2, 1, 1), (1, 1, 1), (2, 1, 0), (2, 1, 2)):
             ctx.set_tuning("probe", probe)
             ctx.set_tuning("stress_probe", stress)
             ctx.set_tuning("code_cache", cache)
@@ -193,3 +193,36 @@ def test_probe_modes_change_nothing(dtype):
     for l1, c1 in res[1:]:
         assert np.array_equal(c1, c0)
         assert np.array_equal(np.asarray(l1)[c1].view(u), np.asarray(l0)[c0].view(u))
+
+
+@pytest.mark.parametrize("dtype,n_rows,n_trees", [(np.float32, 100_000, 31), (np.float64, 100, 40), (np.float32, 3000, 300)])
+def test_small_call_latency_options_change_nothing(dtype, n_rows, n_trees):
+    """The search's call shapes under the latency options: programs read by the kernel from pinned
+    host memory ("host_io" 2), the LDS program cache in the classic kernel ("code_cache" 2), and the
+    partial reduction in a separate launch ("fused_reduce" 0): losses and flags bit for bit equal."""
+    import sr_amd
+    from sr_amd import Dataset, eval_loss_batch, flatten_trees, gen_random_population
+
+    rng = np.random.default_rng(31)
+    X = rng.uniform(0.5, 2.0, (5, n_rows)).astype(dtype)
+    y = (X[0] * X[1] * X[2] / (X[3] * X[4] ** 2 + 1)).astype(dtype)
+    ds = Dataset(X, y)
+    opts = Options(binary_operators=["+", "-", "*", "/"], unary_operators=["cos", "exp"])
+    tb = flatten_trees(gen_random_population(n_trees, opts, 5, max_size=20, seed=31), dtype)
+    ctx = sr_amd.get_context()
+    res = []
+    try:
+        for host_io, cache, fused in ((1, 1, 1 << 30), (2, 1, 1 << 30), (2, 2, 1 << 30), (1, 2, 0), (0, 1, 0)):
+            ctx.set_tuning("host_io", host_io)
+            ctx.set_tuning("code_cache", cache)
+            ctx.set_tuning("fused_reduce", fused)
+            res.append(eval_loss_batch(tb, ds, opts))
+    finally:
+        ctx.set_tuning("host_io", 1)
+        ctx.set_tuning("code_cache", 1)
+        ctx.set_tuning("fused_reduce", 1 << 30)
+    l0, c0 = res[0]
+    assert c0.mean() > 0.2
+    for l1, c1 in res[1:]:
+        assert np.array_equal(c1, c0)
+        assert np.array_equal(np.asarray(l1).view(np.uint8), np.asarray(l0).view(np.uint8))
