@@ -42,3 +42,11 @@ if __name__ == "__main__":
         opts = Options(binary_operators=["+", "-", "*", "/"], unary_operators=["cos", "exp"])
         run("C3 Feynman-style 5 features x 100k rows f32 (31 populations, default options)", X, y, opts,
             int(os.environ.get("C3_ITERS", "5")))
+    if "C5" in which:  # bench.py's C5: the C3-style data in f64, constant optimisation on, 32 populations
+        rng = np.random.default_rng(11)
+        X = rng.uniform(0.5, 2.0, (5, 100_000)).astype(np.float32)
+        y = (X[0] * X[1] * X[2] / (X[3] * X[4] ** 2 + 1)).astype(np.float32)
+        opts = Options(binary_operators=["+", "-", "*", "/"], unary_operators=["cos", "exp", "log"], populations=32,
+                       should_optimize_constants=True)
+        run("C5 f64 5 features x 100k rows, constant optimisation (32 populations)", X.astype(np.float64),
+            y.astype(np.float64), opts, int(os.environ.get("C5_ITERS", "10")))
