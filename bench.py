@@ -152,6 +152,11 @@ class Comm:
         self.d.destroy_process_group()
 
 
+def progress(msg):
+    """A progress line on stderr (long runs: the bench's phases each print one as they start)."""
+    print(f"[bench {time.strftime('%H:%M:%S')}] {msg}", file=sys.stderr, flush=True)
+
+
 def timed(step, steps, warmup, barrier):
     """W untimed steps, then K timed steps between barriers (every library call returns after its
     streams have drained: the device is synchronised on both sides)."""
@@ -262,6 +267,8 @@ def main():
     nodes, ops = int(tb.n_nodes), int(tb.n_operator_nodes)
 
     # ---- headline: C2, weak scaling
+    if rank == 0:
+        progress(f"C2 headline: {nt} trees x {rows} rows, {args.warmup} + {args.steps} steps")
     state = {}
     if world == 1:
         call, out = single_gpu_call(ctx, tb, ds, opts)
@@ -287,18 +294,26 @@ def main():
 
     subs = {}
     if world == 1 and not args.no_sharded_path:
+        if rank == 0:
+            progress("c2_sharded_path")
         subs["c2_sharded_path"] = sharded_path_line(ctx, tb, ds, opts, eval_loss_sharded, args, comm, nodes, rows)
     if not args.no_tree_sharded:
+        if rank == 0:
+            progress("tree_sharded")
         subs["tree_sharded"] = tree_sharded_line(ctx, tb, opts, eval_loss_tree_sharded, args, comm, world, rank,
                                                  nodes, rows, loss if world == 1 else None, comp if world == 1 else None)
     if not args.no_c4:
+        if rank == 0:
+            progress("c4")
         subs["c4"] = c4_line(ctx, opts, eval_loss_sharded, gen_random_batch, Dataset, args, comm, world, rank)
 
     extra = {}
     if rank == 0 and world == 1 and not args.no_extra:
+        progress("complete-only and Float64 lines")
         extra = extra_lines(ctx, opts, trees, comp, X, y, args)
     cpu, parity = None, None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        progress("CPU baseline and parity")
         cpu, parity = cpu_baseline_and_parity(opts, tb, X, y, args.cpu_trees, loss, comp)
     search = None
     if rank == 0 and world == 1 and args.search_iters > 0:
@@ -449,6 +464,8 @@ def c4_line(ctx, opts, eval_loss_sharded, gen_random_batch, Dataset, args, comm,
 
     def call():
         res["l"], res["c"] = eval_loss_sharded(tb, ds, opts)
+    if rank == 0:
+        progress(f"c4 steps: {tb.n_trees} trees x {rows_total} rows / {world}")
     dt, step_ms, kms = timed(lib_step(ctx, call, st), args.c4_steps, 1, comm.barrier)
     dt = comm.max(dt)
     n_local = rows_total // world
@@ -476,6 +493,7 @@ def c4_line(ctx, opts, eval_loss_sharded, gen_random_batch, Dataset, args, comm,
                                 hbm_GBps=(traffic["hbm_read_bytes_per_step"] / (kmean * 1e-3) / 1e9
                                           if traffic else None), hbm_peak_GBps=PEAK_HBM_GBPS)}
     if world == 1 and rank == 0 and not args.no_c4_parity:
+        progress("c4 parity (oracle over all rows for a tree sample)")
         out["parity"] = c4_parity(opts, tb, res, lambda t: eval_loss_sharded(t, ds, opts), rows_total,
                                   args.c4_parity_trees)
     ds.free_device()
@@ -690,6 +708,7 @@ def search_lines(args):
             ("c5", X5, y5, o5, args.search_cpu_iters or 1, threads,
              "C5: the C3 data in f64, constant optimisation (BFGS / Newton, device forward-mode gradients), "
              "32 populations, default options")):
+        progress(f"search {name}")
         t0 = time.perf_counter()
         res = equation_search(X, y, niterations=args.search_iters, options=o, seed=0)
         wall = time.perf_counter() - t0
