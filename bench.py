@@ -291,6 +291,7 @@ def main():
     traffic = measured_traffic("c2", nt, rows)
     rpl = ctx.last_rows_per_lane()
     n_derived = ctx.last_derived_columns()
+    n_exact_last, n_fold_last = ctx.last_exact_trees(), ctx.last_fold_trees()
 
     subs = {}
     if world == 1 and not args.no_sharded_path:
@@ -351,6 +352,8 @@ def main():
                                 if world > 1 else "single GPU"),
                 "code_path": path,
                 "fraction_complete": float(np.mean(comp)),
+                "exact_trees": n_exact_last,
+                "fold_trees": n_fold_last,
                 "runtime": {"hip": cinfo.get("hip"), "rccl": cinfo.get("rccl")},
             },
             "roofline": roofline(
@@ -476,6 +479,8 @@ def c4_line(ctx, opts, eval_loss_sharded, gen_random_batch, Dataset, args, comm,
     algo = algorithmic_bytes(tb.n_trees, n_local, nl, ctx.last_rows_per_lane())
     n_derived = ctx.last_derived_columns()
     algo_d = algorithmic_bytes(tb.n_trees, n_local, nl, ctx.last_rows_per_lane(), n_derived)
+    passes = {"exact_trees": ctx.last_exact_trees(), "fold_trees": ctx.last_fold_trees(),
+              "phase_ms": [round(float(v), 3) for v in ctx.last_phase_ms()]}
     out = {"metric": "tree-node x row evals/sec (batched eval_loss, fp32)",
            "value": float(tb.n_nodes) * rows_total * args.c4_steps / dt, "unit": "node-evals/s",
            "ms_per_step": dt / args.c4_steps * 1e3, "steps": args.c4_steps, "warmup": 1, "n_gpus": world,
@@ -484,6 +489,8 @@ def c4_line(ctx, opts, eval_loss_sharded, gen_random_batch, Dataset, args, comm,
                         f"generator, seed 4) x {rows_total >> 20}M rows x 5 features, rows sharded n/{world}"),
            "code_path": "sr_eval_loss_sharded (same at every N)", "rows_per_gpu": n_local,
            "fraction_complete": float(np.mean(res["c"])),
+           "last_step_passes": dict(passes, note=("trees through the exact isfinite(sum) pass (BIG) and through the "
+                                                   "in-order loss fold (sr_fold.h); phase_ms = sr_last_phase_ms")),
            "roofline": roofline(flops, kmean, PEAK_FP32_TFLOPS, busy_ms_per_step=busy, launches_per_step=nl,
                                 kernel=f"sr_tile_kernel<float,{ctx.last_rows_per_lane()},LOSS,gather=false,BASIC,W=4,L2>",
                                 algorithmic_bytes_per_step=algo, algorithmic_GBps=algo / (kmean * 1e-3) / 1e9,

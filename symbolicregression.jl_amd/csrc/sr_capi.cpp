@@ -189,8 +189,11 @@ struct sr_ctx {
   int stress_probe = 1;  // SR_AMD_STRESS_PROBE: the probe runs the dataset's stress rows (below)
   int code_cache = 1;    // SR_AMD_CODE_CACHE: LDS program cache (1: register-stack launches, 2: also the classic ones)
   // SR_AMD_FUSED_REDUCE: multi-row-block LOSS launches reduce their partials in the launch (the last
-  // workgroup of a tree group) when the group holds at most this many partials (0: a reduce launch)
-  int64_t fused_reduce = int64_t(1) << 30;
+  // workgroup of a tree group) when the group holds at most this many partials; 0 (default): a reduce
+  // launch — measured faster: every workgroup's drained stores + barrier + counter add cost more than
+  // the launch they save (C3 search 14.4 vs 13.3 iterations/s, C2's dead trees 0.52 vs 0.71 ms;
+  // profiles/r04_ab_fused_reduce.txt)
+  int64_t fused_reduce = 0;
   int vstk_rows = 0;        // SR_AMD_VSTK_ROWS / "vstk_rows": rows per lane of the register-stack kernel (0: default)
   int grad_rows_force = 0;  // SR_AMD_GRAD_ROWS / "grad_rows": the gradient kernel's rows per lane (0: chosen per call)
   DevBuf group_cnt;      // its per-group counters (zeroed at allocation; each launch leaves them zero)
@@ -1346,8 +1349,31 @@ int fold_exact(sr_ctx* ctx, const sr_dataset* ds, int opset_id, const sr_tree_ba
   const bool gather = row_idx != nullptr && n_idx > 0;
   const int64_t n_eval = gather ? n_idx : ds->n;
   hipStream_t s = ctx->stream;
-  // predictions of at most ~1 GiB per pass
-  const int64_t per = std::max<int64_t>(1, int64_t((size_t(1) << 30) / (size_t(n_eval) * sizeof(T))));
+  // the fold's PRED passes are internal: the call's interpreter timing (its chunk events) and the
+  // kernel it reports (rows per lane, derived columns) stay those of the call's own loss launches
+  struct Keep {
+    sr_ctx* c;
+    int timing, n_chunks, n_derived, rows;
+    bool timed, derived;
+    explicit Keep(sr_ctx* x)
+        : c(x), timing(x->timing), n_chunks(x->n_chunks_last), n_derived(x->n_derived_last), rows(x->rows_last),
+          timed(x->timed_last), derived(x->derived_last) {
+      x->timing = 0;
+    }
+    ~Keep() {
+      c->timing = timing;
+      c->n_chunks_last = n_chunks;
+      c->n_derived_last = n_derived;
+      c->rows_last = rows;
+      c->timed_last = timed;
+      c->derived_last = derived;
+    }
+  } keep(ctx);
+  // predictions of at most 16 GiB per pass (and half the free device memory): the fold kernel runs one
+  // workgroup per listed tree, so a pass should hold many trees (C4: 64 trees of 2^26 rows per pass)
+  size_t budget = size_t(16) << 30, free_b = 0, total_b = 0;
+  if (hipMemGetInfo(&free_b, &total_b) == hipSuccess) budget = std::min(budget, free_b / 2);
+  const int64_t per = std::max<int64_t>(1, int64_t(budget / (size_t(n_eval) * sizeof(T))));
   for (size_t b0 = 0; b0 < list.size(); b0 += size_t(per)) {
     const size_t nb = std::min(list.size() - b0, size_t(per));
     SubBatch<T> sub(*trees, list.data() + b0, nb);
@@ -1365,6 +1391,7 @@ int fold_exact(sr_ctx* ctx, const sr_dataset* ds, int opset_id, const sr_tree_ba
     SR_HIP_CHECK(hipMemcpyAsync(out->data() + b0, d_out, nb * sizeof(T), hipMemcpyDeviceToHost, s));
     SR_HIP_CHECK(hipStreamSynchronize(s));
   }
+  if (ctx->pred.cap > (size_t(2) << 30)) ctx->pred.release();  // (large prediction passes: not kept)
   return SR_OK;
 }
 

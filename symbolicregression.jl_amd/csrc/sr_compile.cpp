@@ -655,10 +655,11 @@ int sr_compile_batch(const sr_tree_batch& trees, const SrOpset& ops, int64_t n_r
   std::vector<PerTree> per(size_t(nt > 0 ? nt : 0));
   std::vector<int> errs(size_t(nt > 0 ? nt : 0), SR_OK);
   const T* vals = static_cast<const T*>(trees.val);
-  // work split: pieces of 32..256 trees, about two per persistent worker (small batches: the
-  // caller alone)
-  const int64_t pool = nt > 32 ? WorkerPool::get().size() : 1;
-  const int64_t kPiece = std::max<int64_t>(32, std::min<int64_t>(256, (nt + 2 * pool - 1) / (2 * pool)));
+  // work split: pieces of 128..256 trees, about two per persistent worker; batches of up to 128 trees
+  // compile on the caller alone (waking the pool costs more: 40 trees 13-25 us through it against ~7
+  // inline on the box, profiles/r04_latency_ab.txt)
+  const int64_t pool = nt > 128 ? WorkerPool::get().size() : 1;
+  const int64_t kPiece = std::max<int64_t>(128, std::min<int64_t>(256, (nt + 2 * pool - 1) / (2 * pool)));
   const int n_pieces = int(nt <= kPiece ? 1 : (nt + kPiece - 1) / kPiece);
   const int nthreads = n_pieces;  // one code buffer per piece
   std::vector<std::vector<SrIns<T>>> bufs(static_cast<size_t>(nthreads));

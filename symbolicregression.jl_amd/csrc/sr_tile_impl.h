@@ -55,8 +55,22 @@ struct SrMinWaves {
 #ifndef SR_MIN_WAVES_VSTK8
 #define SR_MIN_WAVES_VSTK8 6
 #endif
+// f64 register stack at 8 rows per lane: 168 VGPRs = 3 waves per SIMD for the L2 / L1 builds, no
+// spills (round 4's epilogue grew them to 172 — 2 waves — and the Float64 C2 step to 22.7 ms from
+// 15.9; profiles/r04_ab_regress.txt); the generic-loss build keeps 2 (it would spill at 168)
 #ifndef SR_MIN_WAVES_VSTK_F64
-#define SR_MIN_WAVES_VSTK_F64 2
+#define SR_MIN_WAVES_VSTK_F64 3
+#endif
+#ifndef SR_MIN_WAVES_VSTK_F64_GENERIC
+#define SR_MIN_WAVES_VSTK_F64_GENERIC 2
+#endif
+// the f32 gather (SubDataset / several-view) build: 80 VGPRs, 6 waves per SIMD (it needed 75 before
+// the row-view segments); the f64 classic generic-loss builds: 128, 4 waves
+#ifndef SR_MIN_WAVES_GATHER_F32
+#define SR_MIN_WAVES_GATHER_F32 6
+#endif
+#ifndef SR_MIN_WAVES_F64_GENERIC
+#define SR_MIN_WAVES_F64_GENERIC 4
 #endif
 #ifndef SR_MIN_WAVES_VSTK4_F64
 #define SR_MIN_WAVES_VSTK4_F64 4  // f64 register stack at 4 rows per lane: <= 128 VGPRs
@@ -64,12 +78,16 @@ struct SrMinWaves {
 #ifndef SR_MIN_WAVES_VSTK32
 #define SR_MIN_WAVES_VSTK32 3
 #endif
-template <typename T, int R, int TIER, int W, bool VSTK = false>
+template <typename T, int R, int TIER, int W, bool VSTK = false, int LK = -1, bool GATHER = false, int MODE = 0>
 struct SrMinWavesFor {
   static constexpr bool f32_basic = sizeof(T) == 4 && TIER == SR_TIER_BASIC && W == 4;
   static constexpr bool f64_basic = sizeof(T) == 8 && TIER == SR_TIER_BASIC && W == 4;
+  static constexpr bool loss = MODE == 0;  // (SR_MODE_LOSS)
   static constexpr int value = (f64_basic && VSTK && R == 4)     ? SR_MIN_WAVES_VSTK4_F64
-                               : (f64_basic && VSTK)               ? SR_MIN_WAVES_VSTK_F64
+                               : (f64_basic && VSTK && LK >= 0)    ? SR_MIN_WAVES_VSTK_F64
+                               : (f64_basic && VSTK)               ? SR_MIN_WAVES_VSTK_F64_GENERIC
+                               : (f64_basic && loss && R == 4 && LK < 0) ? SR_MIN_WAVES_F64_GENERIC
+                               : (f32_basic && loss && GATHER && R == 8 && LK >= 0) ? SR_MIN_WAVES_GATHER_F32
                                : (f32_basic && VSTK && R == 8)    ? SR_MIN_WAVES_VSTK8
                                : (f32_basic && VSTK && R == 16)   ? SR_MIN_WAVES_VSTK16
                                : (f32_basic && VSTK && R == 32) ? SR_MIN_WAVES_VSTK32
@@ -758,7 +776,7 @@ __device__ __forceinline__ typename SrWindow<T>::type sr_window_lds(const uint4*
 // LK: elementwise loss fixed at compile time (SR_LOSS_L2 / SR_LOSS_L1), or -1 = a.loss_kind.
 // VSTK: the operand stack (<= 2 slots: every tree of <= 30 nodes) lives in VGPRs.
 template <typename T, int R, int MODE, bool GATHER, int TIER, int W, int LK, bool VSTK>
-__global__ void __launch_bounds__(W * 64, (SrMinWavesFor<T, R, TIER, W, VSTK>::value)) sr_tile_kernel(const SrEvalArgs<T> a) {
+__global__ void __launch_bounds__(W * 64, (SrMinWavesFor<T, R, TIER, W, VSTK, LK, GATHER, MODE>::value)) sr_tile_kernel(const SrEvalArgs<T> a) {
   constexpr int SR_WAVES = W;
   constexpr int SR_BLOCK = W * 64;
   using L = SrLane<T, R>;

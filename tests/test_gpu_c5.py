@@ -90,38 +90,46 @@ def test_c5_constant_optimizer_device_equals_oracle_scored():
     assert frac >= 0.90, np.sort(rel)[-10:]  # measured 0.92 (211 trees; median rel 1.8e-15)
     assert np.mean(dev_imp == ora_imp) >= 0.95
     # VERDICT r3 weak #11, per tree: continue BOTH end points with the same (device) optimiser for 200
-    # more BFGS iterations and no restarts.  Same basin: both continue to the same minimum (to 1e-6) —
-    # the 8-iteration budget stopped the two trajectories at different points of one descent (they
-    # diverged at a rounding-level line-search decision).  Otherwise two different local minima: then
-    # both continued end points must be stationary (the device gradient there is small against the
-    # loss's scale), i.e. legitimate optima of the same objective, not an optimiser stuck by a wrong
-    # gradient.
+    # more BFGS iterations and no restarts.  Same minimum (to 1e-6): the 8-iteration budget stopped
+    # the two trajectories at different points of one descent (they diverged at a rounding-level
+    # line-search decision).  Otherwise two different end points of the same objective: there the
+    # device gradient must still be the objective's gradient — checked against the oracle's
+    # Richardson finite differences at every such end point, so a disagreement is never a wrong
+    # gradient sending one optimiser elsewhere.  (Some end points are not stationary: BFGS stops when
+    # its line search finds no decrease, e.g. next to a pole of a division.)
     idx = np.nonzero(sel)[0][~close]
     if idx.size:
+        from sr_amd import eval_grad_batch
+
         bd, cd = optimize_constants_batch(dev_tb.take(idx), ds, opts, rng=np.random.default_rng(5), iterations=200,
                                           nrestarts=0)[:2]
         bo, co = optimize_constants_batch(ora_tb.take(idx), ds, opts, rng=np.random.default_rng(5), iterations=200,
                                           nrestarts=0)[:2]
         same = np.abs(cd - co) <= 1e-6 * np.maximum(np.abs(co), 1e-300)
         print(f"C5 optimiser disagreements: {idx.size} of {int(sel.sum())} trees; continued 200 iterations: same "
-              f"minimum {int(same.sum())}, different minima {int((~same).sum())}")
+              f"minimum {int(same.sum())}, different end points {int((~same).sum())}")
         assert np.all(cd <= dev_loss[idx] * (1 + 1e-12)) and np.all(co <= ora_loss[idx] * (1 + 1e-12))
         diff = np.nonzero(~same)[0]
+        n_checked = 0
+        for b, lv in ((bd, cd), (bo, co)):
+            if not diff.size:
+                break
+            sub = b.take(diff)
+            _, g, comp = eval_grad_batch(sub, ds, opts)
+            g_fd, _, comp_o, fd_err = orc.loss_grad_fd(sub, X, y, with_error=True)
+            co_off = sub.constant_offsets()
+            for j in range(sub.n_trees):
+                a_, f_, e_ = g[co_off[j]:co_off[j + 1]], g_fd[co_off[j]:co_off[j + 1]], fd_err[co_off[j]:co_off[j + 1]]
+                scale = max(1.0, float(np.abs(f_).max()))
+                print(f"   tree {int(idx[diff[j]])}: loss {float(lv[diff[j]]):.6g}, |grad| {float(np.abs(a_).max()):.3g}, "
+                      f"device - FD {float(np.abs(a_ - f_).max()):.2e} (FD error {float(e_.max()):.1e})")
+                assert comp[j] and comp_o[j]
+                if e_.max() > 1e-6 * scale:  # finite differences unreliable here (strong curvature)
+                    continue
+                assert np.all(np.abs(a_ - f_) <= 1e-6 * scale), (int(idx[diff[j]]), a_, f_)
+                n_checked += 1
         if diff.size:
-            from sr_amd import eval_grad_batch
-
-            for b, lv in ((bd, cd), (bo, co)):
-                sub = b.take(diff)
-                _, g, comp = eval_grad_batch(sub, ds, opts)
-                co_off = sub.constant_offsets()
-                cmask = sub.constant_mask()
-                for j in range(sub.n_trees):
-                    gj = g[co_off[j]:co_off[j + 1]]
-                    cj = sub.val[sub.offsets[j]:sub.offsets[j + 1]][cmask[sub.offsets[j]:sub.offsets[j + 1]]]
-                    scale = float(np.sum(np.abs(gj) * np.maximum(np.abs(cj), 1.0)))
-                    print(f"   different minima: tree {int(idx[diff[j]])} loss {float(lv[diff[j]]):.6g} "
-                          f"|g|.max(|c|,1) {scale:.3g}")
-                    assert comp[j] and scale <= 1e-3 * max(float(lv[diff[j]]), 1e-12), (int(idx[diff[j]]), scale)
+            assert n_checked >= diff.size, (n_checked, diff.size)  # most end points checked on either side
 
 
 def _c5_opts(**kw):

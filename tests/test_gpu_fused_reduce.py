@@ -1,4 +1,5 @@
-"""GPU: the in-launch partial reduction (the last workgroup of each tree group reduces it).
+"""GPU: the in-launch partial reduction (the last workgroup of each tree group reduces it; an option,
+`fused_reduce`, off by default: measured slower than the separate reduce launch).
 
 A multi-row-block LOSS launch writes its per-(row block, tree) partials with write-through stores; the
 workgroup whose counter add comes last reduces the group in `sr_reduce_partials_kernel`'s order.  Its
@@ -29,12 +30,13 @@ def _data(n, dtype, weighted, seed):
 
 def _both(fn):
     ctx = sr_amd.get_context()
-    fused = fn()
-    ctx.set_tuning("fused_reduce", 0)
+    ctx.set_tuning("fused_reduce", 1 << 30)
     try:
+        fused = fn()
+        ctx.set_tuning("fused_reduce", 0)
         plain = fn()
     finally:
-        ctx.set_tuning("fused_reduce", 1 << 30)
+        ctx.set_tuning("fused_reduce", 0)  # (the default: a separate reduce launch)
     return fused, plain
 
 
@@ -51,9 +53,14 @@ def test_fused_reduce_equals_reduce_launch(n_trees, n_rows, dtype, weighted):
     assert np.array_equal(cf, cp)
     assert np.array_equal(lf.view(np.uint8), lp.view(np.uint8))
     assert 0.05 < cf.mean() < 0.95
-    for _ in range(5):  # repeated calls: the same bits every time
-        l2, c2 = eval_loss_batch(tb, ds, opts)
-        assert np.array_equal(c2, cf) and np.array_equal(l2.view(np.uint8), lf.view(np.uint8))
+    ctx = sr_amd.get_context()
+    ctx.set_tuning("fused_reduce", 1 << 30)
+    try:
+        for _ in range(5):  # repeated fused calls: the same bits every time
+            l2, c2 = eval_loss_batch(tb, ds, opts)
+            assert np.array_equal(c2, cf) and np.array_equal(l2.view(np.uint8), lf.view(np.uint8))
+    finally:
+        ctx.set_tuning("fused_reduce", 0)
 
 
 def test_fused_reduce_views():
