@@ -487,7 +487,7 @@ def c4_line(ctx, opts, eval_loss_sharded, gen_random_batch, Dataset, args, comm,
            "scaling": "strong",
            "workload": (f"C4 row-sharded eval_loss: {tb.n_trees // 1000}k random trees (size U{{1..30}}; native "
                         f"generator, seed 4) x {rows_total >> 20}M rows x 5 features, rows sharded n/{world}"),
-           "code_path": "sr_eval_loss_sharded (same at every N)", "rows_per_gpu": n_local,
+           "code_path": "sr_eval_loss_sharded (same at every N)", "rows_per_gpu": n_local, "n_trees": int(tb.n_trees),
            "fraction_complete": float(np.mean(res["c"])),
            "last_step_passes": dict(passes, note=("trees through the exact isfinite(sum) pass (BIG) and through the "
                                                    "in-order loss fold (sr_fold.h); phase_ms = sr_last_phase_ms")),
