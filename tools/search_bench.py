@@ -15,7 +15,8 @@ from sr_amd import Options, equation_search  # noqa: E402
 
 def run(name, X, y, opts, niterations):
     t0 = time.perf_counter()
-    res = equation_search(X, y, niterations=niterations, options=opts, seed=0)
+    res = equation_search(X, y, niterations=niterations, options=opts, seed=0,
+                          scoring_lanes=int(os.environ.get("SR_SEARCH_LANES", "4")))
     wall = time.perf_counter() - t0
     best = min(res.pareto_frontier, key=lambda m: m.loss)
     print(json.dumps({"config": name, "islands": opts.populations, "iterations": niterations,
