@@ -82,7 +82,7 @@ struct HostBuf {
     if (bytes <= cap) return hipSuccess;
     if (p) {
       hipError_t e = hipStreamSynchronize(s);  // no DMA may still read the old buffer
-      if (e == hipSuccess) e = hipStreamSynchronize(s2);
+      if (e == hipSuccess && s2) e = hipStreamSynchronize(s2);  // (a context's second stream is created lazily)
       if (e == hipSuccess) e = hipHostFree(p);
       if (e != hipSuccess) return e;
       p = nullptr;
@@ -126,7 +126,13 @@ int sr_set_error(int code, const std::string& msg) { return set_error(code, msg)
 struct sr_ctx {
   int device = 0;
   hipStream_t stream = nullptr;
-  hipStream_t stream2 = nullptr;  // second stream of the chunked pipeline (odd chunks)
+  // second stream of the chunked pipeline (odd chunks), created on the first chunked call: a HIP
+  // stream takes one of the process's GPU_MAX_HW_QUEUES (4) hardware queues round-robin at creation, so
+  // an idle second stream per context left the search's four scoring lanes sharing two queues
+  hipStream_t stream2 = nullptr;
+  hipError_t need_stream2() {
+    return stream2 ? hipSuccess : hipStreamCreateWithFlags(&stream2, hipStreamNonBlocking);
+  }
   hipEvent_t ev_join = nullptr;
   hipEvent_t ev_start = nullptr, ev_k0 = nullptr, ev_k1 = nullptr, ev_end = nullptr;
   hipEvent_t ev_c0[kMaxChunks] = {}, ev_c1[kMaxChunks] = {};  // per-chunk interpreter launches
@@ -472,7 +478,7 @@ int run_batch(sr_ctx* ctx, const sr_dataset* ds, int opset_id, const sr_tree_bat
   // error exits while chunks are in flight: no DMA may still read the staging buffers
   auto sync_both = [&] {
     (void)hipStreamSynchronize(s);
-    (void)hipStreamSynchronize(ctx->stream2);
+    if (ctx->stream2) (void)hipStreamSynchronize(ctx->stream2);
   };
 
   // chunking (SR_AMD_CHUNKS, default 2; LOSS mode only — PRED writes rows by caller tree index).
@@ -660,6 +666,7 @@ int run_batch(sr_ctx* ctx, const sr_dataset* ds, int opset_id, const sr_tree_bat
                                       ds->n_probe, kProbeRows, spec, ctx->probe_derived.as<T>(), kProbeRows, s));
   }
   if (n_chunks > 1) {  // odd chunks run on the second stream, after the shared setup above
+    SR_HIP_CHECK(ctx->need_stream2());
     SR_HIP_CHECK(hipEventRecord(ctx->ev_join, s));
     SR_HIP_CHECK(hipStreamWaitEvent(ctx->stream2, ctx->ev_join, 0));
   }
@@ -2466,7 +2473,7 @@ int sr_init(int device, sr_ctx** out) {
   if (const char* v = std::getenv("SR_AMD_DERIVED")) ctx->derived = std::atoi(v);
   if (const char* v = std::getenv("SR_AMD_MAX_ROW_BLOCKS")) ctx->max_row_blocks = std::max(1, std::atoi(v));
   hipError_t e = hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking);
-  if (e == hipSuccess) e = hipStreamCreateWithFlags(&ctx->stream2, hipStreamNonBlocking);
+  if (e == hipSuccess && std::getenv("SR_AMD_EAGER_STREAM2")) e = ctx->need_stream2();  // (A/B: the round-4 layout)
   if (e == hipSuccess) e = hipEventCreateWithFlags(&ctx->ev_join, hipEventDisableTiming);
   if (e == hipSuccess) e = hipEventCreate(&ctx->ev_start);
   if (e == hipSuccess) e = hipEventCreate(&ctx->ev_k0);
@@ -2516,9 +2523,9 @@ int sr_shutdown(sr_ctx* ctx) {
       (void)hipEventDestroy(ctx->ev_g0[b]);
       (void)hipEventDestroy(ctx->ev_g1[b]);
     }
-    (void)hipStreamSynchronize(ctx->stream2);
+    if (ctx->stream2) (void)hipStreamSynchronize(ctx->stream2);
     (void)hipEventDestroy(ctx->ev_join);
-    (void)hipStreamDestroy(ctx->stream2);
+    if (ctx->stream2) (void)hipStreamDestroy(ctx->stream2);
     (void)hipEventDestroy(ctx->ev_start);
     (void)hipEventDestroy(ctx->ev_k0);
     (void)hipEventDestroy(ctx->ev_k1);
