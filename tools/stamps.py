@@ -5,7 +5,7 @@ issued, 2 first tile staged, 3 first window consumed, 4 first tile's trees done,
 6 results written.  Prints, per configuration, the median / p90 over waves of each point relative to
 the kernel's first entry and of each segment, plus the spread of wave entries (dispatch ramp).
 
-usage: SR_AMD_LIB=ab/stamps/libsr_amd.so python tools/stamps.py [config ...]   (c3, c1, c2s)"""
+usage: SR_AMD_LIB=ab/stamps/libsr_amd.so python tools/stamps.py [config ...]   (c3, c3s, c5, c1, c2s)"""
 import ctypes
 import os
 import sys
@@ -57,6 +57,10 @@ def main():
             dt, n_rows, n_trees, nf = np.float32, 100_000, 31, 5
         elif cfg == "c1":  # C1: 20 trees x 100 rows f64
             dt, n_rows, n_trees, nf = np.float64, 100, 20, 2
+        elif cfg == "c3s":  # the C3 search's average call: 9 trees x 100k rows f32
+            dt, n_rows, n_trees, nf = np.float32, 100_000, 9, 5
+        elif cfg == "c5":  # the C5 search's average call: 8 trees x 100k rows f64
+            dt, n_rows, n_trees, nf = np.float64, 100_000, 8, 5
         else:  # c2s: 1000 trees x 2^20 rows f32
             dt, n_rows, n_trees, nf = np.float32, 1 << 20, 1000, 5
         rng = np.random.default_rng(0)
