@@ -229,7 +229,13 @@ SRL_HD inline float sr_sincosf_tab(float x, const double* tab) {
   // Taylor terms in Horner form, five f64 operations (round 3; was six)
   const double a = COS ? ck : sk, b = COS ? -sk : ck;
   const double c2 = -0.5 * a, c3 = b * -0x1.5555555555555p-3;
+#ifdef SR_TRIG_DEG4
+  // (A/B: one Taylor term more, r^4 a / 24: two f64 operations more per row)
+  const double c4 = a * 0x1.5555555555555p-5;
+  return float(fma(r, fma(r, fma(r, fma(r, c4, c3), c2), b), a));
+#else
   return float(fma(r, fma(r, fma(r, c3, c2), b), a));
+#endif
 }
 
 // Full range: the table path below 2^20, Payne-Hanek above (the device only comes here when some
