@@ -234,10 +234,13 @@ def main():
     from sr_amd.distributed import comm_info, eval_loss_sharded, eval_loss_tree_sharded, init_device_comm
 
     comm = Comm(world, rank)
-    ctx = sr_amd.get_context(local_rank)
+    # the device: LOCAL_RANK, or SR_AMD_DEVICE (a rehearsal on a one-GPU box puts every rank on device 0;
+    # RCCL refuses two ranks on one device, so that run takes the gloo exchange below)
+    ctx = sr_amd.get_context(int(os.environ.get("SR_AMD_DEVICE", local_rank)))
     # the library's RCCL communicator (every data-path exchange of the sharded calls); if it cannot be
-    # created on every rank, all ranks fall back to exchanging the same partials over gloo (host
-    # copies) and the line says so, rather than printing nothing
+    # created on every rank, all ranks fall back to the library's host transport (the same C++ sharded
+    # path, its collectives staged through host memory over gloo) and the line says so, rather than
+    # printing nothing
     err = None
     try:
         init_device_comm(ctx=ctx)
@@ -250,8 +253,10 @@ def main():
             from sr_amd.distributed import destroy_device_comm
             destroy_device_comm(ctx)
         print(f"[bench] rank {rank}: RCCL communicator unavailable ({err or 'failed on a peer rank'}); "
-              "the sharded calls exchange over gloo", file=sys.stderr, flush=True)
-        cinfo = {"nranks": None, "rccl_error": err or "failed on a peer rank"}
+              "the sharded calls exchange over gloo (host transport)", file=sys.stderr, flush=True)
+        from sr_amd.distributed import init_host_comm
+        init_host_comm(ctx=ctx)
+        cinfo = {"nranks": None, "rccl_error": err or "failed on a peer rank", "transport": "host (gloo)"}
     else:
         cinfo = comm_info(ctx)
 
@@ -329,7 +334,7 @@ def main():
             "unit": "node-evals/s",
             "n_gpus": world,
             "world_size_rccl": cinfo["nranks"],
-            **({"rccl_error": cinfo["rccl_error"]} if cinfo.get("rccl_error") else {}),
+            **({"rccl_error": cinfo["rccl_error"], "transport": cinfo["transport"]} if cinfo.get("rccl_error") else {}),
             "steps": args.steps,
             "warmup": args.warmup,
             "ms_per_step": dt / args.steps * 1e3,
