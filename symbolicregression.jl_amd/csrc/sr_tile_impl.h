@@ -1164,7 +1164,11 @@ __global__ void __launch_bounds__(W * 64, (SrMinWavesFor<T, R, TIER, W, VSTK, LK
           // Base.mapreduce_impl's sequential leaf loop, v = v + a[i] in T, continued across the
           // range's tiles (lane k folds check k; the first row of the range starts the fold)
           __builtin_amdgcn_wave_barrier();
+#ifdef SR_EXACT_NOFOLD
+          const int nk = 0;  // (timing experiment only: the exact pass without its sequential folds)
+#else
           const int nk = check_k < MC ? check_k : MC;
+#endif
           for (int k = lane; k < nk; k += 64) {
             const T* cb = chk + (size_t(wave) * MC + k) * ROWS;
             T v = (tile == 0) ? cb[0] : jst[g * MC + k];
