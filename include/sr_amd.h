@@ -442,7 +442,9 @@ int sr_last_phase_ms(sr_ctx* ctx, double* out, int n);
  * call; Float32 16 / 32 force the register-stack kernel and 4 / 8 the LDS-stack one, Float64 8 / 4
  * likewise), "balance" (0 / 1: deal the cost-ordered trees round-robin over tree groups),
  * "fused_reduce" (the largest tree group, in trees x row blocks, whose partials the interpreter launch
- * reduces itself — its last workgroup per group; 0: always a separate reduce launch).  Results do
+ * reduces itself — its last workgroup per group; 0: always a separate reduce launch), "exact_w" (4 / 1:
+ * waves per workgroup of the exact-sum pass), "exact_g" (listed trees per exact-sum workgroup; 0: the
+ * heuristic).  Results do
  * not depend on any knob.  SR_ERR_INVALID_ARG for an unknown name.  sr_tuning_info (optional outputs)
  * reports how many derived columns the last sr_eval_loss_batch used and how many of its trees went
  * through the exact-sum pass (flagged BIG). */

@@ -436,10 +436,12 @@ hipError_t sr_launch_eval(const SrEvalArgs<T>& a, int mode, bool gather, int tie
     if (mode == SR_MODE_PRED)
       return gather ? sr_launch_tile<T, 4, SR_MODE_PRED, true, SR_TIER_FULL>(a, n_blocks, s)
                     : sr_launch_tile<T, 4, SR_MODE_PRED, false, SR_TIER_FULL>(a, n_blocks, s);
+    if (waves == 4)  // (EXACT: 1 or 4 waves per workgroup, sharing the staged rows)
+      return gather ? sr_launch_tile<T, 4, SR_MODE_EXACT, true, SR_TIER_FULL, 4>(a, n_blocks, s)
+                    : sr_launch_tile<T, 4, SR_MODE_EXACT, false, SR_TIER_FULL, 4>(a, n_blocks, s);
     return gather ? sr_launch_tile<T, 4, SR_MODE_EXACT, true, SR_TIER_FULL, 1>(a, n_blocks, s)
                   : sr_launch_tile<T, 4, SR_MODE_EXACT, false, SR_TIER_FULL, 1>(a, n_blocks, s);
   } else {
-    (void)waves;
     if (vstk) {
       if (mode != SR_MODE_LOSS || tier != SR_TIER_BASIC || gather) return hipErrorInvalidValue;
       if (R == 8) return sr_launch_basic_loss<T, 8, false, true>(a, n_blocks, s);
@@ -455,6 +457,9 @@ hipError_t sr_launch_eval(const SrEvalArgs<T>& a, int mode, bool gather, int tie
     if (mode == SR_MODE_PRED)
       return gather ? sr_launch_tile<T, 2, SR_MODE_PRED, true, SR_TIER_FULL>(a, n_blocks, s)
                     : sr_launch_tile<T, 2, SR_MODE_PRED, false, SR_TIER_FULL>(a, n_blocks, s);
+    if (waves == 4)
+      return gather ? sr_launch_tile<T, 2, SR_MODE_EXACT, true, SR_TIER_FULL, 4>(a, n_blocks, s)
+                    : sr_launch_tile<T, 2, SR_MODE_EXACT, false, SR_TIER_FULL, 4>(a, n_blocks, s);
     return gather ? sr_launch_tile<T, 2, SR_MODE_EXACT, true, SR_TIER_FULL, 1>(a, n_blocks, s)
                   : sr_launch_tile<T, 2, SR_MODE_EXACT, false, SR_TIER_FULL, 1>(a, n_blocks, s);
   }

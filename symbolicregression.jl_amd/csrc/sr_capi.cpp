@@ -178,6 +178,7 @@ struct sr_ctx {
   int debug_hint_regrow = 0;       // tests (sr_set_tuning "debug_hint_regrow"): grow the hint array in place
   void* hint_reserve = nullptr;    // its fixed-address reservation
   int exact_g = 0;          // SR_AMD_EXACT_G (tuning): listed trees per workgroup of the EXACT pass
+  int exact_w = 4;          // SR_AMD_EXACT_W / sr_set_tuning "exact_w": waves per EXACT workgroup (4, or 1)
   // SR_AMD_DERIVED (default 1): nodes unary(feature) shared by several trees of a large LOSS call
   // are evaluated once per call into derived columns (LOAD_DERIVED); 0 disables
   int derived = 1;
@@ -1193,11 +1194,15 @@ int run_exact(sr_ctx* ctx, const sr_dataset* ds, const SrProgramBatch<T>& prog, 
     // profiles/r02_ab_exact_g.txt)
     const int64_t g_fill = (nb * n_ranges + 1023) / 1024;
     int G = int(std::min<int64_t>(nb, ctx->exact_g > 0 ? ctx->exact_g : std::max<int64_t>(1, std::min<int64_t>(16, g_fill))));
+    // four waves per workgroup share the staged rows, each folding its own trees: one wave per
+    // workgroup left ~1 wave per SIMD for C2's 8 listed trees x 1024 leaves (latency-bound)
+    int W = (ctx->exact_w == 4 && G >= 4) ? 4 : 1;
     size_t lds = 0;
     for (;;) {
-      lds = sr_tile_lds_bytes(int(sizeof(T)), int(ds->nf), R, depth, G, max_checks, 1, false);
+      lds = sr_tile_lds_bytes(int(sizeof(T)), int(ds->nf), R, depth, G, max_checks, W, false);
       if (lds <= kLdsMax || G == 1) break;
       G /= 2;
+      if (G < W) W = 1;
     }
     if (lds > kLdsMax) return set_error(SR_ERR_TOO_DEEP, "exact-sum pass needs more LDS than 160 KiB");
     std::vector<uint32_t> list32(static_cast<size_t>(nb));
@@ -1229,7 +1234,7 @@ int run_exact(sr_ctx* ctx, const sr_dataset* ds, const SrProgramBatch<T>& prog, 
     const int64_t blocks = int64_t(a.n_groups) * n_ranges;
     if (blocks > 0x7fffffff) return set_error(SR_ERR_INVALID_ARG, "grid too large");
     SR_HIP_CHECK(hipEventRecord(ctx->ev_k0, s));
-    SR_HIP_CHECK(sr_launch_eval<T>(a, SR_MODE_EXACT, gather, SR_TIER_FULL, R, 1, false, int(blocks), s));
+    SR_HIP_CHECK(sr_launch_eval<T>(a, SR_MODE_EXACT, gather, SR_TIER_FULL, R, W, false, int(blocks), s));
     if (host_finite) {
       const int64_t n_arrays = nb * max_checks;
       SR_HIP_CHECK(ctx->jsum_fin.ensure(size_t(n_arrays) + 16));
@@ -2470,6 +2475,7 @@ int sr_init(int device, sr_ctx** out) {
   if (const char* v = std::getenv("SR_AMD_HOST_IO")) ctx->host_io = std::atoi(v);
   if (const char* v = std::getenv("SR_AMD_SPIN")) ctx->spin = std::atoi(v);
   if (const char* v = std::getenv("SR_AMD_EXACT_G")) ctx->exact_g = std::atoi(v);
+  if (const char* v = std::getenv("SR_AMD_EXACT_W")) ctx->exact_w = std::atoi(v) == 1 ? 1 : 4;
   if (const char* v = std::getenv("SR_AMD_DERIVED")) ctx->derived = std::atoi(v);
   if (const char* v = std::getenv("SR_AMD_MAX_ROW_BLOCKS")) ctx->max_row_blocks = std::max(1, std::atoi(v));
   hipError_t e = hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking);
@@ -3154,6 +3160,14 @@ int sr_set_tuning(sr_ctx* ctx, const char* name, int64_t value) {
   }
   if (std::strcmp(name, "fused_reduce") == 0) {  // in-launch partial reduction bound (SR_AMD_FUSED_REDUCE)
     ctx->fused_reduce = value;
+    return SR_OK;
+  }
+  if (std::strcmp(name, "exact_w") == 0) {  // waves per workgroup of the EXACT pass (SR_AMD_EXACT_W)
+    ctx->exact_w = value == 1 ? 1 : 4;
+    return SR_OK;
+  }
+  if (std::strcmp(name, "exact_g") == 0) {  // listed trees per EXACT workgroup, 0 = heuristic (SR_AMD_EXACT_G)
+    ctx->exact_g = int(value < 0 ? 0 : (value > 64 ? 64 : value));
     return SR_OK;
   }
   if (std::strcmp(name, "code_cache") == 0) {  // LDS program cache (SR_AMD_CODE_CACHE)

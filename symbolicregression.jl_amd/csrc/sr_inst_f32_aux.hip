@@ -4,4 +4,6 @@ SR_INSTANTIATE(float, 4, SR_MODE_PRED, false, SR_TIER_FULL)
 SR_INSTANTIATE(float, 4, SR_MODE_PRED, true, SR_TIER_FULL)
 SR_INSTANTIATE_W(float, 4, SR_MODE_EXACT, false, SR_TIER_FULL, 1)
 SR_INSTANTIATE_W(float, 4, SR_MODE_EXACT, true, SR_TIER_FULL, 1)
+SR_INSTANTIATE_W(float, 4, SR_MODE_EXACT, false, SR_TIER_FULL, 4)
+SR_INSTANTIATE_W(float, 4, SR_MODE_EXACT, true, SR_TIER_FULL, 4)
 SR_INSTANTIATE_DERIVED(float)

@@ -64,7 +64,8 @@ class DeviceContext:
 
     def set_tuning(self, name, value):
         """Run-time tuning knob (results never depend on one; include/sr_amd.h lists them): "derived",
-        "probe", "stress_probe", "code_cache", "timing", "rows_per_lane", "balance", "fused_reduce"; tests:
+        "probe", "stress_probe", "code_cache", "timing", "rows_per_lane", "balance", "fused_reduce", "exact_w",
+        "exact_g"; tests:
         "inject_failure", "debug_hint_regrow"."""
         _lib.check(_lib.lib.sr_set_tuning(self.handle, name.encode(), int(value)))
 
