@@ -673,6 +673,8 @@ int run_batch(sr_ctx* ctx, const sr_dataset* ds, int opset_id, const sr_tree_bat
   }
 
   uint32_t code_base = 0;
+  static const bool phase_debug = std::getenv("SR_AMD_PHASE_DEBUG") != nullptr;  // (latency analysis)
+  const auto t_pre = std::chrono::steady_clock::now();
   Grid glast = g0;
   std::string err;
   for (int c = 0; c < n_chunks && nt > 0; ++c) {
@@ -704,7 +706,15 @@ int run_batch(sr_ctx* ctx, const sr_dataset* ds, int opset_id, const sr_tree_bat
       }
       return set_error(rc, err);
     }
-    if (c == 0) ctx->mark_phase(0);
+    if (c == 0) {
+      if (phase_debug) {
+        const auto now = std::chrono::steady_clock::now();
+        std::fprintf(stderr, "[sr phase] trees %lld chunks %d: setup %.3f ms, compile of chunk 0 (%lld trees) %.3f ms\n",
+                     (long long)nt, n_chunks, std::chrono::duration<double, std::milli>(t_pre - ctx->phase_t).count(),
+                     (long long)nc, std::chrono::duration<double, std::milli>(now - t_pre).count());
+      }
+      ctx->mark_phase(0);
+    }
     const int depth = pc.max_depth > 0 ? pc.max_depth : 1;
     // Trees whose programs fit the register stack (<= 2 slots: every tree of < 23 nodes, most of the
     // rest) run on the register-stack kernel; the few deeper ones follow in a second launch of the
