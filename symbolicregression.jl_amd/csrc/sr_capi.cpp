@@ -179,6 +179,7 @@ struct sr_ctx {
   void* hint_reserve = nullptr;    // its fixed-address reservation
   int exact_g = 0;          // SR_AMD_EXACT_G (tuning): listed trees per workgroup of the EXACT pass
   int exact_w = 4;          // SR_AMD_EXACT_W / sr_set_tuning "exact_w": waves per EXACT workgroup (4, or 1)
+  int par_stage = 1;        // SR_AMD_PAR_STAGE: large chunks' programs copied to the staging buffer in parallel
   // SR_AMD_DERIVED (default 1): nodes unary(feature) shared by several trees of a large LOSS call
   // are evaluated once per call into derived columns (LOAD_DERIVED); 0 disables
   int derived = 1;
@@ -692,6 +693,7 @@ int run_batch(sr_ctx* ctx, const sr_dataset* ds, int opset_id, const sr_tree_bat
     sub.n_trees = nc;
     sub.offsets = trees->offsets + t0;  // node arrays stay indexed by absolute offsets
     SrProgramBatch<T> pc;
+    pc.keep_pieces = true;  // (staged below straight from the compile workers' buffers)
     int rc = sr_compile_batch<T>(sub, ctx->opsets[opset_id], n_total, ds->nf, false, &pc, &err,
                                  dmap.empty() ? nullptr : dmap.data());
     if (rc != SR_OK) {
@@ -723,7 +725,7 @@ int run_batch(sr_ctx* ctx, const sr_dataset* ds, int opset_id, const sr_tree_bat
     if (Rv > 0)
       for (int64_t i = 0; i < nc; ++i) n_vs += pc.depth[size_t(i)] <= SR_VSTK_SLOTS ? 1 : 0;
     // stage: code at code_base, offsets made absolute, static_bad, launch order (chunk-local)
-    const size_t ncode = pc.code.size();
+    const size_t ncode = pc.n_code;
     if (code_base + ncode > code_cap) {
       sync_both();
       return set_error(SR_ERR_INVALID_ARG, "program longer than its node count");
@@ -777,13 +779,30 @@ int run_batch(sr_ctx* ctx, const sr_dataset* ds, int opset_id, const sr_tree_bat
       // programs in launch order: a tree group's code is one contiguous span (the kernel's LDS program
       // cache copies it in one pass); offsets / ends stay indexed by tree
       uint32_t at = code_base;
-      for (int64_t p = 0; p < nc; ++p) {
+      for (int64_t p = 0; p < nc; ++p) {  // destinations: a prefix over the launch order
         const uint32_t i = h_perm[t0 + p];
-        const uint32_t b = pc.offsets[size_t(i)], e = pc.offsets[size_t(i) + 1];
-        if (e > b) std::memcpy(h_code + at, pc.code.data() + b, size_t(e - b) * sizeof(SrIns<T>));
+        const uint32_t len = pc.offsets[size_t(i) + 1] - pc.offsets[size_t(i)];
         h_off[t0 + i] = at;
-        h_end[t0 + i] = at + (e - b);
-        at += e - b;
+        h_end[t0 + i] = at + len;
+        at += len;
+      }
+      // the copies into the pinned staging buffer: a large chunk's ~2 MB on the compile workers
+      // (single-threaded they sat on the host path between the first chunk's launch and the second's)
+      auto copy = [&](int64_t p0, int64_t p1) {
+        for (int64_t p = p0; p < p1; ++p) {
+          const uint32_t i = h_perm[t0 + p];
+          const uint32_t len = h_end[t0 + i] - h_off[t0 + i];
+          if (len) std::memcpy(h_code + h_off[t0 + i], pc.tree_code(i), size_t(len) * sizeof(SrIns<T>));
+        }
+      };
+      constexpr int64_t kCopyPiece = 512;
+      if (ctx->par_stage && nc >= 4 * kCopyPiece) {
+        sr_parallel_for(int((nc + kCopyPiece - 1) / kCopyPiece), [&](int w) {
+          const int64_t p0 = int64_t(w) * kCopyPiece;
+          copy(p0, std::min<int64_t>(nc, p0 + kCopyPiece));
+        });
+      } else {
+        copy(0, nc);
       }
     }
     // several views: one segment per view present (launch positions in view order), tree groups of the
@@ -2486,6 +2505,7 @@ int sr_init(int device, sr_ctx** out) {
   if (const char* v = std::getenv("SR_AMD_SPIN")) ctx->spin = std::atoi(v);
   if (const char* v = std::getenv("SR_AMD_EXACT_G")) ctx->exact_g = std::atoi(v);
   if (const char* v = std::getenv("SR_AMD_EXACT_W")) ctx->exact_w = std::atoi(v) == 1 ? 1 : 4;
+  if (const char* v = std::getenv("SR_AMD_PAR_STAGE")) ctx->par_stage = std::atoi(v);
   if (const char* v = std::getenv("SR_AMD_DERIVED")) ctx->derived = std::atoi(v);
   if (const char* v = std::getenv("SR_AMD_MAX_ROW_BLOCKS")) ctx->max_row_blocks = std::max(1, std::atoi(v));
   hipError_t e = hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking);

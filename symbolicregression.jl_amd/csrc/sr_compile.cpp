@@ -634,6 +634,14 @@ uint32_t sr_binary_id(const char* name) {
   return 0;
 }
 
+void sr_parallel_for(int n, const std::function<void(int)>& fn) {
+  if (n <= 1) {
+    if (n == 1) fn(0);
+    return;
+  }
+  WorkerPool::get().run(n, fn);
+}
+
 template <typename T>
 int sr_compile_batch(const sr_tree_batch& trees, const SrOpset& ops, int64_t n_rows, int64_t nfeatures,
                      bool with_const_index, SrProgramBatch<T>* out, std::string* err, const int16_t* derived) {
@@ -730,12 +738,24 @@ int sr_compile_batch(const sr_tree_batch& trees, const SrOpset& ops, int64_t n_r
   out->total_ops = 0;
   size_t total = 0;
   for (int64_t k = 0; k < nt; ++k) total += per[k].len;
-  out->code.resize(total);
+  out->n_code = total;
+  const bool lazy = out->keep_pieces;
+  if (lazy) {
+    out->piece.resize(size_t(nt));
+    out->begin.resize(size_t(nt));
+  } else {
+    out->code.resize(total);
+  }
   size_t at = 0;
   for (int64_t k = 0; k < nt; ++k) {
     const PerTree& p = per[k];
     out->offsets[k] = uint32_t(at);
-    if (p.len) std::memcpy(out->code.data() + at, bufs[size_t(p.thread)].data() + p.begin, size_t(p.len) * sizeof(SrIns<T>));
+    if (lazy) {
+      out->piece[size_t(k)] = uint32_t(p.thread);
+      out->begin[size_t(k)] = p.begin;
+    } else if (p.len) {
+      std::memcpy(out->code.data() + at, bufs[size_t(p.thread)].data() + p.begin, size_t(p.len) * sizeof(SrIns<T>));
+    }
     at += p.len;
     out->static_bad[k] = p.bad;
     out->cost[k] = p.bad ? 0u : p.cost;
@@ -748,7 +768,8 @@ int sr_compile_batch(const sr_tree_batch& trees, const SrOpset& ops, int64_t n_r
     out->total_nodes += p.nodes;
     out->total_ops += p.ops;
   }
-  out->offsets[nt] = uint32_t(out->code.size());
+  out->offsets[nt] = uint32_t(total);
+  if (lazy) out->pieces = std::move(bufs);
   return SR_OK;
 }
 

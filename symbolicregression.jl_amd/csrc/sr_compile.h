@@ -14,6 +14,7 @@
 // the `complete` flag is the AND of all check predicates, independent of order.
 #pragma once
 #include <stdint.h>
+#include <functional>
 #include <string>
 #include <vector>
 #include "sr_ops.h"
@@ -42,11 +43,25 @@ struct SrProgramBatch {
   int max_checks = 0;
   int64_t total_nodes = 0;          // Σ count_nodes (metric unit)
   int64_t total_ops = 0;            // Σ operator nodes
+  // Lazy form (the caller sets keep_pieces before compiling): `code` stays empty and tree k's
+  // offsets[k + 1] - offsets[k] instructions sit at pieces[piece[k]][begin[k]...] (the compile
+  // workers' own buffers), so a caller that re-stages the programs anyway (run_batch, in launch
+  // order) copies them once instead of twice.  n_code counts the instructions in either form.
+  bool keep_pieces = false;
+  std::vector<std::vector<SrIns<T>>> pieces;
+  std::vector<uint32_t> piece, begin;
+  size_t n_code = 0;
+  const SrIns<T>* tree_code(size_t k) const {
+    return keep_pieces ? pieces[piece[k]].data() + begin[k] : code.data() + offsets[k];
+  }
 };
 
 // Compile a batch.  n_rows: rows the programs will be evaluated on (static overflow checks of
 // constant arrays).  nfeatures: columns of X.  with_const_index: emit constant-slot indices in
 // `arg` of CONST loads (gradient kernels).  Returns SR_OK or an error code with *err set.
+// fn(0) .. fn(n - 1) on the compile workers and the caller (the persistent pool sr_compile_batch uses).
+void sr_parallel_for(int n, const std::function<void(int)>& fn);
+
 // Estimated cost of one program instruction on the device, in VALU-instruction-like units per row
 // step (dispatch overhead included): used only to order trees for load balance.
 uint32_t sr_instruction_cost(uint32_t opcode);
