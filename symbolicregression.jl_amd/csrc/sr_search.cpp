@@ -1138,7 +1138,12 @@ struct Engine : sr_search_base {
     } else {
       // contiguous shares of the owned islands, one host thread per extra lane
       std::vector<std::vector<int>> share(nl);
-      for (size_t k = 0; k < owned.size(); ++k) share[k * nl / owned.size()].push_back(owned[k]);
+      static const bool interleave = [] {  // SR_AMD_LANE_INTERLEAVE=1: island k on lane k mod lanes (A/B)
+        const char* v = std::getenv("SR_AMD_LANE_INTERLEAVE");
+        return v && std::atoi(v) != 0;
+      }();
+      for (size_t k = 0; k < owned.size(); ++k)
+        share[interleave ? k % nl : k * nl / owned.size()].push_back(owned[k]);
       std::vector<int> rcs(nl, SR_OK);
       std::vector<std::string> msgs(nl);
       std::vector<std::thread> th;
