@@ -210,8 +210,10 @@ SRL_HD inline double sr_rem_pio2f_fast(float x, int* q) {
 // ulp after the final rounding (tools/libm_exhaustive.cpp: every Float32 |x| < 2^20).  Five f64
 // operations after the reduction, the terms in Horner form in r (six as (c_k cos r - s_k sin r) in
 // round 3's first version, eight with the degree-5/4 polynomials of a 128-entry table).
-template <bool COS>
-SRL_HD inline float sr_sincosf_tab(float x, const double* tab) {
+struct SrTrigArg {
+  double r, sk, ck;
+};
+SRL_HD inline SrTrigArg sr_trig_arg(float x, const double* tab) {
   const double xd = double(x);
   // n = x 128/pi rounded to an integer by the 1.5 * 2^52 shifter: k = n mod 256 is the shifter's
   // low bits (no conversions; a NaN x only yields a NaN result).  Two-part Cody-Waite with fused
@@ -224,7 +226,11 @@ SRL_HD inline float sr_sincosf_tab(float x, const double* tab) {
   __builtin_memcpy(&tb, &t, 8);
   // entry k = 16 bytes at byte offset 16 k
   const double* e = reinterpret_cast<const double*>(reinterpret_cast<const char*>(tab) + ((uint32_t(tb) << 4) & 0xff0u));
-  const double sk = e[0], ck = e[1];
+  return SrTrigArg{r, e[0], e[1]};
+}
+template <bool COS>
+SRL_HD inline float sr_trig_poly(const SrTrigArg& p) {
+  const double r = p.r, sk = p.sk, ck = p.ck;
   // cos x = ck + r (-sk + r (-ck/2 + r sk/6)), sin x = sk + r (ck + r (-sk/2 - r ck/6)): the same
   // Taylor terms in Horner form, five f64 operations (round 3; was six)
   const double a = COS ? ck : sk, b = COS ? -sk : ck;
@@ -236,6 +242,10 @@ SRL_HD inline float sr_sincosf_tab(float x, const double* tab) {
 #else
   return float(fma(r, fma(r, fma(r, c3, c2), b), a));
 #endif
+}
+template <bool COS>
+SRL_HD inline float sr_sincosf_tab(float x, const double* tab) {
+  return sr_trig_poly<COS>(sr_trig_arg(x, tab));
 }
 
 // Full range: the table path below 2^20, Payne-Hanek above (the device only comes here when some

@@ -309,11 +309,28 @@ __device__ SR_LIBM_CALL SrRowVec<R> sr_log_rows(SrRowVec<R> v) {
 // all caller-saved, so the common call saves nothing)
 template <uint32_t ID, int R>
 __device__ SR_LIBM_CALL SrRowVec<R> sr_trig_rows_fast(SrRowVec<R> v) {
+#ifdef SR_TRIG_PIPE
+  // (A/B) table reads one row ahead: row r+1's reduction and (sin, cos)(k pi/128) read are issued
+  // before row r's polynomial, so the LDS latency overlaps the previous row's five f64 operations
+  // (same arithmetic per row: bit-identical)
+  const double* tab = sr_trig_tab();
+  SrTrigArg cur = sr_trig_arg(v[0], tab);
+#pragma unroll
+  for (int r = 0; r < R; ++r) {
+    SrTrigArg nxt = cur;
+    if (r + 1 < R) nxt = sr_trig_arg(v[r + 1], tab);
+    __builtin_amdgcn_sched_barrier(0);
+    v[r] = sr_trig_poly<ID == SR_U_COS>(cur);
+    __builtin_amdgcn_sched_barrier(0);
+    cur = nxt;
+  }
+#else
 #pragma unroll
   for (int r = 0; r < R; ++r) {
     v[r] = (ID == SR_U_COS) ? sr_cosf_fast(v[r]) : sr_sinf_fast(v[r]);
     SR_LIBM_ROW_END(r);
   }
+#endif
   return v;
 }
 
