@@ -512,6 +512,47 @@ def c4_line(ctx, opts, eval_loss_sharded, gen_random_batch, Dataset, args, comm,
     return out
 
 
+_LIBM_EXACT_UNARY = {"neg", "square", "cube", "abs", "sign", "relu", "inv", "round", "floor", "ceil", "sqrt",
+                     "safe_sqrt"}
+
+
+def held_trees(opts, orc, sub, X, y, rows, d_loss, l64, bar, threads, ids=None, limit=40):
+    """For every tree held to its libm-spread bar (device vs f64-accumulated oracle past the plain
+    relative bar): the expression, the relative difference, and the operator whose +-1-ulp last-bit
+    differences the tree's loss amplifies most — the oracle's conditioning probe restricted to one
+    operator at a time (oracle/de_eval_impl.h perturb codes), four sign patterns each."""
+    from sr_amd.node import string_tree
+
+    out = []
+    ops = opts.operators
+    for j, k in enumerate(rows[:limit]):
+        one = sub.take([k])
+        present = set()
+        for d, o in zip(one.degree, one.op):
+            if d == 1 and ops.unaops[o - 1] not in _LIBM_EXACT_UNARY:
+                present.add((ops.unaops[o - 1], 1))
+            elif d == 2 and ops.binops[o - 1] in ("^", "safe_pow", "pow"):
+                present.add((ops.binops[o - 1], 2))
+        l0, _ = orc.eval_loss_batch(one, X, y, accum="f64", n_threads=threads)
+        spreads = {}
+        for name, deg in sorted(present):
+            s = 0.0
+            for seed in (1, 2, 3, 4):
+                lp, cp = orc.eval_loss_batch(one, X, y, accum="f64", n_threads=threads,
+                                             perturb=seed | orc.perturb_code(name, deg))
+                dd = abs(float(lp[0]) - float(l0[0]))
+                if cp[0] and np.isfinite(dd):
+                    s = max(s, dd)
+            spreads[name] = s / max(abs(float(l0[0])), 1e-300)
+        amp = max(spreads, key=spreads.get) if spreads else None
+        ref = float(l64[k])
+        out.append({"tree": int(ids[k] if ids is not None else k), "expr": string_tree(sub.tree(int(k)), ops),
+                    "rel": abs(float(d_loss[k]) - ref) / max(abs(ref), 1e-300),
+                    "bar_rel": float(bar[k]) / max(abs(ref), 1e-300),
+                    "amplified_op": amp, "rel_spread_per_op": spreads})
+    return out
+
+
 def per_tree_bar(orc, sub, X, y, d_loss, l64, ok, rel_bar, threads):
     """The tests' per-tree loss bar (tests/parity_util.py): max(rel_bar |oracle|, 4 x the tree's spread
     under +-1-ulp libm perturbations), the spread measured only for the trees the plain bar misses."""
@@ -572,7 +613,9 @@ def c4_parity(opts, tb, res, device_call, rows_total, n_sample):
                      "flag_mismatches": int(np.sum(d_comp != c64)) + int(np.sum(cref != c64)),
                      "ref_fold_inf_trees": int(np.sum(ok & np.isinf(lref))), "ref_fold_inf_mismatches": inf_m,
                      "max_rel_vs_f64_accum": float(np.max(np.where(np.isfinite(r[ok]), r[ok], 0.0), initial=0.0)),
-                     "n_held_to_libm_spread_bar": n_wide, "loss_failures": int(fail.sum())}
+                     "n_held_to_libm_spread_bar": n_wide, "loss_failures": int(fail.sum()),
+                     "held_trees": held_trees(opts, orc, t, X, y, np.nonzero(ok & (r > 1e-4))[0], d_loss,
+                                              l64.astype(np.float64), bar, threads, ids=idx if name == "sample" else None)}
     out["rows"] = int(rows_total)
     out["pass"] = all(v["flag_mismatches"] == 0 and v["loss_failures"] == 0 and v["ref_fold_inf_mismatches"] == 0
                       for v in (out["sample"], out["planted_big"]))
@@ -657,6 +700,8 @@ def f64_parity_sample(opts, tb64, X64, y64, o64, n=320):
             "flag_mismatches": int(np.sum(d_comp != c64)), "loss_failures": int(fail.sum()),
             "max_rel": float(np.max(r[fin], initial=0.0)), "median_rel": float(np.median(r[fin])) if fin.any() else 0.0,
             "n_held_to_libm_spread_bar": n_wide, "pass": bool(np.all(d_comp == c64) and not fail.any()),
+            "held_trees": held_trees(opts, orc, sub, X64, y64, np.nonzero(ok & (r > 1e-10))[0], d_loss, l64, bar,
+                                     threads, ids=idx),
             "rule": "flags bit-exact; every complete tree within max(1e-10 |oracle|, 4 x libm spread)",
             "cpu_s": time.perf_counter() - t0}
 
@@ -898,6 +943,7 @@ def cpu_baseline_and_parity(opts, tb, X, y, n_sample, dev_loss, dev_comp):
               "median_rel_vs_f64_accum": float(np.median(r64[ok])) if ok.any() else 0.0,
               "n_rel_vs_f64_accum_over_1e-4": int(np.sum(r64[ok] > 1e-4)),
               "n_held_to_libm_spread_bar": int(worst.size),
+              "held_trees": held_trees(opts, orc, sub, X, y, worst, d_loss, l64, bar, threads, ids=idx),
               "loss_failures_vs_f64_accum": int(fail64.sum()),
               "max_rel_vs_ref_f32_fold": float(np.max(rref[fin], initial=0.0)),
               "median_rel_vs_ref_f32_fold": float(np.median(rref[fin])) if fin.any() else 0.0,

@@ -133,8 +133,12 @@ static int FN(psign)(int node, int64_t row, int p) {
   h ^= h >> 16; h *= 0x7FEB352Du; h ^= h >> 15; h *= 0x846CA68Bu; h ^= h >> 16;
   return (h & 1u) ? 1 : -1;
 }
+/* p = seed | (op << 8): a non-zero op (unary id, or 64 + binary id) restricts the probe to that one
+ * operator (bench.py's parity.held_trees names the operator a tree's loss is most sensitive to). */
 static T FN(perturb_unary)(int id, T v, int p, int node, int64_t row) {
   if (!p) return v;
+  if ((p >> 8) && (p >> 8) != id) return v;
+  p &= 0xff;
   switch (id) {
     case O_NEG: case O_SQUARE: case O_CUBE: case O_ABS: case O_SIGN: case O_RELU: case O_INV:
     case O_ROUND: case O_FLOOR: case O_CEIL: case O_SQRT:
@@ -144,6 +148,8 @@ static T FN(perturb_unary)(int id, T v, int p, int node, int64_t row) {
 }
 static T FN(perturb_binary)(int id, T v, int p, int node, int64_t row) {
   if (!p || id != O_POW) return v;
+  if ((p >> 8) && (p >> 8) != 64 + id) return v;
+  p &= 0xff;
   return v * ((T)1 + (T)FN(psign)(node, row, p) * PERTURB_EPS);
 }
 

@@ -79,6 +79,11 @@ class Oracle:
     def from_options(cls, options):
         return cls(options.operators.unaops, options.operators.binops)
 
+    def perturb_code(self, name, degree):
+        """`perturb` bits that restrict the +-1-ulp conditioning probe to one operator: pass
+        `seed | perturb_code(name, degree)` (de_eval_impl.h: perturb_unary / perturb_binary)."""
+        return int(_ids([name], degree)[0] + (0 if degree == 1 else 64)) << 8
+
     @staticmethod
     def _sfx(dtype):
         return "f32" if np.dtype(dtype) == np.float32 else "f64"

@@ -5,8 +5,8 @@
 // on the fixture points of tests/golden/libm_ulp.json (profiles/r02_libm_ocml.txt), so those three
 // are computed here in double and rounded once, table-driven so the work per value stays close to
 // OCML's: log from a 64-cell table of an offset octave and a degree-4 log1p (within 2^-30 relative
-// before the final rounding: <= 0.5101 ulp), cos / sin from (sin, cos)(k pi/128) and degree-3/2 polynomials on |r| <= pi/256 (within
-// 2^-28 relative before the final rounding: <= 0.5223 ulp over every Float32 |x| < 2^20, checked
+// before the final rounding: <= 0.5101 ulp), cos / sin from (sin, cos)(k pi/128) and degree-4 Taylor terms on |r| <= pi/256 (<= 0.5025
+// ulp over every Float32 |x| < 2^20, checked
 // exhaustively by tools/libm_exhaustive.cpp; profiles/r03_libm_exhaustive.txt).  OCML's Float32 exp
 // measured 0.675 ulp and is kept on the device (sr_expf below, also correctly rounded but for
 // 2^-46-close midpoints, serves the host's constant folding).
@@ -204,12 +204,12 @@ SRL_HD inline double sr_rem_pio2f_fast(float x, int* q) {
 
 // |x| < 2^20: x = n pi/128 + r (Cody-Waite in double), |r| <= pi/256; with (s_k, c_k) =
 // (sin, cos)(k pi/128), k = n mod 256: sin x = s_k cos r + c_k sin r, cos x = c_k cos r - s_k sin r,
-// with cos r = 1 - r^2/2 and sin r = r (1 - r^2/6).  The dropped Taylor terms (r^4/24 <= 2^-30 of c_k,
-// r^5/120 <= 2^-38) stay below 2^-28 of the result wherever it is (|result| >= |c_k| / 2 next to a
-// zero of the function, where c_k = 0 exactly and the result is -s_k sin r itself): <= 0.5 + 2^-4
-// ulp after the final rounding (tools/libm_exhaustive.cpp: every Float32 |x| < 2^20).  Five f64
-// operations after the reduction, the terms in Horner form in r (six as (c_k cos r - s_k sin r) in
-// round 3's first version, eight with the degree-5/4 polynomials of a 128-entry table).
+// with the Taylor terms of cos r and sin r through r^4 (round 5; -DSR_TRIG_DEG3 keeps rounds 3-4's
+// cos r = 1 - r^2/2, sin r = r (1 - r^2/6), whose dropped r^4/24 <= 2^-30 of c_k gave <= 0.5223 ulp).
+// The dropped r^5/120 <= 2^-38 stays far below the result's ulp wherever it is (next to a zero of the
+// function c_k = 0 exactly and the result is -s_k sin r itself): <= 0.5025 ulp after the final
+// rounding (tools/libm_exhaustive.cpp: every Float32 |x| < 2^20).  Seven f64 operations after the
+// reduction, the terms in Horner form in r.
 struct SrTrigArg {
   double r, sk, ck;
 };
@@ -235,8 +235,11 @@ SRL_HD inline float sr_trig_poly(const SrTrigArg& p) {
   // Taylor terms in Horner form, five f64 operations (round 3; was six)
   const double a = COS ? ck : sk, b = COS ? -sk : ck;
   const double c2 = -0.5 * a, c3 = b * -0x1.5555555555555p-3;
-#ifdef SR_TRIG_DEG4
-  // (A/B: one Taylor term more, r^4 a / 24: two f64 operations more per row)
+#ifndef SR_TRIG_DEG3
+  // round 5 default: one Taylor term more, r^4 a / 24 (two f64 operations per row).  Julia's Float32
+  // cos / sin round a Float64 result; against that rounded double this body disagrees on 6,270 (cos)
+  // and 32,478 (sin) of the 2.47e9 Float32 |x| < 2^20, the round-3/4 degree-3 body (-DSR_TRIG_DEG3)
+  // on 1,274,326 and 1,170,066 (profiles/r04_trig_accuracy_ab.txt): parity comes before the 1-3 %
   const double c4 = a * 0x1.5555555555555p-5;
   return float(fma(r, fma(r, fma(r, fma(r, c4, c3), c2), b), a));
 #else

@@ -16,22 +16,20 @@ for p in (ROOT, PKG, os.path.join(ROOT, "oracle")):
 
 
 def _lib_is_current():
-    """libsr_amd.so was built from exactly these sources: the hash its Makefile wrote beside it equals
-    the hash of the sources here (a GPU-box snapshot carries the library but no object files, so make
+    """libsr_amd.so was built from exactly these sources and compile flags: the hash its link rule
+    wrote beside it (untracked, written only next to a library make actually linked) equals
+    `make print-srchash` here (a GPU-box snapshot carries the library but no object files, so make
     alone would rebuild everything)."""
-    import glob
-    import hashlib
-
     stamp = os.path.join(PKG, "lib", "libsr_amd.so.srchash")
     if not (os.path.exists(stamp) and os.path.exists(os.path.join(PKG, "lib", "libsr_amd.so"))):
         return False
-    files = sorted(glob.glob("csrc/*", root_dir=PKG) + ["../include/sr_amd.h", "Makefile"])
-    h = hashlib.sha256()
-    for f in files:
-        with open(os.path.join(PKG, f), "rb") as fh:
-            h.update(fh.read())
+    try:
+        want = subprocess.run(["make", "-s", "--no-print-directory", "-C", PKG, "print-srchash"], check=True,
+                              capture_output=True, text=True).stdout.strip()
+    except (FileNotFoundError, subprocess.CalledProcessError):
+        return False
     with open(stamp) as fh:
-        return fh.read().strip() == h.hexdigest()
+        return bool(want) and fh.read().strip() == want
 
 
 def _ensure_built():
