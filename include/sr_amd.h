@@ -428,8 +428,10 @@ int sr_last_kernel_ms(sr_ctx* ctx, double* eval_ms, double* total_ms);
  * interpreter kernel, out[8] (n >= 9) = the device-busy time of those launches: the UNION of their
  * intervals (launches on the two pipeline streams overlap, so their summed durations can exceed it),
  * out[9] (n >= 10) = the number of trees whose loss fold was computed in row order (the overflow rule of
- * the reference's T-precision fold: csrc/sr_fold.h).  sr_last_kernel_ms's eval_ms is the sum of those
- * launches' durations. */
+ * the reference's T-precision fold: csrc/sr_fold.h), out[10] (n >= 11) = the segments of those folds
+ * folded row by row (the rest advanced by their composed steps), out[11] (n >= 12) = the fold's
+ * segment length in rows (0: one scan over every row).  sr_last_kernel_ms's eval_ms is the sum of
+ * those launches' durations. */
 int sr_last_phase_ms(sr_ctx* ctx, double* out, int n);
 
 /* Run-time tuning of a context (the SR_AMD_* environment variables are read once at sr_init):
@@ -444,7 +446,8 @@ int sr_last_phase_ms(sr_ctx* ctx, double* out, int n);
  * "fused_reduce" (the largest tree group, in trees x row blocks, whose partials the interpreter launch
  * reduces itself — its last workgroup per group; 0: always a separate reduce launch), "exact_w" (4 / 1:
  * waves per workgroup of the exact-sum pass), "exact_g" (listed trees per exact-sum workgroup; 0: the
- * heuristic).  Results do
+ * heuristic), "fold_seg" (rows per segment of the in-order loss fold: -1 automatic, 0 one workgroup
+ * scan over every row per tree, as rounds 3-4).  Results do
  * not depend on any knob.  SR_ERR_INVALID_ARG for an unknown name.  sr_tuning_info (optional outputs)
  * reports how many derived columns the last sr_eval_loss_batch used and how many of its trees went
  * through the exact-sum pass (flagged BIG). */

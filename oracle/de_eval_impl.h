@@ -450,12 +450,16 @@ int FN(oracle_eval_loss)(int64_t n_nodes, const uint8_t* degree, const uint8_t* 
     return 1;
   }
   if (accum == 0) {
-    T s = (T)0, ws = (T)0;
+    /* LossFunctions 0.11: mean(loss, x, y) = the left fold of the losses / n; the weighted
+     * sum(loss, x, y, w; normalize=true) = the left fold of w_i * l_i / sum(w), where sum(w) is Base's
+     * pairwise sum of the weight vector in T (jl_sum_range; ADVICE r4: not a sequential fold) */
+    T s = (T)0;
     for (int64_t j = 0; j < n; ++j) {
       T l = FN(elem_loss)(loss_kind, loss_param, pred[j], y[j]);
-      if (w) { l = w[j] * l; ws = ws + w[j]; }
-      s = s + l;
+      if (w) l = w[j] * l;
+      s = j == 0 ? l : s + l;
     }
+    const T ws = (w && n > 0) ? FN(jl_sum_range)(w, 0, n - 1) : (T)0;
     *loss = w ? s / ws : s / (T)n;
   } else {
     /* the value from an f64 accumulation (the device's arithmetic), the overflow verdict from the

@@ -127,14 +127,26 @@ template hipError_t sr_launch_finalize_packed<double>(const double*, int, double
 // ---------------------------------------------------------------- the reference's loss fold, exactly
 // LossFunctions' mean / weighted sum fold the elementwise losses left to right in T
 // (src/LossFunctions.jl:38-58; sr_fold.h).  For the rare trees whose overflow the bounds of sr_fold.h
-// cannot decide, this kernel computes that fold bit for bit, in parallel: while the running value p
-// stays in one binade [2^e, 2^(e+1)), fl(p + l) = p + ulp * (m + r), where l / ulp = m + f (m integer)
-// and r rounds f half-to-even against the parity of p / ulp + m — so a step is a function of the
-// parity of the running value only, and chunks of steps compose (a scan over pairs: the increment from
-// an even and from an odd start).  The first step that would leave the binade is done with the
-// hardware add itself and the scan restarts there (p only grows: at most ~280 binades for Float32).
-// One workgroup per listed tree; pred[b][n] its predictions over the view; carry[b] (or NULL) the
-// value of the fold over the rows before this shard; out[b] = the fold (+Inf when it overflows).
+// cannot decide, these kernels compute that fold bit for bit.  While the running value p stays in one
+// binade [2^e, 2^(e+1)) with spacing 2^q, fl(p + l) = p + 2^q (m + r), where l / 2^q = m + f (m integer)
+// and r rounds f half-to-even against the parity of p / 2^q + m — so a step depends on the running
+// value only through its parity, and runs of steps compose (a pair: the ulps added from an even and
+// from an odd start; compose(x, y)(b) = x(b) + y((b + x(b)) & 1)).  The step that leaves the binade is
+// the hardware add itself.
+//
+// Round 5: the whole GPU folds, not one workgroup per tree.  The rows are cut into segments of
+// seg_len rows and three launches run:
+//   segsum  (one workgroup per tree and segment) the f64 sum of each segment's losses;
+//   segtab  (the same grid) the composed step of each segment for the binades holding the fold's value
+//           at the segment start if that value is within 2^-7 of the f64 prefix sum before it (<= 2
+//           binades; the fold's real relative error over 64M rows is ~1e-4);
+//   chain   (one workgroup per tree) walks the segments in order: a segment whose table covers the
+//           running value's binade and that ends inside it advances in O(1); any other segment (the
+//           first, those where the fold crosses a binade, a value outside the speculated window) is
+//           folded exactly by the workgroup scan of rounds 3-4 (fold_range).
+// Every O(1) advance is an exact composition of the segment's steps, so the result does not depend on
+// the segmentation (seg_len = 0: the whole view through fold_range, rounds 3-4's kernel;
+// tests/test_gpu_fold.py compares both bit for bit).
 template <typename T>
 struct SrFoldStep {
   int64_t m;
@@ -156,7 +168,7 @@ template <typename T>
 __device__ __forceinline__ int64_t sr_fold_inc(const SrFoldStep<T>& st, int64_t b) {
   return st.m + (st.kind == 2 ? 1 : (st.kind == 1 ? ((b + st.m) & 1) : 0));
 }
-// (a0, a1): ulps added from an even / odd start; compose(x, y)(b) = x(b) + y((b + x(b)) & 1)
+// (a0, a1): ulps added from an even / odd start; y := x then y (saturating at cap)
 __device__ __forceinline__ void sr_fold_compose(int64_t x0, int64_t x1, int64_t& y0, int64_t& y1, int64_t cap) {
   const int64_t n0 = x0 + ((x0 & 1) ? y1 : y0);
   const int64_t n1 = x1 + (((1 + x1) & 1) ? y1 : y0);
@@ -164,42 +176,157 @@ __device__ __forceinline__ void sr_fold_compose(int64_t x0, int64_t x1, int64_t&
   y1 = n1 < cap ? n1 : cap;
 }
 
+template <typename T>
+struct SrFoldRows {  // the listed tree's elementwise losses (the interpreter's product, in the same order)
+  const T* pr;
+  const T* y;
+  const T* w;
+  const int64_t* row_idx;
+  int lk;
+  T lp;
+  __device__ __forceinline__ T operator()(int64_t i) const {
+    const int64_t ri = row_idx ? row_idx[i] : i;
+    T e = sr_elem_loss<T>(lk, pr[i], y[ri], lp);
+    if (w) e *= w[ri];
+    return e;
+  }
+};
+
+// binade spacing exponent q of a value >= 0 (subnormals and 0: the fixed subnormal spacing); values
+// past the type's range get a q no finite running value has
+template <typename T>
+__device__ __forceinline__ int sr_fold_q(double x) {
+  using Tr = SrFoldTraits<T>;
+  constexpr double MIN_NORMAL = sizeof(T) == 4 ? 1.17549435e-38 : 2.2250738585072014e-308;
+  if (!(x >= MIN_NORMAL)) return Tr::qmin;
+  if (!(x <= double(SrM<T>::big))) return 1 << 20;
+  int ex;
+  (void)frexp(x, &ex);
+  return ex - 1 - Tr::mant;
+}
+
+template <typename T>
+__global__ void __launch_bounds__(256) sr_fold_segsum_kernel(SrFoldRows<T> rows, int64_t pred_ld, int64_t n,
+                                                             int64_t seg_len, int n_seg, double* __restrict__ segsum) {
+  const int seg = int(blockIdx.x), b = int(blockIdx.y), tid = int(threadIdx.x);
+  SrFoldRows<T> rw = rows;
+  rw.pr = rows.pr + int64_t(b) * pred_ld;
+  const int64_t lo = int64_t(seg) * seg_len, hi = lo + seg_len < n ? lo + seg_len : n;
+  double acc = 0.0;
+  for (int64_t i = lo + tid; i < hi; i += 256) acc += double(rw(i));
+  __shared__ double s_w[4];
+  for (int off = 32; off >= 1; off >>= 1) acc += __shfl_xor(acc, off, 64);
+  if ((tid & 63) == 0) s_w[tid >> 6] = acc;
+  __syncthreads();
+  if (tid == 0) segsum[int64_t(b) * n_seg + seg] = (s_w[0] + s_w[1]) + (s_w[2] + s_w[3]);
+}
+
+// composed steps of one segment for binades qa and qb: tab[b][seg] = {a0(qa), a1(qa), a0(qb), a1(qb)}
 template <typename T, int R>
-__global__ void __launch_bounds__(1024) sr_fold_kernel(const T* __restrict__ pred, int64_t pred_ld,
-                                                       const T* __restrict__ y, const T* __restrict__ w,
-                                                       const int64_t* __restrict__ row_idx, int64_t n, int lk, T lp,
-                                                       const T* __restrict__ carry, T* __restrict__ out) {
+__global__ void __launch_bounds__(256) sr_fold_segtab_kernel(SrFoldRows<T> rows, int64_t pred_ld, int64_t n,
+                                                             int64_t seg_len, int n_seg,
+                                                             const double* __restrict__ segsum,
+                                                             const double* __restrict__ carry_est,
+                                                             int2* __restrict__ tq, int64_t* __restrict__ tab) {
+  using Tr = SrFoldTraits<T>;
+  constexpr int64_t CAP = int64_t(1) << (Tr::mant + 3);
+  const int seg = int(blockIdx.x), b = int(blockIdx.y), tid = int(threadIdx.x), lane = tid & 63, wave = tid >> 6;
+  SrFoldRows<T> rw = rows;
+  rw.pr = rows.pr + int64_t(b) * pred_ld;
+  __shared__ double s_d[4];
+  __shared__ int64_t s_v[4][4];
+  // the f64 prefix before this segment (any order: it only chooses the binades to tabulate)
+  const double* ss = segsum + int64_t(b) * n_seg;
+  double pre = 0.0;
+  for (int j = tid; j < seg; j += 256) pre += ss[j];
+  for (int off = 32; off >= 1; off >>= 1) pre += __shfl_xor(pre, off, 64);
+  if (lane == 0) s_d[wave] = pre;
+  __syncthreads();
+  const double S = (carry_est ? carry_est[b] : 0.0) + ((s_d[0] + s_d[1]) + (s_d[2] + s_d[3]));
+  const int qa = sr_fold_q<T>(S * (1.0 - 0x1p-7)), qb = sr_fold_q<T>(S * (1.0 + 0x1p-7));
+  const int64_t lo = int64_t(seg) * seg_len, hi = lo + seg_len < n ? lo + seg_len : n;
+  int64_t ta0 = 0, ta1 = 0, tb0 = 0, tb1 = 0;  // the segment so far (meaningful in thread 0)
+  for (int64_t base = lo; base < hi; base += 256 * R) {
+    int64_t a0 = 0, a1 = 0, c0 = 0, c1 = 0;  // this thread's R consecutive rows, binades qa and qb
+    const int64_t r0 = base + int64_t(tid) * R;
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+      const T e = (r0 + r < hi) ? rw(r0 + r) : T(0);  // (a zero loss adds nothing)
+      const SrFoldStep<T> sa = sr_fold_step<T>(e, qa, CAP);
+      int64_t e0 = sr_fold_inc<T>(sa, a0 & 1), e1 = sr_fold_inc<T>(sa, (1 + a1) & 1);
+      a0 = a0 + e0 < CAP ? a0 + e0 : CAP;
+      a1 = a1 + e1 < CAP ? a1 + e1 : CAP;
+      if (qb != qa) {
+        const SrFoldStep<T> sb = sr_fold_step<T>(e, qb, CAP);
+        e0 = sr_fold_inc<T>(sb, c0 & 1);
+        e1 = sr_fold_inc<T>(sb, (1 + c1) & 1);
+        c0 = c0 + e0 < CAP ? c0 + e0 : CAP;
+        c1 = c1 + e1 < CAP ? c1 + e1 : CAP;
+      }
+    }
+    // ordered reduction over the wave's lanes (lane l's rows precede lane l + 1's), then the waves
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+      int64_t o0 = __shfl_down(a0, off, 64), o1 = __shfl_down(a1, off, 64);
+      int64_t p0 = __shfl_down(c0, off, 64), p1 = __shfl_down(c1, off, 64);
+      if ((lane & (2 * off - 1)) == 0) {
+        sr_fold_compose(a0, a1, o0, o1, CAP);
+        a0 = o0;
+        a1 = o1;
+        sr_fold_compose(c0, c1, p0, p1, CAP);
+        c0 = p0;
+        c1 = p1;
+      }
+    }
+    if (lane == 0) {
+      s_v[wave][0] = a0;
+      s_v[wave][1] = a1;
+      s_v[wave][2] = c0;
+      s_v[wave][3] = c1;
+    }
+    __syncthreads();
+    if (tid == 0) {
+      for (int v = 0; v < 4; ++v) {
+        int64_t y0 = s_v[v][0], y1 = s_v[v][1];
+        sr_fold_compose(ta0, ta1, y0, y1, CAP);
+        ta0 = y0;
+        ta1 = y1;
+        y0 = s_v[v][2];
+        y1 = s_v[v][3];
+        sr_fold_compose(tb0, tb1, y0, y1, CAP);
+        tb0 = y0;
+        tb1 = y1;
+      }
+    }
+    __syncthreads();
+  }
+  if (tid == 0) {
+    const int64_t o = int64_t(b) * n_seg + seg;
+    tq[o] = make_int2(qa, qb);
+    tab[4 * o + 0] = ta0;
+    tab[4 * o + 1] = ta1;
+    tab[4 * o + 2] = qb != qa ? tb0 : ta0;
+    tab[4 * o + 3] = qb != qa ? tb1 : ta1;
+  }
+}
+
+// The workgroup scan of rounds 3-4 over rows [s_k, hi) from the running value s_p (every thread
+// calls it; the state lives in LDS): CHUNK rows per round, restarting at each binade crossing.
+template <typename T, int R>
+__device__ void sr_fold_range(const SrFoldRows<T>& elem, int64_t hi, T* s_p, int64_t* s_k, int64_t* s_w0,
+                              int64_t* s_w1) {
   using Tr = SrFoldTraits<T>;
   constexpr int NT = 1024;
   constexpr int64_t CHUNK = int64_t(NT) * R;
   constexpr int64_t CAP = int64_t(1) << (Tr::mant + 3);
   constexpr T MIN_NORMAL = sizeof(T) == 4 ? T(1.17549435e-38f) : T(2.2250738585072014e-308);
-  __shared__ T s_p;
-  __shared__ int64_t s_k;
-  __shared__ int64_t s_w0[NT / 64], s_w1[NT / 64];
   const int tid = int(threadIdx.x), lane = tid & 63, wave = tid >> 6;
-  const T* pr = pred + int64_t(blockIdx.x) * pred_ld;
-  auto elem = [&](int64_t i) -> T {
-    const int64_t ri = row_idx ? row_idx[i] : i;
-    T e = sr_elem_loss<T>(lk, pr[i], y[ri], lp);
-    if (w) e *= w[ri];  // (the interpreter's product, in the same order)
-    return e;
-  };
-  if (tid == 0) {
-    if (carry) {
-      s_p = carry[blockIdx.x];
-      s_k = 0;
-    } else {  // Statistics.mean / Base.sum over a generator: the first loss starts the fold
-      s_p = n > 0 ? elem(0) : T(0);
-      s_k = 1;
-    }
-  }
   for (;;) {
     __syncthreads();
-    const T p = s_p;
-    const int64_t k = s_k;
+    const T p = *s_p;
+    const int64_t k = *s_k;
     __syncthreads();  // every thread has read the state before thread 0 may write it again
-    if (k >= n || !(p <= SrM<T>::big)) break;  // done, or +Inf / NaN (a fold that stays so)
+    if (k >= hi || !(p <= SrM<T>::big)) break;  // done, or +Inf / NaN (a fold that stays so)
     // p = P 2^q, P < lim: the binade's spacing (subnormals: the fixed spacing up to the first normal)
     int q;
     int64_t lim;
@@ -219,7 +346,7 @@ __global__ void __launch_bounds__(1024) sr_fold_kernel(const T* __restrict__ pre
     int64_t a0 = 0, a1 = 0;
 #pragma unroll
     for (int r = 0; r < R; ++r) {
-      ev[r] = (base + r < n) ? elem(base + r) : T(0);  // (a zero loss adds nothing)
+      ev[r] = (base + r < hi) ? elem(base + r) : T(0);  // (a zero loss adds nothing)
       const SrFoldStep<T> st = sr_fold_step<T>(ev[r], q, CAP);
       int64_t e0 = sr_fold_inc<T>(st, (0 + a0) & 1), e1 = sr_fold_inc<T>(st, (1 + a1) & 1);
       a0 = a0 + e0 < CAP ? a0 + e0 : CAP;
@@ -255,8 +382,8 @@ __global__ void __launch_bounds__(1024) sr_fold_kernel(const T* __restrict__ pre
     const int64_t tot = b0 ? t1 : t0;
     if (P + tot < lim) {  // the whole chunk stays in this binade
       if (tid == 0) {
-        s_p = T(ldexp(double(P + tot), q));
-        s_k = k + CHUNK < n ? k + CHUNK : n;
+        *s_p = T(ldexp(double(P + tot), q));
+        *s_k = k + CHUNK < hi ? k + CHUNK : hi;
       }
       continue;
     }
@@ -273,32 +400,162 @@ __global__ void __launch_bounds__(1024) sr_fold_kernel(const T* __restrict__ pre
       int64_t run = pre;
 #pragma unroll
       for (int r = 0; r < R; ++r) {
-        if (base + r >= n) break;
+        if (base + r >= hi) break;
         const int64_t d = sr_fold_inc<T>(sr_fold_step<T>(ev[r], q, CAP), run & 1);
         if (run + d >= lim) {
-          s_p = T(ldexp(double(run), q)) + ev[r];  // the hardware's own rounding of this step
-          s_k = base + r + 1;
+          *s_p = T(ldexp(double(run), q)) + ev[r];  // the hardware's own rounding of this step
+          *s_k = base + r + 1;
           break;
         }
         run += d;
       }
     }
   }
-  if (tid == 0) out[blockIdx.x] = s_p;
+}
+
+template <typename T, int R>
+__global__ void __launch_bounds__(1024) sr_fold_chain_kernel(SrFoldRows<T> rows, int64_t pred_ld, int64_t n,
+                                                             int64_t seg_len, int n_seg, const int2* __restrict__ tq,
+                                                             const int64_t* __restrict__ tab,
+                                                             const T* __restrict__ carry, T* __restrict__ out,
+                                                             int* __restrict__ n_slow) {
+  using Tr = SrFoldTraits<T>;
+  constexpr int SB = 512;  // segments per LDS batch of tables
+  constexpr T MIN_NORMAL = sizeof(T) == 4 ? T(1.17549435e-38f) : T(2.2250738585072014e-308);
+  __shared__ T s_p;
+  __shared__ int64_t s_k, s_seg;
+  __shared__ int64_t s_w0[16], s_w1[16];
+  __shared__ int2 s_tq[SB];
+  __shared__ int64_t s_tab[SB * 4];
+  const int b = int(blockIdx.x), tid = int(threadIdx.x);
+  SrFoldRows<T> rw = rows;
+  rw.pr = rows.pr + int64_t(b) * pred_ld;
+  if (tid == 0) {
+    if (carry) {
+      s_p = carry[b];
+      s_k = 0;
+    } else {  // Statistics.mean / Base.sum over a generator: the first loss starts the fold
+      s_p = n > 0 ? rw(0) : T(0);
+      s_k = n > 0 ? 1 : 0;
+    }
+  }
+  int slow = 0;
+  if (seg_len <= 0) {
+    sr_fold_range<T, R>(rw, n, &s_p, &s_k, s_w0, s_w1);
+  } else {
+    for (int64_t sb = 0; sb < n_seg; sb += SB) {
+      const int nb = int(n_seg - sb < SB ? n_seg - sb : SB);
+      __syncthreads();  // (thread 0 is done with the previous batch's tables)
+      for (int i = tid; i < nb; i += 1024) s_tq[i] = tq[int64_t(b) * n_seg + sb + i];
+      for (int i = tid; i < 4 * nb; i += 1024) s_tab[i] = tab[4 * (int64_t(b) * n_seg + sb) + i];
+      __syncthreads();
+      int64_t s = sb;
+      bool stop = false;
+      while (s < sb + nb) {
+        if (tid == 0) {  // O(1) advances through the segments the tables cover
+          T p = s_p;
+          int64_t k = s_k, sg = s;
+          for (; sg < sb + nb; ++sg) {
+            if (!(p <= SrM<T>::big)) break;
+            const int64_t lo = sg * seg_len, hi = lo + seg_len < n ? lo + seg_len : n;
+            if (k != lo) break;  // (the first segment without a carry starts at row 1)
+            int q;
+            int64_t lim;
+            if (p < MIN_NORMAL) {
+              q = Tr::qmin;
+              lim = int64_t(1) << Tr::mant;
+            } else {
+              int ex;
+              (void)frexp(double(p), &ex);
+              q = ex - 1 - Tr::mant;
+              lim = int64_t(1) << (Tr::mant + 1);
+            }
+            const int2 qq = s_tq[sg - sb];
+            const int j = q == qq.x ? 0 : (q == qq.y ? 2 : -1);
+            if (j < 0) break;
+            const int64_t P = int64_t(ldexp(double(p), -q));
+            const int64_t g = s_tab[4 * (sg - sb) + j + int(P & 1)];
+            if (P + g >= lim) break;  // the fold crosses a binade inside this segment
+            p = T(ldexp(double(P + g), q));
+            k = hi;
+          }
+          s_p = p;
+          s_k = k;
+          s_seg = sg;
+        }
+        __syncthreads();
+        const int64_t sg = s_seg;
+        const T p = s_p;
+        __syncthreads();
+        if (!(p <= SrM<T>::big)) {
+          stop = true;
+          break;
+        }
+        if (sg >= sb + nb) break;
+        const int64_t hi = sg * seg_len + seg_len < n ? sg * seg_len + seg_len : n;
+        sr_fold_range<T, R>(rw, hi, &s_p, &s_k, s_w0, s_w1);  // this segment, exactly
+        ++slow;
+        s = sg + 1;
+      }
+      if (stop) break;
+    }
+  }
+  __syncthreads();
+  if (tid == 0) {
+    out[b] = s_p;
+    if (n_slow) n_slow[b] = slow;
+  }
 }
 
 template <typename T>
-hipError_t sr_launch_fold(const T* pred, int64_t pred_ld, int n_trees, const T* y, const T* w, const int64_t* row_idx,
-                          int64_t n, int loss_kind, T loss_param, const T* carry, T* out, hipStream_t s) {
-  if (n_trees <= 0) return hipSuccess;
-  hipLaunchKernelGGL((sr_fold_kernel<T, 8>), dim3(unsigned(n_trees)), dim3(1024), 0, s, pred, pred_ld, y, w, row_idx, n,
-                     loss_kind, loss_param, carry, out);
+hipError_t sr_launch_fold_segsum(const T* pred, int64_t pred_ld, int n_trees, const T* y, const T* w,
+                                 const int64_t* row_idx, int64_t n, int loss_kind, T loss_param, int64_t seg_len,
+                                 double* segsum, hipStream_t s) {
+  if (n_trees <= 0 || seg_len <= 0 || n <= 0) return hipSuccess;
+  const int n_seg = int((n + seg_len - 1) / seg_len);
+  const SrFoldRows<T> rows{pred, y, w, row_idx, loss_kind, loss_param};
+  hipLaunchKernelGGL(sr_fold_segsum_kernel<T>, dim3(unsigned(n_seg), unsigned(n_trees)), dim3(256), 0, s, rows, pred_ld,
+                     n, seg_len, n_seg, segsum);
   return hipGetLastError();
 }
+template <typename T>
+hipError_t sr_launch_fold_segtab(const T* pred, int64_t pred_ld, int n_trees, const T* y, const T* w,
+                                 const int64_t* row_idx, int64_t n, int loss_kind, T loss_param, int64_t seg_len,
+                                 const double* segsum, const double* carry_est, int2* tq, int64_t* tab, hipStream_t s) {
+  if (n_trees <= 0 || seg_len <= 0 || n <= 0) return hipSuccess;
+  const int n_seg = int((n + seg_len - 1) / seg_len);
+  const SrFoldRows<T> rows{pred, y, w, row_idx, loss_kind, loss_param};
+  hipLaunchKernelGGL((sr_fold_segtab_kernel<T, 16>), dim3(unsigned(n_seg), unsigned(n_trees)), dim3(256), 0, s, rows,
+                     pred_ld, n, seg_len, n_seg, segsum, carry_est, tq, tab);
+  return hipGetLastError();
+}
+template <typename T>
+hipError_t sr_launch_fold(const T* pred, int64_t pred_ld, int n_trees, const T* y, const T* w, const int64_t* row_idx,
+                          int64_t n, int loss_kind, T loss_param, int64_t seg_len, const int2* tq, const int64_t* tab,
+                          const T* carry, T* out, int* n_slow, hipStream_t s) {
+  if (n_trees <= 0) return hipSuccess;
+  const int n_seg = seg_len > 0 ? int((n + seg_len - 1) / seg_len) : 0;
+  const SrFoldRows<T> rows{pred, y, w, row_idx, loss_kind, loss_param};
+  hipLaunchKernelGGL((sr_fold_chain_kernel<T, 8>), dim3(unsigned(n_trees)), dim3(1024), 0, s, rows, pred_ld, n,
+                     seg_len, n_seg, tq, tab, carry, out, n_slow);
+  return hipGetLastError();
+}
+template hipError_t sr_launch_fold_segsum<float>(const float*, int64_t, int, const float*, const float*, const int64_t*,
+                                                 int64_t, int, float, int64_t, double*, hipStream_t);
+template hipError_t sr_launch_fold_segsum<double>(const double*, int64_t, int, const double*, const double*,
+                                                  const int64_t*, int64_t, int, double, int64_t, double*, hipStream_t);
+template hipError_t sr_launch_fold_segtab<float>(const float*, int64_t, int, const float*, const float*, const int64_t*,
+                                                 int64_t, int, float, int64_t, const double*, const double*, int2*,
+                                                 int64_t*, hipStream_t);
+template hipError_t sr_launch_fold_segtab<double>(const double*, int64_t, int, const double*, const double*,
+                                                  const int64_t*, int64_t, int, double, int64_t, const double*,
+                                                  const double*, int2*, int64_t*, hipStream_t);
 template hipError_t sr_launch_fold<float>(const float*, int64_t, int, const float*, const float*, const int64_t*, int64_t,
-                                          int, float, const float*, float*, hipStream_t);
+                                          int, float, int64_t, const int2*, const int64_t*, const float*, float*, int*,
+                                          hipStream_t);
 template hipError_t sr_launch_fold<double>(const double*, int64_t, int, const double*, const double*, const int64_t*,
-                                           int64_t, int, double, const double*, double*, hipStream_t);
+                                           int64_t, int, double, int64_t, const int2*, const int64_t*, const double*,
+                                           double*, int*, hipStream_t);
 
 // Julia [nf, n] column-major -> per-feature rows [nf][ld]; padded rows replicate row 0 so that the
 // interpreter's validity checks never see a value that is not in the dataset.

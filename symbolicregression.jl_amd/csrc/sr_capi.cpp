@@ -150,6 +150,9 @@ struct sr_ctx {
   int n_derived_last = 0;
   int64_t n_exact_last = 0;  // trees of the last eval_loss call sent through the exact-sum pass
   int64_t n_fold_last = 0;   // trees of the last eval_loss call whose loss fold was computed in order (sr_fold.h)
+  int64_t fold_slow_last = 0;  // ... their segments folded row by row (the rest: composed steps)
+  int64_t fold_seg_last = 0;   // ... and the segment length used
+  int64_t fold_seg = -1;       // SR_AMD_FOLD_SEG / sr_set_tuning "fold_seg": -1 automatic, 0 one scan per tree
   double exact_kernel_ms = 0.0;  // device time of that pass (its interpreter + combine launches)
   // programs + per-tree metadata of the last run_batch: ONE device allocation and ONE pinned staging
   // buffer with the same layout (code | offsets | static_bad | launch order), so a single-chunk call
@@ -1373,67 +1376,175 @@ struct SubBatch {
   }
 };
 
-// The reference's fold of the listed trees' losses over this view (or shard), exactly and in row order
-// (sr_fold_kernel): their predictions from the PRED interpreter (the values the LOSS kernels saw), then
-// one workgroup per tree.  carry (host, may be NULL): per listed tree the fold over the rows before this
-// shard.  out: the folds (T; +Inf where the fold overflows).  Runs after the call's other passes (it
-// reuses the context's program buffers).
+// Rows per segment of the fold's segmented chain (sr_aux.hip): ctx->fold_seg < 0 chooses (<= 1024
+// segments of 8k-64k rows), 0 folds the whole view with one workgroup scan per tree (rounds 3-4).
+inline int64_t fold_seg_len(const sr_ctx* ctx, int64_t n) {
+  if (ctx->fold_seg >= 0) return ctx->fold_seg;
+  const int64_t L = ((n / 512 + 8191) / 8192) * 8192;
+  return std::min<int64_t>(std::max<int64_t>(L, 8192), 65536);
+}
+
+// Device scratch of one fold batch of nb trees and n_seg segments (ctx->fold_io): segment sums,
+// binades and composed steps, carries, estimates, results and slow-segment counts.
 template <typename T>
-int fold_exact(sr_ctx* ctx, const sr_dataset* ds, int opset_id, const sr_tree_batch* trees, const int64_t* row_idx,
-               int64_t n_idx, int64_t n_total, int loss_kind, const std::vector<int64_t>& list, const T* carry,
-               std::vector<T>* out) {
-  out->assign(list.size(), T(0));
-  if (list.empty()) return SR_OK;
+struct FoldDev {
+  double* segsum = nullptr;
+  int2* tq = nullptr;
+  int64_t* tab = nullptr;
+  double* carry_est = nullptr;
+  T* carry = nullptr;
+  T* out = nullptr;
+  int* slow = nullptr;
+  static size_t al(size_t b) { return (b + 255) & ~size_t(255); }
+  static size_t bytes(size_t nb, int64_t n_seg) {
+    const size_t ns = nb * size_t(n_seg > 0 ? n_seg : 1);
+    return al(ns * 8) + al(ns * 8) + al(ns * 32) + al(nb * 8) + 2 * al(nb * sizeof(T)) + al(nb * 4);
+  }
+  void bind(void* base, size_t nb, int64_t n_seg) {
+    const size_t ns = nb * size_t(n_seg > 0 ? n_seg : 1);
+    char* c = static_cast<char*>(base);
+    segsum = reinterpret_cast<double*>(c);
+    c += al(ns * 8);
+    tq = reinterpret_cast<int2*>(c);
+    c += al(ns * 8);
+    tab = reinterpret_cast<int64_t*>(c);
+    c += al(ns * 32);
+    carry_est = reinterpret_cast<double*>(c);
+    c += al(nb * 8);
+    carry = reinterpret_cast<T*>(c);
+    c += al(nb * sizeof(T));
+    out = reinterpret_cast<T*>(c);
+    c += al(nb * sizeof(T));
+    slow = reinterpret_cast<int*>(c);
+  }
+};
+
+// The fold's PRED passes are internal: the call's interpreter timing (its chunk events) and the kernel
+// it reports (rows per lane, derived columns) stay those of the call's own loss launches.
+struct KeepCallInfo {
+  sr_ctx* c;
+  int timing, n_chunks, n_derived, rows;
+  bool timed, derived;
+  explicit KeepCallInfo(sr_ctx* x)
+      : c(x), timing(x->timing), n_chunks(x->n_chunks_last), n_derived(x->n_derived_last), rows(x->rows_last),
+        timed(x->timed_last), derived(x->derived_last) {
+    x->timing = 0;
+  }
+  ~KeepCallInfo() {
+    c->timing = timing;
+    c->n_chunks_last = n_chunks;
+    c->n_derived_last = n_derived;
+    c->rows_last = rows;
+    c->timed_last = timed;
+    c->derived_last = derived;
+  }
+};
+
+// Trees per PRED pass of the fold: predictions of at most `budget` bytes (and half the free device
+// memory when `use_free`; the row-sharded call uses a fixed budget so that every rank cuts the list
+// alike).
+inline int64_t fold_batch_trees(int64_t n_eval, size_t elem, bool use_free) {
+  size_t budget = size_t(8) << 30, free_b = 0, total_b = 0;
+  if (use_free && hipMemGetInfo(&free_b, &total_b) == hipSuccess) budget = std::min(budget, free_b / 2);
+  return std::max<int64_t>(1, int64_t(budget / (size_t(std::max<int64_t>(n_eval, 1)) * elem)));
+}
+
+// One batch of listed trees, first half: the PRED interpreter over this view (or shard) into ctx->pred,
+// the device scratch bound, and (segmented) the segment sums.
+template <typename T>
+int fold_prepare(sr_ctx* ctx, const sr_dataset* ds, int opset_id, const sr_tree_batch* trees, const int64_t* row_idx,
+                 int64_t n_idx, int64_t n_total, int loss_kind, const int64_t* list, size_t nb, int64_t seg_len,
+                 FoldDev<T>* fd) {
+  int lkind = 0;
+  double lparam = 0.0;
+  if (decode_loss(ctx, loss_kind, &lkind, &lparam) != SR_OK) return SR_ERR_INVALID_ARG;
+  const bool gather = row_idx != nullptr && n_idx > 0;
+  const int64_t n_eval = gather ? n_idx : ds->n;
+  SubBatch<T> sub(*trees, list, nb);
+  SrProgramBatch<T> prog;
+  Grid g;
+  int rc = run_batch<T>(ctx, ds, opset_id, &sub.b, row_idx, n_idx, n_total, loss_kind, SR_MODE_PRED, &prog, &g);
+  if (rc != SR_OK) return rc;
+  const int64_t n_seg = seg_len > 0 ? (n_eval + seg_len - 1) / seg_len : 0;
+  SR_HIP_CHECK(ctx->fold_io.ensure(FoldDev<T>::bytes(nb, n_seg)));
+  fd->bind(ctx->fold_io.p, nb, n_seg);
+  if (seg_len > 0)
+    SR_HIP_CHECK(sr_launch_fold_segsum<T>(ctx->pred.as<T>(), n_eval, int(nb), static_cast<const T*>(ds->y),
+                                          static_cast<const T*>(ds->w), gather ? ctx->row_idx.as<int64_t>() : nullptr,
+                                          n_eval, lkind, T(lparam), seg_len, fd->segsum, ctx->stream));
+  return SR_OK;
+}
+
+// Second half: the segments' composed steps (carry_est: device, per tree, or NULL) and the chain
+// (carry: device, per tree, or NULL); the folds into out (host) after one synchronisation.
+template <typename T>
+int fold_finish(sr_ctx* ctx, const sr_dataset* ds, const int64_t* row_idx, int64_t n_idx, int loss_kind, size_t nb,
+                int64_t seg_len, const FoldDev<T>& fd, bool with_carry_est, bool with_carry, T* out) {
   int lkind = 0;
   double lparam = 0.0;
   if (decode_loss(ctx, loss_kind, &lkind, &lparam) != SR_OK) return SR_ERR_INVALID_ARG;
   const bool gather = row_idx != nullptr && n_idx > 0;
   const int64_t n_eval = gather ? n_idx : ds->n;
   hipStream_t s = ctx->stream;
-  // the fold's PRED passes are internal: the call's interpreter timing (its chunk events) and the
-  // kernel it reports (rows per lane, derived columns) stay those of the call's own loss launches
-  struct Keep {
-    sr_ctx* c;
-    int timing, n_chunks, n_derived, rows;
-    bool timed, derived;
-    explicit Keep(sr_ctx* x)
-        : c(x), timing(x->timing), n_chunks(x->n_chunks_last), n_derived(x->n_derived_last), rows(x->rows_last),
-          timed(x->timed_last), derived(x->derived_last) {
-      x->timing = 0;
-    }
-    ~Keep() {
-      c->timing = timing;
-      c->n_chunks_last = n_chunks;
-      c->n_derived_last = n_derived;
-      c->rows_last = rows;
-      c->timed_last = timed;
-      c->derived_last = derived;
-    }
-  } keep(ctx);
-  // predictions of at most 16 GiB per pass (and half the free device memory): the fold kernel runs one
-  // workgroup per listed tree, so a pass should hold many trees (C4: 64 trees of 2^26 rows per pass)
-  size_t budget = size_t(16) << 30, free_b = 0, total_b = 0;
-  if (hipMemGetInfo(&free_b, &total_b) == hipSuccess) budget = std::min(budget, free_b / 2);
-  const int64_t per = std::max<int64_t>(1, int64_t(budget / (size_t(n_eval) * sizeof(T))));
+  const T* y = static_cast<const T*>(ds->y);
+  const T* w = static_cast<const T*>(ds->w);
+  const int64_t* ri = gather ? ctx->row_idx.as<int64_t>() : nullptr;
+  if (seg_len > 0)
+    SR_HIP_CHECK(sr_launch_fold_segtab<T>(ctx->pred.as<T>(), n_eval, int(nb), y, w, ri, n_eval, lkind, T(lparam),
+                                          seg_len, fd.segsum, with_carry_est ? fd.carry_est : nullptr, fd.tq, fd.tab, s));
+  SR_HIP_CHECK(sr_launch_fold<T>(ctx->pred.as<T>(), n_eval, int(nb), y, w, ri, n_eval, lkind, T(lparam), seg_len, fd.tq,
+                                 fd.tab, with_carry ? fd.carry : nullptr, fd.out, fd.slow, s));
+  std::vector<int> slow(nb, 0);
+  SR_HIP_CHECK(hipMemcpyAsync(out, fd.out, nb * sizeof(T), hipMemcpyDeviceToHost, s));
+  SR_HIP_CHECK(hipMemcpyAsync(slow.data(), fd.slow, nb * sizeof(int), hipMemcpyDeviceToHost, s));
+  SR_HIP_CHECK(hipStreamSynchronize(s));
+  for (int v : slow) ctx->fold_slow_last += v;
+  ctx->fold_seg_last = seg_len;
+  return SR_OK;
+}
+
+// The reference's fold of the listed trees' losses over this view, exactly and in row order
+// (sr_fold.h; sr_aux.hip): their predictions from the PRED interpreter (the values the LOSS kernels
+// saw), then the segmented fold.  out: the folds (T; +Inf where the fold overflows).  Runs after the
+// call's other passes (it reuses the context's program buffers).
+template <typename T>
+int fold_exact(sr_ctx* ctx, const sr_dataset* ds, int opset_id, const sr_tree_batch* trees, const int64_t* row_idx,
+               int64_t n_idx, int64_t n_total, int loss_kind, const std::vector<int64_t>& list, std::vector<T>* out) {
+  out->assign(list.size(), T(0));
+  if (list.empty()) return SR_OK;
+  const bool gather = row_idx != nullptr && n_idx > 0;
+  const int64_t n_eval = gather ? n_idx : ds->n;
+  const int64_t seg_len = fold_seg_len(ctx, n_eval);
+  KeepCallInfo keep(ctx);
+  const int64_t per = fold_batch_trees(n_eval, sizeof(T), true);
   for (size_t b0 = 0; b0 < list.size(); b0 += size_t(per)) {
     const size_t nb = std::min(list.size() - b0, size_t(per));
-    SubBatch<T> sub(*trees, list.data() + b0, nb);
-    SrProgramBatch<T> prog;
-    Grid g;
-    int rc = run_batch<T>(ctx, ds, opset_id, &sub.b, row_idx, n_idx, n_total, loss_kind, SR_MODE_PRED, &prog, &g);
+    FoldDev<T> fd;
+    int rc = fold_prepare<T>(ctx, ds, opset_id, trees, row_idx, n_idx, n_total, loss_kind, list.data() + b0, nb, seg_len,
+                             &fd);
     if (rc != SR_OK) return rc;
-    SR_HIP_CHECK(ctx->fold_io.ensure(2 * nb * sizeof(T) + 16));
-    T* d_carry = ctx->fold_io.as<T>();
-    T* d_out = d_carry + nb;
-    if (carry) SR_HIP_CHECK(hipMemcpyAsync(d_carry, carry + b0, nb * sizeof(T), hipMemcpyHostToDevice, s));
-    SR_HIP_CHECK(sr_launch_fold<T>(ctx->pred.as<T>(), n_eval, int(nb), static_cast<const T*>(ds->y),
-                                   static_cast<const T*>(ds->w), gather ? ctx->row_idx.as<int64_t>() : nullptr, n_eval,
-                                   lkind, T(lparam), carry ? d_carry : nullptr, d_out, s));
-    SR_HIP_CHECK(hipMemcpyAsync(out->data() + b0, d_out, nb * sizeof(T), hipMemcpyDeviceToHost, s));
-    SR_HIP_CHECK(hipStreamSynchronize(s));
+    rc = fold_finish<T>(ctx, ds, row_idx, n_idx, loss_kind, nb, seg_len, fd, false, false, out->data() + b0);
+    if (rc != SR_OK) return rc;
   }
   if (ctx->pred.cap > (size_t(2) << 30)) ctx->pred.release();  // (large prediction passes: not kept)
   return SR_OK;
+}
+
+// Base.sum in T of v[idx[i]] (or v[i]), i < n: Base.mapreduce_impl's pairwise recursion (blocks of
+// < 1024 folded sequentially) — the reference's sum(w) (LossFunctions' normalize = true).
+template <typename T>
+T jl_sum_T(const double* v, const int64_t* idx, int64_t lo, int64_t hi) {  // inclusive [lo, hi]
+  auto at = [&](int64_t i) { return T(v[idx ? idx[i] : i]); };
+  if (lo == hi) return at(lo);
+  if (hi - lo < 1024) {
+    T a = at(lo) + at(lo + 1);
+    for (int64_t i = lo + 2; i <= hi; ++i) a = a + at(i);
+    return a;
+  }
+  const int64_t mid = lo + ((hi - lo) >> 1);
+  const T x = jl_sum_T<T>(v, idx, lo, mid);
+  const T y = jl_sum_T<T>(v, idx, mid + 1, hi);
+  return x + y;
 }
 
 template <typename T>
@@ -1526,16 +1637,18 @@ int eval_loss_impl(sr_ctx* ctx, const sr_dataset* ds, int opset_id, const sr_tre
               static_cast<T*>(out_loss), out_complete, fold_terms(ds, n_eval), &fold_list,
               views ? denoms.data() : nullptr);
   ctx->n_fold_last = int64_t(fold_list.size());
+  ctx->fold_slow_last = ctx->fold_seg_last = 0;
   for (int v = 0; v < n_views && !fold_list.empty(); ++v) {  // rare: the reference's own fold, in row order (sr_fold.h)
     std::vector<int64_t> fv;
     for (int64_t t : fold_list)
       if (view_of(t) == v) fv.push_back(t);
     if (fv.empty()) continue;
     std::vector<T> fold;
-    rc = fold_exact<T>(ctx, ds, opset_id, trees, rows_of(v), n_idx, n_eval, loss_kind, fv, nullptr, &fold);
+    rc = fold_exact<T>(ctx, ds, opset_id, trees, rows_of(v), n_idx, n_eval, loss_kind, fv, &fold);
     if (rc != SR_OK) return rc;
-    for (size_t i = 0; i < fv.size(); ++i)
-      static_cast<T*>(out_loss)[fv[i]] = T(fold[i] / T(vden[size_t(v)]));  // mean: total / count, in T
+    // mean: total / count, in T; weighted: total / sum(w), the reference's pairwise Base.sum in T
+    const T den = (ds->w && n_eval > 0) ? jl_sum_T<T>(ds->w_host.data(), rows_of(v), 0, n_eval - 1) : T(vden[size_t(v)]);
+    for (size_t i = 0; i < fv.size(); ++i) static_cast<T*>(out_loss)[fv[i]] = T(fold[i] / den);
   }
   ctx->mark_phase(4);
   auto t1 = std::chrono::steady_clock::now();
@@ -2223,55 +2336,154 @@ int exact_sharded(sr_ctx* ctx, const sr_dataset* ds, const SrProgramBatch<T>& pr
   return SR_OK;
 }
 
-// The reference's loss fold of the listed trees over the GLOBAL rows, in row order: the shards fold in
-// rank order, each continuing from the previous shard's value (one all-gather per rank: the round's
-// folding rank broadcasts its values with an error word).  Collective; out = the folds (T).
+// One all-gather of `payload` bytes per rank plus an error word (every rank enters it, also after a
+// local failure: its payload zeroed, its error word set); every[r] = rank r's payload.  Returns the
+// local error, or an error when any rank's word is set.
+int gather_checked(sr_ctx* ctx, const void* payload, size_t bytes, int local, std::vector<char>* every, size_t* slot_out,
+                   const char* what) {
+  const int nr = ctx->comm_ranks;
+  const size_t slot = (bytes + sizeof(double) + 255) & ~size_t(255);
+  *slot_out = slot;
+  std::vector<char> mine(slot, 0);
+  if (local == SR_OK && bytes) std::memcpy(mine.data(), payload, bytes);
+  const double err = local != SR_OK ? 1.0 : 0.0;
+  std::memcpy(mine.data() + bytes, &err, sizeof(double));
+  hipStream_t s = ctx->stream;
+  char* d = ctx->coll_buf.as<char>();
+  if (hipMemcpyAsync(d, mine.data(), slot, hipMemcpyHostToDevice, s) != hipSuccess) {
+    std::memset(mine.data() + bytes, 0xff, sizeof(double));  // (poisoned error word)
+    (void)hipMemcpy(d, mine.data(), slot, hipMemcpyHostToDevice);
+  }
+  int rc = ctx->xport->allgather(d, d + slot, slot, s);
+  if (rc != SR_OK) return local != SR_OK ? local : rc;
+  every->assign(slot * size_t(nr), 0);
+  bool copied = hipMemcpyAsync(every->data(), d + slot, every->size(), hipMemcpyDeviceToHost, s) == hipSuccess;
+  copied = hipStreamSynchronize(s) == hipSuccess && copied;
+  if (local != SR_OK) return local;
+  if (!copied) return set_error(SR_ERR_HIP, std::string(what) + ": copy of the gathered payloads failed");
+  for (int r = 0; r < nr; ++r) {
+    double e = 0.0;
+    std::memcpy(&e, every->data() + slot * size_t(r) + bytes, sizeof(double));
+    if (e != 0.0) return set_error(SR_ERR_HIP, std::string(what) + " failed on rank " + std::to_string(r));
+  }
+  return SR_OK;
+}
+
+// The reference's loss fold of the listed trees over the GLOBAL rows, in row order.  Per batch of trees:
+// every rank runs its shard's PRED pass and segment sums in parallel; one all-gather of the shards'
+// f64 totals gives each rank the estimate of the fold's value at its first row, and every rank
+// tabulates its segments' composed steps in parallel; then the chain runs rank after rank, each
+// continuing from the previous shard's fold (one all-gather per rank; a rank's chain is O(1) per
+// segment but for the segments where the fold crosses a binade).  Collective; out = the folds (T).
 template <typename T>
 int fold_sharded(sr_ctx* ctx, const sr_dataset* ds, int opset_id, const sr_tree_batch* trees, int loss_kind,
                  const std::vector<int64_t>& list, std::vector<T>* out) {
   out->assign(list.size(), T(0));
   if (list.empty()) return SR_OK;
   const int nr = ctx->comm_ranks, me = ctx->comm_rank;
-  const int64_t n_total = ds->shard_offs[size_t(nr)];
-  if (nr == 1) return fold_exact<T>(ctx, ds, opset_id, trees, nullptr, 0, n_total, loss_kind, list, nullptr, out);
-  const size_t payload = list.size() * sizeof(T);
-  const size_t slot = (payload + sizeof(double) + 255) & ~size_t(255);
-  hipStream_t s = ctx->stream;
+  const std::vector<int64_t>& offs = ds->shard_offs;
+  const int64_t n_total = offs[size_t(nr)];
+  if (nr == 1) return fold_exact<T>(ctx, ds, opset_id, trees, nullptr, 0, n_total, loss_kind, list, out);
+  int64_t max_rows = 0;
+  for (int r = 0; r < nr; ++r) max_rows = std::max(max_rows, offs[size_t(r) + 1] - offs[size_t(r)]);
+  const int64_t per = fold_batch_trees(max_rows, sizeof(T), false);  // the same cut on every rank
+  const size_t max_nb = std::min(list.size(), size_t(per));
   Prep prep{ctx};
-  prep.need(ctx->coll_buf, slot * size_t(nr + 1));
+  prep.need(ctx->coll_buf, ((max_nb * sizeof(double) + sizeof(double) + 255) & ~size_t(255)) * size_t(nr + 1));
   int rc = agree_prep(ctx, prep);
   if (rc != SR_OK) return rc;
-  char* d = ctx->coll_buf.as<char>();
-  std::vector<T> carry;
-  std::vector<char> mine(slot, 0), every(slot * size_t(nr));
-  for (int r = 0; r < nr; ++r) {
-    int local = SR_OK;
-    std::fill(mine.begin(), mine.end(), 0);
-    if (me == r) {
-      std::vector<T> vals;
-      local = fold_exact<T>(ctx, ds, opset_id, trees, nullptr, 0, n_total, loss_kind, list, r == 0 ? nullptr : carry.data(),
-                            &vals);
-      if (local == SR_OK) std::memcpy(mine.data(), vals.data(), payload);
-      const double err = local != SR_OK ? 1.0 : 0.0;
-      std::memcpy(mine.data() + payload, &err, sizeof(double));
+  const int64_t seg_len = fold_seg_len(ctx, ds->n);
+  const int64_t n_seg = seg_len > 0 ? (ds->n + seg_len - 1) / seg_len : 0;
+  hipStream_t s = ctx->stream;
+  KeepCallInfo keep(ctx);
+  std::vector<char> every;
+  size_t slot = 0;
+  for (size_t b0 = 0; b0 < list.size(); b0 += size_t(per)) {
+    const size_t nb = std::min(list.size() - b0, size_t(per));
+    // 1. this shard's predictions and segment sums; its per-tree total
+    FoldDev<T> fd;
+    int local = fold_prepare<T>(ctx, ds, opset_id, trees, nullptr, 0, n_total, loss_kind, list.data() + b0, nb, seg_len,
+                                &fd);
+    std::vector<double> tot(nb, 0.0);
+    if (local == SR_OK && seg_len > 0) {
+      std::vector<double> ss(nb * size_t(n_seg));
+      if (hipMemcpyAsync(ss.data(), fd.segsum, ss.size() * sizeof(double), hipMemcpyDeviceToHost, s) != hipSuccess ||
+          hipStreamSynchronize(s) != hipSuccess) {
+        local = set_error(SR_ERR_HIP, "fold: segment sums copy failed");
+      } else {
+        for (size_t b = 0; b < nb; ++b)
+          for (int64_t j = 0; j < n_seg; ++j) tot[b] += ss[b * size_t(n_seg) + size_t(j)];
+      }
     }
-    if (hipMemcpyAsync(d, mine.data(), slot, hipMemcpyHostToDevice, s) != hipSuccess) {
-      std::memset(mine.data() + payload, 0xff, sizeof(double));
-      (void)hipMemcpy(d, mine.data(), slot, hipMemcpyHostToDevice);
-    }
-    rc = ctx->xport->allgather(d, d + slot, slot, s);
+    // 2. every shard's totals -> the f64 sum of the rows before this shard; the composed steps
+    rc = gather_checked(ctx, tot.data(), nb * sizeof(double), local, &every, &slot, "the loss fold's shard totals");
     if (rc != SR_OK) return rc;
-    SR_HIP_CHECK(hipMemcpyAsync(every.data(), d + slot, every.size(), hipMemcpyDeviceToHost, s));
-    SR_HIP_CHECK(hipStreamSynchronize(s));
-    for (int q = 0; q < nr; ++q) {
-      double e = 0.0;
-      std::memcpy(&e, every.data() + slot * size_t(q) + payload, sizeof(double));
-      if (e != 0.0) return local != SR_OK ? local : set_error(SR_ERR_HIP, "the loss fold failed on rank " + std::to_string(q));
+    std::vector<double> est(nb, 0.0);
+    for (int r = 0; r < me; ++r) {
+      const double* v = reinterpret_cast<const double*>(every.data() + slot * size_t(r));
+      for (size_t b = 0; b < nb; ++b) est[b] += v[b];
     }
-    carry.assign(reinterpret_cast<const T*>(every.data() + slot * size_t(r)),
-                 reinterpret_cast<const T*>(every.data() + slot * size_t(r)) + list.size());
+    if (seg_len > 0 && hipMemcpyAsync(fd.carry_est, est.data(), nb * sizeof(double), hipMemcpyHostToDevice, s) != hipSuccess)
+      local = set_error(SR_ERR_HIP, "fold: estimate upload failed");
+    // 3. the chain, shard after shard
+    std::vector<T> carry(nb, T(0)), vals(nb, T(0));
+    for (int r = 0; r < nr; ++r) {
+      if (me == r && local == SR_OK) {
+        if (r > 0 && hipMemcpyAsync(fd.carry, carry.data(), nb * sizeof(T), hipMemcpyHostToDevice, s) != hipSuccess)
+          local = set_error(SR_ERR_HIP, "fold: carry upload failed");
+        if (local == SR_OK) local = fold_finish<T>(ctx, ds, nullptr, 0, loss_kind, nb, seg_len, fd, true, r > 0, vals.data());
+      }
+      rc = gather_checked(ctx, vals.data(), nb * sizeof(T), me == r ? local : SR_OK, &every, &slot, "the loss fold");
+      if (rc != SR_OK) return local != SR_OK ? local : rc;
+      std::memcpy(carry.data(), every.data() + slot * size_t(r), nb * sizeof(T));
+    }
+    std::copy(carry.begin(), carry.end(), out->begin() + ptrdiff_t(b0));
   }
-  *out = carry;
+  if (ctx->pred.cap > (size_t(2) << 30)) ctx->pred.release();
+  return SR_OK;
+}
+
+// Base.sum(w) in T over the GLOBAL rows of a row-sharded dataset: each shard folds its Julia leaf
+// blocks (one-row heads continue a block begun on an earlier shard), one all-gather, and every rank
+// combines them in Base.mapreduce_impl's recursion order.  Collective.
+template <typename T>
+int jl_wsum_sharded(sr_ctx* ctx, const sr_dataset* ds, T* out) {
+  const int nr = ctx->comm_ranks, me = ctx->comm_rank;
+  const std::vector<int64_t>& offs = ds->shard_offs;
+  const int64_t n_total = offs[size_t(nr)];
+  std::vector<std::vector<JlRange>> ranges(static_cast<size_t>(nr));
+  size_t max_r = 0;
+  for (int r = 0; r < nr; ++r) {
+    ranges[size_t(r)] = jl_ranges(offs[size_t(r)], offs[size_t(r) + 1] - offs[size_t(r)], n_total);
+    max_r = std::max(max_r, ranges[size_t(r)].size());
+  }
+  std::vector<T> mine(max_r, T(0));
+  for (size_t i = 0; i < ranges[size_t(me)].size(); ++i) {
+    const JlRange& g = ranges[size_t(me)][i];
+    T a = T(ds->w_host[size_t(g.lo)]);
+    for (int64_t k = g.lo + 1; k <= g.hi; ++k) a = a + T(ds->w_host[size_t(k)]);
+    mine[i] = a;
+  }
+  Prep prep{ctx};
+  prep.need(ctx->coll_buf, ((max_r * sizeof(T) + sizeof(double) + 255) & ~size_t(255)) * size_t(nr + 1));
+  int rc = agree_prep(ctx, prep);
+  if (rc != SR_OK) return rc;
+  std::vector<char> every;
+  size_t slot = 0;
+  rc = gather_checked(ctx, mine.data(), max_r * sizeof(T), SR_OK, &every, &slot, "the weights' sum");
+  if (rc != SR_OK) return rc;
+  std::vector<const T*> rank_vals(static_cast<size_t>(nr));
+  for (int r = 0; r < nr; ++r) rank_vals[size_t(r)] = reinterpret_cast<const T*>(every.data() + slot * size_t(r));
+  std::vector<T> leafval(jl_leaves(n_total).size());
+  for (int r = 0; r < nr; ++r) {
+    const std::vector<JlRange>& rg = ranges[size_t(r)];
+    for (size_t i = 0; i < rg.size(); ++i) {
+      T& dst = leafval[size_t(rg[i].leaf)];
+      dst = rg[i].head ? T(dst + rank_vals[size_t(r)][i]) : rank_vals[size_t(r)][i];
+    }
+  }
+  size_t idx = 0;
+  *out = n_total > 0 ? jl_reduce<T>(leafval, 0, n_total - 1, &idx) : T(0);
   return SR_OK;
 }
 
@@ -2363,10 +2575,18 @@ int eval_sharded_impl(sr_ctx* ctx, const sr_dataset* ds, int opset_id, const sr_
   for (int64_t t = 0; t < nt; ++t)
     if ((out_complete[t] & 1) && (out_complete[t] & SR_COMP_FOLD)) fold_list.push_back(t);
   ctx->n_fold_last = int64_t(fold_list.size());
+  ctx->fold_slow_last = ctx->fold_seg_last = 0;
   std::vector<T> fold;
   rc = fold_sharded<T>(ctx, ds, opset_id, trees, loss_kind, fold_list, &fold);
   if (rc != SR_OK) return rc;
-  for (size_t i = 0; i < fold_list.size(); ++i) out_loss[fold_list[i]] = T(fold[i] / T(denom));
+  // mean: total / count, in T; weighted: total / sum(w), the reference's pairwise Base.sum in T
+  T fden = T(denom);
+  if (ds->w && !fold_list.empty()) {
+    rc = nr > 1 ? jl_wsum_sharded<T>(ctx, ds, &fden)
+                : (ds->n > 0 ? (fden = jl_sum_T<T>(ds->w_host.data(), nullptr, 0, ds->n - 1), SR_OK) : SR_OK);
+    if (rc != SR_OK) return rc;
+  }
+  for (size_t i = 0; i < fold_list.size(); ++i) out_loss[fold_list[i]] = T(fold[i] / fden);
   for (int64_t t = 0; t < nt; ++t) out_complete[t] &= 1;
   ctx->mark_phase(3);
   ctx->last_total_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
@@ -2495,6 +2715,7 @@ int sr_init(int device, sr_ctx** out) {
   if (const char* v = std::getenv("SR_AMD_NO_HINT")) ctx->dead_hints = std::atoi(v) == 0;
   if (const char* v = std::getenv("SR_AMD_CHUNKS")) ctx->chunks = std::atoi(v);
   if (const char* v = std::getenv("SR_AMD_PROBE")) ctx->probe = std::atoi(v);
+  if (const char* v = std::getenv("SR_AMD_FOLD_SEG")) ctx->fold_seg = std::atoll(v);
   if (const char* v = std::getenv("SR_AMD_STRESS_PROBE")) ctx->stress_probe = std::atoi(v);
   if (const char* v = std::getenv("SR_AMD_CODE_CACHE")) ctx->code_cache = std::atoi(v);
   if (const char* v = std::getenv("SR_AMD_FUSED_REDUCE")) ctx->fused_reduce = std::atoll(v);
@@ -3160,6 +3381,8 @@ int sr_last_phase_ms(sr_ctx* ctx, double* out, int n) {
   if (n > 7) out[7] = double(ctx->rows_last);
   if (n > 8) out[8] = ctx->last_busy_ms;
   if (n > 9) out[9] = double(ctx->n_fold_last);
+  if (n > 10) out[10] = double(ctx->fold_slow_last);
+  if (n > 11) out[11] = double(ctx->fold_seg_last);
   return SR_OK;
 }
 
@@ -3190,6 +3413,10 @@ int sr_set_tuning(sr_ctx* ctx, const char* name, int64_t value) {
   }
   if (std::strcmp(name, "fused_reduce") == 0) {  // in-launch partial reduction bound (SR_AMD_FUSED_REDUCE)
     ctx->fused_reduce = value;
+    return SR_OK;
+  }
+  if (std::strcmp(name, "fold_seg") == 0) {  // rows per segment of the in-order loss fold (SR_AMD_FOLD_SEG)
+    ctx->fold_seg = value < 0 ? -1 : value;
     return SR_OK;
   }
   if (std::strcmp(name, "exact_w") == 0) {  // waves per workgroup of the EXACT pass (SR_AMD_EXACT_W)

@@ -253,8 +253,19 @@ inline int sr_grad_launch_rows(int elem_size, int kt, int nf, bool weighted, int
 }
 hipError_t sr_launch_grad_reduce(const double* part, int n_row_blocks, int n_vals, double* out, hipStream_t s);
 // The reference's loss fold in row order for listed trees (sr_fold.h; sr_aux.hip): predictions
-// pred[b][pred_ld] of n rows, losses against y (and w) at row_idx (or the row itself), carry[b] the fold
-// over earlier shards (NULL: none); out[b] = the fold in T (+Inf when it overflows).
+// pred[b][pred_ld] of n rows, losses against y (and w) at row_idx (or the row itself).
+// sr_launch_fold_segsum: per segment of seg_len rows, segsum[b][seg] = the f64 sum of its losses;
+// sr_launch_fold_segtab: the segment's composed steps tq / tab for the binades around the f64 prefix
+// (carry_est[b]: the f64 sum of the rows before this shard, or NULL).
+template <typename T>
+hipError_t sr_launch_fold_segsum(const T* pred, int64_t pred_ld, int n_trees, const T* y, const T* w,
+                                 const int64_t* row_idx, int64_t n, int loss_kind, T loss_param, int64_t seg_len,
+                                 double* segsum, hipStream_t s);
+template <typename T>
+hipError_t sr_launch_fold_segtab(const T* pred, int64_t pred_ld, int n_trees, const T* y, const T* w,
+                                 const int64_t* row_idx, int64_t n, int loss_kind, T loss_param, int64_t seg_len,
+                                 const double* segsum, const double* carry_est, int2* tq, int64_t* tab, hipStream_t s);
 template <typename T>
 hipError_t sr_launch_fold(const T* pred, int64_t pred_ld, int n_trees, const T* y, const T* w, const int64_t* row_idx,
-                          int64_t n, int loss_kind, T loss_param, const T* carry, T* out, hipStream_t s);
+                          int64_t n, int loss_kind, T loss_param, int64_t seg_len, const int2* tq, const int64_t* tab,
+                          const T* carry, T* out, int* n_slow, hipStream_t s);

@@ -65,7 +65,7 @@ class DeviceContext:
     def set_tuning(self, name, value):
         """Run-time tuning knob (results never depend on one; include/sr_amd.h lists them): "derived",
         "probe", "stress_probe", "code_cache", "timing", "rows_per_lane", "balance", "fused_reduce", "exact_w",
-        "exact_g"; tests:
+        "exact_g", "fold_seg"; tests:
         "inject_failure", "debug_hint_regrow"."""
         _lib.check(_lib.lib.sr_set_tuning(self.handle, name.encode(), int(value)))
 
@@ -105,6 +105,13 @@ class DeviceContext:
         out = (ctypes.c_double * 10)()
         _lib.check(_lib.lib.sr_last_phase_ms(self.handle, out, 10))
         return int(out[9])
+
+    def last_fold_info(self):
+        """The last eval_loss call's in-order loss folds: (trees folded, segments folded row by row,
+        segment length in rows; 0 = one scan over every row) — sr_last_phase_ms out[9..11]."""
+        out = (ctypes.c_double * 12)()
+        _lib.check(_lib.lib.sr_last_phase_ms(self.handle, out, 12))
+        return int(out[9]), int(out[10]), int(out[11])
 
     def last_grad_info(self):
         """The last gradient call's tangent kernels per bucket (1, 2, 4, 8, 16 tangents): list of dicts

@@ -4,7 +4,8 @@ LossFunctions' `mean(loss, x, y)` and `sum(loss, x, y, w; normalize=true)` fold 
 left to right in T, so a complete tree whose losses are finite but whose running Float32 sum passes
 floatmax scores `L(Inf)` in the reference.  The library decides that from bounds on its f64 sum, from a
 +Inf loss or pair of losses in its tiles, and for the undecided band folds the losses in row order on
-the device (csrc/sr_fold.h, sr_fold_kernel).  The oracle's "ref" accumulation is that sequential fold,
+the device (csrc/sr_fold.h; sr_aux.hip: the segmented fold — segment sums, composed steps per
+segment, a chain over the segments with row-by-row scans where the fold crosses a binade).  The oracle's "ref" accumulation is that sequential fold,
 so every case here is compared with it: +Inf exactly where it is +Inf, and — for the trees folded in
 order — the same Float32 bits.
 """
@@ -120,3 +121,48 @@ def test_population_with_huge_predictions_matches_reference_fold():
     ref, rcomp = Oracle.from_options(opts).eval_loss_batch(tb, X, y, accum="ref", n_threads=8)
     assert np.array_equal(comp, rcomp)
     assert np.array_equal(np.isinf(loss[comp]), np.isinf(ref[comp]))
+
+
+def _fold_with_seg(tb, ds, opts, seg):
+    ctx = sr_amd.get_context()
+    ctx.set_tuning("fold_seg", seg)
+    try:
+        loss, comp = eval_loss_batch(tb, ds, opts)
+        return loss, comp, ctx.last_fold_info()
+    finally:
+        ctx.set_tuning("fold_seg", -1)
+
+
+@pytest.mark.parametrize("weighted", [False, True])
+def test_segmented_fold_equals_single_scan(weighted):
+    """The segmented fold (round 5) against rounds 3-4's single workgroup scan and the oracle's
+    sequential Float32 fold, bit for bit, at 2^20 rows, for segment lengths 8k / 16k (automatic) / 64k /
+    one scan: band trees (most segments advance by their composed steps; the fold crosses binades in a
+    few), weights whose Float32 sum is inexact (the reference divides by its pairwise sum(w) in T)."""
+    n = 1 << 20
+    rng = np.random.default_rng(7)
+    X = rng.standard_normal((5, n)).astype(np.float32)
+    y = np.zeros(n, dtype=np.float32)
+    w = rng.uniform(0.1, 1.9, n).astype(np.float32) if weighted else None
+    opts = Options(**OPTS)
+    wf = 1.0 if w is None else float(np.mean(w.astype(np.float64)))
+    s2 = float(np.sum(X[0].astype(np.float64) ** 2)) * wf
+    fracs = [0.95, 0.97, 0.985, 0.995, 0.999, 1.0, 1.001, 1.003, 1.01, 1.02]
+    exprs = [f"x1 * {float(np.float32(np.sqrt(M * f / s2)))!r}" for f in fracs]
+    exprs += [f"cos(x2) * {float(np.float32(np.sqrt(M * 0.999 / n)))!r} + x1 * 1.0e17"]
+    tb = flatten_trees([parse_expression(e, opts) for e in exprs], np.float32)
+    ds = Dataset(X, y, weights=w)
+    ref, rcomp = Oracle.from_options(opts).eval_loss_batch(tb, X, y, w, accum="ref", n_threads=8)
+    got = {}
+    for seg in (0, 8192, -1, 65536):
+        loss, comp, info = _fold_with_seg(tb, ds, opts, seg)
+        assert comp.all() and rcomp.all()
+        assert info[0] > 0, (seg, info)
+        if seg > 0:
+            assert info[2] == seg and info[1] < info[0] * (n // seg), (seg, info)  # most segments in O(1)
+        got[seg] = loss
+        assert np.array_equal(np.isinf(loss), np.isinf(ref)), (seg, loss, ref)
+        fin = np.isfinite(ref)
+        assert np.array_equal(loss[fin].view(np.uint32), ref[fin].view(np.uint32)), (seg, loss[fin], ref[fin])
+    for seg in (8192, -1, 65536):
+        assert np.array_equal(got[seg].view(np.uint32), got[0].view(np.uint32)), seg
