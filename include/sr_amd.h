@@ -341,6 +341,7 @@ typedef struct sr_search_options {
   int64_t batch_size;
   float warmup_maxsize_by;
   double mutation_weights[SR_N_MUTATIONS];
+  int64_t optimizer_f_calls_limit; /* Optim.Options f_calls_limit (the reference's default 10_000; 0: none) */
 } sr_search_options;
 
 typedef struct sr_search_info {
@@ -402,21 +403,23 @@ int sr_gen_random_population(int dtype, int64_t n_trees, int64_t nfeatures, int 
  * tree: BFGS with BackTracking (Newton for one constant, its curvature from the device gradient)
  * from the tree's constants and from `nrestarts` starts x0 .* (1 + eps/2), eps ~ randn(T) from the
  * stream `seed`; each round of line-search trials is one batched loss call, each gradient one
- * sr_eval_grad_batch call.  Out: the constants (pre-order per tree, concatenated; unchanged where
+ * sr_eval_grad_batch call; `iterations` and `f_calls_limit` are Optim.Options' (Options.jl:988-997:
+ * optimizer_iterations, optimizer_f_calls_limit; 0 = no call limit): a start stops after the iteration
+ * at whose end its objective calls reach the limit.  Out: the constants (pre-order per tree, concatenated; unchanged where
  * not improved), the loss at them, improved = the minimum beat the start, and the objective
  * evaluations per tree (num_evals = (f_calls + improved) x dataset fraction).
  */
 int sr_optimize_constants_batch(sr_ctx* ctx, const sr_dataset* ds, int opset_id, const sr_tree_batch* trees,
-                                const int64_t* row_idx, int64_t n_idx, int loss_kind, int iterations, int nrestarts,
-                                uint64_t seed, void* out_consts, void* out_loss, uint8_t* out_improved,
-                                int64_t* out_f_calls);
+                                const int64_t* row_idx, int64_t n_idx, int loss_kind, int iterations,
+                                int64_t f_calls_limit, int nrestarts, uint64_t seed, void* out_consts, void* out_loss,
+                                uint8_t* out_improved, int64_t* out_f_calls);
 
 /* The same optimiser with the scoring calls answered by CPU callbacks (sr_loss_fn / sr_grad_fn, as
  * sr_search_use_callbacks): a test seam and the host-port baseline.  dtype = the trees' element type. */
 int sr_optimize_constants_callbacks(int dtype, const sr_tree_batch* trees, const int64_t* row_idx, int64_t n_idx,
-                                    int iterations, int nrestarts, uint64_t seed, sr_loss_fn loss, sr_grad_fn grad,
-                                    void* user, void* out_consts, void* out_loss, uint8_t* out_improved,
-                                    int64_t* out_f_calls);
+                                    int iterations, int64_t f_calls_limit, int nrestarts, uint64_t seed, sr_loss_fn loss,
+                                    sr_grad_fn grad, void* user, void* out_consts, void* out_loss,
+                                    uint8_t* out_improved, int64_t* out_f_calls);
 
 /* Timing of the last device call on this context (ms): kernel-only, via HIP events. */
 int sr_last_kernel_ms(sr_ctx* ctx, double* eval_ms, double* total_ms);

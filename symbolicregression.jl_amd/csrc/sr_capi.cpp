@@ -221,6 +221,9 @@ struct sr_ctx {
   DevBuf coll_buf, coll_packed, ctl;
   HostBuf h_coll;        // pinned staging of the tree-sharded results
   int inject_fail = 0;   // tests (sr_set_tuning "inject_failure"): the next k collective-buffer growths fail
+  int inject_post = 0;         // tests ("inject_failure_post"): a HIP failure right after the sharded all-reduce
+  int inject_post_exact = 0;   // tests ("inject_failure_post_exact"): ... after the exact-sum all-gather
+  int inject_post_gather = 0;  // tests ("inject_failure_post_gather" k): this rank's copy of the k-th fold gather fails
   double last_eval_ms = 0.0, last_total_ms = 0.0;
   double last_busy_ms = 0.0;  // union of the last call's interpreter launch intervals (sr_last_phase_ms out[8])
   // the two above are read from the last call's events lazily, when asked for (sr_last_kernel_ms /
@@ -2201,21 +2204,25 @@ struct Prep {
 
 // Every rank's readiness before a collective: one Σ of error words (a rank whose preparation failed
 // still enters it), so either every rank proceeds or every rank returns an error.
-int agree(sr_ctx* ctx, int local) {
+int agree(sr_ctx* ctx, int local, const char* what = "failed to prepare its collective buffers") {
   hipStream_t s = ctx->stream;
   double* d = ctx->ctl.as<double>();
-  const double e = local != SR_OK ? 1.0 : 0.0;
+  double e = local != SR_OK ? 1.0 : 0.0;
   double sum = 0.0;
-  const bool set = hipMemcpyAsync(d, &e, sizeof(double), hipMemcpyHostToDevice, s) == hipSuccess;
-  int rc = ctx->xport->allreduce_sum(d, 1, s);
-  if (rc == SR_OK) {
-    SR_HIP_CHECK(hipMemcpyAsync(&sum, d, sizeof(double), hipMemcpyDeviceToHost, s));
-    SR_HIP_CHECK(hipStreamSynchronize(s));
+  bool set = hipMemcpyAsync(d, &e, sizeof(double), hipMemcpyHostToDevice, s) == hipSuccess;
+  if (!set) {  // the word must not be stale: poison it synchronously, so every peer sees a non-zero sum
+    e = 1.0;
+    (void)hipMemcpy(d, &e, sizeof(double), hipMemcpyHostToDevice);
   }
+  int rc = ctx->xport->allreduce_sum(d, 1, s);
+  bool got = false;
+  if (rc == SR_OK) got = hipMemcpyAsync(&sum, d, sizeof(double), hipMemcpyDeviceToHost, s) == hipSuccess &&
+                         hipStreamSynchronize(s) == hipSuccess;
   if (local != SR_OK) return local;
   if (!set) return set_error(SR_ERR_HIP, "error word upload failed");
   if (rc != SR_OK) return rc;
-  if (sum != 0.0) return set_error(SR_ERR_HIP, "a peer rank failed to prepare its collective buffers");
+  if (!got) return set_error(SR_ERR_HIP, "agreement: copy of the error sum failed");
+  if (sum != 0.0) return set_error(SR_ERR_HIP, std::string("a peer rank ") + what);
   return SR_OK;
 }
 // Grown buffers are agreed on; after a failure every rank releases them, so the next call grows them
@@ -2320,8 +2327,18 @@ int exact_sharded(sr_ctx* ctx, const sr_dataset* ds, const SrProgramBatch<T>& pr
   rc = ctx->xport->allgather(d, d + slot, slot, s);
   if (rc != SR_OK) return rc;
   std::vector<char> every(slot * size_t(nr));
-  SR_HIP_CHECK(hipMemcpyAsync(every.data(), d + slot, every.size(), hipMemcpyDeviceToHost, s));
-  SR_HIP_CHECK(hipStreamSynchronize(s));
+  // a copy failure here must not leave this rank out of the fold collectives its peers may enter next
+  // (the fold list depends on these verdicts): the ranks agree on it first
+  int post = SR_OK;
+  if (hipMemcpyAsync(every.data(), d + slot, every.size(), hipMemcpyDeviceToHost, s) != hipSuccess ||
+      hipStreamSynchronize(s) != hipSuccess)
+    post = set_error(SR_ERR_HIP, "the exact-sum pass: copy of the gathered folds failed");
+  if (ctx->inject_post_exact > 0) {  // tests
+    --ctx->inject_post_exact;
+    if (post == SR_OK) post = set_error(SR_ERR_HIP, "injected failure after the exact-sum all-gather");
+  }
+  rc = agree(ctx, post, "failed after the exact-sum all-gather");
+  if (rc != SR_OK) return local != SR_OK ? local : rc;
   for (int r = 0; r < nr; ++r) {
     double e = 0.0;
     std::memcpy(&e, every.data() + slot * size_t(r) + payload, sizeof(double));
@@ -2340,7 +2357,11 @@ int exact_sharded(sr_ctx* ctx, const sr_dataset* ds, const SrProgramBatch<T>& pr
 // local failure: its payload zeroed, its error word set); every[r] = rank r's payload.  Returns the
 // local error, or an error when any rank's word is set.
 int gather_checked(sr_ctx* ctx, const void* payload, size_t bytes, int local, std::vector<char>* every, size_t* slot_out,
-                   const char* what) {
+                   const char* what, int* pending) {
+  // a failure of this rank's copy of the gathered payloads is not returned here (its peers have theirs
+  // and go on to the next collective): it goes to *pending, which the caller sends in the next
+  // collective's error word (or agrees on after the last one)
+  if (*pending != SR_OK && local == SR_OK) local = *pending;
   const int nr = ctx->comm_ranks;
   const size_t slot = (bytes + sizeof(double) + 255) & ~size_t(255);
   *slot_out = slot;
@@ -2360,7 +2381,11 @@ int gather_checked(sr_ctx* ctx, const void* payload, size_t bytes, int local, st
   bool copied = hipMemcpyAsync(every->data(), d + slot, every->size(), hipMemcpyDeviceToHost, s) == hipSuccess;
   copied = hipStreamSynchronize(s) == hipSuccess && copied;
   if (local != SR_OK) return local;
-  if (!copied) return set_error(SR_ERR_HIP, std::string(what) + ": copy of the gathered payloads failed");
+  if (ctx->inject_post_gather > 0 && --ctx->inject_post_gather == 0) copied = false;  // tests: the k-th gather's copy
+  if (!copied) {
+    *pending = set_error(SR_ERR_HIP, std::string(what) + ": copy of the gathered payloads failed");
+    return SR_OK;
+  }
   for (int r = 0; r < nr; ++r) {
     double e = 0.0;
     std::memcpy(&e, every->data() + slot * size_t(r) + bytes, sizeof(double));
@@ -2398,6 +2423,7 @@ int fold_sharded(sr_ctx* ctx, const sr_dataset* ds, int opset_id, const sr_tree_
   KeepCallInfo keep(ctx);
   std::vector<char> every;
   size_t slot = 0;
+  int pending = SR_OK;  // a local failure after a gather: sent in the next one's error word
   for (size_t b0 = 0; b0 < list.size(); b0 += size_t(per)) {
     const size_t nb = std::min(list.size() - b0, size_t(per));
     // 1. this shard's predictions and segment sums; its per-tree total
@@ -2416,7 +2442,8 @@ int fold_sharded(sr_ctx* ctx, const sr_dataset* ds, int opset_id, const sr_tree_
       }
     }
     // 2. every shard's totals -> the f64 sum of the rows before this shard; the composed steps
-    rc = gather_checked(ctx, tot.data(), nb * sizeof(double), local, &every, &slot, "the loss fold's shard totals");
+    rc = gather_checked(ctx, tot.data(), nb * sizeof(double), local, &every, &slot, "the loss fold's shard totals",
+                        &pending);
     if (rc != SR_OK) return rc;
     std::vector<double> est(nb, 0.0);
     for (int r = 0; r < me; ++r) {
@@ -2428,19 +2455,21 @@ int fold_sharded(sr_ctx* ctx, const sr_dataset* ds, int opset_id, const sr_tree_
     // 3. the chain, shard after shard
     std::vector<T> carry(nb, T(0)), vals(nb, T(0));
     for (int r = 0; r < nr; ++r) {
-      if (me == r && local == SR_OK) {
+      if (me == r && local == SR_OK && pending == SR_OK) {
         if (r > 0 && hipMemcpyAsync(fd.carry, carry.data(), nb * sizeof(T), hipMemcpyHostToDevice, s) != hipSuccess)
           local = set_error(SR_ERR_HIP, "fold: carry upload failed");
         if (local == SR_OK) local = fold_finish<T>(ctx, ds, nullptr, 0, loss_kind, nb, seg_len, fd, true, r > 0, vals.data());
       }
-      rc = gather_checked(ctx, vals.data(), nb * sizeof(T), me == r ? local : SR_OK, &every, &slot, "the loss fold");
+      rc = gather_checked(ctx, vals.data(), nb * sizeof(T), me == r ? local : SR_OK, &every, &slot, "the loss fold",
+                          &pending);
       if (rc != SR_OK) return local != SR_OK ? local : rc;
       std::memcpy(carry.data(), every.data() + slot * size_t(r), nb * sizeof(T));
     }
     std::copy(carry.begin(), carry.end(), out->begin() + ptrdiff_t(b0));
   }
   if (ctx->pred.cap > (size_t(2) << 30)) ctx->pred.release();
-  return SR_OK;
+  // a failure after the last gather: the ranks agree on it (the weights' sum gather may follow)
+  return agree(ctx, pending, "failed in the loss fold");
 }
 
 // Base.sum(w) in T over the GLOBAL rows of a row-sharded dataset: each shard folds its Julia leaf
@@ -2470,8 +2499,10 @@ int jl_wsum_sharded(sr_ctx* ctx, const sr_dataset* ds, T* out) {
   if (rc != SR_OK) return rc;
   std::vector<char> every;
   size_t slot = 0;
-  rc = gather_checked(ctx, mine.data(), max_r * sizeof(T), SR_OK, &every, &slot, "the weights' sum");
+  int pending = SR_OK;
+  rc = gather_checked(ctx, mine.data(), max_r * sizeof(T), SR_OK, &every, &slot, "the weights' sum", &pending);
   if (rc != SR_OK) return rc;
+  if (pending != SR_OK) return pending;  // (no collective follows: the peers do not wait for this rank)
   std::vector<const T*> rank_vals(static_cast<size_t>(nr));
   for (int r = 0; r < nr; ++r) rank_vals[size_t(r)] = reinterpret_cast<const T*>(every.data() + slot * size_t(r));
   std::vector<T> leafval(jl_leaves(n_total).size());
@@ -2544,17 +2575,34 @@ int eval_sharded_impl(sr_ctx* ctx, const sr_dataset* ds, int opset_id, const sr_
   T* d_loss = reinterpret_cast<T*>(base + o_loss);
   uint8_t* d_comp = reinterpret_cast<uint8_t*>(base + o_comp);
   double err_sum = 0.0;
-  SR_HIP_CHECK(hipMemcpyAsync(&err_sum, dst + n5, sizeof(double), hipMemcpyDeviceToHost, s));
+  // After the all-reduce a local HIP failure must not return on this rank alone: its peers would
+  // enter the exact / fold collectives below without it.  The failure rides in `post`, and the ranks
+  // agree on it (one Σ of error words) before any further collective.
+  int post = SR_OK;
+  auto hip_post = [&](hipError_t e, const char* what) {
+    if (e != hipSuccess && post == SR_OK) post = set_error(SR_ERR_HIP, std::string(what) + ": " + hipGetErrorString(e));
+  };
+  hip_post(hipMemcpyAsync(&err_sum, dst + n5, sizeof(double), hipMemcpyDeviceToHost, s), "error sum copy");
   const int64_t n_terms = (ds->w && ds->shard_w_min < 0.0) ? 0 : n_total;
-  SR_HIP_CHECK(sr_launch_finalize_packed<T>(dst, int(nt), denom, n_terms, d_loss, d_comp, s));
-  if (nt > 0) {
-    SR_HIP_CHECK(hipMemcpyAsync(out_loss, d_loss, size_t(nt) * sizeof(T), hipMemcpyDeviceToHost, s));
-    SR_HIP_CHECK(hipMemcpyAsync(out_complete, d_comp, size_t(nt), hipMemcpyDeviceToHost, s));
+  if (post == SR_OK) hip_post(sr_launch_finalize_packed<T>(dst, int(nt), denom, n_terms, d_loss, d_comp, s), "finalize");
+  if (nt > 0 && post == SR_OK) {
+    hip_post(hipMemcpyAsync(out_loss, d_loss, size_t(nt) * sizeof(T), hipMemcpyDeviceToHost, s), "loss copy");
+    hip_post(hipMemcpyAsync(out_complete, d_comp, size_t(nt), hipMemcpyDeviceToHost, s), "flag copy");
   }
-  SR_HIP_CHECK(hipStreamSynchronize(s));
-  ctx->timing_pending = local == SR_OK && nt > 0;
+  hip_post(hipStreamSynchronize(s), "stream synchronize");
+  if (ctx->inject_post > 0) {  // tests: a local failure between the all-reduce and the exact / fold passes
+    --ctx->inject_post;
+    if (post == SR_OK) post = set_error(SR_ERR_HIP, "injected failure after the all-reduce");
+  }
+  ctx->timing_pending = local == SR_OK && post == SR_OK && nt > 0;
   if (!ctx->timing_pending) ctx->last_eval_ms = ctx->last_busy_ms = 0.0;
   ctx->mark_phase(2);
+  if (nr > 1) {
+    rc = agree(ctx, local != SR_OK ? local : post, "failed after the all-reduce");
+    if (rc != SR_OK) return local != SR_OK ? local : rc;
+  } else if (post != SR_OK) {
+    return local != SR_OK ? local : post;
+  }
   if (err_sum != 0.0) return local != SR_OK ? local : set_error(SR_ERR_HIP, "the row-sharded step failed on a peer rank");
   // 5. rare: BIG-only trees, DynamicExpressions' exact check over the global rows
   std::vector<int64_t> list;
@@ -3449,6 +3497,18 @@ int sr_set_tuning(sr_ctx* ctx, const char* name, int64_t value) {
   }
   if (std::strcmp(name, "debug_hint_regrow") == 0) {  // tests: hint-array growth in place, stale epochs in it
     ctx->debug_hint_regrow = value != 0 ? 1 : 0;
+    return SR_OK;
+  }
+  if (std::strcmp(name, "inject_failure_post") == 0) {
+    ctx->inject_post = int(value);
+    return SR_OK;
+  }
+  if (std::strcmp(name, "inject_failure_post_exact") == 0) {
+    ctx->inject_post_exact = int(value);
+    return SR_OK;
+  }
+  if (std::strcmp(name, "inject_failure_post_gather") == 0) {
+    ctx->inject_post_gather = int(value);
     return SR_OK;
   }
   if (std::strcmp(name, "inject_failure") == 0) {  // tests: the next `value` collective-buffer growths fail

@@ -78,7 +78,7 @@ inline double backtrack_step(double phi0, double dphi0, double a1, double a2, do
 inline int line_search(SrObjective& obj, const std::vector<int>& items, const std::vector<std::vector<double>>& xs,
                        const std::vector<double>& fs, const std::vector<std::vector<double>>& gs,
                        const std::vector<std::vector<double>>& dirs, std::vector<double>* alpha,
-                       std::vector<double>* fnew, std::vector<uint8_t>* ok) {
+                       std::vector<double>* fnew, std::vector<uint8_t>* ok, std::vector<int>* trials) {
   const size_t n = items.size();
   const double c1 = 1e-4;
   std::vector<double> phi0(fs), dphi0(n), a1(n, 1.0), a2(n, 1.0), phix0(fs), phix1;
@@ -89,6 +89,7 @@ inline int line_search(SrObjective& obj, const std::vector<int>& items, const st
   if (rc) return rc;
   std::vector<int> it(n, 0);
   std::vector<uint8_t> done(n, 0);
+  trials->assign(n, 1);  // objective calls per item (the first trial above)
   for (int round = 0; round < 40; ++round) {
     std::vector<int> todo;
     for (size_t k = 0; k < n; ++k) {
@@ -119,7 +120,10 @@ inline int line_search(SrObjective& obj, const std::vector<int>& items, const st
     std::vector<double> vals;
     rc = obj.f(sub, tx, &vals);
     if (rc) return rc;
-    for (size_t j = 0; j < todo.size(); ++j) phix1[size_t(todo[j])] = vals[j];
+    for (size_t j = 0; j < todo.size(); ++j) {
+      phix1[size_t(todo[j])] = vals[j];
+      ++(*trials)[size_t(todo[j])];
+    }
   }
   alpha->assign(a2.begin(), a2.end());
   *fnew = phix1;
@@ -132,13 +136,16 @@ inline int line_search(SrObjective& obj, const std::vector<int>& items, const st
 // x0s; minimisers and minima out.  Every item runs its own algorithm on its own values: the batch only
 // decides which items share a call (each item's k-th line-search trial is in round k whatever the
 // others do), so the restarts and both groups of a batch run in one lock-step pass.
+// f_calls_limit > 0: Optim.Options' f_calls_limit — an item stops after the iteration at whose end its
+// own objective calls (as Optim counts them: the curvature probes excluded) reach the limit.
 inline int minimize(SrObjective& obj, const std::vector<int>& items, std::vector<std::vector<double>> xs,
                     int iterations, const std::vector<uint8_t>& newton, std::vector<std::vector<double>>* x_out,
-                    std::vector<double>* f_out) {
+                    std::vector<double>* f_out, int64_t f_calls_limit = 0) {
   const double g_tol = 1e-8;
   const size_t n = items.size();
   std::vector<double> fs;
   std::vector<std::vector<double>> gs;
+  std::vector<int64_t> calls(n, 1);  // per item (start): the first value + gradient
   int rc = obj.fg(items, xs, &fs, &gs);
   if (rc) return rc;
   std::vector<std::vector<double>> invH(n);
@@ -208,7 +215,9 @@ inline int minimize(SrObjective& obj, const std::vector<int>& items, std::vector
     }
     std::vector<double> alpha, fnew;
     std::vector<uint8_t> ok;
-    if ((rc = line_search(obj, sub, sx, sf, sg, dirs, &alpha, &fnew, &ok))) return rc;
+    std::vector<int> trials;
+    if ((rc = line_search(obj, sub, sx, sf, sg, dirs, &alpha, &fnew, &ok, &trials))) return rc;
+    for (size_t j = 0; j < act.size(); ++j) calls[size_t(act[j])] += trials[j];
     std::vector<int> moved;
     for (size_t j = 0; j < act.size(); ++j) {
       if (ok[j])
@@ -228,6 +237,7 @@ inline int minimize(SrObjective& obj, const std::vector<int>& items, std::vector
     if ((rc = obj.fg(msub, xnew, &f2, &g2))) return rc;
     for (size_t m = 0; m < moved.size(); ++m) {
       const size_t k = size_t(act[size_t(moved[m])]);
+      ++calls[k];
       const size_t d = xs[k].size();
       std::vector<double> dx(d), dg(d);
       for (size_t i = 0; i < d; ++i) {
@@ -256,6 +266,9 @@ inline int minimize(SrObjective& obj, const std::vector<int>& items, std::vector
           invH[k][i * d + j] += c1 * dx[i] * dx[j] - c2 * (u[i] * dx[j] + dx[i] * u[j]);
       if (max_abs(gs[k]) <= g_tol) active[k] = 0;
     }
+    if (f_calls_limit > 0)
+      for (int k : act)
+        if (calls[size_t(k)] >= f_calls_limit) active[size_t(k)] = 0;  // (Optim: f_calls >= f_calls_limit)
   }
   *x_out = xs;
   *f_out = fs;
@@ -270,7 +283,7 @@ inline int minimize(SrObjective& obj, const std::vector<int>& items, std::vector
 inline int sr_optimize_batch(SrObjective& obj, const std::vector<std::vector<double>>& x0,
                              const std::vector<std::vector<std::vector<double>>>& restarts, int iterations,
                              std::vector<std::vector<double>>* best_x, std::vector<double>* best_f,
-                             std::vector<double>* baseline) {
+                             std::vector<double>* baseline, int64_t f_calls_limit = 0) {
   const size_t n = x0.size();
   std::vector<int> all(n);
   for (size_t k = 0; k < n; ++k) all[k] = int(k);
@@ -294,7 +307,7 @@ inline int sr_optimize_batch(SrObjective& obj, const std::vector<std::vector<dou
   if (items.empty()) return 0;
   std::vector<std::vector<double>> xs;
   std::vector<double> fs;
-  if ((rc = srco::minimize(obj, items, starts, iterations, newton, &xs, &fs))) return rc;
+  if ((rc = srco::minimize(obj, items, starts, iterations, newton, &xs, &fs, f_calls_limit))) return rc;
   for (size_t j = 0; j < items.size(); ++j) {  // the best over starts, earlier starts winning ties
     const size_t k = size_t(items[j]);
     if (fs[j] < (*best_f)[k]) {

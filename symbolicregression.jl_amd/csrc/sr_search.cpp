@@ -414,7 +414,8 @@ int optimize_trees(Scorer<T>& sc, Flat& flat, const std::vector<const SrTree<T>*
                    const std::vector<std::vector<double>>& x0,
                    const std::vector<std::vector<std::vector<double>>>& restarts, int iterations,
                    const typename Scorer<T>::TreeRows& rows, std::vector<std::vector<double>>* best_x,
-                   std::vector<uint8_t>* improved, std::vector<T>* adopted_loss, std::vector<int64_t>* f_calls) {
+                   std::vector<uint8_t>* improved, std::vector<T>* adopted_loss, std::vector<int64_t>* f_calls,
+                   int64_t f_calls_limit) {
   const size_t n = trees.size();
   TreeObjective<T> obj;
   obj.sc = &sc;
@@ -423,7 +424,7 @@ int optimize_trees(Scorer<T>& sc, Flat& flat, const std::vector<const SrTree<T>*
   obj.rows = &rows;
   obj.f_calls.assign(n, 0);
   std::vector<double> bf, base;
-  int rc = sr_optimize_batch(obj, x0, restarts, iterations, best_x, &bf, &base);
+  int rc = sr_optimize_batch(obj, x0, restarts, iterations, best_x, &bf, &base, f_calls_limit);
   if (rc) return rc;
   improved->assign(n, 0);
   adopted_loss->assign(n, T(0));
@@ -585,7 +586,8 @@ struct Engine : sr_search_base {
     std::vector<uint8_t> imp;
     std::vector<T> loss;
     std::vector<int64_t> f_calls;
-    const int rc = optimize_trees<T>(*L.sc, *L.flat, trees, x0, restarts, o.optimizer_iterations, rows, &bx, &imp, &loss, &f_calls);
+    const int rc = optimize_trees<T>(*L.sc, *L.flat, trees, x0, restarts, o.optimizer_iterations, rows, &bx, &imp, &loss, &f_calls,
+                                    o.optimizer_f_calls_limit);
     if (rc) return rc;
     const double frac = fraction(rows);
     for (size_t k = 0; k < n; ++k) {
@@ -1372,9 +1374,10 @@ int dispatch(sr_search* s, F f) {
 // reference's optimize_constants per tree (src/ConstantOptimization.jl:29-116), all trees in lock-step.
 template <typename T>
 int optimize_common(Scorer<T>& sc, const sr_tree_batch* trees, const int64_t* row_idx, int64_t n_idx, int iterations,
-                    int nrestarts, uint64_t seed, void* out_consts, void* out_loss, uint8_t* out_improved,
-                    int64_t* out_f_calls) {
-  if (iterations < 0 || nrestarts < 0) return sr_set_error(SR_ERR_INVALID_ARG, "negative iterations / restarts");
+                    int64_t f_calls_limit, int nrestarts, uint64_t seed, void* out_consts, void* out_loss,
+                    uint8_t* out_improved, int64_t* out_f_calls) {
+  if (iterations < 0 || nrestarts < 0 || f_calls_limit < 0)
+    return sr_set_error(SR_ERR_INVALID_ARG, "negative iterations / f_calls_limit / restarts");
   const int64_t nt = trees->n_trees;
   if (nt < 0) return sr_set_error(SR_ERR_INVALID_ARG, "negative tree count");
   if (nt == 0) return SR_OK;
@@ -1411,7 +1414,7 @@ int optimize_common(Scorer<T>& sc, const sr_tree_batch* trees, const int64_t* ro
   std::vector<uint8_t> imp;
   std::vector<T> loss;
   std::vector<int64_t> f_calls;
-  const int e = optimize_trees<T>(sc, flat, ptr, x0, restarts, iterations, rows, &bx, &imp, &loss, &f_calls);
+  const int e = optimize_trees<T>(sc, flat, ptr, x0, restarts, iterations, rows, &bx, &imp, &loss, &f_calls, f_calls_limit);
   if (e) return e;
   size_t at = 0;
   for (int64_t t = 0; t < nt; ++t) {
@@ -1438,7 +1441,7 @@ int sr_search_create(int dtype, int64_t nfeatures, int64_t n_rows, int n_unary, 
   const sr_search_options& o = *opts;
   // (tournament_selection_n > population_size samples the whole island: min(n, pop) as Population.jl)
   if (o.populations < 1 || o.population_size < 2 || o.tournament_selection_n < 1 || o.maxsize < 1 || o.ncycles_per_iteration < 1 ||
-      o.optimizer_nrestarts < 0 || o.optimizer_iterations < 0 || (o.batching && o.batch_size < 1))
+      o.optimizer_nrestarts < 0 || o.optimizer_iterations < 0 || o.optimizer_f_calls_limit < 0 || (o.batching && o.batch_size < 1))
     return sr_set_error(SR_ERR_INVALID_ARG, "invalid search options");
   if (n_unary < 0 || n_binary < 0 || n_unary + n_binary == 0 || n_unary > 255 || n_binary > 255)
     return sr_set_error(SR_ERR_INVALID_ARG, "bad operator counts");
@@ -1683,9 +1686,9 @@ int sr_search_members(sr_search* s, int which, int64_t* offsets, uint8_t* degree
 }
 
 int sr_optimize_constants_batch(sr_ctx* ctx, const sr_dataset* ds, int opset_id, const sr_tree_batch* trees,
-                                const int64_t* row_idx, int64_t n_idx, int loss_kind, int iterations, int nrestarts,
-                                uint64_t seed, void* out_consts, void* out_loss, uint8_t* out_improved,
-                                int64_t* out_f_calls) {
+                                const int64_t* row_idx, int64_t n_idx, int loss_kind, int iterations,
+                                int64_t f_calls_limit, int nrestarts, uint64_t seed, void* out_consts, void* out_loss,
+                                uint8_t* out_improved, int64_t* out_f_calls) {
   if (!ctx || !ds || !trees) return sr_set_error(SR_ERR_INVALID_ARG, "NULL context, dataset or trees");
   int dt = 0;
   int64_t nf = 0, n = 0;
@@ -1698,16 +1701,16 @@ int sr_optimize_constants_batch(sr_ctx* ctx, const sr_dataset* ds, int opset_id,
     sc.ds = ds;
     sc.opset_id = opset_id;
     sc.loss_code = loss_kind;
-    return optimize_common<T>(sc, trees, row_idx, n_idx, iterations, nrestarts, seed, out_consts, out_loss,
-                              out_improved, out_f_calls);
+    return optimize_common<T>(sc, trees, row_idx, n_idx, iterations, f_calls_limit, nrestarts, seed, out_consts,
+                              out_loss, out_improved, out_f_calls);
   };
   return dt == SR_DTYPE_F32 ? run(0.0f) : run(0.0);
 }
 
 int sr_optimize_constants_callbacks(int dtype, const sr_tree_batch* trees, const int64_t* row_idx, int64_t n_idx,
-                                    int iterations, int nrestarts, uint64_t seed, sr_loss_fn loss, sr_grad_fn grad,
-                                    void* user, void* out_consts, void* out_loss, uint8_t* out_improved,
-                                    int64_t* out_f_calls) {
+                                    int iterations, int64_t f_calls_limit, int nrestarts, uint64_t seed, sr_loss_fn loss,
+                                    sr_grad_fn grad, void* user, void* out_consts, void* out_loss,
+                                    uint8_t* out_improved, int64_t* out_f_calls) {
   if (!trees || !loss || !grad) return sr_set_error(SR_ERR_INVALID_ARG, "NULL trees or scorer callbacks");
   if (dtype != SR_DTYPE_F32 && dtype != SR_DTYPE_F64) return sr_set_error(SR_ERR_INVALID_ARG, "unknown dtype");
   auto run = [&](auto zero) -> int {
@@ -1716,8 +1719,8 @@ int sr_optimize_constants_callbacks(int dtype, const sr_tree_batch* trees, const
     sc.loss_cb = loss;
     sc.grad_cb = grad;
     sc.cb_user = user;
-    return optimize_common<T>(sc, trees, row_idx, n_idx, iterations, nrestarts, seed, out_consts, out_loss,
-                              out_improved, out_f_calls);
+    return optimize_common<T>(sc, trees, row_idx, n_idx, iterations, f_calls_limit, nrestarts, seed, out_consts,
+                              out_loss, out_improved, out_f_calls);
   };
   return dtype == SR_DTYPE_F32 ? run(0.0f) : run(0.0);
 }

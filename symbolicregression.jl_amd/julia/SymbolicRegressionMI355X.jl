@@ -340,6 +340,32 @@ function LossFunctionsModule._eval_loss(tree::Union{AbstractExpression{T},Abstra
 end
 
 # ---------------------------------------------------------------- batched constant optimisation
+const Optim = ConstantOptimizationModule.Optim
+const LineSearches = ConstantOptimizationModule.LineSearches
+
+"""The device optimiser is the reference's DEFAULT one only: `Optim.BFGS(; linesearch=LineSearches.
+BackTracking())` (src/Options.jl:613-615), with Newton for a single constant as `optimize_constants`
+itself chooses (src/ConstantOptimization.jl:38-56).  Returns `(iterations, f_calls_limit)` from
+`options.optimizer_options` (the `Optim.Options` built at src/Options.jl:988-997) when the device can
+run it, or `nothing`: any other `optimizer_algorithm` (`NelderMead`, accepted at Options.jl:738-746),
+another line search or BackTracking setting, a non-identity initial inverse Hessian, or Optim options
+beyond `iterations` / `f_calls_limit` at non-default values — the caller then keeps the reference's
+per-member `optimize_constants` (INTEGRATION.md §4)."""
+function device_optimizer(options)
+    alg = options.optimizer_algorithm
+    alg isa Optim.BFGS || return nothing
+    ls = getfield(alg, :linesearch!)
+    ls isa LineSearches.BackTracking || return nothing
+    (ls.c_1 == 1e-4 && ls.ρ_hi == 0.5 && ls.ρ_lo == 0.1 && ls.order == 3) || return nothing
+    getfield(alg, :initial_invH) === nothing || return nothing
+    getfield(alg, :alphaguess!) isa LineSearches.InitialStatic || return nothing
+    o = options.optimizer_options
+    # the device's stopping rules: g_abstol 1e-8 (Optim's default), iterations, f_calls_limit
+    (o.g_abstol == 1e-8 && o.x_abstol == 0 && o.f_abstol == 0 && o.f_reltol == 0 && o.x_reltol == 0 &&
+     o.callback === nothing && isnan(o.time_limit)) || return nothing
+    return (Cint(o.iterations), Int64(o.f_calls_limit))
+end
+
 """Batched `optimize_constants` (src/ConstantOptimization.jl:29-116) of `members` on `dataset` (a full
 dataset or a SubDataset view): ONE `sr_optimize_constants_batch` call runs the reference's algorithm
 for every member in lock-step on the device (BFGS + BackTracking, Newton for one constant, from the
@@ -347,10 +373,14 @@ constants and `optimizer_nrestarts` perturbed starts, the minimum adopted only i
 each line-search round one batched loss launch, each gradient one forward-mode launch).  Updates the
 improved members' constants, loss, cost and birth like `_optimize_constants_inner` and returns their
 `num_evals` (objective calls x dataset fraction, +1 per improved member), or `nothing` when the device
-cannot take these trees (the caller then keeps the reference's per-member path)."""
+cannot take these trees or this optimiser (`device_optimizer`; the caller then keeps the reference's
+per-member path)."""
 function optimize_constants_batch!(dataset::Dataset{T,L}, members::AbstractVector, options::MI355XOptions
                                    ) where {T,L}
     isempty(members) && return Float64[]
+    limits = device_optimizer(options)
+    limits === nothing && return nothing
+    iterations, f_calls_limit = limits
     trees = [m.tree for m in members]
     all(device_tree, trees) || return nothing
     ctx = context()
@@ -372,10 +402,10 @@ function optimize_constants_batch!(dataset::Dataset{T,L}, members::AbstractVecto
         b = SrTreeBatch(n, pointer(f.offsets), pointer(f.degree), pointer(f.op), pointer(f.feature),
                         pointer(f.constant), Ptr{Cvoid}(pointer(f.val)))
         rc = ccall((:sr_optimize_constants_batch, LIB), Cint,
-                   (Ptr{Cvoid}, Ptr{Cvoid}, Cint, Ref{SrTreeBatch}, Ptr{Int64}, Int64, Cint, Cint, Cint, UInt64,
-                    Ptr{T}, Ptr{T}, Ptr{UInt8}, Ptr{Int64}),
+                   (Ptr{Cvoid}, Ptr{Cvoid}, Cint, Ref{SrTreeBatch}, Ptr{Int64}, Int64, Cint, Cint, Int64, Cint,
+                    UInt64, Ptr{T}, Ptr{T}, Ptr{UInt8}, Ptr{Int64}),
                    ctx.handle, dsh, oid, b, rows === nothing ? C_NULL : pointer(rows),
-                   rows === nothing ? 0 : length(rows), lk, options.optimizer_iterations,
+                   rows === nothing ? 0 : length(rows), lk, iterations, f_calls_limit,
                    options.optimizer_nrestarts, seed, consts, losses, improved, f_calls)
         rc == SR_ERR_UNSUPPORTED_OP && return nothing
         check(rc)

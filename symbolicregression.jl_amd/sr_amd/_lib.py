@@ -139,6 +139,7 @@ class SrSearchOptions(ctypes.Structure):
         ("should_simplify", c_int), ("should_optimize_constants", c_int), ("optimizer_probability", c_float),
         ("optimizer_iterations", c_int), ("optimizer_nrestarts", c_int), ("batching", c_int),
         ("batch_size", c_int64), ("warmup_maxsize_by", c_float), ("mutation_weights", c_double * len(MUTATIONS)),
+        ("optimizer_f_calls_limit", c_int64),
     ]
 
 
@@ -257,7 +258,8 @@ def _load():
         "sr_search_members": (c_int, [P, c_int, P, P, P, P, P, P, P, P, P, P, P, P]),
         "sr_optimize_constants_callbacks": (
             c_int,
-            [c_int, POINTER(SrTreeBatch), P, c_int64, c_int, c_int, ctypes.c_uint64, LOSS_FN, GRAD_FN, P, P, P, P, P],
+            [c_int, POINTER(SrTreeBatch), P, c_int64, c_int, c_int64, c_int, ctypes.c_uint64, LOSS_FN, GRAD_FN, P, P, P,
+             P, P],
         ),
         "sr_gen_random_population": (
             c_int,
@@ -265,7 +267,7 @@ def _load():
         ),
         "sr_optimize_constants_batch": (
             c_int,
-            [P, P, c_int, POINTER(SrTreeBatch), P, c_int64, c_int, c_int, c_int, ctypes.c_uint64, P, P, P, P],
+            [P, P, c_int, POINTER(SrTreeBatch), P, c_int64, c_int, c_int, c_int64, c_int, ctypes.c_uint64, P, P, P, P],
         ),
     }
     for name, (res, args) in proto.items():

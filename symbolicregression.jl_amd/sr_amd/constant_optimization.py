@@ -20,19 +20,35 @@ from . import _lib
 from .device import get_context
 
 
-def optimize_constants_batch(trees, dataset, options, rng=None, *, iterations=None, nrestarts=None, ctx=None):
+def device_optimizer_supported(options) -> bool:
+    """The device path runs the reference's default optimiser only: Optim.BFGS with BackTracking
+    (Newton for one constant, as optimize_constants chooses; src/ConstantOptimization.jl:38-56).  A
+    caller with another ``optimizer_algorithm`` keeps the reference's CPU optimize_constants (the
+    Julia glue's gate)."""
+    return getattr(options, "optimizer_algorithm", "BFGS") == "BFGS"
+
+
+def optimize_constants_batch(trees, dataset, options, rng=None, *, iterations=None, nrestarts=None, ctx=None,
+                             f_calls_limit=None):
     """Optimise the constants of every tree of ``trees`` (TreeBatch or Nodes) on ``dataset``.
 
     Returns ``(new_batch, losses, improved, num_evals)``: the batch with adopted constants, the
     loss of each tree after optimisation (the starting loss when not improved), which trees improved
     (``result.minimum < baseline``), and the reference's ``num_evals`` accounting (objective calls x
     dataset fraction, +1 for the re-evaluation of an improved member, src/ConstantOptimization.jl:92-109).
-    ``rng`` (numpy Generator) seeds the restart perturbations.
+    ``rng`` (numpy Generator) seeds the restart perturbations.  ``iterations`` / ``f_calls_limit``
+    default to the options' ``optimizer_iterations`` / ``optimizer_f_calls_limit`` (Optim.Options,
+    src/Options.jl:988-997); a non-BFGS ``optimizer_algorithm`` raises NotImplementedError (the
+    reference's CPU optimiser is the caller's path for it).
     """
     from .loss import _as_batch
 
+    if not device_optimizer_supported(options):
+        raise NotImplementedError(f"optimizer_algorithm={options.optimizer_algorithm!r} runs on the reference's CPU "
+                                  "optimize_constants; the device optimiser is BFGS + BackTracking")
     ctx = ctx or get_context()
     iterations = iterations if iterations is not None else getattr(options, "optimizer_iterations", 8)
+    f_calls_limit = f_calls_limit if f_calls_limit is not None else getattr(options, "optimizer_f_calls_limit", 10_000)
     nrestarts = nrestarts if nrestarts is not None else getattr(options, "optimizer_nrestarts", 2)
     full = dataset.full
     tb = _as_batch(trees, full.dtype)
@@ -48,7 +64,7 @@ def optimize_constants_batch(trees, dataset, options, rng=None, *, iterations=No
     s = tb.to_struct()
     _lib.check(_lib.lib.sr_optimize_constants_batch(
         ctx.handle, full.device_handle(ctx), ctx.opset_id(options.operators), ctypes.byref(s), p(rows),
-        0 if rows is None else rows.size, ctx.loss_code(options), int(iterations), int(nrestarts),
+        0 if rows is None else rows.size, ctx.loss_code(options), int(iterations), int(f_calls_limit), int(nrestarts),
         ctypes.c_uint64(seed), p(consts), p(losses), p(improved), p(f_calls)))
     n_const = int(np.count_nonzero(tb.constant_mask()))
     new_tb = tb.with_constants(consts[:n_const])
@@ -58,7 +74,7 @@ def optimize_constants_batch(trees, dataset, options, rng=None, *, iterations=No
 
 
 def optimize_constants_callbacks(trees, loss_fn, grad_fn, *, dtype=np.float64, seed=0, iterations=8, nrestarts=2,
-                                 rows=None):
+                                 rows=None, f_calls_limit=0):
     """The same batched optimiser with CPU scorers (``sr_optimize_constants_callbacks``; test seam):
     loss_fn(TreeBatch, rows) -> losses, grad_fn(TreeBatch, rows) -> (losses, gradients).  The restart
     draws come from ``seed`` exactly as ``optimize_constants_batch``'s.  Returns (new_batch, losses,
@@ -79,6 +95,7 @@ def optimize_constants_callbacks(trees, loss_fn, grad_fn, *, dtype=np.float64, s
     s = tb.to_struct()
     _lib.check(_lib.lib.sr_optimize_constants_callbacks(
         _lib.SR_DTYPE_F32 if np.dtype(dtype) == np.float32 else _lib.SR_DTYPE_F64, ctypes.byref(s), p(r),
-        0 if r is None else r.size, int(iterations), int(nrestarts), ctypes.c_uint64(int(seed)), cbs[0], cbs[1], None,
+        0 if r is None else r.size, int(iterations), int(f_calls_limit), int(nrestarts), ctypes.c_uint64(int(seed)),
+        cbs[0], cbs[1], None,
         p(consts), p(losses), p(improved), p(f_calls)))
     return tb.with_constants(consts[:n_const]), losses[:nt].copy(), improved[:nt].astype(bool), f_calls[:nt].copy()

@@ -76,6 +76,8 @@ class Options:
         optimizer_probability: float = 0.14,
         optimizer_nrestarts: int = 2,
         optimizer_iterations: int | None = None,
+        optimizer_f_calls_limit: int | None = None,
+        optimizer_algorithm: str = "BFGS",
         turbo: bool = False,
         bumper: bool = False,
         device: str = "mi355x",
@@ -104,6 +106,13 @@ class Options:
         self.optimizer_probability = optimizer_probability
         self.optimizer_nrestarts = optimizer_nrestarts
         self.optimizer_iterations = 8 if optimizer_iterations is None else int(optimizer_iterations)
+        self.optimizer_f_calls_limit = 10_000 if optimizer_f_calls_limit is None else int(optimizer_f_calls_limit)
+        # the device optimiser is Optim's BFGS with BackTracking (Newton for one constant, as the
+        # reference chooses); any other algorithm (the reference accepts "NelderMead",
+        # src/Options.jl:738-746) stays on the reference's CPU optimize_constants
+        if str(optimizer_algorithm) not in ("BFGS", "NelderMead"):
+            raise ValueError(f"unknown optimizer_algorithm {optimizer_algorithm!r}")
+        self.optimizer_algorithm = str(optimizer_algorithm)
         self.turbo = turbo
         self.bumper = bumper
         if device not in ("mi355x", "gpu", "hip"):

@@ -199,6 +199,10 @@ def search_options_struct(options, so: SearchOptions) -> _lib.SrSearchOptions:
     o.optimizer_probability = float(options.optimizer_probability)
     o.optimizer_iterations = int(options.optimizer_iterations)
     o.optimizer_nrestarts = int(options.optimizer_nrestarts)
+    o.optimizer_f_calls_limit = int(options.optimizer_f_calls_limit)
+    if options.should_optimize_constants and getattr(options, "optimizer_algorithm", "BFGS") != "BFGS":
+        raise NotImplementedError(f"optimizer_algorithm={options.optimizer_algorithm!r}: the native search runs the "
+                                  "device BFGS optimiser only; the reference's CPU search is the path for it")
     o.batching = int(bool(options.batching))
     o.batch_size = int(options.batch_size)
     o.warmup_maxsize_by = float(so.warmup_maxsize_by)

@@ -146,6 +146,32 @@ def test_bfgs_batch_recovers_constants():
         np.testing.assert_array_equal(new_tb.get_constants()[co[k]:co[k + 1]], tb.get_constants()[co[k]:co[k + 1]])
 
 
+def test_f_calls_limit_is_honoured():
+    """Optim.Options' f_calls_limit crosses the C ABI (sr_optimize_constants_batch) and
+    the device optimiser honours it: a limit of 3 objective calls stops every start after its first
+    iteration (each costs >= 3 calls), exactly as iterations = 1 does — constants, losses and num_evals
+    bit for bit — while the default limit (10_000) equals no limit."""
+    from sr_amd import optimize_constants_batch
+
+    opts = Options(binary_operators=["+", "-", "*", "/"], unary_operators=["cos", "exp"])
+    rng = np.random.default_rng(12)
+    X = rng.standard_normal((3, 4000)).astype(np.float64)
+    y = 3.0 * X[0] * np.cos(X[1] * 0.7) + 1.5
+    trees = [parse_expression(e, opts) for e in ("1.0 * x1 + 1.0", "x1 * cos(x2 * 0.5) * 2.0 + 1.0", "x1 * 1.0",
+                                                 "exp(x3 * 0.1) * 0.3 + x1 * 2.5")]
+    tb = flatten_trees(trees, np.float64)
+    ds = Dataset(X, y)
+    run = lambda **kw: optimize_constants_batch(tb, ds, opts, np.random.default_rng(4), **kw)  # noqa: E731
+    lim, one = run(f_calls_limit=3), run(iterations=1)
+    for a, b in zip(lim, one):
+        a, b = (a.val, b.val) if hasattr(a, "val") else (a, b)
+        assert np.array_equal(a, b)
+    full, dflt = run(f_calls_limit=0), run()
+    assert np.array_equal(full[0].val, dflt[0].val) and np.array_equal(full[3], dflt[3])
+    assert np.all(lim[3] <= full[3]) and np.any(lim[3] < full[3])
+    assert np.any(full[1] < lim[1])
+
+
 def test_grad_f64_many_features_deep_trees_weighted():
     """Float64 with 10 features, weights, maxsize 30 and unary operators — trees of
     stack depth 3 and two-constant trees in one batch.  The 8-rows-per-lane buckets' LDS operand stacks

@@ -6,7 +6,9 @@ refuses two ranks on one device).  Everything else is the C++ path the 8-GPU run
 layout exchange, the packed all-reduce with its error word, the exact Julia-order pass whose leaf
 blocks straddle the cut between the shards (head ranges), the in-order loss fold continued across the
 shards, the tree owners' results all-gather, and the failure protocol (an injected buffer failure on
-one rank makes BOTH ranks return an error; the next call works on both).
+one rank makes BOTH ranks return an error; so does an injected HIP failure on one rank after the packed
+all-reduce, after the exact pass's all-gather, or in the loss fold's gathers; the next call works on
+both).
 
 Uneven shards (rank 0 holds 60,001 of 143,417 rows), huge values around the cut (BIG trees), weights.
 Results must equal the single-GPU call on the whole dataset (flags bit for bit, losses to 1e-6; the
@@ -106,6 +108,23 @@ def _worker(rank, world, port, q):
             ctx.set_tuning("inject_failure", 0)
         out["errors"] = errs
         out["after"] = eval_loss_sharded(big, shard, opts)
+        # local HIP failures AFTER a collective: after the packed all-reduce, after
+        # the exact pass's all-gather, and in the loss fold's gathers (the first, and the last of the
+        # chain, which only the final agreement catches); the band and BIG trees make every later
+        # collective run, so a rank returning alone would leave its peer waiting
+        post = []
+        for knob, who, k in (("inject_failure_post", 1, 1), ("inject_failure_post_exact", 0, 1),
+                             ("inject_failure_post_gather", 1, 1), ("inject_failure_post_gather", 0, 3)):
+            if rank == who:
+                ctx.set_tuning(knob, k)
+            try:
+                eval_loss_sharded(tb, shard, opts)
+                post.append(None)
+            except Exception as e:  # noqa: BLE001
+                post.append(str(e)[:200])
+            ctx.set_tuning(knob, 0)
+        out["post_errors"] = post
+        out["post_after"] = eval_loss_sharded(tb, shard, opts)
         q.put(out)
     except Exception as e:  # noqa: BLE001
         import traceback
@@ -162,3 +181,6 @@ def test_two_ranks_on_one_gpu_run_the_library_sharded_paths():
         assert all(e is not None for e in g["errors"]), g["errors"]  # both ranks failed, neither hung
         loss, comp = g["after"]
         assert np.array_equal(comp, np.concatenate([got[0]["u_ref"][1]] * 3))
+        assert all(e is not None for e in g["post_errors"]), g["post_errors"]  # failures after a collective
+        loss, comp = g["post_after"]
+        assert np.array_equal(comp, got[0]["u_ref"][1])

@@ -89,3 +89,42 @@ def test_callback_optimiser_items_independent_of_batch():
         o1, l1, i1, f1 = optimize_constants_callbacks(one, lossf, gradf, nrestarts=0)
         assert l1[0] == loss[k] and i1[0] == improved[k] and f1[0] == f_calls[k], exprs[k]
         assert np.array_equal(o1.val, out.val[out.offsets[k]:out.offsets[k + 1]]), exprs[k]
+
+
+def test_callback_optimiser_honours_f_calls_limit():
+    """Optim.Options' f_calls_limit (src/Options.jl:988-997, passed through the C ABI): a start stops
+    after the iteration at whose end its objective calls reach the limit.  Every iteration costs at
+    least three calls (value + gradient, one line-search trial, value + gradient at the new point), so
+    a limit of 3 stops every start after its first iteration — exactly what iterations = 1 gives; the
+    default limit (10_000) never binds at 8 iterations."""
+    rng = np.random.default_rng(8)
+    X = rng.uniform(0.5, 2.0, (3, 300))
+    y = 2.5 * X[0] * X[1] / (X[2] + 0.75)
+    opts = Options(**OPS)
+    lossf, gradf = _scorers(opts, X, y)
+    exprs = ["1.9 * x1 * x2 / (x3 + 0.5)", "1.3 * x1 * x2 / x3", "cos(x1 * 0.7) + x2 * 1.1",
+             "x1 * x2 / (x3 * 0.5 + 0.2)"]
+    tb = flatten_trees([parse_expression(e, opts) for e in exprs], np.float64)
+    lim = optimize_constants_callbacks(tb, lossf, gradf, seed=5, f_calls_limit=3)
+    one = optimize_constants_callbacks(tb, lossf, gradf, seed=5, iterations=1)
+    full = optimize_constants_callbacks(tb, lossf, gradf, seed=5)
+    dflt = optimize_constants_callbacks(tb, lossf, gradf, seed=5, f_calls_limit=10_000)
+    assert np.array_equal(lim[0].val, one[0].val) and np.array_equal(lim[1], one[1]) and np.array_equal(lim[3], one[3])
+    assert np.array_equal(dflt[0].val, full[0].val) and np.array_equal(dflt[3], full[3])
+    assert np.all(lim[3] <= full[3]) and np.sum(lim[3] < full[3]) >= 3  # (Newton's tree converges in one)
+    assert np.any(full[1] < lim[1])
+
+
+def test_non_bfgs_optimizer_is_not_run_on_the_device():
+    """A non-default optimizer_algorithm (the reference accepts NelderMead, src/Options.jl:738-746) is
+    never replaced by the device's BFGS: the Python mirror refuses it (the Julia glue's
+    device_optimizer gate hands it to the reference's optimize_constants)."""
+    from sr_amd.constant_optimization import device_optimizer_supported, optimize_constants_batch
+
+    assert device_optimizer_supported(Options(**OPS))
+    nm = Options(**OPS, optimizer_algorithm="NelderMead")
+    assert not device_optimizer_supported(nm)
+    with pytest.raises(NotImplementedError):
+        optimize_constants_batch([parse_expression("x1 * 2.0", nm)], None, nm)
+    with pytest.raises(ValueError):
+        Options(**OPS, optimizer_algorithm="LBFGS")
