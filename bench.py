@@ -484,8 +484,12 @@ def c4_line(ctx, opts, eval_loss_sharded, gen_random_batch, Dataset, args, comm,
     algo = algorithmic_bytes(tb.n_trees, n_local, nl, ctx.last_rows_per_lane())
     n_derived = ctx.last_derived_columns()
     algo_d = algorithmic_bytes(tb.n_trees, n_local, nl, ctx.last_rows_per_lane(), n_derived)
+    fi = ctx.last_fold_info()
     passes = {"exact_trees": ctx.last_exact_trees(), "fold_trees": ctx.last_fold_trees(),
-              "phase_ms": [round(float(v), 3) for v in ctx.last_phase_ms()]}
+              "phase_ms": [round(float(v), 3) for v in ctx.last_phase_ms()],
+              "exact_kernel_ms": round(ctx.last_exact_kernel_ms(), 3),
+              "fold_device_ms": {k: round(v, 3) for k, v in ctx.last_fold_ms().items()},
+              "fold_segments_row_by_row": fi[1], "fold_segment_rows": fi[2]}
     out = {"metric": "tree-node x row evals/sec (batched eval_loss, fp32)",
            "value": float(tb.n_nodes) * rows_total * args.c4_steps / dt, "unit": "node-evals/s",
            "ms_per_step": dt / args.c4_steps * 1e3, "steps": args.c4_steps, "warmup": 1, "n_gpus": world,
@@ -504,12 +508,57 @@ def c4_line(ctx, opts, eval_loss_sharded, gen_random_batch, Dataset, args, comm,
                                 traffic_source=traffic.get("source") if traffic else None,
                                 hbm_GBps=(traffic["hbm_read_bytes_per_step"] / (kmean * 1e-3) / 1e9
                                           if traffic else None), hbm_peak_GBps=PEAK_HBM_GBPS)}
+    if world == 1 and rank == 0:
+        progress("c4 projection to 8 ranks (rank 0's 8M-row shard)")
+        out["projection_8_ranks"] = c4_projection(ctx, opts, tb, eval_loss_sharded, Dataset, args, comm, rows_total,
+                                                  out["ms_per_step"], passes)
     if world == 1 and rank == 0 and not args.no_c4_parity:
         progress("c4 parity (oracle over all rows for a tree sample)")
         out["parity"] = c4_parity(opts, tb, res, lambda t: eval_loss_sharded(t, ds, opts), rows_total,
                                   args.c4_parity_trees)
     ds.free_device()
     return out
+
+
+# latency of one small collective (an error-word agreement, a gather of a few KB) and of the packed
+# [5, 100k] f64 all-reduce over xGMI at 8 ranks, as assumed by the projection (not measured here: the
+# driver's 8-GPU run is the first multi-rank one)
+COLL_SMALL_MS, COLL_PACKED_MS = 0.05, 0.2
+
+
+def c4_projection(ctx, opts, tb, eval_loss_sharded, Dataset, args, comm, rows_total, t1_ms, passes):
+    """C4 at 8 ranks, projected from one GPU: rank 0's shard (rows [0, n/8)) through
+    the same sharded call at world size 1 — compile, probe, interpreter and exact pass over its 8M rows —
+    plus the terms the single shard does not see: the in-order loss fold's parallel phases (PRED pass,
+    segment sums, composed steps) at 1/8 of the 1-GPU step's, its chain in full (the shards run it one
+    after another), and the collectives (the packed all-reduce and ~14 small ones, assumed latencies)."""
+    X, y = c4_shard(0, 8, rows_total)
+    ds = Dataset(X, y)
+    ds.device_handle(ctx)
+    del X, y
+    st = {}
+
+    def call():
+        eval_loss_sharded(tb, ds, opts)
+    steps = max(2, args.c4_steps)
+    dt, step_ms, _ = timed(lib_step(ctx, call, st), steps, 1, comm.barrier)
+    shard_ms = dt / steps * 1e3
+    shard_phases = [round(float(v), 3) for v in ctx.last_phase_ms()]
+    ds.free_device()
+    f = passes.get("fold_device_ms", {})
+    fold_par = (f.get("pred", 0.0) + f.get("segsum", 0.0) + f.get("segtab", 0.0)) / 8.0
+    fold_chain = f.get("chain", 0.0)
+    n_small = 14 if passes.get("fold_trees", 0) else 4
+    coll = COLL_PACKED_MS + n_small * COLL_SMALL_MS
+    t8 = shard_ms + fold_par + fold_chain + coll
+    return {"rank0_shard_rows": rows_total // 8, "rank0_shard_ms_per_step": shard_ms,
+            "rank0_shard_phase_ms": shard_phases, "fold_parallel_ms_over_8": fold_par, "fold_chain_ms": fold_chain,
+            "collectives_ms_assumed": coll, "projected_ms_per_step": t8, "one_gpu_ms_per_step": t1_ms,
+            "efficiency": t1_ms / (8.0 * t8),
+            "model": ("t8 = rank 0's 8M-row shard through sr_eval_loss_sharded at world 1 (measured) + the 1-GPU "
+                      "step's fold PRED / segment-sum / composed-step device time / 8 + its fold chain (sequential "
+                      f"over the shards) + collectives ({COLL_PACKED_MS} ms packed all-reduce + {n_small} x "
+                      f"{COLL_SMALL_MS} ms small ones, assumed); efficiency = t1 / (8 t8)")}
 
 
 _LIBM_EXACT_UNARY = {"neg", "square", "cube", "abs", "sign", "relu", "inv", "round", "floor", "ceil", "sqrt",

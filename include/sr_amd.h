@@ -433,7 +433,8 @@ int sr_last_kernel_ms(sr_ctx* ctx, double* eval_ms, double* total_ms);
  * out[9] (n >= 10) = the number of trees whose loss fold was computed in row order (the overflow rule of
  * the reference's T-precision fold: csrc/sr_fold.h), out[10] (n >= 11) = the segments of those folds
  * folded row by row (the rest advanced by their composed steps), out[11] (n >= 12) = the fold's
- * segment length in rows (0: one scan over every row).  sr_last_kernel_ms's eval_ms is the sum of
+ * segment length in rows (0: one scan over every row), out[12..15] (n >= 16) = the fold's device time
+ * (ms, HIP events, summed over its batches) in its PRED pass, segment sums, composed steps and chain.  sr_last_kernel_ms's eval_ms is the sum of
  * those launches' durations. */
 int sr_last_phase_ms(sr_ctx* ctx, double* out, int n);
 

@@ -141,6 +141,10 @@ struct sr_ctx {
   // algorithmic flops (sr_last_grad_info), work items, rows per lane
   static constexpr int kGradBuckets = 5;
   hipEvent_t ev_g0[kGradBuckets] = {}, ev_g1[kGradBuckets] = {};
+  // the in-order loss fold's device phases (sr_last_fold_ms): PRED pass, segment sums, composed steps,
+  // chain; events around each, accumulated over the call's fold batches (the fold is rare: always timed)
+  hipEvent_t ev_f[5] = {};
+  double fold_ms[4] = {0, 0, 0, 0};
   bool grad_timed[kGradBuckets] = {};
   double grad_flops[kGradBuckets] = {};
   int64_t grad_items[kGradBuckets] = {};
@@ -1466,8 +1470,10 @@ int fold_prepare(sr_ctx* ctx, const sr_dataset* ds, int opset_id, const sr_tree_
   SubBatch<T> sub(*trees, list, nb);
   SrProgramBatch<T> prog;
   Grid g;
+  SR_HIP_CHECK(hipEventRecord(ctx->ev_f[0], ctx->stream));
   int rc = run_batch<T>(ctx, ds, opset_id, &sub.b, row_idx, n_idx, n_total, loss_kind, SR_MODE_PRED, &prog, &g);
   if (rc != SR_OK) return rc;
+  SR_HIP_CHECK(hipEventRecord(ctx->ev_f[1], ctx->stream));
   const int64_t n_seg = seg_len > 0 ? (n_eval + seg_len - 1) / seg_len : 0;
   SR_HIP_CHECK(ctx->fold_io.ensure(FoldDev<T>::bytes(nb, n_seg)));
   fd->bind(ctx->fold_io.p, nb, n_seg);
@@ -1475,6 +1481,7 @@ int fold_prepare(sr_ctx* ctx, const sr_dataset* ds, int opset_id, const sr_tree_
     SR_HIP_CHECK(sr_launch_fold_segsum<T>(ctx->pred.as<T>(), n_eval, int(nb), static_cast<const T*>(ds->y),
                                           static_cast<const T*>(ds->w), gather ? ctx->row_idx.as<int64_t>() : nullptr,
                                           n_eval, lkind, T(lparam), seg_len, fd->segsum, ctx->stream));
+  SR_HIP_CHECK(hipEventRecord(ctx->ev_f[2], ctx->stream));
   return SR_OK;
 }
 
@@ -1495,13 +1502,19 @@ int fold_finish(sr_ctx* ctx, const sr_dataset* ds, const int64_t* row_idx, int64
   if (seg_len > 0)
     SR_HIP_CHECK(sr_launch_fold_segtab<T>(ctx->pred.as<T>(), n_eval, int(nb), y, w, ri, n_eval, lkind, T(lparam),
                                           seg_len, fd.segsum, with_carry_est ? fd.carry_est : nullptr, fd.tq, fd.tab, s));
+  SR_HIP_CHECK(hipEventRecord(ctx->ev_f[3], s));
   SR_HIP_CHECK(sr_launch_fold<T>(ctx->pred.as<T>(), n_eval, int(nb), y, w, ri, n_eval, lkind, T(lparam), seg_len, fd.tq,
                                  fd.tab, with_carry ? fd.carry : nullptr, fd.out, fd.slow, s));
+  SR_HIP_CHECK(hipEventRecord(ctx->ev_f[4], s));
   std::vector<int> slow(nb, 0);
   SR_HIP_CHECK(hipMemcpyAsync(out, fd.out, nb * sizeof(T), hipMemcpyDeviceToHost, s));
   SR_HIP_CHECK(hipMemcpyAsync(slow.data(), fd.slow, nb * sizeof(int), hipMemcpyDeviceToHost, s));
   SR_HIP_CHECK(hipStreamSynchronize(s));
   for (int v : slow) ctx->fold_slow_last += v;
+  for (int i = 0; i < 4; ++i) {  // (events 0-2 were recorded by fold_prepare on the same stream)
+    float ms = 0.0f;
+    if (hipEventElapsedTime(&ms, ctx->ev_f[i], ctx->ev_f[i + 1]) == hipSuccess) ctx->fold_ms[i] += double(ms);
+  }
   ctx->fold_seg_last = seg_len;
   return SR_OK;
 }
@@ -1641,6 +1654,7 @@ int eval_loss_impl(sr_ctx* ctx, const sr_dataset* ds, int opset_id, const sr_tre
               views ? denoms.data() : nullptr);
   ctx->n_fold_last = int64_t(fold_list.size());
   ctx->fold_slow_last = ctx->fold_seg_last = 0;
+  for (double& v : ctx->fold_ms) v = 0.0;
   for (int v = 0; v < n_views && !fold_list.empty(); ++v) {  // rare: the reference's own fold, in row order (sr_fold.h)
     std::vector<int64_t> fv;
     for (int64_t t : fold_list)
@@ -2624,6 +2638,7 @@ int eval_sharded_impl(sr_ctx* ctx, const sr_dataset* ds, int opset_id, const sr_
     if ((out_complete[t] & 1) && (out_complete[t] & SR_COMP_FOLD)) fold_list.push_back(t);
   ctx->n_fold_last = int64_t(fold_list.size());
   ctx->fold_slow_last = ctx->fold_seg_last = 0;
+  for (double& v : ctx->fold_ms) v = 0.0;
   std::vector<T> fold;
   rc = fold_sharded<T>(ctx, ds, opset_id, trees, loss_kind, fold_list, &fold);
   if (rc != SR_OK) return rc;
@@ -2794,6 +2809,8 @@ int sr_init(int device, sr_ctx** out) {
     if (e == hipSuccess) e = hipEventCreate(&ctx->ev_g0[b]);
     if (e == hipSuccess) e = hipEventCreate(&ctx->ev_g1[b]);
   }
+  for (hipEvent_t& ev : ctx->ev_f)
+    if (e == hipSuccess) e = hipEventCreate(&ev);
   if (e != hipSuccess) {
     delete ctx;
     return set_error(SR_ERR_HIP, std::string("stream/event creation: ") + hipGetErrorString(e));
@@ -2828,6 +2845,7 @@ int sr_shutdown(sr_ctx* ctx) {
       (void)hipEventDestroy(ctx->ev_g0[b]);
       (void)hipEventDestroy(ctx->ev_g1[b]);
     }
+    for (hipEvent_t ev : ctx->ev_f) (void)hipEventDestroy(ev);
     if (ctx->stream2) (void)hipStreamSynchronize(ctx->stream2);
     (void)hipEventDestroy(ctx->ev_join);
     if (ctx->stream2) (void)hipStreamDestroy(ctx->stream2);
@@ -3431,6 +3449,8 @@ int sr_last_phase_ms(sr_ctx* ctx, double* out, int n) {
   if (n > 9) out[9] = double(ctx->n_fold_last);
   if (n > 10) out[10] = double(ctx->fold_slow_last);
   if (n > 11) out[11] = double(ctx->fold_seg_last);
+  for (int i = 0; i < 4; ++i)
+    if (n > 12 + i) out[12 + i] = ctx->fold_ms[i];
   return SR_OK;
 }
 

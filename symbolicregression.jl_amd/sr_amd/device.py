@@ -113,6 +113,12 @@ class DeviceContext:
         _lib.check(_lib.lib.sr_last_phase_ms(self.handle, out, 12))
         return int(out[9]), int(out[10]), int(out[11])
 
+    def last_fold_ms(self):
+        """The last call's in-order loss fold, device ms (HIP events): {pred, segsum, segtab, chain}."""
+        out = (ctypes.c_double * 16)()
+        _lib.check(_lib.lib.sr_last_phase_ms(self.handle, out, 16))
+        return dict(zip(("pred", "segsum", "segtab", "chain"), (float(v) for v in out[12:16])))
+
     def last_grad_info(self):
         """The last gradient call's tangent kernels per bucket (1, 2, 4, 8, 16 tangents): list of dicts
         {kt, kernel_ms, flops, items, rows_per_lane} (csrc: sr_last_grad_info)."""

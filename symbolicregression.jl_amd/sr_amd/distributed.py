@@ -270,8 +270,12 @@ def eval_loss_sharded(trees, shard, options, n_total=None, *, denom=None, group=
     `sr_eval_loss_sharded` call.  Otherwise (CPU tests of the protocol, stand-ins for the GPU calls)
     the protocol runs here over the gloo `group` on host arrays: `partials_fn(tb)` -> this shard's
     packed [5, n_trees] partials (default: the GPU call), `exact_fn(tb, tree_list, max_checks,
-    row_offset)` -> [n_list, max_checks, n_ranges] folds (default: the GPU call); this restatement
-    stops at the overflow rule's bounds (no in-order fold across shards).  A failure on one rank is
+    row_offset)` -> [n_list, max_checks, n_ranges] folds (default: the GPU call).  This host
+    restatement finalizes through `sr_finalize_losses`, which applies only the elementwise +Inf flag
+    (SR_FLAG_ELEMINF): NOT the overflow rule's bounds and NOT the in-order fold of the reference's
+    T-precision loss sum, so a tree whose Float32 fold overflows while its f64 sum stays finite scores
+    finite here but +Inf through the library's own sharded call (use a library
+    communicator for the reference's L(Inf) verdicts).  A failure on one rank is
     all-reduced as an error word, so every rank raises instead of waiting in a collective.  `denom`
     applies to this restatement only (the library divides by the shards' n or Σw)."""
     import torch.distributed as dist
