@@ -835,6 +835,22 @@ def search_lines(args):
                 "best_loss": float(min(m.loss for m in res.pareto_frontier)), "config": desc}
         if name == "c5":
             line["grad_roofline"] = grad_roofline(res, X, y, o)
+            # island sharding at 8 ranks: rank 0's share (islands i % 8 == 0, 4 of 32) —
+            # its islands' rounds and constant optimisation on its own GPU, the head over all islands —
+            # measured in one process without the per-iteration island exchange (a few KB all-gather)
+            progress("search c5: rank 0's share of an 8-rank island-sharded search")
+            share = equation_search(X, y, niterations=args.search_iters, options=o, seed=0, _rank_share=(0, 8))
+            swall = share.wall_s  # (the search loop; the helper engines' start is before it)
+            rate32, rate4 = args.search_iters / res.wall_s, args.search_iters / swall
+            line["projection_8_ranks"] = {
+                "rank0_islands": len(range(0, o.populations, 8)), "rank0_iterations_per_s": rate4,
+                "rank0_device_calls": share.device_calls, "one_gpu_iterations_per_s": rate32,
+                "speedup": rate4 / rate32, "efficiency": rate4 / rate32 / 8.0,
+                "model": ("the 8-rank search runs at the rate of its slowest rank; rank 0's share measured alone "
+                          "(equation_search(_rank_share=(0, 8)): its 4 islands' regularised-evolution rounds and "
+                          "constant optimisation, the other islands imported every iteration as initialised, the "
+                          "head over all 32 islands), without the all-gather itself; rates from the search loops' "
+                          "own wall clocks")}
         sc = SearchScorer(Oracle.from_options(o), X, y, n_threads=cpu_threads)
         t0 = time.perf_counter()
         cres = equation_search(X, y, niterations=cpu_iters, options=o, seed=0, _native_scorer=sc)

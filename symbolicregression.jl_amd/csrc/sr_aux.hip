@@ -221,6 +221,53 @@ __global__ void __launch_bounds__(256) sr_fold_segsum_kernel(SrFoldRows<T> rows,
   if (tid == 0) segsum[int64_t(b) * n_seg + seg] = (s_w[0] + s_w[1]) + (s_w[2] + s_w[3]);
 }
 
+// The step of one loss for the segment tables, in the narrowest exact arithmetic: Float32 losses in
+// Float32 (e 2^-q is exact but for an underflow, which only ever hides a fraction below 1/2; the
+// saturation CAP = 2^26 keeps the counts in int32), Float64 losses in Float64 / int64.
+template <typename T>
+struct SrFoldTab;
+template <>
+struct SrFoldTab<float> {
+  using I = int32_t;
+  static __device__ __forceinline__ void step(float e, int q, I& m, int& kind) {
+    constexpr float CAPF = float(1 << 26);
+    const float t = ldexpf(e, -q);
+    if (!(t < CAPF)) {  // (also NaN / Inf)
+      m = I(1) << 26;
+      kind = 0;
+      return;
+    }
+    const float fl = floorf(t);
+    const float f = t - fl;
+    m = I(fl);
+    kind = f > 0.5f ? 2 : (f == 0.5f ? 1 : 0);
+  }
+};
+template <>
+struct SrFoldTab<double> {
+  using I = int64_t;
+  static __device__ __forceinline__ void step(double e, int q, I& m, int& kind) {
+    const SrFoldStep<double> st = sr_fold_step<double>(e, q, int64_t(1) << 55);
+    m = st.m;
+    kind = st.kind;
+  }
+};
+template <typename I>
+__device__ __forceinline__ void sr_fold_compose_i(I x0, I x1, I& y0, I& y1, I cap) {
+  const I n0 = x0 + ((x0 & 1) ? y1 : y0);
+  const I n1 = x1 + (((1 + x1) & 1) ? y1 : y0);
+  y0 = n0 < cap ? n0 : cap;
+  y1 = n1 < cap ? n1 : cap;
+}
+template <typename I>
+__device__ __forceinline__ void sr_fold_add_i(I m, int kind, I cap, I& a0, I& a1) {
+  // (a0, a1) then the step (m, kind): from start parity b the running value's parity is b + a_b
+  const I e0 = m + (kind == 2 ? 1 : (kind == 1 ? ((a0 + m) & 1) : 0));
+  const I e1 = m + (kind == 2 ? 1 : (kind == 1 ? ((1 + a1 + m) & 1) : 0));
+  a0 = a0 + e0 < cap ? a0 + e0 : cap;
+  a1 = a1 + e1 < cap ? a1 + e1 : cap;
+}
+
 // composed steps of one segment for binades qa and qb: tab[b][seg] = {a0(qa), a1(qa), a0(qb), a1(qb)}
 template <typename T, int R>
 __global__ void __launch_bounds__(256) sr_fold_segtab_kernel(SrFoldRows<T> rows, int64_t pred_ld, int64_t n,
@@ -229,12 +276,13 @@ __global__ void __launch_bounds__(256) sr_fold_segtab_kernel(SrFoldRows<T> rows,
                                                              const double* __restrict__ carry_est,
                                                              int2* __restrict__ tq, int64_t* __restrict__ tab) {
   using Tr = SrFoldTraits<T>;
-  constexpr int64_t CAP = int64_t(1) << (Tr::mant + 3);
+  using I = typename SrFoldTab<T>::I;
+  constexpr I CAP = I(1) << (Tr::mant + 3);
   const int seg = int(blockIdx.x), b = int(blockIdx.y), tid = int(threadIdx.x), lane = tid & 63, wave = tid >> 6;
   SrFoldRows<T> rw = rows;
   rw.pr = rows.pr + int64_t(b) * pred_ld;
   __shared__ double s_d[4];
-  __shared__ int64_t s_v[4][4];
+  __shared__ I s_v[4][4];
   // the f64 prefix before this segment (any order: it only chooses the binades to tabulate)
   const double* ss = segsum + int64_t(b) * n_seg;
   double pre = 0.0;
@@ -244,38 +292,47 @@ __global__ void __launch_bounds__(256) sr_fold_segtab_kernel(SrFoldRows<T> rows,
   __syncthreads();
   const double S = (carry_est ? carry_est[b] : 0.0) + ((s_d[0] + s_d[1]) + (s_d[2] + s_d[3]));
   const int qa = sr_fold_q<T>(S * (1.0 - 0x1p-7)), qb = sr_fold_q<T>(S * (1.0 + 0x1p-7));
+  const bool two = qb != qa;
   const int64_t lo = int64_t(seg) * seg_len, hi = lo + seg_len < n ? lo + seg_len : n;
-  int64_t ta0 = 0, ta1 = 0, tb0 = 0, tb1 = 0;  // the segment so far (meaningful in thread 0)
+  I ta0 = 0, ta1 = 0, tb0 = 0, tb1 = 0;  // the segment so far (meaningful in thread 0)
   for (int64_t base = lo; base < hi; base += 256 * R) {
-    int64_t a0 = 0, a1 = 0, c0 = 0, c1 = 0;  // this thread's R consecutive rows, binades qa and qb
+    I a0 = 0, a1 = 0, c0 = 0, c1 = 0;  // this thread's R consecutive rows, binades qa and qb
     const int64_t r0 = base + int64_t(tid) * R;
+    T ev[R];
+#pragma unroll
+    for (int r = 0; r < R; ++r) ev[r] = (r0 + r < hi) ? rw(r0 + r) : T(0);  // (a zero loss adds nothing)
 #pragma unroll
     for (int r = 0; r < R; ++r) {
-      const T e = (r0 + r < hi) ? rw(r0 + r) : T(0);  // (a zero loss adds nothing)
-      const SrFoldStep<T> sa = sr_fold_step<T>(e, qa, CAP);
-      int64_t e0 = sr_fold_inc<T>(sa, a0 & 1), e1 = sr_fold_inc<T>(sa, (1 + a1) & 1);
-      a0 = a0 + e0 < CAP ? a0 + e0 : CAP;
-      a1 = a1 + e1 < CAP ? a1 + e1 : CAP;
-      if (qb != qa) {
-        const SrFoldStep<T> sb = sr_fold_step<T>(e, qb, CAP);
-        e0 = sr_fold_inc<T>(sb, c0 & 1);
-        e1 = sr_fold_inc<T>(sb, (1 + c1) & 1);
-        c0 = c0 + e0 < CAP ? c0 + e0 : CAP;
-        c1 = c1 + e1 < CAP ? c1 + e1 : CAP;
+      I m;
+      int kind;
+      SrFoldTab<T>::step(ev[r], qa, m, kind);
+      sr_fold_add_i<I>(m, kind, CAP, a0, a1);
+    }
+    if (two) {
+#pragma unroll
+      for (int r = 0; r < R; ++r) {
+        I m;
+        int kind;
+        SrFoldTab<T>::step(ev[r], qb, m, kind);
+        sr_fold_add_i<I>(m, kind, CAP, c0, c1);
       }
     }
     // ordered reduction over the wave's lanes (lane l's rows precede lane l + 1's), then the waves
 #pragma unroll
     for (int off = 1; off < 64; off <<= 1) {
-      int64_t o0 = __shfl_down(a0, off, 64), o1 = __shfl_down(a1, off, 64);
-      int64_t p0 = __shfl_down(c0, off, 64), p1 = __shfl_down(c1, off, 64);
+      I o0 = __shfl_down(a0, off, 64), o1 = __shfl_down(a1, off, 64);
       if ((lane & (2 * off - 1)) == 0) {
-        sr_fold_compose(a0, a1, o0, o1, CAP);
+        sr_fold_compose_i<I>(a0, a1, o0, o1, CAP);
         a0 = o0;
         a1 = o1;
-        sr_fold_compose(c0, c1, p0, p1, CAP);
-        c0 = p0;
-        c1 = p1;
+      }
+      if (two) {
+        I p0 = __shfl_down(c0, off, 64), p1 = __shfl_down(c1, off, 64);
+        if ((lane & (2 * off - 1)) == 0) {
+          sr_fold_compose_i<I>(c0, c1, p0, p1, CAP);
+          c0 = p0;
+          c1 = p1;
+        }
       }
     }
     if (lane == 0) {
@@ -287,13 +344,13 @@ __global__ void __launch_bounds__(256) sr_fold_segtab_kernel(SrFoldRows<T> rows,
     __syncthreads();
     if (tid == 0) {
       for (int v = 0; v < 4; ++v) {
-        int64_t y0 = s_v[v][0], y1 = s_v[v][1];
-        sr_fold_compose(ta0, ta1, y0, y1, CAP);
+        I y0 = s_v[v][0], y1 = s_v[v][1];
+        sr_fold_compose_i<I>(ta0, ta1, y0, y1, CAP);
         ta0 = y0;
         ta1 = y1;
         y0 = s_v[v][2];
         y1 = s_v[v][3];
-        sr_fold_compose(tb0, tb1, y0, y1, CAP);
+        sr_fold_compose_i<I>(tb0, tb1, y0, y1, CAP);
         tb0 = y0;
         tb1 = y1;
       }
@@ -303,10 +360,10 @@ __global__ void __launch_bounds__(256) sr_fold_segtab_kernel(SrFoldRows<T> rows,
   if (tid == 0) {
     const int64_t o = int64_t(b) * n_seg + seg;
     tq[o] = make_int2(qa, qb);
-    tab[4 * o + 0] = ta0;
-    tab[4 * o + 1] = ta1;
-    tab[4 * o + 2] = qb != qa ? tb0 : ta0;
-    tab[4 * o + 3] = qb != qa ? tb1 : ta1;
+    tab[4 * o + 0] = int64_t(ta0);
+    tab[4 * o + 1] = int64_t(ta1);
+    tab[4 * o + 2] = int64_t(two ? tb0 : ta0);
+    tab[4 * o + 3] = int64_t(two ? tb1 : ta1);
   }
 }
 

@@ -243,7 +243,9 @@ struct sr_ctx {
     phase_t = t;
     for (double& v : phase_ms) v = 0.0;
   }
+  bool internal_pass = false;  // the fold's PRED passes: run_batch leaves the call's phase clock alone
   void mark_phase(int i) {
+    if (internal_pass) return;
     const auto now = std::chrono::steady_clock::now();
     phase_ms[i] = std::chrono::duration<double, std::milli>(now - phase_t).count();
     phase_t = now;
@@ -456,6 +458,9 @@ int run_batch(sr_ctx* ctx, const sr_dataset* ds, int opset_id, const sr_tree_bat
               int64_t n_idx, int64_t n_total, int loss_kind, int mode, SrProgramBatch<T>* prog, Grid* grid_out,
               bool allow_derived = false, const ShardCtl* shard = nullptr, const ViewSpec* views = nullptr) {
   const bool gather = row_idx != nullptr && n_idx > 0;
+  // PRED passes (the fold's few band trees) write no partials: more row blocks fill the GPU (C4's 14 trees
+  // x 2^26 rows ran 1,024 workgroups at 256)
+  const int mrb = mode == SR_MODE_PRED ? std::max(ctx->max_row_blocks, 4096) : ctx->max_row_blocks;
   const int64_t n_eval = gather ? n_idx : ds->n;
   if (n_eval <= 0) return set_error(SR_ERR_INVALID_ARG, "no rows to evaluate");
   // several views: one launch, its tree groups view-pure (SrSegment); rows uploaded for every view
@@ -483,7 +488,7 @@ int run_batch(sr_ctx* ctx, const sr_dataset* ds, int opset_id, const sr_tree_bat
   // a wide dataset whose register-stack tile (its rows per lane are twice the classic kernel's) would
   // not fit the LDS runs the classic kernel instead (Float64 with ~40-75 features)
   if (Rv > 0 && make_grid<T>(n_eval, nt > 0 ? nt : 1, Rv, W, int(ds->nf), 0, 0, ds->w != nullptr, ctx->tree_group,
-                             ctx->max_row_blocks).lds > kLdsMax)
+                             mrb).lds > kLdsMax)
     Rv = 0;
   ctx->rows_last = Rv > 0 ? Rv : R;  // (every C2-like tree fits the register stack)
   hipStream_t s = ctx->stream;
@@ -512,11 +517,11 @@ int run_batch(sr_ctx* ctx, const sr_dataset* ds, int opset_id, const sr_tree_bat
   // device + pinned buffers sized for the whole batch up front (a chunk's kernel may still run while
   // the next one is staged): a program has at most one instruction per node
   Grid g0 = make_grid<T>(n_eval, nt > 0 ? nt : 1, R, W, int(ds->nf), 1, 0, ds->w != nullptr, ctx->tree_group,
-                         ctx->max_row_blocks);
+                         mrb);
   int n_rb = g0.n_row_blocks;  // row blocks the partial buffers hold per tree (the most any kernel uses)
   if (Rv > 0)
     n_rb = std::max(n_rb, make_grid<T>(n_eval, nt > 0 ? nt : 1, Rv, W, int(ds->nf), 0, 0, ds->w != nullptr,
-                                       ctx->tree_group, ctx->max_row_blocks).n_row_blocks);
+                                       ctx->tree_group, mrb).n_row_blocks);
   const size_t code_cap = size_t(total_nodes) + 16;
   auto align256 = [](size_t x) { return (x + 255) & ~size_t(255); };
   const size_t o_off = align256(code_cap * sizeof(SrIns<T>));
@@ -770,7 +775,7 @@ int run_batch(sr_ctx* ctx, const sr_dataset* ds, int opset_id, const sr_tree_bat
         auto deal = [&](int64_t p0, int64_t np, int Rc, int depth_c) {
           if (np <= 1) return;
           const Grid gc = make_grid<T>(n_eval, np, Rc, W, int(ds->nf), depth_c, 0, ds->w != nullptr, ctx->tree_group,
-                                       ctx->max_row_blocks);
+                                       mrb);
           const int64_t G = gc.G, ng = gc.n_groups;
           if (ng <= 1) return;
           std::vector<uint32_t> ranked(h_perm + t0 + p0, h_perm + t0 + p0 + np);
@@ -821,7 +826,7 @@ int run_batch(sr_ctx* ctx, const sr_dataset* ds, int opset_id, const sr_tree_bat
     int64_t seg_blocks = 0;
     if (multi && nc > 0) {
       const Grid gm = make_grid<T>(n_eval, nc, R, W, int(ds->nf), depth, 0, ds->w != nullptr, ctx->tree_group,
-                                   ctx->max_row_blocks);
+                                   mrb);
       SrSegment* hs = reinterpret_cast<SrSegment*>(hprog + o_seg);
       for (int64_t p = 0; p < nc;) {
         const int v = views->tree_view[t0 + h_perm[t0 + p]];
@@ -867,7 +872,7 @@ int run_batch(sr_ctx* ctx, const sr_dataset* ds, int opset_id, const sr_tree_bat
     auto launch = [&](int64_t p0, int64_t np, bool vstk) -> int {
       const int Rc = vstk ? Rv : R;
       Grid g = make_grid<T>(n_eval, np, Rc, W, int(ds->nf), vstk ? 0 : depth, 0, ds->w != nullptr, ctx->tree_group,
-                           ctx->max_row_blocks);
+                           mrb);
       if (g.lds > kLdsMax)
         return set_error(SR_ERR_TOO_DEEP, "the row tile (" + std::to_string(ds->nf) + " features, " +
                                               std::to_string(depth) + " stack slots) needs " + std::to_string(g.lds) +
@@ -1391,6 +1396,16 @@ inline int64_t fold_seg_len(const sr_ctx* ctx, int64_t n) {
   return std::min<int64_t>(std::max<int64_t>(L, 8192), 65536);
 }
 
+// The prediction buffer of the fold's PRED passes is kept up to 1/32 of the device memory (9 GB on a
+// 288 GB MI355X: C4's 14 band trees x 2^26 rows are 3.6 GB, and a re-allocation cost the step ~35 ms);
+// anything larger is released after the call.
+inline void release_large_pred(sr_ctx* ctx) {
+  size_t free_b = 0, total_b = 0;
+  const size_t keep = hipMemGetInfo(&free_b, &total_b) == hipSuccess ? std::max(total_b / 32, size_t(2) << 30)
+                                                                       : (size_t(2) << 30);
+  if (ctx->pred.cap > keep) ctx->pred.release();
+}
+
 // Device scratch of one fold batch of nb trees and n_seg segments (ctx->fold_io): segment sums,
 // binades and composed steps, carries, estimates, results and slow-segment counts.
 template <typename T>
@@ -1436,8 +1451,10 @@ struct KeepCallInfo {
       : c(x), timing(x->timing), n_chunks(x->n_chunks_last), n_derived(x->n_derived_last), rows(x->rows_last),
         timed(x->timed_last), derived(x->derived_last) {
     x->timing = 0;
+    x->internal_pass = true;
   }
   ~KeepCallInfo() {
+    c->internal_pass = false;
     c->timing = timing;
     c->n_chunks_last = n_chunks;
     c->n_derived_last = n_derived;
@@ -1542,7 +1559,7 @@ int fold_exact(sr_ctx* ctx, const sr_dataset* ds, int opset_id, const sr_tree_ba
     rc = fold_finish<T>(ctx, ds, row_idx, n_idx, loss_kind, nb, seg_len, fd, false, false, out->data() + b0);
     if (rc != SR_OK) return rc;
   }
-  if (ctx->pred.cap > (size_t(2) << 30)) ctx->pred.release();  // (large prediction passes: not kept)
+  release_large_pred(ctx);
   return SR_OK;
 }
 
@@ -2481,7 +2498,7 @@ int fold_sharded(sr_ctx* ctx, const sr_dataset* ds, int opset_id, const sr_tree_
     }
     std::copy(carry.begin(), carry.end(), out->begin() + ptrdiff_t(b0));
   }
-  if (ctx->pred.cap > (size_t(2) << 30)) ctx->pred.release();
+  release_large_pred(ctx);
   // a failure after the last gather: the ranks agree on it (the weights' sum gather may follow)
   return agree(ctx, pending, "failed in the loss fold");
 }

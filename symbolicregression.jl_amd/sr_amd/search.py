@@ -337,7 +337,7 @@ def _torch_comm():
 
 def equation_search(X=None, y=None, *, niterations=10, options, weights=None, search_options=None, seed=0,
                     verbosity=0, dataset=None, distributed=False, scoring_lanes=4, _loss_fn=None, _grad_fn=None,
-                    _native_scorer=None):
+                    _native_scorer=None, _rank_share=None):
     """Batched-island ``equation_search`` (src/SymbolicRegression.jl:967-1216) -> SearchResult.
 
     distributed=True (torch.distributed initialised, one process per GPU; SURVEY §8(e) island
@@ -348,30 +348,53 @@ def equation_search(X=None, y=None, *, niterations=10, options, weights=None, se
     so device round trips overlap; results do not depend on it (num_evals up to rounding).
     ``_loss_fn`` / ``_grad_fn`` replace the device scorer with CPU callbacks (tests only);
     ``_native_scorer`` (an object with ``loss_addr``, ``grad_addr``, ``user``: C callbacks) likewise,
-    without Python in the loop (bench.py's CPU baseline)."""
+    without Python in the loop (bench.py's CPU baseline).
+    ``_rank_share=(r, N)`` (bench.py's island-sharding projection, one process): the engine of rank r
+    of N — it advances only its own islands i % N == r and runs the head over all of them; the other
+    ranks' islands are imported every iteration as they were initialised (helper engines started before
+    the timed loop): the per-rank work of an N-rank search without the all-gather itself."""
     so = search_options or SearchOptions()
     comm = _torch_comm() if distributed else None
     rank, world, allgather = comm if comm else (0, 1, None)
+    if _rank_share is not None:
+        if comm:
+            raise ValueError("_rank_share is a one-process measurement")
+        rank, world = int(_rank_share[0]), int(_rank_share[1])
     if dataset is None:
         dataset = Dataset(np.asarray(X), np.asarray(y), weights=weights)
-    eng = NativeSearch(dataset, options, so, seed, rank, world)
-    if _native_scorer is not None:
-        eng.use_native_callbacks(_native_scorer.loss_addr, _native_scorer.grad_addr, _native_scorer.user)
-    elif _loss_fn is not None:
-        eng.use_callbacks(_loss_fn, _grad_fn)
-    else:
-        from .device import get_lane_context
+    def scorer(e, lanes):
+        if _native_scorer is not None:
+            e.use_native_callbacks(_native_scorer.loss_addr, _native_scorer.grad_addr, _native_scorer.user)
+        elif _loss_fn is not None:
+            e.use_callbacks(_loss_fn, _grad_fn)
+        else:
+            from .device import get_lane_context
 
-        eng.use_device(dataset)
-        n_own = len(range(rank, options.populations, world))
-        for lane in range(1, max(1, min(int(scoring_lanes), n_own))):
-            eng.add_device(dataset, get_lane_context(lane))
+            e.use_device(dataset)
+            for lane in range(1, lanes):
+                e.add_device(dataset, get_lane_context(lane))
+
+    eng = NativeSearch(dataset, options, so, seed, rank, world)
+    scorer(eng, max(1, min(int(scoring_lanes), len(range(rank, options.populations, world)))))
+    stale = []
+    if _rank_share is not None and world > 1:
+        for r in range(world):
+            if r != rank:
+                h = NativeSearch(dataset, options, so, seed, r, world)
+                scorer(h, 1)
+                h.start(niterations)
+                stale.append(h.export())
+                del h
+        allgather = lambda part: [part] + stale  # noqa: E731  (this rank's own part first: skipped below)
+        rank_in_gather = 0
+    else:
+        rank_in_gather = rank
 
     def exchange():
-        if world == 1:
+        if world == 1 or allgather is None:
             return
         for r, part in enumerate(allgather(eng.export())):
-            if r != rank:
+            if r != rank_in_gather:
                 eng.import_(part)
 
     t0 = time.perf_counter()
@@ -390,7 +413,7 @@ def equation_search(X=None, y=None, *, niterations=10, options, weights=None, se
     inf = eng.info()
     info = dict(num_evals=inf.num_evals, calls=inf.device_calls, dev=inf.device_ms, host=inf.host_ms,
                 kernel=inf.kernel_ms)
-    if world > 1:
+    if world > 1 and allgather is not None and not stale:
         parts = allgather(info)
         info = {k: sum(p[k] for p in parts) for k in info}
     info_base = eng.info()
