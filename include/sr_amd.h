@@ -424,8 +424,9 @@ int sr_optimize_constants_callbacks(int dtype, const sr_tree_batch* trees, const
 /* Timing of the last device call on this context (ms): kernel-only, via HIP events. */
 int sr_last_kernel_ms(sr_ctx* ctx, double* eval_ms, double* total_ms);
 
-/* Host-side phases of the last sr_eval_loss_batch call (ms, wall clock), up to n of: compile,
- * upload + launch, wait for the interpreter + reduction, exact-sum pass, finalize; out[5] (n >= 6)
+/* Host-side phases of the last sr_eval_loss_batch / sr_eval_loss_sharded call (ms, wall clock), up to
+ * n of: compile, upload + launch, wait for the interpreter + reduction (sharded: + the all-reduce),
+ * exact-sum pass, finalize (with the in-order loss fold of sr_fold.h, when any); out[5] (n >= 6)
  * = the number of interpreter launches of the call (the batch is compiled and launched in chunks),
  * out[6] (n >= 7) = device time of the exact-sum pass (ms), out[7] (n >= 8) = rows per lane of its
  * interpreter kernel, out[8] (n >= 9) = the device-busy time of those launches: the UNION of their

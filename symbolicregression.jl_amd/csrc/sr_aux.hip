@@ -3,6 +3,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <type_traits>
+
 #include "sr_eval.h"
 #include "sr_fold.h"
 
@@ -190,6 +192,40 @@ struct SrFoldRows {  // the listed tree's elementwise losses (the interpreter's 
     if (w) e *= w[ri];
     return e;
   }
+  // R consecutive losses from row r0 (rows >= hi: 0, which adds nothing).  A full, 16-byte aligned run
+  // of a full view is read with 16-byte loads: a thread's R rows are contiguous, so one scalar load per
+  // row would make every load instruction touch 64 cache lines (one per lane)
+  template <int R>
+  __device__ __forceinline__ void rows_from(int64_t r0, int64_t hi, T (&ev)[R]) const {
+    constexpr int C = 16 / int(sizeof(T));
+    using V = typename std::conditional<sizeof(T) == 4, float4, double2>::type;
+    const bool vec = !row_idx && r0 + R <= hi && ((reinterpret_cast<uintptr_t>(pr + r0) | reinterpret_cast<uintptr_t>(y + r0) |
+                                                  (w ? reinterpret_cast<uintptr_t>(w + r0) : 0)) & 15u) == 0;
+    if (vec) {
+#pragma unroll
+      for (int c = 0; c < R / C; ++c) {
+        const V pv = *reinterpret_cast<const V*>(pr + r0 + c * C);
+        const V yv = *reinterpret_cast<const V*>(y + r0 + c * C);
+        const T* pp = reinterpret_cast<const T*>(&pv);
+        const T* yy = reinterpret_cast<const T*>(&yv);
+        T wv[C];
+        if (w) {
+          const V wq = *reinterpret_cast<const V*>(w + r0 + c * C);
+#pragma unroll
+          for (int j = 0; j < C; ++j) wv[j] = reinterpret_cast<const T*>(&wq)[j];
+        }
+#pragma unroll
+        for (int j = 0; j < C; ++j) {
+          T e = sr_elem_loss<T>(lk, pp[j], yy[j], lp);
+          if (w) e *= wv[j];
+          ev[c * C + j] = e;
+        }
+      }
+    } else {
+#pragma unroll
+      for (int r = 0; r < R; ++r) ev[r] = (r0 + r < hi) ? (*this)(r0 + r) : T(0);
+    }
+  }
 };
 
 // binade spacing exponent q of a value >= 0 (subnormals and 0: the fixed subnormal spacing); values
@@ -299,8 +335,7 @@ __global__ void __launch_bounds__(256) sr_fold_segtab_kernel(SrFoldRows<T> rows,
     I a0 = 0, a1 = 0, c0 = 0, c1 = 0;  // this thread's R consecutive rows, binades qa and qb
     const int64_t r0 = base + int64_t(tid) * R;
     T ev[R];
-#pragma unroll
-    for (int r = 0; r < R; ++r) ev[r] = (r0 + r < hi) ? rw(r0 + r) : T(0);  // (a zero loss adds nothing)
+    rw.template rows_from<R>(r0, hi, ev);
 #pragma unroll
     for (int r = 0; r < R; ++r) {
       I m;
@@ -400,10 +435,10 @@ __device__ void sr_fold_range(const SrFoldRows<T>& elem, int64_t hi, T* s_p, int
     // this thread's R consecutive losses and their composed step
     const int64_t base = k + int64_t(tid) * R;
     T ev[R];
+    elem.template rows_from<R>(base, hi, ev);
     int64_t a0 = 0, a1 = 0;
 #pragma unroll
     for (int r = 0; r < R; ++r) {
-      ev[r] = (base + r < hi) ? elem(base + r) : T(0);  // (a zero loss adds nothing)
       const SrFoldStep<T> st = sr_fold_step<T>(ev[r], q, CAP);
       int64_t e0 = sr_fold_inc<T>(st, (0 + a0) & 1), e1 = sr_fold_inc<T>(st, (1 + a1) & 1);
       a0 = a0 + e0 < CAP ? a0 + e0 : CAP;

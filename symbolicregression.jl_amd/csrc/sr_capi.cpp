@@ -2649,6 +2649,7 @@ int eval_sharded_impl(sr_ctx* ctx, const sr_dataset* ds, int opset_id, const sr_
     out_complete[t] = uint8_t((out_complete[t] & ~3) | (list_ok[i] ? 1 : 0));
     if (!list_ok[i]) out_loss[t] = T(INFINITY);
   }
+  ctx->mark_phase(3);
   // 6. rarer: the loss fold in row order across the shards (sr_fold.h)
   std::vector<int64_t> fold_list;
   for (int64_t t = 0; t < nt; ++t)
@@ -2668,7 +2669,7 @@ int eval_sharded_impl(sr_ctx* ctx, const sr_dataset* ds, int opset_id, const sr_
   }
   for (size_t i = 0; i < fold_list.size(); ++i) out_loss[fold_list[i]] = T(fold[i] / fden);
   for (int64_t t = 0; t < nt; ++t) out_complete[t] &= 1;
-  ctx->mark_phase(3);
+  ctx->mark_phase(4);
   ctx->last_total_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
   return SR_OK;
 }
