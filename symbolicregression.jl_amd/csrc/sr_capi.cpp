@@ -162,6 +162,21 @@ struct sr_ctx {
   // buffer with the same layout (code | offsets | static_bad | launch order), so a single-chunk call
   // uploads with one DMA; per-tree {Σ loss, flags} likewise share one allocation (one DMA back)
   HostBuf h_prog, h_outs, h_grad;  // (h_grad: the gradient call's staging image, then its results)
+  // Small calls with several row blocks (round 5, SR_AMD_HOST_REDUCE / "host_reduce", default on): the
+  // interpreter writes its per-(row block, tree) partials straight into pinned host memory (h_part)
+  // and the host reduces them after the one stream synchronisation, in the reduce kernel's own order
+  // (sr_reduce_positions: lane l folds row blocks l, l + 64, ...; a shfl_xor butterfly over the 64
+  // lanes), so the bits are the reduce launch's; a C3 scoring call loses that launch and its gap.
+  int host_reduce = 1;
+  HostBuf h_part;
+  struct HostReduction {
+    int64_t p0, np;
+    int n_rb;
+  };
+  std::vector<HostReduction> host_reductions;  // this call's launches whose partials await the host
+  int64_t host_red_rb = 0;                     // their partial buffer's row-block stride (n_rb)
+  const uint8_t* h_bad_last = nullptr;         // the last run_batch's staged static flags and launch order
+  const uint32_t* h_perm_last = nullptr;
   void* d_code = nullptr;
   uint32_t* d_off = nullptr;
   uint8_t* d_bad = nullptr;
@@ -556,6 +571,10 @@ int run_batch(sr_ctx* ctx, const sr_dataset* ds, int opset_id, const sr_tree_bat
   const bool host_prog = small_call && ctx->host_io >= 2;
   if (host_out) SR_HIP_CHECK(ctx->h_outs.ensure(outs_bytes, s, ctx->stream2));
   ctx->outs_on_host = host_out;
+  const bool host_red = host_out && ctx->host_reduce && !multi && n_rb > 1;
+  ctx->host_reductions.clear();
+  ctx->host_red_rb = n_rb;
+  if (host_red) SR_HIP_CHECK(ctx->h_part.ensure(n_part * (sizeof(double) + sizeof(uint32_t)) + 16, s, ctx->stream2));
   ctx->d_out_sum = reinterpret_cast<double*>(host_out ? ctx->h_outs.as<char>() : ctx->outs.as<char>());
   ctx->d_out_flag = reinterpret_cast<uint32_t*>((host_out ? ctx->h_outs.as<char>() : ctx->outs.as<char>()) +
                                                 ctx->outs_flag_off);
@@ -638,6 +657,8 @@ int run_batch(sr_ctx* ctx, const sr_dataset* ds, int opset_id, const sr_tree_bat
   uint32_t* h_off = reinterpret_cast<uint32_t*>(hprog + o_off);
   uint8_t* h_bad = reinterpret_cast<uint8_t*>(hprog + o_bad);
   uint32_t* h_perm = reinterpret_cast<uint32_t*>(hprog + o_perm);
+  ctx->h_bad_last = h_bad;
+  ctx->h_perm_last = h_perm;
   uint32_t* h_end = reinterpret_cast<uint32_t*>(hprog + o_end);
   ctx->n_chunks_last = 0;
   ctx->derived_last = false;
@@ -906,8 +927,9 @@ int run_batch(sr_ctx* ctx, const sr_dataset* ds, int opset_id, const sr_tree_bat
       a.track_x = !(max_abs_x < double(a.tbig)) ? 1 : 0;
       a.loss_kind = lkind;
       a.loss_param = T(lparam);
-      a.part_sum = ctx->part_sum.as<double>() + size_t(n_rb) * size_t(t0 + p0);
-      a.part_flag = ctx->part_flag.as<uint32_t>() + size_t(n_rb) * size_t(t0 + p0);
+      a.part_sum = (host_red ? ctx->h_part.as<double>() : ctx->part_sum.as<double>()) + size_t(n_rb) * size_t(t0 + p0);
+      a.part_flag = (host_red ? reinterpret_cast<uint32_t*>(ctx->h_part.as<double>() + n_part)
+                              : ctx->part_flag.as<uint32_t>()) + size_t(n_rb) * size_t(t0 + p0);
       a.pred = ctx->pred.as<T>();
       a.pred_ld = n_eval;
       // LDS program cache (register-stack launches: 4 workgroups per CU leave ~36 KiB of dynamic LDS
@@ -942,7 +964,7 @@ int run_batch(sr_ctx* ctx, const sr_dataset* ds, int opset_id, const sr_tree_bat
         a.static_bad = ctx->d_bad + t0;
       }
       // several row blocks: the last workgroup of each tree group reduces it (no reduce launch)
-      const bool fused = !direct && mode == SR_MODE_LOSS && ctx->fused_reduce > 0 &&
+      const bool fused = !direct && !host_red && mode == SR_MODE_LOSS && ctx->fused_reduce > 0 &&
                          int64_t(g.G) * int64_t(g.n_row_blocks) <= ctx->fused_reduce;
       if (fused) {
         a.group_cnt = ctx->group_cnt.as<uint32_t>() + t0 + p0;
@@ -989,7 +1011,9 @@ int run_batch(sr_ctx* ctx, const sr_dataset* ds, int opset_id, const sr_tree_bat
       a.stamps = ctx->stamps.as<uint64_t>();
 #endif
       SR_HIP_CHECK(sr_launch_eval<T>(a, mode, gather, tier, Rc, g.W, vstk, int(n_blocks), cs));
-      if (!direct && !fused)
+      if (!direct && !fused && host_red)
+        ctx->host_reductions.push_back({t0 + p0, np, g.n_row_blocks});
+      else if (!direct && !fused)
         SR_HIP_CHECK(sr_launch_reduce(a.part_sum, a.part_flag, int(np), g.n_row_blocks, a.perm,
                                     ctx->d_bad + t0, ctx->d_out_sum + t0, ctx->d_out_flag + t0, cs));
       return SR_OK;
@@ -1580,6 +1604,47 @@ T jl_sum_T(const double* v, const int64_t* idx, int64_t lo, int64_t hi) {  // in
   return x + y;
 }
 
+// The partials of the call's launches (ctx->host_reductions) reduced on the host into {Σ, flags}, in
+// sr_reduce_positions' order: lane l sums row blocks l, l + 64, ... from 0.0, then for off = 32 .. 1 every
+// lane adds its partner l ^ off (IEEE addition commutes, so both partners hold the same bits), lane 0's
+// value is the result; flags ORed; the static flags from the staging image.
+void host_reduce_partials(sr_ctx* ctx, int64_t nt) {
+  const size_t n_part = size_t(nt) * size_t(ctx->host_red_rb);
+  const double* ps = ctx->h_part.as<double>();
+  const uint32_t* pf = reinterpret_cast<const uint32_t*>(ps + n_part);
+  double* out_sum = ctx->h_outs.as<double>();
+  uint32_t* out_flag = reinterpret_cast<uint32_t*>(ctx->h_outs.as<char>() + ctx->outs_flag_off);
+  const uint32_t* perm = ctx->h_perm_last;
+  const uint8_t* bad = ctx->h_bad_last;
+  for (const sr_ctx::HostReduction& hr : ctx->host_reductions) {
+    const double* s0 = ps + size_t(ctx->host_red_rb) * size_t(hr.p0);
+    const uint32_t* f0 = pf + size_t(ctx->host_red_rb) * size_t(hr.p0);
+    for (int64_t pos = 0; pos < hr.np; ++pos) {
+      double v[64];
+      uint32_t fl = 0;
+      for (int l = 0; l < 64; ++l) {
+        double a = 0.0;
+        for (int i = l; i < hr.n_rb; i += 64) {
+          const size_t o = size_t(i) * size_t(hr.np) + size_t(pos);
+          a += s0[o];
+          fl |= f0[o];
+        }
+        v[l] = a;
+      }
+      for (int off = 32; off >= 1; off >>= 1) {
+        double nv[64];
+        for (int l = 0; l < 64; ++l) nv[l] = v[l] + v[l ^ off];
+        std::memcpy(v, nv, sizeof(v));
+      }
+      const uint32_t tree = perm[hr.p0 + pos];
+      if (bad[tree]) fl |= SR_FLAG_STATIC | SR_FLAG_NONFINITE;
+      out_sum[tree] = v[0];
+      out_flag[tree] = fl;
+    }
+  }
+  ctx->host_reductions.clear();
+}
+
 template <typename T>
 double view_denominator(const sr_dataset* ds, const int64_t* row_idx, int64_t n_idx) {
   const bool gather = row_idx != nullptr && n_idx > 0;
@@ -1632,6 +1697,7 @@ int eval_loss_impl(sr_ctx* ctx, const sr_dataset* ds, int opset_id, const sr_tre
   } else {
     SR_HIP_CHECK(hipStreamSynchronize(s));
   }
+  if (!ctx->host_reductions.empty()) host_reduce_partials(ctx, nt);
   const double* hs = ctx->h_outs.as<double>();
   const uint32_t* hf = reinterpret_cast<const uint32_t*>(ctx->h_outs.as<char>() + ctx->outs_flag_off);
   std::vector<double> sums(hs, hs + nt);
@@ -2797,6 +2863,7 @@ int sr_init(int device, sr_ctx** out) {
   if (const char* v = std::getenv("SR_AMD_CHUNKS")) ctx->chunks = std::atoi(v);
   if (const char* v = std::getenv("SR_AMD_PROBE")) ctx->probe = std::atoi(v);
   if (const char* v = std::getenv("SR_AMD_FOLD_SEG")) ctx->fold_seg = std::atoll(v);
+  if (const char* v = std::getenv("SR_AMD_HOST_REDUCE")) ctx->host_reduce = std::atoi(v);
   if (const char* v = std::getenv("SR_AMD_STRESS_PROBE")) ctx->stress_probe = std::atoi(v);
   if (const char* v = std::getenv("SR_AMD_CODE_CACHE")) ctx->code_cache = std::atoi(v);
   if (const char* v = std::getenv("SR_AMD_FUSED_REDUCE")) ctx->fused_reduce = std::atoll(v);
@@ -2854,7 +2921,7 @@ int sr_shutdown(sr_ctx* ctx) {
                       &ctx->hint, &ctx->jsum_prog, &ctx->jsum_fin, &ctx->jsum_scratch, &ctx->probe_sum, &ctx->probe_flag, &ctx->g_code, &ctx->g_offsets, &ctx->g_consts, &ctx->g_const_off,
                       &ctx->g_items, &ctx->g_part, &ctx->g_out, &ctx->derived_cols, &ctx->probe_derived, &ctx->coll_buf, &ctx->coll_packed, &ctx->ctl, &ctx->fold_io, &ctx->group_cnt})
       b->release();
-    for (HostBuf* b : {&ctx->h_prog, &ctx->h_outs, &ctx->h_grad, &ctx->h_coll}) b->release();
+    for (HostBuf* b : {&ctx->h_prog, &ctx->h_outs, &ctx->h_grad, &ctx->h_coll, &ctx->h_part}) b->release();
     for (int c = 0; c < kMaxChunks; ++c) {
       (void)hipEventDestroy(ctx->ev_c0[c]);
       (void)hipEventDestroy(ctx->ev_c1[c]);
@@ -3495,6 +3562,10 @@ int sr_set_tuning(sr_ctx* ctx, const char* name, int64_t value) {
   }
   if (std::strcmp(name, "grad_rows") == 0) {  // gradient kernel rows per lane (SR_AMD_GRAD_ROWS; 0: automatic)
     ctx->grad_rows_force = int(value);
+    return SR_OK;
+  }
+  if (std::strcmp(name, "host_reduce") == 0) {  // small calls' partials reduced on the host (SR_AMD_HOST_REDUCE)
+    ctx->host_reduce = value != 0 ? 1 : 0;
     return SR_OK;
   }
   if (std::strcmp(name, "fused_reduce") == 0) {  // in-launch partial reduction bound (SR_AMD_FUSED_REDUCE)

@@ -198,8 +198,9 @@ def test_probe_modes_change_nothing(dtype):
 @pytest.mark.parametrize("dtype,n_rows,n_trees", [(np.float32, 100_000, 31), (np.float64, 100, 40), (np.float32, 3000, 300)])
 def test_small_call_latency_options_change_nothing(dtype, n_rows, n_trees):
     """The search's call shapes under the latency options: programs read by the kernel from pinned
-    host memory ("host_io" 2), the LDS program cache in the classic kernel ("code_cache" 2), and the
-    partial reduction in a separate launch ("fused_reduce" 0): losses and flags bit for bit equal."""
+    host memory ("host_io" 2), the LDS program cache in the classic kernel ("code_cache" 2), the
+    partial reduction in a separate launch ("fused_reduce" 0) or on the host from partials the kernel
+    wrote into pinned memory ("host_reduce" 1, round 5's default): losses and flags bit for bit equal."""
     import sr_amd
     from sr_amd import Dataset, eval_loss_batch, flatten_trees, gen_random_population
 
@@ -212,15 +213,18 @@ def test_small_call_latency_options_change_nothing(dtype, n_rows, n_trees):
     ctx = sr_amd.get_context()
     res = []
     try:
-        for host_io, cache, fused in ((1, 1, 1 << 30), (2, 1, 1 << 30), (2, 2, 1 << 30), (1, 2, 0), (0, 1, 0)):
+        for host_io, cache, fused, hred in ((1, 1, 1 << 30, 0), (2, 1, 1 << 30, 0), (2, 2, 1 << 30, 0), (1, 2, 0, 0),
+                                            (0, 1, 0, 0), (1, 1, 0, 1), (2, 2, 0, 1), (0, 1, 0, 1)):
             ctx.set_tuning("host_io", host_io)
             ctx.set_tuning("code_cache", cache)
             ctx.set_tuning("fused_reduce", fused)
+            ctx.set_tuning("host_reduce", hred)
             res.append(eval_loss_batch(tb, ds, opts))
     finally:
         ctx.set_tuning("host_io", 1)
         ctx.set_tuning("code_cache", 1)
         ctx.set_tuning("fused_reduce", 0)
+        ctx.set_tuning("host_reduce", 1)
     l0, c0 = res[0]
     assert c0.mean() > 0.2
     for l1, c1 in res[1:]:
