@@ -13,3 +13,4 @@ for pass in 1 2; do
     SR_AMD_HOST_REDUCE=$hr timeout -k 10 300 python3 tools/search_ab.py C3 C5 share >> $OUT 2>> gpurun_out/${TAG}_search_ab.err || exit $?
   done
 done
+timeout -k 10 300 python3 tools/share_probe.py > gpurun_out/${TAG}_share_probe.jsonl 2> gpurun_out/${TAG}_share_probe.err || exit $?
