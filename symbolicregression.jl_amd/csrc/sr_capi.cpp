@@ -924,6 +924,10 @@ int run_batch(sr_ctx* ctx, const sr_dataset* ds, int opset_id, const sr_tree_bat
       a.stack_depth = vstk ? std::min(depth, SR_VSTK_SLOTS) : depth;  // (the register-stack trees need <= SR_VSTK_SLOTS)
       // Σ over n_total rows of values below tbig cannot overflow T, even with rounding slack.
       a.tbig = T(t_max<T>() / (2.0 * double(n_total > 0 ? n_total : 1)));
+      {  // the view's padded rows over every shard: n_total + at most one 2048-row tile of padding per shard
+        const double padded = double(n_total > 0 ? n_total : 1) + 2048.0 * double(shard ? ctx->comm_ranks : 1);
+        a.big_budget = 64.0 * t_max<T>() / (1.01 * padded);
+      }
       a.track_x = !(max_abs_x < double(a.tbig)) ? 1 : 0;
       a.loss_kind = lkind;
       a.loss_param = T(lparam);

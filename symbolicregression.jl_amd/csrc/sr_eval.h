@@ -111,6 +111,9 @@ struct SrEvalArgs {
   int code_lds;                // LOSS: instructions of LDS program cache per workgroup (0: windows
                                // stream from global memory); a group whose span exceeds it streams too
   T tbig;                      // |v| >= tbig may overflow the array-sum check
+  double big_budget;           // a tile holding |v| >= tbig is BIG only when its lanes' Σ max|v| passes this
+                               // (64 x floatmax / (1.01 x the view's padded rows, every shard)): below it,
+                               // no checked array's Julia-order sum can reach floatmax (sr_tile_impl.h)
   int track_x;                 // the data holds |x| >= tbig or non-finite values: checked feature
                                // loads join the deferred checks (FAST path)
   int loss_kind;               // SrLossKind

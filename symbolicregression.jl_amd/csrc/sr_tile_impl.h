@@ -1259,7 +1259,16 @@ __global__ void __launch_bounds__(W * 64, (SrMinWavesFor<T, R, TIER, W, VSTK, LK
               if (sr_ballot(nan_root || !(mrun <= SrM<T>::big))) {
                 dead = true;
               } else if (sr_ballot(!(mrun < tbig))) {
-                susp_any = true;
+                // (rare) a value >= tbig: DynamicExpressions' isfinite(sum(x)) of some checked array may
+                // fail.  Every tracked array x has Σ_rows |x_i| <= Σ over tiles of R Σ_lanes mrun, and a
+                // Julia-order sum of it stays below Σ|x_i| (1 + u)^1044 (leaf folds of < 1024, <= 20
+                // pairwise levels); a tile within its share of floatmax — R Σ_lanes mrun <= 64 R x
+                // floatmax / (1.01 x padded rows), i.e. Σ_lanes mrun <= big_budget — cannot make any
+                // sum reach it, so only a tile past its share sends the tree to the exact pass (round 5:
+                // C2's typical BIG tree, one huge row per tile, no longer pays that pass).  Untracked
+                // feature rows are < tbig, their sums < floatmax / 2 on their own.
+                const double msum = sr_wave_sum<double>(double(mrun));
+                if (!(msum <= a.big_budget)) susp_any = true;
               }
             }
             if (!dead) {
