@@ -162,12 +162,15 @@ struct sr_ctx {
   // buffer with the same layout (code | offsets | static_bad | launch order), so a single-chunk call
   // uploads with one DMA; per-tree {Σ loss, flags} likewise share one allocation (one DMA back)
   HostBuf h_prog, h_outs, h_grad;  // (h_grad: the gradient call's staging image, then its results)
-  // Small calls with several row blocks (round 5, SR_AMD_HOST_REDUCE / "host_reduce", default on): the
+  // Small calls with several row blocks (round 5, SR_AMD_HOST_REDUCE / "host_reduce"): the
   // interpreter writes its per-(row block, tree) partials straight into pinned host memory (h_part)
   // and the host reduces them after the one stream synchronisation, in the reduce kernel's own order
   // (sr_reduce_positions: lane l folds row blocks l, l + 64, ...; a shfl_xor butterfly over the 64
   // lanes), so the bits are the reduce launch's; a C3 scoring call loses that launch and its gap.
-  int host_reduce = 1;
+  // The bound is on the call's partials (trees x row blocks): a C3 / C5 scoring call has ~1,600; a
+  // 1,250-tree x 256-row-block call (320k partials) wrote 3.8 MB over PCIe and spent ~1 ms reducing on
+  // the host (tools/share_probe.py: 2.47 ms per call against 1.1 with the reduce launch).
+  int64_t host_reduce = 8192;
   HostBuf h_part;
   struct HostReduction {
     int64_t p0, np;
@@ -571,7 +574,7 @@ int run_batch(sr_ctx* ctx, const sr_dataset* ds, int opset_id, const sr_tree_bat
   const bool host_prog = small_call && ctx->host_io >= 2;
   if (host_out) SR_HIP_CHECK(ctx->h_outs.ensure(outs_bytes, s, ctx->stream2));
   ctx->outs_on_host = host_out;
-  const bool host_red = host_out && ctx->host_reduce && !multi && n_rb > 1;
+  const bool host_red = host_out && ctx->host_reduce > 0 && !multi && n_rb > 1 && int64_t(n_part) <= ctx->host_reduce;
   ctx->host_reductions.clear();
   ctx->host_red_rb = n_rb;
   if (host_red) SR_HIP_CHECK(ctx->h_part.ensure(n_part * (sizeof(double) + sizeof(uint32_t)) + 16, s, ctx->stream2));
@@ -2867,7 +2870,7 @@ int sr_init(int device, sr_ctx** out) {
   if (const char* v = std::getenv("SR_AMD_CHUNKS")) ctx->chunks = std::atoi(v);
   if (const char* v = std::getenv("SR_AMD_PROBE")) ctx->probe = std::atoi(v);
   if (const char* v = std::getenv("SR_AMD_FOLD_SEG")) ctx->fold_seg = std::atoll(v);
-  if (const char* v = std::getenv("SR_AMD_HOST_REDUCE")) ctx->host_reduce = std::atoi(v);
+  if (const char* v = std::getenv("SR_AMD_HOST_REDUCE")) ctx->host_reduce = std::atoll(v);
   if (const char* v = std::getenv("SR_AMD_STRESS_PROBE")) ctx->stress_probe = std::atoi(v);
   if (const char* v = std::getenv("SR_AMD_CODE_CACHE")) ctx->code_cache = std::atoi(v);
   if (const char* v = std::getenv("SR_AMD_FUSED_REDUCE")) ctx->fused_reduce = std::atoll(v);
@@ -3568,8 +3571,8 @@ int sr_set_tuning(sr_ctx* ctx, const char* name, int64_t value) {
     ctx->grad_rows_force = int(value);
     return SR_OK;
   }
-  if (std::strcmp(name, "host_reduce") == 0) {  // small calls' partials reduced on the host (SR_AMD_HOST_REDUCE)
-    ctx->host_reduce = value != 0 ? 1 : 0;
+  if (std::strcmp(name, "host_reduce") == 0) {  // largest call (trees x row blocks) reduced on the host (SR_AMD_HOST_REDUCE)
+    ctx->host_reduce = value < 0 ? 0 : value;
     return SR_OK;
   }
   if (std::strcmp(name, "fused_reduce") == 0) {  // in-launch partial reduction bound (SR_AMD_FUSED_REDUCE)

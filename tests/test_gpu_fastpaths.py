@@ -200,7 +200,8 @@ def test_small_call_latency_options_change_nothing(dtype, n_rows, n_trees):
     """The search's call shapes under the latency options: programs read by the kernel from pinned
     host memory ("host_io" 2), the LDS program cache in the classic kernel ("code_cache" 2), the
     partial reduction in a separate launch ("fused_reduce" 0) or on the host from partials the kernel
-    wrote into pinned memory ("host_reduce" 1, round 5's default): losses and flags bit for bit equal."""
+    wrote into pinned memory ("host_reduce": by default for calls of <= 8192 partials): losses and flags
+    bit for bit equal."""
     import sr_amd
     from sr_amd import Dataset, eval_loss_batch, flatten_trees, gen_random_population
 
@@ -214,7 +215,7 @@ def test_small_call_latency_options_change_nothing(dtype, n_rows, n_trees):
     res = []
     try:
         for host_io, cache, fused, hred in ((1, 1, 1 << 30, 0), (2, 1, 1 << 30, 0), (2, 2, 1 << 30, 0), (1, 2, 0, 0),
-                                            (0, 1, 0, 0), (1, 1, 0, 1), (2, 2, 0, 1), (0, 1, 0, 1)):
+                                            (0, 1, 0, 0), (1, 1, 0, 1 << 20), (2, 2, 0, 1 << 20), (0, 1, 0, 1 << 20)):
             ctx.set_tuning("host_io", host_io)
             ctx.set_tuning("code_cache", cache)
             ctx.set_tuning("fused_reduce", fused)
@@ -224,7 +225,7 @@ def test_small_call_latency_options_change_nothing(dtype, n_rows, n_trees):
         ctx.set_tuning("host_io", 1)
         ctx.set_tuning("code_cache", 1)
         ctx.set_tuning("fused_reduce", 0)
-        ctx.set_tuning("host_reduce", 1)
+        ctx.set_tuning("host_reduce", 8192)
     l0, c0 = res[0]
     assert c0.mean() > 0.2
     for l1, c1 in res[1:]:

@@ -25,11 +25,11 @@ def main():
     trees = gen_random_population(10_000, opts, 5, max_size=30, seed=1)
     tb = flatten_trees(trees, np.float32)
     share = tb.take(np.nonzero(tree_owners(tb, 8) == 0)[0])
-    knobs = [dict(), dict(probe=1)]
+    knobs = [dict()] + ([dict(probe=1)] if "probe" in sys.argv[1:] else [])
     for kn in knobs:
         for k, v in kn.items():
             ctx.set_tuning(k, v)
-        row = {"knobs": kn}
+        row = {"knobs": kn, "env": {k: v for k, v in os.environ.items() if k.startswith("SR_AMD_")}}
         for name, b in (("all", tb), ("share", share)):
             call, _ = bench.single_gpu_call(ctx, b, ds, opts)
             st = {}
