@@ -842,10 +842,22 @@ def search_lines(args):
             share = equation_search(X, y, niterations=args.search_iters, options=o, seed=0, _rank_share=(0, 8))
             swall = share.wall_s  # (the search loop; the helper engines' start is before it)
             rate32, rate4 = args.search_iters / res.wall_s, args.search_iters / swall
+            # weak scaling (the north star's "island populations sharded": more islands per job): 8 ranks
+            # x 32 islands = 256, rank 0's 32 own islands and the head over all 256
+            import copy
+            o256 = copy.copy(o)
+            o256.populations = 8 * o.populations
+            progress("search c5: rank 0's share of an 8-rank search with 8x the islands (weak scaling)")
+            weak = equation_search(X, y, niterations=args.search_iters, options=o256, seed=0, _rank_share=(0, 8))
+            rate_w = args.search_iters / weak.wall_s
             line["projection_8_ranks"] = {
                 "rank0_islands": len(range(0, o.populations, 8)), "rank0_iterations_per_s": rate4,
                 "rank0_device_calls": share.device_calls, "one_gpu_iterations_per_s": rate32,
                 "speedup": rate4 / rate32, "efficiency": rate4 / rate32 / 8.0,
+                "weak_scaling": {"islands_total": o256.populations, "rank0_islands": len(range(0, o256.populations, 8)),
+                                 "rank0_iterations_per_s": rate_w, "efficiency": rate_w / rate32,
+                                 "note": ("8 ranks x the one-GPU island count: the job runs 8x the islands at rank "
+                                          "0's rate; efficiency = that rate / the one-GPU 32-island rate")},
                 "model": ("the 8-rank search runs at the rate of its slowest rank; rank 0's share measured alone "
                           "(equation_search(_rank_share=(0, 8)): its 4 islands' regularised-evolution rounds and "
                           "constant optimisation, the other islands imported every iteration as initialised, the "

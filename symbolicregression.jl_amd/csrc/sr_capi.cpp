@@ -276,7 +276,12 @@ struct sr_ctx {
   bool cost_order = true;   // launch trees in decreasing estimated cost (SR_AMD_NO_SORT=1 disables)
   bool balance_groups = true;  // deal the cost order round-robin over tree groups (SR_AMD_BALANCE=0: contiguous)
   bool dead_hints = true;   // share dead-tree hints across row blocks (SR_AMD_NO_HINT=1 disables)
-  int max_row_blocks = 256; // SR_AMD_MAX_ROW_BLOCKS (tuning): upper bound on row blocks per tree
+  // SR_AMD_MAX_ROW_BLOCKS (tuning): upper bound on row blocks per tree.  512 since round 5 (A/B, three
+  // alternating passes on one box, profiles/r05_ab_row_blocks.txt): C2 4.47 vs 4.51 ms per step, C4
+  // 1,520 vs 1,533 ms, the tree-sharding share (1,250 trees) 1.03 vs 1.09 ms: a small population keeps
+  // 128 trees per workgroup instead of halving it to fill the GPU.  Results do not depend on it only
+  // up to the f64 summation order of the partials (row blocks are a function of the rows alone).
+  int max_row_blocks = 512;
   int chunks = 2;           // SR_AMD_CHUNKS: pipeline compile/launch over this many tree chunks (1 = off)
   int probe = 2;            // dead-tree probe launch (SR_AMD_PROBE): 0 off, 1 before every chunk,
                             // 2 (default) only before the chunks after the first, whose probe
