@@ -453,6 +453,28 @@ def tree_sharded_line(ctx, tb, opts, eval_loss_tree_sharded, args, comm, world, 
         out["overhead_vs_single_call"] = out["ms_per_step"] / t1
         out["projection_8_ranks"] = {"rank0_share_trees": share.n_trees, "rank0_share_ms": t8,
                                      "efficiency_excluding_allgather": t1 / (8 * t8)}
+        # tree sharding's own regime: a population ten times C2's (100k trees, the C4 generator) over the
+        # same replicated 1M rows — the per-call fixed costs (compile of the first chunk, exact pass,
+        # launch latency) amortise over 12.5k trees per rank
+        from sr_amd import gen_random_batch
+
+        big = gen_random_batch(100_000, opts, 5, max_size=30, seed=4)
+        callb, _ = single_gpu_call(ctx, big, ds, opts)
+        share_b = big.take(np.nonzero(tree_owners(big, 8) == 0)[0])
+        callb8, _ = single_gpu_call(ctx, share_b, ds, opts)
+
+        def run(c):
+            def f():
+                t = time.perf_counter()
+                c()
+                return (time.perf_counter() - t) * 1e3
+            return f
+        dtb, _, _ = timed(run(callb), 5, 2, comm.barrier)
+        dtb8, _, _ = timed(run(callb8), 5, 2, comm.barrier)
+        tb1, tb8 = dtb / 5 * 1e3, dtb8 / 5 * 1e3
+        out["projection_8_ranks_100k_trees"] = {"trees": int(big.n_trees), "single_call_ms": tb1,
+                                                "rank0_share_trees": int(share_b.n_trees), "rank0_share_ms": tb8,
+                                                "efficiency_excluding_allgather": tb1 / (8 * tb8)}
     ds.free_device()
     return out
 

@@ -92,6 +92,10 @@ int sr_version(void);
 int sr_device_count(int* count);
 /* Open a context on HIP device `device` (one process per GPU: pass LOCAL_RANK). */
 int sr_init(int device, sr_ctx** out);
+/* A second context on `parent`'s device and HIP stream (one hardware queue for both), using the
+ * parent's datasets and the operator sets / losses registered on it so far (same ids): a host thread
+ * can keep one call in flight on each (sr_eval_loss_submit).  Shut it down before the parent. */
+int sr_init_shared(sr_ctx* parent, sr_ctx** out);
 int sr_shutdown(sr_ctx* ctx);
 
 /*
@@ -140,6 +144,20 @@ int sr_eval_loss_batch(sr_ctx* ctx, const sr_dataset* ds, int opset_id, const sr
 int sr_eval_loss_batch_views(sr_ctx* ctx, const sr_dataset* ds, int opset_id, const sr_tree_batch* trees,
                              const int32_t* tree_view, int n_views, const int64_t* view_rows, int64_t view_len,
                              int loss_kind, void* out_loss, uint8_t* out_complete);
+
+/*
+ * The same call in two halves: _submit compiles, stages and launches it and returns; _wait finishes it
+ * (waits for the device, runs the rare exact-sum / in-order fold passes, finalizes) and fills the
+ * outputs given at submit.  n_views <= 1: one view (view_rows = NULL: the full dataset, else view_len
+ * rows).  One pending call per context; every array the call reads (trees, views, outputs) must stay
+ * valid until _wait returns; other calls on the context are refused meanwhile.  Results equal the
+ * synchronous call's.  With sr_init_shared a host thread keeps two calls in flight on one stream: the
+ * search overlaps one half of a lane's islands' host work with the other half's device work.
+ */
+int sr_eval_loss_submit(sr_ctx* ctx, const sr_dataset* ds, int opset_id, const sr_tree_batch* trees,
+                        const int32_t* tree_view, int n_views, const int64_t* view_rows, int64_t view_len, int loss_kind,
+                        void* out_loss, uint8_t* out_complete);
+int sr_eval_loss_wait(sr_ctx* ctx);
 
 /*
  * Batched eval_tree_array (src/InterfaceDynamicExpressions.jl:58-88): predictions

@@ -262,6 +262,13 @@ struct sr_ctx {
     for (double& v : phase_ms) v = 0.0;
   }
   bool internal_pass = false;  // the fold's PRED passes: run_batch leaves the call's phase clock alone
+  // Asynchronous loss calls (sr_eval_loss_submit / sr_eval_loss_wait, round 5): the pending call's
+  // second half, and the event after its device work (a context made by sr_init_shared runs on
+  // another context's stream, which may hold that context's later calls: waits go to the event)
+  std::function<int()> pending;
+  hipEvent_t ev_done = nullptr;
+  bool owns_stream = true;
+  sr_ctx* parent = nullptr;  // sr_init_shared: the context whose stream, datasets, opsets and losses it uses
   void mark_phase(int i) {
     if (internal_pass) return;
     const auto now = std::chrono::steady_clock::now();
@@ -385,7 +392,9 @@ int check_ctx(sr_ctx* ctx) {
 
 int validate_common(sr_ctx* ctx, const sr_dataset* ds, int opset_id, const sr_tree_batch* trees) {
   if (check_ctx(ctx) != SR_OK) return SR_ERR_INVALID_ARG;
-  if (!ds || ds->ctx != ctx) return set_error(SR_ERR_INVALID_ARG, "dataset is NULL or belongs to another context");
+  if (!ds || (ds->ctx != ctx && ds->ctx != ctx->parent))
+    return set_error(SR_ERR_INVALID_ARG, "dataset is NULL or belongs to another context");
+  if (ctx->pending) return set_error(SR_ERR_INVALID_ARG, "a submitted call is pending on this context: sr_eval_loss_wait first");
   if (opset_id < 0 || opset_id >= int(ctx->opsets.size()))
     return set_error(SR_ERR_INVALID_ARG, "unknown opset id " + std::to_string(opset_id));
   if (!trees) return set_error(SR_ERR_INVALID_ARG, "NULL tree batch");
@@ -1673,20 +1682,49 @@ inline int64_t fold_terms(const sr_dataset* ds, int64_t n_rows) { return (ds->w 
 
 // views (may be NULL): several row views in one call (sr_eval_loss_batch_views); row_idx then holds
 // views->n_views views of n_idx rows each.
+// The second half of an eval_loss call: what finishing it needs once its device work is enqueued.
 template <typename T>
-int eval_loss_impl(sr_ctx* ctx, const sr_dataset* ds, int opset_id, const sr_tree_batch* trees,
-                   const int64_t* row_idx, int64_t n_idx, int loss_kind, void* out_loss, uint8_t* out_complete,
-                   const ViewSpec* views = nullptr) {
+struct LossCall {
+  const sr_dataset* ds = nullptr;
+  int opset_id = 0, loss_kind = 0;
+  sr_tree_batch trees{};
+  const int64_t* row_idx = nullptr;
+  int64_t n_idx = 0;
+  void* out_loss = nullptr;
+  uint8_t* out_complete = nullptr;
+  bool has_views = false;
+  ViewSpec views{};
+  SrProgramBatch<T> prog;
+  std::chrono::steady_clock::time_point t0;
+  bool async = false;  // wait on ctx->ev_done (the stream may be shared and hold later work)
+};
+template <typename T>
+int eval_loss_finish(sr_ctx* ctx, LossCall<T>& c);
+
+// First half: compile, stage, launch, and the copy of {Σ, flags} (or the kernel's own writes into
+// pinned memory); *c holds what eval_loss_finish needs.
+template <typename T>
+int eval_loss_submit(sr_ctx* ctx, const sr_dataset* ds, int opset_id, const sr_tree_batch* trees,
+                     const int64_t* row_idx, int64_t n_idx, int loss_kind, void* out_loss, uint8_t* out_complete,
+                     const ViewSpec* views, LossCall<T>* c) {
   const int64_t nt = trees->n_trees;
   if (nt > 0 && (!out_loss || !out_complete)) return set_error(SR_ERR_INVALID_ARG, "NULL output buffers");
   const bool gather = row_idx != nullptr && n_idx > 0;
   const int64_t n_eval = gather ? n_idx : ds->n;
-  const int n_views = views ? views->n_views : 1;
-  auto view_of = [&](int64_t t) -> int { return views ? int(views->tree_view[t]) : 0; };
-  auto rows_of = [&](int v) -> const int64_t* { return gather ? row_idx + int64_t(v) * n_idx : nullptr; };
   auto t0 = std::chrono::steady_clock::now();
   ctx->start_phases(t0);
-  SrProgramBatch<T> prog;
+  c->ds = ds;
+  c->opset_id = opset_id;
+  c->loss_kind = loss_kind;
+  c->trees = *trees;
+  c->row_idx = row_idx;
+  c->n_idx = n_idx;
+  c->out_loss = out_loss;
+  c->out_complete = out_complete;
+  c->has_views = views != nullptr;
+  if (views) c->views = *views;
+  c->t0 = t0;
+  SrProgramBatch<T>& prog = c->prog;
   Grid g;
   ctx->want_host_out = true;
   int rc = run_batch<T>(ctx, ds, opset_id, trees, row_idx, n_idx, n_eval, loss_kind, SR_MODE_LOSS, &prog, &g, true,
@@ -1701,11 +1739,40 @@ int eval_loss_impl(sr_ctx* ctx, const sr_dataset* ds, int opset_id, const sr_tre
     SR_HIP_CHECK(ctx->h_outs.ensure(out_bytes, s, ctx->stream2));
     SR_HIP_CHECK(hipMemcpyAsync(ctx->h_outs.p, ctx->outs.p, out_bytes, hipMemcpyDeviceToHost, s));
   }
+  if (c->async) SR_HIP_CHECK(hipEventRecord(ctx->ev_done, s));
+  return SR_OK;
+}
+
+template <typename T>
+int eval_loss_finish(sr_ctx* ctx, LossCall<T>& c) {
+  const sr_dataset* ds = c.ds;
+  const int opset_id = c.opset_id;
+  const sr_tree_batch* trees = &c.trees;
+  const int64_t* row_idx = c.row_idx;
+  const int64_t n_idx = c.n_idx;
+  const int loss_kind = c.loss_kind;
+  void* out_loss = c.out_loss;
+  uint8_t* out_complete = c.out_complete;
+  const ViewSpec* views = c.has_views ? &c.views : nullptr;
+  SrProgramBatch<T>& prog = c.prog;
+  const auto t0 = c.t0;
+  const int64_t nt = trees->n_trees;
+  if (nt == 0) return SR_OK;
+  const bool gather = row_idx != nullptr && n_idx > 0;
+  const int64_t n_eval = gather ? n_idx : ds->n;
+  const int n_views = views ? views->n_views : 1;
+  auto view_of = [&](int64_t t) -> int { return views ? int(views->tree_view[t]) : 0; };
+  auto rows_of = [&](int v) -> const int64_t* { return gather ? row_idx + int64_t(v) * n_idx : nullptr; };
+  hipStream_t s = ctx->stream;
+  int rc = SR_OK;
+
   if (ctx->spin && ctx->outs_on_host) {
     hipError_t e;
-    while ((e = hipStreamQuery(s)) == hipErrorNotReady) {
+    while ((e = c.async ? hipEventQuery(ctx->ev_done) : hipStreamQuery(s)) == hipErrorNotReady) {
     }
     SR_HIP_CHECK(e);
+  } else if (c.async) {
+    SR_HIP_CHECK(hipEventSynchronize(ctx->ev_done));
   } else {
     SR_HIP_CHECK(hipStreamSynchronize(s));
   }
@@ -1767,6 +1834,18 @@ int eval_loss_impl(sr_ctx* ctx, const sr_dataset* ds, int opset_id, const sr_tre
   ctx->last_total_ms = std::chrono::duration<double, std::milli>(t1 - t0).count();
   (void)n_eval;
   return SR_OK;
+}
+
+// The whole call (sr_eval_loss_batch / _views): submit, then finish.
+template <typename T>
+int eval_loss_impl(sr_ctx* ctx, const sr_dataset* ds, int opset_id, const sr_tree_batch* trees,
+                   const int64_t* row_idx, int64_t n_idx, int loss_kind, void* out_loss, uint8_t* out_complete,
+                   const ViewSpec* views = nullptr) {
+  LossCall<T> c;
+  const int rc = eval_loss_submit<T>(ctx, ds, opset_id, trees, row_idx, n_idx, loss_kind, out_loss, out_complete, views,
+                                     &c);
+  if (rc != SR_OK) return rc;
+  return eval_loss_finish<T>(ctx, c);
 }
 
 template <typename T>
@@ -2908,11 +2987,42 @@ int sr_init(int device, sr_ctx** out) {
   }
   for (hipEvent_t& ev : ctx->ev_f)
     if (e == hipSuccess) e = hipEventCreate(&ev);
+  if (e == hipSuccess) e = hipEventCreateWithFlags(&ctx->ev_done, hipEventDisableTiming);
   if (e != hipSuccess) {
     delete ctx;
     return set_error(SR_ERR_HIP, std::string("stream/event creation: ") + hipGetErrorString(e));
   }
   *out = ctx;
+  return SR_OK;
+}
+
+int sr_init_shared(sr_ctx* parent, sr_ctx** out) {
+  if (!parent || !out) return set_error(SR_ERR_INVALID_ARG, "NULL parent context or output");
+  int rc = sr_init(parent->device, out);
+  if (rc != SR_OK) return rc;
+  sr_ctx* c = *out;
+  (void)hipStreamSynchronize(c->stream);
+  (void)hipStreamDestroy(c->stream);
+  c->stream = parent->stream;  // one hardware queue for both contexts
+  c->owns_stream = false;
+  c->parent = parent;
+  {  // the parent's operator sets and registered losses, at the same ids (register them before this call)
+    Lock lp(parent);
+    c->opsets = parent->opsets;
+    c->tiers = parent->tiers;
+    c->losses = parent->losses;
+  }
+  // the parent's run-time knobs (sr_set_tuning)
+  c->timing = parent->timing;
+  c->host_io = parent->host_io;
+  c->host_reduce = parent->host_reduce;
+  c->code_cache = parent->code_cache;
+  c->fused_reduce = parent->fused_reduce;
+  c->derived = parent->derived;
+  c->probe = parent->probe;
+  c->stress_probe = parent->stress_probe;
+  c->fold_seg = parent->fold_seg;
+  c->spin = parent->spin;
   return SR_OK;
 }
 
@@ -2943,6 +3053,7 @@ int sr_shutdown(sr_ctx* ctx) {
       (void)hipEventDestroy(ctx->ev_g1[b]);
     }
     for (hipEvent_t ev : ctx->ev_f) (void)hipEventDestroy(ev);
+    (void)hipEventDestroy(ctx->ev_done);
     if (ctx->stream2) (void)hipStreamSynchronize(ctx->stream2);
     (void)hipEventDestroy(ctx->ev_join);
     if (ctx->stream2) (void)hipStreamDestroy(ctx->stream2);
@@ -2952,7 +3063,7 @@ int sr_shutdown(sr_ctx* ctx) {
     (void)hipEventDestroy(ctx->ev_end);
     (void)hipEventDestroy(ctx->ev_d0);
     (void)hipEventDestroy(ctx->ev_d1);
-    (void)hipStreamDestroy(ctx->stream);
+    if (ctx->owns_stream) (void)hipStreamDestroy(ctx->stream);
   }
   delete ctx;
   return SR_OK;
@@ -3072,6 +3183,43 @@ int sr_eval_loss_batch_views(sr_ctx* ctx, const sr_dataset* ds, int opset_id, co
   if (ds->dtype == SR_DTYPE_F32)
     return eval_loss_impl<float>(ctx, ds, opset_id, trees, view_rows, view_len, loss_kind, out_loss, out_complete, v);
   return eval_loss_impl<double>(ctx, ds, opset_id, trees, view_rows, view_len, loss_kind, out_loss, out_complete, v);
+}
+
+int sr_eval_loss_submit(sr_ctx* ctx, const sr_dataset* ds, int opset_id, const sr_tree_batch* trees,
+                        const int32_t* tree_view, int n_views, const int64_t* view_rows, int64_t view_len, int loss_kind,
+                        void* out_loss, uint8_t* out_complete) {
+  int rc = validate_common(ctx, ds, opset_id, trees);
+  if (rc != SR_OK) return rc;
+  if (n_views > 1 && (rc = check_views(trees, tree_view, n_views, view_rows, view_len)) != SR_OK) return rc;
+  Lock l(ctx);
+  if (ctx->pending) return set_error(SR_ERR_INVALID_ARG, "a submitted call is pending on this context: sr_eval_loss_wait first");
+  SR_HIP_CHECK(hipSetDevice(ctx->device));
+  const ViewSpec vs{tree_view, n_views, view_len};
+  const ViewSpec* v = n_views > 1 ? &vs : nullptr;
+  auto go = [&](auto zero) -> int {
+    using T = decltype(zero);
+    auto c = std::make_shared<LossCall<T>>();
+    c->async = true;
+    const int r = eval_loss_submit<T>(ctx, ds, opset_id, trees, view_rows, view_len, loss_kind, out_loss, out_complete,
+                                      v, c.get());
+    if (r != SR_OK) {
+      (void)hipStreamSynchronize(ctx->stream);  // (nothing of it may still run when the caller retries)
+      return r;
+    }
+    ctx->pending = [ctx, c]() { return eval_loss_finish<T>(ctx, *c); };
+    return SR_OK;
+  };
+  return ds->dtype == SR_DTYPE_F32 ? go(0.0f) : go(0.0);
+}
+
+int sr_eval_loss_wait(sr_ctx* ctx) {
+  if (check_ctx(ctx) != SR_OK) return SR_ERR_INVALID_ARG;
+  Lock l(ctx);
+  if (!ctx->pending) return set_error(SR_ERR_INVALID_ARG, "no submitted call is pending on this context");
+  SR_HIP_CHECK(hipSetDevice(ctx->device));
+  std::function<int()> f = std::move(ctx->pending);
+  ctx->pending = nullptr;
+  return f();
 }
 
 int sr_eval_grad_batch_views(sr_ctx* ctx, const sr_dataset* ds, int opset_id, const sr_tree_batch* trees,

@@ -303,6 +303,64 @@ struct Scorer {
     ++calls;
     return rc;
   }
+  // Asynchronous loss (round 5): loss_submit launches the call and returns, loss_wait finishes it into
+  // the `out` given at submit (+Inf where incomplete).  The device path keeps the call's view arrays
+  // here until the wait; CPU scorers run the whole call at submit.
+  struct AsyncLoss {
+    std::vector<int32_t> tv;
+    std::vector<int64_t> cat;
+    std::vector<uint8_t> comp;
+    std::vector<T>* out = nullptr;
+    bool device = false;
+    int timing_was = -1;
+    Clock::time_point t0;
+  };
+  int loss_submit(const Flat& flat, const TreeRows& tr, std::vector<T>* out, AsyncLoss* a) {
+    a->device = false;
+    a->out = out;
+    const int64_t nt = int64_t(flat.offsets.size()) - 1;
+    if (loss_cb || nt <= 0) return loss(flat, tr, out);
+    const std::vector<int64_t>* one = nullptr;
+    int nv = 1;
+    int64_t len = 0;
+    const bool multi = !tr.empty() && make_views(tr, &a->tv, &a->cat, &nv, &len, &one);
+    out->assign(size_t(nt), T(0));
+    a->comp.assign(size_t(nt), 0);
+    const sr_tree_batch b = flat.batch<T>();
+    a->t0 = Clock::now();
+    a->timing_was = !time_kernels ? sr_ctx_swap_timing(ctx, 0) : -1;
+    int rc;
+    if (multi) {
+      rc = sr_eval_loss_submit(ctx, ds, opset_id, &b, a->tv.data(), nv, a->cat.data(), len, loss_code, out->data(),
+                               a->comp.data());
+    } else {
+      const bool rows = one != nullptr && !one->empty();
+      rc = sr_eval_loss_submit(ctx, ds, opset_id, &b, nullptr, 1, rows ? one->data() : nullptr,
+                               rows ? int64_t(one->size()) : 0, loss_code, out->data(), a->comp.data());
+    }
+    if (rc != SR_OK) {
+      if (a->timing_was >= 0) sr_ctx_swap_timing(ctx, a->timing_was);
+      return rc;
+    }
+    a->device = true;
+    return SR_OK;
+  }
+  int loss_wait(AsyncLoss* a) {
+    if (!a->device) return SR_OK;  // (CPU scorers: done at submit)
+    a->device = false;
+    const int rc = sr_eval_loss_wait(ctx);
+    if (a->timing_was >= 0) sr_ctx_swap_timing(ctx, a->timing_was);
+    ms += ms_since(a->t0);
+    ++calls;
+    if (rc != SR_OK) return rc;
+    if (time_kernels) {
+      double ph[9] = {0};
+      if (sr_last_phase_ms(ctx, ph, 9) == SR_OK) kernel_ms += ph[8];
+    }
+    for (size_t k = 0; k < a->comp.size(); ++k)
+      if (!a->comp[k]) (*a->out)[k] = T(INFINITY);
+    return SR_OK;
+  }
   // losses of `flat`'s trees (+Inf where incomplete)
   int loss(const Flat& flat, const std::vector<int64_t>& rows, std::vector<T>* out) {
     const sr_tree_batch b = flat.batch<T>();
@@ -508,19 +566,62 @@ struct Engine : sr_search_base {
   // Scoring lanes: lane 0 is (sc, flat, num_evals, host_ms); further lanes (sr_search_add_device:
   // their own context and dataset copy) each run a share of the owned islands' iteration on their
   // own host thread, so one lane's device round trip overlaps the others' host work and calls.
+  struct Pipe {  // a lane's second scoring context (sr_init_shared: the lane's stream) and its Flat
+    Scorer<T>* sc;
+    Flat* flat;
+  };
   struct Lane {
     Scorer<T>* sc;
     Flat* flat;
     double* num_evals;
     double* host_ms;
+    const Pipe* pipe = nullptr;  // set: the lane pipelines two halves of its islands (iterate_islands)
   };
   struct ExtraLane {
     Scorer<T> sc;
     Flat flat;
     double num_evals = 0.0, host_ms = 0.0;
+    Scorer<T> sc2;  // the pipeline partner (its own context on sc's stream), when enabled
+    Flat flat2;
+    Pipe pipe{};
   };
   std::vector<std::unique_ptr<ExtraLane>> extra;
-  Lane lane0() { return Lane{&sc, &flat, &num_evals, &host_ms}; }
+  // the pipeline partners (round 5; SR_AMD_SEARCH_PIPELINE, default on): every device lane gets a
+  // second context on its own stream (sr_init_shared) at the first iteration
+  Scorer<T> sc2;
+  Flat flat2;
+  Pipe pipe0{};
+  std::vector<sr_ctx*> pipe_ctx;
+  bool pipes_made = false;
+  const bool pipeline = [] {
+    const char* v = std::getenv("SR_AMD_SEARCH_PIPELINE");
+    return !v || std::atoi(v) != 0;
+  }();
+  ~Engine() override {
+    for (sr_ctx* c : pipe_ctx) (void)sr_shutdown(c);
+  }
+  int make_pipes() {
+    if (pipes_made || !pipeline) return SR_OK;
+    pipes_made = true;
+    auto mk = [&](Scorer<T>& base, Scorer<T>& two, Flat& f2, Pipe& pp) -> int {
+      if (!base.ctx) return SR_OK;  // (CPU scorers: nothing to overlap)
+      sr_ctx* c2 = nullptr;
+      const int rc = sr_init_shared(base.ctx, &c2);
+      if (rc != SR_OK) return rc;
+      pipe_ctx.push_back(c2);
+      two.ctx = c2;
+      two.ds = base.ds;
+      two.opset_id = base.opset_id;
+      two.loss_code = base.loss_code;
+      pp = Pipe{&two, &f2};
+      return SR_OK;
+    };
+    int rc = mk(sc, sc2, flat2, pipe0);
+    for (auto& x : extra)
+      if (rc == SR_OK) rc = mk(x->sc, x->sc2, x->flat2, x->pipe);
+    return rc;
+  }
+  Lane lane0() { return Lane{&sc, &flat, &num_evals, &host_ms, pipe0.sc ? &pipe0 : nullptr}; }
   double total_num_evals() const {
     double v = num_evals;
     for (const auto& x : extra) v += x->num_evals;
@@ -758,11 +859,34 @@ struct Engine : sr_search_base {
     size_t slot = 0;
   };
 
+  // One regularised-evolution round of a set of islands, in two halves: round_submit selects and mutates
+  // (host) and launches ONE scoring call for every island's children; round_finish waits for it and
+  // replaces members.  A lane with a second scoring context pipelines two halves of its islands: one
+  // half's host work runs while the other half's call is on the device (iterate_islands).
+  struct RoundState {
+    std::vector<Plan> plans;
+    std::vector<const SrTree<T>*> pending;
+    std::vector<int> pend_island;
+    TreeRows rows;
+    std::vector<T> loss, cost;
+    typename Scorer<T>::AsyncLoss async;
+    double temperature = 1.0;
+  };
   int round(Lane L, const std::vector<int>& islands, double temperature,
             const std::vector<std::vector<int64_t>>& rows_by_island) {
-    std::vector<Plan> plans;
+    RoundState st;
+    int rc = round_submit(L, islands, temperature, rows_by_island, &st);
+    if (rc) return rc;
+    return round_finish(L, rows_by_island, &st);
+  }
+  int round_submit(Lane L, const std::vector<int>& islands, double temperature,
+                   const std::vector<std::vector<int64_t>>& rows_by_island, RoundState* st) {
+    st->temperature = temperature;
+    std::vector<Plan>& plans = st->plans;
+    plans.clear();
     plans.reserve(islands.size());
-    std::vector<const SrTree<T>*> pending;
+    std::vector<const SrTree<T>*>& pending = st->pending;
+    pending.clear();
     auto tp = Clock::now();
     for (int i : islands) {
       SrRng& rng = rngs[size_t(i)];
@@ -804,7 +928,8 @@ struct Engine : sr_search_base {
       }
       plans.push_back(std::move(pl));
     }
-    std::vector<int> pend_island;
+    std::vector<int>& pend_island = st->pend_island;
+    pend_island.clear();
     for (auto& pl : plans) {
       if (pl.kind == K_MUT || pl.kind == K_CROSS) {
         pl.slot = pending.size();
@@ -816,14 +941,24 @@ struct Engine : sr_search_base {
         }
       }
     }
-    *L.host_ms += ms_since(tp);
     // device: ONE batched eval_cost for every island's children (each on its island's minibatch)
-    std::vector<T> loss, cost;
-    const TreeRows rows = rows_for(pend_island, rows_by_island);
-    int rc = score_trees(L, pending, rows, &loss, &cost);
+    st->rows = rows_for(pend_island, rows_by_island);
+    L.flat->clear();
+    for (auto* t : pending) L.flat->add(*t);
+    *L.host_ms += ms_since(tp);
+    return L.sc->loss_submit(*L.flat, st->rows, &st->loss, &st->async);
+  }
+  int round_finish(Lane L, const std::vector<std::vector<int64_t>>& rows_by_island, RoundState* st) {
+    int rc = L.sc->loss_wait(&st->async);
     if (rc) return rc;
-    const double frac = fraction(rows);
-    *L.num_evals += double(pending.size()) * frac;
+    std::vector<Plan>& plans = st->plans;
+    const std::vector<T>& loss = st->loss;
+    std::vector<T>& cost = st->cost;
+    cost.resize(loss.size());
+    for (size_t k = 0; k < loss.size(); ++k) cost[k] = cost_of(loss[k], int(st->pending[k]->size()));
+    const double temperature = st->temperature;
+    const double frac = fraction(st->rows);
+    *L.num_evals += double(st->pending.size()) * frac;
     // batched optimize mutations (rare: weight 0 by default)
     {
       std::vector<Member<T>*> om;
@@ -836,7 +971,7 @@ struct Engine : sr_search_base {
       std::vector<uint8_t> imp;
       if ((rc = optimize_members(L, om, oi, rows_by_island, &imp))) return rc;
     }
-    tp = Clock::now();
+    const auto tp = Clock::now();
     for (auto& pl : plans) {
       const int i = pl.island;
       SrRng& rng = rngs[size_t(i)];
@@ -1055,14 +1190,11 @@ struct Engine : sr_search_base {
     const int64_t calls0 = L.sc->calls;
     const int ncyc = o.ncycles_per_iteration;
     const int n_evol = (o.population_size + o.tournament_selection_n - 1) / o.tournament_selection_n;
-    for (int c = 0; c < ncyc; ++c) {
-      const double temperature =
-          ncyc > 1 ? (o.annealing ? 1.0 - double(c) / double(ncyc - 1) : 1.0) : 1.0;  // LinRange(1, 0, ncyc)
-      for (int r = 0; r < n_evol; ++r) {
-        int rc = round(L, islands, temperature, rows);
-        if (rc) return rc;
-      }
-      for (int i : islands)
+    auto temp_of = [&](int c) {  // LinRange(1, 0, ncyc)
+      return ncyc > 1 ? (o.annealing ? 1.0 - double(c) / double(ncyc - 1) : 1.0) : 1.0;
+    };
+    auto cycle_end = [&](const std::vector<int>& isl) {  // best-seen members per complexity
+      for (int i : isl)
         for (const auto& m : pops[size_t(i)]) {
           const int s = m.complexity;
           auto& h = best_seen[size_t(i)];
@@ -1071,6 +1203,40 @@ struct Engine : sr_search_base {
             h.m[size_t(s - 1)] = m;
           }
         }
+    };
+    if (L.pipe && islands.size() >= 2) {
+      // two halves of the lane's islands, each on its own context (one stream): half h's round k is
+      // submitted, then the other half's round k finishes and its round k + 1 is submitted, so one
+      // half's host work overlaps the other half's device work.  Every island sees the same sequence
+      // of its own operations and every tree's score is independent of its batch: the results equal
+      // the unpipelined lane's.
+      const size_t mid = islands.size() / 2;
+      const std::vector<int> half[2] = {std::vector<int>(islands.begin(), islands.begin() + ptrdiff_t(mid)),
+                                        std::vector<int>(islands.begin() + ptrdiff_t(mid), islands.end())};
+      const Lane HL[2] = {L, Lane{L.pipe->sc, L.pipe->flat, L.num_evals, L.host_ms, nullptr}};
+      RoundState st[2];
+      const int S = ncyc * n_evol;
+      int rc = SR_OK;
+      for (int h = 0; h < 2 && !rc; ++h) rc = round_submit(HL[h], half[h], temp_of(0), rows, &st[h]);
+      for (int k = 0; k < S && !rc; ++k)
+        for (int h = 0; h < 2 && !rc; ++h) {
+          rc = round_finish(HL[h], rows, &st[h]);
+          if (rc) break;
+          if ((k + 1) % n_evol == 0) cycle_end(half[h]);
+          if (k + 1 < S) rc = round_submit(HL[h], half[h], temp_of((k + 1) / n_evol), rows, &st[h]);
+        }
+      if (rc) {  // (no call may stay pending on either context)
+        for (int h = 0; h < 2; ++h) (void)HL[h].sc->loss_wait(&st[h].async);
+        return rc;
+      }
+    } else {
+      for (int c = 0; c < ncyc; ++c) {
+        for (int r = 0; r < n_evol; ++r) {
+          int rc = round(L, islands, temp_of(c), rows);
+          if (rc) return rc;
+        }
+        cycle_end(islands);
+      }
     }
     // optimize_and_simplify_population: the simplification of every member, then one batched
     // constant optimisation over every island's selected members
@@ -1127,6 +1293,7 @@ struct Engine : sr_search_base {
   }
 
   int iterate() {
+    if (int rc = make_pipes()) return rc;
     std::vector<std::vector<int64_t>> rows(size_t(o.populations)), orows(size_t(o.populations));
     for (int i : owned) {
       rows[size_t(i)] = draw_batch(i, 0);
@@ -1152,7 +1319,8 @@ struct Engine : sr_search_base {
       for (size_t q = 1; q < nl; ++q)
         th.emplace_back([&, q] {
           ExtraLane& x = *extra[q - 1];
-          rcs[q] = iterate_islands(Lane{&x.sc, &x.flat, &x.num_evals, &x.host_ms}, share[q], rows, orows);
+          rcs[q] = iterate_islands(Lane{&x.sc, &x.flat, &x.num_evals, &x.host_ms, x.pipe.sc ? &x.pipe : nullptr},
+                                   share[q], rows, orows);
           if (rcs[q]) msgs[q] = sr_last_error();
         });
       rcs[0] = iterate_islands(lane0(), share[0], rows, orows);
@@ -1620,14 +1788,14 @@ int sr_search_get_info(sr_search* s, sr_search_info* out) {
     out->iterations = e->iteration;
     out->s_r_cycles = e->s_r_cycles;
     out->num_evals = e->total_num_evals();
-    out->device_calls = e->sc.calls;
-    out->device_ms = e->sc.ms;
-    out->kernel_ms = e->sc.kernel_ms;
+    out->device_calls = e->sc.calls + e->sc2.calls;
+    out->device_ms = e->sc.ms + e->sc2.ms;
+    out->kernel_ms = e->sc.kernel_ms + e->sc2.kernel_ms;
     out->host_ms = e->host_ms;
     for (const auto& x : e->extra) {  // (summed over lanes: lanes run concurrently)
-      out->device_calls += x->sc.calls;
-      out->device_ms += x->sc.ms;
-      out->kernel_ms += x->sc.kernel_ms;
+      out->device_calls += x->sc.calls + x->sc2.calls;
+      out->device_ms += x->sc.ms + x->sc2.ms;
+      out->kernel_ms += x->sc.kernel_ms + x->sc2.kernel_ms;
       out->host_ms += x->host_ms;
     }
     out->baseline_loss = double(e->baseline);

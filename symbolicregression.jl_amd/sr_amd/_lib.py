@@ -39,6 +39,7 @@ EXPORTED_SYMBOLS = (
     "sr_version",
     "sr_device_count",
     "sr_init",
+    "sr_init_shared",
     "sr_shutdown",
     "sr_register_opset",
     "sr_register_loss",
@@ -47,6 +48,8 @@ EXPORTED_SYMBOLS = (
     "sr_dataset_info",
     "sr_eval_loss_batch",
     "sr_eval_loss_batch_views",
+    "sr_eval_loss_submit",
+    "sr_eval_loss_wait",
     "sr_eval_tree_array",
     "sr_eval_loss_partials",
     "sr_eval_loss_partials_packed",
@@ -189,6 +192,12 @@ def _load():
             c_int,
             [P, P, c_int, POINTER(SrTreeBatch), P, c_int, P, c_int64, c_int, P, P],
         ),
+        "sr_eval_loss_submit": (
+            c_int,
+            [P, P, c_int, POINTER(SrTreeBatch), P, c_int, P, c_int64, c_int, P, P],
+        ),
+        "sr_eval_loss_wait": (c_int, [P]),
+        "sr_init_shared": (c_int, [P, POINTER(P)]),
         "sr_eval_grad_batch_views": (
             c_int,
             [P, P, c_int, POINTER(SrTreeBatch), P, c_int, P, c_int64, c_int, P, P, P],
