@@ -107,7 +107,9 @@ def test_c3_search_device_equals_oracle_scored_search(monkeypatch):
     assert dev.device_calls > ref.device_calls
     piped = equation_search(X, y, niterations=2, options=opts, seed=5, scoring_lanes=1)
     assert trees(piped) == trees(ref)
-    assert piped.device_calls == 2 * ref.device_calls
+    # (each half of the lane's islands calls per round; a half whose islands made no child that round
+    #  makes no call)
+    assert ref.device_calls < piped.device_calls <= 2 * ref.device_calls
 
 
 @pytest.mark.parametrize("batching", [False, True])
