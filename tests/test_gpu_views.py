@@ -86,7 +86,8 @@ def test_batching_search_device_equals_oracle_scored(optimize):
         ref = equation_search(X, y, niterations=2, options=opts, seed=5, _loss_fn=oracle_loss)
         assert [[string_tree(m.tree, opts.operators) for m in p] for p in dev.populations] == \
                [[string_tree(m.tree, opts.operators) for m in p] for p in ref.populations]
-        assert dev.device_calls == ref.device_calls
+        # the pipelined lane scores each round's islands in two halves -> up to 2x the calls
+        assert ref.device_calls <= dev.device_calls <= 2 * ref.device_calls
     members = [m for p in dev.populations for m in p]
     ol, oc = orc.eval_loss_batch(flatten_trees([m.tree for m in members], np.float32), X, y, accum="f64", n_threads=8)
     stored = np.array([m.loss for m in members], dtype=np.float64)
