@@ -231,6 +231,7 @@ struct sr_ctx {
   int grad_rows_force = 0;  // SR_AMD_GRAD_ROWS / "grad_rows": the gradient kernel's rows per lane (0: chosen per call)
   DevBuf group_cnt;      // its per-group counters (zeroed at allocation; each launch leaves them zero)
   int first_chunk = 6;   // SR_AMD_FIRST_CHUNK: the two-chunk pipeline's first chunk is 1/first_chunk
+  int64_t chunk_min = 1024;  // SR_AMD_CHUNK_MIN: the two-chunk pipeline runs when its first chunk holds this many trees
   // data-path transport of the sharded calls: the library's own RCCL over xGMI on its own HIP runtime
   // (sr_comm_init; torch's bundled runtime cannot share the GPU with this one in a process), or the
   // caller's host collectives (sr_comm_init_host)
@@ -539,7 +540,7 @@ int run_batch(sr_ctx* ctx, const sr_dataset* ds, int opset_id, const sr_tree_bat
   if (multi) {
     // (one chunk: the segments cover the whole launch)
   } else if (mode == SR_MODE_LOSS && ctx->chunks == 2) {
-    n_chunks = nt / ctx->first_chunk >= kChunkTrees / 2 ? 2 : 1;  // the small first chunk holds >= 1024 trees
+    n_chunks = nt / ctx->first_chunk >= ctx->chunk_min ? 2 : 1;  // the small first chunk holds >= chunk_min trees
   } else if (mode == SR_MODE_LOSS && ctx->chunks > 2) {
     const int64_t k = nt / kChunkTrees;
     const int64_t cap = ctx->chunks < kMaxChunks ? ctx->chunks : kMaxChunks;
@@ -2961,6 +2962,7 @@ int sr_init(int device, sr_ctx** out) {
   if (const char* v = std::getenv("SR_AMD_GRAD_ROWS")) ctx->grad_rows_force = std::atoi(v);
   if (const char* v = std::getenv("SR_AMD_VSTK_ROWS")) ctx->vstk_rows = std::atoi(v);
   if (const char* v = std::getenv("SR_AMD_FIRST_CHUNK")) ctx->first_chunk = std::max(2, std::atoi(v));
+  if (const char* v = std::getenv("SR_AMD_CHUNK_MIN")) ctx->chunk_min = std::max<int64_t>(1, std::atoll(v));
   if (const char* v = std::getenv("SR_AMD_HOST_IO")) ctx->host_io = std::atoi(v);
   if (const char* v = std::getenv("SR_AMD_SPIN")) ctx->spin = std::atoi(v);
   if (const char* v = std::getenv("SR_AMD_EXACT_G")) ctx->exact_g = std::atoi(v);
@@ -3705,6 +3707,14 @@ int sr_set_tuning(sr_ctx* ctx, const char* name, int64_t value) {
   Lock l(ctx);
   if (std::strcmp(name, "derived") == 0) {
     ctx->derived = value != 0 ? 1 : 0;
+    return SR_OK;
+  }
+  if (std::strcmp(name, "chunk_min") == 0) {  // the two-chunk pipeline's smallest first chunk (SR_AMD_CHUNK_MIN)
+    ctx->chunk_min = std::max<int64_t>(1, value);
+    return SR_OK;
+  }
+  if (std::strcmp(name, "max_row_blocks") == 0) {  // row blocks per tree of a LOSS launch (SR_AMD_MAX_ROW_BLOCKS)
+    ctx->max_row_blocks = int(std::max<int64_t>(1, std::min<int64_t>(value, 1 << 16)));
     return SR_OK;
   }
   if (std::strcmp(name, "probe") == 0) {  // dead-tree probe mode (SR_AMD_PROBE)

@@ -586,8 +586,9 @@ struct Engine : sr_search_base {
     Pipe pipe{};
   };
   std::vector<std::unique_ptr<ExtraLane>> extra;
-  // the pipeline partners (round 5; SR_AMD_SEARCH_PIPELINE, default on): every device lane gets a
-  // second context on its own stream (sr_init_shared) at the first iteration
+  // the pipeline partners (round 5; SR_AMD_SEARCH_PIPELINE=1, default off: C1 -15 %, C3 / C5 within
+  // noise, profiles/r05_ab_search_pipeline.txt): every device lane gets a second context sharing its
+  // stream (sr_init_shared) at the first iteration
   Scorer<T> sc2;
   Flat flat2;
   Pipe pipe0{};
@@ -595,7 +596,7 @@ struct Engine : sr_search_base {
   bool pipes_made = false;
   const bool pipeline = [] {
     const char* v = std::getenv("SR_AMD_SEARCH_PIPELINE");
-    return !v || std::atoi(v) != 0;
+    return v && std::atoi(v) != 0;
   }();
   ~Engine() override {
     for (sr_ctx* c : pipe_ctx) (void)sr_shutdown(c);

@@ -99,13 +99,13 @@ def test_c3_search_device_equals_oracle_scored_search(monkeypatch):
     # several scoring lanes (the default) split each round's launch; one unpipelined lane makes
     # exactly the oracle-scored search's calls, and neither the lane count nor the pipeline (two
     # halves of a lane's islands, one call in flight each) changes any result
-    monkeypatch.setenv("SR_AMD_SEARCH_PIPELINE", "0")
     one = equation_search(X, y, niterations=2, options=opts, seed=5, scoring_lanes=1)
-    monkeypatch.delenv("SR_AMD_SEARCH_PIPELINE")
     assert trees(one) == trees(ref)
     assert one.device_calls == ref.device_calls > 40
     assert dev.device_calls > ref.device_calls
+    monkeypatch.setenv("SR_AMD_SEARCH_PIPELINE", "1")
     piped = equation_search(X, y, niterations=2, options=opts, seed=5, scoring_lanes=1)
+    monkeypatch.delenv("SR_AMD_SEARCH_PIPELINE")
     assert trees(piped) == trees(ref)
     # (each half of the lane's islands calls per round; a half whose islands made no child that round
     #  makes no call)
@@ -115,8 +115,8 @@ def test_c3_search_device_equals_oracle_scored_search(monkeypatch):
 @pytest.mark.parametrize("batching", [False, True])
 def test_scoring_lanes_change_nothing(batching, monkeypatch):
     """Islands split over 1, 2 and 3 scoring lanes (own contexts and streams, one host thread each),
-    each lane pipelining two halves of its islands on a second context that shares its stream
-    (sr_init_shared, sr_eval_loss_submit / _wait; round 5), and one lane without the pipeline, evolve
+    and one lane pipelining two halves of its islands on a second context that shares its stream
+    (SR_AMD_SEARCH_PIPELINE=1: sr_init_shared, sr_eval_loss_submit / _wait; round 5), evolve
     identically: same populations, costs and losses bit for bit; num_evals up to rounding."""
     X, y = _readme_data(300, seed=5)
     opts = Options(binary_operators=["+", "*", "-", "/"], unary_operators=["cos", "exp"], populations=6,
@@ -128,7 +128,7 @@ def test_scoring_lanes_change_nothing(batching, monkeypatch):
         pops = [[(string_tree(m.tree, opts.operators), np.float32(m.cost).tobytes(), np.float32(m.loss).tobytes(),
                   m.birth, m.ref, m.parent) for m in p] for p in res.populations]
         runs.append((pops, res.num_evals, res.device_calls))
-    monkeypatch.setenv("SR_AMD_SEARCH_PIPELINE", "0")
+    monkeypatch.setenv("SR_AMD_SEARCH_PIPELINE", "1")
     res = equation_search(X, y, niterations=3, options=opts, seed=9, scoring_lanes=1)
     monkeypatch.delenv("SR_AMD_SEARCH_PIPELINE")
     flat = [[(string_tree(m.tree, opts.operators), np.float32(m.cost).tobytes(), np.float32(m.loss).tobytes(),
