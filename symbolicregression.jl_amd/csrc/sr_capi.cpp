@@ -229,6 +229,7 @@ struct sr_ctx {
   int64_t fused_reduce = 0;
   int vstk_rows = 0;        // SR_AMD_VSTK_ROWS / "vstk_rows": rows per lane of the register-stack kernel (0: default)
   int grad_rows_force = 0;  // SR_AMD_GRAD_ROWS / "grad_rows": the gradient kernel's rows per lane (0: chosen per call)
+  int grad_sort = 1;        // SR_AMD_GRAD_SORT / "grad_sort": gradient work items ordered by program cost
   DevBuf group_cnt;      // its per-group counters (zeroed at allocation; each launch leaves them zero)
   int first_chunk = 6;   // SR_AMD_FIRST_CHUNK: the two-chunk pipeline's first chunk is 1/first_chunk
   int64_t chunk_min = 1024;  // SR_AMD_CHUNK_MIN: the two-chunk pipeline runs when its first chunk holds this many trees
@@ -2042,6 +2043,35 @@ int eval_grad_impl(sr_ctx* ctx, const sr_dataset* ds, int opset_id, const sr_tre
       k0s[b].push_back(k0);
     }
   }
+  // each bucket's items by estimated program cost, longest first (stable): the kWaves waves of a
+  // workgroup share every row tile and wait for each other at its barrier, so items of similar cost go
+  // together (an item's gradient does not depend on its position: bit-identical either way)
+  if (ctx->grad_sort) {
+    std::vector<double> tcost(size_t(nt), 0.0);
+    for (int64_t t = 0; t < nt; ++t) {
+      double c = 0.0;
+      for (uint32_t i = prog.offsets[size_t(t)]; i < prog.offsets[size_t(t) + 1]; ++i) {
+        const uint32_t opc = prog.code[i].op & SR_OP_MASK;
+        const uint32_t u = opc >= SR_OP_UNARY_INF0 ? opc - SR_OP_UNARY_INF0 : opc - SR_OP_UNARY0;
+        const bool transc = opc >= SR_OP_UNARY0 && opc < SR_OP_LOAD_DERIVED &&
+                            (u == SR_U_EXP || u == SR_U_LOG || u == SR_U_COS || u == SR_U_SIN);
+        c += transc ? 5.0 : 1.0;
+      }
+      tcost[size_t(t)] = c;
+    }
+    for (int b = 0; b < kNB; ++b) {
+      std::vector<size_t> ord(items[b].size());
+      for (size_t i = 0; i < ord.size(); ++i) ord[i] = i;
+      std::stable_sort(ord.begin(), ord.end(), [&](size_t x, size_t y) { return tcost[items[b][x]] > tcost[items[b][y]]; });
+      std::vector<uint32_t> it2(ord.size()), k2(ord.size());
+      for (size_t i = 0; i < ord.size(); ++i) {
+        it2[i] = items[b][ord[i]];
+        k2[i] = k0s[b][ord[i]];
+      }
+      items[b].swap(it2);
+      k0s[b].swap(k2);
+    }
+  }
   hipStream_t s = ctx->stream;
   // the loss pass's in-order folds re-upload their own view's rows: put every view's rows back
   if (gather && ctx->n_fold_last > 0) {
@@ -2960,6 +2990,7 @@ int sr_init(int device, sr_ctx** out) {
   if (const char* v = std::getenv("SR_AMD_CODE_CACHE")) ctx->code_cache = std::atoi(v);
   if (const char* v = std::getenv("SR_AMD_FUSED_REDUCE")) ctx->fused_reduce = std::atoll(v);
   if (const char* v = std::getenv("SR_AMD_GRAD_ROWS")) ctx->grad_rows_force = std::atoi(v);
+  if (const char* v = std::getenv("SR_AMD_GRAD_SORT")) ctx->grad_sort = std::atoi(v) != 0 ? 1 : 0;
   if (const char* v = std::getenv("SR_AMD_VSTK_ROWS")) ctx->vstk_rows = std::atoi(v);
   if (const char* v = std::getenv("SR_AMD_FIRST_CHUNK")) ctx->first_chunk = std::max(2, std::atoi(v));
   if (const char* v = std::getenv("SR_AMD_CHUNK_MIN")) ctx->chunk_min = std::max<int64_t>(1, std::atoll(v));
@@ -3707,6 +3738,10 @@ int sr_set_tuning(sr_ctx* ctx, const char* name, int64_t value) {
   Lock l(ctx);
   if (std::strcmp(name, "derived") == 0) {
     ctx->derived = value != 0 ? 1 : 0;
+    return SR_OK;
+  }
+  if (std::strcmp(name, "grad_sort") == 0) {  // gradient work items ordered by program cost (SR_AMD_GRAD_SORT)
+    ctx->grad_sort = value != 0 ? 1 : 0;
     return SR_OK;
   }
   if (std::strcmp(name, "chunk_min") == 0) {  // the two-chunk pipeline's smallest first chunk (SR_AMD_CHUNK_MIN)

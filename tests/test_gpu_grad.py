@@ -211,7 +211,8 @@ def test_gradients_independent_of_rows_per_lane(dtype):
     """The gradient kernel's rows per lane is a tuning choice (sr_set_tuning "grad_rows"): its row
     blocks cover the same rows whatever the choice and each lane accumulates its rows in order, so the
     gradients are bit-identical for every choice — also with FULL-tier operators (their row callees),
-    weights, a non-L2 loss and every tangent bucket."""
+    weights, a non-L2 loss and every tangent bucket.  Likewise the work items' order (sr_set_tuning
+    "grad_sort": by program cost, or in tree order)."""
     import sr_amd
 
     rng = np.random.default_rng(8)
@@ -238,5 +239,11 @@ def test_gradients_independent_of_rows_per_lane(dtype):
                     continue
                 assert np.array_equal(c, ref[2]), rows
                 assert np.array_equal(g.view(np.uint8), ref[1].view(np.uint8)), (rows, kw)
+            ctx.set_tuning("grad_rows", 0)
+            ctx.set_tuning("grad_sort", 0)
+            l, g, c = eval_grad_batch(tb, ds, opts)
+            assert np.array_equal(c, ref[2])
+            assert np.array_equal(g.view(np.uint8), ref[1].view(np.uint8)), ("unsorted", kw)
         finally:
             ctx.set_tuning("grad_rows", 0)
+            ctx.set_tuning("grad_sort", 1)

@@ -139,4 +139,4 @@ def test_scoring_lanes_change_nothing(batching, monkeypatch):
     assert runs[1][1] == pytest.approx(runs[0][1], rel=1e-12)
     assert res.num_evals == pytest.approx(runs[0][1], rel=1e-12)
     assert runs[2][2] > runs[0][2]  # the islands' rounds went through several lanes
-    assert runs[0][2] > res.device_calls  # (one pipelined lane: two calls per round)
+    assert res.device_calls > runs[0][2]  # (one pipelined lane: up to two calls per round)
