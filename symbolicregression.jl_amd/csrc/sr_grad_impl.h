@@ -101,7 +101,11 @@ __device__ __attribute__((noinline)) SrGVec<T, R> sr_grad_loss_der(int kind, SrG
 // R: rows per lane (sr_grad_launch_rows: up to 8 for 1-2 tangents, 4 for 4, 2 for 8, 1 for 16): the
 // value and its KT tangents of R rows stay in VGPRs, so one dispatch of an instruction covers R x 64
 // rows (round 3: one row per lane made every dispatch and operand decode cover 64 rows only).
-template <typename T, int KT, int W, bool GATHER, int R>
+// VSTK (round 5): programs of at most two operand-stack slots keep both slots in VGPRs (value and
+// tangents of R rows each) instead of the per-wave LDS stack — no LDS traffic per push / operand, and
+// a workgroup's LDS is its row tile only, so more workgroups share a CU.  The same arithmetic in the
+// same order: bit-identical to the LDS-stack kernel.
+template <typename T, int KT, int W, bool GATHER, int R, bool VSTK>
 __global__ void __launch_bounds__(W * 64) sr_grad_kernel(const SrGradArgs<T> a) {
   // rows per lane: lane + 64 j, j < R
   constexpr int ROWS = 64 * R;               // rows per staged tile
@@ -116,12 +120,12 @@ __global__ void __launch_bounds__(W * 64) sr_grad_kernel(const SrGradArgs<T> a) 
   T* stk = wsv + (a.w ? ROWS : 0);                             // [W][depth][NV][R][64]
   T* my_stk = stk + size_t(wave) * a.stack_depth * NV * R * 64 + lane;
 
-  int tg, rb, item, item_end = a.n_items;
+  int tg, rb, item, item_end = a.item_end;
   const int64_t* ridx = a.row_idx;  // GATHER: this block's row view
-  if (a.segs == nullptr) {
+  if (a.segs == nullptr) {  // (this launch's items: [item0, item_end) of the bucket's n_items)
     tg = int(blockIdx.x) % a.n_groups;
     rb = int(blockIdx.x) / a.n_groups;
-    item = tg * W + wave;
+    item = a.item0 + tg * W + wave;
   } else {
     // several row views in one launch (sr_eval_grad_batch_views): segment = one view's work items
     int lo = 0, hi = a.n_segs - 1;
@@ -176,11 +180,19 @@ __global__ void __launch_bounds__(W * 64) sr_grad_kernel(const SrGradArgs<T> a) 
 
     T v[R];
     T dv[R][KT];
+    T s0v[VSTK ? R : 1], s1v[VSTK ? R : 1];  // VSTK: stack slots 0 and 1 (value, tangents)
+    T s0d[VSTK ? R : 1][KT], s1d[VSTK ? R : 1][KT];
 #pragma unroll
     for (int j = 0; j < R; ++j) {
       v[j] = T(0);
 #pragma unroll
       for (int q = 0; q < KT; ++q) dv[j][q] = T(0);
+    }
+#pragma unroll
+    for (int j = 0; j < (VSTK ? R : 1); ++j) {
+      s0v[j] = s1v[j] = T(0);
+#pragma unroll
+      for (int q = 0; q < KT; ++q) s0d[j][q] = s1d[j][q] = T(0);
     }
     for (uint32_t base = pb; base < pe; base += 64u) {
       uint4 cw = make_uint4(0u, 0u, 0u, 0u);
@@ -205,12 +217,31 @@ __global__ void __launch_bounds__(W * 64) sr_grad_kernel(const SrGradArgs<T> a) 
         const T* sp = my_stk + size_t(idx) * NV * R * 64;
         if (load) {
           if (opc >= SR_OP_LOAD_FEAT_PUSH) {
-            T* pp = my_stk + size_t(((meta >> SR_M_PUSH_SHIFT) & 0x3fu) - 1u) * NV * R * 64;
+            const uint32_t ps = ((meta >> SR_M_PUSH_SHIFT) & 0x3fu) - 1u;
+            if constexpr (VSTK) {
+              if (ps == 0u) {
 #pragma unroll
-            for (int j = 0; j < R; ++j) {
-              pp[j * 64] = v[j];
+                for (int j = 0; j < R; ++j) {
+                  s0v[j] = v[j];
 #pragma unroll
-              for (int q = 0; q < KT; ++q) pp[((q + 1) * R + j) * 64] = dv[j][q];
+                  for (int q = 0; q < KT; ++q) s0d[j][q] = dv[j][q];
+                }
+              } else {
+#pragma unroll
+                for (int j = 0; j < R; ++j) {
+                  s1v[j] = v[j];
+#pragma unroll
+                  for (int q = 0; q < KT; ++q) s1d[j][q] = dv[j][q];
+                }
+              }
+            } else {
+              T* pp = my_stk + size_t(ps) * NV * R * 64;
+#pragma unroll
+              for (int j = 0; j < R; ++j) {
+                pp[j * 64] = v[j];
+#pragma unroll
+                for (int q = 0; q < KT; ++q) pp[((q + 1) * R + j) * 64] = dv[j][q];
+              }
             }
           }
 #pragma unroll
@@ -317,9 +348,21 @@ __global__ void __launch_bounds__(W * 64) sr_grad_kernel(const SrGradArgs<T> a) 
 #pragma unroll
               for (int q = 0; q < KT; ++q) od[q] = T(0);
             } else if (from_stack) {
-              ov = sp[j * 64];
+              if constexpr (VSTK) {
+                if (idx == 0u) {
+                  ov = s0v[j];
 #pragma unroll
-              for (int q = 0; q < KT; ++q) od[q] = sp[((q + 1) * R + j) * 64];
+                  for (int q = 0; q < KT; ++q) od[q] = s0d[j][q];
+                } else {
+                  ov = s1v[j];
+#pragma unroll
+                  for (int q = 0; q < KT; ++q) od[q] = s1d[j][q];
+                }
+              } else {
+                ov = sp[j * 64];
+#pragma unroll
+                for (int q = 0; q < KT; ++q) od[q] = sp[((q + 1) * R + j) * 64];
+              }
             } else {
               ov = cv;
 #pragma unroll
@@ -418,40 +461,45 @@ __global__ void __launch_bounds__(W * 64) sr_grad_kernel(const SrGradArgs<T> a) 
   }
 }
 
-template <typename T, int KT, int W, bool GATHER, int R>
+template <typename T, int KT, int W, bool GATHER, int R, bool VSTK>
 hipError_t sr_launch_grad(const SrGradArgs<T>& a, int n_blocks, hipStream_t s) {
-  const size_t lds = sr_grad_lds_bytes(int(sizeof(T)), KT, R, a.nf, a.w != nullptr, a.stack_depth, W);
-  const void* fn = reinterpret_cast<const void*>(&sr_grad_kernel<T, KT, W, GATHER, R>);
+  const size_t lds = sr_grad_lds_bytes(int(sizeof(T)), KT, R, a.nf, a.w != nullptr, VSTK ? 0 : a.stack_depth, W);
+  const void* fn = reinterpret_cast<const void*>(&sr_grad_kernel<T, KT, W, GATHER, R, VSTK>);
   if (lds > 65536) {
     const hipError_t e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, int(lds));
     if (e != hipSuccess) return e;
   }
-  hipLaunchKernelGGL((sr_grad_kernel<T, KT, W, GATHER, R>), dim3(n_blocks), dim3(W * 64), lds, s, a);
+  hipLaunchKernelGGL((sr_grad_kernel<T, KT, W, GATHER, R, VSTK>), dim3(n_blocks), dim3(W * 64), lds, s, a);
   return hipGetLastError();
 }
 
 // Launch with `rows` rows per lane: the kernels exist for the bucket's default (sr_grad_rows_per_lane),
 // its halves down to 2, and 1 (sr_grad_launch_rows picks one; results do not depend on it: the row
 // blocks cover the same rows whatever the rows per lane, see sr_capi.cpp eval_grad_impl).
-template <typename T, bool GATHER, int KT, int RR>
+template <typename T, bool GATHER, int KT, int RR, bool VSTK>
 hipError_t sr_launch_grad_rows_from(const SrGradArgs<T>& a, int rows, int n_blocks, hipStream_t s) {
-  if (rows == RR) return sr_launch_grad<T, KT, 4, GATHER, RR>(a, n_blocks, s);
-  if constexpr (RR > 1) return sr_launch_grad_rows_from<T, GATHER, KT, RR / 2>(a, rows, n_blocks, s);
+  if (rows == RR) return sr_launch_grad<T, KT, 4, GATHER, RR, VSTK>(a, n_blocks, s);
+  if constexpr (RR > 1) return sr_launch_grad_rows_from<T, GATHER, KT, RR / 2, VSTK>(a, rows, n_blocks, s);
   return hipErrorInvalidValue;
 }
 
 template <typename T>
-hipError_t sr_launch_grad_any(const SrGradArgs<T>& a, int kt, bool gather, int rows, int n_blocks, hipStream_t s) {
-  auto go = [&](auto g) -> hipError_t {
+hipError_t sr_launch_grad_any(const SrGradArgs<T>& a, int kt, bool gather, int rows, bool vstk, int n_blocks,
+                              hipStream_t s) {
+  auto go = [&](auto g, auto v) -> hipError_t {
     constexpr bool G = decltype(g)::value;
+    constexpr bool V = decltype(v)::value;
     switch (kt) {
-      case 1: return sr_launch_grad_rows_from<T, G, 1, sr_grad_rows_per_lane(1)>(a, rows, n_blocks, s);
-      case 2: return sr_launch_grad_rows_from<T, G, 2, sr_grad_rows_per_lane(2)>(a, rows, n_blocks, s);
-      case 4: return sr_launch_grad_rows_from<T, G, 4, sr_grad_rows_per_lane(4)>(a, rows, n_blocks, s);
-      case 8: return sr_launch_grad_rows_from<T, G, 8, sr_grad_rows_per_lane(8)>(a, rows, n_blocks, s);
-      case 16: return sr_launch_grad_rows_from<T, G, 16, sr_grad_rows_per_lane(16)>(a, rows, n_blocks, s);
+      case 1: return sr_launch_grad_rows_from<T, G, 1, sr_grad_rows_per_lane(1), V>(a, rows, n_blocks, s);
+      case 2: return sr_launch_grad_rows_from<T, G, 2, sr_grad_rows_per_lane(2), V>(a, rows, n_blocks, s);
+      case 4: return sr_launch_grad_rows_from<T, G, 4, sr_grad_rows_per_lane(4), V>(a, rows, n_blocks, s);
+      case 8: return sr_launch_grad_rows_from<T, G, 8, sr_grad_rows_per_lane(8), V>(a, rows, n_blocks, s);
+      case 16:  // (16 tangents: two register slots would cost the kernel its occupancy; LDS stack only)
+        if constexpr (V) return hipErrorInvalidValue;
+        else return sr_launch_grad_rows_from<T, G, 16, sr_grad_rows_per_lane(16), false>(a, rows, n_blocks, s);
       default: return hipErrorInvalidValue;
     }
   };
-  return gather ? go(std::true_type{}) : go(std::false_type{});
+  if (vstk) return gather ? go(std::true_type{}, std::true_type{}) : go(std::false_type{}, std::true_type{});
+  return gather ? go(std::true_type{}, std::false_type{}) : go(std::false_type{}, std::false_type{});
 }

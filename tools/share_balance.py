@@ -24,7 +24,7 @@ UNARY_COST = {"cos": 6.7, "sin": 6.7, "exp": 2.6, "log": 3.0}
 
 def static_cost(tb, opts):
     deg, op = tb.degree, tb.op
-    names = list(opts.unary_operators)
+    names = list(bench.C2_OPS["unary_operators"])
     node = np.zeros(len(deg))
     node[deg == 2] = 0.95
     for i, n in enumerate(names):  # (op is the 1-based operator index)
