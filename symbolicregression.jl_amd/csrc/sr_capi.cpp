@@ -149,7 +149,6 @@ struct sr_ctx {
   double grad_flops[kGradBuckets] = {};
   int64_t grad_items[kGradBuckets] = {};
   int grad_rows[kGradBuckets] = {};
-  int64_t grad_items_vstk[kGradBuckets] = {};  // items of the register-stack launch
   int n_chunks_last = 0;
   bool derived_last = false;  // the last run_batch launched derived columns (timed by ev_d0/ev_d1)
   int n_derived_last = 0;
@@ -231,7 +230,6 @@ struct sr_ctx {
   int vstk_rows = 0;        // SR_AMD_VSTK_ROWS / "vstk_rows": rows per lane of the register-stack kernel (0: default)
   int grad_rows_force = 0;  // SR_AMD_GRAD_ROWS / "grad_rows": the gradient kernel's rows per lane (0: chosen per call)
   int grad_sort = 1;        // SR_AMD_GRAD_SORT / "grad_sort": gradient work items ordered by program cost
-  int grad_vstk = 1;        // SR_AMD_GRAD_VSTK / "grad_vstk": register-stack gradient launches for shallow programs
   DevBuf group_cnt;      // its per-group counters (zeroed at allocation; each launch leaves them zero)
   int first_chunk = 6;   // SR_AMD_FIRST_CHUNK: the two-chunk pipeline's first chunk is 1/first_chunk
   int64_t chunk_min = 1024;  // SR_AMD_CHUNK_MIN: the two-chunk pipeline runs when its first chunk holds this many trees
@@ -2045,16 +2043,11 @@ int eval_grad_impl(sr_ctx* ctx, const sr_dataset* ds, int opset_id, const sr_tre
       k0s[b].push_back(k0);
     }
   }
-  // register-stack launches (round 5, sr_grad_impl.h VSTK): items whose program needs <= 2 operand-stack
-  // slots, at most 8 tangents.  Without views they go first in their bucket (one launch), the others
-  // after them (a second launch over the same row blocks and partials); with views a bucket is one
-  // launch, register-stack when every item qualifies.
-  auto vstk_ok = [&](uint32_t t, int kt) { return ctx->grad_vstk && kt <= 8 && prog.depth[t] <= 2; };
   // each bucket's items by estimated program cost, longest first (stable): the kWaves waves of a
   // workgroup share every row tile and wait for each other at its barrier, so items of similar cost go
   // together (an item's gradient does not depend on its position: bit-identical either way)
-  std::vector<double> tcost(size_t(nt), 0.0);
-  if (ctx->grad_sort)
+  if (ctx->grad_sort) {
+    std::vector<double> tcost(size_t(nt), 0.0);
     for (int64_t t = 0; t < nt; ++t) {
       double c = 0.0;
       for (uint32_t i = prog.offsets[size_t(t)]; i < prog.offsets[size_t(t) + 1]; ++i) {
@@ -2066,27 +2059,18 @@ int eval_grad_impl(sr_ctx* ctx, const sr_dataset* ds, int opset_id, const sr_tre
       }
       tcost[size_t(t)] = c;
     }
-  int64_t n_vstk[kNB] = {};  // items of the register-stack launch (the bucket's first n_vstk)
-  for (int b = 0; b < kNB; ++b) {
-    const int kt = kts[b];
-    std::vector<size_t> ord(items[b].size());
-    for (size_t i = 0; i < ord.size(); ++i) ord[i] = i;
-    const bool split = n_views == 1;
-    std::stable_sort(ord.begin(), ord.end(), [&](size_t x, size_t y) {
-      const uint32_t tx = items[b][x], ty = items[b][y];
-      if (split && vstk_ok(tx, kt) != vstk_ok(ty, kt)) return vstk_ok(tx, kt);
-      return tcost[tx] > tcost[ty];
-    });
-    std::vector<uint32_t> it2(ord.size()), k2(ord.size());
-    for (size_t i = 0; i < ord.size(); ++i) {
-      it2[i] = items[b][ord[i]];
-      k2[i] = k0s[b][ord[i]];
+    for (int b = 0; b < kNB; ++b) {
+      std::vector<size_t> ord(items[b].size());
+      for (size_t i = 0; i < ord.size(); ++i) ord[i] = i;
+      std::stable_sort(ord.begin(), ord.end(), [&](size_t x, size_t y) { return tcost[items[b][x]] > tcost[items[b][y]]; });
+      std::vector<uint32_t> it2(ord.size()), k2(ord.size());
+      for (size_t i = 0; i < ord.size(); ++i) {
+        it2[i] = items[b][ord[i]];
+        k2[i] = k0s[b][ord[i]];
+      }
+      items[b].swap(it2);
+      k0s[b].swap(k2);
     }
-    items[b].swap(it2);
-    k0s[b].swap(k2);
-    int64_t nv = 0;
-    for (uint32_t t : items[b]) nv += vstk_ok(t, kt) ? 1 : 0;
-    n_vstk[b] = split ? nv : (nv == int64_t(items[b].size()) ? nv : 0);
   }
   hipStream_t s = ctx->stream;
   // the loss pass's in-order folds re-upload their own view's rows: put every view's rows back
@@ -2161,24 +2145,19 @@ int eval_grad_impl(sr_ctx* ctx, const sr_dataset* ds, int opset_id, const sr_tre
   std::vector<double> vden(static_cast<size_t>(n_views));
   for (int v = 0; v < n_views; ++v) vden[size_t(v)] = view_denominator<T>(ds, gather ? row_idx + int64_t(v) * n_idx : nullptr, n_idx);
   size_t part_need = 0;
-  // per bucket: the register-stack launch (items [0, nv): rows_v rows per lane, groups_v) and the
-  // LDS-stack launch (items [nv, ni)); both over the same row blocks, one partials array, one reduce
-  struct Launch { int64_t n_rb, tiles_per_block, n_groups, nv, groups_v, tiles_v; int rows, depth, rows_v; };
+  struct Launch { int64_t n_rb, tiles_per_block, n_groups; int rows, depth; };
   Launch lc[kNB] = {};
   for (int b = 0; b < kNB; ++b) {
     const int64_t ni = int64_t(items[b].size());
     if (ni == 0) continue;
     const int kt = kts[b];
-    const int64_t nv = n_vstk[b];
-    // the LDS launch's deepest program sizes its operand stacks; rows per lane drop to 1 when the
+    // the bucket's own deepest program sizes its LDS operand stacks; rows per lane drop to 1 when the
     // default's tile + stacks would not fit (many features, Float64, deep trees: ADVICE r3)
     int bdepth = 1;
-    for (int64_t i = nv; i < ni; ++i) bdepth = std::max(bdepth, int(prog.depth[items[b][size_t(i)]]));
+    for (uint32_t t : items[b]) bdepth = std::max(bdepth, int(prog.depth[t]));
     const int rows = sr_grad_launch_rows(int(sizeof(T)), kt, int(ds->nf), ds->w != nullptr, bdepth, kWaves, kLdsMax,
                                          ctx->grad_rows_force);
-    const int rows_v = nv > 0 ? sr_grad_launch_rows(int(sizeof(T)), kt, int(ds->nf), ds->w != nullptr, 0, kWaves,
-                                                    kLdsMax, ctx->grad_rows_force) : 1;
-    if (rows == 0 || rows_v == 0) return set_error(SR_ERR_TOO_DEEP, "gradient tile needs more than 160 KiB of LDS");
+    if (rows == 0) return set_error(SR_ERR_TOO_DEEP, "gradient tile needs more than 160 KiB of LDS");
     int64_t n_groups = (ni + kWaves - 1) / kWaves;
     if (!segs[b].empty()) {  // (view-pure groups: a few more than ni / kWaves)
       n_groups = 0;
@@ -2195,7 +2174,6 @@ int eval_grad_impl(sr_ctx* ctx, const sr_dataset* ds, int opset_id, const sr_tre
     const int64_t units_per_block = (n_units + n_rb - 1) / n_rb;
     n_rb = (n_units + units_per_block - 1) / units_per_block;
     const int64_t tiles_per_block = units_per_block * (kUnit / (64 * int64_t(rows)));
-    const int64_t tiles_v = units_per_block * (kUnit / (64 * int64_t(rows_v)));
     if (n_rb * n_groups > 0x7fffffff) return set_error(SR_ERR_INVALID_ARG, "grid too large");
     int64_t blk = 0;  // segments' first blocks
     for (SrSegment& sg : segs[b]) {
@@ -2203,7 +2181,7 @@ int eval_grad_impl(sr_ctx* ctx, const sr_dataset* ds, int opset_id, const sr_tre
       blk += int64_t(sg.groups) * n_rb;
     }
     if (!segs[b].empty()) std::memcpy(hs + o_segs[b], segs[b].data(), segs[b].size() * sizeof(SrSegment));
-    lc[b] = Launch{n_rb, tiles_per_block, n_groups, nv, (nv + kWaves - 1) / kWaves, tiles_v, rows, bdepth, rows_v};
+    lc[b] = Launch{n_rb, tiles_per_block, n_groups, rows, bdepth};
     part_need = std::max(part_need, size_t(n_rb) * size_t(ni) * size_t(kt));
   }
   SR_HIP_CHECK(hipMemcpyAsync(ds_, hs, stage_bytes, hipMemcpyHostToDevice, s));
@@ -2218,8 +2196,7 @@ int eval_grad_impl(sr_ctx* ctx, const sr_dataset* ds, int opset_id, const sr_tre
   for (int b = 0; b < kNB; ++b) {
     ctx->grad_timed[b] = false;
     ctx->grad_items[b] = int64_t(items[b].size());
-    ctx->grad_rows[b] = lc[b].nv * 2 >= int64_t(items[b].size()) ? lc[b].rows_v : lc[b].rows;
-    ctx->grad_items_vstk[b] = lc[b].nv;
+    ctx->grad_rows[b] = lc[b].rows;
     double per_row = 0.0;
     const double kt = kts[b];
     for (uint32_t t : items[b]) {
@@ -2244,8 +2221,6 @@ int eval_grad_impl(sr_ctx* ctx, const sr_dataset* ds, int opset_id, const sr_tre
     a.item_tree = reinterpret_cast<const uint32_t*>(ds_ + o_items[b]);
     a.item_k0 = a.item_tree + ni;
     a.n_items = int(ni);
-    a.item0 = 0;
-    a.item_end = int(ni);
     a.X = static_cast<const T*>(ds->X);
     a.y = static_cast<const T*>(ds->y);
     a.w = static_cast<const T*>(ds->w);
@@ -2265,26 +2240,7 @@ int eval_grad_impl(sr_ctx* ctx, const sr_dataset* ds, int opset_id, const sr_tre
       a.n_segs = int(segs[b].size());
     }
     if (ctx->timing) SR_HIP_CHECK(hipEventRecord(ctx->ev_g0[b], s));
-    if (!segs[b].empty()) {  // several views: one launch (register-stack iff every item qualifies)
-      const bool v = lc[b].nv == ni;
-      if (v) a.tiles_per_block = int(lc[b].tiles_v);
-      SR_HIP_CHECK(sr_launch_grad_any<T>(a, kt, gather, v ? lc[b].rows_v : lc[b].rows, v,
-                                         int(lc[b].n_rb * lc[b].n_groups), s));
-    } else {
-      if (lc[b].nv > 0) {  // items [0, nv): register stack
-        SrGradArgs<T> av = a;
-        av.item_end = int(lc[b].nv);
-        av.n_groups = int(lc[b].groups_v);
-        av.tiles_per_block = int(lc[b].tiles_v);
-        SR_HIP_CHECK(sr_launch_grad_any<T>(av, kt, gather, lc[b].rows_v, true, int(lc[b].n_rb * lc[b].groups_v), s));
-      }
-      if (lc[b].nv < ni) {  // items [nv, ni): LDS stack
-        SrGradArgs<T> al = a;
-        al.item0 = int(lc[b].nv);
-        al.n_groups = int((ni - lc[b].nv + kWaves - 1) / kWaves);
-        SR_HIP_CHECK(sr_launch_grad_any<T>(al, kt, gather, lc[b].rows, false, int(lc[b].n_rb * al.n_groups), s));
-      }
-    }
+    SR_HIP_CHECK(sr_launch_grad_any<T>(a, kt, gather, lc[b].rows, int(lc[b].n_rb * lc[b].n_groups), s));
     if (ctx->timing) {
       SR_HIP_CHECK(hipEventRecord(ctx->ev_g1[b], s));
       ctx->grad_timed[b] = true;
@@ -3035,7 +2991,6 @@ int sr_init(int device, sr_ctx** out) {
   if (const char* v = std::getenv("SR_AMD_FUSED_REDUCE")) ctx->fused_reduce = std::atoll(v);
   if (const char* v = std::getenv("SR_AMD_GRAD_ROWS")) ctx->grad_rows_force = std::atoi(v);
   if (const char* v = std::getenv("SR_AMD_GRAD_SORT")) ctx->grad_sort = std::atoi(v) != 0 ? 1 : 0;
-  if (const char* v = std::getenv("SR_AMD_GRAD_VSTK")) ctx->grad_vstk = std::atoi(v) != 0 ? 1 : 0;
   if (const char* v = std::getenv("SR_AMD_VSTK_ROWS")) ctx->vstk_rows = std::atoi(v);
   if (const char* v = std::getenv("SR_AMD_FIRST_CHUNK")) ctx->first_chunk = std::max(2, std::atoi(v));
   if (const char* v = std::getenv("SR_AMD_CHUNK_MIN")) ctx->chunk_min = std::max<int64_t>(1, std::atoll(v));
@@ -3783,10 +3738,6 @@ int sr_set_tuning(sr_ctx* ctx, const char* name, int64_t value) {
   Lock l(ctx);
   if (std::strcmp(name, "derived") == 0) {
     ctx->derived = value != 0 ? 1 : 0;
-    return SR_OK;
-  }
-  if (std::strcmp(name, "grad_vstk") == 0) {  // register-stack gradient launches (SR_AMD_GRAD_VSTK)
-    ctx->grad_vstk = value != 0 ? 1 : 0;
     return SR_OK;
   }
   if (std::strcmp(name, "grad_sort") == 0) {  // gradient work items ordered by program cost (SR_AMD_GRAD_SORT)

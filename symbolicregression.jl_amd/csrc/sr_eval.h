@@ -207,8 +207,7 @@ struct SrGradArgs {
   const uint32_t* const_off; // [n_trees + 1]
   const uint32_t* item_tree; // work item -> tree
   const uint32_t* item_k0;   // work item -> first tangent (constant index)
-  int n_items;                // the bucket's items (the partials' stride)
-  int item0, item_end;        // this launch's items [item0, item_end) (no segments)
+  int n_items;
   const T* X;
   const T* y;
   const T* w;
@@ -228,10 +227,8 @@ struct SrGradArgs {
 };
 
 // rows: rows per lane, sr_grad_rows_per_lane(kt) or 1 (sr_grad_launch_rows)
-// vstk: the register-stack build (programs of <= 2 operand-stack slots; kt <= 8)
 template <typename T>
-hipError_t sr_launch_grad_any(const SrGradArgs<T>& a, int kt, bool gather, int rows, bool vstk, int n_blocks,
-                              hipStream_t s);
+hipError_t sr_launch_grad_any(const SrGradArgs<T>& a, int kt, bool gather, int rows, int n_blocks, hipStream_t s);
 // Largest rows per lane of the gradient kernel for KT tangents (a staged tile is 64 x that many rows);
 // kernels exist for it, its halves down to 2, and 1.
 constexpr int sr_grad_rows_per_lane(int kt) { return kt <= 2 ? 8 : (kt <= 4 ? 4 : (kt <= 8 ? 2 : 1)); }

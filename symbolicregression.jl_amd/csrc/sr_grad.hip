@@ -24,5 +24,5 @@ hipError_t sr_launch_grad_reduce(const double* part, int n_row_blocks, int n_val
   return hipGetLastError();
 }
 
-template hipError_t sr_launch_grad_any<float>(const SrGradArgs<float>&, int, bool, int, bool, int, hipStream_t);
+template hipError_t sr_launch_grad_any<float>(const SrGradArgs<float>&, int, bool, int, int, hipStream_t);
 // (Float64: sr_grad_f64.hip, a translation unit of its own so the two compile in parallel)

@@ -101,11 +101,7 @@ __device__ __attribute__((noinline)) SrGVec<T, R> sr_grad_loss_der(int kind, SrG
 // R: rows per lane (sr_grad_launch_rows: up to 8 for 1-2 tangents, 4 for 4, 2 for 8, 1 for 16): the
 // value and its KT tangents of R rows stay in VGPRs, so one dispatch of an instruction covers R x 64
 // rows (round 3: one row per lane made every dispatch and operand decode cover 64 rows only).
-// VSTK (round 5): programs of at most two operand-stack slots keep both slots in VGPRs (value and
-// tangents of R rows each) instead of the per-wave LDS stack — no LDS traffic per push / operand, and
-// a workgroup's LDS is its row tile only, so more workgroups share a CU.  The same arithmetic in the
-// same order: bit-identical to the LDS-stack kernel.
-template <typename T, int KT, int W, bool GATHER, int R, bool VSTK>
+template <typename T, int KT, int W, bool GATHER, int R>
 __global__ void __launch_bounds__(W * 64) sr_grad_kernel(const SrGradArgs<T> a) {
   // rows per lane: lane + 64 j, j < R
   constexpr int ROWS = 64 * R;               // rows per staged tile
@@ -120,12 +116,12 @@ __global__ void __launch_bounds__(W * 64) sr_grad_kernel(const SrGradArgs<T> a) 
   T* stk = wsv + (a.w ? ROWS : 0);                             // [W][depth][NV][R][64]
   T* my_stk = stk + size_t(wave) * a.stack_depth * NV * R * 64 + lane;
 
-  int tg, rb, item, item_end = a.item_end;
+  int tg, rb, item, item_end = a.n_items;
   const int64_t* ridx = a.row_idx;  // GATHER: this block's row view
-  if (a.segs == nullptr) {  // (this launch's items: [item0, item_end) of the bucket's n_items)
+  if (a.segs == nullptr) {
     tg = int(blockIdx.x) % a.n_groups;
     rb = int(blockIdx.x) / a.n_groups;
-    item = a.item0 + tg * W + wave;
+    item = tg * W + wave;
   } else {
     // several row views in one launch (sr_eval_grad_batch_views): segment = one view's work items
     int lo = 0, hi = a.n_segs - 1;
@@ -180,19 +176,11 @@ __global__ void __launch_bounds__(W * 64) sr_grad_kernel(const SrGradArgs<T> a) 
 
     T v[R];
     T dv[R][KT];
-    T s0v[VSTK ? R : 1], s1v[VSTK ? R : 1];  // VSTK: stack slots 0 and 1 (value, tangents)
-    T s0d[VSTK ? R : 1][KT], s1d[VSTK ? R : 1][KT];
 #pragma unroll
     for (int j = 0; j < R; ++j) {
       v[j] = T(0);
 #pragma unroll
       for (int q = 0; q < KT; ++q) dv[j][q] = T(0);
-    }
-#pragma unroll
-    for (int j = 0; j < (VSTK ? R : 1); ++j) {
-      s0v[j] = s1v[j] = T(0);
-#pragma unroll
-      for (int q = 0; q < KT; ++q) s0d[j][q] = s1d[j][q] = T(0);
     }
     for (uint32_t base = pb; base < pe; base += 64u) {
       uint4 cw = make_uint4(0u, 0u, 0u, 0u);
@@ -202,207 +190,253 @@ __global__ void __launch_bounds__(W * 64) sr_grad_kernel(const SrGradArgs<T> a) 
         const uint32_t opc = uint32_t(__builtin_amdgcn_readlane(int(cw.x), int(k)));
         const uint32_t meta = uint32_t(__builtin_amdgcn_readlane(int(cw.y), int(k)));
         const uint32_t idx = meta & SR_M_INDEX;  // feature / stack slot / constant slot
-        uint32_t variant = 6u;
-        if (opc >= SR_OP_BINARY0) variant = (opc - SR_OP_BINARY0) % 6u;
-        const bool load = opc <= SR_OP_LOAD_CONST_PUSH;
-        const bool from_feat = (load && (opc == SR_OP_LOAD_FEAT || opc == SR_OP_LOAD_FEAT_PUSH)) ||
-                               variant == SR_V_FL || variant == SR_V_FR;
-        const bool from_stack = variant == SR_V_SL || variant == SR_V_SR;
         // a constant operand: its value (wave-uniform) and its one-hot tangent e_{idx-k0}
-        T cv = T(0);
+        auto const_val = [&]() -> T {
+          return idx < 64u ? sr_readlane_val<T>(cval0, idx) : sr_readlane_val<T>(cval1, idx - 64u);
+        };
         const int jj = int(idx) - int(k0);
-        if (!from_feat && !from_stack)
-          cv = idx < 64u ? sr_readlane_val<T>(cval0, idx) : sr_readlane_val<T>(cval1, idx - 64u);
         const T* xrow = xs + size_t(idx) * ROWS + lane;
         const T* sp = my_stk + size_t(idx) * NV * R * 64;
-        if (load) {
-          if (opc >= SR_OP_LOAD_FEAT_PUSH) {
-            const uint32_t ps = ((meta >> SR_M_PUSH_SHIFT) & 0x3fu) - 1u;
-            if constexpr (VSTK) {
-              if (ps == 0u) {
+        auto push = [&]() {
+          T* pp = my_stk + size_t(((meta >> SR_M_PUSH_SHIFT) & 0x3fu) - 1u) * NV * R * 64;
 #pragma unroll
-                for (int j = 0; j < R; ++j) {
-                  s0v[j] = v[j];
+          for (int j = 0; j < R; ++j) {
+            pp[j * 64] = v[j];
 #pragma unroll
-                  for (int q = 0; q < KT; ++q) s0d[j][q] = dv[j][q];
-                }
-              } else {
+            for (int q = 0; q < KT; ++q) pp[((q + 1) * R + j) * 64] = dv[j][q];
+          }
+        };
+        // r = op(a, b) and its tangents dr = pa da + pb db (pa, pb: the partials) for one of the
+        // BASIC binaries with the operand variant known at compile time (round 5: one flat dispatch
+        // per instruction instead of decoding the variant; the operand's tangent is known zero for a
+        // feature and one-hot for a constant, so those products are not computed).  Every value is
+        // the one the general form fma(pa, da, pb db) gives: a product by an exact 0 or 1 and a sum
+        // with an exact 0 are exact (up to the sign of a zero, which the gradient sums cannot see).
+        auto basic_bin = [&](auto op_c, auto var_c) {
+          constexpr uint32_t B = decltype(op_c)::value;
+          constexpr uint32_t V = decltype(var_c)::value;
+          constexpr bool LEFT = V == SR_V_SL || V == SR_V_FL || V == SR_V_CL;  // the operand is a
+          constexpr int SRC = (V == SR_V_SL || V == SR_V_SR) ? 0 : ((V == SR_V_FL || V == SR_V_FR) ? 1 : 2);
+          T cv = T(0);
+          if constexpr (SRC == 2) cv = const_val();
+          T fix[R] = {};  // constant operand: the tangent at its own slot jj, from the unscaled dv
+          const bool hot = SRC == 2 && jj >= 0 && jj < KT;
 #pragma unroll
-                for (int j = 0; j < R; ++j) {
-                  s1v[j] = v[j];
-#pragma unroll
-                  for (int q = 0; q < KT; ++q) s1d[j][q] = dv[j][q];
-                }
-              }
+          for (int j = 0; j < R; ++j) {
+            const T ov = SRC == 0 ? sp[j * 64] : (SRC == 1 ? xrow[j * 64] : cv);
+            const T av = LEFT ? ov : v[j], bv = LEFT ? v[j] : ov;
+            const T rv = sr_binary<T>(B, av, bv);
+            T pa, pbv;
+            if constexpr (B == SR_B_DIV) {  // d/da = 1/b, d/db = -(a/b)/b = -r (1/b): one division fewer
+              pa = T(1) / bv;
+              pbv = -rv * pa;
             } else {
-              T* pp = my_stk + size_t(ps) * NV * R * 64;
-#pragma unroll
-              for (int j = 0; j < R; ++j) {
-                pp[j * 64] = v[j];
-#pragma unroll
-                for (int q = 0; q < KT; ++q) pp[((q + 1) * R + j) * 64] = dv[j][q];
-              }
+              sr_binary_partials<T>(B, av, bv, rv, &pa, &pbv);
             }
-          }
+            v[j] = rv;
+            if constexpr (SRC == 0) {  // stack operand: its tangents from the slot
 #pragma unroll
-          for (int j = 0; j < R; ++j) {
-            v[j] = from_feat ? xrow[j * 64] : cv;
-#pragma unroll
-            for (int q = 0; q < KT; ++q) dv[j][q] = (!from_feat && q == jj) ? T(1) : T(0);
-          }
-        } else if (opc < SR_OP_BINARY0) {
-          const uint32_t u = opc >= SR_OP_UNARY_INF0 ? opc - SR_OP_UNARY_INF0 : opc - SR_OP_UNARY0;
-          // value and derivative rows: the BASIC operators with the loss kernel's own row bodies
-          // (sr_unary_rows: the same values), the rest through the noinline row callees
-          // (fused unaries: complete trees have finite inner values, so INFSUB never fires)
-          T dfx[R];
-          switch (u) {
-            case SR_U_NEG:
-#pragma unroll
-              for (int j = 0; j < R; ++j) {
-                v[j] = -v[j];
-                dfx[j] = T(-1);
-              }
-              break;
-            case SR_U_SQUARE:
-#pragma unroll
-              for (int j = 0; j < R; ++j) {
-                const T x = v[j];
-                v[j] = x * x;
-                dfx[j] = T(2) * x;
-              }
-              break;
-            case SR_U_CUBE:
-#pragma unroll
-              for (int j = 0; j < R; ++j) {
-                const T x = v[j];
-                v[j] = x * x * x;
-                dfx[j] = T(3) * x * x;
-              }
-              break;
-            case SR_U_ABS:
-#pragma unroll
-              for (int j = 0; j < R; ++j) {
-                const T x = v[j];
-                v[j] = sr_unary<T>(SR_U_ABS, x);
-                dfx[j] = sr_unary_deriv<T>(SR_U_ABS, x, v[j]);
-              }
-              break;
-            case SR_U_SQRT:
-#pragma unroll
-              for (int j = 0; j < R; ++j) {
-                v[j] = sr_unary<T>(SR_U_SQRT, v[j]);
-                dfx[j] = T(0.5) / v[j];
-              }
-              break;
-            case SR_U_EXP:
-              sr_unary_rows<T, SR_U_EXP, R>(v);
-#pragma unroll
-              for (int j = 0; j < R; ++j) dfx[j] = v[j];
-              break;
-            case SR_U_LOG:
-#pragma unroll
-              for (int j = 0; j < R; ++j) dfx[j] = T(1) / v[j];
-              sr_unary_rows<T, SR_U_LOG, R>(v);
-              break;
-            case SR_U_COS:
-#pragma unroll
-              for (int j = 0; j < R; ++j) dfx[j] = v[j];
-              sr_unary_rows<T, SR_U_COS, R>(v);
-              sr_unary_rows<T, SR_U_SIN, R>(dfx);
-#pragma unroll
-              for (int j = 0; j < R; ++j) dfx[j] = -dfx[j];
-              break;
-            case SR_U_SIN:
-#pragma unroll
-              for (int j = 0; j < R; ++j) dfx[j] = v[j];
-              sr_unary_rows<T, SR_U_SIN, R>(v);
-              sr_unary_rows<T, SR_U_COS, R>(dfx);
-              break;
-            default: {
-              SrGVec<T, R> x, y;
-#pragma unroll
-              for (int j = 0; j < R; ++j) x[j] = v[j];
-              y = sr_grad_unary_val<T, R>(u, x);
-              x = sr_grad_unary_der<T, R>(u, x, y);
-#pragma unroll
-              for (int j = 0; j < R; ++j) {
-                v[j] = y[j];
-                dfx[j] = x[j];
-              }
-              break;
-            }
-          }
-#pragma unroll
-          for (int j = 0; j < R; ++j) {
-#pragma unroll
-            for (int q = 0; q < KT; ++q) dv[j][q] = dfx[j] * dv[j][q];
-          }
-        } else {
-          const uint32_t b = (opc - SR_OP_BINARY0) / 6u + 1u;
-          const bool left = variant == SR_V_SL || variant == SR_V_FL || variant == SR_V_CL;
-          // operand row j: value and tangents (feature / stack slot / constant)
-          auto operand = [&](int j, T& ov, T (&od)[KT]) {
-            if (from_feat) {
-              ov = xrow[j * 64];
-#pragma unroll
-              for (int q = 0; q < KT; ++q) od[q] = T(0);
-            } else if (from_stack) {
-              if constexpr (VSTK) {
-                if (idx == 0u) {
-                  ov = s0v[j];
-#pragma unroll
-                  for (int q = 0; q < KT; ++q) od[q] = s0d[j][q];
+              for (int q = 0; q < KT; ++q) {
+                const T od = sp[((q + 1) * R + j) * 64];
+                if constexpr (B == SR_B_ADD) {
+                  dv[j][q] = LEFT ? od + dv[j][q] : dv[j][q] + od;
+                } else if constexpr (B == SR_B_SUB) {
+                  dv[j][q] = LEFT ? od - dv[j][q] : dv[j][q] - od;
                 } else {
-                  ov = s1v[j];
-#pragma unroll
-                  for (int q = 0; q < KT; ++q) od[q] = s1d[j][q];
+                  dv[j][q] = LEFT ? __builtin_fma(pa, od, pbv * dv[j][q]) : __builtin_fma(pa, dv[j][q], pbv * od);
                 }
-              } else {
-                ov = sp[j * 64];
-#pragma unroll
-                for (int q = 0; q < KT; ++q) od[q] = sp[((q + 1) * R + j) * 64];
               }
             } else {
-              ov = cv;
+              // feature (zero tangent) or constant (one-hot at jj): every slot is the tos tangent
+              // scaled by its own partial; a constant's own slot adds the constant's partial
+              if (SRC == 2 && hot) {
+                T d0 = T(0);
 #pragma unroll
-              for (int q = 0; q < KT; ++q) od[q] = q == jj ? T(1) : T(0);
+                for (int q = 0; q < KT; ++q)
+                  if (q == jj) d0 = dv[j][q];  // (jj is uniform: a scalar-selected move)
+                fix[j] = LEFT ? pa + pbv * d0 : __builtin_fma(pa, d0, pbv);
+              }
+              if constexpr (B == SR_B_ADD) {
+                // scale 1: unchanged
+              } else if constexpr (B == SR_B_SUB) {
+                if constexpr (LEFT) {
+#pragma unroll
+                  for (int q = 0; q < KT; ++q) dv[j][q] = -dv[j][q];
+                }
+              } else {
+                const T sc = LEFT ? pbv : pa;
+#pragma unroll
+                for (int q = 0; q < KT; ++q) dv[j][q] = sc * dv[j][q];
+              }
             }
-          };
-          auto tangents = [&](int j, T pa, T pbv, const T (&od)[KT]) {
-            if (left) {
+          }
+          if (SRC == 2 && hot) {
 #pragma unroll
-              for (int q = 0; q < KT; ++q) dv[j][q] = __builtin_fma(pa, od[q], pbv * dv[j][q]);
-            } else {
+            for (int q = 0; q < KT; ++q)
+              if (q == jj) {
 #pragma unroll
-              for (int q = 0; q < KT; ++q) dv[j][q] = __builtin_fma(pa, dv[j][q], pbv * od[q]);
-            }
-          };
-          auto basic_rows = [&](auto op_c) {
-            constexpr uint32_t BID = decltype(op_c)::value;
+                for (int j = 0; j < R; ++j) dv[j][q] = fix[j];
+              }
+          }
+        };
+        switch (opc) {
+          case SR_OP_LOAD_FEAT_PUSH:
+            push();
+            [[fallthrough]];
+          case SR_OP_LOAD_FEAT:
 #pragma unroll
             for (int j = 0; j < R; ++j) {
-              T ov, od[KT];
-              operand(j, ov, od);
-              const T av = left ? ov : v[j], bv = left ? v[j] : ov;
-              const T rv = sr_binary<T>(BID, av, bv);
-              T pa, pbv;
-              if constexpr (BID == SR_B_DIV) {  // d/da = 1/b, d/db = -(a/b)/b = -r (1/b): one division fewer
-                pa = T(1) / bv;
-                pbv = -rv * pa;
-              } else {
-                sr_binary_partials<T>(BID, av, bv, rv, &pa, &pbv);
-              }
-              v[j] = rv;
-              tangents(j, pa, pbv, od);
+              v[j] = xrow[j * 64];
+#pragma unroll
+              for (int q = 0; q < KT; ++q) dv[j][q] = T(0);
             }
-          };
-          switch (b) {
-            case SR_B_ADD: basic_rows(std::integral_constant<uint32_t, SR_B_ADD>{}); break;
-            case SR_B_SUB: basic_rows(std::integral_constant<uint32_t, SR_B_SUB>{}); break;
-            case SR_B_MUL: basic_rows(std::integral_constant<uint32_t, SR_B_MUL>{}); break;
-            case SR_B_DIV: basic_rows(std::integral_constant<uint32_t, SR_B_DIV>{}); break;
-            default: {  // the other operators: value and partials through the row callees
+            break;
+          case SR_OP_LOAD_CONST_PUSH:
+            push();
+            [[fallthrough]];
+          case SR_OP_LOAD_CONST: {
+            const T cv = const_val();
+#pragma unroll
+            for (int j = 0; j < R; ++j) {
+              v[j] = cv;
+#pragma unroll
+              for (int q = 0; q < KT; ++q) dv[j][q] = q == jj ? T(1) : T(0);
+            }
+            break;
+          }
+#define SR_GRAD_BCASE(B)                                                                                  \
+  case SR_BIN_OPC(B, SR_V_SL): basic_bin(std::integral_constant<uint32_t, B>{}, std::integral_constant<uint32_t, SR_V_SL>{}); break; \
+  case SR_BIN_OPC(B, SR_V_SR): basic_bin(std::integral_constant<uint32_t, B>{}, std::integral_constant<uint32_t, SR_V_SR>{}); break; \
+  case SR_BIN_OPC(B, SR_V_FL): basic_bin(std::integral_constant<uint32_t, B>{}, std::integral_constant<uint32_t, SR_V_FL>{}); break; \
+  case SR_BIN_OPC(B, SR_V_FR): basic_bin(std::integral_constant<uint32_t, B>{}, std::integral_constant<uint32_t, SR_V_FR>{}); break; \
+  case SR_BIN_OPC(B, SR_V_CL): basic_bin(std::integral_constant<uint32_t, B>{}, std::integral_constant<uint32_t, SR_V_CL>{}); break; \
+  case SR_BIN_OPC(B, SR_V_CR): basic_bin(std::integral_constant<uint32_t, B>{}, std::integral_constant<uint32_t, SR_V_CR>{}); break;
+          SR_GRAD_BCASE(SR_B_ADD)
+          SR_GRAD_BCASE(SR_B_SUB)
+          SR_GRAD_BCASE(SR_B_MUL)
+          SR_GRAD_BCASE(SR_B_DIV)
+#undef SR_GRAD_BCASE
+          default:
+            if (opc < SR_OP_BINARY0) {
+              const uint32_t u = opc >= SR_OP_UNARY_INF0 ? opc - SR_OP_UNARY_INF0 : opc - SR_OP_UNARY0;
+              // value and derivative rows: the BASIC operators with the loss kernel's own row bodies
+              // (sr_unary_rows: the same values), the rest through the noinline row callees
+              // (fused unaries: complete trees have finite inner values, so INFSUB never fires)
+              T dfx[R];
+              switch (u) {
+                case SR_U_NEG:
+#pragma unroll
+                  for (int j = 0; j < R; ++j) {
+                    v[j] = -v[j];
+                    dfx[j] = T(-1);
+                  }
+                  break;
+                case SR_U_SQUARE:
+#pragma unroll
+                  for (int j = 0; j < R; ++j) {
+                    const T x = v[j];
+                    v[j] = x * x;
+                    dfx[j] = T(2) * x;
+                  }
+                  break;
+                case SR_U_CUBE:
+#pragma unroll
+                  for (int j = 0; j < R; ++j) {
+                    const T x = v[j];
+                    v[j] = x * x * x;
+                    dfx[j] = T(3) * x * x;
+                  }
+                  break;
+                case SR_U_ABS:
+#pragma unroll
+                  for (int j = 0; j < R; ++j) {
+                    const T x = v[j];
+                    v[j] = sr_unary<T>(SR_U_ABS, x);
+                    dfx[j] = sr_unary_deriv<T>(SR_U_ABS, x, v[j]);
+                  }
+                  break;
+                case SR_U_SQRT:
+#pragma unroll
+                  for (int j = 0; j < R; ++j) {
+                    v[j] = sr_unary<T>(SR_U_SQRT, v[j]);
+                    dfx[j] = T(0.5) / v[j];
+                  }
+                  break;
+                case SR_U_EXP:
+                  sr_unary_rows<T, SR_U_EXP, R>(v);
+#pragma unroll
+                  for (int j = 0; j < R; ++j) dfx[j] = v[j];
+                  break;
+                case SR_U_LOG:
+#pragma unroll
+                  for (int j = 0; j < R; ++j) dfx[j] = T(1) / v[j];
+                  sr_unary_rows<T, SR_U_LOG, R>(v);
+                  break;
+                case SR_U_COS:
+#pragma unroll
+                  for (int j = 0; j < R; ++j) dfx[j] = v[j];
+                  sr_unary_rows<T, SR_U_COS, R>(v);
+                  sr_unary_rows<T, SR_U_SIN, R>(dfx);
+#pragma unroll
+                  for (int j = 0; j < R; ++j) dfx[j] = -dfx[j];
+                  break;
+                case SR_U_SIN:
+#pragma unroll
+                  for (int j = 0; j < R; ++j) dfx[j] = v[j];
+                  sr_unary_rows<T, SR_U_SIN, R>(v);
+                  sr_unary_rows<T, SR_U_COS, R>(dfx);
+                  break;
+                default: {
+                  SrGVec<T, R> x, y;
+#pragma unroll
+                  for (int j = 0; j < R; ++j) x[j] = v[j];
+                  y = sr_grad_unary_val<T, R>(u, x);
+                  x = sr_grad_unary_der<T, R>(u, x, y);
+#pragma unroll
+                  for (int j = 0; j < R; ++j) {
+                    v[j] = y[j];
+                    dfx[j] = x[j];
+                  }
+                  break;
+                }
+              }
+#pragma unroll
+              for (int j = 0; j < R; ++j) {
+#pragma unroll
+                for (int q = 0; q < KT; ++q) dv[j][q] = dfx[j] * dv[j][q];
+              }
+            } else {
+              // the other binaries: value and partials through the row callees, the general tangent form
+              const uint32_t b = (opc - SR_OP_BINARY0) / 6u + 1u;
+              const uint32_t variant = (opc - SR_OP_BINARY0) % 6u;
+              const bool left = variant == SR_V_SL || variant == SR_V_FL || variant == SR_V_CL;
+              const bool from_feat = variant == SR_V_FL || variant == SR_V_FR;
+              const bool from_stack = variant == SR_V_SL || variant == SR_V_SR;
+              const T cv = (!from_feat && !from_stack) ? const_val() : T(0);
+              auto operand = [&](int j, T& ov, T (&od)[KT]) {
+                if (from_feat) {
+                  ov = xrow[j * 64];
+#pragma unroll
+                  for (int q = 0; q < KT; ++q) od[q] = T(0);
+                } else if (from_stack) {
+                  ov = sp[j * 64];
+#pragma unroll
+                  for (int q = 0; q < KT; ++q) od[q] = sp[((q + 1) * R + j) * 64];
+                } else {
+                  ov = cv;
+#pragma unroll
+                  for (int q = 0; q < KT; ++q) od[q] = q == jj ? T(1) : T(0);
+                }
+              };
+              auto tangents = [&](int j, T pa, T pbv, const T (&od)[KT]) {
+                if (left) {
+#pragma unroll
+                  for (int q = 0; q < KT; ++q) dv[j][q] = __builtin_fma(pa, od[q], pbv * dv[j][q]);
+                } else {
+#pragma unroll
+                  for (int q = 0; q < KT; ++q) dv[j][q] = __builtin_fma(pa, dv[j][q], pbv * od[q]);
+                }
+              };
               SrGVec<T, R> av, bv;
 #pragma unroll
               for (int j = 0; j < R; ++j) {
@@ -421,9 +455,8 @@ __global__ void __launch_bounds__(W * 64) sr_grad_kernel(const SrGradArgs<T> a) 
                 v[j] = rv[j];
                 tangents(j, pa[j], pbv[j], od);
               }
-              break;
             }
-          }
+            break;
         }
       }
     }
@@ -461,45 +494,40 @@ __global__ void __launch_bounds__(W * 64) sr_grad_kernel(const SrGradArgs<T> a) 
   }
 }
 
-template <typename T, int KT, int W, bool GATHER, int R, bool VSTK>
+template <typename T, int KT, int W, bool GATHER, int R>
 hipError_t sr_launch_grad(const SrGradArgs<T>& a, int n_blocks, hipStream_t s) {
-  const size_t lds = sr_grad_lds_bytes(int(sizeof(T)), KT, R, a.nf, a.w != nullptr, VSTK ? 0 : a.stack_depth, W);
-  const void* fn = reinterpret_cast<const void*>(&sr_grad_kernel<T, KT, W, GATHER, R, VSTK>);
+  const size_t lds = sr_grad_lds_bytes(int(sizeof(T)), KT, R, a.nf, a.w != nullptr, a.stack_depth, W);
+  const void* fn = reinterpret_cast<const void*>(&sr_grad_kernel<T, KT, W, GATHER, R>);
   if (lds > 65536) {
     const hipError_t e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, int(lds));
     if (e != hipSuccess) return e;
   }
-  hipLaunchKernelGGL((sr_grad_kernel<T, KT, W, GATHER, R, VSTK>), dim3(n_blocks), dim3(W * 64), lds, s, a);
+  hipLaunchKernelGGL((sr_grad_kernel<T, KT, W, GATHER, R>), dim3(n_blocks), dim3(W * 64), lds, s, a);
   return hipGetLastError();
 }
 
 // Launch with `rows` rows per lane: the kernels exist for the bucket's default (sr_grad_rows_per_lane),
 // its halves down to 2, and 1 (sr_grad_launch_rows picks one; results do not depend on it: the row
 // blocks cover the same rows whatever the rows per lane, see sr_capi.cpp eval_grad_impl).
-template <typename T, bool GATHER, int KT, int RR, bool VSTK>
+template <typename T, bool GATHER, int KT, int RR>
 hipError_t sr_launch_grad_rows_from(const SrGradArgs<T>& a, int rows, int n_blocks, hipStream_t s) {
-  if (rows == RR) return sr_launch_grad<T, KT, 4, GATHER, RR, VSTK>(a, n_blocks, s);
-  if constexpr (RR > 1) return sr_launch_grad_rows_from<T, GATHER, KT, RR / 2, VSTK>(a, rows, n_blocks, s);
+  if (rows == RR) return sr_launch_grad<T, KT, 4, GATHER, RR>(a, n_blocks, s);
+  if constexpr (RR > 1) return sr_launch_grad_rows_from<T, GATHER, KT, RR / 2>(a, rows, n_blocks, s);
   return hipErrorInvalidValue;
 }
 
 template <typename T>
-hipError_t sr_launch_grad_any(const SrGradArgs<T>& a, int kt, bool gather, int rows, bool vstk, int n_blocks,
-                              hipStream_t s) {
-  auto go = [&](auto g, auto v) -> hipError_t {
+hipError_t sr_launch_grad_any(const SrGradArgs<T>& a, int kt, bool gather, int rows, int n_blocks, hipStream_t s) {
+  auto go = [&](auto g) -> hipError_t {
     constexpr bool G = decltype(g)::value;
-    constexpr bool V = decltype(v)::value;
     switch (kt) {
-      case 1: return sr_launch_grad_rows_from<T, G, 1, sr_grad_rows_per_lane(1), V>(a, rows, n_blocks, s);
-      case 2: return sr_launch_grad_rows_from<T, G, 2, sr_grad_rows_per_lane(2), V>(a, rows, n_blocks, s);
-      case 4: return sr_launch_grad_rows_from<T, G, 4, sr_grad_rows_per_lane(4), V>(a, rows, n_blocks, s);
-      case 8: return sr_launch_grad_rows_from<T, G, 8, sr_grad_rows_per_lane(8), V>(a, rows, n_blocks, s);
-      case 16:  // (16 tangents: two register slots would cost the kernel its occupancy; LDS stack only)
-        if constexpr (V) return hipErrorInvalidValue;
-        else return sr_launch_grad_rows_from<T, G, 16, sr_grad_rows_per_lane(16), false>(a, rows, n_blocks, s);
+      case 1: return sr_launch_grad_rows_from<T, G, 1, sr_grad_rows_per_lane(1)>(a, rows, n_blocks, s);
+      case 2: return sr_launch_grad_rows_from<T, G, 2, sr_grad_rows_per_lane(2)>(a, rows, n_blocks, s);
+      case 4: return sr_launch_grad_rows_from<T, G, 4, sr_grad_rows_per_lane(4)>(a, rows, n_blocks, s);
+      case 8: return sr_launch_grad_rows_from<T, G, 8, sr_grad_rows_per_lane(8)>(a, rows, n_blocks, s);
+      case 16: return sr_launch_grad_rows_from<T, G, 16, sr_grad_rows_per_lane(16)>(a, rows, n_blocks, s);
       default: return hipErrorInvalidValue;
     }
   };
-  if (vstk) return gather ? go(std::true_type{}, std::true_type{}) : go(std::false_type{}, std::true_type{});
-  return gather ? go(std::true_type{}, std::false_type{}) : go(std::false_type{}, std::false_type{});
+  return gather ? go(std::true_type{}) : go(std::false_type{});
 }

@@ -212,8 +212,7 @@ def test_gradients_independent_of_rows_per_lane(dtype):
     blocks cover the same rows whatever the choice and each lane accumulates its rows in order, so the
     gradients are bit-identical for every choice — also with FULL-tier operators (their row callees),
     weights, a non-L2 loss and every tangent bucket.  Likewise the work items' order (sr_set_tuning
-    "grad_sort": by program cost, or in tree order) and the operand stack (shallow programs' register
-    stack, "grad_vstk", or every program's LDS stack)."""
+    "grad_sort": by program cost, or in tree order)."""
     import sr_amd
 
     rng = np.random.default_rng(8)
@@ -245,15 +244,6 @@ def test_gradients_independent_of_rows_per_lane(dtype):
             l, g, c = eval_grad_batch(tb, ds, opts)
             assert np.array_equal(c, ref[2])
             assert np.array_equal(g.view(np.uint8), ref[1].view(np.uint8)), ("unsorted", kw)
-            ctx.set_tuning("grad_sort", 1)
-            for rows in (0, 1, 2):  # LDS operand stacks only (no register-stack launches)
-                ctx.set_tuning("grad_vstk", 0)
-                ctx.set_tuning("grad_rows", rows)
-                l, g, c = eval_grad_batch(tb, ds, opts)
-                assert np.array_equal(c, ref[2])
-                assert np.array_equal(g.view(np.uint8), ref[1].view(np.uint8)), ("lds stack", rows, kw)
-            ctx.set_tuning("grad_vstk", 1)
         finally:
             ctx.set_tuning("grad_rows", 0)
             ctx.set_tuning("grad_sort", 1)
-            ctx.set_tuning("grad_vstk", 1)
