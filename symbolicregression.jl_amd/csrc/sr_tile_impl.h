@@ -1165,7 +1165,14 @@ __global__ void __launch_bounds__(W * 64, (SrMinWavesFor<T, R, TIER, W, VSTK, LK
           // the POST unary fused into this instruction (the node whose child it computed)
           const uint32_t post = (op >> SR_OP_POST_SHIFT) & 0x3fu;
           if (post != 0u && !dead) {
-            sr_post_unary<T, R, TIER, FAST_CHECK>(post, (op & SR_OP_POST_INF) != 0u, tos);
+            // (an opaque copy: LLVM would otherwise fold the test above into the post switch's
+            //  balanced compare tree, where post = 0 — most instructions — is a leaf three levels
+            //  down: 7 scalar instructions per dispatch instead of 3)
+            uint32_t pu = post;
+#ifndef SR_POST_FOLDED
+            asm volatile("" : "+s"(pu));
+#endif
+            sr_post_unary<T, R, TIER, FAST_CHECK>(pu, (op & SR_OP_POST_INF) != 0u, tos);
             SR_TRACK();
             if (!FAST_CHECK && (op & SR_OP_POST_CHECK)) {
               SR_CHECK_NODE();
