@@ -108,7 +108,7 @@ __global__ void __launch_bounds__(W * 64) sr_grad_kernel(const SrGradArgs<T> a) 
   constexpr int NV = 1 + KT;                 // value + tangents
   extern __shared__ __attribute__((aligned(16))) unsigned char sr_smem[];
   const int tid = threadIdx.x;
-  const int wave = tid >> 6;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // (uniform: item, k0 and jj live in SGPRs)
   const int lane = tid & 63;
   T* xs = reinterpret_cast<T*>(sr_smem);                       // [nf][ROWS]
   T* ys = xs + size_t(a.nf) * ROWS;                            // [ROWS]
@@ -191,13 +191,13 @@ __global__ void __launch_bounds__(W * 64) sr_grad_kernel(const SrGradArgs<T> a) 
         const uint32_t meta = uint32_t(__builtin_amdgcn_readlane(int(cw.y), int(k)));
         const uint32_t idx = meta & SR_M_INDEX;  // feature / stack slot / constant slot
         // a constant operand: its value (wave-uniform) and its one-hot tangent e_{idx-k0}
-        auto const_val = [&]() -> T {
+        auto const_val = [&]() __attribute__((always_inline)) -> T {
           return idx < 64u ? sr_readlane_val<T>(cval0, idx) : sr_readlane_val<T>(cval1, idx - 64u);
         };
         const int jj = int(idx) - int(k0);
         const T* xrow = xs + size_t(idx) * ROWS + lane;
         const T* sp = my_stk + size_t(idx) * NV * R * 64;
-        auto push = [&]() {
+        auto push = [&]() __attribute__((always_inline)) {
           T* pp = my_stk + size_t(((meta >> SR_M_PUSH_SHIFT) & 0x3fu) - 1u) * NV * R * 64;
 #pragma unroll
           for (int j = 0; j < R; ++j) {
@@ -212,7 +212,7 @@ __global__ void __launch_bounds__(W * 64) sr_grad_kernel(const SrGradArgs<T> a) 
         // feature and one-hot for a constant, so those products are not computed).  Every value is
         // the one the general form fma(pa, da, pb db) gives: a product by an exact 0 or 1 and a sum
         // with an exact 0 are exact (up to the sign of a zero, which the gradient sums cannot see).
-        auto basic_bin = [&](auto op_c, auto var_c) {
+        auto basic_bin = [&](auto op_c, auto var_c) __attribute__((always_inline)) {
           constexpr uint32_t B = decltype(op_c)::value;
           constexpr uint32_t V = decltype(var_c)::value;
           constexpr bool LEFT = V == SR_V_SL || V == SR_V_FL || V == SR_V_CL;  // the operand is a
@@ -220,7 +220,14 @@ __global__ void __launch_bounds__(W * 64) sr_grad_kernel(const SrGradArgs<T> a) 
           T cv = T(0);
           if constexpr (SRC == 2) cv = const_val();
           T fix[R] = {};  // constant operand: the tangent at its own slot jj, from the unscaled dv
+          T d0[R] = {};
           const bool hot = SRC == 2 && jj >= 0 && jj < KT;
+          if (hot) {
+#pragma unroll
+            for (int q = 0; q < KT; ++q)
+#pragma unroll
+              for (int j = 0; j < R; ++j) d0[j] = q == jj ? dv[j][q] : d0[j];
+          }
 #pragma unroll
           for (int j = 0; j < R; ++j) {
             const T ov = SRC == 0 ? sp[j * 64] : (SRC == 1 ? xrow[j * 64] : cv);
@@ -249,13 +256,7 @@ __global__ void __launch_bounds__(W * 64) sr_grad_kernel(const SrGradArgs<T> a) 
             } else {
               // feature (zero tangent) or constant (one-hot at jj): every slot is the tos tangent
               // scaled by its own partial; a constant's own slot adds the constant's partial
-              if (SRC == 2 && hot) {
-                T d0 = T(0);
-#pragma unroll
-                for (int q = 0; q < KT; ++q)
-                  if (q == jj) d0 = dv[j][q];  // (jj is uniform: a scalar-selected move)
-                fix[j] = LEFT ? pa + pbv * d0 : __builtin_fma(pa, d0, pbv);
-              }
+              if (SRC == 2 && hot) fix[j] = LEFT ? pa + pbv * d0[j] : __builtin_fma(pa, d0[j], pbv);
               if constexpr (B == SR_B_ADD) {
                 // scale 1: unchanged
               } else if constexpr (B == SR_B_SUB) {
@@ -273,10 +274,8 @@ __global__ void __launch_bounds__(W * 64) sr_grad_kernel(const SrGradArgs<T> a) 
           if (SRC == 2 && hot) {
 #pragma unroll
             for (int q = 0; q < KT; ++q)
-              if (q == jj) {
 #pragma unroll
-                for (int j = 0; j < R; ++j) dv[j][q] = fix[j];
-              }
+              for (int j = 0; j < R; ++j) dv[j][q] = q == jj ? fix[j] : dv[j][q];
           }
         };
         switch (opc) {
