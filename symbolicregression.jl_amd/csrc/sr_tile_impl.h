@@ -805,7 +805,11 @@ __global__ void __launch_bounds__(W * 64, (SrMinWavesFor<T, R, TIER, W, VSTK, LK
   static_assert(R % 4 == 0 || R == 2, "rows per lane: 2 or a multiple of 4");
   extern __shared__ __attribute__((aligned(16))) unsigned char sr_smem[];
   const int tid = threadIdx.x;
+#ifndef SR_WAVE_VGPR
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // (uniform: per-wave values in SGPRs)
+#else
   const int wave = tid >> 6;
+#endif
   const int lane = tid & 63;
   SR_STAMP(0);
   const int G = a.trees_per_block;
