@@ -2178,7 +2178,7 @@ int eval_grad_impl(sr_ctx* ctx, const sr_dataset* ds, int opset_id, const sr_tre
     if (n_rb < 1) n_rb = 1;
     const int64_t units_per_block = (n_units + n_rb - 1) / n_rb;
     n_rb = (n_units + units_per_block - 1) / units_per_block;
-    const int64_t tiles_per_block = units_per_block * (kUnit / (64 * int64_t(rows)));
+    const int64_t tiles_per_block = units_per_block * (kUnit / int64_t(sr_grad_tile_rows(rows)));
     if (n_rb * n_groups > 0x7fffffff) return set_error(SR_ERR_INVALID_ARG, "grid too large");
     int64_t blk = 0;  // segments' first blocks
     for (SrSegment& sg : segs[b]) {

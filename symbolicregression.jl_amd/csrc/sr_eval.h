@@ -232,10 +232,13 @@ hipError_t sr_launch_grad_any(const SrGradArgs<T>& a, int kt, bool gather, int r
 // Largest rows per lane of the gradient kernel for KT tangents (a staged tile is 64 x that many rows);
 // kernels exist for it, its halves down to 2, and 1.
 constexpr int sr_grad_rows_per_lane(int kt) { return kt <= 2 ? 8 : (kt <= 4 ? 4 : (kt <= 8 ? 2 : 1)); }
+// Rows of a staged gradient tile at `rows` rows per lane: 256, or one program pass when that is longer
+// (a divisor of the host's 512-row units)
+constexpr int sr_grad_tile_rows(int rows) { return 64 * rows > 256 ? 64 * rows : 256; }
 // LDS of one gradient workgroup (W waves): the X / y / w tile and the waves' operand stacks (value +
 // KT tangents per row, stack_depth slots)
 inline size_t sr_grad_lds_bytes(int elem_size, int kt, int rows, int nf, bool weighted, int stack_depth, int waves) {
-  return (size_t(nf) + 1 + (weighted ? 1 : 0)) * 64 * size_t(rows) * size_t(elem_size) +
+  return (size_t(nf) + 1 + (weighted ? 1 : 0)) * size_t(sr_grad_tile_rows(rows)) * size_t(elem_size) +
          size_t(waves) * size_t(stack_depth) * size_t(1 + kt) * size_t(rows) * 64 * size_t(elem_size);
 }
 // Rows per lane a bucket of KT tangents runs with (results do not depend on it): `force` when it is

@@ -103,17 +103,22 @@ __device__ __attribute__((noinline)) SrGVec<T, R> sr_grad_loss_der(int kind, SrG
 // rows (round 3: one row per lane made every dispatch and operand decode cover 64 rows only).
 template <typename T, int KT, int W, bool GATHER, int R>
 __global__ void __launch_bounds__(W * 64) sr_grad_kernel(const SrGradArgs<T> a) {
-  // rows per lane: lane + 64 j, j < R
-  constexpr int ROWS = 64 * R;               // rows per staged tile
+  // rows per lane: lane + 64 j, j < R; a staged tile of TROWS rows is interpreted in TROWS / ROWS
+  // sub-passes (round 5: one barrier pair and one staging round per 256 rows, not per 64 R; a lane
+  // still meets its rows in row order, so the sums are the same bit for bit)
+  constexpr int ROWS = 64 * R;                      // rows per program pass
+  constexpr int TROWS = sr_grad_tile_rows(R);       // rows per staged tile
+  constexpr int SUBS = TROWS / ROWS;
+  static_assert(TROWS % ROWS == 0, "tile rows");
   constexpr int NV = 1 + KT;                 // value + tangents
   extern __shared__ __attribute__((aligned(16))) unsigned char sr_smem[];
   const int tid = threadIdx.x;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // (uniform: item, k0 and jj live in SGPRs)
   const int lane = tid & 63;
-  T* xs = reinterpret_cast<T*>(sr_smem);                       // [nf][ROWS]
-  T* ys = xs + size_t(a.nf) * ROWS;                            // [ROWS]
-  T* wsv = ys + ROWS;                                          // [ROWS] (weighted)
-  T* stk = wsv + (a.w ? ROWS : 0);                             // [W][depth][NV][R][64]
+  T* xs = reinterpret_cast<T*>(sr_smem);                       // [nf][TROWS]
+  T* ys = xs + size_t(a.nf) * TROWS;                           // [TROWS]
+  T* wsv = ys + TROWS;                                         // [TROWS] (weighted)
+  T* stk = wsv + (a.w ? TROWS : 0);                            // [W][depth][NV][R][64]
   T* my_stk = stk + size_t(wave) * a.stack_depth * NV * R * 64 + lane;
 
   int tg, rb, item, item_end = a.n_items;
@@ -161,18 +166,25 @@ __global__ void __launch_bounds__(W * 64) sr_grad_kernel(const SrGradArgs<T> a) 
   sr_libm_lds_fill(tid, W * 64);  // libm tables (visible after the first tile's barrier)
 
   for (int tile = 0; tile < a.tiles_per_block; ++tile) {
-    const int64_t row0 = (int64_t(rb) * a.tiles_per_block + tile) * ROWS;
-    if (row0 >= a.n_rows) break;
+    const int64_t tile0 = (int64_t(rb) * a.tiles_per_block + tile) * TROWS;
+    if (tile0 >= a.n_rows) break;
     __syncthreads();
-    for (int i = tid; i < ROWS; i += W * 64) {
-      const int64_t v = row0 + i;
+    for (int i = tid; i < TROWS; i += W * 64) {
+      const int64_t v = tile0 + i;
       const int64_t src = GATHER ? ridx[v < a.n_rows ? v : 0] : (v < a.n_rows ? v : 0);
-      for (int f = 0; f < a.nf; ++f) xs[f * ROWS + i] = a.X[int64_t(f) * a.ld + src];
+      for (int f = 0; f < a.nf; ++f) xs[f * TROWS + i] = a.X[int64_t(f) * a.ld + src];
       ys[i] = a.y[src];
       if (weighted) wsv[i] = a.w[src];
     }
     __syncthreads();
     if (!active || pe == pb) continue;
+    // the program's first window, kept across the sub-passes (programs are almost always <= 64)
+    uint4 cw0 = make_uint4(0u, 0u, 0u, 0u);
+    if (pb + lane < pe) cw0 = sr_load_window(a.code, pb + lane);
+    for (int sub = 0; sub < SUBS; ++sub) {
+    const int ro = sub * ROWS;  // the sub-pass's first row in the tile
+    const int64_t row0 = tile0 + ro;
+    if (row0 >= a.n_rows) break;
 
     T v[R];
     T dv[R][KT];
@@ -183,8 +195,11 @@ __global__ void __launch_bounds__(W * 64) sr_grad_kernel(const SrGradArgs<T> a) 
       for (int q = 0; q < KT; ++q) dv[j][q] = T(0);
     }
     for (uint32_t base = pb; base < pe; base += 64u) {
-      uint4 cw = make_uint4(0u, 0u, 0u, 0u);
-      if (base + lane < pe) cw = sr_load_window(a.code, base + lane);
+      uint4 cw = cw0;
+      if (base != pb) {
+        cw = make_uint4(0u, 0u, 0u, 0u);
+        if (base + lane < pe) cw = sr_load_window(a.code, base + lane);
+      }
       const uint32_t n_here = __builtin_amdgcn_readfirstlane((pe - base < 64u) ? pe - base : 64u);
       for (uint32_t k = 0; k < n_here; ++k) {
         const uint32_t opc = uint32_t(__builtin_amdgcn_readlane(int(cw.x), int(k)));
@@ -195,7 +210,7 @@ __global__ void __launch_bounds__(W * 64) sr_grad_kernel(const SrGradArgs<T> a) 
           return idx < 64u ? sr_readlane_val<T>(cval0, idx) : sr_readlane_val<T>(cval1, idx - 64u);
         };
         const int jj = int(idx) - int(k0);
-        const T* xrow = xs + size_t(idx) * ROWS + lane;
+        const T* xrow = xs + size_t(idx) * TROWS + ro + lane;
         const T* sp = my_stk + size_t(idx) * NV * R * 64;
         auto push = [&]() __attribute__((always_inline)) {
           T* pp = my_stk + size_t(((meta >> SR_M_PUSH_SHIFT) & 0x3fu) - 1u) * NV * R * 64;
@@ -463,13 +478,13 @@ __global__ void __launch_bounds__(W * 64) sr_grad_kernel(const SrGradArgs<T> a) 
     T coefs[R];
     if (a.loss_kind == SR_LOSS_L2) {
 #pragma unroll
-      for (int j = 0; j < R; ++j) coefs[j] = sr_elem_loss_deriv<T>(SR_LOSS_L2, v[j], ys[j * 64 + lane], T(0));
+      for (int j = 0; j < R; ++j) coefs[j] = sr_elem_loss_deriv<T>(SR_LOSS_L2, v[j], ys[ro + j * 64 + lane], T(0));
     } else {
       SrGVec<T, R> pv, yv;
 #pragma unroll
       for (int j = 0; j < R; ++j) {
         pv[j] = v[j];
-        yv[j] = ys[j * 64 + lane];
+        yv[j] = ys[ro + j * 64 + lane];
       }
       pv = sr_grad_loss_der<T, R>(a.loss_kind, pv, yv, a.loss_param);
 #pragma unroll
@@ -479,11 +494,12 @@ __global__ void __launch_bounds__(W * 64) sr_grad_kernel(const SrGradArgs<T> a) 
     for (int j = 0; j < R; ++j) {
       const int r = j * 64 + lane;
       T coef = coefs[j];
-      if (weighted) coef *= wsv[r];
+      if (weighted) coef *= wsv[ro + r];
       if (row0 + r >= a.n_rows) coef = T(0);
 #pragma unroll
       for (int q = 0; q < KT; ++q) acc[q] = __builtin_fma(double(coef), double(dv[j][q]), acc[q]);
     }
+    }  // sub-passes
   }
   if (!active) return;
 #pragma unroll
