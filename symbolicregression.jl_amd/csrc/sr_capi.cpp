@@ -213,8 +213,15 @@ struct sr_ctx {
   std::vector<int> tiers;
   std::vector<std::pair<int, double>> losses;  // registered (kind, param); code = kLossCodeBase + index
   DevBuf prog, outs, part_sum, part_flag, pred, row_idx, tree_list,
-      range_lo, range_hi, range_sums, packed, hint, jsum_prog, jsum_fin, jsum_scratch, probe_sum, probe_flag, g_code, g_offsets, g_consts, g_const_off, g_items, g_part, g_out,
+      range_lo, range_hi, range_sums, packed, hint, jsum_prog, jsum_scratch, probe_sum, probe_flag, g_code, g_offsets, g_consts, g_const_off, g_items, g_part, g_out,
       derived_cols, probe_derived, fold_io;
+  // The exact-sum pass's small transfers (round 5): the leaf ranges and the Julia-sum level program
+  // depend only on the view's row count, so they stay on the device between calls (host mirrors below;
+  // a buffer that grows loses them); the tree list goes up and the verdicts come back through pinned
+  // memory.  Pageable copies cost ~15 us each, and a one-tree pass made five of them.
+  HostBuf h_exact;
+  std::vector<int64_t> exact_lo_dev, exact_hi_dev;  // what range_lo / range_hi hold
+  int64_t jsum_n_dev = -1;                          // the row count jsum_prog was built for
 #ifdef SR_STAMPS
   DevBuf stamps;  // latency-analysis builds: the last main launch's per-wave stamps (sr_debug_stamps)
   int64_t n_stamps = 0;
@@ -1261,26 +1268,50 @@ int run_exact(sr_ctx* ctx, const sr_dataset* ds, const SrProgramBatch<T>& prog, 
     if (hi[size_t(i)] < lo[size_t(i)] || hi[size_t(i)] >= n_eval) return set_error(SR_ERR_INVALID_ARG, "bad row range");
     max_len = std::max(max_len, hi[size_t(i)] - lo[size_t(i)] + 1);
   }
-  SR_HIP_CHECK(ctx->range_lo.ensure(size_t(n_ranges) * sizeof(int64_t)));
-  SR_HIP_CHECK(ctx->range_hi.ensure(size_t(n_ranges) * sizeof(int64_t)));
-  SR_HIP_CHECK(hipMemcpyAsync(ctx->range_lo.p, lo.data(), size_t(n_ranges) * sizeof(int64_t), hipMemcpyHostToDevice, s));
-  SR_HIP_CHECK(hipMemcpyAsync(ctx->range_hi.p, hi.data(), size_t(n_ranges) * sizeof(int64_t), hipMemcpyHostToDevice, s));
+  // listed trees in batches whose range folds fit a bounded scratch buffer
+  const size_t per_tree = size_t(max_checks) * size_t(n_ranges) * sizeof(T);
+  const int64_t batch = std::max<int64_t>(1, int64_t((size_t(256) << 20) / per_tree));
+  // pinned staging: [leaf ranges lo | hi | Julia-sum level program | tree list | verdicts]
+  const JlLevels lv = host_finite ? jl_levels(n_eval) : JlLevels{};
+  const size_t n_lvp = lv.nodes.size() + lv.level_off.size();
+  const size_t o_hi = size_t(n_ranges) * sizeof(int64_t), o_lvp = 2 * o_hi;
+  const size_t o_list = (o_lvp + n_lvp * sizeof(int32_t) + 15) & ~size_t(15);
+  const size_t o_fin = (o_list + size_t(std::min(batch, n_list)) * sizeof(uint32_t) + 15) & ~size_t(15);
+  const size_t n_fin = host_finite ? size_t(std::min(batch, n_list)) * size_t(max_checks) : 0;
+  SR_HIP_CHECK(ctx->h_exact.ensure(o_fin + n_fin + 16, s, ctx->stream2));
+  char* const hx = ctx->h_exact.as<char>();
+  {
+    const size_t cap_lo = ctx->range_lo.cap, cap_hi = ctx->range_hi.cap;
+    SR_HIP_CHECK(ctx->range_lo.ensure(size_t(n_ranges) * sizeof(int64_t)));
+    SR_HIP_CHECK(ctx->range_hi.ensure(size_t(n_ranges) * sizeof(int64_t)));
+    if (ctx->range_lo.cap != cap_lo || ctx->range_hi.cap != cap_hi || ctx->exact_lo_dev != lo || ctx->exact_hi_dev != hi) {
+      ctx->exact_lo_dev.clear();  // (re-set only once the copies are queued)
+      std::memcpy(hx, lo.data(), o_hi);
+      std::memcpy(hx + o_hi, hi.data(), o_hi);
+      SR_HIP_CHECK(hipMemcpyAsync(ctx->range_lo.p, hx, o_hi, hipMemcpyHostToDevice, s));
+      SR_HIP_CHECK(hipMemcpyAsync(ctx->range_hi.p, hx + o_hi, o_hi, hipMemcpyHostToDevice, s));
+      ctx->exact_lo_dev = lo;
+      ctx->exact_hi_dev = hi;
+    }
+  }
   int n_internal = 0, n_levels = 0;
   if (host_finite) {
-    const JlLevels lv = jl_levels(n_eval);
     n_internal = int(lv.nodes.size() / 2);
     n_levels = int(lv.level_off.size()) - 1;
     if (n_internal != n_ranges - 1 && !(n_ranges == 1 && n_internal == 0))
       return set_error(SR_ERR_INVALID_ARG, "bad leaf structure");
-    // nodes then level offsets, one upload
-    std::vector<int32_t> buf(lv.nodes);
-    buf.insert(buf.end(), lv.level_off.begin(), lv.level_off.end());
-    SR_HIP_CHECK(ctx->jsum_prog.ensure(buf.size() * sizeof(int32_t)));
-    SR_HIP_CHECK(hipMemcpyAsync(ctx->jsum_prog.p, buf.data(), buf.size() * sizeof(int32_t), hipMemcpyHostToDevice, s));
+    // nodes then level offsets, one upload (kept for the next call over as many rows)
+    const size_t cap = ctx->jsum_prog.cap;
+    SR_HIP_CHECK(ctx->jsum_prog.ensure(n_lvp * sizeof(int32_t)));
+    if (ctx->jsum_prog.cap != cap || ctx->jsum_n_dev != n_eval) {
+      ctx->jsum_n_dev = -1;
+      int32_t* b = reinterpret_cast<int32_t*>(hx + o_lvp);
+      std::copy(lv.nodes.begin(), lv.nodes.end(), b);
+      std::copy(lv.level_off.begin(), lv.level_off.end(), b + lv.nodes.size());
+      SR_HIP_CHECK(hipMemcpyAsync(ctx->jsum_prog.p, b, n_lvp * sizeof(int32_t), hipMemcpyHostToDevice, s));
+      ctx->jsum_n_dev = n_eval;
+    }
   }
-  // listed trees in batches whose range folds fit a bounded scratch buffer
-  const size_t per_tree = size_t(max_checks) * size_t(n_ranges) * sizeof(T);
-  const int64_t batch = std::max<int64_t>(1, int64_t((size_t(256) << 20) / per_tree));
   for (int64_t b0 = 0; b0 < n_list; b0 += batch) {
     const int64_t nb = std::min(batch, n_list - b0);
     // one wave per workgroup, G listed trees per workgroup (LDS: X tile + one wave's checked
@@ -1301,10 +1332,10 @@ int run_exact(sr_ctx* ctx, const sr_dataset* ds, const SrProgramBatch<T>& prog, 
       if (G < W) W = 1;
     }
     if (lds > kLdsMax) return set_error(SR_ERR_TOO_DEEP, "exact-sum pass needs more LDS than 160 KiB");
-    std::vector<uint32_t> list32(static_cast<size_t>(nb));
-    for (int64_t i = 0; i < nb; ++i) list32[size_t(i)] = uint32_t(list[b0 + i]);
+    uint32_t* list32 = reinterpret_cast<uint32_t*>(hx + o_list);  // (the previous batch's copy has completed)
+    for (int64_t i = 0; i < nb; ++i) list32[i] = uint32_t(list[b0 + i]);
     SR_HIP_CHECK(ctx->tree_list.ensure(size_t(nb) * sizeof(uint32_t)));
-    SR_HIP_CHECK(hipMemcpyAsync(ctx->tree_list.p, list32.data(), size_t(nb) * sizeof(uint32_t), hipMemcpyHostToDevice, s));
+    SR_HIP_CHECK(hipMemcpyAsync(ctx->tree_list.p, list32, size_t(nb) * sizeof(uint32_t), hipMemcpyHostToDevice, s));
     SR_HIP_CHECK(ctx->range_sums.ensure(size_t(nb) * per_tree));
     SrEvalArgs<T> a{};
     a.code = static_cast<const SrIns<T>*>(ctx->d_code);
@@ -1333,20 +1364,21 @@ int run_exact(sr_ctx* ctx, const sr_dataset* ds, const SrProgramBatch<T>& prog, 
     SR_HIP_CHECK(sr_launch_eval<T>(a, SR_MODE_EXACT, gather, SR_TIER_FULL, R, W, false, int(blocks), s));
     if (host_finite) {
       const int64_t n_arrays = nb * max_checks;
-      SR_HIP_CHECK(ctx->jsum_fin.ensure(size_t(n_arrays) + 16));
       SR_HIP_CHECK(ctx->jsum_scratch.ensure(size_t(std::max<int64_t>(1, n_arrays * n_internal)) * sizeof(T)));
       const int32_t* lvp = ctx->jsum_prog.as<int32_t>();
+      // (the verdicts go straight into the pinned staging buffer: no copy back)
+      uint8_t* fin = reinterpret_cast<uint8_t*>(hx + o_fin);
       SR_HIP_CHECK(sr_launch_jsum_levels<T>(static_cast<const T*>(ctx->range_sums.p), n_arrays, int(n_ranges),
                                             reinterpret_cast<const int2*>(lvp), n_internal, lvp + 2 * n_internal,
-                                            n_levels, ctx->jsum_scratch.as<T>(), ctx->jsum_fin.as<uint8_t>(), s));
-      SR_HIP_CHECK(hipMemcpyAsync(host_finite + size_t(b0) * max_checks, ctx->jsum_fin.p, size_t(n_arrays),
-                                  hipMemcpyDeviceToHost, s));
+                                            n_levels, ctx->jsum_scratch.as<T>(), fin, s));
     } else {
       SR_HIP_CHECK(hipMemcpyAsync(host_vals + size_t(b0) * max_checks * size_t(n_ranges), ctx->range_sums.p,
                                   size_t(nb) * per_tree, hipMemcpyDeviceToHost, s));
     }
     SR_HIP_CHECK(hipEventRecord(ctx->ev_k1, s));
     SR_HIP_CHECK(hipStreamSynchronize(s));
+    if (host_finite)
+      std::memcpy(host_finite + size_t(b0) * max_checks, hx + o_fin, size_t(nb) * size_t(max_checks));
     float km = 0.f;
     if (hipEventElapsedTime(&km, ctx->ev_k0, ctx->ev_k1) == hipSuccess) ctx->exact_kernel_ms += double(km);
   }
@@ -2977,6 +3009,15 @@ int sr_init(int device, sr_ctx** out) {
   if (hipGetDeviceCount(&c) != hipSuccess || c <= 0) return set_error(SR_ERR_NO_DEVICE, "no HIP device visible");
   if (device < 0 || device >= c) return set_error(SR_ERR_INVALID_ARG, "device index out of range");
   SR_HIP_CHECK(hipSetDevice(device));
+  // SR_AMD_SCHED (A/B only): how the host waits for the device — spin / yield / block
+  if (const char* v = std::getenv("SR_AMD_SCHED")) {
+    const unsigned f = std::strcmp(v, "spin") == 0    ? hipDeviceScheduleSpin
+                       : std::strcmp(v, "yield") == 0 ? hipDeviceScheduleYield
+                       : std::strcmp(v, "block") == 0 ? hipDeviceScheduleBlockingSync
+                                                      : hipDeviceScheduleAuto;
+    const hipError_t e = hipSetDeviceFlags(f);
+    if (e != hipSuccess) std::fprintf(stderr, "[sr] hipSetDeviceFlags(%s): %s\n", v, hipGetErrorString(e));
+  }
   auto* ctx = new sr_ctx();
   ctx->device = device;
   hipDeviceProp_t prop;
@@ -3078,10 +3119,10 @@ int sr_shutdown(sr_ctx* ctx) {
     if (ctx->hint_reserve) (void)hipFree(ctx->hint_reserve);
     ctx->hint_reserve = nullptr;
     for (DevBuf* b : {&ctx->prog, &ctx->outs, &ctx->part_sum, &ctx->part_flag, &ctx->pred, &ctx->row_idx, &ctx->tree_list, &ctx->range_lo, &ctx->range_hi, &ctx->range_sums, &ctx->packed,
-                      &ctx->hint, &ctx->jsum_prog, &ctx->jsum_fin, &ctx->jsum_scratch, &ctx->probe_sum, &ctx->probe_flag, &ctx->g_code, &ctx->g_offsets, &ctx->g_consts, &ctx->g_const_off,
+                      &ctx->hint, &ctx->jsum_prog, &ctx->jsum_scratch, &ctx->probe_sum, &ctx->probe_flag, &ctx->g_code, &ctx->g_offsets, &ctx->g_consts, &ctx->g_const_off,
                       &ctx->g_items, &ctx->g_part, &ctx->g_out, &ctx->derived_cols, &ctx->probe_derived, &ctx->coll_buf, &ctx->coll_packed, &ctx->ctl, &ctx->fold_io, &ctx->group_cnt})
       b->release();
-    for (HostBuf* b : {&ctx->h_prog, &ctx->h_outs, &ctx->h_grad, &ctx->h_coll, &ctx->h_part}) b->release();
+    for (HostBuf* b : {&ctx->h_prog, &ctx->h_outs, &ctx->h_grad, &ctx->h_coll, &ctx->h_part, &ctx->h_exact}) b->release();
     for (int c = 0; c < kMaxChunks; ++c) {
       (void)hipEventDestroy(ctx->ev_c0[c]);
       (void)hipEventDestroy(ctx->ev_c1[c]);
@@ -3751,6 +3792,10 @@ int sr_set_tuning(sr_ctx* ctx, const char* name, int64_t value) {
   }
   if (std::strcmp(name, "chunk_min") == 0) {  // the two-chunk pipeline's smallest first chunk (SR_AMD_CHUNK_MIN)
     ctx->chunk_min = std::max<int64_t>(1, value);
+    return SR_OK;
+  }
+  if (std::strcmp(name, "first_chunk") == 0) {  // the two-chunk pipeline's first chunk is 1/value (SR_AMD_FIRST_CHUNK)
+    ctx->first_chunk = int(std::max<int64_t>(2, std::min<int64_t>(64, value)));
     return SR_OK;
   }
   if (std::strcmp(name, "max_row_blocks") == 0) {  // row blocks per tree of a LOSS launch (SR_AMD_MAX_ROW_BLOCKS)

@@ -8,7 +8,9 @@ import sys
 import time
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-sys.path[:0] = [ROOT, os.path.join(ROOT, "symbolicregression.jl_amd")]
+# SR_AMD_PKG=ab/<name>: another revision's package + library (tools/ab_lib.sh)
+sys.path[:0] = [ROOT, os.path.join(ROOT, os.environ["SR_AMD_PKG"]) if os.environ.get("SR_AMD_PKG")
+                else os.path.join(ROOT, "symbolicregression.jl_amd")]
 import numpy as np  # noqa: E402
 
 import bench  # noqa: E402
@@ -25,7 +27,10 @@ def main():
     trees = gen_random_population(10_000, opts, 5, max_size=30, seed=1)
     tb = flatten_trees(trees, np.float32)
     share = tb.take(np.nonzero(tree_owners(tb, 8) == 0)[0])
+    # extra settings: "probe" (mode 1), or knob=value arguments (e.g. chunk_min=128), each on its own
     knobs = [dict()] + ([dict(probe=1)] if "probe" in sys.argv[1:] else [])
+    knobs += [{a.split("=")[0]: int(a.split("=")[1])} for a in sys.argv[1:] if "=" in a]
+    defaults = {"probe": 2, "chunk_min": 1024, "max_row_blocks": 512, "first_chunk": 6}
     for kn in knobs:
         for k, v in kn.items():
             ctx.set_tuning(k, v)
@@ -39,7 +44,8 @@ def main():
                          "exact_trees": ctx.last_exact_trees(), "exact_kernel_ms": ctx.last_exact_kernel_ms()}
         row["efficiency_8"] = row["all"]["ms"] / (8 * row["share"]["ms"])
         print(json.dumps(row), flush=True)
-        ctx.set_tuning("probe", 2)
+        for k in kn:
+            ctx.set_tuning(k, defaults[k])
 
 
 if __name__ == "__main__":
