@@ -1006,7 +1006,9 @@ int run_batch(sr_ctx* ctx, const sr_dataset* ds, int opset_id, const sr_tree_bat
       // and a single-chunk call when it is large (>= 512 trees x 2^18 rows: the tree-sharding share,
       // 1,250 trees x 1M rows, 1.09 -> 1.01 ms; the search's small calls pay the probe's launch and
       // keep none: profiles/r05_ab_probe.txt)
-      const bool probe_first = n_chunks == 1 && nt >= 512 && n_eval >= (int64_t(1) << 18);
+      // (round 5, later: also the first of two chunks when it is that large — C4's 8M-row shard
+      //  216.9 -> 214.4 ms per call, C2 unchanged; tools/c4_shard_probe.py, profiles/r05_ab_c4_shard.txt)
+      const bool probe_first = nc >= 512 && n_eval >= (int64_t(1) << 18);
       if (use_probe && p0 == 0 && g.n_row_blocks >= 16 && (ctx->probe != 2 || c > 0 || probe_first)) {
         // Trees that are non-finite on the first rows are flagged before the main launch, so its
         // workgroups skip them from their first tile (without the probe, the ~16 row blocks that

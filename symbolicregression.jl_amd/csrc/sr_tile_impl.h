@@ -549,6 +549,19 @@ __device__ __forceinline__ void sr_post_unary(uint32_t u, bool inf, T (&tos)[R])
       tos[r] = sr_binary<T>(ID, aa, bb);                                  \
     }                                                                     \
   }
+// Outputs the deferred checks need not track (SR_TRACK_LITE, round 5): bounded by 1 (cos, sin), by
+// their input (neg, abs, sqrt: max(1, |x|)), or by the sum of their operands' magnitudes (+ and - of two
+// stack values / features); the launch's tbig and BIG budget are divided by the largest tree's node
+// count, which bounds every untracked value by that many tracked ones (sr_capi.cpp run_batch).
+#ifdef SR_TRACK_LITE
+constexpr bool sr_untracked_u(uint32_t id) {
+  return id == SR_U_COS || id == SR_U_SIN || id == SR_U_NEG || id == SR_U_ABS || id == SR_U_SQRT;
+}
+constexpr bool sr_untracked_b(uint32_t id) { return id == SR_B_ADD || id == SR_B_SUB; }
+#else
+constexpr bool sr_untracked_u(uint32_t) { return false; }
+constexpr bool sr_untracked_b(uint32_t) { return false; }
+#endif
 // FAST_CHECK: every operator output joins the running max |v| of the tree
 #define SR_TRACK()                                                        \
   if constexpr (FAST_CHECK) {                                             \
@@ -574,7 +587,7 @@ __device__ __forceinline__ void sr_post_unary(uint32_t u, bool inf, T (&tos)[R])
   case SR_OP_UNARY0 + ID: {                                         \
     if (ENABLED) {                                                  \
       sr_unary_rows<T, ID, R>(tos);                                 \
-      SR_TRACK();                                                   \
+      if constexpr (!sr_untracked_u(ID)) SR_TRACK();                \
     }                                                               \
     break;                                                          \
   }
@@ -607,7 +620,7 @@ __device__ __forceinline__ void sr_post_unary(uint32_t u, bool inf, T (&tos)[R])
   case SR_BIN_OPC(ID, SR_V_SR): {      \
     if (ENABLED) {                     \
       SR_STK_BIN(ID, false);           \
-      SR_TRACK();                      \
+      if constexpr (!sr_untracked_b(ID)) SR_TRACK(); \
     }                                  \
     break;                             \
   }                                    \
@@ -616,7 +629,7 @@ __device__ __forceinline__ void sr_post_unary(uint32_t u, bool inf, T (&tos)[R])
       T o[R];                          \
       L::load(SR_OPND_X(), o);         \
       SR_BIN_EACH(tos[r], o[r], ID);   \
-      SR_TRACK();                      \
+      if constexpr (!sr_untracked_b(ID)) SR_TRACK(); \
     }                                  \
     break;                             \
   }                                    \
@@ -632,7 +645,7 @@ __device__ __forceinline__ void sr_post_unary(uint32_t u, bool inf, T (&tos)[R])
   case SR_BIN_OPC(ID, SR_V_SL): {      \
     if (ENABLED) {                     \
       SR_STK_BIN(ID, true);            \
-      SR_TRACK();                      \
+      if constexpr (!sr_untracked_b(ID)) SR_TRACK(); \
     }                                  \
     break;                             \
   }                                    \
@@ -641,7 +654,7 @@ __device__ __forceinline__ void sr_post_unary(uint32_t u, bool inf, T (&tos)[R])
       T o[R];                          \
       L::load(SR_OPND_X(), o);         \
       SR_BIN_EACH(o[r], tos[r], ID);   \
-      SR_TRACK();                      \
+      if constexpr (!sr_untracked_b(ID)) SR_TRACK(); \
     }                                  \
     break;                             \
   }                                    \
@@ -659,7 +672,7 @@ __device__ __forceinline__ void sr_post_unary(uint32_t u, bool inf, T (&tos)[R])
   case SR_PAIR_OPC(ID, PV): {                                    \
     if (ENABLED) {                                               \
       BODY;                                                      \
-      SR_TRACK();                                                \
+      if constexpr (!(PV == SR_P_FF && sr_untracked_b(ID))) SR_TRACK(); \
     }                                                            \
     break;                                                       \
   }                                                              \
@@ -667,7 +680,7 @@ __device__ __forceinline__ void sr_post_unary(uint32_t u, bool inf, T (&tos)[R])
     if (ENABLED) {                                               \
       SR_PUSH_TOS();                                             \
       BODY;                                                      \
-      SR_TRACK();                                                \
+      if constexpr (!(PV == SR_P_FF && sr_untracked_b(ID))) SR_TRACK(); \
     }                                                            \
     break;                                                       \
   }
@@ -1177,6 +1190,9 @@ __global__ void __launch_bounds__(W * 64, (SrMinWavesFor<T, R, TIER, W, VSTK, LK
             asm volatile("" : "+s"(pu));
 #endif
             sr_post_unary<T, R, TIER, FAST_CHECK>(pu, (op & SR_OP_POST_INF) != 0u, tos);
+#ifdef SR_TRACK_LITE
+            if (!sr_untracked_u(pu))
+#endif
             SR_TRACK();
             if (!FAST_CHECK && (op & SR_OP_POST_CHECK)) {
               SR_CHECK_NODE();
