@@ -749,6 +749,9 @@ int run_batch(sr_ctx* ctx, const sr_dataset* ds, int opset_id, const sr_tree_bat
       return n_chunks == 2 ? nt / ctx->first_chunk : nt * k / n_chunks;
     };
     const int64_t t0 = bound(c), t1 = bound(c + 1), nc = t1 - t0;
+    uint32_t max_nodes = 1;  // the chunk's largest tree (bounds the untracked values: SR_TRACK_LITE)
+    for (int64_t t = t0; t < t1; ++t)
+      max_nodes = std::max<uint32_t>(max_nodes, uint32_t(trees->offsets[t + 1] - trees->offsets[t]));
     // chunks alternate between two streams: chunk c+1's workgroups fill the GPU while chunk c drains
     const hipStream_t cs = (c & 1) ? ctx->stream2 : s;
     sr_tree_batch sub = *trees;
@@ -955,6 +958,22 @@ int run_batch(sr_ctx* ctx, const sr_dataset* ds, int opset_id, const sr_tree_bat
         a.big_budget = 64.0 * t_max<T>() / (1.01 * padded);
       }
       a.track_x = !(max_abs_x < double(a.tbig)) ? 1 : 0;
+#ifdef SR_TRACK_LITE
+      if (mode == SR_MODE_LOSS && tier == SR_TIER_BASIC) {
+        // (the deferred-check kernels leave +, - of stack values / features and cos, sin, neg, abs,
+        //  sqrt untracked: such a value is at most L x max(tracked max, max|x|, 1) for a tree of L
+        //  nodes, so with tbig / L as the tracked threshold every value stays below tbig, and a tile
+        //  within budget / L - 64 (max|x| + 1) keeps every array's sum within the original budget.
+        //  Data at or above tbig / L: track_x, and the kernel tracks + and - again, at the full tbig)
+        const double L = double(std::max<uint32_t>(1u, max_nodes));
+        if (max_abs_x < double(a.tbig) / L) {
+          a.tbig = T(double(a.tbig) / L);
+          a.big_budget = a.big_budget / L - 64.0 * (max_abs_x + 1.0);
+        } else {
+          a.track_x = 1;
+        }
+      }
+#endif
       a.loss_kind = lkind;
       a.loss_param = T(lparam);
       a.part_sum = (host_red ? ctx->h_part.as<double>() : ctx->part_sum.as<double>()) + size_t(n_rb) * size_t(t0 + p0);

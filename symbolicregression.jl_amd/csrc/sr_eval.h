@@ -8,6 +8,11 @@
 enum { SR_MODE_LOSS = 0, SR_MODE_PRED = 1, SR_MODE_EXACT = 2 };
 // operand-stack slots the register-stack kernels hold in VGPRs (1: trees needing a second slot —
 // 6 % of C2's — run on the LDS-stack kernel instead)
+// The deferred checks leave bounded outputs untracked (sr_tile_impl.h sr_untracked_u / _b; round 5:
+// C2 kernel -4 %, arithmetic-only -9 %, profiles/r05_ab_track_lite.txt); -DSR_TRACK_FULL tracks all.
+#ifndef SR_TRACK_FULL
+#define SR_TRACK_LITE 1
+#endif
 #ifndef SR_VSTK_SLOTS
 #define SR_VSTK_SLOTS 2
 #endif

@@ -311,6 +311,35 @@ def test_sum_overflow_exact_path():
     assert list(oc) == [False, True, True, True, False]
 
 
+@pytest.mark.parametrize("dtype", [np.float32, np.float64])
+def test_untracked_outputs_keep_the_checks(dtype):
+    """SR_TRACK_LITE (sr_tile_impl.h): + and - of stack values / features and cos, sin, neg, abs, sqrt
+    leave the deferred checks' running max; the launch's thresholds are divided by the largest tree's
+    node count, and data at or above that bound tracks + and - again.  Positive data at scales around
+    those bounds (including sums of untracked nodes whose array sums overflow): flags equal the
+    oracle's, losses within the per-tree bar."""
+    opts = Options(binary_operators=["+", "-", "*", "/"], unary_operators=["cos", "sin", "sqrt", "abs", "neg"])
+    n = 4000
+    fmax = float(np.finfo(dtype).max)
+    tbig = fmax / (2 * n)
+    exprs = ["((x1 + x2) + x3) + x4", "(x1 + x2) - (x3 + x4)",
+             "((x1 + x2) + (x3 + x4)) + ((x5 + x1) + (x2 + x3))", "sqrt(abs((x1 + x2) + x3))",
+             "neg((x1 + x2) + (x3 + x4))", "cos(x1 + x2) + x3", "sin(x1 - x2) * x3", "(x1 + x2) * 2.0",
+             "x1 * 3.0 + x2", "((x1 + x2) + x3) / 0.5", "x1 + x2", "abs(x1 - x2) + cos(x3)"]
+    trees = [parse_expression(e, opts) for e in exprs]
+    tb = flatten_trees(trees, dtype)
+    orc = Oracle.from_options(opts)
+    rng = np.random.default_rng(5)
+    # below tbig / L, between tbig / L and tbig (track_x), past the point where 4-leaf sums overflow
+    for scale in (1e-3 * tbig, 0.02 * tbig, 0.3 * tbig, 0.52 * tbig, 2.2 * tbig / 2, 1e4):
+        X = (scale * (1.0 + 0.01 * rng.random((5, n)))).astype(dtype)
+        y = np.zeros(n, dtype=dtype)
+        loss, comp = eval_loss_batch(tb, Dataset(X, y), opts)
+        tol, ol, oc, _ = loss_tolerance(orc, tb, X, y)
+        assert np.array_equal(comp, oc), (scale, [(e, c, o) for e, c, o in zip(exprs, comp, oc) if c != o])
+        assert_losses_within(loss, ol, comp, tol, scale)
+
+
 def test_ragged_sizes_and_determinism():
     opts = Options(**C2_OPTS)
     trees = gen_random_population(400, opts, 5, seed=41)
