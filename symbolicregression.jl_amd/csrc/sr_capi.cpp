@@ -517,7 +517,18 @@ int run_batch(sr_ctx* ctx, const sr_dataset* ds, int opset_id, const sr_tree_bat
   const int64_t total_nodes = nt > 0 ? trees->offsets[nt] - trees->offsets[0] : 0;
   if (total_nodes < 0 || total_nodes > int64_t(0xffffffffu) / 2)
     return set_error(SR_ERR_INVALID_ARG, "tree batch node count out of range");
-  const int tier = ctx->tiers[opset_id];
+  // (SR_TRACK_LITE: the deferred-check kernels bound untracked values by L x max|x| for trees of up to
+  //  L nodes; data at or above tbig / L — huge or non-finite values, never seen in practice — runs the
+  //  per-node-check kernels instead, whose checks hold for any data)
+  int tier = ctx->tiers[opset_id];
+#ifdef SR_TRACK_LITE
+  if (tier == SR_TIER_BASIC && mode == SR_MODE_LOSS && nt > 0) {
+    int64_t lmax = 1;
+    for (int64_t t = 0; t < nt; ++t) lmax = std::max<int64_t>(lmax, trees->offsets[t + 1] - trees->offsets[t]);
+    const double mx = shard ? shard->max_abs_x : ds->max_abs_x;
+    if (!(mx < double(T(t_max<T>() / (2.0 * double(n_total > 0 ? n_total : 1)))) / double(lmax))) tier = SR_TIER_FULL;
+  }
+#endif
   const int R = sr_rows_per_lane<T>(mode, tier, ctx->rows_override);
   const int W = sr_waves_per_block(int(sizeof(T)), mode, tier, R, ctx->waves_override);
   // register-stack kernel (f32 BASIC loss over the full dataset): Rv rows per lane, used for every
@@ -955,7 +966,7 @@ int run_batch(sr_ctx* ctx, const sr_dataset* ds, int opset_id, const sr_tree_bat
       a.tbig = T(t_max<T>() / (2.0 * double(n_total > 0 ? n_total : 1)));
       {  // the view's padded rows over every shard: n_total + at most one 2048-row tile of padding per shard
         const double padded = double(n_total > 0 ? n_total : 1) + 2048.0 * double(shard ? ctx->comm_ranks : 1);
-        a.big_budget = 64.0 * t_max<T>() / (1.01 * padded);
+        a.big_budget = 64.0 * (t_max<T>() / (1.01 * padded));  // (f64: 64 x DBL_MAX alone is +Inf)
       }
       a.track_x = !(max_abs_x < double(a.tbig)) ? 1 : 0;
 #ifdef SR_TRACK_LITE
@@ -963,15 +974,12 @@ int run_batch(sr_ctx* ctx, const sr_dataset* ds, int opset_id, const sr_tree_bat
         // (the deferred-check kernels leave +, - of stack values / features and cos, sin, neg, abs,
         //  sqrt untracked: such a value is at most L x max(tracked max, max|x|, 1) for a tree of L
         //  nodes, so with tbig / L as the tracked threshold every value stays below tbig, and a tile
-        //  within budget / L - 64 (max|x| + 1) keeps every array's sum within the original budget.
-        //  Data at or above tbig / L: track_x, and the kernel tracks + and - again, at the full tbig)
+        //  within budget / L - 64 (max|x| + 1) keeps every array's sum within the original budget;
+        //  max|x| < tbig / L here: larger data took the per-node-check tier above)
         const double L = double(std::max<uint32_t>(1u, max_nodes));
-        if (max_abs_x < double(a.tbig) / L) {
-          a.tbig = T(double(a.tbig) / L);
-          a.big_budget = a.big_budget / L - 64.0 * (max_abs_x + 1.0);
-        } else {
-          a.track_x = 1;
-        }
+        a.tbig = T(double(a.tbig) / L);
+        a.big_budget = a.big_budget / L - 64.0 * (max_abs_x + 1.0);
+        a.track_x = 0;
       }
 #endif
       a.loss_kind = lkind;

@@ -553,8 +553,7 @@ __device__ __forceinline__ void sr_post_unary(uint32_t u, bool inf, T (&tos)[R])
 // their input (neg, abs, sqrt: max(1, |x|)), or by the sum of their operands' magnitudes (+ and - of two
 // stack values / features); the launch's tbig and BIG budget are divided by the largest tree's node
 // count L, which bounds every untracked value by L x max(tracked max, max|x|, 1) (sr_capi.cpp
-// run_batch).  Data at or above tbig / L sets track_x, and + and - are then tracked as before (`trk`:
-// their operands may be untracked feature rows).
+// run_batch).  Data at or above tbig / L runs the per-node-check (FULL tier) kernels instead.
 #ifdef SR_TRACK_LITE
 constexpr bool sr_untracked_u(uint32_t id) {
   return id == SR_U_COS || id == SR_U_SIN || id == SR_U_NEG || id == SR_U_ABS || id == SR_U_SQRT;
@@ -622,7 +621,7 @@ constexpr bool sr_untracked_b(uint32_t) { return false; }
   case SR_BIN_OPC(ID, SR_V_SR): {      \
     if (ENABLED) {                     \
       SR_STK_BIN(ID, false);           \
-      if (!sr_untracked_b(ID) || trk) SR_TRACK(); \
+      if constexpr (!sr_untracked_b(ID)) SR_TRACK(); \
     }                                  \
     break;                             \
   }                                    \
@@ -631,7 +630,7 @@ constexpr bool sr_untracked_b(uint32_t) { return false; }
       T o[R];                          \
       L::load(SR_OPND_X(), o);         \
       SR_BIN_EACH(tos[r], o[r], ID);   \
-      if (!sr_untracked_b(ID) || trk) SR_TRACK(); \
+      if constexpr (!sr_untracked_b(ID)) SR_TRACK(); \
     }                                  \
     break;                             \
   }                                    \
@@ -647,7 +646,7 @@ constexpr bool sr_untracked_b(uint32_t) { return false; }
   case SR_BIN_OPC(ID, SR_V_SL): {      \
     if (ENABLED) {                     \
       SR_STK_BIN(ID, true);            \
-      if (!sr_untracked_b(ID) || trk) SR_TRACK(); \
+      if constexpr (!sr_untracked_b(ID)) SR_TRACK(); \
     }                                  \
     break;                             \
   }                                    \
@@ -656,7 +655,7 @@ constexpr bool sr_untracked_b(uint32_t) { return false; }
       T o[R];                          \
       L::load(SR_OPND_X(), o);         \
       SR_BIN_EACH(o[r], tos[r], ID);   \
-      if (!sr_untracked_b(ID) || trk) SR_TRACK(); \
+      if constexpr (!sr_untracked_b(ID)) SR_TRACK(); \
     }                                  \
     break;                             \
   }                                    \
@@ -674,7 +673,7 @@ constexpr bool sr_untracked_b(uint32_t) { return false; }
   case SR_PAIR_OPC(ID, PV): {                                    \
     if (ENABLED) {                                               \
       BODY;                                                      \
-      if (!(PV == SR_P_FF && sr_untracked_b(ID)) || trk) SR_TRACK(); \
+      if constexpr (!(PV == SR_P_FF && sr_untracked_b(ID))) SR_TRACK(); \
     }                                                            \
     break;                                                       \
   }                                                              \
@@ -682,7 +681,7 @@ constexpr bool sr_untracked_b(uint32_t) { return false; }
     if (ENABLED) {                                               \
       SR_PUSH_TOS();                                             \
       BODY;                                                      \
-      if (!(PV == SR_P_FF && sr_untracked_b(ID)) || trk) SR_TRACK(); \
+      if constexpr (!(PV == SR_P_FF && sr_untracked_b(ID))) SR_TRACK(); \
     }                                                            \
     break;                                                       \
   }
@@ -1023,7 +1022,6 @@ __global__ void __launch_bounds__(W * 64, (SrMinWavesFor<T, R, TIER, W, VSTK, LK
     bool susp_any = false;
     int check_k = 0;
     T mrun = T(0), mrun1 = T(0);  // FAST_CHECK: running max |v| over this lane's rows (2 chains)
-    const bool trk = a.track_x != 0;  // (SR_TRACK_LITE: + and - of untracked rows are tracked too)
     bool more = true;
     while (more) {
       const typename SrWindow<T>::type cw = nx;
