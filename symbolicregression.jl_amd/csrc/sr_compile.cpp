@@ -169,6 +169,14 @@ struct TreeCompiler {
   int64_t n_ops = 0;
 
   const int16_t* derived = nullptr;  // [SR_U_COUNT][nfeatures]: derived column of unary(feature), -1 none
+  // constant-operand binaries fused as PBC fields (SR_AMD_PBC=0 turns it off: A/B runs)
+  const bool fuse_pbc = [] {
+    static const bool on = [] {
+      const char* v = std::getenv("SR_AMD_PBC");
+      return !(v && v[0] == '0');
+    }();
+    return on;
+  }();
 
   TreeCompiler(const SrOpset& o, int64_t nr, int64_t nf, bool wci, const int16_t* dm = nullptr)
       : ops(o), n_rows(nr), nfeatures(nf), with_const_index(wci), derived(dm) {}
@@ -466,6 +474,47 @@ struct TreeCompiler {
     return true;
   }
 
+  // A folded constant subtree DE evaluates as an array (a general deg2 child) is checked statically,
+  // as in emit_pair (round 5: the operand forms CR / CL had skipped it — (x1 + x2) * (1e30 * 1e8) over
+  // 4,000 rows scored complete where DE's isfinite(sum) of that child array fails)
+  void const_operand_check(int leaf) {
+    if (arr_check[leaf] && (folded[leaf] || t.constant[leaf])) static_array_check(folded[leaf] ? fold_val[leaf] : t.val[leaf]);
+  }
+
+  // A binary node op(tos, c) / op(c, tos) whose constant operand `leaf` (a constant or folded subtree) rides on
+  // the instruction that computed tos as its PBC field (sr_ops.h), when that instruction holds no
+  // constant of its own and no PBC yet; its own check becomes PBC_CHECK.  Gradient programs keep the
+  // plain form.  Returns false when the fused form does not apply.
+  bool fuse_const_operand(int i, int leaf, uint32_t bop, bool left) {
+    if (with_const_index || code.empty() || !fuse_pbc) return false;
+    SrIns<T> lf = leaf_ins(leaf);
+    if (lf.op != SR_OP_LOAD_CONST) return false;
+    SrIns<T>& last = code.back();
+    if ((last.op >> SR_OP_PBC_SHIFT) != 0u) return false;
+    const uint32_t base = last.op & SR_OP_MASK;
+    const bool free_c = base == SR_OP_LOAD_FEAT || base == SR_OP_LOAD_FEAT_PUSH ||
+                        (base >= SR_OP_UNARY0 && base < SR_OP_LOAD_DERIVED) ||
+                        (base >= SR_OP_BINARY0 && base < SR_OP_PAIR0 && (base - SR_OP_BINARY0) % 6u < SR_V_CL);
+    if (!free_c) return false;
+    uint32_t v = 0;
+    switch (bop) {
+      case SR_B_ADD: v = SR_PBC_ADD; break;
+      case SR_B_SUB: v = left ? SR_PBC_SUB_L : SR_PBC_SUB_R; break;
+      case SR_B_MUL: v = SR_PBC_MUL; break;
+      case SR_B_DIV: v = left ? SR_PBC_DIV_L : SR_PBC_DIV_R; break;
+      default: return false;
+    }
+    const_operand_check(leaf);
+    last.op |= v << SR_OP_PBC_SHIFT;
+    last.c0 = lf.c0;
+    last.c1 = lf.c1;
+    if (arr_check[i]) {
+      last.op |= SR_OP_PBC_CHECK;
+      ++n_checks;
+    }
+    return true;
+  }
+
   void emit(int i) {
     if (effleaf(i)) {
       code.push_back(leaf_ins(i));
@@ -490,7 +539,7 @@ struct TreeCompiler {
       // the child's code ends with the instruction computing it: the unary rides on it as its POST
       // operator (one dispatch for both), unless that instruction carries one already; gradient
       // programs keep the plain form (their kernel has no post operators)
-      if (!with_const_index && !code.empty() && (code.back().op >> SR_OP_POST_SHIFT) == 0u) {
+      if (!with_const_index && !code.empty() && (code.back().op >> SR_OP_POST_SHIFT) == 0u) {  // (no POST, no PBC)
         code.back().op |= (unary_id(i) << SR_OP_POST_SHIFT) | (infsub[i] ? SR_OP_POST_INF : 0u);
         if (arr_check[i]) {
           code.back().op |= SR_OP_POST_CHECK;
@@ -512,9 +561,13 @@ struct TreeCompiler {
       // both operands in one instruction
     } else if (effleaf(b)) {  // op(tos = left, operand = right leaf)
       emit(a);
+      if (fuse_const_operand(i, b, bop, false)) return;
+      const_operand_check(b);
       code.push_back(operand_ins(b, bop, false));
     } else if (effleaf(a)) {  // op(operand = left leaf, tos = right)
       emit(b);
+      if (fuse_const_operand(i, a, bop, true)) return;
+      const_operand_check(a);
       code.push_back(operand_ins(a, bop, true));
     } else {  // the operand needing more slots first, pushed to slot `depth`; the other in tos
       const bool left_first = need[a] >= need[b];
@@ -599,8 +652,10 @@ static uint32_t sr_unary_cost(uint32_t u) {
 
 uint32_t sr_instruction_cost(uint32_t code) {
   const uint32_t post = (code >> SR_OP_POST_SHIFT) & 0x3fu;
+  const uint32_t pbc = (code >> SR_OP_PBC_SHIFT) & 7u;
   uint32_t c = 6;  // dispatch + operand fetch + validity tracking
   if (post) c += 2 + sr_unary_cost(post) + ((code & SR_OP_POST_INF) ? 2u : 0u);
+  if (pbc) c += 3 + ((pbc == SR_PBC_DIV_R || pbc == SR_PBC_DIV_L) ? 6u : 1u);
   code &= SR_OP_MASK;
   if (code == SR_OP_LOAD_FEAT_PUSH || code == SR_OP_LOAD_CONST_PUSH || code == SR_OP_LOAD_DERIVED_PUSH) c += 2;
   if (code == SR_OP_LOAD_DERIVED || code == SR_OP_LOAD_DERIVED_PUSH) return c + 3;

@@ -105,6 +105,11 @@ SR_HD inline bool sr_loss_propagates_nan(int32_t kind) {
 //                     fused into the instruction computing its child (one dispatch for both)
 //   op bit  22      : POST_INF  the post unary is DynamicExpressions' fused form (non-finite -> +Inf)
 //   op bit  23      : POST_CHECK  the post unary's output array is validity-checked
+//   op bits 24-26   : PBC  a binary node with a constant operand fused into the instruction computing
+//                     its other operand (round 5: one dispatch for both), applied after the POST unary:
+//                     1 tos + c, 2 tos - c, 3 c - tos, 4 tos * c, 5 tos / c, 6 c / tos (c in c0 / c1:
+//                     only instructions that use no constant carry it: LOAD_FEAT, unary, S / F binaries)
+//   op bit  27      : PBC_CHECK  the post binary's output array is validity-checked
 //   meta bits  0-15 : operand index: feature f (F variants, LOAD_FEAT*), stack slot k (S variants),
 //                     pre-order constant slot of a constant leaf (gradient programs; else 0)
 //   meta bits 24-29 : push slot + 1 (LOAD_*_PUSH)
@@ -122,6 +127,8 @@ enum : uint32_t {
   SR_V_SL = 0u, SR_V_SR = 1u, SR_V_FL = 2u, SR_V_FR = 3u, SR_V_CL = 4u, SR_V_CR = 5u,
   SR_P_FF = 0u, SR_P_FC = 1u, SR_P_CF = 2u, SR_P_PUSH = 3u,
   SR_OP_MASK = 0x1ffu, SR_OP_POST_SHIFT = 16u, SR_OP_POST_INF = 1u << 22, SR_OP_POST_CHECK = 1u << 23,
+  SR_OP_PBC_SHIFT = 24u, SR_OP_PBC_CHECK = 1u << 27,
+  SR_PBC_ADD = 1u, SR_PBC_SUB_R = 2u, SR_PBC_SUB_L = 3u, SR_PBC_MUL = 4u, SR_PBC_DIV_R = 5u, SR_PBC_DIV_L = 6u,
   SR_M_INDEX = 0xffffu, SR_M_PUSH_SHIFT = 24u, SR_M_PUSH_MASK = 0x3fu << 24, SR_M_CHECK = 1u << 31,
   SR_MAX_STACK_SLOTS = 62u,
 };

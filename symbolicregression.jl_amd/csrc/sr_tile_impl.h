@@ -1154,7 +1154,6 @@ __global__ void __launch_bounds__(W * 64, (SrMinWavesFor<T, R, TIER, W, VSTK, LK
             default:
               break;
           }
-#undef SR_CVAL
 #undef SR_PUSH_TOS
           // DynamicExpressions' check of a node's output array (per node: FULL tier, PRED, EXACT)
 #define SR_CHECK_NODE()                                                                                      \
@@ -1180,26 +1179,47 @@ __global__ void __launch_bounds__(W * 64, (SrMinWavesFor<T, R, TIER, W, VSTK, LK
           if (!FAST_CHECK && (SR_META() & SR_M_CHECK)) {
             SR_CHECK_NODE();
           }
-          // the POST unary fused into this instruction (the node whose child it computed)
-          const uint32_t post = (op >> SR_OP_POST_SHIFT) & 0x3fu;
-          if (post != 0u && !dead) {
-            // (an opaque copy: LLVM would otherwise fold the test above into the post switch's
-            //  balanced compare tree, where post = 0 — most instructions — is a leaf three levels
-            //  down: 7 scalar instructions per dispatch instead of 3)
-            uint32_t pu = post;
+          // the POST unary and the post binary with a constant (PBC) fused into this instruction (the
+          // node whose child it computed, then that node's parent): ONE test of the op word's upper
+          // half on the common path (most instructions carry neither)
+          if ((op >> SR_OP_POST_SHIFT) != 0u && !dead) {
+            const uint32_t post = (op >> SR_OP_POST_SHIFT) & 0x3fu;
+            if (post != 0u) {
+              // (an opaque copy: LLVM would otherwise fold the test above into the post switch's
+              //  balanced compare tree)
+              uint32_t pu = post;
 #ifndef SR_POST_FOLDED
-            asm volatile("" : "+s"(pu));
+              asm volatile("" : "+s"(pu));
 #endif
-            sr_post_unary<T, R, TIER, FAST_CHECK>(pu, (op & SR_OP_POST_INF) != 0u, tos);
+              sr_post_unary<T, R, TIER, FAST_CHECK>(pu, (op & SR_OP_POST_INF) != 0u, tos);
 #ifdef SR_TRACK_LITE
-            if (!sr_untracked_u(pu))
+              if (!sr_untracked_u(pu))
 #endif
-            SR_TRACK();
-            if (!FAST_CHECK && (op & SR_OP_POST_CHECK)) {
-              SR_CHECK_NODE();
+              SR_TRACK();
+              if (!FAST_CHECK && (op & SR_OP_POST_CHECK)) {
+                SR_CHECK_NODE();
+              }
+            }
+            const uint32_t pbc = (op >> SR_OP_PBC_SHIFT) & 7u;
+            if (pbc != 0u && !dead) {
+              // the same row bodies as the CR / CL instructions (a constant operand: always tracked)
+              const T cv = SR_CVAL();
+              switch (pbc) {
+                case SR_PBC_ADD: { SR_BIN_EACH(tos[r], cv, SR_B_ADD); break; }
+                case SR_PBC_SUB_R: { SR_BIN_EACH(tos[r], cv, SR_B_SUB); break; }
+                case SR_PBC_SUB_L: { SR_BIN_EACH(cv, tos[r], SR_B_SUB); break; }
+                case SR_PBC_MUL: { SR_BIN_EACH(tos[r], cv, SR_B_MUL); break; }
+                case SR_PBC_DIV_R: { SR_BIN_EACH(tos[r], cv, SR_B_DIV); break; }
+                default: { SR_BIN_EACH(cv, tos[r], SR_B_DIV); break; }
+              }
+              SR_TRACK();
+              if (!FAST_CHECK && (op & SR_OP_PBC_CHECK)) {
+                SR_CHECK_NODE();
+              }
             }
           }
 #undef SR_CHECK_NODE
+#undef SR_CVAL
         }
       }
 

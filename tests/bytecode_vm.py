@@ -80,6 +80,7 @@ LOAD_FEAT, LOAD_CONST, LOAD_FEAT_PUSH, LOAD_CONST_PUSH = 0, 1, 2, 3
 UNARY0, UNARY_INF0, BINARY0, PAIR0 = 4, 40, 80, 256
 CHECK = 1 << 31
 OP_MASK, POST_SHIFT, POST_INF, POST_CHECK = 0x1FF, 16, 1 << 22, 1 << 23
+PBC_SHIFT, PBC_CHECK = 24, 1 << 27  # post binary with a constant: 1 +c, 2 -c, 3 c-, 4 *c, 5 /c, 6 c/
 
 
 def operand(meta):
@@ -163,6 +164,14 @@ def run_program(code, lo, hi, X, T):
                 v = np.where(np.isfinite(tos), v, T(np.inf)).astype(T)
             tos = v
             if (word & POST_CHECK) and not checked(tos):
+                complete = False
+        pbc = (word >> PBC_SHIFT) & 7  # then a binary node with a constant operand
+        if pbc:
+            c = np.full(n, val, dtype=T)
+            bid, a, b = {1: (B["ADD"], tos, c), 2: (B["SUB"], tos, c), 3: (B["SUB"], c, tos), 4: (B["MUL"], tos, c),
+                         5: (B["DIV"], tos, c), 6: (B["DIV"], c, tos)}[pbc]
+            tos = _binary(bid, a, b).astype(T)
+            if (word & PBC_CHECK) and not checked(tos):
                 complete = False
     return tos, complete
 

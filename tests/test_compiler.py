@@ -35,6 +35,44 @@ def test_compiled_programs_match_oracle(seed):
     assert_losses_within(loss, ol, comp, tol)
 
 
+@pytest.mark.parametrize("dtype", [np.float32, np.float64])
+def test_post_binary_constant_fusion(dtype):
+    """A binary node with a constant operand rides on the instruction computing its other operand (the
+    PBC field, csrc/sr_ops.h): one instruction fewer, every variant (+, - and / on both sides, *), the
+    fused node's own array check (PBC_CHECK) and a folded constant operand's static check."""
+    opts = Options(binary_operators=["+", "-", "*", "/"], unary_operators=["cos", "exp"])
+    cases = {  # expression: (instructions, PBC variant of the last instruction)
+        "(x1 + x2) * 3.0": (2, 0),                         # PAIR computes tos: no free constant word
+        "cos(x1 + x2) * 3.0": (2, 0),                      # PAIR + POST cos: the constant stays separate
+        "(x1 + cos(x2)) + 3.0": (2, 1),                    # LOAD+cos, FR add, then PBC +c
+        "(x1 + cos(x2)) - 3.0": (2, 2),
+        "3.0 - (x1 + cos(x2))": (2, 3),
+        "(x1 + cos(x2)) * 3.0": (2, 4),
+        "(x1 + cos(x2)) / 3.0": (2, 5),
+        "3.0 / (x1 + cos(x2))": (2, 6),
+        "cos(x1) * 1.0e30": (1, 4),                        # LOAD + POST cos + PBC
+        "(x1 * cos(x2)) * (1.0e30 * 1.0e3)": (2, 4),      # folded operand: checked statically,
+        "(x1 * cos(x2)) * (BIG * 1.0e8)": (0, 0),         # ... its 4000-row sum overflows: static_bad
+        "(x1 + x2) * (BIG * 1.0e8)": (0, 0),              # (the unfused operand form checks it too)
+        "exp(x1 * cos(x2)) - 1.0e38": (2, 2),
+    }
+    big = "1.0e30" if dtype == np.float32 else "1.0e300"
+    trees = [parse_expression(e.replace("BIG", big), opts) for e in cases]
+    tb = flatten_trees(trees, dtype)
+    code, offs, bad, _ = vm.compile_info(opts, tb, 4000, 5, dtype)
+    got = [(int(offs[k + 1] - offs[k]), (int(code["op"][offs[k + 1] - 1]) >> 24 & 7) if offs[k + 1] > offs[k] else 0)
+           for k in range(len(cases))]
+    assert got == list(cases.values()), list(zip(cases, got))
+    rng = np.random.default_rng(3)
+    X = rng.standard_normal((5, 4000)).astype(dtype)
+    X[0] = np.abs(X[0]) + 50.0  # exp(x1 cos(x2)) reaches Inf on some rows: the PBC node's input check
+    y = rng.standard_normal(4000).astype(dtype)
+    loss, comp = vm.eval_loss_batch(opts, tb, X, y, dtype)
+    tol, ol, oc, _ = loss_tolerance(Oracle.from_options(opts), tb, X, y)
+    assert np.array_equal(comp, oc), [(e, c, o) for e, c, o in zip(cases, comp, oc) if c != o]
+    assert_losses_within(loss, ol, comp, tol)
+
+
 def test_stack_depth_bound_for_maxsize_30():
     # Sethi-Ullman: a tree needing d stack slots has >= 1 + 2*m(d-1) nodes, m(0)=2 -> d <= 3 at 30 nodes
     opts = Options(**OPTS)
