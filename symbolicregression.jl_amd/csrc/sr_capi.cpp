@@ -78,6 +78,7 @@ struct DevBuf {
 struct HostBuf {
   void* p = nullptr;
   size_t cap = 0;
+  unsigned flags = hipHostMallocDefault;  // (SR_AMD_PROG_NC: the program staging buffer non-coherent)
   hipError_t ensure(size_t bytes, hipStream_t s, hipStream_t s2) {
     if (bytes <= cap) return hipSuccess;
     if (p) {
@@ -89,7 +90,7 @@ struct HostBuf {
       cap = 0;
     }
     size_t want = bytes < 65536 ? 65536 : bytes + bytes / 4;
-    hipError_t e = hipHostMalloc(&p, want, hipHostMallocDefault);
+    hipError_t e = hipHostMalloc(&p, want, flags);
     if (e == hipSuccess) cap = want;
     return e;
   }
@@ -3057,6 +3058,9 @@ int sr_init(int device, sr_ctx** out) {
   if (const char* v = std::getenv("SR_AMD_NO_SORT")) ctx->cost_order = std::atoi(v) == 0;
   if (const char* v = std::getenv("SR_AMD_BALANCE")) ctx->balance_groups = std::atoi(v) != 0;
   if (const char* v = std::getenv("SR_AMD_NO_HINT")) ctx->dead_hints = std::atoi(v) == 0;
+  // (A/B: the program staging buffer allocated non-coherent, so that kernels reading programs from it
+  //  — SR_AMD_HOST_IO=2 — may cache them in L2; the dispatch's acquire makes each call's writes visible)
+  if (const char* v = std::getenv("SR_AMD_PROG_NC")) ctx->h_prog.flags = std::atoi(v) ? hipHostMallocNonCoherent : hipHostMallocDefault;
   if (const char* v = std::getenv("SR_AMD_CHUNKS")) ctx->chunks = std::atoi(v);
   if (const char* v = std::getenv("SR_AMD_PROBE")) ctx->probe = std::atoi(v);
   if (const char* v = std::getenv("SR_AMD_FOLD_SEG")) ctx->fold_seg = std::atoll(v);
@@ -3131,6 +3135,7 @@ int sr_init_shared(sr_ctx* parent, sr_ctx** out) {
   c->stress_probe = parent->stress_probe;
   c->fold_seg = parent->fold_seg;
   c->spin = parent->spin;
+  c->h_prog.flags = parent->h_prog.flags;
   return SR_OK;
 }
 
