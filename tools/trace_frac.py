@@ -31,8 +31,14 @@ def main(out, workload="c2"):
     prefix = f"void sr_tile_kernel<float, {rpl}, 0,"
     interp = [r for r in rows if pat.match(r["Kernel_Name"])]
     interp.sort(key=lambda r: int(r["Start_Timestamp"]))
-    # probes: each step after the first chunk adds one probe launch (small grid)
-    probes_per_step = 1 if per_step == 2 else 0
+    # probes: dead-tree probe launches (small grids) before the large chunks — since round 5 before a
+    # large first chunk too; when every launch of the run belongs to its warm-up + timed steps (the
+    # C2-only command of tools/r05_evidence.sh), the launches per step follow from the count
+    warm = line.get("warmup", 0)
+    if len(interp) % (steps + warm) == 0 and len(interp) // (steps + warm) >= per_step:
+        probes_per_step = len(interp) // (steps + warm) - per_step
+    else:
+        probes_per_step = 1 if per_step == 2 else 0
     k = steps * (per_step + probes_per_step)
     timed = interp[-k:]
     ns = sum(int(r["End_Timestamp"]) - int(r["Start_Timestamp"]) for r in timed)
