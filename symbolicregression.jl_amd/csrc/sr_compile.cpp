@@ -8,7 +8,9 @@
 
 #include <unistd.h>
 
+#include <algorithm>
 #include <atomic>
+#include <chrono>
 #include <cstdlib>
 #include <cmath>
 #include <condition_variable>
@@ -46,6 +48,7 @@ class WorkerPool {
       n_jobs_ = n;
       done_.store(0);
       ticket_.store(g << 32);
+      gen_pub_.store(g, std::memory_order_release);
     }
     if (n > 1 && !threads_.empty()) cv_.notify_all();
     drain(g, &fn, n);
@@ -57,6 +60,7 @@ class WorkerPool {
     unsigned hc = std::thread::hardware_concurrency();
     int n = int(hc == 0 ? 4 : (hc > 16 ? 16 : hc));
     if (const char* v = std::getenv("SR_AMD_COMPILE_THREADS")) n = std::atoi(v) > 0 ? std::atoi(v) : 1;
+    if (const char* v = std::getenv("SR_AMD_COMPILE_SPIN_US")) spin_us_ = std::max(0, std::atoi(v));
     --n;  // the caller is a worker too
     for (int i = 0; i < n; ++i) threads_.emplace_back([this] { loop(); });
     for (auto& t : threads_) t.detach();  // lives for the process
@@ -78,6 +82,13 @@ class WorkerPool {
       uint64_t g;
       const std::function<void(int)>* job;
       int n;
+      // a short spin before sleeping: a batch that follows soon (a chunked call's second compile, a
+      // few tens of us after its first) finds the workers awake instead of paying their wake-ups
+      // (round 5: the tree-sharding share's 1,250 trees took 0.17 ms on the box, ~3x their work)
+      const auto t0 = std::chrono::steady_clock::now();
+      while (gen_pub_.load(std::memory_order_acquire) == seen &&
+             std::chrono::steady_clock::now() - t0 < std::chrono::microseconds(spin_us_))
+        std::this_thread::yield();
       {
         std::unique_lock<std::mutex> lk(mu_);
         cv_.wait(lk, [&] { return gen_ != seen; });
@@ -97,6 +108,8 @@ class WorkerPool {
   std::atomic<uint64_t> ticket_{0};
   std::atomic<int> done_{0};
   uint64_t gen_ = 0;
+  std::atomic<uint64_t> gen_pub_{0};  // gen_, readable without the mutex (the spin above)
+  int spin_us_ = 300;                 // SR_AMD_COMPILE_SPIN_US
 };
 
 struct NameId {
@@ -718,11 +731,16 @@ int sr_compile_batch(const sr_tree_batch& trees, const SrOpset& ops, int64_t n_r
   std::vector<PerTree> per(size_t(nt > 0 ? nt : 0));
   std::vector<int> errs(size_t(nt > 0 ? nt : 0), SR_OK);
   const T* vals = static_cast<const T*>(trees.val);
-  // work split: pieces of 128..256 trees, about two per persistent worker; batches of up to 128 trees
-  // compile on the caller alone (waking the pool costs more: 40 trees 13-25 us through it against ~7
-  // inline on the box, profiles/r04_latency_ab.txt)
+  // work split: pieces of 32..256 trees, about four per persistent worker (round 5: 128 at least
+  // left a 1,250-tree batch in 10 pieces, the caller and the first workers awake doing most of them);
+  // batches of up to 128 trees compile on the caller alone (waking the pool costs more: 40 trees
+  // 13-25 us through it against ~7 inline on the box, profiles/r04_latency_ab.txt)
   const int64_t pool = nt > 128 ? WorkerPool::get().size() : 1;
-  const int64_t kPiece = std::max<int64_t>(128, std::min<int64_t>(256, (nt + 2 * pool - 1) / (2 * pool)));
+  static const int64_t min_piece = [] {
+    const char* v = std::getenv("SR_AMD_COMPILE_PIECE");  // (A/B: the smallest piece)
+    return v ? std::max<int64_t>(1, std::atoll(v)) : int64_t(32);
+  }();
+  const int64_t kPiece = std::max<int64_t>(min_piece, std::min<int64_t>(256, (nt + 4 * pool - 1) / (4 * pool)));
   const int n_pieces = int(nt <= kPiece ? 1 : (nt + kPiece - 1) / kPiece);
   const int nthreads = n_pieces;  // one code buffer per piece
   std::vector<std::vector<SrIns<T>>> bufs(static_cast<size_t>(nthreads));
