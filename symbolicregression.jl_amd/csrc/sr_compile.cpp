@@ -156,6 +156,14 @@ struct Tree {
   int64_t n;
 };
 
+// v[0..n) = x, growing v only when it is too short (the compiler's per-tree arrays keep their
+// capacity from tree to tree: an out-of-line vector::assign per array was ~10 % of a small batch)
+template <typename V, typename X>
+inline void reset_n(V& v, int64_t n, X x) {
+  if (int64_t(v.size()) < n) v.resize(size_t(n));
+  std::fill(v.begin(), v.begin() + n, x);
+}
+
 template <typename T>
 struct TreeCompiler {
   const SrOpset& ops;
@@ -238,8 +246,8 @@ struct TreeCompiler {
       fail(SR_ERR_BAD_TREE, "empty tree");
       return false;
     }
-    t.l.assign(n, -1);
-    t.r.assign(n, -1);
+    reset_n(t.l, n, -1);
+    reset_n(t.r, n, -1);
     int64_t pos = 0;
     // recursive descent with an explicit stack of pending child slots
     pending.clear();
@@ -281,7 +289,7 @@ struct TreeCompiler {
   // is_constant(tree) == all leaves constant (post-order over pre-order positions, reversed).
   void mark_const() {
     const int64_t n = t.n;
-    is_const.assign(n, 0);
+    reset_n(is_const, n, 0);
     for (int64_t i = n - 1; i >= 0; --i) {
       const int d = t.degree[i];
       if (d == 0) is_const[i] = t.constant[i] ? 1 : 0;
@@ -599,7 +607,7 @@ struct TreeCompiler {
 
   // Pre-order constant numbering (get_scalar_constants order).
   void number_constants() {
-    const_slot.assign(t.n, -1);
+    reset_n(const_slot, t.n, -1);
     uint32_t k = 0;
     for (int64_t i = 0; i < t.n; ++i)
       if (t.degree[i] == 0 && t.constant[i]) const_slot[i] = int32_t(k++);
@@ -623,15 +631,15 @@ struct TreeCompiler {
     n_ops = 0;
     if (!parse()) return false;
     const int64_t n = t.n;
-    folded.assign(n, 0);
-    arr_check.assign(n, 0);
-    infsub.assign(n, 0);
-    fold_val.assign(n, T(0));
-    need.assign(n, 0);
+    reset_n(folded, n, 0);
+    reset_n(arr_check, n, 0);
+    reset_n(infsub, n, 0);
+    reset_n(fold_val, n, T(0));
+    reset_n(need, n, 0);
     number_constants();
     if (with_const_index) {
       // gradient programs keep every constant leaf live: no folding (is_const stays 0)
-      is_const.assign(n, 0);
+      reset_n(is_const, n, 0);
     } else {
       mark_const();
     }
@@ -663,7 +671,7 @@ static uint32_t sr_unary_cost(uint32_t u) {
   }
 }
 
-uint32_t sr_instruction_cost(uint32_t code) {
+static uint32_t sr_instruction_cost_slow(uint32_t code) {
   const uint32_t post = (code >> SR_OP_POST_SHIFT) & 0x3fu;
   const uint32_t pbc = (code >> SR_OP_PBC_SHIFT) & 7u;
   uint32_t c = 6;  // dispatch + operand fetch + validity tracking
@@ -689,6 +697,22 @@ uint32_t sr_instruction_cost(uint32_t code) {
     c += 1;
   }
   return c;
+}
+
+// The same, from tables: the opcode's own cost (512 entries) plus the POST unary's (64) and the PBC
+// binary's (8) — called per compiled instruction, a switch per call was ~10 % of a small batch
+uint32_t sr_instruction_cost(uint32_t code) {
+  struct Tabs {
+    uint16_t op[SR_OP_MASK + 1], post[64], pbc[8];
+    Tabs() {
+      for (uint32_t c = 0; c <= SR_OP_MASK; ++c) op[c] = uint16_t(sr_instruction_cost_slow(c));
+      for (uint32_t u = 0; u < 64; ++u) post[u] = uint16_t(u ? sr_instruction_cost_slow(u << SR_OP_POST_SHIFT) - op[0] : 0);
+      for (uint32_t b = 0; b < 8; ++b) pbc[b] = uint16_t(b ? sr_instruction_cost_slow(b << SR_OP_PBC_SHIFT) - op[0] : 0);
+    }
+  };
+  static const Tabs t;
+  return t.op[code & SR_OP_MASK] + t.post[(code >> SR_OP_POST_SHIFT) & 0x3fu] + ((code & SR_OP_POST_INF) ? 2u : 0u) +
+         t.pbc[(code >> SR_OP_PBC_SHIFT) & 7u];
 }
 
 uint32_t sr_unary_id(const char* name) {
