@@ -176,11 +176,7 @@ struct TreeCompiler {
   std::vector<int32_t> const_slot;  // pre-order constant index of constant leaves
   std::vector<int32_t> need;
   std::vector<SrIns<T>> code;
-  struct Slot {
-    int32_t parent;
-    int which;
-  };
-  std::vector<Slot> pending;  // parse() work stack (kept across trees: no per-tree allocation)
+  std::vector<int32_t> sz;  // parse(): subtree sizes (kept across trees: no per-tree allocation)
   bool bad = false;
   int err = SR_OK;
   std::string msg;
@@ -239,7 +235,11 @@ struct TreeCompiler {
     }
   }
 
-  // Parse pre-order arrays into child links.
+  // Parse pre-order arrays into child links, in ONE reverse scan (round 5: the explicit-stack descent
+  // plus separate constant-numbering and constant-marking passes were ~40 % of a small batch): a
+  // node's children come after it, so subtree sizes are known when it is reached — left child i + 1,
+  // right child i + 1 + size(left) — and so is whether its subtree is all constants (`is_const`,
+  // DE's constant-tree test).  The root's subtree must cover every node.
   bool parse() {
     const int64_t n = t.n;
     if (n <= 0) {
@@ -248,54 +248,53 @@ struct TreeCompiler {
     }
     reset_n(t.l, n, -1);
     reset_n(t.r, n, -1);
-    int64_t pos = 0;
-    // recursive descent with an explicit stack of pending child slots
-    pending.clear();
-    pending.push_back({-1, 0});
-    while (!pending.empty()) {
-      Slot s = pending.back();
-      pending.pop_back();
-      if (pos >= n) {
-        fail(SR_ERR_BAD_TREE, "pre-order arrays end inside a subtree");
-        return false;
-      }
-      const int32_t i = int32_t(pos++);
-      if (s.parent >= 0) (s.which == 0 ? t.l : t.r)[s.parent] = i;
+    if (int64_t(sz.size()) < n) sz.resize(size_t(n));
+    if (int64_t(is_const.size()) < n) is_const.resize(size_t(n));
+    for (int64_t i = n - 1; i >= 0; --i) {
       const int d = t.degree[i];
+      if (d == 0) {
+        sz[i] = 1;
+        if (t.constant[i]) {
+          is_const[i] = 1;
+        } else {
+          is_const[i] = 0;
+          const int f = int(t.feature[i]);
+          if (f < 1 || f > nfeatures) {
+            fail(SR_ERR_BAD_TREE, "feature index out of range");
+            return false;
+          }
+        }
+        continue;
+      }
       if (d > 2) {
         fail(SR_ERR_BAD_TREE, "degree > 2");
         return false;
       }
-      if (d == 2) {
-        pending.push_back({i, 1});  // right after left
-        pending.push_back({i, 0});
-      } else if (d == 1) {
-        pending.push_back({i, 0});
-      } else if (!t.constant[i]) {
-        const int f = int(t.feature[i]);
-        if (f < 1 || f > nfeatures) {
-          fail(SR_ERR_BAD_TREE, "feature index out of range");
+      const int64_t a = i + 1;
+      if (a >= n) {
+        fail(SR_ERR_BAD_TREE, "pre-order arrays end inside a subtree");
+        return false;
+      }
+      t.l[i] = int32_t(a);
+      if (d == 1) {
+        sz[i] = 1 + sz[a];
+        is_const[i] = is_const[a];
+      } else {
+        const int64_t b = a + sz[a];
+        if (b >= n) {
+          fail(SR_ERR_BAD_TREE, "pre-order arrays end inside a subtree");
           return false;
         }
+        t.r[i] = int32_t(b);
+        sz[i] = 1 + sz[a] + sz[b];
+        is_const[i] = is_const[a] & is_const[b];
       }
     }
-    if (pos != n) {
+    if (sz[0] != n) {
       fail(SR_ERR_BAD_TREE, "extra nodes after the root subtree");
       return false;
     }
     return true;
-  }
-
-  // is_constant(tree) == all leaves constant (post-order over pre-order positions, reversed).
-  void mark_const() {
-    const int64_t n = t.n;
-    reset_n(is_const, n, 0);
-    for (int64_t i = n - 1; i >= 0; --i) {
-      const int d = t.degree[i];
-      if (d == 0) is_const[i] = t.constant[i] ? 1 : 0;
-      else if (d == 1) is_const[i] = is_const[t.l[i]];
-      else is_const[i] = is_const[t.l[i]] && is_const[t.r[i]];
-    }
   }
 
   // dispatch_constant_tree: scalar fold with is_valid after every op.  Leaf constants are
@@ -637,12 +636,8 @@ struct TreeCompiler {
     reset_n(fold_val, n, T(0));
     reset_n(need, n, 0);
     number_constants();
-    if (with_const_index) {
-      // gradient programs keep every constant leaf live: no folding (is_const stays 0)
-      reset_n(is_const, n, 0);
-    } else {
-      mark_const();
-    }
+    // (is_const from parse(); gradient programs keep every constant leaf live: no folding)
+    if (with_const_index) reset_n(is_const, n, 0);
     evalmark(0);
     arr_check[0] = 1;  // final is_bad_array check on the output
     if (err != SR_OK) return false;
