@@ -785,6 +785,13 @@ hipError_t sr_launch_eval(const SrEvalArgs<T>& a, int mode, bool gather, int tie
     if (mode == SR_MODE_PRED)
       return gather ? sr_launch_tile<T, 4, SR_MODE_PRED, true, SR_TIER_FULL>(a, n_blocks, s)
                     : sr_launch_tile<T, 4, SR_MODE_PRED, false, SR_TIER_FULL>(a, n_blocks, s);
+    if (tier == SR_TIER_BASIC) {  // (EXACT over a BASIC operator set: the smaller dispatch)
+      if (waves == 4)
+        return gather ? sr_launch_tile<T, 4, SR_MODE_EXACT, true, SR_TIER_BASIC, 4>(a, n_blocks, s)
+                      : sr_launch_tile<T, 4, SR_MODE_EXACT, false, SR_TIER_BASIC, 4>(a, n_blocks, s);
+      return gather ? sr_launch_tile<T, 4, SR_MODE_EXACT, true, SR_TIER_BASIC, 1>(a, n_blocks, s)
+                    : sr_launch_tile<T, 4, SR_MODE_EXACT, false, SR_TIER_BASIC, 1>(a, n_blocks, s);
+    }
     if (waves == 4)  // (EXACT: 1 or 4 waves per workgroup, sharing the staged rows)
       return gather ? sr_launch_tile<T, 4, SR_MODE_EXACT, true, SR_TIER_FULL, 4>(a, n_blocks, s)
                     : sr_launch_tile<T, 4, SR_MODE_EXACT, false, SR_TIER_FULL, 4>(a, n_blocks, s);
@@ -806,6 +813,13 @@ hipError_t sr_launch_eval(const SrEvalArgs<T>& a, int mode, bool gather, int tie
     if (mode == SR_MODE_PRED)
       return gather ? sr_launch_tile<T, 2, SR_MODE_PRED, true, SR_TIER_FULL>(a, n_blocks, s)
                     : sr_launch_tile<T, 2, SR_MODE_PRED, false, SR_TIER_FULL>(a, n_blocks, s);
+    if (tier == SR_TIER_BASIC) {
+      if (waves == 4)
+        return gather ? sr_launch_tile<T, 2, SR_MODE_EXACT, true, SR_TIER_BASIC, 4>(a, n_blocks, s)
+                      : sr_launch_tile<T, 2, SR_MODE_EXACT, false, SR_TIER_BASIC, 4>(a, n_blocks, s);
+      return gather ? sr_launch_tile<T, 2, SR_MODE_EXACT, true, SR_TIER_BASIC, 1>(a, n_blocks, s)
+                    : sr_launch_tile<T, 2, SR_MODE_EXACT, false, SR_TIER_BASIC, 1>(a, n_blocks, s);
+    }
     if (waves == 4)
       return gather ? sr_launch_tile<T, 2, SR_MODE_EXACT, true, SR_TIER_FULL, 4>(a, n_blocks, s)
                     : sr_launch_tile<T, 2, SR_MODE_EXACT, false, SR_TIER_FULL, 4>(a, n_blocks, s);

@@ -680,6 +680,7 @@ int run_batch(sr_ctx* ctx, const sr_dataset* ds, int opset_id, const sr_tree_bat
   prog->static_bad.assign(size_t(nt), 0);
   prog->n_checks.assign(size_t(nt), 0);
   prog->max_depth = 0;
+  prog->tier = tier;
   prog->max_checks = 0;
   prog->total_nodes = 0;
   prog->total_ops = 0;
@@ -1289,6 +1290,13 @@ int run_exact(sr_ctx* ctx, const sr_dataset* ds, const SrProgramBatch<T>& prog, 
   const int depth = prog.max_depth > 0 ? prog.max_depth : 1;
   const int R = sr_rows_per_lane<T>(SR_MODE_EXACT, SR_TIER_FULL, 0);
   const int64_t rows = 64 * int64_t(R);
+  // (BASIC operator sets: the BASIC-tier build of the pass, same rows and LDS plan, a smaller
+  //  dispatch; SR_AMD_EXACT_TIER=full keeps the FULL-tier build for A/B runs)
+  static const bool exact_full = [] {
+    const char* v = std::getenv("SR_AMD_EXACT_TIER");
+    return v && std::strcmp(v, "full") == 0;
+  }();
+  const int etier = (prog.tier == SR_TIER_BASIC && !exact_full) ? SR_TIER_BASIC : SR_TIER_FULL;
   const int64_t n_ranges = int64_t(ranges.size());
   int64_t max_len = 1;
   std::vector<int64_t> lo(static_cast<size_t>(n_ranges)), hi(static_cast<size_t>(n_ranges));
@@ -1391,7 +1399,7 @@ int run_exact(sr_ctx* ctx, const sr_dataset* ds, const SrProgramBatch<T>& prog, 
     const int64_t blocks = int64_t(a.n_groups) * n_ranges;
     if (blocks > 0x7fffffff) return set_error(SR_ERR_INVALID_ARG, "grid too large");
     SR_HIP_CHECK(hipEventRecord(ctx->ev_k0, s));
-    SR_HIP_CHECK(sr_launch_eval<T>(a, SR_MODE_EXACT, gather, SR_TIER_FULL, R, W, false, int(blocks), s));
+    SR_HIP_CHECK(sr_launch_eval<T>(a, SR_MODE_EXACT, gather, etier, R, W, false, int(blocks), s));
     if (host_finite) {
       const int64_t n_arrays = nb * max_checks;
       SR_HIP_CHECK(ctx->jsum_scratch.ensure(size_t(std::max<int64_t>(1, n_arrays * n_internal)) * sizeof(T)));

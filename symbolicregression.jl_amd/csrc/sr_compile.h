@@ -40,6 +40,8 @@ struct SrProgramBatch {
   std::vector<uint32_t> cost;       // estimated device cost per tree (launch ordering / balancing)
   std::vector<uint8_t> depth;       // operand-stack slots each tree needs
   int max_depth = 0;                // operand-stack slots needed (below top-of-stack)
+  int tier = 1;                     // operator tier the programs ran under (SR_TIER_*; set by run_batch):
+                                    // the exact-sum pass runs the same tier's kernel
   int max_checks = 0;
   int64_t total_nodes = 0;          // Σ count_nodes (metric unit)
   int64_t total_ops = 0;            // Σ operator nodes
