@@ -82,9 +82,9 @@ class WorkerPool {
       uint64_t g;
       const std::function<void(int)>* job;
       int n;
-      // a short spin before sleeping: a batch that follows soon (a chunked call's second compile, a
-      // few tens of us after its first) finds the workers awake instead of paying their wake-ups
-      // (round 5: the tree-sharding share's 1,250 trees took 0.17 ms on the box, ~3x their work)
+      // optional spin before sleeping (SR_AMD_COMPILE_SPIN_US; off by default: on the box the spinning
+      // workers cost the calling thread more than their wake-ups — C2 4.07-4.16 ms per step without,
+      // 4.16-4.24 with 300 us, 4.22 with 2 ms; profiles/r05_ab_exact_compile.txt)
       const auto t0 = std::chrono::steady_clock::now();
       while (gen_pub_.load(std::memory_order_acquire) == seen &&
              std::chrono::steady_clock::now() - t0 < std::chrono::microseconds(spin_us_))
@@ -109,7 +109,7 @@ class WorkerPool {
   std::atomic<int> done_{0};
   uint64_t gen_ = 0;
   std::atomic<uint64_t> gen_pub_{0};  // gen_, readable without the mutex (the spin above)
-  int spin_us_ = 300;                 // SR_AMD_COMPILE_SPIN_US
+  int spin_us_ = 0;                   // SR_AMD_COMPILE_SPIN_US
 };
 
 struct NameId {
@@ -751,7 +751,8 @@ int sr_compile_batch(const sr_tree_batch& trees, const SrOpset& ops, int64_t n_r
   std::vector<int> errs(size_t(nt > 0 ? nt : 0), SR_OK);
   const T* vals = static_cast<const T*>(trees.val);
   // work split: pieces of 32..256 trees, about four per persistent worker (round 5: 128 at least
-  // left a 1,250-tree batch in 10 pieces, the caller and the first workers awake doing most of them);
+  // left a 1,250-tree batch in 10 pieces, the caller and the first workers awake doing most of them:
+  // the tree-sharding share's compile phase 0.13-0.14 -> 0.10-0.12 ms, profiles/r05_ab_exact_compile.txt);
   // batches of up to 128 trees compile on the caller alone (waking the pool costs more: 40 trees
   // 13-25 us through it against ~7 inline on the box, profiles/r04_latency_ab.txt)
   const int64_t pool = nt > 128 ? WorkerPool::get().size() : 1;
