@@ -178,6 +178,8 @@ struct sr_ctx {
     int n_rb;
   };
   std::vector<HostReduction> host_reductions;  // this call's launches whose partials await the host
+  std::vector<double> host_acc;                // (their per-(position, lane) accumulators)
+  std::vector<uint32_t> host_fl;
   int64_t host_red_rb = 0;                     // their partial buffer's row-block stride (n_rb)
   const uint8_t* h_bad_last = nullptr;         // the last run_batch's staged static flags and launch order
   const uint32_t* h_perm_last = nullptr;
@@ -1714,26 +1716,36 @@ void host_reduce_partials(sr_ctx* ctx, int64_t nt) {
   uint32_t* out_flag = reinterpret_cast<uint32_t*>(ctx->h_outs.as<char>() + ctx->outs_flag_off);
   const uint32_t* perm = ctx->h_perm_last;
   const uint8_t* bad = ctx->h_bad_last;
+  // (the partials are read once, in memory order — row block by row block, each a contiguous run of
+  //  positions — into per-(position, lane) accumulators; lane l still adds its row blocks l, l + 64,
+  //  ... in increasing order, so the sums are the reduce kernel's bit for bit.  Round 5: the column
+  //  walk it replaces touched a new cache line per partial, ~6k device-written lines per C3 call)
+  std::vector<double>& acc = ctx->host_acc;
+  std::vector<uint32_t>& fls = ctx->host_fl;
   for (const sr_ctx::HostReduction& hr : ctx->host_reductions) {
     const double* s0 = ps + size_t(ctx->host_red_rb) * size_t(hr.p0);
     const uint32_t* f0 = pf + size_t(ctx->host_red_rb) * size_t(hr.p0);
-    for (int64_t pos = 0; pos < hr.np; ++pos) {
-      double v[64];
-      uint32_t fl = 0;
-      for (int l = 0; l < 64; ++l) {
-        double a = 0.0;
-        for (int i = l; i < hr.n_rb; i += 64) {
-          const size_t o = size_t(i) * size_t(hr.np) + size_t(pos);
-          a += s0[o];
-          fl |= f0[o];
-        }
-        v[l] = a;
+    const size_t np = size_t(hr.np);
+    acc.assign(np * 64, 0.0);
+    fls.assign(np, 0u);
+    for (int i = 0; i < hr.n_rb; ++i) {
+      double* a = acc.data() + size_t(i & 63);
+      const double* srow = s0 + size_t(i) * np;
+      const uint32_t* frow = f0 + size_t(i) * np;
+      for (size_t pos = 0; pos < np; ++pos) {
+        a[pos * 64] += srow[pos];
+        fls[pos] |= frow[pos];
       }
+    }
+    for (size_t pos = 0; pos < np; ++pos) {
+      double v[64];
+      std::memcpy(v, acc.data() + pos * 64, sizeof(v));
       for (int off = 32; off >= 1; off >>= 1) {
         double nv[64];
         for (int l = 0; l < 64; ++l) nv[l] = v[l] + v[l ^ off];
         std::memcpy(v, nv, sizeof(v));
       }
+      uint32_t fl = fls[pos];
       const uint32_t tree = perm[hr.p0 + pos];
       if (bad[tree]) fl |= SR_FLAG_STATIC | SR_FLAG_NONFINITE;
       out_sum[tree] = v[0];
