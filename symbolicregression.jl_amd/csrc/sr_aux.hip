@@ -712,8 +712,7 @@ size_t sr_tile_lds_bytes(int elem_size, int nf, int rows_per_lane, int stack_dep
   // program cache (16-byte instructions)
   const size_t rows = size_t(64) * rows_per_lane;
   return size_t(nf) * rows * elem_size + (weighted ? 2 : 1) * rows * elem_size +
-         size_t(waves) * stack_depth * rows * elem_size +
-         size_t(waves) * size_t(max_checks) * size_t(sr_chk_stride(int(rows), elem_size)) * elem_size +
+         size_t(waves) * stack_depth * rows * elem_size + size_t(waves) * size_t(max_checks) * rows * elem_size +
          (size_t(trees_per_block) * size_t(max_checks) * elem_size + 15) / 16 * 16 + size_t(code_lds) * 16;
 }
 

@@ -13,15 +13,6 @@ enum { SR_MODE_LOSS = 0, SR_MODE_PRED = 1, SR_MODE_EXACT = 2 };
 #ifndef SR_TRACK_FULL
 #define SR_TRACK_LITE 1
 #endif
-// EXACT mode's checked values [W][MC][stride]: each check's row padded by 16 bytes, so the lanes
-// folding consecutive checks (lane k: check k) read different 16-byte bank slots (round 5: with the
-// unpadded 1 KiB stride every lane hit the same four banks — 57 % of the exact pass's LDS cycles were
-// bank conflicts, profiles/r05_prof_c2c.txt)
-#if defined(__HIPCC__)
-__host__ __device__
-#endif
-constexpr int sr_chk_stride(int rows, int elem_size) { return rows + 16 / elem_size; }
-
 #ifndef SR_VSTK_SLOTS
 #define SR_VSTK_SLOTS 2
 #endif

@@ -726,7 +726,7 @@ struct SrLdsPlan {
     stk = o;
     o += size_t(waves) * size_t(depth) * rows * sizeof(T);
     chk = o;
-    o += size_t(waves) * size_t(max_checks) * size_t(sr_chk_stride(rows, int(sizeof(T)))) * sizeof(T);
+    o += size_t(waves) * size_t(max_checks) * rows * sizeof(T);
     jst = o;
     o += (size_t(G) * size_t(max_checks) * sizeof(T) + 15) / 16 * 16;
     code = o;
@@ -833,8 +833,7 @@ __global__ void __launch_bounds__(W * 64, (SrMinWavesFor<T, R, TIER, W, VSTK, LK
   T* xs = reinterpret_cast<T*>(sr_smem + plan.x);
   T* ys = reinterpret_cast<T*>(sr_smem + plan.y);
   T* wsv = reinterpret_cast<T*>(sr_smem + plan.w);
-  T* chk = reinterpret_cast<T*>(sr_smem + plan.chk);  // EXACT: [W][MC][CHK] checked values of a tile
-  constexpr int CHK = sr_chk_stride(ROWS, int(sizeof(T)));
+  T* chk = reinterpret_cast<T*>(sr_smem + plan.chk);  // EXACT: [W][MC][ROWS] checked values of a tile
   T* jst = reinterpret_cast<T*>(sr_smem + plan.jst);  // EXACT: [G][MC] running sums
   const T* x_lane = xs + lane * C;
   const T* y_lane = ys + lane * C;
@@ -1160,7 +1159,7 @@ __global__ void __launch_bounds__(W * 64, (SrMinWavesFor<T, R, TIER, W, VSTK, LK
 #define SR_CHECK_NODE()                                                                                      \
   if (MODE == SR_MODE_EXACT) {                                                                               \
     /* the checked array's rows of this tile, in row order, for the Julia-order fold below */                \
-    if (check_k < MC) L::store(chk + (size_t(wave) * MC + check_k) * CHK + lane * C, tos);                   \
+    if (check_k < MC) L::store(chk + (size_t(wave) * MC + check_k) * ROWS + lane * C, tos);                  \
     ++check_k;                                                                                               \
   } else {                                                                                                   \
     /* |v| >= tbig (or NaN / Inf) in any row: one integer max per lane + one ballot; padded rows */          \
@@ -1236,7 +1235,7 @@ __global__ void __launch_bounds__(W * 64, (SrMinWavesFor<T, R, TIER, W, VSTK, LK
           const int nk = check_k < MC ? check_k : MC;
 #endif
           for (int k = lane; k < nk; k += 64) {
-            const T* cb = chk + (size_t(wave) * MC + k) * CHK;
+            const T* cb = chk + (size_t(wave) * MC + k) * ROWS;
             T v = (tile == 0) ? cb[0] : jst[g * MC + k];
             int i = (tile == 0) ? 1 : 0;
             // the adds stay sequential in row order; the LDS reads go 16 rows at a time (16-byte
