@@ -225,6 +225,9 @@ struct sr_ctx {
   HostBuf h_exact;
   std::vector<int64_t> exact_lo_dev, exact_hi_dev;  // what range_lo / range_hi hold
   int64_t jsum_n_dev = -1;                          // the row count jsum_prog was built for
+  // SR_AMD_EXACT_LIST_HOST (default 1): the pass reads its tree list from the pinned staging buffer
+  // (no upload ahead of the kernel); 0 copies it to the device first
+  int exact_list_host = 1;
 #ifdef SR_STAMPS
   DevBuf stamps;  // latency-analysis builds: the last main launch's per-wave stamps (sr_debug_stamps)
   int64_t n_stamps = 0;
@@ -1277,6 +1280,27 @@ JlLevels jl_levels(int64_t n) {
   return out;
 }
 
+// One view's leaves and combine program depend only on its row count: built once per thread and
+// count (every call of a search or a step sees the same n; ~2k recursive calls for 1M rows).
+const std::vector<JlRange>& jl_ranges_cached(int64_t n) {
+  thread_local int64_t cn = -1;
+  thread_local std::vector<JlRange> c;
+  if (cn != n) {
+    c = jl_ranges(0, n, n);
+    cn = n;
+  }
+  return c;
+}
+const JlLevels& jl_levels_cached(int64_t n) {
+  thread_local int64_t cn = -1;
+  thread_local JlLevels c;
+  if (cn != n) {
+    c = jl_levels(n);
+    cn = n;
+  }
+  return c;
+}
+
 // EXACT pass: the Julia-order fold of every checked array of the listed trees over `ranges` of this
 // view -> host_vals[n_list][max_checks][ranges] (T; a tree's unused check slots hold 0).  With
 // host_finite (single view: the ranges are the view's leaves in order) the leaves are combined on
@@ -1312,7 +1336,8 @@ int run_exact(sr_ctx* ctx, const sr_dataset* ds, const SrProgramBatch<T>& prog, 
   const size_t per_tree = size_t(max_checks) * size_t(n_ranges) * sizeof(T);
   const int64_t batch = std::max<int64_t>(1, int64_t((size_t(256) << 20) / per_tree));
   // pinned staging: [leaf ranges lo | hi | Julia-sum level program | tree list | verdicts]
-  const JlLevels lv = host_finite ? jl_levels(n_eval) : JlLevels{};
+  static const JlLevels kNoLevels{};
+  const JlLevels& lv = host_finite ? jl_levels_cached(n_eval) : kNoLevels;
   const size_t n_lvp = lv.nodes.size() + lv.level_off.size();
   const size_t o_hi = size_t(n_ranges) * sizeof(int64_t), o_lvp = 2 * o_hi;
   const size_t o_list = (o_lvp + n_lvp * sizeof(int32_t) + 15) & ~size_t(15);
@@ -1372,16 +1397,18 @@ int run_exact(sr_ctx* ctx, const sr_dataset* ds, const SrProgramBatch<T>& prog, 
       if (G < W) W = 1;
     }
     if (lds > kLdsMax) return set_error(SR_ERR_TOO_DEEP, "exact-sum pass needs more LDS than 160 KiB");
-    uint32_t* list32 = reinterpret_cast<uint32_t*>(hx + o_list);  // (the previous batch's copy has completed)
+    uint32_t* list32 = reinterpret_cast<uint32_t*>(hx + o_list);  // (the previous batch's pass has completed)
     for (int64_t i = 0; i < nb; ++i) list32[i] = uint32_t(list[b0 + i]);
-    SR_HIP_CHECK(ctx->tree_list.ensure(size_t(nb) * sizeof(uint32_t)));
-    SR_HIP_CHECK(hipMemcpyAsync(ctx->tree_list.p, list32, size_t(nb) * sizeof(uint32_t), hipMemcpyHostToDevice, s));
+    if (!ctx->exact_list_host) {
+      SR_HIP_CHECK(ctx->tree_list.ensure(size_t(nb) * sizeof(uint32_t)));
+      SR_HIP_CHECK(hipMemcpyAsync(ctx->tree_list.p, list32, size_t(nb) * sizeof(uint32_t), hipMemcpyHostToDevice, s));
+    }
     SR_HIP_CHECK(ctx->range_sums.ensure(size_t(nb) * per_tree));
     SrEvalArgs<T> a{};
     a.code = static_cast<const SrIns<T>*>(ctx->d_code);
     a.offsets = ctx->d_off;
     a.ends = ctx->d_end;
-    a.perm = ctx->tree_list.as<uint32_t>();
+    a.perm = ctx->exact_list_host ? list32 : ctx->tree_list.as<uint32_t>();
     a.n_trees = int(nb);
     a.trees_per_block = G;
     a.X = static_cast<const T*>(ds->X);
@@ -1435,7 +1462,7 @@ int exact_list_ok(sr_ctx* ctx, const sr_dataset* ds, const SrProgramBatch<T>& pr
   if (list.empty() || prog.max_checks == 0) return SR_OK;
   const bool gather = row_idx != nullptr && n_idx > 0;
   const int64_t n_eval = gather ? n_idx : ds->n;
-  const std::vector<JlRange> ranges = jl_ranges(0, n_eval, n_eval);
+  const std::vector<JlRange>& ranges = jl_ranges_cached(n_eval);
   // check slots: the most any LISTED tree has (the LDS image and the fold buffers scale with it)
   int mc = 0;
   for (int64_t t : list) mc = std::max(mc, int(prog.n_checks[size_t(t)]));
@@ -3097,6 +3124,7 @@ int sr_init(int device, sr_ctx** out) {
   if (const char* v = std::getenv("SR_AMD_SPIN")) ctx->spin = std::atoi(v);
   if (const char* v = std::getenv("SR_AMD_EXACT_G")) ctx->exact_g = std::atoi(v);
   if (const char* v = std::getenv("SR_AMD_EXACT_W")) ctx->exact_w = std::atoi(v) == 1 ? 1 : 4;
+  if (const char* v = std::getenv("SR_AMD_EXACT_LIST_HOST")) ctx->exact_list_host = std::atoi(v) != 0 ? 1 : 0;
   if (const char* v = std::getenv("SR_AMD_PAR_STAGE")) ctx->par_stage = std::atoi(v);
   if (const char* v = std::getenv("SR_AMD_DERIVED")) ctx->derived = std::atoi(v);
   if (const char* v = std::getenv("SR_AMD_MAX_ROW_BLOCKS")) ctx->max_row_blocks = std::max(1, std::atoi(v));
