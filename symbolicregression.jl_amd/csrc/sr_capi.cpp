@@ -228,6 +228,38 @@ struct sr_ctx {
   // SR_AMD_EXACT_LIST_HOST (default 1): the pass reads its tree list from the pinned staging buffer
   // (no upload ahead of the kernel); 0 copies it to the device first
   int exact_list_host = 1;
+  // Speculative exact-sum pass (round 5; SR_AMD_SPEC_EXACT / "spec_exact", default 1).  A large
+  // one-view LOSS call's dead-tree probe runs its trees over the dataset's stress rows (the extremes of
+  // every feature) before the main launch; a tree the probe already flags BIG (and not non-finite) is
+  // BIG on the whole view too (the same thresholds over a subset of the rows), so its exact pass starts
+  // on a third stream while the main launch runs, instead of after it.  The main launch's flags still
+  // decide: a BIG tree the probe missed takes the ordinary pass afterwards, and a speculated tree the
+  // main launch finds non-finite or not BIG leaves its verdict unused.  Verdicts are the same either way.
+  int spec_exact = 1;
+  bool want_spec = false;  // set by eval_loss_submit around its run_batch (one full view, no gather)
+  hipStream_t stream3 = nullptr;
+  // (SR_AMD_SPEC_PRIO: the third stream's priority, -1 the least, 0 normal, 1 the greatest)
+  int spec_prio = -1;
+  hipError_t need_stream3() {
+    if (stream3) return hipSuccess;
+    int least = 0, greatest = 0;
+    if (spec_prio == 0 || hipDeviceGetStreamPriorityRange(&least, &greatest) != hipSuccess)
+      return hipStreamCreateWithFlags(&stream3, hipStreamNonBlocking);
+    return hipStreamCreateWithPriority(&stream3, hipStreamNonBlocking, spec_prio < 0 ? least : greatest);
+  }
+  hipEvent_t ev_pr[kMaxChunks] = {};  // after each probed chunk's probe (cross-stream, untimed)
+  hipEvent_t ev_spec = nullptr;       // after the probe flags' copies on stream3
+  HostBuf h_pflag;                    // the probes' per-(tile, position) flags, copied back on stream3
+  struct SpecChunk {
+    int64_t t0, np;  // a probed launch: positions [0, np) of the chunk starting at tree t0
+  };
+  std::vector<SpecChunk> spec_chunks;  // this call's probed launches (set by run_batch)
+  std::vector<int64_t> spec_list;      // trees whose exact pass is in flight on stream3
+  std::vector<uint8_t> spec_ok;        // ... their verdicts once collected
+  int spec_mc = 0;                     // ... their check slots
+  size_t spec_fin_off = 0;             // ... where their verdicts land in h_exact
+  bool spec_pending = false;
+  int64_t n_spec_last = 0, n_spec_used_last = 0;  // speculated trees of the last call, and those used
 #ifdef SR_STAMPS
   DevBuf stamps;  // latency-analysis builds: the last main launch's per-wave stamps (sr_debug_stamps)
   int64_t n_stamps = 0;
@@ -350,6 +382,7 @@ namespace {
 
 constexpr int64_t kRowAlign = 2048;  // a multiple of every kernel's row tile (64 lanes x R rows)
 constexpr int64_t kProbeRows = 2048;
+constexpr int kProbeTiles = 4;  // row tiles of a dead-tree probe launch
 // dynamic LDS a register-stack workgroup may use with its program cache: with the 5 KiB of static
 // libm tables, 4 workgroups still fit a CU's 160 KiB
 constexpr size_t kCodeCacheLds = 34 * 1024;
@@ -500,10 +533,19 @@ struct ViewSpec {
   int64_t view_len;
 };
 
+// The speculative exact pass's stream (sr_ctx::spec_exact) drained: nothing of an earlier call (its
+// probe-flag copies, a pass an error path left running) may still use h_pflag / h_exact.
+inline void spec_drain(sr_ctx* ctx) {
+  if (ctx->stream3 && (ctx->spec_pending || !ctx->spec_chunks.empty())) (void)hipStreamSynchronize(ctx->stream3);
+  ctx->spec_pending = false;
+  ctx->spec_chunks.clear();
+}
+
 template <typename T>
 int run_batch(sr_ctx* ctx, const sr_dataset* ds, int opset_id, const sr_tree_batch* trees, const int64_t* row_idx,
               int64_t n_idx, int64_t n_total, int loss_kind, int mode, SrProgramBatch<T>* prog, Grid* grid_out,
               bool allow_derived = false, const ShardCtl* shard = nullptr, const ViewSpec* views = nullptr) {
+  spec_drain(ctx);
   const bool gather = row_idx != nullptr && n_idx > 0;
   // PRED passes (the fold's few band trees) write no partials: more row blocks fill the GPU (C4's 14 trees
   // x 2^26 rows ran 1,024 workgroups at 256)
@@ -663,7 +705,6 @@ int run_batch(sr_ctx* ctx, const sr_dataset* ds, int opset_id, const sr_tree_bat
     ++ctx->hint_epoch;
   }
   // dead-tree probe: the first kProbeTiles row tiles of the view, hints only (scratch partials)
-  constexpr int kProbeTiles = 4;
   const bool use_probe = use_hint && ctx->probe && n_rb >= 16 && !multi;  // (per chunk: its grid has >= 16 row blocks)
   if (use_probe) {
     SR_HIP_CHECK(ctx->probe_sum.ensure(size_t(nt) * kProbeTiles * sizeof(double) + 8));
@@ -746,6 +787,13 @@ int run_batch(sr_ctx* ctx, const sr_dataset* ds, int opset_id, const sr_tree_bat
     SR_HIP_CHECK(ctx->probe_derived.ensure(size_t(spec.n) * size_t(kProbeRows) * sizeof(T)));
     SR_HIP_CHECK(sr_launch_derived<T>(static_cast<const T*>(ds->X), ds->ld, static_cast<const int64_t*>(ds->probe_rows),
                                       ds->n_probe, kProbeRows, spec, ctx->probe_derived.as<T>(), kProbeRows, s));
+  }
+  // the speculative exact-sum pass (sr_ctx::spec_exact): each probe's flags come back on a third
+  // stream while the main launches run (each probed launch writes its own part of the scratch)
+  const bool spec_x = stress_probe && mode == SR_MODE_LOSS && ctx->spec_exact && ctx->want_spec && !shard;
+  if (spec_x) {
+    SR_HIP_CHECK(ctx->need_stream3());
+    SR_HIP_CHECK(ctx->h_pflag.ensure(size_t(nt) * kProbeTiles * sizeof(uint32_t) + 16, ctx->stream3, nullptr));
   }
   if (n_chunks > 1) {  // odd chunks run on the second stream, after the shared setup above
     SR_HIP_CHECK(ctx->need_stream2());
@@ -1063,8 +1111,8 @@ int run_batch(sr_ctx* ctx, const sr_dataset* ds, int opset_id, const sr_tree_bat
         pa.tiles_per_block = 1;
         pa.n_row_blocks = kProbeTiles;
         pa.n_rows = std::min<int64_t>(n_eval, int64_t(kProbeTiles) * 64 * R);
-        pa.part_sum = ctx->probe_sum.as<double>();
-        pa.part_flag = ctx->probe_flag.as<uint32_t>();
+        pa.part_sum = ctx->probe_sum.as<double>() + (spec_x ? size_t(t0) * kProbeTiles : 0);
+        pa.part_flag = ctx->probe_flag.as<uint32_t>() + (spec_x ? size_t(t0) * kProbeTiles : 0);
         if (stress_probe) {  // the stress rows first (sr_dataset::probe_rows), through the gather build
           pa.row_idx = static_cast<const int64_t*>(ds->probe_rows);
           pa.n_rows = std::min<int64_t>(ds->n_probe, int64_t(kProbeTiles) * 64 * R);
@@ -1074,6 +1122,13 @@ int run_batch(sr_ctx* ctx, const sr_dataset* ds, int opset_id, const sr_tree_bat
           }
         }
         SR_HIP_CHECK(sr_launch_eval<T>(pa, mode, gather || stress_probe, tier, R, W, false, pa.n_groups * kProbeTiles, cs));
+        if (spec_x && stress_probe) {  // ([row tile][position] flags of this launch's np positions)
+          SR_HIP_CHECK(hipEventRecord(ctx->ev_pr[c], cs));
+          SR_HIP_CHECK(hipStreamWaitEvent(ctx->stream3, ctx->ev_pr[c], 0));
+          SR_HIP_CHECK(hipMemcpyAsync(ctx->h_pflag.as<uint32_t>() + size_t(t0) * kProbeTiles, pa.part_flag,
+                                      size_t(np) * kProbeTiles * sizeof(uint32_t), hipMemcpyDeviceToHost, ctx->stream3));
+          ctx->spec_chunks.push_back({t0, np});
+        }
       }
 #ifdef SR_STAMPS
       ctx->n_stamps = g.n_blocks * g.W * SR_NSTAMPS;
@@ -1100,6 +1155,7 @@ int run_batch(sr_ctx* ctx, const sr_dataset* ds, int opset_id, const sr_tree_bat
     ctx->n_chunks_last = c + 1;
     code_base += uint32_t(ncode);
   }
+  if (!ctx->spec_chunks.empty()) SR_HIP_CHECK(hipEventRecord(ctx->ev_spec, ctx->stream3));
   if (n_chunks > 1) {  // the caller continues on the first stream: join the second
     SR_HIP_CHECK(hipEventRecord(ctx->ev_join, ctx->stream2));
     SR_HIP_CHECK(hipStreamWaitEvent(s, ctx->ev_join, 0));
@@ -1305,14 +1361,19 @@ const JlLevels& jl_levels_cached(int64_t n) {
 // view -> host_vals[n_list][max_checks][ranges] (T; a tree's unused check slots hold 0).  With
 // host_finite (single view: the ranges are the view's leaves in order) the leaves are combined on
 // the device in recursion order and only isfinite(sum) per array comes back: host_finite[n_list][max_checks].
+// Speculative use (stream `st`, sync = false; host_finite required, one batch): the launches are
+// only enqueued — after a synchronisation of `st` the verdicts are at h_exact + *fin_off
+// ([n_list][max_checks]) and ev_k0 / ev_k1 bracket the pass.
 template <typename T>
 int run_exact(sr_ctx* ctx, const sr_dataset* ds, const SrProgramBatch<T>& prog, const int64_t* row_idx,
               int64_t n_idx, const int64_t* list, int64_t n_list, int max_checks, const std::vector<JlRange>& ranges,
-              T* host_vals, uint8_t* host_finite = nullptr, int64_t dev_row_off = 0) {
+              T* host_vals, uint8_t* host_finite = nullptr, int64_t dev_row_off = 0, hipStream_t st = nullptr,
+              bool sync = true, size_t* fin_off = nullptr) {
   if (n_list == 0 || max_checks == 0 || ranges.empty()) return SR_OK;
+  if (!sync && (!host_finite || !fin_off)) return set_error(SR_ERR_INVALID_ARG, "speculative exact pass: no verdict buffer");
   const bool gather = row_idx != nullptr && n_idx > 0;
   const int64_t n_eval = gather ? n_idx : ds->n;
-  hipStream_t s = ctx->stream;
+  hipStream_t s = st ? st : ctx->stream;
   const int depth = prog.max_depth > 0 ? prog.max_depth : 1;
   const int R = sr_rows_per_lane<T>(SR_MODE_EXACT, SR_TIER_FULL, 0);
   const int64_t rows = 64 * int64_t(R);
@@ -1377,6 +1438,7 @@ int run_exact(sr_ctx* ctx, const sr_dataset* ds, const SrProgramBatch<T>& prog, 
       ctx->jsum_n_dev = n_eval;
     }
   }
+  if (!sync && batch < n_list) return set_error(SR_ERR_INVALID_ARG, "speculative exact pass: list too long");
   for (int64_t b0 = 0; b0 < n_list; b0 += batch) {
     const int64_t nb = std::min(batch, n_list - b0);
     // one wave per workgroup, G listed trees per workgroup (LDS: X tile + one wave's checked
@@ -1443,6 +1505,10 @@ int run_exact(sr_ctx* ctx, const sr_dataset* ds, const SrProgramBatch<T>& prog, 
                                   size_t(nb) * per_tree, hipMemcpyDeviceToHost, s));
     }
     SR_HIP_CHECK(hipEventRecord(ctx->ev_k1, s));
+    if (!sync) {
+      *fin_off = o_fin;
+      return SR_OK;
+    }
     SR_HIP_CHECK(hipStreamSynchronize(s));
     if (host_finite)
       std::memcpy(host_finite + size_t(b0) * max_checks, hx + o_fin, size_t(nb) * size_t(max_checks));
@@ -1474,6 +1540,64 @@ int exact_list_ok(sr_ctx* ctx, const sr_dataset* ds, const SrProgramBatch<T>& pr
   if (rc != SR_OK) return rc;
   for (size_t i = 0; i < list.size(); ++i)
     for (int k = 0; k < mc; ++k) (*list_ok)[i] &= fin[i * size_t(mc) + size_t(k)];
+  return SR_OK;
+}
+
+// The speculative exact pass (sr_ctx::spec_exact), first half: once the probes' flags are back (they
+// finish early in the main launches), the trees they flag BIG and not non-finite go through the pass
+// on the third stream while the main launches run.  At most kSpecMax trees (one pass batch).
+constexpr int64_t kSpecMax = 1024;
+template <typename T>
+int spec_launch(sr_ctx* ctx, const sr_dataset* ds, const SrProgramBatch<T>& prog, int64_t nt) {
+  if (ctx->spec_chunks.empty()) return SR_OK;
+  SR_HIP_CHECK(hipEventSynchronize(ctx->ev_spec));
+  const uint32_t* pf = ctx->h_pflag.as<uint32_t>();
+  const uint32_t* perm = ctx->h_perm_last;
+  std::vector<int64_t>& list = ctx->spec_list;
+  list.clear();
+  int mc = 0;
+  for (const sr_ctx::SpecChunk& ch : ctx->spec_chunks) {
+    const uint32_t* f = pf + size_t(ch.t0) * kProbeTiles;  // [tile][position]
+    for (int64_t p = 0; p < ch.np; ++p) {
+      uint32_t o = 0;
+      for (int k = 0; k < kProbeTiles; ++k) o |= f[size_t(k) * size_t(ch.np) + size_t(p)];
+      if ((o & SR_FLAG_BIG) == 0 || (o & SR_FLAG_NONFINITE) != 0) continue;
+      const int64_t t = ch.t0 + int64_t(perm[ch.t0 + p]);
+      if (t < 0 || t >= nt || prog.static_bad[size_t(t)] || prog.n_checks[size_t(t)] == 0) continue;
+      list.push_back(t);
+      mc = std::max(mc, int(prog.n_checks[size_t(t)]));
+    }
+  }
+  ctx->spec_chunks.clear();  // (the copies are complete: ev_spec)
+  if (list.empty() || int64_t(list.size()) > kSpecMax) {
+    list.clear();
+    return SR_OK;
+  }
+  ctx->n_spec_last = int64_t(list.size());
+  ctx->spec_mc = mc;
+  ctx->spec_ok.assign(list.size() * size_t(mc), 1);  // (run_exact's host_finite: unused until collected)
+  const int rc = run_exact<T>(ctx, ds, prog, nullptr, 0, list.data(), int64_t(list.size()), mc, jl_ranges_cached(ds->n),
+                              nullptr, ctx->spec_ok.data(), 0, ctx->stream3, false, &ctx->spec_fin_off);
+  if (rc != SR_OK) {
+    list.clear();
+    return rc;
+  }
+  ctx->spec_pending = true;
+  return SR_OK;
+}
+
+// Second half: wait for the speculative pass; spec_ok[i] = every checked array of spec_list[i] passes.
+inline int spec_collect(sr_ctx* ctx) {
+  if (!ctx->spec_pending) return SR_OK;
+  ctx->spec_pending = false;
+  SR_HIP_CHECK(hipStreamSynchronize(ctx->stream3));
+  float km = 0.f;
+  if (hipEventElapsedTime(&km, ctx->ev_k0, ctx->ev_k1) == hipSuccess) ctx->exact_kernel_ms += double(km);
+  const uint8_t* v = reinterpret_cast<const uint8_t*>(ctx->h_exact.as<char>() + ctx->spec_fin_off);
+  const size_t n = ctx->spec_list.size(), mc = size_t(ctx->spec_mc);
+  ctx->spec_ok.assign(n, 1);
+  for (size_t i = 0; i < n; ++i)
+    for (size_t k = 0; k < mc; ++k) ctx->spec_ok[i] &= v[i * mc + k];
   return SR_OK;
 }
 
@@ -1843,9 +1967,11 @@ int eval_loss_submit(sr_ctx* ctx, const sr_dataset* ds, int opset_id, const sr_t
   SrProgramBatch<T>& prog = c->prog;
   Grid g;
   ctx->want_host_out = true;
+  ctx->want_spec = views == nullptr && !gather;
   int rc = run_batch<T>(ctx, ds, opset_id, trees, row_idx, n_idx, n_eval, loss_kind, SR_MODE_LOSS, &prog, &g, true,
                         nullptr, views);
   ctx->want_host_out = false;
+  ctx->want_spec = false;
   if (rc != SR_OK) return rc;
   if (nt == 0) return SR_OK;
   hipStream_t s = ctx->stream;
@@ -1881,6 +2007,11 @@ int eval_loss_finish(sr_ctx* ctx, LossCall<T>& c) {
   auto rows_of = [&](int v) -> const int64_t* { return gather ? row_idx + int64_t(v) * n_idx : nullptr; };
   hipStream_t s = ctx->stream;
   int rc = SR_OK;
+  ctx->n_spec_last = ctx->n_spec_used_last = 0;
+  if (!ctx->spec_chunks.empty()) {  // the speculative exact pass starts while the main launches run
+    rc = spec_launch<T>(ctx, ds, prog, nt);
+    if (rc != SR_OK) return rc;
+  }
 
   if (ctx->spin && ctx->outs_on_host) {
     hipError_t e;
@@ -1905,11 +2036,25 @@ int eval_loss_finish(sr_ctx* ctx, LossCall<T>& c) {
   std::vector<uint8_t> list_ok(list.size(), 1);
   ctx->n_exact_last = int64_t(list.size());
   ctx->exact_kernel_ms = 0.0;
+  std::vector<uint8_t> have(list.size(), 0);  // verdicts the speculative pass already holds
+  if (ctx->spec_pending) {
+    rc = spec_collect(ctx);
+    if (rc != SR_OK) return rc;
+    std::vector<int32_t> at_spec(size_t(nt), -1);
+    for (size_t i = 0; i < ctx->spec_list.size(); ++i) at_spec[size_t(ctx->spec_list[i])] = int32_t(i);
+    for (size_t i = 0; i < list.size(); ++i) {
+      const int32_t p = at_spec[size_t(list[i])];
+      if (p < 0) continue;
+      list_ok[i] = ctx->spec_ok[size_t(p)];
+      have[i] = 1;
+      ++ctx->n_spec_used_last;
+    }
+  }
   for (int v = 0; v < n_views && !list.empty(); ++v) {  // (each view's listed trees over its own rows)
     std::vector<int64_t> lv;
     std::vector<size_t> at;
     for (size_t i = 0; i < list.size(); ++i)
-      if (view_of(list[i]) == v) {
+      if (!have[i] && view_of(list[i]) == v) {
         lv.push_back(list[i]);
         at.push_back(i);
       }
@@ -3125,6 +3270,8 @@ int sr_init(int device, sr_ctx** out) {
   if (const char* v = std::getenv("SR_AMD_EXACT_G")) ctx->exact_g = std::atoi(v);
   if (const char* v = std::getenv("SR_AMD_EXACT_W")) ctx->exact_w = std::atoi(v) == 1 ? 1 : 4;
   if (const char* v = std::getenv("SR_AMD_EXACT_LIST_HOST")) ctx->exact_list_host = std::atoi(v) != 0 ? 1 : 0;
+  if (const char* v = std::getenv("SR_AMD_SPEC_EXACT")) ctx->spec_exact = std::atoi(v) != 0 ? 1 : 0;
+  if (const char* v = std::getenv("SR_AMD_SPEC_PRIO")) ctx->spec_prio = std::atoi(v);
   if (const char* v = std::getenv("SR_AMD_PAR_STAGE")) ctx->par_stage = std::atoi(v);
   if (const char* v = std::getenv("SR_AMD_DERIVED")) ctx->derived = std::atoi(v);
   if (const char* v = std::getenv("SR_AMD_MAX_ROW_BLOCKS")) ctx->max_row_blocks = std::max(1, std::atoi(v));
@@ -3140,7 +3287,9 @@ int sr_init(int device, sr_ctx** out) {
   for (int c = 0; c < kMaxChunks; ++c) {
     if (e == hipSuccess) e = hipEventCreate(&ctx->ev_c0[c]);
     if (e == hipSuccess) e = hipEventCreate(&ctx->ev_c1[c]);
+    if (e == hipSuccess) e = hipEventCreateWithFlags(&ctx->ev_pr[c], hipEventDisableTiming);
   }
+  if (e == hipSuccess) e = hipEventCreateWithFlags(&ctx->ev_spec, hipEventDisableTiming);
   for (int b = 0; b < sr_ctx::kGradBuckets; ++b) {
     if (e == hipSuccess) e = hipEventCreate(&ctx->ev_g0[b]);
     if (e == hipSuccess) e = hipEventCreate(&ctx->ev_g1[b]);
@@ -3181,6 +3330,7 @@ int sr_init_shared(sr_ctx* parent, sr_ctx** out) {
   c->derived = parent->derived;
   c->probe = parent->probe;
   c->stress_probe = parent->stress_probe;
+  c->spec_exact = parent->spec_exact;
   c->fold_seg = parent->fold_seg;
   c->spin = parent->spin;
   c->h_prog.flags = parent->h_prog.flags;
@@ -3204,11 +3354,16 @@ int sr_shutdown(sr_ctx* ctx) {
                       &ctx->hint, &ctx->jsum_prog, &ctx->jsum_scratch, &ctx->probe_sum, &ctx->probe_flag, &ctx->g_code, &ctx->g_offsets, &ctx->g_consts, &ctx->g_const_off,
                       &ctx->g_items, &ctx->g_part, &ctx->g_out, &ctx->derived_cols, &ctx->probe_derived, &ctx->coll_buf, &ctx->coll_packed, &ctx->ctl, &ctx->fold_io, &ctx->group_cnt})
       b->release();
-    for (HostBuf* b : {&ctx->h_prog, &ctx->h_outs, &ctx->h_grad, &ctx->h_coll, &ctx->h_part, &ctx->h_exact}) b->release();
+    if (ctx->stream3) (void)hipStreamSynchronize(ctx->stream3);
+    for (HostBuf* b : {&ctx->h_prog, &ctx->h_outs, &ctx->h_grad, &ctx->h_coll, &ctx->h_part, &ctx->h_exact, &ctx->h_pflag})
+      b->release();
     for (int c = 0; c < kMaxChunks; ++c) {
       (void)hipEventDestroy(ctx->ev_c0[c]);
       (void)hipEventDestroy(ctx->ev_c1[c]);
+      (void)hipEventDestroy(ctx->ev_pr[c]);
     }
+    (void)hipEventDestroy(ctx->ev_spec);
+    if (ctx->stream3) (void)hipStreamDestroy(ctx->stream3);
     for (int b = 0; b < sr_ctx::kGradBuckets; ++b) {
       (void)hipEventDestroy(ctx->ev_g0[b]);
       (void)hipEventDestroy(ctx->ev_g1[b]);
@@ -3913,6 +4068,10 @@ int sr_set_tuning(sr_ctx* ctx, const char* name, int64_t value) {
     ctx->fold_seg = value < 0 ? -1 : value;
     return SR_OK;
   }
+  if (std::strcmp(name, "spec_exact") == 0) {  // speculative exact-sum pass (SR_AMD_SPEC_EXACT)
+    ctx->spec_exact = value != 0 ? 1 : 0;
+    return SR_OK;
+  }
   if (std::strcmp(name, "exact_w") == 0) {  // waves per workgroup of the EXACT pass (SR_AMD_EXACT_W)
     ctx->exact_w = value == 1 ? 1 : 4;
     return SR_OK;
@@ -3982,6 +4141,13 @@ int sr_tuning_info(sr_ctx* ctx, int* used_derived_columns, int64_t* exact_trees)
   if (check_ctx(ctx) != SR_OK) return SR_ERR_INVALID_ARG;
   if (used_derived_columns) *used_derived_columns = ctx->n_derived_last;
   if (exact_trees) *exact_trees = ctx->n_exact_last;
+  return SR_OK;
+}
+
+int sr_spec_exact_info(sr_ctx* ctx, int64_t* speculated, int64_t* used) {
+  if (check_ctx(ctx) != SR_OK) return SR_ERR_INVALID_ARG;
+  if (speculated) *speculated = ctx->n_spec_last;
+  if (used) *used = ctx->n_spec_used_last;
   return SR_OK;
 }
 

@@ -81,6 +81,14 @@ class DeviceContext:
         _lib.check(_lib.lib.sr_tuning_info(self.handle, None, ctypes.byref(n)))
         return int(n.value)
 
+    def last_spec_exact(self):
+        """(speculated, used) of the last eval_loss call's speculative exact-sum pass: trees the
+        dead-tree probe flagged BIG, passed during the main launch, and those the main launch flagged
+        BIG too (their verdicts taken)."""
+        a, b = ctypes.c_int64(0), ctypes.c_int64(0)
+        _lib.check(_lib.lib.sr_spec_exact_info(self.handle, ctypes.byref(a), ctypes.byref(b)))
+        return int(a.value), int(b.value)
+
     def last_exact_kernel_ms(self):
         """Device time of the last eval_loss call's exact-sum pass (ms)."""
         out = (ctypes.c_double * 7)()

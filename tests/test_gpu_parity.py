@@ -563,6 +563,47 @@ def test_row_sharded_packed_with_exact_path():
     assert np.array_equal(comp, oc)
 
 
+@pytest.mark.parametrize("dtype", [np.float32, np.float64])
+def test_speculative_exact_pass_equals_the_ordinary_one(dtype):
+    """Round 5: trees the dead-tree probe flags BIG over the stress rows go through the exact-sum pass
+    on a third stream during the main launch (tuning "spec_exact").  The results must equal the
+    ordinary after-the-launch pass bit for bit (the main launch's flags decide which verdicts are
+    used), the speculative path must actually have run, and the flags must equal the oracle's."""
+    from test_jsum import cases
+
+    opts = Options(**C2_OPTS)
+    n = 1 << 16
+    X, y = _c2_data(n, seed=93)
+    X, y = X.astype(dtype), y.astype(dtype)
+    big = float(np.finfo(dtype).max)
+    blocks = np.resize(cases()["mixed_overflow_pairwise"], n).astype(np.float64)  # +-2e35 blocks
+    X[2] = (blocks * (big / 3.4028235e38)).astype(dtype)
+    X[4, :30000] = big / 30000 * 1.3  # x5's array sums just past floatmax
+    trees = gen_random_population(600, opts, 5, seed=93)
+    trees += [parse_expression(e, opts) for e in ("x3 * 1.0", "x3 + x1", "x5 * 1.0", "(x5 * 0.5) + (x1 * 1.0)",
+                                                  "cos(x3) + (x5 * 1.0)", "(x3 * x2) - x5")]
+    tb = flatten_trees(trees, dtype)
+    ds = Dataset(X, y)
+    ctx = sr_amd.get_context()
+    try:
+        ctx.set_tuning("probe", 1)  # (a probe before every chunk: this call is below the default's size)
+        ctx.set_tuning("spec_exact", 1)
+        loss_s, comp_s = eval_loss_batch(tb, ds, opts)
+        spec, used = ctx.last_spec_exact()
+        n_exact = ctx.last_exact_trees()
+        ctx.set_tuning("spec_exact", 0)
+        loss_o, comp_o = eval_loss_batch(tb, ds, opts)
+        assert ctx.last_spec_exact() == (0, 0)
+    finally:
+        ctx.set_tuning("probe", 2)
+        ctx.set_tuning("spec_exact", 1)
+    assert spec > 0 and used > 0 and used <= n_exact, (spec, used, n_exact)
+    assert np.array_equal(comp_s, comp_o)
+    assert np.array_equal(loss_s, loss_o, equal_nan=True)
+    _, oc = Oracle.from_options(opts).eval_loss_batch(tb, X, y, n_threads=8)
+    assert np.array_equal(comp_s, oc)
+
+
 def test_wide_f64_dataset_large_view_falls_back_to_classic_kernel():
     """Float64 over >= 2^17 rows defaults to the 8-rows/lane register-stack kernel,
     whose X tile (4096 (nf + 1) bytes) passes 160 KiB at ~40 features; such a call must run the classic
