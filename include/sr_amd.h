@@ -467,8 +467,8 @@ int sr_last_phase_ms(sr_ctx* ctx, double* out, int n);
  * call; Float32 16 / 32 force the register-stack kernel and 4 / 8 the LDS-stack one, Float64 8 / 4
  * likewise), "balance" (0 / 1: deal the cost-ordered trees round-robin over tree groups),
  * "fused_reduce" (the largest tree group, in trees x row blocks, whose partials the interpreter launch
- * reduces itself — its last workgroup per group; 0: always a separate reduce launch), "spec_exact" (1 / 0: the
- * speculative exact-sum pass, sr_spec_exact_info), "exact_w" (4 / 1:
+ * reduces itself — its last workgroup per group; 0: always a separate reduce launch), "spec_exact" (0 / 1: the
+ * speculative exact-sum pass, off by default, sr_spec_exact_info), "exact_w" (4 / 1:
  * waves per workgroup of the exact-sum pass), "exact_g" (listed trees per exact-sum workgroup; 0: the
  * heuristic), "fold_seg" (rows per segment of the in-order loss fold: -1 automatic, 0 one workgroup
  * scan over every row per tree, as rounds 3-4).  Results do
@@ -483,7 +483,7 @@ int sr_set_tuning(sr_ctx* ctx, const char* name, int64_t value);
  * work items and rows per lane. */
 int sr_last_grad_info(sr_ctx* ctx, int n, double* kernel_ms, double* flops, int64_t* items, int* rows_per_lane);
 int sr_tuning_info(sr_ctx* ctx, int* used_derived_columns, int64_t* exact_trees);
-/* The last sr_eval_loss_batch's speculative exact-sum pass (tuning "spec_exact", default on): trees the
+/* The last sr_eval_loss_batch's speculative exact-sum pass (tuning "spec_exact", default off): trees the
  * dead-tree probe flagged BIG, whose pass ran during the main launch (`speculated`), and how many of
  * them the main launch flagged BIG too (`used`: their verdicts were taken; the rest of its BIG trees
  * took the pass afterwards).  Verdicts do not depend on it. */

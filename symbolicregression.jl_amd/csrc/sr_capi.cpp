@@ -228,14 +228,17 @@ struct sr_ctx {
   // SR_AMD_EXACT_LIST_HOST (default 1): the pass reads its tree list from the pinned staging buffer
   // (no upload ahead of the kernel); 0 copies it to the device first
   int exact_list_host = 1;
-  // Speculative exact-sum pass (round 5; SR_AMD_SPEC_EXACT / "spec_exact", default 1).  A large
+  // Speculative exact-sum pass (round 5; SR_AMD_SPEC_EXACT / "spec_exact", default 0).  A large
   // one-view LOSS call's dead-tree probe runs its trees over the dataset's stress rows (the extremes of
   // every feature) before the main launch; a tree the probe already flags BIG (and not non-finite) is
   // BIG on the whole view too (the same thresholds over a subset of the rows), so its exact pass starts
   // on a third stream while the main launch runs, instead of after it.  The main launch's flags still
   // decide: a BIG tree the probe missed takes the ordinary pass afterwards, and a speculated tree the
   // main launch finds non-finite or not BIG leaves its verdict unused.  Verdicts are the same either way.
-  int spec_exact = 1;
+  // Off by default: measured neutral on C2's step and -3 % on the tree-sharding share
+  // (profiles/r05_ab_spec_exact.txt), but the pass shares the CUs with the main launch, whose measured
+  // duration (the roofline's denominator) then carries the pass's work.
+  int spec_exact = 0;
   bool want_spec = false;  // set by eval_loss_submit around its run_batch (one full view, no gather)
   hipStream_t stream3 = nullptr;
   // (SR_AMD_SPEC_PRIO: the third stream's priority, -1 the least, 0 normal, 1 the greatest)

@@ -596,7 +596,7 @@ def test_speculative_exact_pass_equals_the_ordinary_one(dtype):
         assert ctx.last_spec_exact() == (0, 0)
     finally:
         ctx.set_tuning("probe", 2)
-        ctx.set_tuning("spec_exact", 1)
+        ctx.set_tuning("spec_exact", 0)
     assert spec > 0 and used > 0 and used <= n_exact, (spec, used, n_exact)
     assert np.array_equal(comp_s, comp_o)
     assert np.array_equal(loss_s, loss_o, equal_nan=True)
