@@ -40,15 +40,23 @@ def run(expr, reps=10000):
     return float(np.median(ks)), bool(c.all())
 
 
-for label, u in (("arith", None), ("cos", "cos"), ("exp", "exp"), ("log", "log")):
+for label, u in (("arith", None), ("cos", "cos"), ("exp", "exp"), ("log", "log"), ("div", "div"), ("logexp", "logexp")):
     for k in (1, 2, 4, 8, 16):
-        if u == "exp" and k > 4:
+        if u in ("exp", "logexp") and k > 4:
             continue
-        e = chain(k, u if u != "exp" else None)
+        e = chain(k, u if u in ("cos", "log") else None)
         if u == "exp":  # exp of a bounded argument: cos inside keeps it finite
             e = "x1"
             for i in range(k):
                 e = f"exp(cos({e} * x{(i % 4) + 2}))"
+        if u == "logexp":  # log of a positive argument: the exp chain above with a log on each level
+            e = "x1"
+            for i in range(k):
+                e = f"log(exp(cos({e} * x{(i % 4) + 2})))"
+        if u == "div":  # x1 / x2 / x3 ...: the Julia-faithful Float32 division (X > 0 almost surely)
+            e = "x1"
+            for i in range(k):
+                e = f"({e} / x{(i % 4) + 2})"
         ms, comp = run(e)
         print(f"{label:6s} k={k:2d} kernel={ms:8.3f}ms  per-tree-row={ms / 10000 / n * 1e12:7.2f}ps complete={comp}  {e[:60]}",
               flush=True)
