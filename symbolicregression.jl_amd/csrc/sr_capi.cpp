@@ -539,7 +539,7 @@ struct ViewSpec {
 // The speculative exact pass's stream (sr_ctx::spec_exact) drained: nothing of an earlier call (its
 // probe-flag copies, a pass an error path left running) may still use h_pflag / h_exact.
 inline void spec_drain(sr_ctx* ctx) {
-  if (ctx->stream3 && (ctx->spec_pending || !ctx->spec_chunks.empty())) (void)hipStreamSynchronize(ctx->stream3);
+  if (ctx->stream3) (void)hipStreamSynchronize(ctx->stream3);  // (only contexts that ever speculated have one)
   ctx->spec_pending = false;
   ctx->spec_chunks.clear();
 }
