@@ -5,6 +5,8 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path[:0] = [os.path.join(ROOT, os.environ["SR_AMD_PKG"]) if os.environ.get("SR_AMD_PKG")
                 else os.path.join(ROOT, "symbolicregression.jl_amd")]
 import numpy as np
+import hashlib  # noqa: E402
+
 import sr_amd
 from sr_amd import Options, Dataset, flatten_trees, gen_random_population, eval_loss_batch
 
@@ -53,5 +55,6 @@ for name, kw in mixes.items():
           f"kernel={k:7.3f}ms step={t:7.3f}ms  {ne / k / 1e9:8.1f} Gnode/s(kernel)  {ne / t / 1e9:8.1f} Gnode/s(step)"
           f"  phases(compile/launch/wait/exact/final)=" + "/".join(f"{v:.2f}" for v in np.median(np.array(ph), 0))
           + f"  derived={ctx.last_derived_columns()} exact_trees={ctx.last_exact_trees()}"
-          f" exact_kernel={ctx.last_exact_kernel_ms():.3f}ms",
+          f" exact_kernel={ctx.last_exact_kernel_ms():.3f}ms"
+          f"  results={hashlib.sha1(np.ascontiguousarray(l).tobytes() + np.ascontiguousarray(c).tobytes()).hexdigest()[:12]}",
           flush=True)
