@@ -386,8 +386,99 @@ def main():
         }
         line.update(subs)
         line.update(extra)
-        print(json.dumps(line), flush=True)
+        print(json.dumps(compact_line(line)), flush=True)
     comm.close()
+
+
+# keys of the printed line's sub-objects kept inline; everything else (held-tree expressions, per-bucket
+# gradient tables, projection internals, phase breakdowns) goes to the detail file only.  Round 5's
+# 20.9 KB line was not parsed by the driver: the printed line stays well under 12 KB.
+_KEEP = {
+    "roofline": ("bound", "achieved", "peak", "unit", "frac", "traffic", "kernel_ms_per_step", "busy_ms_per_step",
+                 "flops_per_step", "kernel", "algorithmic_bytes_per_step", "algorithmic_GBps", "launches_per_step",
+                 "n_trees", "ms_per_step", "node_evals_per_s", "hbm_GBps", "kernel_sum_ms_per_step",
+                 "fraction_complete"),
+    "parity": ("trees", "rows", "complete", "flags_bit_exact", "flag_mismatches", "max_rel_vs_f64_accum",
+               "median_rel_vs_f64_accum", "n_held_to_libm_spread_bar", "loss_failures_vs_f64_accum",
+               "max_rel_vs_ref_f32_fold", "median_rel_vs_ref_f32_fold", "n_bit_exact_vs_ref_f32_fold",
+               "loss_failures_vs_ref_fold", "ref_fold_inf_trees", "ref_fold_inf_mismatches", "accumulation", "pass",
+               "max_rel", "median_rel", "loss_failures", "cpu_s"),
+}
+
+
+def _pick(d, keys):
+    return {k: d[k] for k in keys if isinstance(d, dict) and k in d}
+
+
+def compact_line(line):
+    """The printed JSON line: the contract's keys and each sub-object's headline numbers.  The full line
+    (every held tree, gradient bucket and projection input) is written to the detail file
+    (SR_BENCH_DETAIL, default gpurun_out/bench_detail.json) and named in the line."""
+    path = os.environ.get("SR_BENCH_DETAIL", os.path.join(ROOT, "gpurun_out", "bench_detail.json"))
+    try:
+        os.makedirs(os.path.dirname(path), exist_ok=True)
+        with open(path, "w") as f:
+            json.dump(line, f)
+    except OSError:
+        path = None
+    out = {k: v for k, v in line.items()
+           if k not in ("roofline", "parity", "search", "c4", "tree_sharded", "c2_sharded_path", "f64",
+                        "roofline_complete_only", "config")}
+    cfg = dict(line.get("config") or {})
+    out["config"] = cfg
+    out["roofline"] = _pick(line.get("roofline") or {}, _KEEP["roofline"])
+    par = line.get("parity")
+    out["parity"] = _pick(par, _KEEP["parity"]) if par else par
+    if "roofline_complete_only" in line:
+        out["roofline_complete_only"] = _pick(line["roofline_complete_only"], _KEEP["roofline"])
+    if "f64" in line:
+        f = line["f64"]
+        out["f64"] = dict(_pick(f, _KEEP["roofline"]), parity=_pick(f.get("parity") or {}, _KEEP["parity"]))
+    if "c2_sharded_path" in line:
+        out["c2_sharded_path"] = _pick(line["c2_sharded_path"], ("ms_per_step", "value", "kernel_ms_per_step"))
+    if "tree_sharded" in line:
+        t = line["tree_sharded"]
+        out["tree_sharded"] = _pick(t, ("value", "unit", "ms_per_step", "scaling", "n_gpus", "equals_single_gpu",
+                                        "single_call_ms_per_step", "overhead_vs_single_call"))
+        for k in ("projection_8_ranks", "projection_8_ranks_100k_trees"):
+            if k in t:
+                out["tree_sharded"][k] = _pick(t[k], ("rank0_share_ms", "single_call_ms", "efficiency_excluding_allgather"))
+    if "c4" in line:
+        c = line["c4"]
+        o = _pick(c, ("value", "unit", "ms_per_step", "steps", "n_gpus", "scaling", "rows_per_gpu", "n_trees",
+                      "fraction_complete", "skipped"))
+        if "roofline" in c:
+            o["roofline"] = _pick(c["roofline"], _KEEP["roofline"])
+        lp = c.get("last_step_passes") or {}
+        o["passes"] = _pick(lp, ("exact_trees", "fold_trees", "ref_fold_trees", "fold_segments_row_by_row"))
+        if "projection_8_ranks" in c:
+            o["projection_8_ranks"] = _pick(c["projection_8_ranks"], ("projected_ms_per_step", "efficiency"))
+        if "parity" in c:
+            p = c["parity"]
+            o["parity"] = {"pass": p.get("pass"), "rows": p.get("rows")}
+            for k in ("sample", "planted_big"):
+                if k in p:
+                    o["parity"][k] = _pick(p[k], ("trees", "complete", "flag_mismatches", "ref_fold_inf_mismatches",
+                                                  "max_rel_vs_f64_accum", "n_held_to_libm_spread_bar",
+                                                  "loss_failures", "n_bit_exact_vs_ref_f32_fold"))
+        out["c4"] = o
+    if line.get("search"):
+        s = {}
+        for name, v in line["search"].items():
+            o = _pick(v, ("value", "unit", "iterations_per_s", "islands", "wall_s", "device_calls",
+                          "device_wall_per_call_us", "kernel_busy_per_call_us", "best_loss"))
+            if "cpu_baseline" in v:
+                o["cpu_baseline"] = _pick(v["cpu_baseline"], ("value", "unit", "iterations_per_s", "cores", "kind"))
+            if "grad_roofline" in v:
+                o["grad_roofline"] = _pick(v["grad_roofline"], ("achieved", "peak", "unit", "frac", "kernel_ms_per_call"))
+            if "projection_8_ranks" in v:
+                pr = v["projection_8_ranks"]
+                o["projection_8_ranks"] = dict(_pick(pr, ("speedup", "efficiency")),
+                                               weak_efficiency=(pr.get("weak_scaling") or {}).get("efficiency"))
+            s[name] = o
+        out["search"] = s
+    out["detail_file"] = os.path.relpath(path, ROOT) if path else None
+    return out
 
 
 def sharded_path_line(ctx, tb, ds, opts, eval_loss_sharded, args, comm, nodes, rows):

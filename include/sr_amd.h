@@ -471,8 +471,13 @@ int sr_last_phase_ms(sr_ctx* ctx, double* out, int n);
  * speculative exact-sum pass, off by default, sr_spec_exact_info), "exact_w" (4 / 1:
  * waves per workgroup of the exact-sum pass), "exact_g" (listed trees per exact-sum workgroup; 0: the
  * heuristic), "fold_seg" (rows per segment of the in-order loss fold: -1 automatic, 0 one workgroup
- * scan over every row per tree, as rounds 3-4).  Results do
- * not depend on any knob.  SR_ERR_INVALID_ARG for an unknown name.  sr_tuning_info (optional outputs)
+ * scan over every row per tree, as rounds 3-4), "ref_fold" (1, the default: every complete tree's loss
+ * is the reference's in-order fold in T of its elementwise losses (src/LossFunctions.jl:38-58), divided
+ * in T; 0: the f64 sum of rounds 1-5, whose last bits — ~5e-4 relative at 2^20 rows in Float32 —
+ * differ), "fold_store_mb" / "fold_slot_mb" (the fold's stored-loss and slow-segment budgets),
+ * "fold_delta_log2" (the fold plan's window).  Results do not depend on any knob but two: "ref_fold",
+ * and — with "ref_fold" 0 only — "max_row_blocks", which sets how many f64 partials a tree's sum adds
+ * (the last bit of a loss may differ).  SR_ERR_INVALID_ARG for an unknown name.  sr_tuning_info (optional outputs)
  * reports how many derived columns the last sr_eval_loss_batch used and how many of its trees went
  * through the exact-sum pass (flagged BIG). */
 int sr_set_tuning(sr_ctx* ctx, const char* name, int64_t value);
@@ -488,6 +493,13 @@ int sr_tuning_info(sr_ctx* ctx, int* used_derived_columns, int64_t* exact_trees)
  * them the main launch flagged BIG too (`used`: their verdicts were taken; the rest of its BIG trees
  * took the pass afterwards).  Verdicts do not depend on it. */
 int sr_spec_exact_info(sr_ctx* ctx, int64_t* speculated, int64_t* used);
+/* The last sr_eval_loss_batch(_views)'s in-order loss fold (tuning "ref_fold"; each output may be NULL):
+ * the path (0 none — "ref_fold" 0, negative weights, a row-sharded call, or a Float64 call too large
+ * to keep its losses; 1 the loss launch kept every tree's losses; 2 the FOLD-mode pass re-ran the
+ * complete trees), the trees whose loss is the walk's exact fold, those whose walk left the plan's
+ * window and were folded through the prediction pass instead, and the fold launches' device time (ms,
+ * HIP events; 0 with "timing" off). */
+int sr_ref_fold_info(sr_ctx* ctx, int* path, int64_t* n_folded, int64_t* n_fallback, double* fold_kernel_ms);
 
 #ifdef __cplusplus
 }

@@ -7,6 +7,7 @@
 
 #include "sr_eval.h"
 #include "sr_fold.h"
+#include "sr_fold_dev.h"
 
 
 // The result goes to the caller's tree index perm[position].  One wave per tree: lane l folds row blocks l, l + 64, ... in order, then a fixed butterfly adds the
@@ -150,35 +151,6 @@ template hipError_t sr_launch_finalize_packed<double>(const double*, int, double
 // the segmentation (seg_len = 0: the whole view through fold_range, rounds 3-4's kernel;
 // tests/test_gpu_fold.py compares both bit for bit).
 template <typename T>
-struct SrFoldStep {
-  int64_t m;
-  int kind;  // 0: f < 1/2, 1: f == 1/2 (tie), 2: f > 1/2
-};
-
-template <typename T>
-__device__ __forceinline__ SrFoldStep<T> sr_fold_step(T e, int q, int64_t cap) {
-  SrFoldStep<T> st{cap, 0};
-  const double t = ldexp(double(e), -q);  // exact: a power-of-two scaling of a T value
-  if (!(t < double(cap))) return st;      // (also NaN / Inf: a crossing, taken by the hardware add)
-  const double fl = floor(t);
-  const double f = t - fl;
-  st.m = int64_t(fl);
-  st.kind = f > 0.5 ? 2 : (f == 0.5 ? 1 : 0);
-  return st;
-}
-template <typename T>
-__device__ __forceinline__ int64_t sr_fold_inc(const SrFoldStep<T>& st, int64_t b) {
-  return st.m + (st.kind == 2 ? 1 : (st.kind == 1 ? ((b + st.m) & 1) : 0));
-}
-// (a0, a1): ulps added from an even / odd start; y := x then y (saturating at cap)
-__device__ __forceinline__ void sr_fold_compose(int64_t x0, int64_t x1, int64_t& y0, int64_t& y1, int64_t cap) {
-  const int64_t n0 = x0 + ((x0 & 1) ? y1 : y0);
-  const int64_t n1 = x1 + (((1 + x1) & 1) ? y1 : y0);
-  y0 = n0 < cap ? n0 : cap;
-  y1 = n1 < cap ? n1 : cap;
-}
-
-template <typename T>
 struct SrFoldRows {  // the listed tree's elementwise losses (the interpreter's product, in the same order)
   const T* pr;
   const T* y;
@@ -228,19 +200,6 @@ struct SrFoldRows {  // the listed tree's elementwise losses (the interpreter's 
   }
 };
 
-// binade spacing exponent q of a value >= 0 (subnormals and 0: the fixed subnormal spacing); values
-// past the type's range get a q no finite running value has
-template <typename T>
-__device__ __forceinline__ int sr_fold_q(double x) {
-  using Tr = SrFoldTraits<T>;
-  constexpr double MIN_NORMAL = sizeof(T) == 4 ? 1.17549435e-38 : 2.2250738585072014e-308;
-  if (!(x >= MIN_NORMAL)) return Tr::qmin;
-  if (!(x <= double(SrM<T>::big))) return 1 << 20;
-  int ex;
-  (void)frexp(x, &ex);
-  return ex - 1 - Tr::mant;
-}
-
 template <typename T>
 __global__ void __launch_bounds__(256) sr_fold_segsum_kernel(SrFoldRows<T> rows, int64_t pred_ld, int64_t n,
                                                              int64_t seg_len, int n_seg, double* __restrict__ segsum) {
@@ -255,53 +214,6 @@ __global__ void __launch_bounds__(256) sr_fold_segsum_kernel(SrFoldRows<T> rows,
   if ((tid & 63) == 0) s_w[tid >> 6] = acc;
   __syncthreads();
   if (tid == 0) segsum[int64_t(b) * n_seg + seg] = (s_w[0] + s_w[1]) + (s_w[2] + s_w[3]);
-}
-
-// The step of one loss for the segment tables, in the narrowest exact arithmetic: Float32 losses in
-// Float32 (e 2^-q is exact but for an underflow, which only ever hides a fraction below 1/2; the
-// saturation CAP = 2^26 keeps the counts in int32), Float64 losses in Float64 / int64.
-template <typename T>
-struct SrFoldTab;
-template <>
-struct SrFoldTab<float> {
-  using I = int32_t;
-  static __device__ __forceinline__ void step(float e, int q, I& m, int& kind) {
-    constexpr float CAPF = float(1 << 26);
-    const float t = ldexpf(e, -q);
-    if (!(t < CAPF)) {  // (also NaN / Inf)
-      m = I(1) << 26;
-      kind = 0;
-      return;
-    }
-    const float fl = floorf(t);
-    const float f = t - fl;
-    m = I(fl);
-    kind = f > 0.5f ? 2 : (f == 0.5f ? 1 : 0);
-  }
-};
-template <>
-struct SrFoldTab<double> {
-  using I = int64_t;
-  static __device__ __forceinline__ void step(double e, int q, I& m, int& kind) {
-    const SrFoldStep<double> st = sr_fold_step<double>(e, q, int64_t(1) << 55);
-    m = st.m;
-    kind = st.kind;
-  }
-};
-template <typename I>
-__device__ __forceinline__ void sr_fold_compose_i(I x0, I x1, I& y0, I& y1, I cap) {
-  const I n0 = x0 + ((x0 & 1) ? y1 : y0);
-  const I n1 = x1 + (((1 + x1) & 1) ? y1 : y0);
-  y0 = n0 < cap ? n0 : cap;
-  y1 = n1 < cap ? n1 : cap;
-}
-template <typename I>
-__device__ __forceinline__ void sr_fold_add_i(I m, int kind, I cap, I& a0, I& a1) {
-  // (a0, a1) then the step (m, kind): from start parity b the running value's parity is b + a_b
-  const I e0 = m + (kind == 2 ? 1 : (kind == 1 ? ((a0 + m) & 1) : 0));
-  const I e1 = m + (kind == 2 ? 1 : (kind == 1 ? ((1 + a1 + m) & 1) : 0));
-  a0 = a0 + e0 < cap ? a0 + e0 : cap;
-  a1 = a1 + e1 < cap ? a1 + e1 : cap;
 }
 
 // composed steps of one segment for binades qa and qb: tab[b][seg] = {a0(qa), a1(qa), a0(qb), a1(qb)}
@@ -404,9 +316,8 @@ __global__ void __launch_bounds__(256) sr_fold_segtab_kernel(SrFoldRows<T> rows,
 
 // The workgroup scan of rounds 3-4 over rows [s_k, hi) from the running value s_p (every thread
 // calls it; the state lives in LDS): CHUNK rows per round, restarting at each binade crossing.
-template <typename T, int R>
-__device__ void sr_fold_range(const SrFoldRows<T>& elem, int64_t hi, T* s_p, int64_t* s_k, int64_t* s_w0,
-                              int64_t* s_w1) {
+template <typename T, int R, typename Rows>
+__device__ void sr_fold_range(const Rows& elem, int64_t hi, T* s_p, int64_t* s_k, int64_t* s_w0, int64_t* s_w1) {
   using Tr = SrFoldTraits<T>;
   constexpr int NT = 1024;
   constexpr int64_t CHUNK = int64_t(NT) * R;
@@ -649,6 +560,474 @@ template hipError_t sr_launch_fold<double>(const double*, int64_t, int, const do
                                            int64_t, int, double, int64_t, const int2*, const int64_t*, const double*,
                                            double*, int*, hipStream_t);
 
+// ---------------------------------------------------------------- every complete tree's fold (round 6)
+// The reference's loss of a complete tree IS the in-order fold in T (LossFunctions.jl:38-58), not the
+// f64 sum (at 2^20 rows the two differ by ~5e-4 relative, past north_star's 1e-4).  The call's loss
+// launch already leaves one f64 partial per (row block, tree); a row block is a fold segment:
+//   plan   the f64 prefix before and after each segment (from those partials) brackets the fold's value
+//          there within a relative window delta; a segment whose window lies in ONE binade gets that
+//          binade's composed step (code q), the first segment and every segment whose window meets a
+//          binade edge are slow (their losses are kept, code SLOT0 + slot);
+//   steps  small calls: the loss launch stored every tree's losses, and sr_fold_stab_kernel composes
+//          each segment's steps from them; large calls: the interpreter runs the complete trees again in
+//          FOLD mode (sr_tile_impl.h), composing each tile's steps in registers and storing only the slow
+//          segments' losses (plan: sr_fold_plan_kernel, slots from a call-wide counter);
+//   walk   one workgroup per tree walks the segments in order: a steps segment advances in O(1) when
+//          the running value is in its binade and stays there, a slow one is folded row by row by the
+//          workgroup scan (sr_fold_range); anything else fails the tree (SR_FST_FAIL), which the host
+//          folds through the prediction pass instead (fold_exact).
+// Every O(1) advance is an exact composition, so the result is the reference's fold bit for bit whatever
+// the window; delta only trades slow segments against failures.
+
+// A segment's stored losses (the loss launch's store or a FOLD slot): row i of the view at base[i - lo].
+template <typename T>
+struct SrStoredRows {
+  const T* base;
+  int64_t lo;
+  __device__ __forceinline__ T operator()(int64_t i) const { return base[i - lo]; }
+  template <int R>
+  __device__ __forceinline__ void rows_from(int64_t r0, int64_t hi, T (&ev)[R]) const {
+    constexpr int C = 16 / int(sizeof(T));
+    using V = typename std::conditional<sizeof(T) == 4, float4, double2>::type;
+    const T* p = base + (r0 - lo);
+    if (r0 + R <= hi && (reinterpret_cast<uintptr_t>(p) & 15u) == 0) {
+#pragma unroll
+      for (int c = 0; c < R / C; ++c) {
+        const V v = *reinterpret_cast<const V*>(p + c * C);
+#pragma unroll
+        for (int j = 0; j < C; ++j) ev[c * C + j] = reinterpret_cast<const T*>(&v)[j];
+      }
+    } else {
+#pragma unroll
+      for (int r = 0; r < R; ++r) ev[r] = (r0 + r < hi) ? p[r] : T(0);
+    }
+  }
+};
+
+// Large calls: one wave per launch position; codes [rb][np] (slots of the FOLD mode's slow segments
+// from the call's counter; past slot_cap a slow segment gets SKIP, which fails its tree in the walk).
+template <typename T>
+__global__ void __launch_bounds__(256) sr_fold_plan_kernel(const double* __restrict__ part, int np, int n_rb,
+                                                           const uint32_t* __restrict__ perm, SrFoldWho who,
+                                                           double delta, int32_t* __restrict__ code,
+                                                           int* __restrict__ slot_next, int slot_cap) {
+  const int lane = int(threadIdx.x) & 63;
+  const int p = int(blockIdx.x) * 4 + int(threadIdx.x) / 64;
+  if (p >= np) return;  // wave-uniform
+  const uint32_t t = perm ? perm[p] : uint32_t(p);
+  const bool ok = who.eligible<T>(t);
+  double run = who.est ? who.est[t] : 0.0;  // (a row shard after the first: the shards before it)
+  for (int c0 = 0; c0 < n_rb; c0 += 64) {
+    const int rb = c0 + lane;
+    const bool in = rb < n_rb;
+    // (one row block: its sum is the tree's total on this view)
+    const double v = !(ok && in) ? 0.0 : (part ? part[size_t(rb) * size_t(np) + size_t(p)] : who.sums[t]);
+    double inc = v;
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+      const double o = __shfl_up(inc, off, 64);
+      if (lane >= off) inc += o;
+    }
+    const double sb = run + (inc - v), sa = run + inc;  // (estimates: they only choose binades)
+    run += __shfl(inc, 63, 64);
+    int32_t cd = SR_FCODE_SKIP;
+    bool slow = false;
+    if (ok && in) {
+      const int qa = sr_fold_q<T>(sb * (1.0 - delta));
+      slow = (rb == 0 && who.first) || qa != sr_fold_q<T>(sa * (1.0 + delta));
+      cd = qa;
+    }
+    const uint64_t sm = __builtin_amdgcn_ballot_w64(slow);
+    if (sm) {
+      int base = 0;
+      if (lane == 0) base = atomicAdd(slot_next, __popcll(sm));
+      base = __shfl(base, 0, 64);
+      const int k = base + __popcll(sm & ((uint64_t(1) << lane) - 1u));
+      if (slow) cd = k < slot_cap ? SR_FCODE_SLOT0 + k : SR_FCODE_SKIP;
+    }
+    if (in) code[size_t(rb) * size_t(np) + size_t(p)] = cd;
+  }
+}
+
+// Small calls: the loss launch stored every position's losses ([position][pos_stride], pos_stride =
+// n_rb x rb_rows, so segment rb of position p is slot p n_rb + rb); one workgroup per (segment,
+// position) decides its code and composes a steps segment's pair in row order.
+template <typename T, int R>
+__global__ void __launch_bounds__(256) sr_fold_stab_kernel(const double* __restrict__ part, int np, int n_rb,
+                                                           int64_t rb_rows, int64_t n, const uint32_t* __restrict__ perm,
+                                                           SrFoldWho who, double delta, const T* __restrict__ losses,
+                                                           int32_t* __restrict__ code,
+                                                           typename SrFoldTab<T>::Pair* __restrict__ tab) {
+  using I = typename SrFoldTab<T>::I;
+  constexpr I CAP = I(1) << (SrFoldTraits<T>::mant + 3);
+  const int rb = int(blockIdx.x), p = int(blockIdx.y), tid = int(threadIdx.x), lane = tid & 63, wave = tid >> 6;
+  const uint32_t t = perm ? perm[p] : uint32_t(p);
+  const size_t o = size_t(rb) * size_t(np) + size_t(p);
+  if (!who.eligible<T>(t)) {
+    if (tid == 0) code[o] = SR_FCODE_SKIP;
+    return;
+  }
+  const int32_t slow_code = SR_FCODE_SLOT0 + p * n_rb + rb;
+  if (rb == 0 && who.first) {
+    if (tid == 0) code[o] = slow_code;
+    return;
+  }
+  __shared__ double s_d[4];
+  __shared__ I s_v[4][2];
+  double pre = 0.0;
+  for (int i = tid; i < rb; i += 256) pre += part[size_t(i) * size_t(np) + size_t(p)];  // (rb > 0: part is set)
+#pragma unroll
+  for (int off = 32; off >= 1; off >>= 1) pre += __shfl_xor(pre, off, 64);
+  if (lane == 0) s_d[wave] = pre;
+  __syncthreads();
+  const double sb = (who.est ? who.est[t] : 0.0) + ((s_d[0] + s_d[1]) + (s_d[2] + s_d[3]));
+  const double sa = sb + (part ? part[o] : who.sums[t]);  // (one row block: the view's total)
+  const int q = sr_fold_q<T>(sb * (1.0 - delta));
+  if (q != sr_fold_q<T>(sa * (1.0 + delta))) {
+    if (tid == 0) code[o] = slow_code;
+    return;
+  }
+  const int64_t lo = int64_t(rb) * rb_rows, hi = lo + rb_rows < n ? lo + rb_rows : n;
+  const SrStoredRows<T> rw{losses + (size_t(p) * size_t(n_rb) + size_t(rb)) * size_t(rb_rows), lo};
+  I ta0 = 0, ta1 = 0;  // the segment so far (thread 0)
+  for (int64_t base = lo; base < hi; base += 256 * R) {
+    I a0 = 0, a1 = 0;
+    const int64_t r0 = base + int64_t(tid) * R;
+    T ev[R];
+    rw.template rows_from<R>(r0, hi, ev);
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+      I m;
+      int kind;
+      SrFoldTab<T>::step(ev[r], q, m, kind);
+      sr_fold_add_i<I>(m, kind, CAP, a0, a1);
+    }
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {  // ordered over the lanes, then the waves
+      I o0 = __shfl_down(a0, off, 64), o1 = __shfl_down(a1, off, 64);
+      if ((lane & (2 * off - 1)) == 0) {
+        sr_fold_compose_i<I>(a0, a1, o0, o1, CAP);
+        a0 = o0;
+        a1 = o1;
+      }
+    }
+    if (lane == 0) {
+      s_v[wave][0] = a0;
+      s_v[wave][1] = a1;
+    }
+    __syncthreads();
+    if (tid == 0) {
+      for (int v = 0; v < 4; ++v) {
+        I y0 = s_v[v][0], y1 = s_v[v][1];
+        sr_fold_compose_i<I>(ta0, ta1, y0, y1, CAP);
+        ta0 = y0;
+        ta1 = y1;
+      }
+    }
+    __syncthreads();
+  }
+  if (tid == 0) {
+    tab[o] = SrFoldTab<T>::pair(ta0, ta1);
+    code[o] = q;
+  }
+}
+
+// One wave folds rows [k, hi) of a slow segment into F exactly (row i's loss at base[i - lo]), 64 x RW
+// rows per load: each lane holds RW consecutive rows.  Per round, under the binade of F: every row's
+// step, each lane's composition, an ordered inclusive scan over the lanes; a round that leaves the
+// binade ends at the first row whose step reaches it (that lane re-walks its rows from its exclusive
+// prefix), the hardware add takes that row, and the next round continues in the SAME registers from the
+// row after it (rows before k are identity steps) until the load is used up.  Fast path (no row of the
+// round at an exact half ulp): every step is rint(l 2^-q) whatever the parity, so the compositions are
+// plain sums; otherwise the pair composition (sr_fold_add_i / sr_fold_compose_i).
+template <typename T, int RW>
+__device__ T sr_fold_rows_wave(const T* __restrict__ base, int64_t lo, int64_t k, int64_t hi, T F, int lane) {
+  using Tr = SrFoldTraits<T>;
+  using I = typename SrFoldTab<T>::I;
+  constexpr I CAP = I(1) << (Tr::mant + 3);
+  constexpr T CLAMP = T(int64_t(1) << (Tr::mant + 2));
+  constexpr int C = 16 / int(sizeof(T));
+  using V = typename std::conditional<sizeof(T) == 4, float4, double2>::type;
+  constexpr T MIN_NORMAL = sizeof(T) == 4 ? T(1.17549435e-38f) : T(2.2250738585072014e-308);
+  while (k < hi) {
+    const int64_t b0 = k - ((k - lo) % C);  // (16-byte aligned runs of the segment's storage)
+    const int64_t r0 = b0 + int64_t(lane) * RW;
+    const int64_t pass_end = b0 + int64_t(64) * RW;
+    T ev[RW];
+#pragma unroll
+    for (int c = 0; c < RW / C; ++c) {
+      const int64_t rc = r0 + c * C;
+      if (rc < hi) {
+        const V v = *reinterpret_cast<const V*>(base + (rc - lo));
+#pragma unroll
+        for (int j = 0; j < C; ++j) ev[c * C + j] = (rc + j < hi) ? reinterpret_cast<const T*>(&v)[j] : T(0);
+      } else {
+#pragma unroll
+        for (int j = 0; j < C; ++j) ev[c * C + j] = T(0);
+      }
+    }
+    while (k < hi && k < pass_end) {
+      if (!(F <= SrM<T>::big)) return F;  // +Inf / NaN stays
+      int q;
+      I lim;
+      if (F < MIN_NORMAL) {
+        q = Tr::qmin;
+        lim = I(1) << Tr::mant;
+      } else {
+        int ex;
+        (void)frexp(double(F), &ex);
+        q = ex - 1 - Tr::mant;
+        lim = I(1) << (Tr::mant + 1);
+      }
+      const I P = I(ldexp(double(F), -q));
+      const bool odd = (P & 1) != 0;
+      // fast path: the round's steps are rint(l 2^-q) unless some row is an exact half
+      T sr[RW];
+      T lsum = T(0), dmax = T(0);
+#pragma unroll
+      for (int r = 0; r < RW; ++r) {
+        const T e = (r0 + r >= k) ? ev[r] : T(0);
+        const T v = sizeof(T) == 4 ? T(ldexpf(float(e), -q)) : T(ldexp(double(e), -q));
+        T st = sizeof(T) == 4 ? T(rintf(float(v))) : T(rint(double(v)));
+        const T d = v - st;
+        const T ad = d < T(0) ? -d : d;
+        dmax = ad > dmax ? ad : dmax;
+        st = st < CLAMP ? st : CLAMP;  // (also NaN: the clamp)
+        sr[r] = st;
+        lsum += st;
+      }
+      I i0, i1, x0, x1;  // inclusive / exclusive prefixes over the lanes, from an even and an odd start
+      const bool fast = __builtin_amdgcn_ballot_w64(dmax == T(0.5)) == 0;
+      if (fast) {
+        I a = lsum < T(CAP) ? I(lsum) : CAP;
+        I inc = a;
+#pragma unroll
+        for (int off = 1; off < 64; off <<= 1) {
+          const I o = __shfl_up(inc, off, 64);
+          if (lane >= off) inc = inc + o < CAP ? inc + o : CAP;
+        }
+        i0 = i1 = inc;
+        x0 = x1 = inc - a;
+      } else {
+        I a0 = 0, a1 = 0;
+#pragma unroll
+        for (int r = 0; r < RW; ++r) {
+          I m;
+          int kind;
+          SrFoldTab<T>::step((r0 + r >= k) ? ev[r] : T(0), q, m, kind);
+          sr_fold_add_i<I>(m, kind, CAP, a0, a1);
+        }
+        i0 = a0;
+        i1 = a1;
+#pragma unroll
+        for (int off = 1; off < 64; off <<= 1) {
+          const I l0 = __shfl_up(i0, off, 64), l1 = __shfl_up(i1, off, 64);
+          if (lane >= off) sr_fold_compose_i<I>(l0, l1, i0, i1, CAP);
+        }
+        x0 = __shfl_up(i0, 1, 64);
+        x1 = __shfl_up(i1, 1, 64);
+        if (lane == 0) x0 = x1 = 0;
+      }
+      const I inc = P + (odd ? i1 : i0);
+      const uint64_t cross = __builtin_amdgcn_ballot_w64(inc >= lim);
+      if (cross == 0) {  // the rest of this load stays in the binade
+        F = T(ldexp(double(__shfl(inc, 63, 64)), q));
+        k = pass_end;
+        break;
+      }
+      const int cl = __builtin_ctzll(cross);  // the lane whose rows leave the binade
+      T nF = T(0);
+      int64_t nk = 0;
+      if (lane == cl) {
+        I run = P + (odd ? x1 : x0);
+        bool done = false;
+#pragma unroll
+        for (int r = 0; r < RW; ++r) {
+          const T e = (r0 + r >= k) ? ev[r] : T(0);
+          I d;
+          if (fast) {
+            d = I(sr[r]);
+          } else {
+            I m;
+            int kind;
+            SrFoldTab<T>::step(e, q, m, kind);
+            d = m + (kind == 2 ? 1 : (kind == 1 ? ((run + m) & 1) : 0));
+          }
+          if (!done && run + d >= lim) {
+            nF = T(ldexp(double(run), q)) + e;  // the hardware's own rounding of this step
+            nk = r0 + r + 1;
+            done = true;
+          }
+          if (!done) run += d;
+        }
+      }
+      F = __shfl(nF, cl, 64);
+      k = __shfl(nk, cl, 64);
+    }
+  }
+  return F;
+}
+
+// The walk: one wave per launch position (4 per workgroup), its segments in row order, 64 at a time.
+// Between two slow segments the steps segments share one binade (adjacent windows cannot straddle
+// apart), so each such run is ONE composition — a segmented ordered scan of the chunk's pairs over the
+// lanes — checked against the running value once: its binade must be the run's and the run must end
+// inside it.  A slow segment is folded by sr_fold_rows_wave.  Anything else fails the tree.  carry (at
+// the caller's tree index): the fold's value before this view's first row (a row shard after the
+// first), or NULL: the first loss starts the fold.  out_val / out_st at the caller's tree index.
+template <typename T, int RW>
+__global__ void __launch_bounds__(256) sr_fold_walk_kernel(const int32_t* __restrict__ code,
+                                                           const typename SrFoldTab<T>::Pair* __restrict__ tab, int np,
+                                                           int n_rb, int64_t rb_rows, int64_t n,
+                                                           const T* __restrict__ losses, int64_t slot_rows,
+                                                           const uint32_t* __restrict__ perm,
+                                                           const T* __restrict__ carry, T* __restrict__ out_val,
+                                                           int32_t* __restrict__ out_st) {
+  using Tr = SrFoldTraits<T>;
+  using I = typename SrFoldTab<T>::I;
+  constexpr I CAP = I(1) << (Tr::mant + 3);
+  constexpr T MIN_NORMAL = sizeof(T) == 4 ? T(1.17549435e-38f) : T(2.2250738585072014e-308);
+  const int lane = int(threadIdx.x) & 63;
+  const int p = int(blockIdx.x) * 4 + int(threadIdx.x) / 64;
+  if (p >= np) return;  // wave-uniform
+  const uint32_t t = perm ? perm[p] : uint32_t(p);
+  const int32_t c_first = code[p];
+  if (c_first == SR_FCODE_SKIP) {
+    if (lane == 0) out_st[t] = SR_FST_NONE;
+    return;
+  }
+  auto seg_base = [&](int32_t c) { return losses + size_t(c - SR_FCODE_SLOT0) * size_t(slot_rows); };
+  bool fail = false;
+  T F = T(0);
+  int64_t k = 0;
+  if (carry) {
+    F = carry[t];
+  } else if (c_first >= SR_FCODE_SLOT0 && n > 0) {  // Statistics.mean / Base.sum over a generator: the
+    F = seg_base(c_first)[0];                       // first loss starts the fold
+    k = 1;
+  } else {
+    fail = n > 0;  // (the plan keeps the first segment's losses)
+  }
+  for (int c0 = 0; c0 < n_rb && !fail; c0 += 64) {
+    const int sg = c0 + lane;
+    const bool in = sg < n_rb;
+    const int32_t cd = in ? code[size_t(sg) * size_t(np) + size_t(p)] : SR_FCODE_SKIP;
+    const bool slow = in && cd >= SR_FCODE_SLOT0;
+    I x0 = 0, x1 = 0;
+    if (in && !slow && cd != SR_FCODE_SKIP) {
+      const auto pr = tab[size_t(sg) * size_t(np) + size_t(p)];
+      x0 = I(pr.x);
+      x1 = I(pr.y);
+    }
+    if (__builtin_amdgcn_ballot_w64(in && cd == SR_FCODE_SKIP)) {  // (a plan out of slots)
+      fail = true;
+      break;
+    }
+    const uint64_t slowm = __builtin_amdgcn_ballot_w64(slow);
+    // segmented inclusive scan: a run starts at the chunk's first lane and after each slow lane
+    bool head = lane == 0 || (lane > 0 && ((slowm >> (lane - 1)) & 1u));
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+      const I l0 = __shfl_up(x0, off, 64), l1 = __shfl_up(x1, off, 64);
+      const bool lh = __shfl_up(int(head), off, 64) != 0;
+      if (lane >= off && !head) {
+        sr_fold_compose_i<I>(l0, l1, x0, x1, CAP);
+        head = lh;
+      }
+    }
+    const int end = n_rb - c0 < 64 ? n_rb - c0 : 64;
+    int pos = 0;
+    while (pos < end && !fail) {
+      const int64_t lo = int64_t(c0 + pos) * rb_rows;
+      if ((slowm >> pos) & 1u) {  // a slow segment, row by row
+        const int32_t c = __shfl(cd, pos, 64);
+        const int64_t hi = lo + rb_rows < n ? lo + rb_rows : n;
+        if (k < lo || k > hi) {
+          fail = true;
+          break;
+        }
+        F = sr_fold_rows_wave<T, RW>(seg_base(c), lo, k, hi, F, lane);
+        k = hi;
+        if (!(F <= SrM<T>::big)) fail = true;  // (an overflow: not the plan's case)
+        ++pos;
+        continue;
+      }
+      // the run [pos, e): its composition is the scan's value at lane e - 1
+      const uint64_t after = (slowm >> pos) >> 1;
+      int e = after ? pos + 1 + __builtin_ctzll(after) : end;
+      if (e > end) e = end;
+      const int32_t q = __shfl(cd, pos, 64);
+      const I g0 = __shfl(x0, e - 1, 64), g1 = __shfl(x1, e - 1, 64);
+      int qf;
+      I lim;
+      if (F < MIN_NORMAL) {
+        qf = Tr::qmin;
+        lim = I(1) << Tr::mant;
+      } else {
+        int ex;
+        (void)frexp(double(F), &ex);
+        qf = ex - 1 - Tr::mant;
+        lim = I(1) << (Tr::mant + 1);
+      }
+      if (k != lo || qf != q || !(F <= SrM<T>::big)) {  // the running value left the plan's window
+        fail = true;
+        break;
+      }
+      const I P = I(ldexp(double(F), -q));
+      const I g = (P & 1) ? g1 : g0;
+      if (P + g >= lim) {  // the fold crosses a binade inside a run the plan called safe
+        fail = true;
+        break;
+      }
+      F = T(ldexp(double(P + g), q));
+      const int64_t hl = int64_t(c0 + e) * rb_rows;
+      k = hl < n ? hl : n;
+      pos = e;
+    }
+  }
+  if (lane == 0) {
+    out_val[t] = F;
+    out_st[t] = fail ? SR_FST_FAIL : SR_FST_OK;
+  }
+}
+
+template <typename T>
+hipError_t sr_launch_fold_plan(const double* part, int np, int n_rb, const uint32_t* perm, const SrFoldWho& who,
+                               double delta, int32_t* code, int* slot_next, int slot_cap, hipStream_t s) {
+  if (np <= 0) return hipSuccess;
+  hipLaunchKernelGGL(sr_fold_plan_kernel<T>, dim3(unsigned((np + 3) / 4)), dim3(256), 0, s, part, np, n_rb, perm, who,
+                     delta, code, slot_next, slot_cap);
+  return hipGetLastError();
+}
+template <typename T>
+hipError_t sr_launch_fold_stab(const double* part, int np, int n_rb, int64_t rb_rows, int64_t n, const uint32_t* perm,
+                               const SrFoldWho& who, double delta, const T* losses, int32_t* code, void* tab,
+                               hipStream_t s) {
+  if (np <= 0 || n_rb <= 0) return hipSuccess;
+  hipLaunchKernelGGL((sr_fold_stab_kernel<T, 8>), dim3(unsigned(n_rb), unsigned(np)), dim3(256), 0, s, part, np, n_rb,
+                     rb_rows, n, perm, who, delta, losses, code, static_cast<typename SrFoldTab<T>::Pair*>(tab));
+  return hipGetLastError();
+}
+template <typename T>
+hipError_t sr_launch_fold_walk(const int32_t* code, const void* tab, int np, int n_rb, int64_t rb_rows, int64_t n,
+                               const T* losses, int64_t slot_rows, const uint32_t* perm, const T* carry, T* out_val,
+                               int32_t* out_st, hipStream_t s) {
+  if (np <= 0) return hipSuccess;
+  hipLaunchKernelGGL((sr_fold_walk_kernel<T, sizeof(T) == 4 ? 16 : 8>), dim3(unsigned((np + 3) / 4)), dim3(256), 0, s, code,
+                     static_cast<const typename SrFoldTab<T>::Pair*>(tab), np, n_rb, rb_rows, n, losses, slot_rows, perm,
+                     carry, out_val, out_st);
+  return hipGetLastError();
+}
+#define SR_INSTANTIATE_FOLD2(T)                                                                                      \
+  template hipError_t sr_launch_fold_plan<T>(const double*, int, int, const uint32_t*, const SrFoldWho&, double,   \
+                                             int32_t*, int*, int, hipStream_t);                                        \
+  template hipError_t sr_launch_fold_stab<T>(const double*, int, int, int64_t, int64_t, const uint32_t*,              \
+                                             const SrFoldWho&, double, const T*, int32_t*, void*, hipStream_t);        \
+  template hipError_t sr_launch_fold_walk<T>(const int32_t*, const void*, int, int, int64_t, int64_t, const T*, int64_t, \
+                                             const uint32_t*, const T*, T*, int32_t*, hipStream_t);
+SR_INSTANTIATE_FOLD2(float)
+SR_INSTANTIATE_FOLD2(double)
+
 // Julia [nf, n] column-major -> per-feature rows [nf][ld]; padded rows replicate row 0 so that the
 // interpreter's validity checks never see a value that is not in the dataset.
 template <typename T>
@@ -763,6 +1142,23 @@ template <typename T>
 hipError_t sr_launch_eval(const SrEvalArgs<T>& a, int mode, bool gather, int tier, int R, int waves, bool vstk,
                           int n_blocks, hipStream_t s) {
   if constexpr (sizeof(T) == 4) {
+    if (mode == SR_MODE_FOLD) {  // (the launch shapes of the loss launches a large call runs: sr_inst_f32_fold*.hip)
+      const bool l2 = a.loss_kind == SR_LOSS_L2;
+      if (vstk) {
+        if (tier != SR_TIER_BASIC || gather || R != 16) return hipErrorInvalidValue;
+        return l2 ? sr_launch_tile<T, 16, SR_MODE_FOLD, false, SR_TIER_BASIC, 4, SR_LOSS_L2, true>(a, n_blocks, s)
+                  : sr_launch_tile<T, 16, SR_MODE_FOLD, false, SR_TIER_BASIC, 4, -1, true>(a, n_blocks, s);
+      }
+      if (tier == SR_TIER_BASIC) {
+        if (R != 8 || waves != 4) return hipErrorInvalidValue;
+        if (gather) return sr_launch_tile<T, 8, SR_MODE_FOLD, true, SR_TIER_BASIC, 4, -1>(a, n_blocks, s);
+        return l2 ? sr_launch_tile<T, 8, SR_MODE_FOLD, false, SR_TIER_BASIC, 4, SR_LOSS_L2>(a, n_blocks, s)
+                  : sr_launch_tile<T, 8, SR_MODE_FOLD, false, SR_TIER_BASIC, 4, -1>(a, n_blocks, s);
+      }
+      if (R != 4) return hipErrorInvalidValue;
+      return gather ? sr_launch_tile<T, 4, SR_MODE_FOLD, true, SR_TIER_FULL>(a, n_blocks, s)
+                    : sr_launch_tile<T, 4, SR_MODE_FOLD, false, SR_TIER_FULL>(a, n_blocks, s);
+    }
     if (vstk) {
       if (mode != SR_MODE_LOSS || tier != SR_TIER_BASIC || gather) return hipErrorInvalidValue;
       if (R == 32) return sr_launch_basic_loss<T, 32, false, true>(a, n_blocks, s);
@@ -798,6 +1194,7 @@ hipError_t sr_launch_eval(const SrEvalArgs<T>& a, int mode, bool gather, int tie
     return gather ? sr_launch_tile<T, 4, SR_MODE_EXACT, true, SR_TIER_FULL, 1>(a, n_blocks, s)
                   : sr_launch_tile<T, 4, SR_MODE_EXACT, false, SR_TIER_FULL, 1>(a, n_blocks, s);
   } else {
+    if (mode == SR_MODE_FOLD) return hipErrorInvalidValue;  // (Float64: small calls only, from stored losses)
     if (vstk) {
       if (mode != SR_MODE_LOSS || tier != SR_TIER_BASIC || gather) return hipErrorInvalidValue;
       if (R == 8) return sr_launch_basic_loss<T, 8, false, true>(a, n_blocks, s);

@@ -28,6 +28,7 @@
 #include "sr_compile.h"
 #include "sr_eval.h"
 #include "sr_fold.h"
+#include "sr_fold_dev.h"
 
 namespace {
 
@@ -344,6 +345,30 @@ struct sr_ctx {
                             // 2 (default) only before the chunks after the first, whose probe
                             // overlaps the first chunk's kernel (profiles/r01_ab_probe_modes.txt)
   std::vector<uint32_t> perm_host;
+  // The reference's in-order loss fold for EVERY complete tree (round 6; sr_fold_dev.h, sr_aux.hip): a
+  // complete tree's loss is LossFunctions' left-to-right fold in T of its elementwise losses
+  // (src/LossFunctions.jl:38-58), divided in T, not the device's f64 sum.  SR_AMD_REF_FOLD / "ref_fold":
+  // 1 (default) single-GPU loss calls with weights >= 0; 0 the f64 sums (rounds 1-5).  Small calls
+  // (every tree's losses fit fold_store_mb) keep the loss launch's losses; larger Float32 calls run the
+  // complete trees again in FOLD mode (slow segments' losses in up to fold_slot_mb of slots); larger
+  // Float64 calls keep the f64 sum (within ~1e-13 of the fold, north_star's f64 bar is 1e-10).
+  int ref_fold = 1;
+  int64_t fold_store_mb = 512;
+  int64_t fold_slot_mb = 2048;
+  // the plan's window: the fold within 2^-8 of the f64 prefix, else the tree fails (C2's trees: the fold is
+  // within 2.1e-3 of the f64 sum at 2^20 rows; 2^-6 kept twice the slow segments)
+  int fold_delta_log2 = 8;
+  int fold_debug_fail = 0;   // (tests: "fold_debug_fail")
+  bool want_fold = false;    // set by eval_loss_submit around its run_batch
+  int fold_path_last = 0;    // 0 none, 1 stored losses, 2 FOLD mode
+  DevBuf fold_code, fold_tab, fold_store, fold_ctl, fold_io2;
+  std::shared_ptr<void> fold_job;  // a row-sharded call's FoldJob<T>, until its ranks agree on the verdicts
+  int inject_post_wsum = 0;        // tests ("inject_failure_post_wsum"): this rank's copy of the weights' sum gather fails
+  size_t outs_fval_off = 0, outs_fst_off = 0, outs_bytes_all = 0;
+  hipEvent_t ev_fc0[kMaxChunks] = {}, ev_fc1[kMaxChunks] = {};  // each chunk's fold launches
+  bool fold_timed_last = false;
+  int64_t n_ref_ok_last = 0, n_ref_fail_last = 0;  // trees whose loss is the walk's fold / that fell back
+  double fold_kernel_ms_last = 0.0;
 };
 
 // For the search engine (sr_search.cpp, not in the public header): set the context's "timing" knob
@@ -367,6 +392,7 @@ struct sr_dataset {
   double wsum = 0.0;
   double w_min = 0.0;      // smallest weight (the loss-fold overflow rule needs w >= 0: sr_fold.h)
   double max_abs_x = 0.0;  // max |X| over the data (NaN / Inf if any value is non-finite)
+  mutable double wsum_jl_f32 = NAN, wsum_jl_f64 = NAN;  // Base.sum(w) in Float32 / Float64 (cached on first use)
   // dead-tree probe rows (large datasets): the "stress rows" — per feature the K largest, K smallest
   // and K smallest-magnitude values, where exp overflows, logs and divisions blow up — then rows 0, 1,
   // ... up to kProbeRows; int64 row indices on the device (NULL for small datasets)
@@ -536,6 +562,89 @@ struct ViewSpec {
   int64_t view_len;
 };
 
+// Rows of the reference's loss fold for the overflow rule (sr_fold.h), or 0 when the rule does not
+// apply (negative weights: the fold is not monotone).
+inline int64_t fold_terms(const sr_dataset* ds, int64_t n_rows) { return (ds->w && ds->w_min < 0.0) ? 0 : n_rows; }
+
+// ---------------------------------------------------------------- every complete tree's in-order fold
+// One loss launch of a call whose trees the in-order fold covers (sr_ctx::ref_fold): its arguments (the
+// FOLD pass re-launches them), launch positions [pos0, pos0 + np) of the call (chunk t0: perm values and
+// per-tree arrays are chunk-local), grid and kernel build.
+template <typename T>
+struct FoldRegion {
+  SrEvalArgs<T> a;
+  int64_t t0, pos0, np, n_blocks;
+  int Rc;
+  bool vstk;
+  Grid g;
+};
+// A call's fold: its regions and the launch facts every fold kernel needs (kept by a row-sharded call's
+// run_batch until the ranks have agreed on the verdicts: FoldJob::deferred).
+template <typename T>
+struct FoldJob {
+  std::vector<FoldRegion<T>> regions;
+  int path = 0;  // 1 stored losses, 2 FOLD pass
+  int tier = 0;
+  bool gather = false;
+  int64_t n_eval = 0, n_rb = 0, slot_rows = 0, n_terms = 0;
+  int slot_cap = 0;
+  double delta = 0.0;
+};
+
+// A region's steps: the stored-loss tables (path 1) or the plan and the FOLD pass (path 2).  who: the
+// call's whole-batch arrays (sums / flags / elig / est at the caller's tree index; this function adds
+// the region's chunk offset).
+template <typename T>
+int fold_steps(sr_ctx* ctx, const FoldJob<T>& job, const FoldRegion<T>& fr, SrFoldWho who, hipStream_t cs) {
+  const int nrb = fr.g.n_row_blocks;
+  const int64_t rb_rows = int64_t(fr.g.tiles) * 64 * fr.Rc;
+  const size_t off = size_t(job.n_rb) * size_t(fr.pos0);  // (the region's offset in the partial buffers)
+  int32_t* code = ctx->fold_code.as<int32_t>() + off;
+  void* tab = ctx->fold_tab.as<char>() + off * sizeof(typename SrFoldTab<T>::Pair);
+  const double* part = nrb > 1 ? fr.a.part_sum : nullptr;
+  const int np = int(fr.np);
+  if (who.sums) who.sums += fr.t0;
+  if (who.flags) who.flags += fr.t0;
+  if (who.elig) who.elig += fr.t0;
+  if (who.est) who.est += fr.t0;
+  if (job.path == 1) {
+    SR_HIP_CHECK(sr_launch_fold_stab<T>(part, np, nrb, rb_rows, job.n_eval, fr.a.perm, who, job.delta, fr.a.fold_loss,
+                                        code, tab, cs));
+    return SR_OK;
+  }
+  SR_HIP_CHECK(sr_launch_fold_plan<T>(part, np, nrb, fr.a.perm, who, job.delta, code, ctx->fold_ctl.as<int>(),
+                                      job.slot_cap, cs));
+  SrEvalArgs<T> fa = fr.a;
+  fa.hint = nullptr;
+  fa.out_sum = nullptr;
+  fa.out_flag = nullptr;
+  fa.group_cnt = nullptr;
+  fa.stamps = nullptr;
+  fa.fold_code = code;
+  fa.fold_tab = tab;
+  fa.fold_loss = ctx->fold_store.as<T>();
+  fa.fold_slot_rows = job.slot_rows;
+  fa.fold_pos_stride = 0;
+  SR_HIP_CHECK(sr_launch_eval<T>(fa, SR_MODE_FOLD, job.gather, job.tier, fr.Rc, fr.g.W, fr.vstk, int(fr.n_blocks), cs));
+  return SR_OK;
+}
+// A region's walk: the folds' values and status at the caller's tree index (out arrays and carry are
+// whole-batch, tree-indexed).
+template <typename T>
+int fold_walk(sr_ctx* ctx, const FoldJob<T>& job, const FoldRegion<T>& fr, const T* carry, T* out_val, int32_t* out_st,
+              hipStream_t cs) {
+  const int nrb = fr.g.n_row_blocks;
+  const int64_t rb_rows = int64_t(fr.g.tiles) * 64 * fr.Rc;
+  const size_t off = size_t(job.n_rb) * size_t(fr.pos0);
+  const int32_t* code = ctx->fold_code.as<int32_t>() + off;
+  const void* tab = ctx->fold_tab.as<char>() + off * sizeof(typename SrFoldTab<T>::Pair);
+  const T* losses = job.path == 1 ? fr.a.fold_loss : ctx->fold_store.as<T>();
+  const int64_t slot_rows = job.path == 1 ? rb_rows : job.slot_rows;
+  SR_HIP_CHECK(sr_launch_fold_walk<T>(code, tab, int(fr.np), nrb, rb_rows, job.n_eval, losses, slot_rows, fr.a.perm,
+                                      carry ? carry + fr.t0 : nullptr, out_val + fr.t0, out_st + fr.t0, cs));
+  return SR_OK;
+}
+
 // The speculative exact pass's stream (sr_ctx::spec_exact) drained: nothing of an earlier call (its
 // probe-flag copies, a pass an error path left running) may still use h_pflag / h_exact.
 inline void spec_drain(sr_ctx* ctx) {
@@ -650,12 +759,63 @@ int run_batch(sr_ctx* ctx, const sr_dataset* ds, int opset_id, const sr_tree_bat
     SR_HIP_CHECK(ctx->group_cnt.ensure(size_t(nt) * sizeof(uint32_t) + 4));
     SR_HIP_CHECK(hipMemset(ctx->group_cnt.p, 0, ctx->group_cnt.cap));
   }
+  // the reference's in-order loss fold of every complete tree (sr_ctx::ref_fold): 1 = the loss launch
+  // stores every tree's losses (they fit fold_store_mb), 2 = the FOLD-mode pass over the complete trees
+  // (a row-sharded call: the global rows and every shard's weights; its ranks fold or not together —
+  //  the choice below depends on the largest shard's rows, known to every rank)
+  const int64_t fold_n_terms = shard ? ((ds->w && ds->shard_w_min < 0.0) ? 0 : n_total) : fold_terms(ds, n_eval);
+  int fold_path = 0;
+  int64_t fold_slot_rows = 0;
+  if (shard) ctx->fold_job.reset();
+  if (ctx->want_fold && ctx->ref_fold && mode == SR_MODE_LOSS && nt > 0 && fold_n_terms > 0) {
+    // rows a position's store covers under either kernel's grid (row blocks x rows: >= the view)
+    auto cover = [&](int Rc, int depth_c, int64_t* rb_rows) {
+      const Grid gg = make_grid<T>(n_eval, nt, Rc, W, int(ds->nf), depth_c, 0, ds->w != nullptr, ctx->tree_group, mrb);
+      *rb_rows = int64_t(gg.tiles) * 64 * Rc;
+      return int64_t(gg.n_row_blocks) * *rb_rows;
+    };
+    int64_t rbr = 0, rbv = 0;
+    int64_t pos_rows = cover(R, 1, &rbr);
+    if (Rv > 0) pos_rows = std::max(pos_rows, cover(Rv, 0, &rbv));
+    fold_slot_rows = std::max(rbr, rbv);
+    const bool fold_mode_builds = tier == SR_TIER_BASIC ? (R == 8 && (Rv == 0 || Rv == 16)) : R == 4;
+    int64_t max_shard = n_eval;
+    if (shard)
+      for (size_t r = 0; r + 1 < ds->shard_offs.size(); ++r) max_shard = std::max(max_shard, ds->shard_offs[r + 1] - ds->shard_offs[r]);
+    // Float64: only with stored losses (no FOLD build), decided on the largest shard so every rank agrees
+    const bool f64_off = sizeof(T) == 8 && double(nt) * double(pos_rows) * double(max_shard) / double(n_eval) *
+                                               double(sizeof(T)) > double(ctx->fold_store_mb) * 1048576.0;
+    if (f64_off) {
+    } else if (double(nt) * double(pos_rows) * double(sizeof(T)) <= double(ctx->fold_store_mb) * 1048576.0) {
+      fold_path = 1;
+      SR_HIP_CHECK(ctx->fold_store.ensure(size_t(nt) * size_t(pos_rows) * sizeof(T)));
+    } else if (sizeof(T) == 4 && fold_mode_builds) {
+      fold_path = 2;
+      const int64_t slots = std::max<int64_t>(1, ctx->fold_slot_mb * 1048576 / (fold_slot_rows * int64_t(sizeof(T))));
+      SR_HIP_CHECK(ctx->fold_store.ensure(size_t(slots) * size_t(fold_slot_rows) * sizeof(T)));
+      SR_HIP_CHECK(ctx->fold_ctl.ensure(64));
+      SR_HIP_CHECK(hipMemsetAsync(ctx->fold_ctl.p, 0, sizeof(int), s));  // the call's slot counter
+    }
+    if (fold_path) {
+      SR_HIP_CHECK(ctx->fold_code.ensure(n_part * sizeof(int32_t) + 4));
+      SR_HIP_CHECK(ctx->fold_tab.ensure(n_part * sizeof(typename SrFoldTab<T>::Pair) + 16));
+    }
+  }
+  if (!ctx->internal_pass) {  // (the fallback's prediction passes leave the call's record alone)
+    ctx->fold_path_last = fold_path;
+    ctx->fold_timed_last = false;
+  }
+  // {Σ loss | flags | the fold's values | their status}, one allocation (one DMA back)
   ctx->outs_flag_off = align256(size_t(nt) * sizeof(double) + 8);
-  const size_t outs_bytes = ctx->outs_flag_off + size_t(nt) * sizeof(uint32_t) + 4;
+  ctx->outs_fval_off = align256(ctx->outs_flag_off + size_t(nt) * sizeof(uint32_t) + 4);
+  ctx->outs_fst_off = align256(ctx->outs_fval_off + size_t(nt) * sizeof(T) + 8);
+  const size_t outs_bytes = ctx->outs_fst_off + size_t(nt) * sizeof(int32_t) + 4;
+  ctx->outs_bytes_all = outs_bytes;
   SR_HIP_CHECK(ctx->outs.ensure(outs_bytes));
   // latency path (see host_io): results written to pinned host memory, programs read from it
   const bool small_call = n_chunks == 1 && mode == SR_MODE_LOSS;
-  const bool host_out = small_call && ctx->host_io >= 1 && ctx->want_host_out;
+  // (under the in-order fold the plan reads the call's flags and partials on the device)
+  const bool host_out = small_call && ctx->host_io >= 1 && ctx->want_host_out && fold_path == 0;
   const bool host_prog = small_call && ctx->host_io >= 2;
   if (host_out) SR_HIP_CHECK(ctx->h_outs.ensure(outs_bytes, s, ctx->stream2));
   ctx->outs_on_host = host_out;
@@ -804,6 +964,22 @@ int run_batch(sr_ctx* ctx, const sr_dataset* ds, int opset_id, const sr_tree_bat
     SR_HIP_CHECK(hipStreamWaitEvent(ctx->stream2, ctx->ev_join, 0));
   }
 
+  // the fold's launches per chunk: every launch of the chunk, then its plan / tables / FOLD pass / walk
+  FoldJob<T> fjob;  // (the regions of the chunk being launched; a row-sharded call's: all of them, kept)
+  fjob.path = fold_path;
+  fjob.tier = tier;
+  fjob.gather = gather;
+  fjob.n_eval = n_eval;
+  fjob.n_rb = n_rb;
+  fjob.slot_rows = fold_slot_rows;
+  fjob.n_terms = fold_n_terms;
+  fjob.delta = std::ldexp(1.0, -ctx->fold_delta_log2);
+  fjob.slot_cap = fold_path == 2 ? int(std::min<int64_t>(INT_MAX / 2, int64_t(ctx->fold_store.cap /
+                                                                             (size_t(fold_slot_rows) * sizeof(T)))))
+                                 : 0;
+  size_t fold_store_at = 0;  // (stored losses: the regions one after another, [position][n_rb x rb rows])
+  T* const d_fval = reinterpret_cast<T*>(ctx->outs.as<char>() + ctx->outs_fval_off);
+  int32_t* const d_fst = reinterpret_cast<int32_t*>(ctx->outs.as<char>() + ctx->outs_fst_off);
   uint32_t code_base = 0;
   static const bool phase_debug = std::getenv("SR_AMD_PHASE_DEBUG") != nullptr;  // (latency analysis)
   const auto t_pre = std::chrono::steady_clock::now();
@@ -1047,6 +1223,11 @@ int run_batch(sr_ctx* ctx, const sr_dataset* ds, int opset_id, const sr_tree_bat
                               : ctx->part_flag.as<uint32_t>()) + size_t(n_rb) * size_t(t0 + p0);
       a.pred = ctx->pred.as<T>();
       a.pred_ld = n_eval;
+      if (fold_path == 1) {  // (small calls under the in-order fold: every live tree's losses, [position][rows])
+        a.fold_pos_stride = int64_t(g.n_row_blocks) * int64_t(g.tiles) * 64 * Rc;
+        a.fold_loss = ctx->fold_store.as<T>() + fold_store_at;
+        fold_store_at += size_t(np) * size_t(a.fold_pos_stride);
+      }
       // LDS program cache (register-stack launches: 4 workgroups per CU leave ~36 KiB of dynamic LDS
       // each): sized for the longest group span of this launch, capped by that budget (groups longer
       // than the cap stream their windows from global memory)
@@ -1103,6 +1284,7 @@ int run_batch(sr_ctx* ctx, const sr_dataset* ds, int opset_id, const sr_tree_bat
         // classic kernel at R rows per lane (a register-stack launch's 2x longer tiles would double the
         // probe's work for the same verdicts: C2's dead trees 0.88 -> 0.6x ms)
         SrEvalArgs<T> pa = a;
+        pa.fold_loss = nullptr;  // (its rows are the stress rows; the main launch stores the view's)
         pa.stack_depth = depth;
         pa.out_sum = nullptr;
         pa.out_flag = nullptr;
@@ -1140,6 +1322,7 @@ int run_batch(sr_ctx* ctx, const sr_dataset* ds, int opset_id, const sr_tree_bat
       a.stamps = ctx->stamps.as<uint64_t>();
 #endif
       SR_HIP_CHECK(sr_launch_eval<T>(a, mode, gather, tier, Rc, g.W, vstk, int(n_blocks), cs));
+      if (fold_path) fjob.regions.push_back({a, t0, t0 + p0, np, n_blocks, Rc, vstk, g});
       if (!direct && !fused && host_red)
         ctx->host_reductions.push_back({t0 + p0, np, g.n_row_blocks});
       else if (!direct && !fused)
@@ -1155,6 +1338,25 @@ int run_batch(sr_ctx* ctx, const sr_dataset* ds, int opset_id, const sr_tree_bat
       return lrc;
     }
     if (ctx->timed_last) SR_HIP_CHECK(hipEventRecord(ctx->ev_c1[c], cs));
+    if (fold_path && !shard && !fjob.regions.empty()) {
+      // the in-order fold of this chunk's complete trees (sr_aux.hip): the launches' partials and flags
+      // are final here (reduce / direct write / in-launch reduction ran on this stream)
+      if (ctx->timed_last) SR_HIP_CHECK(hipEventRecord(ctx->ev_fc0[c], cs));
+      const SrFoldWho who{ctx->d_out_sum, ctx->d_out_flag, fold_n_terms, nullptr, nullptr, 1};
+      for (const FoldRegion<T>& fr : fjob.regions) {
+        int frc = fold_steps<T>(ctx, fjob, fr, who, cs);
+        if (frc == SR_OK) frc = fold_walk<T>(ctx, fjob, fr, nullptr, d_fval, d_fst, cs);
+        if (frc != SR_OK) {
+          sync_both();
+          return frc;
+        }
+      }
+      fjob.regions.clear();
+      if (ctx->timed_last) {
+        SR_HIP_CHECK(hipEventRecord(ctx->ev_fc1[c], cs));
+        ctx->fold_timed_last = true;
+      }
+    }
     ctx->n_chunks_last = c + 1;
     code_base += uint32_t(ncode);
   }
@@ -1165,6 +1367,7 @@ int run_batch(sr_ctx* ctx, const sr_dataset* ds, int opset_id, const sr_tree_bat
   }
   if (nt == 0) ctx->mark_phase(0);
   *grid_out = glast;
+  if (fold_path && shard) ctx->fold_job = std::make_shared<FoldJob<T>>(std::move(fjob));  // (eval_sharded_impl)
   ctx->mark_phase(1);
   return SR_OK;
 }
@@ -1197,6 +1400,8 @@ inline double chunk_busy_ms(sr_ctx* ctx) {
   };
   for (int c = 0; c < ctx->n_chunks_last; ++c) add(ctx->ev_c0[c], ctx->ev_c1[c]);
   if (ctx->derived_last) add(ctx->ev_d0, ctx->ev_d1);
+  if (ctx->fold_timed_last)  // (the in-order fold's launches: device work of the call too)
+    for (int c = 0; c < ctx->n_chunks_last; ++c) add(ctx->ev_fc0[c], ctx->ev_fc1[c]);
   std::sort(iv.begin(), iv.end());
   double busy = 0.0, lo = 0.0, hi = -1.0;
   for (const auto& [a, b] : iv) {
@@ -1608,10 +1813,21 @@ inline int spec_collect(sr_ctx* ctx) {
 // complete tree's loss is Σ / denom, or +Inf where the reference's T-precision fold of the losses
 // overflows (sr_fold.h; n_terms = rows of the fold, 0: only SR_FLAG_ELEMINF is applied).  Trees the
 // bounds cannot decide are appended to *fold_list (when given) for the exact in-order fold.
+// fold (may be NULL): every complete tree's in-order fold from the call's walk (values, SR_FST_* status,
+// and the T denominators: T(count), or Base.sum(w) in T, per tree); a tree the walk folded takes
+// fold / denominator in T (the reference's own arithmetic), one whose walk failed joins *fold_list.
+template <typename T>
+struct FoldResults {
+  const T* val;
+  const int32_t* st;
+  std::function<T(int64_t)> den;
+  int64_t n_ok = 0, n_fail = 0;
+  int debug_fail = 0;  // (tests, "fold_debug_fail" k: trees t % k == 0 take the fallback as if their walk failed)
+};
 template <typename T>
 void finalize(int64_t nt, const double* sums, const uint32_t* flags, double denom, const int64_t* list,
               int64_t n_list, const uint8_t* list_ok, T* out_loss, uint8_t* out_complete, int64_t n_terms = 0,
-              std::vector<int64_t>* fold_list = nullptr, const double* denoms = nullptr) {
+              std::vector<int64_t>* fold_list = nullptr, const double* denoms = nullptr, FoldResults<T>* fold = nullptr) {
   std::vector<int64_t> pos;
   if (n_list > 0) {
     pos.assign(size_t(nt), -1);
@@ -1632,6 +1848,14 @@ void finalize(int64_t nt, const double* sums, const uint32_t* flags, double deno
       out_loss[t] = T(INFINITY);
     } else if (cls == SR_FOLD_EXACT && fold_list) {
       fold_list->push_back(t);
+    } else if (cls == SR_FOLD_FINITE && fold) {
+      if (fold->st[t] == SR_FST_OK && !(fold->debug_fail > 0 && t % fold->debug_fail == 0)) {
+        out_loss[t] = T(fold->val[t] / fold->den(t));
+        ++fold->n_ok;
+      } else if (fold->st[t] != SR_FST_NONE && fold_list) {
+        fold_list->push_back(t);
+        ++fold->n_fail;
+      }
     }
   }
 }
@@ -1909,6 +2133,17 @@ void host_reduce_partials(sr_ctx* ctx, int64_t nt) {
   ctx->host_reductions.clear();
 }
 
+// Base.sum(w) in T over a view (the reference's normalize = true denominator); the full view's is cached
+// per dataset and type.
+template <typename T>
+T jl_wsum_view(const sr_dataset* ds, const int64_t* row_idx, int64_t n) {
+  if (n <= 0) return T(0);
+  if (row_idx) return jl_sum_T<T>(ds->w_host.data(), row_idx, 0, n - 1);
+  double& c = sizeof(T) == 4 ? ds->wsum_jl_f32 : ds->wsum_jl_f64;
+  if (!(c == c)) c = double(jl_sum_T<T>(ds->w_host.data(), nullptr, 0, n - 1));
+  return T(c);
+}
+
 template <typename T>
 double view_denominator(const sr_dataset* ds, const int64_t* row_idx, int64_t n_idx) {
   const bool gather = row_idx != nullptr && n_idx > 0;
@@ -1919,9 +2154,6 @@ double view_denominator(const sr_dataset* ds, const int64_t* row_idx, int64_t n_
   return s;
 }
 
-// Rows of the reference's loss fold for the overflow rule (sr_fold.h), or 0 when the rule does not
-// apply (negative weights: the fold is not monotone).
-inline int64_t fold_terms(const sr_dataset* ds, int64_t n_rows) { return (ds->w && ds->w_min < 0.0) ? 0 : n_rows; }
 
 // views (may be NULL): several row views in one call (sr_eval_loss_batch_views); row_idx then holds
 // views->n_views views of n_idx rows each.
@@ -1971,16 +2203,18 @@ int eval_loss_submit(sr_ctx* ctx, const sr_dataset* ds, int opset_id, const sr_t
   Grid g;
   ctx->want_host_out = true;
   ctx->want_spec = views == nullptr && !gather;
+  ctx->want_fold = true;
   int rc = run_batch<T>(ctx, ds, opset_id, trees, row_idx, n_idx, n_eval, loss_kind, SR_MODE_LOSS, &prog, &g, true,
                         nullptr, views);
   ctx->want_host_out = false;
   ctx->want_spec = false;
+  ctx->want_fold = false;
   if (rc != SR_OK) return rc;
   if (nt == 0) return SR_OK;
   hipStream_t s = ctx->stream;
   // {Σ loss, flags} of every tree: already in pinned memory (host_io), or one DMA there
   if (!ctx->outs_on_host) {
-    const size_t out_bytes = ctx->outs_flag_off + size_t(nt) * sizeof(uint32_t);
+    const size_t out_bytes = ctx->fold_path_last ? ctx->outs_bytes_all : ctx->outs_flag_off + size_t(nt) * sizeof(uint32_t);
     SR_HIP_CHECK(ctx->h_outs.ensure(out_bytes, s, ctx->stream2));
     SR_HIP_CHECK(hipMemcpyAsync(ctx->h_outs.p, ctx->outs.p, out_bytes, hipMemcpyDeviceToHost, s));
   }
@@ -2075,9 +2309,23 @@ int eval_loss_finish(sr_ctx* ctx, LossCall<T>& c) {
     for (int64_t t = 0; t < nt; ++t) denoms[size_t(t)] = vden[size_t(view_of(t))];
   }
   std::vector<int64_t> fold_list;
+  // the in-order fold's results (sr_ctx::ref_fold) and the reference's T denominators per view
+  std::vector<T> tden(static_cast<size_t>(n_views));
+  FoldResults<T> fres;
+  const bool have_fold = ctx->fold_path_last != 0;
+  if (have_fold) {
+    for (int v = 0; v < n_views; ++v)
+      tden[size_t(v)] = (ds->w && n_eval > 0) ? jl_wsum_view<T>(ds, rows_of(v), n_eval) : T(double(n_eval));
+    fres.val = reinterpret_cast<const T*>(ctx->h_outs.as<char>() + ctx->outs_fval_off);
+    fres.st = reinterpret_cast<const int32_t*>(ctx->h_outs.as<char>() + ctx->outs_fst_off);
+    fres.den = [&](int64_t t) { return tden[size_t(view_of(t))]; };
+    fres.debug_fail = ctx->fold_debug_fail;
+  }
   finalize<T>(nt, sums.data(), flags.data(), vden[0], list.data(), int64_t(list.size()), list_ok.data(),
               static_cast<T*>(out_loss), out_complete, fold_terms(ds, n_eval), &fold_list,
-              views ? denoms.data() : nullptr);
+              views ? denoms.data() : nullptr, have_fold ? &fres : nullptr);
+  ctx->n_ref_ok_last = fres.n_ok;
+  ctx->n_ref_fail_last = fres.n_fail;
   ctx->n_fold_last = int64_t(fold_list.size());
   ctx->fold_slow_last = ctx->fold_seg_last = 0;
   for (double& v : ctx->fold_ms) v = 0.0;
@@ -2090,7 +2338,7 @@ int eval_loss_finish(sr_ctx* ctx, LossCall<T>& c) {
     rc = fold_exact<T>(ctx, ds, opset_id, trees, rows_of(v), n_idx, n_eval, loss_kind, fv, &fold);
     if (rc != SR_OK) return rc;
     // mean: total / count, in T; weighted: total / sum(w), the reference's pairwise Base.sum in T
-    const T den = (ds->w && n_eval > 0) ? jl_sum_T<T>(ds->w_host.data(), rows_of(v), 0, n_eval - 1) : T(vden[size_t(v)]);
+    const T den = (ds->w && n_eval > 0) ? jl_wsum_view<T>(ds, rows_of(v), n_eval) : T(vden[size_t(v)]);
     for (size_t i = 0; i < fv.size(); ++i) static_cast<T*>(out_loss)[fv[i]] = T(fold[i] / den);
   }
   ctx->mark_phase(4);
@@ -2953,6 +3201,103 @@ int fold_sharded(sr_ctx* ctx, const sr_dataset* ds, int opset_id, const sr_tree_
   return agree(ctx, pending, "failed in the loss fold");
 }
 
+// Every complete tree's in-order loss fold across the shards (sr_ctx::ref_fold; round 6).  The verdicts
+// the ranks agreed on after the all-reduce and the exact pass choose the trees (the same bytes on every
+// rank); one all-gather of the shards' per-tree f64 totals gives each rank the fold's estimated value at
+// its first row; every rank's steps (stored-loss tables, or the plan and the FOLD pass) run in parallel;
+// the walks run rank after rank, each from the previous shard's fold values (one all-gather per rank).
+// folds / ok: the trees every walk took; *fallback: those some walk failed (the caller folds them
+// through the prediction pass).  Collective (every rank enters every gather, also after a failure).
+template <typename T>
+int fold_all_sharded(sr_ctx* ctx, int64_t nt, const uint8_t* out_complete, const T* out_loss, std::vector<T>* folds,
+                     std::vector<uint8_t>* ok, std::vector<int64_t>* fallback) {
+  folds->assign(size_t(nt), T(0));
+  ok->assign(size_t(nt), 0);
+  std::shared_ptr<FoldJob<T>> job = std::static_pointer_cast<FoldJob<T>>(ctx->fold_job);
+  ctx->fold_job.reset();
+  if (!job || nt == 0) return SR_OK;  // (the ranks decide to fold or not alike: run_batch)
+  const int nr = ctx->comm_ranks, me = ctx->comm_rank;
+  hipStream_t s = ctx->stream;
+  std::vector<uint8_t> elig(static_cast<size_t>(nt));
+  bool any = false;
+  for (int64_t t = 0; t < nt; ++t) {
+    elig[size_t(t)] = ((out_complete[t] & 1) && !(out_complete[t] & SR_COMP_FOLD) && std::isfinite(double(out_loss[t]))) ? 1 : 0;
+    any = any || elig[size_t(t)];
+  }
+  if (!any) return SR_OK;
+  const size_t pay = size_t(nt) * (sizeof(T) + sizeof(int32_t));
+  Prep prep{ctx};
+  prep.need(ctx->coll_buf, ((std::max(size_t(nt) * sizeof(double), pay) + sizeof(double) + 255) & ~size_t(255)) * size_t(nr + 1));
+  const size_t o_est = (size_t(nt) + 255) & ~size_t(255), o_car = o_est + ((size_t(nt) * 8 + 255) & ~size_t(255));
+  prep.need(ctx->fold_io2, o_car + size_t(nt) * sizeof(T) + 64);
+  int rc = agree_prep(ctx, prep);
+  if (rc != SR_OK) return rc;
+  int local = SR_OK, pending = SR_OK;
+  auto hip_local = [&](hipError_t e, const char* what) {
+    if (e != hipSuccess && local == SR_OK) local = set_error(SR_ERR_HIP, std::string("fold: ") + what + ": " + hipGetErrorString(e));
+  };
+  std::vector<double> tot(static_cast<size_t>(nt), 0.0);
+  hip_local(hipMemcpyAsync(tot.data(), ctx->d_out_sum, size_t(nt) * sizeof(double), hipMemcpyDeviceToHost, s), "totals copy");
+  hip_local(hipStreamSynchronize(s), "totals copy");
+  std::vector<char> every;
+  size_t slot = 0;
+  rc = gather_checked(ctx, tot.data(), size_t(nt) * sizeof(double), local, &every, &slot, "the loss fold's shard totals",
+                      &pending);
+  if (rc != SR_OK) return rc;
+  std::vector<double> est(static_cast<size_t>(nt), 0.0);
+  for (int r = 0; r < me; ++r) {
+    const double* v = reinterpret_cast<const double*>(every.data() + slot * size_t(r));
+    for (int64_t t = 0; t < nt; ++t) est[size_t(t)] += v[t];
+  }
+  char* io = ctx->fold_io2.as<char>();
+  uint8_t* d_elig = reinterpret_cast<uint8_t*>(io);
+  double* d_est = reinterpret_cast<double*>(io + o_est);
+  T* d_carry = reinterpret_cast<T*>(io + o_car);
+  T* d_fval = reinterpret_cast<T*>(ctx->outs.as<char>() + ctx->outs_fval_off);
+  int32_t* d_fst = reinterpret_cast<int32_t*>(ctx->outs.as<char>() + ctx->outs_fst_off);
+  int step = SR_OK;  // (a failure from here on rides in the next gather's error word)
+  auto hip_step = [&](hipError_t e, const char* what) {
+    if (e != hipSuccess && step == SR_OK) step = set_error(SR_ERR_HIP, std::string("fold: ") + what + ": " + hipGetErrorString(e));
+  };
+  hip_step(hipMemcpyAsync(d_elig, elig.data(), size_t(nt), hipMemcpyHostToDevice, s), "verdicts upload");
+  hip_step(hipMemcpyAsync(d_est, est.data(), size_t(nt) * sizeof(double), hipMemcpyHostToDevice, s), "estimates upload");
+  const SrFoldWho who{ctx->d_out_sum, ctx->d_out_flag, job->n_terms, d_elig, d_est, me == 0 ? 1 : 0};
+  if (step == SR_OK && pending == SR_OK)
+    for (const FoldRegion<T>& fr : job->regions)
+      if (step == SR_OK) step = fold_steps<T>(ctx, *job, fr, who, s);
+  std::vector<T> carry(static_cast<size_t>(nt), T(0));
+  std::vector<uint8_t> failed(static_cast<size_t>(nt), 0);
+  std::vector<char> payload(pay, 0);
+  for (int r = 0; r < nr; ++r) {
+    if (me == r && step == SR_OK && pending == SR_OK) {
+      if (r > 0) hip_step(hipMemcpyAsync(d_carry, carry.data(), size_t(nt) * sizeof(T), hipMemcpyHostToDevice, s), "carry upload");
+      for (const FoldRegion<T>& fr : job->regions)
+        if (step == SR_OK) step = fold_walk<T>(ctx, *job, fr, r > 0 ? d_carry : nullptr, d_fval, d_fst, s);
+      hip_step(hipMemcpyAsync(payload.data(), d_fval, size_t(nt) * sizeof(T), hipMemcpyDeviceToHost, s), "walk copy");
+      hip_step(hipMemcpyAsync(payload.data() + size_t(nt) * sizeof(T), d_fst, size_t(nt) * sizeof(int32_t),
+                              hipMemcpyDeviceToHost, s), "walk copy");
+      hip_step(hipStreamSynchronize(s), "walk");
+    }
+    rc = gather_checked(ctx, payload.data(), pay, me == r ? step : SR_OK, &every, &slot, "the loss fold's walk", &pending);
+    if (rc != SR_OK) return rc;
+    const char* got = every.data() + slot * size_t(r);
+    std::memcpy(carry.data(), got, size_t(nt) * sizeof(T));
+    const int32_t* st = reinterpret_cast<const int32_t*>(got + size_t(nt) * sizeof(T));
+    for (int64_t t = 0; t < nt; ++t)
+      if (elig[size_t(t)] && st[t] != SR_FST_OK) failed[size_t(t)] = 1;
+  }
+  for (int64_t t = 0; t < nt; ++t) {
+    if (!elig[size_t(t)]) continue;
+    if (failed[size_t(t)]) {
+      fallback->push_back(t);
+    } else {
+      (*folds)[size_t(t)] = carry[size_t(t)];
+      (*ok)[size_t(t)] = 1;
+    }
+  }
+  return agree(ctx, pending, "failed in the loss fold");
+}
+
 // Base.sum(w) in T over the GLOBAL rows of a row-sharded dataset: each shard folds its Julia leaf
 // blocks (one-row heads continue a block begun on an earlier shard), one all-gather, and every rank
 // combines them in Base.mapreduce_impl's recursion order.  Collective.
@@ -2983,7 +3328,13 @@ int jl_wsum_sharded(sr_ctx* ctx, const sr_dataset* ds, T* out) {
   int pending = SR_OK;
   rc = gather_checked(ctx, mine.data(), max_r * sizeof(T), SR_OK, &every, &slot, "the weights' sum", &pending);
   if (rc != SR_OK) return rc;
-  if (pending != SR_OK) return pending;  // (no collective follows: the peers do not wait for this rank)
+  if (ctx->inject_post_wsum > 0 && --ctx->inject_post_wsum == 0 && pending == SR_OK)  // (tests)
+    pending = set_error(SR_ERR_HIP, "injected failure after the weights' sum gather");
+  // a local failure after the gather (this rank's copy of it): every rank learns of it and fails
+  // together, as after the fold's gathers (a lone failing rank left its peers to enter the
+  // next step's all-reduce without it)
+  rc = agree(ctx, pending, "failed in the weights' sum");
+  if (rc != SR_OK) return rc;
   std::vector<const T*> rank_vals(static_cast<size_t>(nr));
   for (int r = 0; r < nr; ++r) rank_vals[size_t(r)] = reinterpret_cast<const T*>(every.data() + slot * size_t(r));
   std::vector<T> leafval(jl_leaves(n_total).size());
@@ -3034,9 +3385,11 @@ int eval_sharded_impl(sr_ctx* ctx, const sr_dataset* ds, int opset_id, const sr_
   // 3. this shard
   SrProgramBatch<T> prog;
   Grid g;
+  ctx->want_fold = true;  // (the in-order fold's steps and walks follow the ranks' agreement, step 6)
   int local = nt > 0 ? run_batch<T>(ctx, ds, opset_id, trees, nullptr, 0, n_total, loss_kind, SR_MODE_LOSS, &prog, &g,
                                     true, &sc)
                      : SR_OK;
+  ctx->want_fold = false;
   hipStream_t s = ctx->stream;
   char* base = ctx->coll_packed.as<char>();
   double* dst = reinterpret_cast<double*>(base);
@@ -3100,10 +3453,19 @@ int eval_sharded_impl(sr_ctx* ctx, const sr_dataset* ds, int opset_id, const sr_
     if (!list_ok[i]) out_loss[t] = T(INFINITY);
   }
   ctx->mark_phase(3);
-  // 6. rarer: the loss fold in row order across the shards (sr_fold.h)
+  // 6. every complete tree's in-order fold across the shards (sr_ctx::ref_fold), and — rarer — the trees
+  //    whose fold the overflow band or a failed walk leaves to the prediction pass (sr_fold.h)
   std::vector<int64_t> fold_list;
+  std::vector<T> rfold;
+  std::vector<uint8_t> rok;
+  rc = fold_all_sharded<T>(ctx, nt, out_complete, out_loss, &rfold, &rok, &fold_list);
+  if (rc != SR_OK) return rc;
+  ctx->n_ref_fail_last = int64_t(fold_list.size());
+  ctx->n_ref_ok_last = 0;
+  for (uint8_t v : rok) ctx->n_ref_ok_last += v;
   for (int64_t t = 0; t < nt; ++t)
     if ((out_complete[t] & 1) && (out_complete[t] & SR_COMP_FOLD)) fold_list.push_back(t);
+  std::sort(fold_list.begin(), fold_list.end());
   ctx->n_fold_last = int64_t(fold_list.size());
   ctx->fold_slow_last = ctx->fold_seg_last = 0;
   for (double& v : ctx->fold_ms) v = 0.0;
@@ -3112,12 +3474,13 @@ int eval_sharded_impl(sr_ctx* ctx, const sr_dataset* ds, int opset_id, const sr_
   if (rc != SR_OK) return rc;
   // mean: total / count, in T; weighted: total / sum(w), the reference's pairwise Base.sum in T
   T fden = T(denom);
-  if (ds->w && !fold_list.empty()) {
-    rc = nr > 1 ? jl_wsum_sharded<T>(ctx, ds, &fden)
-                : (ds->n > 0 ? (fden = jl_sum_T<T>(ds->w_host.data(), nullptr, 0, ds->n - 1), SR_OK) : SR_OK);
+  if (ds->w && (!fold_list.empty() || ctx->n_ref_ok_last > 0)) {  // (the same on every rank)
+    rc = nr > 1 ? jl_wsum_sharded<T>(ctx, ds, &fden) : (fden = jl_wsum_view<T>(ds, nullptr, ds->n), SR_OK);
     if (rc != SR_OK) return rc;
   }
   for (size_t i = 0; i < fold_list.size(); ++i) out_loss[fold_list[i]] = T(fold[i] / fden);
+  for (int64_t t = 0; t < nt; ++t)
+    if (rok[size_t(t)]) out_loss[t] = T(rfold[size_t(t)] / fden);
   for (int64_t t = 0; t < nt; ++t) out_complete[t] &= 1;
   ctx->mark_phase(4);
   ctx->last_total_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
@@ -3278,6 +3641,10 @@ int sr_init(int device, sr_ctx** out) {
   if (const char* v = std::getenv("SR_AMD_PAR_STAGE")) ctx->par_stage = std::atoi(v);
   if (const char* v = std::getenv("SR_AMD_DERIVED")) ctx->derived = std::atoi(v);
   if (const char* v = std::getenv("SR_AMD_MAX_ROW_BLOCKS")) ctx->max_row_blocks = std::max(1, std::atoi(v));
+  if (const char* v = std::getenv("SR_AMD_REF_FOLD")) ctx->ref_fold = std::atoi(v) != 0 ? 1 : 0;
+  if (const char* v = std::getenv("SR_AMD_FOLD_STORE_MB")) ctx->fold_store_mb = std::max<int64_t>(0, std::atoll(v));
+  if (const char* v = std::getenv("SR_AMD_FOLD_SLOT_MB")) ctx->fold_slot_mb = std::max<int64_t>(1, std::atoll(v));
+  if (const char* v = std::getenv("SR_AMD_FOLD_DELTA_LOG2")) ctx->fold_delta_log2 = std::max(1, std::min(40, std::atoi(v)));
   hipError_t e = hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking);
   if (e == hipSuccess && std::getenv("SR_AMD_EAGER_STREAM2")) e = ctx->need_stream2();  // (A/B: the round-4 layout)
   if (e == hipSuccess) e = hipEventCreateWithFlags(&ctx->ev_join, hipEventDisableTiming);
@@ -3291,6 +3658,8 @@ int sr_init(int device, sr_ctx** out) {
     if (e == hipSuccess) e = hipEventCreate(&ctx->ev_c0[c]);
     if (e == hipSuccess) e = hipEventCreate(&ctx->ev_c1[c]);
     if (e == hipSuccess) e = hipEventCreateWithFlags(&ctx->ev_pr[c], hipEventDisableTiming);
+    if (e == hipSuccess) e = hipEventCreate(&ctx->ev_fc0[c]);
+    if (e == hipSuccess) e = hipEventCreate(&ctx->ev_fc1[c]);
   }
   if (e == hipSuccess) e = hipEventCreateWithFlags(&ctx->ev_spec, hipEventDisableTiming);
   for (int b = 0; b < sr_ctx::kGradBuckets; ++b) {
@@ -3335,6 +3704,10 @@ int sr_init_shared(sr_ctx* parent, sr_ctx** out) {
   c->stress_probe = parent->stress_probe;
   c->spec_exact = parent->spec_exact;
   c->fold_seg = parent->fold_seg;
+  c->ref_fold = parent->ref_fold;
+  c->fold_store_mb = parent->fold_store_mb;
+  c->fold_slot_mb = parent->fold_slot_mb;
+  c->fold_delta_log2 = parent->fold_delta_log2;
   c->spin = parent->spin;
   c->h_prog.flags = parent->h_prog.flags;
   return SR_OK;
@@ -3364,6 +3737,8 @@ int sr_shutdown(sr_ctx* ctx) {
       (void)hipEventDestroy(ctx->ev_c0[c]);
       (void)hipEventDestroy(ctx->ev_c1[c]);
       (void)hipEventDestroy(ctx->ev_pr[c]);
+      (void)hipEventDestroy(ctx->ev_fc0[c]);
+      (void)hipEventDestroy(ctx->ev_fc1[c]);
     }
     (void)hipEventDestroy(ctx->ev_spec);
     if (ctx->stream3) (void)hipStreamDestroy(ctx->stream3);
@@ -3999,6 +4374,12 @@ static void settle_timing(sr_ctx* ctx) {
   ctx->timing_pending = false;
   ctx->last_eval_ms = chunk_kernel_ms(ctx);
   ctx->last_busy_ms = chunk_busy_ms(ctx);
+  ctx->fold_kernel_ms_last = 0.0;
+  if (ctx->fold_timed_last)
+    for (int c = 0; c < ctx->n_chunks_last; ++c) {
+      float m = 0.f;
+      if (hipEventElapsedTime(&m, ctx->ev_fc0[c], ctx->ev_fc1[c]) == hipSuccess) ctx->fold_kernel_ms_last += double(m);
+    }
 }
 
 int sr_last_phase_ms(sr_ctx* ctx, double* out, int n) {
@@ -4067,6 +4448,26 @@ int sr_set_tuning(sr_ctx* ctx, const char* name, int64_t value) {
     ctx->fused_reduce = value;
     return SR_OK;
   }
+  if (std::strcmp(name, "ref_fold") == 0) {  // every complete tree's loss = the in-order fold (SR_AMD_REF_FOLD)
+    ctx->ref_fold = value != 0 ? 1 : 0;
+    return SR_OK;
+  }
+  if (std::strcmp(name, "fold_store_mb") == 0) {  // small calls: stored losses up to this size (SR_AMD_FOLD_STORE_MB)
+    ctx->fold_store_mb = value < 0 ? 0 : value;
+    return SR_OK;
+  }
+  if (std::strcmp(name, "fold_slot_mb") == 0) {  // FOLD mode: slow-segment slots (SR_AMD_FOLD_SLOT_MB)
+    ctx->fold_slot_mb = value < 1 ? 1 : value;
+    return SR_OK;
+  }
+  if (std::strcmp(name, "fold_debug_fail") == 0) {  // tests: trees t % value == 0 take the fold's fallback
+    ctx->fold_debug_fail = int(value < 0 ? 0 : value);
+    return SR_OK;
+  }
+  if (std::strcmp(name, "fold_delta_log2") == 0) {  // the plan's window 2^-value around the f64 prefix
+    ctx->fold_delta_log2 = int(value < 1 ? 1 : (value > 40 ? 40 : value));
+    return SR_OK;
+  }
   if (std::strcmp(name, "fold_seg") == 0) {  // rows per segment of the in-order loss fold (SR_AMD_FOLD_SEG)
     ctx->fold_seg = value < 0 ? -1 : value;
     return SR_OK;
@@ -4115,6 +4516,10 @@ int sr_set_tuning(sr_ctx* ctx, const char* name, int64_t value) {
     ctx->inject_post_exact = int(value);
     return SR_OK;
   }
+  if (std::strcmp(name, "inject_failure_post_wsum") == 0) {  // tests: this rank's copy of the k-th Σw gather fails
+    ctx->inject_post_wsum = int(value);
+    return SR_OK;
+  }
   if (std::strcmp(name, "inject_failure_post_gather") == 0) {
     ctx->inject_post_gather = int(value);
     return SR_OK;
@@ -4144,6 +4549,17 @@ int sr_tuning_info(sr_ctx* ctx, int* used_derived_columns, int64_t* exact_trees)
   if (check_ctx(ctx) != SR_OK) return SR_ERR_INVALID_ARG;
   if (used_derived_columns) *used_derived_columns = ctx->n_derived_last;
   if (exact_trees) *exact_trees = ctx->n_exact_last;
+  return SR_OK;
+}
+
+int sr_ref_fold_info(sr_ctx* ctx, int* path, int64_t* n_folded, int64_t* n_fallback, double* fold_kernel_ms) {
+  if (check_ctx(ctx) != SR_OK) return SR_ERR_INVALID_ARG;
+  Lock l(ctx);
+  settle_timing(ctx);
+  if (path) *path = ctx->fold_path_last;
+  if (n_folded) *n_folded = ctx->n_ref_ok_last;
+  if (n_fallback) *n_fallback = ctx->n_ref_fail_last;
+  if (fold_kernel_ms) *fold_kernel_ms = ctx->fold_kernel_ms_last;
   return SR_OK;
 }
 

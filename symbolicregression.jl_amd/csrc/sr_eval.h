@@ -5,7 +5,9 @@
 #include "sr_ops.h"
 #include "../../include/sr_amd.h"
 
-enum { SR_MODE_LOSS = 0, SR_MODE_PRED = 1, SR_MODE_EXACT = 2 };
+// SR_MODE_FOLD (round 6): the loss programs of complete trees again, composing each row tile's steps of
+// the reference's in-order loss fold for the binades of the call's fold plan (sr_fold_dev.h), no checks
+enum { SR_MODE_LOSS = 0, SR_MODE_PRED = 1, SR_MODE_EXACT = 2, SR_MODE_FOLD = 3 };
 // operand-stack slots the register-stack kernels hold in VGPRs (1: trees needing a second slot —
 // 6 % of C2's — run on the LDS-stack kernel instead)
 // The deferred checks leave bounded outputs untracked (sr_tile_impl.h sr_untracked_u / _b; round 5:
@@ -149,6 +151,16 @@ struct SrEvalArgs {
   // several row views in one launch (GATHER LOSS; NULL: one view, blockIdx = row_block * n_groups + group)
   const SrSegment* segs;
   int n_segs;
+  // the reference's in-order loss fold (round 6, sr_fold_dev.h).  LOSS: fold_loss non-NULL stores every
+  // evaluated tree's elementwise losses at fold_loss[position * fold_pos_stride + row] (small calls: the
+  // fold's tables are composed from them).  FOLD: fold_code [n_row_blocks][n_trees] per position (the
+  // plan), fold_tab the same shape of composed-step pairs (SrFoldTab<T>::Pair, written for steps
+  // segments), fold_loss the slow segments' losses, slot (code - SR_FCODE_SLOT0) x fold_slot_rows.
+  T* fold_loss;
+  int64_t fold_pos_stride;
+  const int32_t* fold_code;
+  void* fold_tab;
+  int64_t fold_slot_rows;
   // -DSR_STAMPS builds only (latency analysis, tools/stamps.py): per wave, SR_NSTAMPS wall-clock
   // stamps at fixed points of the kernel, [block][wave][SR_NSTAMPS]; NULL otherwise
   uint64_t* stamps;
@@ -276,6 +288,21 @@ template <typename T>
 hipError_t sr_launch_fold_segtab(const T* pred, int64_t pred_ld, int n_trees, const T* y, const T* w,
                                  const int64_t* row_idx, int64_t n, int loss_kind, T loss_param, int64_t seg_len,
                                  const double* segsum, const double* carry_est, int2* tq, int64_t* tab, hipStream_t s);
+// Every complete tree's fold (round 6; sr_aux.hip): the plan of a large call (codes per (row block,
+// position), slots for the FOLD mode's slow segments), the stored-loss tables of a small call, and the
+// walk (per position: the fold's value and status at the caller's tree index perm[position]).
+struct SrFoldWho;  // (sr_fold_dev.h)
+template <typename T>
+hipError_t sr_launch_fold_plan(const double* part, int np, int n_rb, const uint32_t* perm, const SrFoldWho& who,
+                               double delta, int32_t* code, int* slot_next, int slot_cap, hipStream_t s);
+template <typename T>
+hipError_t sr_launch_fold_stab(const double* part, int np, int n_rb, int64_t rb_rows, int64_t n, const uint32_t* perm,
+                               const SrFoldWho& who, double delta, const T* losses, int32_t* code, void* tab,
+                               hipStream_t s);
+template <typename T>
+hipError_t sr_launch_fold_walk(const int32_t* code, const void* tab, int np, int n_rb, int64_t rb_rows, int64_t n,
+                               const T* losses, int64_t slot_rows, const uint32_t* perm, const T* carry, T* out_val,
+                               int32_t* out_st, hipStream_t s);
 template <typename T>
 hipError_t sr_launch_fold(const T* pred, int64_t pred_ld, int n_trees, const T* y, const T* w, const int64_t* row_idx,
                           int64_t n, int loss_kind, T loss_param, int64_t seg_len, const int2* tq, const int64_t* tab,

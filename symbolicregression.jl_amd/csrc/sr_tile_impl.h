@@ -30,6 +30,7 @@
 #include <type_traits>
 
 #include "sr_eval.h"
+#include "sr_fold_dev.h"
 #include "sr_ops.h"
 
 // Waves per workgroup W is a template parameter (4 by default); the minimum resident waves per
@@ -565,7 +566,7 @@ constexpr bool sr_untracked_b(uint32_t) { return false; }
 #endif
 // FAST_CHECK: every operator output joins the running max |v| of the tree
 #define SR_TRACK()                                                        \
-  if constexpr (FAST_CHECK) {                                             \
+  if constexpr (FAST_CHECK && MODE == SR_MODE_LOSS) {                     \
     _Pragma("unroll") for (int r = 0; r < R; r += 4) {                    \
       mrun = SrMaxAbs<T>::step(mrun, tos[r], tos[r + 1]);                 \
       if (r + 3 < R) mrun1 = SrMaxAbs<T>::step(mrun1, tos[r + 2], tos[r + 3]); \
@@ -815,7 +816,10 @@ __global__ void __launch_bounds__(W * 64, (SrMinWavesFor<T, R, TIER, W, VSTK, LK
   constexpr int ROWS = 64 * R;
   // Deferred validity checks (BASIC tier loss kernels): no per-node branch, ballot or
   // early exit; the tree's running max |v| and the root's NaN test decide at the end of the program.
-  constexpr bool FAST_CHECK = (TIER == SR_TIER_BASIC) && (MODE == SR_MODE_LOSS);
+  // FOLD mode runs complete trees only: the deferred-check kernels' operator bodies (FAST_CHECK), no
+  // tracking (SR_TRACK), no per-node checks
+  constexpr bool FAST_CHECK = (TIER == SR_TIER_BASIC) && (MODE == SR_MODE_LOSS || MODE == SR_MODE_FOLD);
+  constexpr bool NODE_CHECKS = !FAST_CHECK && MODE != SR_MODE_FOLD;
   static_assert(R % 4 == 0 || R == 2, "rows per lane: 2 or a multiple of 4");
   extern __shared__ __attribute__((aligned(16))) unsigned char sr_smem[];
   const int tid = threadIdx.x;
@@ -829,7 +833,7 @@ __global__ void __launch_bounds__(W * 64, (SrMinWavesFor<T, R, TIER, W, VSTK, LK
   const int G = a.trees_per_block;
   const int MC = (MODE == SR_MODE_EXACT) ? a.max_checks : 0;
   const SrLdsPlan<T> plan(a.nf, ROWS, VSTK ? 0 : a.stack_depth, G, MC, W, a.w != nullptr,
-                          MODE == SR_MODE_LOSS ? a.code_lds : 0);
+                          (MODE == SR_MODE_LOSS || MODE == SR_MODE_FOLD) ? a.code_lds : 0);
   T* xs = reinterpret_cast<T*>(sr_smem + plan.x);
   T* ys = reinterpret_cast<T*>(sr_smem + plan.y);
   T* wsv = reinterpret_cast<T*>(sr_smem + plan.w);
@@ -887,7 +891,7 @@ __global__ void __launch_bounds__(W * 64, (SrMinWavesFor<T, R, TIER, W, VSTK, LK
   // (first position's start .. last position's end); copied once, read by every tile's windows
   const uint4* lcode = reinterpret_cast<const uint4*>(sr_smem + plan.code);
   bool lds_code = false;
-  if (MODE == SR_MODE_LOSS && a.code_lds > 0 && a.ends != nullptr && gcount > 0) {
+  if ((MODE == SR_MODE_LOSS || MODE == SR_MODE_FOLD) && a.code_lds > 0 && a.ends != nullptr && gcount > 0) {
     const uint32_t t_first = a.perm ? a.perm[tree0] : uint32_t(tree0);
     const uint32_t t_last = a.perm ? a.perm[tree0 + gcount - 1] : uint32_t(tree0 + gcount - 1);
     const uint32_t gbase = __builtin_amdgcn_readfirstlane(a.offsets[t_first]);
@@ -903,7 +907,12 @@ __global__ void __launch_bounds__(W * 64, (SrMinWavesFor<T, R, TIER, W, VSTK, LK
       }
     }
   }
-  const uint64_t live = sr_ballot(lane < S && my_pe > my_pb);  // empty program: statically incomplete
+  // FOLD: this row block's plan code of each of the wave's trees (lane j: tree j); SKIP trees are not run
+  int32_t my_code = SR_FCODE_SKIP;
+  if (MODE == SR_MODE_FOLD && lane < S) my_code = a.fold_code[size_t(rb) * size_t(a.n_trees) + size_t(my_pos)];
+  const uint64_t live = sr_ballot(lane < S && my_pe > my_pb &&  // empty program: statically incomplete
+                                  (MODE != SR_MODE_FOLD || my_code != SR_FCODE_SKIP));
+  typename SrFoldTab<T>::I facc0 = 0, facc1 = 0;  // FOLD: lane j's tree's composed steps over this row block
   uint64_t dmask = 0u, bmask = 0u, emask = 0u;
   double accv = 0.0;
   // dead-tree hints shared across row blocks (LOSS mode): a tree found non-finite by any block is
@@ -1176,7 +1185,7 @@ __global__ void __launch_bounds__(W * 64, (SrMinWavesFor<T, R, TIER, W, VSTK, LK
       }                                                                                                      \
     }                                                                                                        \
   }
-          if (!FAST_CHECK && (SR_META() & SR_M_CHECK)) {
+          if (NODE_CHECKS && (SR_META() & SR_M_CHECK)) {
             SR_CHECK_NODE();
           }
           // the POST unary and the post binary with a constant (PBC) fused into this instruction (the
@@ -1196,7 +1205,7 @@ __global__ void __launch_bounds__(W * 64, (SrMinWavesFor<T, R, TIER, W, VSTK, LK
               if (!sr_untracked_u(pu))
 #endif
               SR_TRACK();
-              if (!FAST_CHECK && (op & SR_OP_POST_CHECK)) {
+              if (NODE_CHECKS && (op & SR_OP_POST_CHECK)) {
                 SR_CHECK_NODE();
               }
             }
@@ -1213,7 +1222,7 @@ __global__ void __launch_bounds__(W * 64, (SrMinWavesFor<T, R, TIER, W, VSTK, LK
                 default: { SR_BIN_EACH(cv, tos[r], SR_B_DIV); break; }
               }
               SR_TRACK();
-              if (!FAST_CHECK && (op & SR_OP_PBC_CHECK)) {
+              if (NODE_CHECKS && (op & SR_OP_PBC_CHECK)) {
                 SR_CHECK_NODE();
               }
             }
@@ -1272,6 +1281,9 @@ __global__ void __launch_bounds__(W * 64, (SrMinWavesFor<T, R, TIER, W, VSTK, LK
 #pragma unroll
               for (int r = 0; r < R; ++r) l[r] = (row0 + L::row(lane, r) < a.n_rows) ? l[r] : T(0);
             }
+            // (small calls under the in-order fold: every live tree's losses, the fold's tables are
+            //  composed from them; a tree found dead later leaves garbage the fold never reads)
+            if (a.fold_loss) L::store(a.fold_loss + size_t(tree0 + g) * size_t(a.fold_pos_stride) + size_t(row0) + lane * C, l);
             // pairwise over the lane's rows by halves (rows r and r + h: adjacent pairs of rows add as
             // one packed instruction, R - 1 adds in R / 2 instructions); the wave sum follows.  The
             // first level's sums are sums of TWO losses: one of them +Inf means an elementwise loss,
@@ -1334,6 +1346,47 @@ __global__ void __launch_bounds__(W * 64, (SrMinWavesFor<T, R, TIER, W, VSTK, LK
             if (use_hint && lane == 0)
               __hip_atomic_fetch_max(a.hint + tree0 + g, a.hint_epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
           }
+        } else if (MODE == SR_MODE_FOLD) {
+          // the same losses as the LOSS epilogue (rows past the view: 0, which the fold skips)
+          T l[R];
+          T yv[R];
+          L::load(y_lane, yv);
+          if (weighted) {
+            T wv[R];
+            L::load(w_lane, wv);
+#pragma unroll
+            for (int r = 0; r < R; ++r) l[r] = sr_elem_loss<T>(lk, tos[r], yv[r], a.loss_param) * wv[r];
+          } else {
+#pragma unroll
+            for (int r = 0; r < R; ++r) l[r] = sr_elem_loss<T>(lk, tos[r], yv[r], a.loss_param);
+          }
+          if (!full_tile) {
+#pragma unroll
+            for (int r = 0; r < R; ++r) l[r] = (row0 + L::row(lane, r) < a.n_rows) ? l[r] : T(0);
+          }
+          const int32_t code = __builtin_amdgcn_readlane(my_code, j);
+          if (code >= SR_FCODE_SLOT0) {  // a slow segment: keep its losses for the walk (row order)
+            L::store(a.fold_loss + size_t(code - SR_FCODE_SLOT0) * size_t(a.fold_slot_rows) + size_t(tile) * ROWS +
+                         lane * C,
+                     l);
+          } else {  // this tile's composed step under the segment's binade, then the block's so far
+            using I = typename SrFoldTab<T>::I;
+            I y0, y1;
+            sr_fold_tile_step<T, R, C>(l, code, lane, y0, y1);
+            I x0 = I(0), x1 = I(0);
+            if constexpr (sizeof(I) == 4) {
+              x0 = __builtin_amdgcn_readlane(int(facc0), j);
+              x1 = __builtin_amdgcn_readlane(int(facc1), j);
+            } else {
+              x0 = __shfl(facc0, j, 64);
+              x1 = __shfl(facc1, j, 64);
+            }
+            sr_fold_compose_i<I>(x0, x1, y0, y1, I(1) << (SrFoldTraits<T>::mant + 3));
+            if (lane == j) {
+              facc0 = y0;
+              facc1 = y1;
+            }
+          }
         } else if (MODE == SR_MODE_PRED) {
           const uint32_t tree = a.perm ? a.perm[tree0 + g] : uint32_t(tree0 + g);
           T* out = a.pred + int64_t(tree) * a.pred_ld + row0;
@@ -1351,6 +1404,12 @@ __global__ void __launch_bounds__(W * 64, (SrMinWavesFor<T, R, TIER, W, VSTK, LK
   }
   SR_STAMP(5);
 
+  if (MODE == SR_MODE_FOLD) {  // the steps segments' pairs, [row block][position]
+    if (lane < S && my_code != SR_FCODE_SKIP && my_code < SR_FCODE_SLOT0)
+      static_cast<typename SrFoldTab<T>::Pair*>(a.fold_tab)[size_t(rb) * size_t(a.n_trees) + size_t(my_pos)] =
+          SrFoldTab<T>::pair(facc0, facc1);
+    return;
+  }
   if (MODE == SR_MODE_EXACT) {
     __syncthreads();
     // this range's sum of every checked array: [list position][check][range]
@@ -1406,7 +1465,7 @@ hipError_t sr_launch_tile(const SrEvalArgs<T>& a, int n_blocks, hipStream_t s) {
   if (VSTK && a.stack_depth > SR_VSTK_SLOTS) return hipErrorInvalidValue;  // host routes deeper programs elsewhere
   const SrLdsPlan<T> plan(a.nf, 64 * R, VSTK ? 0 : a.stack_depth, a.trees_per_block,
                           MODE == SR_MODE_EXACT ? a.max_checks : 0, W, a.w != nullptr,
-                          MODE == SR_MODE_LOSS ? a.code_lds : 0);
+                          (MODE == SR_MODE_LOSS || MODE == SR_MODE_FOLD) ? a.code_lds : 0);
   const void* fn = reinterpret_cast<const void*>(&sr_tile_kernel<T, R, MODE, GATHER, TIER, W, LK, VSTK>);
   if (plan.total > 65536) {  // many features / a deep stack: opt in to the full 160 KiB of LDS
     const hipError_t e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, int(plan.total));

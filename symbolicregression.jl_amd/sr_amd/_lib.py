@@ -78,6 +78,7 @@ EXPORTED_SYMBOLS = (
     "sr_set_tuning",
     "sr_tuning_info",
     "sr_spec_exact_info",
+    "sr_ref_fold_info",
     "sr_last_grad_info",
     "sr_search_create",
     "sr_search_free",
@@ -249,6 +250,7 @@ def _load():
         "sr_set_tuning": (c_int, [P, ctypes.c_char_p, ctypes.c_int64]),
         "sr_tuning_info": (c_int, [P, POINTER(c_int), POINTER(c_int64)]),
         "sr_spec_exact_info": (c_int, [P, POINTER(c_int64), POINTER(c_int64)]),
+        "sr_ref_fold_info": (c_int, [P, POINTER(c_int), POINTER(c_int64), POINTER(c_int64), POINTER(c_double)]),
         "sr_last_grad_info": (c_int, [P, c_int, P, P, P, P]),
         "sr_search_create": (
             c_int,

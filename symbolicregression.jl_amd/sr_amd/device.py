@@ -89,6 +89,15 @@ class DeviceContext:
         _lib.check(_lib.lib.sr_spec_exact_info(self.handle, ctypes.byref(a), ctypes.byref(b)))
         return int(a.value), int(b.value)
 
+    def last_ref_fold(self):
+        """The last eval_loss call's in-order loss fold (csrc/sr_fold_dev.h): {path: 0 none / 1 stored
+        losses / 2 FOLD-mode pass, folded: trees whose loss is the exact fold, fallback: trees folded
+        through the prediction pass instead, kernel_ms: the fold launches' device time}."""
+        p, a, b, ms = ctypes.c_int(0), ctypes.c_int64(0), ctypes.c_int64(0), ctypes.c_double(0.0)
+        _lib.check(_lib.lib.sr_ref_fold_info(self.handle, ctypes.byref(p), ctypes.byref(a), ctypes.byref(b),
+                                             ctypes.byref(ms)))
+        return {"path": int(p.value), "folded": int(a.value), "fallback": int(b.value), "kernel_ms": float(ms.value)}
+
     def last_exact_kernel_ms(self):
         """Device time of the last eval_loss call's exact-sum pass (ms)."""
         out = (ctypes.c_double * 7)()

@@ -4,15 +4,15 @@
 their collectives going through `sr_comm_init_host` (the caller's gloo group instead of RCCL, which
 refuses two ranks on one device).  Everything else is the C++ path the 8-GPU run takes: the shard
 layout exchange, the packed all-reduce with its error word, the exact Julia-order pass whose leaf
-blocks straddle the cut between the shards (head ranges), the in-order loss fold continued across the
-shards, the tree owners' results all-gather, and the failure protocol (an injected buffer failure on
-one rank makes BOTH ranks return an error; so does an injected HIP failure on one rank after the packed
-all-reduce, after the exact pass's all-gather, or in the loss fold's gathers; the next call works on
-both).
+blocks straddle the cut between the shards (head ranges), every complete tree's in-order loss fold
+walked rank after rank (round 6), the tree owners' results all-gather, and the failure protocol (an
+injected buffer failure on one rank makes BOTH ranks return an error; so does an injected HIP failure
+on one rank after the packed all-reduce, after the exact pass's all-gather, in the loss folds'
+gathers, or in the weights' sum gather of a weighted call; the next call works on both).
 
 Uneven shards (rank 0 holds 60,001 of 143,417 rows), huge values around the cut (BIG trees), weights.
-Results must equal the single-GPU call on the whole dataset (flags bit for bit, losses to 1e-6; the
-in-order folds bit for bit) and the oracle's flags.
+Results must equal the single-GPU call on the whole dataset (flags and losses bit for bit: both are the
+in-order fold) and the oracle's flags.
 """
 import os
 import socket
@@ -113,12 +113,17 @@ def _worker(rank, world, port, q):
         # chain, which only the final agreement catches); the band and BIG trees make every later
         # collective run, so a rank returning alone would leave its peer waiting
         post = []
-        for knob, who, k in (("inject_failure_post", 1, 1), ("inject_failure_post_exact", 0, 1),
-                             ("inject_failure_post_gather", 1, 1), ("inject_failure_post_gather", 0, 3)):
+        # (a weighted call's Base.sum(w) gather: ADVICE r5, a failure there must fail both ranks too)
+        Xw, yw, ww = _data(True)
+        wshard = Dataset(np.ascontiguousarray(Xw[:, lo:hi]), np.ascontiguousarray(yw[lo:hi]),
+                         weights=np.ascontiguousarray(ww[lo:hi]))
+        for knob, who, k, ds_ in (("inject_failure_post", 1, 1, shard), ("inject_failure_post_exact", 0, 1, shard),
+                                  ("inject_failure_post_gather", 1, 1, shard), ("inject_failure_post_gather", 0, 3, shard),
+                                  ("inject_failure_post_gather", 1, 5, shard), ("inject_failure_post_wsum", 0, 1, wshard)):
             if rank == who:
                 ctx.set_tuning(knob, k)
             try:
-                eval_loss_sharded(tb, shard, opts)
+                eval_loss_sharded(tb, ds_, opts)
                 post.append(None)
             except Exception as e:  # noqa: BLE001
                 post.append(str(e)[:200])
@@ -165,12 +170,13 @@ def test_two_ranks_on_one_gpu_run_the_library_sharded_paths():
         for g in got:
             loss, comp, n_exact, n_fold = g[key + "_rows"]
             assert n_exact > 0, (key, "no tree took the exact (BIG) pass")
-            assert n_fold == ref_fold, (key, n_fold, ref_fold)
+            assert n_fold >= 1, (key, n_fold, ref_fold)  # (the band trees, and any walk that fell back)
             assert np.array_equal(comp, ref_comp), key
             assert np.array_equal(np.isinf(loss), np.isinf(ref_loss)), key
-            sel = comp & np.isfinite(ref_loss)
-            rel = np.abs(loss[sel].astype(np.float64) - ref_loss[sel]) / np.maximum(np.abs(ref_loss[sel]), 1e-30)
-            assert float(rel.max(initial=0.0)) < 1e-6, key
+            # every complete tree's loss is the in-order fold across the two shards (round 6): the single
+            # call's bits (NaN losses compare as NaN)
+            sel = comp & ~np.isnan(ref_loss)
+            assert np.array_equal(loss[sel].view(np.uint32), ref_loss[sel].view(np.uint32)), key
             # the band trees (the last four) are folded in row order across the shards: bit for bit
             assert np.array_equal(loss[-4:].view(np.uint32), ref_loss[-4:].view(np.uint32)), (key, loss[-4:], ref_loss[-4:])
             tl, tc = g[key + "_trees"]

@@ -1,0 +1,156 @@
+"""GPU: every complete tree's loss is the reference's in-order loss fold (round 6).
+
+The reference scores a complete tree with LossFunctions' `mean(loss, x, y)` / `sum(loss, x, y, w;
+normalize=true)` (src/LossFunctions.jl:38-58): the elementwise losses folded left to right in T, then
+divided in T.  Rounds 1-5 returned the f64 sum instead (~5e-4 relative off at 2^20 rows in Float32).
+The library now computes the fold itself for every complete tree (csrc/sr_fold_dev.h): a plan from the
+loss launch's f64 partials, each row block's composed steps (from the stored losses of a small call, or
+from a FOLD-mode pass of the interpreter in a large one), and a walk over the row blocks.  So:
+
+* the device loss equals a sequential Float32 fold (numpy's add.accumulate) of the device's OWN
+  predictions bit for bit, for every complete tree, on both paths and at 2^20 rows;
+* the two paths and the prediction-pass fallback give the same bits;
+* against the oracle's `accum="ref"` (the C restatement of the reference's evaluator and fold): bit for
+  bit for every tree without a transcendental, and for the rest within the libm bar.
+"""
+import numpy as np
+import pytest
+
+import sr_amd
+from sr_amd import Dataset, Options, eval_loss_batch, eval_tree_array_batch, flatten_trees, gen_random_population
+
+pytestmark = pytest.mark.gpu
+
+OPTS = dict(binary_operators=["+", "-", "*", "/"], unary_operators=["cos", "exp", "log"])
+
+
+def _data(n, seed=2, weighted=False):
+    rng = np.random.default_rng(seed)
+    X = rng.standard_normal((5, n)).astype(np.float32)
+    y = (2 * np.cos(X[3]) + X[0] ** 2 - 2 + 0.1 * rng.standard_normal(n)).astype(np.float32)
+    w = (0.25 + rng.random(n)).astype(np.float32) if weighted else None
+    return X, y, w
+
+
+def _jl_sum32(v):
+    """Base.sum of a Float32 vector: mapreduce_impl's pairwise recursion, leaves of < 1024 folded in order."""
+    def rec(lo, hi):
+        if hi - lo < 1024:
+            return np.add.accumulate(v[lo:hi + 1], dtype=np.float32)[-1]
+        mid = lo + ((hi - lo) >> 1)
+        return np.float32(rec(lo, mid) + rec(mid + 1, hi))
+    return np.float32(rec(0, len(v) - 1))
+
+
+def _np_fold_losses(pred, y, w=None):
+    """LossFunctions' L2 mean (or weighted sum / sum(w)) of the given predictions, in Float32 and in row
+    order: numpy's add.accumulate is a sequential left fold."""
+    d = (pred - y).astype(np.float32)
+    lo = d * d
+    if w is not None:
+        lo = (lo * w).astype(np.float32)
+    total = np.add.accumulate(lo, dtype=np.float32)[-1]
+    den = _jl_sum32(w) if w is not None else np.float32(len(y))
+    return np.float32(total / den)
+
+
+def _bits(a):
+    return np.asarray(a, dtype=np.float32).view(np.uint32)
+
+
+def _run(tb, ds, opts, **knobs):
+    ctx = sr_amd.get_context()
+    for k, v in knobs.items():
+        ctx.set_tuning(k, v)
+    try:
+        loss, comp = eval_loss_batch(tb, ds, opts)
+        info = ctx.last_ref_fold()
+    finally:
+        ctx.set_tuning("ref_fold", 1)
+        ctx.set_tuning("fold_store_mb", 512)
+        ctx.set_tuning("fold_delta_log2", 8)
+        ctx.set_tuning("fold_debug_fail", 0)
+    return loss, comp, info
+
+
+@pytest.mark.parametrize("weighted", [False, True])
+def test_fold_equals_sequential_fold_of_device_predictions(weighted):
+    """Both paths (stored losses / FOLD mode) and a window so narrow that trees fall back to the
+    prediction pass: every complete tree's loss is the sequential Float32 fold of its device
+    predictions, bit for bit; ref_fold = 0 keeps the f64 sums (which differ in the last bits)."""
+    n = 40_000
+    X, y, w = _data(n, weighted=weighted)
+    opts = Options(**OPTS)
+    tb = flatten_trees(gen_random_population(1200, opts, 5, max_size=30, seed=7), np.float32)
+    ds = Dataset(X, y, weights=w)
+    l_s, c_s, i_s = _run(tb, ds, opts)
+    assert i_s["path"] == 1 and i_s["folded"] > 300, i_s
+    l_l, c_l, i_l = _run(tb, ds, opts, fold_store_mb=0)
+    assert i_l["path"] == 2 and i_l["folded"] > 300, i_l
+    # (every third tree through the fallback — the prediction pass and the segmented fold — as if its walk
+    #  had left the plan's window; and a window of 2^-30 around the f64 prefix: far fewer slow segments)
+    l_n, c_n, i_n = _run(tb, ds, opts, fold_store_mb=0, fold_delta_log2=30, fold_debug_fail=3)
+    assert i_n["fallback"] > 100, i_n
+    l_0, c_0, i_0 = _run(tb, ds, opts, ref_fold=0)
+    assert i_0["path"] == 0
+    for c in (c_l, c_n, c_0):
+        assert np.array_equal(c, c_s)
+    fin = c_s & np.isfinite(l_s)
+    assert np.array_equal(_bits(l_s[fin]), _bits(l_l[fin]))
+    assert np.array_equal(_bits(l_s[fin]), _bits(l_n[fin]))
+    assert not np.array_equal(_bits(l_s[fin]), _bits(l_0[fin]))  # (the f64 sums: other last bits)
+    pred, pcomp = eval_tree_array_batch(tb, ds, opts)
+    idx = np.nonzero(fin)[0]
+    want = np.array([_np_fold_losses(pred[t], y, w) for t in idx], dtype=np.float32)
+    bad = idx[_bits(l_s[idx]) != _bits(want)]
+    assert bad.size == 0, (bad[:5], l_s[bad[:5]], want[:5])
+
+
+def test_fold_at_2p20_rows_c2_distribution():
+    """C2's distribution at its full row count (FOLD-mode path): a 1,000-tree sample of the C2
+    population generator, every complete tree's loss the sequential Float32 fold of its predictions."""
+    n = 1 << 20
+    X, y, _ = _data(n, seed=2)
+    opts = Options(**OPTS)
+    tb = flatten_trees(gen_random_population(1000, opts, 5, max_size=30, seed=1), np.float32)
+    ds = Dataset(X, y)
+    loss, comp, info = _run(tb, ds, opts)
+    assert info["path"] == 2, info
+    fin = comp & np.isfinite(loss)
+    assert info["folded"] + info["fallback"] >= int(fin.sum()) - 5, (info, int(fin.sum()))
+    idx = np.nonzero(fin)[0]
+    rng = np.random.default_rng(0)
+    pick = np.sort(rng.choice(idx, size=min(120, idx.size), replace=False))
+    sub = tb.take(pick)
+    pred, _ = eval_tree_array_batch(sub, ds, opts)
+    want = np.array([_np_fold_losses(pred[k], y) for k in range(len(pick))], dtype=np.float32)
+    assert np.array_equal(_bits(loss[pick]), _bits(want)), (loss[pick][:4], want[:4])
+    # the f64 sum differs from the fold by ~5e-4 relative here (what rounds 1-5 returned)
+    l64, _, _ = _run(tb, ds, opts, ref_fold=0)
+    rel = np.abs(l64[fin].astype(np.float64) - loss[fin]) / np.abs(loss[fin].astype(np.float64))
+    assert float(np.median(rel)) > 1e-5
+
+
+def test_fold_vs_oracle_reference_accumulation():
+    """Against the oracle's accum="ref" (the C restatement of DE's evaluator and of LossFunctions'
+    fold): every complete tree built from + - * / only equals it bit for bit; the others (Float32
+    cos / exp / log: last-bit libm differences) within 1e-4, most bit for bit."""
+    from oracle import Oracle
+
+    n = 30_000
+    X, y, _ = _data(n, seed=5)
+    opts = Options(**OPTS)
+    tb = flatten_trees(gen_random_population(800, opts, 5, max_size=30, seed=3), np.float32)
+    loss, comp, info = _run(tb, Dataset(X, y), opts)
+    ref, rcomp = Oracle.from_options(opts).eval_loss_batch(tb, X, y, accum="ref", n_threads=8)
+    assert np.array_equal(comp, rcomp)
+    fin = comp & np.isfinite(ref)
+    deg = np.asarray(tb.degree)
+    offs = np.asarray(tb.offsets)
+    arith = np.array([not np.any(deg[offs[t]:offs[t + 1]] == 1) for t in range(tb.n_trees)])
+    sel = fin & arith
+    assert sel.sum() > 50
+    assert np.array_equal(_bits(loss[sel]), _bits(ref[sel]))
+    rel = np.abs(loss[fin].astype(np.float64) - ref[fin]) / np.maximum(np.abs(ref[fin].astype(np.float64)), 1e-30)
+    assert float(np.max(rel)) < 1e-4
+    assert float(np.mean(_bits(loss[fin]) == _bits(ref[fin]))) > 0.9

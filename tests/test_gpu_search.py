@@ -65,20 +65,21 @@ def _c3_data(n=100_000, seed=11):
 
 
 def test_c3_search_device_equals_oracle_scored_search(monkeypatch):
-    """The same seeded C3 search scored on the device and by the CPU oracle (same trees, data, seeds,
-    random streams): identical populations and hall of fame.  Scores agree to the loss bar; every
-    selection / acceptance decision therefore agrees unless two candidates tie within it, which does
-    not happen on this run (the test would show it)."""
+    """The same seeded C3 search scored on the device and by the CPU oracle with the REFERENCE's
+    accumulation (accum="ref": LossFunctions' in-order Float32 fold, which the device computes too since
+    round 6; same trees, data, seeds, random streams): identical populations and hall of fame at 8
+    islands x 50 cycles.  Losses agree bit for bit but for last-bit libm differences (cos / exp / log,
+    DESIGN §4.5); every selection / acceptance decision agrees (the test would show a tie it broke)."""
     from oracle import Oracle
 
     X, y = _c3_data()
-    opts = Options(binary_operators=["+", "-", "*", "/"], unary_operators=["cos", "exp", "log"], populations=4,
-                   population_size=20, ncycles_per_iteration=12, maxsize=20, should_optimize_constants=False)
+    opts = Options(binary_operators=["+", "-", "*", "/"], unary_operators=["cos", "exp", "log"], populations=8,
+                   population_size=20, ncycles_per_iteration=50, maxsize=20, should_optimize_constants=False)
     orc = Oracle.from_options(opts)
 
     def oracle_loss(tb, rows):
         Xv, yv = (X, y) if rows is None else (X[:, rows], y[rows])
-        losses, comp = orc.eval_loss_batch(tb, Xv, yv, accum="f64", n_threads=8)
+        losses, comp = orc.eval_loss_batch(tb, Xv, yv, accum="ref", n_threads=8)
         return np.where(comp, losses, np.inf)
 
     dev = equation_search(X, y, niterations=2, options=opts, seed=5)
@@ -88,12 +89,16 @@ def test_c3_search_device_equals_oracle_scored_search(monkeypatch):
         return [[string_tree(m.tree, opts.operators) for m in p] for p in res.populations]
 
     assert trees(dev) == trees(ref)
+    n_exact = n_fin = 0
     for pd, pr in zip(dev.populations, ref.populations):
         ld = np.array([m.loss for m in pd], dtype=np.float64)
         lr = np.array([m.loss for m in pr], dtype=np.float64)
         assert np.array_equal(np.isfinite(ld), np.isfinite(lr))
         fin = np.isfinite(lr)
-        np.testing.assert_allclose(ld[fin], lr[fin], rtol=1e-4)
+        np.testing.assert_allclose(ld[fin], lr[fin], rtol=1e-5)
+        n_exact += int(np.sum(ld[fin] == lr[fin]))
+        n_fin += int(fin.sum())
+    assert n_exact >= 0.9 * n_fin, (n_exact, n_fin)  # (the rest: libm last bits)
     assert ([string_tree(m.tree, opts.operators) for m in dev.pareto_frontier] ==
             [string_tree(m.tree, opts.operators) for m in ref.pareto_frontier])
     # several scoring lanes (the default) split each round's launch; one unpipelined lane makes
@@ -101,7 +106,7 @@ def test_c3_search_device_equals_oracle_scored_search(monkeypatch):
     # halves of a lane's islands, one call in flight each) changes any result
     one = equation_search(X, y, niterations=2, options=opts, seed=5, scoring_lanes=1)
     assert trees(one) == trees(ref)
-    assert one.device_calls == ref.device_calls > 40
+    assert one.device_calls == ref.device_calls > 100
     assert dev.device_calls > ref.device_calls
     monkeypatch.setenv("SR_AMD_SEARCH_PIPELINE", "1")
     piped = equation_search(X, y, niterations=2, options=opts, seed=5, scoring_lanes=1)
