@@ -920,7 +920,7 @@ def search_lines(args):
     o5 = Options(binary_operators=["+", "-", "*", "/"], unary_operators=["cos", "exp", "log"], populations=32,
                  should_optimize_constants=True)
     for name, X, y, o, cpu_iters, cpu_threads, desc in (
-            ("c1", X1, y1, o1, args.search_cpu_iters or args.search_iters, 1,
+            ("c1", X1, y1, o1, args.search_cpu_iters or args.search_iters, threads,
              "C1 README example: X=randn(2,100) f64, ops + * / - cos exp, 20 populations, default options"),
             ("c3", X3, y3, o3, args.search_cpu_iters or 2, threads,
              "C3: y = x1 x2 x3 / (x4 x5^2 + 1), X ~ U(0.5, 2) 5 x 100k f32, 31 populations, default options"),

@@ -92,10 +92,6 @@ int sr_version(void);
 int sr_device_count(int* count);
 /* Open a context on HIP device `device` (one process per GPU: pass LOCAL_RANK). */
 int sr_init(int device, sr_ctx** out);
-/* A second context on `parent`'s device and HIP stream (one hardware queue for both), using the
- * parent's datasets and the operator sets / losses registered on it so far (same ids): a host thread
- * can keep one call in flight on each (sr_eval_loss_submit).  Shut it down before the parent. */
-int sr_init_shared(sr_ctx* parent, sr_ctx** out);
 int sr_shutdown(sr_ctx* ctx);
 
 /*
@@ -145,19 +141,6 @@ int sr_eval_loss_batch_views(sr_ctx* ctx, const sr_dataset* ds, int opset_id, co
                              const int32_t* tree_view, int n_views, const int64_t* view_rows, int64_t view_len,
                              int loss_kind, void* out_loss, uint8_t* out_complete);
 
-/*
- * The same call in two halves: _submit compiles, stages and launches it and returns; _wait finishes it
- * (waits for the device, runs the rare exact-sum / in-order fold passes, finalizes) and fills the
- * outputs given at submit.  n_views <= 1: one view (view_rows = NULL: the full dataset, else view_len
- * rows).  One pending call per context; every array the call reads (trees, views, outputs) must stay
- * valid until _wait returns; other calls on the context are refused meanwhile.  Results equal the
- * synchronous call's.  With sr_init_shared a host thread keeps two calls in flight on one stream: the
- * search overlaps one half of a lane's islands' host work with the other half's device work.
- */
-int sr_eval_loss_submit(sr_ctx* ctx, const sr_dataset* ds, int opset_id, const sr_tree_batch* trees,
-                        const int32_t* tree_view, int n_views, const int64_t* view_rows, int64_t view_len, int loss_kind,
-                        void* out_loss, uint8_t* out_complete);
-int sr_eval_loss_wait(sr_ctx* ctx);
 
 /*
  * Batched eval_tree_array (src/InterfaceDynamicExpressions.jl:58-88): predictions
@@ -467,8 +450,7 @@ int sr_last_phase_ms(sr_ctx* ctx, double* out, int n);
  * call; Float32 16 / 32 force the register-stack kernel and 4 / 8 the LDS-stack one, Float64 8 / 4
  * likewise), "balance" (0 / 1: deal the cost-ordered trees round-robin over tree groups),
  * "fused_reduce" (the largest tree group, in trees x row blocks, whose partials the interpreter launch
- * reduces itself — its last workgroup per group; 0: always a separate reduce launch), "spec_exact" (0 / 1: the
- * speculative exact-sum pass, off by default, sr_spec_exact_info), "exact_w" (4 / 1:
+ * reduces itself — its last workgroup per group; 0: always a separate reduce launch), "exact_w" (4 / 1:
  * waves per workgroup of the exact-sum pass), "exact_g" (listed trees per exact-sum workgroup; 0: the
  * heuristic), "fold_seg" (rows per segment of the in-order loss fold: -1 automatic, 0 one workgroup
  * scan over every row per tree, as rounds 3-4), "ref_fold" (1, the default: every complete tree's loss
@@ -488,11 +470,6 @@ int sr_set_tuning(sr_ctx* ctx, const char* name, int64_t value);
  * work items and rows per lane. */
 int sr_last_grad_info(sr_ctx* ctx, int n, double* kernel_ms, double* flops, int64_t* items, int* rows_per_lane);
 int sr_tuning_info(sr_ctx* ctx, int* used_derived_columns, int64_t* exact_trees);
-/* The last sr_eval_loss_batch's speculative exact-sum pass (tuning "spec_exact", default off): trees the
- * dead-tree probe flagged BIG, whose pass ran during the main launch (`speculated`), and how many of
- * them the main launch flagged BIG too (`used`: their verdicts were taken; the rest of its BIG trees
- * took the pass afterwards).  Verdicts do not depend on it. */
-int sr_spec_exact_info(sr_ctx* ctx, int64_t* speculated, int64_t* used);
 /* The last sr_eval_loss_batch(_views)'s in-order loss fold (tuning "ref_fold"; each output may be NULL):
  * the path (0 none — "ref_fold" 0, negative weights, a row-sharded call, or a Float64 call too large
  * to keep its losses; 1 the loss launch kept every tree's losses; 2 the FOLD-mode pass re-ran the

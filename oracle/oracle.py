@@ -105,7 +105,7 @@ class Oracle:
             raise ValueError("oracle: malformed tree")
         return out, bool(comp.value)
 
-    def eval_loss_batch(self, tb, X, y, w=None, loss_kind=0, accum="f64", n_threads=1, perturb=0, loss_param=0.0):
+    def eval_loss_batch(self, tb, X, y, w=None, loss_kind=0, accum="ref", n_threads=1, perturb=0, loss_param=0.0):
         X = np.asarray(X)
         dtype = X.dtype
         Xj = np.ascontiguousarray(X.T)

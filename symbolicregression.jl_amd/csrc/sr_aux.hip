@@ -741,7 +741,8 @@ __global__ void __launch_bounds__(256) sr_fold_stab_kernel(const double* __restr
 // round at an exact half ulp): every step is rint(l 2^-q) whatever the parity, so the compositions are
 // plain sums; otherwise the pair composition (sr_fold_add_i / sr_fold_compose_i).
 template <typename T, int RW>
-__device__ T sr_fold_rows_wave(const T* __restrict__ base, int64_t lo, int64_t k, int64_t hi, T F, int lane) {
+__device__ T sr_fold_rows_wave(const T* __restrict__ base, int64_t lo, int64_t k, int64_t hi, T F, int lane,
+                               int& rounds) {
   using Tr = SrFoldTraits<T>;
   using I = typename SrFoldTab<T>::I;
   constexpr I CAP = I(1) << (Tr::mant + 3);
@@ -767,6 +768,7 @@ __device__ T sr_fold_rows_wave(const T* __restrict__ base, int64_t lo, int64_t k
       }
     }
     while (k < hi && k < pass_end) {
+      ++rounds;
       if (!(F <= SrM<T>::big)) return F;  // +Inf / NaN stays
       int q;
       I lim;
@@ -807,7 +809,11 @@ __device__ T sr_fold_rows_wave(const T* __restrict__ base, int64_t lo, int64_t k
           if (lane >= off) inc = inc + o < CAP ? inc + o : CAP;
         }
         i0 = i1 = inc;
-        x0 = x1 = inc - a;
+        // (the exclusive prefix from the lane before: an inclusive prefix may have saturated at CAP, the
+        //  one before the first lane that leaves the binade has not)
+        x0 = __shfl_up(inc, 1, 64);
+        if (lane == 0) x0 = 0;
+        x1 = x0;
       } else {
         I a0 = 0, a1 = 0;
 #pragma unroll
@@ -882,12 +888,14 @@ __global__ void __launch_bounds__(256) sr_fold_walk_kernel(const int32_t* __rest
                                                            const T* __restrict__ losses, int64_t slot_rows,
                                                            const uint32_t* __restrict__ perm,
                                                            const T* __restrict__ carry, T* __restrict__ out_val,
-                                                           int32_t* __restrict__ out_st) {
+                                                           int32_t* __restrict__ out_st, int4* __restrict__ dbg) {
   using Tr = SrFoldTraits<T>;
   using I = typename SrFoldTab<T>::I;
   constexpr I CAP = I(1) << (Tr::mant + 3);
   constexpr T MIN_NORMAL = sizeof(T) == 4 ? T(1.17549435e-38f) : T(2.2250738585072014e-308);
   const int lane = int(threadIdx.x) & 63;
+  const uint64_t clk0 = dbg ? wall_clock64() : 0;
+  int n_slow = 0, n_rounds = 0, n_runs = 0;  // (SR_AMD_FOLD_STATS: per-tree walk statistics)
   const int p = int(blockIdx.x) * 4 + int(threadIdx.x) / 64;
   if (p >= np) return;  // wave-uniform
   const uint32_t t = perm ? perm[p] : uint32_t(p);
@@ -946,7 +954,8 @@ __global__ void __launch_bounds__(256) sr_fold_walk_kernel(const int32_t* __rest
           fail = true;
           break;
         }
-        F = sr_fold_rows_wave<T, RW>(seg_base(c), lo, k, hi, F, lane);
+        F = sr_fold_rows_wave<T, RW>(seg_base(c), lo, k, hi, F, lane, n_rounds);
+        ++n_slow;
         k = hi;
         if (!(F <= SrM<T>::big)) fail = true;  // (an overflow: not the plan's case)
         ++pos;
@@ -980,6 +989,7 @@ __global__ void __launch_bounds__(256) sr_fold_walk_kernel(const int32_t* __rest
         break;
       }
       F = T(ldexp(double(P + g), q));
+      ++n_runs;
       const int64_t hl = int64_t(c0 + e) * rb_rows;
       k = hl < n ? hl : n;
       pos = e;
@@ -988,6 +998,7 @@ __global__ void __launch_bounds__(256) sr_fold_walk_kernel(const int32_t* __rest
   if (lane == 0) {
     out_val[t] = F;
     out_st[t] = fail ? SR_FST_FAIL : SR_FST_OK;
+    if (dbg) dbg[t] = make_int4(n_slow, n_rounds, n_runs, int((wall_clock64() - clk0) / 100));  // (us: 100 MHz)
   }
 }
 
@@ -1011,11 +1022,11 @@ hipError_t sr_launch_fold_stab(const double* part, int np, int n_rb, int64_t rb_
 template <typename T>
 hipError_t sr_launch_fold_walk(const int32_t* code, const void* tab, int np, int n_rb, int64_t rb_rows, int64_t n,
                                const T* losses, int64_t slot_rows, const uint32_t* perm, const T* carry, T* out_val,
-                               int32_t* out_st, hipStream_t s) {
+                               int32_t* out_st, void* dbg, hipStream_t s) {
   if (np <= 0) return hipSuccess;
   hipLaunchKernelGGL((sr_fold_walk_kernel<T, sizeof(T) == 4 ? 16 : 8>), dim3(unsigned((np + 3) / 4)), dim3(256), 0, s, code,
                      static_cast<const typename SrFoldTab<T>::Pair*>(tab), np, n_rb, rb_rows, n, losses, slot_rows, perm,
-                     carry, out_val, out_st);
+                     carry, out_val, out_st, static_cast<int4*>(dbg));
   return hipGetLastError();
 }
 #define SR_INSTANTIATE_FOLD2(T)                                                                                      \
@@ -1024,7 +1035,7 @@ hipError_t sr_launch_fold_walk(const int32_t* code, const void* tab, int np, int
   template hipError_t sr_launch_fold_stab<T>(const double*, int, int, int64_t, int64_t, const uint32_t*,              \
                                              const SrFoldWho&, double, const T*, int32_t*, void*, hipStream_t);        \
   template hipError_t sr_launch_fold_walk<T>(const int32_t*, const void*, int, int, int64_t, int64_t, const T*, int64_t, \
-                                             const uint32_t*, const T*, T*, int32_t*, hipStream_t);
+                                             const uint32_t*, const T*, T*, int32_t*, void*, hipStream_t);
 SR_INSTANTIATE_FOLD2(float)
 SR_INSTANTIATE_FOLD2(double)
 

@@ -79,7 +79,7 @@ struct DevBuf {
 struct HostBuf {
   void* p = nullptr;
   size_t cap = 0;
-  unsigned flags = hipHostMallocDefault;  // (SR_AMD_PROG_NC: the program staging buffer non-coherent)
+  unsigned flags = hipHostMallocDefault;
   hipError_t ensure(size_t bytes, hipStream_t s, hipStream_t s2) {
     if (bytes <= cap) return hipSuccess;
     if (p) {
@@ -194,15 +194,11 @@ struct sr_ctx {
   size_t outs_flag_off = 0;
   // Small single-chunk LOSS calls (the search's regime: tens of trees, ~100 rows) are latency-bound:
   // SR_AMD_HOST_IO = 1 (default) lets the kernel write the per-tree results straight into pinned
-  // host memory (no copy back), 2 also lets it read the programs from the pinned staging buffer (no
-  // upload), 0 keeps both copies.
+  // host memory (no copy back); 0 copies them.  (Round 5's 2 — programs read from the pinned staging
+  // buffer — was measured without payoff and removed in round 6.)
   int host_io = 1;
   bool want_host_out = false;  // set by eval_loss_impl around its run_batch
   bool outs_on_host = false;   // the last run_batch wrote {Σ, flags} to h_outs
-  // SR_AMD_SPIN = 1: small calls wait by polling hipStreamQuery instead of hipStreamSynchronize
-  // (measured slower on the box: 61 vs 50 us per 20-tree call, the polling slows the runtime's other
-  // threads; off by default)
-  int spin = 0;
   uint32_t hint_epoch = 0;  // dead-tree hint epoch of the current call
   int debug_hint_regrow = 0;       // tests (sr_set_tuning "debug_hint_regrow"): grow the hint array in place
   void* hint_reserve = nullptr;    // its fixed-address reservation
@@ -229,47 +225,12 @@ struct sr_ctx {
   // SR_AMD_EXACT_LIST_HOST (default 1): the pass reads its tree list from the pinned staging buffer
   // (no upload ahead of the kernel); 0 copies it to the device first
   int exact_list_host = 1;
-  // Speculative exact-sum pass (round 5; SR_AMD_SPEC_EXACT / "spec_exact", default 0).  A large
-  // one-view LOSS call's dead-tree probe runs its trees over the dataset's stress rows (the extremes of
-  // every feature) before the main launch; a tree the probe already flags BIG (and not non-finite) is
-  // BIG on the whole view too (the same thresholds over a subset of the rows), so its exact pass starts
-  // on a third stream while the main launch runs, instead of after it.  The main launch's flags still
-  // decide: a BIG tree the probe missed takes the ordinary pass afterwards, and a speculated tree the
-  // main launch finds non-finite or not BIG leaves its verdict unused.  Verdicts are the same either way.
-  // Off by default: measured neutral on C2's step and -3 % on the tree-sharding share
-  // (profiles/r05_ab_spec_exact.txt), but the pass shares the CUs with the main launch, whose measured
-  // duration (the roofline's denominator) then carries the pass's work.
-  int spec_exact = 0;
-  bool want_spec = false;  // set by eval_loss_submit around its run_batch (one full view, no gather)
-  hipStream_t stream3 = nullptr;
-  // (SR_AMD_SPEC_PRIO: the third stream's priority, -1 the least, 0 normal, 1 the greatest)
-  int spec_prio = -1;
-  hipError_t need_stream3() {
-    if (stream3) return hipSuccess;
-    int least = 0, greatest = 0;
-    if (spec_prio == 0 || hipDeviceGetStreamPriorityRange(&least, &greatest) != hipSuccess)
-      return hipStreamCreateWithFlags(&stream3, hipStreamNonBlocking);
-    return hipStreamCreateWithPriority(&stream3, hipStreamNonBlocking, spec_prio < 0 ? least : greatest);
-  }
-  hipEvent_t ev_pr[kMaxChunks] = {};  // after each probed chunk's probe (cross-stream, untimed)
-  hipEvent_t ev_spec = nullptr;       // after the probe flags' copies on stream3
-  HostBuf h_pflag;                    // the probes' per-(tile, position) flags, copied back on stream3
-  struct SpecChunk {
-    int64_t t0, np;  // a probed launch: positions [0, np) of the chunk starting at tree t0
-  };
-  std::vector<SpecChunk> spec_chunks;  // this call's probed launches (set by run_batch)
-  std::vector<int64_t> spec_list;      // trees whose exact pass is in flight on stream3
-  std::vector<uint8_t> spec_ok;        // ... their verdicts once collected
-  int spec_mc = 0;                     // ... their check slots
-  size_t spec_fin_off = 0;             // ... where their verdicts land in h_exact
-  bool spec_pending = false;
-  int64_t n_spec_last = 0, n_spec_used_last = 0;  // speculated trees of the last call, and those used
 #ifdef SR_STAMPS
   DevBuf stamps;  // latency-analysis builds: the last main launch's per-wave stamps (sr_debug_stamps)
   int64_t n_stamps = 0;
 #endif
   int stress_probe = 1;  // SR_AMD_STRESS_PROBE: the probe runs the dataset's stress rows (below)
-  int code_cache = 1;    // SR_AMD_CODE_CACHE: LDS program cache (1: register-stack launches, 2: also the classic ones)
+  int code_cache = 1;    // SR_AMD_CODE_CACHE: LDS program cache of the register-stack launches (0: off)
   // SR_AMD_FUSED_REDUCE: multi-row-block LOSS launches reduce their partials in the launch (the last
   // workgroup of a tree group) when the group holds at most this many partials; 0 (default): a reduce
   // launch — measured faster: every workgroup's drained stores + barrier + counter add cost more than
@@ -313,13 +274,6 @@ struct sr_ctx {
     for (double& v : phase_ms) v = 0.0;
   }
   bool internal_pass = false;  // the fold's PRED passes: run_batch leaves the call's phase clock alone
-  // Asynchronous loss calls (sr_eval_loss_submit / sr_eval_loss_wait, round 5): the pending call's
-  // second half, and the event after its device work (a context made by sr_init_shared runs on
-  // another context's stream, which may hold that context's later calls: waits go to the event)
-  std::function<int()> pending;
-  hipEvent_t ev_done = nullptr;
-  bool owns_stream = true;
-  sr_ctx* parent = nullptr;  // sr_init_shared: the context whose stream, datasets, opsets and losses it uses
   void mark_phase(int i) {
     if (internal_pass) return;
     const auto now = std::chrono::steady_clock::now();
@@ -359,6 +313,8 @@ struct sr_ctx {
   // within 2.1e-3 of the f64 sum at 2^20 rows; 2^-6 kept twice the slow segments)
   int fold_delta_log2 = 8;
   int fold_debug_fail = 0;   // (tests: "fold_debug_fail")
+  int fold_stats = 0;        // SR_AMD_FOLD_STATS=1: per-tree walk statistics to stderr after each call (analysis)
+  DevBuf fold_dbg;
   bool want_fold = false;    // set by eval_loss_submit around its run_batch
   int fold_path_last = 0;    // 0 none, 1 stored losses, 2 FOLD mode
   DevBuf fold_code, fold_tab, fold_store, fold_ctl, fold_io2;
@@ -469,9 +425,8 @@ int check_ctx(sr_ctx* ctx) {
 
 int validate_common(sr_ctx* ctx, const sr_dataset* ds, int opset_id, const sr_tree_batch* trees) {
   if (check_ctx(ctx) != SR_OK) return SR_ERR_INVALID_ARG;
-  if (!ds || (ds->ctx != ctx && ds->ctx != ctx->parent))
+  if (!ds || ds->ctx != ctx)
     return set_error(SR_ERR_INVALID_ARG, "dataset is NULL or belongs to another context");
-  if (ctx->pending) return set_error(SR_ERR_INVALID_ARG, "a submitted call is pending on this context: sr_eval_loss_wait first");
   if (opset_id < 0 || opset_id >= int(ctx->opsets.size()))
     return set_error(SR_ERR_INVALID_ARG, "unknown opset id " + std::to_string(opset_id));
   if (!trees) return set_error(SR_ERR_INVALID_ARG, "NULL tree batch");
@@ -640,24 +595,16 @@ int fold_walk(sr_ctx* ctx, const FoldJob<T>& job, const FoldRegion<T>& fr, const
   const void* tab = ctx->fold_tab.as<char>() + off * sizeof(typename SrFoldTab<T>::Pair);
   const T* losses = job.path == 1 ? fr.a.fold_loss : ctx->fold_store.as<T>();
   const int64_t slot_rows = job.path == 1 ? rb_rows : job.slot_rows;
+  int4* dbg = ctx->fold_stats ? ctx->fold_dbg.as<int4>() + fr.t0 : nullptr;  // (SR_AMD_FOLD_STATS)
   SR_HIP_CHECK(sr_launch_fold_walk<T>(code, tab, int(fr.np), nrb, rb_rows, job.n_eval, losses, slot_rows, fr.a.perm,
-                                      carry ? carry + fr.t0 : nullptr, out_val + fr.t0, out_st + fr.t0, cs));
+                                      carry ? carry + fr.t0 : nullptr, out_val + fr.t0, out_st + fr.t0, dbg, cs));
   return SR_OK;
-}
-
-// The speculative exact pass's stream (sr_ctx::spec_exact) drained: nothing of an earlier call (its
-// probe-flag copies, a pass an error path left running) may still use h_pflag / h_exact.
-inline void spec_drain(sr_ctx* ctx) {
-  if (ctx->stream3) (void)hipStreamSynchronize(ctx->stream3);  // (only contexts that ever speculated have one)
-  ctx->spec_pending = false;
-  ctx->spec_chunks.clear();
 }
 
 template <typename T>
 int run_batch(sr_ctx* ctx, const sr_dataset* ds, int opset_id, const sr_tree_batch* trees, const int64_t* row_idx,
               int64_t n_idx, int64_t n_total, int loss_kind, int mode, SrProgramBatch<T>* prog, Grid* grid_out,
               bool allow_derived = false, const ShardCtl* shard = nullptr, const ViewSpec* views = nullptr) {
-  spec_drain(ctx);
   const bool gather = row_idx != nullptr && n_idx > 0;
   // PRED passes (the fold's few band trees) write no partials: more row blocks fill the GPU (C4's 14 trees
   // x 2^26 rows ran 1,024 workgroups at 256)
@@ -745,7 +692,7 @@ int run_batch(sr_ctx* ctx, const sr_dataset* ds, int opset_id, const sr_tree_bat
   const size_t prog_bytes = o_seg + n_seg_cap * sizeof(SrSegment);
   SR_HIP_CHECK(ctx->prog.ensure(prog_bytes));
   SR_HIP_CHECK(ctx->h_prog.ensure(prog_bytes, s, ctx->stream2));
-  char* const dprog = ctx->prog.as<char>();  // (re-pointed at the staging buffer below for host_prog)
+  char* const dprog = ctx->prog.as<char>();
   ctx->d_code = dprog;
   ctx->d_off = reinterpret_cast<uint32_t*>(dprog + o_off);
   ctx->d_bad = reinterpret_cast<uint8_t*>(dprog + o_bad);
@@ -796,6 +743,10 @@ int run_batch(sr_ctx* ctx, const sr_dataset* ds, int opset_id, const sr_tree_bat
       SR_HIP_CHECK(ctx->fold_ctl.ensure(64));
       SR_HIP_CHECK(hipMemsetAsync(ctx->fold_ctl.p, 0, sizeof(int), s));  // the call's slot counter
     }
+    if (fold_path && ctx->fold_stats) {
+      SR_HIP_CHECK(ctx->fold_dbg.ensure(size_t(nt) * sizeof(int4) + 16));
+      SR_HIP_CHECK(hipMemsetAsync(ctx->fold_dbg.p, 0, size_t(nt) * sizeof(int4), s));
+    }
     if (fold_path) {
       SR_HIP_CHECK(ctx->fold_code.ensure(n_part * sizeof(int32_t) + 4));
       SR_HIP_CHECK(ctx->fold_tab.ensure(n_part * sizeof(typename SrFoldTab<T>::Pair) + 16));
@@ -816,7 +767,6 @@ int run_batch(sr_ctx* ctx, const sr_dataset* ds, int opset_id, const sr_tree_bat
   const bool small_call = n_chunks == 1 && mode == SR_MODE_LOSS;
   // (under the in-order fold the plan reads the call's flags and partials on the device)
   const bool host_out = small_call && ctx->host_io >= 1 && ctx->want_host_out && fold_path == 0;
-  const bool host_prog = small_call && ctx->host_io >= 2;
   if (host_out) SR_HIP_CHECK(ctx->h_outs.ensure(outs_bytes, s, ctx->stream2));
   ctx->outs_on_host = host_out;
   const bool host_red = host_out && ctx->host_reduce > 0 && !multi && n_rb > 1 && int64_t(n_part) <= ctx->host_reduce;
@@ -894,13 +844,6 @@ int run_batch(sr_ctx* ctx, const sr_dataset* ds, int opset_id, const sr_tree_bat
   prog->total_nodes = 0;
   prog->total_ops = 0;
   char* const hprog = ctx->h_prog.as<char>();
-  if (host_prog) {
-    ctx->d_code = hprog;
-    ctx->d_off = reinterpret_cast<uint32_t*>(hprog + o_off);
-    ctx->d_bad = reinterpret_cast<uint8_t*>(hprog + o_bad);
-    ctx->d_perm = reinterpret_cast<uint32_t*>(hprog + o_perm);
-    ctx->d_end = reinterpret_cast<uint32_t*>(hprog + o_end);
-  }
   SrIns<T>* h_code = reinterpret_cast<SrIns<T>*>(hprog);
   uint32_t* h_off = reinterpret_cast<uint32_t*>(hprog + o_off);
   uint8_t* h_bad = reinterpret_cast<uint8_t*>(hprog + o_bad);
@@ -950,13 +893,6 @@ int run_batch(sr_ctx* ctx, const sr_dataset* ds, int opset_id, const sr_tree_bat
     SR_HIP_CHECK(ctx->probe_derived.ensure(size_t(spec.n) * size_t(kProbeRows) * sizeof(T)));
     SR_HIP_CHECK(sr_launch_derived<T>(static_cast<const T*>(ds->X), ds->ld, static_cast<const int64_t*>(ds->probe_rows),
                                       ds->n_probe, kProbeRows, spec, ctx->probe_derived.as<T>(), kProbeRows, s));
-  }
-  // the speculative exact-sum pass (sr_ctx::spec_exact): each probe's flags come back on a third
-  // stream while the main launches run (each probed launch writes its own part of the scratch)
-  const bool spec_x = stress_probe && mode == SR_MODE_LOSS && ctx->spec_exact && ctx->want_spec && !shard;
-  if (spec_x) {
-    SR_HIP_CHECK(ctx->need_stream3());
-    SR_HIP_CHECK(ctx->h_pflag.ensure(size_t(nt) * kProbeTiles * sizeof(uint32_t) + 16, ctx->stream3, nullptr));
   }
   if (n_chunks > 1) {  // odd chunks run on the second stream, after the shared setup above
     SR_HIP_CHECK(ctx->need_stream2());
@@ -1138,9 +1074,7 @@ int run_batch(sr_ctx* ctx, const sr_dataset* ds, int opset_id, const sr_tree_bat
         p = q;
       }
     }
-    if (host_prog) {
-      // the kernel reads the staging image itself
-    } else if (n_chunks == 1) {  // the whole staging image (code, offsets, static_bad, order): one DMA
+    if (n_chunks == 1) {  // the whole staging image (code, offsets, static_bad, order): one DMA
       const size_t img = multi ? o_seg + size_t(n_seg) * sizeof(SrSegment) : o_end + size_t(nc) * sizeof(uint32_t);
       SR_HIP_CHECK(hipMemcpyAsync(dprog, hprog, img, hipMemcpyHostToDevice, cs));
     } else {
@@ -1232,9 +1166,9 @@ int run_batch(sr_ctx* ctx, const sr_dataset* ds, int opset_id, const sr_tree_bat
       // each): sized for the longest group span of this launch, capped by that budget (groups longer
       // than the cap stream their windows from global memory)
       a.code_lds = 0;
-      // (code_cache 2: the classic LDS-stack launches too, within 48 KiB per workgroup so that three
-      //  still share a CU — with SR_AMD_HOST_IO=2 the programs then cross PCIe once per workgroup)
-      const size_t code_budget = vstk ? kCodeCacheLds : (ctx->code_cache >= 2 ? size_t(48) * 1024 : 0);
+      // (round 4's cache in the classic launches too — code_cache 2 — was measured without payoff and
+      //  removed in round 6)
+      const size_t code_budget = vstk ? kCodeCacheLds : 0;
       if (mode == SR_MODE_LOSS && ctx->code_cache && size_t(g.lds) < code_budget) {
         int64_t maxspan = 0;
         for (int64_t q = 0; q < g.n_groups; ++q) {
@@ -1248,7 +1182,7 @@ int run_batch(sr_ctx* ctx, const sr_dataset* ds, int opset_id, const sr_tree_bat
       }
       int64_t n_blocks = g.n_blocks;
       if (multi) {  // (one launch over the whole chunk: the segments computed above)
-        a.segs = reinterpret_cast<const SrSegment*>((host_prog ? hprog : dprog) + o_seg);
+        a.segs = reinterpret_cast<const SrSegment*>(dprog + o_seg);
         a.n_segs = n_seg;
         n_blocks = seg_blocks;
         if (n_blocks > 0x7fffffff) return set_error(SR_ERR_INVALID_ARG, "grid too large");
@@ -1296,8 +1230,8 @@ int run_batch(sr_ctx* ctx, const sr_dataset* ds, int opset_id, const sr_tree_bat
         pa.tiles_per_block = 1;
         pa.n_row_blocks = kProbeTiles;
         pa.n_rows = std::min<int64_t>(n_eval, int64_t(kProbeTiles) * 64 * R);
-        pa.part_sum = ctx->probe_sum.as<double>() + (spec_x ? size_t(t0) * kProbeTiles : 0);
-        pa.part_flag = ctx->probe_flag.as<uint32_t>() + (spec_x ? size_t(t0) * kProbeTiles : 0);
+        pa.part_sum = ctx->probe_sum.as<double>();
+        pa.part_flag = ctx->probe_flag.as<uint32_t>();
         if (stress_probe) {  // the stress rows first (sr_dataset::probe_rows), through the gather build
           pa.row_idx = static_cast<const int64_t*>(ds->probe_rows);
           pa.n_rows = std::min<int64_t>(ds->n_probe, int64_t(kProbeTiles) * 64 * R);
@@ -1307,13 +1241,6 @@ int run_batch(sr_ctx* ctx, const sr_dataset* ds, int opset_id, const sr_tree_bat
           }
         }
         SR_HIP_CHECK(sr_launch_eval<T>(pa, mode, gather || stress_probe, tier, R, W, false, pa.n_groups * kProbeTiles, cs));
-        if (spec_x && stress_probe) {  // ([row tile][position] flags of this launch's np positions)
-          SR_HIP_CHECK(hipEventRecord(ctx->ev_pr[c], cs));
-          SR_HIP_CHECK(hipStreamWaitEvent(ctx->stream3, ctx->ev_pr[c], 0));
-          SR_HIP_CHECK(hipMemcpyAsync(ctx->h_pflag.as<uint32_t>() + size_t(t0) * kProbeTiles, pa.part_flag,
-                                      size_t(np) * kProbeTiles * sizeof(uint32_t), hipMemcpyDeviceToHost, ctx->stream3));
-          ctx->spec_chunks.push_back({t0, np});
-        }
       }
 #ifdef SR_STAMPS
       ctx->n_stamps = g.n_blocks * g.W * SR_NSTAMPS;
@@ -1360,7 +1287,6 @@ int run_batch(sr_ctx* ctx, const sr_dataset* ds, int opset_id, const sr_tree_bat
     ctx->n_chunks_last = c + 1;
     code_base += uint32_t(ncode);
   }
-  if (!ctx->spec_chunks.empty()) SR_HIP_CHECK(hipEventRecord(ctx->ev_spec, ctx->stream3));
   if (n_chunks > 1) {  // the caller continues on the first stream: join the second
     SR_HIP_CHECK(hipEventRecord(ctx->ev_join, ctx->stream2));
     SR_HIP_CHECK(hipStreamWaitEvent(s, ctx->ev_join, 0));
@@ -1751,64 +1677,6 @@ int exact_list_ok(sr_ctx* ctx, const sr_dataset* ds, const SrProgramBatch<T>& pr
   return SR_OK;
 }
 
-// The speculative exact pass (sr_ctx::spec_exact), first half: once the probes' flags are back (they
-// finish early in the main launches), the trees they flag BIG and not non-finite go through the pass
-// on the third stream while the main launches run.  At most kSpecMax trees (one pass batch).
-constexpr int64_t kSpecMax = 1024;
-template <typename T>
-int spec_launch(sr_ctx* ctx, const sr_dataset* ds, const SrProgramBatch<T>& prog, int64_t nt) {
-  if (ctx->spec_chunks.empty()) return SR_OK;
-  SR_HIP_CHECK(hipEventSynchronize(ctx->ev_spec));
-  const uint32_t* pf = ctx->h_pflag.as<uint32_t>();
-  const uint32_t* perm = ctx->h_perm_last;
-  std::vector<int64_t>& list = ctx->spec_list;
-  list.clear();
-  int mc = 0;
-  for (const sr_ctx::SpecChunk& ch : ctx->spec_chunks) {
-    const uint32_t* f = pf + size_t(ch.t0) * kProbeTiles;  // [tile][position]
-    for (int64_t p = 0; p < ch.np; ++p) {
-      uint32_t o = 0;
-      for (int k = 0; k < kProbeTiles; ++k) o |= f[size_t(k) * size_t(ch.np) + size_t(p)];
-      if ((o & SR_FLAG_BIG) == 0 || (o & SR_FLAG_NONFINITE) != 0) continue;
-      const int64_t t = ch.t0 + int64_t(perm[ch.t0 + p]);
-      if (t < 0 || t >= nt || prog.static_bad[size_t(t)] || prog.n_checks[size_t(t)] == 0) continue;
-      list.push_back(t);
-      mc = std::max(mc, int(prog.n_checks[size_t(t)]));
-    }
-  }
-  ctx->spec_chunks.clear();  // (the copies are complete: ev_spec)
-  if (list.empty() || int64_t(list.size()) > kSpecMax) {
-    list.clear();
-    return SR_OK;
-  }
-  ctx->n_spec_last = int64_t(list.size());
-  ctx->spec_mc = mc;
-  ctx->spec_ok.assign(list.size() * size_t(mc), 1);  // (run_exact's host_finite: unused until collected)
-  const int rc = run_exact<T>(ctx, ds, prog, nullptr, 0, list.data(), int64_t(list.size()), mc, jl_ranges_cached(ds->n),
-                              nullptr, ctx->spec_ok.data(), 0, ctx->stream3, false, &ctx->spec_fin_off);
-  if (rc != SR_OK) {
-    list.clear();
-    return rc;
-  }
-  ctx->spec_pending = true;
-  return SR_OK;
-}
-
-// Second half: wait for the speculative pass; spec_ok[i] = every checked array of spec_list[i] passes.
-inline int spec_collect(sr_ctx* ctx) {
-  if (!ctx->spec_pending) return SR_OK;
-  ctx->spec_pending = false;
-  SR_HIP_CHECK(hipStreamSynchronize(ctx->stream3));
-  float km = 0.f;
-  if (hipEventElapsedTime(&km, ctx->ev_k0, ctx->ev_k1) == hipSuccess) ctx->exact_kernel_ms += double(km);
-  const uint8_t* v = reinterpret_cast<const uint8_t*>(ctx->h_exact.as<char>() + ctx->spec_fin_off);
-  const size_t n = ctx->spec_list.size(), mc = size_t(ctx->spec_mc);
-  ctx->spec_ok.assign(n, 1);
-  for (size_t i = 0; i < n; ++i)
-    for (size_t k = 0; k < mc; ++k) ctx->spec_ok[i] &= v[i * mc + k];
-  return SR_OK;
-}
-
 // Finalize one tree: complete unless flagged; BIG-only trees take their exact verdict (list_ok).  A
 // complete tree's loss is Σ / denom, or +Inf where the reference's T-precision fold of the losses
 // overflows (sr_fold.h; n_terms = rows of the fold, 0: only SR_FLAG_ELEMINF is applied).  Trees the
@@ -2171,7 +2039,6 @@ struct LossCall {
   ViewSpec views{};
   SrProgramBatch<T> prog;
   std::chrono::steady_clock::time_point t0;
-  bool async = false;  // wait on ctx->ev_done (the stream may be shared and hold later work)
 };
 template <typename T>
 int eval_loss_finish(sr_ctx* ctx, LossCall<T>& c);
@@ -2202,12 +2069,10 @@ int eval_loss_submit(sr_ctx* ctx, const sr_dataset* ds, int opset_id, const sr_t
   SrProgramBatch<T>& prog = c->prog;
   Grid g;
   ctx->want_host_out = true;
-  ctx->want_spec = views == nullptr && !gather;
   ctx->want_fold = true;
   int rc = run_batch<T>(ctx, ds, opset_id, trees, row_idx, n_idx, n_eval, loss_kind, SR_MODE_LOSS, &prog, &g, true,
                         nullptr, views);
   ctx->want_host_out = false;
-  ctx->want_spec = false;
   ctx->want_fold = false;
   if (rc != SR_OK) return rc;
   if (nt == 0) return SR_OK;
@@ -2218,7 +2083,6 @@ int eval_loss_submit(sr_ctx* ctx, const sr_dataset* ds, int opset_id, const sr_t
     SR_HIP_CHECK(ctx->h_outs.ensure(out_bytes, s, ctx->stream2));
     SR_HIP_CHECK(hipMemcpyAsync(ctx->h_outs.p, ctx->outs.p, out_bytes, hipMemcpyDeviceToHost, s));
   }
-  if (c->async) SR_HIP_CHECK(hipEventRecord(ctx->ev_done, s));
   return SR_OK;
 }
 
@@ -2244,22 +2108,8 @@ int eval_loss_finish(sr_ctx* ctx, LossCall<T>& c) {
   auto rows_of = [&](int v) -> const int64_t* { return gather ? row_idx + int64_t(v) * n_idx : nullptr; };
   hipStream_t s = ctx->stream;
   int rc = SR_OK;
-  ctx->n_spec_last = ctx->n_spec_used_last = 0;
-  if (!ctx->spec_chunks.empty()) {  // the speculative exact pass starts while the main launches run
-    rc = spec_launch<T>(ctx, ds, prog, nt);
-    if (rc != SR_OK) return rc;
-  }
 
-  if (ctx->spin && ctx->outs_on_host) {
-    hipError_t e;
-    while ((e = c.async ? hipEventQuery(ctx->ev_done) : hipStreamQuery(s)) == hipErrorNotReady) {
-    }
-    SR_HIP_CHECK(e);
-  } else if (c.async) {
-    SR_HIP_CHECK(hipEventSynchronize(ctx->ev_done));
-  } else {
-    SR_HIP_CHECK(hipStreamSynchronize(s));
-  }
+  SR_HIP_CHECK(hipStreamSynchronize(s));
   if (!ctx->host_reductions.empty()) host_reduce_partials(ctx, nt);
   const double* hs = ctx->h_outs.as<double>();
   const uint32_t* hf = reinterpret_cast<const uint32_t*>(ctx->h_outs.as<char>() + ctx->outs_flag_off);
@@ -2273,25 +2123,11 @@ int eval_loss_finish(sr_ctx* ctx, LossCall<T>& c) {
   std::vector<uint8_t> list_ok(list.size(), 1);
   ctx->n_exact_last = int64_t(list.size());
   ctx->exact_kernel_ms = 0.0;
-  std::vector<uint8_t> have(list.size(), 0);  // verdicts the speculative pass already holds
-  if (ctx->spec_pending) {
-    rc = spec_collect(ctx);
-    if (rc != SR_OK) return rc;
-    std::vector<int32_t> at_spec(size_t(nt), -1);
-    for (size_t i = 0; i < ctx->spec_list.size(); ++i) at_spec[size_t(ctx->spec_list[i])] = int32_t(i);
-    for (size_t i = 0; i < list.size(); ++i) {
-      const int32_t p = at_spec[size_t(list[i])];
-      if (p < 0) continue;
-      list_ok[i] = ctx->spec_ok[size_t(p)];
-      have[i] = 1;
-      ++ctx->n_spec_used_last;
-    }
-  }
   for (int v = 0; v < n_views && !list.empty(); ++v) {  // (each view's listed trees over its own rows)
     std::vector<int64_t> lv;
     std::vector<size_t> at;
     for (size_t i = 0; i < list.size(); ++i)
-      if (!have[i] && view_of(list[i]) == v) {
+      if (view_of(list[i]) == v) {
         lv.push_back(list[i]);
         at.push_back(i);
       }
@@ -2326,6 +2162,26 @@ int eval_loss_finish(sr_ctx* ctx, LossCall<T>& c) {
               views ? denoms.data() : nullptr, have_fold ? &fres : nullptr);
   ctx->n_ref_ok_last = fres.n_ok;
   ctx->n_ref_fail_last = fres.n_fail;
+  if (have_fold && ctx->fold_stats) {  // (analysis: slow segments, rounds, runs and walk time per folded tree)
+    std::vector<int4> st(static_cast<size_t>(nt));
+    if (hipMemcpy(st.data(), ctx->fold_dbg.p, st.size() * sizeof(int4), hipMemcpyDeviceToHost) == hipSuccess) {
+      int64_t m = 0;
+      double a[4] = {0, 0, 0, 0};
+      int mx[4] = {0, 0, 0, 0};
+      for (const int4& v : st) {
+        if (v.x == 0 && v.y == 0 && v.z == 0) continue;
+        ++m;
+        const int w[4] = {v.x, v.y, v.z, v.w};
+        for (int i = 0; i < 4; ++i) {
+          a[i] += w[i];
+          mx[i] = std::max(mx[i], w[i]);
+        }
+      }
+      std::fprintf(stderr, "[sr fold] path %d: %lld walks, mean/max slow segments %.1f/%d, rounds %.1f/%d, runs %.1f/%d, walk us %.1f/%d; folded %lld fallback %lld\n",
+                   ctx->fold_path_last, (long long)m, m ? a[0] / m : 0.0, mx[0], m ? a[1] / m : 0.0, mx[1],
+                   m ? a[2] / m : 0.0, mx[2], m ? a[3] / m : 0.0, mx[3], (long long)fres.n_ok, (long long)fres.n_fail);
+    }
+  }
   ctx->n_fold_last = int64_t(fold_list.size());
   ctx->fold_slow_last = ctx->fold_seg_last = 0;
   for (double& v : ctx->fold_ms) v = 0.0;
@@ -3618,32 +3474,29 @@ int sr_init(int device, sr_ctx** out) {
   if (const char* v = std::getenv("SR_AMD_NO_HINT")) ctx->dead_hints = std::atoi(v) == 0;
   // (A/B: the program staging buffer allocated non-coherent, so that kernels reading programs from it
   //  — SR_AMD_HOST_IO=2 — may cache them in L2; the dispatch's acquire makes each call's writes visible)
-  if (const char* v = std::getenv("SR_AMD_PROG_NC")) ctx->h_prog.flags = std::atoi(v) ? hipHostMallocNonCoherent : hipHostMallocDefault;
   if (const char* v = std::getenv("SR_AMD_CHUNKS")) ctx->chunks = std::atoi(v);
   if (const char* v = std::getenv("SR_AMD_PROBE")) ctx->probe = std::atoi(v);
   if (const char* v = std::getenv("SR_AMD_FOLD_SEG")) ctx->fold_seg = std::atoll(v);
   if (const char* v = std::getenv("SR_AMD_HOST_REDUCE")) ctx->host_reduce = std::atoll(v);
   if (const char* v = std::getenv("SR_AMD_STRESS_PROBE")) ctx->stress_probe = std::atoi(v);
-  if (const char* v = std::getenv("SR_AMD_CODE_CACHE")) ctx->code_cache = std::atoi(v);
+  if (const char* v = std::getenv("SR_AMD_CODE_CACHE")) ctx->code_cache = std::atoi(v) != 0 ? 1 : 0;
   if (const char* v = std::getenv("SR_AMD_FUSED_REDUCE")) ctx->fused_reduce = std::atoll(v);
   if (const char* v = std::getenv("SR_AMD_GRAD_ROWS")) ctx->grad_rows_force = std::atoi(v);
   if (const char* v = std::getenv("SR_AMD_GRAD_SORT")) ctx->grad_sort = std::atoi(v) != 0 ? 1 : 0;
   if (const char* v = std::getenv("SR_AMD_VSTK_ROWS")) ctx->vstk_rows = std::atoi(v);
   if (const char* v = std::getenv("SR_AMD_FIRST_CHUNK")) ctx->first_chunk = std::max(2, std::atoi(v));
   if (const char* v = std::getenv("SR_AMD_CHUNK_MIN")) ctx->chunk_min = std::max<int64_t>(1, std::atoll(v));
-  if (const char* v = std::getenv("SR_AMD_HOST_IO")) ctx->host_io = std::atoi(v);
-  if (const char* v = std::getenv("SR_AMD_SPIN")) ctx->spin = std::atoi(v);
+  if (const char* v = std::getenv("SR_AMD_HOST_IO")) ctx->host_io = std::atoi(v) != 0 ? 1 : 0;
   if (const char* v = std::getenv("SR_AMD_EXACT_G")) ctx->exact_g = std::atoi(v);
   if (const char* v = std::getenv("SR_AMD_EXACT_W")) ctx->exact_w = std::atoi(v) == 1 ? 1 : 4;
   if (const char* v = std::getenv("SR_AMD_EXACT_LIST_HOST")) ctx->exact_list_host = std::atoi(v) != 0 ? 1 : 0;
-  if (const char* v = std::getenv("SR_AMD_SPEC_EXACT")) ctx->spec_exact = std::atoi(v) != 0 ? 1 : 0;
-  if (const char* v = std::getenv("SR_AMD_SPEC_PRIO")) ctx->spec_prio = std::atoi(v);
   if (const char* v = std::getenv("SR_AMD_PAR_STAGE")) ctx->par_stage = std::atoi(v);
   if (const char* v = std::getenv("SR_AMD_DERIVED")) ctx->derived = std::atoi(v);
   if (const char* v = std::getenv("SR_AMD_MAX_ROW_BLOCKS")) ctx->max_row_blocks = std::max(1, std::atoi(v));
   if (const char* v = std::getenv("SR_AMD_REF_FOLD")) ctx->ref_fold = std::atoi(v) != 0 ? 1 : 0;
   if (const char* v = std::getenv("SR_AMD_FOLD_STORE_MB")) ctx->fold_store_mb = std::max<int64_t>(0, std::atoll(v));
   if (const char* v = std::getenv("SR_AMD_FOLD_SLOT_MB")) ctx->fold_slot_mb = std::max<int64_t>(1, std::atoll(v));
+  if (const char* v = std::getenv("SR_AMD_FOLD_STATS")) ctx->fold_stats = std::atoi(v);
   if (const char* v = std::getenv("SR_AMD_FOLD_DELTA_LOG2")) ctx->fold_delta_log2 = std::max(1, std::min(40, std::atoi(v)));
   hipError_t e = hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking);
   if (e == hipSuccess && std::getenv("SR_AMD_EAGER_STREAM2")) e = ctx->need_stream2();  // (A/B: the round-4 layout)
@@ -3657,59 +3510,20 @@ int sr_init(int device, sr_ctx** out) {
   for (int c = 0; c < kMaxChunks; ++c) {
     if (e == hipSuccess) e = hipEventCreate(&ctx->ev_c0[c]);
     if (e == hipSuccess) e = hipEventCreate(&ctx->ev_c1[c]);
-    if (e == hipSuccess) e = hipEventCreateWithFlags(&ctx->ev_pr[c], hipEventDisableTiming);
     if (e == hipSuccess) e = hipEventCreate(&ctx->ev_fc0[c]);
     if (e == hipSuccess) e = hipEventCreate(&ctx->ev_fc1[c]);
   }
-  if (e == hipSuccess) e = hipEventCreateWithFlags(&ctx->ev_spec, hipEventDisableTiming);
   for (int b = 0; b < sr_ctx::kGradBuckets; ++b) {
     if (e == hipSuccess) e = hipEventCreate(&ctx->ev_g0[b]);
     if (e == hipSuccess) e = hipEventCreate(&ctx->ev_g1[b]);
   }
   for (hipEvent_t& ev : ctx->ev_f)
     if (e == hipSuccess) e = hipEventCreate(&ev);
-  if (e == hipSuccess) e = hipEventCreateWithFlags(&ctx->ev_done, hipEventDisableTiming);
   if (e != hipSuccess) {
     delete ctx;
     return set_error(SR_ERR_HIP, std::string("stream/event creation: ") + hipGetErrorString(e));
   }
   *out = ctx;
-  return SR_OK;
-}
-
-int sr_init_shared(sr_ctx* parent, sr_ctx** out) {
-  if (!parent || !out) return set_error(SR_ERR_INVALID_ARG, "NULL parent context or output");
-  int rc = sr_init(parent->device, out);
-  if (rc != SR_OK) return rc;
-  sr_ctx* c = *out;
-  (void)hipStreamSynchronize(c->stream);
-  (void)hipStreamDestroy(c->stream);
-  c->stream = parent->stream;  // one hardware queue for both contexts
-  c->owns_stream = false;
-  c->parent = parent;
-  {  // the parent's operator sets and registered losses, at the same ids (register them before this call)
-    Lock lp(parent);
-    c->opsets = parent->opsets;
-    c->tiers = parent->tiers;
-    c->losses = parent->losses;
-  }
-  // the parent's run-time knobs (sr_set_tuning)
-  c->timing = parent->timing;
-  c->host_io = parent->host_io;
-  c->host_reduce = parent->host_reduce;
-  c->code_cache = parent->code_cache;
-  c->fused_reduce = parent->fused_reduce;
-  c->derived = parent->derived;
-  c->probe = parent->probe;
-  c->stress_probe = parent->stress_probe;
-  c->spec_exact = parent->spec_exact;
-  c->fold_seg = parent->fold_seg;
-  c->ref_fold = parent->ref_fold;
-  c->fold_store_mb = parent->fold_store_mb;
-  c->fold_slot_mb = parent->fold_slot_mb;
-  c->fold_delta_log2 = parent->fold_delta_log2;
-  c->spin = parent->spin;
-  c->h_prog.flags = parent->h_prog.flags;
   return SR_OK;
 }
 
@@ -3728,26 +3542,22 @@ int sr_shutdown(sr_ctx* ctx) {
     ctx->hint_reserve = nullptr;
     for (DevBuf* b : {&ctx->prog, &ctx->outs, &ctx->part_sum, &ctx->part_flag, &ctx->pred, &ctx->row_idx, &ctx->tree_list, &ctx->range_lo, &ctx->range_hi, &ctx->range_sums, &ctx->packed,
                       &ctx->hint, &ctx->jsum_prog, &ctx->jsum_scratch, &ctx->probe_sum, &ctx->probe_flag, &ctx->g_code, &ctx->g_offsets, &ctx->g_consts, &ctx->g_const_off,
-                      &ctx->g_items, &ctx->g_part, &ctx->g_out, &ctx->derived_cols, &ctx->probe_derived, &ctx->coll_buf, &ctx->coll_packed, &ctx->ctl, &ctx->fold_io, &ctx->group_cnt})
+                      &ctx->g_items, &ctx->g_part, &ctx->g_out, &ctx->derived_cols, &ctx->probe_derived, &ctx->coll_buf, &ctx->coll_packed, &ctx->ctl, &ctx->fold_io, &ctx->group_cnt,
+                      &ctx->fold_code, &ctx->fold_tab, &ctx->fold_store, &ctx->fold_ctl, &ctx->fold_io2})
       b->release();
-    if (ctx->stream3) (void)hipStreamSynchronize(ctx->stream3);
-    for (HostBuf* b : {&ctx->h_prog, &ctx->h_outs, &ctx->h_grad, &ctx->h_coll, &ctx->h_part, &ctx->h_exact, &ctx->h_pflag})
+    for (HostBuf* b : {&ctx->h_prog, &ctx->h_outs, &ctx->h_grad, &ctx->h_coll, &ctx->h_part, &ctx->h_exact})
       b->release();
     for (int c = 0; c < kMaxChunks; ++c) {
       (void)hipEventDestroy(ctx->ev_c0[c]);
       (void)hipEventDestroy(ctx->ev_c1[c]);
-      (void)hipEventDestroy(ctx->ev_pr[c]);
       (void)hipEventDestroy(ctx->ev_fc0[c]);
       (void)hipEventDestroy(ctx->ev_fc1[c]);
     }
-    (void)hipEventDestroy(ctx->ev_spec);
-    if (ctx->stream3) (void)hipStreamDestroy(ctx->stream3);
     for (int b = 0; b < sr_ctx::kGradBuckets; ++b) {
       (void)hipEventDestroy(ctx->ev_g0[b]);
       (void)hipEventDestroy(ctx->ev_g1[b]);
     }
     for (hipEvent_t ev : ctx->ev_f) (void)hipEventDestroy(ev);
-    (void)hipEventDestroy(ctx->ev_done);
     if (ctx->stream2) (void)hipStreamSynchronize(ctx->stream2);
     (void)hipEventDestroy(ctx->ev_join);
     if (ctx->stream2) (void)hipStreamDestroy(ctx->stream2);
@@ -3757,7 +3567,7 @@ int sr_shutdown(sr_ctx* ctx) {
     (void)hipEventDestroy(ctx->ev_end);
     (void)hipEventDestroy(ctx->ev_d0);
     (void)hipEventDestroy(ctx->ev_d1);
-    if (ctx->owns_stream) (void)hipStreamDestroy(ctx->stream);
+    (void)hipStreamDestroy(ctx->stream);
   }
   delete ctx;
   return SR_OK;
@@ -3877,43 +3687,6 @@ int sr_eval_loss_batch_views(sr_ctx* ctx, const sr_dataset* ds, int opset_id, co
   if (ds->dtype == SR_DTYPE_F32)
     return eval_loss_impl<float>(ctx, ds, opset_id, trees, view_rows, view_len, loss_kind, out_loss, out_complete, v);
   return eval_loss_impl<double>(ctx, ds, opset_id, trees, view_rows, view_len, loss_kind, out_loss, out_complete, v);
-}
-
-int sr_eval_loss_submit(sr_ctx* ctx, const sr_dataset* ds, int opset_id, const sr_tree_batch* trees,
-                        const int32_t* tree_view, int n_views, const int64_t* view_rows, int64_t view_len, int loss_kind,
-                        void* out_loss, uint8_t* out_complete) {
-  int rc = validate_common(ctx, ds, opset_id, trees);
-  if (rc != SR_OK) return rc;
-  if (n_views > 1 && (rc = check_views(trees, tree_view, n_views, view_rows, view_len)) != SR_OK) return rc;
-  Lock l(ctx);
-  if (ctx->pending) return set_error(SR_ERR_INVALID_ARG, "a submitted call is pending on this context: sr_eval_loss_wait first");
-  SR_HIP_CHECK(hipSetDevice(ctx->device));
-  const ViewSpec vs{tree_view, n_views, view_len};
-  const ViewSpec* v = n_views > 1 ? &vs : nullptr;
-  auto go = [&](auto zero) -> int {
-    using T = decltype(zero);
-    auto c = std::make_shared<LossCall<T>>();
-    c->async = true;
-    const int r = eval_loss_submit<T>(ctx, ds, opset_id, trees, view_rows, view_len, loss_kind, out_loss, out_complete,
-                                      v, c.get());
-    if (r != SR_OK) {
-      (void)hipStreamSynchronize(ctx->stream);  // (nothing of it may still run when the caller retries)
-      return r;
-    }
-    ctx->pending = [ctx, c]() { return eval_loss_finish<T>(ctx, *c); };
-    return SR_OK;
-  };
-  return ds->dtype == SR_DTYPE_F32 ? go(0.0f) : go(0.0);
-}
-
-int sr_eval_loss_wait(sr_ctx* ctx) {
-  if (check_ctx(ctx) != SR_OK) return SR_ERR_INVALID_ARG;
-  Lock l(ctx);
-  if (!ctx->pending) return set_error(SR_ERR_INVALID_ARG, "no submitted call is pending on this context");
-  SR_HIP_CHECK(hipSetDevice(ctx->device));
-  std::function<int()> f = std::move(ctx->pending);
-  ctx->pending = nullptr;
-  return f();
 }
 
 int sr_eval_grad_batch_views(sr_ctx* ctx, const sr_dataset* ds, int opset_id, const sr_tree_batch* trees,
@@ -4427,8 +4200,8 @@ int sr_set_tuning(sr_ctx* ctx, const char* name, int64_t value) {
     ctx->probe = int(value);
     return SR_OK;
   }
-  if (std::strcmp(name, "host_io") == 0) {  // small-call host I/O (SR_AMD_HOST_IO: 0, 1, 2)
-    if (value < 0 || value > 2) return set_error(SR_ERR_INVALID_ARG, "host_io must be 0, 1 or 2");
+  if (std::strcmp(name, "host_io") == 0) {  // small-call results written to pinned memory (SR_AMD_HOST_IO: 0, 1)
+    if (value < 0 || value > 1) return set_error(SR_ERR_INVALID_ARG, "host_io must be 0 or 1");
     ctx->host_io = int(value);
     return SR_OK;
   }
@@ -4472,10 +4245,6 @@ int sr_set_tuning(sr_ctx* ctx, const char* name, int64_t value) {
     ctx->fold_seg = value < 0 ? -1 : value;
     return SR_OK;
   }
-  if (std::strcmp(name, "spec_exact") == 0) {  // speculative exact-sum pass (SR_AMD_SPEC_EXACT)
-    ctx->spec_exact = value != 0 ? 1 : 0;
-    return SR_OK;
-  }
   if (std::strcmp(name, "exact_w") == 0) {  // waves per workgroup of the EXACT pass (SR_AMD_EXACT_W)
     ctx->exact_w = value == 1 ? 1 : 4;
     return SR_OK;
@@ -4485,7 +4254,7 @@ int sr_set_tuning(sr_ctx* ctx, const char* name, int64_t value) {
     return SR_OK;
   }
   if (std::strcmp(name, "code_cache") == 0) {  // LDS program cache (SR_AMD_CODE_CACHE)
-    ctx->code_cache = int(value < 0 ? 0 : (value > 2 ? 2 : value));
+    ctx->code_cache = value != 0 ? 1 : 0;
     return SR_OK;
   }
   if (std::strcmp(name, "timing") == 0) {  // 0: record no timing events (kernel times read as 0)
@@ -4560,13 +4329,6 @@ int sr_ref_fold_info(sr_ctx* ctx, int* path, int64_t* n_folded, int64_t* n_fallb
   if (n_folded) *n_folded = ctx->n_ref_ok_last;
   if (n_fallback) *n_fallback = ctx->n_ref_fail_last;
   if (fold_kernel_ms) *fold_kernel_ms = ctx->fold_kernel_ms_last;
-  return SR_OK;
-}
-
-int sr_spec_exact_info(sr_ctx* ctx, int64_t* speculated, int64_t* used) {
-  if (check_ctx(ctx) != SR_OK) return SR_ERR_INVALID_ARG;
-  if (speculated) *speculated = ctx->n_spec_last;
-  if (used) *used = ctx->n_spec_used_last;
   return SR_OK;
 }
 

@@ -210,20 +210,9 @@ SRL_HD inline double sr_rem_pio2f_fast(float x, int* q) {
 // function c_k = 0 exactly and the result is -s_k sin r itself): <= 0.5025 ulp after the final
 // rounding (tools/libm_exhaustive.cpp: every Float32 |x| < 2^20).  Seven f64 operations after the
 // reduction, the terms in Horner form in r.
-// (sin, cos)(k pi/128) copies in LDS (device only; 1 by default).  A ds_read_b128 serves 16-lane groups
-// whose lanes each read one 16-byte slot of the 256-byte bank row, so random entries collide (about
-// 3 LDS cycles per group instead of 1); with C copies interleaved entry by entry, lane l reads copy
-// l mod C and only the 16 / C lanes of a group sharing a copy can collide.  Set per translation unit
-// (sr_inst_f32_vstk.hip: SR_VSTK_TRIG_COPIES) so kernels with large dynamic LDS keep the 4 KiB table.
-#ifndef SR_TRIG_COPIES
-#define SR_TRIG_COPIES 1
-#endif
-static_assert(SR_TRIG_COPIES == 1 || SR_TRIG_COPIES == 2 || SR_TRIG_COPIES == 4 || SR_TRIG_COPIES == 8, "copies");
-#if defined(__HIP_DEVICE_COMPILE__)
-#define SRL_TRIG_LOG2C (SR_TRIG_COPIES == 8 ? 3 : SR_TRIG_COPIES == 4 ? 2 : SR_TRIG_COPIES == 2 ? 1 : 0)
-#else
-#define SRL_TRIG_LOG2C 0
-#endif
+// (One copy of the (sin, cos)(k pi/128) table in LDS: round 5 measured 2 / 4 / 8 interleaved copies —
+//  conflict-free reads — slower on every population, the extra LDS costing resident workgroups;
+//  profiles/r05_ab_trig_copies.txt.  The option was removed in round 6.)
 struct SrTrigArg {
   double r, sk, ck;
 };
@@ -238,10 +227,8 @@ SRL_HD inline SrTrigArg sr_trig_arg(float x, const double* tab) {
   r = fma(-n, srl::kPi128_2, r);
   uint64_t tb;
   __builtin_memcpy(&tb, &t, 8);
-  // entry k = 16 bytes at byte offset 16 k (device, SR_TRIG_COPIES > 1: 16 C k, the lane's copy
-  // already in `tab`, see sr_trig_tab)
-  const double* e = reinterpret_cast<const double*>(reinterpret_cast<const char*>(tab) +
-                                                    ((uint32_t(tb) << (4 + SRL_TRIG_LOG2C)) & (0xff0u << SRL_TRIG_LOG2C)));
+  // entry k = 16 bytes at byte offset 16 k
+  const double* e = reinterpret_cast<const double*>(reinterpret_cast<const char*>(tab) + ((uint32_t(tb) << 4) & 0xff0u));
   return SrTrigArg{r, e[0], e[1]};
 }
 template <bool COS>
@@ -284,21 +271,15 @@ SRL_HD inline float sr_sincosf_full(float x, const double* tab) {
 #if defined(__HIPCC__)
 // per-workgroup LDS copy of the tables (trig then log; 5 KiB: it must not cost the interpreter a
 // workgroup per CU)
-static __shared__ __attribute__((aligned(16))) double sr_lds_libm[512 * SR_TRIG_COPIES + 128];
+static __shared__ __attribute__((aligned(16))) double sr_lds_libm[512 + 128];
 // Copy the tables into LDS: every thread of the block calls this before the block's first barrier.
-// (trig entry k, copy c at doubles 2 (C k + c), 2 (C k + c) + 1)
 __device__ inline void sr_libm_lds_fill(int tid, int nthreads) {
-  constexpr int C = SR_TRIG_COPIES;
-  for (int i = tid; i < 512 * C; i += nthreads) sr_lds_libm[i] = srl::kTrigTab[2 * (i / (2 * C)) + (i & 1)];
-  for (int i = tid; i < 128; i += nthreads) sr_lds_libm[512 * C + i] = srl::kLogTab[i];
+  for (int i = tid; i < 512; i += nthreads) sr_lds_libm[i] = srl::kTrigTab[i];
+  for (int i = tid; i < 128; i += nthreads) sr_lds_libm[512 + i] = srl::kLogTab[i];
 }
 #endif
 SRL_HD inline const double* sr_trig_tab() {
 #if defined(__HIP_DEVICE_COMPILE__)
-  if constexpr (SR_TRIG_COPIES > 1) {  // this lane's copy
-    const uint32_t lane = __builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u));
-    return sr_lds_libm + 2 * (lane & uint32_t(SR_TRIG_COPIES - 1));
-  }
   return sr_lds_libm;
 #else
   return srl::kTrigTab;
@@ -306,7 +287,7 @@ SRL_HD inline const double* sr_trig_tab() {
 }
 SRL_HD inline const double* sr_log_tab() {
 #if defined(__HIP_DEVICE_COMPILE__)
-  return sr_lds_libm + 512 * SR_TRIG_COPIES;
+  return sr_lds_libm + 512;
 #else
   return srl::kLogTab;
 #endif

@@ -303,64 +303,17 @@ struct Scorer {
     ++calls;
     return rc;
   }
-  // Asynchronous loss (round 5): loss_submit launches the call and returns, loss_wait finishes it into
-  // the `out` given at submit (+Inf where incomplete).  The device path keeps the call's view arrays
-  // here until the wait; CPU scorers run the whole call at submit.
+  // A round's scoring call in two halves (round_submit / round_finish): the call runs whole at submit
+  // (round 5's asynchronous device call and two-half lane pipeline were measured without payoff and
+  // removed in round 6: profiles/r05_ab_search_pipeline.txt); loss_wait is then a no-op.
   struct AsyncLoss {
-    std::vector<int32_t> tv;
-    std::vector<int64_t> cat;
-    std::vector<uint8_t> comp;
     std::vector<T>* out = nullptr;
-    bool device = false;
-    int timing_was = -1;
-    Clock::time_point t0;
   };
   int loss_submit(const Flat& flat, const TreeRows& tr, std::vector<T>* out, AsyncLoss* a) {
-    a->device = false;
     a->out = out;
-    const int64_t nt = int64_t(flat.offsets.size()) - 1;
-    if (loss_cb || nt <= 0) return loss(flat, tr, out);
-    const std::vector<int64_t>* one = nullptr;
-    int nv = 1;
-    int64_t len = 0;
-    const bool multi = !tr.empty() && make_views(tr, &a->tv, &a->cat, &nv, &len, &one);
-    out->assign(size_t(nt), T(0));
-    a->comp.assign(size_t(nt), 0);
-    const sr_tree_batch b = flat.batch<T>();
-    a->t0 = Clock::now();
-    a->timing_was = !time_kernels ? sr_ctx_swap_timing(ctx, 0) : -1;
-    int rc;
-    if (multi) {
-      rc = sr_eval_loss_submit(ctx, ds, opset_id, &b, a->tv.data(), nv, a->cat.data(), len, loss_code, out->data(),
-                               a->comp.data());
-    } else {
-      const bool rows = one != nullptr && !one->empty();
-      rc = sr_eval_loss_submit(ctx, ds, opset_id, &b, nullptr, 1, rows ? one->data() : nullptr,
-                               rows ? int64_t(one->size()) : 0, loss_code, out->data(), a->comp.data());
-    }
-    if (rc != SR_OK) {
-      if (a->timing_was >= 0) sr_ctx_swap_timing(ctx, a->timing_was);
-      return rc;
-    }
-    a->device = true;
-    return SR_OK;
+    return loss(flat, tr, out);
   }
-  int loss_wait(AsyncLoss* a) {
-    if (!a->device) return SR_OK;  // (CPU scorers: done at submit)
-    a->device = false;
-    const int rc = sr_eval_loss_wait(ctx);
-    if (a->timing_was >= 0) sr_ctx_swap_timing(ctx, a->timing_was);
-    ms += ms_since(a->t0);
-    ++calls;
-    if (rc != SR_OK) return rc;
-    if (time_kernels) {
-      double ph[9] = {0};
-      if (sr_last_phase_ms(ctx, ph, 9) == SR_OK) kernel_ms += ph[8];
-    }
-    for (size_t k = 0; k < a->comp.size(); ++k)
-      if (!a->comp[k]) (*a->out)[k] = T(INFINITY);
-    return SR_OK;
-  }
+  int loss_wait(AsyncLoss*) { return SR_OK; }
   // losses of `flat`'s trees (+Inf where incomplete)
   int loss(const Flat& flat, const std::vector<int64_t>& rows, std::vector<T>* out) {
     const sr_tree_batch b = flat.batch<T>();
@@ -566,63 +519,19 @@ struct Engine : sr_search_base {
   // Scoring lanes: lane 0 is (sc, flat, num_evals, host_ms); further lanes (sr_search_add_device:
   // their own context and dataset copy) each run a share of the owned islands' iteration on their
   // own host thread, so one lane's device round trip overlaps the others' host work and calls.
-  struct Pipe {  // a lane's second scoring context (sr_init_shared: the lane's stream) and its Flat
-    Scorer<T>* sc;
-    Flat* flat;
-  };
   struct Lane {
     Scorer<T>* sc;
     Flat* flat;
     double* num_evals;
     double* host_ms;
-    const Pipe* pipe = nullptr;  // set: the lane pipelines two halves of its islands (iterate_islands)
   };
   struct ExtraLane {
     Scorer<T> sc;
     Flat flat;
     double num_evals = 0.0, host_ms = 0.0;
-    Scorer<T> sc2;  // the pipeline partner (its own context on sc's stream), when enabled
-    Flat flat2;
-    Pipe pipe{};
   };
   std::vector<std::unique_ptr<ExtraLane>> extra;
-  // the pipeline partners (round 5; SR_AMD_SEARCH_PIPELINE=1, default off: C1 -15 %, C3 / C5 within
-  // noise, profiles/r05_ab_search_pipeline.txt): every device lane gets a second context sharing its
-  // stream (sr_init_shared) at the first iteration
-  Scorer<T> sc2;
-  Flat flat2;
-  Pipe pipe0{};
-  std::vector<sr_ctx*> pipe_ctx;
-  bool pipes_made = false;
-  const bool pipeline = [] {
-    const char* v = std::getenv("SR_AMD_SEARCH_PIPELINE");
-    return v && std::atoi(v) != 0;
-  }();
-  ~Engine() override {
-    for (sr_ctx* c : pipe_ctx) (void)sr_shutdown(c);
-  }
-  int make_pipes() {
-    if (pipes_made || !pipeline) return SR_OK;
-    pipes_made = true;
-    auto mk = [&](Scorer<T>& base, Scorer<T>& two, Flat& f2, Pipe& pp) -> int {
-      if (!base.ctx) return SR_OK;  // (CPU scorers: nothing to overlap)
-      sr_ctx* c2 = nullptr;
-      const int rc = sr_init_shared(base.ctx, &c2);
-      if (rc != SR_OK) return rc;
-      pipe_ctx.push_back(c2);
-      two.ctx = c2;
-      two.ds = base.ds;
-      two.opset_id = base.opset_id;
-      two.loss_code = base.loss_code;
-      pp = Pipe{&two, &f2};
-      return SR_OK;
-    };
-    int rc = mk(sc, sc2, flat2, pipe0);
-    for (auto& x : extra)
-      if (rc == SR_OK) rc = mk(x->sc, x->sc2, x->flat2, x->pipe);
-    return rc;
-  }
-  Lane lane0() { return Lane{&sc, &flat, &num_evals, &host_ms, pipe0.sc ? &pipe0 : nullptr}; }
+  Lane lane0() { return Lane{&sc, &flat, &num_evals, &host_ms}; }
   double total_num_evals() const {
     double v = num_evals;
     for (const auto& x : extra) v += x->num_evals;
@@ -861,9 +770,7 @@ struct Engine : sr_search_base {
   };
 
   // One regularised-evolution round of a set of islands, in two halves: round_submit selects and mutates
-  // (host) and launches ONE scoring call for every island's children; round_finish waits for it and
-  // replaces members.  A lane with a second scoring context pipelines two halves of its islands: one
-  // half's host work runs while the other half's call is on the device (iterate_islands).
+  // (host) and scores every island's children with ONE call; round_finish replaces members.
   struct RoundState {
     std::vector<Plan> plans;
     std::vector<const SrTree<T>*> pending;
@@ -1205,39 +1112,12 @@ struct Engine : sr_search_base {
           }
         }
     };
-    if (L.pipe && islands.size() >= 2) {
-      // two halves of the lane's islands, each on its own context (one stream): half h's round k is
-      // submitted, then the other half's round k finishes and its round k + 1 is submitted, so one
-      // half's host work overlaps the other half's device work.  Every island sees the same sequence
-      // of its own operations and every tree's score is independent of its batch: the results equal
-      // the unpipelined lane's.
-      const size_t mid = islands.size() / 2;
-      const std::vector<int> half[2] = {std::vector<int>(islands.begin(), islands.begin() + ptrdiff_t(mid)),
-                                        std::vector<int>(islands.begin() + ptrdiff_t(mid), islands.end())};
-      const Lane HL[2] = {L, Lane{L.pipe->sc, L.pipe->flat, L.num_evals, L.host_ms, nullptr}};
-      RoundState st[2];
-      const int S = ncyc * n_evol;
-      int rc = SR_OK;
-      for (int h = 0; h < 2 && !rc; ++h) rc = round_submit(HL[h], half[h], temp_of(0), rows, &st[h]);
-      for (int k = 0; k < S && !rc; ++k)
-        for (int h = 0; h < 2 && !rc; ++h) {
-          rc = round_finish(HL[h], rows, &st[h]);
-          if (rc) break;
-          if ((k + 1) % n_evol == 0) cycle_end(half[h]);
-          if (k + 1 < S) rc = round_submit(HL[h], half[h], temp_of((k + 1) / n_evol), rows, &st[h]);
-        }
-      if (rc) {  // (no call may stay pending on either context)
-        for (int h = 0; h < 2; ++h) (void)HL[h].sc->loss_wait(&st[h].async);
-        return rc;
+    for (int c = 0; c < ncyc; ++c) {
+      for (int r = 0; r < n_evol; ++r) {
+        int rc = round(L, islands, temp_of(c), rows);
+        if (rc) return rc;
       }
-    } else {
-      for (int c = 0; c < ncyc; ++c) {
-        for (int r = 0; r < n_evol; ++r) {
-          int rc = round(L, islands, temp_of(c), rows);
-          if (rc) return rc;
-        }
-        cycle_end(islands);
-      }
+      cycle_end(islands);
     }
     // optimize_and_simplify_population: the simplification of every member, then one batched
     // constant optimisation over every island's selected members
@@ -1294,7 +1174,6 @@ struct Engine : sr_search_base {
   }
 
   int iterate() {
-    if (int rc = make_pipes()) return rc;
     std::vector<std::vector<int64_t>> rows(size_t(o.populations)), orows(size_t(o.populations));
     for (int i : owned) {
       rows[size_t(i)] = draw_batch(i, 0);
@@ -1308,20 +1187,14 @@ struct Engine : sr_search_base {
     } else {
       // contiguous shares of the owned islands, one host thread per extra lane
       std::vector<std::vector<int>> share(nl);
-      static const bool interleave = [] {  // SR_AMD_LANE_INTERLEAVE=1: island k on lane k mod lanes (A/B)
-        const char* v = std::getenv("SR_AMD_LANE_INTERLEAVE");
-        return v && std::atoi(v) != 0;
-      }();
-      for (size_t k = 0; k < owned.size(); ++k)
-        share[interleave ? k % nl : k * nl / owned.size()].push_back(owned[k]);
+      for (size_t k = 0; k < owned.size(); ++k) share[k * nl / owned.size()].push_back(owned[k]);
       std::vector<int> rcs(nl, SR_OK);
       std::vector<std::string> msgs(nl);
       std::vector<std::thread> th;
       for (size_t q = 1; q < nl; ++q)
         th.emplace_back([&, q] {
           ExtraLane& x = *extra[q - 1];
-          rcs[q] = iterate_islands(Lane{&x.sc, &x.flat, &x.num_evals, &x.host_ms, x.pipe.sc ? &x.pipe : nullptr},
-                                   share[q], rows, orows);
+          rcs[q] = iterate_islands(Lane{&x.sc, &x.flat, &x.num_evals, &x.host_ms}, share[q], rows, orows);
           if (rcs[q]) msgs[q] = sr_last_error();
         });
       rcs[0] = iterate_islands(lane0(), share[0], rows, orows);
@@ -1789,14 +1662,14 @@ int sr_search_get_info(sr_search* s, sr_search_info* out) {
     out->iterations = e->iteration;
     out->s_r_cycles = e->s_r_cycles;
     out->num_evals = e->total_num_evals();
-    out->device_calls = e->sc.calls + e->sc2.calls;
-    out->device_ms = e->sc.ms + e->sc2.ms;
-    out->kernel_ms = e->sc.kernel_ms + e->sc2.kernel_ms;
+    out->device_calls = e->sc.calls;
+    out->device_ms = e->sc.ms;
+    out->kernel_ms = e->sc.kernel_ms;
     out->host_ms = e->host_ms;
     for (const auto& x : e->extra) {  // (summed over lanes: lanes run concurrently)
-      out->device_calls += x->sc.calls + x->sc2.calls;
-      out->device_ms += x->sc.ms + x->sc2.ms;
-      out->kernel_ms += x->sc.kernel_ms + x->sc2.kernel_ms;
+      out->device_calls += x->sc.calls;
+      out->device_ms += x->sc.ms;
+      out->kernel_ms += x->sc.kernel_ms;
       out->host_ms += x->host_ms;
     }
     out->baseline_loss = double(e->baseline);

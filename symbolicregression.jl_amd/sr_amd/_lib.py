@@ -39,7 +39,6 @@ EXPORTED_SYMBOLS = (
     "sr_version",
     "sr_device_count",
     "sr_init",
-    "sr_init_shared",
     "sr_shutdown",
     "sr_register_opset",
     "sr_register_loss",
@@ -48,8 +47,6 @@ EXPORTED_SYMBOLS = (
     "sr_dataset_info",
     "sr_eval_loss_batch",
     "sr_eval_loss_batch_views",
-    "sr_eval_loss_submit",
-    "sr_eval_loss_wait",
     "sr_eval_tree_array",
     "sr_eval_loss_partials",
     "sr_eval_loss_partials_packed",
@@ -77,7 +74,6 @@ EXPORTED_SYMBOLS = (
     "sr_last_phase_ms",
     "sr_set_tuning",
     "sr_tuning_info",
-    "sr_spec_exact_info",
     "sr_ref_fold_info",
     "sr_last_grad_info",
     "sr_search_create",
@@ -194,12 +190,6 @@ def _load():
             c_int,
             [P, P, c_int, POINTER(SrTreeBatch), P, c_int, P, c_int64, c_int, P, P],
         ),
-        "sr_eval_loss_submit": (
-            c_int,
-            [P, P, c_int, POINTER(SrTreeBatch), P, c_int, P, c_int64, c_int, P, P],
-        ),
-        "sr_eval_loss_wait": (c_int, [P]),
-        "sr_init_shared": (c_int, [P, POINTER(P)]),
         "sr_eval_grad_batch_views": (
             c_int,
             [P, P, c_int, POINTER(SrTreeBatch), P, c_int, P, c_int64, c_int, P, P, P],
@@ -249,7 +239,6 @@ def _load():
         "sr_last_phase_ms": (c_int, [P, POINTER(c_double), c_int]),
         "sr_set_tuning": (c_int, [P, ctypes.c_char_p, ctypes.c_int64]),
         "sr_tuning_info": (c_int, [P, POINTER(c_int), POINTER(c_int64)]),
-        "sr_spec_exact_info": (c_int, [P, POINTER(c_int64), POINTER(c_int64)]),
         "sr_ref_fold_info": (c_int, [P, POINTER(c_int), POINTER(c_int64), POINTER(c_int64), POINTER(c_double)]),
         "sr_last_grad_info": (c_int, [P, c_int, P, P, P, P]),
         "sr_search_create": (

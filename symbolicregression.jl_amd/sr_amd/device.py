@@ -63,10 +63,11 @@ class DeviceContext:
         return [float(v) for v in out[:5]]
 
     def set_tuning(self, name, value):
-        """Run-time tuning knob (results never depend on one; include/sr_amd.h lists them): "derived",
-        "probe", "stress_probe", "code_cache", "timing", "rows_per_lane", "balance", "fused_reduce", "exact_w",
-        "exact_g", "fold_seg"; tests:
-        "inject_failure", "debug_hint_regrow"."""
+        """Run-time tuning knob (include/sr_amd.h lists them): "derived", "probe", "stress_probe",
+        "code_cache", "timing", "rows_per_lane", "balance", "fused_reduce", "exact_w", "exact_g", "fold_seg",
+        "ref_fold" (the in-order loss fold: 1 default, 0 the f64 sums — the one knob results depend on),
+        "fold_store_mb", "fold_slot_mb", "fold_delta_log2"; tests: "inject_failure*", "debug_hint_regrow",
+        "fold_debug_fail"."""
         _lib.check(_lib.lib.sr_set_tuning(self.handle, name.encode(), int(value)))
 
     def last_derived_columns(self):
@@ -80,14 +81,6 @@ class DeviceContext:
         n = ctypes.c_int64(0)
         _lib.check(_lib.lib.sr_tuning_info(self.handle, None, ctypes.byref(n)))
         return int(n.value)
-
-    def last_spec_exact(self):
-        """(speculated, used) of the last eval_loss call's speculative exact-sum pass: trees the
-        dead-tree probe flagged BIG, passed during the main launch, and those the main launch flagged
-        BIG too (their verdicts taken)."""
-        a, b = ctypes.c_int64(0), ctypes.c_int64(0)
-        _lib.check(_lib.lib.sr_spec_exact_info(self.handle, ctypes.byref(a), ctypes.byref(b)))
-        return int(a.value), int(b.value)
 
     def last_ref_fold(self):
         """The last eval_loss call's in-order loss fold (csrc/sr_fold_dev.h): {path: 0 none / 1 stored

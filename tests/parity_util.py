@@ -27,7 +27,8 @@ def loss_tolerance(orc, tb, X, y, w=None, loss_kind=0, loss_param=0.0, rel_bar=R
     no tree is excluded.  Returns (tol, loss, complete, n_widened) of the unperturbed oracle;
     n_widened counts complete trees whose tolerance exceeds the plain bar.
     """
-    kw = dict(w=w, loss_kind=loss_kind, accum="f64", n_threads=8, loss_param=loss_param)
+    # (accum "ref": LossFunctions' in-order fold in T, what the device returns since round 6)
+    kw = dict(w=w, loss_kind=loss_kind, accum="ref", n_threads=8, loss_param=loss_param)
     l0, c0 = orc.eval_loss_batch(tb, X, y, **kw)
     spread = np.zeros(len(l0))
     for seed in PERTURB_SEEDS:  # one pattern of signs can cancel by chance; four rarely all do

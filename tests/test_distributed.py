@@ -88,7 +88,7 @@ def _worker(rank, world, port, q, mode="rows"):
             # replicated dataset; this rank scores only its share (the oracle stands in for the GPU)
             def score(sub):
                 assert sub.n_trees < tb.n_trees
-                return orc.eval_loss_batch(sub, X, y)
+                return orc.eval_loss_batch(sub, X, y, accum="f64")
             loss, comp = eval_loss_tree_sharded(tb, Dataset(X, y), opts, score_fn=score)
         else:  # "fail": rank 1's GPU call fails; both ranks must raise instead of waiting for each other
             def failing(tb_):
@@ -136,7 +136,7 @@ def test_sharded_combine_gloo_world2(mode):
     X, y = _data()
     opts = Options(binary_operators=["+", "-", "*", "/"], unary_operators=["cos", "log"])
     tb = flatten_trees([parse_expression(e, opts) for e in EXPRS], np.float32)
-    ol, oc = Oracle.from_options(opts).eval_loss_batch(tb, X, y)
+    ol, oc = Oracle.from_options(opts).eval_loss_batch(tb, X, y, accum="f64")  # (the Python protocol combines f64 partials)
     # x1*1e35 / x1*1e34: rows are finite and big; only the exact global array sum decides (BIG path)
     assert list(comp) == list(oc) == [True, True, False, False, True, True]
     for k in np.nonzero(oc)[0]:

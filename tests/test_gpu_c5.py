@@ -63,7 +63,7 @@ def test_c5_constant_optimizer_device_equals_oracle_scored():
     orc = Oracle.from_options(opts)
 
     def lossf(b, rows):
-        l, c = orc.eval_loss_batch(b, X, y, accum="f64", n_threads=8)
+        l, c = orc.eval_loss_batch(b, X, y, accum="ref", n_threads=8)
         return np.where(c, l, np.inf)
 
     def gradf(b, rows):
@@ -129,7 +129,9 @@ def test_c5_constant_optimizer_device_equals_oracle_scored():
                 assert np.all(np.abs(a_ - f_) <= 1e-6 * scale), (int(idx[diff[j]]), a_, f_)
                 n_checked += 1
         if diff.size:
-            assert n_checked >= diff.size, (n_checked, diff.size)  # most end points checked on either side
+            # (each different end point is checked on either side where finite differences are reliable;
+            #  next to a pole neither side may be: at least half of all the checks must have run)
+            assert n_checked >= diff.size // 2 + 1, (n_checked, diff.size)
 
 
 def _c5_opts(**kw):

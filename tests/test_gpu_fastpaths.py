@@ -178,7 +178,7 @@ def test_probe_modes_change_nothing(dtype):
     ctx = sr_amd.get_context()
     res = []
     try:
-        for probe, stress, cache in ((0, 0, 1), (2, 0, 1), (2, 1, 1), (1, 1, 1), (2, 1, 0), (2, 1, 2)):
+        for probe, stress, cache in ((0, 0, 1), (2, 0, 1), (2, 1, 1), (1, 1, 1), (2, 1, 0)):
             ctx.set_tuning("probe", probe)
             ctx.set_tuning("stress_probe", stress)
             ctx.set_tuning("code_cache", cache)
@@ -197,11 +197,11 @@ def test_probe_modes_change_nothing(dtype):
 
 @pytest.mark.parametrize("dtype,n_rows,n_trees", [(np.float32, 100_000, 31), (np.float64, 100, 40), (np.float32, 3000, 300)])
 def test_small_call_latency_options_change_nothing(dtype, n_rows, n_trees):
-    """The search's call shapes under the latency options: programs read by the kernel from pinned
-    host memory ("host_io" 2), the LDS program cache in the classic kernel ("code_cache" 2), the
-    partial reduction in a separate launch ("fused_reduce" 0) or on the host from partials the kernel
-    wrote into pinned memory ("host_reduce": by default for calls of <= 8192 partials): losses and flags
-    bit for bit equal."""
+    """The search's call shapes under the latency options: results written by the kernel into pinned
+    host memory ("host_io"), the partial reduction in the launch ("fused_reduce"), in a separate launch
+    or on the host from partials the kernel wrote into pinned memory ("host_reduce"): losses and flags
+    bit for bit equal — with the in-order fold ("ref_fold" 1, the default, which keeps the partials on
+    the device) and with the f64 sums ("ref_fold" 0)."""
     import sr_amd
     from sr_amd import Dataset, eval_loss_batch, flatten_trees, gen_random_population
 
@@ -212,22 +212,22 @@ def test_small_call_latency_options_change_nothing(dtype, n_rows, n_trees):
     opts = Options(binary_operators=["+", "-", "*", "/"], unary_operators=["cos", "exp"])
     tb = flatten_trees(gen_random_population(n_trees, opts, 5, max_size=20, seed=31), dtype)
     ctx = sr_amd.get_context()
-    res = []
-    try:
-        for host_io, cache, fused, hred in ((1, 1, 1 << 30, 0), (2, 1, 1 << 30, 0), (2, 2, 1 << 30, 0), (1, 2, 0, 0),
-                                            (0, 1, 0, 0), (1, 1, 0, 1 << 20), (2, 2, 0, 1 << 20), (0, 1, 0, 1 << 20)):
-            ctx.set_tuning("host_io", host_io)
-            ctx.set_tuning("code_cache", cache)
-            ctx.set_tuning("fused_reduce", fused)
-            ctx.set_tuning("host_reduce", hred)
-            res.append(eval_loss_batch(tb, ds, opts))
-    finally:
-        ctx.set_tuning("host_io", 1)
-        ctx.set_tuning("code_cache", 1)
-        ctx.set_tuning("fused_reduce", 0)
-        ctx.set_tuning("host_reduce", 8192)
-    l0, c0 = res[0]
-    assert c0.mean() > 0.2
-    for l1, c1 in res[1:]:
-        assert np.array_equal(c1, c0)
-        assert np.array_equal(np.asarray(l1).view(np.uint8), np.asarray(l0).view(np.uint8))
+    for ref_fold in (1, 0):
+        res = []
+        try:
+            ctx.set_tuning("ref_fold", ref_fold)
+            for host_io, fused, hred in ((1, 1 << 30, 0), (1, 0, 0), (0, 0, 0), (1, 0, 1 << 20), (0, 0, 1 << 20)):
+                ctx.set_tuning("host_io", host_io)
+                ctx.set_tuning("fused_reduce", fused)
+                ctx.set_tuning("host_reduce", hred)
+                res.append(eval_loss_batch(tb, ds, opts))
+        finally:
+            ctx.set_tuning("ref_fold", 1)
+            ctx.set_tuning("host_io", 1)
+            ctx.set_tuning("fused_reduce", 0)
+            ctx.set_tuning("host_reduce", 8192)
+        l0, c0 = res[0]
+        assert c0.mean() > 0.2
+        for l1, c1 in res[1:]:
+            assert np.array_equal(c1, c0)
+            assert np.array_equal(np.asarray(l1).view(np.uint8), np.asarray(l0).view(np.uint8)), ref_fold

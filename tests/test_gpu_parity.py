@@ -426,7 +426,9 @@ def test_empty_batch_and_errors():
 
 # ------------------------------------------------------------------ large sizes: size-independent properties
 def test_large_rows_properties():
-    """1M rows (BASELINE C2 size): linear trees against closed forms computed in f64 by numpy."""
+    """1M rows (BASELINE C2 size): linear trees against LossFunctions' in-order Float32 fold of their
+    Float32 predictions (numpy's add.accumulate is a sequential fold), bit for bit; the f64 closed form
+    is ~1e-3 away at this size (the fold's own rounding)."""
     opts = Options(**C2_OPTS)
     n = 1 << 20
     X, y = _c2_data(n, seed=51)
@@ -435,27 +437,33 @@ def test_large_rows_properties():
     trees = [parse_expression(e, opts) for e in exprs]
     loss, comp = eval_loss_batch(trees, d, opts)
     assert comp.all()
-    x = X.astype(np.float64)
-    yy = y.astype(np.float64)
-    pred = [x[0], x[0] * 2.0, x[0] + x[1]]
+    pred = [X[0], X[0] * np.float32(2.0), X[0] + X[1]]
     for k in range(3):
-        exact = np.mean((pred[k] - yy) ** 2)
-        assert _rel(loss[k], exact) < 1e-5, (exprs[k], loss[k], exact)
+        d2 = ((pred[k] - y) * (pred[k] - y)).astype(np.float32)
+        fold = np.float32(np.add.accumulate(d2, dtype=np.float32)[-1] / np.float32(n))
+        assert loss[k].view(np.uint32) == fold.view(np.uint32), (exprs[k], loss[k], fold)
+        exact = np.mean((pred[k].astype(np.float64) - y) ** 2)
+        assert _rel(loss[k], exact) < 1e-2
     # the generating formula: loss ~ noise variance 0.01
     assert abs(float(loss[3]) - 0.01) < 1e-3
-    # same answer through a SubDataset covering all rows in order (gather path)
+    # same answer through a SubDataset covering all rows in order (gather path): bit for bit
     l2, c2 = eval_loss_batch(trees, batch(d, np.arange(n)), opts)
-    assert np.max(_rel(l2, loss)) < 1e-6
+    assert np.array_equal(l2.view(np.uint32), loss.view(np.uint32))
 
 
 def test_row_sharded_partials_match_single():
-    """The multi-GPU building block: Σ over row shards of sr_eval_loss_partials == one full eval."""
+    """The multi-GPU building block: Σ over row shards of sr_eval_loss_partials (f64 partial sums) == one
+    full eval with the f64 sums ("ref_fold" 0)."""
     opts = Options(**C2_OPTS)
     n = 20000
     X, y = _c2_data(n, seed=61)
     tb = flatten_trees(gen_random_population(700, opts, 5, seed=61), np.float32)
-    full_loss, full_comp = eval_loss_batch(tb, Dataset(X, y), opts)
     ctx = sr_amd.get_context()
+    ctx.set_tuning("ref_fold", 0)
+    try:
+        full_loss, full_comp = eval_loss_batch(tb, Dataset(X, y), opts)
+    finally:
+        ctx.set_tuning("ref_fold", 1)
     oid = ctx.opset_id(opts.operators)
     sums = np.zeros(tb.n_trees)
     flags = np.zeros(tb.n_trees, dtype=np.uint32)
@@ -480,8 +488,8 @@ def test_row_sharded_partials_match_single():
 @pytest.mark.parametrize("max_rb", [1, 7, 1000])
 def test_row_block_bound_keeps_results(monkeypatch, max_rb):
     """SR_AMD_MAX_ROW_BLOCKS only regroups rows into workgroups (one tile per block up to every tile
-    in one block): flags stay bit-identical to the default grid and to the oracle, losses move only
-    by the f64 partial-sum grouping."""
+    in one block): flags and losses (the in-order fold) stay bit-identical to the default grid, and
+    equal the oracle's."""
     opts = Options(**C2_OPTS)
     X, y = _c2_data(100_000, seed=83)
     trees = flatten_trees(gen_random_population(1500, opts, 5, max_size=30, seed=83), np.float32)
@@ -494,7 +502,8 @@ def test_row_block_bound_keeps_results(monkeypatch, max_rb):
     assert np.array_equal(comp, ref_comp)
     fin = np.isfinite(ref_loss)
     assert np.array_equal(fin, np.isfinite(loss))
-    assert np.max(_rel(loss[fin], ref_loss[fin]), initial=0.0) < 1e-6
+    # the in-order fold does not depend on how rows are grouped: bit for bit
+    assert np.array_equal(loss[fin].view(np.uint32), ref_loss[fin].view(np.uint32))
     sub = flatten_trees([trees.tree(i) for i in range(0, 1500, 15)], np.float32)
     tol, ol, oc, _ = loss_tolerance(Oracle.from_options(opts), sub, X, y)
     assert np.array_equal(comp[::15], oc)
@@ -544,7 +553,12 @@ def test_row_sharded_packed_with_exact_path():
     trees = gen_random_population(600, opts, 5, seed=91)
     trees += [parse_expression(e, opts) for e in ("x3 * 1.0", "x3 + x1", "x5 * 1.0", "(x5 * 0.5) + (x1 * 1.0)")]
     tb = flatten_trees(trees, np.float32)
-    full_loss, full_comp = eval_loss_batch(tb, Dataset(X, y), opts)
+    ctx = sr_amd.get_context()
+    ctx.set_tuning("ref_fold", 0)  # (the building blocks return f64 sums)
+    try:
+        full_loss, full_comp = eval_loss_batch(tb, Dataset(X, y), opts)
+    finally:
+        ctx.set_tuning("ref_fold", 1)
     cut = 4321
     shards = [Dataset(np.ascontiguousarray(X[:, :cut]), np.ascontiguousarray(y[:cut])),
               Dataset(np.ascontiguousarray(X[:, cut:]), np.ascontiguousarray(y[cut:]))]
@@ -564,11 +578,11 @@ def test_row_sharded_packed_with_exact_path():
 
 
 @pytest.mark.parametrize("dtype", [np.float32, np.float64])
-def test_speculative_exact_pass_equals_the_ordinary_one(dtype):
-    """Round 5: trees the dead-tree probe flags BIG over the stress rows go through the exact-sum pass
-    on a third stream during the main launch (tuning "spec_exact").  The results must equal the
-    ordinary after-the-launch pass bit for bit (the main launch's flags decide which verdicts are
-    used), the speculative path must actually have run, and the flags must equal the oracle's."""
+def test_exact_pass_after_a_probed_launch(dtype):
+    """Trees the dead-tree probe already sees BIG over the stress rows (mixed +-2e35 blocks, sums just
+    past floatmax) go through the exact-sum pass after the main launch; with a probe before every
+    chunk the flags must equal the oracle's and the call must equal the unprobed one.  (Round 5's
+    speculative pass that ran this pass during the main launch was measured neutral and removed.)"""
     from test_jsum import cases
 
     opts = Options(**C2_OPTS)
@@ -587,17 +601,13 @@ def test_speculative_exact_pass_equals_the_ordinary_one(dtype):
     ctx = sr_amd.get_context()
     try:
         ctx.set_tuning("probe", 1)  # (a probe before every chunk: this call is below the default's size)
-        ctx.set_tuning("spec_exact", 1)
         loss_s, comp_s = eval_loss_batch(tb, ds, opts)
-        spec, used = ctx.last_spec_exact()
         n_exact = ctx.last_exact_trees()
-        ctx.set_tuning("spec_exact", 0)
+        ctx.set_tuning("probe", 0)
         loss_o, comp_o = eval_loss_batch(tb, ds, opts)
-        assert ctx.last_spec_exact() == (0, 0)
     finally:
         ctx.set_tuning("probe", 2)
-        ctx.set_tuning("spec_exact", 0)
-    assert spec > 0 and used > 0 and used <= n_exact, (spec, used, n_exact)
+    assert n_exact > 0
     assert np.array_equal(comp_s, comp_o)
     assert np.array_equal(loss_s, loss_o, equal_nan=True)
     _, oc = Oracle.from_options(opts).eval_loss_batch(tb, X, y, n_threads=8)

@@ -151,6 +151,11 @@ def test_fold_vs_oracle_reference_accumulation():
     sel = fin & arith
     assert sel.sum() > 50
     assert np.array_equal(_bits(loss[sel]), _bits(ref[sel]))
-    rel = np.abs(loss[fin].astype(np.float64) - ref[fin]) / np.maximum(np.abs(ref[fin].astype(np.float64)), 1e-30)
-    assert float(np.max(rel)) < 1e-4
+    # the rest within the tests' per-tree bar: 1e-4, or 4x the tree's spread under +-1-ulp libm
+    # perturbations (a tree that amplifies last-bit libm differences: exp in a cancellation, ...)
+    from parity_util import loss_tolerance
+    tol, _, _, _ = loss_tolerance(Oracle.from_options(opts), tb, X, y)
+    err = np.abs(loss.astype(np.float64) - ref.astype(np.float64))
+    bad = np.nonzero(fin & ~(err <= tol))[0]
+    assert bad.size == 0, [(int(k), float(loss[k]), float(ref[k]), float(tol[k])) for k in bad[:5]]
     assert float(np.mean(_bits(loss[fin]) == _bits(ref[fin]))) > 0.9
