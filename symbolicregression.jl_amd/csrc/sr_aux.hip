@@ -609,8 +609,8 @@ struct SrStoredRows {
 template <typename T>
 __global__ void __launch_bounds__(256) sr_fold_plan_kernel(const double* __restrict__ part, int np, int n_rb,
                                                            const uint32_t* __restrict__ perm, SrFoldWho who,
-                                                           double delta, int32_t* __restrict__ code,
-                                                           int* __restrict__ slot_next, int slot_cap) {
+                                                           double delta, SrFoldTabs ft, int* __restrict__ slot_next,
+                                                           int slot_cap) {
   const int lane = int(threadIdx.x) & 63;
   const int p = int(blockIdx.x) * 4 + int(threadIdx.x) / 64;
   if (p >= np) return;  // wave-uniform
@@ -630,12 +630,14 @@ __global__ void __launch_bounds__(256) sr_fold_plan_kernel(const double* __restr
     }
     const double sb = run + (inc - v), sa = run + inc;  // (estimates: they only choose binades)
     run += __shfl(inc, 63, 64);
-    int32_t cd = SR_FCODE_SKIP;
+    int32_t cd = SR_FCODE_SKIP, sqv = SR_FCODE_SKIP;
     bool slow = false;
     if (ok && in) {
       const int qa = sr_fold_q<T>(sb * (1.0 - delta));
-      slow = (rb == 0 && who.first) || qa != sr_fold_q<T>(sa * (1.0 + delta));
+      const bool first = rb == 0 && who.first;
+      slow = first || qa != sr_fold_q<T>(sa * (1.0 + delta));
       cd = qa;
+      if (slow && !first) sqv = qa;  // (the FOLD pass composes its steps under qa and qa + 1 too)
     }
     const uint64_t sm = __builtin_amdgcn_ballot_w64(slow);
     if (sm) {
@@ -645,50 +647,21 @@ __global__ void __launch_bounds__(256) sr_fold_plan_kernel(const double* __restr
       const int k = base + __popcll(sm & ((uint64_t(1) << lane) - 1u));
       if (slow) cd = k < slot_cap ? SR_FCODE_SLOT0 + k : SR_FCODE_SKIP;
     }
-    if (in) code[size_t(rb) * size_t(np) + size_t(p)] = cd;
+    if (in) {
+      ft.code[size_t(rb) * size_t(np) + size_t(p)] = cd;
+      ft.sq[size_t(rb) * size_t(np) + size_t(p)] = sqv;
+    }
   }
 }
 
-// Small calls: the loss launch stored every position's losses ([position][pos_stride], pos_stride =
-// n_rb x rb_rows, so segment rb of position p is slot p n_rb + rb); one workgroup per (segment,
-// position) decides its code and composes a steps segment's pair in row order.
+// the ordered composition of a stored segment's steps under binade spacing 2^q (the whole workgroup;
+// thread 0 holds the result)
 template <typename T, int R>
-__global__ void __launch_bounds__(256) sr_fold_stab_kernel(const double* __restrict__ part, int np, int n_rb,
-                                                           int64_t rb_rows, int64_t n, const uint32_t* __restrict__ perm,
-                                                           SrFoldWho who, double delta, const T* __restrict__ losses,
-                                                           int32_t* __restrict__ code,
-                                                           typename SrFoldTab<T>::Pair* __restrict__ tab) {
+__device__ typename SrFoldTab<T>::Pair sr_fold_stab_pair(const SrStoredRows<T>& rw, int64_t lo, int64_t hi, int q,
+                                                         int tid, typename SrFoldTab<T>::I (*s_v)[2]) {
   using I = typename SrFoldTab<T>::I;
   constexpr I CAP = I(1) << (SrFoldTraits<T>::mant + 3);
-  const int rb = int(blockIdx.x), p = int(blockIdx.y), tid = int(threadIdx.x), lane = tid & 63, wave = tid >> 6;
-  const uint32_t t = perm ? perm[p] : uint32_t(p);
-  const size_t o = size_t(rb) * size_t(np) + size_t(p);
-  if (!who.eligible<T>(t)) {
-    if (tid == 0) code[o] = SR_FCODE_SKIP;
-    return;
-  }
-  const int32_t slow_code = SR_FCODE_SLOT0 + p * n_rb + rb;
-  if (rb == 0 && who.first) {
-    if (tid == 0) code[o] = slow_code;
-    return;
-  }
-  __shared__ double s_d[4];
-  __shared__ I s_v[4][2];
-  double pre = 0.0;
-  for (int i = tid; i < rb; i += 256) pre += part[size_t(i) * size_t(np) + size_t(p)];  // (rb > 0: part is set)
-#pragma unroll
-  for (int off = 32; off >= 1; off >>= 1) pre += __shfl_xor(pre, off, 64);
-  if (lane == 0) s_d[wave] = pre;
-  __syncthreads();
-  const double sb = (who.est ? who.est[t] : 0.0) + ((s_d[0] + s_d[1]) + (s_d[2] + s_d[3]));
-  const double sa = sb + (part ? part[o] : who.sums[t]);  // (one row block: the view's total)
-  const int q = sr_fold_q<T>(sb * (1.0 - delta));
-  if (q != sr_fold_q<T>(sa * (1.0 + delta))) {
-    if (tid == 0) code[o] = slow_code;
-    return;
-  }
-  const int64_t lo = int64_t(rb) * rb_rows, hi = lo + rb_rows < n ? lo + rb_rows : n;
-  const SrStoredRows<T> rw{losses + (size_t(p) * size_t(n_rb) + size_t(rb)) * size_t(rb_rows), lo};
+  const int lane = tid & 63, wave = tid >> 6;
   I ta0 = 0, ta1 = 0;  // the segment so far (thread 0)
   for (int64_t base = lo; base < hi; base += 256 * R) {
     I a0 = 0, a1 = 0;
@@ -726,46 +699,126 @@ __global__ void __launch_bounds__(256) sr_fold_stab_kernel(const double* __restr
     }
     __syncthreads();
   }
+  return SrFoldTab<T>::pair(ta0, ta1);
+}
+
+// Small calls: the loss launch stored every position's losses ([position][pos_stride], pos_stride =
+// n_rb x rb_rows, so segment rb of position p is slot p n_rb + rb); one workgroup per (segment,
+// position) decides its code and composes a steps segment's pair in row order (a slow segment's under
+// its lower window binade and the next).
+template <typename T, int R>
+__global__ void __launch_bounds__(256) sr_fold_stab_kernel(const double* __restrict__ part, int np, int n_rb,
+                                                           int64_t rb_rows, int64_t n, const uint32_t* __restrict__ perm,
+                                                           SrFoldWho who, double delta, const T* __restrict__ losses,
+                                                           SrFoldTabs ft) {
+  using I = typename SrFoldTab<T>::I;
+  using Pair = typename SrFoldTab<T>::Pair;
+  int32_t* __restrict__ code = ft.code;
+  const int rb = int(blockIdx.x), p = int(blockIdx.y), tid = int(threadIdx.x), lane = tid & 63, wave = tid >> 6;
+  const uint32_t t = perm ? perm[p] : uint32_t(p);
+  const size_t o = size_t(rb) * size_t(np) + size_t(p);
+  if (!who.eligible<T>(t)) {
+    if (tid == 0) {
+      code[o] = SR_FCODE_SKIP;
+      ft.sq[o] = SR_FCODE_SKIP;
+    }
+    return;
+  }
+  const int32_t slow_code = SR_FCODE_SLOT0 + p * n_rb + rb;
+  if (rb == 0 && who.first) {
+    if (tid == 0) {
+      code[o] = slow_code;
+      ft.sq[o] = SR_FCODE_SKIP;
+    }
+    return;
+  }
+  __shared__ double s_d[4];
+  __shared__ I s_v[4][2];
+  double pre = 0.0;
+  for (int i = tid; i < rb; i += 256) pre += part[size_t(i) * size_t(np) + size_t(p)];  // (rb > 0: part is set)
+#pragma unroll
+  for (int off = 32; off >= 1; off >>= 1) pre += __shfl_xor(pre, off, 64);
+  if (lane == 0) s_d[wave] = pre;
+  __syncthreads();
+  const double sb = (who.est ? who.est[t] : 0.0) + ((s_d[0] + s_d[1]) + (s_d[2] + s_d[3]));
+  const double sa = sb + (part ? part[o] : who.sums[t]);  // (one row block: the view's total)
+  const int q = sr_fold_q<T>(sb * (1.0 - delta));
+  const bool slow = q != sr_fold_q<T>(sa * (1.0 + delta));
+  const int64_t lo = int64_t(rb) * rb_rows, hi = lo + rb_rows < n ? lo + rb_rows : n;
+  const SrStoredRows<T> rw{losses + (size_t(p) * size_t(n_rb) + size_t(rb)) * size_t(rb_rows), lo};
+  // a steps segment's pair under q; a slow segment's under q and q + 1 (the walk uses them when the
+  // running value stays in one binade there after all)
+  for (int v = 0; v < (slow ? 2 : 1); ++v) {
+    const Pair pr = sr_fold_stab_pair<T, R>(rw, lo, hi, q + v, tid, s_v);
+    if (tid == 0) (v == 0 ? static_cast<Pair*>(ft.tab) : static_cast<Pair*>(ft.tab2))[o] = pr;
+  }
   if (tid == 0) {
-    tab[o] = SrFoldTab<T>::pair(ta0, ta1);
-    code[o] = q;
+    code[o] = slow ? slow_code : q;
+    ft.sq[o] = slow ? q : SR_FCODE_SKIP;
+  }
+}
+// One pass of a slow segment: 64 x RW rows from b0 (16-byte aligned in the segment's storage, row i at
+// base[i - lo]), lane l holding rows b0 + l RW ...  Branch-free and unmasked: a chunk past the view
+// loads the view's last chunk (a valid address) and the rows at or past hi are masked where they are
+// used, so the loads stay in flight until then (a load under a branch, or one whose value is selected
+// right away, waits at once).
+template <typename T, int RW>
+__device__ __forceinline__ void sr_fold_load(const T* __restrict__ base, int64_t lo, int64_t b0, int64_t hi, int lane,
+                                             T (&ev)[RW]) {
+  constexpr int C = 16 / int(sizeof(T));
+  using V = typename std::conditional<sizeof(T) == 4, float4, double2>::type;
+  const int64_t r0 = b0 + int64_t(lane) * RW;
+  const int64_t last = hi - 1 - ((hi - 1 - lo) % C);
+#pragma unroll
+  for (int c = 0; c < RW / C; ++c) {
+    const int64_t rc = r0 + c * C;
+    const V v = *reinterpret_cast<const V*>(base + ((rc < last ? rc : last) - lo));
+#pragma unroll
+    for (int j = 0; j < C; ++j) ev[c * C + j] = reinterpret_cast<const T*>(&v)[j];
   }
 }
 
 // One wave folds rows [k, hi) of a slow segment into F exactly (row i's loss at base[i - lo]), 64 x RW
-// rows per load: each lane holds RW consecutive rows.  Per round, under the binade of F: every row's
+// rows per pass: each lane holds RW consecutive rows.  Per round, under the binade of F: every row's
 // step, each lane's composition, an ordered inclusive scan over the lanes; a round that leaves the
 // binade ends at the first row whose step reaches it (that lane re-walks its rows from its exclusive
 // prefix), the hardware add takes that row, and the next round continues in the SAME registers from the
-// row after it (rows before k are identity steps) until the load is used up.  Fast path (no row of the
+// row after it (rows before k are identity steps) until the pass is used up.  Fast path (no row of the
 // round at an exact half ulp): every step is rint(l 2^-q) whatever the parity, so the compositions are
-// plain sums; otherwise the pair composition (sr_fold_add_i / sr_fold_compose_i).
+// plain sums (a DPP scan in T: exact below the binade's limit, monotone past it); otherwise the pair
+// composition (sr_fold_add_i / sr_fold_compose_i).
+// Software pipelining: ev holds the pass at k's 16-byte boundary on entry (k is the segment's first row
+// or row 1); each pass first issues the load of the next one — the segment's next pass, else the first
+// pass of the next slow segment (nbase, rows [nlo, nhi); NULL: none) — into nx, so its latency hides
+// behind this pass's rounds.  On return ev holds the next slow segment's first pass when nbase was set.
 template <typename T, int RW>
 __device__ T sr_fold_rows_wave(const T* __restrict__ base, int64_t lo, int64_t k, int64_t hi, T F, int lane,
-                               int& rounds) {
+                               int& rounds, T (&ev)[RW], const T* __restrict__ nbase, int64_t nlo, int64_t nhi) {
   using Tr = SrFoldTraits<T>;
   using I = typename SrFoldTab<T>::I;
   constexpr I CAP = I(1) << (Tr::mant + 3);
   constexpr T CLAMP = T(int64_t(1) << (Tr::mant + 2));
   constexpr int C = 16 / int(sizeof(T));
-  using V = typename std::conditional<sizeof(T) == 4, float4, double2>::type;
   constexpr T MIN_NORMAL = sizeof(T) == 4 ? T(1.17549435e-38f) : T(2.2250738585072014e-308);
+  T nx[RW];
   while (k < hi) {
-    const int64_t b0 = k - ((k - lo) % C);  // (16-byte aligned runs of the segment's storage)
+    const int64_t b0 = k - ((k - lo) % C);
     const int64_t r0 = b0 + int64_t(lane) * RW;
     const int64_t pass_end = b0 + int64_t(64) * RW;
-    T ev[RW];
+    {  // (one unconditional load: no next pass re-loads this one)
+      const bool same = pass_end < hi;
+      const T* pb = same ? base : (nbase ? nbase : base);
+      const int64_t plo = same ? lo : (nbase ? nlo : lo), pb0 = same ? pass_end : (nbase ? nlo : b0),
+                    phi = same ? hi : (nbase ? nhi : hi);
+      sr_fold_load<T, RW>(pb, plo, pb0, phi, lane, nx);
+    }
+    // the pass's rows before k and at or past hi are identity steps: zeroed once here, and the rows up to
+    // each crossing once after it (the rounds read ev as it is)
+    {
+      const int64_t dk = k - r0, dh = hi - r0;
+      const int rk = dk < 0 ? 0 : (dk > RW ? RW : int(dk)), rh = dh < 0 ? 0 : (dh > RW ? RW : int(dh));
 #pragma unroll
-    for (int c = 0; c < RW / C; ++c) {
-      const int64_t rc = r0 + c * C;
-      if (rc < hi) {
-        const V v = *reinterpret_cast<const V*>(base + (rc - lo));
-#pragma unroll
-        for (int j = 0; j < C; ++j) ev[c * C + j] = (rc + j < hi) ? reinterpret_cast<const T*>(&v)[j] : T(0);
-      } else {
-#pragma unroll
-        for (int j = 0; j < C; ++j) ev[c * C + j] = T(0);
-      }
+      for (int r = 0; r < RW; ++r) ev[r] = (r >= rk && r < rh) ? ev[r] : T(0);
     }
     while (k < hi && k < pass_end) {
       ++rounds;
@@ -783,73 +836,69 @@ __device__ T sr_fold_rows_wave(const T* __restrict__ base, int64_t lo, int64_t k
       }
       const I P = I(ldexp(double(F), -q));
       const bool odd = (P & 1) != 0;
-      // fast path: the round's steps are rint(l 2^-q) unless some row is an exact half
+      // fast path: the round's steps are rint(l 2^-q) unless some row is an exact half (6 VALU a row:
+      // scale, round, residual, max |residual|, clamp, sum; a NaN loss clamps, its residual is ignored)
       T sr[RW];
       T lsum = T(0), dmax = T(0);
 #pragma unroll
       for (int r = 0; r < RW; ++r) {
-        const T e = (r0 + r >= k) ? ev[r] : T(0);
-        const T v = sizeof(T) == 4 ? T(ldexpf(float(e), -q)) : T(ldexp(double(e), -q));
-        T st = sizeof(T) == 4 ? T(rintf(float(v))) : T(rint(double(v)));
-        const T d = v - st;
-        const T ad = d < T(0) ? -d : d;
-        dmax = ad > dmax ? ad : dmax;
-        st = st < CLAMP ? st : CLAMP;  // (also NaN: the clamp)
-        sr[r] = st;
-        lsum += st;
+        const T v = sizeof(T) == 4 ? T(ldexpf(float(ev[r]), -q)) : T(ldexp(double(ev[r]), -q));
+        const T st = sizeof(T) == 4 ? T(rintf(float(v))) : T(rint(double(v)));
+        dmax = sizeof(T) == 4 ? T(fmaxf(float(dmax), fabsf(float(v - st)))) : T(fmax(double(dmax), fabs(double(v - st))));
+        sr[r] = sizeof(T) == 4 ? T(fminf(float(st), float(CLAMP))) : T(fmin(double(st), double(CLAMP)));
+        lsum += sr[r];
       }
-      I i0, i1, x0, x1;  // inclusive / exclusive prefixes over the lanes, from an even and an odd start
       const bool fast = __builtin_amdgcn_ballot_w64(dmax == T(0.5)) == 0;
+      uint64_t cross;
+      I xp = 0;  // the crossing lane's exclusive prefix (from the parity of P)
+      int cl = 0;
       if (fast) {
-        I a = lsum < T(CAP) ? I(lsum) : CAP;
-        I inc = a;
-#pragma unroll
-        for (int off = 1; off < 64; off <<= 1) {
-          const I o = __shfl_up(inc, off, 64);
-          if (lane >= off) inc = inc + o < CAP ? inc + o : CAP;
+        const T inc = sr_fold_scan(lsum);
+        cross = __builtin_amdgcn_ballot_w64(T(P) + inc >= T(lim));
+        if (cross == 0) {  // the rest of this pass stays in the binade
+          F = T(ldexp(double(T(P) + sr_fold_lane(inc, 63)), q));
+          k = pass_end;
+          break;
         }
-        i0 = i1 = inc;
-        // (the exclusive prefix from the lane before: an inclusive prefix may have saturated at CAP, the
-        //  one before the first lane that leaves the binade has not)
-        x0 = __shfl_up(inc, 1, 64);
-        if (lane == 0) x0 = 0;
-        x1 = x0;
+        cl = __builtin_ctzll(cross);
+        // (the prefix before the first lane that leaves the binade is exact)
+        if (cl > 0) xp = I(sr_fold_lane(inc, cl - 1));
       } else {
-        I a0 = 0, a1 = 0;
+        I i0 = 0, i1 = 0;
 #pragma unroll
         for (int r = 0; r < RW; ++r) {
           I m;
           int kind;
-          SrFoldTab<T>::step((r0 + r >= k) ? ev[r] : T(0), q, m, kind);
-          sr_fold_add_i<I>(m, kind, CAP, a0, a1);
+          SrFoldTab<T>::step(ev[r], q, m, kind);
+          sr_fold_add_i<I>(m, kind, CAP, i0, i1);
         }
-        i0 = a0;
-        i1 = a1;
 #pragma unroll
         for (int off = 1; off < 64; off <<= 1) {
           const I l0 = __shfl_up(i0, off, 64), l1 = __shfl_up(i1, off, 64);
           if (lane >= off) sr_fold_compose_i<I>(l0, l1, i0, i1, CAP);
         }
-        x0 = __shfl_up(i0, 1, 64);
-        x1 = __shfl_up(i1, 1, 64);
-        if (lane == 0) x0 = x1 = 0;
+        const I inc = P + (odd ? i1 : i0);
+        cross = __builtin_amdgcn_ballot_w64(inc >= lim);
+        if (cross == 0) {
+          F = T(ldexp(double(__shfl(inc, 63, 64)), q));
+          k = pass_end;
+          break;
+        }
+        cl = __builtin_ctzll(cross);
+        const I x0 = __shfl(i0, cl > 0 ? cl - 1 : 0, 64), x1 = __shfl(i1, cl > 0 ? cl - 1 : 0, 64);
+        if (cl > 0) xp = odd ? x1 : x0;
       }
-      const I inc = P + (odd ? i1 : i0);
-      const uint64_t cross = __builtin_amdgcn_ballot_w64(inc >= lim);
-      if (cross == 0) {  // the rest of this load stays in the binade
-        F = T(ldexp(double(__shfl(inc, 63, 64)), q));
-        k = pass_end;
-        break;
-      }
-      const int cl = __builtin_ctzll(cross);  // the lane whose rows leave the binade
+      // the lane whose rows leave the binade
       T nF = T(0);
       int64_t nk = 0;
       if (lane == cl) {
-        I run = P + (odd ? x1 : x0);
+        I run = P + xp;
         bool done = false;
+        nF = T(__builtin_nan(""));  // (not reached: the lane's rows do leave the binade)
+        nk = pass_end;
 #pragma unroll
         for (int r = 0; r < RW; ++r) {
-          const T e = (r0 + r >= k) ? ev[r] : T(0);
+          const T e = ev[r];
           I d;
           if (fast) {
             d = I(sr[r]);
@@ -869,12 +918,20 @@ __device__ T sr_fold_rows_wave(const T* __restrict__ base, int64_t lo, int64_t k
       }
       F = __shfl(nF, cl, 64);
       k = __shfl(nk, cl, 64);
+      {  // the rows up to the crossing are done
+        const int64_t dk = k - r0;
+        const int rk = dk < 0 ? 0 : (dk > RW ? RW : int(dk));
+#pragma unroll
+        for (int r = 0; r < RW; ++r) ev[r] = r >= rk ? ev[r] : T(0);
+      }
     }
+#pragma unroll
+    for (int r = 0; r < RW; ++r) ev[r] = nx[r];
   }
   return F;
 }
 
-// The walk: one wave per launch position (4 per workgroup), its segments in row order, 64 at a time.
+// The walk: one wave per launch position (one per workgroup), its segments in row order, 64 at a time.
 // Between two slow segments the steps segments share one binade (adjacent windows cannot straddle
 // apart), so each such run is ONE composition — a segmented ordered scan of the chunk's pairs over the
 // lanes — checked against the running value once: its binade must be the run's and the run must end
@@ -882,21 +939,24 @@ __device__ T sr_fold_rows_wave(const T* __restrict__ base, int64_t lo, int64_t k
 // the caller's tree index): the fold's value before this view's first row (a row shard after the
 // first), or NULL: the first loss starts the fold.  out_val / out_st at the caller's tree index.
 template <typename T, int RW>
-__global__ void __launch_bounds__(256) sr_fold_walk_kernel(const int32_t* __restrict__ code,
-                                                           const typename SrFoldTab<T>::Pair* __restrict__ tab, int np,
-                                                           int n_rb, int64_t rb_rows, int64_t n,
+__global__ void __launch_bounds__(64) sr_fold_walk_kernel(SrFoldTabs ft, int np, int n_rb, int64_t rb_rows, int64_t n,
                                                            const T* __restrict__ losses, int64_t slot_rows,
                                                            const uint32_t* __restrict__ perm,
                                                            const T* __restrict__ carry, T* __restrict__ out_val,
                                                            int32_t* __restrict__ out_st, int4* __restrict__ dbg) {
   using Tr = SrFoldTraits<T>;
   using I = typename SrFoldTab<T>::I;
+  using Pair = typename SrFoldTab<T>::Pair;
   constexpr I CAP = I(1) << (Tr::mant + 3);
   constexpr T MIN_NORMAL = sizeof(T) == 4 ? T(1.17549435e-38f) : T(2.2250738585072014e-308);
+  const int32_t* __restrict__ code = ft.code;
+  const Pair* __restrict__ tab = static_cast<const Pair*>(ft.tab);
+  const Pair* __restrict__ tab2 = static_cast<const Pair*>(ft.tab2);
   const int lane = int(threadIdx.x) & 63;
   const uint64_t clk0 = dbg ? wall_clock64() : 0;
-  int n_slow = 0, n_rounds = 0, n_runs = 0;  // (SR_AMD_FOLD_STATS: per-tree walk statistics)
-  const int p = int(blockIdx.x) * 4 + int(threadIdx.x) / 64;
+  int n_slow = 0, n_rounds = 0, n_runs = 0, n_skip = 0;  // (SR_AMD_FOLD_STATS: per-tree walk statistics)
+  uint64_t slow_clk = 0;
+  const int p = int(blockIdx.x);  // (one wave per workgroup: a finished walk frees its slot at once)
   if (p >= np) return;  // wave-uniform
   const uint32_t t = perm ? perm[p] : uint32_t(p);
   const int32_t c_first = code[p];
@@ -906,6 +966,7 @@ __global__ void __launch_bounds__(256) sr_fold_walk_kernel(const int32_t* __rest
   }
   auto seg_base = [&](int32_t c) { return losses + size_t(c - SR_FCODE_SLOT0) * size_t(slot_rows); };
   bool fail = false;
+  int why = 0;  // (SR_AMD_FOLD_STATS: the failure site)
   T F = T(0);
   int64_t k = 0;
   if (carry) {
@@ -915,20 +976,39 @@ __global__ void __launch_bounds__(256) sr_fold_walk_kernel(const int32_t* __rest
     k = 1;
   } else {
     fail = n > 0;  // (the plan keeps the first segment's losses)
+    why = 1;
   }
+  T ev[RW];  // a slow segment's current pass (have: ev holds the next slow segment's first pass)
+  bool have = false;
   for (int c0 = 0; c0 < n_rb && !fail; c0 += 64) {
+    have = false;
     const int sg = c0 + lane;
     const bool in = sg < n_rb;
-    const int32_t cd = in ? code[size_t(sg) * size_t(np) + size_t(p)] : SR_FCODE_SKIP;
+    const size_t so = size_t(sg) * size_t(np) + size_t(p);
+    const int32_t cd = in ? code[so] : SR_FCODE_SKIP;
     const bool slow = in && cd >= SR_FCODE_SLOT0;
     I x0 = 0, x1 = 0;
     if (in && !slow && cd != SR_FCODE_SKIP) {
-      const auto pr = tab[size_t(sg) * size_t(np) + size_t(p)];
+      const auto pr = tab[so];
       x0 = I(pr.x);
       x1 = I(pr.y);
     }
+    // a slow segment's lower window binade and its steps under that binade and the next
+    int32_t sq = SR_FCODE_SKIP;
+    I s0 = 0, s1 = 0, u0 = 0, u1 = 0;
+    if (slow) {
+      sq = ft.sq[so];
+      if (sq != SR_FCODE_SKIP) {
+        const auto pa = tab[so], pb = tab2[so];
+        s0 = I(pa.x);
+        s1 = I(pa.y);
+        u0 = I(pb.x);
+        u1 = I(pb.y);
+      }
+    }
     if (__builtin_amdgcn_ballot_w64(in && cd == SR_FCODE_SKIP)) {  // (a plan out of slots)
       fail = true;
+      why = 2;
       break;
     }
     const uint64_t slowm = __builtin_amdgcn_ballot_w64(slow);
@@ -952,12 +1032,59 @@ __global__ void __launch_bounds__(256) sr_fold_walk_kernel(const int32_t* __rest
         const int64_t hi = lo + rb_rows < n ? lo + rb_rows : n;
         if (k < lo || k > hi) {
           fail = true;
+          why = 3;
           break;
         }
-        F = sr_fold_rows_wave<T, RW>(seg_base(c), lo, k, hi, F, lane, n_rounds);
+        {  // the running value may not leave a binade in this segment after all: its composed steps
+          const int32_t q0 = __shfl(sq, pos, 64);
+          if (k == lo && q0 != SR_FCODE_SKIP && F <= SrM<T>::big) {
+            int qf;
+            I lim;
+            if (F < MIN_NORMAL) {
+              qf = Tr::qmin;
+              lim = I(1) << Tr::mant;
+            } else {
+              int ex;
+              (void)frexp(double(F), &ex);
+              qf = ex - 1 - Tr::mant;
+              lim = I(1) << (Tr::mant + 1);
+            }
+            const I P = I(ldexp(double(F), -qf));
+            const bool odd = (P & 1) != 0;
+            const I ga = __shfl(odd ? s1 : s0, pos, 64), gb = __shfl(odd ? u1 : u0, pos, 64);
+            const I g = qf == q0 ? ga : (qf == q0 + 1 ? gb : lim);
+            if (P + g < lim) {
+              F = T(ldexp(double(P + g), qf));
+              k = hi;
+              have = false;  // (ev held this segment's prefetched rows)
+              ++n_skip;
+              ++pos;
+              continue;
+            }
+          }
+        }
+        const int64_t b0 = k - ((k - lo) % (16 / int64_t(sizeof(T))));  // (the pass sr_fold_rows_wave expects)
+        if (!have || b0 != lo) sr_fold_load<T, RW>(seg_base(c), lo, b0, hi, lane, ev);
+        // the chunk's next slow segment: its first pass is prefetched during this one
+        const uint64_t later = (slowm >> pos) >> 1;
+        const int np2 = later ? pos + 1 + __builtin_ctzll(later) : 64;
+        const T* nbase = nullptr;
+        int64_t nlo = 0, nhi = 0;
+        if (np2 < end) {
+          nbase = seg_base(__shfl(cd, np2, 64));
+          nlo = int64_t(c0 + np2) * rb_rows;
+          nhi = nlo + rb_rows < n ? nlo + rb_rows : n;
+        }
+        const uint64_t cs0 = dbg ? wall_clock64() : 0;
+        F = sr_fold_rows_wave<T, RW>(seg_base(c), lo, k, hi, F, lane, n_rounds, ev, nbase, nlo, nhi);
+        if (dbg) slow_clk += wall_clock64() - cs0;
+        have = nbase != nullptr;
         ++n_slow;
         k = hi;
-        if (!(F <= SrM<T>::big)) fail = true;  // (an overflow: not the plan's case)
+        if (!(F <= SrM<T>::big)) {  // (an overflow: not the plan's case)
+          fail = true;
+          why = 4;
+        }
         ++pos;
         continue;
       }
@@ -980,12 +1107,14 @@ __global__ void __launch_bounds__(256) sr_fold_walk_kernel(const int32_t* __rest
       }
       if (k != lo || qf != q || !(F <= SrM<T>::big)) {  // the running value left the plan's window
         fail = true;
+        why = qf < q ? 5 : (qf > q ? 6 : 7);
         break;
       }
       const I P = I(ldexp(double(F), -q));
       const I g = (P & 1) ? g1 : g0;
       if (P + g >= lim) {  // the fold crosses a binade inside a run the plan called safe
         fail = true;
+        why = 8;
         break;
       }
       F = T(ldexp(double(P + g), q));
@@ -998,43 +1127,41 @@ __global__ void __launch_bounds__(256) sr_fold_walk_kernel(const int32_t* __rest
   if (lane == 0) {
     out_val[t] = F;
     out_st[t] = fail ? SR_FST_FAIL : SR_FST_OK;
-    if (dbg) dbg[t] = make_int4(n_slow, n_rounds, n_runs, int((wall_clock64() - clk0) / 100));  // (us: 100 MHz)
+    if (dbg) dbg[t] = make_int4(n_slow * 1000 + (n_skip < 999 ? n_skip : 999), n_rounds, fail ? -why : int(slow_clk / 100), int((wall_clock64() - clk0) / 100));  // (us: 100 MHz)
   }
 }
 
 template <typename T>
 hipError_t sr_launch_fold_plan(const double* part, int np, int n_rb, const uint32_t* perm, const SrFoldWho& who,
-                               double delta, int32_t* code, int* slot_next, int slot_cap, hipStream_t s) {
+                               double delta, SrFoldTabs ft, int* slot_next, int slot_cap, hipStream_t s) {
   if (np <= 0) return hipSuccess;
   hipLaunchKernelGGL(sr_fold_plan_kernel<T>, dim3(unsigned((np + 3) / 4)), dim3(256), 0, s, part, np, n_rb, perm, who,
-                     delta, code, slot_next, slot_cap);
+                     delta, ft, slot_next, slot_cap);
   return hipGetLastError();
 }
 template <typename T>
 hipError_t sr_launch_fold_stab(const double* part, int np, int n_rb, int64_t rb_rows, int64_t n, const uint32_t* perm,
-                               const SrFoldWho& who, double delta, const T* losses, int32_t* code, void* tab,
-                               hipStream_t s) {
+                               const SrFoldWho& who, double delta, const T* losses, SrFoldTabs ft, hipStream_t s) {
   if (np <= 0 || n_rb <= 0) return hipSuccess;
   hipLaunchKernelGGL((sr_fold_stab_kernel<T, 8>), dim3(unsigned(n_rb), unsigned(np)), dim3(256), 0, s, part, np, n_rb,
-                     rb_rows, n, perm, who, delta, losses, code, static_cast<typename SrFoldTab<T>::Pair*>(tab));
+                     rb_rows, n, perm, who, delta, losses, ft);
   return hipGetLastError();
 }
 template <typename T>
-hipError_t sr_launch_fold_walk(const int32_t* code, const void* tab, int np, int n_rb, int64_t rb_rows, int64_t n,
-                               const T* losses, int64_t slot_rows, const uint32_t* perm, const T* carry, T* out_val,
-                               int32_t* out_st, void* dbg, hipStream_t s) {
+hipError_t sr_launch_fold_walk(SrFoldTabs ft, int np, int n_rb, int64_t rb_rows, int64_t n, const T* losses,
+                               int64_t slot_rows, const uint32_t* perm, const T* carry, T* out_val, int32_t* out_st,
+                               void* dbg, hipStream_t s) {
   if (np <= 0) return hipSuccess;
-  hipLaunchKernelGGL((sr_fold_walk_kernel<T, sizeof(T) == 4 ? 16 : 8>), dim3(unsigned((np + 3) / 4)), dim3(256), 0, s, code,
-                     static_cast<const typename SrFoldTab<T>::Pair*>(tab), np, n_rb, rb_rows, n, losses, slot_rows, perm,
-                     carry, out_val, out_st, static_cast<int4*>(dbg));
+  hipLaunchKernelGGL((sr_fold_walk_kernel<T, sizeof(T) == 4 ? 16 : 8>), dim3(unsigned(np)), dim3(64), 0, s, ft,
+                     np, n_rb, rb_rows, n, losses, slot_rows, perm, carry, out_val, out_st, static_cast<int4*>(dbg));
   return hipGetLastError();
 }
 #define SR_INSTANTIATE_FOLD2(T)                                                                                      \
   template hipError_t sr_launch_fold_plan<T>(const double*, int, int, const uint32_t*, const SrFoldWho&, double,   \
-                                             int32_t*, int*, int, hipStream_t);                                        \
+                                             SrFoldTabs, int*, int, hipStream_t);                                      \
   template hipError_t sr_launch_fold_stab<T>(const double*, int, int, int64_t, int64_t, const uint32_t*,              \
-                                             const SrFoldWho&, double, const T*, int32_t*, void*, hipStream_t);        \
-  template hipError_t sr_launch_fold_walk<T>(const int32_t*, const void*, int, int, int64_t, int64_t, const T*, int64_t, \
+                                             const SrFoldWho&, double, const T*, SrFoldTabs, hipStream_t);             \
+  template hipError_t sr_launch_fold_walk<T>(SrFoldTabs, int, int, int64_t, int64_t, const T*, int64_t,               \
                                              const uint32_t*, const T*, T*, int32_t*, void*, hipStream_t);
 SR_INSTANTIATE_FOLD2(float)
 SR_INSTANTIATE_FOLD2(double)

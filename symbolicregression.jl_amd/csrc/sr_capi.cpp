@@ -317,7 +317,7 @@ struct sr_ctx {
   DevBuf fold_dbg;
   bool want_fold = false;    // set by eval_loss_submit around its run_batch
   int fold_path_last = 0;    // 0 none, 1 stored losses, 2 FOLD mode
-  DevBuf fold_code, fold_tab, fold_store, fold_ctl, fold_io2;
+  DevBuf fold_code, fold_tab, fold_store, fold_ctl, fold_io2, fold_sq, fold_tab2;
   std::shared_ptr<void> fold_job;  // a row-sharded call's FoldJob<T>, until its ranks agree on the verdicts
   int inject_post_wsum = 0;        // tests ("inject_failure_post_wsum"): this rank's copy of the weights' sum gather fails
   size_t outs_fval_off = 0, outs_fst_off = 0, outs_bytes_all = 0;
@@ -546,6 +546,13 @@ struct FoldJob {
   double delta = 0.0;
 };
 
+// a region's plan arrays at partial-buffer offset off
+template <typename T>
+SrFoldTabs fold_tabs(sr_ctx* ctx, size_t off) {
+  using Pair = typename SrFoldTab<T>::Pair;
+  return SrFoldTabs{ctx->fold_code.as<int32_t>() + off, ctx->fold_tab.as<char>() + off * sizeof(Pair),
+                    ctx->fold_sq.as<int32_t>() + off, ctx->fold_tab2.as<char>() + off * sizeof(Pair)};
+}
 // A region's steps: the stored-loss tables (path 1) or the plan and the FOLD pass (path 2).  who: the
 // call's whole-batch arrays (sums / flags / elig / est at the caller's tree index; this function adds
 // the region's chunk offset).
@@ -554,8 +561,7 @@ int fold_steps(sr_ctx* ctx, const FoldJob<T>& job, const FoldRegion<T>& fr, SrFo
   const int nrb = fr.g.n_row_blocks;
   const int64_t rb_rows = int64_t(fr.g.tiles) * 64 * fr.Rc;
   const size_t off = size_t(job.n_rb) * size_t(fr.pos0);  // (the region's offset in the partial buffers)
-  int32_t* code = ctx->fold_code.as<int32_t>() + off;
-  void* tab = ctx->fold_tab.as<char>() + off * sizeof(typename SrFoldTab<T>::Pair);
+  const SrFoldTabs ft = fold_tabs<T>(ctx, off);
   const double* part = nrb > 1 ? fr.a.part_sum : nullptr;
   const int np = int(fr.np);
   if (who.sums) who.sums += fr.t0;
@@ -564,10 +570,10 @@ int fold_steps(sr_ctx* ctx, const FoldJob<T>& job, const FoldRegion<T>& fr, SrFo
   if (who.est) who.est += fr.t0;
   if (job.path == 1) {
     SR_HIP_CHECK(sr_launch_fold_stab<T>(part, np, nrb, rb_rows, job.n_eval, fr.a.perm, who, job.delta, fr.a.fold_loss,
-                                        code, tab, cs));
+                                        ft, cs));
     return SR_OK;
   }
-  SR_HIP_CHECK(sr_launch_fold_plan<T>(part, np, nrb, fr.a.perm, who, job.delta, code, ctx->fold_ctl.as<int>(),
+  SR_HIP_CHECK(sr_launch_fold_plan<T>(part, np, nrb, fr.a.perm, who, job.delta, ft, ctx->fold_ctl.as<int>(),
                                       job.slot_cap, cs));
   SrEvalArgs<T> fa = fr.a;
   fa.hint = nullptr;
@@ -575,8 +581,10 @@ int fold_steps(sr_ctx* ctx, const FoldJob<T>& job, const FoldRegion<T>& fr, SrFo
   fa.out_flag = nullptr;
   fa.group_cnt = nullptr;
   fa.stamps = nullptr;
-  fa.fold_code = code;
-  fa.fold_tab = tab;
+  fa.fold_code = ft.code;
+  fa.fold_tab = ft.tab;
+  fa.fold_sq = ft.sq;
+  fa.fold_tab2 = ft.tab2;
   fa.fold_loss = ctx->fold_store.as<T>();
   fa.fold_slot_rows = job.slot_rows;
   fa.fold_pos_stride = 0;
@@ -591,13 +599,15 @@ int fold_walk(sr_ctx* ctx, const FoldJob<T>& job, const FoldRegion<T>& fr, const
   const int nrb = fr.g.n_row_blocks;
   const int64_t rb_rows = int64_t(fr.g.tiles) * 64 * fr.Rc;
   const size_t off = size_t(job.n_rb) * size_t(fr.pos0);
-  const int32_t* code = ctx->fold_code.as<int32_t>() + off;
-  const void* tab = ctx->fold_tab.as<char>() + off * sizeof(typename SrFoldTab<T>::Pair);
+  const SrFoldTabs ft = fold_tabs<T>(ctx, off);
   const T* losses = job.path == 1 ? fr.a.fold_loss : ctx->fold_store.as<T>();
   const int64_t slot_rows = job.path == 1 ? rb_rows : job.slot_rows;
   int4* dbg = ctx->fold_stats ? ctx->fold_dbg.as<int4>() + fr.t0 : nullptr;  // (SR_AMD_FOLD_STATS)
-  SR_HIP_CHECK(sr_launch_fold_walk<T>(code, tab, int(fr.np), nrb, rb_rows, job.n_eval, losses, slot_rows, fr.a.perm,
+  SR_HIP_CHECK(sr_launch_fold_walk<T>(ft, int(fr.np), nrb, rb_rows, job.n_eval, losses, slot_rows, fr.a.perm,
                                       carry ? carry + fr.t0 : nullptr, out_val + fr.t0, out_st + fr.t0, dbg, cs));
+  if (ctx->fold_stats == 2)  // (analysis: the same walk again, its loads now warm: the statistics are the second's)
+    SR_HIP_CHECK(sr_launch_fold_walk<T>(ft, int(fr.np), nrb, rb_rows, job.n_eval, losses, slot_rows, fr.a.perm,
+                                        carry ? carry + fr.t0 : nullptr, out_val + fr.t0, out_st + fr.t0, dbg, cs));
   return SR_OK;
 }
 
@@ -750,6 +760,8 @@ int run_batch(sr_ctx* ctx, const sr_dataset* ds, int opset_id, const sr_tree_bat
     if (fold_path) {
       SR_HIP_CHECK(ctx->fold_code.ensure(n_part * sizeof(int32_t) + 4));
       SR_HIP_CHECK(ctx->fold_tab.ensure(n_part * sizeof(typename SrFoldTab<T>::Pair) + 16));
+      SR_HIP_CHECK(ctx->fold_sq.ensure(n_part * sizeof(int32_t) + 4));
+      SR_HIP_CHECK(ctx->fold_tab2.ensure(n_part * sizeof(typename SrFoldTab<T>::Pair) + 16));
     }
   }
   if (!ctx->internal_pass) {  // (the fallback's prediction passes leave the call's record alone)
@@ -2168,18 +2180,26 @@ int eval_loss_finish(sr_ctx* ctx, LossCall<T>& c) {
       int64_t m = 0;
       double a[4] = {0, 0, 0, 0};
       int mx[4] = {0, 0, 0, 0};
-      for (const int4& v : st) {
+      int64_t n_skip = 0;
+      for (size_t i = 0; i < st.size(); ++i) {
+        int4 v = st[i];
         if (v.x == 0 && v.y == 0 && v.z == 0) continue;
+        n_skip += v.x % 1000;  // (x: slow segments x 1000 + those advanced by their steps)
+        v.x /= 1000;
         ++m;
-        const int w[4] = {v.x, v.y, v.z, v.w};
+        if (v.z < 0)
+          std::fprintf(stderr, "[sr fold] tree %zu failed: site %d after %d slow segments, %d rounds, %d us\n", i, -v.z,
+                       v.x, v.y, v.w);
+        const int w[4] = {v.x, v.y, v.z < 0 ? 0 : v.z, v.w};
         for (int i = 0; i < 4; ++i) {
           a[i] += w[i];
           mx[i] = std::max(mx[i], w[i]);
         }
       }
-      std::fprintf(stderr, "[sr fold] path %d: %lld walks, mean/max slow segments %.1f/%d, rounds %.1f/%d, runs %.1f/%d, walk us %.1f/%d; folded %lld fallback %lld\n",
+      std::fprintf(stderr, "[sr fold] path %d: %lld walks, mean/max slow segments %.1f/%d, rounds %.1f/%d, slow-segment us %.1f/%d, walk us %.1f/%d; folded %lld fallback %lld\n",
                    ctx->fold_path_last, (long long)m, m ? a[0] / m : 0.0, mx[0], m ? a[1] / m : 0.0, mx[1],
                    m ? a[2] / m : 0.0, mx[2], m ? a[3] / m : 0.0, mx[3], (long long)fres.n_ok, (long long)fres.n_fail);
+      std::fprintf(stderr, "[sr fold] slow segments advanced by their steps (no rows read): %lld\n", (long long)n_skip);
     }
   }
   ctx->n_fold_last = int64_t(fold_list.size());
@@ -3543,7 +3563,8 @@ int sr_shutdown(sr_ctx* ctx) {
     for (DevBuf* b : {&ctx->prog, &ctx->outs, &ctx->part_sum, &ctx->part_flag, &ctx->pred, &ctx->row_idx, &ctx->tree_list, &ctx->range_lo, &ctx->range_hi, &ctx->range_sums, &ctx->packed,
                       &ctx->hint, &ctx->jsum_prog, &ctx->jsum_scratch, &ctx->probe_sum, &ctx->probe_flag, &ctx->g_code, &ctx->g_offsets, &ctx->g_consts, &ctx->g_const_off,
                       &ctx->g_items, &ctx->g_part, &ctx->g_out, &ctx->derived_cols, &ctx->probe_derived, &ctx->coll_buf, &ctx->coll_packed, &ctx->ctl, &ctx->fold_io, &ctx->group_cnt,
-                      &ctx->fold_code, &ctx->fold_tab, &ctx->fold_store, &ctx->fold_ctl, &ctx->fold_io2})
+                      &ctx->fold_code, &ctx->fold_tab, &ctx->fold_store, &ctx->fold_ctl, &ctx->fold_io2, &ctx->fold_sq,
+                      &ctx->fold_tab2})
       b->release();
     for (HostBuf* b : {&ctx->h_prog, &ctx->h_outs, &ctx->h_grad, &ctx->h_coll, &ctx->h_part, &ctx->h_exact})
       b->release();

@@ -156,11 +156,16 @@ struct SrEvalArgs {
   // fold's tables are composed from them).  FOLD: fold_code [n_row_blocks][n_trees] per position (the
   // plan), fold_tab the same shape of composed-step pairs (SrFoldTab<T>::Pair, written for steps
   // segments), fold_loss the slow segments' losses, slot (code - SR_FCODE_SLOT0) x fold_slot_rows.
+  // fold_sq / fold_tab2 (same shape): a slow segment's lower window binade, and the composed steps of
+  // its rows under that binade (in fold_tab) and the next (fold_tab2), so that the walk advances a slow
+  // segment the running value does not actually leave a binade in without reading its rows
   T* fold_loss;
   int64_t fold_pos_stride;
   const int32_t* fold_code;
   void* fold_tab;
   int64_t fold_slot_rows;
+  const int32_t* fold_sq;
+  void* fold_tab2;
   // -DSR_STAMPS builds only (latency analysis, tools/stamps.py): per wave, SR_NSTAMPS wall-clock
   // stamps at fixed points of the kernel, [block][wave][SR_NSTAMPS]; NULL otherwise
   uint64_t* stamps;
@@ -292,17 +297,25 @@ hipError_t sr_launch_fold_segtab(const T* pred, int64_t pred_ld, int n_trees, co
 // position), slots for the FOLD mode's slow segments), the stored-loss tables of a small call, and the
 // walk (per position: the fold's value and status at the caller's tree index perm[position]).
 struct SrFoldWho;  // (sr_fold_dev.h)
+// a region's plan arrays, [row block][position] each: codes, composed-step pairs (steps segments; a slow
+// segment's under its lower window binade sq), sq (slow segments; SR_FCODE_SKIP: none), and a slow
+// segment's pair under sq + 1
+struct SrFoldTabs {
+  int32_t* code;
+  void* tab;
+  int32_t* sq;
+  void* tab2;
+};
 template <typename T>
 hipError_t sr_launch_fold_plan(const double* part, int np, int n_rb, const uint32_t* perm, const SrFoldWho& who,
-                               double delta, int32_t* code, int* slot_next, int slot_cap, hipStream_t s);
+                               double delta, SrFoldTabs ft, int* slot_next, int slot_cap, hipStream_t s);
 template <typename T>
 hipError_t sr_launch_fold_stab(const double* part, int np, int n_rb, int64_t rb_rows, int64_t n, const uint32_t* perm,
-                               const SrFoldWho& who, double delta, const T* losses, int32_t* code, void* tab,
-                               hipStream_t s);
+                               const SrFoldWho& who, double delta, const T* losses, SrFoldTabs ft, hipStream_t s);
 template <typename T>
-hipError_t sr_launch_fold_walk(const int32_t* code, const void* tab, int np, int n_rb, int64_t rb_rows, int64_t n,
-                               const T* losses, int64_t slot_rows, const uint32_t* perm, const T* carry, T* out_val,
-                               int32_t* out_st, void* dbg, hipStream_t s);
+hipError_t sr_launch_fold_walk(SrFoldTabs ft, int np, int n_rb, int64_t rb_rows, int64_t n, const T* losses,
+                               int64_t slot_rows, const uint32_t* perm, const T* carry, T* out_val, int32_t* out_st,
+                               void* dbg, hipStream_t s);
 template <typename T>
 hipError_t sr_launch_fold(const T* pred, int64_t pred_ld, int n_trees, const T* y, const T* w, const int64_t* row_idx,
                           int64_t n, int loss_kind, T loss_param, int64_t seg_len, const int2* tq, const int64_t* tab,

@@ -110,6 +110,46 @@ __device__ __forceinline__ void sr_fold_add_i(I m, int kind, I cap, I& a0, I& a1
   a1 = a1 + e1 < cap ? a1 + e1 : cap;
 }
 
+// Inclusive wave scan of nonnegative values in lane order, by DPP lane moves (pure VALU, no LDS round
+// trips): row_shr 1, 2, 4, 8 within each row of 16 lanes (lanes shifted in from outside the row read
+// 0), then row 0's total into rows 1 and 3 (row_bcast:15) and rows 0 + 1 into rows 2 and 3
+// (row_bcast:31).  Integer-valued sums are exact below 2^(mant+1) and monotone above.
+template <int CTRL, int ROW_MASK>
+__device__ __forceinline__ int sr_fold_dpp(int v) {
+  return __builtin_amdgcn_update_dpp(0, v, CTRL, ROW_MASK, 0xf, true);
+}
+template <int CTRL, int ROW_MASK = 0xf>
+__device__ __forceinline__ float sr_fold_dpp_add(float v) {
+  return v + __int_as_float(sr_fold_dpp<CTRL, ROW_MASK>(__float_as_int(v)));
+}
+template <int CTRL, int ROW_MASK = 0xf>
+__device__ __forceinline__ double sr_fold_dpp_add(double v) {
+  const uint64_t b = uint64_t(__double_as_longlong(v));
+  const uint32_t lo = uint32_t(sr_fold_dpp<CTRL, ROW_MASK>(int(uint32_t(b))));
+  const uint32_t hi = uint32_t(sr_fold_dpp<CTRL, ROW_MASK>(int(uint32_t(b >> 32))));
+  return v + __longlong_as_double(int64_t((uint64_t(hi) << 32) | lo));
+}
+template <typename T>
+__device__ __forceinline__ T sr_fold_scan(T v) {
+  v = sr_fold_dpp_add<0x111>(v);       // row_shr:1
+  v = sr_fold_dpp_add<0x112>(v);       // row_shr:2
+  v = sr_fold_dpp_add<0x114>(v);       // row_shr:4
+  v = sr_fold_dpp_add<0x118>(v);       // row_shr:8
+  v = sr_fold_dpp_add<0x142, 0xa>(v);  // row_bcast:15 into rows 1, 3
+  v = sr_fold_dpp_add<0x143, 0xc>(v);  // row_bcast:31 into rows 2, 3
+  return v;
+}
+// the value of lane l (wave-uniform l), by readlane
+__device__ __forceinline__ float sr_fold_lane(float v, int l) {
+  return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), l));
+}
+__device__ __forceinline__ double sr_fold_lane(double v, int l) {
+  const uint64_t b = uint64_t(__double_as_longlong(v));
+  const uint32_t lo = uint32_t(__builtin_amdgcn_readlane(int(uint32_t(b)), l));
+  const uint32_t hi = uint32_t(__builtin_amdgcn_readlane(int(uint32_t(b >> 32)), l));
+  return __longlong_as_double(int64_t((uint64_t(hi) << 32) | lo));
+}
+
 // binade spacing exponent q of a value >= 0 (subnormals and 0: the fixed subnormal spacing); values
 // past the type's range get a q no finite running value has
 template <typename T>
@@ -175,10 +215,9 @@ __device__ __forceinline__ void sr_fold_tile_step(const T (&l)[R], int q, int la
     tsum += (s < CLAMP) ? s : CLAMP;
   }
   if (__builtin_amdgcn_ballot_w64(dmax == T(0.5)) == 0) {
-    // fixed-order wave sum (lane 63 reads the total); nonnegative terms
-    T v = tsum;
-#pragma unroll
-    for (int off = 1; off < 64; off <<= 1) v += __shfl_xor(v, off, 64);
+    // wave sum of nonnegative integer values (lane 63's inclusive scan): exact below 2^(mant+1), and any
+    // sum past that fails a run the same way
+    const T v = sr_fold_lane(sr_fold_scan(tsum), 63);
     const I t = v < T(CAP) ? I(v) : CAP;
     t0 = t;
     t1 = t;

@@ -908,11 +908,16 @@ __global__ void __launch_bounds__(W * 64, (SrMinWavesFor<T, R, TIER, W, VSTK, LK
     }
   }
   // FOLD: this row block's plan code of each of the wave's trees (lane j: tree j); SKIP trees are not run
-  int32_t my_code = SR_FCODE_SKIP;
-  if (MODE == SR_MODE_FOLD && lane < S) my_code = a.fold_code[size_t(rb) * size_t(a.n_trees) + size_t(my_pos)];
+  int32_t my_code = SR_FCODE_SKIP, my_sq = SR_FCODE_SKIP;  // (my_sq: a slow segment's lower window binade)
+  if (MODE == SR_MODE_FOLD && lane < S) {
+    my_code = a.fold_code[size_t(rb) * size_t(a.n_trees) + size_t(my_pos)];
+    if (my_code >= SR_FCODE_SLOT0 && a.fold_sq) my_sq = a.fold_sq[size_t(rb) * size_t(a.n_trees) + size_t(my_pos)];
+  }
   const uint64_t live = sr_ballot(lane < S && my_pe > my_pb &&  // empty program: statically incomplete
                                   (MODE != SR_MODE_FOLD || my_code != SR_FCODE_SKIP));
-  typename SrFoldTab<T>::I facc0 = 0, facc1 = 0;  // FOLD: lane j's tree's composed steps over this row block
+  // FOLD: lane j's tree's composed steps over this row block (a slow segment's: under my_sq, and under
+  // my_sq + 1 in facc2 / facc3)
+  typename SrFoldTab<T>::I facc0 = 0, facc1 = 0, facc2 = 0, facc3 = 0;
   uint64_t dmask = 0u, bmask = 0u, emask = 0u;
   double accv = 0.0;
   // dead-tree hints shared across row blocks (LOSS mode): a tree found non-finite by any block is
@@ -1364,28 +1369,37 @@ __global__ void __launch_bounds__(W * 64, (SrMinWavesFor<T, R, TIER, W, VSTK, LK
 #pragma unroll
             for (int r = 0; r < R; ++r) l[r] = (row0 + L::row(lane, r) < a.n_rows) ? l[r] : T(0);
           }
+          using I = typename SrFoldTab<T>::I;
+          // this tile's composed step under binade q, then the block's so far (lane j's pair)
+          auto accumulate = [&](int q, I& acc0, I& acc1) {
+            I y0, y1;
+            sr_fold_tile_step<T, R, C>(l, q, lane, y0, y1);
+            I x0 = I(0), x1 = I(0);
+            if constexpr (sizeof(I) == 4) {
+              x0 = __builtin_amdgcn_readlane(int(acc0), j);
+              x1 = __builtin_amdgcn_readlane(int(acc1), j);
+            } else {
+              x0 = __shfl(acc0, j, 64);
+              x1 = __shfl(acc1, j, 64);
+            }
+            sr_fold_compose_i<I>(x0, x1, y0, y1, I(1) << (SrFoldTraits<T>::mant + 3));
+            if (lane == j) {
+              acc0 = y0;
+              acc1 = y1;
+            }
+          };
           const int32_t code = __builtin_amdgcn_readlane(my_code, j);
           if (code >= SR_FCODE_SLOT0) {  // a slow segment: keep its losses for the walk (row order)
             L::store(a.fold_loss + size_t(code - SR_FCODE_SLOT0) * size_t(a.fold_slot_rows) + size_t(tile) * ROWS +
                          lane * C,
                      l);
-          } else {  // this tile's composed step under the segment's binade, then the block's so far
-            using I = typename SrFoldTab<T>::I;
-            I y0, y1;
-            sr_fold_tile_step<T, R, C>(l, code, lane, y0, y1);
-            I x0 = I(0), x1 = I(0);
-            if constexpr (sizeof(I) == 4) {
-              x0 = __builtin_amdgcn_readlane(int(facc0), j);
-              x1 = __builtin_amdgcn_readlane(int(facc1), j);
-            } else {
-              x0 = __shfl(facc0, j, 64);
-              x1 = __shfl(facc1, j, 64);
+            const int32_t sq = __builtin_amdgcn_readlane(my_sq, j);
+            if (sq != SR_FCODE_SKIP) {
+              accumulate(sq, facc0, facc1);
+              accumulate(sq + 1, facc2, facc3);
             }
-            sr_fold_compose_i<I>(x0, x1, y0, y1, I(1) << (SrFoldTraits<T>::mant + 3));
-            if (lane == j) {
-              facc0 = y0;
-              facc1 = y1;
-            }
+          } else {
+            accumulate(code, facc0, facc1);
           }
         } else if (MODE == SR_MODE_PRED) {
           const uint32_t tree = a.perm ? a.perm[tree0 + g] : uint32_t(tree0 + g);
@@ -1404,10 +1418,14 @@ __global__ void __launch_bounds__(W * 64, (SrMinWavesFor<T, R, TIER, W, VSTK, LK
   }
   SR_STAMP(5);
 
-  if (MODE == SR_MODE_FOLD) {  // the steps segments' pairs, [row block][position]
+  if (MODE == SR_MODE_FOLD) {  // the steps segments' pairs, [row block][position] (and the slow ones')
+    const size_t o = size_t(rb) * size_t(a.n_trees) + size_t(my_pos);
     if (lane < S && my_code != SR_FCODE_SKIP && my_code < SR_FCODE_SLOT0)
-      static_cast<typename SrFoldTab<T>::Pair*>(a.fold_tab)[size_t(rb) * size_t(a.n_trees) + size_t(my_pos)] =
-          SrFoldTab<T>::pair(facc0, facc1);
+      static_cast<typename SrFoldTab<T>::Pair*>(a.fold_tab)[o] = SrFoldTab<T>::pair(facc0, facc1);
+    if (lane < S && my_sq != SR_FCODE_SKIP) {
+      static_cast<typename SrFoldTab<T>::Pair*>(a.fold_tab)[o] = SrFoldTab<T>::pair(facc0, facc1);
+      static_cast<typename SrFoldTab<T>::Pair*>(a.fold_tab2)[o] = SrFoldTab<T>::pair(facc2, facc3);
+    }
     return;
   }
   if (MODE == SR_MODE_EXACT) {
