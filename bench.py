@@ -452,7 +452,7 @@ def compact_line(line):
     if "c4" in line:
         c = line["c4"]
         o = _pick(c, ("value", "unit", "ms_per_step", "steps", "n_gpus", "scaling", "rows_per_gpu", "n_trees",
-                      "fraction_complete", "skipped"))
+                      "fraction_complete", "skipped", "loss_accumulation"))
         if "roofline" in c:
             o["roofline"] = _pick(c["roofline"], _KEEP["roofline"])
         lp = c.get("last_step_passes") or {}
@@ -461,12 +461,13 @@ def compact_line(line):
             o["projection_8_ranks"] = _pick(c["projection_8_ranks"], ("projected_ms_per_step", "efficiency"))
         if "parity" in c:
             p = c["parity"]
-            o["parity"] = {"pass": p.get("pass"), "rows": p.get("rows")}
+            o["parity"] = {"pass": p.get("pass"), "rows": p.get("rows"), "accumulation": p.get("accumulation")}
             for k in ("sample", "planted_big"):
                 if k in p:
                     o["parity"][k] = _pick(p[k], ("trees", "complete", "flag_mismatches", "ref_fold_inf_mismatches",
-                                                  "max_rel_vs_f64_accum", "n_held_to_libm_spread_bar",
-                                                  "loss_failures", "n_bit_exact_vs_ref_f32_fold"))
+                                                  "max_rel_vs_f64_accum", "max_rel_vs_ref_f32_fold",
+                                                  "n_held_to_libm_spread_bar", "loss_failures",
+                                                  "n_bit_exact_vs_ref_f32_fold"))
         out["c4"] = o
     if line.get("search"):
         s = {}
@@ -633,8 +634,12 @@ def c4_line(ctx, opts, eval_loss_sharded, gen_random_batch, Dataset, args, comm,
                                                   out["ms_per_step"], passes)
     if world == 1 and rank == 0 and not args.no_c4_parity:
         progress("c4 parity (oracle over all rows for a tree sample)")
+        # (2^26 rows per GPU: row blocks past fold_seg_max keep the f64 sum, ref_fold path 0)
+        folded = ctx.last_ref_fold()["path"] > 0
+        out["loss_accumulation"] = ("the reference's in-order fold in Float32" if folded else
+                                    "f64 per-tree sums (row blocks of 2^18 rows pass fold_seg_max: no fold)")
         out["parity"] = c4_parity(opts, tb, res, lambda t: eval_loss_sharded(t, ds, opts), rows_total,
-                                  args.c4_parity_trees)
+                                  args.c4_parity_trees, accum="ref" if folded else "f64")
     ds.free_device()
     return out
 
@@ -744,7 +749,7 @@ def per_tree_bar(orc, sub, X, y, d_loss, l64, ok, rel_bar, threads, accum="ref")
     return r, bar, err, int(worst.size)
 
 
-def c4_parity(opts, tb, res, device_call, rows_total, n_sample):
+def c4_parity(opts, tb, res, device_call, rows_total, n_sample, accum="ref"):
     """C4 at full size against the oracle: a stratified sample of the timed step's trees (complete and
     incomplete, every size) over all rows, plus planted trees whose values reach the exact-sum
     threshold (max|v| >= floatmax / 2n: DynamicExpressions' isfinite(sum) decided in Julia's pairwise
@@ -776,9 +781,9 @@ def c4_parity(opts, tb, res, device_call, rows_total, n_sample):
         lref, cref = orc.eval_loss_batch(t, X, y, accum="ref", n_threads=threads)
         d_loss = np.asarray(d_loss, dtype=np.float64)
         ok = d_comp & c64
-        lr = lref.astype(np.float64)
+        lr = (lref if accum == "ref" else l64).astype(np.float64)
         fin = ok & np.isfinite(lr)
-        r, bar, err, n_wide = per_tree_bar(orc, t, X, y, d_loss, lr, fin, 1e-4, threads)
+        r, bar, err, n_wide = per_tree_bar(orc, t, X, y, d_loss, lr, fin, 1e-4, threads, accum=accum)
         fail = fin & ~(err <= bar)
         inf_m = int(np.sum(ok & (np.isinf(d_loss) != np.isinf(lref))))
         with np.errstate(invalid="ignore", divide="ignore"):
@@ -786,13 +791,17 @@ def c4_parity(opts, tb, res, device_call, rows_total, n_sample):
         out[name] = {"trees": int(t.n_trees), "complete": int(ok.sum()),
                      "flag_mismatches": int(np.sum(d_comp != c64)) + int(np.sum(cref != c64)),
                      "ref_fold_inf_trees": int(np.sum(ok & np.isinf(lref))), "ref_fold_inf_mismatches": inf_m,
-                     "n_bit_exact_vs_ref_f32_fold": int(np.sum(fin & (d_loss.astype(np.float32) == lref))),
-                     "max_rel_vs_ref_f32_fold": float(np.max(np.where(np.isfinite(r[fin]), r[fin], 0.0), initial=0.0)),
+                     ("n_bit_exact_vs_ref_f32_fold" if accum == "ref" else "n_bit_exact_vs_f64_accum"):
+                         int(np.sum(fin & (d_loss.astype(np.float32) == lr.astype(np.float32)))),
+                     ("max_rel_vs_ref_f32_fold" if accum == "ref" else "max_rel_vs_oracle"):
+                         float(np.max(np.where(np.isfinite(r[fin]), r[fin], 0.0), initial=0.0)),
                      "max_rel_vs_f64_accum": float(np.max(np.where(np.isfinite(r64[fin]), r64[fin], 0.0), initial=0.0)),
                      "n_held_to_libm_spread_bar": n_wide, "loss_failures": int(fail.sum()),
                      "held_trees": held_trees(opts, orc, t, X, y, np.nonzero(fin & (r > 1e-4))[0], d_loss,
-                                              lr, bar, threads, ids=idx if name == "sample" else None)}
+                                              lr, bar, threads, ids=idx if name == "sample" else None,
+                                              accum=accum)}
     out["rows"] = int(rows_total)
+    out["accumulation"] = accum
     out["pass"] = all(v["flag_mismatches"] == 0 and v["loss_failures"] == 0 and v["ref_fold_inf_mismatches"] == 0
                       for v in (out["sample"], out["planted_big"]))
     out["rule"] = ("flags bit-exact vs the oracle over all rows; +Inf exactly where the reference's Float32 fold is; "

@@ -799,7 +799,6 @@ __device__ T sr_fold_rows_wave(const T* __restrict__ base, int64_t lo, int64_t k
   constexpr I CAP = I(1) << (Tr::mant + 3);
   constexpr T CLAMP = T(int64_t(1) << (Tr::mant + 2));
   constexpr int C = 16 / int(sizeof(T));
-  constexpr T MIN_NORMAL = sizeof(T) == 4 ? T(1.17549435e-38f) : T(2.2250738585072014e-308);
   T nx[RW];
   while (k < hi) {
     const int64_t b0 = k - ((k - lo) % C);
@@ -823,18 +822,9 @@ __device__ T sr_fold_rows_wave(const T* __restrict__ base, int64_t lo, int64_t k
     while (k < hi && k < pass_end) {
       ++rounds;
       if (!(F <= SrM<T>::big)) return F;  // +Inf / NaN stays
-      int q;
-      I lim;
-      if (F < MIN_NORMAL) {
-        q = Tr::qmin;
-        lim = I(1) << Tr::mant;
-      } else {
-        int ex;
-        (void)frexp(double(F), &ex);
-        q = ex - 1 - Tr::mant;
-        lim = I(1) << (Tr::mant + 1);
-      }
-      const I P = I(ldexp(double(F), -q));
+      const SrFoldBinade<T> bn(F);
+      const int q = bn.q;
+      const I P = bn.P, lim = bn.lim;
       const bool odd = (P & 1) != 0;
       // fast path: the round's steps are rint(l 2^-q) unless some row is an exact half (6 VALU a row:
       // scale, round, residual, max |residual|, clamp, sum; a NaN loss clamps, its residual is ignored)
@@ -856,7 +846,7 @@ __device__ T sr_fold_rows_wave(const T* __restrict__ base, int64_t lo, int64_t k
         const T inc = sr_fold_scan(lsum);
         cross = __builtin_amdgcn_ballot_w64(T(P) + inc >= T(lim));
         if (cross == 0) {  // the rest of this pass stays in the binade
-          F = T(ldexp(double(T(P) + sr_fold_lane(inc, 63)), q));
+          F = SrFoldBinade<T>::value(P + I(sr_fold_lane(inc, 63)), q);
           k = pass_end;
           break;
         }
@@ -880,12 +870,12 @@ __device__ T sr_fold_rows_wave(const T* __restrict__ base, int64_t lo, int64_t k
         const I inc = P + (odd ? i1 : i0);
         cross = __builtin_amdgcn_ballot_w64(inc >= lim);
         if (cross == 0) {
-          F = T(ldexp(double(__shfl(inc, 63, 64)), q));
+          F = SrFoldBinade<T>::value(sr_fold_lane(inc, 63), q);
           k = pass_end;
           break;
         }
         cl = __builtin_ctzll(cross);
-        const I x0 = __shfl(i0, cl > 0 ? cl - 1 : 0, 64), x1 = __shfl(i1, cl > 0 ? cl - 1 : 0, 64);
+        const I x0 = sr_fold_lane(i0, cl > 0 ? cl - 1 : 0), x1 = sr_fold_lane(i1, cl > 0 ? cl - 1 : 0);
         if (cl > 0) xp = odd ? x1 : x0;
       }
       // the lane whose rows leave the binade
@@ -909,15 +899,15 @@ __device__ T sr_fold_rows_wave(const T* __restrict__ base, int64_t lo, int64_t k
             d = m + (kind == 2 ? 1 : (kind == 1 ? ((run + m) & 1) : 0));
           }
           if (!done && run + d >= lim) {
-            nF = T(ldexp(double(run), q)) + e;  // the hardware's own rounding of this step
+            nF = SrFoldBinade<T>::value(run, q) + e;  // the hardware's own rounding of this step
             nk = r0 + r + 1;
             done = true;
           }
           if (!done) run += d;
         }
       }
-      F = __shfl(nF, cl, 64);
-      k = __shfl(nk, cl, 64);
+      F = sr_fold_lane(nF, cl);
+      k = sr_fold_lane(nk, cl);
       {  // the rows up to the crossing are done
         const int64_t dk = k - r0;
         const int rk = dk < 0 ? 0 : (dk > RW ? RW : int(dk));
@@ -943,18 +933,18 @@ __global__ void __launch_bounds__(64) sr_fold_walk_kernel(SrFoldTabs ft, int np,
                                                            const T* __restrict__ losses, int64_t slot_rows,
                                                            const uint32_t* __restrict__ perm,
                                                            const T* __restrict__ carry, T* __restrict__ out_val,
-                                                           int32_t* __restrict__ out_st, int4* __restrict__ dbg) {
+                                                           int32_t* __restrict__ out_st, int4* __restrict__ dbg,
+                                                           int all_rows) {
   using Tr = SrFoldTraits<T>;
   using I = typename SrFoldTab<T>::I;
   using Pair = typename SrFoldTab<T>::Pair;
   constexpr I CAP = I(1) << (Tr::mant + 3);
-  constexpr T MIN_NORMAL = sizeof(T) == 4 ? T(1.17549435e-38f) : T(2.2250738585072014e-308);
   const int32_t* __restrict__ code = ft.code;
   const Pair* __restrict__ tab = static_cast<const Pair*>(ft.tab);
   const Pair* __restrict__ tab2 = static_cast<const Pair*>(ft.tab2);
   const int lane = int(threadIdx.x) & 63;
   const uint64_t clk0 = dbg ? wall_clock64() : 0;
-  int n_slow = 0, n_rounds = 0, n_runs = 0, n_skip = 0;  // (SR_AMD_FOLD_STATS: per-tree walk statistics)
+  int n_slow = 0, n_rounds = 0, n_skip = 0;  // (SR_AMD_FOLD_STATS: per-tree walk statistics)
   uint64_t slow_clk = 0;
   const int p = int(blockIdx.x);  // (one wave per workgroup: a finished walk frees its slot at once)
   if (p >= np) return;  // wave-uniform
@@ -972,40 +962,58 @@ __global__ void __launch_bounds__(64) sr_fold_walk_kernel(SrFoldTabs ft, int np,
   if (carry) {
     F = carry[t];
   } else if (c_first >= SR_FCODE_SLOT0 && n > 0) {  // Statistics.mean / Base.sum over a generator: the
-    F = seg_base(c_first)[0];                       // first loss starts the fold
-    k = 1;
+    // first loss starts the fold; the first rows then go one by one, in the hardware's own adds (the
+    // running value leaves a binade every few rows here: a round per crossing would cost ~1 us each)
+    const T* b = seg_base(c_first);
+    const int64_t ks = (rb_rows < n ? rb_rows : n) < 256 ? (rb_rows < n ? rb_rows : n) : 256;
+    T v[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) v[j] = (4 * lane + j < ks) ? b[4 * lane + j] : T(0);
+    F = sr_fold_lane(v[0], 0);
+    for (int L = 0; L < 64 && 4 * L < ks; ++L) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int r = 4 * L + j;
+        if (r >= 1 && r < ks) F = F + sr_fold_lane(v[j], L);
+      }
+    }
+    k = ks;
   } else {
     fail = n > 0;  // (the plan keeps the first segment's losses)
     why = 1;
   }
   T ev[RW];  // a slow segment's current pass (have: ev holds the next slow segment's first pass)
   bool have = false;
+  // the chunk's four arrays in one round trip (unconditional loads at a valid index, then selects: a
+  // load under a branch on another load's value costs a second round trip), the next chunk's issued
+  // at the start of this one
+  auto chunk_at = [&](int c) { return size_t(c + lane < n_rb ? c + lane : n_rb - 1) * size_t(np) + size_t(p); };
+  size_t so_n = chunk_at(0);
+  int32_t cd_n = code[so_n], sq_n = ft.sq[so_n];
+  Pair pa_n = tab[so_n], pb_n = tab2[so_n];
   for (int c0 = 0; c0 < n_rb && !fail; c0 += 64) {
     have = false;
     const int sg = c0 + lane;
     const bool in = sg < n_rb;
-    const size_t so = size_t(sg) * size_t(np) + size_t(p);
-    const int32_t cd = in ? code[so] : SR_FCODE_SKIP;
+    const int32_t cd_l = cd_n, sq_l = sq_n;
+    const Pair pa = pa_n, pb = pb_n;
+    if (c0 + 64 < n_rb) {
+      so_n = chunk_at(c0 + 64);
+      cd_n = code[so_n];
+      sq_n = ft.sq[so_n];
+      pa_n = tab[so_n];
+      pb_n = tab2[so_n];
+    }
+    const int32_t cd = in ? cd_l : SR_FCODE_SKIP;
     const bool slow = in && cd >= SR_FCODE_SLOT0;
-    I x0 = 0, x1 = 0;
-    if (in && !slow && cd != SR_FCODE_SKIP) {
-      const auto pr = tab[so];
-      x0 = I(pr.x);
-      x1 = I(pr.y);
-    }
-    // a slow segment's lower window binade and its steps under that binade and the next
-    int32_t sq = SR_FCODE_SKIP;
-    I s0 = 0, s1 = 0, u0 = 0, u1 = 0;
-    if (slow) {
-      sq = ft.sq[so];
-      if (sq != SR_FCODE_SKIP) {
-        const auto pa = tab[so], pb = tab2[so];
-        s0 = I(pa.x);
-        s1 = I(pa.y);
-        u0 = I(pb.x);
-        u1 = I(pb.y);
-      }
-    }
+    // a steps segment's pair; a slow segment's lower window binade and its steps under that binade
+    // (s0, s1) and the next (u0, u1)
+    const bool steps = in && !slow && cd != SR_FCODE_SKIP;
+    I x0 = steps ? I(pa.x) : I(0), x1 = steps ? I(pa.y) : I(0);
+    const int32_t sq = slow ? sq_l : SR_FCODE_SKIP;
+    const bool has2 = sq != SR_FCODE_SKIP;
+    const I s0 = has2 ? I(pa.x) : I(0), s1 = has2 ? I(pa.y) : I(0);
+    const I u0 = has2 ? I(pb.x) : I(0), u1 = has2 ? I(pb.y) : I(0);
     if (__builtin_amdgcn_ballot_w64(in && cd == SR_FCODE_SKIP)) {  // (a plan out of slots)
       fail = true;
       why = 2;
@@ -1028,7 +1036,7 @@ __global__ void __launch_bounds__(64) sr_fold_walk_kernel(SrFoldTabs ft, int np,
     while (pos < end && !fail) {
       const int64_t lo = int64_t(c0 + pos) * rb_rows;
       if ((slowm >> pos) & 1u) {  // a slow segment, row by row
-        const int32_t c = __shfl(cd, pos, 64);
+        const int32_t c = sr_fold_lane(cd, pos);
         const int64_t hi = lo + rb_rows < n ? lo + rb_rows : n;
         if (k < lo || k > hi) {
           fail = true;
@@ -1036,25 +1044,16 @@ __global__ void __launch_bounds__(64) sr_fold_walk_kernel(SrFoldTabs ft, int np,
           break;
         }
         {  // the running value may not leave a binade in this segment after all: its composed steps
-          const int32_t q0 = __shfl(sq, pos, 64);
+          const int32_t q0 = sr_fold_lane(sq, pos);
           if (k == lo && q0 != SR_FCODE_SKIP && F <= SrM<T>::big) {
-            int qf;
-            I lim;
-            if (F < MIN_NORMAL) {
-              qf = Tr::qmin;
-              lim = I(1) << Tr::mant;
-            } else {
-              int ex;
-              (void)frexp(double(F), &ex);
-              qf = ex - 1 - Tr::mant;
-              lim = I(1) << (Tr::mant + 1);
-            }
-            const I P = I(ldexp(double(F), -qf));
+            const SrFoldBinade<T> bn(F);
+            const int qf = bn.q;
+            const I P = bn.P, lim = bn.lim;
             const bool odd = (P & 1) != 0;
-            const I ga = __shfl(odd ? s1 : s0, pos, 64), gb = __shfl(odd ? u1 : u0, pos, 64);
+            const I ga = sr_fold_lane(odd ? s1 : s0, pos), gb = sr_fold_lane(odd ? u1 : u0, pos);
             const I g = qf == q0 ? ga : (qf == q0 + 1 ? gb : lim);
             if (P + g < lim) {
-              F = T(ldexp(double(P + g), qf));
+              F = SrFoldBinade<T>::value(P + g, qf);
               k = hi;
               have = false;  // (ev held this segment's prefetched rows)
               ++n_skip;
@@ -1071,7 +1070,7 @@ __global__ void __launch_bounds__(64) sr_fold_walk_kernel(SrFoldTabs ft, int np,
         const T* nbase = nullptr;
         int64_t nlo = 0, nhi = 0;
         if (np2 < end) {
-          nbase = seg_base(__shfl(cd, np2, 64));
+          nbase = seg_base(sr_fold_lane(cd, np2));
           nlo = int64_t(c0 + np2) * rb_rows;
           nhi = nlo + rb_rows < n ? nlo + rb_rows : n;
         }
@@ -1092,33 +1091,44 @@ __global__ void __launch_bounds__(64) sr_fold_walk_kernel(SrFoldTabs ft, int np,
       const uint64_t after = (slowm >> pos) >> 1;
       int e = after ? pos + 1 + __builtin_ctzll(after) : end;
       if (e > end) e = end;
-      const int32_t q = __shfl(cd, pos, 64);
-      const I g0 = __shfl(x0, e - 1, 64), g1 = __shfl(x1, e - 1, 64);
-      int qf;
-      I lim;
-      if (F < MIN_NORMAL) {
-        qf = Tr::qmin;
-        lim = I(1) << Tr::mant;
-      } else {
-        int ex;
-        (void)frexp(double(F), &ex);
-        qf = ex - 1 - Tr::mant;
-        lim = I(1) << (Tr::mant + 1);
-      }
-      if (k != lo || qf != q || !(F <= SrM<T>::big)) {  // the running value left the plan's window
+      const int32_t q = sr_fold_lane(cd, pos);
+      const I g0 = sr_fold_lane(x0, e - 1), g1 = sr_fold_lane(x1, e - 1);
+      if (!(F <= SrM<T>::big)) {
         fail = true;
-        why = qf < q ? 5 : (qf > q ? 6 : 7);
+        why = 7;
         break;
       }
-      const I P = I(ldexp(double(F), -q));
+      const SrFoldBinade<T> bn(F);
+      const int qf = bn.q;
+      const I lim = bn.lim;
+      const I P = bn.P;
       const I g = (P & 1) ? g1 : g0;
-      if (P + g >= lim) {  // the fold crosses a binade inside a run the plan called safe
-        fail = true;
-        why = 8;
-        break;
+      if (k != lo || qf != q || P + g >= lim) {
+        // the running value left the plan's window (it drifted from the f64 prefix past delta), or the
+        // fold crosses a binade inside a run the plan called safe: with every row kept (stored losses,
+        // slot p n_rb + row block), the run's segments row by row; otherwise the tree fails
+        if (!all_rows || k != lo) {
+          fail = true;
+          why = k != lo ? 7 : (qf < q ? 5 : (qf > q ? 6 : 8));
+          break;
+        }
+        for (int s2 = pos; s2 < e && !fail; ++s2) {
+          const int64_t l2 = int64_t(c0 + s2) * rb_rows, h2 = l2 + rb_rows < n ? l2 + rb_rows : n;
+          const T* b2 = losses + (size_t(p) * size_t(n_rb) + size_t(c0 + s2)) * size_t(slot_rows);
+          sr_fold_load<T, RW>(b2, l2, l2, h2, lane, ev);
+          F = sr_fold_rows_wave<T, RW>(b2, l2, k, h2, F, lane, n_rounds, ev, nullptr, 0, 0);
+          ++n_slow;
+          k = h2;
+          if (!(F <= SrM<T>::big)) {
+            fail = true;
+            why = 4;
+          }
+        }
+        have = false;
+        pos = e;
+        continue;
       }
-      F = T(ldexp(double(P + g), q));
-      ++n_runs;
+      F = SrFoldBinade<T>::value(P + g, q);
       const int64_t hl = int64_t(c0 + e) * rb_rows;
       k = hl < n ? hl : n;
       pos = e;
@@ -1150,10 +1160,11 @@ hipError_t sr_launch_fold_stab(const double* part, int np, int n_rb, int64_t rb_
 template <typename T>
 hipError_t sr_launch_fold_walk(SrFoldTabs ft, int np, int n_rb, int64_t rb_rows, int64_t n, const T* losses,
                                int64_t slot_rows, const uint32_t* perm, const T* carry, T* out_val, int32_t* out_st,
-                               void* dbg, hipStream_t s) {
+                               void* dbg, int all_rows, hipStream_t s) {
   if (np <= 0) return hipSuccess;
   hipLaunchKernelGGL((sr_fold_walk_kernel<T, sizeof(T) == 4 ? 16 : 8>), dim3(unsigned(np)), dim3(64), 0, s, ft,
-                     np, n_rb, rb_rows, n, losses, slot_rows, perm, carry, out_val, out_st, static_cast<int4*>(dbg));
+                     np, n_rb, rb_rows, n, losses, slot_rows, perm, carry, out_val, out_st, static_cast<int4*>(dbg),
+                     all_rows);
   return hipGetLastError();
 }
 #define SR_INSTANTIATE_FOLD2(T)                                                                                      \
@@ -1162,7 +1173,7 @@ hipError_t sr_launch_fold_walk(SrFoldTabs ft, int np, int n_rb, int64_t rb_rows,
   template hipError_t sr_launch_fold_stab<T>(const double*, int, int, int64_t, int64_t, const uint32_t*,              \
                                              const SrFoldWho&, double, const T*, SrFoldTabs, hipStream_t);             \
   template hipError_t sr_launch_fold_walk<T>(SrFoldTabs, int, int, int64_t, int64_t, const T*, int64_t,               \
-                                             const uint32_t*, const T*, T*, int32_t*, void*, hipStream_t);
+                                             const uint32_t*, const T*, T*, int32_t*, void*, int, hipStream_t);
 SR_INSTANTIATE_FOLD2(float)
 SR_INSTANTIATE_FOLD2(double)
 

@@ -305,13 +305,15 @@ struct sr_ctx {
   // 1 (default) single-GPU loss calls with weights >= 0; 0 the f64 sums (rounds 1-5).  Small calls
   // (every tree's losses fit fold_store_mb) keep the loss launch's losses; larger Float32 calls run the
   // complete trees again in FOLD mode (slow segments' losses in up to fold_slot_mb of slots); larger
-  // Float64 calls keep the f64 sum (within ~1e-13 of the fold, north_star's f64 bar is 1e-10).
+  // Float64 calls, and calls whose row blocks pass fold_seg_max rows (C4: 2^26 rows per GPU), keep the f64
+  // sum (Float64: within ~1e-13 of the fold, north_star's f64 bar is 1e-10).
   int ref_fold = 1;
   int64_t fold_store_mb = 512;
-  int64_t fold_slot_mb = 2048;
+  int64_t fold_slot_mb = 4096;
   // the plan's window: the fold within 2^-8 of the f64 prefix, else the tree fails (C2's trees: the fold is
   // within 2.1e-3 of the f64 sum at 2^20 rows; 2^-6 kept twice the slow segments)
   int fold_delta_log2 = 8;
+  int64_t fold_seg_max = 16384;  // SR_AMD_FOLD_SEG_MAX: calls whose row blocks are longer keep the f64 sum
   int fold_debug_fail = 0;   // (tests: "fold_debug_fail")
   int fold_stats = 0;        // SR_AMD_FOLD_STATS=1: per-tree walk statistics to stderr after each call (analysis)
   DevBuf fold_dbg;
@@ -604,10 +606,12 @@ int fold_walk(sr_ctx* ctx, const FoldJob<T>& job, const FoldRegion<T>& fr, const
   const int64_t slot_rows = job.path == 1 ? rb_rows : job.slot_rows;
   int4* dbg = ctx->fold_stats ? ctx->fold_dbg.as<int4>() + fr.t0 : nullptr;  // (SR_AMD_FOLD_STATS)
   SR_HIP_CHECK(sr_launch_fold_walk<T>(ft, int(fr.np), nrb, rb_rows, job.n_eval, losses, slot_rows, fr.a.perm,
-                                      carry ? carry + fr.t0 : nullptr, out_val + fr.t0, out_st + fr.t0, dbg, cs));
+                                      carry ? carry + fr.t0 : nullptr, out_val + fr.t0, out_st + fr.t0, dbg,
+                                      job.path == 1, cs));
   if (ctx->fold_stats == 2)  // (analysis: the same walk again, its loads now warm: the statistics are the second's)
     SR_HIP_CHECK(sr_launch_fold_walk<T>(ft, int(fr.np), nrb, rb_rows, job.n_eval, losses, slot_rows, fr.a.perm,
-                                        carry ? carry + fr.t0 : nullptr, out_val + fr.t0, out_st + fr.t0, dbg, cs));
+                                        carry ? carry + fr.t0 : nullptr, out_val + fr.t0, out_st + fr.t0, dbg,
+                                      job.path == 1, cs));
   return SR_OK;
 }
 
@@ -742,13 +746,22 @@ int run_batch(sr_ctx* ctx, const sr_dataset* ds, int opset_id, const sr_tree_bat
     // Float64: only with stored losses (no FOLD build), decided on the largest shard so every rank agrees
     const bool f64_off = sizeof(T) == 8 && double(nt) * double(pos_rows) * double(max_shard) / double(n_eval) *
                                                double(sizeof(T)) > double(ctx->fold_store_mb) * 1048576.0;
-    if (f64_off) {
+    // segments (row blocks) past fold_seg_max rows on the largest shard: no fold (a slow segment's rows
+    // are kept whole: C4's 2^26 rows per GPU make 1 MiB segments, ~10 per complete tree)
+    int64_t rb_big = 0;
+    {
+      const Grid gb = make_grid<T>(max_shard, nt, R, W, int(ds->nf), 1, 0, ds->w != nullptr, ctx->tree_group, mrb);
+      rb_big = int64_t(gb.tiles) * 64 * R;
+    }
+    if (f64_off || rb_big > ctx->fold_seg_max) {
     } else if (double(nt) * double(pos_rows) * double(sizeof(T)) <= double(ctx->fold_store_mb) * 1048576.0) {
       fold_path = 1;
       SR_HIP_CHECK(ctx->fold_store.ensure(size_t(nt) * size_t(pos_rows) * sizeof(T)));
     } else if (sizeof(T) == 4 && fold_mode_builds) {
       fold_path = 2;
-      const int64_t slots = std::max<int64_t>(1, ctx->fold_slot_mb * 1048576 / (fold_slot_rows * int64_t(sizeof(T))));
+      // (slots for ~24 slow segments per tree — C2 averages 10 — up to fold_slot_mb)
+      const int64_t slots = std::max<int64_t>(1, std::min<int64_t>(int64_t(nt) * 24, ctx->fold_slot_mb * 1048576 /
+                                                                                     (fold_slot_rows * int64_t(sizeof(T)))));
       SR_HIP_CHECK(ctx->fold_store.ensure(size_t(slots) * size_t(fold_slot_rows) * sizeof(T)));
       SR_HIP_CHECK(ctx->fold_ctl.ensure(64));
       SR_HIP_CHECK(hipMemsetAsync(ctx->fold_ctl.p, 0, sizeof(int), s));  // the call's slot counter
@@ -3518,6 +3531,7 @@ int sr_init(int device, sr_ctx** out) {
   if (const char* v = std::getenv("SR_AMD_FOLD_SLOT_MB")) ctx->fold_slot_mb = std::max<int64_t>(1, std::atoll(v));
   if (const char* v = std::getenv("SR_AMD_FOLD_STATS")) ctx->fold_stats = std::atoi(v);
   if (const char* v = std::getenv("SR_AMD_FOLD_DELTA_LOG2")) ctx->fold_delta_log2 = std::max(1, std::min(40, std::atoi(v)));
+  if (const char* v = std::getenv("SR_AMD_FOLD_SEG_MAX")) ctx->fold_seg_max = std::max<int64_t>(0, std::atoll(v));
   hipError_t e = hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking);
   if (e == hipSuccess && std::getenv("SR_AMD_EAGER_STREAM2")) e = ctx->need_stream2();  // (A/B: the round-4 layout)
   if (e == hipSuccess) e = hipEventCreateWithFlags(&ctx->ev_join, hipEventDisableTiming);
@@ -4260,6 +4274,10 @@ int sr_set_tuning(sr_ctx* ctx, const char* name, int64_t value) {
   }
   if (std::strcmp(name, "fold_delta_log2") == 0) {  // the plan's window 2^-value around the f64 prefix
     ctx->fold_delta_log2 = int(value < 1 ? 1 : (value > 40 ? 40 : value));
+    return SR_OK;
+  }
+  if (std::strcmp(name, "fold_seg_max") == 0) {  // longest row block folded (SR_AMD_FOLD_SEG_MAX)
+    ctx->fold_seg_max = value < 0 ? 0 : value;
     return SR_OK;
   }
   if (std::strcmp(name, "fold_seg") == 0) {  // rows per segment of the in-order loss fold (SR_AMD_FOLD_SEG)

@@ -139,7 +139,7 @@ __device__ __forceinline__ T sr_fold_scan(T v) {
   v = sr_fold_dpp_add<0x143, 0xc>(v);  // row_bcast:31 into rows 2, 3
   return v;
 }
-// the value of lane l (wave-uniform l), by readlane
+// the value of lane l (wave-uniform l), by readlane (a few cycles; __shfl is an LDS permute round trip)
 __device__ __forceinline__ float sr_fold_lane(float v, int l) {
   return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), l));
 }
@@ -149,6 +149,50 @@ __device__ __forceinline__ double sr_fold_lane(double v, int l) {
   const uint32_t hi = uint32_t(__builtin_amdgcn_readlane(int(uint32_t(b >> 32)), l));
   return __longlong_as_double(int64_t((uint64_t(hi) << 32) | lo));
 }
+
+__device__ __forceinline__ int32_t sr_fold_lane(int32_t v, int l) { return __builtin_amdgcn_readlane(v, l); }
+__device__ __forceinline__ int64_t sr_fold_lane(int64_t v, int l) {
+  const uint32_t lo = uint32_t(__builtin_amdgcn_readlane(int(uint32_t(uint64_t(v))), l));
+  const uint32_t hi = uint32_t(__builtin_amdgcn_readlane(int(uint32_t(uint64_t(v) >> 32)), l));
+  return int64_t((uint64_t(hi) << 32) | lo);
+}
+
+// A finite running value F >= 0 as (q, P, lim): F = P 2^q with P < lim in F's binade (spacing 2^q; the
+// subnormals share the lowest normal binade's spacing, lim = 2^mant), by the bits alone (no f64
+// round trip: the walk's rounds are a chain of these).  And back: (P, q) with P < lim -> F, bits =
+// ((q - qmin) << mant) + P for the normal and the subnormal binades alike.
+template <typename T>
+struct SrFoldBinade;
+template <>
+struct SrFoldBinade<float> {
+  int q;
+  int32_t P, lim;
+  __device__ __forceinline__ explicit SrFoldBinade(float F) {
+    const uint32_t b = __float_as_uint(F);
+    const int e = int(b >> 23);
+    q = e == 0 ? -149 : e - 150;
+    P = e == 0 ? int32_t(b) : int32_t((b & 0x7fffffu) | 0x800000u);
+    lim = e == 0 ? (1 << 23) : (1 << 24);
+  }
+  static __device__ __forceinline__ float value(int32_t P, int q) {
+    return __uint_as_float((uint32_t(q + 149) << 23) + uint32_t(P));
+  }
+};
+template <>
+struct SrFoldBinade<double> {
+  int q;
+  int64_t P, lim;
+  __device__ __forceinline__ explicit SrFoldBinade(double F) {
+    const uint64_t b = uint64_t(__double_as_longlong(F));
+    const int e = int(b >> 52);
+    q = e == 0 ? -1074 : e - 1075;
+    P = e == 0 ? int64_t(b) : int64_t((b & 0xfffffffffffffull) | 0x10000000000000ull);
+    lim = e == 0 ? (int64_t(1) << 52) : (int64_t(1) << 53);
+  }
+  static __device__ __forceinline__ double value(int64_t P, int q) {
+    return __longlong_as_double(int64_t((uint64_t(q + 1074) << 52) + uint64_t(P)));
+  }
+};
 
 // binade spacing exponent q of a value >= 0 (subnormals and 0: the fixed subnormal spacing); values
 // past the type's range get a q no finite running value has

@@ -19,7 +19,7 @@ struct SrFoldTabs {
 template <typename T>
 hipError_t sr_launch_fold_walk(SrFoldTabs ft, int np, int n_rb, int64_t rb_rows, int64_t n, const T* losses,
                                int64_t slot_rows, const uint32_t* perm, const T* carry, T* out_val, int32_t* out_st,
-                               void* dbg, hipStream_t s);
+                               void* dbg, int all_rows, hipStream_t s);
 
 #define CK(x)                                                             \
   do {                                                                    \
@@ -65,7 +65,7 @@ int main(int argc, char** argv) {
   CK(hipEventCreate(&e1));
   for (int rep = 0; rep < 3; ++rep) {
     CK(hipEventRecord(e0, 0));
-    CK(sr_launch_fold_walk<float>(ft, np, n_rb, rb_rows, n, d_loss, rb_rows, nullptr, nullptr, d_val, d_st, d_dbg, 0));
+    CK(sr_launch_fold_walk<float>(ft, np, n_rb, rb_rows, n, d_loss, rb_rows, nullptr, nullptr, d_val, d_st, d_dbg, 1, 0));
     CK(hipEventRecord(e1, 0));
     CK(hipEventSynchronize(e1));
     float ms = 0;
