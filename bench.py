@@ -300,6 +300,18 @@ def main():
     ref_fold = ctx.last_ref_fold()
 
     subs = {}
+    if world == 1:  # the fold's cost on the headline step: the same step with the f64 sums
+        ctx.set_tuning("ref_fold", 0)
+        call0, _ = single_gpu_call(ctx, tb, ds, opts)
+        st0 = {}
+        dt0, _, km0 = timed(lib_step(ctx, call0, st0), max(3, args.steps // 2), 2, comm.barrier)
+        ctx.set_tuning("ref_fold", 1)
+        subs["fold_cost"] = {
+            "ms_per_step_fold": dt / args.steps * 1e3, "ms_per_step_f64_sum": dt0 / max(3, args.steps // 2) * 1e3,
+            "fold_kernel_ms_per_step": ref_fold["kernel_ms"], "trees_folded": ref_fold["folded"],
+            "trees_fallback": ref_fold["fallback"], "path": ref_fold["path"],
+            "note": ("ref_fold 1 (default): every complete tree's loss is the reference's in-order Float32 fold; "
+                     "ref_fold 0: the f64 per-tree sums of rounds 1-5 (~5e-4 relative off at 2^20 rows)")}
     if world == 1 and not args.no_sharded_path:
         if rank == 0:
             progress("c2_sharded_path")
@@ -472,7 +484,8 @@ def compact_line(line):
     if line.get("search"):
         s = {}
         for name, v in line["search"].items():
-            o = _pick(v, ("value", "unit", "iterations_per_s", "islands", "wall_s", "device_calls",
+            o = _pick(v, ("value", "unit", "iterations_per_s", "iterations_per_s_f64_sum",
+                          "device_wall_per_call_us_f64_sum", "islands", "wall_s", "device_calls",
                           "device_wall_per_call_us", "kernel_busy_per_call_us", "best_loss"))
             if "cpu_baseline" in v:
                 o["cpu_baseline"] = _pick(v["cpu_baseline"], ("value", "unit", "iterations_per_s", "cores", "kind"))
@@ -920,6 +933,15 @@ def chunk_groups(nt, rows, n_launch, rows_per_lane=8):
     return out
 
 
+def set_ref_fold(v, lanes=4):
+    """The in-order loss fold on (1) or off (0: the f64 per-tree sums) for every scoring context of this
+    process (the default context and the search's extra lanes)."""
+    from sr_amd.device import get_lane_context
+
+    for lane in range(lanes):
+        get_lane_context(lane).set_tuning("ref_fold", int(v))
+
+
 def search_lines(args):
     """BASELINE.json metric, second half: search iterations/sec of C1 (the README example) and C3
     (Feynman-style 5-feature target, 100k rows, f32), device-scored, each beside the same engine with
@@ -961,7 +983,16 @@ def search_lines(args):
         os.environ["SR_AMD_SEARCH_KERNEL_TIMES"] = "1"
         diag = equation_search(X, y, niterations=min(5, args.search_iters), options=o, seed=0)
         del os.environ["SR_AMD_SEARCH_KERNEL_TIMES"]
+        # the fold's cost: the same search scored with the f64 per-tree sums
+        set_ref_fold(0)
+        t0 = time.perf_counter()
+        res0 = equation_search(X, y, niterations=args.search_iters, options=o, seed=0)
+        wall0 = time.perf_counter() - t0
+        set_ref_fold(1)
         line = {"metric": "search iterations/sec", "value": res.s_r_cycles / wall, "unit": "s_r_cycles/s",
+                "loss_accumulation": "the reference's in-order fold in T (ref_fold 1, the default)",
+                "iterations_per_s_f64_sum": args.search_iters / wall0,
+                "device_wall_per_call_us_f64_sum": res0.device_s / max(res0.device_calls, 1) * 1e6,
                 "iterations_per_s": args.search_iters / wall, "islands": o.populations,
                 "iterations": args.search_iters, "wall_s": wall, "device_calls": res.device_calls,
                 "device_wall_s": res.device_s, "host_s": res.host_s,

@@ -617,6 +617,26 @@ __global__ void __launch_bounds__(256) sr_fold_plan_kernel(const double* __restr
   const uint32_t t = perm ? perm[p] : uint32_t(p);
   const bool ok = who.eligible<T>(t);
   double run = who.est ? who.est[t] : 0.0;  // (a row shard after the first: the shards before it)
+  // A tree whose losses hardly vary — a huge constant tree, (c - y)^2 with |c| >> |y| — drifts from the
+  // f64 prefix systematically: once the running value's ulp exceeds the losses' spread, every step
+  // rounds the same way (up to ~1 % at 2^20 rows: C2's failed walks, round 6).  Its window is widened to
+  // 2^-5 when its full row blocks' sums agree to 2^-7 (a tree with varied losses: ~10 %; the last block
+  // may be shorter and is left out).
+  if (ok && part && n_rb >= 3) {
+    double mn = 1.7976931348623157e308, mx = 0.0;
+    for (int rb = lane; rb < n_rb - 1; rb += 64) {
+      const double v = part[size_t(rb) * size_t(np) + size_t(p)];
+      mn = v < mn ? v : mn;
+      mx = v > mx ? v : mx;
+    }
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) {
+      const double a = __shfl_xor(mn, off, 64), b = __shfl_xor(mx, off, 64);
+      mn = a < mn ? a : mn;
+      mx = b > mx ? b : mx;
+    }
+    if (mx <= mn * (1.0 + 0.0078125) && delta < 0.03125) delta = 0.03125;
+  }
   for (int c0 = 0; c0 < n_rb; c0 += 64) {
     const int rb = c0 + lane;
     const bool in = rb < n_rb;

@@ -226,7 +226,10 @@ __global__ void __launch_bounds__(W * 64) sr_grad_kernel(const SrGradArgs<T> a) 
         // per instruction instead of decoding the variant; the operand's tangent is known zero for a
         // feature and one-hot for a constant, so those products are not computed).  Every value is
         // the one the general form fma(pa, da, pb db) gives: a product by an exact 0 or 1 and a sum
-        // with an exact 0 are exact (up to the sign of a zero, which the gradient sums cannot see).
+        // with an exact 0 are exact (up to the sign of a zero, which the gradient sums cannot see),
+        // and the skipped product by the zero tangent is still added as (partial x 0) — NaN when that
+        // partial is not finite (a DIV by a tiny feature: r finite, -r / x overflows), as in the
+        // general form.
         auto basic_bin = [&](auto op_c, auto var_c) __attribute__((always_inline)) {
           constexpr uint32_t B = decltype(op_c)::value;
           constexpr uint32_t V = decltype(var_c)::value;
@@ -281,8 +284,9 @@ __global__ void __launch_bounds__(W * 64) sr_grad_kernel(const SrGradArgs<T> a) 
                 }
               } else {
                 const T sc = LEFT ? pbv : pa;
+                const T z = (LEFT ? pa : pbv) * T(0);  // (the zero-tangent operand's product)
 #pragma unroll
-                for (int q = 0; q < KT; ++q) dv[j][q] = sc * dv[j][q];
+                for (int q = 0; q < KT; ++q) dv[j][q] = __builtin_fma(sc, dv[j][q], z);
               }
             }
           }

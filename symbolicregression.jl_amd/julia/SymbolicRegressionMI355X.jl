@@ -348,7 +348,8 @@ BackTracking())` (src/Options.jl:613-615), with Newton for a single constant as 
 itself chooses (src/ConstantOptimization.jl:38-56).  Returns `(iterations, f_calls_limit)` from
 `options.optimizer_options` (the `Optim.Options` built at src/Options.jl:988-997) when the device can
 run it, or `nothing`: any other `optimizer_algorithm` (`NelderMead`, accepted at Options.jl:738-746),
-another line search or BackTracking setting, a non-identity initial inverse Hessian, or Optim options
+another line search or BackTracking setting (incl. `iterations`, `maxstep`), a non-identity initial
+inverse Hessian, an `initial_stepnorm`, a manifold other than `Flat`, or Optim options
 beyond `iterations` / `f_calls_limit` at non-default values — the caller then keeps the reference's
 per-member `optimize_constants` (INTEGRATION.md §4)."""
 function device_optimizer(options)
@@ -357,7 +358,12 @@ function device_optimizer(options)
     ls = getfield(alg, :linesearch!)
     ls isa LineSearches.BackTracking || return nothing
     (ls.c_1 == 1e-4 && ls.ρ_hi == 0.5 && ls.ρ_lo == 0.1 && ls.order == 3) || return nothing
+    # (BackTracking's remaining fields and BFGS's step norm / manifold at their defaults too: the device
+    #  optimiser implements exactly that configuration — ADVICE r5)
+    (ls.iterations == 1000 && isinf(ls.maxstep)) || return nothing
     getfield(alg, :initial_invH) === nothing || return nothing
+    getfield(alg, :initial_stepnorm) === nothing || return nothing
+    getfield(alg, :manifold) isa Optim.Flat || return nothing
     getfield(alg, :alphaguess!) isa LineSearches.InitialStatic || return nothing
     o = options.optimizer_options
     # the device's stopping rules: g_abstol 1e-8 (Optim's default), iterations, f_calls_limit
