@@ -457,11 +457,11 @@ int sr_last_phase_ms(sr_ctx* ctx, double* out, int n);
  * is the reference's in-order fold in T of its elementwise losses (src/LossFunctions.jl:38-58), divided
  * in T; 0: the f64 sum of rounds 1-5, whose last bits — ~5e-4 relative at 2^20 rows in Float32 —
  * differ), "fold_store_mb" / "fold_slot_mb" (the fold's stored-loss and slow-segment budgets),
- * "fold_delta_log2" (the fold plan's window), "fold_seg_max" (the longest row block folded: a call whose
- * row blocks are longer — 2^26 rows per GPU — keeps the f64 sum, as "ref_fold" 0).  Results do not
- * depend on any knob but three: "ref_fold", "fold_seg_max" (whether a long call folds), and — without
- * the fold only — "max_row_blocks", which sets how many f64 partials a tree's sum adds (the last bit of
- * a loss may differ).  SR_ERR_INVALID_ARG for an unknown name.  sr_tuning_info (optional outputs)
+ * "fold_delta_log2" (the fold plan's window), "fold_seg_max" (the longest row block folded, on the
+ * default grid: a call whose row blocks are longer — 2^26 rows per GPU — keeps the f64 sum, as "ref_fold"
+ * 0).  Results do not depend on any knob but three: "ref_fold", "fold_seg_max" (whether a long call
+ * folds), and — without the fold only — "max_row_blocks", which sets how many f64 partials a tree's sum
+ * adds (the last bit of a loss may differ).  SR_ERR_INVALID_ARG for an unknown name.  sr_tuning_info (optional outputs)
  * reports how many derived columns the last sr_eval_loss_batch used and how many of its trees went
  * through the exact-sum pass (flagged BIG). */
 int sr_set_tuning(sr_ctx* ctx, const char* name, int64_t value);

@@ -981,6 +981,9 @@ __global__ void __launch_bounds__(64) sr_fold_walk_kernel(SrFoldTabs ft, int np,
   int64_t k = 0;
   if (carry) {
     F = carry[t];
+  } else if (c_first >= SR_FCODE_SLOT0 && n > 0 && (all_rows & 4)) {  // (debug: no serial start)
+    F = seg_base(c_first)[0];
+    k = 1;
   } else if (c_first >= SR_FCODE_SLOT0 && n > 0) {  // Statistics.mean / Base.sum over a generator: the
     // first loss starts the fold; the first rows then go one by one, in the hardware's own adds (the
     // running value leaves a binade every few rows here: a round per crossing would cost ~1 us each)
@@ -1065,7 +1068,7 @@ __global__ void __launch_bounds__(64) sr_fold_walk_kernel(SrFoldTabs ft, int np,
         }
         {  // the running value may not leave a binade in this segment after all: its composed steps
           const int32_t q0 = sr_fold_lane(sq, pos);
-          if (k == lo && q0 != SR_FCODE_SKIP && F <= SrM<T>::big) {
+          if (k == lo && q0 != SR_FCODE_SKIP && F <= SrM<T>::big && !(all_rows & 2)) {
             const SrFoldBinade<T> bn(F);
             const int qf = bn.q;
             const I P = bn.P, lim = bn.lim;
@@ -1081,6 +1084,11 @@ __global__ void __launch_bounds__(64) sr_fold_walk_kernel(SrFoldTabs ft, int np,
               continue;
             }
           }
+        }
+        if (k == hi) {  // (the first block wholly inside the serial start: nothing left here, nothing loaded)
+          have = false;
+          ++pos;
+          continue;
         }
         const int64_t b0 = k - ((k - lo) % (16 / int64_t(sizeof(T))));  // (the pass sr_fold_rows_wave expects)
         if (!have || b0 != lo) sr_fold_load<T, RW>(seg_base(c), lo, b0, hi, lane, ev);
@@ -1127,7 +1135,7 @@ __global__ void __launch_bounds__(64) sr_fold_walk_kernel(SrFoldTabs ft, int np,
         // the running value left the plan's window (it drifted from the f64 prefix past delta), or the
         // fold crosses a binade inside a run the plan called safe: with every row kept (stored losses,
         // slot p n_rb + row block), the run's segments row by row; otherwise the tree fails
-        if (!all_rows || k != lo) {
+        if (!(all_rows & 1) || k != lo) {
           fail = true;
           why = k != lo ? 7 : (qf < q ? 5 : (qf > q ? 6 : 8));
           break;

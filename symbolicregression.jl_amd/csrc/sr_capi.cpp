@@ -315,6 +315,7 @@ struct sr_ctx {
   int fold_delta_log2 = 8;
   int64_t fold_seg_max = 16384;  // SR_AMD_FOLD_SEG_MAX: calls whose row blocks are longer keep the f64 sum
   int fold_debug_fail = 0;   // (tests: "fold_debug_fail")
+  int fold_walk_dbg = 0;     // SR_AMD_FOLD_WALK_DBG (analysis): 2 no O(1) slow blocks, 4 no serial start
   int fold_stats = 0;        // SR_AMD_FOLD_STATS=1: per-tree walk statistics to stderr after each call (analysis)
   DevBuf fold_dbg;
   bool want_fold = false;    // set by eval_loss_submit around its run_batch
@@ -607,11 +608,11 @@ int fold_walk(sr_ctx* ctx, const FoldJob<T>& job, const FoldRegion<T>& fr, const
   int4* dbg = ctx->fold_stats ? ctx->fold_dbg.as<int4>() + fr.t0 : nullptr;  // (SR_AMD_FOLD_STATS)
   SR_HIP_CHECK(sr_launch_fold_walk<T>(ft, int(fr.np), nrb, rb_rows, job.n_eval, losses, slot_rows, fr.a.perm,
                                       carry ? carry + fr.t0 : nullptr, out_val + fr.t0, out_st + fr.t0, dbg,
-                                      job.path == 1, cs));
+                                      int(job.path == 1) | ctx->fold_walk_dbg, cs));
   if (ctx->fold_stats == 2)  // (analysis: the same walk again, its loads now warm: the statistics are the second's)
     SR_HIP_CHECK(sr_launch_fold_walk<T>(ft, int(fr.np), nrb, rb_rows, job.n_eval, losses, slot_rows, fr.a.perm,
                                         carry ? carry + fr.t0 : nullptr, out_val + fr.t0, out_st + fr.t0, dbg,
-                                      job.path == 1, cs));
+                                      int(job.path == 1) | ctx->fold_walk_dbg, cs));
   return SR_OK;
 }
 
@@ -747,10 +748,11 @@ int run_batch(sr_ctx* ctx, const sr_dataset* ds, int opset_id, const sr_tree_bat
     const bool f64_off = sizeof(T) == 8 && double(nt) * double(pos_rows) * double(max_shard) / double(n_eval) *
                                                double(sizeof(T)) > double(ctx->fold_store_mb) * 1048576.0;
     // segments (row blocks) past fold_seg_max rows on the largest shard: no fold (a slow segment's rows
-    // are kept whole: C4's 2^26 rows per GPU make 1 MiB segments, ~10 per complete tree)
+    // are kept whole: C4's 2^26 rows per GPU make 1 MiB segments, ~10 per complete tree).  Decided on the
+    // default grid, so that the max_row_blocks knob never changes a result.
     int64_t rb_big = 0;
     {
-      const Grid gb = make_grid<T>(max_shard, nt, R, W, int(ds->nf), 1, 0, ds->w != nullptr, ctx->tree_group, mrb);
+      const Grid gb = make_grid<T>(max_shard, nt, R, W, int(ds->nf), 1, 0, ds->w != nullptr, ctx->tree_group, 512);
       rb_big = int64_t(gb.tiles) * 64 * R;
     }
     if (f64_off || rb_big > ctx->fold_seg_max) {
@@ -3532,6 +3534,7 @@ int sr_init(int device, sr_ctx** out) {
   if (const char* v = std::getenv("SR_AMD_FOLD_STATS")) ctx->fold_stats = std::atoi(v);
   if (const char* v = std::getenv("SR_AMD_FOLD_DELTA_LOG2")) ctx->fold_delta_log2 = std::max(1, std::min(40, std::atoi(v)));
   if (const char* v = std::getenv("SR_AMD_FOLD_SEG_MAX")) ctx->fold_seg_max = std::max<int64_t>(0, std::atoll(v));
+  if (const char* v = std::getenv("SR_AMD_FOLD_WALK_DBG")) ctx->fold_walk_dbg = std::atoi(v) & 6;
   hipError_t e = hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking);
   if (e == hipSuccess && std::getenv("SR_AMD_EAGER_STREAM2")) e = ctx->need_stream2();  // (A/B: the round-4 layout)
   if (e == hipSuccess) e = hipEventCreateWithFlags(&ctx->ev_join, hipEventDisableTiming);
