@@ -713,6 +713,7 @@ def held_trees(opts, orc, sub, X, y, rows, d_loss, l64, bar, threads, ids=None, 
     out = []
     ops = opts.operators
     for j, k in enumerate(rows[:limit]):
+        progress(f"held tree {j + 1} of {min(len(rows), limit)}")
         one = sub.take([k])
         present = set()
         for d, o in zip(one.degree, one.op):
@@ -749,6 +750,7 @@ def per_tree_bar(orc, sub, X, y, d_loss, l64, ok, rel_bar, threads, accum="ref")
     worst = np.nonzero(ok & (r > rel_bar))[0]
     spread = np.zeros(len(d_loss))
     if worst.size:
+        progress(f"per-tree libm spread of {worst.size} trees")
         wsub = sub.take(worst)
         l0, c0 = orc.eval_loss_batch(wsub, X, y, accum=accum, n_threads=threads)
         for seed in (1, 2, 3, 4):
@@ -790,8 +792,11 @@ def c4_parity(opts, tb, res, device_call, rows_total, n_sample, accum="ref"):
     out = {}
     for name, t, d_loss, d_comp in (("sample", sub, np.asarray(res["l"])[idx], comp[idx]),
                                     ("planted_big", planted, pl_loss, pl_comp)):
+        progress(f"c4 parity: oracle f64 sums of {name} ({t.n_trees} trees)")
         l64, c64 = orc.eval_loss_batch(t, X, y, accum="f64", n_threads=threads)
+        progress(f"c4 parity: oracle in-order folds of {name}")
         lref, cref = orc.eval_loss_batch(t, X, y, accum="ref", n_threads=threads)
+        progress(f"c4 parity: per-tree bars of {name}")
         d_loss = np.asarray(d_loss, dtype=np.float64)
         ok = d_comp & c64
         lr = (lref if accum == "ref" else l64).astype(np.float64)
@@ -812,7 +817,7 @@ def c4_parity(opts, tb, res, device_call, rows_total, n_sample, accum="ref"):
                      "n_held_to_libm_spread_bar": n_wide, "loss_failures": int(fail.sum()),
                      "held_trees": held_trees(opts, orc, t, X, y, np.nonzero(fin & (r > 1e-4))[0], d_loss,
                                               lr, bar, threads, ids=idx if name == "sample" else None,
-                                              accum=accum)}
+                                              accum=accum, limit=8)}
     out["rows"] = int(rows_total)
     out["accumulation"] = accum
     out["pass"] = all(v["flag_mismatches"] == 0 and v["loss_failures"] == 0 and v["ref_fold_inf_mismatches"] == 0
