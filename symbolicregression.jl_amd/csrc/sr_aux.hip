@@ -1190,9 +1190,16 @@ hipError_t sr_launch_fold_walk(SrFoldTabs ft, int np, int n_rb, int64_t rb_rows,
                                int64_t slot_rows, const uint32_t* perm, const T* carry, T* out_val, int32_t* out_st,
                                void* dbg, int all_rows, hipStream_t s) {
   if (np <= 0) return hipSuccess;
-  hipLaunchKernelGGL((sr_fold_walk_kernel<T, sizeof(T) == 4 ? 16 : 8>), dim3(unsigned(np)), dim3(64), 0, s, ft,
-                     np, n_rb, rb_rows, n, losses, slot_rows, perm, carry, out_val, out_st, static_cast<int4*>(dbg),
-                     all_rows);
+  // (row blocks of at most 512 rows, e.g. the search's 100k-row calls: half-width passes, half the
+  //  per-round work of a crossing block that a 1,024-row pass would spend on idle lanes)
+  if (rb_rows <= 512)
+    hipLaunchKernelGGL((sr_fold_walk_kernel<T, sizeof(T) == 4 ? 8 : 4>), dim3(unsigned(np)), dim3(64), 0, s, ft, np,
+                       n_rb, rb_rows, n, losses, slot_rows, perm, carry, out_val, out_st, static_cast<int4*>(dbg),
+                       all_rows);
+  else
+    hipLaunchKernelGGL((sr_fold_walk_kernel<T, sizeof(T) == 4 ? 16 : 8>), dim3(unsigned(np)), dim3(64), 0, s, ft,
+                       np, n_rb, rb_rows, n, losses, slot_rows, perm, carry, out_val, out_st, static_cast<int4*>(dbg),
+                       all_rows);
   return hipGetLastError();
 }
 #define SR_INSTANTIATE_FOLD2(T)                                                                                      \
