@@ -478,6 +478,7 @@ def compact_line(line):
                 if k in p:
                     o["parity"][k] = _pick(p[k], ("trees", "complete", "flag_mismatches", "ref_fold_inf_mismatches",
                                                   "max_rel_vs_f64_accum", "max_rel_vs_ref_f32_fold",
+                                                  "max_rel_device_vs_ref_f32_fold",
                                                   "n_held_to_libm_spread_bar", "loss_failures",
                                                   "n_bit_exact_vs_ref_f32_fold"))
         out["c4"] = o
@@ -609,6 +610,7 @@ def c4_line(ctx, opts, eval_loss_sharded, gen_random_batch, Dataset, args, comm,
         progress(f"c4 steps: {tb.n_trees} trees x {rows_total} rows / {world}")
     dt, step_ms, kms = timed(lib_step(ctx, call, st), args.c4_steps, 1, comm.barrier)
     dt = comm.max(dt)
+    c4_fold = ctx.last_ref_fold()  # (2^26 rows: past fold_rows_max, the f64 sums)
     n_local = rows_total // world
     kmean, busy = float(np.mean(kms)), float(np.mean(st["busy"][-args.c4_steps:]))
     flops = float(n_local) * (tb.n_operator_nodes + 3 * tb.n_trees)
@@ -643,14 +645,18 @@ def c4_line(ctx, opts, eval_loss_sharded, gen_random_batch, Dataset, args, comm,
                                           if traffic else None), hbm_peak_GBps=PEAK_HBM_GBPS)}
     if world == 1 and rank == 0:
         progress("c4 projection to 8 ranks (rank 0's 8M-row shard)")
+        # (rank 0 of the 8-rank run folds as the whole 2^26-row call does: here, not at all)
+        ctx.set_tuning("ref_fold", 1 if c4_fold["path"] > 0 else 0)
         out["projection_8_ranks"] = c4_projection(ctx, opts, tb, eval_loss_sharded, Dataset, args, comm, rows_total,
                                                   out["ms_per_step"], passes)
+        ctx.set_tuning("ref_fold", 1)
     if world == 1 and rank == 0 and not args.no_c4_parity:
         progress("c4 parity (oracle over all rows for a tree sample)")
-        # (2^26 rows per GPU: row blocks past fold_seg_max keep the f64 sum, ref_fold path 0)
-        folded = ctx.last_ref_fold()["path"] > 0
+        # (2^26 rows: past fold_rows_max the f64 sums, ref_fold path 0)
+        folded = c4_fold["path"] > 0
         out["loss_accumulation"] = ("the reference's in-order fold in Float32" if folded else
-                                    "f64 per-tree sums (row blocks of 2^18 rows pass fold_seg_max: no fold)")
+                                    "f64 per-tree sums: 2^26 rows pass fold_rows_max (2^24), where the reference's "
+                                    "Float32 fold stalls up to 50 % below the exact mean (DESIGN 4.4)")
         out["parity"] = c4_parity(opts, tb, res, lambda t: eval_loss_sharded(t, ds, opts), rows_total,
                                   args.c4_parity_trees, accum="ref" if folded else "f64")
     ds.free_device()
@@ -806,6 +812,9 @@ def c4_parity(opts, tb, res, device_call, rows_total, n_sample, accum="ref"):
         inf_m = int(np.sum(ok & (np.isinf(d_loss) != np.isinf(lref))))
         with np.errstate(invalid="ignore", divide="ignore"):
             r64 = np.where(d_loss == l64, 0.0, np.abs(d_loss - l64) / np.maximum(np.abs(l64.astype(np.float64)), 1e-300))
+            lrf = lref.astype(np.float64)
+            rrf = np.where(d_loss == lrf, 0.0, np.abs(d_loss - lrf) / np.maximum(np.abs(lrf), 1e-300))
+        fin_r = fin & np.isfinite(lrf)
         out[name] = {"trees": int(t.n_trees), "complete": int(ok.sum()),
                      "flag_mismatches": int(np.sum(d_comp != c64)) + int(np.sum(cref != c64)),
                      "ref_fold_inf_trees": int(np.sum(ok & np.isinf(lref))), "ref_fold_inf_mismatches": inf_m,
@@ -814,6 +823,10 @@ def c4_parity(opts, tb, res, device_call, rows_total, n_sample, accum="ref"):
                      ("max_rel_vs_ref_f32_fold" if accum == "ref" else "max_rel_vs_oracle"):
                          float(np.max(np.where(np.isfinite(r[fin]), r[fin], 0.0), initial=0.0)),
                      "max_rel_vs_f64_accum": float(np.max(np.where(np.isfinite(r64[fin]), r64[fin], 0.0), initial=0.0)),
+                     # (the reference's own Float32 fold, whatever the device accumulated: at 2^26 rows it
+                     #  stalls far below the exact mean)
+                     "max_rel_device_vs_ref_f32_fold": float(np.max(np.where(np.isfinite(rrf[fin_r]), rrf[fin_r], 0.0),
+                                                                    initial=0.0)),
                      "n_held_to_libm_spread_bar": n_wide, "loss_failures": int(fail.sum()),
                      "held_trees": held_trees(opts, orc, t, X, y, np.nonzero(fin & (r > 1e-4))[0], d_loss,
                                               lr, bar, threads, ids=idx if name == "sample" else None,

@@ -457,11 +457,12 @@ int sr_last_phase_ms(sr_ctx* ctx, double* out, int n);
  * is the reference's in-order fold in T of its elementwise losses (src/LossFunctions.jl:38-58), divided
  * in T; 0: the f64 sum of rounds 1-5, whose last bits — ~5e-4 relative at 2^20 rows in Float32 —
  * differ), "fold_store_mb" / "fold_slot_mb" (the fold's stored-loss and slow-segment budgets),
- * "fold_delta_log2" (the fold plan's window), "fold_seg_max" (the longest row block folded, on the
- * default grid: a call whose row blocks are longer — 2^26 rows per GPU — keeps the f64 sum, as "ref_fold"
- * 0).  Results do not depend on any knob but three: "ref_fold", "fold_seg_max" (whether a long call
- * folds), and — without the fold only — "max_row_blocks", which sets how many f64 partials a tree's sum
- * adds (the last bit of a loss may differ).  SR_ERR_INVALID_ARG for an unknown name.  sr_tuning_info (optional outputs)
+ * "fold_delta_log2" (the fold plan's window), "fold_seg_max" (the longest row block folded: a folding
+ * call takes enough row blocks for it), "fold_rows_max" (the longest fold, 2^24 rows: a longer call —
+ * C4's 2^26 rows — keeps the f64 sum, as "ref_fold" 0).  Results do not depend on any knob but these
+ * three ("ref_fold", "fold_seg_max", "fold_rows_max": whether a call folds) and — without the fold only
+ * — "max_row_blocks", which sets how many f64 partials a tree's sum adds (the last bit of a loss may
+ * differ).  SR_ERR_INVALID_ARG for an unknown name.  sr_tuning_info (optional outputs)
  * reports how many derived columns the last sr_eval_loss_batch used and how many of its trees went
  * through the exact-sum pass (flagged BIG). */
 int sr_set_tuning(sr_ctx* ctx, const char* name, int64_t value);
@@ -473,7 +474,7 @@ int sr_set_tuning(sr_ctx* ctx, const char* name, int64_t value);
 int sr_last_grad_info(sr_ctx* ctx, int n, double* kernel_ms, double* flops, int64_t* items, int* rows_per_lane);
 int sr_tuning_info(sr_ctx* ctx, int* used_derived_columns, int64_t* exact_trees);
 /* The last sr_eval_loss_batch(_views)'s in-order loss fold (tuning "ref_fold"; each output may be NULL):
- * the path (0 none — "ref_fold" 0, negative weights, row blocks past "fold_seg_max", or a Float64 call
+ * the path (0 none — "ref_fold" 0, negative weights, a fold past "fold_rows_max", or a Float64 call
  * too large to keep its losses; 1 the loss launch kept every tree's losses; 2 the FOLD-mode pass re-ran the
  * complete trees), the trees whose loss is the walk's exact fold, those whose walk left the plan's
  * window and were folded through the prediction pass instead, and the fold launches' device time (ms,

@@ -620,8 +620,8 @@ __global__ void __launch_bounds__(256) sr_fold_plan_kernel(const double* __restr
   // A tree whose losses hardly vary — a huge constant tree, (c - y)^2 with |c| >> |y| — drifts from the
   // f64 prefix systematically: once the running value's ulp exceeds the losses' spread, every step
   // rounds the same way (up to ~1 % at 2^20 rows: C2's failed walks, round 6).  Its window is widened to
-  // 2^-5 when its full row blocks' sums agree to 2^-7 (a tree with varied losses: ~10 %; the last block
-  // may be shorter and is left out).
+  // n 2^-26 (at least 2^-5, at most 2^-2) when its full row blocks' sums agree to 2^-7 (a tree with
+  // varied losses: ~10 %; the last block may be shorter and is left out).
   if (ok && part && n_rb >= 3) {
     double mn = 1.7976931348623157e308, mx = 0.0;
     for (int rb = lane; rb < n_rb - 1; rb += 64) {
@@ -635,7 +635,11 @@ __global__ void __launch_bounds__(256) sr_fold_plan_kernel(const double* __restr
       mn = a < mn ? a : mn;
       mx = b > mx ? b : mx;
     }
-    if (mx <= mn * (1.0 + 0.0078125) && delta < 0.03125) delta = 0.03125;
+    // (the drift grows with the fold's length: ~1 % at 2^20 rows, ~8 % at 2^23)
+    const double wide = double(who.n_terms) * 1.4901161193847656e-08 < 0.03125 ? 0.03125
+                        : (double(who.n_terms) * 1.4901161193847656e-08 > 0.25 ? 0.25
+                                                                               : double(who.n_terms) * 1.4901161193847656e-08);
+    if (mx <= mn * (1.0 + 0.0078125) && delta < wide) delta = wide;
   }
   for (int c0 = 0; c0 < n_rb; c0 += 64) {
     const int rb = c0 + lane;

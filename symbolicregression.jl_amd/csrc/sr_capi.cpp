@@ -309,11 +309,12 @@ struct sr_ctx {
   // sum (Float64: within ~1e-13 of the fold, north_star's f64 bar is 1e-10).
   int ref_fold = 1;
   int64_t fold_store_mb = 512;
-  int64_t fold_slot_mb = 4096;
+  int64_t fold_slot_mb = 24576;  // (allocated as needed: ~24 slots per tree; C4's 2^26 rows take ~21 GB)
   // the plan's window: the fold within 2^-8 of the f64 prefix, else the tree fails (C2's trees: the fold is
   // within 2.1e-3 of the f64 sum at 2^20 rows; 2^-6 kept twice the slow segments)
   int fold_delta_log2 = 8;
   int64_t fold_seg_max = 16384;  // SR_AMD_FOLD_SEG_MAX: calls whose row blocks are longer keep the f64 sum
+  int64_t fold_rows_max = int64_t(1) << 24;  // SR_AMD_FOLD_ROWS_MAX: longer folds keep the f64 sum
   int fold_debug_fail = 0;   // (tests: "fold_debug_fail")
   int fold_walk_dbg = 0;     // SR_AMD_FOLD_WALK_DBG (analysis): 2 no O(1) slow blocks, 4 no serial start
   int fold_stats = 0;        // SR_AMD_FOLD_STATS=1: per-tree walk statistics to stderr after each call (analysis)
@@ -623,9 +624,19 @@ int run_batch(sr_ctx* ctx, const sr_dataset* ds, int opset_id, const sr_tree_bat
   const bool gather = row_idx != nullptr && n_idx > 0;
   // PRED passes (the fold's few band trees) write no partials: more row blocks fill the GPU (C4's 14 trees
   // x 2^26 rows ran 1,024 workgroups at 256)
-  const int mrb = mode == SR_MODE_PRED ? std::max(ctx->max_row_blocks, 4096) : ctx->max_row_blocks;
+  int mrb = mode == SR_MODE_PRED ? std::max(ctx->max_row_blocks, 4096) : ctx->max_row_blocks;
   const int64_t n_eval = gather ? n_idx : ds->n;
   if (n_eval <= 0) return set_error(SR_ERR_INVALID_ARG, "no rows to evaluate");
+  // under the in-order fold, row blocks of at most fold_seg_max rows on the largest shard (every rank
+  // the same count): a slow block's rows are kept whole (C4's 2^26 rows per GPU: 4,096 blocks of 16k)
+  if (mode == SR_MODE_LOSS && ctx->want_fold && ctx->ref_fold && sizeof(T) == 4 && ctx->fold_seg_max > 0 &&
+      (shard ? n_total : n_eval) <= ctx->fold_rows_max) {
+    int64_t max_rows = n_eval;
+    if (shard)
+      for (size_t r = 0; r + 1 < ds->shard_offs.size(); ++r) max_rows = std::max(max_rows, ds->shard_offs[r + 1] - ds->shard_offs[r]);
+    const int64_t need = (max_rows + ctx->fold_seg_max - 1) / ctx->fold_seg_max;
+    if (need > mrb) mrb = int(std::min<int64_t>(need, 16384));
+  }
   // several views: one launch, its tree groups view-pure (SrSegment); rows uploaded for every view
   const bool multi = views != nullptr && gather && mode == SR_MODE_LOSS;
   const int64_t n_rows_up = multi ? int64_t(views->n_views) * n_idx : n_idx;
@@ -748,14 +759,20 @@ int run_batch(sr_ctx* ctx, const sr_dataset* ds, int opset_id, const sr_tree_bat
     const bool f64_off = sizeof(T) == 8 && double(nt) * double(pos_rows) * double(max_shard) / double(n_eval) *
                                                double(sizeof(T)) > double(ctx->fold_store_mb) * 1048576.0;
     // segments (row blocks) past fold_seg_max rows on the largest shard: no fold (a slow segment's rows
-    // are kept whole: C4's 2^26 rows per GPU make 1 MiB segments, ~10 per complete tree).  Decided on the
-    // default grid, so that the max_row_blocks knob never changes a result.
+    // are kept whole).  The launch above already takes enough row blocks for fold_seg_max (up to 16,384
+    // blocks); decided on that grid whatever max_row_blocks says, so the knob never changes a result.
     int64_t rb_big = 0;
     {
-      const Grid gb = make_grid<T>(max_shard, nt, R, W, int(ds->nf), 1, 0, ds->w != nullptr, ctx->tree_group, 512);
+      const Grid gb = make_grid<T>(max_shard, nt, R, W, int(ds->nf), 1, 0, ds->w != nullptr, ctx->tree_group,
+                                   std::max<int64_t>(512, (max_shard + ctx->fold_seg_max - 1) / std::max<int64_t>(1, ctx->fold_seg_max)));
       rb_big = int64_t(gb.tiles) * 64 * R;
     }
-    if (f64_off || rb_big > ctx->fold_seg_max) {
+    // folds longer than fold_rows_max (2^24) keep the f64 sum: past ~2^23 rows the reference's Float32
+    // fold stalls (a loss below half an ulp of the running sum adds nothing; C4's 2^26 rows: up to 50 %
+    // below the exact mean) and drifts out of every window the f64 prefix gives the plan, so the walks
+    // fail and the fallback's prediction pass takes the call (C4 folded: 26.6k trees, 37.7 s a step)
+    const int64_t fold_len = shard ? n_total : n_eval;
+    if (f64_off || rb_big > ctx->fold_seg_max || fold_len > ctx->fold_rows_max) {
     } else if (double(nt) * double(pos_rows) * double(sizeof(T)) <= double(ctx->fold_store_mb) * 1048576.0) {
       fold_path = 1;
       SR_HIP_CHECK(ctx->fold_store.ensure(size_t(nt) * size_t(pos_rows) * sizeof(T)));
@@ -3534,6 +3551,7 @@ int sr_init(int device, sr_ctx** out) {
   if (const char* v = std::getenv("SR_AMD_FOLD_STATS")) ctx->fold_stats = std::atoi(v);
   if (const char* v = std::getenv("SR_AMD_FOLD_DELTA_LOG2")) ctx->fold_delta_log2 = std::max(1, std::min(40, std::atoi(v)));
   if (const char* v = std::getenv("SR_AMD_FOLD_SEG_MAX")) ctx->fold_seg_max = std::max<int64_t>(0, std::atoll(v));
+  if (const char* v = std::getenv("SR_AMD_FOLD_ROWS_MAX")) ctx->fold_rows_max = std::max<int64_t>(0, std::atoll(v));
   if (const char* v = std::getenv("SR_AMD_FOLD_WALK_DBG")) ctx->fold_walk_dbg = std::atoi(v) & 6;
   hipError_t e = hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking);
   if (e == hipSuccess && std::getenv("SR_AMD_EAGER_STREAM2")) e = ctx->need_stream2();  // (A/B: the round-4 layout)
@@ -4281,6 +4299,10 @@ int sr_set_tuning(sr_ctx* ctx, const char* name, int64_t value) {
   }
   if (std::strcmp(name, "fold_seg_max") == 0) {  // longest row block folded (SR_AMD_FOLD_SEG_MAX)
     ctx->fold_seg_max = value < 0 ? 0 : value;
+    return SR_OK;
+  }
+  if (std::strcmp(name, "fold_rows_max") == 0) {  // longest fold (SR_AMD_FOLD_ROWS_MAX)
+    ctx->fold_rows_max = value < 0 ? 0 : value;
     return SR_OK;
   }
   if (std::strcmp(name, "fold_seg") == 0) {  // rows per segment of the in-order loss fold (SR_AMD_FOLD_SEG)
