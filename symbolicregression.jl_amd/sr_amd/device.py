@@ -65,9 +65,10 @@ class DeviceContext:
     def set_tuning(self, name, value):
         """Run-time tuning knob (include/sr_amd.h lists them): "derived", "probe", "stress_probe",
         "code_cache", "timing", "rows_per_lane", "balance", "fused_reduce", "exact_w", "exact_g", "fold_seg",
-        "ref_fold" (the in-order loss fold: 1 default, 0 the f64 sums — the one knob results depend on),
-        "fold_store_mb", "fold_slot_mb", "fold_delta_log2"; tests: "inject_failure*", "debug_hint_regrow",
-        "fold_debug_fail"."""
+        "ref_fold" (the in-order loss fold: 1 default, 0 the f64 sums), "fold_seg_max" / "fold_rows_max"
+        (the longest row block / fold folded: past them a call keeps the f64 sums — these three are the
+        knobs results depend on), "fold_store_mb", "fold_slot_mb", "fold_delta_log2"; tests:
+        "inject_failure*", "debug_hint_regrow", "fold_debug_fail"."""
         _lib.check(_lib.lib.sr_set_tuning(self.handle, name.encode(), int(value)))
 
     def last_derived_columns(self):

@@ -159,3 +159,92 @@ def test_fold_vs_oracle_reference_accumulation():
     bad = np.nonzero(fin & ~(err <= tol))[0]
     assert bad.size == 0, [(int(k), float(loss[k]), float(ref[k]), float(tol[k])) for k in bad[:5]]
     assert float(np.mean(_bits(loss[fin]) == _bits(ref[fin]))) > 0.9
+
+
+def _fold_np(l, dtype):
+    f = dtype(l[0])
+    for v in l[1:]:
+        f = dtype(f + v)
+    return f
+
+
+@pytest.mark.parametrize("dtype", [np.float64, np.float32])
+@pytest.mark.parametrize("n", [100, 256, 257, 3001, 40_000])
+def test_short_views_and_the_serial_start(dtype, n):
+    """The walk folds the first 256 rows one by one in hardware adds, then row blocks: views shorter
+    than, equal to and just past that, a block wholly inside it (Float64 R4 tiles of 256 rows: round 6's
+    bug read the next block's rows from a stale pass), and two paths of blocks."""
+    from sr_amd import parse_expression
+
+    opts = Options(binary_operators=["+", "*", "-", "/"], unary_operators=["cos", "exp"])
+    rng = np.random.default_rng(n)
+    X = rng.standard_normal((3, n)).astype(dtype)
+    y = (X[0] * 2 + 0.1 * rng.standard_normal(n)).astype(dtype)
+    tb = flatten_trees([parse_expression(e, opts) for e in ("3.2 * x1", "x1 * x2", "(x1 - x3) * 0.7")], dtype)
+    loss, comp, info = _run(tb, Dataset(X, y), opts)
+    assert info["path"] == 1 and info["folded"] == 3 and info["fallback"] == 0, info
+    preds = [dtype(dtype(3.2) * X[0]), X[0] * X[1], (X[0] - X[2]) * dtype(0.7)]
+    for k, p in enumerate(preds):
+        d = (p - y).astype(dtype)
+        want = dtype(_fold_np((d * d).astype(dtype), dtype) / dtype(n))
+        assert loss[k] == want, (k, loss[k], want)
+
+
+def test_stored_path_folds_drifted_runs_row_by_row():
+    """With every loss kept (a small call), a run of blocks whose binade the plan mispredicted is folded
+    row by row on the spot: a window of 2^-30 around the f64 prefix (every run the fold drifts out of)
+    gives the default window's bits and no fallback."""
+    n = 40_000
+    X, y, _ = _data(n, seed=9)
+    opts = Options(**OPTS)
+    tb = flatten_trees(gen_random_population(600, opts, 5, max_size=30, seed=11), np.float32)
+    ds = Dataset(X, y)
+    l_s, c_s, i_s = _run(tb, ds, opts)
+    l_n, c_n, i_n = _run(tb, ds, opts, fold_delta_log2=30)
+    assert i_s["path"] == 1 and i_n["path"] == 1
+    assert i_n["fallback"] == 0 and i_n["folded"] == i_s["folded"], (i_s, i_n)
+    fin = c_s & np.isfinite(l_s)
+    assert np.array_equal(_bits(l_s[fin]), _bits(l_n[fin]))
+
+
+def test_constant_trees_fold_without_fallback_at_2p20_rows():
+    """Trees whose losses hardly vary ((c - y)^2 with a huge constant c) drift from the f64 prefix by up
+    to ~1 % at 2^20 rows (every step rounds the same way): the plan widens their window, and the
+    FOLD-mode path folds them with no fallback, bit for bit."""
+    from sr_amd import parse_expression
+
+    n = 1 << 20
+    X, y, _ = _data(n, seed=2)
+    opts = Options(**OPTS)
+    exprs = ["exp(exp(exp(1.0642476)))", "exp(exp(2.2194602))", "(exp(exp(1.8301688)) / 0.39640316)",
+             "exp(exp(2.477696)) + (x2 - cos(0.019))", "x1 + 3000.0", "(x2 * 0.001) + 77.5"]
+    tb = flatten_trees([parse_expression(e, opts) for e in exprs], np.float32)
+    ds = Dataset(X, y)
+    loss, comp, info = _run(tb, ds, opts, fold_store_mb=0)
+    assert info["path"] == 2 and info["fallback"] == 0 and info["folded"] == int(comp.sum()), info
+    pred, _ = eval_tree_array_batch(tb, ds, opts)
+    for k in range(tb.n_trees):
+        if comp[k]:
+            want = _np_fold_losses(pred[k], y)
+            assert _bits(loss[k]) == _bits(want), (exprs[k], loss[k], want)
+
+
+def test_fold_rows_max_keeps_the_f64_sum_past_it():
+    """Calls longer than fold_rows_max (2^24 rows by default: C4's 2^26-row Float32 fold stalls far below
+    the exact mean) keep the f64 sums; ref_fold_info says path 0."""
+    n = 20_000
+    X, y, _ = _data(n, seed=4)
+    opts = Options(**OPTS)
+    tb = flatten_trees(gen_random_population(200, opts, 5, max_size=20, seed=5), np.float32)
+    ds = Dataset(X, y)
+    l1, c1, i1 = _run(tb, ds, opts)
+    ctx = sr_amd.get_context()
+    try:
+        l0, c0, i0 = _run(tb, ds, opts, fold_rows_max=n - 1)
+    finally:
+        ctx.set_tuning("fold_rows_max", 1 << 24)
+    l2, c2, i2 = _run(tb, ds, opts, ref_fold=0)
+    assert i1["path"] == 1 and i0["path"] == 0
+    assert np.array_equal(c0, c1)
+    fin = c1 & np.isfinite(l1)
+    assert np.array_equal(_bits(l0[fin]), _bits(l2[fin]))  # exactly the ref_fold 0 results
