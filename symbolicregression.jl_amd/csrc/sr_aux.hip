@@ -617,6 +617,13 @@ __global__ void __launch_bounds__(256) sr_fold_plan_kernel(const double* __restr
   const uint32_t t = perm ? perm[p] : uint32_t(p);
   const bool ok = who.eligible<T>(t);
   double run = who.est ? who.est[t] : 0.0;  // (a row shard after the first: the shards before it)
+  // (any tree's fold drifts from the f64 prefix more the longer it is: ~2e-3 at most over C2's trees at
+  //  2^20 rows, 4x that at 2^22 — the 4-rank rehearsal's 243 fallbacks at 2^-8 — so the window is at least
+  //  n 2^-28: 2^-8 up to 2^20 rows, 2^-5 at 2^23)
+  {
+    const double len_w = double(who.n_terms) * 3.725290298461914e-09;
+    if (delta < len_w) delta = len_w < 0.0625 ? len_w : 0.0625;
+  }
   // A tree whose losses hardly vary — a huge constant tree, (c - y)^2 with |c| >> |y| — drifts from the
   // f64 prefix systematically: once the running value's ulp exceeds the losses' spread, every step
   // rounds the same way (up to ~1 % at 2^20 rows: C2's failed walks, round 6).  Its window is widened to
