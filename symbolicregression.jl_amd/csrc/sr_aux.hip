@@ -998,19 +998,28 @@ __global__ void __launch_bounds__(64) sr_fold_walk_kernel(SrFoldTabs ft, int np,
   } else if (c_first >= SR_FCODE_SLOT0 && n > 0) {  // Statistics.mean / Base.sum over a generator: the
     // first loss starts the fold; the first rows then go one by one, in the hardware's own adds (the
     // running value leaves a binade every few rows here: a round per crossing would cost ~1 us each)
+    // (through LDS: lane 0 reads its rows ahead of the adds, 8 at a time; a readlane per row costs
+    //  ~100 cycles of hazards, 11 us for 256 rows)
     const T* b = seg_base(c_first);
-    const int64_t ks = (rb_rows < n ? rb_rows : n) < 256 ? (rb_rows < n ? rb_rows : n) : 256;
-    T v[4];
+    const int ks = int((rb_rows < n ? rb_rows : n) < 256 ? (rb_rows < n ? rb_rows : n) : 256);
+    __shared__ T s_first[256];
 #pragma unroll
-    for (int j = 0; j < 4; ++j) v[j] = (4 * lane + j < ks) ? b[4 * lane + j] : T(0);
-    F = sr_fold_lane(v[0], 0);
-    for (int L = 0; L < 64 && 4 * L < ks; ++L) {
+    for (int j = 0; j < 4; ++j) s_first[4 * lane + j] = (4 * lane + j < ks) ? b[4 * lane + j] : T(0);
+    __syncthreads();
+    T f0 = T(0);
+    if (lane == 0) {
+      f0 = s_first[0];
+      int r = 1;
+      for (; r + 8 <= ks; r += 8) {
+        T u[8];
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const int r = 4 * L + j;
-        if (r >= 1 && r < ks) F = F + sr_fold_lane(v[j], L);
+        for (int j = 0; j < 8; ++j) u[j] = s_first[r + j];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) f0 = f0 + u[j];
       }
+      for (; r < ks; ++r) f0 = f0 + s_first[r];
     }
+    F = sr_fold_lane(f0, 0);
     k = ks;
   } else {
     fail = n > 0;  // (the plan keeps the first segment's losses)
