@@ -685,20 +685,21 @@ __global__ void __launch_bounds__(256) sr_fold_plan_kernel(const double* __restr
   }
 }
 
-// the ordered composition of a stored segment's steps under binade spacing 2^q (the whole workgroup;
-// thread 0 holds the result)
+// Small calls: the loss launch stored every position's losses ([position][pos_stride], pos_stride =
+// n_rb x rb_rows, so segment rb of position p is slot p n_rb + rb); one wave per (segment, position)
+// decides its code and composes a steps segment's pair in row order (a slow segment's under its lower
+// window binade and the next).  (One wave, no barriers: round 6 measured the 256-thread form at ~11 us
+// a search call, most of it barriers and idle waves for 512-row segments.)
 template <typename T, int R>
-__device__ typename SrFoldTab<T>::Pair sr_fold_stab_pair(const SrStoredRows<T>& rw, int64_t lo, int64_t hi, int q,
-                                                         int tid, typename SrFoldTab<T>::I (*s_v)[2]) {
+__device__ typename SrFoldTab<T>::Pair sr_fold_stab_pair_wave(const SrStoredRows<T>& rw, int64_t lo, int64_t hi, int q,
+                                                              int lane) {
   using I = typename SrFoldTab<T>::I;
   constexpr I CAP = I(1) << (SrFoldTraits<T>::mant + 3);
-  const int lane = tid & 63, wave = tid >> 6;
-  I ta0 = 0, ta1 = 0;  // the segment so far (thread 0)
-  for (int64_t base = lo; base < hi; base += 256 * R) {
+  I ta0 = 0, ta1 = 0;  // the segment so far (uniform)
+  for (int64_t base = lo; base < hi; base += 64 * R) {
     I a0 = 0, a1 = 0;
-    const int64_t r0 = base + int64_t(tid) * R;
     T ev[R];
-    rw.template rows_from<R>(r0, hi, ev);
+    rw.template rows_from<R>(base + int64_t(lane) * R, hi, ev);
 #pragma unroll
     for (int r = 0; r < R; ++r) {
       I m;
@@ -707,7 +708,7 @@ __device__ typename SrFoldTab<T>::Pair sr_fold_stab_pair(const SrStoredRows<T>& 
       sr_fold_add_i<I>(m, kind, CAP, a0, a1);
     }
 #pragma unroll
-    for (int off = 1; off < 64; off <<= 1) {  // ordered over the lanes, then the waves
+    for (int off = 1; off < 64; off <<= 1) {  // ordered over the lanes: lane 0 ends with the pass
       I o0 = __shfl_down(a0, off, 64), o1 = __shfl_down(a1, off, 64);
       if ((lane & (2 * off - 1)) == 0) {
         sr_fold_compose_i<I>(a0, a1, o0, o1, CAP);
@@ -715,41 +716,25 @@ __device__ typename SrFoldTab<T>::Pair sr_fold_stab_pair(const SrStoredRows<T>& 
         a1 = o1;
       }
     }
-    if (lane == 0) {
-      s_v[wave][0] = a0;
-      s_v[wave][1] = a1;
-    }
-    __syncthreads();
-    if (tid == 0) {
-      for (int v = 0; v < 4; ++v) {
-        I y0 = s_v[v][0], y1 = s_v[v][1];
-        sr_fold_compose_i<I>(ta0, ta1, y0, y1, CAP);
-        ta0 = y0;
-        ta1 = y1;
-      }
-    }
-    __syncthreads();
+    I y0 = sr_fold_lane(a0, 0), y1 = sr_fold_lane(a1, 0);
+    sr_fold_compose_i<I>(ta0, ta1, y0, y1, CAP);
+    ta0 = y0;
+    ta1 = y1;
   }
   return SrFoldTab<T>::pair(ta0, ta1);
 }
-
-// Small calls: the loss launch stored every position's losses ([position][pos_stride], pos_stride =
-// n_rb x rb_rows, so segment rb of position p is slot p n_rb + rb); one workgroup per (segment,
-// position) decides its code and composes a steps segment's pair in row order (a slow segment's under
-// its lower window binade and the next).
 template <typename T, int R>
-__global__ void __launch_bounds__(256) sr_fold_stab_kernel(const double* __restrict__ part, int np, int n_rb,
-                                                           int64_t rb_rows, int64_t n, const uint32_t* __restrict__ perm,
-                                                           SrFoldWho who, double delta, const T* __restrict__ losses,
-                                                           SrFoldTabs ft) {
-  using I = typename SrFoldTab<T>::I;
+__global__ void __launch_bounds__(64) sr_fold_stab_kernel(const double* __restrict__ part, int np, int n_rb,
+                                                          int64_t rb_rows, int64_t n, const uint32_t* __restrict__ perm,
+                                                          SrFoldWho who, double delta, const T* __restrict__ losses,
+                                                          SrFoldTabs ft) {
   using Pair = typename SrFoldTab<T>::Pair;
   int32_t* __restrict__ code = ft.code;
-  const int rb = int(blockIdx.x), p = int(blockIdx.y), tid = int(threadIdx.x), lane = tid & 63, wave = tid >> 6;
+  const int rb = int(blockIdx.x), p = int(blockIdx.y), lane = int(threadIdx.x);
   const uint32_t t = perm ? perm[p] : uint32_t(p);
   const size_t o = size_t(rb) * size_t(np) + size_t(p);
   if (!who.eligible<T>(t)) {
-    if (tid == 0) {
+    if (lane == 0) {
       code[o] = SR_FCODE_SKIP;
       ft.sq[o] = SR_FCODE_SKIP;
     }
@@ -757,21 +742,17 @@ __global__ void __launch_bounds__(256) sr_fold_stab_kernel(const double* __restr
   }
   const int32_t slow_code = SR_FCODE_SLOT0 + p * n_rb + rb;
   if (rb == 0 && who.first) {
-    if (tid == 0) {
+    if (lane == 0) {
       code[o] = slow_code;
       ft.sq[o] = SR_FCODE_SKIP;
     }
     return;
   }
-  __shared__ double s_d[4];
-  __shared__ I s_v[4][2];
   double pre = 0.0;
-  for (int i = tid; i < rb; i += 256) pre += part[size_t(i) * size_t(np) + size_t(p)];  // (rb > 0: part is set)
+  for (int i = lane; i < rb; i += 64) pre += part[size_t(i) * size_t(np) + size_t(p)];  // (rb > 0: part is set)
 #pragma unroll
   for (int off = 32; off >= 1; off >>= 1) pre += __shfl_xor(pre, off, 64);
-  if (lane == 0) s_d[wave] = pre;
-  __syncthreads();
-  const double sb = (who.est ? who.est[t] : 0.0) + ((s_d[0] + s_d[1]) + (s_d[2] + s_d[3]));
+  const double sb = (who.est ? who.est[t] : 0.0) + pre;  // (an estimate: it only chooses binades)
   const double sa = sb + (part ? part[o] : who.sums[t]);  // (one row block: the view's total)
   const int q = sr_fold_q<T>(sb * (1.0 - delta));
   const bool slow = q != sr_fold_q<T>(sa * (1.0 + delta));
@@ -779,11 +760,13 @@ __global__ void __launch_bounds__(256) sr_fold_stab_kernel(const double* __restr
   const SrStoredRows<T> rw{losses + (size_t(p) * size_t(n_rb) + size_t(rb)) * size_t(rb_rows), lo};
   // a steps segment's pair under q; a slow segment's under q and q + 1 (the walk uses them when the
   // running value stays in one binade there after all)
-  for (int v = 0; v < (slow ? 2 : 1); ++v) {
-    const Pair pr = sr_fold_stab_pair<T, R>(rw, lo, hi, q + v, tid, s_v);
-    if (tid == 0) (v == 0 ? static_cast<Pair*>(ft.tab) : static_cast<Pair*>(ft.tab2))[o] = pr;
+  const Pair pr = sr_fold_stab_pair_wave<T, R>(rw, lo, hi, q, lane);
+  if (lane == 0) static_cast<Pair*>(ft.tab)[o] = pr;
+  if (slow) {
+    const Pair pr2 = sr_fold_stab_pair_wave<T, R>(rw, lo, hi, q + 1, lane);
+    if (lane == 0) static_cast<Pair*>(ft.tab2)[o] = pr2;
   }
-  if (tid == 0) {
+  if (lane == 0) {
     code[o] = slow ? slow_code : q;
     ft.sq[o] = slow ? q : SR_FCODE_SKIP;
   }
@@ -1201,7 +1184,7 @@ template <typename T>
 hipError_t sr_launch_fold_stab(const double* part, int np, int n_rb, int64_t rb_rows, int64_t n, const uint32_t* perm,
                                const SrFoldWho& who, double delta, const T* losses, SrFoldTabs ft, hipStream_t s) {
   if (np <= 0 || n_rb <= 0) return hipSuccess;
-  hipLaunchKernelGGL((sr_fold_stab_kernel<T, 8>), dim3(unsigned(n_rb), unsigned(np)), dim3(256), 0, s, part, np, n_rb,
+  hipLaunchKernelGGL((sr_fold_stab_kernel<T, 8>), dim3(unsigned(n_rb), unsigned(np)), dim3(64), 0, s, part, np, n_rb,
                      rb_rows, n, perm, who, delta, losses, ft);
   return hipGetLastError();
 }
