@@ -238,8 +238,8 @@ struct SrFoldWho {
 // in the tile layout (chunk c of lane l = tile rows c*64*C + l*C + j, sr_tile_impl.h SrLane), rows past
 // the view already 0.  Returns the wave-uniform pair (from an even / an odd start).  Fast path: no loss
 // of the tile is an exact half ulp of the binade, so every step is rint(l 2^-q) whatever the parity and
-// the tile's step is their sum (Float32: each term clamped to 2^25, partial sums exact below 2^24 and
-// monotone above, so a sum that leaves the binade still reads as one); otherwise the ordered
+// the tile's step is their sum (partial sums of integers exact below 2^(mant+1) and monotone above, +Inf
+// included, so a sum that leaves the binade still reads as one); otherwise the ordered
 // composition, row by row in the lane, then over the lanes (lane order = row order in a chunk), then
 // over the chunks.
 template <typename T, int R, int C>
@@ -247,7 +247,6 @@ __device__ __forceinline__ void sr_fold_tile_step(const T (&l)[R], int q, int la
                                                   typename SrFoldTab<T>::I& t1) {
   using I = typename SrFoldTab<T>::I;
   constexpr I CAP = I(1) << (SrFoldTraits<T>::mant + 3);
-  constexpr T CLAMP = T(int64_t(1) << (SrFoldTraits<T>::mant + 2));
   T tsum = T(0), dmax = T(0);
 #pragma unroll
   for (int r = 0; r < R; ++r) {
@@ -255,8 +254,8 @@ __device__ __forceinline__ void sr_fold_tile_step(const T (&l)[R], int q, int la
     const T s = sizeof(T) == 4 ? T(rintf(float(v))) : T(rint(double(v)));
     const T d = v - s;
     const T ad = d < T(0) ? -d : d;
-    dmax = ad > dmax ? ad : dmax;  // (NaN: ignored; a NaN loss clamps below)
-    tsum += (s < CLAMP) ? s : CLAMP;
+    dmax = ad > dmax ? ad : dmax;  // (NaN — a step past the type's range, Inf - Inf — ignored)
+    tsum += s;  // (no clamp: a sum past 2^(mant+1) reads as CAP below whatever it is, +Inf included)
   }
   if (__builtin_amdgcn_ballot_w64(dmax == T(0.5)) == 0) {
     // wave sum of nonnegative integer values (lane 63's inclusive scan): exact below 2^(mant+1), and any
