@@ -943,7 +943,8 @@ __device__ T sr_fold_rows_wave(const T* __restrict__ base, int64_t lo, int64_t k
 // the caller's tree index): the fold's value before this view's first row (a row shard after the
 // first), or NULL: the first loss starts the fold.  out_val / out_st at the caller's tree index.
 template <typename T, int RW>
-__global__ void __launch_bounds__(64) sr_fold_walk_kernel(SrFoldTabs ft, int np, int n_rb, int64_t rb_rows, int64_t n,
+__global__ void __launch_bounds__(64) sr_fold_walk_kernel(SrFoldTabs ft, SrFoldWho who, int np, int n_rb,
+                                                           int64_t rb_rows, int64_t n,
                                                            const T* __restrict__ losses, int64_t slot_rows,
                                                            const uint32_t* __restrict__ perm,
                                                            const T* __restrict__ carry, T* __restrict__ out_val,
@@ -963,7 +964,10 @@ __global__ void __launch_bounds__(64) sr_fold_walk_kernel(SrFoldTabs ft, int np,
   const int p = int(blockIdx.x);  // (one wave per workgroup: a finished walk frees its slot at once)
   if (p >= np) return;  // wave-uniform
   const uint32_t t = perm ? perm[p] : uint32_t(p);
-  const int32_t c_first = code[p];
+  // (all_rows & 16: a call of one row block of at most 256 rows with its losses kept — the serial start
+  //  is the whole fold, and no pair kernel ran: eligibility from the call's flags, slot p)
+  const bool tiny = (all_rows & 16) != 0;
+  const int32_t c_first = tiny ? (who.eligible<T>(t) ? SR_FCODE_SLOT0 + p : SR_FCODE_SKIP) : code[p];
   if (c_first == SR_FCODE_SKIP) {
     if (lane == 0) out_st[t] = SR_FST_NONE;
     return;
@@ -1013,6 +1017,14 @@ __global__ void __launch_bounds__(64) sr_fold_walk_kernel(SrFoldTabs ft, int np,
   // the chunk's four arrays in one round trip (unconditional loads at a valid index, then selects: a
   // load under a branch on another load's value costs a second round trip), the next chunk's issued
   // at the start of this one
+  if (tiny) {  // (k == n: the serial start folded every row)
+    if (lane == 0) {
+      out_val[t] = F;
+      out_st[t] = fail ? SR_FST_FAIL : SR_FST_OK;
+      if (dbg) dbg[t] = make_int4(1000, 0, 0, int((wall_clock64() - clk0) / 100));
+    }
+    return;
+  }
   auto chunk_at = [&](int c) { return size_t(c + lane < n_rb ? c + lane : n_rb - 1) * size_t(np) + size_t(p); };
   size_t so_n = chunk_at(0);
   int32_t cd_n = code[so_n], sq_n = ft.sq[so_n];
@@ -1189,18 +1201,18 @@ hipError_t sr_launch_fold_stab(const double* part, int np, int n_rb, int64_t rb_
   return hipGetLastError();
 }
 template <typename T>
-hipError_t sr_launch_fold_walk(SrFoldTabs ft, int np, int n_rb, int64_t rb_rows, int64_t n, const T* losses,
-                               int64_t slot_rows, const uint32_t* perm, const T* carry, T* out_val, int32_t* out_st,
-                               void* dbg, int all_rows, hipStream_t s) {
+hipError_t sr_launch_fold_walk(SrFoldTabs ft, const SrFoldWho& who, int np, int n_rb, int64_t rb_rows, int64_t n,
+                               const T* losses, int64_t slot_rows, const uint32_t* perm, const T* carry, T* out_val,
+                               int32_t* out_st, void* dbg, int all_rows, hipStream_t s) {
   if (np <= 0) return hipSuccess;
   // (row blocks of at most 512 rows, e.g. the search's 100k-row calls: half-width passes, half the
   //  per-round work of a crossing block that a 1,024-row pass would spend on idle lanes)
   if (rb_rows <= 512)
-    hipLaunchKernelGGL((sr_fold_walk_kernel<T, sizeof(T) == 4 ? 8 : 4>), dim3(unsigned(np)), dim3(64), 0, s, ft, np,
+    hipLaunchKernelGGL((sr_fold_walk_kernel<T, sizeof(T) == 4 ? 8 : 4>), dim3(unsigned(np)), dim3(64), 0, s, ft, who, np,
                        n_rb, rb_rows, n, losses, slot_rows, perm, carry, out_val, out_st, static_cast<int4*>(dbg),
                        all_rows);
   else
-    hipLaunchKernelGGL((sr_fold_walk_kernel<T, sizeof(T) == 4 ? 16 : 8>), dim3(unsigned(np)), dim3(64), 0, s, ft,
+    hipLaunchKernelGGL((sr_fold_walk_kernel<T, sizeof(T) == 4 ? 16 : 8>), dim3(unsigned(np)), dim3(64), 0, s, ft, who,
                        np, n_rb, rb_rows, n, losses, slot_rows, perm, carry, out_val, out_st, static_cast<int4*>(dbg),
                        all_rows);
   return hipGetLastError();
@@ -1210,8 +1222,8 @@ hipError_t sr_launch_fold_walk(SrFoldTabs ft, int np, int n_rb, int64_t rb_rows,
                                              SrFoldTabs, int*, int, hipStream_t);                                      \
   template hipError_t sr_launch_fold_stab<T>(const double*, int, int, int64_t, int64_t, const uint32_t*,              \
                                              const SrFoldWho&, double, const T*, SrFoldTabs, hipStream_t);             \
-  template hipError_t sr_launch_fold_walk<T>(SrFoldTabs, int, int, int64_t, int64_t, const T*, int64_t,               \
-                                             const uint32_t*, const T*, T*, int32_t*, void*, int, hipStream_t);
+  template hipError_t sr_launch_fold_walk<T>(SrFoldTabs, const SrFoldWho&, int, int, int64_t, int64_t, const T*,      \
+                                             int64_t, const uint32_t*, const T*, T*, int32_t*, void*, int, hipStream_t);
 SR_INSTANTIATE_FOLD2(float)
 SR_INSTANTIATE_FOLD2(double)
 

@@ -557,6 +557,14 @@ SrFoldTabs fold_tabs(sr_ctx* ctx, size_t off) {
   return SrFoldTabs{ctx->fold_code.as<int32_t>() + off, ctx->fold_tab.as<char>() + off * sizeof(Pair),
                     ctx->fold_sq.as<int32_t>() + off, ctx->fold_tab2.as<char>() + off * sizeof(Pair)};
 }
+// A stored-loss call of one row block of at most 256 rows that starts the fold (C1's 100-row calls): the
+// walk's serial start folds every row and takes eligibility from the call's flags itself, so the pair
+// kernel's launch is skipped (round 6: ~5 us of a ~45 us call)
+template <typename T>
+bool fold_tiny(const FoldJob<T>& job, const FoldRegion<T>& fr, const SrFoldWho& who) {
+  return job.path == 1 && fr.g.n_row_blocks == 1 && job.n_eval <= 256 && who.first && who.elig == nullptr &&
+         who.est == nullptr;
+}
 // A region's steps: the stored-loss tables (path 1) or the plan and the FOLD pass (path 2).  who: the
 // call's whole-batch arrays (sums / flags / elig / est at the caller's tree index; this function adds
 // the region's chunk offset).
@@ -573,6 +581,7 @@ int fold_steps(sr_ctx* ctx, const FoldJob<T>& job, const FoldRegion<T>& fr, SrFo
   if (who.elig) who.elig += fr.t0;
   if (who.est) who.est += fr.t0;
   if (job.path == 1) {
+    if (fold_tiny(job, fr, who)) return SR_OK;  // (the walk's serial start is the whole fold: no pairs)
     SR_HIP_CHECK(sr_launch_fold_stab<T>(part, np, nrb, rb_rows, job.n_eval, fr.a.perm, who, job.delta, fr.a.fold_loss,
                                         ft, cs));
     return SR_OK;
@@ -598,22 +607,27 @@ int fold_steps(sr_ctx* ctx, const FoldJob<T>& job, const FoldRegion<T>& fr, SrFo
 // A region's walk: the folds' values and status at the caller's tree index (out arrays and carry are
 // whole-batch, tree-indexed).
 template <typename T>
-int fold_walk(sr_ctx* ctx, const FoldJob<T>& job, const FoldRegion<T>& fr, const T* carry, T* out_val, int32_t* out_st,
-              hipStream_t cs) {
+int fold_walk(sr_ctx* ctx, const FoldJob<T>& job, const FoldRegion<T>& fr, SrFoldWho who, const T* carry, T* out_val,
+              int32_t* out_st, hipStream_t cs) {
   const int nrb = fr.g.n_row_blocks;
+  const int tiny = carry == nullptr && fold_tiny(job, fr, who) ? 16 : 0;
+  if (who.sums) who.sums += fr.t0;
+  if (who.flags) who.flags += fr.t0;
+  if (who.elig) who.elig += fr.t0;
+  if (who.est) who.est += fr.t0;
   const int64_t rb_rows = int64_t(fr.g.tiles) * 64 * fr.Rc;
   const size_t off = size_t(job.n_rb) * size_t(fr.pos0);
   const SrFoldTabs ft = fold_tabs<T>(ctx, off);
   const T* losses = job.path == 1 ? fr.a.fold_loss : ctx->fold_store.as<T>();
   const int64_t slot_rows = job.path == 1 ? rb_rows : job.slot_rows;
   int4* dbg = ctx->fold_stats ? ctx->fold_dbg.as<int4>() + fr.t0 : nullptr;  // (SR_AMD_FOLD_STATS)
-  SR_HIP_CHECK(sr_launch_fold_walk<T>(ft, int(fr.np), nrb, rb_rows, job.n_eval, losses, slot_rows, fr.a.perm,
+  SR_HIP_CHECK(sr_launch_fold_walk<T>(ft, who, int(fr.np), nrb, rb_rows, job.n_eval, losses, slot_rows, fr.a.perm,
                                       carry ? carry + fr.t0 : nullptr, out_val + fr.t0, out_st + fr.t0, dbg,
-                                      int(job.path == 1) | ctx->fold_walk_dbg, cs));
+                                      int(job.path == 1) | tiny | ctx->fold_walk_dbg, cs));
   if (ctx->fold_stats == 2)  // (analysis: the same walk again, its loads now warm: the statistics are the second's)
-    SR_HIP_CHECK(sr_launch_fold_walk<T>(ft, int(fr.np), nrb, rb_rows, job.n_eval, losses, slot_rows, fr.a.perm,
+    SR_HIP_CHECK(sr_launch_fold_walk<T>(ft, who, int(fr.np), nrb, rb_rows, job.n_eval, losses, slot_rows, fr.a.perm,
                                         carry ? carry + fr.t0 : nullptr, out_val + fr.t0, out_st + fr.t0, dbg,
-                                      int(job.path == 1) | ctx->fold_walk_dbg, cs));
+                                        int(job.path == 1) | tiny | ctx->fold_walk_dbg, cs));
   return SR_OK;
 }
 
@@ -1316,7 +1330,7 @@ int run_batch(sr_ctx* ctx, const sr_dataset* ds, int opset_id, const sr_tree_bat
       const SrFoldWho who{ctx->d_out_sum, ctx->d_out_flag, fold_n_terms, nullptr, nullptr, 1};
       for (const FoldRegion<T>& fr : fjob.regions) {
         int frc = fold_steps<T>(ctx, fjob, fr, who, cs);
-        if (frc == SR_OK) frc = fold_walk<T>(ctx, fjob, fr, nullptr, d_fval, d_fst, cs);
+        if (frc == SR_OK) frc = fold_walk<T>(ctx, fjob, fr, who, nullptr, d_fval, d_fst, cs);
         if (frc != SR_OK) {
           sync_both();
           return frc;
@@ -3180,7 +3194,7 @@ int fold_all_sharded(sr_ctx* ctx, int64_t nt, const uint8_t* out_complete, const
     if (me == r && step == SR_OK && pending == SR_OK) {
       if (r > 0) hip_step(hipMemcpyAsync(d_carry, carry.data(), size_t(nt) * sizeof(T), hipMemcpyHostToDevice, s), "carry upload");
       for (const FoldRegion<T>& fr : job->regions)
-        if (step == SR_OK) step = fold_walk<T>(ctx, *job, fr, r > 0 ? d_carry : nullptr, d_fval, d_fst, s);
+        if (step == SR_OK) step = fold_walk<T>(ctx, *job, fr, who, r > 0 ? d_carry : nullptr, d_fval, d_fst, s);
       hip_step(hipMemcpyAsync(payload.data(), d_fval, size_t(nt) * sizeof(T), hipMemcpyDeviceToHost, s), "walk copy");
       hip_step(hipMemcpyAsync(payload.data() + size_t(nt) * sizeof(T), d_fst, size_t(nt) * sizeof(int32_t),
                               hipMemcpyDeviceToHost, s), "walk copy");

@@ -313,9 +313,9 @@ template <typename T>
 hipError_t sr_launch_fold_stab(const double* part, int np, int n_rb, int64_t rb_rows, int64_t n, const uint32_t* perm,
                                const SrFoldWho& who, double delta, const T* losses, SrFoldTabs ft, hipStream_t s);
 template <typename T>
-hipError_t sr_launch_fold_walk(SrFoldTabs ft, int np, int n_rb, int64_t rb_rows, int64_t n, const T* losses,
-                               int64_t slot_rows, const uint32_t* perm, const T* carry, T* out_val, int32_t* out_st,
-                               void* dbg, int all_rows, hipStream_t s);
+hipError_t sr_launch_fold_walk(SrFoldTabs ft, const SrFoldWho& who, int np, int n_rb, int64_t rb_rows, int64_t n,
+                               const T* losses, int64_t slot_rows, const uint32_t* perm, const T* carry, T* out_val,
+                               int32_t* out_st, void* dbg, int all_rows, hipStream_t s);
 template <typename T>
 hipError_t sr_launch_fold(const T* pred, int64_t pred_ld, int n_trees, const T* y, const T* w, const int64_t* row_idx,
                           int64_t n, int loss_kind, T loss_param, int64_t seg_len, const int2* tq, const int64_t* tab,

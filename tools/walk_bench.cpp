@@ -16,10 +16,18 @@ struct SrFoldTabs {
   int32_t* sq;
   void* tab2;
 };
+struct SrFoldWho {  // (layout of csrc/sr_fold_dev.h's)
+  const double* sums;
+  const uint32_t* flags;
+  int64_t n_terms;
+  const uint8_t* elig;
+  const double* est;
+  int first;
+};
 template <typename T>
-hipError_t sr_launch_fold_walk(SrFoldTabs ft, int np, int n_rb, int64_t rb_rows, int64_t n, const T* losses,
-                               int64_t slot_rows, const uint32_t* perm, const T* carry, T* out_val, int32_t* out_st,
-                               void* dbg, int all_rows, hipStream_t s);
+hipError_t sr_launch_fold_walk(SrFoldTabs ft, const SrFoldWho& who, int np, int n_rb, int64_t rb_rows, int64_t n,
+                               const T* losses, int64_t slot_rows, const uint32_t* perm, const T* carry, T* out_val,
+                               int32_t* out_st, void* dbg, int all_rows, hipStream_t s);
 
 #define CK(x)                                                             \
   do {                                                                    \
@@ -65,7 +73,7 @@ int main(int argc, char** argv) {
   CK(hipEventCreate(&e1));
   for (int rep = 0; rep < 3; ++rep) {
     CK(hipEventRecord(e0, 0));
-    CK(sr_launch_fold_walk<float>(ft, np, n_rb, rb_rows, n, d_loss, rb_rows, nullptr, nullptr, d_val, d_st, d_dbg, 1, 0));
+    CK(sr_launch_fold_walk<float>(ft, SrFoldWho{nullptr, nullptr, n, nullptr, nullptr, 1}, np, n_rb, rb_rows, n, d_loss, rb_rows, nullptr, nullptr, d_val, d_st, d_dbg, 1, 0));
     CK(hipEventRecord(e1, 0));
     CK(hipEventSynchronize(e1));
     float ms = 0;
