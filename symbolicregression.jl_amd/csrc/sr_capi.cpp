@@ -823,8 +823,10 @@ int run_batch(sr_ctx* ctx, const sr_dataset* ds, int opset_id, const sr_tree_bat
   SR_HIP_CHECK(ctx->outs.ensure(outs_bytes));
   // latency path (see host_io): results written to pinned host memory, programs read from it
   const bool small_call = n_chunks == 1 && mode == SR_MODE_LOSS;
-  // (under the in-order fold the plan reads the call's flags and partials on the device)
-  const bool host_out = small_call && ctx->host_io >= 1 && ctx->want_host_out && fold_path == 0;
+  // (under the in-order fold the plan reads the call's flags and partials on the device; a stored-loss
+  // fold of one row block of <= 256 rows — fold_tiny, the walk alone — reads and writes pinned memory)
+  const bool fold_small = fold_path == 1 && n_rb == 1 && n_eval <= 256;
+  const bool host_out = small_call && ctx->host_io >= 1 && ctx->want_host_out && (fold_path == 0 || fold_small);
   if (host_out) SR_HIP_CHECK(ctx->h_outs.ensure(outs_bytes, s, ctx->stream2));
   ctx->outs_on_host = host_out;
   const bool host_red = host_out && ctx->host_reduce > 0 && !multi && n_rb > 1 && int64_t(n_part) <= ctx->host_reduce;
@@ -972,8 +974,9 @@ int run_batch(sr_ctx* ctx, const sr_dataset* ds, int opset_id, const sr_tree_bat
                                                                              (size_t(fold_slot_rows) * sizeof(T)))))
                                  : 0;
   size_t fold_store_at = 0;  // (stored losses: the regions one after another, [position][n_rb x rb rows])
-  T* const d_fval = reinterpret_cast<T*>(ctx->outs.as<char>() + ctx->outs_fval_off);
-  int32_t* const d_fst = reinterpret_cast<int32_t*>(ctx->outs.as<char>() + ctx->outs_fst_off);
+  char* const outs_base = host_out ? ctx->h_outs.as<char>() : ctx->outs.as<char>();
+  T* const d_fval = reinterpret_cast<T*>(outs_base + ctx->outs_fval_off);
+  int32_t* const d_fst = reinterpret_cast<int32_t*>(outs_base + ctx->outs_fst_off);
   uint32_t code_base = 0;
   static const bool phase_debug = std::getenv("SR_AMD_PHASE_DEBUG") != nullptr;  // (latency analysis)
   const auto t_pre = std::chrono::steady_clock::now();
