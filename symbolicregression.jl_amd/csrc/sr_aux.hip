@@ -964,6 +964,10 @@ __global__ void __launch_bounds__(64) sr_fold_walk_kernel(SrFoldTabs ft, SrFoldW
   const int p = int(blockIdx.x);  // (one wave per workgroup: a finished walk frees its slot at once)
   if (p >= np) return;  // wave-uniform
   const uint32_t t = perm ? perm[p] : uint32_t(p);
+  if (who.msum && lane == 0) {  // (every position of the call has its walk workgroup, skipped trees too)
+    who.msum[t] = who.sums[t];
+    who.mflag[t] = who.flags[t];
+  }
   // (all_rows & 16: a call of one row block of at most 256 rows with its losses kept — the serial start
   //  is the whole fold, and no pair kernel ran: eligibility from the call's flags, slot p)
   const bool tiny = (all_rows & 16) != 0;

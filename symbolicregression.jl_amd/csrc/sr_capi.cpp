@@ -615,6 +615,8 @@ int fold_walk(sr_ctx* ctx, const FoldJob<T>& job, const FoldRegion<T>& fr, SrFol
   if (who.flags) who.flags += fr.t0;
   if (who.elig) who.elig += fr.t0;
   if (who.est) who.est += fr.t0;
+  if (who.msum) who.msum += fr.t0;
+  if (who.mflag) who.mflag += fr.t0;
   const int64_t rb_rows = int64_t(fr.g.tiles) * 64 * fr.Rc;
   const size_t off = size_t(job.n_rb) * size_t(fr.pos0);
   const SrFoldTabs ft = fold_tabs<T>(ctx, off);
@@ -827,8 +829,12 @@ int run_batch(sr_ctx* ctx, const sr_dataset* ds, int opset_id, const sr_tree_bat
   // fold of one row block of <= 256 rows — fold_tiny, the walk alone — reads and writes pinned memory)
   const bool fold_small = fold_path == 1 && n_rb == 1 && n_eval <= 256;
   const bool host_out = small_call && ctx->host_io >= 1 && ctx->want_host_out && (fold_path == 0 || fold_small);
-  if (host_out) SR_HIP_CHECK(ctx->h_outs.ensure(outs_bytes, s, ctx->stream2));
-  ctx->outs_on_host = host_out;
+  // (other stored-loss folds of a small call: Σ and flags stay on the device for the pair kernel, and the
+  //  walk copies them to pinned memory beside the fold's values — no copy back, SrFoldWho::msum)
+  const bool fold_mirror = small_call && ctx->host_io >= 1 && ctx->want_host_out && fold_path == 1 && !fold_small &&
+                           !shard;
+  if (host_out || fold_mirror) SR_HIP_CHECK(ctx->h_outs.ensure(outs_bytes, s, ctx->stream2));
+  ctx->outs_on_host = host_out || fold_mirror;
   const bool host_red = host_out && ctx->host_reduce > 0 && !multi && n_rb > 1 && int64_t(n_part) <= ctx->host_reduce;
   ctx->host_reductions.clear();
   ctx->host_red_rb = n_rb;
@@ -974,7 +980,7 @@ int run_batch(sr_ctx* ctx, const sr_dataset* ds, int opset_id, const sr_tree_bat
                                                                              (size_t(fold_slot_rows) * sizeof(T)))))
                                  : 0;
   size_t fold_store_at = 0;  // (stored losses: the regions one after another, [position][n_rb x rb rows])
-  char* const outs_base = host_out ? ctx->h_outs.as<char>() : ctx->outs.as<char>();
+  char* const outs_base = (host_out || fold_mirror) ? ctx->h_outs.as<char>() : ctx->outs.as<char>();
   T* const d_fval = reinterpret_cast<T*>(outs_base + ctx->outs_fval_off);
   int32_t* const d_fst = reinterpret_cast<int32_t*>(outs_base + ctx->outs_fst_off);
   uint32_t code_base = 0;
@@ -1330,7 +1336,11 @@ int run_batch(sr_ctx* ctx, const sr_dataset* ds, int opset_id, const sr_tree_bat
       // the in-order fold of this chunk's complete trees (sr_aux.hip): the launches' partials and flags
       // are final here (reduce / direct write / in-launch reduction ran on this stream)
       if (ctx->timed_last) SR_HIP_CHECK(hipEventRecord(ctx->ev_fc0[c], cs));
-      const SrFoldWho who{ctx->d_out_sum, ctx->d_out_flag, fold_n_terms, nullptr, nullptr, 1};
+      SrFoldWho who{ctx->d_out_sum, ctx->d_out_flag, fold_n_terms, nullptr, nullptr, 1};
+      if (fold_mirror) {
+        who.msum = ctx->h_outs.as<double>();
+        who.mflag = reinterpret_cast<uint32_t*>(ctx->h_outs.as<char>() + ctx->outs_flag_off);
+      }
       for (const FoldRegion<T>& fr : fjob.regions) {
         int frc = fold_steps<T>(ctx, fjob, fr, who, cs);
         if (frc == SR_OK) frc = fold_walk<T>(ctx, fjob, fr, who, nullptr, d_fval, d_fst, cs);

@@ -228,6 +228,10 @@ struct SrFoldWho {
   const uint8_t* elig;
   const double* est;
   int first;
+  // (a small stored-loss call's results in pinned memory: the walk copies each tree's Σ and flags there
+  //  beside its value, so the call needs no copy back; nullptr: none)
+  double* msum = nullptr;
+  uint32_t* mflag = nullptr;
   template <typename T>
   __device__ __forceinline__ bool eligible(uint32_t t) const {
     return elig ? elig[t] != 0 : sr_fold_eligible<T>(sums[t], flags[t], n_terms);

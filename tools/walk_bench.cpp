@@ -23,6 +23,8 @@ struct SrFoldWho {  // (layout of csrc/sr_fold_dev.h's)
   const uint8_t* elig;
   const double* est;
   int first;
+  double* msum = nullptr;
+  uint32_t* mflag = nullptr;
 };
 template <typename T>
 hipError_t sr_launch_fold_walk(SrFoldTabs ft, const SrFoldWho& who, int np, int n_rb, int64_t rb_rows, int64_t n,
