@@ -727,13 +727,41 @@ template <typename T, int R>
 __global__ void __launch_bounds__(64) sr_fold_stab_kernel(const double* __restrict__ part, int np, int n_rb,
                                                           int64_t rb_rows, int64_t n, const uint32_t* __restrict__ perm,
                                                           SrFoldWho who, double delta, const T* __restrict__ losses,
-                                                          SrFoldTabs ft) {
+                                                          SrFoldTabs ft, const uint32_t* __restrict__ part_flag,
+                                                          const uint8_t* __restrict__ static_bad,
+                                                          double* __restrict__ red_sum, uint32_t* __restrict__ red_flag) {
   using Pair = typename SrFoldTab<T>::Pair;
   int32_t* __restrict__ code = ft.code;
   const int rb = int(blockIdx.x), p = int(blockIdx.y), lane = int(threadIdx.x);
   const uint32_t t = perm ? perm[p] : uint32_t(p);
   const size_t o = size_t(rb) * size_t(np) + size_t(p);
-  if (!who.eligible<T>(t)) {
+  bool elig;
+  if (red_sum) {
+    // the call's reduce, here instead of its own launch: every wave of the tree folds the partials with
+    // the reduce launch's arithmetic (sr_reduce_positions: lane-strided in order, then the xor
+    // butterfly), so all agree bit for bit; the first segment's wave writes the tree's Σ and flags
+    double S = 0.0;
+    uint32_t fl = 0u;
+    for (int i = lane; i < n_rb; i += 64) {
+      const size_t oi = size_t(i) * size_t(np) + size_t(p);
+      S += part[oi];
+      fl |= part_flag[oi];
+    }
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) {
+      S += __shfl_xor(S, off, 64);
+      fl |= __shfl_xor(fl, off, 64);
+    }
+    if (static_bad && static_bad[t]) fl |= SR_FLAG_STATIC | SR_FLAG_NONFINITE;
+    if (rb == 0 && lane == 0) {
+      red_sum[t] = S;
+      red_flag[t] = fl;
+    }
+    elig = sr_fold_eligible<T>(S, fl, who.n_terms);
+  } else {
+    elig = who.eligible<T>(t);
+  }
+  if (!elig) {
     if (lane == 0) {
       code[o] = SR_FCODE_SKIP;
       ft.sq[o] = SR_FCODE_SKIP;
@@ -753,7 +781,7 @@ __global__ void __launch_bounds__(64) sr_fold_stab_kernel(const double* __restri
 #pragma unroll
   for (int off = 32; off >= 1; off >>= 1) pre += __shfl_xor(pre, off, 64);
   const double sb = (who.est ? who.est[t] : 0.0) + pre;  // (an estimate: it only chooses binades)
-  const double sa = sb + (part ? part[o] : who.sums[t]);  // (one row block: the view's total)
+  const double sa = sb + (part ? part[o] : who.sums[t]);  // (one row block: the view's total; no fused reduce)
   const int q = sr_fold_q<T>(sb * (1.0 - delta));
   const bool slow = q != sr_fold_q<T>(sa * (1.0 + delta));
   const int64_t lo = int64_t(rb) * rb_rows, hi = lo + rb_rows < n ? lo + rb_rows : n;
@@ -1198,10 +1226,13 @@ hipError_t sr_launch_fold_plan(const double* part, int np, int n_rb, const uint3
 }
 template <typename T>
 hipError_t sr_launch_fold_stab(const double* part, int np, int n_rb, int64_t rb_rows, int64_t n, const uint32_t* perm,
-                               const SrFoldWho& who, double delta, const T* losses, SrFoldTabs ft, hipStream_t s) {
+                               const SrFoldWho& who, double delta, const T* losses, SrFoldTabs ft,
+                               const uint32_t* part_flag, const uint8_t* static_bad, double* red_sum,
+                               uint32_t* red_flag, hipStream_t s) {
   if (np <= 0 || n_rb <= 0) return hipSuccess;
+  if (red_sum && (part == nullptr || part_flag == nullptr || red_flag == nullptr)) return hipErrorInvalidValue;
   hipLaunchKernelGGL((sr_fold_stab_kernel<T, 8>), dim3(unsigned(n_rb), unsigned(np)), dim3(64), 0, s, part, np, n_rb,
-                     rb_rows, n, perm, who, delta, losses, ft);
+                     rb_rows, n, perm, who, delta, losses, ft, part_flag, static_bad, red_sum, red_flag);
   return hipGetLastError();
 }
 template <typename T>
@@ -1225,7 +1256,8 @@ hipError_t sr_launch_fold_walk(SrFoldTabs ft, const SrFoldWho& who, int np, int 
   template hipError_t sr_launch_fold_plan<T>(const double*, int, int, const uint32_t*, const SrFoldWho&, double,   \
                                              SrFoldTabs, int*, int, hipStream_t);                                      \
   template hipError_t sr_launch_fold_stab<T>(const double*, int, int, int64_t, int64_t, const uint32_t*,              \
-                                             const SrFoldWho&, double, const T*, SrFoldTabs, hipStream_t);             \
+                                             const SrFoldWho&, double, const T*, SrFoldTabs, const uint32_t*,          \
+                                             const uint8_t*, double*, uint32_t*, hipStream_t);                         \
   template hipError_t sr_launch_fold_walk<T>(SrFoldTabs, const SrFoldWho&, int, int, int64_t, int64_t, const T*,      \
                                              int64_t, const uint32_t*, const T*, T*, int32_t*, void*, int, hipStream_t);
 SR_INSTANTIATE_FOLD2(float)

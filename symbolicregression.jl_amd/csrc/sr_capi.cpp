@@ -316,6 +316,7 @@ struct sr_ctx {
   int64_t fold_seg_max = 16384;  // SR_AMD_FOLD_SEG_MAX: calls whose row blocks are longer keep the f64 sum
   int64_t fold_rows_max = int64_t(1) << 24;  // SR_AMD_FOLD_ROWS_MAX: longer folds keep the f64 sum
   int fold_debug_fail = 0;   // (tests: "fold_debug_fail")
+  int fold_reduce = 1;       // SR_AMD_FOLD_REDUCE: stored-loss folds reduce in the pair kernel (0: a reduce launch)
   int fold_walk_dbg = 0;     // SR_AMD_FOLD_WALK_DBG (analysis): 2 no O(1) slow blocks, 4 no serial start
   int fold_stats = 0;        // SR_AMD_FOLD_STATS=1: per-tree walk statistics to stderr after each call (analysis)
   DevBuf fold_dbg;
@@ -548,6 +549,7 @@ struct FoldJob {
   int64_t n_eval = 0, n_rb = 0, slot_rows = 0, n_terms = 0;
   int slot_cap = 0;
   double delta = 0.0;
+  bool fuse_reduce = false;  // (stored losses, one GPU: the pair kernel does the call's reduce)
 };
 
 // a region's plan arrays at partial-buffer offset off
@@ -582,8 +584,11 @@ int fold_steps(sr_ctx* ctx, const FoldJob<T>& job, const FoldRegion<T>& fr, SrFo
   if (who.est) who.est += fr.t0;
   if (job.path == 1) {
     if (fold_tiny(job, fr, who)) return SR_OK;  // (the walk's serial start is the whole fold: no pairs)
+    const bool fr_red = job.fuse_reduce && nrb > 1;
     SR_HIP_CHECK(sr_launch_fold_stab<T>(part, np, nrb, rb_rows, job.n_eval, fr.a.perm, who, job.delta, fr.a.fold_loss,
-                                        ft, cs));
+                                        ft, fr_red ? fr.a.part_flag : nullptr, fr_red ? ctx->d_bad + fr.t0 : nullptr,
+                                        fr_red ? ctx->d_out_sum + fr.t0 : nullptr,
+                                        fr_red ? ctx->d_out_flag + fr.t0 : nullptr, cs));
     return SR_OK;
   }
   SR_HIP_CHECK(sr_launch_fold_plan<T>(part, np, nrb, fr.a.perm, who, job.delta, ft, ctx->fold_ctl.as<int>(),
@@ -976,6 +981,9 @@ int run_batch(sr_ctx* ctx, const sr_dataset* ds, int opset_id, const sr_tree_bat
   fjob.slot_rows = fold_slot_rows;
   fjob.n_terms = fold_n_terms;
   fjob.delta = std::ldexp(1.0, -ctx->fold_delta_log2);
+  // stored losses on one GPU: the pair kernel reduces the partials itself (one launch fewer a call;
+  // SR_AMD_FOLD_REDUCE=0: the reduce launch)
+  fjob.fuse_reduce = fold_path == 1 && !shard && mode == SR_MODE_LOSS && ctx->fold_reduce;
   fjob.slot_cap = fold_path == 2 ? int(std::min<int64_t>(INT_MAX / 2, int64_t(ctx->fold_store.cap /
                                                                              (size_t(fold_slot_rows) * sizeof(T)))))
                                  : 0;
@@ -1319,7 +1327,7 @@ int run_batch(sr_ctx* ctx, const sr_dataset* ds, int opset_id, const sr_tree_bat
       if (fold_path) fjob.regions.push_back({a, t0, t0 + p0, np, n_blocks, Rc, vstk, g});
       if (!direct && !fused && host_red)
         ctx->host_reductions.push_back({t0 + p0, np, g.n_row_blocks});
-      else if (!direct && !fused)
+      else if (!direct && !fused && !fjob.fuse_reduce)
         SR_HIP_CHECK(sr_launch_reduce(a.part_sum, a.part_flag, int(np), g.n_row_blocks, a.perm,
                                     ctx->d_bad + t0, ctx->d_out_sum + t0, ctx->d_out_flag + t0, cs));
       return SR_OK;
@@ -3580,6 +3588,7 @@ int sr_init(int device, sr_ctx** out) {
   if (const char* v = std::getenv("SR_AMD_FOLD_SEG_MAX")) ctx->fold_seg_max = std::max<int64_t>(0, std::atoll(v));
   if (const char* v = std::getenv("SR_AMD_FOLD_ROWS_MAX")) ctx->fold_rows_max = std::max<int64_t>(0, std::atoll(v));
   if (const char* v = std::getenv("SR_AMD_FOLD_WALK_DBG")) ctx->fold_walk_dbg = std::atoi(v) & 6;
+  if (const char* v = std::getenv("SR_AMD_FOLD_REDUCE")) ctx->fold_reduce = std::atoi(v) != 0 ? 1 : 0;
   hipError_t e = hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking);
   if (e == hipSuccess && std::getenv("SR_AMD_EAGER_STREAM2")) e = ctx->need_stream2();  // (A/B: the round-4 layout)
   if (e == hipSuccess) e = hipEventCreateWithFlags(&ctx->ev_join, hipEventDisableTiming);

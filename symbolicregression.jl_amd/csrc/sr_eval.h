@@ -311,7 +311,9 @@ hipError_t sr_launch_fold_plan(const double* part, int np, int n_rb, const uint3
                                double delta, SrFoldTabs ft, int* slot_next, int slot_cap, hipStream_t s);
 template <typename T>
 hipError_t sr_launch_fold_stab(const double* part, int np, int n_rb, int64_t rb_rows, int64_t n, const uint32_t* perm,
-                               const SrFoldWho& who, double delta, const T* losses, SrFoldTabs ft, hipStream_t s);
+                               const SrFoldWho& who, double delta, const T* losses, SrFoldTabs ft,
+                               const uint32_t* part_flag, const uint8_t* static_bad, double* red_sum,
+                               uint32_t* red_flag, hipStream_t s);
 template <typename T>
 hipError_t sr_launch_fold_walk(SrFoldTabs ft, const SrFoldWho& who, int np, int n_rb, int64_t rb_rows, int64_t n,
                                const T* losses, int64_t slot_rows, const uint32_t* perm, const T* carry, T* out_val,
