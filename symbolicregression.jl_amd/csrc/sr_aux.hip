@@ -685,6 +685,39 @@ __global__ void __launch_bounds__(256) sr_fold_plan_kernel(const double* __restr
   }
 }
 
+// The fold's first rows one by one (Statistics.mean / Base.sum over a generator: the first loss starts
+// the fold), in the hardware's own adds — the running value leaves a binade every few rows here, so a
+// round per crossing would cost ~1 us each.  Rows [0, ks), ks <= 256, of a stored segment b; one wave
+// (64 lanes): through LDS, lane 0 reads its rows ahead of the adds, 8 at a time (a readlane per row
+// costs ~100 cycles of hazards, 11 us for 256 rows).  Wave-uniform result.  The walk's serial start
+// and, for stored-loss calls, the pair kernel's first-segment wave (off the walk's critical path).
+template <typename T>
+__device__ __forceinline__ T sr_fold_serial_start(const T* __restrict__ b, int ks, int lane) {
+  __shared__ T s_first[256];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) s_first[4 * lane + j] = (4 * lane + j < ks) ? b[4 * lane + j] : T(0);
+  __syncthreads();
+  T f0 = T(0);
+  if (lane == 0) {
+    f0 = s_first[0];
+    int r = 1;
+    for (; r + 8 <= ks; r += 8) {
+      T u[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) u[j] = s_first[r + j];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) f0 = f0 + u[j];
+    }
+    for (; r < ks; ++r) f0 = f0 + s_first[r];
+  }
+  return sr_fold_lane(f0, 0);
+}
+template <typename T>
+__device__ __forceinline__ int sr_fold_serial_rows(int64_t rb_rows, int64_t n) {
+  const int64_t m = rb_rows < n ? rb_rows : n;
+  return int(m < 256 ? m : 256);
+}
+
 // Small calls: the loss launch stored every position's losses ([position][pos_stride], pos_stride =
 // n_rb x rb_rows, so segment rb of position p is slot p n_rb + rb); one wave per (segment, position)
 // decides its code and composes a steps segment's pair in row order (a slow segment's under its lower
@@ -770,9 +803,15 @@ __global__ void __launch_bounds__(64) sr_fold_stab_kernel(const double* __restri
   }
   const int32_t slow_code = SR_FCODE_SLOT0 + p * n_rb + rb;
   if (rb == 0 && who.first) {
+    // the fold's start: its first rows one by one, here (the walk reads the value from the segment's
+    // pair slot, so its critical path skips them)
+    const T f0 = n > 0 ? sr_fold_serial_start<T>(losses + size_t(p) * size_t(n_rb) * size_t(rb_rows),
+                                                 sr_fold_serial_rows<T>(rb_rows, n), lane)
+                       : T(0);
     if (lane == 0) {
       code[o] = slow_code;
       ft.sq[o] = SR_FCODE_SKIP;
+      *reinterpret_cast<T*>(static_cast<Pair*>(ft.tab) + o) = f0;
     }
     return;
   }
@@ -1014,32 +1053,12 @@ __global__ void __launch_bounds__(64) sr_fold_walk_kernel(SrFoldTabs ft, SrFoldW
   } else if (c_first >= SR_FCODE_SLOT0 && n > 0 && (all_rows & 4)) {  // (debug: no serial start)
     F = seg_base(c_first)[0];
     k = 1;
-  } else if (c_first >= SR_FCODE_SLOT0 && n > 0) {  // Statistics.mean / Base.sum over a generator: the
-    // first loss starts the fold; the first rows then go one by one, in the hardware's own adds (the
-    // running value leaves a binade every few rows here: a round per crossing would cost ~1 us each)
-    // (through LDS: lane 0 reads its rows ahead of the adds, 8 at a time; a readlane per row costs
-    //  ~100 cycles of hazards, 11 us for 256 rows)
-    const T* b = seg_base(c_first);
-    const int ks = int((rb_rows < n ? rb_rows : n) < 256 ? (rb_rows < n ? rb_rows : n) : 256);
-    __shared__ T s_first[256];
-#pragma unroll
-    for (int j = 0; j < 4; ++j) s_first[4 * lane + j] = (4 * lane + j < ks) ? b[4 * lane + j] : T(0);
-    __syncthreads();
-    T f0 = T(0);
-    if (lane == 0) {
-      f0 = s_first[0];
-      int r = 1;
-      for (; r + 8 <= ks; r += 8) {
-        T u[8];
-#pragma unroll
-        for (int j = 0; j < 8; ++j) u[j] = s_first[r + j];
-#pragma unroll
-        for (int j = 0; j < 8; ++j) f0 = f0 + u[j];
-      }
-      for (; r < ks; ++r) f0 = f0 + s_first[r];
-    }
-    F = sr_fold_lane(f0, 0);
-    k = ks;
+  } else if (c_first >= SR_FCODE_SLOT0 && n > 0 && (all_rows & 32)) {  // (the pair kernel's serial start)
+    F = *reinterpret_cast<const T*>(tab + p);
+    k = sr_fold_serial_rows<T>(rb_rows, n);
+  } else if (c_first >= SR_FCODE_SLOT0 && n > 0) {  // the first rows one by one (sr_fold_serial_start)
+    F = sr_fold_serial_start<T>(seg_base(c_first), sr_fold_serial_rows<T>(rb_rows, n), lane);
+    k = sr_fold_serial_rows<T>(rb_rows, n);
   } else {
     fail = n > 0;  // (the plan keeps the first segment's losses)
     why = 1;

@@ -316,7 +316,8 @@ struct sr_ctx {
   int64_t fold_seg_max = 16384;  // SR_AMD_FOLD_SEG_MAX: calls whose row blocks are longer keep the f64 sum
   int64_t fold_rows_max = int64_t(1) << 24;  // SR_AMD_FOLD_ROWS_MAX: longer folds keep the f64 sum
   int fold_debug_fail = 0;   // (tests: "fold_debug_fail")
-  int fold_reduce = 1;       // SR_AMD_FOLD_REDUCE: stored-loss folds reduce in the pair kernel (0: a reduce launch)
+  int fold_reduce = 1;
+  int fold_pre_start = 1;    // SR_AMD_FOLD_PRE_START: stored-loss folds start in the pair kernel (0: in the walk)       // SR_AMD_FOLD_REDUCE: stored-loss folds reduce in the pair kernel (0: a reduce launch)
   int fold_walk_dbg = 0;     // SR_AMD_FOLD_WALK_DBG (analysis): 2 no O(1) slow blocks, 4 no serial start
   int fold_stats = 0;        // SR_AMD_FOLD_STATS=1: per-tree walk statistics to stderr after each call (analysis)
   DevBuf fold_dbg;
@@ -616,6 +617,8 @@ int fold_walk(sr_ctx* ctx, const FoldJob<T>& job, const FoldRegion<T>& fr, SrFol
               int32_t* out_st, hipStream_t cs) {
   const int nrb = fr.g.n_row_blocks;
   const int tiny = carry == nullptr && fold_tiny(job, fr, who) ? 16 : 0;
+  // (stored losses, the pair kernel launched, the fold starting here: it did the serial start)
+  const int pre = job.path == 1 && !tiny && carry == nullptr && who.first && ctx->fold_pre_start ? 32 : 0;
   if (who.sums) who.sums += fr.t0;
   if (who.flags) who.flags += fr.t0;
   if (who.elig) who.elig += fr.t0;
@@ -630,11 +633,11 @@ int fold_walk(sr_ctx* ctx, const FoldJob<T>& job, const FoldRegion<T>& fr, SrFol
   int4* dbg = ctx->fold_stats ? ctx->fold_dbg.as<int4>() + fr.t0 : nullptr;  // (SR_AMD_FOLD_STATS)
   SR_HIP_CHECK(sr_launch_fold_walk<T>(ft, who, int(fr.np), nrb, rb_rows, job.n_eval, losses, slot_rows, fr.a.perm,
                                       carry ? carry + fr.t0 : nullptr, out_val + fr.t0, out_st + fr.t0, dbg,
-                                      int(job.path == 1) | tiny | ctx->fold_walk_dbg, cs));
+                                      int(job.path == 1) | tiny | pre | ctx->fold_walk_dbg, cs));
   if (ctx->fold_stats == 2)  // (analysis: the same walk again, its loads now warm: the statistics are the second's)
     SR_HIP_CHECK(sr_launch_fold_walk<T>(ft, who, int(fr.np), nrb, rb_rows, job.n_eval, losses, slot_rows, fr.a.perm,
                                         carry ? carry + fr.t0 : nullptr, out_val + fr.t0, out_st + fr.t0, dbg,
-                                        int(job.path == 1) | tiny | ctx->fold_walk_dbg, cs));
+                                        int(job.path == 1) | tiny | pre | ctx->fold_walk_dbg, cs));
   return SR_OK;
 }
 
@@ -3589,6 +3592,7 @@ int sr_init(int device, sr_ctx** out) {
   if (const char* v = std::getenv("SR_AMD_FOLD_ROWS_MAX")) ctx->fold_rows_max = std::max<int64_t>(0, std::atoll(v));
   if (const char* v = std::getenv("SR_AMD_FOLD_WALK_DBG")) ctx->fold_walk_dbg = std::atoi(v) & 6;
   if (const char* v = std::getenv("SR_AMD_FOLD_REDUCE")) ctx->fold_reduce = std::atoi(v) != 0 ? 1 : 0;
+  if (const char* v = std::getenv("SR_AMD_FOLD_PRE_START")) ctx->fold_pre_start = std::atoi(v) != 0 ? 1 : 0;
   hipError_t e = hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking);
   if (e == hipSuccess && std::getenv("SR_AMD_EAGER_STREAM2")) e = ctx->need_stream2();  // (A/B: the round-4 layout)
   if (e == hipSuccess) e = hipEventCreateWithFlags(&ctx->ev_join, hipEventDisableTiming);
